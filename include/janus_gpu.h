@@ -1,0 +1,149 @@
+/* janus_gpu.h — C ABI of the MI355X (gfx950) CRDT state-merge engine.
+ *
+ * Drop-in boundary for the Janus state-merge hot path.  The C#/.NET host binds
+ * these with [DllImport("janusgpu")]; tests bind them with ctypes.  Rules:
+ *   - extern "C", cdecl, blittable types only (uint8_t instead of bool, no structs with references);
+ *   - every pointer argument is caller-owned HOST memory, read or written only during the call;
+ *     device memory is library-owned and freed by the matching *_destroy;
+ *   - every call returns JG_OK or an error code; the message is in jg_last_error (thread-local);
+ *     no exception or abort crosses the ABI;
+ *   - calls are synchronous (return after the work is complete) unless they take `async` != 0,
+ *     in which case jg_fence(ctx) waits for them;
+ *   - one writer per store handle at a time (the reference serialises its stable apply with a
+ *     SemaphoreSlim and its prospective merges with lock(crdt)), concurrent readers allowed;
+ *     each context owns one HIP stream on one device.
+ *
+ * Reference interfaces each entry point replaces are cited per function (paths relative to the
+ * reference root, MSRG/Janus-CRDT @ 2025-03-10).
+ */
+#ifndef JANUS_GPU_H
+#define JANUS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JG_ABI_VERSION 1
+
+/* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
+#define JG_OK        0
+#define JG_EINVAL    1  /* bad argument (ArgumentException / KeyNotFoundException)            */
+#define JG_ENOMEM    2  /* device or host allocation failed (OutOfMemoryException)           */
+#define JG_EOVERFLOW 3  /* PNCounter.Get checked Sum overflowed (OverflowException)          */
+#define JG_ETYPE     4  /* message of the wrong CRDT type (NotSupportedException, ORSet.cs:290) */
+#define JG_EHIP      5  /* HIP runtime error                                                  */
+#define JG_ESTATE    6  /* precondition broken: unsorted / duplicate records, capacity, timeout */
+
+/* elem id of the C# null element of an ORSet<string?> (ORSet.cs:136-140, nullAddGuid/nullRemoveGuid). */
+#define JG_NULL_ELEM 0xFFFFFFFFu
+
+typedef struct jg_ctx jg_ctx;     /* one device + one HIP stream                               */
+typedef struct jg_pnc jg_pnc;     /* PN-Counter store: P and N, [n_keys x n_replicas] row-major */
+typedef struct jg_rows jg_rows;   /* device-resident batch of received PN-Counter rows          */
+typedef struct jg_orset jg_orset; /* OR-Set store: sorted add and tombstone tag records         */
+
+/* One OR-Set tag record: key = (uint64_t)set << 32 | elem, tag = 16 opaque bytes (a C# Guid:
+ * tag_lo = bytes 0..7, tag_hi = bytes 8..15, little-endian).  Streams are sorted strictly
+ * increasing by (key, tag_lo, tag_hi), unsigned.  24 bytes, 8-byte aligned. */
+typedef struct jg_tagrec {
+    uint64_t key;
+    uint64_t tag_lo;
+    uint64_t tag_hi;
+} jg_tagrec;
+
+/* ---------------------------------------------------------------------------------------------
+ * Context
+ * ------------------------------------------------------------------------------------------- */
+int jg_abi_version(void);
+/* Open device `device` (HIP ordinal) with a private non-blocking stream. */
+int jg_open(int device, jg_ctx** out);
+int jg_close(jg_ctx* ctx);
+/* Copy the calling thread's last error message (NUL-terminated, truncated to n). */
+int jg_last_error(char* buf, size_t n);
+/* Wait for every async call issued on ctx. */
+int jg_fence(jg_ctx* ctx);
+/* The context's hipStream_t (for host-side event timing). */
+int jg_stream(jg_ctx* ctx, void** hip_stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * PN-Counter store — replaces PNCounter's Dictionary<Guid,int> P/N vectors
+ * (MergeSharp/MergeSharp/CRDTs/PNCounters.cs:56-153) for a whole keyspace at once.
+ * Row = key (host-interned key Guid -> key_idx), column = replica (per-key replica Guid -> column,
+ * assigned in first-insertion order so column order = the Dictionary's enumeration order).
+ * elem_bytes 4 = the reference's int; 8 = the long variant of BASELINE.json.
+ * In RECEIVED rows the most negative value of the width (INT32_MIN / INT64_MIN) means "replica
+ * absent from the message": Merge only visits entries the message holds (PNCounters.cs:133-143).
+ * ------------------------------------------------------------------------------------------- */
+int jg_pnc_create(jg_ctx* ctx, uint64_t n_keys, uint32_t n_replicas, uint32_t elem_bytes, jg_pnc** out);
+int jg_pnc_destroy(jg_pnc* pnc);
+/* Overwrite rows (key_idx NULL = rows 0..n_rows-1).  Initial load / restore. */
+int jg_pnc_write_rows(jg_pnc* pnc, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N);
+/* Snapshot rows to the host: GetLastSynchronizedUpdate (PNCounters.cs:115-118). */
+int jg_pnc_read_rows(jg_pnc* pnc, const uint32_t* key_idx, uint64_t n_rows, void* P, void* N);
+/* Merge received states: for each row m and column c whose value is not ABSENT,
+ * A[key_idx[m]][c] = max(A[key_idx[m]][c], B[m][c]) for P and N — PNCounter.Merge
+ * (PNCounters.cs:131-144) reached through ApplySynchronizedUpdate (:121-125), SafeCRDT.ApplyUpdateStable
+ * (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83) and the committed-batch loop
+ * (BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:122-146).  key_idx may repeat (the result is the same
+ * in any order: max is associative, commutative, idempotent).  key_idx NULL = identity. */
+int jg_pnc_merge_rows(jg_pnc* pnc, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N);
+/* Increment / Decrement (PNCounters.cs:97-112, unchecked '+='): cell (key[i], col[i]) of P
+ * (is_n[i] == 0) or N (is_n[i] != 0) += delta[i], wrapping at the store's width. */
+int jg_pnc_apply_ops(jg_pnc* pnc, uint64_t n_ops, const uint32_t* key, const uint32_t* col,
+                     const int64_t* delta, const uint8_t* is_n);
+/* PNCounter.Get (PNCounters.cs:87-90) per key: checked Sum(P) - checked Sum(N), the sums taken in
+ * column order, the subtraction wrapping at the store's width.  overflow[i] = 1 (and out[i] = 0)
+ * where a checked Sum throws; the call still returns JG_OK.  key_idx NULL = keys 0..n-1. */
+int jg_pnc_values(jg_pnc* pnc, const uint32_t* key_idx, uint64_t n, int64_t* out, uint8_t* overflow);
+
+/* Device-resident received batch (the committed state messages of a wave, decoded to rows).
+ * key_idx NULL at upload = identity rows (requires n_rows == the store's n_keys at merge time). */
+int jg_rows_create(jg_ctx* ctx, uint64_t n_rows, uint32_t n_replicas, uint32_t elem_bytes, jg_rows** out);
+int jg_rows_destroy(jg_rows* rows);
+int jg_rows_upload(jg_rows* rows, const uint32_t* key_idx, const void* P, const void* N);
+int jg_pnc_merge_batch(jg_pnc* pnc, const jg_rows* rows, int async);
+
+/* ---------------------------------------------------------------------------------------------
+ * OR-Set store — replaces ORSet<string>'s Dictionary<T,HashSet<Guid>> add/remove maps and null
+ * tag sets (MergeSharp/MergeSharp/CRDTs/ORSet.cs:78-327) for a whole keyspace of sets.
+ * ------------------------------------------------------------------------------------------- */
+int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** out);
+int jg_orset_destroy(jg_orset* s);
+/* Replace the state with the given sorted streams (validated: JG_ESTATE if not strictly increasing). */
+int jg_orset_load(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem);
+int jg_orset_size(jg_orset* s, uint64_t* n_add, uint64_t* n_rem);
+/* Canonical snapshot (GetLastSynchronizedUpdate, ORSet.cs:305-308). */
+int jg_orset_read(jg_orset* s, jg_tagrec* add, uint64_t cap_add, jg_tagrec* rem, uint64_t cap_rem);
+/* ORSet.Merge (ORSet.cs:253-283): per element UnionWith of the add and tombstone tag sets (null
+ * element included), from host records (sorted, strictly increasing). */
+int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem);
+/* dst = dst ∪ src for two device-resident stores. */
+int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async);
+/* out = a ∪ b (out must have capacity for a+b; it may not alias a or b). */
+int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int async);
+/* ORSet.Contains (ORSet.cs:204-237) for (set[i], elem[i]): elem present iff its add set exists
+ * and (it has no tombstone set or the two tag sets differ: !SetEquals); the null element is
+ * present iff !SetEquals(nullRemove, nullAdd).  out[i] = 0/1. */
+int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, uint64_t n, uint8_t* out);
+
+/* ---------------------------------------------------------------------------------------------
+ * Synthetic workloads (bench / size-independent parity): device-side counter-based generators,
+ * defined in DESIGN.md §Synthetic inputs and mirrored on the host by the test oracle.
+ * ------------------------------------------------------------------------------------------- */
+/* which: 0 = local P, 1 = local N, 2 = received P, 3 = received N.  Local unseen cells are 0;
+ * received unseen cells are ABSENT. */
+int jg_synth_pnc_store(jg_pnc* pnc, uint64_t seed);
+int jg_synth_pnc_rows(jg_rows* rows, uint64_t seed, uint64_t key0);
+/* Fill a store with n_groups (set, elem) groups (group g = set*elems_per_set + elem): adds carry
+ * tags u in [add_u0, add_u0+add_per_group), tombstones u in [rem_u0, rem_u0+rem_per_group). */
+int jg_synth_orset(jg_orset* s, uint64_t seed, uint64_t n_groups, uint32_t elems_per_set,
+                   uint32_t add_per_group, uint32_t add_u0, uint32_t rem_per_group, uint32_t rem_u0);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* JANUS_GPU_H */

@@ -1,0 +1,124 @@
+// ctx.hip — context, errors and device buffers of libjanusgpu.
+#include <cstring>
+
+#include "jg_internal.hpp"
+
+namespace jg {
+
+static thread_local char g_err[1024];
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+void clear_error() { g_err[0] = 0; }
+
+void fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    throw Error{code, buf};
+}
+
+void DevBuf::alloc(size_t n) {
+    release();
+    if (n == 0) return;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) {
+        p = nullptr;
+        (void)hipGetLastError();
+        fail(JG_ENOMEM, "hipMalloc(%zu) failed: %s", n, hipGetErrorString(e));
+    }
+    bytes = n;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+void ensure_device(jg_ctx* ctx) { JG_HIP(hipSetDevice(ctx->device)); }
+
+void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes) {
+    if (b.bytes < bytes) {
+        JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block may still be in use
+        b.alloc(bytes + bytes / 4);
+    }
+    return b.p;
+}
+
+}  // namespace jg
+
+extern "C" {
+
+int jg_abi_version(void) { return JG_ABI_VERSION; }
+
+int jg_last_error(char* buf, size_t n) {
+    if (!buf || n == 0) return JG_EINVAL;
+    std::strncpy(buf, jg::g_err, n - 1);
+    buf[n - 1] = 0;
+    return JG_OK;
+}
+
+int jg_open(int device, jg_ctx** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(out, JG_EINVAL, "jg_open: out is NULL");
+        int count = 0;
+        JG_HIP(hipGetDeviceCount(&count));
+        JG_REQUIRE(device >= 0 && device < count, JG_EINVAL, "jg_open: device %d of %d", device, count);
+        hipDeviceProp_t prop;
+        JG_HIP(hipGetDeviceProperties(&prop, device));
+        JG_REQUIRE(std::strncmp(prop.gcnArchName, "gfx950", 6) == 0, JG_EINVAL,
+                   "jg_open: device %d is %s; this build targets gfx950 only", device, prop.gcnArchName);
+        auto* c = new jg_ctx();
+        c->device = device;
+        c->num_cus = prop.multiProcessorCount;
+        try {
+            JG_HIP(hipSetDevice(device));
+            JG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            c->flags.alloc(256);
+            JG_HIP(hipMemset(c->flags.p, 0, 256));
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+int jg_close(jg_ctx* ctx) {
+    return jg::guard([&] {
+        if (!ctx) return;
+        jg::ensure_device(ctx);
+        (void)hipStreamSynchronize(ctx->stream);
+        ctx->scratch.release();
+        ctx->scratch2.release();
+        ctx->scratch3.release();
+        ctx->flags.release();
+        (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+    });
+}
+
+int jg_fence(jg_ctx* ctx) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx, JG_EINVAL, "jg_fence: ctx is NULL");
+        jg::ensure_device(ctx);
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_stream(jg_ctx* ctx, void** s) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && s, JG_EINVAL, "jg_stream: NULL argument");
+        *s = (void*)ctx->stream;
+    });
+}
+
+}  // extern "C"

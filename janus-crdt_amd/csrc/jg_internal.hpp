@@ -1,0 +1,120 @@
+// jg_internal.hpp — shared internals of libjanusgpu (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <new>
+#include <string>
+
+#include "janus_gpu.h"
+
+namespace jg {
+
+// ---- errors ------------------------------------------------------------------------------------
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+
+struct Error {  // thrown inside the library only; converted to a code at the ABI edge
+    int code;
+    std::string msg;
+};
+
+[[noreturn]] void fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define JG_HIP(call)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (call);                                                                 \
+        if (e_ != hipSuccess) ::jg::fail(JG_EHIP, "%s failed: %s (%s:%d)", #call,               \
+                                        hipGetErrorString(e_), __FILE__, __LINE__);             \
+    } while (0)
+
+#define JG_REQUIRE(cond, code, ...) \
+    do { if (!(cond)) ::jg::fail((code), __VA_ARGS__); } while (0)
+
+// Run `body` and translate any library error / bad_alloc into an ABI return code.
+template <class F> int guard(F&& body) {
+    try {
+        clear_error();
+        body();
+        return JG_OK;
+    } catch (const Error& e) {
+        set_error("%s", e.msg.c_str());
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        set_error("host allocation failed");
+        return JG_ENOMEM;
+    } catch (...) {
+        set_error("unexpected C++ exception");
+        return JG_EINVAL;
+    }
+}
+
+// ---- device buffers ------------------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void alloc(size_t n);  // frees the old block; n == 0 leaves p null
+    void release();
+    ~DevBuf() { release(); }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace jg
+
+// ---- handle types (opaque at the ABI) ------------------------------------------------------------
+struct jg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 256;
+    jg::DevBuf scratch;  // reusable per-call device scratch (key indices, query keys, staging)
+    jg::DevBuf scratch2;
+    jg::DevBuf scratch3;
+    jg::DevBuf flags;    // small zero-initialised status words (error flags)
+};
+
+struct jg_pnc {
+    jg_ctx* ctx;
+    uint64_t n_keys;
+    uint32_t R;
+    uint32_t eb;  // elem bytes (4 | 8)
+    jg::DevBuf P, N;
+};
+
+struct jg_rows {
+    jg_ctx* ctx;
+    uint64_t n_rows;
+    uint32_t R;
+    uint32_t eb;
+    bool has_keys = false;
+    uint32_t max_key = 0;  // largest key_idx uploaded (validated against the store at merge)
+    jg::DevBuf P, N, keys;
+};
+
+// One sorted tag-record stream, structure of arrays: key[i] (8 B) and tag[i] (16 B).
+struct jg_stream_soa {
+    jg::DevBuf key, tag;
+    uint64_t cap = 0;
+    uint64_t n = 0;
+    void reserve(uint64_t c);
+    void swap(jg_stream_soa& o);
+};
+
+struct jg_orset {
+    jg_ctx* ctx;
+    jg_stream_soa add, rem;
+    jg_stream_soa spare_add, spare_rem;  // union target for in-place merges (swapped in)
+    jg::DevBuf counts;     // device-side uint64 [2]: n_add, n_rem written by the union kernel
+    bool counts_pending = false;  // an async union wrote `counts`; host n's are stale
+};
+
+namespace jg {
+void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
+void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
+void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
+}  // namespace jg

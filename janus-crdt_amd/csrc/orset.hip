@@ -1,0 +1,571 @@
+// orset.hip — OR-Set store and kernels (gfx950, wave64; integer/byte work, no MFMA).
+//
+// Layout in HBM: two record streams per store (adds, tombstones), each structure-of-arrays
+//   key[i] : uint64  = set << 32 | elem          (elem 0xFFFFFFFF = C# null)
+//   tag[i] : 16 B    = the Guid, as {lo, hi} little-endian words
+// sorted strictly increasing by (key, tag.lo, tag.hi).  A (set, elem)'s HashSet<Guid> is the run of
+// its records; Dictionary membership of elem = the run being non-empty.
+//
+// ORSet.Merge (ORSet.cs:253-283) over a keyspace of sets = per-stream sorted set UNION:
+//   k_partition : merge-path split of each TILE-record output diagonal (one binary search each).
+//   k_union     : one tile per workgroup, tickets in launch order.  Stage the tile's slices of A
+//                 and B in LDS, merge (A first on ties), drop a B record equal to the A record
+//                 before it in merged order (the only way a duplicate can appear, since each input
+//                 is duplicate-free), compact through a block scan, and place the tile with a
+//                 decoupled look-back over 8-byte {flag, count} status words (agent-scope relaxed
+//                 atomics: the word IS the data, no payload is handed off between workgroups).
+//   Roofline: HBM.  Reads 24 B per input record, writes 24 B per output record.
+// ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams,
+// then SetEquals of the two sorted runs.
+#include <algorithm>
+#include <vector>
+
+#include "jg_internal.hpp"
+
+namespace {
+
+constexpr int kOB = 256;        // threads per workgroup
+constexpr int kItems = 8;       // records per thread per tile
+constexpr int kTile = kOB * kItems;
+
+constexpr unsigned long long kFlagAgg = 1ull << 62;
+constexpr unsigned long long kFlagIncl = 2ull << 62;
+constexpr unsigned long long kValMask = (1ull << 62) - 1;
+constexpr unsigned kSpinLimit = 1u << 22;
+
+struct Tag { unsigned long long lo, hi; };
+
+__device__ __forceinline__ Tag ld_tag(const uint4* p) { return __builtin_bit_cast(Tag, *p); }
+__device__ __forceinline__ uint4 to_u4(Tag t) { return __builtin_bit_cast(uint4, t); }
+
+// Branch-free lexicographic compare on (key, tag.lo, tag.hi), unsigned.
+__device__ __forceinline__ bool rec_lt(unsigned long long ka, Tag ta, unsigned long long kb, Tag tb) {
+    return (ka < kb) | ((ka == kb) & ((ta.lo < tb.lo) | ((ta.lo == tb.lo) & (ta.hi < tb.hi))));
+}
+__device__ __forceinline__ bool rec_eq(unsigned long long ka, Tag ta, unsigned long long kb, Tag tb) {
+    return (ka == kb) & (ta.lo == tb.lo) & (ta.hi == tb.hi);
+}
+
+// Merge-path split for diagonal d over (a, b): number of A records among the first d merged.
+__global__ __launch_bounds__(kOB) void k_partition(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
+                                                   const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
+                                                   uint64_t n_parts, uint64_t* __restrict__ part) {
+    const uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x;
+    if (i >= n_parts) return;
+    const uint64_t total = na + nb;
+    const uint64_t d = i * kTile < total ? i * kTile : total;
+    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const unsigned long long ka = ak[mid], kb = bk[d - 1 - mid];
+        bool a_le_b;  // a[mid] <= b[d-1-mid]  -> take more from A
+        if (ka != kb) a_le_b = ka < kb;
+        else a_le_b = !rec_lt(kb, ld_tag(bt + d - 1 - mid), ka, ld_tag(at + mid));
+        if (a_le_b) lo = mid + 1;
+        else hi = mid;
+    }
+    part[i] = lo;
+}
+
+// Wave 0 of a tile: sum the counts of all earlier tiles (decoupled look-back).
+__device__ unsigned long long lookback(unsigned long long* status, long long tile, int lane, unsigned* err) {
+    unsigned long long excl = 0;
+    long long base = tile - 1;
+    for (;;) {
+        const long long idx = base - lane;
+        unsigned long long w;
+        unsigned spins = 0;
+        for (;;) {
+            w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+            if (__all((w >> 62) != 0)) break;
+            if (++spins > kSpinLimit) {  // wave-uniform: give up, flag the call, let the grid drain
+                if (lane == 0) atomicOr(err, 1u);
+                w = kFlagIncl;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long incl = __ballot((w >> 62) == 2);
+        const int first = incl ? __ffsll((long long)incl) - 1 : 64;
+        unsigned long long v = lane <= first ? (w & kValMask) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (incl) return excl;
+        base -= 64;
+    }
+}
+
+__global__ __launch_bounds__(kOB) void k_union(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
+                                               const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
+                                               const uint64_t* __restrict__ part, uint64_t n_tiles,
+                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
+                                               unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
+                                               unsigned* err) {
+    __shared__ unsigned long long s_key[kTile];
+    __shared__ uint4 s_tag[kTile];
+    __shared__ unsigned long long s_prev_key;
+    __shared__ uint4 s_prev_tag;
+    __shared__ int s_has_prev;
+    __shared__ unsigned s_tile;
+    __shared__ unsigned long long s_excl;
+    __shared__ int s_wsum[kOB / 64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint64_t tile = s_tile;
+    const uint64_t total_in = na + nb;
+    const uint64_t d0 = tile * kTile;
+    const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
+    const uint64_t i0 = part[tile], i1 = part[tile + 1];
+    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0), n = nA + nB;
+
+    // ---- stage the tile's A and B slices in LDS ----
+    // Loads are unconditional (index clamped into the tile, n >= 1) so all 2 x kItems of them are
+    // in flight before the first LDS write; only the LDS writes are predicated.
+    {
+        unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {
+            const int x = min(it * kOB + tid, n - 1);
+            const bool from_a = x < nA;
+            const uint64_t gi = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
+            rk[it] = (from_a ? ak : bk)[gi];
+            const Tag t = ld_tag((from_a ? at : bt) + gi);
+            rlo[it] = t.lo;
+            rhi[it] = t.hi;
+        }
+        if (tid == 0) {
+            s_has_prev = i0 > 0;
+            if (i0 > 0) { s_prev_key = ak[i0 - 1]; s_prev_tag = at[i0 - 1]; }
+        }
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
+            const int x = it * kOB + tid;
+            s_key[x] = rk[it];
+            s_tag[x] = to_u4(Tag{rlo[it], rhi[it]});
+        }
+    }
+    __syncthreads();
+
+    // ---- per-thread merge path + serial merge of kItems outputs ----
+    const int diag = min(tid * kItems, n);
+    int lo = diag > nB ? diag - nB : 0, hi = min(diag, nA);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const int bj = nA + diag - 1 - mid;
+        const bool a_le_b = !rec_lt(s_key[bj], __builtin_bit_cast(Tag, s_tag[bj]), s_key[mid], __builtin_bit_cast(Tag, s_tag[mid]));
+        if (a_le_b) lo = mid + 1;
+        else hi = mid;
+    }
+    int ai = lo, bi = diag - lo;
+    bool hp;
+    unsigned long long pk;
+    Tag pt;
+    if (ai > 0) { hp = true; pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); }
+    else { hp = s_has_prev != 0; pk = s_prev_key; pt = __builtin_bit_cast(Tag, s_prev_tag); }
+
+    const int my_n = n - diag < kItems ? n - diag : kItems;
+    unsigned long long ka = 0, kb = 0;
+    Tag ta{0, 0}, tb{0, 0};
+    if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
+    if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
+    int src[kItems];
+    unsigned keep = 0;
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) {
+        src[it] = 0;
+        if (it < my_n) {
+            const bool take_a = ai < nA && (bi >= nB || !rec_lt(kb, tb, ka, ta));
+            if (take_a) {
+                src[it] = ai;
+                keep |= 1u << it;
+                hp = true; pk = ka; pt = ta;
+                ++ai;
+                if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
+            } else {
+                src[it] = nA + bi;
+                if (!(hp && rec_eq(pk, pt, kb, tb))) keep |= 1u << it;
+                ++bi;
+                if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
+            }
+        }
+    }
+
+    // ---- block scan of kept counts ----
+    const int cnt = __popc(keep);
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_wsum[wid] = incl;
+    __syncthreads();
+    int wbase = 0, block_total = 0;
+#pragma unroll
+    for (int w = 0; w < kOB / 64; ++w) {
+        const int v = s_wsum[w];
+        if (w < wid) wbase += v;
+        block_total += v;
+    }
+    const int my_off = wbase + incl - cnt;
+
+    // ---- publish and look back (wave 0) ----
+    if (wid == 0) {
+        unsigned long long excl = 0;
+        if (tile == 0) {
+            if (lane == 0) __hip_atomic_store(status, kFlagIncl | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(status + tile, kFlagAgg | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            excl = lookback(status, (long long)tile, lane, err);
+            if (lane == 0)
+                __hip_atomic_store(status + tile, kFlagIncl | (excl + (unsigned long long)block_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if (tile == n_tiles - 1) *out_count = excl + (unsigned long long)block_total;
+        }
+    }
+
+    // ---- gather kept records, compact through LDS, store coalesced ----
+    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) {  // src[it] is a valid LDS index even for dropped items
+        rk[it] = s_key[src[it]];
+        const Tag t = __builtin_bit_cast(Tag, s_tag[src[it]]);
+        rlo[it] = t.lo;
+        rhi[it] = t.hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) {
+        if (keep & (1u << it)) {
+            const int o = my_off + __popc(keep & ((1u << it) - 1u));
+            s_key[o] = rk[it];
+            s_tag[o] = to_u4(Tag{rlo[it], rhi[it]});
+        }
+    }
+    __syncthreads();
+    const unsigned long long base = s_excl;
+    for (int x = tid; x < block_total; x += kOB) {
+        ok[base + x] = s_key[x];
+        ot[base + x] = s_tag[x];
+    }
+}
+
+// Strictly increasing check: err |= 1 at the first non-increasing neighbour pair.
+__global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* __restrict__ k, const uint4* __restrict__ t, uint64_t n,
+                                                      unsigned* err) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i + 1 < n; i += (uint64_t)gridDim.x * kOB) {
+        if (!rec_lt(k[i], ld_tag(t + i), k[i + 1], ld_tag(t + i + 1))) atomicOr(err, 1u);
+    }
+}
+
+// AoS <-> SoA for host transfers.
+__global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in, uint64_t n, unsigned long long* __restrict__ k,
+                                                uint4* __restrict__ t) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        const jg_tagrec r = in[i];
+        k[i] = r.key;
+        t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
+    }
+}
+__global__ __launch_bounds__(kOB) void k_pack(const unsigned long long* __restrict__ k, const uint4* __restrict__ t, uint64_t n,
+                                              jg_tagrec* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        const Tag g = ld_tag(t + i);
+        out[i] = jg_tagrec{k[i], g.lo, g.hi};
+    }
+}
+
+__device__ __forceinline__ uint64_t lower_key(const unsigned long long* k, uint64_t n, unsigned long long q) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (k[m] < q) lo = m + 1; else hi = m; }
+    return lo;
+}
+__device__ __forceinline__ uint64_t upper_key(const unsigned long long* k, uint64_t n, unsigned long long q) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (k[m] <= q) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+__global__ __launch_bounds__(kOB) void k_contains(const unsigned long long* __restrict__ akey, const uint4* __restrict__ atag, uint64_t na,
+                                                  const unsigned long long* __restrict__ rkey, const uint4* __restrict__ rtag, uint64_t nr,
+                                                  const unsigned long long* __restrict__ q, uint64_t nq, uint8_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kOB) {
+        const unsigned long long key = q[i];
+        const uint64_t a0 = lower_key(akey, na, key), a1 = upper_key(akey, na, key);
+        const uint64_t r0 = lower_key(rkey, nr, key), r1 = upper_key(rkey, nr, key);
+        const uint64_t ca = a1 - a0, cr = r1 - r0;
+        bool same = ca == cr;
+        for (uint64_t j = 0; same && j < ca; ++j) {
+            const Tag x = ld_tag(atag + a0 + j), y = ld_tag(rtag + r0 + j);
+            same = x.lo == y.lo && x.hi == y.hi;
+        }
+        bool present;
+        if ((unsigned)key == JG_NULL_ELEM) present = !same;  // !nullRemoveGuid.SetEquals(nullAddGuid)
+        else present = ca > 0 && (cr == 0 || !same);        // add key, and not in removeSet or !SetEquals
+        out[i] = present ? 1 : 0;
+    }
+}
+
+unsigned grid_for(jg_ctx* ctx, uint64_t items, unsigned per_cu = 8) {
+    uint64_t g = (items + kOB - 1) / kOB;
+    const uint64_t cap = (uint64_t)ctx->num_cus * per_cu;
+    if (g > cap) g = cap;
+    return g == 0 ? 1u : (unsigned)g;
+}
+
+// Workspace of one union: [status n_tiles x 8 | ticket | pad to 256][part (n_tiles+1) x 8 | pad].
+size_t union_ws_bytes(uint64_t total) {
+    const uint64_t n_tiles = (total + kTile - 1) / kTile;
+    return (((n_tiles * 8 + 16) + 255) & ~(size_t)255) + (((n_tiles + 1) * 8 + 255) & ~(size_t)255);
+}
+
+// Union of two streams into `out` (capacity checked by the caller).  Async on ctx->stream; the
+// output count lands in *d_count (device).  `ws` holds union_ws_bytes(a.n + b.n) bytes.
+void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws) {
+    const uint64_t total = a.n + b.n;
+    if (total == 0) {
+        JG_HIP(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), ctx->stream));
+        return;
+    }
+    const uint64_t n_tiles = (total + kTile - 1) / kTile;
+    const size_t status_bytes = ((n_tiles * 8 + 16) + 255) & ~(size_t)255;
+    auto* status = reinterpret_cast<unsigned long long*>(ws);
+    auto* ticket = reinterpret_cast<unsigned*>(ws + n_tiles * 8);
+    auto* part = reinterpret_cast<uint64_t*>(ws + status_bytes);
+    JG_HIP(hipMemsetAsync(ws, 0, status_bytes, ctx->stream));  // every polled word zeroed per call
+    hipLaunchKernelGGL(k_partition, dim3((unsigned)((n_tiles + 1 + kOB - 1) / kOB)), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(),
+                       a.tag.as<uint4>(), a.n, b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, n_tiles + 1, part);
+    JG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_union, dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(), a.tag.as<uint4>(), a.n,
+                       b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, part, n_tiles, out.key.as<unsigned long long>(),
+                       out.tag.as<uint4>(), status, ticket, d_count, ctx->flags.as<unsigned>());
+    JG_HIP(hipGetLastError());
+}
+
+// Union of both streams of two stores into `oa`/`orr`; counts to counted->counts.
+void union_store(jg_ctx* ctx, const jg_orset* a, const jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted) {
+    JG_REQUIRE(oa.cap >= a->add.n + b->add.n && orr.cap >= a->rem.n + b->rem.n, JG_ESTATE,
+               "union: output capacity (%llu, %llu) < inputs (%llu, %llu)", (unsigned long long)oa.cap, (unsigned long long)orr.cap,
+               (unsigned long long)(a->add.n + b->add.n), (unsigned long long)(a->rem.n + b->rem.n));
+    unsigned long long* d = counted->counts.as<unsigned long long>();
+    const size_t ws_add = union_ws_bytes(a->add.n + b->add.n);
+    char* ws = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, ws_add + union_ws_bytes(a->rem.n + b->rem.n)));
+    launch_union(ctx, a->add, b->add, oa, d, ws);
+    launch_union(ctx, a->rem, b->rem, orr, d + 1, ws + ws_add);
+    counted->counts_pending = true;
+}
+
+void check_err_flag(jg_ctx* ctx, const char* fn) {
+    unsigned h = 0;
+    JG_HIP(hipMemcpyAsync(&h, ctx->flags.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    if (h) {
+        JG_HIP(hipMemsetAsync(ctx->flags.p, 0, sizeof h, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        jg::fail(JG_ESTATE, "%s: device reported a broken precondition or look-back timeout (flag %u)", fn, h);
+    }
+}
+
+void upload_stream(jg_ctx* ctx, jg_stream_soa& s, const jg_tagrec* recs, uint64_t n, const char* fn) {
+    s.reserve(n);
+    s.n = n;
+    if (n == 0) return;
+    auto* st = static_cast<jg_tagrec*>(jg::scratch(ctx, ctx->scratch2, n * sizeof(jg_tagrec)));
+    JG_HIP(hipMemcpyAsync(st, recs, n * sizeof(jg_tagrec), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_unpack, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st, n, s.key.as<unsigned long long>(), s.tag.as<uint4>());
+    JG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s.key.as<unsigned long long>(),
+                       s.tag.as<uint4>(), n, ctx->flags.as<unsigned>());
+    JG_HIP(hipGetLastError());
+    check_err_flag(ctx, fn);
+}
+
+void download_stream(jg_ctx* ctx, const jg_stream_soa& s, jg_tagrec* out) {
+    if (s.n == 0) return;
+    auto* st = static_cast<jg_tagrec*>(jg::scratch(ctx, ctx->scratch2, s.n * sizeof(jg_tagrec)));
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(ctx, s.n, 16)), dim3(kOB), 0, ctx->stream, s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.n,
+                       st);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(out, st, s.n * sizeof(jg_tagrec), hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+// In-place merge: s = s ∪ src (src may be a temporary store).
+void merge_into(jg_orset* s, const jg_orset* src, bool async) {
+    jg_ctx* ctx = s->ctx;
+    jg::sync_counts(s);
+    s->spare_add.reserve(s->add.n + src->add.n);
+    s->spare_rem.reserve(s->rem.n + src->rem.n);
+    union_store(ctx, s, src, s->spare_add, s->spare_rem, s);
+    s->add.swap(s->spare_add);
+    s->rem.swap(s->spare_rem);
+    if (!async) {
+        check_err_flag(ctx, "jg_orset_merge");
+        jg::sync_counts(s);
+    }
+}
+
+}  // namespace
+
+void jg_stream_soa::swap(jg_stream_soa& o) {
+    std::swap(key.p, o.key.p); std::swap(key.bytes, o.key.bytes);
+    std::swap(tag.p, o.tag.p); std::swap(tag.bytes, o.tag.bytes);
+    std::swap(cap, o.cap); std::swap(n, o.n);
+}
+
+void jg_stream_soa::reserve(uint64_t c) {
+    if (c <= cap) return;
+    key.alloc(c * 8);
+    tag.alloc(c * 16);
+    cap = c;
+}
+
+namespace jg {
+void sync_counts(jg_orset* s) {
+    if (!s->counts_pending) return;
+    unsigned long long h[2];
+    JG_HIP(hipMemcpyAsync(h, s->counts.p, sizeof h, hipMemcpyDeviceToHost, s->ctx->stream));
+    JG_HIP(hipStreamSynchronize(s->ctx->stream));
+    s->add.n = h[0];
+    s->rem.n = h[1];
+    s->counts_pending = false;
+}
+}  // namespace jg
+
+extern "C" {
+
+int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && out, JG_EINVAL, "jg_orset_create: NULL argument");
+        jg::ensure_device(ctx);
+        auto* s = new jg_orset();
+        s->ctx = ctx;
+        try {
+            s->add.reserve(cap_add);
+            s->rem.reserve(cap_rem);
+            s->counts.alloc(16);
+            JG_HIP(hipMemset(s->counts.p, 0, 16));
+        } catch (...) {
+            delete s;
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int jg_orset_destroy(jg_orset* s) {
+    return jg::guard([&] {
+        if (!s) return;
+        jg::ensure_device(s->ctx);
+        JG_HIP(hipStreamSynchronize(s->ctx->stream));
+        delete s;
+    });
+}
+
+int jg_orset_load(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_load: store is NULL");
+        JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_load: NULL records");
+        jg::ensure_device(s->ctx);
+        JG_HIP(hipStreamSynchronize(s->ctx->stream));
+        s->counts_pending = false;
+        upload_stream(s->ctx, s->add, add, n_add, "jg_orset_load(add)");
+        upload_stream(s->ctx, s->rem, rem, n_rem, "jg_orset_load(rem)");
+    });
+}
+
+int jg_orset_size(jg_orset* s, uint64_t* n_add, uint64_t* n_rem) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_size: store is NULL");
+        jg::ensure_device(s->ctx);
+        if (s->counts_pending) check_err_flag(s->ctx, "jg_orset_size");
+        jg::sync_counts(s);
+        if (n_add) *n_add = s->add.n;
+        if (n_rem) *n_rem = s->rem.n;
+    });
+}
+
+int jg_orset_read(jg_orset* s, jg_tagrec* add, uint64_t cap_add, jg_tagrec* rem, uint64_t cap_rem) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_read: store is NULL");
+        jg::ensure_device(s->ctx);
+        jg::sync_counts(s);
+        JG_REQUIRE(cap_add >= s->add.n && cap_rem >= s->rem.n, JG_EINVAL, "jg_orset_read: buffers (%llu, %llu) < state (%llu, %llu)",
+                   (unsigned long long)cap_add, (unsigned long long)cap_rem, (unsigned long long)s->add.n, (unsigned long long)s->rem.n);
+        JG_REQUIRE((add || s->add.n == 0) && (rem || s->rem.n == 0), JG_EINVAL, "jg_orset_read: NULL buffer");
+        download_stream(s->ctx, s->add, add);
+        download_stream(s->ctx, s->rem, rem);
+    });
+}
+
+int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_merge: store is NULL");
+        JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_merge: NULL records");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset tmp;
+        tmp.ctx = ctx;
+        upload_stream(ctx, tmp.add, add, n_add, "jg_orset_merge(add)");
+        upload_stream(ctx, tmp.rem, rem, n_rem, "jg_orset_merge(rem)");
+        merge_into(s, &tmp, false);
+    });
+}
+
+int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
+    return jg::guard([&] {
+        JG_REQUIRE(dst && src && dst != src, JG_EINVAL, "jg_orset_merge_store: bad stores");
+        JG_REQUIRE(dst->ctx == src->ctx, JG_EINVAL, "jg_orset_merge_store: stores belong to different contexts");
+        jg::ensure_device(dst->ctx);
+        jg::sync_counts(const_cast<jg_orset*>(src));
+        merge_into(dst, src, async == 0 ? false : true);
+    });
+}
+
+int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int async) {
+    return jg::guard([&] {
+        JG_REQUIRE(a && b && out, JG_EINVAL, "jg_orset_union: NULL store");
+        JG_REQUIRE(out != a && out != b, JG_EINVAL, "jg_orset_union: out may not alias an input");
+        JG_REQUIRE(a->ctx == b->ctx && a->ctx == out->ctx, JG_EINVAL, "jg_orset_union: stores belong to different contexts");
+        jg_ctx* ctx = out->ctx;
+        jg::ensure_device(ctx);
+        jg::sync_counts(const_cast<jg_orset*>(a));
+        jg::sync_counts(const_cast<jg_orset*>(b));
+        union_store(ctx, a, b, out->add, out->rem, out);
+        if (!async) {
+            check_err_flag(ctx, "jg_orset_union");
+            jg::sync_counts(out);
+        }
+    });
+}
+
+int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, uint64_t n, uint8_t* out) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_contains: store is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(set && elem && out, JG_EINVAL, "jg_orset_contains: NULL argument");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg::sync_counts(s);
+        std::vector<unsigned long long> q(n);
+        for (uint64_t i = 0; i < n; ++i) q[i] = ((unsigned long long)set[i] << 32) | elem[i];
+        char* st = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 9 + 64));
+        auto* dq = reinterpret_cast<unsigned long long*>(st);
+        auto* dout = reinterpret_cast<uint8_t*>(st + n * 8);
+        JG_HIP(hipMemcpyAsync(dq, q.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_contains, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s->add.key.as<unsigned long long>(),
+                           s->add.tag.as<uint4>(), s->add.n, s->rem.key.as<unsigned long long>(), s->rem.tag.as<uint4>(), s->rem.n, dq, n,
+                           dout);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+}  // extern "C"

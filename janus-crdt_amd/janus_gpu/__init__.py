@@ -1,0 +1,285 @@
+"""ctypes binding of libjanusgpu (include/janus_gpu.h) — the same C ABI the C#/.NET host binds with
+[DllImport("janusgpu")].  No torch types cross it: plain pointers and sizes.
+
+There is no fallback: if the HIP library is missing or the device is not gfx950, every entry point
+raises.  Arrays are numpy; the library copies them during the call (caller-owned host memory).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent.parent  # janus-crdt_amd/
+LIB_PATH = Path(os.environ.get("JANUS_GPU_LIB", _PKG / "lib" / "libjanusgpu.so"))
+
+JG_OK, JG_EINVAL, JG_ENOMEM, JG_EOVERFLOW, JG_ETYPE, JG_EHIP, JG_ESTATE = range(7)
+NULL_ELEM = 0xFFFFFFFF
+REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8")])  # jg_tagrec
+
+# Every entry point include/janus_gpu.h declares (tests check the .so exports all of them).
+EXPORTS = [
+    "jg_abi_version", "jg_open", "jg_close", "jg_last_error", "jg_fence", "jg_stream",
+    "jg_pnc_create", "jg_pnc_destroy", "jg_pnc_write_rows", "jg_pnc_read_rows", "jg_pnc_merge_rows",
+    "jg_pnc_apply_ops", "jg_pnc_values",
+    "jg_rows_create", "jg_rows_destroy", "jg_rows_upload", "jg_pnc_merge_batch",
+    "jg_orset_create", "jg_orset_destroy", "jg_orset_load", "jg_orset_size", "jg_orset_read",
+    "jg_orset_merge", "jg_orset_merge_store", "jg_orset_union", "jg_orset_contains",
+    "jg_synth_pnc_store", "jg_synth_pnc_rows", "jg_synth_orset",
+]
+
+_u8p = C.POINTER(C.c_uint8)
+_vp = C.c_void_p
+_u64 = C.c_uint64
+_u32 = C.c_uint32
+_SIGS = {
+    "jg_abi_version": ([], C.c_int),
+    "jg_open": ([C.c_int, C.POINTER(_vp)], C.c_int),
+    "jg_close": ([_vp], C.c_int),
+    "jg_last_error": ([C.c_char_p, C.c_size_t], C.c_int),
+    "jg_fence": ([_vp], C.c_int),
+    "jg_stream": ([_vp, C.POINTER(_vp)], C.c_int),
+    "jg_pnc_create": ([_vp, _u64, _u32, _u32, C.POINTER(_vp)], C.c_int),
+    "jg_pnc_destroy": ([_vp], C.c_int),
+    "jg_pnc_write_rows": ([_vp, _vp, _u64, _vp, _vp], C.c_int),
+    "jg_pnc_read_rows": ([_vp, _vp, _u64, _vp, _vp], C.c_int),
+    "jg_pnc_merge_rows": ([_vp, _vp, _u64, _vp, _vp], C.c_int),
+    "jg_pnc_apply_ops": ([_vp, _u64, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_values": ([_vp, _vp, _u64, _vp, _vp], C.c_int),
+    "jg_rows_create": ([_vp, _u64, _u32, _u32, C.POINTER(_vp)], C.c_int),
+    "jg_rows_destroy": ([_vp], C.c_int),
+    "jg_rows_upload": ([_vp, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_merge_batch": ([_vp, _vp, C.c_int], C.c_int),
+    "jg_orset_create": ([_vp, _u64, _u64, C.POINTER(_vp)], C.c_int),
+    "jg_orset_destroy": ([_vp], C.c_int),
+    "jg_orset_load": ([_vp, _vp, _u64, _vp, _u64], C.c_int),
+    "jg_orset_size": ([_vp, C.POINTER(_u64), C.POINTER(_u64)], C.c_int),
+    "jg_orset_read": ([_vp, _vp, _u64, _vp, _u64], C.c_int),
+    "jg_orset_merge": ([_vp, _vp, _u64, _vp, _u64], C.c_int),
+    "jg_orset_merge_store": ([_vp, _vp, C.c_int], C.c_int),
+    "jg_orset_union": ([_vp, _vp, _vp, C.c_int], C.c_int),
+    "jg_orset_contains": ([_vp, _vp, _vp, _u64, _vp], C.c_int),
+    "jg_synth_pnc_store": ([_vp, _u64], C.c_int),
+    "jg_synth_pnc_rows": ([_vp, _u64, _u64], C.c_int),
+    "jg_synth_orset": ([_vp, _u64, _u64, _u32, _u32, _u32, _u32, _u32], C.c_int),
+}
+
+
+class JanusError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+_lib: C.CDLL | None = None
+
+
+def load(path: str | os.PathLike | None = None) -> C.CDLL:
+    """Load libjanusgpu.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise FileNotFoundError(f"libjanusgpu not built: {p} (run __graft_entry__.build())")
+    lib = C.CDLL(str(p))
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != JG_OK:
+        buf = C.create_string_buffer(1024)
+        load().jg_last_error(buf, 1024)
+        raise JanusError(rc, buf.value.decode(errors="replace"))
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def _arr(a, dtype) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class Context:
+    """One device + one HIP stream (jg_open)."""
+
+    def __init__(self, device: int = 0):
+        self._h = _vp()
+        _check(load().jg_open(device, C.byref(self._h)))
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def fence(self) -> None:
+        _check(load().jg_fence(self._h))
+
+    def stream(self) -> int:
+        s = _vp()
+        _check(load().jg_stream(self._h, C.byref(s)))
+        return s.value or 0
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_close(self._h))
+            self._h = _vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def _elem_dtype(eb: int):
+    return np.int32 if eb == 4 else np.int64
+
+
+class Rows:
+    """Device-resident batch of received PN-Counter rows (jg_rows)."""
+
+    def __init__(self, ctx: Context, n_rows: int, n_replicas: int, elem_bytes: int = 8):
+        self.ctx, self.n_rows, self.R, self.eb = ctx, n_rows, n_replicas, elem_bytes
+        self._h = _vp()
+        _check(load().jg_rows_create(ctx.handle, n_rows, n_replicas, elem_bytes, C.byref(self._h)))
+
+    def upload(self, P, N, key_idx=None) -> None:
+        dt = _elem_dtype(self.eb)
+        P, N = _arr(P, dt), _arr(N, dt)
+        assert P.size == N.size == self.n_rows * self.R
+        k = None if key_idx is None else _arr(key_idx, np.uint32)
+        _check(load().jg_rows_upload(self._h, _ptr(k), _ptr(P), _ptr(N)))
+
+    def synth(self, seed: int, key0: int = 0) -> None:
+        _check(load().jg_synth_pnc_rows(self._h, seed, key0))
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_rows_destroy(self._h))
+            self._h = _vp()
+
+
+class PNCStore:
+    """PN-Counter store [n_keys x n_replicas] (jg_pnc)."""
+
+    ABSENT = {4: np.iinfo(np.int32).min, 8: np.iinfo(np.int64).min}
+
+    def __init__(self, ctx: Context, n_keys: int, n_replicas: int, elem_bytes: int = 8):
+        self.ctx, self.n_keys, self.R, self.eb = ctx, n_keys, n_replicas, elem_bytes
+        self.dtype = _elem_dtype(elem_bytes)
+        self._h = _vp()
+        _check(load().jg_pnc_create(ctx.handle, n_keys, n_replicas, elem_bytes, C.byref(self._h)))
+
+    def _rows(self, P, N):
+        P, N = _arr(P, self.dtype), _arr(N, self.dtype)
+        if P.shape != N.shape or P.size % self.R:
+            raise ValueError("P/N must be [n_rows x R] of the store's width")
+        return P, N, P.size // self.R
+
+    def write_rows(self, P, N, key_idx=None) -> None:
+        P, N, n = self._rows(P, N)
+        k = None if key_idx is None else _arr(key_idx, np.uint32)
+        _check(load().jg_pnc_write_rows(self._h, _ptr(k), n, _ptr(P), _ptr(N)))
+
+    def read_rows(self, key_idx=None, n: int | None = None):
+        k = None if key_idx is None else _arr(key_idx, np.uint32)
+        n = (self.n_keys if n is None else n) if k is None else k.size
+        P = np.empty((n, self.R), self.dtype)
+        N = np.empty((n, self.R), self.dtype)
+        _check(load().jg_pnc_read_rows(self._h, _ptr(k), n, _ptr(P), _ptr(N)))
+        return P, N
+
+    def merge_rows(self, P, N, key_idx=None) -> None:
+        P, N, n = self._rows(P, N)
+        k = None if key_idx is None else _arr(key_idx, np.uint32)
+        _check(load().jg_pnc_merge_rows(self._h, _ptr(k), n, _ptr(P), _ptr(N)))
+
+    def merge_batch(self, rows: Rows, async_: bool = False) -> None:
+        _check(load().jg_pnc_merge_batch(self._h, rows._h, 1 if async_ else 0))
+
+    def apply_ops(self, key, col, delta, is_n) -> None:
+        key, col = _arr(key, np.uint32), _arr(col, np.uint32)
+        delta, is_n = _arr(delta, np.int64), _arr(is_n, np.uint8)
+        _check(load().jg_pnc_apply_ops(self._h, key.size, _ptr(key), _ptr(col), _ptr(delta), _ptr(is_n)))
+
+    def values(self, key_idx=None, n: int | None = None):
+        k = None if key_idx is None else _arr(key_idx, np.uint32)
+        n = (self.n_keys if n is None else n) if k is None else k.size
+        out = np.empty(n, np.int64)
+        ovf = np.empty(n, np.uint8)
+        _check(load().jg_pnc_values(self._h, _ptr(k), n, _ptr(out), _ptr(ovf)))
+        return out, ovf
+
+    def synth(self, seed: int) -> None:
+        _check(load().jg_synth_pnc_store(self._h, seed))
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_pnc_destroy(self._h))
+            self._h = _vp()
+
+
+def records(key=None, tag_lo=None, tag_hi=None, n: int = 0) -> np.ndarray:
+    r = np.zeros(n if key is None else len(key), REC_DTYPE)
+    if key is not None:
+        r["key"], r["tag_lo"], r["tag_hi"] = key, tag_lo, tag_hi
+    return r
+
+
+class ORSetStore:
+    """OR-Set store: sorted add and tombstone tag-record streams (jg_orset)."""
+
+    def __init__(self, ctx: Context, cap_add: int = 0, cap_rem: int = 0):
+        self.ctx = ctx
+        self._h = _vp()
+        _check(load().jg_orset_create(ctx.handle, cap_add, cap_rem, C.byref(self._h)))
+
+    def load(self, add, rem) -> None:
+        add, rem = _arr(add, REC_DTYPE), _arr(rem, REC_DTYPE)
+        _check(load().jg_orset_load(self._h, _ptr(add), add.size, _ptr(rem), rem.size))
+
+    def size(self):
+        a, r = _u64(), _u64()
+        _check(load().jg_orset_size(self._h, C.byref(a), C.byref(r)))
+        return a.value, r.value
+
+    def read(self):
+        na, nr = self.size()
+        add, rem = np.empty(na, REC_DTYPE), np.empty(nr, REC_DTYPE)
+        _check(load().jg_orset_read(self._h, _ptr(add), na, _ptr(rem), nr))
+        return add, rem
+
+    def merge(self, add, rem) -> None:
+        add, rem = _arr(add, REC_DTYPE), _arr(rem, REC_DTYPE)
+        _check(load().jg_orset_merge(self._h, _ptr(add), add.size, _ptr(rem), rem.size))
+
+    def merge_store(self, src: "ORSetStore", async_: bool = False) -> None:
+        _check(load().jg_orset_merge_store(self._h, src._h, 1 if async_ else 0))
+
+    @staticmethod
+    def union(a: "ORSetStore", b: "ORSetStore", out: "ORSetStore", async_: bool = False) -> None:
+        _check(load().jg_orset_union(a._h, b._h, out._h, 1 if async_ else 0))
+
+    def contains(self, set_ids, elems) -> np.ndarray:
+        s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)
+        out = np.empty(s.size, np.uint8)
+        _check(load().jg_orset_contains(self._h, _ptr(s), _ptr(e), s.size, _ptr(out)))
+        return out
+
+    def synth(self, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0) -> None:
+        _check(load().jg_synth_orset(self._h, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0))
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_orset_destroy(self._h))
+            self._h = _vp()

@@ -1,0 +1,139 @@
+"""ctypes binding of the TEST-ONLY CPU oracle (oracle/capi.cpp).  Only tests/, smoke() and bench.py's
+cpu_baseline leg use this; the product path never does."""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB = ROOT / "oracle" / "build" / "liboracle.so"
+REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8")])
+NULL_ELEM = 0xFFFFFFFF
+
+_vp, _u64, _u32, _i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+_SIGS = {
+    "orc_version": ([], C.c_int),
+    "orc_synth_pnc_rows": ([_u64, _u32, _u64, _u64, _u32, _u32, _vp], None),
+    "orc_synth_orset": ([_u64, _u64, _u64, _u32, _u32, _u32, _vp], None),
+    "orc_pnc_merge_dense": ([_u64, _u32, _u32, _vp, _vp, _u64, _vp, _vp, _vp], C.c_int),
+    "orc_pnc_values_dense": ([_u64, _u32, _u32, _vp, _vp, _u64, _vp, _vp, _vp], C.c_int),
+    "orc_pnc_apply_ops_dense": ([_u64, _u32, _u32, _vp, _vp, _u64, _vp, _vp, _vp, _vp], C.c_int),
+    "orc_orset_merge": ([_vp, _u64, _vp, _u64, _vp, _u64, _vp, _u64, _vp, C.POINTER(_u64), _vp, C.POINTER(_u64)], C.c_int),
+    "orc_orset_contains": ([_vp, _u64, _vp, _u64, _u64, _vp, _vp, _vp], C.c_int),
+    "orc_orset_lookup_all": ([_vp, _u64, _vp, _u64, _u32, _vp, _u64], C.c_int64),
+    "orc_bench_pnc_merge": ([_u64, _u32, _u64, _i32, _i32], C.c_double),
+    "orc_bench_orset_merge": ([_u64, _u32, _u32, _u32, _u32, _u32, _u64, _i32, _i32], C.c_double),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            raise FileNotFoundError(f"oracle not built: {LIB} (make -C oracle)")
+        _lib = C.CDLL(str(LIB))
+        for n, (a, r) in _SIGS.items():
+            f = getattr(_lib, n)
+            f.argtypes, f.restype = a, r
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def _dt(eb):
+    return np.int32 if eb == 4 else np.int64
+
+
+# ---- synthetic inputs (host copy of janus-crdt_amd/csrc/synth.hip) ----
+def synth_pnc(seed: int, which: int, key0: int, n_keys: int, R: int, eb: int) -> np.ndarray:
+    out = np.empty((n_keys, R), _dt(eb))
+    lib().orc_synth_pnc_rows(seed, which, key0, n_keys, R, eb, _p(out))
+    return out
+
+
+def synth_orset(seed: int, first: int, n: int, elems_per_set: int, per_group: int, u0: int) -> np.ndarray:
+    out = np.empty(n, REC_DTYPE)
+    lib().orc_synth_orset(seed, first, n, elems_per_set, per_group, u0, _p(out))
+    return out
+
+
+# ---- PN-Counter ----
+def pnc_merge(AP, AN, BP, BN, key_idx=None):
+    """PNCounter.Merge of each received row into its key (dictionary-faithful); returns new (P, N)."""
+    eb = AP.dtype.itemsize
+    AP, AN = np.array(AP, copy=True), np.array(AN, copy=True)
+    BP, BN = np.ascontiguousarray(BP), np.ascontiguousarray(BN)
+    n_keys, R = AP.shape
+    k = None if key_idx is None else np.ascontiguousarray(key_idx, np.uint32)
+    n_rows = BP.shape[0]
+    rc = lib().orc_pnc_merge_dense(n_keys, R, eb, _p(AP), _p(AN), n_rows, _p(k), _p(BP), _p(BN))
+    assert rc == 0, rc
+    return AP, AN
+
+
+def pnc_values(P, N, key_idx=None):
+    eb = P.dtype.itemsize
+    P, N = np.ascontiguousarray(P), np.ascontiguousarray(N)
+    n_keys, R = P.shape
+    k = None if key_idx is None else np.ascontiguousarray(key_idx, np.uint32)
+    n = n_keys if k is None else k.size
+    out, ovf = np.empty(n, np.int64), np.empty(n, np.uint8)
+    assert lib().orc_pnc_values_dense(n_keys, R, eb, _p(P), _p(N), n, _p(k), _p(out), _p(ovf)) == 0
+    return out, ovf
+
+
+def pnc_apply_ops(P, N, key, col, delta, is_n):
+    eb = P.dtype.itemsize
+    P, N = np.array(P, copy=True), np.array(N, copy=True)
+    n_keys, R = P.shape
+    key, col = np.ascontiguousarray(key, np.uint32), np.ascontiguousarray(col, np.uint32)
+    delta, is_n = np.ascontiguousarray(delta, np.int64), np.ascontiguousarray(is_n, np.uint8)
+    assert lib().orc_pnc_apply_ops_dense(n_keys, R, eb, _p(P), _p(N), key.size, _p(key), _p(col), _p(delta), _p(is_n)) == 0
+    return P, N
+
+
+# ---- OR-Set ----
+def _recs(a):
+    return np.ascontiguousarray(a, REC_DTYPE)
+
+
+def orset_merge(La, Lr, Ra, Rr):
+    """ORSet.Merge per set (dictionary-faithful), exported canonically sorted."""
+    La, Lr, Ra, Rr = map(_recs, (La, Lr, Ra, Rr))
+    oa = np.empty(La.size + Ra.size, REC_DTYPE)
+    orr = np.empty(Lr.size + Rr.size, REC_DTYPE)
+    na, nr = _u64(), _u64()
+    assert lib().orc_orset_merge(_p(La), La.size, _p(Lr), Lr.size, _p(Ra), Ra.size, _p(Rr), Rr.size,
+                                 _p(oa), C.byref(na), _p(orr), C.byref(nr)) == 0
+    return oa[: na.value], orr[: nr.value]
+
+
+def orset_contains(A, Rm, sets, elems):
+    A, Rm = _recs(A), _recs(Rm)
+    s, e = np.ascontiguousarray(sets, np.uint32), np.ascontiguousarray(elems, np.uint32)
+    out = np.empty(s.size, np.uint8)
+    assert lib().orc_orset_contains(_p(A), A.size, _p(Rm), Rm.size, s.size, _p(s), _p(e), _p(out)) == 0
+    return out
+
+
+def orset_lookup_all(A, Rm, set_id, cap=1 << 16):
+    A, Rm = _recs(A), _recs(Rm)
+    out = np.empty(cap, np.uint32)
+    n = lib().orc_orset_lookup_all(_p(A), A.size, _p(Rm), Rm.size, set_id, _p(out), cap)
+    assert n >= 0
+    return out[:n]
+
+
+# ---- CPU baseline ----
+def bench_pnc_merge(n_keys, R, seed, threads=1, reps=5) -> float:
+    return lib().orc_bench_pnc_merge(n_keys, R, seed, threads, reps)
+
+
+def bench_orset_merge(n_sets, E, a, ov, t, tov, seed, threads=1, reps=5) -> float:
+    return lib().orc_bench_orset_merge(n_sets, E, a, ov, t, tov, seed, threads, reps)

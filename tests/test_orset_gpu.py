@@ -1,0 +1,193 @@
+"""GPU parity of the OR-Set path (through the C ABI) against the oracle.
+
+Oracle = dictionary-faithful ORSet<string?> (oracle/oracle.hpp) pinned by the reference's
+ORSetTests.cs known answers; comparisons are exact on canonical (sorted) record streams.
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import janus_gpu as jg
+import oracle_ref as orc
+from gen import random_orset_pair, recs
+
+pytestmark = pytest.mark.gpu
+
+
+def _store(ctx, add, rem):
+    s = jg.ORSetStore(ctx, len(add), len(rem))
+    s.load(add, rem)
+    return s
+
+
+def _queries(n_sets, n_elems):
+    sets = np.repeat(np.arange(n_sets + 1, dtype=np.uint32), n_elems + 2)
+    elems = np.tile(np.array(list(range(n_elems + 1)) + [jg.NULL_ELEM], np.uint32), n_sets + 1)
+    return sets, elems
+
+
+@pytest.mark.parametrize("seed,n_sets,n_elems,pool", [(1, 4, 3, 6), (2, 50, 20, 16), (3, 300, 30, 12), (4, 7, 500, 4)])
+def test_union_matches_oracle(ctx, seed, n_sets, n_elems, pool):
+    rng = np.random.default_rng(seed)
+    La, Lr, Ra, Rr = random_orset_pair(rng, n_sets=n_sets, n_elems=n_elems, pool=pool)
+    ea, er = orc.orset_merge(La, Lr, Ra, Rr)
+    a, b = _store(ctx, La, Lr), _store(ctx, Ra, Rr)
+    out = jg.ORSetStore(ctx, len(La) + len(Ra), len(Lr) + len(Rr))
+    try:
+        jg.ORSetStore.union(a, b, out)
+        ga, gr = out.read()
+        assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+        s, e = _queries(n_sets, min(n_elems, 40))
+        assert np.array_equal(out.contains(s, e), orc.orset_contains(ea, er, s, e))
+        # in-place merge of a device store and of host records give the same state
+        a.merge_store(b)
+        assert all(np.array_equal(x, y) for x, y in zip(a.read(), (ea, er)))
+        c = _store(ctx, Ra, Rr)
+        c.merge(La, Lr)
+        assert all(np.array_equal(x, y) for x, y in zip(c.read(), (ea, er)))
+        c.close()
+    finally:
+        for h in (a, b, out):
+            h.close()
+
+
+def _interleaved(n, start, step, tag_seed=0):
+    k = np.arange(start, start + step * n, step, dtype=np.uint64) // 7
+    lo = np.arange(start, start + step * n, step, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    return recs(k, lo, lo ^ np.uint64(tag_seed))
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2048, 2049, 50_000])
+def test_union_duplicates_and_tiles(ctx, n):
+    """All-duplicate, disjoint-interleaved and half-overlapping inputs across tile boundaries."""
+    A = _interleaved(n, 0, 2)
+    B = _interleaved(n, 1, 2)
+    empty = np.empty(0, jg.REC_DTYPE)
+    cases = [(A, A), (A, B), (A, np.unique(np.concatenate([A[::2], B[: n // 2]]))), (A, empty), (empty, B)]
+    for x, y in cases:
+        exp = np.unique(np.concatenate([x, y]))
+        a, b = _store(ctx, x, empty), _store(ctx, y, empty)
+        out = jg.ORSetStore(ctx, len(x) + len(y), 0)
+        try:
+            jg.ORSetStore.union(a, b, out)
+            ga, gr = out.read()
+            assert np.array_equal(ga, exp) and gr.size == 0
+        finally:
+            for h in (a, b, out):
+                h.close()
+
+
+def test_equal_keys_long_runs(ctx):
+    """One (set, elem) with 20k tags on each side: runs far longer than a tile; tag order decides."""
+    rng = np.random.default_rng(9)
+    lo = rng.integers(0, 1 << 62, 40_000, dtype=np.uint64)
+    hi = rng.integers(0, 1 << 62, 40_000, dtype=np.uint64)
+    key = np.full(40_000, (5 << 32) | 3, np.uint64)
+    A = recs(key[:25_000], lo[:25_000], hi[:25_000])
+    B = recs(key[15_000:], lo[15_000:], hi[15_000:])
+    exp = np.unique(np.concatenate([A, B]))
+    a, b = _store(ctx, A, A[:100]), _store(ctx, B, B[:50])
+    out = jg.ORSetStore(ctx, len(A) + len(B), 150)
+    try:
+        jg.ORSetStore.union(a, b, out)
+        ga, gr = out.read()
+        assert np.array_equal(ga, exp)
+        assert np.array_equal(gr, np.unique(np.concatenate([A[:100], B[:50]])))
+        assert out.contains([5], [3])[0] == 1
+    finally:
+        for h in (a, b, out):
+            h.close()
+
+
+def test_reference_scenarios_on_gpu(ctx):
+    """ORSetTests.cs:102-129 (Multiple) and :314-328 (MergeNull) replayed as record states."""
+    def rec(s, e, t):
+        return ((s << 32) | e, t, 7)
+
+    NUL = jg.NULL_ELEM
+    # set1 = {1: t1}, set2 = {2: t2}; set1 <- set2  => 1, 2 present
+    s1 = _store(ctx, np.array([rec(0, 1, 1)], jg.REC_DTYPE), np.empty(0, jg.REC_DTYPE))
+    s1.merge(np.array([rec(0, 2, 2)], jg.REC_DTYPE), np.empty(0, jg.REC_DTYPE))
+    assert list(s1.contains([0, 0], [1, 2])) == [1, 1]
+    # set1.Remove(2): tombstone its observed tags
+    s1.merge(np.empty(0, jg.REC_DTYPE), np.array([rec(0, 2, 2)], jg.REC_DTYPE))
+    assert list(s1.contains([0, 0], [1, 2])) == [1, 0]
+    # concurrent Add(2) on set1 vs Remove(2) on set2 -> add wins
+    s1.merge(np.array([rec(0, 2, 3)], jg.REC_DTYPE), np.empty(0, jg.REC_DTYPE))
+    assert list(s1.contains([0, 0], [1, 2])) == [1, 1]
+    s1.close()
+    # MergeNull: set1 {hi, null}; set2.Remove(null) was a no-op (empty message)
+    s2 = _store(ctx, np.array([rec(0, 4, 9), rec(0, NUL, 10)], jg.REC_DTYPE), np.empty(0, jg.REC_DTYPE))
+    s2.merge(np.empty(0, jg.REC_DTYPE), np.empty(0, jg.REC_DTYPE))
+    assert list(s2.contains([0, 0, 0], [4, NUL, 5])) == [1, 1, 0]
+    # RemoveNull: nullRemove = nullAdd -> null absent
+    s2.merge(np.empty(0, jg.REC_DTYPE), np.array([rec(0, NUL, 10)], jg.REC_DTYPE))
+    assert list(s2.contains([0], [NUL])) == [0]
+    s2.close()
+
+
+def test_unsorted_or_duplicate_input_rejected(ctx):
+    a = np.array([(5, 1, 1), (4, 1, 1)], jg.REC_DTYPE)
+    d = np.array([(5, 1, 1), (5, 1, 1)], jg.REC_DTYPE)
+    s = jg.ORSetStore(ctx, 4, 4)
+    try:
+        for bad in (a, d):
+            with pytest.raises(jg.JanusError) as e:
+                s.load(bad, np.empty(0, jg.REC_DTYPE))
+            assert e.value.code == jg.JG_ESTATE
+        s.load(np.sort(a), np.empty(0, jg.REC_DTYPE))  # the store stays usable
+        assert s.size() == (2, 0)
+    finally:
+        s.close()
+
+
+def test_golden_fixture(ctx):
+    z = np.load(Path(__file__).parent / "golden" / "orset_merge.npz")
+    s = _store(ctx, z["La"], z["Lr"])
+    try:
+        s.merge(z["Ra"], z["Rr"])
+        ga, gr = s.read()
+        assert np.array_equal(ga, z["out_add"]) and np.array_equal(gr, z["out_rem"])
+        assert np.array_equal(s.contains(z["q_set"], z["q_elem"]), z["contains"])
+    finally:
+        s.close()
+
+
+def test_synth_matches_host_generator(ctx):
+    s = jg.ORSetStore(ctx, 0, 0)
+    try:
+        s.synth(77, 1000, 10, 7, 3, 2, 1)
+        ga, gr = s.read()
+    finally:
+        s.close()
+    assert np.array_equal(ga, orc.synth_orset(77, 0, 7000, 10, 7, 3))
+    assert np.array_equal(gr, orc.synth_orset(77, 0, 2000, 10, 2, 1))
+
+
+def test_full_size_c3(ctx):
+    """BASELINE config C3: 1M sets x 10 elems; L = 100M adds + 20M tombstones, R the same size with
+    50 % of its adds (and tombstones) shared.  The union is known in closed form from the generator:
+    tags u in [0, 15) per group for adds, [0, 3) for tombstones — compared record for record."""
+    seed, G, E = 0x4A414E5553, 10_000_000, 10
+    L, R = jg.ORSetStore(ctx, 0, 0), jg.ORSetStore(ctx, 0, 0)
+    out = jg.ORSetStore(ctx, 200_000_000, 40_000_000)
+    try:
+        L.synth(seed, G, E, 10, 0, 2, 0)
+        R.synth(seed, G, E, 10, 5, 2, 1)
+        jg.ORSetStore.union(L, R, out)
+        assert out.size() == (150_000_000, 30_000_000)
+        ga, gr = out.read()
+        assert np.array_equal(gr, orc.synth_orset(seed, 0, 30_000_000, E, 3, 0))
+        del gr
+        for lo in range(0, 150_000_000, 25_000_000):
+            assert np.array_equal(ga[lo:lo + 25_000_000], orc.synth_orset(seed, lo, 25_000_000, E, 15, 0)), lo
+        del ga
+        rng = np.random.default_rng(3)
+        sets = rng.integers(0, G // E, 100_000).astype(np.uint32)
+        elems = rng.integers(0, E + 2, 100_000).astype(np.uint32)
+        got = out.contains(sets, elems)
+        assert np.array_equal(got, (elems < E).astype(np.uint8))  # 15 adds vs 3 tombstones: present
+    finally:
+        for h in (L, R, out):
+            h.close()
