@@ -20,7 +20,6 @@ import argparse
 import json
 import os
 import platform
-import subprocess
 import sys
 import time
 from pathlib import Path
@@ -81,27 +80,53 @@ class Sync:
             self.dist.destroy_process_group()
 
 
+class HipEvents:
+    """hipEvent pair on the library's own stream (the stream the kernels are launched on), via ctypes
+    on libamdhip64 — torch.cuda.Event only sees torch's streams."""
+
+    def __init__(self, stream: int):
+        import ctypes as C
+        self.C = C
+        self.hip = C.CDLL("libamdhip64.so")
+        self.stream = C.c_void_p(stream)
+        self.e = [C.c_void_p(), C.c_void_p()]
+        for e in self.e:
+            assert self.hip.hipEventCreate(C.byref(e)) == 0
+
+    def record(self, i: int):
+        assert self.hip.hipEventRecord(self.e[i], self.stream) == 0
+
+    def elapsed_s(self) -> float:
+        C = self.C
+        assert self.hip.hipEventSynchronize(self.e[1]) == 0
+        ms = C.c_float()
+        assert self.hip.hipEventElapsedTime(C.byref(ms), self.e[0], self.e[1]) == 0
+        return ms.value / 1e3
+
+    def close(self):
+        for e in self.e:
+            self.hip.hipEventDestroy(e)
+
+
 def timed(ctx, sync, fn, steps, warmup):
     """Run fn() warmup+steps times; returns (max-over-ranks wall seconds, event seconds) of the K steps."""
-    import torch
-    stream = torch.cuda.ExternalStream(ctx.stream())
+    ev = HipEvents(ctx.stream())
     for _ in range(warmup):
         fn()
     ctx.fence()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     sync.barrier()
     ctx.fence()
     t0 = time.perf_counter()
-    e0.record(stream)
+    ev.record(0)
     for _ in range(steps):
         fn()
-    e1.record(stream)
+    ev.record(1)
     ctx.fence()
     sync.barrier()
     wall = time.perf_counter() - t0
-    e1.synchronize()
-    ev = e0.elapsed_time(e1) / 1e3
-    return sync.max(wall), sync.max(ev)
+    ev_s = ev.elapsed_s()
+    ev.close()
+    return sync.max(wall), sync.max(ev_s)
 
 
 def cpu_info():
@@ -136,7 +161,6 @@ def bench_pnc(jg, ctx, sync, rank, world, steps, warmup):
     store.synth(SEED + rank)
     rows.synth(SEED + rank, key0=0)
     wall, ev = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, warmup)
-    # smoke parity on a handful of rows (host restatement of the max rule; full parity lives in tests/)
     store.close()
     rows.close()
     cells = n_keys * PNC_R
