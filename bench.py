@@ -254,7 +254,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0] if traffic else None,
-                         "kernel": "k_merge_dense<8,4>", "algorithmic_bytes_per_launch": p["bytes_per_launch"],
+                         "kernel": "k_merge_dense<8>", "algorithmic_bytes_per_launch": p["bytes_per_launch"],
                          "kernel_ms": kern * 1e3, "traffic_source": traffic[1] if traffic else None},
         })
     if "orset" in res:

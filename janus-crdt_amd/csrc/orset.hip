@@ -21,240 +21,20 @@
 #include <vector>
 
 #include "jg_internal.hpp"
+#include "orset_union.hpp"
 
 namespace {
 
-constexpr int kOB = 256;        // threads per workgroup
-constexpr int kItems = 8;       // records per thread per tile
+// Tile shape chosen by measurement (tools/tune_orset.hip; profiles/r01/tune_orset_*.txt): 512 x 6 =
+// 3072 records per tile, 74 KB LDS, 2 workgroups per CU.
+constexpr int kOB = 512;   // threads per workgroup
+constexpr int kItems = 6;  // records per thread per tile
 constexpr int kTile = kOB * kItems;
 
-constexpr unsigned long long kFlagAgg = 1ull << 62;
-constexpr unsigned long long kFlagIncl = 2ull << 62;
-constexpr unsigned long long kValMask = (1ull << 62) - 1;
-constexpr unsigned kSpinLimit = 1u << 22;
-
-struct Tag { unsigned long long lo, hi; };
-
-__device__ __forceinline__ Tag ld_tag(const uint4* p) { return __builtin_bit_cast(Tag, *p); }
-__device__ __forceinline__ uint4 to_u4(Tag t) { return __builtin_bit_cast(uint4, t); }
-
-// Branch-free lexicographic compare on (key, tag.lo, tag.hi), unsigned.
-__device__ __forceinline__ bool rec_lt(unsigned long long ka, Tag ta, unsigned long long kb, Tag tb) {
-    return (ka < kb) | ((ka == kb) & ((ta.lo < tb.lo) | ((ta.lo == tb.lo) & (ta.hi < tb.hi))));
-}
-__device__ __forceinline__ bool rec_eq(unsigned long long ka, Tag ta, unsigned long long kb, Tag tb) {
-    return (ka == kb) & (ta.lo == tb.lo) & (ta.hi == tb.hi);
-}
-
-// Merge-path split for diagonal d over (a, b): number of A records among the first d merged.
-__global__ __launch_bounds__(kOB) void k_partition(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                                   const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                                   uint64_t n_parts, uint64_t* __restrict__ part) {
-    const uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x;
-    if (i >= n_parts) return;
-    const uint64_t total = na + nb;
-    const uint64_t d = i * kTile < total ? i * kTile : total;
-    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        const unsigned long long ka = ak[mid], kb = bk[d - 1 - mid];
-        bool a_le_b;  // a[mid] <= b[d-1-mid]  -> take more from A
-        if (ka != kb) a_le_b = ka < kb;
-        else a_le_b = !rec_lt(kb, ld_tag(bt + d - 1 - mid), ka, ld_tag(at + mid));
-        if (a_le_b) lo = mid + 1;
-        else hi = mid;
-    }
-    part[i] = lo;
-}
-
-// Wave 0 of a tile: sum the counts of all earlier tiles (decoupled look-back).
-__device__ unsigned long long lookback(unsigned long long* status, long long tile, int lane, unsigned* err) {
-    unsigned long long excl = 0;
-    long long base = tile - 1;
-    for (;;) {
-        const long long idx = base - lane;
-        unsigned long long w;
-        unsigned spins = 0;
-        for (;;) {
-            w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
-            if (__all((w >> 62) != 0)) break;
-            if (++spins > kSpinLimit) {  // wave-uniform: give up, flag the call, let the grid drain
-                if (lane == 0) atomicOr(err, 1u);
-                w = kFlagIncl;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const unsigned long long incl = __ballot((w >> 62) == 2);
-        const int first = incl ? __ffsll((long long)incl) - 1 : 64;
-        unsigned long long v = lane <= first ? (w & kValMask) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        excl += v;
-        if (incl) return excl;
-        base -= 64;
-    }
-}
-
-__global__ __launch_bounds__(kOB) void k_union(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                               const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                               const uint64_t* __restrict__ part, uint64_t n_tiles,
-                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
-                                               unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
-                                               unsigned* err) {
-    __shared__ unsigned long long s_key[kTile];
-    __shared__ uint4 s_tag[kTile];
-    __shared__ unsigned long long s_prev_key;
-    __shared__ uint4 s_prev_tag;
-    __shared__ int s_has_prev;
-    __shared__ unsigned s_tile;
-    __shared__ unsigned long long s_excl;
-    __shared__ int s_wsum[kOB / 64];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint64_t tile = s_tile;
-    const uint64_t total_in = na + nb;
-    const uint64_t d0 = tile * kTile;
-    const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
-    const uint64_t i0 = part[tile], i1 = part[tile + 1];
-    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
-    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0), n = nA + nB;
-
-    // ---- stage the tile's A and B slices in LDS ----
-    // Loads are unconditional (index clamped into the tile, n >= 1) so all 2 x kItems of them are
-    // in flight before the first LDS write; only the LDS writes are predicated.
-    {
-        unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {
-            const int x = min(it * kOB + tid, n - 1);
-            const bool from_a = x < nA;
-            const uint64_t gi = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
-            rk[it] = (from_a ? ak : bk)[gi];
-            const Tag t = ld_tag((from_a ? at : bt) + gi);
-            rlo[it] = t.lo;
-            rhi[it] = t.hi;
-        }
-        if (tid == 0) {
-            s_has_prev = i0 > 0;
-            if (i0 > 0) { s_prev_key = ak[i0 - 1]; s_prev_tag = at[i0 - 1]; }
-        }
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
-            const int x = it * kOB + tid;
-            s_key[x] = rk[it];
-            s_tag[x] = to_u4(Tag{rlo[it], rhi[it]});
-        }
-    }
-    __syncthreads();
-
-    // ---- per-thread merge path + serial merge of kItems outputs ----
-    const int diag = min(tid * kItems, n);
-    int lo = diag > nB ? diag - nB : 0, hi = min(diag, nA);
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const int bj = nA + diag - 1 - mid;
-        const bool a_le_b = !rec_lt(s_key[bj], __builtin_bit_cast(Tag, s_tag[bj]), s_key[mid], __builtin_bit_cast(Tag, s_tag[mid]));
-        if (a_le_b) lo = mid + 1;
-        else hi = mid;
-    }
-    int ai = lo, bi = diag - lo;
-    bool hp;
-    unsigned long long pk;
-    Tag pt;
-    if (ai > 0) { hp = true; pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); }
-    else { hp = s_has_prev != 0; pk = s_prev_key; pt = __builtin_bit_cast(Tag, s_prev_tag); }
-
-    const int my_n = n - diag < kItems ? n - diag : kItems;
-    unsigned long long ka = 0, kb = 0;
-    Tag ta{0, 0}, tb{0, 0};
-    if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
-    if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
-    int src[kItems];
-    unsigned keep = 0;
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {
-        src[it] = 0;
-        if (it < my_n) {
-            const bool take_a = ai < nA && (bi >= nB || !rec_lt(kb, tb, ka, ta));
-            if (take_a) {
-                src[it] = ai;
-                keep |= 1u << it;
-                hp = true; pk = ka; pt = ta;
-                ++ai;
-                if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
-            } else {
-                src[it] = nA + bi;
-                if (!(hp && rec_eq(pk, pt, kb, tb))) keep |= 1u << it;
-                ++bi;
-                if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
-            }
-        }
-    }
-
-    // ---- block scan of kept counts ----
-    const int cnt = __popc(keep);
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) s_wsum[wid] = incl;
-    __syncthreads();
-    int wbase = 0, block_total = 0;
-#pragma unroll
-    for (int w = 0; w < kOB / 64; ++w) {
-        const int v = s_wsum[w];
-        if (w < wid) wbase += v;
-        block_total += v;
-    }
-    const int my_off = wbase + incl - cnt;
-
-    // ---- publish and look back (wave 0) ----
-    if (wid == 0) {
-        unsigned long long excl = 0;
-        if (tile == 0) {
-            if (lane == 0) __hip_atomic_store(status, kFlagIncl | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(status + tile, kFlagAgg | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            excl = lookback(status, (long long)tile, lane, err);
-            if (lane == 0)
-                __hip_atomic_store(status + tile, kFlagIncl | (excl + (unsigned long long)block_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_excl = excl;
-            if (tile == n_tiles - 1) *out_count = excl + (unsigned long long)block_total;
-        }
-    }
-
-    // ---- gather kept records, compact through LDS, store coalesced ----
-    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {  // src[it] is a valid LDS index even for dropped items
-        rk[it] = s_key[src[it]];
-        const Tag t = __builtin_bit_cast(Tag, s_tag[src[it]]);
-        rlo[it] = t.lo;
-        rhi[it] = t.hi;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {
-        if (keep & (1u << it)) {
-            const int o = my_off + __popc(keep & ((1u << it) - 1u));
-            s_key[o] = rk[it];
-            s_tag[o] = to_u4(Tag{rlo[it], rhi[it]});
-        }
-    }
-    __syncthreads();
-    const unsigned long long base = s_excl;
-    for (int x = tid; x < block_total; x += kOB) {
-        ok[base + x] = s_key[x];
-        ot[base + x] = s_tag[x];
-    }
-}
+using jgk::Tag;
+using jgk::ld_tag;
+using jgk::to_u4;
+using jgk::rec_lt;
 
 // Strictly increasing check: err |= 1 at the first non-increasing neighbour pair.
 __global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* __restrict__ k, const uint4* __restrict__ t, uint64_t n,
@@ -339,10 +119,10 @@ void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, j
     auto* ticket = reinterpret_cast<unsigned*>(ws + n_tiles * 8);
     auto* part = reinterpret_cast<uint64_t*>(ws + status_bytes);
     JG_HIP(hipMemsetAsync(ws, 0, status_bytes, ctx->stream));  // every polled word zeroed per call
-    hipLaunchKernelGGL(k_partition, dim3((unsigned)((n_tiles + 1 + kOB - 1) / kOB)), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(),
+    hipLaunchKernelGGL((jgk::k_partition<kOB, kItems>), dim3((unsigned)((n_tiles + 1 + kOB - 1) / kOB)), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(),
                        a.tag.as<uint4>(), a.n, b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, n_tiles + 1, part);
     JG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_union, dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(), a.tag.as<uint4>(), a.n,
+    hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(), a.tag.as<uint4>(), a.n,
                        b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, part, n_tiles, out.key.as<unsigned long long>(),
                        out.tag.as<uint4>(), status, ticket, d_count, ctx->flags.as<unsigned>());
     JG_HIP(hipGetLastError());

@@ -5,8 +5,8 @@
 //
 // Kernels and their roofline (HBM):
 //   k_merge_dense    A = max(A, B) over identity rows.  Reads A.P A.N B.P B.N, writes A.P A.N:
-//                    6 x elem_bytes per cell (48 B at int64).  16-B vectors, U vectors in flight
-//                    per lane, grid-stride.  This is PNCounter.Merge (PNCounters.cs:131-144).
+//                    6 x elem_bytes per cell (48 B at int64).  One 16-B vector per array per lane,
+//                    non-temporal.  This is PNCounter.Merge (PNCounters.cs:131-144).
 //   k_merge_indexed  scatter-max of received rows into their keys (atomicMax: rows may repeat a
 //                    key inside one committed batch, SafeCRDTManager.cs:122-146).
 //   k_apply_ops      Increment/Decrement (PNCounters.cs:97-112): wrapping atomic adds.
@@ -33,36 +33,32 @@ template <> __device__ __forceinline__ uint4 vmax<4>(uint4 a, uint4 b) {
     return __builtin_bit_cast(uint4, r);
 }
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load(const uint4* p) {
+    return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p)));
+}
+__device__ __forceinline__ void nt_store(uint4* p, uint4 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(v4u, v), reinterpret_cast<v4u*>(p));
+}
+
 template <int EB> struct Elem;
 template <> struct Elem<4> { using T = int; };
 template <> struct Elem<8> { using T = long long; };
 
-// Dense merge: nv 16-byte vectors per array, plus `tail` trailing cells (< 16 B) done by block 0.
-template <int EB, int U>
+// Dense merge: nv 16-byte vectors per array, one vector of each array per lane, plus `tail` trailing
+// cells (< 16 B) done by block 0.  Measured on MI355X against grid-stride / multi-vector-per-lane /
+// block-chunk variants (tools/tune_pnc.hip, profiles/r01/tune_pnc_*.txt): a flat grid with one
+// vector per lane and non-temporal loads/stores (every byte is touched once) was fastest.
+template <int EB>
 __global__ __launch_bounds__(kBlock) void k_merge_dense(uint4* __restrict__ AP, uint4* __restrict__ AN,
                                                         const uint4* __restrict__ BP, const uint4* __restrict__ BN,
                                                         uint64_t nv, uint32_t tail) {
     using T = typename Elem<EB>::T;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + (U - 1) * stride < nv; i += U * stride) {
-        uint4 ap[U], an[U], bp[U], bn[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            ap[u] = AP[i + u * stride];
-            bp[u] = BP[i + u * stride];
-            an[u] = AN[i + u * stride];
-            bn[u] = BN[i + u * stride];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            AP[i + u * stride] = vmax<EB>(ap[u], bp[u]);
-            AN[i + u * stride] = vmax<EB>(an[u], bn[u]);
-        }
-    }
-    for (; i < nv; i += stride) {
-        AP[i] = vmax<EB>(AP[i], BP[i]);
-        AN[i] = vmax<EB>(AN[i], BN[i]);
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < nv) {
+        const uint4 ap = nt_load(AP + i), bp = nt_load(BP + i), an = nt_load(AN + i), bn = nt_load(BN + i);
+        nt_store(AP + i, vmax<EB>(ap, bp));
+        nt_store(AN + i, vmax<EB>(an, bn));
     }
     if (blockIdx.x == 0 && threadIdx.x < tail) {
         T* ap = reinterpret_cast<T*>(AP + nv) + threadIdx.x;
@@ -214,14 +210,15 @@ void launch_merge_dense(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void
     const uint64_t bytes = n_cells * eb;
     const uint64_t nv = bytes / 16;
     const uint32_t tail = (uint32_t)((bytes - nv * 16) / eb);
-    constexpr int U = 4;
-    const unsigned grid = grid_for(ctx, (nv + U - 1) / U, 16);
+    const uint64_t blocks = (nv + kBlock - 1) / kBlock;
+    JG_REQUIRE(blocks < 0xFFFFFFFFull, JG_EINVAL, "merge: %llu cells exceed one launch", (unsigned long long)n_cells);
+    const unsigned grid = blocks ? (unsigned)blocks : 1u;
     if (eb == 8)
-        hipLaunchKernelGGL((k_merge_dense<8, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (uint4*)AP, (uint4*)AN,
-                           (const uint4*)BP, (const uint4*)BN, nv, tail);
+        hipLaunchKernelGGL(k_merge_dense<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, (uint4*)AP, (uint4*)AN, (const uint4*)BP,
+                           (const uint4*)BN, nv, tail);
     else
-        hipLaunchKernelGGL((k_merge_dense<4, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (uint4*)AP, (uint4*)AN,
-                           (const uint4*)BP, (const uint4*)BN, nv, tail);
+        hipLaunchKernelGGL(k_merge_dense<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, (uint4*)AP, (uint4*)AN, (const uint4*)BP,
+                           (const uint4*)BN, nv, tail);
     JG_HIP(hipGetLastError());
 }
 
