@@ -1,0 +1,162 @@
+// janus_host.cpp — see janus_host.hpp.
+#include "janus_host.hpp"
+
+#include <algorithm>
+#include <limits>
+
+namespace janus {
+
+namespace {
+std::string last_error() {
+    char buf[1024];
+    jg_last_error(buf, sizeof buf);
+    return buf;
+}
+bool rec_less(const jg_tagrec& a, const jg_tagrec& b) {
+    if (a.key != b.key) return a.key < b.key;
+    if (a.tag_lo != b.tag_lo) return a.tag_lo < b.tag_lo;
+    return a.tag_hi < b.tag_hi;
+}
+bool rec_eq(const jg_tagrec& a, const jg_tagrec& b) { return a.key == b.key && a.tag_lo == b.tag_lo && a.tag_hi == b.tag_hi; }
+void sort_unique(std::vector<jg_tagrec>& v) {
+    std::sort(v.begin(), v.end(), rec_less);
+    v.erase(std::unique(v.begin(), v.end(), rec_eq), v.end());
+}
+}  // namespace
+
+void GpuStableStore::check(int rc) const {
+    if (rc != JG_OK) throw EngineError(rc, last_error());
+}
+
+GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas, uint32_t elem_bytes)
+    : max_keys_(max_keys), R_(replicas), eb_(elem_bytes) {
+    check(jg_open(device, &ctx_));
+    check(jg_pnc_create(ctx_, max_keys, replicas, elem_bytes, &pnc_));
+    check(jg_orset_create(ctx_, 0, 0, &orset_));
+}
+
+GpuStableStore::~GpuStableStore() {
+    if (orset_) jg_orset_destroy(orset_);
+    if (pnc_) jg_pnc_destroy(pnc_);
+    if (ctx_) jg_close(ctx_);
+}
+
+uint32_t GpuStableStore::column(PncKey& k, const Guid& g) {
+    auto it = k.cols.find(g);
+    if (it != k.cols.end()) return it->second;
+    if (k.cols.size() >= R_) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
+    const uint32_t c = (uint32_t)k.cols.size();
+    k.cols.emplace(g, c);
+    return c;
+}
+
+uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e, bool create) {
+    if (!e) return JG_NULL_ELEM;
+    auto it = s.elems.find(*e);
+    if (it != s.elems.end()) return it->second;
+    if (!create) return JG_NULL_ELEM - 1;  // never allocated: no records carry it
+    const uint32_t id = (uint32_t)s.elems.size();
+    if (id >= JG_NULL_ELEM - 1) throw EngineError(JG_ESTATE, "too many elements in one OR-Set");
+    s.elems.emplace(*e, id);
+    return id;
+}
+
+void GpuStableStore::CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid) {
+    if (type_.count(uid)) return;
+    type_[uid] = type;
+    if (type == CrdtType::PNCounter) {
+        if (next_row_ >= max_keys_) throw EngineError(JG_ESTATE, "PNCounter store full");
+        PncKey k;
+        k.row = next_row_++;
+        column(k, stableReplicaGuid);  // {self: 0} — the row is zero already
+        pnc_keys_.emplace(uid, std::move(k));
+    } else {
+        SetKey s;
+        s.set = next_set_++;
+        set_keys_.emplace(uid, std::move(s));
+    }
+}
+
+std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
+                                                     std::unordered_map<uint64_t, uint64_t>* tracker) {
+    std::vector<uint32_t> rows;
+    std::vector<int64_t> P64, N64;
+    std::vector<int32_t> P32, N32;
+    std::vector<jg_tagrec> adds, rems;
+    std::vector<uint64_t> completed;
+    const int64_t absent = eb_ == 4 ? (int64_t)std::numeric_limits<int32_t>::min() : std::numeric_limits<int64_t>::min();
+
+    for (const auto& list : updates)
+        for (const auto& block : list)
+            for (const auto& u : block.update) {
+                if (u.syncMsgType == NetworkProtocol::ManagerMsg_Create || u.uid.is_empty()) continue;
+                auto ty = type_.find(u.uid);
+                if (ty == type_.end()) continue;
+                if (u.type != ty->second) {  // ORSet.cs:288-291 / the PNCounter cast
+                    throw EngineError(JG_ETYPE, "committed state of the wrong CRDT type for its key");
+                }
+                if (ty->second == CrdtType::PNCounter) {
+                    PncKey& k = pnc_keys_.at(u.uid);
+                    const size_t base = rows.size() * R_;
+                    rows.push_back(k.row);
+                    if (eb_ == 4) { P32.resize(base + R_, (int32_t)absent); N32.resize(base + R_, (int32_t)absent); }
+                    else { P64.resize(base + R_, absent); N64.resize(base + R_, absent); }
+                    for (const auto& e : u.pnc.pVector) {
+                        const uint32_t c = column(k, e.first);
+                        if (eb_ == 4) P32[base + c] = (int32_t)e.second; else P64[base + c] = e.second;
+                    }
+                    for (const auto& e : u.pnc.nVector) {
+                        const uint32_t c = column(k, e.first);
+                        if (eb_ == 4) N32[base + c] = (int32_t)e.second; else N64[base + c] = e.second;
+                    }
+                } else {
+                    SetKey& s = set_keys_.at(u.uid);
+                    const uint64_t hi = (uint64_t)s.set << 32;
+                    for (const auto& e : u.orset.addSet) {
+                        if (e.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
+                        const uint64_t key = hi | elem_id(s, e.first, true);
+                        for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
+                    }
+                    for (const auto& e : u.orset.removeSet) {
+                        const uint64_t key = hi | elem_id(s, e.first, true);
+                        for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
+                    }
+                    for (const auto& g : u.orset.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+                    for (const auto& g : u.orset.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+                }
+                if (tracker) {
+                    auto tr = tracker->find(u.seq);
+                    if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
+                }
+            }
+
+    if (!rows.empty()) {
+        if (eb_ == 4) check(jg_pnc_merge_rows(pnc_, rows.data(), rows.size(), P32.data(), N32.data()));
+        else check(jg_pnc_merge_rows(pnc_, rows.data(), rows.size(), P64.data(), N64.data()));
+    }
+    if (!adds.empty() || !rems.empty()) {
+        sort_unique(adds);
+        sort_unique(rems);
+        check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
+    }
+    return completed;
+}
+
+int64_t GpuStableStore::QueryStablePNC(const Guid& uid) {
+    const PncKey& k = pnc_keys_.at(uid);
+    int64_t v = 0;
+    uint8_t ovf = 0;
+    check(jg_pnc_values(pnc_, &k.row, 1, &v, &ovf));
+    if (ovf) throw EngineError(JG_EOVERFLOW, "Arithmetic operation resulted in an overflow.");
+    return v;
+}
+
+bool GpuStableStore::QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem) {
+    SetKey& s = set_keys_.at(uid);
+    const uint32_t id = elem_id(s, elem, false);
+    uint8_t out = 0;
+    check(jg_orset_contains(orset_, &s.set, &id, 1, &out));
+    return out != 0;
+}
+
+}  // namespace janus

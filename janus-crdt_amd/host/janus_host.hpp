@@ -1,0 +1,117 @@
+// janus_host.hpp — host-side mirror of the reference's stable-apply surface over the C ABI.
+//
+// The reference host is C#/.NET (absent from this image), so this C++ layer plays the part the C#
+// integration plays: it keeps the reference's names and message shapes and turns
+// a DAG-committed wave into ONE batched engine call per CRDT type.
+//
+//   SafeCRDTManager.CreateSafeCRDT       (BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:61-101)
+//   SafeCRDTManager.HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160)   -> ApplyCommitted
+//   SafeCRDT.ApplyUpdateStable / QueryStable    (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:64-83)
+//   PNCounterWrapper.Query / ORSetWrapper.Query (PNCounterWrapper.cs:28, ORSetWrapper.cs:24-28)
+//
+// Interning: key uid -> row; per-key replica Guid -> column in first-insertion
+// order (= the stable Dictionary's enumeration order, so PNCounter.Get's checked Sum sees the same
+// prefix order); per-set element string -> elem id (null -> JG_NULL_ELEM).
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "janus_gpu.h"
+
+namespace janus {
+
+struct Guid {
+    uint64_t lo = 0, hi = 0;
+    bool operator==(const Guid& o) const { return lo == o.lo && hi == o.hi; }
+    bool is_empty() const { return lo == 0 && hi == 0; }
+};
+struct GuidHash {
+    size_t operator()(const Guid& g) const {
+        uint64_t x = g.lo ^ (g.hi * 0x9E3779B97F4A7C15ull);
+        x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 29;
+        return (size_t)x;
+    }
+};
+
+enum class CrdtType { PNCounter, ORSet };
+
+// Decoded PNCounterMsg (PNCounters.cs:13-50): entries in the message's dictionary order.
+struct PNCounterState {
+    std::vector<std::pair<Guid, int64_t>> pVector, nVector;
+};
+// Decoded ORSetMsg<string?> (ORSet.cs:15-70).
+struct ORSetState {
+    std::vector<std::pair<std::string, std::vector<Guid>>> addSet, removeSet;
+    std::vector<Guid> nullAddGuid, nullRemoveGuid;
+};
+
+// NetworkProtocol (MergeSharp/MergeSharp/proto/SyncProtocol.cs:12-62), message already decoded.
+struct NetworkProtocol {
+    enum SyncMsgType { ManagerMsg_Create = 0, CRDTMsg = 1 };
+    Guid uid;
+    SyncMsgType syncMsgType = CRDTMsg;
+    uint64_t seq = 0;  // identity of the message object for the safe-update tracker
+    CrdtType type = CrdtType::PNCounter;
+    PNCounterState pnc;
+    ORSetState orset;
+};
+struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
+    std::vector<NetworkProtocol> update;
+};
+
+struct EngineError : std::runtime_error {
+    int code;
+    EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// The stable copies of every key of one node, resident on one GPU.
+class GpuStableStore {
+  public:
+    GpuStableStore(int device, uint32_t max_keys, uint32_t replicas, uint32_t elem_bytes);
+    ~GpuStableStore();
+    GpuStableStore(const GpuStableStore&) = delete;
+    GpuStableStore& operator=(const GpuStableStore&) = delete;
+
+    // CreateSafeCRDT: the stable copy is a fresh instance (SafeCRDTManager.cs:68-69, 91-92); a
+    // PNCounter's own replica Guid takes column 0 with value 0 (PNCounters.cs:73-81).
+    void CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid = Guid{});
+
+    // HandleAfterConsensusUpdates: walk the committed wave in order, skip ManagerMsg_Create and
+    // Guid.Empty (:133-134) and unknown uids (:136), decode every state into one SoA batch per CRDT
+    // type, apply each batch with ONE engine call, then report the safe updates that completed, in
+    // commit order (:141-142).  `tracker` maps message seq -> client origin; matched entries are
+    // removed like ConcurrentDictionary.TryRemove.
+    std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
+                                         std::unordered_map<uint64_t, uint64_t>* tracker = nullptr);
+
+    // QueryStable: PNCounter.Get (throws EngineError JG_EOVERFLOW where the checked Sum would throw
+    // OverflowException) and ORSet.Contains.
+    int64_t QueryStablePNC(const Guid& uid);
+    bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
+
+    jg_ctx* ctx() const { return ctx_; }
+
+  private:
+    struct PncKey { uint32_t row; std::unordered_map<Guid, uint32_t, GuidHash> cols; };
+    struct SetKey { uint32_t set; std::unordered_map<std::string, uint32_t> elems; };
+    uint32_t column(PncKey& k, const Guid& g);
+    uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
+    void check(int rc) const;
+
+    jg_ctx* ctx_ = nullptr;
+    jg_pnc* pnc_ = nullptr;
+    jg_orset* orset_ = nullptr;
+    uint32_t max_keys_, R_, eb_;
+    uint32_t next_row_ = 0, next_set_ = 0;
+    std::unordered_map<Guid, CrdtType, GuidHash> type_;
+    std::unordered_map<Guid, PncKey, GuidHash> pnc_keys_;
+    std::unordered_map<Guid, SetKey, GuidHash> set_keys_;
+};
+
+}  // namespace janus

@@ -1,0 +1,176 @@
+// test_host.cpp — GPU parity of the committed-batch apply loop against the oracle.
+//
+// A 4-node cluster is simulated with the oracle (oracle/oracle.hpp: SafeCRDT + SafeCRDTManager,
+// pinned by the reference's KVStoreTests).  Random client updates (PNCounter Increment/Decrement,
+// ORSet Add/Remove/Clear, null elements, safe and non-safe) run on random nodes; every few updates
+// the submitted UpdateMessages of all nodes form a committed wave.  The wave is applied to every
+// oracle node (prospective merge on block receipt + HandleAfterConsensusUpdates) and, through
+// janus::GpuStableStore (one batched engine call per CRDT type), to node 0's stable state on the GPU.
+// After each wave every key's QueryStable (value / OverflowException / Contains of every element and
+// null) and the order of completed safe updates must match node 0 of the oracle exactly.
+// Exit 0 = parity; prints the first mismatch otherwise.
+#include <cstdio>
+#include <memory>
+
+#include "janus_host.hpp"
+#include "oracle.hpp"
+
+namespace {
+
+janus::Guid G(const oracle::Guid& g) { return janus::Guid{g.lo, g.hi}; }
+
+janus::NetworkProtocol convert(const oracle::NetworkProtocol& np) {
+    janus::NetworkProtocol o;
+    o.uid = G(np.uid);
+    o.syncMsgType = np.syncMsgType == oracle::NetworkProtocol::ManagerMsg_Create ? janus::NetworkProtocol::ManagerMsg_Create
+                                                                                  : janus::NetworkProtocol::CRDTMsg;
+    o.seq = np.seq;
+    if (np.message.type == oracle::CrdtType::PNCounter) {
+        o.type = janus::CrdtType::PNCounter;
+        for (const auto& e : np.message.pnc.pVector) o.pnc.pVector.emplace_back(G(e.first), e.second);
+        for (const auto& e : np.message.pnc.nVector) o.pnc.nVector.emplace_back(G(e.first), e.second);
+    } else {
+        o.type = janus::CrdtType::ORSet;
+        for (const auto& e : np.message.orset.addSet) {
+            std::vector<janus::Guid> tags;
+            for (const auto& g : e.second) tags.push_back(G(g));
+            o.orset.addSet.emplace_back(e.first, std::move(tags));
+        }
+        for (const auto& e : np.message.orset.removeSet) {
+            std::vector<janus::Guid> tags;
+            for (const auto& g : e.second) tags.push_back(G(g));
+            o.orset.removeSet.emplace_back(e.first, std::move(tags));
+        }
+        for (const auto& g : np.message.orset.nullAddGuid) o.orset.nullAddGuid.push_back(G(g));
+        for (const auto& g : np.message.orset.nullRemoveGuid) o.orset.nullRemoveGuid.push_back(G(g));
+    }
+    return o;
+}
+
+struct Rng {
+    uint64_t s;
+    uint64_t next() { s = oracle::mix64(s + 0x9E3779B97F4A7C15ull); return s; }
+    uint64_t below(uint64_t n) { return next() % n; }
+};
+
+int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batch, uint32_t eb) {
+    const int n_nodes = 4;
+    std::vector<std::unique_ptr<oracle::SafeCRDTManager>> nodes;
+    for (int i = 0; i < n_nodes; ++i) nodes.push_back(std::make_unique<oracle::SafeCRDTManager>(batch, seed * 31 + i));
+    janus::GpuStableStore gpu(0, n_pnc + 1, 8, eb);
+    std::vector<std::string> keys;
+    for (int k = 0; k < n_pnc + n_set; ++k) {
+        const bool is_pnc = k < n_pnc;
+        std::string key = (is_pnc ? "pnc" : "set") + std::to_string(k);
+        oracle::Guid uid = nodes[0]->gen.next();
+        for (auto& n : nodes) n->CreateSafeCRDT(key, is_pnc ? oracle::CrdtType::PNCounter : oracle::CrdtType::ORSet, uid);
+        oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(key);
+        gpu.CreateSafeCRDT(G(uid), is_pnc ? janus::CrdtType::PNCounter : janus::CrdtType::ORSet,
+                           is_pnc ? G(s0.pncStable->pnc.replicaIdx()) : janus::Guid{});
+        keys.push_back(key);
+    }
+    Rng rng{seed};
+    uint64_t origin = 1;
+    std::vector<uint64_t> gpu_done;
+    auto commit = [&]() -> int {
+        std::vector<std::vector<oracle::UpdateMessage>> wave;
+        for (auto& n : nodes) { wave.push_back(n->submitted); n->submitted.clear(); }
+        for (size_t r = 0; r < nodes.size(); ++r)  // prospective merge on block receipt
+            for (size_t src = 0; src < nodes.size(); ++src) {
+                if (src == r) continue;
+                for (const auto& um : wave[src])
+                    for (const auto& np : um.update) {
+                        oracle::SafeCRDT& sc = *nodes[r]->safeCRDTsIndexedByuid.at(np.uid);
+                        if (sc.type == oracle::CrdtType::PNCounter) sc.pncProspective->pnc.ApplySynchronizedUpdate(np.message.pnc);
+                        else sc.orProspective->orset.ApplySynchronizedUpdate(np.message.orset);
+                    }
+            }
+        std::vector<std::vector<janus::UpdateMessage>> jw;
+        for (const auto& list : wave) {
+            std::vector<janus::UpdateMessage> l;
+            for (const auto& um : list) {
+                janus::UpdateMessage m;
+                for (const auto& np : um.update) m.update.push_back(convert(np));
+                l.push_back(std::move(m));
+            }
+            jw.push_back(std::move(l));
+        }
+        std::unordered_map<uint64_t, uint64_t> tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
+        const size_t before = nodes[0]->notified.size();
+        for (auto& n : nodes) n->HandleAfterConsensusUpdates(wave);
+        auto done = gpu.ApplyCommitted(jw, &tracker);
+        std::vector<uint64_t> exp(nodes[0]->notified.begin() + before, nodes[0]->notified.end());
+        if (done != exp) { std::printf("FAIL safe-update notifications differ (%zu vs %zu)\n", done.size(), exp.size()); return 1; }
+        // compare every stable query on node 0
+        for (int k = 0; k < (int)keys.size(); ++k) {
+            oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(keys[k]);
+            if (k < n_pnc) {
+                bool o_ovf = false, g_ovf = false;
+                int64_t ov = 0, gv = 0;
+                try { ov = s0.QueryStable().i; } catch (const oracle::OverflowException&) { o_ovf = true; }
+                try { gv = gpu.QueryStablePNC(G(s0.guid)); } catch (const janus::EngineError& e) {
+                    if (e.code != JG_EOVERFLOW) throw;
+                    g_ovf = true;
+                }
+                if (o_ovf != g_ovf || ov != gv) {
+                    std::printf("FAIL %s: oracle %lld%s gpu %lld%s\n", keys[k].c_str(), (long long)ov, o_ovf ? " (overflow)" : "", (long long)gv,
+                                g_ovf ? " (overflow)" : "");
+                    return 1;
+                }
+            } else {
+                for (int e = -1; e < 10; ++e) {
+                    std::optional<std::string> el = e < 0 ? std::nullopt : std::optional<std::string>(std::to_string(e));
+                    std::vector<oracle::Arg> q{e < 0 ? oracle::Arg::N() : oracle::Arg::S(*el)};
+                    const bool o = s0.QueryStable(q).b, g = gpu.QueryStableORSet(G(s0.guid), el);
+                    if (o != g) { std::printf("FAIL %s elem %d: oracle %d gpu %d\n", keys[k].c_str(), e, o, g); return 1; }
+                }
+            }
+        }
+        return 0;
+    };
+    for (int i = 0; i < n_ops; ++i) {
+        const int node = (int)rng.below(n_nodes);
+        const int k = (int)rng.below(keys.size());
+        oracle::SafeCRDT& sc = *nodes[node]->safeCRDTs.at(keys[k]);
+        const bool safe = rng.below(2) == 0;
+        const uint64_t org = safe ? origin++ : 0;
+        if (k < n_pnc) {
+            const int op = 1 + (int)rng.below(2);
+            int64_t amt = 1 + (int64_t)rng.below(99);           // PNCWorkload.cs:63 Next(1,100)
+            if (eb == 4 && rng.below(50) == 0) amt = 0x7FFFFFF0 - (int64_t)rng.below(100);  // push toward the checked-Sum edge
+            sc.Update(op, {oracle::Arg::I(amt)}, safe, org);
+        } else {
+            const uint64_t r = rng.below(20);
+            const int e = (int)rng.below(10);
+            std::vector<oracle::Arg> a{rng.below(8) == 0 ? oracle::Arg::N() : oracle::Arg::S(std::to_string(e))};
+            if (r < 11) sc.Update(1, a, safe, org);
+            else if (r < 19) sc.Update(2, a, safe, org);
+            else sc.Update(3, {}, false, 0);
+        }
+        if ((i + 1) % wave_every == 0 && commit()) return 1;
+    }
+    if (commit()) return 1;
+    return 0;
+}
+
+}  // namespace
+
+int main() {
+    struct Case { uint64_t seed; int n_pnc, n_set, n_ops, wave_every, batch; uint32_t eb; };
+    const Case cases[] = {
+        {1, 6, 4, 400, 7, 1, 4},    // KVStoreTests: clientBatchSize = 1
+        {2, 20, 10, 3000, 97, 8, 4},  // batched client updates, state compaction (SafeCRDTManager.cs:165-198)
+        {3, 3, 3, 2000, 500, 1000, 4},  // JanusService: clientBatchSize = 1000, big waves, hot keys
+        {4, 10, 0, 1500, 50, 4, 8},   // long (int64) PN-Counter variant
+    };
+    int fails = 0;
+    for (const auto& c : cases) {
+        int rc = 1;
+        try { rc = run(c.seed, c.n_pnc, c.n_set, c.n_ops, c.wave_every, c.batch, c.eb); }
+        catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
+        std::printf("%s case seed=%llu pnc=%d sets=%d ops=%d wave=%d batch=%d eb=%u\n", rc ? "FAIL" : "PASS", (unsigned long long)c.seed, c.n_pnc,
+                    c.n_set, c.n_ops, c.wave_every, c.batch, c.eb);
+        fails += rc != 0;
+    }
+    return fails ? 1 : 0;
+}
