@@ -52,17 +52,23 @@ def dist_env():
 
 
 class Sync:
-    """Barrier + max-over-ranks; plain no-ops at world size 1."""
+    """Barrier + max-over-ranks; plain no-ops at world size 1.  backend "nccl" (RCCL) on the GPU box;
+    "gloo" on CPU (tests/test_dist.py)."""
 
-    def __init__(self, world, local):
+    def __init__(self, world, local, backend="nccl"):
         self.world = world
         self.dist = None
         if world > 1:
             import torch
             import torch.distributed as dist
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            self.dist, self.torch, self.dev = dist, torch, torch.device("cuda", local)
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                self.dev = torch.device("cuda", local)
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                self.dev = torch.device("cpu")
+                dist.init_process_group(backend)
+            self.dist, self.torch = dist, torch
 
     def barrier(self):
         if self.dist:

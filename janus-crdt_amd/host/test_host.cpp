@@ -71,7 +71,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     }
     Rng rng{seed};
     uint64_t origin = 1;
-    std::vector<uint64_t> gpu_done;
+    uint64_t n_ovf = 0, n_val = 0, n_in = 0, n_out = 0, n_done = 0, n_waves = 0;
     auto commit = [&]() -> int {
         std::vector<std::vector<oracle::UpdateMessage>> wave;
         for (auto& n : nodes) { wave.push_back(n->submitted); n->submitted.clear(); }
@@ -101,6 +101,8 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         auto done = gpu.ApplyCommitted(jw, &tracker);
         std::vector<uint64_t> exp(nodes[0]->notified.begin() + before, nodes[0]->notified.end());
         if (done != exp) { std::printf("FAIL safe-update notifications differ (%zu vs %zu)\n", done.size(), exp.size()); return 1; }
+        n_done += done.size();
+        ++n_waves;
         // compare every stable query on node 0
         for (int k = 0; k < (int)keys.size(); ++k) {
             oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(keys[k]);
@@ -112,6 +114,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
                     if (e.code != JG_EOVERFLOW) throw;
                     g_ovf = true;
                 }
+                (o_ovf ? n_ovf : n_val)++;
                 if (o_ovf != g_ovf || ov != gv) {
                     std::printf("FAIL %s: oracle %lld%s gpu %lld%s\n", keys[k].c_str(), (long long)ov, o_ovf ? " (overflow)" : "", (long long)gv,
                                 g_ovf ? " (overflow)" : "");
@@ -122,6 +125,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
                     std::optional<std::string> el = e < 0 ? std::nullopt : std::optional<std::string>(std::to_string(e));
                     std::vector<oracle::Arg> q{e < 0 ? oracle::Arg::N() : oracle::Arg::S(*el)};
                     const bool o = s0.QueryStable(q).b, g = gpu.QueryStableORSet(G(s0.guid), el);
+                    (o ? n_in : n_out)++;
                     if (o != g) { std::printf("FAIL %s elem %d: oracle %d gpu %d\n", keys[k].c_str(), e, o, g); return 1; }
                 }
             }
@@ -150,6 +154,9 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         if ((i + 1) % wave_every == 0 && commit()) return 1;
     }
     if (commit()) return 1;
+    std::printf("  waves %llu, safe completions %llu, Get: %llu values + %llu overflows, Contains: %llu true / %llu false\n",
+                (unsigned long long)n_waves, (unsigned long long)n_done, (unsigned long long)n_val, (unsigned long long)n_ovf,
+                (unsigned long long)n_in, (unsigned long long)n_out);
     return 0;
 }
 

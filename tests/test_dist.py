@@ -1,0 +1,55 @@
+"""CPU-only: the N>1 path of bench.py with world size 2 over gloo — keyspace shards are disjoint
+and cover N x the per-GPU shard (weak scaling), the barrier completes, and the timing reduction is
+the max over ranks (the driver launches bench.py with torch.distributed.run, one rank per GPU)."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT))
+    import bench
+    w, r, local = bench.dist_env()
+    sync = bench.Sync(w, local, backend="gloo")
+    sync.barrier()
+    key0, n = bench.shard_keys(bench.PNC_KEYS, r, w)
+    worst = sync.max(1.0 + r)  # rank r "took" 1 + r seconds
+    sync.barrier()
+    sync.close()
+    q.put((r, key0, n, worst))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_weak_scaling_shards_and_max_over_ranks(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    spans = [(k0, k0 + n) for _, k0, n, _ in res]
+    assert all(n == res[0][2] for _, _, n, _ in res)  # fixed per-GPU work
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 == b0  # disjoint, contiguous
+    assert spans[0][0] == 0 and spans[-1][1] == world * res[0][2]
+    assert all(w == float(world) for *_, w in res)  # max over ranks reached every rank
