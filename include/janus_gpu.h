@@ -124,6 +124,14 @@ int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_t
 int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async);
 /* out = a ∪ b (out must have capacity for a+b; it may not alias a or b). */
 int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int async);
+/* ORSet.Add / Remove / Clear (ORSet.cs:134-198), the OR-Set ApplyOp, applied in op order per set
+ * (ORSetWrapper.Update op ids, BFT-CRDT/SafeCRDTs/ORSetWrapper.cs:30-46): op[i] = 1 Add(elem[i]) with
+ * the fresh tag (tag_lo[i], tag_hi[i]) the caller drew (Guid.NewGuid()); 2 Remove(elem[i]) — tombstones
+ * every tag of the element's add set if Contains(elem) at that point; 3 Clear() of set[i].
+ * result[i] = the op's bool result (Remove: 0 when the element was absent).  Any other op id is
+ * JG_EINVAL before anything changes (the wrapper's InvalidOperationException). */
+int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op,
+                       const uint64_t* tag_lo, const uint64_t* tag_hi, uint8_t* result);
 /* ORSet.Contains (ORSet.cs:204-237) for (set[i], elem[i]): elem present iff its add set exists
  * and (it has no tombstone set or the two tag sets differ: !SetEquals); the null element is
  * present iff !SetEquals(nullRemove, nullAdd).  out[i] = 0/1. */

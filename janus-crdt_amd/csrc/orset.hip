@@ -18,6 +18,8 @@
 // ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams,
 // then SetEquals of the two sorted runs.
 #include <algorithm>
+#include <set>
+#include <unordered_map>
 #include <vector>
 
 #include "jg_internal.hpp"
@@ -92,6 +94,30 @@ __global__ __launch_bounds__(kOB) void k_contains(const unsigned long long* __re
     }
 }
 
+// Run bounds of each queried key in both streams: out[4i..4i+3] = a0, a1, r0, r1.
+__global__ __launch_bounds__(kOB) void k_runs(const unsigned long long* __restrict__ akey, uint64_t na, const unsigned long long* __restrict__ rkey,
+                                              uint64_t nr, const unsigned long long* __restrict__ q, uint64_t nq, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kOB) {
+        const unsigned long long key = q[i];
+        out[4 * i + 0] = lower_key(akey, na, key);
+        out[4 * i + 1] = upper_key(akey, na, key);
+        out[4 * i + 2] = lower_key(rkey, nr, key);
+        out[4 * i + 3] = upper_key(rkey, nr, key);
+    }
+}
+
+// Copy ranges [src_off[i], src_off[i] + len[i]) of a stream to dst[dst_off[i] ...] as AoS records.
+__global__ __launch_bounds__(kOB) void k_gather_ranges(const unsigned long long* __restrict__ k, const uint4* __restrict__ t,
+                                                       const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ len,
+                                                       const uint64_t* __restrict__ dst_off, uint64_t n, jg_tagrec* __restrict__ dst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        for (uint64_t j = 0; j < len[i]; ++j) {
+            const Tag g = ld_tag(t + src_off[i] + j);
+            dst[dst_off[i] + j] = jg_tagrec{k[src_off[i] + j], g.lo, g.hi};
+        }
+    }
+}
+
 unsigned grid_for(jg_ctx* ctx, uint64_t items, unsigned per_cu = 8) {
     uint64_t g = (items + kOB - 1) / kOB;
     const uint64_t cap = (uint64_t)ctx->num_cus * per_cu;
@@ -107,7 +133,8 @@ size_t union_ws_bytes(uint64_t total) {
 
 // Union of two streams into `out` (capacity checked by the caller).  Async on ctx->stream; the
 // output count lands in *d_count (device).  `ws` holds union_ws_bytes(a.n + b.n) bytes.
-void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws) {
+void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws,
+                  const unsigned* drop = nullptr) {
     const uint64_t total = a.n + b.n;
     if (total == 0) {
         JG_HIP(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), ctx->stream));
@@ -124,20 +151,21 @@ void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, j
     JG_HIP(hipGetLastError());
     hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(), a.tag.as<uint4>(), a.n,
                        b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, part, n_tiles, out.key.as<unsigned long long>(),
-                       out.tag.as<uint4>(), status, ticket, d_count, ctx->flags.as<unsigned>());
+                       out.tag.as<uint4>(), status, ticket, d_count, ctx->flags.as<unsigned>(), drop);
     JG_HIP(hipGetLastError());
 }
 
 // Union of both streams of two stores into `oa`/`orr`; counts to counted->counts.
-void union_store(jg_ctx* ctx, const jg_orset* a, const jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted) {
+void union_store(jg_ctx* ctx, const jg_orset* a, const jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted,
+                 const unsigned* drop = nullptr) {
     JG_REQUIRE(oa.cap >= a->add.n + b->add.n && orr.cap >= a->rem.n + b->rem.n, JG_ESTATE,
                "union: output capacity (%llu, %llu) < inputs (%llu, %llu)", (unsigned long long)oa.cap, (unsigned long long)orr.cap,
                (unsigned long long)(a->add.n + b->add.n), (unsigned long long)(a->rem.n + b->rem.n));
     unsigned long long* d = counted->counts.as<unsigned long long>();
     const size_t ws_add = union_ws_bytes(a->add.n + b->add.n);
     char* ws = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, ws_add + union_ws_bytes(a->rem.n + b->rem.n)));
-    launch_union(ctx, a->add, b->add, oa, d, ws);
-    launch_union(ctx, a->rem, b->rem, orr, d + 1, ws + ws_add);
+    launch_union(ctx, a->add, b->add, oa, d, ws, drop);
+    launch_union(ctx, a->rem, b->rem, orr, d + 1, ws + ws_add, drop);
     counted->counts_pending = true;
 }
 
@@ -176,19 +204,175 @@ void download_stream(jg_ctx* ctx, const jg_stream_soa& s, jg_tagrec* out) {
     JG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
-// In-place merge: s = s ∪ src (src may be a temporary store).
-void merge_into(jg_orset* s, const jg_orset* src, bool async) {
+// In-place merge: s = (s minus the records of sets flagged in `drop`) ∪ src.
+void merge_into(jg_orset* s, const jg_orset* src, bool async, const unsigned* drop = nullptr) {
     jg_ctx* ctx = s->ctx;
     jg::sync_counts(s);
     s->spare_add.reserve(s->add.n + src->add.n);
     s->spare_rem.reserve(s->rem.n + src->rem.n);
-    union_store(ctx, s, src, s->spare_add, s->spare_rem, s);
+    union_store(ctx, s, src, s->spare_add, s->spare_rem, s, drop);
     s->add.swap(s->spare_add);
     s->rem.swap(s->spare_rem);
     if (!async) {
         check_err_flag(ctx, "jg_orset_merge");
         jg::sync_counts(s);
     }
+}
+
+// Records of the queried keys (sorted, unique) currently in the store, per key.
+struct Runs {
+    std::vector<jg_tagrec> add, rem;
+    std::vector<uint64_t> add_off, rem_off;  // n + 1 offsets into add / rem
+};
+
+void gather_stream(jg_ctx* ctx, const jg_stream_soa& st, const std::vector<uint64_t>& bounds, int which, uint64_t n,
+                   std::vector<jg_tagrec>& out, std::vector<uint64_t>& off) {
+    std::vector<uint64_t> src(n), len(n);
+    off.assign(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) {
+        src[i] = bounds[4 * i + 2 * which];
+        len[i] = bounds[4 * i + 2 * which + 1] - src[i];
+        off[i + 1] = off[i] + len[i];
+    }
+    out.resize(off[n]);
+    if (off[n] == 0) return;
+    jg::DevBuf meta, data;
+    meta.alloc(3 * n * 8);
+    data.alloc(off[n] * sizeof(jg_tagrec));
+    uint64_t* m = meta.as<uint64_t>();
+    JG_HIP(hipMemcpyAsync(m, src.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+    JG_HIP(hipMemcpyAsync(m + n, len.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+    JG_HIP(hipMemcpyAsync(m + 2 * n, off.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st.key.as<unsigned long long>(),
+                       st.tag.as<uint4>(), m, m + n, m + 2 * n, n, data.as<jg_tagrec>());
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(out.data(), data.p, off[n] * sizeof(jg_tagrec), hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+Runs fetch_runs(jg_orset* s, const std::vector<unsigned long long>& keys) {
+    Runs r;
+    const uint64_t n = keys.size();
+    r.add_off.assign(n + 1, 0);
+    r.rem_off.assign(n + 1, 0);
+    if (n == 0) return r;
+    jg_ctx* ctx = s->ctx;
+    jg::DevBuf q;
+    q.alloc(n * 8 * 5);
+    auto* dq = q.as<unsigned long long>();
+    auto* db = reinterpret_cast<uint64_t*>(dq + n);
+    JG_HIP(hipMemcpyAsync(dq, keys.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_runs, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s->add.key.as<unsigned long long>(), s->add.n,
+                       s->rem.key.as<unsigned long long>(), s->rem.n, dq, n, db);
+    JG_HIP(hipGetLastError());
+    std::vector<uint64_t> bounds(4 * n);
+    JG_HIP(hipMemcpyAsync(bounds.data(), db, 4 * n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    gather_stream(ctx, s->add, bounds, 0, n, r.add, r.add_off);
+    gather_stream(ctx, s->rem, bounds, 1, n, r.rem, r.rem_off);
+    return r;
+}
+
+using TagSet = std::set<std::pair<uint64_t, uint64_t>>;
+
+// ORSet.Add / Remove / Clear (ORSet.cs:134-198) in op order per set.  Host-side sequential
+// semantics over the store's runs of every element a Remove touches (gathered from the device),
+// then ONE device union: (store minus the sets Cleared in the batch) ∪ (records added after each
+// set's last Clear).
+void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
+               const uint64_t* tag_hi, uint8_t* result) {
+    std::vector<uint64_t> order(n_ops);
+    for (uint64_t i = 0; i < n_ops; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return set[a] < set[b]; });
+    std::vector<unsigned long long> need;
+    for (uint64_t i = 0; i < n_ops; ++i)
+        if (op[i] == 2) need.push_back(((unsigned long long)set[i] << 32) | elem[i]);
+    std::sort(need.begin(), need.end());
+    need.erase(std::unique(need.begin(), need.end()), need.end());
+    const Runs runs = fetch_runs(s, need);
+
+    std::vector<jg_tagrec> dadd, drem;
+    std::vector<uint32_t> cleared;
+    struct ElemState { TagSet add, rem; };
+    for (uint64_t g = 0; g < n_ops;) {
+        const uint32_t sid = set[order[g]];
+        uint64_t h = g;
+        while (h < n_ops && set[order[h]] == sid) ++h;
+        std::unordered_map<uint32_t, ElemState> st;
+        bool was_cleared = false;
+        std::vector<jg_tagrec> sa, sr;
+        auto state = [&](uint32_t e) -> ElemState& {
+            auto it = st.find(e);
+            if (it != st.end()) return it->second;
+            ElemState es;
+            const unsigned long long key = ((unsigned long long)sid << 32) | e;
+            auto nk = std::lower_bound(need.begin(), need.end(), key);
+            if (!was_cleared && nk != need.end() && *nk == key) {
+                const size_t q = nk - need.begin();
+                for (uint64_t j = runs.add_off[q]; j < runs.add_off[q + 1]; ++j) es.add.emplace(runs.add[j].tag_lo, runs.add[j].tag_hi);
+                for (uint64_t j = runs.rem_off[q]; j < runs.rem_off[q + 1]; ++j) es.rem.emplace(runs.rem[j].tag_lo, runs.rem[j].tag_hi);
+            }
+            return st.emplace(e, std::move(es)).first->second;
+        };
+        for (uint64_t x = g; x < h; ++x) {
+            const uint64_t i = order[x];
+            const unsigned long long key = ((unsigned long long)sid << 32) | elem[i];
+            if (op[i] == 1) {  // Add: a fresh tag (ORSet.cs:134-153)
+                state(elem[i]).add.emplace(tag_lo[i], tag_hi[i]);
+                sa.push_back(jg_tagrec{key, tag_lo[i], tag_hi[i]});
+                result[i] = 1;
+            } else if (op[i] == 2) {  // Remove: if Contains, tombstone every observed tag (ORSet.cs:161-186)
+                ElemState& es = state(elem[i]);
+                const bool present = elem[i] == JG_NULL_ELEM ? es.add != es.rem : !es.add.empty() && (es.rem.empty() || es.add != es.rem);
+                if (present)
+                    for (const auto& t : es.add) {
+                        es.rem.insert(t);
+                        sr.push_back(jg_tagrec{key, t.first, t.second});
+                    }
+                result[i] = present ? 1 : 0;
+            } else {  // Clear (ORSet.cs:192-198)
+                st.clear();
+                sa.clear();
+                sr.clear();
+                was_cleared = true;
+                result[i] = 1;
+            }
+        }
+        if (was_cleared) cleared.push_back(sid);
+        dadd.insert(dadd.end(), sa.begin(), sa.end());
+        drem.insert(drem.end(), sr.begin(), sr.end());
+        g = h;
+    }
+    auto lt = [](const jg_tagrec& a, const jg_tagrec& b) {
+        return a.key != b.key ? a.key < b.key : a.tag_lo != b.tag_lo ? a.tag_lo < b.tag_lo : a.tag_hi < b.tag_hi;
+    };
+    auto eq = [](const jg_tagrec& a, const jg_tagrec& b) { return a.key == b.key && a.tag_lo == b.tag_lo && a.tag_hi == b.tag_hi; };
+    std::sort(dadd.begin(), dadd.end(), lt);
+    dadd.erase(std::unique(dadd.begin(), dadd.end(), eq), dadd.end());
+    std::sort(drem.begin(), drem.end(), lt);
+    drem.erase(std::unique(drem.begin(), drem.end(), eq), drem.end());
+
+    jg_ctx* ctx = s->ctx;
+    jg::DevBuf drop;
+    if (!cleared.empty()) {
+        // The union reads drop[set >> 5] for every store record, so the bitmap covers the largest set
+        // id in the store (the last key of each sorted stream), not just the cleared ones.
+        uint64_t max_set = *std::max_element(cleared.begin(), cleared.end());
+        unsigned long long last[2] = {0, 0};
+        if (s->add.n) JG_HIP(hipMemcpy(&last[0], s->add.key.as<unsigned long long>() + s->add.n - 1, 8, hipMemcpyDeviceToHost));
+        if (s->rem.n) JG_HIP(hipMemcpy(&last[1], s->rem.key.as<unsigned long long>() + s->rem.n - 1, 8, hipMemcpyDeviceToHost));
+        max_set = std::max<uint64_t>(max_set, std::max(last[0] >> 32, last[1] >> 32));
+        std::vector<unsigned> bits((max_set >> 5) + 1, 0u);
+        for (uint32_t c : cleared) bits[c >> 5] |= 1u << (c & 31);
+        drop.alloc(bits.size() * 4);
+        JG_HIP(hipMemcpyAsync(drop.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (dadd.empty() && drem.empty() && cleared.empty()) return;
+    jg_orset tmp;
+    tmp.ctx = ctx;
+    upload_stream(ctx, tmp.add, dadd.data(), dadd.size(), "jg_orset_apply_ops(add)");
+    upload_stream(ctx, tmp.rem, drem.data(), drem.size(), "jg_orset_apply_ops(rem)");
+    merge_into(s, &tmp, false, drop.as<unsigned>());
 }
 
 }  // namespace
@@ -322,6 +506,21 @@ int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int asyn
             check_err_flag(ctx, "jg_orset_union");
             jg::sync_counts(out);
         }
+    });
+}
+
+int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
+                       const uint64_t* tag_hi, uint8_t* result) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_apply_ops: store is NULL");
+        if (n_ops == 0) return;
+        JG_REQUIRE(set && elem && op && tag_lo && tag_hi && result, JG_EINVAL, "jg_orset_apply_ops: NULL argument");
+        for (uint64_t i = 0; i < n_ops; ++i)
+            JG_REQUIRE(op[i] >= 1 && op[i] <= 3, JG_EINVAL, "jg_orset_apply_ops: op[%llu] = %u is not 1 (Add), 2 (Remove) or 3 (Clear)",
+                       (unsigned long long)i, op[i]);
+        jg::ensure_device(s->ctx);
+        jg::sync_counts(s);
+        apply_ops(s, n_ops, set, elem, op, tag_lo, tag_hi, result);
     });
 }
 

@@ -51,32 +51,42 @@ __global__ __launch_bounds__(kOB) void k_partition(const unsigned long long* __r
     part[i] = lo;
 }
 
-// Wave 0 of a tile: sum the counts of all earlier tiles (decoupled look-back).
+// Wave 0 of a tile: sum the counts of all earlier tiles (decoupled look-back).  kLB windows of 64
+// predecessors are fetched per round trip (one status word per lane and window); a window is only
+// re-polled while some of its tiles have not published yet.
+template <int kLB>
 __device__ inline unsigned long long lookback(unsigned long long* status, long long tile, int lane, unsigned* err) {
     unsigned long long excl = 0;
     long long base = tile - 1;
+    unsigned spins = 0;
     for (;;) {
-        const long long idx = base - lane;
-        unsigned long long w;
-        unsigned spins = 0;
-        for (;;) {
-            w = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
-            if (__all((w >> 62) != 0)) break;
-            if (++spins > kSpinLimit) {  // wave-uniform: give up, flag the call, let the grid drain
-                if (lane == 0) atomicOr(err, 1u);
-                w = kFlagIncl;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const unsigned long long incl = __ballot((w >> 62) == 2);
-        const int first = incl ? __ffsll((long long)incl) - 1 : 64;
-        unsigned long long v = lane <= first ? (w & kValMask) : 0ull;
+        unsigned long long w[kLB];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        excl += v;
-        if (incl) return excl;
-        base -= 64;
+        for (int j = 0; j < kLB; ++j) {
+            const long long idx = base - 64 * j - lane;
+            w[j] = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+        }
+#pragma unroll
+        for (int j = 0; j < kLB; ++j) {
+            const long long idx = base - 64 * j - lane;
+            while (!__all((w[j] >> 62) != 0)) {
+                if (++spins > kSpinLimit) {  // wave-uniform: give up, flag the call, let the grid drain
+                    if (lane == 0) atomicOr(err, 1u);
+                    w[j] = kFlagIncl;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                w[j] = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
+            }
+            const unsigned long long incl = __ballot((w[j] >> 62) == 2);
+            const int first = incl ? __ffsll((long long)incl) - 1 : 64;
+            unsigned long long v = lane <= first ? (w[j] & kValMask) : 0ull;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            excl += v;
+            if (incl) return excl;
+        }
+        base -= 64 * kLB;
     }
 }
 
@@ -133,6 +143,14 @@ __device__ __forceinline__ void tile_load(TileRegs<kItems>& r, const TileBounds&
     }
 }
 
+// Set-indexed drop bitmap (ORSet.Clear applied inside a batch of ops): A-side records whose set bit
+// is 1 are removed from the union.  nullptr = keep everything.
+__device__ __forceinline__ bool dropped(const unsigned* drop, unsigned long long key) {
+    if (!drop) return false;
+    const unsigned set = (unsigned)(key >> 32);
+    return (drop[set >> 5] >> (set & 31)) & 1u;
+}
+
 struct TileLds {
     unsigned long long* key;
     uint4* tag;
@@ -144,7 +162,8 @@ struct TileLds {
 };
 
 template <int kOB, int kItems>
-__device__ __forceinline__ void tile_stage(const TileRegs<kItems>& r, const TileBounds& b, const TileLds& L, int tid) {
+__device__ __forceinline__ void tile_stage(const TileRegs<kItems>& r, const TileBounds& b, const TileLds& L, int tid,
+                                           const unsigned* drop = nullptr) {
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
         const int x = it * kOB + tid;
@@ -152,7 +171,7 @@ __device__ __forceinline__ void tile_stage(const TileRegs<kItems>& r, const Tile
         L.tag[x] = to_u4(Tag{r.lo[it], r.hi[it]});
     }
     if (tid == 0) {
-        *L.has_prev = b.i0 > 0;
+        *L.has_prev = b.i0 > 0 && !dropped(drop, r.pk);
         if (b.i0 > 0) { *L.prev_key = r.pk; *L.prev_tag = to_u4(Tag{r.plo, r.phi}); }
     }
 }
@@ -164,10 +183,11 @@ struct NoStamp {
 // Merge, de-duplicate, scan, look back, compact and store one staged tile.  Called by the whole
 // workgroup after a barrier that follows tile_stage; ends with the LDS image read for the stores.
 // `stamp(i)` marks phase boundaries in the diagnostic build (tools/tune_orset.hip); a no-op here.
-template <int kOB, int kItems, class Stamp = NoStamp>
+template <int kOB, int kItems, class Stamp = NoStamp, int kLB = 1>
 __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b, uint64_t n_tiles, const TileLds& L,
                                              unsigned long long* __restrict__ ok, uint4* __restrict__ ot, unsigned long long* status,
-                                             unsigned long long* out_count, unsigned* err, int tid, const Stamp& stamp = Stamp()) {
+                                             unsigned long long* out_count, unsigned* err, int tid, const Stamp& stamp = Stamp(),
+                                             const unsigned* drop = nullptr) {
     const int lane = tid & 63, wid = tid >> 6;
     const int nA = b.nA, nB = b.nB, n = nA + nB;
     unsigned long long* s_key = L.key;
@@ -188,7 +208,9 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
     bool hp;
     unsigned long long pk;
     Tag pt;
-    if (ai > 0) { hp = true; pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); }
+    // hp: the A record just before the next B record in merged order exists and survives the drop
+    // filter (a B record can only equal that one, since A and B are strictly increasing).
+    if (ai > 0) { pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); hp = !dropped(drop, pk); }
     else { hp = *L.has_prev != 0; pk = *L.prev_key; pt = __builtin_bit_cast(Tag, *L.prev_tag); }
 
     const int my_n = n - diag < kItems ? n - diag : kItems;
@@ -205,8 +227,9 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
             const bool take_a = ai < nA && (bi >= nB || !rec_lt(kb, tb, ka, ta));
             if (take_a) {
                 src[it] = ai;
-                keep |= 1u << it;
-                hp = true; pk = ka; pt = ta;
+                hp = !dropped(drop, ka);
+                if (hp) keep |= 1u << it;
+                pk = ka; pt = ta;
                 ++ai;
                 if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
             } else {
@@ -246,7 +269,7 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
             if (lane == 0) __hip_atomic_store(status, kFlagIncl | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             if (lane == 0) __hip_atomic_store(status + tile, kFlagAgg | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            excl = lookback(status, (long long)tile, lane, err);
+            excl = lookback<kLB>(status, (long long)tile, lane, err);
             if (lane == 0)
                 __hip_atomic_store(status + tile, kFlagIncl | (excl + (unsigned long long)block_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -297,13 +320,13 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
 
 // One tile per workgroup; grid = n_tiles.  Tickets (not blockIdx) order the tiles, so a tile only
 // ever waits for tiles already owned by running workgroups.
-template <int kOB, int kItems>
+template <int kOB, int kItems, int kLB = 1>
 __global__ __launch_bounds__(kOB) void k_union(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
                                                const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
                                                const uint64_t* __restrict__ part, uint64_t n_tiles,
                                                unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
                                                unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
-                                               unsigned* err) {
+                                               unsigned* err, const unsigned* __restrict__ drop = nullptr) {
     JGK_TILE_LDS(kOB, kItems);
     const int tid = threadIdx.x;
     if (tid == 0) s_tile = atomicAdd(ticket, 1u);
@@ -312,9 +335,9 @@ __global__ __launch_bounds__(kOB) void k_union(const unsigned long long* __restr
     const TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
     TileRegs<kItems> r;
     tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
-    tile_stage<kOB, kItems>(r, b, L, tid);
+    tile_stage<kOB, kItems>(r, b, L, tid, drop);
     __syncthreads();
-    tile_process<kOB, kItems>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid);
+    tile_process<kOB, kItems, NoStamp, kLB>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid, NoStamp(), drop);
 }
 
 // Persistent variant: each workgroup loops over tickets and loads tile t+1 into registers while it
@@ -347,6 +370,43 @@ __global__ __launch_bounds__(kOB) void k_union_pp(const unsigned long long* __re
             tile_load<kOB, kItems>(r, nb2, ak, at, bk, bt, tid);
         }
         tile_process<kOB, kItems>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid);
+        if (next >= n_tiles) break;
+        tile = next;
+        b = nb2;
+        __syncthreads();  // every wave's stores read the LDS image before it is restaged
+    }
+}
+
+// Persistent, statically assigned variant: workgroup b owns tiles b, b+G, b+2G, ... (G = grid) and
+// loads its next tile into registers while it merges the current one.  Tile t only waits on
+// lower tiles, all owned by co-resident workgroups that process theirs in increasing order, so
+// the grid MUST be fully resident (G <= resident workgroups); the bounded spin flags a violation.
+template <int kOB, int kItems, int kLB = 1>
+__global__ __launch_bounds__(kOB) void k_union_ps(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
+                                                  const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
+                                                  const uint64_t* __restrict__ part, uint64_t n_tiles,
+                                                  unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
+                                                  unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
+                                                  unsigned* err) {
+    JGK_TILE_LDS(kOB, kItems);
+    (void)ticket;
+    (void)s_tile;
+    const int tid = threadIdx.x;
+    uint64_t tile = blockIdx.x;
+    if (tile >= n_tiles) return;
+    TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
+    TileRegs<kItems> r;
+    tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
+    for (;;) {
+        tile_stage<kOB, kItems>(r, b, L, tid);
+        __syncthreads();
+        const uint64_t next = tile + gridDim.x;
+        TileBounds nb2{0, 0, 0, 0};
+        if (next < n_tiles) {
+            nb2 = tile_bounds<kOB, kItems>(next, part, na, nb);
+            tile_load<kOB, kItems>(r, nb2, ak, at, bk, bt, tid);
+        }
+        tile_process<kOB, kItems, NoStamp, kLB>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid);
         if (next >= n_tiles) break;
         tile = next;
         b = nb2;

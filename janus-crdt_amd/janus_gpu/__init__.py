@@ -26,7 +26,7 @@ EXPORTS = [
     "jg_pnc_apply_ops", "jg_pnc_values",
     "jg_rows_create", "jg_rows_destroy", "jg_rows_upload", "jg_pnc_merge_batch",
     "jg_orset_create", "jg_orset_destroy", "jg_orset_load", "jg_orset_size", "jg_orset_read",
-    "jg_orset_merge", "jg_orset_merge_store", "jg_orset_union", "jg_orset_contains",
+    "jg_orset_merge", "jg_orset_merge_store", "jg_orset_union", "jg_orset_contains", "jg_orset_apply_ops",
     "jg_synth_pnc_store", "jg_synth_pnc_rows", "jg_synth_orset",
 ]
 
@@ -61,6 +61,7 @@ _SIGS = {
     "jg_orset_merge_store": ([_vp, _vp, C.c_int], C.c_int),
     "jg_orset_union": ([_vp, _vp, _vp, C.c_int], C.c_int),
     "jg_orset_contains": ([_vp, _vp, _vp, _u64, _vp], C.c_int),
+    "jg_orset_apply_ops": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_synth_pnc_store": ([_vp, _u64], C.c_int),
     "jg_synth_pnc_rows": ([_vp, _u64, _u64], C.c_int),
     "jg_synth_orset": ([_vp, _u64, _u64, _u32, _u32, _u32, _u32, _u32], C.c_int),
@@ -269,6 +270,17 @@ class ORSetStore:
     @staticmethod
     def union(a: "ORSetStore", b: "ORSetStore", out: "ORSetStore", async_: bool = False) -> None:
         _check(load().jg_orset_union(a._h, b._h, out._h, 1 if async_ else 0))
+
+    ADD, REMOVE, CLEAR = 1, 2, 3
+
+    def apply_ops(self, set_ids, elems, ops, tag_lo, tag_hi) -> np.ndarray:
+        """ORSet.Add/Remove/Clear in order (jg_orset_apply_ops); returns each op's bool result."""
+        s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)
+        o = _arr(ops, np.uint8)
+        lo, hi = _arr(tag_lo, np.uint64), _arr(tag_hi, np.uint64)
+        out = np.empty(s.size, np.uint8)
+        _check(load().jg_orset_apply_ops(self._h, s.size, _ptr(s), _ptr(e), _ptr(o), _ptr(lo), _ptr(hi), _ptr(out)))
+        return out
 
     def contains(self, set_ids, elems) -> np.ndarray:
         s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)

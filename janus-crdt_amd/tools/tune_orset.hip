@@ -74,7 +74,7 @@ struct Buf { unsigned long long* key; uint4* tag; unsigned long long n; };
 
 int num_cus;
 
-template <int OB, int IT, bool PP = false>
+template <int OB, int IT, bool PP = false, int LB = 1, bool PS = false>
 float run(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, unsigned long long* cnt, hipStream_t s, float* part_ms) {
     const unsigned long long total = a.n + b.n, tile = OB * IT, nt = (total + tile - 1) / tile;
     const size_t sb = ((nt * 8 + 16) + 255) & ~255ull;
@@ -85,7 +85,14 @@ float run(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, unsigned 
     hipLaunchKernelGGL((jgk::k_partition<OB, IT>), dim3((nt + 1 + OB - 1) / OB), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, nt + 1,
                        (uint64_t*)(ws + sb));
     CK(hipEventRecord(e1, s));
-    if constexpr (PP) {
+    if constexpr (PS) {
+        int occ = 0;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, jgk::k_union_ps<OB, IT, LB>, OB, 0));
+        unsigned long long g = (unsigned long long)num_cus * (occ > 0 ? occ : 1);
+        if (g > nt) g = nt;
+        hipLaunchKernelGGL((jgk::k_union_ps<OB, IT, LB>), dim3(g), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n,
+                           (const uint64_t*)(ws + sb), nt, o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err);
+    } else if constexpr (PP) {
         int occ = 0;
         CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, jgk::k_union_pp<OB, IT>, OB, 0));
         static bool said = false;
@@ -95,7 +102,7 @@ float run(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, unsigned 
         hipLaunchKernelGGL((jgk::k_union_pp<OB, IT>), dim3(g), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n,
                            (const uint64_t*)(ws + sb), nt, o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err);
     } else {
-        hipLaunchKernelGGL((jgk::k_union<OB, IT>), dim3(nt), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, (const uint64_t*)(ws + sb), nt,
+        hipLaunchKernelGGL((jgk::k_union<OB, IT, LB>), dim3(nt), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, (const uint64_t*)(ws + sb), nt,
                            o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err);
     }
     CK(hipEventRecord(e2, s));
@@ -107,7 +114,47 @@ float run(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, unsigned 
     return u;
 }
 
-template <int OB, int IT>
+// Persistent variant with stamps: 1 iteration start (staged), 2 next ticket read, 3 next loads issued.
+template <int kOB, int kItems>
+__global__ __launch_bounds__(kOB) void k_union_pp_stamped(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
+                                                          const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
+                                                          const uint64_t* __restrict__ part, uint64_t n_tiles,
+                                                          unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
+                                                          unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
+                                                          unsigned* err, unsigned long long* stamps) {
+    using namespace jgk;
+    JGK_TILE_LDS(kOB, kItems);
+    const int tid = threadIdx.x;
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    uint64_t tile = s_tile;
+    if (tile >= n_tiles) return;
+    TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
+    TileRegs<kItems> r;
+    tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
+    for (;;) {
+        StampW st{stamps + (size_t)tile * 16};
+        st(1);
+        tile_stage<kOB, kItems>(r, b, L, tid);
+        if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+        __syncthreads();
+        st(2);
+        const uint64_t next = s_tile;
+        TileBounds nb2{0, 0, 0, 0};
+        if (next < n_tiles) {
+            nb2 = tile_bounds<kOB, kItems>(next, part, na, nb);
+            tile_load<kOB, kItems>(r, nb2, ak, at, bk, bt, tid);
+        }
+        st(3);
+        tile_process<kOB, kItems, StampW>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid, st);
+        if (next >= n_tiles) break;
+        tile = next;
+        b = nb2;
+        __syncthreads();
+    }
+}
+
+template <int OB, int IT, bool PP = false>
 void run_stamped(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, unsigned long long* cnt, hipStream_t s) {
     const unsigned long long total = a.n + b.n, tile = OB * IT, nt = (total + tile - 1) / tile;
     const size_t sb = ((nt * 8 + 16) + 255) & ~255ull;
@@ -117,8 +164,16 @@ void run_stamped(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, un
     CK(hipMemsetAsync(ws, 0, sb, s));
     hipLaunchKernelGGL((jgk::k_partition<OB, IT>), dim3((nt + 1 + OB - 1) / OB), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, nt + 1,
                        (uint64_t*)(ws + sb));
-    hipLaunchKernelGGL((k_union_stamped<OB, IT>), dim3(nt), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, (const uint64_t*)(ws + sb), nt,
-                       o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err, stamps);
+    if constexpr (PP) {
+        int occ = 0;
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_union_pp_stamped<OB, IT>, OB, 0));
+        unsigned long long g = (unsigned long long)num_cus * (occ > 0 ? occ : 1);
+        hipLaunchKernelGGL((k_union_pp_stamped<OB, IT>), dim3(g), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n,
+                           (const uint64_t*)(ws + sb), nt, o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err, stamps);
+    } else {
+        hipLaunchKernelGGL((k_union_stamped<OB, IT>), dim3(nt), dim3(OB), 0, s, a.key, a.tag, a.n, b.key, b.tag, b.n, (const uint64_t*)(ws + sb), nt,
+                           o.key, o.tag, (unsigned long long*)ws, (unsigned*)(ws + nt * 8), cnt, err, stamps);
+    }
     CK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(nt * 16);
     CK(hipMemcpy(h.data(), stamps, nt * 16 * 8, hipMemcpyDeviceToHost));
@@ -128,8 +183,9 @@ void run_stamped(const Buf& a, const Buf& b, Buf& o, char* ws, unsigned* err, un
         for (int i = 2; i < 10; ++i) sum[i] += (double)(h[t * 16 + i] - h[t * 16 + i - 1]);
         tmin = std::min(tmin, h[t * 16 + 1]); tmax = std::max(tmax, h[t * 16 + 9]);
     }
-    const char* nm[10] = {"", "", "bounds(part ld)", "load+stage", "mp search", "serial merge", "scan", "lookback", "compact", "store issue"};
-    std::printf("stamps OB%d IT%d (cycles @100MHz memtime? avg per tile):", OB, IT);
+    const char* nm[10] = {"", "", PP ? "stage+ticket" : "bounds(part ld)", PP ? "next bounds+loads" : "load+stage", "mp search", "serial merge",
+                          "scan", "lookback", "compact", "store issue"};
+    std::printf("stamps %sOB%d IT%d (shader cycles, avg per tile):", PP ? "PP " : "", OB, IT);
     double tot = 0;
     for (int i = 2; i < 10; ++i) tot += sum[i];
     for (int i = 2; i < 10; ++i) std::printf(" %s=%.0f (%.0f%%)", nm[i], sum[i] / nt, 100 * sum[i] / tot);
@@ -155,11 +211,17 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     { unsigned e0; CK(hipMemcpy(&e0, err, 4, hipMemcpyDeviceToHost)); std::printf("err after init %u\n", e0); }
     std::vector<V> vs = {
-        {"OB256 IT8 (prod)", run<256, 8>}, {"OB256 IT12", run<256, 12>}, {"OB512 IT6", run<512, 6>}, {"OB512 IT8", run<512, 8>},
-        {"OB256 IT16", run<256, 16>},
-        {"PP OB256 IT8", run<256, 8, true>}, {"PP OB256 IT4", run<256, 4, true>}, {"PP OB256 IT6", run<256, 6, true>},
-        {"PP OB512 IT4", run<512, 4, true>}, {"PP OB512 IT6", run<512, 6, true>}, {"PP OB256 IT12", run<256, 12, true>},
-        {"PP OB128 IT8", run<128, 8, true>},
+        {"OB512 IT6 (prod)", run<512, 6>},
+        {"OB512 IT6 LB4", run<512, 6, false, 4>},
+        {"OB512 IT6 LB8", run<512, 6, false, 8>},
+        {"OB256 IT8 LB4", run<256, 8, false, 4>},
+        {"OB256 IT12 LB4", run<256, 12, false, 4>},
+        {"PS OB512 IT6 LB1", run<512, 6, false, 1, true>},
+        {"PS OB512 IT6 LB4", run<512, 6, false, 4, true>},
+        {"PS OB256 IT8 LB4", run<256, 8, false, 4, true>},
+        {"PS OB256 IT6 LB4", run<256, 6, false, 4, true>},
+        {"PS OB256 IT4 LB4", run<256, 4, false, 4, true>},
+        {"PS OB512 IT4 LB4", run<512, 4, false, 4, true>},
     };
     const int rounds = argc > 1 ? std::atoi(argv[1]) : 7;
     std::vector<std::vector<float>> tu(vs.size()), tp(vs.size());
@@ -176,9 +238,8 @@ int main(int argc, char** argv) {
         if (k == 0) { ref_cnt = c; ref_sum = sm; }
         std::printf("%-20s count %llu checksum %016llx err %u %s\n", vs[k].name, c, sm, ev, (c == ref_cnt && sm == ref_sum) ? "OK" : "MISMATCH");
     }
-    run_stamped<256, 8>(a, b, o, ws, err, cnt, s);
     run_stamped<512, 6>(a, b, o, ws, err, cnt, s);
-    run_stamped<256, 12>(a, b, o, ws, err, cnt, s);
+
     for (int r = 0; r < rounds; ++r)
         for (size_t k = 0; k < vs.size(); ++k) { float p; tu[k].push_back(vs[k].fn(a, b, o, ws, err, cnt, s, &p)); tp[k].push_back(p); }
     const double bytes = (2.0 * n + ref_cnt) * 24;

@@ -227,6 +227,30 @@ int orc_orset_contains(const Rec* A, uint64_t nA, const Rec* Rm, uint64_t nR, ui
     return 0;
 }
 
+// ORSet.Add / Remove / Clear applied in op order (op 1 Add with the given tag, 2 Remove, 3 Clear)
+// to the state (A adds, Rm tombstones) through ORSet objects; exports the new state canonically and
+// each op's bool result.  out arrays need room for nA + n_ops / nR + (all tags that could be
+// tombstoned: nA + n_ops).
+int orc_orset_apply_ops(const Rec* A, uint64_t nA, const Rec* Rm, uint64_t nR, uint64_t n_ops, const uint32_t* set, const uint32_t* elem,
+                        const uint8_t* op, const uint64_t* tag_lo, const uint64_t* tag_hi, uint8_t* result, Rec* out_a, uint64_t* n_out_a,
+                        Rec* out_r, uint64_t* n_out_r) {
+    std::map<uint32_t, ORSet> sets;
+    build_sets(sets, A, nA, Rm, nR);
+    for (uint64_t i = 0; i < n_ops; ++i) {
+        ORSet& o = sets[set[i]];
+        const Elem e = elem_of(elem[i]);
+        if (op[i] == 1) result[i] = o.AddTag(e, Guid{tag_lo[i], tag_hi[i]}) ? 1 : 0;
+        else if (op[i] == 2) result[i] = o.Remove(e) ? 1 : 0;
+        else if (op[i] == 3) { o.Clear(); result[i] = 1; }
+        else return -1;
+    }
+    std::vector<Rec> a, r;
+    export_sets(sets, a, r);
+    std::copy(a.begin(), a.end(), out_a); *n_out_a = a.size();
+    std::copy(r.begin(), r.end(), out_r); *n_out_r = r.size();
+    return 0;
+}
+
 // ORSet.LookupAll() of one set, in the reference's order (the state is built from canonical
 // records, so insertion order = ascending elem id).  Returns the count; out needs room for it.
 int64_t orc_orset_lookup_all(const Rec* A, uint64_t nA, const Rec* Rm, uint64_t nR, uint32_t set, uint32_t* out, uint64_t cap) {

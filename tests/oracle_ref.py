@@ -22,6 +22,7 @@ _SIGS = {
     "orc_pnc_apply_ops_dense": ([_u64, _u32, _u32, _vp, _vp, _u64, _vp, _vp, _vp, _vp], C.c_int),
     "orc_orset_merge": ([_vp, _u64, _vp, _u64, _vp, _u64, _vp, _u64, _vp, C.POINTER(_u64), _vp, C.POINTER(_u64)], C.c_int),
     "orc_orset_contains": ([_vp, _u64, _vp, _u64, _u64, _vp, _vp, _vp], C.c_int),
+    "orc_orset_apply_ops": ([_vp, _u64, _vp, _u64, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.POINTER(_u64), _vp, C.POINTER(_u64)], C.c_int),
     "orc_orset_lookup_all": ([_vp, _u64, _vp, _u64, _u32, _vp, _u64], C.c_int64),
     "orc_bench_pnc_merge": ([_u64, _u32, _u64, _i32, _i32], C.c_double),
     "orc_bench_orset_merge": ([_u64, _u32, _u32, _u32, _u32, _u32, _u64, _i32, _i32], C.c_double),
@@ -120,6 +121,21 @@ def orset_contains(A, Rm, sets, elems):
     out = np.empty(s.size, np.uint8)
     assert lib().orc_orset_contains(_p(A), A.size, _p(Rm), Rm.size, s.size, _p(s), _p(e), _p(out)) == 0
     return out
+
+
+def orset_apply_ops(A, Rm, sets, elems, ops, tag_lo, tag_hi):
+    """ORSet.Add/Remove/Clear in order; returns (adds, tombstones, results)."""
+    A, Rm = _recs(A), _recs(Rm)
+    s, e = np.ascontiguousarray(sets, np.uint32), np.ascontiguousarray(elems, np.uint32)
+    o = np.ascontiguousarray(ops, np.uint8)
+    lo, hi = np.ascontiguousarray(tag_lo, np.uint64), np.ascontiguousarray(tag_hi, np.uint64)
+    res = np.empty(s.size, np.uint8)
+    oa = np.empty(A.size + s.size, REC_DTYPE)
+    orr = np.empty(Rm.size + A.size + s.size, REC_DTYPE)
+    na, nr = _u64(), _u64()
+    assert lib().orc_orset_apply_ops(_p(A), A.size, _p(Rm), Rm.size, s.size, _p(s), _p(e), _p(o), _p(lo), _p(hi), _p(res),
+                                     _p(oa), C.byref(na), _p(orr), C.byref(nr)) == 0
+    return oa[: na.value], orr[: nr.value], res
 
 
 def orset_lookup_all(A, Rm, set_id, cap=1 << 16):

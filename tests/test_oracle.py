@@ -204,3 +204,16 @@ def test_golden_orset():
     assert np.array_equal(oa, z["out_add"]) and np.array_equal(orr, z["out_rem"])
     got = orc.orset_contains(oa, orr, z["q_set"], z["q_elem"])
     assert np.array_equal(got, z["contains"])
+
+
+def test_orset_apply_ops_bridge_reference_sequence():
+    """ORSetTests.cs:10-40 (SingleORSetValueType1) as an op batch on one set: Add 1, Add 2,
+    Remove 1 -> true, Remove 3 -> false, Add 3, then Clear, Add 1."""
+    empty = np.empty(0, orc.REC_DTYPE)
+    ops = [(1, 1), (1, 2), (2, 1), (2, 3), (1, 3)]
+    a, r, res = orc.orset_apply_ops(empty, empty, [0] * 5, [e for _, e in ops], [o for o, _ in ops],
+                                    np.arange(1, 6), np.zeros(5))
+    assert list(res) == [1, 1, 1, 0, 1]
+    assert sorted(orc.orset_lookup_all(a, r, 0)) == [2, 3]
+    a2, r2, res2 = orc.orset_apply_ops(a, r, [0, 0], [0, 1], [3, 1], [0, 9], [0, 0])
+    assert list(res2) == [1, 1] and list(orc.orset_lookup_all(a2, r2, 0)) == [1] and r2.size == 0

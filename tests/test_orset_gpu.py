@@ -191,3 +191,39 @@ def test_full_size_c3(ctx):
     finally:
         for h in (L, R, out):
             h.close()
+
+
+@pytest.mark.parametrize("seed,n_sets,n_elems,n_ops,p_clear", [(1, 3, 4, 60, 0.05), (2, 40, 12, 3000, 0.01), (3, 5, 3, 500, 0.2),
+                                                                (4, 300, 20, 20000, 0.002)])
+def test_apply_ops_match_oracle(ctx, seed, n_sets, n_elems, n_ops, p_clear):
+    """ORSet.Add/Remove/Clear (ORSet.cs:134-198) batched on the device in op order per set,
+    interleaved across sets, on top of an existing merged state, vs the oracle op by op."""
+    rng = np.random.default_rng(seed)
+    La, Lr, _, _ = random_orset_pair(rng, n_sets=n_sets, n_elems=n_elems, pool=6)
+    sets = rng.integers(0, n_sets + 1, n_ops).astype(np.uint32)
+    elems = rng.integers(0, n_elems + 1, n_ops).astype(np.uint32)
+    elems[rng.random(n_ops) < 0.1] = jg.NULL_ELEM
+    r = rng.random(n_ops)
+    ops = np.where(r < p_clear, 3, np.where(r < 0.55, 1, 2)).astype(np.uint8)
+    lo = rng.integers(1, 1 << 63, n_ops, dtype=np.uint64)
+    hi = rng.integers(1, 1 << 63, n_ops, dtype=np.uint64)
+    ea, er, eres = orc.orset_apply_ops(La, Lr, sets, elems, ops, lo, hi)
+    s = _store(ctx, La, Lr)
+    try:
+        gres = s.apply_ops(sets, elems, ops, lo, hi)
+        ga, gr = s.read()
+    finally:
+        s.close()
+    assert np.array_equal(gres, eres)
+    assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+
+
+def test_apply_ops_rejects_bad_op(ctx):
+    s = jg.ORSetStore(ctx, 0, 0)
+    try:
+        with pytest.raises(jg.JanusError) as e:
+            s.apply_ops([0], [1], [4], [1], [1])  # ORSetWrapper: InvalidOperationException
+        assert e.value.code == jg.JG_EINVAL
+        assert s.size() == (0, 0)
+    finally:
+        s.close()
