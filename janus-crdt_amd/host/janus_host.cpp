@@ -142,6 +142,50 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
     return completed;
 }
 
+std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) {
+    std::vector<uint8_t> result(ops.size(), 1);
+    std::vector<uint32_t> pkey, pcol;
+    std::vector<int64_t> pdelta;
+    std::vector<uint8_t> pisn;
+    std::vector<uint32_t> oset, oelem;
+    std::vector<uint8_t> oop;
+    std::vector<uint64_t> olo, ohi;
+    std::vector<size_t> oidx;
+    for (size_t i = 0; i < ops.size(); ++i) {  // validate everything first: no partial application
+        auto ty = type_.find(ops[i].uid);
+        if (ty == type_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
+        const int hi = ty->second == CrdtType::PNCounter ? 2 : 3;
+        if (ops[i].opId < 1 || ops[i].opId > hi)
+            throw EngineError(JG_EINVAL, ty->second == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+    }
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const ClientOp& op = ops[i];
+        if (type_.at(op.uid) == CrdtType::PNCounter) {
+            const PncKey& k = pnc_keys_.at(op.uid);
+            pkey.push_back(k.row);
+            pcol.push_back(0);
+            pdelta.push_back(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
+            pisn.push_back(op.opId == 2 ? 1 : 0);
+        } else {
+            SetKey& sk = set_keys_.at(op.uid);
+            oset.push_back(sk.set);
+            // an element first seen in a Remove gets an id too: its (empty) runs are what Contains sees
+            oelem.push_back(op.opId == 3 ? 0u : elem_id(sk, op.elem, true));
+            oop.push_back((uint8_t)op.opId);
+            olo.push_back(op.tag.lo);
+            ohi.push_back(op.tag.hi);
+            oidx.push_back(i);
+        }
+    }
+    if (!pkey.empty()) check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
+    if (!oset.empty()) {
+        std::vector<uint8_t> r(oset.size());
+        check(jg_orset_apply_ops(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data()));
+        for (size_t j = 0; j < oidx.size(); ++j) result[oidx[j]] = r[j];
+    }
+    return result;
+}
+
 int64_t GpuStableStore::QueryStablePNC(const Guid& uid) {
     const PncKey& k = pnc_keys_.at(uid);
     int64_t v = 0;

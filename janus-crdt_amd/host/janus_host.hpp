@@ -70,7 +70,17 @@ struct EngineError : std::runtime_error {
     EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
-// The stable copies of every key of one node, resident on one GPU.
+// One client operation for PNCounterWrapper.Update / ORSetWrapper.Update
+// (BFT-CRDT/SafeCRDTs/PNCounterWrapper.cs:33-47, ORSetWrapper.cs:30-46).
+struct ClientOp {
+    Guid uid;
+    int opId = 0;                     // PNC: 1 Increment, 2 Decrement; ORSet: 1 Add, 2 Remove, 3 Clear
+    int64_t amount = 0;               // PNC argument (args[0] as int)
+    std::optional<std::string> elem;  // ORSet argument (args[0] as string; nullopt = null)
+    Guid tag;                         // ORSet Add: the Guid.NewGuid() drawn for this add
+};
+
+// One CRDT copy (stable or prospective) of every key of one node, resident on one GPU.
 class GpuStableStore {
   public:
     GpuStableStore(int device, uint32_t max_keys, uint32_t replicas, uint32_t elem_bytes);
@@ -89,6 +99,12 @@ class GpuStableStore {
     // removed like ConcurrentDictionary.TryRemove.
     std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                          std::unordered_map<uint64_t, uint64_t>* tracker = nullptr);
+
+    // Wrapper Update, batched: ops run in order (PNC increments commute; OR-Set ops keep their order
+    // per set).  Returns each op's bool result.  An unknown op id throws EngineError(JG_EINVAL) (the
+    // wrappers' InvalidOperationException) before anything is applied.  A PNC op writes this copy's
+    // own replica column (column 0, registered by CreateSafeCRDT).
+    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops);
 
     // QueryStable: PNCounter.Get (throws EngineError JG_EOVERFLOW where the checked Sum would throw
     // OverflowException) and ORSet.Contains.

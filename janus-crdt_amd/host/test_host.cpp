@@ -7,7 +7,10 @@
 // oracle node (prospective merge on block receipt + HandleAfterConsensusUpdates) and, through
 // janus::GpuStableStore (one batched engine call per CRDT type), to node 0's stable state on the GPU.
 // After each wave every key's QueryStable (value / OverflowException / Contains of every element and
-// null) and the order of completed safe updates must match node 0 of the oracle exactly.
+// null) and the order of completed safe updates must match node 0 of the oracle exactly.  Node 0's
+// PROSPECTIVE copies also live on the GPU: its client ops (wrapper Update -> jg_pnc_apply_ops /
+// jg_orset_apply_ops) and the other nodes' states on block receipt (§8f F2)
+// are applied there, and QueryProspective plus every op result must match too.
 // Exit 0 = parity; prints the first mismatch otherwise.
 #include <cstdio>
 #include <memory>
@@ -58,6 +61,9 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     std::vector<std::unique_ptr<oracle::SafeCRDTManager>> nodes;
     for (int i = 0; i < n_nodes; ++i) nodes.push_back(std::make_unique<oracle::SafeCRDTManager>(batch, seed * 31 + i));
     janus::GpuStableStore gpu(0, n_pnc + 1, 8, eb);
+    janus::GpuStableStore gpu_p(0, n_pnc + 1, 8, eb);  // node 0's PROSPECTIVE copies (ApplyOp + block-receipt merges)
+    std::vector<janus::ClientOp> pending;               // node 0's client ops since the last wave
+    std::vector<uint8_t> pending_res;                   // the oracle's results for them
     std::vector<std::string> keys;
     for (int k = 0; k < n_pnc + n_set; ++k) {
         const bool is_pnc = k < n_pnc;
@@ -67,6 +73,8 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(key);
         gpu.CreateSafeCRDT(G(uid), is_pnc ? janus::CrdtType::PNCounter : janus::CrdtType::ORSet,
                            is_pnc ? G(s0.pncStable->pnc.replicaIdx()) : janus::Guid{});
+        gpu_p.CreateSafeCRDT(G(uid), is_pnc ? janus::CrdtType::PNCounter : janus::CrdtType::ORSet,
+                             is_pnc ? G(s0.pncProspective->pnc.replicaIdx()) : janus::Guid{});
         keys.push_back(key);
     }
     Rng rng{seed};
@@ -95,6 +103,14 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
             }
             jw.push_back(std::move(l));
         }
+        // node 0's prospective copies on the GPU: its own ops first (they ran before the blocks
+        // arrived), then the other nodes' states of this wave (ReplicationManager.cs:327-344)
+        auto res = gpu_p.ApplyOps(pending);
+        if (res != pending_res) { std::printf("FAIL ApplyOp results differ from the wrappers'\n"); return 1; }
+        pending.clear();
+        pending_res.clear();
+        std::vector<std::vector<janus::UpdateMessage>> others(jw.begin() + 1, jw.end());
+        gpu_p.ApplyCommitted(others, nullptr);
         std::unordered_map<uint64_t, uint64_t> tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
         const size_t before = nodes[0]->notified.size();
         for (auto& n : nodes) n->HandleAfterConsensusUpdates(wave);
@@ -107,6 +123,18 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         for (int k = 0; k < (int)keys.size(); ++k) {
             oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(keys[k]);
             if (k < n_pnc) {
+                bool po = false, pg = false;
+                int64_t pv = 0, gpv = 0;
+                try { pv = s0.QueryProspective().i; } catch (const oracle::OverflowException&) { po = true; }
+                try { gpv = gpu_p.QueryStablePNC(G(s0.guid)); } catch (const janus::EngineError& e) {
+                    if (e.code != JG_EOVERFLOW) throw;
+                    pg = true;
+                }
+                if (po != pg || pv != gpv) {
+                    std::printf("FAIL prospective %s: oracle %lld%s gpu %lld%s\n", keys[k].c_str(), (long long)pv, po ? " (overflow)" : "",
+                                (long long)gpv, pg ? " (overflow)" : "");
+                    return 1;
+                }
                 bool o_ovf = false, g_ovf = false;
                 int64_t ov = 0, gv = 0;
                 try { ov = s0.QueryStable().i; } catch (const oracle::OverflowException&) { o_ovf = true; }
@@ -127,6 +155,8 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
                     const bool o = s0.QueryStable(q).b, g = gpu.QueryStableORSet(G(s0.guid), el);
                     (o ? n_in : n_out)++;
                     if (o != g) { std::printf("FAIL %s elem %d: oracle %d gpu %d\n", keys[k].c_str(), e, o, g); return 1; }
+                    const bool op_ = s0.QueryProspective(q).b, gp = gpu_p.QueryStableORSet(G(s0.guid), el);
+                    if (op_ != gp) { std::printf("FAIL prospective %s elem %d: oracle %d gpu %d\n", keys[k].c_str(), e, op_, gp); return 1; }
                 }
             }
         }
@@ -142,14 +172,28 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
             const int op = 1 + (int)rng.below(2);
             int64_t amt = 1 + (int64_t)rng.below(99);           // PNCWorkload.cs:63 Next(1,100)
             if (eb == 4 && rng.below(50) == 0) amt = 0x7FFFFFF0 - (int64_t)rng.below(100);  // push toward the checked-Sum edge
-            sc.Update(op, {oracle::Arg::I(amt)}, safe, org);
+            const auto r = sc.Update(op, {oracle::Arg::I(amt)}, safe, org);
+            if (node == 0) {
+                janus::ClientOp c;
+                c.uid = G(sc.guid); c.opId = op; c.amount = amt;
+                pending.push_back(c);
+                pending_res.push_back(r.b ? 1 : 0);
+            }
         } else {
             const uint64_t r = rng.below(20);
             const int e = (int)rng.below(10);
             std::vector<oracle::Arg> a{rng.below(8) == 0 ? oracle::Arg::N() : oracle::Arg::S(std::to_string(e))};
-            if (r < 11) sc.Update(1, a, safe, org);
-            else if (r < 19) sc.Update(2, a, safe, org);
-            else sc.Update(3, {}, false, 0);
+            const int opid = r < 11 ? 1 : r < 19 ? 2 : 3;
+            oracle::GuidGen peek = *sc.gen;  // the Guid.NewGuid() an Add will draw
+            const oracle::Guid tag = peek.next();
+            const auto res = opid == 3 ? sc.Update(3, {}, false, 0) : sc.Update(opid, a, safe, org);
+            if (node == 0) {
+                janus::ClientOp c;
+                c.uid = G(sc.guid); c.opId = opid; c.tag = G(tag);
+                if (a[0].kind == oracle::Arg::Str) c.elem = a[0].s;
+                pending.push_back(c);
+                pending_res.push_back(res.b ? 1 : 0);
+            }
         }
         if ((i + 1) % wave_every == 0 && commit()) return 1;
     }
