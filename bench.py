@@ -189,6 +189,17 @@ def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
             "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
 
 
+def bench_apply_loop():
+    """C5 committed-batch apply through the C++ host mirror; its own JSON."""
+    import subprocess
+    exe = ROOT / "janus-crdt_amd" / "build" / "bench_apply"
+    out = subprocess.run([str(exe), "--accounts", "1000000", "--msgs", "1000000", "--waves", "2", "--cpu-msgs", "100000"],
+                         capture_output=True, text=True, timeout=240)
+    if out.returncode != 0:
+        return {"error": out.stderr[-500:]}
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
 def cpu_baseline():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as orc
@@ -235,6 +246,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
+    apply_loop = bench_apply_loop() if rank == 0 and world == 1 and args.workload == "all" else None
     sync.close()
     if rank != 0:
         return
@@ -279,6 +291,8 @@ def main():
         if "value" not in line:
             line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,
                          "dtype": "u64+u128 records", "config": {"workload": line["orset"]["workload"]}})
+    if apply_loop is not None:
+        line["apply_loop"] = apply_loop
     line["cpu_baseline"] = cpu
     print(json.dumps(line), flush=True)
 

@@ -112,12 +112,30 @@ class GpuStableStore {
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
 
     jg_ctx* ctx() const { return ctx_; }
+    // Wall time of the last ApplyCommitted: host decode/interning vs the engine calls (incl. H2D).
+    double last_apply_host_s() const { return host_s_; }
+    double last_apply_engine_s() const { return engine_s_; }
 
   private:
-    struct PncKey { uint32_t row; std::unordered_map<Guid, uint32_t, GuidHash> cols; };
-    struct SetKey { uint32_t set; std::unordered_map<std::string, uint32_t> elems; };
-    uint32_t column(PncKey& k, const Guid& g);
+    struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id
+    // uid -> KeyRef, open addressing with linear probing: one cache line per lookup on the apply path.
+    class UidTable {
+      public:
+        const KeyRef* find(const Guid& g) const;
+        bool insert(const Guid& g, KeyRef v);  // false if present
+      private:
+        void grow();
+        std::vector<Guid> keys_;
+        std::vector<KeyRef> vals_;
+        std::vector<uint8_t> used_;
+        size_t n_ = 0;
+    };
+    struct SetKey { std::unordered_map<std::string, uint32_t> elems; };
+    // Column of replica g in PNC row `row`; `hint` = its position in the message (messages list
+    // replicas in the sender's insertion order, which usually equals ours).  Appends new replicas.
+    uint32_t column(uint32_t row, const Guid& g, uint32_t hint);
     uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
+    const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
 
     jg_ctx* ctx_ = nullptr;
@@ -125,9 +143,11 @@ class GpuStableStore {
     jg_orset* orset_ = nullptr;
     uint32_t max_keys_, R_, eb_;
     uint32_t next_row_ = 0, next_set_ = 0;
-    std::unordered_map<Guid, CrdtType, GuidHash> type_;
-    std::unordered_map<Guid, PncKey, GuidHash> pnc_keys_;
-    std::unordered_map<Guid, SetKey, GuidHash> set_keys_;
+    double host_s_ = 0, engine_s_ = 0;
+    UidTable uids_;
+    std::vector<uint32_t> ncols_;  // per PNC row: replica columns in use
+    std::vector<Guid> cols_;       // per PNC row: R replica Guids, in first-insertion order
+    std::vector<SetKey> sets_;
 };
 
 }  // namespace janus
