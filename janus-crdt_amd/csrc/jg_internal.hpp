@@ -96,12 +96,20 @@ struct jg_rows {
     jg::DevBuf P, N, keys;
 };
 
-// One sorted tag-record stream, structure of arrays: key[i] (8 B) and tag[i] (16 B).
+// One sorted tag-record stream in the CHUNKED layout (orset_union.hpp): structure of arrays
+// key[slot] (8 B) and tag[slot] (16 B); chunk c holds ranks [off[c], off[c+1]) in slots
+// [c*kChunk, c*kChunk + cnt[c]); lut[q] = the last chunk starting at or before rank q*512.
+constexpr uint32_t kChunk = 3072;  // = one union tile (orset.hip kOB * kItems)
 struct jg_stream_soa {
-    jg::DevBuf key, tag;
-    uint64_t cap = 0;
-    uint64_t n = 0;
-    void reserve(uint64_t c);
+    jg::DevBuf key, tag;  // cap_chunks * kChunk slots
+    jg::DevBuf cnt;       // uint32 [cap_chunks]
+    jg::DevBuf off;       // uint64 [cap_chunks + 1]
+    jg::DevBuf lut;       // uint32 [(cap_chunks * kChunk >> 9) + 2]
+    uint64_t cap_chunks = 0;
+    uint64_t n = 0;       // records (host copy; see jg_orset::counts_pending)
+    uint32_t nch = 0;     // chunks in use
+    bool dense = true;    // chunks full except the last (slot = rank): uploads and generated streams
+    void reserve_records(uint64_t records);  // room for a dense stream or a union output of `records`
     void swap(jg_stream_soa& o);
 };
 
@@ -117,4 +125,6 @@ namespace jg {
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
+// Dense chunk metadata for a stream whose n records sit contiguously in slots [0, n) (async).
+void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n);
 }  // namespace jg

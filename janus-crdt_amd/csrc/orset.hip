@@ -1,22 +1,22 @@
 // orset.hip — OR-Set store and kernels (gfx950, wave64; integer/byte work, no MFMA).
 //
 // Layout in HBM: two record streams per store (adds, tombstones), each structure-of-arrays
-//   key[i] : uint64  = set << 32 | elem          (elem 0xFFFFFFFF = C# null)
-//   tag[i] : 16 B    = the Guid, as {lo, hi} little-endian words
-// sorted strictly increasing by (key, tag.lo, tag.hi).  A (set, elem)'s HashSet<Guid> is the run of
-// its records; Dictionary membership of elem = the run being non-empty.
+//   key : uint64  = set << 32 | elem          (elem 0xFFFFFFFF = C# null)
+//   tag : 16 B    = the Guid, as {lo, hi} little-endian words
+// sorted strictly increasing by (key, tag.lo, tag.hi) in rank order, stored in the chunked layout
+// of orset_union.hpp (chunk = one union tile of kChunk slots).  A (set, elem)'s HashSet<Guid> is the
+// run of its records; Dictionary membership of elem = the run being non-empty.
 //
 // ORSet.Merge (ORSet.cs:253-283) over a keyspace of sets = per-stream sorted set UNION:
-//   k_partition : merge-path split of each TILE-record output diagonal (one binary search each).
-//   k_union     : one tile per workgroup, tickets in launch order.  Stage the tile's slices of A
-//                 and B in LDS, merge (A first on ties), drop a B record equal to the A record
-//                 before it in merged order (the only way a duplicate can appear, since each input
-//                 is duplicate-free), compact through a block scan, and place the tile with a
-//                 decoupled look-back over 8-byte {flag, count} status words (agent-scope relaxed
-//                 atomics: the word IS the data, no payload is handed off between workgroups).
+//   k_partition : merge-path split of every tile boundary (one wave, 64-ary search, each).
+//   k_union     : one tile per workgroup.  Stage the tile's slices of A and B in LDS, merge (A first
+//                 on ties), drop a B record equal to the A record before it in merged order (the only
+//                 way a duplicate can appear, since each input is duplicate-free), compact through a
+//                 block scan, write the tile into ITS OWN output chunk.  No inter-workgroup traffic.
+//   k_finish    : the output's chunk offsets and rank -> chunk table (one small launch).
 //   Roofline: HBM.  Reads 24 B per input record, writes 24 B per output record.
-// ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams,
-// then SetEquals of the two sorted runs.
+// ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams
+// (rank space), then SetEquals of the two sorted runs.
 #include <algorithm>
 #include <set>
 #include <unordered_map>
@@ -27,18 +27,25 @@
 
 namespace {
 
-// Tile shape chosen by measurement (tools/tune_orset.hip; profiles/r01/tune_orset_*.txt): 512 x 6 =
-// 3072 records per tile, 74 KB LDS, 2 workgroups per CU.
+// Tile shape chosen by measurement (tools/tune_orset_lookback.hip; profiles/r01/tune_orset_*.txt):
+// 512 x 6 = 3072 records per tile, 74 KB LDS, 2 workgroups per CU.
 constexpr int kOB = 512;   // threads per workgroup
 constexpr int kItems = 6;  // records per thread per tile
 constexpr int kTile = kOB * kItems;
+static_assert(kTile == (int)kChunk, "a union tile fills exactly one stream chunk");
+constexpr int kPartLanes = 1;  // lanes per tile boundary in k_partition (tools/tune_orset.hip)
 
 using jgk::Tag;
 using jgk::ld_tag;
 using jgk::to_u4;
 using jgk::rec_lt;
+using jgk::View;
 
-// Strictly increasing check: err |= 1 at the first non-increasing neighbour pair.
+View view(const jg_stream_soa& s) {
+    return View{s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.off.as<uint64_t>(), s.lut.as<uint32_t>(), s.n, s.nch, kChunk, s.dense ? 1u : 0u};
+}
+
+// Strictly increasing check of a DENSE stream: err |= 1 at the first non-increasing neighbour pair.
 __global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* __restrict__ k, const uint4* __restrict__ t, uint64_t n,
                                                       unsigned* err) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i + 1 < n; i += (uint64_t)gridDim.x * kOB) {
@@ -46,7 +53,7 @@ __global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* 
     }
 }
 
-// AoS <-> SoA for host transfers.
+// Host AoS records -> dense SoA stream.
 __global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in, uint64_t n, unsigned long long* __restrict__ k,
                                                 uint4* __restrict__ t) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
@@ -55,36 +62,39 @@ __global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in
         t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
     }
 }
-__global__ __launch_bounds__(kOB) void k_pack(const unsigned long long* __restrict__ k, const uint4* __restrict__ t, uint64_t n,
-                                              jg_tagrec* __restrict__ out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
-        const Tag g = ld_tag(t + i);
-        out[i] = jg_tagrec{k[i], g.lo, g.hi};
+// Chunked SoA stream -> AoS records in rank order (walks slots; skips each chunk's unused tail).
+__global__ __launch_bounds__(kOB) void k_pack(View v, const uint32_t* __restrict__ cnt, jg_tagrec* __restrict__ out) {
+    const uint64_t slots = (uint64_t)v.nch * v.C;
+    for (uint64_t x = (uint64_t)blockIdx.x * kOB + threadIdx.x; x < slots; x += (uint64_t)gridDim.x * kOB) {
+        const uint64_t c = x / v.C, j = x - c * v.C;
+        if (j < cnt[c]) {
+            const Tag g = ld_tag(v.tag + x);
+            out[v.off[c] + j] = jg_tagrec{v.key[x], g.lo, g.hi};
+        }
     }
 }
 
-__device__ __forceinline__ uint64_t lower_key(const unsigned long long* k, uint64_t n, unsigned long long q) {
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (k[m] < q) lo = m + 1; else hi = m; }
+__device__ __forceinline__ unsigned long long key_at(const View& v, uint64_t r) { return v.key[jgk::slot_of(v, r)]; }
+__device__ __forceinline__ uint64_t lower_key(const View& v, unsigned long long q) {
+    uint64_t lo = 0, hi = v.n;
+    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (key_at(v, m) < q) lo = m + 1; else hi = m; }
     return lo;
 }
-__device__ __forceinline__ uint64_t upper_key(const unsigned long long* k, uint64_t n, unsigned long long q) {
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (k[m] <= q) lo = m + 1; else hi = m; }
+__device__ __forceinline__ uint64_t upper_key(const View& v, unsigned long long q) {
+    uint64_t lo = 0, hi = v.n;
+    while (lo < hi) { const uint64_t m = (lo + hi) >> 1; if (key_at(v, m) <= q) lo = m + 1; else hi = m; }
     return lo;
 }
 
-__global__ __launch_bounds__(kOB) void k_contains(const unsigned long long* __restrict__ akey, const uint4* __restrict__ atag, uint64_t na,
-                                                  const unsigned long long* __restrict__ rkey, const uint4* __restrict__ rtag, uint64_t nr,
-                                                  const unsigned long long* __restrict__ q, uint64_t nq, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(kOB) void k_contains(View a, View r, const unsigned long long* __restrict__ q, uint64_t nq, uint8_t* __restrict__ out) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kOB) {
         const unsigned long long key = q[i];
-        const uint64_t a0 = lower_key(akey, na, key), a1 = upper_key(akey, na, key);
-        const uint64_t r0 = lower_key(rkey, nr, key), r1 = upper_key(rkey, nr, key);
+        const uint64_t a0 = lower_key(a, key), a1 = upper_key(a, key);
+        const uint64_t r0 = lower_key(r, key), r1 = upper_key(r, key);
         const uint64_t ca = a1 - a0, cr = r1 - r0;
         bool same = ca == cr;
         for (uint64_t j = 0; same && j < ca; ++j) {
-            const Tag x = ld_tag(atag + a0 + j), y = ld_tag(rtag + r0 + j);
+            const Tag x = ld_tag(a.tag + jgk::slot_of(a, a0 + j)), y = ld_tag(r.tag + jgk::slot_of(r, r0 + j));
             same = x.lo == y.lo && x.hi == y.hi;
         }
         bool present;
@@ -94,26 +104,25 @@ __global__ __launch_bounds__(kOB) void k_contains(const unsigned long long* __re
     }
 }
 
-// Run bounds of each queried key in both streams: out[4i..4i+3] = a0, a1, r0, r1.
-__global__ __launch_bounds__(kOB) void k_runs(const unsigned long long* __restrict__ akey, uint64_t na, const unsigned long long* __restrict__ rkey,
-                                              uint64_t nr, const unsigned long long* __restrict__ q, uint64_t nq, uint64_t* __restrict__ out) {
+// Rank bounds of each queried key's run in both streams: out[4i..4i+3] = a0, a1, r0, r1.
+__global__ __launch_bounds__(kOB) void k_runs(View a, View r, const unsigned long long* __restrict__ q, uint64_t nq, uint64_t* __restrict__ out) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kOB) {
         const unsigned long long key = q[i];
-        out[4 * i + 0] = lower_key(akey, na, key);
-        out[4 * i + 1] = upper_key(akey, na, key);
-        out[4 * i + 2] = lower_key(rkey, nr, key);
-        out[4 * i + 3] = upper_key(rkey, nr, key);
+        out[4 * i + 0] = lower_key(a, key);
+        out[4 * i + 1] = upper_key(a, key);
+        out[4 * i + 2] = lower_key(r, key);
+        out[4 * i + 3] = upper_key(r, key);
     }
 }
 
-// Copy ranges [src_off[i], src_off[i] + len[i]) of a stream to dst[dst_off[i] ...] as AoS records.
-__global__ __launch_bounds__(kOB) void k_gather_ranges(const unsigned long long* __restrict__ k, const uint4* __restrict__ t,
-                                                       const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ len,
+// Copy rank ranges [src_off[i], src_off[i] + len[i]) of a stream to dst[dst_off[i] ...] as AoS records.
+__global__ __launch_bounds__(kOB) void k_gather_ranges(View v, const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ len,
                                                        const uint64_t* __restrict__ dst_off, uint64_t n, jg_tagrec* __restrict__ dst) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
         for (uint64_t j = 0; j < len[i]; ++j) {
-            const Tag g = ld_tag(t + src_off[i] + j);
-            dst[dst_off[i] + j] = jg_tagrec{k[src_off[i] + j], g.lo, g.hi};
+            const uint64_t x = jgk::slot_of(v, src_off[i] + j);
+            const Tag g = ld_tag(v.tag + x);
+            dst[dst_off[i] + j] = jg_tagrec{v.key[x], g.lo, g.hi};
         }
     }
 }
@@ -125,42 +134,46 @@ unsigned grid_for(jg_ctx* ctx, uint64_t items, unsigned per_cu = 8) {
     return g == 0 ? 1u : (unsigned)g;
 }
 
-// Workspace of one union: [status n_tiles x 8 | ticket | pad to 256][part (n_tiles+1) x 8 | pad].
+uint64_t tiles_for(uint64_t records) { return (records + kTile - 1) / kTile; }
+
+// Workspace of one union: [part (n_tiles+1) x 8 | pad][pchunk 2 (n_tiles+1) x 4 | pad].
 size_t union_ws_bytes(uint64_t total) {
-    const uint64_t n_tiles = (total + kTile - 1) / kTile;
-    return (((n_tiles * 8 + 16) + 255) & ~(size_t)255) + (((n_tiles + 1) * 8 + 255) & ~(size_t)255);
+    const uint64_t p = tiles_for(total) + 1;
+    return ((p * 8 + 255) & ~(size_t)255) + ((p * 8 + 255) & ~(size_t)255);
 }
 
-// Union of two streams into `out` (capacity checked by the caller).  Async on ctx->stream; the
-// output count lands in *d_count (device).  `ws` holds union_ws_bytes(a.n + b.n) bytes.
+// Union of two streams into `out` (chunk capacity ensured here).  Async on ctx->stream; the output
+// record count lands in *d_count (device) and out.n is left for sync_counts.
 void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws,
-                  const unsigned* drop = nullptr) {
+                  jgk::Drop drop) {
     const uint64_t total = a.n + b.n;
+    out.reserve_records(total);
     if (total == 0) {
+        jg::set_dense(ctx, out, 0);
         JG_HIP(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), ctx->stream));
         return;
     }
-    const uint64_t n_tiles = (total + kTile - 1) / kTile;
-    const size_t status_bytes = ((n_tiles * 8 + 16) + 255) & ~(size_t)255;
-    auto* status = reinterpret_cast<unsigned long long*>(ws);
-    auto* ticket = reinterpret_cast<unsigned*>(ws + n_tiles * 8);
-    auto* part = reinterpret_cast<uint64_t*>(ws + status_bytes);
-    JG_HIP(hipMemsetAsync(ws, 0, status_bytes, ctx->stream));  // every polled word zeroed per call
-    hipLaunchKernelGGL((jgk::k_partition<kOB, kItems>), dim3((unsigned)((n_tiles + 1 + kOB - 1) / kOB)), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(),
-                       a.tag.as<uint4>(), a.n, b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, n_tiles + 1, part);
+    const uint64_t n_tiles = tiles_for(total);
+    JG_REQUIRE(n_tiles < 0xFFFFFFFFull, JG_EINVAL, "union: %llu records exceed the chunk index range", (unsigned long long)total);
+    auto* part = reinterpret_cast<uint64_t*>(ws);
+    auto* pchunk = reinterpret_cast<uint32_t*>(ws + (((n_tiles + 1) * 8 + 255) & ~(size_t)255));
+    const View va = view(a), vb = view(b);
+    hipLaunchKernelGGL((jgk::k_partition<kTile, kPartLanes>), dim3((unsigned)(((n_tiles + 1) * kPartLanes + 255) / 256)), dim3(256), 0,
+                       ctx->stream, va, vb, n_tiles + 1, part, pchunk);
     JG_HIP(hipGetLastError());
-    hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, a.key.as<unsigned long long>(), a.tag.as<uint4>(), a.n,
-                       b.key.as<unsigned long long>(), b.tag.as<uint4>(), b.n, part, n_tiles, out.key.as<unsigned long long>(),
-                       out.tag.as<uint4>(), status, ticket, d_count, ctx->flags.as<unsigned>(), drop);
+    hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, va, vb, part, pchunk,
+                       out.key.as<unsigned long long>(), out.tag.as<uint4>(), out.cnt.as<uint32_t>(), drop);
     JG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(jgk::k_finish, dim3((unsigned)((n_tiles + 1023) / 1024)), dim3(1024), 0, ctx->stream, out.cnt.as<uint32_t>(),
+                       (uint32_t)n_tiles, out.off.as<uint64_t>(), out.lut.as<uint32_t>(), (total >> jgk::kQShift) + 2, d_count);
+    JG_HIP(hipGetLastError());
+    out.nch = (uint32_t)n_tiles;
+    out.dense = false;
 }
 
 // Union of both streams of two stores into `oa`/`orr`; counts to counted->counts.
 void union_store(jg_ctx* ctx, const jg_orset* a, const jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted,
-                 const unsigned* drop = nullptr) {
-    JG_REQUIRE(oa.cap >= a->add.n + b->add.n && orr.cap >= a->rem.n + b->rem.n, JG_ESTATE,
-               "union: output capacity (%llu, %llu) < inputs (%llu, %llu)", (unsigned long long)oa.cap, (unsigned long long)orr.cap,
-               (unsigned long long)(a->add.n + b->add.n), (unsigned long long)(a->rem.n + b->rem.n));
+                 jgk::Drop drop = {nullptr, 0}) {
     unsigned long long* d = counted->counts.as<unsigned long long>();
     const size_t ws_add = union_ws_bytes(a->add.n + b->add.n);
     char* ws = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, ws_add + union_ws_bytes(a->rem.n + b->rem.n)));
@@ -176,13 +189,13 @@ void check_err_flag(jg_ctx* ctx, const char* fn) {
     if (h) {
         JG_HIP(hipMemsetAsync(ctx->flags.p, 0, sizeof h, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
-        jg::fail(JG_ESTATE, "%s: device reported a broken precondition or look-back timeout (flag %u)", fn, h);
+        jg::fail(JG_ESTATE, "%s: device reported a broken precondition (flag %u)", fn, h);
     }
 }
 
 void upload_stream(jg_ctx* ctx, jg_stream_soa& s, const jg_tagrec* recs, uint64_t n, const char* fn) {
-    s.reserve(n);
-    s.n = n;
+    s.reserve_records(n);
+    jg::set_dense(ctx, s, n);
     if (n == 0) return;
     auto* st = static_cast<jg_tagrec*>(jg::scratch(ctx, ctx->scratch2, n * sizeof(jg_tagrec)));
     JG_HIP(hipMemcpyAsync(st, recs, n * sizeof(jg_tagrec), hipMemcpyHostToDevice, ctx->stream));
@@ -197,19 +210,16 @@ void upload_stream(jg_ctx* ctx, jg_stream_soa& s, const jg_tagrec* recs, uint64_
 void download_stream(jg_ctx* ctx, const jg_stream_soa& s, jg_tagrec* out) {
     if (s.n == 0) return;
     auto* st = static_cast<jg_tagrec*>(jg::scratch(ctx, ctx->scratch2, s.n * sizeof(jg_tagrec)));
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(ctx, s.n, 16)), dim3(kOB), 0, ctx->stream, s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.n,
-                       st);
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(ctx, (uint64_t)s.nch * kChunk, 16)), dim3(kOB), 0, ctx->stream, view(s), s.cnt.as<uint32_t>(), st);
     JG_HIP(hipGetLastError());
     JG_HIP(hipMemcpyAsync(out, st, s.n * sizeof(jg_tagrec), hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 // In-place merge: s = (s minus the records of sets flagged in `drop`) ∪ src.
-void merge_into(jg_orset* s, const jg_orset* src, bool async, const unsigned* drop = nullptr) {
+void merge_into(jg_orset* s, const jg_orset* src, bool async, jgk::Drop drop = {nullptr, 0}) {
     jg_ctx* ctx = s->ctx;
     jg::sync_counts(s);
-    s->spare_add.reserve(s->add.n + src->add.n);
-    s->spare_rem.reserve(s->rem.n + src->rem.n);
     union_store(ctx, s, src, s->spare_add, s->spare_rem, s, drop);
     s->add.swap(s->spare_add);
     s->rem.swap(s->spare_rem);
@@ -243,8 +253,8 @@ void gather_stream(jg_ctx* ctx, const jg_stream_soa& st, const std::vector<uint6
     JG_HIP(hipMemcpyAsync(m, src.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
     JG_HIP(hipMemcpyAsync(m + n, len.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
     JG_HIP(hipMemcpyAsync(m + 2 * n, off.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st.key.as<unsigned long long>(),
-                       st.tag.as<uint4>(), m, m + n, m + 2 * n, n, data.as<jg_tagrec>());
+    hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(st), m, m + n, m + 2 * n, n,
+                       data.as<jg_tagrec>());
     JG_HIP(hipGetLastError());
     JG_HIP(hipMemcpyAsync(out.data(), data.p, off[n] * sizeof(jg_tagrec), hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
@@ -262,8 +272,7 @@ Runs fetch_runs(jg_orset* s, const std::vector<unsigned long long>& keys) {
     auto* dq = q.as<unsigned long long>();
     auto* db = reinterpret_cast<uint64_t*>(dq + n);
     JG_HIP(hipMemcpyAsync(dq, keys.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_runs, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s->add.key.as<unsigned long long>(), s->add.n,
-                       s->rem.key.as<unsigned long long>(), s->rem.n, dq, n, db);
+    hipLaunchKernelGGL(k_runs, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dq, n, db);
     JG_HIP(hipGetLastError());
     std::vector<uint64_t> bounds(4 * n);
     JG_HIP(hipMemcpyAsync(bounds.data(), db, 4 * n * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -354,43 +363,66 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
 
     jg_ctx* ctx = s->ctx;
     jg::DevBuf drop;
+    jgk::Drop d{nullptr, 0};
     if (!cleared.empty()) {
-        // The union reads drop[set >> 5] for every store record, so the bitmap covers the largest set
-        // id in the store (the last key of each sorted stream), not just the cleared ones.
-        uint64_t max_set = *std::max_element(cleared.begin(), cleared.end());
-        unsigned long long last[2] = {0, 0};
-        if (s->add.n) JG_HIP(hipMemcpy(&last[0], s->add.key.as<unsigned long long>() + s->add.n - 1, 8, hipMemcpyDeviceToHost));
-        if (s->rem.n) JG_HIP(hipMemcpy(&last[1], s->rem.key.as<unsigned long long>() + s->rem.n - 1, 8, hipMemcpyDeviceToHost));
-        max_set = std::max<uint64_t>(max_set, std::max(last[0] >> 32, last[1] >> 32));
+        const uint32_t max_set = *std::max_element(cleared.begin(), cleared.end());
         std::vector<unsigned> bits((max_set >> 5) + 1, 0u);
         for (uint32_t c : cleared) bits[c >> 5] |= 1u << (c & 31);
         drop.alloc(bits.size() * 4);
         JG_HIP(hipMemcpyAsync(drop.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        d = jgk::Drop{drop.as<unsigned>(), (uint32_t)bits.size()};
     }
     if (dadd.empty() && drem.empty() && cleared.empty()) return;
     jg_orset tmp;
     tmp.ctx = ctx;
     upload_stream(ctx, tmp.add, dadd.data(), dadd.size(), "jg_orset_apply_ops(add)");
     upload_stream(ctx, tmp.rem, drem.data(), drem.size(), "jg_orset_apply_ops(rem)");
-    merge_into(s, &tmp, false, drop.as<unsigned>());
+    merge_into(s, &tmp, false, d);
 }
 
 }  // namespace
 
 void jg_stream_soa::swap(jg_stream_soa& o) {
-    std::swap(key.p, o.key.p); std::swap(key.bytes, o.key.bytes);
-    std::swap(tag.p, o.tag.p); std::swap(tag.bytes, o.tag.bytes);
-    std::swap(cap, o.cap); std::swap(n, o.n);
+    auto swap_buf = [](jg::DevBuf& x, jg::DevBuf& y) {
+        std::swap(x.p, y.p);
+        std::swap(x.bytes, y.bytes);
+    };
+    swap_buf(key, o.key);
+    swap_buf(tag, o.tag);
+    swap_buf(cnt, o.cnt);
+    swap_buf(off, o.off);
+    swap_buf(lut, o.lut);
+    std::swap(cap_chunks, o.cap_chunks);
+    std::swap(n, o.n);
+    std::swap(nch, o.nch);
+    std::swap(dense, o.dense);
 }
 
-void jg_stream_soa::reserve(uint64_t c) {
-    if (c <= cap) return;
-    key.alloc(c * 8);
-    tag.alloc(c * 16);
-    cap = c;
+void jg_stream_soa::reserve_records(uint64_t records) {
+    const uint64_t c = (records + kChunk - 1) / kChunk;
+    if (c <= cap_chunks && off.p) return;
+    const uint64_t slots = c * kChunk;
+    key.alloc(slots * 8);
+    tag.alloc(slots * 16);
+    cnt.alloc((c ? c : 1) * 4);
+    off.alloc((c + 1) * 8);
+    lut.alloc(((slots >> jgk::kQShift) + 2) * 4);
+    cap_chunks = c;
 }
 
 namespace jg {
+void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n) {
+    s.reserve_records(n);
+    const uint64_t nch = (n + kChunk - 1) / kChunk;
+    const uint64_t nlut = (n >> jgk::kQShift) + 2;
+    hipLaunchKernelGGL(jgk::k_dense_meta, dim3(grid_for(ctx, std::max(nch + 1, nlut), 4)), dim3(256), 0, ctx->stream, n, kChunk, (uint32_t)nch,
+                       s.cnt.as<uint32_t>(), s.off.as<uint64_t>(), s.lut.as<uint32_t>(), nlut);
+    JG_HIP(hipGetLastError());
+    s.n = n;
+    s.nch = (uint32_t)nch;
+    s.dense = true;
+}
+
 void sync_counts(jg_orset* s) {
     if (!s->counts_pending) return;
     unsigned long long h[2];
@@ -411,8 +443,10 @@ int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** 
         auto* s = new jg_orset();
         s->ctx = ctx;
         try {
-            s->add.reserve(cap_add);
-            s->rem.reserve(cap_rem);
+            s->add.reserve_records(cap_add);
+            s->rem.reserve_records(cap_rem);
+            jg::set_dense(ctx, s->add, 0);
+            jg::set_dense(ctx, s->rem, 0);
             s->counts.alloc(16);
             JG_HIP(hipMemset(s->counts.p, 0, 16));
         } catch (...) {
@@ -538,9 +572,7 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
         auto* dq = reinterpret_cast<unsigned long long*>(st);
         auto* dout = reinterpret_cast<uint8_t*>(st + n * 8);
         JG_HIP(hipMemcpyAsync(dq, q.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_contains, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s->add.key.as<unsigned long long>(),
-                           s->add.tag.as<uint4>(), s->add.n, s->rem.key.as<unsigned long long>(), s->rem.tag.as<uint4>(), s->rem.n, dq, n,
-                           dout);
+        hipLaunchKernelGGL(k_contains, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dq, n, dout);
         JG_HIP(hipGetLastError());
         JG_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));

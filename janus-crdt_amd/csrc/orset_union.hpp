@@ -1,6 +1,16 @@
-// orset_union.hpp — OR-Set stream-union kernels (merge path + decoupled look-back), templated on
-// the workgroup size and records per thread so the production build (orset.hip) and the tuning tool
-// (tools/tune_orset.hip) compile the same code.  See orset.hip for the algorithm summary.
+// orset_union.hpp — OR-Set record streams in the CHUNKED layout, and their union kernels.
+//
+// A stream is sorted strictly increasing by (key, tag.lo, tag.hi) in RANK space, stored in chunks of
+// C slots: chunk c holds ranks [off[c], off[c+1]) in slots [c*C, c*C + cnt[c]).  A union tile writes
+// its output straight into its own chunk, so no workgroup ever waits on another: the contiguous
+// layout needed a decoupled look-back that measured 32-36 % of every tile and 57 % more kernel time
+// (tools/tune_orset_lookback.hip).  Readers translate rank -> slot with a lookup table:
+// lut[q] = the last chunk starting at or before rank q * 512, so the chunk of rank r lies in
+// [lut[r >> 9], lut[(r >> 9) + 1]] — usually one candidate, a short binary search when a Clear left
+// empty chunks behind.
+//
+// Templated on the workgroup size and records per thread so the production build (orset.hip) and
+// the tuning tool (tools/tune_orset.hip) compile the same code.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -9,11 +19,7 @@
 
 namespace jgk {
 
-
-constexpr unsigned long long kFlagAgg = 1ull << 62;
-constexpr unsigned long long kFlagIncl = 2ull << 62;
-constexpr unsigned long long kValMask = (1ull << 62) - 1;
-constexpr unsigned kSpinLimit = 1u << 22;
+constexpr int kQShift = 9;  // LUT granularity: one entry per 512 ranks
 
 struct Tag { unsigned long long lo, hi; };
 
@@ -28,170 +34,170 @@ __device__ __forceinline__ bool rec_eq(unsigned long long ka, Tag ta, unsigned l
     return (ka == kb) & (ta.lo == tb.lo) & (ta.hi == tb.hi);
 }
 
-// Merge-path split for diagonal d over (a, b): number of A records among the first d merged.
-template <int kOB, int kItems>
-__global__ __launch_bounds__(kOB) void k_partition(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                                   const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                                   uint64_t n_parts, uint64_t* __restrict__ part) {
-    constexpr int kTile = kOB * kItems;
-    const uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x;
-    if (i >= n_parts) return;
-    const uint64_t total = na + nb;
-    const uint64_t d = i * kTile < total ? i * kTile : total;
-    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+// Read view of one chunked stream (plain pointers: passed by value to kernels).
+struct View {
+    const unsigned long long* key;
+    const uint4* tag;
+    const uint64_t* off;  // [nch + 1]
+    const uint32_t* lut;  // [(n >> kQShift) + 2]
+    uint64_t n;
+    uint32_t nch;
+    uint32_t C;
+    uint32_t dense;  // 1: off[c] = c*C (slot = rank), set for uploaded and generated streams
+};
+
+__device__ __forceinline__ uint32_t chunk_of(const View& v, uint64_t r) {  // r < n: the last chunk with off <= r
+    if (v.dense) return (uint32_t)(r / v.C);
+    const uint64_t q = r >> kQShift;
+    uint32_t lo = v.lut[q], hi = v.lut[q + 1];
     while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        const unsigned long long ka = ak[mid], kb = bk[d - 1 - mid];
-        bool a_le_b;  // a[mid] <= b[d-1-mid]  -> take more from A
-        if (ka != kb) a_le_b = ka < kb;
-        else a_le_b = !rec_lt(kb, ld_tag(bt + d - 1 - mid), ka, ld_tag(at + mid));
-        if (a_le_b) lo = mid + 1;
-        else hi = mid;
+        const uint32_t m = (lo + hi + 1) >> 1;
+        if (v.off[m] <= r) lo = m;
+        else hi = m - 1;
     }
-    part[i] = lo;
+    return lo;
 }
-
-// Wave 0 of a tile: sum the counts of all earlier tiles (decoupled look-back).  kLB windows of 64
-// predecessors are fetched per round trip (one status word per lane and window); a window is only
-// re-polled while some of its tiles have not published yet.
-template <int kLB>
-__device__ inline unsigned long long lookback(unsigned long long* status, long long tile, int lane, unsigned* err) {
-    unsigned long long excl = 0;
-    long long base = tile - 1;
-    unsigned spins = 0;
-    for (;;) {
-        unsigned long long w[kLB];
-#pragma unroll
-        for (int j = 0; j < kLB; ++j) {
-            const long long idx = base - 64 * j - lane;
-            w[j] = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
-        }
-#pragma unroll
-        for (int j = 0; j < kLB; ++j) {
-            const long long idx = base - 64 * j - lane;
-            while (!__all((w[j] >> 62) != 0)) {
-                if (++spins > kSpinLimit) {  // wave-uniform: give up, flag the call, let the grid drain
-                    if (lane == 0) atomicOr(err, 1u);
-                    w[j] = kFlagIncl;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-                w[j] = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kFlagIncl;
-            }
-            const unsigned long long incl = __ballot((w[j] >> 62) == 2);
-            const int first = incl ? __ffsll((long long)incl) - 1 : 64;
-            unsigned long long v = lane <= first ? (w[j] & kValMask) : 0ull;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-            excl += v;
-            if (incl) return excl;
-        }
-        base -= 64 * kLB;
-    }
-}
-
-// ---- one tile of the union, split into phases so the one-shot and the persistent kernels share it ----
-struct TileBounds {
-    uint64_t i0, j0;  // first A / B record of the tile
-    int nA, nB;       // records of A / B in the tile
-};
-
-template <int kOB, int kItems>
-__device__ __forceinline__ TileBounds tile_bounds(uint64_t tile, const uint64_t* __restrict__ part, uint64_t na, uint64_t nb) {
-    constexpr uint64_t kTile = (uint64_t)kOB * kItems;
-    const uint64_t total = na + nb;
-    const uint64_t d0 = tile * kTile;
-    const uint64_t d1 = d0 + kTile < total ? d0 + kTile : total;
-    const uint64_t i0 = part[tile], i1 = part[tile + 1];
-    TileBounds b;
-    b.i0 = i0;
-    b.j0 = d0 - i0;
-    b.nA = (int)(i1 - i0);
-    b.nB = (int)((d1 - i1) - b.j0);
-    return b;
-}
-
-// A tile's records held in registers between the global loads and the LDS writes (scalar arrays:
-// they stay in VGPRs; arrays of uint4 went to scratch).
-template <int kItems>
-struct TileRegs {
-    unsigned long long k[kItems], lo[kItems], hi[kItems];
-    unsigned long long pk, plo, phi;  // A record before the tile (thread 0 only)
-};
-
-// Issue every global load of the tile (unconditional: index clamped into the tile, n >= 1).
-template <int kOB, int kItems>
-__device__ __forceinline__ void tile_load(TileRegs<kItems>& r, const TileBounds& b, const unsigned long long* __restrict__ ak,
-                                          const uint4* __restrict__ at, const unsigned long long* __restrict__ bk,
-                                          const uint4* __restrict__ bt, int tid) {
-    const int n = b.nA + b.nB;
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {
-        const int x = min(it * kOB + tid, n - 1);
-        const bool from_a = x < b.nA;
-        const uint64_t gi = from_a ? b.i0 + (uint64_t)x : b.j0 + (uint64_t)(x - b.nA);
-        r.k[it] = (from_a ? ak : bk)[gi];
-        const Tag t = ld_tag((from_a ? at : bt) + gi);
-        r.lo[it] = t.lo;
-        r.hi[it] = t.hi;
-    }
-    if (tid == 0 && b.i0 > 0) {
-        r.pk = ak[b.i0 - 1];
-        const Tag t = ld_tag(at + b.i0 - 1);
-        r.plo = t.lo;
-        r.phi = t.hi;
-    }
+__device__ __forceinline__ uint64_t slot_of(const View& v, uint64_t r) {
+    if (v.dense) return r;
+    const uint32_t c = chunk_of(v, r);
+    return (uint64_t)c * v.C + (r - v.off[c]);
 }
 
 // Set-indexed drop bitmap (ORSet.Clear applied inside a batch of ops): A-side records whose set bit
-// is 1 are removed from the union.  nullptr = keep everything.
-__device__ __forceinline__ bool dropped(const unsigned* drop, unsigned long long key) {
-    if (!drop) return false;
+// is 1 are removed from the union; sets past the bitmap's `words` are kept.  nullptr = keep all.
+struct Drop {
+    const unsigned* bits;
+    uint32_t words;
+};
+__device__ __forceinline__ bool dropped(const Drop& d, unsigned long long key) {
     const unsigned set = (unsigned)(key >> 32);
-    return (drop[set >> 5] >> (set & 31)) & 1u;
+    return d.bits && (set >> 5) < d.words && ((d.bits[set >> 5] >> (set & 31)) & 1u);
 }
 
-struct TileLds {
-    unsigned long long* key;
-    uint4* tag;
-    unsigned long long* prev_key;
-    uint4* prev_tag;
-    int* has_prev;
-    unsigned long long* excl;
-    int* wsum;
-};
+// Merge-path split of output tile boundary w (diagonal d = w*C in merged order): the number of A
+// records among the first d (A first on ties).  L lanes cooperate on one boundary with an
+// (L+1)-ary search (L = 1: plain binary search); tags are read only when keys tie.  Also records
+// the chunk holding the first A and B rank of the tile (saves the tile one dependent lookup).
+template <int C, int L>
+__global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_parts, uint64_t* __restrict__ part,
+                                                   uint32_t* __restrict__ pchunk) {
+    static_assert(L >= 1 && L <= 64 && 64 % L == 0, "lanes per boundary must divide the wave");
+    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t w = gt / L;
+    const int gl = (int)(gt % L);
+    const int gbase = (int)(threadIdx.x & 63) - gl;  // first lane of this boundary's group
+    const uint64_t total = a.n + b.n;
+    const bool active = w < n_parts;
+    const uint64_t d = !active ? 0 : w * C < total ? w * C : total;
+    uint64_t lo = d > b.n ? d - b.n : 0, hi = d < a.n ? d : a.n;
+    if (!active) hi = lo;
+    while (__ballot(lo < hi)) {  // invariant: A[m] <= B[d-1-m] holds for m < split, fails from split on
+        const uint64_t W = hi - lo;
+        const bool valid = lo < hi;
+        bool fail = false;
+        if (valid) {
+            const uint64_t m = lo + ((uint64_t)(gl + 1) * W) / (L + 1);
+            const uint64_t sa = slot_of(a, m), sb = slot_of(b, d - 1 - m);
+            const unsigned long long ka = a.key[sa], kb = b.key[sb];
+            fail = ka != kb ? kb < ka : rec_lt(kb, ld_tag(b.tag + sb), ka, ld_tag(a.tag + sa));
+        }
+        const unsigned long long fm = __ballot(fail);
+        const unsigned long long mine = L == 64 ? fm : (fm >> gbase) & ((1ull << (L & 63)) - 1);
+        if (valid) {
+            if (mine == 0) {
+                lo = lo + ((uint64_t)L * W) / (L + 1) + 1;
+            } else {
+                const uint64_t k = (uint64_t)(__ffsll((long long)mine) - 1);
+                const uint64_t nlo = k > 0 ? lo + (k * W) / (L + 1) + 1 : lo;
+                hi = lo + ((k + 1) * W) / (L + 1);
+                lo = nlo;
+            }
+        }
+    }
+    if (active && gl == 0) {
+        const uint64_t i = lo, j = d - lo;
+        part[w] = i;
+        pchunk[2 * w] = i < a.n ? chunk_of(a, i) : a.nch;
+        pchunk[2 * w + 1] = j < b.n ? chunk_of(b, j) : b.nch;
+    }
+}
 
+// One tile: A ranks [i0, i1), B ranks [j0, j1) -> chunk `tile` of the output (capacity kOB*kItems).
 template <int kOB, int kItems>
-__device__ __forceinline__ void tile_stage(const TileRegs<kItems>& r, const TileBounds& b, const TileLds& L, int tid,
-                                           const unsigned* drop = nullptr) {
+__global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* __restrict__ part, const uint32_t* __restrict__ pchunk,
+                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ ocnt,
+                                               Drop drop) {
+    constexpr int kTile = kOB * kItems;
+    constexpr int kSeg = 64;  // chunks a tile's A (or B) range may span before the slow path
+    __shared__ unsigned long long s_key[kTile];
+    __shared__ uint4 s_tag[kTile];
+    __shared__ uint64_t s_off[2][kSeg + 1];  // chunk boundaries around the A (0) and B (1) ranges
+    __shared__ unsigned long long s_prev_key;
+    __shared__ uint4 s_prev_tag;
+    __shared__ int s_has_prev;
+    __shared__ int s_wsum[kOB / 64];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t total_in = a.n + b.n;
+    const uint64_t d0 = tile * kTile;
+    const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
+    const uint64_t i0 = part[tile], i1 = part[tile + 1];
+    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0), n = nA + nB;
+    const uint32_t ca = pchunk[2 * tile], cb = pchunk[2 * tile + 1];
+
+    // ---- chunk boundaries around the tile's A and B ranges (waves 0 and 1) ----
+    if (wid == 0) {
+        const uint32_t c = ca + lane;
+        s_off[0][lane] = c <= a.nch ? a.off[c] : a.n;
+        if (lane == 0) s_off[0][kSeg] = ca + kSeg <= a.nch ? a.off[ca + kSeg] : a.n;
+    } else if (wid == 1) {
+        const uint32_t c = cb + lane;
+        s_off[1][lane] = c <= b.nch ? b.off[c] : b.n;
+        if (lane == 0) s_off[1][kSeg] = cb + kSeg <= b.nch ? b.off[cb + kSeg] : b.n;
+    }
+    __syncthreads();
+
+    // ---- stage the tile in LDS; every load issued before the first LDS write ----
+    {
+        unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
 #pragma unroll
-    for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
-        const int x = it * kOB + tid;
-        L.key[x] = r.k[it];
-        L.tag[x] = to_u4(Tag{r.lo[it], r.hi[it]});
+        for (int it = 0; it < kItems; ++it) {
+            const int x = min(it * kOB + tid, n - 1);  // clamped: unconditional loads (n >= 1)
+            const bool from_a = x < nA;
+            const uint64_t r = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
+            const int side = from_a ? 0 : 1;
+            int s = 0;
+            while (s < kSeg && s_off[side][s + 1] <= r) ++s;
+            uint64_t slot;
+            if (s < kSeg) slot = (uint64_t)((from_a ? ca : cb) + s) * (uint64_t)(from_a ? a.C : b.C) + (r - s_off[side][s]);
+            else slot = slot_of(from_a ? a : b, r);  // > 64 tiny chunks under one tile (drop-filtered input)
+            rk[it] = (from_a ? a.key : b.key)[slot];
+            const Tag t = ld_tag((from_a ? a.tag : b.tag) + slot);
+            rlo[it] = t.lo;
+            rhi[it] = t.hi;
+        }
+        unsigned long long pk = 0;
+        Tag pt{0, 0};
+        if (tid == 0 && i0 > 0) {  // the A record before the tile (duplicate check at the seam)
+            const uint64_t ps = slot_of(a, i0 - 1);
+            pk = a.key[ps];
+            pt = ld_tag(a.tag + ps);
+        }
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
+            const int x = it * kOB + tid;
+            s_key[x] = rk[it];
+            s_tag[x] = to_u4(Tag{rlo[it], rhi[it]});
+        }
+        if (tid == 0) {
+            s_has_prev = i0 > 0 && !dropped(drop, pk);
+            s_prev_key = pk;
+            s_prev_tag = to_u4(pt);
+        }
     }
-    if (tid == 0) {
-        *L.has_prev = b.i0 > 0 && !dropped(drop, r.pk);
-        if (b.i0 > 0) { *L.prev_key = r.pk; *L.prev_tag = to_u4(Tag{r.plo, r.phi}); }
-    }
-}
-
-struct NoStamp {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-
-// Merge, de-duplicate, scan, look back, compact and store one staged tile.  Called by the whole
-// workgroup after a barrier that follows tile_stage; ends with the LDS image read for the stores.
-// `stamp(i)` marks phase boundaries in the diagnostic build (tools/tune_orset.hip); a no-op here.
-template <int kOB, int kItems, class Stamp = NoStamp, int kLB = 1>
-__device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b, uint64_t n_tiles, const TileLds& L,
-                                             unsigned long long* __restrict__ ok, uint4* __restrict__ ot, unsigned long long* status,
-                                             unsigned long long* out_count, unsigned* err, int tid, const Stamp& stamp = Stamp(),
-                                             const unsigned* drop = nullptr) {
-    const int lane = tid & 63, wid = tid >> 6;
-    const int nA = b.nA, nB = b.nB, n = nA + nB;
-    unsigned long long* s_key = L.key;
-    uint4* s_tag = L.tag;
+    __syncthreads();
 
     // ---- per-thread merge path + serial merge of kItems outputs ----
     const int diag = min(tid * kItems, n);
@@ -203,15 +209,14 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
         if (a_le_b) lo = mid + 1;
         else hi = mid;
     }
-    stamp(4);
     int ai = lo, bi = diag - lo;
+    // hp: the A record just before the next B record in merged order exists and survives the drop
+    // filter (a B record can only equal that one, since A and B are strictly increasing).
     bool hp;
     unsigned long long pk;
     Tag pt;
-    // hp: the A record just before the next B record in merged order exists and survives the drop
-    // filter (a B record can only equal that one, since A and B are strictly increasing).
     if (ai > 0) { pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); hp = !dropped(drop, pk); }
-    else { hp = *L.has_prev != 0; pk = *L.prev_key; pt = __builtin_bit_cast(Tag, *L.prev_tag); }
+    else { hp = s_has_prev != 0; pk = s_prev_key; pt = __builtin_bit_cast(Tag, s_prev_tag); }
 
     const int my_n = n - diag < kItems ? n - diag : kItems;
     unsigned long long ka = 0, kb = 0;
@@ -241,46 +246,26 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
         }
     }
 
-    stamp(5);
     // ---- block scan of kept counts ----
     const int cnt = __popc(keep);
     int incl = cnt;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const int y = __shfl_up(incl, dd, 64);
+        if (lane >= dd) incl += y;
     }
-    if (lane == 63) L.wsum[wid] = incl;
+    if (lane == 63) s_wsum[wid] = incl;
     __syncthreads();
     int wbase = 0, block_total = 0;
 #pragma unroll
     for (int w = 0; w < kOB / 64; ++w) {
-        const int v = L.wsum[w];
+        const int v = s_wsum[w];
         if (w < wid) wbase += v;
         block_total += v;
     }
     const int my_off = wbase + incl - cnt;
-    stamp(6);
 
-    // ---- publish and look back (wave 0) ----
-    if (wid == 0) {
-        unsigned long long excl = 0;
-        if (tile == 0) {
-            if (lane == 0) __hip_atomic_store(status, kFlagIncl | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(status + tile, kFlagAgg | (unsigned long long)block_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            excl = lookback<kLB>(status, (long long)tile, lane, err);
-            if (lane == 0)
-                __hip_atomic_store(status + tile, kFlagIncl | (excl + (unsigned long long)block_total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            *L.excl = excl;
-            if (tile == n_tiles - 1) *out_count = excl + (unsigned long long)block_total;
-        }
-    }
-
-    stamp(7);
-    // ---- gather kept records, compact through LDS, store coalesced ----
+    // ---- gather kept records, compact through LDS, store coalesced into this tile's chunk ----
     unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {  // src[it] is a valid LDS index even for dropped items
@@ -299,118 +284,80 @@ __device__ __forceinline__ void tile_process(uint64_t tile, const TileBounds& b,
         }
     }
     __syncthreads();
-    stamp(8);
-    const unsigned long long base = *L.excl;
+    const uint64_t base = tile * (uint64_t)kTile;
     for (int x = tid; x < block_total; x += kOB) {
         ok[base + x] = s_key[x];
         ot[base + x] = s_tag[x];
     }
-    stamp(9);
+    if (tid == 0) ocnt[tile] = (uint32_t)block_total;
 }
 
-#define JGK_TILE_LDS(kOB, kItems)                                                                          \
-    __shared__ unsigned long long s_key[(kOB) * (kItems)];                                                 \
-    __shared__ uint4 s_tag[(kOB) * (kItems)];                                                              \
-    __shared__ unsigned long long s_prev_key, s_excl;                                                      \
-    __shared__ uint4 s_prev_tag;                                                                           \
-    __shared__ int s_has_prev;                                                                             \
-    __shared__ unsigned s_tile;                                                                            \
-    __shared__ int s_wsum[(kOB) / 64];                                                                     \
-    const TileLds L{s_key, s_tag, &s_prev_key, &s_prev_tag, &s_has_prev, &s_excl, s_wsum}
-
-// One tile per workgroup; grid = n_tiles.  Tickets (not blockIdx) order the tiles, so a tile only
-// ever waits for tiles already owned by running workgroups.
-template <int kOB, int kItems, int kLB = 1>
-__global__ __launch_bounds__(kOB) void k_union(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                               const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                               const uint64_t* __restrict__ part, uint64_t n_tiles,
-                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
-                                               unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
-                                               unsigned* err, const unsigned* __restrict__ drop = nullptr) {
-    JGK_TILE_LDS(kOB, kItems);
-    const int tid = threadIdx.x;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+// After a union: off = exclusive scan of the tiles' counts (off[nch] = *total = the record count)
+// and the rank -> chunk table, in one launch of ceil(nch / 1024) workgroups.  Each workgroup sums
+// the counts before its 1024 chunks itself (coalesced, L2-resident), so no workgroup waits on
+// another.  lut[q] = the chunk holding rank q*512; entries past the last record name the last chunk
+// (nlut = (n_bound >> kQShift) + 2 for a bound n_bound >= n).
+__global__ __launch_bounds__(1024) void k_finish(const uint32_t* __restrict__ cnt, uint32_t nch, uint64_t* __restrict__ off,
+                                                 uint32_t* __restrict__ lut, uint64_t nlut, unsigned long long* __restrict__ total) {
+    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_base, s_n;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t c0 = blockIdx.x * 1024u;
+    uint64_t pre = 0;
+    for (uint32_t i = tid; i < c0; i += 1024) pre += cnt[i];
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) pre += __shfl_xor(pre, dd, 64);
+    if (lane == 0) s_w[wid] = pre;
     __syncthreads();
-    const uint64_t tile = s_tile;
-    const TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
-    TileRegs<kItems> r;
-    tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
-    tile_stage<kOB, kItems>(r, b, L, tid, drop);
+    if (tid == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < 16; ++w) t += s_w[w];
+        s_base = t;
+    }
     __syncthreads();
-    tile_process<kOB, kItems, NoStamp, kLB>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid, NoStamp(), drop);
-}
-
-// Persistent variant: each workgroup loops over tickets and loads tile t+1 into registers while it
-// merges tile t.  A workgroup takes ticket t+1 before finishing t; the smallest unfinished tile is
-// always some workgroup's current tile, which waits only on finished ones, so progress holds.
-template <int kOB, int kItems>
-__global__ __launch_bounds__(kOB) void k_union_pp(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                                  const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                                  const uint64_t* __restrict__ part, uint64_t n_tiles,
-                                                  unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
-                                                  unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
-                                                  unsigned* err) {
-    JGK_TILE_LDS(kOB, kItems);
-    const int tid = threadIdx.x;
-    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    const uint32_t c = c0 + tid;
+    const uint64_t v = c < nch ? cnt[c] : 0;
+    uint64_t incl = v;
+#pragma unroll
+    for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint64_t y = __shfl_up(incl, dd, 64);
+        if (lane >= dd) incl += y;
+    }
+    if (lane == 63) s_w[wid] = incl;  // s_w reuse: every thread read it before the barrier above
     __syncthreads();
-    uint64_t tile = s_tile;
-    if (tile >= n_tiles) return;
-    TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
-    TileRegs<kItems> r;
-    tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
-    for (;;) {
-        tile_stage<kOB, kItems>(r, b, L, tid);
-        if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+    uint64_t wb = s_base;
+    for (int w = 0; w < wid; ++w) wb += s_w[w];
+    const uint64_t o = wb + incl - v;
+    if (c < nch) {
+        off[c] = o;
+        constexpr uint64_t Q = 1ull << kQShift;
+        for (uint64_t q = (o + Q - 1) >> kQShift; (q << kQShift) < o + v; ++q) lut[q] = c;
+    }
+    if (c + 1 == nch) {  // the last chunk's thread: totals
+        off[nch] = o + v;
+        *total = o + v;
+    }
+    if (blockIdx.x == gridDim.x - 1) {  // tail of the table: ranks at or past the end
         __syncthreads();
-        const uint64_t next = s_tile;
-        TileBounds nb2{0, 0, 0, 0};
-        if (next < n_tiles) {
-            nb2 = tile_bounds<kOB, kItems>(next, part, na, nb);
-            tile_load<kOB, kItems>(r, nb2, ak, at, bk, bt, tid);
-        }
-        tile_process<kOB, kItems>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid);
-        if (next >= n_tiles) break;
-        tile = next;
-        b = nb2;
-        __syncthreads();  // every wave's stores read the LDS image before it is restaged
+        if (c + 1 == nch) s_n = o + v;
+        __syncthreads();
+        const uint64_t n = s_n;
+        for (uint64_t q = ((n + (1ull << kQShift) - 1) >> kQShift) + tid; q < nlut; q += 1024) lut[q] = nch - 1;
     }
 }
 
-// Persistent, statically assigned variant: workgroup b owns tiles b, b+G, b+2G, ... (G = grid) and
-// loads its next tile into registers while it merges the current one.  Tile t only waits on
-// lower tiles, all owned by co-resident workgroups that process theirs in increasing order, so
-// the grid MUST be fully resident (G <= resident workgroups); the bounded spin flags a violation.
-template <int kOB, int kItems, int kLB = 1>
-__global__ __launch_bounds__(kOB) void k_union_ps(const unsigned long long* __restrict__ ak, const uint4* __restrict__ at, uint64_t na,
-                                                  const unsigned long long* __restrict__ bk, const uint4* __restrict__ bt, uint64_t nb,
-                                                  const uint64_t* __restrict__ part, uint64_t n_tiles,
-                                                  unsigned long long* __restrict__ ok, uint4* __restrict__ ot,
-                                                  unsigned long long* status, unsigned* ticket, unsigned long long* out_count,
-                                                  unsigned* err) {
-    JGK_TILE_LDS(kOB, kItems);
-    (void)ticket;
-    (void)s_tile;
-    const int tid = threadIdx.x;
-    uint64_t tile = blockIdx.x;
-    if (tile >= n_tiles) return;
-    TileBounds b = tile_bounds<kOB, kItems>(tile, part, na, nb);
-    TileRegs<kItems> r;
-    tile_load<kOB, kItems>(r, b, ak, at, bk, bt, tid);
-    for (;;) {
-        tile_stage<kOB, kItems>(r, b, L, tid);
-        __syncthreads();
-        const uint64_t next = tile + gridDim.x;
-        TileBounds nb2{0, 0, 0, 0};
-        if (next < n_tiles) {
-            nb2 = tile_bounds<kOB, kItems>(next, part, na, nb);
-            tile_load<kOB, kItems>(r, nb2, ak, at, bk, bt, tid);
-        }
-        tile_process<kOB, kItems, NoStamp, kLB>(tile, b, n_tiles, L, ok, ot, status, out_count, err, tid);
-        if (next >= n_tiles) break;
-        tile = next;
-        b = nb2;
-        __syncthreads();  // every wave's stores read the LDS image before it is restaged
+// Metadata of a dense stream: chunk c = ranks [c*C, min((c+1)*C, n)).
+__global__ __launch_bounds__(256) void k_dense_meta(uint64_t n, uint32_t C, uint32_t nch, uint32_t* __restrict__ cnt, uint64_t* __restrict__ off,
+                                                    uint32_t* __restrict__ lut, uint64_t nlut) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c <= nch; c += stride) {
+        const uint64_t o = c * C < n ? c * C : n;
+        off[c] = o;
+        if (c < nch) cnt[c] = (uint32_t)((c + 1) * C < n ? C : n - o);
+    }
+    for (uint64_t q = (uint64_t)blockIdx.x * 256 + threadIdx.x; q < nlut; q += stride) {
+        const uint64_t c = (q << kQShift) / C;
+        lut[q] = (uint32_t)(c < nch ? c : (nch ? nch - 1 : 0));
     }
 }
 

@@ -93,10 +93,8 @@ int jg_synth_orset(jg_orset* s, uint64_t seed, uint64_t n_groups, uint32_t elems
         jg::ensure_device(ctx);
         jg::sync_counts(s);
         const uint64_t na = n_groups * add_per_group, nr = n_groups * rem_per_group;
-        s->add.reserve(na);
-        s->rem.reserve(nr);
-        s->add.n = na;
-        s->rem.n = nr;
+        jg::set_dense(ctx, s->add, na);
+        jg::set_dense(ctx, s->rem, nr);
         if (na)
             hipLaunchKernelGGL(k_synth_orset, dim3(grid_for(ctx, na)), dim3(kB), 0, ctx->stream, s->add.key.as<unsigned long long>(),
                                s->add.tag.as<uint4>(), na, elems_per_set, add_per_group, add_u0, (unsigned long long)seed);

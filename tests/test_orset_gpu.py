@@ -227,3 +227,63 @@ def test_apply_ops_rejects_bad_op(ctx):
         assert s.size() == (0, 0)
     finally:
         s.close()
+
+
+def _rand_recs(rng, n, n_sets, n_elems, tag_pool):
+    key = (rng.integers(0, n_sets, n).astype(np.uint64) << np.uint64(32)) | rng.integers(0, n_elems, n).astype(np.uint64)
+    t = rng.integers(0, tag_pool, n).astype(np.uint64)
+    return recs(key, t * np.uint64(0x9E3779B97F4A7C15), t)
+
+
+def test_chunked_chain_and_mass_clear(ctx):
+    """Chunked stream layout: a store merged 8 times (each union's output — partially filled chunks
+    from duplicates — is the next union's input), then a Clear of most sets (runs of EMPTY chunks in
+    the middle of the stream), then more unions, Contains and reads; vs numpy set algebra and the
+    oracle's ORSet ops."""
+    rng = np.random.default_rng(77)
+    n_sets, n_elems, pool = 400, 40, 64
+    empty = np.empty(0, jg.REC_DTYPE)
+    acc_a, acc_r = empty, empty
+    s = jg.ORSetStore(ctx, 0, 0)
+    d = jg.ORSetStore(ctx, 0, 0)
+    try:
+        for step in range(8):
+            xa = _rand_recs(rng, 60_000, n_sets, n_elems, pool)
+            xr = _rand_recs(rng, 20_000, n_sets, n_elems, pool)
+            if step % 2:
+                s.merge(xa, xr)                      # host records
+            else:
+                src = _store(ctx, xa, xr)           # device store
+                s.merge_store(src)
+                src.close()
+            d.merge(xa, xr)
+            acc_a, acc_r = np.unique(np.concatenate([acc_a, xa])), np.unique(np.concatenate([acc_r, xr]))
+            ga, gr = s.read()
+            assert np.array_equal(ga, acc_a) and np.array_equal(gr, acc_r), step
+        # Clear sets 20..379 through the op path: most of the stream's chunks become empty
+        sets = np.arange(20, 380, dtype=np.uint32)
+        ops = np.full(len(sets), 3, np.uint8)
+        zero = np.zeros(len(sets), np.uint64)
+        ea, er, eres = orc.orset_apply_ops(acc_a, acc_r, sets, sets * 0, ops, zero, zero)
+        assert np.array_equal(s.apply_ops(sets, sets * 0, ops, zero, zero), eres)
+        ga, gr = s.read()
+        assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+        q_s = rng.integers(0, n_sets, 5000).astype(np.uint32)
+        q_e = rng.integers(0, n_elems, 5000).astype(np.uint32)
+        assert np.array_equal(s.contains(q_s, q_e), orc.orset_contains(ea, er, q_s, q_e))
+        # unions over the cleared (sparse-chunk) store, both as A and as B
+        out = jg.ORSetStore(ctx, 0, 0)
+        jg.ORSetStore.union(d, s, out)
+        ua, ur = out.read()
+        assert np.array_equal(ua, np.unique(np.concatenate([acc_a, ea]))) and np.array_equal(ur, np.unique(np.concatenate([acc_r, er])))
+        jg.ORSetStore.union(s, s, out)
+        ua, ur = out.read()
+        assert np.array_equal(ua, ea) and np.array_equal(ur, er)
+        xa = _rand_recs(rng, 30_000, n_sets, n_elems, pool)
+        s.merge(xa, empty)
+        ga, _ = s.read()
+        assert np.array_equal(ga, np.unique(np.concatenate([ea, xa])))
+        out.close()
+    finally:
+        s.close()
+        d.close()
