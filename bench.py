@@ -160,6 +160,12 @@ def load_traffic(kernel: str):
     return best
 
 
+def _orset_traffic():
+    """PMC HBM bytes of one OR-Set step (both union launches), from the committed profile, if any."""
+    a, r = load_traffic("orset_union_add"), load_traffic("orset_union_rem")
+    return a[0] + r[0] if a and r else None
+
+
 def bench_pnc(jg, ctx, sync, rank, world, steps, warmup):
     key0, n_keys = shard_keys(PNC_KEYS, rank, world)
     store = jg.PNCStore(ctx, n_keys, PNC_R, PNC_EB)
@@ -225,7 +231,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset"], default="all")
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -237,9 +243,9 @@ def main():
     ctx = jg.Context(local)
 
     res = {}
-    if args.workload in ("all", "pnc"):
+    if args.workload in ("all", "pnc", "pnc-orset"):
         res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup)
-    if args.workload in ("all", "orset"):
+    if args.workload in ("all", "orset", "pnc-orset"):
         res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
     ctx.close()
 
@@ -286,7 +292,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
-                         "scope": "whole step (2 x (memset + k_partition + k_union))"},
+                         "traffic": _orset_traffic(),
+                         "scope": "whole step: adds + tombstones, each k_partition + k_union + k_finish"},
         }
         if "value" not in line:
             line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,
