@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
         return (uint64_t)std::max(0.0, std::min(x, (double)accounts - 1));
     };
 
-    double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0;
+    double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
     uint64_t gpu_n = 0, cpu_n = 0;
     for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
         Wave wave;
@@ -122,6 +122,7 @@ int main(int argc, char** argv) {
             gpu_s += t1 - t0;
             host_s += gpu.last_apply_host_s();
             engine_s += gpu.last_apply_engine_s();
+            for (int q = 0; q < 4; ++q) ph[q] += gpu.last_apply_phases_s()[q];
             gpu_n += msgs;
             const double c0 = now_s();
             cpu.HandleAfterConsensusUpdates(wave.cpu);
@@ -132,10 +133,11 @@ int main(int argc, char** argv) {
     const double bytes = (double)gpu_n * (4 + 2.0 * R * 4);  // key index + P and N rows per message
     std::printf("{\"workload\": \"committed-batch apply (C5 banking-shaped, %s accounts %llu, %d nodes, %llu state msgs per wave)\", "
                 "\"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"host_decode_ms_per_wave\": %.3f, "
-                "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, "
+                "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, \"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, \"kind\": \"port\"}}\n",
                 normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s,
-                1e3 * gpu_s / waves, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, bytes / engine_s / 1e9, cpu_n / cpu_s,
+                1e3 * gpu_s / waves, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, bytes / engine_s / 1e9, janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves,
+                1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves, cpu_n / cpu_s,
                 (unsigned long long)std::min(msgs, cpu_msgs));
     return 0;
 }

@@ -3,7 +3,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <limits>
+#include <memory>
+#include <thread>
 
 namespace janus {
 
@@ -43,34 +46,31 @@ GpuStableStore::~GpuStableStore() {
 }
 
 const GpuStableStore::KeyRef* GpuStableStore::UidTable::find(const Guid& g) const {
-    if (keys_.empty()) return nullptr;
-    const size_t mask = keys_.size() - 1;
+    if (slots_.empty()) return nullptr;
+    const size_t mask = slots_.size() - 1;
     for (size_t i = GuidHash()(g) & mask;; i = (i + 1) & mask) {
-        if (!used_[i]) return nullptr;
-        if (keys_[i] == g) return &vals_[i];
+        const Slot& s = slots_[i];
+        if (!s.used) return nullptr;
+        if (s.key == g) return &s.val;
     }
 }
 
 bool GpuStableStore::UidTable::insert(const Guid& g, KeyRef v) {
-    if ((n_ + 1) * 2 > keys_.size()) grow();
-    const size_t mask = keys_.size() - 1;
+    if ((n_ + 1) * 2 > slots_.size()) grow();
+    const size_t mask = slots_.size() - 1;
     for (size_t i = GuidHash()(g) & mask;; i = (i + 1) & mask) {
-        if (!used_[i]) { used_[i] = 1; keys_[i] = g; vals_[i] = v; ++n_; return true; }
-        if (keys_[i] == g) return false;
+        Slot& s = slots_[i];
+        if (!s.used) { s.used = 1; s.key = g; s.val = v; ++n_; return true; }
+        if (s.key == g) return false;
     }
 }
 
 void GpuStableStore::UidTable::grow() {
-    std::vector<Guid> k = std::move(keys_);
-    std::vector<KeyRef> v = std::move(vals_);
-    std::vector<uint8_t> u = std::move(used_);
-    const size_t cap = k.empty() ? 1024 : k.size() * 2;
-    keys_.assign(cap, Guid{});
-    vals_.assign(cap, KeyRef{CrdtType::PNCounter, 0});
-    used_.assign(cap, 0);
+    std::vector<Slot> old = std::move(slots_);
+    slots_.assign(old.empty() ? 1024 : old.size() * 2, Slot{});
     n_ = 0;
-    for (size_t i = 0; i < k.size(); ++i)
-        if (u[i]) insert(k[i], v[i]);
+    for (const Slot& s : old)
+        if (s.used) insert(s.key, s.val);
 }
 
 const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want) const {
@@ -80,15 +80,30 @@ const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want
     return *r;
 }
 
-uint32_t GpuStableStore::column(uint32_t row, const Guid& g, uint32_t hint) {
+uint32_t GpuStableStore::column_nothrow(uint32_t row, const Guid& g, uint32_t hint) {
     Guid* c = &cols_[(size_t)row * R_];
     uint32_t& n = ncols_[row];
     if (hint < n && c[hint] == g) return hint;
     for (uint32_t j = 0; j < n; ++j)
         if (c[j] == g) return j;
-    if (n >= R_) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
+    if (n >= R_) return UINT32_MAX;
     c[n] = g;
     return n++;
+}
+
+uint32_t GpuStableStore::column(uint32_t row, const Guid& g, uint32_t hint) {
+    const uint32_t c = column_nothrow(row, g, hint);
+    if (c == UINT32_MAX) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
+    return c;
+}
+
+uint32_t GpuStableStore::find_column(uint32_t row, const Guid& g, uint32_t hint) const {
+    const Guid* c = &cols_[(size_t)row * R_];
+    const uint32_t n = ncols_[row];
+    if (hint < n && c[hint] == g) return hint;
+    for (uint32_t j = 0; j < n; ++j)
+        if (c[j] == g) return j;
+    return UINT32_MAX;
 }
 
 uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e, bool create) {
@@ -123,78 +138,195 @@ namespace {
 double wall_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 }  // namespace
 
+namespace {
+// Static contiguous split of [0, n) over up to `threads` workers: fn(begin, end, worker).  Worker t's
+// range precedes worker t+1's, so per-worker results concatenated in worker order keep message order.
+template <class F> void parallel_ranges(size_t n, int threads, F&& fn) {
+    static const size_t min_par = [] {  // below this many messages the wave is decoded inline
+        const char* e = std::getenv("JANUS_HOST_PAR_MIN");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{32768};
+    }();
+    if (threads <= 1 || n < min_par || n < (size_t)threads) {
+        fn(size_t{0}, n, 0);
+        return;
+    }
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back([&, t] { fn(n * t / threads, n * (t + 1) / threads, t); });
+    fn(size_t{0}, n / threads, 0);
+    for (auto& th : pool) th.join();
+}
+}  // namespace
+
+int GpuStableStore::host_threads() {
+    if (const char* e = std::getenv("JANUS_HOST_THREADS")) {
+        const int v = std::atoi(e);
+        if (v >= 1) return v;
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+}
+
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                                      std::unordered_map<uint64_t, uint64_t>* tracker) {
     const double t0 = wall_s();
-    std::vector<uint32_t> rows;
-    std::vector<int64_t> P64, N64;
-    std::vector<int32_t> P32, N32;
-    std::vector<jg_tagrec> adds, rems;
-    std::vector<uint64_t> completed;
-    const int64_t absent = eb_ == 4 ? (int64_t)std::numeric_limits<int32_t>::min() : std::numeric_limits<int64_t>::min();
+    std::vector<const NetworkProtocol*> msgs;
+    {
+        size_t n_msgs = 0;
+        for (const auto& list : updates)
+            for (const auto& block : list) n_msgs += block.update.size();
+        msgs.reserve(n_msgs);
+        for (const auto& list : updates)
+            for (const auto& block : list)
+                for (const auto& u : block.update) msgs.push_back(&u);
+    }
+    const size_t n = msgs.size();
+    const int T = host_threads();
+    phase_s_[0] = wall_s() - t0;
+    constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1, kBadType = UINT32_MAX - 2;
 
-    size_t n_msgs = 0;
-    for (const auto& list : updates)
-        for (const auto& block : list) n_msgs += block.update.size();
-    rows.reserve(n_msgs);
-    if (eb_ == 4) { P32.reserve(n_msgs * R_); N32.reserve(n_msgs * R_); }
-    else { P64.reserve(n_msgs * R_); N64.reserve(n_msgs * R_); }
-
-    for (const auto& list : updates)
-        for (const auto& block : list)
-            for (const auto& u : block.update) {
-                if (u.syncMsgType == NetworkProtocol::ManagerMsg_Create || u.uid.is_empty()) continue;
-                const KeyRef* kr = uids_.find(u.uid);
-                if (!kr) continue;
-                if (u.type != kr->type) {  // ORSet.cs:288-291 / the PNCounter cast
-                    throw EngineError(JG_ETYPE, "committed state of the wrong CRDT type for its key");
-                }
-                if (kr->type == CrdtType::PNCounter) {
-                    const uint32_t row = kr->idx;
-                    const size_t base = rows.size() * R_;
-                    rows.push_back(row);
-                    if (eb_ == 4) { P32.resize(base + R_, (int32_t)absent); N32.resize(base + R_, (int32_t)absent); }
-                    else { P64.resize(base + R_, absent); N64.resize(base + R_, absent); }
-                    uint32_t j = 0;
-                    for (const auto& e : u.pnc.pVector) {
-                        const uint32_t c = column(row, e.first, j++);
-                        if (eb_ == 4) P32[base + c] = (int32_t)e.second; else P64[base + c] = e.second;
-                    }
-                    j = 0;
-                    for (const auto& e : u.pnc.nVector) {
-                        const uint32_t c = column(row, e.first, j++);
-                        if (eb_ == 4) N32[base + c] = (int32_t)e.second; else N64[base + c] = e.second;
-                    }
-                } else {
-                    SetKey& s = sets_[kr->idx];
-                    const uint64_t hi = (uint64_t)kr->idx << 32;
-                    for (const auto& e : u.orset.addSet) {
-                        if (e.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
-                        const uint64_t key = hi | elem_id(s, e.first, true);
-                        for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
-                    }
-                    for (const auto& e : u.orset.removeSet) {
-                        const uint64_t key = hi | elem_id(s, e.first, true);
-                        for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
-                    }
-                    for (const auto& g : u.orset.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
-                    for (const auto& g : u.orset.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
-                }
-                if (tracker) {
-                    auto tr = tracker->find(u.seq);
-                    if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
+    // Phase 1 (parallel, read-only): classify every message — PNC row, OR-Set, or skipped (:133-136).
+    std::vector<uint32_t> cls(n);
+    std::vector<size_t> pnc_count(T, 0), bad(T, SIZE_MAX);
+    parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
+        size_t cnt = 0;
+        for (size_t i = b; i < e; ++i) {
+            if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
+            if (i + 8 < e) uids_.prefetch(msgs[i + 8]->uid);
+            const NetworkProtocol& u = *msgs[i];
+            uint32_t c = kSkip;
+            if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {
+                if (const KeyRef* kr = uids_.find(u.uid)) {
+                    if (u.type != kr->type) c = kBadType;  // ORSet.cs:288-291 / the PNCounter cast
+                    else if (kr->type == CrdtType::PNCounter) { c = kr->idx; ++cnt; }
+                    else c = kSet;
                 }
             }
+            if (c == kBadType && bad[t] == SIZE_MAX) bad[t] = i;
+            cls[i] = c;
+        }
+        pnc_count[t] = cnt;
+    });
+    for (int t = 0; t < T; ++t)
+        if (bad[t] != SIZE_MAX) throw EngineError(JG_ETYPE, "committed state of the wrong CRDT type for its key");
+    phase_s_[1] = wall_s() - t0;
 
+    // Phase 2 (parallel, read-only on the interning): decode PNC states into the SoA batch.  A
+    // state naming a replica this row has not seen yet is deferred to phase 3, which appends
+    // columns in commit order (first-insertion order, as the stable Dictionary would).
+    std::vector<size_t> base(T + 1, 0);
+    for (int t = 0; t < T; ++t) base[t + 1] = base[t] + pnc_count[t];
+    const size_t n_pnc = base[T];
+    const int64_t absent = eb_ == 4 ? (int64_t)std::numeric_limits<int32_t>::min() : std::numeric_limits<int64_t>::min();
+    std::unique_ptr<uint32_t[]> rows(new uint32_t[n_pnc ? n_pnc : 1]);
+    std::unique_ptr<char[]> Pb(new char[(n_pnc ? n_pnc : 1) * R_ * eb_]), Nb(new char[(n_pnc ? n_pnc : 1) * R_ * eb_]);
+    std::vector<std::vector<std::pair<size_t, size_t>>> deferred(T);  // (message, batch position)
+    auto put = [&](char* buf, size_t at, int64_t v) {
+        if (eb_ == 4) reinterpret_cast<int32_t*>(buf)[at] = (int32_t)v;
+        else reinterpret_cast<int64_t*>(buf)[at] = v;
+    };
+    parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
+        size_t p = base[t];
+        for (size_t i = b; i < e; ++i) {
+            if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);  // software pipeline over the pointer chase
+            if (i + 8 < e && cls[i + 8] < kBadType) {
+                __builtin_prefetch(&cols_[(size_t)cls[i + 8] * R_]);
+                __builtin_prefetch(msgs[i + 8]->pnc.pVector.data());
+                __builtin_prefetch(msgs[i + 8]->pnc.nVector.data());
+            }
+            const uint32_t row = cls[i];
+            if (row >= kBadType) continue;
+            const NetworkProtocol& u = *msgs[i];
+            rows[p] = row;
+            for (uint32_t c = 0; c < R_; ++c) { put(Pb.get(), p * R_ + c, absent); put(Nb.get(), p * R_ + c, absent); }
+            bool miss = false;
+            uint32_t j = 0;
+            for (const auto& en : u.pnc.pVector) {
+                const uint32_t c = find_column(row, en.first, j++);
+                if (c == UINT32_MAX) { miss = true; break; }
+                put(Pb.get(), p * R_ + c, en.second);
+            }
+            j = 0;
+            for (const auto& en : u.pnc.nVector) {
+                if (miss) break;
+                const uint32_t c = find_column(row, en.first, j++);
+                if (c == UINT32_MAX) { miss = true; break; }
+                put(Nb.get(), p * R_ + c, en.second);
+            }
+            if (miss) deferred[t].emplace_back(i, p);
+            ++p;
+        }
+    });
+    phase_s_[2] = wall_s() - t0;
+    // Phase 3 (commit order within each row): states that introduce replicas.  Column order only
+    // matters per row, so rows are dealt to workers by row % T and every worker walks the deferred
+    // states in commit order, handling its own rows.
+    std::vector<std::pair<size_t, size_t>> dlist;
+    for (int t = 0; t < T; ++t) dlist.insert(dlist.end(), deferred[t].begin(), deferred[t].end());
+    const int T3 = dlist.size() < 4096 ? 1 : T;
+    std::vector<uint8_t> full(T3, 0);
+    auto run3 = [&](int w) {
+        for (const auto& [i, p] : dlist) {
+            const uint32_t row = cls[i];
+            if ((int)(row % (uint32_t)T3) != w) continue;
+            const NetworkProtocol& u = *msgs[i];
+            uint32_t j = 0;
+            for (const auto& en : u.pnc.pVector) {
+                const uint32_t c = column_nothrow(row, en.first, j++);
+                if (c == UINT32_MAX) { full[w] = 1; return; }
+                put(Pb.get(), p * R_ + c, en.second);
+            }
+            j = 0;
+            for (const auto& en : u.pnc.nVector) {
+                const uint32_t c = column_nothrow(row, en.first, j++);
+                if (c == UINT32_MAX) { full[w] = 1; return; }
+                put(Nb.get(), p * R_ + c, en.second);
+            }
+        }
+    };
+    if (T3 == 1) run3(0);
+    else {
+        std::vector<std::thread> pool;
+        for (int w = 1; w < T3; ++w) pool.emplace_back(run3, w);
+        run3(0);
+        for (auto& th : pool) th.join();
+    }
+    for (uint8_t f : full)
+        if (f) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
+
+    phase_s_[3] = wall_s() - t0;
+    // OR-Set states and the safe-update tracker, serial in commit order.
+    std::vector<jg_tagrec> adds, rems;
+    std::vector<uint64_t> completed;
+    for (size_t i = 0; i < n; ++i) {
+        if (cls[i] == kSkip) continue;
+        const NetworkProtocol& u = *msgs[i];
+        if (cls[i] == kSet) {
+            const KeyRef* kr = uids_.find(u.uid);
+            SetKey& s = sets_[kr->idx];
+            const uint64_t hi = (uint64_t)kr->idx << 32;
+            for (const auto& e : u.orset.addSet) {
+                if (e.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
+                const uint64_t key = hi | elem_id(s, e.first, true);
+                for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
+            }
+            for (const auto& e : u.orset.removeSet) {
+                const uint64_t key = hi | elem_id(s, e.first, true);
+                for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
+            }
+            for (const auto& g : u.orset.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+            for (const auto& g : u.orset.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+        }
+        if (tracker) {
+            auto tr = tracker->find(u.seq);
+            if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
+        }
+    }
     if (!adds.empty() || !rems.empty()) {
         sort_unique(adds);
         sort_unique(rems);
     }
     const double t1 = wall_s();
-    if (!rows.empty()) {
-        if (eb_ == 4) check(jg_pnc_merge_rows(pnc_, rows.data(), rows.size(), P32.data(), N32.data()));
-        else check(jg_pnc_merge_rows(pnc_, rows.data(), rows.size(), P64.data(), N64.data()));
-    }
+    if (n_pnc) check(jg_pnc_merge_rows(pnc_, rows.get(), n_pnc, Pb.get(), Nb.get()));
     if (!adds.empty() || !rems.empty()) check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
     host_s_ = t1 - t0;
     engine_s_ = wall_s() - t1;

@@ -112,9 +112,13 @@ class GpuStableStore {
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
 
     jg_ctx* ctx() const { return ctx_; }
-    // Wall time of the last ApplyCommitted: host decode/interning vs the engine calls (incl. H2D).
+    static int host_threads();  // decode workers: JANUS_HOST_THREADS, else min(16, hardware threads)
+    // Wall time of the last ApplyCommitted: host decode/interning (multi-threaded over the wave's
+    // messages, JANUS_HOST_THREADS) vs the engine calls (incl. H2D).
     double last_apply_host_s() const { return host_s_; }
     double last_apply_engine_s() const { return engine_s_; }
+    // Cumulative host time at the end of: flatten, classify, parallel decode, deferred columns.
+    const double* last_apply_phases_s() const { return phase_s_; }
 
   private:
     struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id
@@ -123,17 +127,25 @@ class GpuStableStore {
       public:
         const KeyRef* find(const Guid& g) const;
         bool insert(const Guid& g, KeyRef v);  // false if present
+        void prefetch(const Guid& g) const {
+            if (!slots_.empty()) __builtin_prefetch(&slots_[GuidHash()(g) & (slots_.size() - 1)]);
+        }
       private:
+        struct alignas(32) Slot {  // one cache line holds two slots: a lookup touches one line
+            Guid key;
+            KeyRef val{CrdtType::PNCounter, 0};
+            uint8_t used = 0;
+        };
         void grow();
-        std::vector<Guid> keys_;
-        std::vector<KeyRef> vals_;
-        std::vector<uint8_t> used_;
+        std::vector<Slot> slots_;
         size_t n_ = 0;
     };
     struct SetKey { std::unordered_map<std::string, uint32_t> elems; };
     // Column of replica g in PNC row `row`; `hint` = its position in the message (messages list
     // replicas in the sender's insertion order, which usually equals ours).  Appends new replicas.
     uint32_t column(uint32_t row, const Guid& g, uint32_t hint);
+    uint32_t column_nothrow(uint32_t row, const Guid& g, uint32_t hint);  // UINT32_MAX if the row is full
+    uint32_t find_column(uint32_t row, const Guid& g, uint32_t hint) const;  // UINT32_MAX if new
     uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
@@ -143,7 +155,7 @@ class GpuStableStore {
     jg_orset* orset_ = nullptr;
     uint32_t max_keys_, R_, eb_;
     uint32_t next_row_ = 0, next_set_ = 0;
-    double host_s_ = 0, engine_s_ = 0;
+    double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0};
     UidTable uids_;
     std::vector<uint32_t> ncols_;  // per PNC row: replica columns in use
     std::vector<Guid> cols_;       // per PNC row: R replica Guids, in first-insertion order

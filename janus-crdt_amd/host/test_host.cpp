@@ -13,6 +13,7 @@
 // are applied there, and QueryProspective plus every op result must match too.
 // Exit 0 = parity; prints the first mismatch otherwise.
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 
 #include "janus_host.hpp"
@@ -207,15 +208,20 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
 }  // namespace
 
 int main() {
-    struct Case { uint64_t seed; int n_pnc, n_set, n_ops, wave_every, batch; uint32_t eb; };
+    struct Case { uint64_t seed; int n_pnc, n_set, n_ops, wave_every, batch; uint32_t eb; const char* threads; };
+    // Waves are decoded by JANUS_HOST_THREADS workers once they hold JANUS_HOST_PAR_MIN messages;
+    // the threshold is lowered to 1 so the parallel decode (and its commit-order column insertion)
+    // runs on these small waves too.
+    setenv("JANUS_HOST_PAR_MIN", "1", 1);
     const Case cases[] = {
-        {1, 6, 4, 400, 7, 1, 4},    // KVStoreTests: clientBatchSize = 1
-        {2, 20, 10, 3000, 97, 8, 4},  // batched client updates, state compaction (SafeCRDTManager.cs:165-198)
-        {3, 3, 3, 2000, 500, 1000, 4},  // JanusService: clientBatchSize = 1000, big waves, hot keys
-        {4, 10, 0, 1500, 50, 4, 8},   // long (int64) PN-Counter variant
+        {1, 6, 4, 400, 7, 1, 4, "1"},      // KVStoreTests: clientBatchSize = 1
+        {2, 20, 10, 3000, 97, 8, 4, "4"},  // batched client updates, state compaction (SafeCRDTManager.cs:165-198)
+        {3, 3, 3, 2000, 500, 1000, 4, "7"},  // JanusService: clientBatchSize = 1000, big waves, hot keys
+        {4, 10, 0, 1500, 50, 4, 8, "3"},   // long (int64) PN-Counter variant
     };
     int fails = 0;
     for (const auto& c : cases) {
+        setenv("JANUS_HOST_THREADS", c.threads, 1);
         int rc = 1;
         try { rc = run(c.seed, c.n_pnc, c.n_set, c.n_ops, c.wave_every, c.batch, c.eb); }
         catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
