@@ -107,6 +107,40 @@ int jg_rows_upload(jg_rows* rows, const uint32_t* key_idx, const void* P, const 
 int jg_pnc_merge_batch(jg_pnc* pnc, const jg_rows* rows, int async);
 
 /* ---------------------------------------------------------------------------------------------
+ * PN-Counter replica table + wire-format apply (csrc/json.hip).  The store keeps, per key, the
+ * replica Guids of its columns in first-insertion order (= the stable PNCounter's Dictionary
+ * enumeration order, PNCounters.cs:19-25,73-81,131-144); allocated on first use, at most 256
+ * replicas per key.  Guids are C# Guid bytes (lo = bytes 0..7, hi = bytes 8..15, little-endian).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct jg_guid { uint64_t lo, hi; } jg_guid;
+typedef struct jg_wave jg_wave;   /* device-resident wave of encoded state messages            */
+
+/* Register replica[i] in row key_idx[i], in order (append if absent); col_out[i] = its column.
+ * The PNCounter() constructor's {self: 0} (PNCounters.cs:73-81): CreateSafeCRDT registers the
+ * stable instance's own Guid first.  JG_ESTATE (nothing registered) if a row would overflow. */
+int jg_pnc_intern(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, const jg_guid* replica, uint32_t* col_out);
+/* Column tables of rows key_idx[0..n): replicas[i*R + c] for c < ncols[i]. */
+int jg_pnc_columns(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, jg_guid* replicas, uint32_t* ncols);
+/* Apply a committed wave of PNCounterMsg wire payloads (System.Text.Json UTF-8, PNCounters.cs:38-49):
+ * message i = bytes[off[i], off[i+1]) (off[0] = 0) is decoded and merged into row key_idx[i]
+ * exactly as SafeCRDT.ApplyUpdateStable (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83) -> Decode -> Merge
+ * would, message after message (SafeCRDTManager.cs:122-146); new replicas get columns in commit
+ * order.  All or nothing: a message outside the accepted JSON form (oracle/json.hpp) returns
+ * JG_EINVAL, a key running out of columns JG_ESTATE, nothing is applied, and *bad_msg (if not NULL)
+ * = the first such message (UINT64_MAX on success).  The caller re-submits the prefix
+ * [0, *bad_msg) to reproduce the reference, whose loop applies the messages before the throwing one. */
+int jg_pnc_merge_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg);
+/* The same with the wave already in device memory (upload once, merge many: the bench). */
+int jg_wave_create(jg_ctx* ctx, uint64_t cap_msgs, uint64_t cap_bytes, jg_wave** out);
+int jg_wave_destroy(jg_wave* wave);
+int jg_wave_upload(jg_wave* wave, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes);
+int jg_pnc_merge_wave(jg_pnc* pnc, const jg_wave* wave, uint64_t* bad_msg);
+
+/* Page-locked host memory for staging waves (PCIe DMA at full rate); free with jg_host_free. */
+int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out);
+int jg_host_free(void* p);
+
+/* ---------------------------------------------------------------------------------------------
  * OR-Set store — replaces ORSet<string>'s Dictionary<T,HashSet<Guid>> add/remove maps and null
  * tag sets (MergeSharp/MergeSharp/CRDTs/ORSet.cs:78-327) for a whole keyspace of sets.
  * ------------------------------------------------------------------------------------------- */

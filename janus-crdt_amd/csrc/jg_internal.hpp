@@ -84,6 +84,8 @@ struct jg_pnc {
     uint32_t R;
     uint32_t eb;  // elem bytes (4 | 8)
     jg::DevBuf P, N;
+    // replica table (json.hip): [n_keys x R] 16-byte Guids + [n_keys] column counts, first use only
+    jg::DevBuf cols, ncols;
 };
 
 struct jg_rows {

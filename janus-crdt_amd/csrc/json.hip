@@ -1,0 +1,661 @@
+// json.hip — committed state messages applied straight from their wire bytes (SURVEY.md §8f F1 + A2/A13).
+//
+// The reference's stable apply decodes every committed state with System.Text.Json and merges it:
+// SafeCRDT.ApplyUpdateStable (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83) -> PNCounter.DecodePropagationMessage
+// -> PNCounterMsg.Decode (MergeSharp/MergeSharp/CRDTs/PNCounters.cs:38-43) -> Merge (:131-144), one
+// message at a time inside HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160).  Here a whole
+// wave of PNCounterMsg JSON payloads is uploaded once and decoded, interned and merged on the GPU:
+//
+//   pass A  k_scan      one thread per message: full parse + validation (the wire contract of
+//                       oracle/json.hpp), every Guid looked up in its row's replica table (read-only);
+//                       a Guid repeated among a vector's known replicas is an error; a message naming a
+//                       replica its row has not seen is DEFERRED (row << 32 | msg appended to a list).
+//   host     one 16-byte D2H: first bad message, deferred count.  A bad message = nothing is written.
+//   sort     hipcub radix sort of the deferred list -> messages grouped by row in commit order.
+//   pass C   k_resolve   one thread per row segment walks its deferred messages in commit order and
+//                       appends the new replica Guids (pVector entries first, then nVector — Merge's
+//                       order) to the row's table: first-insertion order = the stable Dictionary's
+//                       enumeration order.  A full row or a Guid repeated in one vector rolls the
+//                       appended columns back and fails the call.
+//   pass B  k_apply     one thread per message: parse again, every Guid now resolves, atomicMax into
+//                       P / N (messages of one wave may repeat a key; max is order-free).
+//
+// Parsing is byte-serial per thread through a 16-byte window register (one aligned global load per
+// 16 bytes), so a message costs ~len/16 loads; the bound of the end-to-end call is the PCIe upload of
+// the payload, not the parse.
+//
+// Replica table (jg_pnc::cols / ncols, allocated on first use): [n_keys x R] Guids + [n_keys] counts.
+// P and N share one column per replica: the reference keeps two dictionaries whose key orders coincide
+// for every state its nodes produce (constructor inserts self into both, Merge inserts new keys in
+// message order), which the shared order reproduces.
+#include <hipcub/hipcub.hpp>
+
+#include "jg_internal.hpp"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kMaxJsonReplicas = 256;  // per-vector duplicate masks are 4 x 64 bits
+
+enum : uint32_t { kErrSyntax = 0, kErrFull = 1, kErrInternal = 2 };
+
+struct Guid16 { unsigned long long lo, hi; };
+
+// ---- byte cursor over [p, end) with a 16-byte aligned window ---------------------------------------
+struct Cursor {
+    const uint8_t* base;
+    uint64_t p, end;
+    uint64_t wbase;
+    uint4 win;
+    __device__ Cursor(const uint8_t* b, uint64_t beg, uint64_t e) : base(b), p(beg), end(e), wbase(~0ull), win{0, 0, 0, 0} {}
+    __device__ __forceinline__ int peek() {
+        if (p >= end) return -1;
+        const uint64_t a = p & ~15ull;
+        if (a != wbase) {
+            win = *reinterpret_cast<const uint4*>(base + a);
+            wbase = a;
+        }
+        const uint32_t k = (uint32_t)(p - a);
+        const uint32_t w = k < 8 ? (k < 4 ? win.x : win.y) : (k < 12 ? win.z : win.w);
+        return (int)((w >> ((k & 3) * 8)) & 0xFF);
+    }
+    __device__ __forceinline__ int get() {
+        const int c = peek();
+        if (c >= 0) ++p;
+        return c;
+    }
+    __device__ __forceinline__ void ws() {
+        for (;;) {
+            const int c = peek();
+            if (c == ' ' || c == '\t' || c == '\n' || c == '\r') ++p;
+            else return;
+        }
+    }
+    __device__ __forceinline__ bool expect(int ch) {
+        ws();
+        if (peek() != ch) return false;
+        ++p;
+        return true;
+    }
+};
+
+__device__ __forceinline__ int hexv(int c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    const int l = c | 0x20;
+    if (l >= 'a' && l <= 'f') return l - 'a' + 10;
+    return -1;
+}
+
+// 36-char "D" Guid (Guid.ToString() layout: b3b2b1b0-b5b4-b7b6-b8b9-b10..b15) + the closing quote.
+__device__ __forceinline__ bool read_guid(Cursor& c, Guid16& g) {
+    unsigned long long lo = 0, hi = 0;
+    // groups: a (8 hex) -> lo[0:32), b (4) -> lo[32:48), c (4) -> lo[48:64), then 8 bytes of hi in text order
+    uint32_t v = 0;
+    for (int i = 0; i < 8; ++i) { const int h = hexv(c.get()); if (h < 0) return false; v = v << 4 | (uint32_t)h; }
+    lo = v;
+    if (c.get() != '-') return false;
+    v = 0;
+    for (int i = 0; i < 4; ++i) { const int h = hexv(c.get()); if (h < 0) return false; v = v << 4 | (uint32_t)h; }
+    lo |= (unsigned long long)v << 32;
+    if (c.get() != '-') return false;
+    v = 0;
+    for (int i = 0; i < 4; ++i) { const int h = hexv(c.get()); if (h < 0) return false; v = v << 4 | (uint32_t)h; }
+    lo |= (unsigned long long)v << 48;
+    if (c.get() != '-') return false;
+    for (int b = 0; b < 8; ++b) {
+        if (b == 2 && c.get() != '-') return false;
+        const int h = hexv(c.get()), l = hexv(c.get());
+        if (h < 0 || l < 0) return false;
+        hi |= (unsigned long long)(h << 4 | l) << (8 * b);
+    }
+    if (c.get() != '"') return false;
+    g.lo = lo;
+    g.hi = hi;
+    return true;
+}
+
+// -?(0|[1-9][0-9]*) within the width (Utf8JsonReader.GetInt32 / GetInt64).
+template <int EB>
+__device__ __forceinline__ bool read_int(Cursor& c, long long& out) {
+    c.ws();
+    bool neg = false;
+    int ch = c.peek();
+    if (ch == '-') { neg = true; ++c.p; ch = c.peek(); }
+    if (ch < '0' || ch > '9') return false;
+    unsigned long long mag = 0;
+    if (ch == '0') {
+        ++c.p;
+        ch = c.peek();
+        if (ch >= '0' && ch <= '9') return false;  // leading zero
+    } else {
+        while (ch >= '0' && ch <= '9') {
+            const unsigned d = (unsigned)(ch - '0');
+            if (mag > (~0ull - d) / 10) return false;
+            mag = mag * 10 + d;
+            ++c.p;
+            ch = c.peek();
+        }
+    }
+    const unsigned long long lim = EB == 4 ? (neg ? 0x80000000ull : 0x7FFFFFFFull) : (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
+    if (mag > lim) return false;
+    out = neg ? (long long)(0ull - mag) : (long long)mag;
+    return true;
+}
+
+// Property name "pVector" / "nVector" (no escapes).  Returns 0 / 1, or -1.
+__device__ __forceinline__ int read_name(Cursor& c) {
+    if (!c.expect('"')) return -1;
+    const int f = c.get();
+    const char* rest = "Vector\"";
+    for (int i = 0; i < 7; ++i)
+        if (c.get() != rest[i]) return -1;
+    return f == 'p' ? 0 : f == 'n' ? 1 : -1;
+}
+
+// Parse one PNCounterMsg; vis.entry(which, pos, guid, value) returns false to abort (error).
+// `only` = -1 visits both vectors, 0 / 1 only pVector / nVector (the other is still validated).
+template <int EB, class V>
+__device__ bool parse_pnc(Cursor& c, V& vis, int only = -1) {
+    if (!c.expect('{')) return false;
+    int seen = 0;
+    for (;;) {
+        const int which = read_name(c);
+        if (which < 0 || (seen >> which & 1)) return false;
+        seen |= 1 << which;
+        if (!c.expect(':') || !c.expect('{')) return false;  // `null` fails here too
+        vis.begin_vector(which);
+        c.ws();
+        if (c.peek() == '}') {
+            ++c.p;
+        } else {
+            for (uint32_t pos = 0;; ++pos) {
+                if (!c.expect('"')) return false;
+                Guid16 g;
+                long long v;
+                if (!read_guid(c, g) || !c.expect(':') || !read_int<EB>(c, v)) return false;
+                if ((only < 0 || only == which) && !vis.entry(which, pos, g, v)) return false;
+                c.ws();
+                const int ch = c.get();
+                if (ch == '}') break;
+                if (ch != ',') return false;
+            }
+        }
+        c.ws();
+        const int ch = c.get();
+        if (ch == '}') break;
+        if (ch != ',') return false;
+    }
+    c.ws();
+    return seen == 3 && c.p == c.end;
+}
+
+// ---- replica table helpers -------------------------------------------------------------------------
+struct Table {
+    Guid16* cols;   // [n_keys x R]
+    uint32_t* ncols;
+    uint32_t R;
+};
+
+__device__ __forceinline__ uint32_t find_col(const Guid16* row, uint32_t n, const Guid16& g, uint32_t hint) {
+    if (hint < n) {
+        const Guid16 h = row[hint];
+        if (h.lo == g.lo && h.hi == g.hi) return hint;
+    }
+    for (uint32_t j = 0; j < n; ++j) {
+        const Guid16 h = row[j];
+        if (h.lo == g.lo && h.hi == g.hi) return j;
+    }
+    return UINT32_MAX;
+}
+
+// 256-bit column mask without dynamic register indexing (no scratch spills).
+struct Mask256 {
+    unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __device__ void clear() { w0 = w1 = w2 = w3 = 0; }
+    __device__ bool test_set(uint32_t c) {  // returns the old bit
+        const unsigned long long b = 1ull << (c & 63);
+        unsigned long long* w = c < 64 ? &w0 : c < 128 ? &w1 : c < 192 ? &w2 : &w3;
+        const bool old = (*w & b) != 0;
+        *w |= b;
+        return old;
+    }
+};
+
+// Pass A visitor: known Guids checked for repeats; unknown Guids mark the message deferred.
+struct ScanVis {
+    const Guid16* row;
+    uint32_t n;
+    Mask256 m;
+    bool miss = false;
+    __device__ void begin_vector(int) { m.clear(); }
+    __device__ bool entry(int, uint32_t pos, const Guid16& g, long long) {
+        const uint32_t c = find_col(row, n, g, pos);
+        if (c == UINT32_MAX) { miss = true; return true; }
+        return !m.test_set(c);
+    }
+};
+
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                 const uint32_t* __restrict__ rows, uint64_t n, Table t,
+                                                 unsigned long long* __restrict__ status /* [0] first bad, [1] n deferred */,
+                                                 unsigned long long* __restrict__ deferred) {
+    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= n) return;
+    const uint32_t row = rows[m];
+    Cursor c(bytes, off[m], off[m + 1]);
+    ScanVis vis{t.cols + (uint64_t)row * t.R, t.ncols[row]};
+    if (!parse_pnc<EB>(c, vis)) {
+        atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
+        return;
+    }
+    if (vis.miss) {
+        const unsigned long long at = atomicAdd(status + 1, 1ull);
+        deferred[at] = (unsigned long long)row << 32 | m;
+    }
+}
+
+// Pass C visitor: exclusive owner of the row; appends new Guids.
+struct ResolveVis {
+    Guid16* row;
+    uint32_t* ncol;
+    uint32_t R;
+    Mask256 m;
+    uint32_t err = UINT32_MAX;
+    __device__ void begin_vector(int) { m.clear(); }
+    __device__ bool entry(int, uint32_t pos, const Guid16& g, long long) {
+        uint32_t c = find_col(row, *ncol, g, pos);
+        if (c == UINT32_MAX) {
+            if (*ncol >= R) { err = kErrFull; return false; }
+            c = (*ncol)++;
+            row[c] = g;
+        }
+        if (m.test_set(c)) { err = kErrSyntax; return false; }  // repeated Guid in one vector
+        return true;
+    }
+};
+
+// One thread per sorted deferred entry; segment heads (first entry of a row) walk their row's
+// messages in commit order.  saved[i] = the head's ncols before the walk (for roll-back).
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                    const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
+                                                    uint32_t* __restrict__ saved, unsigned long long* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nd) return;
+    const uint32_t row = (uint32_t)(keys[i] >> 32);
+    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;
+    uint32_t* ncol = t.ncols + row;
+    saved[i] = *ncol;
+    ResolveVis vis{t.cols + (uint64_t)row * t.R, ncol, t.R};
+    for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
+        const uint64_t m = (uint32_t)keys[j];
+        // Merge visits every pVector entry before any nVector entry (PNCounters.cs:133-143)
+        for (int which = 0; which < 2; ++which) {
+            Cursor c(bytes, off[m], off[m + 1]);
+            if (!parse_pnc<EB>(c, vis, which)) {
+                atomicMin(status + 2, (unsigned long long)m << 2 | (vis.err == UINT32_MAX ? kErrInternal : vis.err));
+                return;
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rollback(const unsigned long long* __restrict__ keys, uint64_t nd, uint32_t* __restrict__ ncols,
+                                                     const uint32_t* __restrict__ saved) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nd) return;
+    const uint32_t row = (uint32_t)(keys[i] >> 32);
+    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;
+    ncols[row] = saved[i];
+}
+
+// Pass B visitor: max into the cells.
+template <int EB>
+struct ApplyVis {
+    using T = typename std::conditional<EB == 4, int, long long>::type;
+    T* P;
+    T* N;
+    const Guid16* row;
+    uint32_t n;
+    bool bad = false;
+    __device__ void begin_vector(int) {}
+    __device__ bool entry(int which, uint32_t pos, const Guid16& g, long long v) {
+        const uint32_t c = find_col(row, n, g, pos);
+        if (c == UINT32_MAX) { bad = true; return false; }
+        atomicMax((which ? N : P) + c, (T)v);
+        return true;
+    }
+};
+
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ rows, uint64_t n, Table t, void* P, void* N,
+                                                  unsigned long long* __restrict__ status) {
+    using T = typename ApplyVis<EB>::T;
+    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= n) return;
+    const uint32_t row = rows[m];
+    const uint64_t base = (uint64_t)row * t.R;
+    Cursor c(bytes, off[m], off[m + 1]);
+    ApplyVis<EB> vis{static_cast<T*>(P) + base, static_cast<T*>(N) + base, t.cols + base, t.ncols[row]};
+    if (!parse_pnc<EB>(c, vis)) atomicMin(status + 2, (unsigned long long)m << 2 | kErrInternal);
+}
+
+// jg_pnc_intern: entries (row, guid) in order; keys = row << 32 | i sorted; segment heads walk.
+__global__ __launch_bounds__(kBlock) void k_intern(const unsigned long long* __restrict__ keys, uint64_t n, const Guid16* __restrict__ g,
+                                                   Table t, uint32_t* __restrict__ col_out, uint32_t* __restrict__ saved,
+                                                   unsigned long long* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = (uint32_t)(keys[i] >> 32);
+    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;
+    uint32_t* ncol = t.ncols + row;
+    Guid16* cols = t.cols + (uint64_t)row * t.R;
+    saved[i] = *ncol;
+    for (uint64_t j = i; j < n && (uint32_t)(keys[j] >> 32) == row; ++j) {
+        const uint32_t e = (uint32_t)keys[j];
+        uint32_t c = find_col(cols, *ncol, g[e], UINT32_MAX);
+        if (c == UINT32_MAX) {
+            if (*ncol >= t.R) {
+                atomicMin(status + 2, (unsigned long long)e << 2 | kErrFull);
+                return;
+            }
+            c = (*ncol)++;
+            cols[c] = g[e];
+        }
+        col_out[e] = c;
+    }
+}
+
+__global__ void k_make_keys(const uint32_t* __restrict__ rows, uint64_t n, unsigned long long* __restrict__ keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) keys[i] = (unsigned long long)rows[i] << 32 | i;
+}
+
+__global__ void k_gather_cols(const Guid16* __restrict__ cols, const uint32_t* __restrict__ ncols, const uint32_t* __restrict__ rows,
+                              uint64_t n, uint32_t R, Guid16* __restrict__ out, uint32_t* __restrict__ nout) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n * R) return;
+    const uint64_t q = i / R, c = i - q * R;
+    const uint32_t row = rows[q];
+    out[i] = cols[(uint64_t)row * R + c];
+    if (c == 0) nout[q] = ncols[row];
+}
+
+unsigned blocks_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+void ensure_table(jg_pnc* p) {
+    if (p->cols.p) return;
+    JG_REQUIRE(p->R <= kMaxJsonReplicas, JG_EINVAL, "replica table: at most %u replicas per key (store has %u)", kMaxJsonReplicas, p->R);
+    p->cols.alloc((size_t)p->n_keys * p->R * sizeof(Guid16));
+    p->ncols.alloc((size_t)p->n_keys * 4);
+    JG_HIP(hipMemsetAsync(p->ncols.p, 0, p->ncols.bytes, p->ctx->stream));
+}
+
+Table table_of(jg_pnc* p) { return Table{p->cols.as<Guid16>(), p->ncols.as<uint32_t>(), p->R}; }
+
+// Sort `n` 64-bit keys (row << 32 | index) in place through ctx scratch.  end_bit covers the row bits.
+unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n, uint64_t n_keys) {
+    JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "sort: %llu entries exceed one radix sort", (unsigned long long)n);
+    int row_bits = 1;
+    while (row_bits < 32 && (1ull << row_bits) < n_keys) ++row_bits;
+    const int end_bit = 32 + row_bits;
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, temp, keys, keys, (int)n, 0, end_bit, ctx->stream));
+    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, temp + n * 8 + 256));
+    unsigned long long* out = reinterpret_cast<unsigned long long*>(s);
+    void* tmp = s + ((n * 8 + 255) & ~255ull);
+    JG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, temp, keys, out, (int)n, 0, end_bit, ctx->stream));
+    return out;
+}
+
+struct Status { unsigned long long first_bad, n_deferred, resolve_bad, pad; };
+
+Status read_status(jg_ctx* ctx, const unsigned long long* d) {
+    Status s;
+    JG_HIP(hipMemcpyAsync(&s, d, sizeof s, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    return s;
+}
+
+[[noreturn]] void fail_msg(unsigned long long code, uint64_t* bad_msg, const char* what) {
+    const uint64_t m = code >> 2;
+    const uint32_t kind = (uint32_t)(code & 3);
+    if (bad_msg) *bad_msg = m;
+    if (kind == kErrFull)
+        jg::fail(JG_ESTATE, "%s %llu: its key holds more replicas than the store's columns", what, (unsigned long long)m);
+    if (kind == kErrInternal) jg::fail(JG_EHIP, "%s %llu: internal replica-table inconsistency", what, (unsigned long long)m);
+    jg::fail(JG_EINVAL, "%s %llu is not a PNCounterMsg in the accepted JSON form (JsonException)", what, (unsigned long long)m);
+}
+
+// The whole device side of a wave: bytes/off/rows already on the device.
+void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad_msg) {
+    jg_ctx* ctx = p->ctx;
+    ensure_table(p);
+    const Table t = table_of(p);
+    // status words + deferred list + roll-back slots live in ctx scratch
+    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch2, 64 + n * 8 + n * 4 + 256));
+    auto* status = reinterpret_cast<unsigned long long*>(s);
+    auto* deferred = reinterpret_cast<unsigned long long*>(s + 64);
+    auto* saved = reinterpret_cast<uint32_t*>(s + 64 + n * 8);
+    const Status init{~0ull, 0, ~0ull, 0};
+    JG_HIP(hipMemcpyAsync(status, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+    const unsigned g = blocks_for(n);
+    if (p->eb == 8) hipLaunchKernelGGL(k_scan<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, status, deferred);
+    else hipLaunchKernelGGL(k_scan<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, status, deferred);
+    JG_HIP(hipGetLastError());
+    Status st = read_status(ctx, status);
+    if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
+    if (st.n_deferred) {
+        const uint64_t nd = st.n_deferred;
+        unsigned long long* sorted = sort_keys(ctx, deferred, nd, p->n_keys);
+        const unsigned gd = blocks_for(nd);
+        if (p->eb == 8) hipLaunchKernelGGL(k_resolve<8>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, saved, status);
+        else hipLaunchKernelGGL(k_resolve<4>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, saved, status);
+        JG_HIP(hipGetLastError());
+        st = read_status(ctx, status);
+        if (st.resolve_bad != ~0ull) {
+            hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, saved);
+            JG_HIP(hipGetLastError());
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            fail_msg(st.resolve_bad, bad_msg, "state message");
+        }
+    }
+    if (p->eb == 8) hipLaunchKernelGGL(k_apply<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, status);
+    else hipLaunchKernelGGL(k_apply<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, status);
+    JG_HIP(hipGetLastError());
+    st = read_status(ctx, status);
+    if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
+}
+
+void check_wave_host(const jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const char* fn) {
+    JG_REQUIRE(n < 0xFFFFFFFFull, JG_EINVAL, "%s: at most 2^32-2 messages per wave", fn);
+    JG_REQUIRE(off[0] == 0, JG_EINVAL, "%s: off[0] must be 0", fn);
+    for (uint64_t i = 0; i < n; ++i) {
+        JG_REQUIRE(off[i + 1] >= off[i], JG_EINVAL, "%s: offsets decrease at message %llu", fn, (unsigned long long)i);
+        JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "%s: key_idx[%llu] = %u out of range (n_keys %llu)", fn, (unsigned long long)i,
+                   key_idx[i], (unsigned long long)p->n_keys);
+    }
+}
+
+}  // namespace
+
+// Device-resident wave of encoded state messages (bench / pre-staged waves).
+struct jg_wave {
+    jg_ctx* ctx;
+    uint64_t cap_msgs, cap_bytes;
+    uint64_t n = 0, n_bytes = 0;
+    uint32_t max_key = 0;
+    jg::DevBuf bytes, off, keys;
+};
+
+extern "C" {
+
+int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid* replica, uint32_t* col_out) {
+    return jg::guard([&] {
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_intern: store is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(key_idx && replica && col_out, JG_EINVAL, "jg_pnc_intern: NULL argument");
+        JG_REQUIRE(n < 0xFFFFFFFFull, JG_EINVAL, "jg_pnc_intern: at most 2^32-2 entries per call");
+        for (uint64_t i = 0; i < n; ++i)
+            JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "jg_pnc_intern: key_idx[%llu] = %u out of range", (unsigned long long)i, key_idx[i]);
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        ensure_table(p);
+        const Table t = table_of(p);
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, 64 + n * (4 + 16 + 8 + 4 + 4) + 256));
+        auto* status = reinterpret_cast<unsigned long long*>(s);
+        auto* keys = reinterpret_cast<unsigned long long*>(s + 64);
+        auto* g = reinterpret_cast<Guid16*>(s + 64 + n * 8);
+        auto* rows = reinterpret_cast<uint32_t*>(s + 64 + n * 24);
+        auto* cols = rows + n;
+        auto* saved = cols + n;
+        const Status init{~0ull, 0, ~0ull, 0};
+        JG_HIP(hipMemcpyAsync(status, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(rows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(g, replica, n * 16, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_make_keys, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, rows, n, keys);
+        unsigned long long* sorted = sort_keys(ctx, keys, n, p->n_keys);
+        hipLaunchKernelGGL(k_intern, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, sorted, n, g, t, cols, saved, status);
+        JG_HIP(hipGetLastError());
+        const Status st = read_status(ctx, status);
+        if (st.resolve_bad != ~0ull) {
+            hipLaunchKernelGGL(k_rollback, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, sorted, n, t.ncols, saved);
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            jg::fail(JG_ESTATE, "jg_pnc_intern: entry %llu: its key holds more replicas than the store's columns",
+                     (unsigned long long)(st.resolve_bad >> 2));
+        }
+        JG_HIP(hipMemcpyAsync(col_out, cols, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_pnc_columns(jg_pnc* p, uint64_t n, const uint32_t* key_idx, jg_guid* replicas, uint32_t* ncols) {
+    return jg::guard([&] {
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_columns: store is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(key_idx && replicas && ncols, JG_EINVAL, "jg_pnc_columns: NULL argument");
+        for (uint64_t i = 0; i < n; ++i)
+            JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "jg_pnc_columns: key_idx[%llu] = %u out of range", (unsigned long long)i, key_idx[i]);
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        ensure_table(p);
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * (4 + 4 + 16ull * p->R) + 256));
+        auto* rows = reinterpret_cast<uint32_t*>(s);
+        auto* nout = rows + n;
+        auto* out = reinterpret_cast<Guid16*>(s + ((n * 8 + 15) & ~15ull));
+        JG_HIP(hipMemcpyAsync(rows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_gather_cols, dim3(blocks_for(n * p->R)), dim3(kBlock), 0, ctx->stream, p->cols.as<Guid16>(), p->ncols.as<uint32_t>(),
+                           rows, n, p->R, out, nout);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(replicas, out, n * 16ull * p->R, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipMemcpyAsync(ncols, nout, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_wave_create(jg_ctx* ctx, uint64_t cap_msgs, uint64_t cap_bytes, jg_wave** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && out, JG_EINVAL, "jg_wave_create: NULL argument");
+        JG_REQUIRE(cap_msgs < 0xFFFFFFFFull, JG_EINVAL, "jg_wave_create: at most 2^32-2 messages per wave");
+        jg::ensure_device(ctx);
+        auto* w = new jg_wave();
+        w->ctx = ctx;
+        w->cap_msgs = cap_msgs;
+        w->cap_bytes = cap_bytes;
+        try {
+            w->bytes.alloc(((cap_bytes + 15) & ~15ull) + 16);  // the parser reads aligned 16-byte windows
+            w->off.alloc((cap_msgs + 1) * 8);
+            w->keys.alloc(cap_msgs * 4 + 4);
+        } catch (...) {
+            delete w;
+            throw;
+        }
+        *out = w;
+    });
+}
+
+int jg_wave_destroy(jg_wave* w) {
+    return jg::guard([&] {
+        if (!w) return;
+        jg::ensure_device(w->ctx);
+        JG_HIP(hipStreamSynchronize(w->ctx->stream));
+        delete w;
+    });
+}
+
+int jg_wave_upload(jg_wave* w, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(w && key_idx && off && (bytes || n == 0), JG_EINVAL, "jg_wave_upload: NULL argument");
+        JG_REQUIRE(n <= w->cap_msgs && off[n] <= w->cap_bytes, JG_EINVAL, "jg_wave_upload: wave exceeds the capacity");
+        JG_REQUIRE(off[0] == 0, JG_EINVAL, "jg_wave_upload: off[0] must be 0");
+        uint32_t mx = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            JG_REQUIRE(off[i + 1] >= off[i], JG_EINVAL, "jg_wave_upload: offsets decrease at message %llu", (unsigned long long)i);
+            mx = key_idx[i] > mx ? key_idx[i] : mx;
+        }
+        jg_ctx* ctx = w->ctx;
+        jg::ensure_device(ctx);
+        if (off[n]) JG_HIP(hipMemcpyAsync(w->bytes.p, bytes, off[n], hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(w->off.p, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (n) JG_HIP(hipMemcpyAsync(w->keys.p, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        w->n = n;
+        w->n_bytes = off[n];
+        w->max_key = mx;
+    });
+}
+
+int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
+    return jg::guard([&] {
+        if (bad_msg) *bad_msg = UINT64_MAX;
+        JG_REQUIRE(p && w, JG_EINVAL, "jg_pnc_merge_wave: NULL argument");
+        JG_REQUIRE(p->ctx == w->ctx, JG_EINVAL, "jg_pnc_merge_wave: wave and store belong to different contexts");
+        if (w->n == 0) return;
+        JG_REQUIRE(w->max_key < p->n_keys, JG_EINVAL, "jg_pnc_merge_wave: wave addresses key %u >= n_keys %llu", w->max_key,
+                   (unsigned long long)p->n_keys);
+        jg::ensure_device(p->ctx);
+        merge_wave_dev(p, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), w->keys.as<uint32_t>(), w->n, bad_msg);
+    });
+}
+
+int jg_pnc_merge_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+    return jg::guard([&] {
+        if (bad_msg) *bad_msg = UINT64_MAX;
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_merge_json: store is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(key_idx && off && bytes, JG_EINVAL, "jg_pnc_merge_json: NULL argument");
+        check_wave_host(p, n, key_idx, off, "jg_pnc_merge_json");
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        const uint64_t nb = off[n];
+        const uint64_t nb_pad = ((nb + 15) & ~15ull) + 16;
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, nb_pad + (n + 1) * 8 + n * 4 + 512));
+        auto* dbytes = reinterpret_cast<uint8_t*>(s);
+        auto* doff = reinterpret_cast<uint64_t*>(s + nb_pad);
+        auto* drows = reinterpret_cast<uint32_t*>(s + nb_pad + (n + 1) * 8);
+        if (nb) JG_HIP(hipMemcpyAsync(dbytes, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(drows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        merge_wave_dev(p, dbytes, doff, drows, n, bad_msg);
+    });
+}
+
+int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && out, JG_EINVAL, "jg_host_alloc: NULL argument");
+        jg::ensure_device(ctx);
+        *out = nullptr;
+        if (bytes == 0) return;
+        JG_HIP(hipHostMalloc(out, bytes, hipHostMallocDefault));
+    });
+}
+
+int jg_host_free(void* p) {
+    return jg::guard([&] {
+        if (p) JG_HIP(hipHostFree(p));
+    });
+}
+
+}  // extern "C"

@@ -28,6 +28,8 @@ EXPORTS = [
     "jg_orset_create", "jg_orset_destroy", "jg_orset_load", "jg_orset_size", "jg_orset_read",
     "jg_orset_merge", "jg_orset_merge_store", "jg_orset_union", "jg_orset_contains", "jg_orset_apply_ops",
     "jg_synth_pnc_store", "jg_synth_pnc_rows", "jg_synth_orset",
+    "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
+    "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -65,13 +67,24 @@ _SIGS = {
     "jg_synth_pnc_store": ([_vp, _u64], C.c_int),
     "jg_synth_pnc_rows": ([_vp, _u64, _u64], C.c_int),
     "jg_synth_orset": ([_vp, _u64, _u64, _u32, _u32, _u32, _u32, _u32], C.c_int),
+    "jg_pnc_intern": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_columns": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_merge_json": ([_vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
+    "jg_wave_create": ([_vp, _u64, _u64, C.POINTER(_vp)], C.c_int),
+    "jg_wave_destroy": ([_vp], C.c_int),
+    "jg_wave_upload": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
+    "jg_host_alloc": ([_vp, _u64, C.POINTER(_vp)], C.c_int),
+    "jg_host_free": ([_vp], C.c_int),
 }
+GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
 
 class JanusError(RuntimeError):
-    def __init__(self, code: int, msg: str):
+    def __init__(self, code: int, msg: str, bad_msg: int | None = None):
         super().__init__(f"[{code}] {msg}")
         self.code = code
+        self.bad_msg = bad_msg  # jg_pnc_merge_json / merge_wave: first rejected message
 
 
 _lib: C.CDLL | None = None
@@ -95,11 +108,19 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     return lib
 
 
-def _check(rc: int) -> None:
+def _check(rc: int, bad_msg: int | None = None) -> None:
     if rc != JG_OK:
         buf = C.create_string_buffer(1024)
         load().jg_last_error(buf, 1024)
-        raise JanusError(rc, buf.value.decode(errors="replace"))
+        raise JanusError(rc, buf.value.decode(errors="replace"), bad_msg)
+
+
+def pack_wave(msgs) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate encoded messages (bytes) into (payload u8, offsets u64[n+1])."""
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs], dtype=np.uint64) if msgs else []
+    data = np.frombuffer(b"".join(msgs), np.uint8) if msgs else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(data), off
 
 
 def _ptr(a: np.ndarray | None):
@@ -224,9 +245,63 @@ class PNCStore:
     def synth(self, seed: int) -> None:
         _check(load().jg_synth_pnc_store(self._h, seed))
 
+    # ---- replica table + wire-format apply (json.hip) ----
+    def intern(self, key_idx, lo, hi) -> np.ndarray:
+        k = _arr(key_idx, np.uint32)
+        g = np.empty(k.size, GUID_DTYPE)
+        g["lo"], g["hi"] = lo, hi
+        out = np.empty(k.size, np.uint32)
+        _check(load().jg_pnc_intern(self._h, k.size, _ptr(k), _ptr(g), _ptr(out)))
+        return out
+
+    def columns(self, key_idx):
+        """(guids [n x R] of GUID_DTYPE, ncols [n])."""
+        k = _arr(key_idx, np.uint32)
+        g = np.zeros((k.size, self.R), GUID_DTYPE)
+        n = np.empty(k.size, np.uint32)
+        _check(load().jg_pnc_columns(self._h, k.size, _ptr(k), _ptr(g), _ptr(n)))
+        return g, n
+
+    def merge_json(self, key_idx, msgs=None, data=None, off=None) -> None:
+        """Apply encoded PNCounterMsg payloads (list of bytes, or packed data + off)."""
+        if msgs is not None:
+            data, off = pack_wave(msgs)
+        k = _arr(key_idx, np.uint32)
+        data, off = _arr(data, np.uint8), _arr(off, np.uint64)
+        bad = _u64(0)
+        rc = load().jg_pnc_merge_json(self._h, k.size, _ptr(k), _ptr(off), _ptr(data) if data.size else _ptr(np.zeros(16, np.uint8)),
+                                      C.byref(bad))
+        _check(rc, bad.value)
+
+    def merge_wave(self, wave: "Wave") -> None:
+        bad = _u64(0)
+        rc = load().jg_pnc_merge_wave(self._h, wave._h, C.byref(bad))
+        _check(rc, bad.value)
+
     def close(self) -> None:
         if self._h:
             _check(load().jg_pnc_destroy(self._h))
+            self._h = _vp()
+
+
+class Wave:
+    """Device-resident wave of encoded state messages (jg_wave)."""
+
+    def __init__(self, ctx: Context, cap_msgs: int, cap_bytes: int):
+        self.ctx = ctx
+        self._h = _vp()
+        _check(load().jg_wave_create(ctx.handle, cap_msgs, cap_bytes, C.byref(self._h)))
+
+    def upload(self, key_idx, msgs=None, data=None, off=None) -> None:
+        if msgs is not None:
+            data, off = pack_wave(msgs)
+        k = _arr(key_idx, np.uint32)
+        data, off = _arr(data, np.uint8), _arr(off, np.uint64)
+        _check(load().jg_wave_upload(self._h, k.size, _ptr(k), _ptr(off), _ptr(data)))
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_wave_destroy(self._h))
             self._h = _vp()
 
 

@@ -6,9 +6,11 @@
 // arrays.  Also holds the host copy of the synthetic-workload generators (BASELINE.md §2,
 // SURVEY.md §8d D2/D3), which the HIP engine re-states on the device in synth.hip.
 #include <chrono>
+#include <cstring>
 #include <limits>
 #include <thread>
 
+#include "json.hpp"
 #include "oracle.hpp"
 
 using namespace oracle;
@@ -333,6 +335,108 @@ double orc_bench_orset_merge(uint64_t n_sets, uint32_t E, uint32_t a, uint32_t o
         times.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     return median_of(times);
+}
+
+// ---- state-message wire codec (oracle/json.hpp) ------------------------------
+// Encode one PNCounterMsg whose pVector and nVector hold the n Guids (lo[i], hi[i]) in order with
+// values pv[i] / nv[i] (int64 storage; eb = 4 or 8 is the C# width).  Returns the length, or -1 if
+// cap is too small.
+int64_t orc_json_encode_pnc(uint64_t n, const uint64_t* lo, const uint64_t* hi, const int64_t* pv, const int64_t* nv, uint32_t eb,
+                            char* out, uint64_t cap) {
+    std::string s;
+    if (eb == 4) {
+        PNCounterMsg<int32_t> m;
+        for (uint64_t i = 0; i < n; ++i) { m.pVector[Guid{lo[i], hi[i]}] = (int32_t)pv[i]; m.nVector[Guid{lo[i], hi[i]}] = (int32_t)nv[i]; }
+        s = json::EncodePNC(m);
+    } else {
+        PNCounterMsg<int64_t> m;
+        for (uint64_t i = 0; i < n; ++i) { m.pVector[Guid{lo[i], hi[i]}] = pv[i]; m.nVector[Guid{lo[i], hi[i]}] = nv[i]; }
+        s = json::EncodePNC(m);
+    }
+    if (s.size() > cap) return -1;
+    std::memcpy(out, s.data(), s.size());
+    return (int64_t)s.size();
+}
+
+// 1 if the payload is accepted by PNCounterMsg.Decode at width eb (the wire contract), else 0.
+int orc_json_accepts_pnc(const char* bytes, uint64_t len, uint32_t eb) {
+    try {
+        if (eb == 4) json::DecodePNC<int32_t>(std::string_view(bytes, len));
+        else json::DecodePNC<int64_t>(std::string_view(bytes, len));
+        return 1;
+    } catch (const json::JsonException&) {
+        return 0;
+    }
+}
+
+// The stable-apply loop over encoded states (SafeCRDT.ApplyUpdateStable -> Decode -> Merge, in
+// commit order, SafeCRDTManager.cs:122-146) on a dense store with a replica table: row k holds the
+// Guids cols[k*R + c] (c < ncols[k]) with values P/N[k*R + c], i.e. a PNCounter whose P and N
+// dictionaries enumerate those Guids in column order.  Messages are applied in order until the first
+// one Decode rejects (the reference's loop stops at the throwing message): *bad = its index, or
+// UINT64_MAX.  The touched rows are written back (P, N, cols, ncols; columns = P's enumeration order).
+// Returns 0, or -2 if a row would hold more than R replicas (the engine's capacity limit, not a
+// reference behaviour) — *bad is then that message.
+}  // extern "C"
+
+namespace {
+template <class T>
+int json_apply(uint64_t n_keys, uint32_t R, T* P, T* N, uint64_t* cols, uint32_t* ncols, uint64_t n, const uint32_t* key_idx,
+               const uint64_t* off, const char* bytes, uint64_t* bad) {
+    std::unordered_map<uint64_t, PNCounter<T>> live;
+    *bad = UINT64_MAX;
+    auto obj = [&](uint64_t k) -> PNCounter<T>& {
+        auto it = live.find(k);
+        if (it != live.end()) return it->second;
+        it = live.emplace(k, PNCounter<T>(Guid{~0ull, ~0ull})).first;
+        it->second.mutP().Clear(); it->second.mutN().Clear();
+        for (uint32_t c = 0; c < ncols[k]; ++c) {
+            const Guid g{cols[2 * (k * R + c)], cols[2 * (k * R + c) + 1]};
+            it->second.mutP()[g] = P[k * R + c];
+            it->second.mutN()[g] = N[k * R + c];
+        }
+        return it->second;
+    };
+    int rc = 0;
+    for (uint64_t m = 0; m < n; ++m) {
+        const uint64_t k = key_idx[m];
+        if (k >= n_keys) return -1;
+        PNCounterMsg<T> msg;
+        try {
+            msg = json::DecodePNC<T>(std::string_view(bytes + off[m], off[m + 1] - off[m]));
+        } catch (const json::JsonException&) {
+            *bad = m;
+            break;
+        }
+        PNCounter<T>& pc = obj(k);
+        pc.ApplySynchronizedUpdate(msg);
+        if (pc.P().size() > R || pc.N().size() > R) { *bad = m; rc = -2; break; }
+    }
+    for (auto& kv : live) {
+        const uint64_t k = kv.first;
+        uint32_t c = 0;
+        for (const auto& e : kv.second.P()) {
+            if (c >= R) break;
+            cols[2 * (k * R + c)] = e.first.lo;
+            cols[2 * (k * R + c) + 1] = e.first.hi;
+            P[k * R + c] = e.second;
+            T v = 0;
+            kv.second.N().TryGetValue(e.first, v);
+            N[k * R + c] = v;
+            ++c;
+        }
+        ncols[k] = c;
+    }
+    return rc;
+}
+}  // namespace
+
+extern "C" {
+
+int orc_pnc_apply_json(uint64_t n_keys, uint32_t R, uint32_t eb, void* P, void* N, uint64_t* cols, uint32_t* ncols, uint64_t n,
+                       const uint32_t* key_idx, const uint64_t* off, const char* bytes, uint64_t* bad) {
+    if (eb == 4) return json_apply<int32_t>(n_keys, R, (int32_t*)P, (int32_t*)N, cols, ncols, n, key_idx, off, bytes, bad);
+    return json_apply<int64_t>(n_keys, R, (int64_t*)P, (int64_t*)N, cols, ncols, n, key_idx, off, bytes, bad);
 }
 
 }  // extern "C"

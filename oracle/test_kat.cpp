@@ -9,6 +9,7 @@
 #include <functional>
 #include <sstream>
 
+#include "json.hpp"
 #include "oracle.hpp"
 
 using namespace oracle;
@@ -52,7 +53,8 @@ TEST(PNCounterTests_TestPNCMerge) {  // PNCounterTests.cs:21-38
 TEST(PNCounterMsgTests_EncodeDecode) {  // PNCounterTests.cs:46-66
     PNCounter<int32_t> pnc1(G); pnc1.Increment(5); pnc1.Decrement(1);
     PNCounter<int32_t> pnc2(G); pnc2.Increment(2); pnc1.Decrement(2);
-    PNCounterMsg<int32_t> decoded = pnc2.GetLastSynchronizedUpdate();  // JSON round trip = identity on the decoded form
+    const std::string encoded = json::EncodePNC(pnc2.GetLastSynchronizedUpdate());  // Encode -> bytes -> Decode
+    PNCounterMsg<int32_t> decoded = json::DecodePNC<int32_t>(encoded);
     pnc1.ApplySynchronizedUpdate(decoded);
     CHECK_EQ(pnc1.Get(), 5 - 1 + 2 - 2);
 }
@@ -300,9 +302,52 @@ TEST(ORSetMsgTests_EncodeDecode) {  // ORSetTests.cs:453-474 (order-sensitive at
     ORSet set1, set2;
     set1.Add(S("a"), G); set1.Add(S("b"), G);
     set2.Add(S("a"), G); set2.Add(S("b"), G); set2.Remove(S("b"));
-    ORSetMsg decoded = set2.GetLastSynchronizedUpdate();
+    const std::string encoded = json::EncodeORSet(set2.GetLastSynchronizedUpdate());
+    ORSetMsg decoded = json::DecodeORSet(encoded);
     set1.ApplySynchronizedUpdate(decoded);
     CHECK(set1.LookupAll() == (L{S("a"), S("b")}));
+}
+// Wire codec (oracle/json.hpp): the System.Text.Json shapes and the accepted decode contract.
+TEST(Json_PNCShapeAndGuidFormat) {  // PNCounters.cs:46-49, Guid.ToString("D")
+    PNCounterMsg<int32_t> m;
+    Guid g{0x1122334455667788ull, 0x99AABBCCDDEEFF00ull};  // bytes 88 77 66 55 44 33 22 11 00 FF EE DD CC BB AA 99
+    m.pVector[g] = 7; m.nVector[g] = -3;
+    CHECK_EQ(json::GuidD(g), std::string("55667788-3344-1122-00ff-eeddccbbaa99"));
+    CHECK_EQ(json::EncodePNC(m), std::string("{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":7},\"nVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":-3}}"));
+    auto d = json::DecodePNC<int32_t>(" {\"nVector\" : {\"55667788-3344-1122-00FF-EEDDCCBBAA99\" : -3 } ,\n\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":7}}\r\n");
+    int32_t v = 0;
+    CHECK(d.pVector.TryGetValue(g, v) && v == 7);
+    CHECK(d.nVector.TryGetValue(g, v) && v == -3);
+}
+TEST(Json_PNCRejects) {
+    const char* bad[] = {
+        "{\"pVector\":{}}",                                   // nVector missing -> null -> NRE in Merge
+        "{\"pVector\":null,\"nVector\":{}}",                // null vector
+        "{\"pVector\":{},\"nVector\":{},\"x\":1}",        // unknown property (narrowed)
+        "{\"pVector\":{},\"nVector\":{},\"pVector\":{}}", // duplicate property
+        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":1,\"55667788-3344-1122-00ff-eeddccbbaa99\":2},\"nVector\":{}}",
+        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":01},\"nVector\":{}}",
+        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":1.0},\"nVector\":{}}",
+        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":2147483648},\"nVector\":{}}",
+        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa9\":1},\"nVector\":{}}",
+        "{\"pVector\":{},\"nVector\":{}} x",
+        "{\"pVector\":{},\"nVector\":{},}",
+    };
+    for (const char* b : bad) CHECK_THROWS<json::JsonException>([&] { json::DecodePNC<int32_t>(b); }, __LINE__);
+    CHECK_EQ(json::DecodePNC<int32_t>("{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":-2147483648},\"nVector\":{}}").pVector.size(), (size_t)1);
+    CHECK_EQ(json::DecodePNC<int64_t>("{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":2147483648},\"nVector\":{}}").pVector.size(), (size_t)1);
+}
+TEST(Json_ORSetEscapesAndRoundTrip) {  // ORSet.cs:56-69; JavaScriptEncoder.Default
+    ORSet s;
+    s.Add(S("a<b>&\"q\"\\"), G); s.Add(S("caf\xC3\xA9 \xF0\x9F\x98\x80"), G); s.Add(NUL, G); s.Add(S("x"), G); s.Remove(S("x"));
+    const std::string e = json::EncodeORSet(s.GetLastSynchronizedUpdate());
+    CHECK(e.find("a\\u003Cb\\u003E\\u0026\\u0022q\\u0022\\\\") != std::string::npos);
+    CHECK(e.find("caf\\u00E9 \\uD83D\\uDE00") != std::string::npos);
+    ORSet t;
+    t.ApplySynchronizedUpdate(json::DecodeORSet(e));
+    CHECK(t.LookupAll() == s.LookupAll());
+    CHECK_THROWS<json::JsonException>([&] { json::DecodeORSet("{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[]}"); }, __LINE__);
+    CHECK_THROWS<json::JsonException>([&] { json::DecodeORSet("{\"addSet\":{\"\\ud800\":[]},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"); }, __LINE__);
 }
 // Semantics note n4 (SetEquals, not "add \ rem non-empty"), pinned by ORSet.cs:216.
 TEST(ORSet_SetEqualsNotDifference) {

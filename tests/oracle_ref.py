@@ -26,6 +26,9 @@ _SIGS = {
     "orc_orset_lookup_all": ([_vp, _u64, _vp, _u64, _u32, _vp, _u64], C.c_int64),
     "orc_bench_pnc_merge": ([_u64, _u32, _u64, _i32, _i32], C.c_double),
     "orc_bench_orset_merge": ([_u64, _u32, _u32, _u32, _u32, _u32, _u64, _i32, _i32], C.c_double),
+    "orc_json_encode_pnc": ([_u64, _vp, _vp, _vp, _vp, _u32, _vp, _u64], C.c_int64),
+    "orc_json_accepts_pnc": ([C.c_char_p, _u64, _u32], C.c_int),
+    "orc_pnc_apply_json": ([_u64, _u32, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
 }
 
 _lib = None
@@ -153,3 +156,36 @@ def bench_pnc_merge(n_keys, R, seed, threads=1, reps=5) -> float:
 
 def bench_orset_merge(n_sets, E, a, ov, t, tov, seed, threads=1, reps=5) -> float:
     return lib().orc_bench_orset_merge(n_sets, E, a, ov, t, tov, seed, threads, reps)
+
+
+# ---- state-message wire codec (oracle/json.hpp) ----
+GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])
+
+
+def json_encode_pnc(lo, hi, pv, nv, eb: int) -> bytes:
+    """PNCounterMsg.Encode of a message whose pVector/nVector hold Guids (lo[i], hi[i]) in order."""
+    lo, hi = np.ascontiguousarray(lo, np.uint64), np.ascontiguousarray(hi, np.uint64)
+    pv, nv = np.ascontiguousarray(pv, np.int64), np.ascontiguousarray(nv, np.int64)
+    buf = C.create_string_buffer(64 + 128 * len(lo))
+    n = lib().orc_json_encode_pnc(len(lo), _p(lo), _p(hi), _p(pv), _p(nv), eb, buf, len(buf))
+    assert n >= 0
+    return buf.raw[:n]
+
+
+def json_accepts_pnc(payload: bytes, eb: int) -> bool:
+    return bool(lib().orc_json_accepts_pnc(payload, len(payload), eb))
+
+
+def pnc_apply_json(P, N, cols, ncols, key_idx, msgs, eb):
+    """Oracle stable-apply loop over encoded states; returns (P, N, cols, ncols, bad_msg, rc).
+    cols is a GUID_DTYPE [n_keys x R] array."""
+    P, N = P.copy(), N.copy()
+    cols, ncols = cols.copy(), np.ascontiguousarray(ncols, np.uint32).copy()
+    n_keys, R = P.shape
+    k = np.ascontiguousarray(key_idx, np.uint32)
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(m) for m in msgs])
+    data = b"".join(msgs) + b"\0"
+    bad = _u64(0)
+    rc = lib().orc_pnc_apply_json(n_keys, R, eb, _p(P), _p(N), _p(cols), _p(ncols), len(msgs), _p(k), _p(off), data, C.byref(bad))
+    return P, N, cols, ncols, (None if bad.value == 2**64 - 1 else bad.value), rc

@@ -1,0 +1,236 @@
+"""GPU parity of the wire-format apply path (janus-crdt_amd/csrc/json.hip, SURVEY.md §8f F1 + §8a A2/A13)
+against the oracle's Decode + Merge loop (oracle/json.hpp, oracle/capi.cpp orc_pnc_apply_json), through
+the C ABI: the decode contract, replica interning in commit order, all-or-nothing errors, row capacity,
+and the device-resident wave.  Bit-exact on values, replica Guids and column order."""
+import numpy as np
+import pytest
+
+import janus_gpu as jg
+import oracle_ref as orc
+from jsongen import CONTRACT, G1, G2, Cluster, encode_pnc, random_guids
+
+pytestmark = pytest.mark.gpu
+
+
+def _guid_arr(gs):
+    a = np.empty(len(gs), orc.GUID_DTYPE)
+    a["lo"] = [g[0] for g in gs]
+    a["hi"] = [g[1] for g in gs]
+    return a
+
+
+class Pair:
+    """A GPU store and the oracle's dense image of the same state."""
+
+    def __init__(self, ctx, n_keys, R, eb, stable):
+        self.s = jg.PNCStore(ctx, n_keys, R, eb)
+        ga = _guid_arr(stable)
+        cols0 = self.s.intern(np.arange(n_keys, dtype=np.uint32), ga["lo"], ga["hi"])
+        assert (cols0 == 0).all()
+        dt = np.int32 if eb == 4 else np.int64
+        self.P = np.zeros((n_keys, R), dt)
+        self.N = np.zeros((n_keys, R), dt)
+        self.cols = np.zeros((n_keys, R), orc.GUID_DTYPE)
+        self.cols[:, 0] = ga
+        self.ncols = np.ones(n_keys, np.uint32)
+        self.eb, self.n_keys = eb, n_keys
+
+    def oracle(self, keys, msgs):
+        self.P, self.N, self.cols, self.ncols, bad, rc = orc.pnc_apply_json(self.P, self.N, self.cols, self.ncols, keys, msgs, self.eb)
+        return bad, rc
+
+    def check(self):
+        P, N = self.s.read_rows()
+        g, n = self.s.columns(np.arange(self.n_keys, dtype=np.uint32))
+        assert np.array_equal(n, self.ncols), "column counts differ"
+        for k in range(self.n_keys):
+            c = int(n[k])
+            assert np.array_equal(g[k, :c], self.cols[k, :c]), f"replica order differs at key {k}"
+        assert np.array_equal(P, self.P) and np.array_equal(N, self.N), "values differ"
+
+    def close(self):
+        self.s.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
+def test_decode_contract_on_device(ctx, eb):
+    for i, (payload, ok4, ok8) in enumerate(CONTRACT):
+        ok = ok4 if eb == 4 else ok8
+        pr = Pair(ctx, 2, 4, eb, [(7, 7), (8, 8)])
+        bad, rc = pr.oracle(np.array([1], np.uint32), [payload])
+        assert (bad is None) == ok, f"oracle disagrees with the contract on case {i}"
+        if ok:
+            pr.s.merge_json([1], [payload])
+        else:
+            with pytest.raises(jg.JanusError) as e:
+                pr.s.merge_json([1], [payload])
+            assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 0, f"case {i}: {e.value}"
+        pr.check()
+        pr.close()
+
+
+@pytest.mark.parametrize("eb,R,pool", [(4, 8, 6), (8, 8, 6), (4, 64, 40), (8, 200, 150)])
+def test_random_waves_match_oracle(ctx, eb, R, pool):
+    rng = np.random.default_rng(R * 10 + eb)
+    n_keys = 40
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, R, eb, stable)
+    cl = Cluster(rng, n_keys, pool, eb, stable)
+    for wave in range(5):
+        n = int(rng.integers(1, 1500))
+        keys = rng.integers(0, n_keys, n).astype(np.uint32)
+        msgs = [cl.message(int(k), grow=0.05 if R > 8 else 0.3) for k in keys]
+        bad, rc = pr.oracle(keys, msgs)
+        assert bad is None and rc == 0
+        pr.s.merge_json(keys, msgs)
+        pr.check()
+    pr.close()
+
+
+def test_wild_values_and_vector_orders(ctx):
+    """Negative and extreme values, pVector/nVector in different orders, replicas only in one vector."""
+    rng = np.random.default_rng(11)
+    n_keys, R = 8, 16
+    stable = random_guids(rng, n_keys)
+    pool = [random_guids(rng, 10) for _ in range(n_keys)]
+    pr = Pair(ctx, n_keys, R, 4, stable)
+    keys, msgs = [], []
+    for _ in range(400):
+        k = int(rng.integers(0, n_keys))
+        gs = [pool[k][i] for i in rng.permutation(10)[: int(rng.integers(0, 6))]]
+        vals = rng.integers(-2**31, 2**31, len(gs))
+        pv = [int(v) if rng.random() < 0.8 else None for v in vals]
+        nv = [int(v) ^ 0x55 if rng.random() < 0.5 else None for v in vals]
+        p = ",".join(f'"{jg_guid(g)}":{v}' for g, v in zip(gs, pv) if v is not None)
+        order = list(zip(gs, nv))[::-1]
+        q = ",".join(f'"{jg_guid(g)}":{v}' for g, v in order if v is not None)
+        msgs.append(('{"nVector":{' + q + '},"pVector":{' + p + "}}").encode())
+        keys.append(k)
+    keys = np.array(keys, np.uint32)
+    bad, rc = pr.oracle(keys, msgs)
+    assert bad is None and rc == 0
+    pr.s.merge_json(keys, msgs)
+    # values per replica Guid must agree; the column order can differ only where a message lists its
+    # vectors' replicas in different orders (never produced by the reference)
+    P, N = pr.s.read_rows()
+    g, n = pr.s.columns(np.arange(n_keys, dtype=np.uint32))
+    for k in range(n_keys):
+        got = {(int(x["lo"]), int(x["hi"])): (P[k, c], N[k, c]) for c, x in enumerate(g[k, : n[k]])}
+        exp = {(int(x["lo"]), int(x["hi"])): (pr.P[k, c], pr.N[k, c]) for c, x in enumerate(pr.cols[k, : pr.ncols[k]])}
+        # the oracle's export lists P's keys; replicas seen only in nVector exist in the GPU table with P = 0
+        for key, (p, q) in got.items():
+            if key in exp:
+                assert (p, q) == exp[key], f"key {k}"
+            else:
+                assert p == 0
+    pr.close()
+
+
+def jg_guid(g):
+    from jsongen import guid_d
+    return guid_d(*g)
+
+
+def test_bad_message_is_all_or_nothing_then_prefix(ctx):
+    rng = np.random.default_rng(5)
+    n_keys = 30
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, 8, 4, stable)
+    cl = Cluster(rng, n_keys, 6, 4, stable)
+    keys = rng.integers(0, n_keys, 1000).astype(np.uint32)
+    msgs = [cl.message(int(k)) for k in keys]
+    msgs[700] = msgs[700].replace(b'"nVector"', b'"mVector"')
+    msgs[901] = b"{"
+    with pytest.raises(jg.JanusError) as e:
+        pr.s.merge_json(keys, msgs)
+    assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 700
+    pr.check()  # nothing applied (columns included)
+    bad, rc = pr.oracle(keys, msgs)  # the reference's loop: messages before the throwing one applied
+    assert bad == 700
+    pr.s.merge_json(keys[:700], msgs[:700])  # the host re-submits the prefix
+    pr.check()
+    pr.close()
+
+
+def test_row_capacity_rolls_back(ctx):
+    rng = np.random.default_rng(6)
+    stable = random_guids(rng, 3)
+    pr = Pair(ctx, 3, 3, 4, stable)
+    gs = random_guids(rng, 4)
+    msgs = [encode_pnc(gs[:1], [1], [0]), encode_pnc(gs[:2], [2, 2], [0, 0]), encode_pnc([gs[0]], [3], [0]),
+            encode_pnc(gs[:3], [1, 1, 1], [0, 0, 0])]
+    keys = np.array([2, 1, 1, 2], np.uint32)  # key 2 would need 1 + 3 = 4 columns
+    with pytest.raises(jg.JanusError) as e:
+        pr.s.merge_json(keys, msgs)
+    assert e.value.code == jg.JG_ESTATE and e.value.bad_msg == 3
+    pr.check()  # key 1's new columns rolled back too
+    bad, rc = pr.oracle(keys[:3], msgs[:3])
+    pr.s.merge_json(keys[:3], msgs[:3])
+    pr.check()
+    pr.close()
+
+
+def test_intern_order_repeats_and_capacity(ctx):
+    s = jg.PNCStore(ctx, 4, 3, 8)
+    keys = np.array([1, 0, 1, 1, 0, 1], np.uint32)
+    lo = np.array([10, 20, 11, 10, 21, 12], np.uint64)
+    cols = s.intern(keys, lo, lo * 3)
+    assert cols.tolist() == [0, 0, 1, 0, 1, 2]
+    g, n = s.columns(np.array([0, 1, 2], np.uint32))
+    assert n.tolist() == [2, 3, 0]
+    assert g[1, :3]["lo"].tolist() == [10, 11, 12] and g[0, :2]["lo"].tolist() == [20, 21]
+    with pytest.raises(jg.JanusError) as e:
+        s.intern(np.array([2, 1], np.uint32), np.array([5, 99], np.uint64), np.array([5, 99], np.uint64))
+    assert e.value.code == jg.JG_ESTATE
+    g2, n2 = s.columns(np.array([0, 1, 2], np.uint32))
+    assert n2.tolist() == [2, 3, 0]  # all or nothing: key 2's registration was rolled back too
+    s.close()
+
+
+def test_device_resident_wave_equals_host_call(ctx):
+    rng = np.random.default_rng(8)
+    n_keys = 64
+    stable = random_guids(rng, n_keys)
+    a = Pair(ctx, n_keys, 8, 8, stable)
+    b = Pair(ctx, n_keys, 8, 8, stable)
+    cl = Cluster(rng, n_keys, 6, 8, stable)
+    w = jg.Wave(ctx, 5000, 5_000_000)
+    for _ in range(3):
+        keys = rng.integers(0, n_keys, 3000).astype(np.uint32)
+        msgs = [cl.message(int(k)) for k in keys]
+        a.oracle(keys, msgs)
+        a.s.merge_json(keys, msgs)
+        w.upload(keys, msgs)
+        b.s.merge_wave(w)
+        b.s.merge_wave(w)  # idempotent: the same wave twice changes nothing
+        b.P, b.N, b.cols, b.ncols = a.P, a.N, a.cols, a.ncols
+        a.check()
+        b.check()
+    w.close()
+    a.close()
+    b.close()
+
+
+def test_c5_shaped_wave(ctx):
+    """Banking-shaped wave (4 nodes, replicas = stable + one per node): 100k messages over 20k accounts,
+    checked against the oracle on every account."""
+    rng = np.random.default_rng(9)
+    n_keys, nodes = 20_000, 4
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, nodes + 1, 4, stable)
+    reps = [random_guids(rng, nodes) for _ in range(n_keys)]
+    P = np.zeros((n_keys, nodes), np.int64)
+    keys = rng.integers(0, n_keys, 100_000).astype(np.uint32)
+    msgs = []
+    for k in keys:
+        n = int(rng.integers(0, nodes))
+        P[k, n] += int(rng.integers(1, 1000))
+        msgs.append(encode_pnc(reps[k], P[k].tolist(), [0] * nodes))
+    bad, rc = pr.oracle(keys, msgs)
+    assert bad is None and rc == 0
+    pr.s.merge_json(keys, msgs)
+    pr.check()
+    v, o = pr.s.values()
+    # every message carries its node's full row, and rows only grow: Get = the latest row sums
+    assert (o == 0).all() and np.array_equal(v, np.where(np.isin(np.arange(n_keys), keys), P.sum(axis=1), 0))
+    pr.close()
