@@ -6,10 +6,13 @@
 // (SafeCRDT.cs:52), packed clientBatchSize = 1000 states per UpdateMessage (JanusService.cs:29) and
 // 100 UpdateMessages per block (DAG.cs:25).  A wave holds `msgs` state messages.
 //
-// GPU: janus::GpuStableStore::ApplyCommitted (host decode/interning into one SoA batch + ONE
-// jg_pnc_merge_rows).  CPU baseline: the oracle's SafeCRDTManager.HandleAfterConsensusUpdates
-// (dictionary-faithful restatement of SafeCRDTManager.cs:109-160, one thread like the reference's
-// serialized apply task) on the first `cpu_msgs` messages of the same wave.
+// Every state travels as the reference ships it: NetworkProtocol.message = PNCounterMsg JSON
+// (SafeCRDT.cs:49, PNCounters.cs:46-49).
+// GPU: janus::GpuStableStore::ApplyCommitted (classify + gather the payloads into pinned staging +
+// ONE jg_pnc_merge_json: decode, replica interning and merge on the device).  CPU baseline: the
+// oracle's SafeCRDTManager.HandleAfterConsensusUpdates (dictionary-faithful restatement of
+// SafeCRDTManager.cs:109-160: Decode + Merge per message, one thread like the reference's serialized
+// apply task) on the first `cpu_msgs` messages of the same wave.
 // Prints one JSON object.
 #include <chrono>
 #include <cmath>
@@ -21,6 +24,7 @@
 
 #include "janus_host.hpp"
 #include "oracle.hpp"
+#include "wire.hpp"
 
 namespace {
 
@@ -72,7 +76,7 @@ int main(int argc, char** argv) {
     };
 
     double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
-    uint64_t gpu_n = 0, cpu_n = 0;
+    uint64_t gpu_n = 0, cpu_n = 0, payload = 0, payload_timed = 0;
     for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
         Wave wave;
         std::vector<janus::UpdateMessage> block;
@@ -90,18 +94,18 @@ int main(int argc, char** argv) {
             janus::NetworkProtocol np;
             np.uid = G(uid[k]);
             np.seq = m;
-            for (int j = 0; j < nodes; ++j) {         // the node's full state: every replica it has seen
-                np.pnc.pVector.emplace_back(G(rep[k * nodes + j]), P[k * nodes + j]);
-                np.pnc.nVector.emplace_back(G(rep[k * nodes + j]), N[k * nodes + j]);
+            {   // the node's full state: every replica it has seen, encoded (GetLastSynchronizedUpdate().Encode())
+                janus::Guid g[16];
+                int64_t pv[16], nv[16];
+                for (int j = 0; j < nodes; ++j) { g[j] = G(rep[k * nodes + j]); pv[j] = P[k * nodes + j]; nv[j] = N[k * nodes + j]; }
+                janus::wire::AppendPNCounterMsg(np.message, g, pv, nv, nodes);
             }
+            payload += np.message.size();
             if (m < cpu_msgs && w > 0) {
                 oracle::NetworkProtocol cp;
                 cp.uid = uid[k];
                 cp.seq = m;
-                for (int j = 0; j < nodes; ++j) {
-                    cp.message.pnc.pVector[rep[k * nodes + j]] = P[k * nodes + j];
-                    cp.message.pnc.nVector[rep[k * nodes + j]] = N[k * nodes + j];
-                }
+                cp.bytes = np.message;  // the oracle decodes it in ApplyUpdateStable (oracle/json.hpp)
                 cum.update.push_back(std::move(cp));
                 if (cum.update.size() == 1000) { cblock.push_back(std::move(cum)); cum = oracle::UpdateMessage(); }
                 if (cblock.size() == 100) { wave.cpu.push_back(std::move(cblock)); cblock.clear(); }
@@ -115,6 +119,8 @@ int main(int argc, char** argv) {
         if (!cum.update.empty()) cblock.push_back(std::move(cum));
         if (!cblock.empty()) wave.cpu.push_back(std::move(cblock));
 
+        const uint64_t wave_payload = payload;
+        payload = 0;
         const double t0 = now_s();
         gpu.ApplyCommitted(wave.gpu, nullptr);
         const double t1 = now_s();
@@ -124,20 +130,22 @@ int main(int argc, char** argv) {
             engine_s += gpu.last_apply_engine_s();
             for (int q = 0; q < 4; ++q) ph[q] += gpu.last_apply_phases_s()[q];
             gpu_n += msgs;
+            payload_timed += wave_payload;
             const double c0 = now_s();
             cpu.HandleAfterConsensusUpdates(wave.cpu);
             cpu_s += now_s() - c0;
             cpu_n += std::min(msgs, cpu_msgs);
         }
     }
-    const double bytes = (double)gpu_n * (4 + 2.0 * R * 4);  // key index + P and N rows per message
-    std::printf("{\"workload\": \"committed-batch apply (C5 banking-shaped, %s accounts %llu, %d nodes, %llu state msgs per wave)\", "
-                "\"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"host_decode_ms_per_wave\": %.3f, "
+    const double bytes = (double)payload_timed;  // JSON payload bytes uploaded and decoded
+    std::printf("{\"workload\": \"committed-batch apply (C5 banking-shaped, %s accounts %llu, %d nodes, %llu PNCounterMsg JSON states per wave)\", "
+                "\"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"payload_bytes_per_msg\": %.1f, \"host_ms_per_wave\": %.3f, "
                 "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, \"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], "
-                "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, \"kind\": \"port\"}}\n",
+                "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, \"kind\": \"port\", "
+                "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
                 normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s,
-                1e3 * gpu_s / waves, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, bytes / engine_s / 1e9, janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves,
-                1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves, cpu_n / cpu_s,
-                (unsigned long long)std::min(msgs, cpu_msgs));
+                1e3 * gpu_s / waves, bytes / gpu_n, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, bytes / engine_s / 1e9,
+                janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves, 1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves,
+                cpu_n / cpu_s, (unsigned long long)std::min(msgs, cpu_msgs));
     return 0;
 }

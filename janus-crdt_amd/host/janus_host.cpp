@@ -1,12 +1,16 @@
 // janus_host.cpp — see janus_host.hpp.
 #include "janus_host.hpp"
 
+#include <cstring>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <limits>
 #include <memory>
 #include <thread>
+
+#include "wire.hpp"
 
 namespace janus {
 
@@ -40,6 +44,7 @@ GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas,
 }
 
 GpuStableStore::~GpuStableStore() {
+    if (stage_) jg_host_free(stage_);
     if (orset_) jg_orset_destroy(orset_);
     if (pnc_) jg_pnc_destroy(pnc_);
     if (ctx_) jg_close(ctx_);
@@ -80,32 +85,6 @@ const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want
     return *r;
 }
 
-uint32_t GpuStableStore::column_nothrow(uint32_t row, const Guid& g, uint32_t hint) {
-    Guid* c = &cols_[(size_t)row * R_];
-    uint32_t& n = ncols_[row];
-    if (hint < n && c[hint] == g) return hint;
-    for (uint32_t j = 0; j < n; ++j)
-        if (c[j] == g) return j;
-    if (n >= R_) return UINT32_MAX;
-    c[n] = g;
-    return n++;
-}
-
-uint32_t GpuStableStore::column(uint32_t row, const Guid& g, uint32_t hint) {
-    const uint32_t c = column_nothrow(row, g, hint);
-    if (c == UINT32_MAX) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
-    return c;
-}
-
-uint32_t GpuStableStore::find_column(uint32_t row, const Guid& g, uint32_t hint) const {
-    const Guid* c = &cols_[(size_t)row * R_];
-    const uint32_t n = ncols_[row];
-    if (hint < n && c[hint] == g) return hint;
-    for (uint32_t j = 0; j < n; ++j)
-        if (c[j] == g) return j;
-    return UINT32_MAX;
-}
-
 uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e, bool create) {
     if (!e) return JG_NULL_ELEM;
     auto it = s.elems.find(*e);
@@ -122,16 +101,35 @@ void GpuStableStore::CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& 
     if (type == CrdtType::PNCounter) {
         if (next_row_ >= max_keys_) throw EngineError(JG_ESTATE, "PNCounter store full");
         const uint32_t row = next_row_++;
-        if (ncols_.size() <= row) {
-            ncols_.resize((size_t)row + 1, 0);
-            cols_.resize(((size_t)row + 1) * R_);
-        }
-        column(row, stableReplicaGuid, 0);  // {self: 0} — the row is zero already
+        reg_rows_.push_back(row);  // {self: 0} — the row is zero already; column 0 once flushed
+        reg_guids_.push_back(jg_guid{stableReplicaGuid.lo, stableReplicaGuid.hi});
         uids_.insert(uid, KeyRef{type, row});
     } else {
         uids_.insert(uid, KeyRef{type, next_set_++});
         sets_.emplace_back();
     }
+}
+
+void GpuStableStore::flush_registrations() {
+    if (reg_rows_.empty()) return;
+    std::vector<uint32_t> cols(reg_rows_.size());
+    check(jg_pnc_intern(pnc_, reg_rows_.size(), reg_rows_.data(), reg_guids_.data(), cols.data()));
+    reg_rows_.clear();
+    reg_guids_.clear();
+}
+
+char* GpuStableStore::staging(size_t bytes) {
+    if (bytes > stage_bytes_) {
+        if (stage_) jg_host_free(stage_);
+        stage_ = nullptr;
+        stage_bytes_ = 0;
+        void* p = nullptr;
+        const size_t want = bytes + bytes / 4 + 4096;
+        check(jg_host_alloc(ctx_, want, &p));
+        stage_ = static_cast<char*>(p);
+        stage_bytes_ = want;
+    }
+    return stage_;
 }
 
 namespace {
@@ -169,6 +167,7 @@ int GpuStableStore::host_threads() {
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                                      std::unordered_map<uint64_t, uint64_t>* tracker) {
     const double t0 = wall_s();
+    flush_registrations();
     std::vector<const NetworkProtocol*> msgs;
     {
         size_t n_msgs = 0;
@@ -182,13 +181,14 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
     const size_t n = msgs.size();
     const int T = host_threads();
     phase_s_[0] = wall_s() - t0;
-    constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1, kBadType = UINT32_MAX - 2;
+    constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1;
 
-    // Phase 1 (parallel, read-only): classify every message — PNC row, OR-Set, or skipped (:133-136).
+    // Phase 1 (parallel, read-only): classify every message — PNC row, OR-Set, or skipped (:133-136)
+    // — and size the PN-Counter payloads.
     std::vector<uint32_t> cls(n);
-    std::vector<size_t> pnc_count(T, 0), bad(T, SIZE_MAX);
+    std::vector<size_t> pnc_count(T, 0), pnc_bytes(T, 0);
     parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
-        size_t cnt = 0;
+        size_t cnt = 0, bytes = 0;
         for (size_t i = b; i < e; ++i) {
             if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
             if (i + 8 < e) uids_.prefetch(msgs[i + 8]->uid);
@@ -196,140 +196,124 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
             uint32_t c = kSkip;
             if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {
                 if (const KeyRef* kr = uids_.find(u.uid)) {
-                    if (u.type != kr->type) c = kBadType;  // ORSet.cs:288-291 / the PNCounter cast
-                    else if (kr->type == CrdtType::PNCounter) { c = kr->idx; ++cnt; }
+                    if (kr->type == CrdtType::PNCounter) { c = kr->idx; ++cnt; bytes += u.message.size(); }
                     else c = kSet;
                 }
             }
-            if (c == kBadType && bad[t] == SIZE_MAX) bad[t] = i;
             cls[i] = c;
         }
         pnc_count[t] = cnt;
+        pnc_bytes[t] = bytes;
     });
-    for (int t = 0; t < T; ++t)
-        if (bad[t] != SIZE_MAX) throw EngineError(JG_ETYPE, "committed state of the wrong CRDT type for its key");
     phase_s_[1] = wall_s() - t0;
 
-    // Phase 2 (parallel, read-only on the interning): decode PNC states into the SoA batch.  A
-    // state naming a replica this row has not seen yet is deferred to phase 3, which appends
-    // columns in commit order (first-insertion order, as the stable Dictionary would).
-    std::vector<size_t> base(T + 1, 0);
-    for (int t = 0; t < T; ++t) base[t + 1] = base[t] + pnc_count[t];
-    const size_t n_pnc = base[T];
-    const int64_t absent = eb_ == 4 ? (int64_t)std::numeric_limits<int32_t>::min() : std::numeric_limits<int64_t>::min();
-    std::unique_ptr<uint32_t[]> rows(new uint32_t[n_pnc ? n_pnc : 1]);
-    std::unique_ptr<char[]> Pb(new char[(n_pnc ? n_pnc : 1) * R_ * eb_]), Nb(new char[(n_pnc ? n_pnc : 1) * R_ * eb_]);
-    std::vector<std::vector<std::pair<size_t, size_t>>> deferred(T);  // (message, batch position)
-    auto put = [&](char* buf, size_t at, int64_t v) {
-        if (eb_ == 4) reinterpret_cast<int32_t*>(buf)[at] = (int32_t)v;
-        else reinterpret_cast<int64_t*>(buf)[at] = v;
-    };
+    // Phase 2 (parallel): gather the PN-Counter payloads, in commit order, into pinned staging:
+    // [bytes | pad to 16 | off (n_pnc+1) u64 | rows u32 | commit index u64].
+    std::vector<size_t> mbase(T + 1, 0), bbase(T + 1, 0);
+    for (int t = 0; t < T; ++t) { mbase[t + 1] = mbase[t] + pnc_count[t]; bbase[t + 1] = bbase[t] + pnc_bytes[t]; }
+    const size_t n_pnc = mbase[T], nb = bbase[T];
+    const size_t nb_pad = (nb + 15) & ~size_t(15);
+    char* st = staging(nb_pad + (n_pnc + 1) * 8 + n_pnc * 4 + n_pnc * 8 + 64);
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(st);
+    uint64_t* off = reinterpret_cast<uint64_t*>(st + nb_pad);
+    uint32_t* rows = reinterpret_cast<uint32_t*>(off + n_pnc + 1);
+    uint64_t* where = reinterpret_cast<uint64_t*>(st + nb_pad + (n_pnc + 1) * 8 + ((n_pnc * 4 + 7) & ~size_t(7)));
     parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
-        size_t p = base[t];
+        size_t m = mbase[t];
+        uint64_t o = bbase[t];
         for (size_t i = b; i < e; ++i) {
-            if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);  // software pipeline over the pointer chase
-            if (i + 8 < e && cls[i + 8] < kBadType) {
-                __builtin_prefetch(&cols_[(size_t)cls[i + 8] * R_]);
-                __builtin_prefetch(msgs[i + 8]->pnc.pVector.data());
-                __builtin_prefetch(msgs[i + 8]->pnc.nVector.data());
-            }
-            const uint32_t row = cls[i];
-            if (row >= kBadType) continue;
-            const NetworkProtocol& u = *msgs[i];
-            rows[p] = row;
-            for (uint32_t c = 0; c < R_; ++c) { put(Pb.get(), p * R_ + c, absent); put(Nb.get(), p * R_ + c, absent); }
-            bool miss = false;
-            uint32_t j = 0;
-            for (const auto& en : u.pnc.pVector) {
-                const uint32_t c = find_column(row, en.first, j++);
-                if (c == UINT32_MAX) { miss = true; break; }
-                put(Pb.get(), p * R_ + c, en.second);
-            }
-            j = 0;
-            for (const auto& en : u.pnc.nVector) {
-                if (miss) break;
-                const uint32_t c = find_column(row, en.first, j++);
-                if (c == UINT32_MAX) { miss = true; break; }
-                put(Nb.get(), p * R_ + c, en.second);
-            }
-            if (miss) deferred[t].emplace_back(i, p);
-            ++p;
+            if (i + 8 < e) __builtin_prefetch(msgs[i + 8]->message.data());
+            if (cls[i] >= kSet) continue;
+            const std::string& p = msgs[i]->message;
+            std::memcpy(bytes + o, p.data(), p.size());
+            off[m] = o;
+            rows[m] = cls[i];
+            where[m] = i;
+            o += p.size();
+            ++m;
         }
     });
+    off[n_pnc] = nb;
     phase_s_[2] = wall_s() - t0;
-    // Phase 3 (commit order within each row): states that introduce replicas.  Column order only
-    // matters per row, so rows are dealt to workers by row % T and every worker walks the deferred
-    // states in commit order, handling its own rows.
-    std::vector<std::pair<size_t, size_t>> dlist;
-    for (int t = 0; t < T; ++t) dlist.insert(dlist.end(), deferred[t].begin(), deferred[t].end());
-    const int T3 = dlist.size() < 4096 ? 1 : T;
-    std::vector<uint8_t> full(T3, 0);
-    auto run3 = [&](int w) {
-        for (const auto& [i, p] : dlist) {
-            const uint32_t row = cls[i];
-            if ((int)(row % (uint32_t)T3) != w) continue;
-            const NetworkProtocol& u = *msgs[i];
-            uint32_t j = 0;
-            for (const auto& en : u.pnc.pVector) {
-                const uint32_t c = column_nothrow(row, en.first, j++);
-                if (c == UINT32_MAX) { full[w] = 1; return; }
-                put(Pb.get(), p * R_ + c, en.second);
-            }
-            j = 0;
-            for (const auto& en : u.pnc.nVector) {
-                const uint32_t c = column_nothrow(row, en.first, j++);
-                if (c == UINT32_MAX) { full[w] = 1; return; }
-                put(Nb.get(), p * R_ + c, en.second);
-            }
-        }
-    };
-    if (T3 == 1) run3(0);
-    else {
-        std::vector<std::thread> pool;
-        for (int w = 1; w < T3; ++w) pool.emplace_back(run3, w);
-        run3(0);
-        for (auto& th : pool) th.join();
-    }
-    for (uint8_t f : full)
-        if (f) throw EngineError(JG_ESTATE, "PNCounter key holds more replicas than the store's columns");
 
+    // Phase 3: OR-Set payloads, decoded in parallel; the first rejected one (commit order) cuts the wave.
+    std::vector<size_t> set_msgs;
+    for (size_t i = 0; i < n; ++i)
+        if (cls[i] == kSet) set_msgs.push_back(i);
+    std::vector<ORSetState> decoded(set_msgs.size());
+    std::vector<size_t> first_bad(T, SIZE_MAX);
+    std::vector<std::string> why(T);
+    parallel_ranges(set_msgs.size(), T, [&](size_t b, size_t e, int t) {
+        for (size_t j = b; j < e; ++j) {
+            try {
+                decoded[j] = wire::DecodeORSetMsg(msgs[set_msgs[j]]->message);
+                for (const auto& el : decoded[j].addSet)
+                    if (el.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
+            } catch (const EngineError& err) {
+                if (first_bad[t] == SIZE_MAX) { first_bad[t] = set_msgs[j]; why[t] = err.what(); }
+                return;
+            }
+        }
+    });
+    size_t cut = n;
+    int cut_code = JG_OK;
+    std::string cut_why;
+    for (int t = 0; t < T; ++t)
+        if (first_bad[t] < cut) { cut = first_bad[t]; cut_why = why[t]; cut_code = JG_EINVAL; }
     phase_s_[3] = wall_s() - t0;
-    // OR-Set states and the safe-update tracker, serial in commit order.
+
+    const double t1 = wall_s();
+    // PN-Counter wave: one engine call over the messages before the cut (the prefix is re-submitted
+    // if the engine rejects one of them: its calls are all or nothing, the reference's loop is not).
+    size_t n_submit = n_pnc;
+    while (n_submit && where[n_submit - 1] >= cut) --n_submit;
+    if (n_submit) {
+        uint64_t bad = UINT64_MAX;
+        // off[m] = start of message m = end of message m - 1: any prefix of off[] is well formed
+        const int rc = jg_pnc_merge_json(pnc_, n_submit, rows, off, bytes, &bad);
+        if (rc != JG_OK) {
+            if (bad == UINT64_MAX) check(rc);
+            cut = where[bad];
+            cut_code = rc;
+            cut_why = last_error();
+            if (bad) check(jg_pnc_merge_json(pnc_, bad, rows, off, bytes, nullptr));
+        }
+    }
+    pnc_bytes_ = n_submit ? off[n_submit] : 0;
+
+    // OR-Set states before the cut: element interning in commit order, then one merge.
     std::vector<jg_tagrec> adds, rems;
-    std::vector<uint64_t> completed;
-    for (size_t i = 0; i < n; ++i) {
-        if (cls[i] == kSkip) continue;
-        const NetworkProtocol& u = *msgs[i];
-        if (cls[i] == kSet) {
-            const KeyRef* kr = uids_.find(u.uid);
-            SetKey& s = sets_[kr->idx];
-            const uint64_t hi = (uint64_t)kr->idx << 32;
-            for (const auto& e : u.orset.addSet) {
-                if (e.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
-                const uint64_t key = hi | elem_id(s, e.first, true);
-                for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
-            }
-            for (const auto& e : u.orset.removeSet) {
-                const uint64_t key = hi | elem_id(s, e.first, true);
-                for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
-            }
-            for (const auto& g : u.orset.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
-            for (const auto& g : u.orset.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+    for (size_t j = 0; j < set_msgs.size() && set_msgs[j] < cut; ++j) {
+        const KeyRef* kr = uids_.find(msgs[set_msgs[j]]->uid);
+        SetKey& s = sets_[kr->idx];
+        const uint64_t hi = (uint64_t)kr->idx << 32;
+        const ORSetState& d = decoded[j];
+        for (const auto& e : d.addSet) {
+            const uint64_t key = hi | elem_id(s, e.first, true);
+            for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
         }
-        if (tracker) {
-            auto tr = tracker->find(u.seq);
-            if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
+        for (const auto& e : d.removeSet) {
+            const uint64_t key = hi | elem_id(s, e.first, true);
+            for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
         }
+        for (const auto& g : d.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+        for (const auto& g : d.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
     }
     if (!adds.empty() || !rems.empty()) {
         sort_unique(adds);
         sort_unique(rems);
+        check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
     }
-    const double t1 = wall_s();
-    if (n_pnc) check(jg_pnc_merge_rows(pnc_, rows.get(), n_pnc, Pb.get(), Nb.get()));
-    if (!adds.empty() || !rems.empty()) check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
+    std::vector<uint64_t> completed;
+    if (tracker)
+        for (size_t i = 0; i < cut; ++i) {
+            if (cls[i] == kSkip) continue;
+            auto tr = tracker->find(msgs[i]->seq);
+            if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
+        }
     host_s_ = t1 - t0;
     engine_s_ = wall_s() - t1;
+    if (cut < n) throw ApplyError(cut_code, cut_why, cut, std::move(completed));
     return completed;
 }
 

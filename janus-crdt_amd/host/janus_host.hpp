@@ -9,9 +9,14 @@
 //   SafeCRDT.ApplyUpdateStable / QueryStable    (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:64-83)
 //   PNCounterWrapper.Query / ORSetWrapper.Query (PNCounterWrapper.cs:28, ORSetWrapper.cs:24-28)
 //
-// Interning: key uid -> row; per-key replica Guid -> column in first-insertion
+// Interning: key uid -> row (here); per-key replica Guid -> column in first-insertion
 // order (= the stable Dictionary's enumeration order, so PNCounter.Get's checked Sum sees the same
-// prefix order); per-set element string -> elem id (null -> JG_NULL_ELEM).
+// prefix order) in the engine's device replica table (csrc/json.hip); per-set element string -> elem
+// id (null -> JG_NULL_ELEM) here.
+//
+// Committed states arrive as the reference ships them: NetworkProtocol.message = the encoded
+// PropagationMessage bytes (System.Text.Json, SafeCRDT.cs:49).  PN-Counter payloads go to the GPU
+// undecoded (jg_pnc_merge_json); OR-Set payloads are decoded here (wire.hpp) and merged as records.
 #pragma once
 
 #include <cstdint>
@@ -41,25 +46,21 @@ struct GuidHash {
 
 enum class CrdtType { PNCounter, ORSet };
 
-// Decoded PNCounterMsg (PNCounters.cs:13-50): entries in the message's dictionary order.
-struct PNCounterState {
-    std::vector<std::pair<Guid, int64_t>> pVector, nVector;
-};
 // Decoded ORSetMsg<string?> (ORSet.cs:15-70).
 struct ORSetState {
     std::vector<std::pair<std::string, std::vector<Guid>>> addSet, removeSet;
     std::vector<Guid> nullAddGuid, nullRemoveGuid;
 };
 
-// NetworkProtocol (MergeSharp/MergeSharp/proto/SyncProtocol.cs:12-62), message already decoded.
+// NetworkProtocol (MergeSharp/MergeSharp/proto/SyncProtocol.cs:12-62): uid, type, and the encoded
+// state (`byte[] message`); the CRDT type of the payload is the type registered for uid (the stable
+// copy decodes it with its own DecodePropagationMessage, SafeCRDT.cs:80-83).
 struct NetworkProtocol {
     enum SyncMsgType { ManagerMsg_Create = 0, CRDTMsg = 1 };
     Guid uid;
     SyncMsgType syncMsgType = CRDTMsg;
     uint64_t seq = 0;  // identity of the message object for the safe-update tracker
-    CrdtType type = CrdtType::PNCounter;
-    PNCounterState pnc;
-    ORSetState orset;
+    std::string message;
 };
 struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
     std::vector<NetworkProtocol> update;
@@ -68,6 +69,16 @@ struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
 struct EngineError : std::runtime_error {
     int code;
     EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// ApplyCommitted stopped at a state its CRDT rejects (JsonException in the reference, whose apply
+// Task faults there): every message before `commit_index` was applied and `completed` holds their
+// safe-update notifications; nothing at or after it was.
+struct ApplyError : EngineError {
+    uint64_t commit_index;
+    std::vector<uint64_t> completed;
+    ApplyError(int c, const std::string& m, uint64_t at, std::vector<uint64_t> done)
+        : EngineError(c, m), commit_index(at), completed(std::move(done)) {}
 };
 
 // One client operation for PNCounterWrapper.Update / ORSetWrapper.Update
@@ -93,10 +104,11 @@ class GpuStableStore {
     void CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid = Guid{});
 
     // HandleAfterConsensusUpdates: walk the committed wave in order, skip ManagerMsg_Create and
-    // Guid.Empty (:133-134) and unknown uids (:136), decode every state into one SoA batch per CRDT
-    // type, apply each batch with ONE engine call, then report the safe updates that completed, in
-    // commit order (:141-142).  `tracker` maps message seq -> client origin; matched entries are
-    // removed like ConcurrentDictionary.TryRemove.
+    // Guid.Empty (:133-134) and unknown uids (:136), gather the PN-Counter payloads into one pinned
+    // staging buffer for ONE jg_pnc_merge_json, decode the OR-Set payloads into one record batch for
+    // ONE jg_orset_merge, then report the safe updates that completed, in commit order (:141-142).
+    // `tracker` maps message seq -> client origin; matched entries are removed like
+    // ConcurrentDictionary.TryRemove.  A rejected payload throws ApplyError after applying the prefix.
     std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                          std::unordered_map<uint64_t, uint64_t>* tracker = nullptr);
 
@@ -112,12 +124,15 @@ class GpuStableStore {
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
 
     jg_ctx* ctx() const { return ctx_; }
-    static int host_threads();  // decode workers: JANUS_HOST_THREADS, else min(16, hardware threads)
-    // Wall time of the last ApplyCommitted: host decode/interning (multi-threaded over the wave's
-    // messages, JANUS_HOST_THREADS) vs the engine calls (incl. H2D).
+    jg_pnc* pnc() const { return pnc_; }
+    uint32_t pnc_row(const Guid& uid) const { return ref(uid, CrdtType::PNCounter).idx; }
+    static int host_threads();  // host workers: JANUS_HOST_THREADS, else min(16, hardware threads)
+    // Wall time of the last ApplyCommitted: host work (classify, gather into pinned staging, OR-Set
+    // decode; JANUS_HOST_THREADS workers) vs the engine calls (H2D + kernels).
     double last_apply_host_s() const { return host_s_; }
     double last_apply_engine_s() const { return engine_s_; }
-    // Cumulative host time at the end of: flatten, classify, parallel decode, deferred columns.
+    uint64_t last_apply_pnc_bytes() const { return pnc_bytes_; }
+    // Cumulative host time at the end of: flatten, classify, gather, OR-Set decode.
     const double* last_apply_phases_s() const { return phase_s_; }
 
   private:
@@ -141,14 +156,11 @@ class GpuStableStore {
         size_t n_ = 0;
     };
     struct SetKey { std::unordered_map<std::string, uint32_t> elems; };
-    // Column of replica g in PNC row `row`; `hint` = its position in the message (messages list
-    // replicas in the sender's insertion order, which usually equals ours).  Appends new replicas.
-    uint32_t column(uint32_t row, const Guid& g, uint32_t hint);
-    uint32_t column_nothrow(uint32_t row, const Guid& g, uint32_t hint);  // UINT32_MAX if the row is full
-    uint32_t find_column(uint32_t row, const Guid& g, uint32_t hint) const;  // UINT32_MAX if new
     uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
+    void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
+    char* staging(size_t bytes);            // pinned host buffer (jg_host_alloc), grown on demand
 
     jg_ctx* ctx_ = nullptr;
     jg_pnc* pnc_ = nullptr;
@@ -156,9 +168,12 @@ class GpuStableStore {
     uint32_t max_keys_, R_, eb_;
     uint32_t next_row_ = 0, next_set_ = 0;
     double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0};
+    uint64_t pnc_bytes_ = 0;
     UidTable uids_;
-    std::vector<uint32_t> ncols_;  // per PNC row: replica columns in use
-    std::vector<Guid> cols_;       // per PNC row: R replica Guids, in first-insertion order
+    std::vector<uint32_t> reg_rows_;        // CreateSafeCRDT registrations not yet sent
+    std::vector<jg_guid> reg_guids_;
+    char* stage_ = nullptr;
+    size_t stage_bytes_ = 0;
     std::vector<SetKey> sets_;
 };
 

@@ -17,7 +17,9 @@
 #include <memory>
 
 #include "janus_host.hpp"
+#include "json.hpp"
 #include "oracle.hpp"
+#include "wire.hpp"
 
 namespace {
 
@@ -29,25 +31,7 @@ janus::NetworkProtocol convert(const oracle::NetworkProtocol& np) {
     o.syncMsgType = np.syncMsgType == oracle::NetworkProtocol::ManagerMsg_Create ? janus::NetworkProtocol::ManagerMsg_Create
                                                                                   : janus::NetworkProtocol::CRDTMsg;
     o.seq = np.seq;
-    if (np.message.type == oracle::CrdtType::PNCounter) {
-        o.type = janus::CrdtType::PNCounter;
-        for (const auto& e : np.message.pnc.pVector) o.pnc.pVector.emplace_back(G(e.first), e.second);
-        for (const auto& e : np.message.pnc.nVector) o.pnc.nVector.emplace_back(G(e.first), e.second);
-    } else {
-        o.type = janus::CrdtType::ORSet;
-        for (const auto& e : np.message.orset.addSet) {
-            std::vector<janus::Guid> tags;
-            for (const auto& g : e.second) tags.push_back(G(g));
-            o.orset.addSet.emplace_back(e.first, std::move(tags));
-        }
-        for (const auto& e : np.message.orset.removeSet) {
-            std::vector<janus::Guid> tags;
-            for (const auto& g : e.second) tags.push_back(G(g));
-            o.orset.removeSet.emplace_back(e.first, std::move(tags));
-        }
-        for (const auto& g : np.message.orset.nullAddGuid) o.orset.nullAddGuid.push_back(G(g));
-        for (const auto& g : np.message.orset.nullRemoveGuid) o.orset.nullRemoveGuid.push_back(G(g));
-    }
+    o.message = np.bytes;  // the encoded state, exactly what the reference ships (SafeCRDT.cs:49)
     return o;
 }
 
@@ -205,6 +189,107 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     return 0;
 }
 
+// The host writer / reader (janus-crdt_amd/host/wire.cpp) against the oracle's restatement.
+int codec_cross_check() {
+    oracle::GuidGen gen(99);
+    for (int k = 0; k < 200; ++k) {
+        oracle::PNCounterMsg<int32_t> m;
+        std::vector<janus::Guid> g;
+        std::vector<int64_t> p, q;
+        for (int j = 0; j < k % 9; ++j) {
+            const oracle::Guid x = gen.next();
+            const int32_t a = (int32_t)(gen.next().lo), b = (int32_t)(gen.next().hi);
+            m.pVector[x] = a; m.nVector[x] = b;
+            g.push_back(G(x)); p.push_back(a); q.push_back(b);
+        }
+        std::string mine;
+        janus::wire::AppendPNCounterMsg(mine, g.data(), p.data(), q.data(), g.size());
+        if (mine != oracle::json::EncodePNC(m)) { std::printf("FAIL PNCounterMsg writer differs: %s\n", mine.c_str()); return 1; }
+    }
+    const char* names[] = {"a", "b<&>", "caf\xC3\xA9", "\xF0\x9F\x98\x80x", "q\"\\", "\t\x01"};
+    for (int k = 0; k < 50; ++k) {
+        oracle::ORSet s;
+        for (int j = 0; j < 12; ++j) {
+            const int e = (int)(gen.next().lo % 7);
+            const oracle::Elem el = e == 6 ? oracle::Elem() : oracle::Elem(names[e]);
+            if (gen.next().lo % 3) s.Add(el, gen); else s.Remove(el);
+        }
+        const oracle::ORSetMsg om = s.GetLastSynchronizedUpdate();
+        const std::string enc = oracle::json::EncodeORSet(om);
+        janus::ORSetState d = janus::wire::DecodeORSetMsg(enc);
+        if (janus::wire::EncodeORSetMsg(d) != enc) { std::printf("FAIL ORSetMsg round trip differs: %s\n", enc.c_str()); return 1; }
+    }
+    for (const char* bad : {"{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[]}", "{\"addSet\":{\"a\":[],\"a\":[]},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}",
+                            "{\"addSet\":null,\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"}) {
+        bool threw = false;
+        try { janus::wire::DecodeORSetMsg(bad); } catch (const janus::EngineError& e) { threw = e.code == JG_EINVAL; }
+        bool othrew = false;
+        try { oracle::json::DecodeORSet(bad); } catch (const oracle::json::JsonException&) { othrew = true; }
+        if (!threw || !othrew) { std::printf("FAIL ORSetMsg reader accepted %s\n", bad); return 1; }
+    }
+    return 0;
+}
+
+// A committed wave holding a payload the stable copy's Decode rejects: the reference's loop applies
+// everything before it and stops there (its Task faults); the host mirror must do the same.
+int bad_wave() {
+    oracle::SafeCRDTManager node(1, 5);
+    janus::GpuStableStore gpu(0, 8, 6, 4);
+    std::vector<oracle::SafeCRDT*> keys;
+    for (int k = 0; k < 4; ++k) {
+        oracle::SafeCRDT& sc = node.CreateSafeCRDT("k" + std::to_string(k), k < 2 ? oracle::CrdtType::PNCounter : oracle::CrdtType::ORSet);
+        gpu.CreateSafeCRDT(G(sc.guid), k < 2 ? janus::CrdtType::PNCounter : janus::CrdtType::ORSet,
+                           k < 2 ? G(sc.pncStable->pnc.replicaIdx()) : janus::Guid{});
+        keys.push_back(&sc);
+    }
+    for (int bad_at : {3, 6, 9}) {
+        node.submitted.clear();
+        for (int i = 0; i < 12; ++i) {
+            oracle::SafeCRDT& sc = *keys[i % 4];
+            if (i % 4 < 2) sc.Update(1, {oracle::Arg::I(i + 1)}, true, 100 + i);
+            else sc.Update(1, {oracle::Arg::S(std::to_string(i))}, true, 100 + i);
+        }
+        std::vector<std::vector<oracle::UpdateMessage>> wave{node.submitted};
+        int seen = 0;
+        for (auto& um : wave[0])
+            for (auto& np : um.update)
+                if (seen++ == bad_at) np.bytes = bad_at == 9 ? "{\"pVector\":{}}" : "{\"addSet\":null}";
+        std::unordered_map<uint64_t, uint64_t> tracker(node.safeUpdateTracker.begin(), node.safeUpdateTracker.end());
+        const size_t before = node.notified.size();
+        bool othrew = false;
+        try { node.HandleAfterConsensusUpdates(wave); } catch (const oracle::json::JsonException&) { othrew = true; }
+        std::vector<std::vector<janus::UpdateMessage>> jw(1);
+        for (const auto& um : wave[0]) {
+            janus::UpdateMessage m;
+            for (const auto& np : um.update) m.update.push_back(convert(np));
+            jw[0].push_back(std::move(m));
+        }
+        std::vector<uint64_t> done;
+        uint64_t at = UINT64_MAX;
+        try { done = gpu.ApplyCommitted(jw, &tracker); } catch (const janus::ApplyError& e) { done = e.completed; at = e.commit_index; }
+        std::vector<uint64_t> exp(node.notified.begin() + before, node.notified.end());
+        if (!othrew || at != (uint64_t)bad_at || done != exp) {
+            std::printf("FAIL bad wave at %d: oracle threw %d, gpu stopped at %lld, %zu vs %zu completions\n", bad_at, othrew, (long long)at,
+                        done.size(), exp.size());
+            return 1;
+        }
+        for (auto* sc : keys) {
+            if (sc->type == oracle::CrdtType::PNCounter) {
+                if (sc->QueryStable().i != gpu.QueryStablePNC(G(sc->guid))) { std::printf("FAIL bad wave value\n"); return 1; }
+            } else {
+                for (int e = 0; e < 12; ++e) {
+                    const std::string el = std::to_string(e);
+                    if (sc->QueryStable({oracle::Arg::S(el)}).b != gpu.QueryStableORSet(G(sc->guid), el)) { std::printf("FAIL bad wave set\n"); return 1; }
+                }
+            }
+        }
+        // keep the oracle and the GPU in step for the next round: the reference node's tracker keeps
+        // the entries of messages it never applied; so does ours.
+        node.safeUpdateTracker = std::unordered_map<uint64_t, uint64_t>(tracker.begin(), tracker.end());
+    }
+    return 0;
+}
+
 }  // namespace
 
 int main() {
@@ -220,6 +305,15 @@ int main() {
         {4, 10, 0, 1500, 50, 4, 8, "3"},   // long (int64) PN-Counter variant
     };
     int fails = 0;
+    {
+        const int rc = codec_cross_check();
+        std::printf("%s codec cross-check (host writer/reader vs oracle/json.hpp)\n", rc ? "FAIL" : "PASS");
+        fails += rc != 0;
+        int rb = 1;
+        try { rb = bad_wave(); } catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
+        std::printf("%s bad-payload wave (prefix applied, ApplyError at the rejected message)\n", rb ? "FAIL" : "PASS");
+        fails += rb != 0;
+    }
     for (const auto& c : cases) {
         setenv("JANUS_HOST_THREADS", c.threads, 1);
         int rc = 1;

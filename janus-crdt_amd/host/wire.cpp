@@ -1,0 +1,308 @@
+// wire.cpp — see wire.hpp.
+#include "wire.hpp"
+
+#include <cstring>
+#include <unordered_set>
+
+namespace janus::wire {
+
+namespace {
+
+constexpr char kHex[] = "0123456789abcdef";
+
+inline void put_byte_hex(char* d, uint8_t b) {
+    d[0] = kHex[b >> 4];
+    d[1] = kHex[b & 15];
+}
+
+inline int hex_digit(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    const char l = (char)(c | 0x20);
+    return (l >= 'a' && l <= 'f') ? l - 'a' + 10 : -1;
+}
+
+[[noreturn]] void reject(const char* why, size_t at) {
+    throw EngineError(JG_EINVAL, std::string("JsonException: ") + why + " at byte " + std::to_string(at));
+}
+
+// Cursor over one payload; each method consumes one JSON token (with leading whitespace).
+struct Scan {
+    std::string_view s;
+    size_t i = 0;
+    void skip_ws() {
+        while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) ++i;
+    }
+    bool at(char c) {
+        skip_ws();
+        return i < s.size() && s[i] == c;
+    }
+    void need(char c) {
+        if (!at(c)) reject("unexpected token", i);
+        ++i;
+    }
+    bool take(char c) {
+        if (!at(c)) return false;
+        ++i;
+        return true;
+    }
+    bool take_null() {
+        skip_ws();
+        if (s.compare(i, 4, "null") == 0) { i += 4; return true; }
+        return false;
+    }
+    uint32_t hex4() {
+        if (i + 4 > s.size()) reject("bad \\u escape", i);
+        uint32_t u = 0;
+        for (int k = 0; k < 4; ++k) {
+            const int h = hex_digit(s[i++]);
+            if (h < 0) reject("bad \\u escape", i);
+            u = u << 4 | (uint32_t)h;
+        }
+        return u;
+    }
+    static void utf8(std::string& o, uint32_t u) {
+        if (u < 0x80) { o += (char)u; return; }
+        if (u < 0x800) { o += (char)(0xC0 | u >> 6); o += (char)(0x80 | (u & 0x3F)); return; }
+        if (u < 0x10000) { o += (char)(0xE0 | u >> 12); o += (char)(0x80 | (u >> 6 & 0x3F)); o += (char)(0x80 | (u & 0x3F)); return; }
+        o += (char)(0xF0 | u >> 18); o += (char)(0x80 | (u >> 12 & 0x3F)); o += (char)(0x80 | (u >> 6 & 0x3F)); o += (char)(0x80 | (u & 0x3F));
+    }
+    // JSON string -> UTF-8 (escapes decoded, surrogate pairs joined, raw UTF-8 validated).
+    std::string str() {
+        need('"');
+        std::string o;
+        while (true) {
+            if (i >= s.size()) reject("unterminated string", i);
+            const unsigned char c = (unsigned char)s[i++];
+            if (c == '"') return o;
+            if (c < 0x20) reject("control character in string", i);
+            if (c == '\\') {
+                if (i >= s.size()) reject("bad escape", i);
+                const char e = s[i++];
+                const char* simple = std::strchr("\"\\/bfnrt", e);
+                if (e && simple) {
+                    static const char out[] = "\"\\/\b\f\n\r\t";
+                    o += out[simple - "\"\\/bfnrt"];
+                    continue;
+                }
+                if (e != 'u') reject("bad escape", i);
+                uint32_t u = hex4();
+                if (u >= 0xDC00 && u <= 0xDFFF) reject("lone low surrogate", i);
+                if (u >= 0xD800 && u <= 0xDBFF) {
+                    if (i + 2 > s.size() || s[i] != '\\' || s[i + 1] != 'u') reject("lone high surrogate", i);
+                    i += 2;
+                    const uint32_t lo = hex4();
+                    if (lo < 0xDC00 || lo > 0xDFFF) reject("bad surrogate pair", i);
+                    u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
+                }
+                utf8(o, u);
+                continue;
+            }
+            if (c < 0x80) { o += (char)c; continue; }
+            int extra;
+            uint32_t cp;
+            if (c >= 0xC2 && c <= 0xDF) { extra = 1; cp = c & 0x1F; }
+            else if (c >= 0xE0 && c <= 0xEF) { extra = 2; cp = c & 0x0F; }
+            else if (c >= 0xF0 && c <= 0xF4) { extra = 3; cp = c & 0x07; }
+            else reject("invalid UTF-8", i);
+            if (i + extra > s.size()) reject("invalid UTF-8", i);
+            for (int k = 0; k < extra; ++k) {
+                const unsigned char cc = (unsigned char)s[i + k];
+                if ((cc & 0xC0) != 0x80) reject("invalid UTF-8", i);
+                cp = cp << 6 | (cc & 0x3F);
+            }
+            const bool bad = (extra == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (extra == 3 && (cp < 0x10000 || cp > 0x10FFFF));
+            if (bad) reject("invalid UTF-8", i);
+            o.append(s.data() + i - 1, (size_t)extra + 1);
+            i += extra;
+        }
+    }
+    Guid guid() {
+        const size_t at = i;
+        Guid g;
+        if (!ParseGuidD(str(), g)) reject("not a Guid", at);
+        return g;
+    }
+    void guids(std::vector<Guid>& out) {
+        need('[');
+        if (!at(']')) {
+            do out.push_back(guid());
+            while (take(','));
+        }
+        need(']');
+    }
+};
+
+// JavaScriptEncoder.Default for a UTF-8 element string.
+void escape(std::string& o, const std::string& s) {
+    static const char HX[] = "0123456789ABCDEF";
+    auto unit = [&](uint32_t u) {
+        const char e[6] = {'\\', 'u', HX[u >> 12 & 15], HX[u >> 8 & 15], HX[u >> 4 & 15], HX[u & 15]};
+        o.append(e, 6);
+    };
+    size_t i = 0;
+    while (i < s.size()) {
+        const unsigned char c = (unsigned char)s[i];
+        if (c >= 0x80) {
+            const int n = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+            uint32_t cp = c & (n == 4 ? 0x07 : n == 3 ? 0x0F : 0x1F);
+            for (int k = 1; k < n; ++k) cp = cp << 6 | ((unsigned char)s[i + k] & 0x3F);
+            i += n;
+            if (cp >= 0x10000) {
+                unit(0xD800 | (cp - 0x10000) >> 10);
+                unit(0xDC00 | ((cp - 0x10000) & 0x3FF));
+            } else {
+                unit(cp);
+            }
+            continue;
+        }
+        ++i;
+        if (c == '\\') o += "\\\\";
+        else if (c == '\b') o += "\\b";
+        else if (c == '\t') o += "\\t";
+        else if (c == '\n') o += "\\n";
+        else if (c == '\f') o += "\\f";
+        else if (c == '\r') o += "\\r";
+        else if (c < 0x20 || c == 0x7F || std::strchr("\"&'+<>`", (char)c)) unit(c);
+        else o += (char)c;
+    }
+}
+
+void put_tags(std::string& o, const std::vector<Guid>& v) {
+    o += '[';
+    for (size_t k = 0; k < v.size(); ++k) {
+        if (k) o += ',';
+        o += '"';
+        AppendGuidD(o, v[k]);
+        o += '"';
+    }
+    o += ']';
+}
+
+void put_map(std::string& o, const std::vector<std::pair<std::string, std::vector<Guid>>>& m) {
+    o += '{';
+    for (size_t k = 0; k < m.size(); ++k) {
+        if (k) o += ',';
+        o += '"';
+        escape(o, m[k].first);
+        o += "\":";
+        put_tags(o, m[k].second);
+    }
+    o += '}';
+}
+
+}  // namespace
+
+void AppendGuidD(std::string& out, const Guid& g) {
+    // text order of the 16 bytes: b3 b2 b1 b0 - b5 b4 - b7 b6 - b8 b9 - b10..b15
+    char d[36];
+    const uint64_t lo = g.lo, hi = g.hi;
+    static const int lo_order[8] = {3, 2, 1, 0, 5, 4, 7, 6};
+    int p = 0;
+    for (int k = 0; k < 8; ++k) {
+        if (k == 4 || k == 6) d[p++] = '-';
+        put_byte_hex(d + p, (uint8_t)(lo >> (8 * lo_order[k])));
+        p += 2;
+    }
+    for (int k = 0; k < 8; ++k) {
+        if (k == 0 || k == 2) d[p++] = '-';
+        put_byte_hex(d + p, (uint8_t)(hi >> (8 * k)));
+        p += 2;
+    }
+    out.append(d, 36);
+}
+
+bool ParseGuidD(std::string_view s, Guid& g) {
+    if (s.size() != 36 || s[8] != '-' || s[13] != '-' || s[18] != '-' || s[23] != '-') return false;
+    static const int lo_order[8] = {3, 2, 1, 0, 5, 4, 7, 6};
+    static const int pos[16] = {0, 2, 4, 6, 9, 11, 14, 16, 19, 21, 24, 26, 28, 30, 32, 34};
+    uint64_t lo = 0, hi = 0;
+    for (int k = 0; k < 16; ++k) {
+        const int a = hex_digit(s[pos[k]]), b = hex_digit(s[pos[k] + 1]);
+        if (a < 0 || b < 0) return false;
+        const uint64_t byte = (uint64_t)(a << 4 | b);
+        if (k < 8) lo |= byte << (8 * lo_order[k]);
+        else hi |= byte << (8 * (k - 8));
+    }
+    g.lo = lo;
+    g.hi = hi;
+    return true;
+}
+
+void AppendPNCounterMsg(std::string& out, const Guid* g, const int64_t* p, const int64_t* n, size_t k) {
+    char num[24];
+    for (int which = 0; which < 2; ++which) {
+        out += which ? ",\"nVector\":{" : "{\"pVector\":{";
+        const int64_t* v = which ? n : p;
+        for (size_t j = 0; j < k; ++j) {
+            if (j) out += ',';
+            out += '"';
+            AppendGuidD(out, g[j]);
+            out += "\":";
+            const int len = std::snprintf(num, sizeof num, "%lld", (long long)v[j]);
+            out.append(num, (size_t)len);
+        }
+        out += '}';
+    }
+    out += '}';
+}
+
+std::string EncodeORSetMsg(const ORSetState& m) {
+    std::string o = "{\"addSet\":";
+    put_map(o, m.addSet);
+    o += ",\"removeSet\":";
+    put_map(o, m.removeSet);
+    o += ",\"nullAddGuid\":";
+    put_tags(o, m.nullAddGuid);
+    o += ",\"nullRemoveGuid\":";
+    put_tags(o, m.nullRemoveGuid);
+    o += '}';
+    return o;
+}
+
+ORSetState DecodeORSetMsg(std::string_view bytes) {
+    Scan sc{bytes};
+    ORSetState m;
+    unsigned seen = 0;
+    sc.need('{');
+    if (!sc.at('}')) {
+        do {
+            const size_t at = sc.i;
+            const std::string name = sc.str();
+            static const char* names[4] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
+            int which = -1;
+            for (int k = 0; k < 4; ++k)
+                if (name == names[k]) which = k;
+            if (which < 0) reject("unknown property", at);
+            if (seen >> which & 1) reject("duplicate property", at);
+            seen |= 1u << which;
+            sc.need(':');
+            if (sc.take_null()) reject("null member (Merge would throw NullReferenceException)", sc.i);
+            if (which >= 2) {
+                sc.guids(which == 2 ? m.nullAddGuid : m.nullRemoveGuid);
+                continue;
+            }
+            auto& map = which == 0 ? m.addSet : m.removeSet;
+            std::unordered_set<std::string> keys;
+            sc.need('{');
+            if (!sc.at('}')) {
+                do {
+                    const size_t ek = sc.i;
+                    std::string e = sc.str();
+                    if (!keys.insert(e).second) reject("duplicate element in one map", ek);
+                    sc.need(':');
+                    if (sc.take_null()) reject("null tag set", sc.i);
+                    map.emplace_back(std::move(e), std::vector<Guid>());
+                    sc.guids(map.back().second);
+                } while (sc.take(','));
+            }
+            sc.need('}');
+        } while (sc.take(','));
+    }
+    sc.need('}');
+    sc.skip_ws();
+    if (sc.i != bytes.size()) reject("trailing data", sc.i);
+    if (seen != 15) reject("missing member (Merge would throw NullReferenceException)", sc.i);
+    return m;
+}
+
+}  // namespace janus::wire

@@ -1,0 +1,31 @@
+// wire.hpp — host side of the state-message wire format (System.Text.Json).
+//
+// PNCounterMsg payloads are decoded on the GPU (csrc/json.hip); this header holds what the host needs
+// around that: the PNCounterMsg writer (PNCounters.cs:46-49, the producer of those payloads:
+// GetLastSynchronizedUpdate().Encode() in SafeCRDT.Update, BFT-CRDT/SafeCRDTs/SafeCRDT.cs:49) and the
+// ORSetMsg<string> reader/writer (ORSet.cs:56-69), whose element strings are interned on the host.
+// The accepted decode contract is the one stated in oracle/json.hpp (the checker's restatement).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <string_view>
+
+#include "janus_host.hpp"
+
+namespace janus::wire {
+
+// Guid.ToString("D") (lower-case) of C# Guid bytes lo = b0..b7, hi = b8..b15; appends 36 chars.
+void AppendGuidD(std::string& out, const Guid& g);
+bool ParseGuidD(std::string_view s, Guid& g);
+
+// PNCounterMsg.Encode of a state whose pVector and nVector both list the k replicas g[0..k) in that
+// order with values p[i] / n[i]: {"pVector":{"<g>":p,...},"nVector":{"<g>":n,...}}.  Appends.
+void AppendPNCounterMsg(std::string& out, const Guid* g, const int64_t* p, const int64_t* n, size_t k);
+
+// ORSetMsg<string?> codec.  Decode throws EngineError(JG_EINVAL) where System.Text.Json (or the
+// narrowed contract) rejects the payload.
+std::string EncodeORSetMsg(const ORSetState& m);
+ORSetState DecodeORSetMsg(std::string_view bytes);
+
+}  // namespace janus::wire

@@ -3,6 +3,8 @@
 // BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:61-198.
 #include "oracle.hpp"
 
+#include "json.hpp"
+
 namespace oracle {
 
 SafeCRDT::SafeCRDT(Guid uid, std::string k, CrdtType t, GuidGen& g, SafeCRDTManager* m)
@@ -30,6 +32,7 @@ Result SafeCRDT::Update(int op, const std::vector<Arg>& args, bool isSafe, uint6
     syncMsg.uid = guid;
     syncMsg.syncMsgType = NetworkProtocol::CRDTMsg;
     syncMsg.message = ProspectiveState();
+    syncMsg.bytes = type == CrdtType::PNCounter ? json::EncodePNC(syncMsg.message.pnc) : json::EncodeORSet(syncMsg.message.orset);
     syncMsg.seq = sm->nextSeq++;
     if (isSafe && origin != 0) sm->safeUpdateTracker.emplace(syncMsg.seq, origin);
     sm->ActualPropagateSyncMsg(syncMsg, sm->clock_ms);
@@ -43,9 +46,16 @@ Result SafeCRDT::QueryProspective(const std::vector<Arg>& args) const {
     return type == CrdtType::PNCounter ? pncProspective->Query() : orProspective->Query(args);
 }
 
-// SafeCRDT.cs:80-83 — decode + ApplySynchronizedUpdate on the stable copy.  A message of the
-// other CRDT type is ORSet.cs:288-291's NotSupportedException (PNCounter casts: InvalidCast).
+// SafeCRDT.cs:80-83 — decode + ApplySynchronizedUpdate on the stable copy.  Encoded messages are
+// decoded with the stable copy's own codec (json::JsonException where Decode throws); a decoded
+// message of the other CRDT type is ORSet.cs:288-291's NotSupportedException (PNCounter casts:
+// InvalidCast).
 void SafeCRDT::ApplyUpdateStable(const NetworkProtocol& msg) {
+    if (!msg.bytes.empty()) {
+        if (type == CrdtType::PNCounter) pncStable->pnc.ApplySynchronizedUpdate(json::DecodePNC<int32_t>(msg.bytes));
+        else orStable->orset.ApplySynchronizedUpdate(json::DecodeORSet(msg.bytes));
+        return;
+    }
     if (msg.message.type != type) {
         if (type == CrdtType::ORSet) throw NotSupportedException("ReceivedUpdate does not support type");
         throw InvalidCastException("Specified cast is not valid.");

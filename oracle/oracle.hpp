@@ -315,7 +315,9 @@ struct StateMsg {
 struct NetworkProtocol {  // MergeSharp/MergeSharp/proto/SyncProtocol.cs:12-62
     enum SyncMsgType { ManagerMsg_Create = 0, CRDTMsg = 1 };
     Guid uid; SyncMsgType syncMsgType = CRDTMsg; uint64_t seq = 0;  // seq: object identity for the tracker
-    StateMsg message;
+    StateMsg message;   // the state, decoded (what Encode was called on)
+    std::string bytes;  // `byte[] message`: GetLastSynchronizedUpdate().Encode() (SafeCRDT.cs:49); when
+                        // set, ApplyUpdateStable decodes it with the stable copy's codec (oracle/json.hpp)
 };
 
 struct UpdateMessage { std::vector<NetworkProtocol> update; };  // DAGConsensus/DAGUpdateMessage.cs:16-55
