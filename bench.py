@@ -166,17 +166,24 @@ def _orset_traffic():
     return a[0] + r[0] if a and r else None
 
 
-def bench_pnc(jg, ctx, sync, rank, world, steps, warmup):
-    key0, n_keys = shard_keys(PNC_KEYS, rank, world)
-    store = jg.PNCStore(ctx, n_keys, PNC_R, PNC_EB)
-    rows = jg.Rows(ctx, n_keys, PNC_R, PNC_EB)
+# Per-GPU PN-Counter shard: C2 (BASELINE configs[1]) by default; "c4" = one GPU's share of
+# configs[3] (200M keys x 128 replicas over 8 GPUs = 25M x 128 per GPU, 102.4 GB resident per GPU).
+PNC_SHAPES = {"c2": (PNC_KEYS, PNC_R), "c4": (25_000_000, 128)}
+
+
+def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2"):
+    keys, R = PNC_SHAPES[shape]
+    key0, n_keys = shard_keys(keys, rank, world)
+    store = jg.PNCStore(ctx, n_keys, R, PNC_EB)
+    rows = jg.Rows(ctx, n_keys, R, PNC_EB)
     store.synth(SEED + rank)
     rows.synth(SEED + rank, key0=0)
     wall, ev = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, warmup)
     store.close()
     rows.close()
-    cells = n_keys * PNC_R
-    return {"wall_s": wall, "event_s": ev, "cells_per_rank": cells, "bytes_per_launch": cells * PNC_BYTES_PER_CELL}
+    cells = n_keys * R
+    return {"wall_s": wall, "event_s": ev, "cells_per_rank": cells, "bytes_per_launch": cells * PNC_BYTES_PER_CELL,
+            "keys": n_keys, "R": R}
 
 
 def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
@@ -195,15 +202,27 @@ def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
             "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
 
 
-def bench_apply_loop():
-    """C5 committed-batch apply through the C++ host mirror; its own JSON."""
+def bench_apply_loop(sync, rank, world, local):
+    """C5 committed-batch apply through the C++ host mirror, on every rank.  Every
+    rank applies the same committed waves to the accounts it owns (GpuStableStore::ShardOf; other
+    uids are skipped like the reference skips unknown uids), so the wave is split N ways with no
+    collective: strong scaling over a fixed 1M-account keyspace.  msgs_per_s = wave messages / the
+    slowest rank's wave time."""
     import subprocess
     exe = ROOT / "janus-crdt_amd" / "build" / "bench_apply"
-    out = subprocess.run([str(exe), "--accounts", "1000000", "--msgs", "1000000", "--waves", "2", "--cpu-msgs", "100000"],
+    cpu_msgs = "100000" if world == 1 else "0"
+    out = subprocess.run([str(exe), "--accounts", "1000000", "--msgs", "1000000", "--waves", "2", "--cpu-msgs", cpu_msgs,
+                          "--device", str(local), "--rank", str(rank), "--world", str(world)],
                          capture_output=True, text=True, timeout=240)
-    if out.returncode != 0:
-        return {"error": out.stderr[-500:]}
-    return json.loads(out.stdout.strip().splitlines()[-1])
+    ok = out.returncode == 0
+    res = json.loads(out.stdout.strip().splitlines()[-1]) if ok else {"error": out.stderr[-500:]}
+    worst_ms = sync.max(res["ms_per_wave"] if ok else float("inf"))
+    if world > 1 and ok:
+        res = {"workload": res["workload"] + f", key-space sharded x{world}", "scaling": "strong",
+               "msgs_per_s": 1_000_000 / (worst_ms / 1e3), "ms_per_wave": worst_ms,
+               "rank0": {k: res[k] for k in ("ms_per_wave", "host_ms_per_wave", "engine_ms_per_wave", "owned_accounts",
+                                               "applied_msgs_per_wave")}}
+    return res
 
 
 def cpu_baseline():
@@ -214,6 +233,10 @@ def cpu_baseline():
     model, ncpu = cpu_info()
     n_sets = 20_000
     t_or = orc.bench_orset_merge(n_sets, ORSET_E, ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV, SEED, 1, 3)
+    # the same merge split over the host cores this job may use; the box
+    # grants 16 CPUs per GPU, os.cpu_count() shows the whole machine
+    par = max(1, min(16, ncpu or 1))
+    t_par = orc.bench_pnc_merge(4 * n_keys, PNC_R, SEED, par, reps)
     return {
         "value": n_keys * PNC_R / t,
         "unit": "replica-key merges/s",
@@ -223,6 +246,8 @@ def cpu_baseline():
                   f"synthetic workload, int64, dictionary-faithful oracle (oracle/), median of {reps}, 1 thread "
                   f"(the reference's serialized apply task); host: {model}, {ncpu} logical CPUs",
         "orset_records_per_s": n_sets * ORSET_E * 2 * (ORSET_ADD + ORSET_REM) / t_or,
+        "parallel": {"value": 4 * n_keys * PNC_R / t_par, "cores": par,
+                     "sample": f"the same merge over the first {4 * n_keys} keys, keys split over {par} threads"},
     }
 
 
@@ -233,6 +258,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pnc-shape", choices=sorted(PNC_SHAPES), default="c2",
+                    help="per-GPU PN-Counter shard: c2 = BASELINE configs[1] (default), c4 = 1/8 of configs[3]")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
@@ -244,7 +271,7 @@ def main():
 
     res = {}
     if args.workload in ("all", "pnc", "pnc-orset"):
-        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup)
+        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape)
     if args.workload in ("all", "orset", "pnc-orset"):
         res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
     ctx.close()
@@ -252,7 +279,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
-    apply_loop = bench_apply_loop() if rank == 0 and world == 1 and args.workload == "all" else None
+    apply_loop = bench_apply_loop(sync, rank, world, local) if args.workload == "all" else None
     sync.close()
     if rank != 0:
         return
@@ -265,14 +292,16 @@ def main():
         step = p["wall_s"] / args.steps
         kern = p["event_s"] / args.steps
         achieved = p["bytes_per_launch"] / kern / 1e9
-        traffic = load_traffic("pnc_merge_dense")
+        traffic = load_traffic("pnc_merge_dense") if args.pnc_shape == "c2" else None  # PMC pass exists for C2 only
         line.update({
             "value": world * p["cells_per_rank"] / step,
             "unit": "replica-key merges/s",
             "ms_per_step": step * 1e3,
             "dtype": "int64",
-            "config": {"workload": "PNCounter batch merge (BASELINE configs[1]: 10M keys x 64 replicas, int64 P/N)",
-                       "keys_per_gpu": PNC_KEYS, "replicas": PNC_R, "elem_bytes": PNC_EB,
+            "config": {"workload": ("PNCounter batch merge (BASELINE configs[1]: 10M keys x 64 replicas, int64 P/N)"
+                                    if args.pnc_shape == "c2" else
+                                    "PNCounter batch merge (BASELINE configs[3] per-GPU shard: 25M keys x 128 replicas, int64 P/N)"),
+                       "keys_per_gpu": p["keys"], "replicas": p["R"], "elem_bytes": PNC_EB,
                        "parallelism": f"keyspace-sharded x{world}, no data-path collective"},
             "hbm_GBps": world * p["bytes_per_launch"] / step / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -40,7 +40,8 @@ struct Wave {
 
 int main(int argc, char** argv) {
     uint64_t accounts = 1000000, msgs = 1000000, cpu_msgs = 100000;
-    int waves = 5, nodes = 4;
+    int waves = 5, nodes = 4, device = 0;
+    uint32_t rank = 0, world = 1;
     bool normal = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--accounts") && i + 1 < argc) accounts = std::strtoull(argv[++i], nullptr, 10);
@@ -48,6 +49,9 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--cpu-msgs") && i + 1 < argc) cpu_msgs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--normal")) normal = true;
+        else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) world = (uint32_t)std::atoi(argv[++i]);
     }
     const uint32_t R = nodes + 1;  // the stable copy's own replica + one prospective replica per node
     std::mt19937_64 rng(0x4A414E5553ull);
@@ -60,11 +64,19 @@ int main(int argc, char** argv) {
         stable[k] = gen.next();
         for (int n = 0; n < nodes; ++n) rep[k * nodes + n] = gen.next();
     }
-    janus::GpuStableStore gpu(0, (uint32_t)accounts, R, 4);
+    janus::GpuStableStore gpu(device, (uint32_t)accounts, R, 4);
     auto G = [](const oracle::Guid& g) { return janus::Guid{g.lo, g.hi}; };
-    for (uint64_t k = 0; k < accounts; ++k) gpu.CreateSafeCRDT(G(uid[k]), janus::CrdtType::PNCounter, G(stable[k]));
+    // key-space shard of this rank (every rank sees the whole wave and skips the uids it does not own)
+    std::vector<uint8_t> mine(accounts);
+    uint64_t owned = 0;
+    for (uint64_t k = 0; k < accounts; ++k) {
+        mine[k] = janus::GpuStableStore::ShardOf(G(uid[k]), world) == rank;
+        if (mine[k]) { gpu.CreateSafeCRDT(G(uid[k]), janus::CrdtType::PNCounter, G(stable[k])); ++owned; }
+    }
+    uint64_t applied = 0;
     oracle::SafeCRDTManager cpu(1000, 1);
-    for (uint64_t k = 0; k < accounts; ++k) cpu.CreateSafeCRDT("acct" + std::to_string(k), oracle::CrdtType::PNCounter, uid[k]);
+    if (cpu_msgs)
+        for (uint64_t k = 0; k < accounts; ++k) cpu.CreateSafeCRDT("acct" + std::to_string(k), oracle::CrdtType::PNCounter, uid[k]);
 
     // per (account, node) counters: a node's state of an account = its own P/N plus what it merged
     std::vector<int32_t> P(accounts * nodes, 0), N(accounts * nodes, 0);
@@ -76,7 +88,7 @@ int main(int argc, char** argv) {
     };
 
     double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
-    uint64_t gpu_n = 0, cpu_n = 0, payload = 0, payload_timed = 0;
+    uint64_t gpu_n = 0, cpu_n = 0, payload = 0, payload_timed = 0, shard_bytes = 0;
     for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
         Wave wave;
         std::vector<janus::UpdateMessage> block;
@@ -101,6 +113,7 @@ int main(int argc, char** argv) {
                 janus::wire::AppendPNCounterMsg(np.message, g, pv, nv, nodes);
             }
             payload += np.message.size();
+            if (w > 0 && mine[k]) ++applied;
             if (m < cpu_msgs && w > 0) {
                 oracle::NetworkProtocol cp;
                 cp.uid = uid[k];
@@ -131,6 +144,8 @@ int main(int argc, char** argv) {
             for (int q = 0; q < 4; ++q) ph[q] += gpu.last_apply_phases_s()[q];
             gpu_n += msgs;
             payload_timed += wave_payload;
+            shard_bytes += gpu.last_apply_pnc_bytes();
+            if (!cpu_msgs) continue;
             const double c0 = now_s();
             cpu.HandleAfterConsensusUpdates(wave.cpu);
             cpu_s += now_s() - c0;
@@ -141,11 +156,13 @@ int main(int argc, char** argv) {
     std::printf("{\"workload\": \"committed-batch apply (C5 banking-shaped, %s accounts %llu, %d nodes, %llu PNCounterMsg JSON states per wave)\", "
                 "\"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"payload_bytes_per_msg\": %.1f, \"host_ms_per_wave\": %.3f, "
                 "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, \"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], "
+                "\"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
                 normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s,
-                1e3 * gpu_s / waves, bytes / gpu_n, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, bytes / engine_s / 1e9,
+                1e3 * gpu_s / waves, bytes / gpu_n, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, shard_bytes / engine_s / 1e9,
                 janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves, 1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves,
-                cpu_n / cpu_s, (unsigned long long)std::min(msgs, cpu_msgs));
+                rank, world, (unsigned long long)owned, (double)applied / waves, cpu_s > 0 ? cpu_n / cpu_s : 0.0,
+                (unsigned long long)std::min(msgs, cpu_msgs));
     return 0;
 }

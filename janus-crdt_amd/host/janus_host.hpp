@@ -123,6 +123,14 @@ class GpuStableStore {
     int64_t QueryStablePNC(const Guid& uid);
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
 
+    // Key-space sharding over `world` GPUs: the shard owning `uid`.  Every rank
+    // registers only the keys it owns and applies the same committed waves: states of keys it does
+    // not own are skipped exactly like the reference skips unknown uids (SafeCRDTManager.cs:136), so
+    // no state crosses GPUs and the data path needs no collective.
+    static uint32_t ShardOf(const Guid& uid, uint32_t world) {
+        return world <= 1 ? 0u : (uint32_t)((GuidHash()(uid) >> 7) % world);
+    }
+
     jg_ctx* ctx() const { return ctx_; }
     jg_pnc* pnc() const { return pnc_; }
     uint32_t pnc_row(const Guid& uid) const { return ref(uid, CrdtType::PNCounter).idx; }
