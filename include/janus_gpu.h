@@ -130,6 +130,16 @@ int jg_pnc_columns(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, jg_guid* re
  * = the first such message (UINT64_MAX on success).  The caller re-submits the prefix
  * [0, *bad_msg) to reproduce the reference, whose loop applies the messages before the throwing one. */
 int jg_pnc_merge_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg);
+/* The same call streamed in chunks, so the caller's gathering of chunk k+1 overlaps the upload and the
+ * decode/validation pass of chunk k: begin (capacity hints; exceeded capacity grows), append chunks
+ * in commit order (chunk offsets relative to the chunk: off[0] = 0; returns once the upload and pass A
+ * are queued — the chunk's host buffers must stay untouched until commit or abort returns), then
+ * commit (= jg_pnc_merge_json over the concatenation: all or nothing, *bad_msg indexes the whole
+ * wave) or abort (nothing applied).  One open wave per store. */
+int jg_pnc_wave_begin(jg_pnc* pnc, uint64_t cap_msgs, uint64_t cap_bytes);
+int jg_pnc_wave_append(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes);
+int jg_pnc_wave_commit(jg_pnc* pnc, uint64_t* bad_msg);
+int jg_pnc_wave_abort(jg_pnc* pnc);
 /* The same with the wave already in device memory (upload once, merge many: the bench). */
 int jg_wave_create(jg_ctx* ctx, uint64_t cap_msgs, uint64_t cap_bytes, jg_wave** out);
 int jg_wave_destroy(jg_wave* wave);

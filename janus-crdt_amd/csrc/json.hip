@@ -237,11 +237,11 @@ struct ScanVis {
 
 template <int EB>
 __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ rows, uint64_t n, Table t,
+                                                 const uint32_t* __restrict__ rows, uint64_t m0, uint64_t m1, Table t,
                                                  unsigned long long* __restrict__ status /* [0] first bad, [1] n deferred */,
                                                  unsigned long long* __restrict__ deferred) {
-    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= n) return;
+    const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= m1) return;
     const uint32_t row = rows[m];
     Cursor c(bytes, off[m], off[m + 1]);
     ScanVis vis{t.cols + (uint64_t)row * t.R, t.ncols[row]};
@@ -253,6 +253,12 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const unsigned long long at = atomicAdd(status + 1, 1ull);
         deferred[at] = (unsigned long long)row << 32 | m;
     }
+}
+
+// Chunk offsets arrive relative to their chunk: add the chunk's byte base.
+__global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) off[i] += base;
 }
 
 // Pass C visitor: exclusive owner of the row; appends new Guids.
@@ -429,44 +435,88 @@ Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     jg::fail(JG_EINVAL, "%s %llu is not a PNCounterMsg in the accepted JSON form (JsonException)", what, (unsigned long long)m);
 }
 
-// The whole device side of a wave: bytes/off/rows already on the device.
-void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad_msg) {
-    jg_ctx* ctx = p->ctx;
-    ensure_table(p);
-    const Table t = table_of(p);
-    // status words + deferred list + roll-back slots live in ctx scratch
-    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch2, 64 + n * 8 + n * 4 + 256));
-    auto* status = reinterpret_cast<unsigned long long*>(s);
-    auto* deferred = reinterpret_cast<unsigned long long*>(s + 64);
-    auto* saved = reinterpret_cast<uint32_t*>(s + 64 + n * 8);
-    const Status init{~0ull, 0, ~0ull, 0};
+// Grow a wave buffer to `need` bytes keeping the first `keep` bytes (stream-ordered copy).
+void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep) {
+    if (b.bytes >= need) return;
+    jg::DevBuf nb;
+    nb.alloc(need + need / 2);
+    if (keep) JG_HIP(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    std::swap(nb.p, b.p);
+    std::swap(nb.bytes, b.bytes);
+}
+
+// Wave-level device scratch: status words, the deferred list and its roll-back slots (n messages).
+struct WaveScratch {
+    unsigned long long* status;
+    unsigned long long* deferred;
+    uint32_t* saved;
+};
+
+// Room for n messages; growing keeps the status words and the first `keep` deferred entries (a
+// streamed wave grows between chunks).  The roll-back slots follow the deferred list, so their
+// offset depends on the capacity: they are only written at finish time.
+WaveScratch wave_scratch(jg_pnc* p, uint64_t n, uint64_t keep = 0) {
+    const size_t need = 64 + n * 8 + n * 4 + 256;
+    if (p->wstat.bytes < need) grow_keep(p->ctx, p->wstat, need, p->wstat.p ? 64 + keep * 8 : 0);
+    n = (p->wstat.bytes - 64 - 256) / 12;  // the capacity actually there
+    char* s = p->wstat.as<char>();
+    return WaveScratch{reinterpret_cast<unsigned long long*>(s), reinterpret_cast<unsigned long long*>(s + 64),
+                       reinterpret_cast<uint32_t*>(s + 64 + ((n * 8 + 15) & ~15ull))};
+}
+
+void reset_status(jg_ctx* ctx, unsigned long long* status) {
+    static const Status init{~0ull, 0, ~0ull, 0};
     JG_HIP(hipMemcpyAsync(status, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
-    const unsigned g = blocks_for(n);
-    if (p->eb == 8) hipLaunchKernelGGL(k_scan<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, status, deferred);
-    else hipLaunchKernelGGL(k_scan<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, status, deferred);
+}
+
+void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1,
+                 const WaveScratch& w) {
+    if (m1 <= m0) return;
+    const Table t = table_of(p);
+    const unsigned g = blocks_for(m1 - m0);
+    if (p->eb == 8) hipLaunchKernelGGL(k_scan<8>, dim3(g), dim3(kBlock), 0, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred);
+    else hipLaunchKernelGGL(k_scan<4>, dim3(g), dim3(kBlock), 0, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred);
     JG_HIP(hipGetLastError());
-    Status st = read_status(ctx, status);
+}
+
+// After pass A over all n messages: check, resolve new replicas, apply.  All or nothing.
+void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, const WaveScratch& w,
+                 uint64_t* bad_msg) {
+    jg_ctx* ctx = p->ctx;
+    const Table t = table_of(p);
+    Status st = read_status(ctx, w.status);
     if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
     if (st.n_deferred) {
         const uint64_t nd = st.n_deferred;
-        unsigned long long* sorted = sort_keys(ctx, deferred, nd, p->n_keys);
+        unsigned long long* sorted = sort_keys(ctx, w.deferred, nd, p->n_keys);
         const unsigned gd = blocks_for(nd);
-        if (p->eb == 8) hipLaunchKernelGGL(k_resolve<8>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, saved, status);
-        else hipLaunchKernelGGL(k_resolve<4>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, saved, status);
+        if (p->eb == 8) hipLaunchKernelGGL(k_resolve<8>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
+        else hipLaunchKernelGGL(k_resolve<4>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
         JG_HIP(hipGetLastError());
-        st = read_status(ctx, status);
+        st = read_status(ctx, w.status);
         if (st.resolve_bad != ~0ull) {
-            hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, saved);
+            hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, w.saved);
             JG_HIP(hipGetLastError());
             JG_HIP(hipStreamSynchronize(ctx->stream));
             fail_msg(st.resolve_bad, bad_msg, "state message");
         }
     }
-    if (p->eb == 8) hipLaunchKernelGGL(k_apply<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, status);
-    else hipLaunchKernelGGL(k_apply<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, status);
+    const unsigned g = blocks_for(n);
+    if (p->eb == 8) hipLaunchKernelGGL(k_apply<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, w.status);
+    else hipLaunchKernelGGL(k_apply<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, w.status);
     JG_HIP(hipGetLastError());
-    st = read_status(ctx, status);
+    st = read_status(ctx, w.status);
     if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
+}
+
+// The whole device side of a wave already in device memory.
+void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad_msg) {
+    ensure_table(p);
+    const WaveScratch w = wave_scratch(p, n);
+    reset_status(p->ctx, w.status);
+    launch_scan(p, bytes, off, rows, 0, n, w);
+    finish_wave(p, bytes, off, rows, n, w, bad_msg);
 }
 
 void check_wave_host(const jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const char* fn) {
@@ -620,25 +670,88 @@ int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
     });
 }
 
-int jg_pnc_merge_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
     return jg::guard([&] {
-        if (bad_msg) *bad_msg = UINT64_MAX;
-        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_merge_json: store is NULL");
-        if (n == 0) return;
-        JG_REQUIRE(key_idx && off && bytes, JG_EINVAL, "jg_pnc_merge_json: NULL argument");
-        check_wave_host(p, n, key_idx, off, "jg_pnc_merge_json");
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_begin: store is NULL");
         jg_ctx* ctx = p->ctx;
         jg::ensure_device(ctx);
-        const uint64_t nb = off[n];
-        const uint64_t nb_pad = ((nb + 15) & ~15ull) + 16;
-        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, nb_pad + (n + 1) * 8 + n * 4 + 512));
-        auto* dbytes = reinterpret_cast<uint8_t*>(s);
-        auto* doff = reinterpret_cast<uint64_t*>(s + nb_pad);
-        auto* drows = reinterpret_cast<uint32_t*>(s + nb_pad + (n + 1) * 8);
-        if (nb) JG_HIP(hipMemcpyAsync(dbytes, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
-        JG_HIP(hipMemcpyAsync(doff, off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
-        JG_HIP(hipMemcpyAsync(drows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
-        merge_wave_dev(p, dbytes, doff, drows, n, bad_msg);
+        ensure_table(p);
+        grow_keep(ctx, p->wbytes, ((cap_bytes + 15) & ~15ull) + 16, 0);
+        grow_keep(ctx, p->woff, (cap_msgs + 1) * 8, 0);
+        grow_keep(ctx, p->wrows, cap_msgs * 4 + 4, 0);
+        const WaveScratch w = wave_scratch(p, cap_msgs);
+        reset_status(ctx, w.status);
+        JG_HIP(hipMemsetAsync(p->woff.p, 0, 8, ctx->stream));  // off[0] = 0
+        p->wn = 0;
+        p->wnb = 0;
+        p->wopen = true;
+    });
+}
+
+int jg_pnc_wave_append(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_append: no open wave (jg_pnc_wave_begin)");
+        if (n == 0) return;
+        JG_REQUIRE(key_idx && off && bytes, JG_EINVAL, "jg_pnc_wave_append: NULL argument");
+        check_wave_host(p, n, key_idx, off, "jg_pnc_wave_append");
+        JG_REQUIRE(p->wn + n < 0xFFFFFFFFull, JG_EINVAL, "jg_pnc_wave_append: at most 2^32-2 messages per wave");
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        const uint64_t m0 = p->wn, b0 = p->wnb, nb = off[n];
+        // grow (rare: the caller's capacity hint was short); earlier chunks are kept
+        if (p->wbytes.bytes < ((b0 + nb + 15) & ~15ull) + 16 || p->woff.bytes < (m0 + n + 1) * 8 || p->wrows.bytes < (m0 + n) * 4 + 4) {
+            const uint64_t need_m = 2 * (m0 + n), need_b = 2 * (b0 + nb);
+            grow_keep(ctx, p->wbytes, ((need_b + 15) & ~15ull) + 16, b0);
+            grow_keep(ctx, p->woff, (need_m + 1) * 8, (m0 + 1) * 8);
+            grow_keep(ctx, p->wrows, need_m * 4 + 4, m0 * 4);
+        }
+        const WaveScratch w = wave_scratch(p, m0 + n, m0);  // keeps the entries earlier chunks deferred
+        if (nb) JG_HIP(hipMemcpyAsync(p->wbytes.as<uint8_t>() + b0, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(p->woff.as<uint64_t>() + m0 + 1, off + 1, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(p->wrows.as<uint32_t>() + m0, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        if (b0) hipLaunchKernelGGL(k_rebase, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, p->woff.as<uint64_t>() + m0 + 1, n, b0);
+        launch_scan(p, p->wbytes.as<uint8_t>(), p->woff.as<uint64_t>(), p->wrows.as<uint32_t>(), m0, m0 + n, w);
+        p->wn = m0 + n;
+        p->wnb = b0 + nb;
+    });
+}
+
+int jg_pnc_wave_commit(jg_pnc* p, uint64_t* bad_msg) {
+    return jg::guard([&] {
+        if (bad_msg) *bad_msg = UINT64_MAX;
+        JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_commit: no open wave (jg_pnc_wave_begin)");
+        jg::ensure_device(p->ctx);
+        p->wopen = false;
+        if (p->wn == 0) return;
+        finish_wave(p, p->wbytes.as<uint8_t>(), p->woff.as<uint64_t>(), p->wrows.as<uint32_t>(), p->wn, wave_scratch(p, p->wn), bad_msg);
+    });
+}
+
+int jg_pnc_wave_abort(jg_pnc* p) {
+    return jg::guard([&] {
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_abort: store is NULL");
+        jg::ensure_device(p->ctx);
+        JG_HIP(hipStreamSynchronize(p->ctx->stream));  // pass A only read the wave: nothing to undo
+        p->wopen = false;
+    });
+}
+
+int jg_pnc_merge_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+    if (bad_msg) *bad_msg = UINT64_MAX;
+    if (p && n && off) {
+        int rc = jg_pnc_wave_begin(p, n, off[n]);
+        if (rc == JG_OK) rc = jg_pnc_wave_append(p, n, key_idx, off, bytes);
+        if (rc != JG_OK) {
+            char keep[1024];
+            jg_last_error(keep, sizeof keep);
+            jg_pnc_wave_abort(p);
+            return jg::guard([&] { jg::fail(rc, "%s", keep); });
+        }
+        return jg_pnc_wave_commit(p, bad_msg);
+    }
+    return jg::guard([&] {
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_merge_json: store is NULL");
+        JG_REQUIRE(n == 0, JG_EINVAL, "jg_pnc_merge_json: NULL argument");
     });
 }
 

@@ -8,6 +8,9 @@
 #include <cstdlib>
 #include <limits>
 #include <memory>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 
 #include "wire.hpp"
@@ -44,7 +47,8 @@ GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas,
 }
 
 GpuStableStore::~GpuStableStore() {
-    if (stage_) jg_host_free(stage_);
+    for (auto& c : chunks_)
+        if (c.first) jg_host_free(c.first);
     if (orset_) jg_orset_destroy(orset_);
     if (pnc_) jg_pnc_destroy(pnc_);
     if (ctx_) jg_close(ctx_);
@@ -118,40 +122,87 @@ void GpuStableStore::flush_registrations() {
     reg_guids_.clear();
 }
 
-char* GpuStableStore::staging(size_t bytes) {
-    if (bytes > stage_bytes_) {
-        if (stage_) jg_host_free(stage_);
-        stage_ = nullptr;
-        stage_bytes_ = 0;
-        void* p = nullptr;
-        const size_t want = bytes + bytes / 4 + 4096;
-        check(jg_host_alloc(ctx_, want, &p));
-        stage_ = static_cast<char*>(p);
-        stage_bytes_ = want;
-    }
-    return stage_;
-}
 
 namespace {
 double wall_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 }  // namespace
 
+// Persistent host workers (thread creation per phase cost ~0.3 ms per phase; a wave runs ~20).
+class WorkerPool {
+  public:
+    explicit WorkerPool(int n) : n_(n) {
+        for (int t = 1; t < n; ++t) th_.emplace_back([this, t] { loop(t); });
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return n_; }
+    // fn(t) for every worker t in [0, n); t = 0 runs on the caller.  Returns when all are done.
+    void run(const std::function<void(int)>& fn) {
+        if (n_ == 1) { fn(0); return; }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &fn;
+            pending_ = n_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void loop(int t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)>* job;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                job = job_;
+            }
+            (*job)(t);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    int pending_ = 0;
+    bool stop_ = false;
+};
+
 namespace {
-// Static contiguous split of [0, n) over up to `threads` workers: fn(begin, end, worker).  Worker t's
+// Static contiguous split of [0, n) over the pool's workers: fn(begin, end, worker).  Worker t's
 // range precedes worker t+1's, so per-worker results concatenated in worker order keep message order.
-template <class F> void parallel_ranges(size_t n, int threads, F&& fn) {
-    static const size_t min_par = [] {  // below this many messages the wave is decoded inline
+template <class F> void parallel_ranges(WorkerPool& pool, size_t n, F&& fn) {
+    static const size_t min_par = [] {  // below this many messages a phase runs inline
         const char* e = std::getenv("JANUS_HOST_PAR_MIN");
-        return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{32768};
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{8192};
     }();
-    if (threads <= 1 || n < min_par || n < (size_t)threads) {
+    const int T = pool.size();
+    if (T <= 1 || n < min_par || n < (size_t)T) {
         fn(size_t{0}, n, 0);
+        for (int t = 1; t < T; ++t) fn(n, n, t);
         return;
     }
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; ++t) pool.emplace_back([&, t] { fn(n * t / threads, n * (t + 1) / threads, t); });
-    fn(size_t{0}, n / threads, 0);
-    for (auto& th : pool) th.join();
+    pool.run([&](int t) { fn(n * t / T, n * (t + 1) / T, t); });
 }
 }  // namespace
 
@@ -162,6 +213,25 @@ int GpuStableStore::host_threads() {
     }
     const unsigned hw = std::thread::hardware_concurrency();
     return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+}
+
+WorkerPool& GpuStableStore::pool() {
+    if (!pool_ || pool_->size() != host_threads()) pool_ = std::make_unique<WorkerPool>(host_threads());
+    return *pool_;
+}
+
+char* GpuStableStore::chunk_buffer(size_t c, size_t bytes) {
+    if (chunks_.size() <= c) chunks_.resize(c + 1, {nullptr, 0});
+    auto& s = chunks_[c];
+    if (s.second < bytes) {
+        if (s.first) jg_host_free(s.first);
+        s = {nullptr, 0};
+        void* p = nullptr;
+        const size_t want = bytes + bytes / 4 + 4096;
+        check(jg_host_alloc(ctx_, want, &p));
+        s = {static_cast<char*>(p), want};
+    }
+    return s.first;
 }
 
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
@@ -179,71 +249,97 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
                 for (const auto& u : block.update) msgs.push_back(&u);
     }
     const size_t n = msgs.size();
-    const int T = host_threads();
+    WorkerPool& wp = pool();
+    const int T = wp.size();
     phase_s_[0] = wall_s() - t0;
     constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1;
+    static const size_t chunk_msgs = [] {
+        const char* e = std::getenv("JANUS_WAVE_CHUNK");
+        return e ? std::max<size_t>(1, std::strtoull(e, nullptr, 10)) : size_t{131072};
+    }();
 
-    // Phase 1 (parallel, read-only): classify every message — PNC row, OR-Set, or skipped (:133-136)
-    // — and size the PN-Counter payloads.
+    // The wave is streamed in chunks of commit order: classify + gather chunk c on the host workers
+    // while the engine uploads and scans chunk c-1 (jg_pnc_wave_append returns once queued).
+    // A chunk's pinned buffer: [payload | pad 16 | off (m+1) u64 | rows u32]; it stays untouched
+    // until the wave is committed or aborted.
     std::vector<uint32_t> cls(n);
-    std::vector<size_t> pnc_count(T, 0), pnc_bytes(T, 0);
-    parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
-        size_t cnt = 0, bytes = 0;
-        for (size_t i = b; i < e; ++i) {
-            if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
-            if (i + 8 < e) uids_.prefetch(msgs[i + 8]->uid);
-            const NetworkProtocol& u = *msgs[i];
-            uint32_t c = kSkip;
-            if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {
-                if (const KeyRef* kr = uids_.find(u.uid)) {
-                    if (kr->type == CrdtType::PNCounter) { c = kr->idx; ++cnt; bytes += u.message.size(); }
-                    else c = kSet;
+    struct Chunk { size_t m; char* buf; uint64_t* off; uint32_t* rows; uint8_t* bytes; };
+    std::vector<Chunk> chunks;
+    std::vector<uint64_t> where;  // PNC message (wave order) -> commit index
+    std::vector<size_t> cnt(T), nbytes(T), mbase(T + 1), bbase(T + 1);
+    const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
+    bool open = false;
+    double t_classify = 0, t_gather = 0;
+    for (size_t c = 0; c < n_chunks; ++c) {
+        const size_t c0 = c * chunk_msgs, c1 = std::min(n, c0 + chunk_msgs);
+        const double ta = wall_s();
+        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
+            size_t k = 0, bytes = 0;
+            for (size_t i = c0 + b; i < c0 + e; ++i) {
+                if (i + 16 < c0 + e) __builtin_prefetch(msgs[i + 16]);
+                if (i + 8 < c0 + e) uids_.prefetch(msgs[i + 8]->uid);
+                const NetworkProtocol& u = *msgs[i];
+                uint32_t cl = kSkip;
+                if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
+                    if (const KeyRef* kr = uids_.find(u.uid)) {                                  // :136
+                        if (kr->type == CrdtType::PNCounter) { cl = kr->idx; ++k; bytes += u.message.size(); }
+                        else cl = kSet;
+                    }
                 }
+                cls[i] = cl;
             }
-            cls[i] = c;
+            cnt[t] = k;
+            nbytes[t] = bytes;
+        });
+        for (int t = 0; t < T; ++t) { mbase[t + 1] = mbase[t] + cnt[t]; bbase[t + 1] = bbase[t] + nbytes[t]; }
+        const size_t m = mbase[T], nb = bbase[T], nb_pad = (nb + 15) & ~size_t(15);
+        const double tb = wall_s();
+        t_classify += tb - ta;
+        if (m == 0) continue;
+        char* buf = chunk_buffer(chunks.size(), nb_pad + (m + 1) * 8 + m * 4 + 64);
+        Chunk ch{m, buf, reinterpret_cast<uint64_t*>(buf + nb_pad), nullptr, reinterpret_cast<uint8_t*>(buf)};
+        ch.rows = reinterpret_cast<uint32_t*>(ch.off + m + 1);
+        const size_t w0 = where.size();
+        where.resize(w0 + m);
+        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
+            size_t j = mbase[t];
+            uint64_t o = bbase[t];
+            for (size_t i = c0 + b; i < c0 + e; ++i) {
+                if (i + 8 < c0 + e) __builtin_prefetch(msgs[i + 8]->message.data());
+                if (cls[i] >= kSet) continue;
+                const std::string& p = msgs[i]->message;
+                std::memcpy(ch.bytes + o, p.data(), p.size());
+                ch.off[j] = o;
+                ch.rows[j] = cls[i];
+                where[w0 + j] = i;
+                o += p.size();
+                ++j;
+            }
+        });
+        ch.off[m] = nb;
+        t_gather += wall_s() - tb;
+        if (!open) {
+            check(jg_pnc_wave_begin(pnc_, std::max<size_t>(m * n_chunks, 1), std::max<size_t>(nb * n_chunks, 1)));
+            open = true;
         }
-        pnc_count[t] = cnt;
-        pnc_bytes[t] = bytes;
-    });
-    phase_s_[1] = wall_s() - t0;
-
-    // Phase 2 (parallel): gather the PN-Counter payloads, in commit order, into pinned staging:
-    // [bytes | pad to 16 | off (n_pnc+1) u64 | rows u32 | commit index u64].
-    std::vector<size_t> mbase(T + 1, 0), bbase(T + 1, 0);
-    for (int t = 0; t < T; ++t) { mbase[t + 1] = mbase[t] + pnc_count[t]; bbase[t + 1] = bbase[t] + pnc_bytes[t]; }
-    const size_t n_pnc = mbase[T], nb = bbase[T];
-    const size_t nb_pad = (nb + 15) & ~size_t(15);
-    char* st = staging(nb_pad + (n_pnc + 1) * 8 + n_pnc * 4 + n_pnc * 8 + 64);
-    uint8_t* bytes = reinterpret_cast<uint8_t*>(st);
-    uint64_t* off = reinterpret_cast<uint64_t*>(st + nb_pad);
-    uint32_t* rows = reinterpret_cast<uint32_t*>(off + n_pnc + 1);
-    uint64_t* where = reinterpret_cast<uint64_t*>(st + nb_pad + (n_pnc + 1) * 8 + ((n_pnc * 4 + 7) & ~size_t(7)));
-    parallel_ranges(n, T, [&](size_t b, size_t e, int t) {
-        size_t m = mbase[t];
-        uint64_t o = bbase[t];
-        for (size_t i = b; i < e; ++i) {
-            if (i + 8 < e) __builtin_prefetch(msgs[i + 8]->message.data());
-            if (cls[i] >= kSet) continue;
-            const std::string& p = msgs[i]->message;
-            std::memcpy(bytes + o, p.data(), p.size());
-            off[m] = o;
-            rows[m] = cls[i];
-            where[m] = i;
-            o += p.size();
-            ++m;
+        const int rc = jg_pnc_wave_append(pnc_, m, ch.rows, ch.off, ch.bytes);
+        if (rc != JG_OK) {
+            jg_pnc_wave_abort(pnc_);
+            check(rc);
         }
-    });
-    off[n_pnc] = nb;
-    phase_s_[2] = wall_s() - t0;
+        chunks.push_back(ch);
+    }
+    phase_s_[1] = t_classify;
+    phase_s_[2] = t_classify + t_gather;
 
-    // Phase 3: OR-Set payloads, decoded in parallel; the first rejected one (commit order) cuts the wave.
+    // OR-Set payloads, decoded in parallel; the first rejected one (commit order) cuts the wave.
     std::vector<size_t> set_msgs;
     for (size_t i = 0; i < n; ++i)
         if (cls[i] == kSet) set_msgs.push_back(i);
     std::vector<ORSetState> decoded(set_msgs.size());
     std::vector<size_t> first_bad(T, SIZE_MAX);
     std::vector<std::string> why(T);
-    parallel_ranges(set_msgs.size(), T, [&](size_t b, size_t e, int t) {
+    parallel_ranges(wp, set_msgs.size(), [&](size_t b, size_t e, int t) {
         for (size_t j = b; j < e; ++j) {
             try {
                 decoded[j] = wire::DecodeORSetMsg(msgs[set_msgs[j]]->message);
@@ -263,23 +359,38 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
     phase_s_[3] = wall_s() - t0;
 
     const double t1 = wall_s();
-    // PN-Counter wave: one engine call over the messages before the cut (the prefix is re-submitted
-    // if the engine rejects one of them: its calls are all or nothing, the reference's loop is not).
-    size_t n_submit = n_pnc;
-    while (n_submit && where[n_submit - 1] >= cut) --n_submit;
-    if (n_submit) {
-        uint64_t bad = UINT64_MAX;
-        // off[m] = start of message m = end of message m - 1: any prefix of off[] is well formed
-        const int rc = jg_pnc_merge_json(pnc_, n_submit, rows, off, bytes, &bad);
-        if (rc != JG_OK) {
-            if (bad == UINT64_MAX) check(rc);
-            cut = where[bad];
-            cut_code = rc;
-            cut_why = last_error();
-            if (bad) check(jg_pnc_merge_json(pnc_, bad, rows, off, bytes, nullptr));
+    // Re-stream the first `limit` PNC messages (the reference's loop applied the messages before the
+    // one that threw; the engine's waves are all or nothing).
+    auto submit_prefix = [&](size_t limit) {
+        if (limit == 0) return;
+        check(jg_pnc_wave_begin(pnc_, limit, 1));
+        size_t left = limit;
+        for (const Chunk& ch : chunks) {
+            if (!left) break;
+            const size_t k = std::min(left, ch.m);
+            check(jg_pnc_wave_append(pnc_, k, ch.rows, ch.off, ch.bytes));
+            left -= k;
+        }
+        check(jg_pnc_wave_commit(pnc_, nullptr));
+    };
+    if (open) {
+        if (cut < n) {  // an OR-Set state before some of these PNC states was rejected
+            check(jg_pnc_wave_abort(pnc_));
+            submit_prefix((size_t)(std::lower_bound(where.begin(), where.end(), (uint64_t)cut) - where.begin()));
+        } else {
+            uint64_t bad = UINT64_MAX;
+            const int rc = jg_pnc_wave_commit(pnc_, &bad);
+            if (rc != JG_OK) {
+                if (bad == UINT64_MAX) check(rc);
+                cut = where[bad];
+                cut_code = rc;
+                cut_why = last_error();
+                submit_prefix(bad);
+            }
         }
     }
-    pnc_bytes_ = n_submit ? off[n_submit] : 0;
+    pnc_bytes_ = 0;
+    for (const Chunk& ch : chunks) pnc_bytes_ += ch.off[ch.m];
 
     // OR-Set states before the cut: element interning in commit order, then one merge.
     std::vector<jg_tagrec> adds, rems;

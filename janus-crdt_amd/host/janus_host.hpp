@@ -20,6 +20,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <optional>
 #include <stdexcept>
 #include <string>
@@ -30,6 +31,8 @@
 #include "janus_gpu.h"
 
 namespace janus {
+
+class WorkerPool;
 
 struct Guid {
     uint64_t lo = 0, hi = 0;
@@ -168,7 +171,8 @@ class GpuStableStore {
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
     void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
-    char* staging(size_t bytes);            // pinned host buffer (jg_host_alloc), grown on demand
+    char* chunk_buffer(size_t c, size_t bytes);  // pinned staging of wave chunk c (jg_host_alloc), grown on demand
+    WorkerPool& pool();                     // persistent host workers (host_threads())
 
     jg_ctx* ctx_ = nullptr;
     jg_pnc* pnc_ = nullptr;
@@ -180,8 +184,8 @@ class GpuStableStore {
     UidTable uids_;
     std::vector<uint32_t> reg_rows_;        // CreateSafeCRDT registrations not yet sent
     std::vector<jg_guid> reg_guids_;
-    char* stage_ = nullptr;
-    size_t stage_bytes_ = 0;
+    std::vector<std::pair<char*, size_t>> chunks_;  // pinned chunk buffers, reused wave after wave
+    std::unique_ptr<WorkerPool> pool_;
     std::vector<SetKey> sets_;
 };
 

@@ -298,6 +298,7 @@ int main() {
     // the threshold is lowered to 1 so the parallel decode (and its commit-order column insertion)
     // runs on these small waves too.
     setenv("JANUS_HOST_PAR_MIN", "1", 1);
+    setenv("JANUS_WAVE_CHUNK", "37", 1);  // stream every wave in many chunks (jg_pnc_wave_append)
     const Case cases[] = {
         {1, 6, 4, 400, 7, 1, 4, "1"},      // KVStoreTests: clientBatchSize = 1
         {2, 20, 10, 3000, 97, 8, 4, "4"},  // batched client updates, state compaction (SafeCRDTManager.cs:165-198)

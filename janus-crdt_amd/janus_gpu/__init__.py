@@ -30,6 +30,7 @@ EXPORTS = [
     "jg_synth_pnc_store", "jg_synth_pnc_rows", "jg_synth_orset",
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
+    "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -76,6 +77,10 @@ _SIGS = {
     "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_host_alloc": ([_vp, _u64, C.POINTER(_vp)], C.c_int),
     "jg_host_free": ([_vp], C.c_int),
+    "jg_pnc_wave_begin": ([_vp, _u64, _u64], C.c_int),
+    "jg_pnc_wave_append": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_wave_commit": ([_vp, C.POINTER(_u64)], C.c_int),
+    "jg_pnc_wave_abort": ([_vp], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -272,6 +277,28 @@ class PNCStore:
         rc = load().jg_pnc_merge_json(self._h, k.size, _ptr(k), _ptr(off), _ptr(data) if data.size else _ptr(np.zeros(16, np.uint8)),
                                       C.byref(bad))
         _check(rc, bad.value)
+
+    # streamed wave: begin, append chunks (their buffers are kept alive here until commit/abort)
+    def wave_begin(self, cap_msgs: int = 0, cap_bytes: int = 0) -> None:
+        self._chunks = []
+        _check(load().jg_pnc_wave_begin(self._h, cap_msgs, cap_bytes))
+
+    def wave_append(self, key_idx, msgs) -> None:
+        data, off = pack_wave(msgs)
+        k = _arr(key_idx, np.uint32)
+        data = data if data.size else np.zeros(16, np.uint8)
+        self._chunks.append((k, data, off))
+        _check(load().jg_pnc_wave_append(self._h, k.size, _ptr(k), _ptr(off), _ptr(data)))
+
+    def wave_commit(self) -> None:
+        bad = _u64(0)
+        rc = load().jg_pnc_wave_commit(self._h, C.byref(bad))
+        self._chunks = []
+        _check(rc, bad.value)
+
+    def wave_abort(self) -> None:
+        _check(load().jg_pnc_wave_abort(self._h))
+        self._chunks = []
 
     def merge_wave(self, wave: "Wave") -> None:
         bad = _u64(0)

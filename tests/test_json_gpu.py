@@ -234,3 +234,58 @@ def test_c5_shaped_wave(ctx):
     # every message carries its node's full row, and rows only grow: Get = the latest row sums
     assert (o == 0).all() and np.array_equal(v, np.where(np.isin(np.arange(n_keys), keys), P.sum(axis=1), 0))
     pr.close()
+
+
+def test_streamed_wave_chunks_equal_one_call(ctx):
+    """jg_pnc_wave_begin/append/commit over uneven chunks (capacity hint exceeded, so the wave buffers
+    and the deferred list grow mid-wave) = one jg_pnc_merge_json of the concatenation."""
+    rng = np.random.default_rng(12)
+    n_keys = 300
+    stable = random_guids(rng, n_keys)
+    a = Pair(ctx, n_keys, 8, 4, stable)
+    b = Pair(ctx, n_keys, 8, 4, stable)
+    cl = Cluster(rng, n_keys, 6, 4, stable)
+    for wave in range(3):
+        keys = rng.integers(0, n_keys, 5000).astype(np.uint32)
+        msgs = [cl.message(int(k)) for k in keys]
+        a.oracle(keys, msgs)
+        a.s.merge_json(keys, msgs)
+        b.s.wave_begin(100, 10_000)  # deliberately short hints
+        cuts = sorted(set([0, 5000] + rng.integers(0, 5000, 6).tolist()))
+        for c0, c1 in zip(cuts, cuts[1:]):
+            b.s.wave_append(keys[c0:c1], msgs[c0:c1])
+        b.s.wave_append(np.zeros(0, np.uint32), [])
+        b.s.wave_commit()
+        b.P, b.N, b.cols, b.ncols = a.P, a.N, a.cols, a.ncols
+        a.check()
+        b.check()
+    a.close()
+    b.close()
+
+
+def test_streamed_wave_error_and_abort(ctx):
+    rng = np.random.default_rng(13)
+    n_keys = 50
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, 8, 8, stable)
+    cl = Cluster(rng, n_keys, 6, 8, stable)
+    keys = rng.integers(0, n_keys, 900).astype(np.uint32)
+    msgs = [cl.message(int(k)) for k in keys]
+    msgs[650] = b'{"pVector":{},"nVector":{}'
+    pr.s.wave_begin(900, 1 << 20)
+    for c in range(0, 900, 300):
+        pr.s.wave_append(keys[c:c + 300], msgs[c:c + 300])
+    with pytest.raises(jg.JanusError) as e:
+        pr.s.wave_commit()
+    assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 650  # index over the whole wave
+    pr.check()  # nothing applied
+    pr.s.wave_begin(900, 1 << 20)
+    pr.s.wave_append(keys[:300], msgs[:300])
+    pr.s.wave_abort()
+    pr.check()  # abort applies nothing
+    with pytest.raises(jg.JanusError):
+        pr.s.wave_commit()  # no open wave
+    pr.oracle(keys[:650], msgs[:650])
+    pr.s.merge_json(keys[:650], msgs[:650])
+    pr.check()
+    pr.close()
