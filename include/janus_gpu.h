@@ -180,6 +180,12 @@ int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const u
  * and (it has no tombstone set or the two tag sets differ: !SetEquals); the null element is
  * present iff !SetEquals(nullRemove, nullAdd).  out[i] = 0/1. */
 int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, uint64_t n, uint8_t* out);
+/* ORSet.LookupAll (ORSet.cs:204-227) of sets set[0..n): members of set[i] are elems[off[i], off[i+1])
+ * (off has n+1 entries, always filled), in the reference's order: elements with no tombstone set,
+ * then elements whose tag sets differ (each group in ascending elem id = the add Dictionary's
+ * insertion order when elem ids are interned at first insertion), then JG_NULL_ELEM if null is
+ * present.  elems NULL = size query; JG_ESTATE if off[n] > cap (nothing written to elems). */
+int jg_orset_lookup_all(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* off, uint32_t* elems, uint64_t cap);
 
 /* ---------------------------------------------------------------------------------------------
  * Synthetic workloads (bench / size-independent parity): device-side counter-based generators,

@@ -104,6 +104,56 @@ __global__ __launch_bounds__(kOB) void k_contains(View a, View r, const unsigned
     }
 }
 
+// ORSet.LookupAll (ORSet.cs:204-227) per queried set.  Elements of a set are walked in ascending
+// elem id — the host interns elements in first-insertion order of the add Dictionary, so this is the
+// Dictionary's enumeration order — and emitted in the reference's three groups: present elements
+// with no removeSet entry (addSet.Keys.Except(removeSet.Keys)), then present elements with one
+// (the join where !SetEquals), then null if !SetEquals(nullRemoveGuid, nullAddGuid).
+// pass 0: cnt[i] = the set's member count; pass 1: write members at out + off[i].
+__device__ __forceinline__ bool runs_equal(const View& a, uint64_t a0, uint64_t a1, const View& r, uint64_t r0, uint64_t r1) {
+    if (a1 - a0 != r1 - r0) return false;
+    for (uint64_t j = 0; j < a1 - a0; ++j) {
+        const Tag x = ld_tag(a.tag + jgk::slot_of(a, a0 + j)), y = ld_tag(r.tag + jgk::slot_of(r, r0 + j));
+        if (x.lo != y.lo || x.hi != y.hi) return false;
+    }
+    return true;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(kOB) void k_lookup_all(View a, View r, const uint32_t* __restrict__ sets, uint64_t n,
+                                                    uint64_t* __restrict__ cnt_off, uint32_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        const unsigned long long base = (unsigned long long)sets[i] << 32, nullk = base | JG_NULL_ELEM;
+        const uint64_t a_end = lower_key(a, nullk), r_beg = lower_key(r, base), r_end = lower_key(r, nullk);
+        uint64_t w = PASS ? cnt_off[i] : 0;
+        for (int group = 0; group < 2; ++group) {
+            uint64_t x = lower_key(a, base), y = r_beg;
+            while (x < a_end) {
+                const unsigned long long k = key_at(a, x);
+                uint64_t x1 = x + 1;
+                while (x1 < a_end && key_at(a, x1) == k) ++x1;
+                while (y < r_end && key_at(r, y) < k) ++y;
+                uint64_t y1 = y;
+                while (y1 < r_end && key_at(r, y1) == k) ++y1;
+                const bool has_rem = y1 > y;
+                if (has_rem == (group == 1) && (!has_rem || !runs_equal(a, x, x1, r, y, y1))) {
+                    if (PASS) out[w] = (uint32_t)k;
+                    ++w;
+                }
+                x = x1;
+                y = y1;
+            }
+        }
+        // null: present iff the null tag sets differ
+        const uint64_t na1 = upper_key(a, nullk), nr1 = upper_key(r, nullk);
+        if (!runs_equal(a, a_end, na1, r, r_end, nr1)) {
+            if (PASS) out[w] = JG_NULL_ELEM;
+            ++w;
+        }
+        if (!PASS) cnt_off[i] = w;
+    }
+}
+
 // Rank bounds of each queried key's run in both streams: out[4i..4i+3] = a0, a1, r0, r1.
 __global__ __launch_bounds__(kOB) void k_runs(View a, View r, const unsigned long long* __restrict__ q, uint64_t nq, uint64_t* __restrict__ out) {
     for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kOB) {
@@ -575,6 +625,39 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
         hipLaunchKernelGGL(k_contains, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dq, n, dout);
         JG_HIP(hipGetLastError());
         JG_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_orset_lookup_all(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* off, uint32_t* elems, uint64_t cap) {
+    return jg::guard([&] {
+        JG_REQUIRE(s && off, JG_EINVAL, "jg_orset_lookup_all: NULL argument");
+        off[0] = 0;
+        if (n == 0) return;
+        JG_REQUIRE(set, JG_EINVAL, "jg_orset_lookup_all: NULL set list");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg::sync_counts(s);
+        char* st = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 12 + 64));
+        auto* dset = reinterpret_cast<uint32_t*>(st);
+        auto* dcnt = reinterpret_cast<uint64_t*>(st + ((n * 4 + 15) & ~15ull));
+        JG_HIP(hipMemcpyAsync(dset, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        const unsigned g = grid_for(ctx, n, 16);
+        hipLaunchKernelGGL(k_lookup_all<0>, dim3(g), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dset, n, dcnt, nullptr);
+        JG_HIP(hipGetLastError());
+        std::vector<uint64_t> cnt(n);
+        JG_HIP(hipMemcpyAsync(cnt.data(), dcnt, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + cnt[i];
+        if (!elems) return;  // size query
+        JG_REQUIRE(off[n] <= cap, JG_ESTATE, "jg_orset_lookup_all: %llu members exceed cap %llu", (unsigned long long)off[n],
+                   (unsigned long long)cap);
+        if (off[n] == 0) return;
+        auto* dout = static_cast<uint32_t*>(jg::scratch(ctx, ctx->scratch2, off[n] * 4 + 64));
+        JG_HIP(hipMemcpyAsync(dcnt, off, n * 8, hipMemcpyHostToDevice, ctx->stream));  // exclusive offsets
+        hipLaunchKernelGGL(k_lookup_all<1>, dim3(g), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dset, n, dcnt, dout);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(elems, dout, off[n] * 4, hipMemcpyDeviceToHost, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
     });
 }

@@ -94,9 +94,11 @@ uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e,
     auto it = s.elems.find(*e);
     if (it != s.elems.end()) return it->second;
     if (!create) return JG_NULL_ELEM - 1;  // never allocated: no records carry it
-    const uint32_t id = (uint32_t)s.elems.size();
+    // ids only grow (also across Clear), so ascending id = insertion order into the add Dictionary
+    const uint32_t id = (uint32_t)s.names.size();
     if (id >= JG_NULL_ELEM - 1) throw EngineError(JG_ESTATE, "too many elements in one OR-Set");
     s.elems.emplace(*e, id);
+    s.names.push_back(*e);
     return id;
 }
 
@@ -455,8 +457,14 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) 
         } else {
             SetKey& sk = sets_[kr.idx];
             oset.push_back(kr.idx);
-            // an element first seen in a Remove gets an id too: its (empty) runs are what Contains sees
-            oelem.push_back(op.opId == 3 ? 0u : elem_id(sk, op.elem, true));
+            // Add interns (first insertion); Remove of an unknown element addresses an id no record
+            // carries (Contains is false, ORSet.cs:174); Clear empties the Dictionaries, so elements
+            // added afterwards take new, larger ids in their new insertion order (ORSet.cs:192-198)
+            uint32_t id = 0;
+            if (op.opId == 1) id = elem_id(sk, op.elem, true);
+            else if (op.opId == 2) id = elem_id(sk, op.elem, false);
+            else sk.elems.clear();
+            oelem.push_back(id);
             oop.push_back((uint8_t)op.opId);
             olo.push_back(op.tag.lo);
             ohi.push_back(op.tag.hi);
@@ -487,6 +495,21 @@ bool GpuStableStore::QueryStableORSet(const Guid& uid, const std::optional<std::
     uint8_t out = 0;
     check(jg_orset_contains(orset_, &set, &id, 1, &out));
     return out != 0;
+}
+
+std::vector<std::optional<std::string>> GpuStableStore::QueryStableLookupAll(const Guid& uid) {
+    const uint32_t set = ref(uid, CrdtType::ORSet).idx;
+    uint64_t off[2] = {0, 0};
+    check(jg_orset_lookup_all(orset_, 1, &set, off, nullptr, 0));
+    std::vector<uint32_t> ids(off[1] ? off[1] : 1);
+    check(jg_orset_lookup_all(orset_, 1, &set, off, ids.data(), ids.size()));
+    std::vector<std::optional<std::string>> out;
+    const SetKey& sk = sets_[set];
+    for (uint64_t i = 0; i < off[1]; ++i) {
+        if (ids[i] == JG_NULL_ELEM) out.emplace_back(std::nullopt);
+        else out.emplace_back(sk.names.at(ids[i]));
+    }
+    return out;
 }
 
 }  // namespace janus

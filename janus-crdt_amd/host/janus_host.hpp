@@ -125,6 +125,8 @@ class GpuStableStore {
     // OverflowException) and ORSet.Contains.
     int64_t QueryStablePNC(const Guid& uid);
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
+    // ORSetWrapper's enumeration / ORSet.LookupAll (ORSet.cs:204-227) in the reference's order.
+    std::vector<std::optional<std::string>> QueryStableLookupAll(const Guid& uid);
 
     // Key-space sharding over `world` GPUs: the shard owning `uid`.  Every rank
     // registers only the keys it owns and applies the same committed waves: states of keys it does
@@ -166,7 +168,10 @@ class GpuStableStore {
         std::vector<Slot> slots_;
         size_t n_ = 0;
     };
-    struct SetKey { std::unordered_map<std::string, uint32_t> elems; };
+    struct SetKey {
+        std::unordered_map<std::string, uint32_t> elems;  // live interning (reset by Clear)
+        std::vector<std::string> names;                   // id -> element, every id ever issued
+    };
     uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;

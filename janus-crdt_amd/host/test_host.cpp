@@ -143,6 +143,15 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
                     const bool op_ = s0.QueryProspective(q).b, gp = gpu_p.QueryStableORSet(G(s0.guid), el);
                     if (op_ != gp) { std::printf("FAIL prospective %s elem %d: oracle %d gpu %d\n", keys[k].c_str(), e, op_, gp); return 1; }
                 }
+                // LookupAll order (ORSet.cs:204-227) on the stable and the prospective copy
+                if (gpu.QueryStableLookupAll(G(s0.guid)) != s0.orStable->orset.LookupAll()) {
+                    std::printf("FAIL %s: LookupAll differs\n", keys[k].c_str());
+                    return 1;
+                }
+                if (gpu_p.QueryStableLookupAll(G(s0.guid)) != s0.orProspective->orset.LookupAll()) {
+                    std::printf("FAIL prospective %s: LookupAll differs\n", keys[k].c_str());
+                    return 1;
+                }
             }
         }
         return 0;

@@ -31,6 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
+    "jg_orset_lookup_all",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -81,6 +82,7 @@ _SIGS = {
     "jg_pnc_wave_append": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_pnc_wave_commit": ([_vp, C.POINTER(_u64)], C.c_int),
     "jg_pnc_wave_abort": ([_vp], C.c_int),
+    "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -389,6 +391,15 @@ class ORSetStore:
         out = np.empty(s.size, np.uint8)
         _check(load().jg_orset_contains(self._h, _ptr(s), _ptr(e), s.size, _ptr(out)))
         return out
+
+    def lookup_all(self, set_ids):
+        """ORSet.LookupAll of each set (jg_orset_lookup_all): list of uint32 arrays of elem ids."""
+        s = _arr(set_ids, np.uint32)
+        off = np.zeros(s.size + 1, np.uint64)
+        _check(load().jg_orset_lookup_all(self._h, s.size, _ptr(s), _ptr(off), None, 0))
+        out = np.empty(max(1, int(off[-1])), np.uint32)
+        _check(load().jg_orset_lookup_all(self._h, s.size, _ptr(s), _ptr(off), _ptr(out), out.size))
+        return [out[int(off[i]):int(off[i + 1])] for i in range(s.size)]
 
     def synth(self, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0) -> None:
         _check(load().jg_synth_orset(self._h, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0))

@@ -287,3 +287,23 @@ def test_chunked_chain_and_mass_clear(ctx):
     finally:
         s.close()
         d.close()
+
+
+@pytest.mark.parametrize("seed,n_sets,n_elems,pool", [(5, 30, 12, 8), (6, 5, 200, 3), (7, 200, 4, 10)])
+def test_lookup_all_matches_oracle(ctx, seed, n_sets, n_elems, pool):
+    """ORSet.LookupAll order (ORSet.cs:204-227): add-only elements, then elements whose tag sets differ
+    from their tombstones, then null — against the oracle's LookupAll on the merged state."""
+    rng = np.random.default_rng(seed)
+    La, Lr, Ra, Rr = random_orset_pair(rng, n_sets=n_sets, n_elems=n_elems, pool=pool)
+    ea, er = orc.orset_merge(La, Lr, Ra, Rr)
+    st = _store(ctx, La, Lr)
+    try:
+        st.merge(Ra, Rr)
+        ids = np.arange(n_sets + 2, dtype=np.uint32)  # includes sets with no records
+        got = st.lookup_all(ids)
+        for s_id, g in zip(ids, got):
+            exp = orc.orset_lookup_all(ea, er, int(s_id))
+            assert np.array_equal(g, exp), f"set {s_id}"
+        assert sum(len(g) for g in got) > 0
+    finally:
+        st.close()
