@@ -146,6 +146,12 @@ int jg_wave_destroy(jg_wave* wave);
 int jg_wave_upload(jg_wave* wave, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes);
 int jg_pnc_merge_wave(jg_pnc* pnc, const jg_wave* wave, uint64_t* bad_msg);
 
+/* GetLastSynchronizedUpdate().Encode() (PNCounters.cs:115-118, 46-49) of rows key_idx[0..n): state i
+ * = out[off[i], off[i+1]) (off has n+1 entries, always filled), System.Text.Json's compact form over
+ * the row's replica table in column order — what SafeCRDT.Update ships (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:49).
+ * out NULL = size query; JG_ESTATE if off[n] > cap (out untouched). */
+int jg_pnc_encode_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap);
+
 /* Page-locked host memory for staging waves (PCIe DMA at full rate); free with jg_host_free. */
 int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out);
 int jg_host_free(void* p);

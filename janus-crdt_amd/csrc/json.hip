@@ -391,6 +391,83 @@ __global__ void k_gather_cols(const Guid16* __restrict__ cols, const uint32_t* _
 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// ---- GetLastSynchronizedUpdate().Encode() on the device ----------------------
+// PNCounterMsg.Encode (PNCounters.cs:46-49) of a row: {"pVector":{"<guid D>":P,...},"nVector":{...}}
+// over the row's columns in table order (= the Dictionaries' enumeration order), System.Text.Json's
+// compact form (the oracle's json::EncodePNC is the checker).  Pass 0: byte length per row; scan;
+// pass 1: each thread writes its row's bytes.
+__device__ __forceinline__ uint32_t dec_len(long long v) {
+    unsigned long long u = v < 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+    uint32_t n = v < 0 ? 2 : 1;
+    while (u >= 10) { u /= 10; ++n; }
+    return n;
+}
+
+template <int EB>
+__device__ __forceinline__ long long cell(const void* base, uint64_t i) {
+    if constexpr (EB == 4) return static_cast<const int*>(base)[i];
+    else return static_cast<const long long*>(base)[i];
+}
+
+struct Out {
+    uint8_t* p;
+    __device__ void put(char c) { *p++ = (uint8_t)c; }
+    __device__ void str(const char* s) { while (*s) put(*s++); }
+    __device__ void hex2(uint32_t b) {
+        const char* hx = "0123456789abcdef";
+        put(hx[(b >> 4) & 15]);
+        put(hx[b & 15]);
+    }
+    __device__ void guid(const Guid16& g) {  // Guid.ToString("D"): b3b2b1b0-b5b4-b7b6-b8b9-b10..b15
+        for (int k = 3; k >= 0; --k) hex2((uint32_t)(g.lo >> (8 * k)));
+        put('-');
+        hex2((uint32_t)(g.lo >> 40)); hex2((uint32_t)(g.lo >> 32));
+        put('-');
+        hex2((uint32_t)(g.lo >> 56)); hex2((uint32_t)(g.lo >> 48));
+        put('-');
+        hex2((uint32_t)g.hi); hex2((uint32_t)(g.hi >> 8));
+        put('-');
+        for (int k = 2; k < 8; ++k) hex2((uint32_t)(g.hi >> (8 * k)));
+    }
+    __device__ void dec(long long v) {
+        char d[20];
+        int n = 0;
+        unsigned long long u = v < 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+        do { d[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+        if (v < 0) put('-');
+        while (n) put(d[--n]);
+    }
+};
+
+template <int EB, int PASS>
+__global__ __launch_bounds__(kBlock) void k_encode(const uint32_t* __restrict__ rows, uint64_t n, Table t, const void* P, const void* N,
+                                                   unsigned long long* __restrict__ len_off, uint8_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t row = rows[i];
+    const uint32_t nc = t.ncols[row];
+    const uint64_t base = (uint64_t)row * t.R;
+    if (PASS == 0) {
+        unsigned long long len = 27 + (nc ? 2ull * (40ull * nc - 1) : 0);
+        for (uint32_t c = 0; c < nc; ++c) len += dec_len(cell<EB>(P, base + c)) + dec_len(cell<EB>(N, base + c));
+        len_off[i] = len;
+        return;
+    }
+    Out o{out + len_off[i]};
+    for (int which = 0; which < 2; ++which) {
+        o.str(which ? "},\"nVector\":{" : "{\"pVector\":{");
+        const void* V = which ? N : P;
+        for (uint32_t c = 0; c < nc; ++c) {
+            if (c) o.put(',');
+            o.put('"');
+            o.guid(t.cols[base + c]);
+            o.str("\":");
+            o.dec(cell<EB>(V, base + c));
+        }
+    }
+    o.str("}}");
+}
+
 void ensure_table(jg_pnc* p) {
     if (p->cols.p) return;
     JG_REQUIRE(p->R <= kMaxJsonReplicas, JG_EINVAL, "replica table: at most %u replicas per key (store has %u)", kMaxJsonReplicas, p->R);
@@ -768,6 +845,47 @@ int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out) {
 int jg_host_free(void* p) {
     return jg::guard([&] {
         if (p) JG_HIP(hipHostFree(p));
+    });
+}
+
+int jg_pnc_encode_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap) {
+    return jg::guard([&] {
+        JG_REQUIRE(p && off, JG_EINVAL, "jg_pnc_encode_json: NULL argument");
+        off[0] = 0;
+        if (n == 0) return;
+        JG_REQUIRE(key_idx, JG_EINVAL, "jg_pnc_encode_json: NULL key_idx");
+        JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "jg_pnc_encode_json: at most 2^31-1 rows per call");
+        for (uint64_t i = 0; i < n; ++i)
+            JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "jg_pnc_encode_json: key_idx[%llu] = %u out of range", (unsigned long long)i, key_idx[i]);
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        ensure_table(p);
+        const Table t = table_of(p);
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 4 + (n + 1) * 16 + 512));
+        auto* rows = reinterpret_cast<uint32_t*>(s);
+        auto* len = reinterpret_cast<unsigned long long*>(s + ((n * 4 + 255) & ~255ull));
+        auto* doff = len + n + 1;
+        JG_HIP(hipMemcpyAsync(rows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        const unsigned g = blocks_for(n);
+        if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr);
+        else hipLaunchKernelGGL((k_encode<4, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemsetAsync(len + n, 0, 8, ctx->stream));
+        size_t temp = 0;
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, len, doff, (int)(n + 1), ctx->stream));
+        void* tmp = jg::scratch(ctx, ctx->scratch3, temp + 256);
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, temp, len, doff, (int)(n + 1), ctx->stream));
+        JG_HIP(hipMemcpyAsync(off, doff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        if (!out) return;  // size query
+        JG_REQUIRE(off[n] <= cap, JG_ESTATE, "jg_pnc_encode_json: %llu bytes exceed cap %llu", (unsigned long long)off[n],
+                   (unsigned long long)cap);
+        auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
+        if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout);
+        else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
 

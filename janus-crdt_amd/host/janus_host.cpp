@@ -497,6 +497,21 @@ bool GpuStableStore::QueryStableORSet(const Guid& uid, const std::optional<std::
     return out != 0;
 }
 
+std::vector<std::string> GpuStableStore::EncodePNCStates(const std::vector<Guid>& uids) {
+    flush_registrations();
+    std::vector<uint32_t> rows;
+    rows.reserve(uids.size());
+    for (const Guid& u : uids) rows.push_back(ref(u, CrdtType::PNCounter).idx);
+    std::vector<uint64_t> off(rows.size() + 1, 0);
+    check(jg_pnc_encode_json(pnc_, rows.size(), rows.data(), off.data(), nullptr, 0));
+    std::string buf(off.back(), '\0');
+    check(jg_pnc_encode_json(pnc_, rows.size(), rows.data(), off.data(), reinterpret_cast<uint8_t*>(buf.data()), buf.size()));
+    std::vector<std::string> out;
+    out.reserve(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i) out.emplace_back(buf, off[i], off[i + 1] - off[i]);
+    return out;
+}
+
 std::vector<std::optional<std::string>> GpuStableStore::QueryStableLookupAll(const Guid& uid) {
     const uint32_t set = ref(uid, CrdtType::ORSet).idx;
     uint64_t off[2] = {0, 0};

@@ -125,6 +125,9 @@ class GpuStableStore {
     // OverflowException) and ORSet.Contains.
     int64_t QueryStablePNC(const Guid& uid);
     bool QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem);
+    // GetLastSynchronizedUpdate().Encode() of PN-Counter keys, encoded on the device — the payload
+    // SafeCRDT.Update ships after a client op (SafeCRDT.cs:49; batch producer).
+    std::vector<std::string> EncodePNCStates(const std::vector<Guid>& uids);
     // ORSetWrapper's enumeration / ORSet.LookupAll (ORSet.cs:204-227) in the reference's order.
     std::vector<std::optional<std::string>> QueryStableLookupAll(const Guid& uid);
 

@@ -104,6 +104,20 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         if (done != exp) { std::printf("FAIL safe-update notifications differ (%zu vs %zu)\n", done.size(), exp.size()); return 1; }
         n_done += done.size();
         ++n_waves;
+        // the encoded states (GetLastSynchronizedUpdate().Encode()) of every PN-Counter, byte for byte
+        {
+            std::vector<janus::Guid> uids;
+            for (int k = 0; k < n_pnc; ++k) uids.push_back(G(nodes[0]->safeCRDTs.at(keys[k])->guid));
+            const auto es = gpu.EncodePNCStates(uids), ep = gpu_p.EncodePNCStates(uids);
+            for (int k = 0; k < n_pnc; ++k) {
+                oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(keys[k]);
+                if (es[k] != oracle::json::EncodePNC(s0.pncStable->pnc.GetLastSynchronizedUpdate()) ||
+                    ep[k] != oracle::json::EncodePNC(s0.pncProspective->pnc.GetLastSynchronizedUpdate())) {
+                    std::printf("FAIL %s: encoded state differs\n%s\n", keys[k].c_str(), es[k].c_str());
+                    return 1;
+                }
+            }
+        }
         // compare every stable query on node 0
         for (int k = 0; k < (int)keys.size(); ++k) {
             oracle::SafeCRDT& s0 = *nodes[0]->safeCRDTs.at(keys[k]);

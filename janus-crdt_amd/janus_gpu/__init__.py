@@ -31,7 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
-    "jg_orset_lookup_all",
+    "jg_orset_lookup_all", "jg_pnc_encode_json",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -83,6 +83,7 @@ _SIGS = {
     "jg_pnc_wave_commit": ([_vp, C.POINTER(_u64)], C.c_int),
     "jg_pnc_wave_abort": ([_vp], C.c_int),
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -301,6 +302,16 @@ class PNCStore:
     def wave_abort(self) -> None:
         _check(load().jg_pnc_wave_abort(self._h))
         self._chunks = []
+
+    def encode_json(self, key_idx) -> list:
+        """GetLastSynchronizedUpdate().Encode() of each row (jg_pnc_encode_json): list of bytes."""
+        k = _arr(key_idx, np.uint32)
+        off = np.zeros(k.size + 1, np.uint64)
+        _check(load().jg_pnc_encode_json(self._h, k.size, _ptr(k), _ptr(off), None, 0))
+        out = np.empty(max(16, int(off[-1])), np.uint8)
+        _check(load().jg_pnc_encode_json(self._h, k.size, _ptr(k), _ptr(off), _ptr(out), out.size))
+        b = out.tobytes()
+        return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
 
     def merge_wave(self, wave: "Wave") -> None:
         bad = _u64(0)
