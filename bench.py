@@ -92,8 +92,11 @@ class HipEvents:
 
     def __init__(self, stream: int):
         import ctypes as C
+        import janus_gpu as jg
         self.C = C
-        self.hip = C.CDLL("libamdhip64.so")
+        # the HIP runtime libjanusgpu is bound to (dlsym through its handle searches its dependencies):
+        # a second libamdhip64 instance in the process would not know the library's stream
+        self.hip = jg.load()
         self.stream = C.c_void_p(stream)
         self.e = [C.c_void_p(), C.c_void_p()]
         for e in self.e:
@@ -202,6 +205,43 @@ def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
             "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
 
 
+EXCH_KEYS, EXCH_ROWS = 2_000_000, 1_000_000  # per rank: owned shard, received batch (global keys)
+
+
+def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
+    """Cross-shard exchange: every rank receives a batch of EXCH_ROWS PN-Counter
+    rows whose keys are uniform over the WHOLE keyspace (world x EXCH_KEYS), routes it on its GPU
+    (jg_rows_route), exchanges the runs with one RCCL all-to-all per buffer over xGMI, and merges what
+    it owns from device memory (jg_pnc_merge_device).  At world 1 there is nothing to exchange: route +
+    merge only."""
+    import numpy as np
+    import torch
+    from janus_gpu import shard
+    dev = torch.device("cuda", local)
+    ex = shard.Exchange(dev) if world > 1 else None
+    store = jg.PNCStore(ctx, EXCH_KEYS, PNC_R, PNC_EB)
+    rows = jg.Rows(ctx, EXCH_ROWS, PNC_R, PNC_EB)
+    try:
+        store.synth(SEED + 7 + rank)
+        keys = np.random.default_rng(SEED + rank).integers(0, world * EXCH_KEYS, EXCH_ROWS, dtype=np.uint32)
+        zeros = np.zeros((EXCH_ROWS, PNC_R), np.int64)
+        rows.upload(zeros, zeros, keys)   # the key indices; values synthesised on the device next
+        rows.synth(SEED + 11 + rank)
+        last = {}
+        wall, _ = timed(ctx, sync, lambda: last.update(shard.exchange_pnc(store, rows, ex, dev)), steps, warmup)
+    finally:
+        store.close()
+        rows.close()
+    row_bytes = 4 + 2 * PNC_R * PNC_EB
+    sent = last["sent"].astype(np.int64)
+    remote = int(sent.sum() - sent[rank]) if world > 1 else 0
+    return {"workload": f"cross-shard exchange: {EXCH_ROWS} received PN-Counter rows per rank (64 replicas, int64, keys "
+                        f"uniform over {world} x {EXCH_KEYS} keys): route + all-to-all + merge from device memory",
+            "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
+            "xgmi_bytes_per_rank": remote * row_bytes, "row_bytes": row_bytes,
+            "collective": "torch.distributed all_to_all_single over RCCL" if world > 1 else "none (world 1)"}
+
+
 def bench_apply_loop(sync, rank, world, local):
     """C5 committed-batch apply through the C++ host mirror, on every rank.  Every
     rank applies the same committed waves to the accounts it owns (GpuStableStore::ShardOf; other
@@ -256,7 +296,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset"], default="all")
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnc-shape", choices=sorted(PNC_SHAPES), default="c2",
                     help="per-GPU PN-Counter shard: c2 = BASELINE configs[1] (default), c4 = 1/8 of configs[3]")
@@ -265,6 +305,10 @@ def main():
     world, rank, local = dist_env()
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    if world > 1 or args.workload in ("all", "exchange"):
+        # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
+        # instance (torch's libraries also name the runtime by an unversioned soname)
+        import torch  # noqa: F401
     sync = Sync(world, local)
     import janus_gpu as jg
     ctx = jg.Context(local)
@@ -274,6 +318,8 @@ def main():
         res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape)
     if args.workload in ("all", "orset", "pnc-orset"):
         res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
+    if args.workload in ("all", "exchange"):
+        res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
     ctx.close()
 
     cpu = None
@@ -327,6 +373,8 @@ def main():
         if "value" not in line:
             line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,
                          "dtype": "u64+u128 records", "config": {"workload": line["orset"]["workload"]}})
+    if "exchange" in res:
+        line["exchange"] = res["exchange"]
     if apply_loop is not None:
         line["apply_loop"] = apply_loop
     line["cpu_baseline"] = cpu

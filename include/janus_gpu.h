@@ -194,11 +194,40 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
 int jg_orset_lookup_all(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* off, uint32_t* elems, uint64_t cap);
 
 /* ---------------------------------------------------------------------------------------------
+ * Cross-shard exchange (csrc/route.hip).  The keyspace of a node is sharded over
+ * its GPUs: global key k (PN-Counter row / OR-Set set id) belongs to rank k % world, where it is
+ * local key k / world.  The reference has one process per node and no sharding: these entry points
+ * serve the sharded deployment of the same stores (one process per GPU) when a received batch
+ * lands on a rank that does not own all of its keys — the received states still reach
+ * PNCounter.Merge (PNCounters.cs:131-144) / ORSet.Merge (ORSet.cs:253-283) on the owner.
+ * EXCEPTION to the host-pointer rule above: the d_* arguments are caller-owned DEVICE memory of the
+ * context's device (the collective's send / receive buffers, e.g. RCCL all-to-all over xGMI); the
+ * library checks that they are device memory of that device and large enough, and returns after
+ * its stream is idle.
+ * ------------------------------------------------------------------------------------------- */
+/* Stable partition of a device batch by owner rank: d_keys[n_rows] (local keys), d_P/d_N[n_rows x R]
+ * receive the rows grouped by destination rank in batch order; counts[world] (host) = rows per
+ * destination.  world in [1, 64]; cap_rows >= the batch's rows. */
+int jg_rows_route(const jg_rows* rows, uint32_t world, uint64_t* counts, void* d_keys, void* d_P, void* d_N, uint64_t cap_rows);
+/* jg_pnc_merge_rows from device memory: rows (d_keys[i], d_P[i], d_N[i]), ABSENT cells skipped, keys
+ * may repeat; all or nothing (JG_EINVAL if any key >= n_keys, nothing merged). */
+int jg_pnc_merge_device(jg_pnc* pnc, uint64_t n_rows, const void* d_keys, const void* d_P, const void* d_N);
+/* Stable partition of both record streams of a store by owner rank (set id % world; set ids
+ * rewritten to set / world): keys (8 B) and tags (16 B, jg_tagrec order) per stream. */
+int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* rem_counts, void* d_add_key, void* d_add_tag,
+                   uint64_t cap_add, void* d_rem_key, void* d_rem_tag, uint64_t cap_rem);
+/* ORSet.Merge of n_runs received runs (run r = add_counts[r] adds and rem_counts[r] tombstones,
+ * stored run after run; each sorted strictly increasing, JG_ESTATE otherwise) into the store. */
+int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const void* d_add_key,
+                          const void* d_add_tag, const void* d_rem_key, const void* d_rem_tag);
+
+/* ---------------------------------------------------------------------------------------------
  * Synthetic workloads (bench / size-independent parity): device-side counter-based generators,
  * defined in DESIGN.md §Synthetic inputs and mirrored on the host by the test oracle.
  * ------------------------------------------------------------------------------------------- */
 /* which: 0 = local P, 1 = local N, 2 = received P, 3 = received N.  Local unseen cells are 0;
- * received unseen cells are ABSENT. */
+ * received unseen cells are ABSENT.  jg_synth_pnc_rows fills the values of row i from synthetic key
+ * key0 + i and keeps the batch's key indices (identity unless uploaded). */
 int jg_synth_pnc_store(jg_pnc* pnc, uint64_t seed);
 int jg_synth_pnc_rows(jg_rows* rows, uint64_t seed, uint64_t key0);
 /* Fill a store with n_groups (set, elem) groups (group g = set*elems_per_set + elem): adds carry

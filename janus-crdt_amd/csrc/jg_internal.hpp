@@ -133,4 +133,9 @@ void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
 // Dense chunk metadata for a stream whose n records sit contiguously in slots [0, n) (async).
 void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n);
+// pnc.hip: scatter-max of n_rows device rows into the store's keys (async on the store's stream).
+void pnc_merge_indexed(jg_pnc* p, const void* BP, const void* BN, const uint32_t* d_keys, uint64_t n_rows);
+// orset.hip: merge n_runs sorted, duplicate-free runs (device SoA, run after run) into the store.
+void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const unsigned long long* add_key,
+                      const uint4* add_tag, const unsigned long long* rem_key, const uint4* rem_tag);
 }  // namespace jg

@@ -18,6 +18,7 @@
 // ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams
 // (rank space), then SetEquals of the two sorted runs.
 #include <algorithm>
+#include <memory>
 #include <set>
 #include <unordered_map>
 #include <vector>
@@ -481,6 +482,57 @@ void sync_counts(jg_orset* s) {
     s->add.n = h[0];
     s->rem.n = h[1];
     s->counts_pending = false;
+}
+
+// Runs received from the other shards (csrc/route.hip): each run is one source's records for this
+// owner, sorted and duplicate-free (a stable partition of a sorted stream; the set-id rewrite is
+// monotone within one owner).  Each run is copied into a dense stream and checked, the runs are
+// unioned pairwise (log2(n_runs) levels), and the result is merged into the store: the same
+// ORSet.Merge per set as jg_orset_merge, from device memory.
+void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const unsigned long long* add_key,
+                      const uint4* add_tag, const unsigned long long* rem_key, const uint4* rem_tag) {
+    jg_ctx* ctx = s->ctx;
+    sync_counts(s);
+    auto fresh = [ctx] {
+        auto t = std::make_unique<jg_orset>();
+        t->ctx = ctx;
+        t->counts.alloc(16);
+        return t;
+    };
+    auto fill = [ctx](jg_stream_soa& st, const unsigned long long* k, const uint4* t, uint64_t n) {
+        set_dense(ctx, st, n);
+        if (n == 0) return;
+        JG_HIP(hipMemcpyAsync(st.key.p, k, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(st.tag.p, t, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st.key.as<unsigned long long>(),
+                           st.tag.as<uint4>(), n, ctx->flags.as<unsigned>());
+        JG_HIP(hipGetLastError());
+    };
+    std::vector<std::unique_ptr<jg_orset>> level;
+    uint64_t ao = 0, ro = 0;
+    for (uint32_t r = 0; r < n_runs; ++r) {
+        if (add_counts[r] + rem_counts[r] > 0) {
+            auto t = fresh();
+            fill(t->add, add_key + ao, add_tag + ao, add_counts[r]);
+            fill(t->rem, rem_key + ro, rem_tag + ro, rem_counts[r]);
+            level.push_back(std::move(t));
+        }
+        ao += add_counts[r];
+        ro += rem_counts[r];
+    }
+    check_err_flag(ctx, "jg_orset_merge_device (a received run is not strictly increasing)");
+    while (level.size() > 1) {
+        std::vector<std::unique_ptr<jg_orset>> next;
+        for (size_t i = 0; i + 1 < level.size(); i += 2) {
+            auto o = fresh();
+            union_store(ctx, level[i].get(), level[i + 1].get(), o->add, o->rem, o.get());
+            next.push_back(std::move(o));
+        }
+        if (level.size() % 2) next.push_back(std::move(level.back()));
+        for (auto& o : next) sync_counts(o.get());
+        level = std::move(next);
+    }
+    if (!level.empty()) merge_into(s, level[0].get(), false);
 }
 }  // namespace jg
 

@@ -248,6 +248,10 @@ void launch_rows_copy(jg_ctx* ctx, uint32_t eb, void* dst, const void* src, cons
 
 }  // namespace
 
+void jg::pnc_merge_indexed(jg_pnc* p, const void* BP, const void* BN, const uint32_t* d_keys, uint64_t n_rows) {
+    launch_merge_indexed(p->ctx, p->eb, p->P.p, p->N.p, BP, BN, d_keys, n_rows, p->R);
+}
+
 extern "C" {
 
 int jg_pnc_create(jg_ctx* ctx, uint64_t n_keys, uint32_t n_replicas, uint32_t elem_bytes, jg_pnc** out) {

@@ -77,8 +77,7 @@ int jg_synth_pnc_rows(jg_rows* r, uint64_t seed, uint64_t key0) {
         JG_REQUIRE(r, JG_EINVAL, "jg_synth_pnc_rows: rows is NULL");
         jg::ensure_device(r->ctx);
         if (r->eb == 8) fill_pnc<long long>(r->ctx, r->P.p, r->N.p, key0, r->n_rows, r->R, 2, seed);
-        else fill_pnc<int>(r->ctx, r->P.p, r->N.p, key0, r->n_rows, r->R, 2, seed);
-        r->has_keys = false;
+        else fill_pnc<int>(r->ctx, r->P.p, r->N.p, key0, r->n_rows, r->R, 2, seed);  // key indices (if uploaded) are kept
         JG_HIP(hipStreamSynchronize(r->ctx->stream));
     });
 }

@@ -32,6 +32,7 @@ EXPORTS = [
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
     "jg_orset_lookup_all", "jg_pnc_encode_json",
+    "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -84,6 +85,10 @@ _SIGS = {
     "jg_pnc_wave_abort": ([_vp], C.c_int),
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
+    "jg_orset_merge_device": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -193,6 +198,13 @@ class Rows:
     def synth(self, seed: int, key0: int = 0) -> None:
         _check(load().jg_synth_pnc_rows(self._h, seed, key0))
 
+    def route(self, world: int, d_keys: int, d_P: int, d_N: int, cap_rows: int | None = None) -> np.ndarray:
+        """jg_rows_route: stable partition of the batch by owner rank (key % world) into caller DEVICE
+        buffers (raw addresses); returns the rows per destination."""
+        counts = np.zeros(world, np.uint64)
+        _check(load().jg_rows_route(self._h, world, _ptr(counts), d_keys, d_P, d_N, self.n_rows if cap_rows is None else cap_rows))
+        return counts
+
     def close(self) -> None:
         if self._h:
             _check(load().jg_rows_destroy(self._h))
@@ -236,6 +248,10 @@ class PNCStore:
 
     def merge_batch(self, rows: Rows, async_: bool = False) -> None:
         _check(load().jg_pnc_merge_batch(self._h, rows._h, 1 if async_ else 0))
+
+    def merge_device(self, n_rows: int, d_keys: int, d_P: int, d_N: int) -> None:
+        """jg_pnc_merge_device: merge rows held in caller DEVICE memory (raw addresses)."""
+        _check(load().jg_pnc_merge_device(self._h, n_rows, d_keys, d_P, d_N))
 
     def apply_ops(self, key, col, delta, is_n) -> None:
         key, col = _arr(key, np.uint32), _arr(col, np.uint32)
@@ -411,6 +427,20 @@ class ORSetStore:
         out = np.empty(max(1, int(off[-1])), np.uint32)
         _check(load().jg_orset_lookup_all(self._h, s.size, _ptr(s), _ptr(off), _ptr(out), out.size))
         return [out[int(off[i]):int(off[i + 1])] for i in range(s.size)]
+
+    def route(self, world: int, d_add_key: int, d_add_tag: int, cap_add: int, d_rem_key: int, d_rem_tag: int, cap_rem: int):
+        """jg_orset_route: both streams partitioned by owner rank (set % world, set ids rewritten to
+        set // world) into caller DEVICE buffers; returns (add counts, tombstone counts) per rank."""
+        ca, cr = np.zeros(world, np.uint64), np.zeros(world, np.uint64)
+        _check(load().jg_orset_route(self._h, world, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, cap_add, d_rem_key, d_rem_tag, cap_rem))
+        return ca, cr
+
+    def merge_device(self, add_counts, rem_counts, d_add_key: int, d_add_tag: int, d_rem_key: int, d_rem_tag: int) -> None:
+        """jg_orset_merge_device: merge received runs (run r = add_counts[r] / rem_counts[r] records,
+        stored run after run in caller DEVICE buffers)."""
+        ca, cr = _arr(add_counts, np.uint64), _arr(rem_counts, np.uint64)
+        assert ca.size == cr.size
+        _check(load().jg_orset_merge_device(self._h, ca.size, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, d_rem_key, d_rem_tag))
 
     def synth(self, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0) -> None:
         _check(load().jg_synth_orset(self._h, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0))

@@ -15,6 +15,11 @@ for p in (ROOT / "janus-crdt_amd", ROOT / "tests", ROOT):
         sys.path.insert(0, str(p))
 
 
+# torch (device buffers, collectives in the shard tests) loads before libjanusgpu so the process holds
+# ONE HIP runtime instance, as in bench.py
+import torch  # noqa: E402,F401
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) and the built libjanusgpu.so")
 

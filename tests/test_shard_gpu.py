@@ -1,0 +1,389 @@
+"""GPU parity of the cross-shard exchange (csrc/route.hip, janus_gpu/shard.py) against the host route
+rule (tests/shard_ref.py) and the oracle's PNCounter.Merge / ORSet.Merge.
+
+* route kernels: bit-exact stable partitions (counts, local keys, rows / records) for world 1..8,
+  int32 / int64 rows, 16-B-vector and ragged row widths, identity and indexed batches, tile edges;
+* merge from device memory: equal to jg_pnc_merge_rows / the oracle, all or nothing on bad keys;
+* a keyspace sharded over W "ranks" in one process (routing without a collective): every owner's
+  shard equals its slice of the oracle merge of the whole keyspace;
+* two processes sharing device 0 over gloo (host-staged all-to-all): the full exchange path with the
+  real kernels (the RCCL transport itself runs in bench.py on the 8-GPU node).
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import janus_gpu as jg
+import oracle_ref as orc
+import shard_ref as ref
+from gen import random_orset_pair, random_pnc
+from janus_gpu import shard
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def _dev(ctx):
+    return torch.device("cuda", ctx.device)
+
+
+def _route_rows(ctx, keys, P, N, world, eb):
+    n, R = P.shape
+    rows = jg.Rows(ctx, n, R, eb)
+    rows.upload(P, N, keys)
+    dt = torch.int64 if eb == 8 else torch.int32
+    k = torch.empty(n, dtype=torch.int32, device=_dev(ctx))
+    dP = torch.empty((n, R), dtype=dt, device=_dev(ctx))
+    dN = torch.empty((n, R), dtype=dt, device=_dev(ctx))
+    counts = rows.route(world, k.data_ptr(), dP.data_ptr(), dN.data_ptr())
+    rows.close()
+    return counts, k.cpu().numpy().astype(np.uint32), dP.cpu().numpy(), dN.cpu().numpy()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("eb,R", [(8, 64), (4, 64), (8, 5), (4, 3)])
+@pytest.mark.parametrize("n", [1, 1023, 1024, 1025, 20_000])
+def test_rows_route_matches_host_rule(ctx, world, eb, R, n):
+    rng = np.random.default_rng(world * 1000 + n + R)
+    keys = rng.integers(0, 5 * n + 7, n).astype(np.uint32)
+    P, N = random_pnc(rng, n, R, eb), random_pnc(rng, n, R, eb)
+    got = _route_rows(ctx, keys, P, N, world, eb)
+    exp = ref.route_rows(keys, P, N, world)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+
+
+def test_identity_rows_route(ctx):
+    rng = np.random.default_rng(5)
+    n, R, world = 3000, 8, 4
+    P, N = random_pnc(rng, n, R, 8), random_pnc(rng, n, R, 8)
+    rows = jg.Rows(ctx, n, R, 8)
+    rows.upload(P, N)  # no key_idx: row i is key i
+    k = torch.empty(n, dtype=torch.int32, device=_dev(ctx))
+    dP = torch.empty((n, R), dtype=torch.int64, device=_dev(ctx))
+    dN = torch.empty_like(dP)
+    counts = rows.route(world, k.data_ptr(), dP.data_ptr(), dN.data_ptr())
+    rows.close()
+    exp = ref.route_rows(np.arange(n, dtype=np.uint32), P, N, world)
+    assert np.array_equal(counts, exp[0]) and np.array_equal(k.cpu().numpy(), exp[1])
+    assert np.array_equal(dP.cpu().numpy(), exp[2]) and np.array_equal(dN.cpu().numpy(), exp[3])
+
+
+def test_route_rejects_bad_buffers(ctx):
+    rows = jg.Rows(ctx, 100, 4, 8)
+    rows.upload(np.zeros((100, 4), np.int64), np.zeros((100, 4), np.int64), np.arange(100, dtype=np.uint32))
+    small = torch.empty(10, dtype=torch.int64, device=_dev(ctx))
+    big = torch.empty((100, 4), dtype=torch.int64, device=_dev(ctx))
+    host = np.zeros((100, 4), np.int64)
+    with pytest.raises(jg.JanusError) as e:
+        rows.route(2, big.data_ptr(), big.data_ptr(), host.ctypes.data)  # host memory
+    assert e.value.code == jg.JG_EINVAL
+    with pytest.raises(jg.JanusError):
+        rows.route(0, big.data_ptr(), big.data_ptr(), big.data_ptr())    # world 0
+    with pytest.raises(jg.JanusError):
+        rows.route(2, big.data_ptr(), big.data_ptr(), big.data_ptr(), cap_rows=99)
+    del small
+    rows.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
+def test_merge_device_matches_oracle_and_is_all_or_nothing(ctx, eb):
+    rng = np.random.default_rng(11 + eb)
+    K, R, n = 300, 16, 5000
+    AP, AN = random_pnc(rng, K, R, eb, absent=False), random_pnc(rng, K, R, eb, absent=False)
+    BP, BN = random_pnc(rng, n, R, eb), random_pnc(rng, n, R, eb)
+    keys = rng.integers(0, K, n).astype(np.uint32)
+    s = jg.PNCStore(ctx, K, R, eb)
+    s.write_rows(AP, AN)
+    dev = _dev(ctx)
+    dk = torch.from_numpy(keys.astype(np.int32)).to(dev)
+    dP, dN = torch.from_numpy(BP).to(dev), torch.from_numpy(BN).to(dev)
+    torch.cuda.synchronize(dev)
+    s.merge_device(n, dk.data_ptr(), dP.data_ptr(), dN.data_ptr())
+    eP, eN = orc.pnc_merge(AP, AN, BP, BN, keys)
+    P, N = s.read_rows()
+    assert np.array_equal(P, eP) and np.array_equal(N, eN)
+    bad = dk.clone()
+    bad[n // 2] = K  # one key outside the store: nothing merges
+    torch.cuda.synchronize(dev)
+    with pytest.raises(jg.JanusError) as e:
+        s.merge_device(n, bad.data_ptr(), dP.data_ptr(), dN.data_ptr())
+    assert e.value.code == jg.JG_EINVAL
+    P2, N2 = s.read_rows()
+    assert np.array_equal(P2, eP) and np.array_equal(N2, eN)
+    s.close()
+
+
+@pytest.mark.parametrize("world", [2, 4, 7])
+def test_pnc_sharded_keyspace_in_one_process(ctx, world):
+    """W ranks simulated in one process: each routes its batch; each owner merges every source's run
+    (source order) from device memory; owner shards = slices of the oracle's global merge."""
+    rng = np.random.default_rng(40 + world)
+    K_local, R, n = 257, 64, 4000
+    G = K_local * world
+    AP, AN = random_pnc(rng, G, R, 8, absent=False, lo=0), random_pnc(rng, G, R, 8, absent=False, lo=0)
+    batches = [(rng.integers(0, G, n).astype(np.uint32), random_pnc(rng, n, R, 8), random_pnc(rng, n, R, 8)) for _ in range(world)]
+    routed = [_route_rows(ctx, k, P, N, world, 8) for k, P, N in batches]
+    eP, eN = AP, AN
+    for k, P, N in batches:
+        eP, eN = orc.pnc_merge(eP, eN, P, N, k)
+    dev = _dev(ctx)
+    for d in range(world):
+        s = jg.PNCStore(ctx, K_local, R, 8)
+        s.write_rows(ref.shard_rows(AP, world, d), ref.shard_rows(AN, world, d))
+        parts = []
+        for counts, k, P, N in routed:
+            lo = int(counts[:d].sum())
+            hi = lo + int(counts[d])
+            parts.append((k[lo:hi], P[lo:hi], N[lo:hi]))
+        k = torch.from_numpy(np.concatenate([p[0] for p in parts]).astype(np.int32)).to(dev)
+        P = torch.from_numpy(np.concatenate([p[1] for p in parts])).to(dev)
+        N = torch.from_numpy(np.concatenate([p[2] for p in parts])).to(dev)
+        torch.cuda.synchronize(dev)
+        s.merge_device(k.numel(), k.data_ptr(), P.data_ptr(), N.data_ptr())
+        gP, gN = s.read_rows()
+        s.close()
+        assert np.array_equal(gP, ref.shard_rows(eP, world, d)) and np.array_equal(gN, ref.shard_rows(eN, world, d))
+
+
+def _route_store(ctx, add, rem, world):
+    src = jg.ORSetStore(ctx, len(add), len(rem))
+    src.load(add, rem)
+    dev = _dev(ctx)
+    na, nr = len(add), len(rem)
+    ak, rk = torch.empty(na, dtype=torch.int64, device=dev), torch.empty(nr, dtype=torch.int64, device=dev)
+    at, rt = torch.empty((na, 2), dtype=torch.int64, device=dev), torch.empty((nr, 2), dtype=torch.int64, device=dev)
+    ca, cr = src.route(world, ak.data_ptr(), at.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), nr)
+    src.close()
+
+    def recs(k, t):
+        r = np.empty(k.shape[0], jg.REC_DTYPE)
+        r["key"] = k.cpu().numpy().view(np.uint64)
+        tt = t.cpu().numpy().view(np.uint64).reshape(-1, 2)
+        r["tag_lo"], r["tag_hi"] = tt[:, 0], tt[:, 1]
+        return r
+
+    return ca, cr, recs(ak, at), recs(rk, rt)
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+@pytest.mark.parametrize("n_sets", [5, 2000])
+def test_orset_route_matches_host_rule(ctx, world, n_sets):
+    rng = np.random.default_rng(n_sets + world)
+    La, Lr, _, _ = random_orset_pair(rng, n_sets=n_sets, n_elems=6, pool=8)
+    ca, cr, ga, gr = _route_store(ctx, La, Lr, world)
+    ea, er = ref.route_records(La, world), ref.route_records(Lr, world)
+    assert np.array_equal(ca, ea[0]) and np.array_equal(ga, ea[1])
+    assert np.array_equal(cr, er[0]) and np.array_equal(gr, er[1])
+
+
+def test_orset_route_of_a_union_output(ctx):
+    """Route a chunked (non-dense) stream: the output of a union, whose chunks are partly full."""
+    rng = np.random.default_rng(8)
+    La, Lr, Ra, Rr = random_orset_pair(rng, n_sets=3000, n_elems=5, pool=6)
+    a, b = jg.ORSetStore(ctx, len(La), len(Lr)), jg.ORSetStore(ctx, len(Ra), len(Rr))
+    a.load(La, Lr)
+    b.load(Ra, Rr)
+    a.merge_store(b)
+    na, nr = a.size()
+    dev = _dev(ctx)
+    ak, rk = torch.empty(na, dtype=torch.int64, device=dev), torch.empty(nr, dtype=torch.int64, device=dev)
+    at, rt = torch.empty((na, 2), dtype=torch.int64, device=dev), torch.empty((nr, 2), dtype=torch.int64, device=dev)
+    ca, cr = a.route(5, ak.data_ptr(), at.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), nr)
+    ea, er = orc.orset_merge(La, Lr, Ra, Rr)
+    assert np.array_equal(ca, ref.route_records(ea, 5)[0]) and np.array_equal(cr, ref.route_records(er, 5)[0])
+    assert np.array_equal(ak.cpu().numpy().view(np.uint64), ref.route_records(ea, 5)[1]["key"])
+    for h in (a, b):
+        h.close()
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_orset_sharded_keyspace_in_one_process(ctx, world):
+    rng = np.random.default_rng(70 + world)
+    n_sets = 60 * world
+    La, Lr, _, _ = random_orset_pair(rng, n_sets=n_sets, n_elems=5, pool=10)
+    recv = [random_orset_pair(rng, n_sets=n_sets, n_elems=5, pool=10)[2:] for _ in range(world)]
+    routed = [_route_store(ctx, a, r, world) for a, r in recv]
+    ea, er = La, Lr
+    for a, r in recv:
+        ea, er = orc.orset_merge(ea, er, a, r)
+    dev = _dev(ctx)
+    for d in range(world):
+        s = jg.ORSetStore(ctx, 0, 0)
+        s.load(ref.shard_records(La, world, d), ref.shard_records(Lr, world, d))
+        runs_a, runs_r, cnt_a, cnt_r = [], [], [], []
+        for ca, cr, ga, gr in routed:
+            a0, r0 = int(ca[:d].sum()), int(cr[:d].sum())
+            runs_a.append(ga[a0:a0 + int(ca[d])])
+            runs_r.append(gr[r0:r0 + int(cr[d])])
+            cnt_a.append(int(ca[d]))
+            cnt_r.append(int(cr[d]))
+        A, Rm = np.concatenate(runs_a), np.concatenate(runs_r)
+        ak = torch.from_numpy(A["key"].view(np.int64).copy()).to(dev)
+        at = torch.from_numpy(np.stack([A["tag_lo"], A["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+        rk = torch.from_numpy(Rm["key"].view(np.int64).copy()).to(dev)
+        rt = torch.from_numpy(np.stack([Rm["tag_lo"], Rm["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+        torch.cuda.synchronize(dev)
+        s.merge_device(cnt_a, cnt_r, ak.data_ptr(), at.data_ptr(), rk.data_ptr(), rt.data_ptr())
+        ga, gr = s.read()
+        s.close()
+        assert np.array_equal(ga, ref.shard_records(ea, world, d)) and np.array_equal(gr, ref.shard_records(er, world, d))
+
+
+def test_orset_merge_device_rejects_unsorted_run(ctx):
+    rng = np.random.default_rng(2)
+    La, Lr, Ra, _ = random_orset_pair(rng, n_sets=20, n_elems=4, pool=6)
+    s = jg.ORSetStore(ctx, len(La), len(Lr))
+    s.load(La, Lr)
+    bad = Ra[::-1].copy()
+    dev = _dev(ctx)
+    ak = torch.from_numpy(bad["key"].view(np.int64).copy()).to(dev)
+    at = torch.from_numpy(np.stack([bad["tag_lo"], bad["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+    e0 = torch.empty(0, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    with pytest.raises(jg.JanusError) as e:
+        s.merge_device([len(bad)], [0], ak.data_ptr(), at.data_ptr(), e0.data_ptr(), e0.data_ptr())
+    assert e.value.code == jg.JG_ESTATE
+    ga, gr = s.read()  # unchanged
+    assert np.array_equal(ga, La) and np.array_equal(gr, Lr)
+    s.close()
+
+
+# ---- two processes on device 0, gloo (host-staged) all-to-all through janus_gpu.shard ----
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+def _two_rank_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    for p in (ROOT / "janus-crdt_amd", ROOT / "tests"):
+        sys.path.insert(0, str(p))
+    import torch.distributed as dist
+    import janus_gpu as jg_
+    import oracle_ref as orc_
+    import shard_ref as ref_
+    from gen import random_orset_pair as rop, random_pnc as rpnc
+    from janus_gpu import shard as sh
+    dist.init_process_group("gloo")
+    try:
+        dev = torch.device("cuda", 0)
+        ex = sh.Exchange(dev)
+        rng = np.random.default_rng(123)
+        K_local, R, n = 500, 64, 3000
+        G = K_local * world
+        AP, AN = rpnc(rng, G, R, 8, absent=False, lo=0), rpnc(rng, G, R, 8, absent=False, lo=0)
+        batches = [(rng.integers(0, G, n).astype(np.uint32), rpnc(rng, n, R, 8), rpnc(rng, n, R, 8)) for _ in range(world)]
+        La, Lr, _, _ = rop(rng, n_sets=40 * world, n_elems=5, pool=8)
+        recv = [rop(rng, n_sets=40 * world, n_elems=5, pool=8)[2:] for _ in range(world)]
+        with jg_.Context(0) as ctx:
+            s = jg_.PNCStore(ctx, K_local, R, 8)
+            s.write_rows(ref_.shard_rows(AP, world, rank), ref_.shard_rows(AN, world, rank))
+            rows = jg_.Rows(ctx, n, R, 8)
+            k, P, N = batches[rank]
+            rows.upload(P, N, k)
+            sh.exchange_pnc(s, rows, ex, dev)
+            gP, gN = s.read_rows()
+            eP, eN = AP, AN
+            for kk, PP, NN in batches:
+                eP, eN = orc_.pnc_merge(eP, eN, PP, NN, kk)
+            ok_pnc = np.array_equal(gP, ref_.shard_rows(eP, world, rank)) and np.array_equal(gN, ref_.shard_rows(eN, world, rank))
+            o = jg_.ORSetStore(ctx, 0, 0)
+            o.load(ref_.shard_records(La, world, rank), ref_.shard_records(Lr, world, rank))
+            src = jg_.ORSetStore(ctx, 0, 0)
+            src.load(*recv[rank])
+            sh.exchange_orset(o, src, ex, dev)
+            ga, gr = o.read()
+            ea, er = La, Lr
+            for a, r in recv:
+                ea, er = orc_.orset_merge(ea, er, a, r)
+            ok_orset = np.array_equal(ga, ref_.shard_records(ea, world, rank)) and np.array_equal(gr, ref_.shard_records(er, world, rank))
+            for h in (s, rows, o, src):
+                h.close()
+        q.put((rank, ok_pnc, ok_orset, ""))
+    except Exception as e:
+        q.put((rank, False, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_share_device_0_over_gloo():
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted(q.get(timeout=100) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_pnc, ok_orset, err in res:
+        assert not err, f"rank {rank}: {err}"
+        assert ok_pnc and ok_orset, (rank, ok_pnc, ok_orset)
+
+
+# ---- the RCCL path (backend "nccl", device buffers handed to all_to_all_single) at world size 1 ----
+def _rccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    for p in (ROOT / "janus-crdt_amd", ROOT / "tests"):
+        sys.path.insert(0, str(p))
+    import torch.distributed as dist
+    import janus_gpu as jg_
+    import oracle_ref as orc_
+    from gen import random_pnc as rpnc
+    from janus_gpu import shard as sh
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    try:
+        ex = sh.Exchange(dev)
+        assert not ex.staged
+        rng = np.random.default_rng(5)
+        K, R, n = 800, 64, 5000
+        AP, AN = rpnc(rng, K, R, 8, absent=False, lo=0), rpnc(rng, K, R, 8, absent=False, lo=0)
+        k, P, N = rng.integers(0, K, n).astype(np.uint32), rpnc(rng, n, R, 8), rpnc(rng, n, R, 8)
+        with jg_.Context(0) as ctx:
+            s = jg_.PNCStore(ctx, K, R, 8)
+            s.write_rows(AP, AN)
+            rows = jg_.Rows(ctx, n, R, 8)
+            rows.upload(P, N, k)
+            out = sh.exchange_pnc(s, rows, ex, dev)
+            gP, gN = s.read_rows()
+            eP, eN = orc_.pnc_merge(AP, AN, P, N, k)
+            ok = np.array_equal(gP, eP) and np.array_equal(gN, eN) and int(out["received"].sum()) == n
+            s.close()
+            rows.close()
+        q.put((ok, ""))
+    except Exception as e:
+        q.put((False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_exchange_world1():
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    p = ctxm.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        ok, err = q.get(timeout=100)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert not err, err
+    assert ok
