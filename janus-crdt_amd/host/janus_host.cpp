@@ -239,17 +239,41 @@ char* GpuStableStore::chunk_buffer(size_t c, size_t bytes) {
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                                      std::unordered_map<uint64_t, uint64_t>* tracker) {
     const double t0 = wall_s();
-    flush_registrations();
     std::vector<const NetworkProtocol*> msgs;
-    {
-        size_t n_msgs = 0;
-        for (const auto& list : updates)
-            for (const auto& block : list) n_msgs += block.update.size();
-        msgs.reserve(n_msgs);
-        for (const auto& list : updates)
-            for (const auto& block : list)
-                for (const auto& u : block.update) msgs.push_back(&u);
+    size_t n_msgs = 0;
+    for (const auto& list : updates)
+        for (const auto& block : list) n_msgs += block.update.size();
+    msgs.reserve(n_msgs);
+    for (const auto& list : updates)
+        for (const auto& block : list)
+            for (const auto& u : block.update) msgs.push_back(&u);
+    return apply_msgs(msgs, tracker, t0);
+}
+
+void GpuStableStore::ReceivedBlock(const std::vector<UpdateMessage>& block) {
+    const double t0 = wall_s();
+    std::vector<const NetworkProtocol*> msgs;
+    for (const auto& um : block)
+        for (const auto& u : um.update) msgs.push_back(&u);
+    // ReplicationManager.cs:327-330: objectLookupTable[uid] throws KeyNotFoundException for a CRDT
+    // message of an unknown object; the states before it were merged (one at a time, RM:333-336).
+    size_t cut = msgs.size();
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        const NetworkProtocol& u = *msgs[i];
+        if (u.syncMsgType == NetworkProtocol::CRDTMsg && !u.uid.is_empty() && !uids_.find(u.uid)) { cut = i; break; }
     }
+    if (cut == msgs.size()) {
+        apply_msgs(msgs, nullptr, t0);
+        return;
+    }
+    msgs.resize(cut);
+    apply_msgs(msgs, nullptr, t0);
+    throw ApplyError(JG_EINVAL, "The given key was not present in the dictionary. (unknown CRDT uid)", cut, {});
+}
+
+std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const NetworkProtocol*>& msgs,
+                                                 std::unordered_map<uint64_t, uint64_t>* tracker, double t0) {
+    flush_registrations();
     const size_t n = msgs.size();
     WorkerPool& wp = pool();
     const int T = wp.size();

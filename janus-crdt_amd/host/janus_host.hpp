@@ -115,6 +115,14 @@ class GpuStableStore {
     std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
                                          std::unordered_map<uint64_t, uint64_t>* tracker = nullptr);
 
+    // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
+    // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the
+    // PROSPECTIVE merge of one received block, one batched engine call per CRDT type.  Creation
+    // messages (RM:300-302) and the key-space set (Guid.Empty) are not CRDT states of this store and
+    // are skipped; a CRDT state of an unknown uid throws ApplyError(JG_EINVAL) after merging the
+    // states before it (KeyNotFoundException at RM:329); a rejected payload throws like ApplyCommitted.
+    void ReceivedBlock(const std::vector<UpdateMessage>& block);
+
     // Wrapper Update, batched: ops run in order (PNC increments commute; OR-Set ops keep their order
     // per set).  Returns each op's bool result.  An unknown op id throws EngineError(JG_EINVAL) (the
     // wrappers' InvalidOperationException) before anything is applied.  A PNC op writes this copy's
@@ -179,6 +187,9 @@ class GpuStableStore {
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
     void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
+    // The body of ApplyCommitted / ReceivedBlock over the flattened messages (commit order).
+    std::vector<uint64_t> apply_msgs(const std::vector<const NetworkProtocol*>& msgs, std::unordered_map<uint64_t, uint64_t>* tracker,
+                                     double t0);
     char* chunk_buffer(size_t c, size_t bytes);  // pinned staging of wave chunk c (jg_host_alloc), grown on demand
     WorkerPool& pool();                     // persistent host workers (host_threads())
 

@@ -94,8 +94,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         if (res != pending_res) { std::printf("FAIL ApplyOp results differ from the wrappers'\n"); return 1; }
         pending.clear();
         pending_res.clear();
-        std::vector<std::vector<janus::UpdateMessage>> others(jw.begin() + 1, jw.end());
-        gpu_p.ApplyCommitted(others, nullptr);
+        for (size_t src = 1; src < jw.size(); ++src) gpu_p.ReceivedBlock(jw[src]);  // one block per other node
         std::unordered_map<uint64_t, uint64_t> tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
         const size_t before = nodes[0]->notified.size();
         for (auto& n : nodes) n->HandleAfterConsensusUpdates(wave);
@@ -313,6 +312,40 @@ int bad_wave() {
     return 0;
 }
 
+// Block receipt on the prospective path (ReplicationManager.cs:327-344): a CRDT state of an object the
+// node does not know throws KeyNotFoundException after the states before it were merged.
+int unknown_uid_block() {
+    oracle::SafeCRDTManager node(1, 9);
+    janus::GpuStableStore gpu(0, 4, 4, 4);
+    oracle::SafeCRDT& sc = node.CreateSafeCRDT("k", oracle::CrdtType::PNCounter);
+    gpu.CreateSafeCRDT(G(sc.guid), janus::CrdtType::PNCounter, janus::Guid{7, 7});
+    std::vector<int64_t> after;
+    for (int i = 0; i < 4; ++i) {
+        sc.Update(1, {oracle::Arg::I(10 * (i + 1))}, false, 0);
+        after.push_back(sc.QueryProspective().i);
+    }
+    std::vector<janus::UpdateMessage> block;
+    for (const auto& um : node.submitted) {
+        janus::UpdateMessage m;
+        for (const auto& np : um.update) m.update.push_back(convert(np));
+        block.push_back(std::move(m));
+    }
+    // message 2 (commit order) names an object this node never created
+    size_t seen = 0;
+    for (auto& um : block)
+        for (auto& np : um.update)
+            if (seen++ == 2) np.uid = janus::Guid{0x1234, 0x5678};
+    uint64_t at = UINT64_MAX;
+    try { gpu.ReceivedBlock(block); } catch (const janus::ApplyError& e) { at = e.commit_index; }
+    const int64_t v = gpu.QueryStablePNC(G(sc.guid));
+    if (seen < 3 || at != 2 || v != after[1]) {
+        std::printf("FAIL unknown uid block: %zu msgs, stopped at %lld, value %lld (expected %lld)\n", seen, (long long)at, (long long)v,
+                    (long long)after[1]);
+        return 1;
+    }
+    return 0;
+}
+
 }  // namespace
 
 int main() {
@@ -337,6 +370,10 @@ int main() {
         try { rb = bad_wave(); } catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
         std::printf("%s bad-payload wave (prefix applied, ApplyError at the rejected message)\n", rb ? "FAIL" : "PASS");
         fails += rb != 0;
+        int ru = 1;
+        try { ru = unknown_uid_block(); } catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
+        std::printf("%s received block with an unknown uid (prefix merged, KeyNotFoundException)\n", ru ? "FAIL" : "PASS");
+        fails += ru != 0;
     }
     for (const auto& c : cases) {
         setenv("JANUS_HOST_THREADS", c.threads, 1);
