@@ -88,6 +88,27 @@ __global__ __launch_bounds__(kBlock) void k_merge_indexed(typename Elem<EB>::T* 
     }
 }
 
+// The same scatter-max with one wave per received row (lanes over columns): no 64-bit division per
+// cell, coalesced row loads and row-contiguous atomics.  Used when a row fills most of a wave (R >= 32).
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_merge_indexed_rows(typename Elem<EB>::T* __restrict__ AP, typename Elem<EB>::T* __restrict__ AN,
+                                                               const typename Elem<EB>::T* __restrict__ BP,
+                                                               const typename Elem<EB>::T* __restrict__ BN,
+                                                               const uint32_t* __restrict__ keys, uint64_t n_rows, uint32_t R) {
+    using T = typename Elem<EB>::T;
+    const T absent = EB == 4 ? (T)INT32_MIN : (T)INT64_MIN;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * kBlock) >> 6;
+    for (uint64_t m = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; m < n_rows; m += n_waves) {
+        const uint64_t at = (uint64_t)keys[m] * R, src = m * R;
+        for (uint32_t c = lane; c < R; c += 64) {
+            const T p = BP[src + c], q = BN[src + c];
+            if (p != absent) atomicMax(AP + at + c, p);
+            if (q != absent) atomicMax(AN + at + c, q);
+        }
+    }
+}
+
 // Row copy (write: keys on the destination side; read: keys on the source side).
 template <int EB>
 __global__ __launch_bounds__(kBlock) void k_rows_copy(typename Elem<EB>::T* __restrict__ dst, const typename Elem<EB>::T* __restrict__ src,
@@ -224,6 +245,17 @@ void launch_merge_dense(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void
 
 void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void* BP, const void* BN, const uint32_t* keys,
                           uint64_t n_rows, uint32_t R) {
+    if (R >= 32) {
+        const unsigned grid = grid_for(ctx, n_rows * 64, 16);
+        if (eb == 8)
+            hipLaunchKernelGGL(k_merge_indexed_rows<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, (long long*)AP, (long long*)AN,
+                               (const long long*)BP, (const long long*)BN, keys, n_rows, R);
+        else
+            hipLaunchKernelGGL(k_merge_indexed_rows<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, (int*)AP, (int*)AN, (const int*)BP,
+                               (const int*)BN, keys, n_rows, R);
+        JG_HIP(hipGetLastError());
+        return;
+    }
     const unsigned grid = grid_for(ctx, n_rows * R, 16);
     if (eb == 8)
         hipLaunchKernelGGL(k_merge_indexed<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, (long long*)AP, (long long*)AN,

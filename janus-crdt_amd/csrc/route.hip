@@ -27,7 +27,7 @@ namespace {
 constexpr int kRB = 256;              // threads per route workgroup (4 waves)
 constexpr int kRW = kRB / 64;
 constexpr uint32_t kMaxWorld = 64;
-constexpr uint32_t kRowTile = 1024;   // PN-Counter rows per tile
+constexpr uint32_t kRowTile = 256;    // PN-Counter rows per tile (one round of the workgroup)
 
 // Tile t covers slots [t*T, t*T + len(t)): dense rows (len from n) or a chunked OR-Set stream
 // (len = the chunk's record count).
@@ -94,6 +94,14 @@ __global__ __launch_bounds__(1024) void k_route_scan(const uint32_t* __restrict_
     for (uint32_t d = tid; d <= world; d += 1024) bounds[d] = pos[(uint64_t)d * n_tiles];
 }
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load(const uint4* p) {
+    return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p)));
+}
+__device__ __forceinline__ void nt_store(uint4* p, uint4 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(v4u, v), reinterpret_cast<v4u*>(p));
+}
+
 // PN-Counter row mover: one wave per row; VEC = the row (R x EB bytes) is a whole number of 16-B vectors.
 template <int EB, bool VEC>
 struct RowMover {
@@ -104,22 +112,40 @@ struct RowMover {
     char* oP;
     char* oN;
     uint32_t R, world;
+    static constexpr int U = 4;  // rows in flight per wave (all loads issued before the stores)
     __device__ __forceinline__ void move(uint64_t s0, uint32_t cnt, const uint64_t* dst, int lane, int wv) const {
         const uint64_t row_bytes = (uint64_t)R * EB;
+        if constexpr (VEC) {
+            const uint32_t nv = (uint32_t)(row_bytes / 16);
+            for (uint32_t i0 = wv; i0 < cnt; i0 += kRW * U) {
+                if (lane < U && i0 + lane * kRW < cnt) {
+                    const uint64_t s = s0 + i0 + lane * kRW;
+                    okeys[dst[i0 + lane * kRW]] = (keys ? keys[s] : (uint32_t)s) / world;
+                }
+                for (uint32_t v = lane; v < 2 * nv; v += 64) {
+                    const bool isP = v < nv;
+                    const uint32_t w = isP ? v : v - nv;
+                    const char* src = isP ? P : N;
+                    char* out = isP ? oP : oN;
+                    uint4 x[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = i0 + u * kRW;
+                        if (i < cnt) x[u] = nt_load(reinterpret_cast<const uint4*>(src + (s0 + i) * row_bytes) + w);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = i0 + u * kRW;
+                        if (i < cnt) nt_store(reinterpret_cast<uint4*>(out + dst[i] * row_bytes) + w, x[u]);
+                    }
+                }
+            }
+            return;
+        }
         for (uint32_t i = wv; i < cnt; i += kRW) {
             const uint64_t s = s0 + i, d = dst[i];
             if (lane == 0) okeys[d] = (keys ? keys[s] : (uint32_t)s) / world;
-            if constexpr (VEC) {
-                const uint32_t nv = (uint32_t)(row_bytes / 16);
-                const uint4* sp = reinterpret_cast<const uint4*>(P + s * row_bytes);
-                const uint4* sn = reinterpret_cast<const uint4*>(N + s * row_bytes);
-                uint4* dp = reinterpret_cast<uint4*>(oP + d * row_bytes);
-                uint4* dn = reinterpret_cast<uint4*>(oN + d * row_bytes);
-                for (uint32_t v = lane; v < 2 * nv; v += 64) {
-                    if (v < nv) dp[v] = sp[v];
-                    else dn[v - nv] = sn[v - nv];
-                }
-            } else {
+            {
                 using T = std::conditional_t<EB == 4, int, long long>;
                 const T* sp = reinterpret_cast<const T*>(P) + s * R;
                 const T* sn = reinterpret_cast<const T*>(N) + s * R;
