@@ -186,6 +186,12 @@ int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const u
  * and (it has no tombstone set or the two tag sets differ: !SetEquals); the null element is
  * present iff !SetEquals(nullRemove, nullAdd).  out[i] = 0/1. */
 int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, uint64_t n, uint8_t* out);
+/* The records of whole sets set[0..n) (every element and null): set i's adds are
+ * add[add_off[i], add_off[i+1]), its tombstones rem[rem_off[i], rem_off[i+1]), sorted; the offsets
+ * (n+1 entries each) are always filled.  add and rem NULL = size query; JG_ESTATE if a buffer is
+ * short.  The per-set GetLastSynchronizedUpdate (ORSet.cs:305-308) that SafeCRDT.Update encodes. */
+int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* add_off, jg_tagrec* add, uint64_t cap_add, uint64_t* rem_off,
+                       jg_tagrec* rem, uint64_t cap_rem);
 /* ORSet.LookupAll (ORSet.cs:204-227) of sets set[0..n): members of set[i] are elems[off[i], off[i+1])
  * (off has n+1 entries, always filled), in the reference's order: elements with no tombstone set,
  * then elements whose tag sets differ (each group in ascending elem id = the add Dictionary's

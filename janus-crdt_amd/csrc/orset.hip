@@ -166,6 +166,18 @@ __global__ __launch_bounds__(kOB) void k_runs(View a, View r, const unsigned lon
     }
 }
 
+// Rank bounds of whole sets (every element, null included): out[4i..4i+3] = a0, a1, r0, r1 of set[i].
+__global__ __launch_bounds__(kOB) void k_set_runs(View a, View r, const uint32_t* __restrict__ sets, uint64_t n, uint64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        const unsigned long long base = (unsigned long long)sets[i] << 32;
+        const bool last = sets[i] == 0xFFFFFFFFu;
+        out[4 * i + 0] = lower_key(a, base);
+        out[4 * i + 1] = last ? a.n : lower_key(a, base + (1ull << 32));
+        out[4 * i + 2] = lower_key(r, base);
+        out[4 * i + 3] = last ? r.n : lower_key(r, base + (1ull << 32));
+    }
+}
+
 // Copy rank ranges [src_off[i], src_off[i] + len[i]) of a stream to dst[dst_off[i] ...] as AoS records.
 __global__ __launch_bounds__(kOB) void k_gather_ranges(View v, const uint64_t* __restrict__ src_off, const uint64_t* __restrict__ len,
                                                        const uint64_t* __restrict__ dst_off, uint64_t n, jg_tagrec* __restrict__ dst) {
@@ -678,6 +690,43 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
         JG_HIP(hipGetLastError());
         JG_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* add_off, jg_tagrec* add, uint64_t cap_add, uint64_t* rem_off,
+                       jg_tagrec* rem, uint64_t cap_rem) {
+    return jg::guard([&] {
+        JG_REQUIRE(s && add_off && rem_off, JG_EINVAL, "jg_orset_read_sets: NULL argument");
+        add_off[0] = rem_off[0] = 0;
+        if (n == 0) return;
+        JG_REQUIRE(set, JG_EINVAL, "jg_orset_read_sets: NULL set list");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg::sync_counts(s);
+        jg::DevBuf q;
+        q.alloc(n * 4 + n * 32 + 64);
+        auto* dset = q.as<uint32_t>();
+        auto* db = reinterpret_cast<uint64_t*>(q.as<char>() + ((n * 4 + 15) & ~15ull));
+        JG_HIP(hipMemcpyAsync(dset, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_set_runs, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), dset, n, db);
+        JG_HIP(hipGetLastError());
+        std::vector<uint64_t> bounds(4 * n);
+        JG_HIP(hipMemcpyAsync(bounds.data(), db, 4 * n * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        for (uint64_t i = 0; i < n; ++i) {
+            add_off[i + 1] = add_off[i] + (bounds[4 * i + 1] - bounds[4 * i]);
+            rem_off[i + 1] = rem_off[i] + (bounds[4 * i + 3] - bounds[4 * i + 2]);
+        }
+        if (!add && !rem) return;  // size query
+        JG_REQUIRE(add && rem && add_off[n] <= cap_add && rem_off[n] <= cap_rem, JG_ESTATE,
+                   "jg_orset_read_sets: (%llu, %llu) records exceed the buffers (%llu, %llu)", (unsigned long long)add_off[n],
+                   (unsigned long long)rem_off[n], (unsigned long long)cap_add, (unsigned long long)cap_rem);
+        std::vector<jg_tagrec> ra, rr;
+        std::vector<uint64_t> oa, orr;
+        gather_stream(ctx, s->add, bounds, 0, n, ra, oa);
+        gather_stream(ctx, s->rem, bounds, 1, n, rr, orr);
+        std::copy(ra.begin(), ra.end(), add);
+        std::copy(rr.begin(), rr.end(), rem);
     });
 }
 

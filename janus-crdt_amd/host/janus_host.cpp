@@ -536,6 +536,144 @@ std::vector<std::string> GpuStableStore::EncodePNCStates(const std::vector<Guid>
     return out;
 }
 
+std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids) {
+    std::vector<uint32_t> sets;
+    sets.reserve(uids.size());
+    for (const Guid& u : uids) sets.push_back(ref(u, CrdtType::ORSet).idx);
+    const size_t n = sets.size();
+    std::vector<uint64_t> ao(n + 1, 0), ro(n + 1, 0);
+    check(jg_orset_read_sets(orset_, n, sets.data(), ao.data(), nullptr, 0, ro.data(), nullptr, 0));
+    std::vector<jg_tagrec> a(std::max<uint64_t>(ao[n], 1)), r(std::max<uint64_t>(ro[n], 1));
+    check(jg_orset_read_sets(orset_, n, sets.data(), ao.data(), a.data(), a.size(), ro.data(), r.data(), r.size()));
+    std::vector<std::string> out;
+    out.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+        const SetKey& sk = sets_[sets[i]];
+        ORSetState st;
+        // records are sorted by (elem id, tag): one run per element, ascending id = insertion order
+        auto fill = [&](const jg_tagrec* b, const jg_tagrec* e, std::vector<std::pair<std::string, std::vector<Guid>>>& dict,
+                        std::vector<Guid>& nulls) {
+            for (const jg_tagrec* x = b; x < e;) {
+                const uint32_t id = (uint32_t)x->key;
+                const jg_tagrec* y = x;
+                std::vector<Guid> tags;
+                for (; y < e && (uint32_t)y->key == id; ++y) tags.push_back(Guid{y->tag_lo, y->tag_hi});
+                if (id == JG_NULL_ELEM) nulls = std::move(tags);
+                else dict.emplace_back(sk.names.at(id), std::move(tags));
+                x = y;
+            }
+        };
+        fill(a.data() + ao[i], a.data() + ao[i + 1], st.addSet, st.nullAddGuid);
+        fill(r.data() + ro[i], r.data() + ro[i + 1], st.removeSet, st.nullRemoveGuid);
+        out.push_back(wire::EncodeORSetMsg(st));
+    }
+    return out;
+}
+
+std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize,
+                                                         std::vector<UpdateMessage>& submitted,
+                                                         std::unordered_map<uint64_t, uint64_t>& tracker) {
+    const size_t n = ups.size();
+    for (const ClientUpdate& u : ups) {  // the wrappers' checks, before anything is applied or queued
+        const KeyRef* kr = uids_.find(u.op.uid);
+        if (!kr) throw EngineError(JG_EINVAL, "unknown CRDT uid");
+        const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
+        if (u.op.opId < 1 || u.op.opId > hi)
+            throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+    }
+    // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
+    //    q entries: (message, op index or -1 for a message queued by an earlier call).
+    constexpr int64_t kOld = -1;
+    std::vector<std::pair<NetworkProtocol, int64_t>> q;
+    for (auto& np : batch_queue_) q.emplace_back(std::move(np), kOld);
+    batch_queue_.clear();
+    struct Flush { std::vector<std::pair<NetworkProtocol, int64_t>> msgs; };
+    std::vector<Flush> flushes;
+    size_t head = 0;  // q[head..] is the live queue
+    for (size_t i = 0; i < n; ++i) {
+        NetworkProtocol np;
+        np.uid = ups[i].op.uid;
+        np.syncMsgType = NetworkProtocol::CRDTMsg;
+        np.seq = next_seq_++;
+        if (ups[i].isSafe && ups[i].origin != 0) tracker[np.seq] = ups[i].origin;  // SafeCRDT.cs:55-56
+        q.emplace_back(std::move(np), (int64_t)i);
+        if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
+            std::vector<std::pair<NetworkProtocol, int64_t>> safe, appeared;
+            std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared` (first appearance)
+            while (head < q.size()) {
+                auto e = std::move(q[head++]);                       // TryDequeue first ...
+                if (!((int)safe.size() < clientBatchSize)) break;     // ... so this one is lost (:175)
+                if (!tracker.count(e.first.seq)) {
+                    auto it = pos.find(e.first.uid);
+                    if (it == pos.end()) { pos.emplace(e.first.uid, appeared.size()); appeared.push_back(std::move(e)); }
+                    else appeared[it->second] = std::move(e);        // last state wins, position kept
+                } else {
+                    safe.push_back(std::move(e));
+                }
+            }
+            for (auto& e : appeared) safe.push_back(std::move(e));
+            if (!safe.empty()) {
+                flushes.push_back(Flush{std::move(safe)});
+                last_submit_ms_ = ups[i].now_ms;
+            }
+        }
+    }
+    // 2. Which ops' snapshots are needed: those submitted now or still queued.
+    std::vector<uint8_t> need(n, 0);
+    for (const Flush& f : flushes)
+        for (const auto& e : f.msgs)
+            if (e.second != kOld) need[(size_t)e.second] = 1;
+    for (size_t j = head; j < q.size(); ++j)
+        if (q[j].second != kOld) need[(size_t)q[j].second] = 1;
+    // 3. Apply the ops in chunks that end at every needed snapshot whose uid is touched again later
+    //    in the chunk, encode the needed snapshots after each chunk (on the device).
+    std::vector<uint8_t> result(n, 1);
+    std::vector<std::string> snap(n);
+    size_t c0 = 0;
+    while (c0 < n) {
+        std::unordered_map<Guid, size_t, GuidHash> last_need;  // uid -> needed op in this chunk
+        size_t c1 = c0;
+        for (; c1 < n; ++c1) {
+            if (last_need.count(ups[c1].op.uid)) break;
+            if (need[c1]) last_need.emplace(ups[c1].op.uid, c1);
+        }
+        std::vector<ClientOp> ops;
+        ops.reserve(c1 - c0);
+        for (size_t i = c0; i < c1; ++i) ops.push_back(ups[i].op);
+        const auto r = ApplyOps(ops);
+        std::copy(r.begin(), r.end(), result.begin() + c0);
+        std::vector<Guid> pu, ou;
+        std::vector<size_t> pi, oi;
+        for (const auto& kv : last_need) {
+            if (uids_.find(kv.first)->type == CrdtType::PNCounter) { pu.push_back(kv.first); pi.push_back(kv.second); }
+            else { ou.push_back(kv.first); oi.push_back(kv.second); }
+        }
+        if (!pu.empty()) {
+            auto enc = EncodePNCStates(pu);
+            for (size_t j = 0; j < pi.size(); ++j) snap[pi[j]] = std::move(enc[j]);
+        }
+        if (!ou.empty()) {
+            auto enc = EncodeORSetStates(ou);
+            for (size_t j = 0; j < oi.size(); ++j) snap[oi[j]] = std::move(enc[j]);
+        }
+        c0 = c1;
+    }
+    // 4. Submitted UpdateMessages and the remaining queue carry the snapshots.
+    for (Flush& f : flushes) {
+        UpdateMessage um;
+        for (auto& e : f.msgs) {
+            if (e.second != kOld) e.first.message = snap[(size_t)e.second];
+            um.update.push_back(std::move(e.first));
+        }
+        submitted.push_back(std::move(um));
+    }
+    for (size_t j = head; j < q.size(); ++j) {
+        if (q[j].second != kOld) q[j].first.message = snap[(size_t)q[j].second];
+        batch_queue_.push_back(std::move(q[j].first));
+    }
+    return result;
+}
+
 std::vector<std::optional<std::string>> GpuStableStore::QueryStableLookupAll(const Guid& uid) {
     const uint32_t set = ref(uid, CrdtType::ORSet).idx;
     uint64_t off[2] = {0, 0};

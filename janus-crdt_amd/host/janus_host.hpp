@@ -94,6 +94,14 @@ struct ClientOp {
     Guid tag;                         // ORSet Add: the Guid.NewGuid() drawn for this add
 };
 
+// One client update through SafeCRDT.Update (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:39-62).
+struct ClientUpdate {
+    ClientOp op;
+    bool isSafe = false;
+    uint64_t origin = 0;  // the client (Connection, id); 0 = default: never tracked (SafeCRDT.cs:55-56)
+    double now_ms = 0;    // DateTime.Now when the batcher sees it (the 100 ms flush rule, SafeCRDTManager.cs:170)
+};
+
 // One CRDT copy (stable or prospective) of every key of one node, resident on one GPU.
 class GpuStableStore {
   public:
@@ -128,6 +136,28 @@ class GpuStableStore {
     // wrappers' InvalidOperationException) before anything is applied.  A PNC op writes this copy's
     // own replica column (column 0, registered by CreateSafeCRDT).
     std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops);
+
+    // SafeCRDT.Update over a batch of client updates, on this store as the node's PROSPECTIVE copy
+    // (SafeCRDT.cs:39-62) followed by the client batcher SafeCRDTManager.ActualPropagateSyncMsg
+    // (SafeCRDTManager.cs:165-198): every update is applied in order and its full-state snapshot
+    // (GetLastSynchronizedUpdate().Encode()) becomes a NetworkProtocol{uid, CRDTMsg, seq}; safe updates
+    // with an origin are tracked (tracker: seq -> origin); the batcher queues them and, when it holds
+    // clientBatchSize messages or 100 ms passed since its last submit, drains the queue into one
+    // UpdateMessage (appended to `submitted`): safe messages individually in queue order, then the
+    // latest message of each non-safe uid in first-appearance order (state compaction), the message
+    // dequeued once the safe list is full dropped (:175).  Only the snapshots that survive compaction
+    // (or stay queued) are encoded — on the device, after applying the ops up to that point.  Returns
+    // each op's bool result; validation failures throw before anything is applied.
+    std::vector<uint8_t> SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize, std::vector<UpdateMessage>& submitted,
+                                             std::unordered_map<uint64_t, uint64_t>& tracker);
+    // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys from the device store (jg_orset_read_sets):
+    // elements in Dictionary insertion order (= ascending interned id), tags of an element in the
+    // store's canonical (sorted) order — the reference's HashSet enumeration order is not kept, so the
+    // bytes decode to the same state rather than matching byte for byte.
+    std::vector<std::string> EncodeORSetStates(const std::vector<Guid>& uids);
+    // Identity of the next message SubmitClientUpdates creates (NetworkProtocol.seq; the reference keys
+    // its safe-update tracker by message object, so identities only need to be unique per process).
+    void SetNextMessageSeq(uint64_t seq) { next_seq_ = seq; }
 
     // QueryStable: PNCounter.Get (throws EngineError JG_EOVERFLOW where the checked Sum would throw
     // OverflowException) and ORSet.Contains.
@@ -206,6 +236,9 @@ class GpuStableStore {
     std::vector<std::pair<char*, size_t>> chunks_;  // pinned chunk buffers, reused wave after wave
     std::unique_ptr<WorkerPool> pool_;
     std::vector<SetKey> sets_;
+    std::vector<NetworkProtocol> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167)
+    double last_submit_ms_ = 0;                 // lastSumittedTime
+    uint64_t next_seq_ = 1;                     // message identity for the safe-update tracker
 };
 
 }  // namespace janus

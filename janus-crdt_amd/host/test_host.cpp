@@ -13,7 +13,9 @@
 // are applied there, and QueryProspective plus every op result must match too.
 // Exit 0 = parity; prints the first mismatch otherwise.
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
+#include <map>
 #include <memory>
 
 #include "janus_host.hpp"
@@ -41,13 +43,61 @@ struct Rng {
     uint64_t below(uint64_t n) { return next() % n; }
 };
 
-int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batch, uint32_t eb) {
+// An ORSetMsg as a comparable value: addSet in Dictionary order with each HashSet as a sorted set;
+// removeSet as a map (its Dictionary order is first-Remove order, which the device store does not
+// keep; nothing observable depends on it); the null tag sets as sorted sets.
+std::string canonical_orset(const std::string& bytes) {
+    janus::ORSetState st = janus::wire::DecodeORSetMsg(bytes);
+    auto tags = [](std::vector<janus::Guid> v) {
+        std::sort(v.begin(), v.end(), [](const janus::Guid& a, const janus::Guid& b) { return a.lo != b.lo ? a.lo < b.lo : a.hi < b.hi; });
+        std::string o;
+        for (const auto& g : v) janus::wire::AppendGuidD(o, g);
+        return o;
+    };
+    std::string out = "A:";
+    for (const auto& e : st.addSet) out += e.first + "=" + tags(e.second) + ";";
+    std::map<std::string, std::string> rem;
+    for (const auto& e : st.removeSet) rem[e.first] = tags(e.second);
+    out += "R:";
+    for (const auto& e : rem) out += e.first + "=" + e.second + ";";
+    return out + "NA:" + tags(st.nullAddGuid) + "NR:" + tags(st.nullRemoveGuid);
+}
+
+// The GPU producer's batches against what the oracle node submitted: same UpdateMessages, same
+// NetworkProtocols (uid, seq) in the same order; PN-Counter payloads byte for byte, OR-Set payloads
+// as the same state (canonical_orset).  Returns nullptr on a match.
+const char* same_batches(const std::vector<janus::UpdateMessage>& g, const std::vector<oracle::UpdateMessage>& o) {
+    if (g.size() != o.size()) return "number of UpdateMessages";
+    for (size_t i = 0; i < g.size(); ++i) {
+        if (g[i].update.size() != o[i].update.size()) return "UpdateMessage size";
+        for (size_t j = 0; j < g[i].update.size(); ++j) {
+            const auto& a = g[i].update[j];
+            const auto& b = o[i].update[j];
+            if (!(a.uid == G(b.uid)) || a.seq != b.seq) return "message order / identity";
+            if (b.message.type == oracle::CrdtType::PNCounter) {
+                if (a.message != b.bytes) return "PN-Counter payload bytes";
+            } else if (canonical_orset(a.message) != canonical_orset(b.bytes)) {
+                return "OR-Set payload state";
+            }
+        }
+    }
+    return nullptr;
+}
+
+int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batch, uint32_t eb, int clock_step = 0) {
     const int n_nodes = 4;
     std::vector<std::unique_ptr<oracle::SafeCRDTManager>> nodes;
-    for (int i = 0; i < n_nodes; ++i) nodes.push_back(std::make_unique<oracle::SafeCRDTManager>(batch, seed * 31 + i));
+    for (int i = 0; i < n_nodes; ++i) {
+        nodes.push_back(std::make_unique<oracle::SafeCRDTManager>(batch, seed * 31 + i));
+        // the reference's tracker is keyed by NetworkProtocol object identity: messages of different
+        // nodes never match, so their simulated identities are kept disjoint
+        nodes.back()->nextSeq = ((uint64_t)(i + 1) << 40) + 1;
+    }
     janus::GpuStableStore gpu(0, n_pnc + 1, 8, eb);
     janus::GpuStableStore gpu_p(0, n_pnc + 1, 8, eb);  // node 0's PROSPECTIVE copies (ApplyOp + block-receipt merges)
-    std::vector<janus::ClientOp> pending;               // node 0's client ops since the last wave
+    gpu_p.SetNextMessageSeq(nodes[0]->nextSeq);
+    std::vector<janus::ClientUpdate> pending;           // node 0's client updates since the last wave
+    std::unordered_map<uint64_t, uint64_t> tracker_p;   // node 0's safe messages, as produced on the GPU
     std::vector<uint8_t> pending_res;                   // the oracle's results for them
     std::vector<std::string> keys;
     for (int k = 0; k < n_pnc + n_set; ++k) {
@@ -64,7 +114,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     }
     Rng rng{seed};
     uint64_t origin = 1;
-    uint64_t n_ovf = 0, n_val = 0, n_in = 0, n_out = 0, n_done = 0, n_waves = 0;
+    uint64_t n_ovf = 0, n_val = 0, n_in = 0, n_out = 0, n_done = 0, n_waves = 0, n_sub = 0;
     auto commit = [&]() -> int {
         std::vector<std::vector<oracle::UpdateMessage>> wave;
         for (auto& n : nodes) { wave.push_back(n->submitted); n->submitted.clear(); }
@@ -90,8 +140,13 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         }
         // node 0's prospective copies on the GPU: its own ops first (they ran before the blocks
         // arrived), then the other nodes' states of this wave (ReplicationManager.cs:327-344)
-        auto res = gpu_p.ApplyOps(pending);
+        // ... through SafeCRDT.Update + the client batcher: the UpdateMessages node 0 submitted since
+        // the last wave must come out of the GPU path identically (ActualPropagateSyncMsg, A14/F4)
+        std::vector<janus::UpdateMessage> sub;
+        auto res = gpu_p.SubmitClientUpdates(pending, batch, sub, tracker_p);
         if (res != pending_res) { std::printf("FAIL ApplyOp results differ from the wrappers'\n"); return 1; }
+        if (const char* why = same_batches(sub, wave[0])) { std::printf("FAIL submitted batches: %s\n", why); return 1; }
+        n_sub += sub.size();
         pending.clear();
         pending_res.clear();
         for (size_t src = 1; src < jw.size(); ++src) gpu_p.ReceivedBlock(jw[src]);  // one block per other node
@@ -175,14 +230,16 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         oracle::SafeCRDT& sc = *nodes[node]->safeCRDTs.at(keys[k]);
         const bool safe = rng.below(2) == 0;
         const uint64_t org = safe ? origin++ : 0;
+        if (clock_step) nodes[node]->clock_ms += (double)rng.below(clock_step);  // DateTime.Now: the 100 ms flush rule
         if (k < n_pnc) {
             const int op = 1 + (int)rng.below(2);
             int64_t amt = 1 + (int64_t)rng.below(99);           // PNCWorkload.cs:63 Next(1,100)
             if (eb == 4 && rng.below(50) == 0) amt = 0x7FFFFFF0 - (int64_t)rng.below(100);  // push toward the checked-Sum edge
             const auto r = sc.Update(op, {oracle::Arg::I(amt)}, safe, org);
             if (node == 0) {
-                janus::ClientOp c;
-                c.uid = G(sc.guid); c.opId = op; c.amount = amt;
+                janus::ClientUpdate c;
+                c.op.uid = G(sc.guid); c.op.opId = op; c.op.amount = amt;
+                c.isSafe = safe; c.origin = org; c.now_ms = nodes[0]->clock_ms;
                 pending.push_back(c);
                 pending_res.push_back(r.b ? 1 : 0);
             }
@@ -195,9 +252,10 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
             const oracle::Guid tag = peek.next();
             const auto res = opid == 3 ? sc.Update(3, {}, false, 0) : sc.Update(opid, a, safe, org);
             if (node == 0) {
-                janus::ClientOp c;
-                c.uid = G(sc.guid); c.opId = opid; c.tag = G(tag);
-                if (a[0].kind == oracle::Arg::Str) c.elem = a[0].s;
+                janus::ClientUpdate c;
+                c.op.uid = G(sc.guid); c.op.opId = opid; c.op.tag = G(tag);
+                if (a[0].kind == oracle::Arg::Str) c.op.elem = a[0].s;
+                c.isSafe = opid != 3 && safe; c.origin = opid == 3 ? 0 : org; c.now_ms = nodes[0]->clock_ms;
                 pending.push_back(c);
                 pending_res.push_back(res.b ? 1 : 0);
             }
@@ -205,9 +263,9 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         if ((i + 1) % wave_every == 0 && commit()) return 1;
     }
     if (commit()) return 1;
-    std::printf("  waves %llu, safe completions %llu, Get: %llu values + %llu overflows, Contains: %llu true / %llu false\n",
-                (unsigned long long)n_waves, (unsigned long long)n_done, (unsigned long long)n_val, (unsigned long long)n_ovf,
-                (unsigned long long)n_in, (unsigned long long)n_out);
+    std::printf("  waves %llu, node-0 batches %llu, safe completions %llu, Get: %llu values + %llu overflows, Contains: %llu true / %llu false\n",
+                (unsigned long long)n_waves, (unsigned long long)n_sub, (unsigned long long)n_done, (unsigned long long)n_val,
+                (unsigned long long)n_ovf, (unsigned long long)n_in, (unsigned long long)n_out);
     return 0;
 }
 
@@ -349,7 +407,7 @@ int unknown_uid_block() {
 }  // namespace
 
 int main() {
-    struct Case { uint64_t seed; int n_pnc, n_set, n_ops, wave_every, batch; uint32_t eb; const char* threads; };
+    struct Case { uint64_t seed; int n_pnc, n_set, n_ops, wave_every, batch; uint32_t eb; const char* threads; int clock_step; };
     // Waves are decoded by JANUS_HOST_THREADS workers once they hold JANUS_HOST_PAR_MIN messages;
     // the threshold is lowered to 1 so the parallel decode (and its commit-order column insertion)
     // runs on these small waves too.
@@ -360,6 +418,7 @@ int main() {
         {2, 20, 10, 3000, 97, 8, 4, "4"},  // batched client updates, state compaction (SafeCRDTManager.cs:165-198)
         {3, 3, 3, 2000, 500, 1000, 4, "7"},  // JanusService: clientBatchSize = 1000, big waves, hot keys
         {4, 10, 0, 1500, 50, 4, 8, "3"},   // long (int64) PN-Counter variant
+        {5, 8, 8, 2500, 300, 1000, 4, "4", 40},  // clientBatchSize 1000 with a moving clock: the 100 ms flushes
     };
     int fails = 0;
     {
@@ -378,7 +437,7 @@ int main() {
     for (const auto& c : cases) {
         setenv("JANUS_HOST_THREADS", c.threads, 1);
         int rc = 1;
-        try { rc = run(c.seed, c.n_pnc, c.n_set, c.n_ops, c.wave_every, c.batch, c.eb); }
+        try { rc = run(c.seed, c.n_pnc, c.n_set, c.n_ops, c.wave_every, c.batch, c.eb, c.clock_step); }
         catch (const std::exception& e) { std::printf("FAIL exception: %s\n", e.what()); }
         std::printf("%s case seed=%llu pnc=%d sets=%d ops=%d wave=%d batch=%d eb=%u\n", rc ? "FAIL" : "PASS", (unsigned long long)c.seed, c.n_pnc,
                     c.n_set, c.n_ops, c.wave_every, c.batch, c.eb);

@@ -32,7 +32,7 @@ EXPORTS = [
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
     "jg_orset_lookup_all", "jg_pnc_encode_json",
-    "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device",
+    "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -89,6 +89,7 @@ _SIGS = {
     "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
     "jg_orset_merge_device": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_read_sets": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -418,6 +419,15 @@ class ORSetStore:
         out = np.empty(s.size, np.uint8)
         _check(load().jg_orset_contains(self._h, _ptr(s), _ptr(e), s.size, _ptr(out)))
         return out
+
+    def read_sets(self, set_ids):
+        """Records of whole sets (jg_orset_read_sets): list of (adds, tombstones) per set."""
+        s = _arr(set_ids, np.uint32)
+        ao, ro = np.zeros(s.size + 1, np.uint64), np.zeros(s.size + 1, np.uint64)
+        _check(load().jg_orset_read_sets(self._h, s.size, _ptr(s), _ptr(ao), None, 0, _ptr(ro), None, 0))
+        a, r = np.empty(max(1, int(ao[-1])), REC_DTYPE), np.empty(max(1, int(ro[-1])), REC_DTYPE)
+        _check(load().jg_orset_read_sets(self._h, s.size, _ptr(s), _ptr(ao), _ptr(a), a.size, _ptr(ro), _ptr(r), r.size))
+        return [(a[int(ao[i]):int(ao[i + 1])], r[int(ro[i]):int(ro[i + 1])]) for i in range(s.size)]
 
     def lookup_all(self, set_ids):
         """ORSet.LookupAll of each set (jg_orset_lookup_all): list of uint32 arrays of elem ids."""

@@ -307,3 +307,23 @@ def test_lookup_all_matches_oracle(ctx, seed, n_sets, n_elems, pool):
         assert sum(len(g) for g in got) > 0
     finally:
         st.close()
+
+
+@pytest.mark.parametrize("n_sets", [1, 37, 3000])
+def test_read_sets_matches_full_read(ctx, n_sets):
+    """jg_orset_read_sets (the per-set GetLastSynchronizedUpdate) = the slices of the full snapshot,
+    for sets in any order, repeated, empty and out-of-range ids — on a chunked union output too."""
+    rng = np.random.default_rng(n_sets)
+    La, Lr, Ra, Rr = random_orset_pair(rng, n_sets=n_sets, n_elems=5, pool=6)
+    s = _store(ctx, La, Lr)
+    try:
+        s.merge(Ra, Rr)
+        A, Rm = s.read()
+        q = np.concatenate([rng.permutation(n_sets + 2), [0, 0, n_sets + 5, 0xFFFFFFFF]]).astype(np.uint32)
+        got = s.read_sets(q)
+        for sid, (ga, gr) in zip(q, got):
+            ea = A[(A["key"] >> np.uint64(32)) == sid]
+            er = Rm[(Rm["key"] >> np.uint64(32)) == sid]
+            assert np.array_equal(ga, ea) and np.array_equal(gr, er), sid
+    finally:
+        s.close()
