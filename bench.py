@@ -45,9 +45,11 @@ def shard_keys(total_keys: int, rank: int, world: int) -> tuple[int, int]:
 
 
 def dist_env():
+    """(world, rank, device).  JANUS_BENCH_DEVICE pins every rank to one device — only for rehearsing
+    the N > 1 path on a one-GPU box (with JANUS_BENCH_BACKEND=gloo); the driver never sets it."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("JANUS_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     return world, rank, local
 
 
@@ -239,7 +241,9 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
                         f"uniform over {world} x {EXCH_KEYS} keys): route + all-to-all + merge from device memory",
             "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
             "xgmi_bytes_per_rank": remote * row_bytes, "row_bytes": row_bytes,
-            "collective": "torch.distributed all_to_all_single over RCCL" if world > 1 else "none (world 1)"}
+            "collective": ("none (world 1)" if world == 1 else
+                           "torch.distributed all_to_all_single, host-staged (gloo rehearsal)" if ex.staged else
+                           "torch.distributed all_to_all_single over RCCL (xGMI)")}
 
 
 def bench_apply_loop(sync, rank, world, local):
@@ -309,7 +313,7 @@ def main():
         # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
         # instance (torch's libraries also name the runtime by an unversioned soname)
         import torch  # noqa: F401
-    sync = Sync(world, local)
+    sync = Sync(world, local, os.environ.get("JANUS_BENCH_BACKEND", "nccl"))
     import janus_gpu as jg
     ctx = jg.Context(local)
 
