@@ -200,13 +200,21 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     __syncthreads();
 
     // ---- per-thread merge path + serial merge of kItems outputs ----
+    // The search compares keys and reads the two 16-B tags from LDS only when the keys tie (LDS
+    // bandwidth, not HBM, bounded this phase when every probe read both tags).
     const int diag = min(tid * kItems, n);
     int lo = diag > nB ? diag - nB : 0, hi = min(diag, nA);
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
         const int bj = nA + diag - 1 - mid;
-        const bool a_le_b = !rec_lt(s_key[bj], __builtin_bit_cast(Tag, s_tag[bj]), s_key[mid], __builtin_bit_cast(Tag, s_tag[mid]));
-        if (a_le_b) lo = mid + 1;
+        const unsigned long long kb_ = s_key[bj], ka_ = s_key[mid];
+        bool b_lt_a;
+        if (kb_ != ka_) b_lt_a = kb_ < ka_;
+        else {
+            const Tag tb_ = __builtin_bit_cast(Tag, s_tag[bj]), ta_ = __builtin_bit_cast(Tag, s_tag[mid]);
+            b_lt_a = (tb_.lo < ta_.lo) | ((tb_.lo == ta_.lo) & (tb_.hi < ta_.hi));
+        }
+        if (!b_lt_a) lo = mid + 1;
         else hi = mid;
     }
     int ai = lo, bi = diag - lo;
@@ -223,22 +231,23 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     Tag ta{0, 0}, tb{0, 0};
     if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
     if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
-    int src[kItems];
+    // the merged records stay in registers for the compaction (no second LDS gather)
+    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
     unsigned keep = 0;
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {
-        src[it] = 0;
+        rk[it] = 0; rlo[it] = 0; rhi[it] = 0;
         if (it < my_n) {
             const bool take_a = ai < nA && (bi >= nB || !rec_lt(kb, tb, ka, ta));
             if (take_a) {
-                src[it] = ai;
+                rk[it] = ka; rlo[it] = ta.lo; rhi[it] = ta.hi;
                 hp = !dropped(drop, ka);
                 if (hp) keep |= 1u << it;
                 pk = ka; pt = ta;
                 ++ai;
                 if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
             } else {
-                src[it] = nA + bi;
+                rk[it] = kb; rlo[it] = tb.lo; rhi[it] = tb.hi;
                 if (!(hp && rec_eq(pk, pt, kb, tb))) keep |= 1u << it;
                 ++bi;
                 if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
@@ -246,7 +255,7 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
         }
     }
 
-    // ---- block scan of kept counts ----
+    // ---- block scan of kept counts (its barrier also ends every thread's LDS reads of the merge) ----
     const int cnt = __popc(keep);
     int incl = cnt;
 #pragma unroll
@@ -265,16 +274,7 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     }
     const int my_off = wbase + incl - cnt;
 
-    // ---- gather kept records, compact through LDS, store coalesced into this tile's chunk ----
-    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
-#pragma unroll
-    for (int it = 0; it < kItems; ++it) {  // src[it] is a valid LDS index even for dropped items
-        rk[it] = s_key[src[it]];
-        const Tag t = __builtin_bit_cast(Tag, s_tag[src[it]]);
-        rlo[it] = t.lo;
-        rhi[it] = t.hi;
-    }
-    __syncthreads();
+    // ---- compact the kept records through LDS, store coalesced into this tile's chunk ----
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {
         if (keep & (1u << it)) {
