@@ -86,6 +86,8 @@ struct jg_pnc {
     jg::DevBuf P, N;
     // replica table (json.hip): [n_keys x R] 16-byte Guids + [n_keys] column counts, first use only
     jg::DevBuf cols, ncols;
+    // per-key occurrence counters of the batch being merged (k_claim_*), zero between calls; first use
+    jg::DevBuf claim;
     // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list
     jg::DevBuf wbytes, woff, wrows, wstat;
     uint64_t wn = 0, wnb = 0;
