@@ -269,6 +269,24 @@ def bench_apply_loop(sync, rank, world, local):
     return res
 
 
+def bench_apply_orset(sync, rank, world, local):
+    """The committed-batch apply loop for OR-Set states (ORSetWorkload-shaped, host/bench_orset.cpp):
+    2000 sets, 4 nodes, 200k full-state ORSetMsg payloads per wave, through the host mirror (host
+    decode + element interning + one jg_orset_merge), vs the oracle's decode + ORSet.Merge loop."""
+    import subprocess
+    exe = ROOT / "janus-crdt_amd" / "build" / "bench_orset"
+    out = subprocess.run([str(exe), "--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "20000" if world == 1 else "0",
+                          "--device", str(local), "--rank", str(rank), "--world", str(world)],
+                         capture_output=True, text=True, timeout=240)
+    ok = out.returncode == 0
+    res = json.loads(out.stdout.strip().splitlines()[-1]) if ok else {"error": out.stderr[-500:]}
+    worst_ms = sync.max(res["ms_per_wave"] if ok else float("inf"))
+    if world > 1 and ok:
+        res = {"workload": res["workload"] + f", key-space sharded x{world}", "scaling": "strong",
+               "msgs_per_s": 200_000 / (worst_ms / 1e3), "ms_per_wave": worst_ms, "rank0_ms_per_wave": res["ms_per_wave"]}
+    return res
+
+
 def cpu_baseline():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as orc
@@ -333,6 +351,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
     apply_loop = bench_apply_loop(sync, rank, world, local) if args.workload == "all" else None
+    apply_orset = bench_apply_orset(sync, rank, world, local) if args.workload == "all" else None
     sync.close()
     if rank != 0:
         return
@@ -384,6 +403,8 @@ def main():
         line["exchange"] = res["exchange"]
     if apply_loop is not None:
         line["apply_loop"] = apply_loop
+    if apply_orset is not None:
+        line["apply_loop_orset"] = apply_orset
     line["cpu_baseline"] = cpu
     print(json.dumps(line), flush=True)
 

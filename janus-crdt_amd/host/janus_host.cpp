@@ -29,10 +29,6 @@ bool rec_less(const jg_tagrec& a, const jg_tagrec& b) {
     return a.tag_hi < b.tag_hi;
 }
 bool rec_eq(const jg_tagrec& a, const jg_tagrec& b) { return a.key == b.key && a.tag_lo == b.tag_lo && a.tag_hi == b.tag_hi; }
-void sort_unique(std::vector<jg_tagrec>& v) {
-    std::sort(v.begin(), v.end(), rec_less);
-    v.erase(std::unique(v.begin(), v.end(), rec_eq), v.end());
-}
 }  // namespace
 
 void GpuStableStore::check(int rc) const {
@@ -358,30 +354,137 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     phase_s_[1] = t_classify;
     phase_s_[2] = t_classify + t_gather;
 
-    // OR-Set payloads, decoded in parallel; the first rejected one (commit order) cuts the wave.
+    // OR-Set states: one parse per payload, straight into element interning and records (no decoded
+    // ORSetState).  Sets are independent, so the states are grouped by set (stable: commit order
+    // within a set) and the sets split into contiguous id ranges over the workers; each worker interns
+    // its sets' elements in commit order and keeps each set's distinct records (a full-state message
+    // repeats most of them), sorted.  Worker outputs concatenated in worker order are sorted by
+    // (set, elem, tag).  A payload the reader rejects cuts the wave at the first one in commit order:
+    // the records of later states are dropped and the element ids they issued are withdrawn.
     std::vector<size_t> set_msgs;
     for (size_t i = 0; i < n; ++i)
         if (cls[i] == kSet) set_msgs.push_back(i);
-    std::vector<ORSetState> decoded(set_msgs.size());
     std::vector<size_t> first_bad(T, SIZE_MAX);
+    std::vector<int> bad_code(T, JG_OK);
     std::vector<std::string> why(T);
-    parallel_ranges(wp, set_msgs.size(), [&](size_t b, size_t e, int t) {
-        for (size_t j = b; j < e; ++j) {
-            try {
-                decoded[j] = wire::DecodeORSetMsg(msgs[set_msgs[j]]->message);
-                for (const auto& el : decoded[j].addSet)
-                    if (el.second.empty()) throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
-            } catch (const EngineError& err) {
-                if (first_bad[t] == SIZE_MAX) { first_bad[t] = set_msgs[j]; why[t] = err.what(); }
-                return;
-            }
+    std::vector<std::vector<jg_tagrec>> wadd(T), wrem(T);
+    auto rollback = [](SetKey& sk, size_t names0) {  // withdraw the ids issued since names0
+        for (size_t q = names0; q < sk.names.size(); ++q) sk.elems.erase(sk.names[q]);
+        sk.names.resize(names0);
+    };
+    std::vector<uint32_t> names_at_start(next_set_);
+    for (uint32_t q = 0; q < next_set_; ++q) names_at_start[q] = (uint32_t)sets_[q].names.size();
+    const double to0 = wall_s();
+    auto intern_pass = [&](size_t n_set) {  // the first n_set OR-Set states (commit order)
+        std::vector<uint32_t> set_of(n_set);
+        for (size_t j = 0; j < n_set; ++j) set_of[j] = uids_.find(msgs[set_msgs[j]]->uid)->idx;
+        std::vector<uint32_t> first(next_set_ + 1, 0);  // counting sort by set id
+        for (size_t j = 0; j < n_set; ++j) ++first[set_of[j] + 1];
+        for (uint32_t q = 0; q < next_set_; ++q) first[q + 1] += first[q];
+        std::vector<uint32_t> grouped(n_set);
+        {
+            std::vector<uint32_t> at(first.begin(), first.end() - 1);
+            for (size_t j = 0; j < n_set; ++j) grouped[at[set_of[j]]++] = (uint32_t)j;
         }
-    });
+        // worker t takes the sets whose grouped messages start in [n_set*t/T, n_set*(t+1)/T)
+        parallel_ranges(wp, n_set, [&](size_t b, size_t e, int t) {
+            if (b >= e) return;
+            // whole sets only: start at the first set beginning at or after b, end at the first set at or after e
+            uint32_t s0 = set_of[grouped[b]], s1 = e < n_set ? set_of[grouped[e]] : next_set_;
+            if (b > 0 && set_of[grouped[b - 1]] == s0) ++s0;  // that set belongs to the previous worker
+            if (e < n_set && set_of[grouped[e - 1]] == s1) ++s1;
+            // A full-state message repeats most of its set's records: each set's records pass a per-side
+            // hash set before they are stored, so only distinct records are kept and sorted.
+            struct RecSet {
+                std::vector<jg_tagrec> slot;
+                std::vector<uint32_t> gen;  // slot is live iff gen == cur (O(1) reset per set)
+                uint32_t cur = 1;
+                size_t n = 0;
+                static uint64_t h(const jg_tagrec& r) {
+                    uint64_t x = r.key * 0x9E3779B97F4A7C15ull ^ r.tag_lo ^ (r.tag_hi * 0xBF58476D1CE4E5B9ull);
+                    x ^= x >> 31;
+                    x *= 0x94D049BB133111EBull;
+                    return x ^ (x >> 29);
+                }
+                void reset() {
+                    if (++cur == 0) { std::fill(gen.begin(), gen.end(), 0u); cur = 1; }
+                    n = 0;
+                }
+                bool insert(const jg_tagrec& r) {  // true if new
+                    if ((n + 1) * 2 > slot.size()) grow();
+                    const size_t mask = slot.size() - 1;
+                    for (size_t i = h(r) & mask;; i = (i + 1) & mask) {
+                        if (gen[i] != cur) { gen[i] = cur; slot[i] = r; ++n; return true; }
+                        if (rec_eq(slot[i], r)) return false;
+                    }
+                }
+                void grow() {
+                    std::vector<jg_tagrec> old;
+                    std::vector<uint32_t> og;
+                    old.swap(slot);
+                    og.swap(gen);
+                    const size_t sz = old.empty() ? 1024 : old.size() * 2;
+                    slot.assign(sz, jg_tagrec{0, 0, 0});
+                    gen.assign(sz, 0u);
+                    const uint32_t was = cur;
+                    cur = 1;
+                    n = 0;
+                    for (size_t i = 0; i < old.size(); ++i)
+                        if (og[i] == was) insert(old[i]);
+                }
+            };
+            struct Ctx {
+                GpuStableStore* self;
+                SetKey* sk;
+                uint64_t hi;
+                std::vector<jg_tagrec>* out[2];
+                RecSet seen[2];
+            } c{this, nullptr, 0, {&wadd[t], &wrem[t]}, {}};
+            for (uint32_t sid = s0; sid < s1 && sid < next_set_; ++sid) {
+                if (first[sid] == first[sid + 1]) continue;
+                c.sk = &sets_[sid];
+                c.hi = (uint64_t)sid << 32;
+                c.seen[0].reset();
+                c.seen[1].reset();
+                const size_t a0 = wadd[t].size(), r0 = wrem[t].size();
+                for (uint32_t x = first[sid]; x < first[sid + 1]; ++x) {
+                    const size_t i = set_msgs[grouped[x]];
+                    const size_t names0 = c.sk->names.size();
+                    try {
+                        wire::ScanORSetMsg(msgs[i]->message,
+                                           [](void* p, int side, std::string_view name, bool is_null, const Guid* tags, size_t nt) {
+                                               Ctx& k = *static_cast<Ctx*>(p);
+                                               if (side == 0 && !is_null && nt == 0)
+                                                   throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
+                                               const uint64_t key = k.hi | (is_null ? JG_NULL_ELEM : k.self->elem_id(*k.sk, std::string(name), true));
+                                               for (size_t q = 0; q < nt; ++q) {
+                                                   const jg_tagrec r{key, tags[q].lo, tags[q].hi};
+                                                   if (k.seen[side].insert(r)) k.out[side]->push_back(r);
+                                               }
+                                           },
+                                           &c);
+                    } catch (const EngineError& err) {
+                        // the reference's loop stops at this state; later states of this set come after it
+                        rollback(*c.sk, names0);
+                        if (i < first_bad[t]) { first_bad[t] = i; why[t] = err.what(); bad_code[t] = err.code; }
+                        break;
+                    }
+                }
+                auto dedup = [](std::vector<jg_tagrec>& v, size_t from) {
+                    std::sort(v.begin() + from, v.end(), rec_less);
+                    v.erase(std::unique(v.begin() + from, v.end(), rec_eq), v.end());
+                };
+                dedup(wadd[t], a0);
+                dedup(wrem[t], r0);
+            }
+        });
+    };
+    intern_pass(set_msgs.size());
     size_t cut = n;
     int cut_code = JG_OK;
     std::string cut_why;
     for (int t = 0; t < T; ++t)
-        if (first_bad[t] < cut) { cut = first_bad[t]; cut_why = why[t]; cut_code = JG_EINVAL; }
+        if (first_bad[t] < cut) { cut = first_bad[t]; cut_why = why[t]; cut_code = bad_code[t]; }
     phase_s_[3] = wall_s() - t0;
 
     const double t1 = wall_s();
@@ -418,29 +521,35 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     pnc_bytes_ = 0;
     for (const Chunk& ch : chunks) pnc_bytes_ += ch.off[ch.m];
 
-    // OR-Set states before the cut: element interning in commit order, then one merge.
-    std::vector<jg_tagrec> adds, rems;
-    for (size_t j = 0; j < set_msgs.size() && set_msgs[j] < cut; ++j) {
-        const KeyRef* kr = uids_.find(msgs[set_msgs[j]]->uid);
-        SetKey& s = sets_[kr->idx];
-        const uint64_t hi = (uint64_t)kr->idx << 32;
-        const ORSetState& d = decoded[j];
-        for (const auto& e : d.addSet) {
-            const uint64_t key = hi | elem_id(s, e.first, true);
-            for (const auto& g : e.second) adds.push_back(jg_tagrec{key, g.lo, g.hi});
-        }
-        for (const auto& e : d.removeSet) {
-            const uint64_t key = hi | elem_id(s, e.first, true);
-            for (const auto& g : e.second) rems.push_back(jg_tagrec{key, g.lo, g.hi});
-        }
-        for (const auto& g : d.nullAddGuid) adds.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
-        for (const auto& g : d.nullRemoveGuid) rems.push_back(jg_tagrec{hi | JG_NULL_ELEM, g.lo, g.hi});
+    // A cut (a rejected OR-Set or PN-Counter state) before some OR-Set state: redo the OR-Set part over
+    // the states before it, from the element tables as they were.
+    if (!set_msgs.empty() && set_msgs.back() >= cut) {
+        for (uint32_t q = 0; q < next_set_; ++q) rollback(sets_[q], names_at_start[q]);
+        for (int t = 0; t < T; ++t) { wadd[t].clear(); wrem[t].clear(); first_bad[t] = SIZE_MAX; }
+        size_t n_set = 0;
+        while (n_set < set_msgs.size() && set_msgs[n_set] < cut) ++n_set;
+        intern_pass(n_set);
     }
+    std::vector<jg_tagrec> adds, rems;
+    {
+        size_t na = 0, nr = 0;
+        for (int t = 0; t < T; ++t) { na += wadd[t].size(); nr += wrem[t].size(); }
+        adds.reserve(na);
+        rems.reserve(nr);
+        for (int t = 0; t < T; ++t) {
+            adds.insert(adds.end(), wadd[t].begin(), wadd[t].end());
+            rems.insert(rems.end(), wrem[t].begin(), wrem[t].end());
+        }
+    }
+    const double to1 = wall_s();
+    double to2 = to1;
     if (!adds.empty() || !rems.empty()) {
-        sort_unique(adds);
-        sort_unique(rems);
+        to2 = wall_s();
         check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
     }
+    orset_phase_s_[0] = to1 - to0;
+    orset_phase_s_[1] = to2 - to1;
+    orset_phase_s_[2] = wall_s() - to2;
     std::vector<uint64_t> completed;
     if (tracker)
         for (size_t i = 0; i < cut; ++i) {

@@ -188,6 +188,8 @@ class GpuStableStore {
     uint64_t last_apply_pnc_bytes() const { return pnc_bytes_; }
     // Cumulative host time at the end of: flatten, classify, gather, OR-Set decode.
     const double* last_apply_phases_s() const { return phase_s_; }
+    // OR-Set part of the last ApplyCommitted: element interning, record sort, engine merge call.
+    const double* last_apply_orset_phases_s() const { return orset_phase_s_; }
 
   private:
     struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id
@@ -228,7 +230,7 @@ class GpuStableStore {
     jg_orset* orset_ = nullptr;
     uint32_t max_keys_, R_, eb_;
     uint32_t next_row_ = 0, next_set_ = 0;
-    double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0};
+    double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0}, orset_phase_s_[3] = {0, 0, 0};
     uint64_t pnc_bytes_ = 0;
     UidTable uids_;
     std::vector<uint32_t> reg_rows_;        // CreateSafeCRDT registrations not yet sent

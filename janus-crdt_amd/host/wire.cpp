@@ -69,6 +69,20 @@ struct Scan {
     // JSON string -> UTF-8 (escapes decoded, surrogate pairs joined, raw UTF-8 validated).
     std::string str() {
         need('"');
+        {   // fast path: printable ASCII without escapes up to the closing quote (every string the
+            // reference's encoder writes for a Guid, and JavaScriptEncoder.Default output of ASCII text)
+            size_t j = i;
+            while (j < s.size()) {
+                const unsigned char c = (unsigned char)s[j];
+                if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) break;
+                ++j;
+            }
+            if (j < s.size() && s[j] == '"') {
+                std::string o(s.data() + i, j - i);
+                i = j + 1;
+                return o;
+            }
+        }
         std::string o;
         while (true) {
             if (i >= s.size()) reject("unterminated string", i);
@@ -116,9 +130,34 @@ struct Scan {
             i += extra;
         }
     }
+    // The string as a view into the payload when it has no escapes, else decoded into `scratch`.
+    std::string_view str_view(std::string& scratch) {
+        skip_ws();
+        if (i < s.size() && s[i] == '"') {
+            size_t j = i + 1;
+            while (j < s.size()) {
+                const unsigned char c = (unsigned char)s[j];
+                if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) break;
+                ++j;
+            }
+            if (j < s.size() && s[j] == '"') {
+                const std::string_view v = s.substr(i + 1, j - i - 1);
+                i = j + 1;
+                return v;
+            }
+        }
+        scratch = str();
+        return scratch;
+    }
     Guid guid() {
         const size_t at = i;
         Guid g;
+        skip_ws();
+        // fast path: "<36 chars>" parsed in place (no escapes can occur in a valid Guid string)
+        if (i + 38 <= s.size() && s[i] == '"' && s[i + 37] == '"' && ParseGuidD(s.substr(i + 1, 36), g)) {
+            i += 38;
+            return g;
+        }
         if (!ParseGuidD(str(), g)) reject("not a Guid", at);
         return g;
     }
@@ -213,16 +252,29 @@ void AppendGuidD(std::string& out, const Guid& g) {
 
 bool ParseGuidD(std::string_view s, Guid& g) {
     if (s.size() != 36 || s[8] != '-' || s[13] != '-' || s[18] != '-' || s[23] != '-') return false;
-    static const int lo_order[8] = {3, 2, 1, 0, 5, 4, 7, 6};
+    // 256-entry nibble table (0xFF = not a hex digit); bytes in text order, then placed
+    static const struct Tab {
+        uint8_t v[256];
+        Tab() {
+            for (int c = 0; c < 256; ++c) v[c] = 0xFF;
+            for (int c = 0; c < 10; ++c) v['0' + c] = (uint8_t)c;
+            for (int c = 0; c < 6; ++c) v['a' + c] = v['A' + c] = (uint8_t)(10 + c);
+        }
+    } T;
     static const int pos[16] = {0, 2, 4, 6, 9, 11, 14, 16, 19, 21, 24, 26, 28, 30, 32, 34};
-    uint64_t lo = 0, hi = 0;
+    static const int lo_order[8] = {3, 2, 1, 0, 5, 4, 7, 6};
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(s.data());
+    uint8_t b[16];
+    unsigned bad = 0;
     for (int k = 0; k < 16; ++k) {
-        const int a = hex_digit(s[pos[k]]), b = hex_digit(s[pos[k] + 1]);
-        if (a < 0 || b < 0) return false;
-        const uint64_t byte = (uint64_t)(a << 4 | b);
-        if (k < 8) lo |= byte << (8 * lo_order[k]);
-        else hi |= byte << (8 * (k - 8));
+        const uint8_t a = T.v[p[pos[k]]], c = T.v[p[pos[k] + 1]];
+        bad |= (a | c) & 0xF0;
+        b[k] = (uint8_t)(a << 4 | (c & 15));
     }
+    if (bad) return false;
+    uint64_t lo = 0, hi = 0;
+    for (int k = 0; k < 8; ++k) lo |= (uint64_t)b[k] << (8 * lo_order[k]);
+    for (int k = 0; k < 8; ++k) hi |= (uint64_t)b[8 + k] << (8 * k);
     g.lo = lo;
     g.hi = hi;
     return true;
@@ -282,13 +334,21 @@ ORSetState DecodeORSetMsg(std::string_view bytes) {
                 continue;
             }
             auto& map = which == 0 ? m.addSet : m.removeSet;
-            std::unordered_set<std::string> keys;
+            std::unordered_set<std::string> keys;  // duplicate names: linear scan below 32 entries
             sc.need('{');
             if (!sc.at('}')) {
                 do {
                     const size_t ek = sc.i;
                     std::string e = sc.str();
-                    if (!keys.insert(e).second) reject("duplicate element in one map", ek);
+                    bool dup = false;
+                    if (map.size() < 32) {
+                        for (const auto& kv : map) dup |= kv.first == e;
+                    } else {
+                        if (keys.empty())
+                            for (const auto& kv : map) keys.insert(kv.first);
+                        dup = !keys.insert(e).second;
+                    }
+                    if (dup) reject("duplicate element in one map", ek);
                     sc.need(':');
                     if (sc.take_null()) reject("null tag set", sc.i);
                     map.emplace_back(std::move(e), std::vector<Guid>());
@@ -303,6 +363,74 @@ ORSetState DecodeORSetMsg(std::string_view bytes) {
     if (sc.i != bytes.size()) reject("trailing data", sc.i);
     if (seen != 15) reject("missing member (Merge would throw NullReferenceException)", sc.i);
     return m;
+}
+
+void ScanORSetMsg(std::string_view bytes, ORSetEntryFn fn, void* ctx) {
+    Scan sc{bytes};
+    unsigned seen = 0;
+    std::string scratch;
+    std::vector<std::string> names;  // this map's element names so far (duplicate check)
+    std::unordered_set<std::string> big;  // ... hashed once a map holds 32 names
+    std::vector<Guid> tags;
+    // removeSet entries listed before addSet are held back: the receiver's Merge walks addSet first
+    std::vector<std::pair<std::string, std::vector<Guid>>> held;
+    bool add_done = false;
+    sc.need('{');
+    if (!sc.at('}')) {
+        do {
+            const size_t at = sc.i;
+            const std::string_view name = sc.str_view(scratch);
+            static const char* pnames[4] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
+            int which = -1;
+            for (int k = 0; k < 4; ++k)
+                if (name == pnames[k]) which = k;
+            if (which < 0) reject("unknown property", at);
+            if (seen >> which & 1) reject("duplicate property", at);
+            seen |= 1u << which;
+            sc.need(':');
+            if (sc.take_null()) reject("null member (Merge would throw NullReferenceException)", sc.i);
+            if (which >= 2) {
+                tags.clear();
+                sc.guids(tags);
+                fn(ctx, which == 2 ? 0 : 1, std::string_view(), true, tags.data(), tags.size());
+                continue;
+            }
+            names.clear();
+            big.clear();
+            sc.need('{');
+            if (!sc.at('}')) {
+                do {
+                    const size_t ek = sc.i;
+                    const std::string_view e = sc.str_view(scratch);
+                    bool dup = false;
+                    if (names.size() < 32) {
+                        for (const auto& x : names) dup |= x == e;
+                    } else {
+                        if (big.empty()) big.insert(names.begin(), names.end());
+                        dup = !big.emplace(e).second;
+                    }
+                    if (dup) reject("duplicate element in one map", ek);
+                    names.emplace_back(e);
+                    sc.need(':');
+                    if (sc.take_null()) reject("null tag set", sc.i);
+                    tags.clear();
+                    sc.guids(tags);
+                    if (which == 1 && !add_done) held.emplace_back(names.back(), tags);
+                    else fn(ctx, which, names.back(), false, tags.data(), tags.size());
+                } while (sc.take(','));
+            }
+            sc.need('}');
+            if (which == 0) {
+                add_done = true;
+                for (const auto& h : held) fn(ctx, 1, h.first, false, h.second.data(), h.second.size());
+                held.clear();
+            }
+        } while (sc.take(','));
+    }
+    sc.need('}');
+    sc.skip_ws();
+    if (sc.i != bytes.size()) reject("trailing data", sc.i);
+    if (seen != 15) reject("missing member (Merge would throw NullReferenceException)", sc.i);
 }
 
 }  // namespace janus::wire

@@ -10,6 +10,7 @@
 #include <cstdint>
 #include <string>
 #include <string_view>
+#include <vector>
 
 #include "janus_host.hpp"
 
@@ -27,5 +28,13 @@ void AppendPNCounterMsg(std::string& out, const Guid* g, const int64_t* p, const
 // narrowed contract) rejects the payload.
 std::string EncodeORSetMsg(const ORSetState& m);
 ORSetState DecodeORSetMsg(std::string_view bytes);
+
+// The same reader without building an ORSetState: fn(ctx, side, name, is_null, tags, n) once per entry —
+// side 0 = addSet / nullAddGuid, 1 = removeSet / nullRemoveGuid; is_null = the null tag set (name
+// empty); every addSet entry is reported before any removeSet entry, whatever the property order
+// (ORSet.Merge walks addSet first, ORSet.cs:255-279).  `name` and `tags` are valid during the call.
+// Accepts and rejects exactly what DecodeORSetMsg does; an error may come after some callbacks.
+using ORSetEntryFn = void (*)(void* ctx, int side, std::string_view name, bool is_null, const Guid* tags, size_t n);
+void ScanORSetMsg(std::string_view bytes, ORSetEntryFn fn, void* ctx);
 
 }  // namespace janus::wire

@@ -15,7 +15,10 @@ def test_committed_waves_match_oracle():
     out = subprocess.run([str(BIN)], capture_output=True, text=True, timeout=110)
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert out.stdout.count("PASS case") == 4
+    assert "FAIL" not in out.stdout
+    assert out.stdout.count("PASS case") == 5
+    for check in ("codec cross-check", "bad-payload wave", "unknown uid"):
+        assert check in out.stdout
 
 
 BENCH = BIN.parent / "bench_apply"
