@@ -52,6 +52,30 @@ def test_merge_indexed_repeated_keys(ctx, eb):
 
 
 @pytest.mark.parametrize("eb", [4, 8])
+@pytest.mark.parametrize("R", [32, 64, 130])
+def test_merge_indexed_unique_and_repeated_rows(ctx, eb, R):
+    """The duplicate-aware path (R x width a whole number of 16-B vectors, R >= 32): keys seen once
+    in a batch take the plain vector RMW, repeated keys the atomics; the per-key claim counters are
+    reset, so a second batch over the same keys merges exactly too."""
+    rng = np.random.default_rng(R * 10 + eb)
+    n_keys, M = 20_000, 6_000
+    AP, AN = random_pnc(rng, n_keys, R, eb, absent=False), random_pnc(rng, n_keys, R, eb, absent=False)
+    s = jg.PNCStore(ctx, n_keys, R, eb)
+    eP, eN = AP, AN
+    try:
+        s.write_rows(AP, AN)
+        for rnd in range(3):
+            BP, BN = random_pnc(rng, M, R, eb), random_pnc(rng, M, R, eb)
+            keys = rng.integers(0, n_keys if rnd != 1 else 50, M).astype(np.uint32)  # mostly unique / hot keys
+            s.merge_rows(BP, BN, keys)
+            eP, eN = orc.pnc_merge(eP, eN, BP, BN, keys)
+        P, N = s.read_rows()
+    finally:
+        s.close()
+    assert np.array_equal(P, eP) and np.array_equal(N, eN)
+
+
+@pytest.mark.parametrize("eb", [4, 8])
 def test_merge_batch_device_rows(ctx, eb):
     rng = np.random.default_rng(21)
     n_keys, R = 777, 13
