@@ -287,6 +287,17 @@ def bench_apply_orset(sync, rank, world, local):
     return res
 
 
+def bench_c1(local):
+    """BASELINE configs[0] (C1): the reference's own PN-Counter benchmark shape (benchmark_config_example.json:
+    100 objects, opsRatio [0.25, 0.25, 0.5], safeRatio 0.5, 4 servers) as committed waves of 1M client
+    ops through the host mirror, the oracle's apply loop timed on the same waves, every key's stable value
+    checked against it (host/bench_c1.cpp).  Single process: C1 is the reference's CPU-runnable case."""
+    import subprocess
+    exe = ROOT / "janus-crdt_amd" / "build" / "bench_c1"
+    out = subprocess.run([str(exe), "--device", str(local)], capture_output=True, text=True, timeout=240)
+    return json.loads(out.stdout.strip().splitlines()[-1]) if out.stdout.strip() else {"error": out.stderr[-500:]}
+
+
 def cpu_baseline():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as orc
@@ -352,6 +363,7 @@ def main():
         cpu = cpu_baseline()
     apply_loop = bench_apply_loop(sync, rank, world, local) if args.workload == "all" else None
     apply_orset = bench_apply_orset(sync, rank, world, local) if args.workload == "all" else None
+    apply_c1 = bench_c1(local) if args.workload == "all" and world == 1 else None
     sync.close()
     if rank != 0:
         return
@@ -405,6 +417,8 @@ def main():
         line["apply_loop"] = apply_loop
     if apply_orset is not None:
         line["apply_loop_orset"] = apply_orset
+    if apply_c1 is not None:
+        line["apply_loop_c1"] = apply_c1
     line["cpu_baseline"] = cpu
     print(json.dumps(line), flush=True)
 
