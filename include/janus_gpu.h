@@ -200,6 +200,46 @@ int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* a
 int jg_orset_lookup_all(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* off, uint32_t* elems, uint64_t cap);
 
 /* ---------------------------------------------------------------------------------------------
+ * OR-Set wire-format apply (csrc/orset_wire.hip; SURVEY.md §8f F1 + A7/A13).  ORSetMsg<string>
+ * payloads (System.Text.Json UTF-8, ORSet.cs:56-69) decoded, their element strings interned and the
+ * states merged on the device, as SafeCRDT.ApplyUpdateStable (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83)
+ * -> ORSet.DecodePropagationMessage -> Merge (ORSet.cs:253-283) would, message after message.
+ * Element table: per set, element string -> 32-bit element id, ids issued in first-insertion order
+ * (the add/remove Dictionaries' order; addSet entries before removeSet within a state, Merge's walk)
+ * and never reused; Clear drops a set's live strings (later adds take new ids).  The device table
+ * is the wave path's copy of the caller's interning: the caller registers the names it issues itself
+ * (ORSet.Add ops) and the Clears it applies with jg_orset_names_sync before the next wave, and reads
+ * back the ids a wave issued with jg_orset_wave_names.
+ * ------------------------------------------------------------------------------------------- */
+/* Register caller-side interning changes, applied in this order: for each i < n_sets, set[i]'s live
+ * strings are dropped if cleared[i] and its next id becomes next_id[i]; then name i < n_names
+ * (bytes[off[i], off[i+1]), off[0] = 0) is live in set name_set[i] with id name_id[i] (the caller
+ * guarantees it is not live already). */
+int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const uint32_t* next_id, const uint8_t* cleared,
+                        uint64_t n_names, const uint32_t* name_set, const uint32_t* name_id, const uint64_t* off, const uint8_t* bytes);
+/* A committed wave of ORSetMsg payloads, streamed like jg_pnc_wave_*: message i of the wave (chunks in
+ * commit order, chunk-relative offsets, off[0] = 0) is the state of set[i].  append uploads a chunk and
+ * queues its validation pass (host buffers untouched until commit / abort returns).  check ends the
+ * validation (element names repeated inside one map need the whole wave): JG_OK, or the code of the
+ * first message the reference's Decode/Merge would throw on — JG_EINVAL (JsonException: not an
+ * ORSetMsg in the accepted form of oracle/json.hpp, a null member or tag set, an element repeated in
+ * one map) or JG_ESTATE (an empty add tag set, which ORSet.Add never produces) — with *bad_msg = its
+ * wave index (UINT64_MAX if none).  commit merges messages [0, limit) (limit <= *bad_msg): interns
+ * their new element strings in commit order and unions their tag records into the store; the wave
+ * closes.  abort closes the wave with nothing applied. */
+int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes);
+int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes);
+int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg);
+int jg_orset_wave_commit(jg_orset* s, uint64_t limit);
+int jg_orset_wave_abort(jg_orset* s);
+/* The element ids the last commit issued, sorted by (set, id): name i = bytes[off[i], off[i+1]) got id
+ * id[i] in set set[i].  set / id / off / bytes NULL = size query (*n_names, *n_bytes). */
+int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes);
+/* One-shot: begin + append(all) + check, then commit(n) if every message is good; else nothing is
+ * applied and the check's code is returned with *bad_msg (the jg_pnc_merge_json contract). */
+int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg);
+
+/* ---------------------------------------------------------------------------------------------
  * Cross-shard exchange (csrc/route.hip).  The keyspace of a node is sharded over
  * its GPUs: global key k (PN-Counter row / OR-Set set id) belongs to rank k % world, where it is
  * local key k / world.  The reference has one process per node and no sharding: these entry points

@@ -121,12 +121,22 @@ struct jg_stream_soa {
     void swap(jg_stream_soa& o);
 };
 
+struct jg_orset_wire;  // orset_wire.hip: element table + open payload wave (first use only)
+namespace jg {
+void orset_wire_free(jg_orset_wire* w);
+}
+
 struct jg_orset {
     jg_ctx* ctx;
     jg_stream_soa add, rem;
     jg_stream_soa spare_add, spare_rem;  // union target for in-place merges (swapped in)
     jg::DevBuf counts;     // device-side uint64 [2]: n_add, n_rem written by the union kernel
     bool counts_pending = false;  // an async union wrote `counts`; host n's are stale
+    jg_orset_wire* wire = nullptr;
+    jg_orset() = default;
+    jg_orset(const jg_orset&) = delete;
+    jg_orset& operator=(const jg_orset&) = delete;
+    ~jg_orset() { jg::orset_wire_free(wire); }
 };
 
 namespace jg {
@@ -140,4 +150,6 @@ void pnc_merge_indexed(jg_pnc* p, const void* BP, const void* BN, const uint32_t
 // orset.hip: merge n_runs sorted, duplicate-free runs (device SoA, run after run) into the store.
 void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const unsigned long long* add_key,
                       const uint4* add_tag, const unsigned long long* rem_key, const uint4* rem_tag);
+// orset.hip: s = s ∪ src (both streams), synchronous, src's streams may be dense or chunked.
+void orset_merge_store(jg_orset* s, const jg_orset* src);
 }  // namespace jg

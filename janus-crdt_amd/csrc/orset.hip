@@ -546,6 +546,8 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
     }
     if (!level.empty()) merge_into(s, level[0].get(), false);
 }
+
+void orset_merge_store(jg_orset* s, const jg_orset* src) { merge_into(s, src, false); }
 }  // namespace jg
 
 extern "C" {

@@ -1,0 +1,1200 @@
+// orset_wire.hip — committed OR-Set states applied straight from their wire bytes (SURVEY.md §8f F1 + A7/A13).
+//
+// The reference's stable apply decodes every committed OR-Set state with System.Text.Json and merges it:
+// SafeCRDT.ApplyUpdateStable (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83) -> ORSet.DecodePropagationMessage
+// (MergeSharp/MergeSharp/CRDTs/ORSet.cs:297-302) -> ORSetMsg.Decode (:56-69) -> ORSet.Merge (:253-283), one
+// state at a time inside HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160).  The store's records are
+// (set << 32 | element id, 16-byte tag), so element STRINGS must become ids first.  A wave is:
+//
+//   pass 1  k_ow_count   one thread per message: full parse + validation (the accepted form of
+//                        oracle/json.hpp, which host/wire.cpp's reader also follows); counts entries and
+//                        tags; the byte position of the first error it sees: a syntax error (JG_EINVAL) or
+//                        an empty add tag set (JG_ESTATE — the host reader reports it at that entry).
+//   scan    entry / tag offsets per message (hipcub).
+//   pass 2  k_ow_emit    parse again: one entry per (message, map, element) with a 64-bit hash of its
+//                        unescaped string (escaped strings are unescaped in place), one record per tag;
+//                        entries are numbered in commit order with addSet entries before removeSet ones
+//                        (Merge walks addSet first, ORSet.cs:255-279).
+//   sort    entries by (set, string) hash, stable (hipcub radix sort): commit order within a hash.
+//   group   k_ow_link / k_ow_label label every entry with the first entry of its string in the set,
+//                        strings compared byte for byte (a hash collision only takes a slower path).  The
+//                        same string twice in one map of one message is Decode's duplicate-key error
+//                        (JG_EINVAL at the second name).  First bad message = min over messages.
+//   commit(limit)   strings whose first entry precedes the limit are looked up in the set's element
+//                   table; new ones are ordered by (set, first entry) and take the set's next ids in that
+//                   order = first insertion into the reference's Dictionaries.  Tag records get their keys,
+//                   lose their repeats through a hash table (a full-state message repeats most of its
+//                   set's records), are radix-sorted by (key, tag) and unioned into the store (orset.hip).
+//
+// Element table (per store, first use): open addressing over 64-bit words (hash high half << 32 | name
+// index + 1; 0 = empty), names as (set, id, Clear generation, length, pool offset, hash), bytes in a pool.
+// A name is live while its generation equals its set's (a Clear bumps the set's generation).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "jg_internal.hpp"
+#include "wire_cursor.hpp"
+
+namespace {
+
+using jgw::Cursor;
+using jgw::hexv;
+
+constexpr int kBlock = 256;
+constexpr unsigned long long kNone = ~0ull;
+constexpr unsigned long long kKindState = 1, kKindInval = 2;  // error word = position << 2 | kind
+constexpr uint32_t kDead = 0xFFFFFFFFu;                        // id of an entry at or beyond the limit
+constexpr uint32_t kNoName = 0xFFFFFFFFu;
+
+struct Tag16 { unsigned long long lo, hi; };
+
+unsigned blocks_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, (n + kBlock - 1) / kBlock); }
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+constexpr uint64_t kFnvBasis = 0xcbf29ce484222325ull, kFnvPrime = 0x100000001b3ull;
+__device__ __forceinline__ uint64_t name_key(uint32_t set, uint64_t fnv) { return mix64(fnv ^ mix64((uint64_t)set + 0x9E3779B97F4A7C15ull)); }
+
+// ---- string sinks: read_string feeds each unescaped UTF-8 byte to put(), esc() at a backslash -------
+__constant__ char kProp[4][16] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
+__constant__ uint32_t kPropLen[4] = {6, 9, 11, 14};
+
+struct PropSink {  // which of the four ORSetMsg members (after unescaping, as System.Text.Json matches)
+    uint32_t len = 0, mask = 15;
+    __device__ void esc() {}
+    __device__ void put(int b) {
+        for (int k = 0; k < 4; ++k)
+            if ((mask >> k & 1) && (len >= kPropLen[k] || kProp[k][len] != (char)b)) mask &= ~(1u << k);
+        ++len;
+    }
+    __device__ int which() const {
+        for (int k = 0; k < 4; ++k)
+            if ((mask >> k & 1) && kPropLen[k] == len) return k;
+        return -1;
+    }
+};
+
+struct GuidSink {  // Guid.Parse of the "D" form (what Guid's JSON converter accepts), C# byte order
+    uint32_t k = 0, va = 0, vb = 0, vc = 0;
+    unsigned long long hi = 0;
+    bool bad = false;
+    __device__ void esc() {}
+    __device__ void put(int b) {
+        if (k == 8 || k == 13 || k == 18 || k == 23) {
+            bad |= b != '-';
+        } else if (k < 36) {
+            const int h = hexv(b);
+            bad |= h < 0;
+            const uint32_t x = (uint32_t)h & 15;
+            if (k < 8) va = va << 4 | x;
+            else if (k < 13) vb = vb << 4 | x;
+            else if (k < 18) vc = vc << 4 | x;
+            else {
+                const uint32_t j = k < 23 ? k - 19 : k - 20;  // hex digit among the last 16
+                hi |= (unsigned long long)x << (8 * (j >> 1) + ((j & 1) ? 0 : 4));
+            }
+        } else {
+            bad = true;
+        }
+        ++k;
+    }
+    __device__ bool ok() const { return !bad && k == 36; }
+    __device__ Tag16 tag() const { return Tag16{(unsigned long long)va | (unsigned long long)vb << 32 | (unsigned long long)vc << 48, hi}; }
+};
+
+struct NameSink {  // FNV-1a of the unescaped bytes; with w set, the bytes after the first escape are
+                   // written back at the string's start (unescaping never lengthens a string)
+    unsigned long long h = kFnvBasis;
+    uint32_t len = 0;
+    uint8_t* w = nullptr;
+    bool shifted = false;
+    __device__ void esc() { shifted = w != nullptr; }
+    __device__ void put(int b) {
+        h = (h ^ (uint32_t)b) * kFnvPrime;
+        if (shifted) w[len] = (uint8_t)b;
+        ++len;
+    }
+};
+
+__device__ __forceinline__ bool hex4(Cursor& c, uint32_t& u) {
+    u = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int h = hexv(c.get());
+        if (h < 0) return false;
+        u = u << 4 | (uint32_t)h;
+    }
+    return true;
+}
+
+template <class S> __device__ __forceinline__ void put_utf8(S& s, uint32_t u) {
+    if (u < 0x80) { s.put((int)u); return; }
+    if (u < 0x800) { s.put((int)(0xC0 | u >> 6)); s.put((int)(0x80 | (u & 0x3F))); return; }
+    if (u < 0x10000) { s.put((int)(0xE0 | u >> 12)); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F))); return; }
+    s.put((int)(0xF0 | u >> 18)); s.put((int)(0x80 | (u >> 12 & 0x3F))); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F)));
+}
+
+// The rest of a JSON string after its opening quote: escapes decoded (surrogate pairs joined), raw
+// UTF-8 validated, control characters rejected — host/wire.cpp Scan::str.
+template <class S> __device__ __forceinline__ bool read_string(Cursor& c, S& s) {
+    for (;;) {
+        const int ch = c.get();
+        if (ch < 0) return false;
+        if (ch == '"') return true;
+        if (ch < 0x20) return false;
+        if (ch == '\\') {
+            s.esc();
+            const int e = c.get();
+            int out;
+            switch (e) {
+                case '"': out = '"'; break;
+                case '\\': out = '\\'; break;
+                case '/': out = '/'; break;
+                case 'b': out = 8; break;
+                case 'f': out = 12; break;
+                case 'n': out = 10; break;
+                case 'r': out = 13; break;
+                case 't': out = 9; break;
+                case 'u': {
+                    uint32_t u;
+                    if (!hex4(c, u) || (u >= 0xDC00 && u <= 0xDFFF)) return false;
+                    if (u >= 0xD800 && u <= 0xDBFF) {
+                        if (c.get() != '\\' || c.get() != 'u') return false;
+                        uint32_t lo;
+                        if (!hex4(c, lo) || lo < 0xDC00 || lo > 0xDFFF) return false;
+                        u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
+                    }
+                    put_utf8(s, u);
+                    continue;
+                }
+                default: return false;
+            }
+            s.put(out);
+            continue;
+        }
+        if (ch < 0x80) { s.put(ch); continue; }
+        int extra;
+        uint32_t cp;
+        if (ch >= 0xC2 && ch <= 0xDF) { extra = 1; cp = ch & 0x1F; }
+        else if (ch >= 0xE0 && ch <= 0xEF) { extra = 2; cp = ch & 0x0F; }
+        else if (ch >= 0xF0 && ch <= 0xF4) { extra = 3; cp = ch & 0x07; }
+        else return false;
+        s.put(ch);
+        for (int k = 0; k < extra; ++k) {
+            const int cc = c.get();
+            if (cc < 0 || (cc & 0xC0) != 0x80) return false;
+            cp = cp << 6 | (uint32_t)(cc & 0x3F);
+            s.put(cc);
+        }
+        if (extra == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) return false;
+        if (extra == 3 && (cp < 0x10000 || cp > 0x10FFFF)) return false;
+    }
+}
+
+// A tag array after its '['.  Null tag sets (nullAddGuid / nullRemoveGuid) report is_null.
+template <class V> __device__ __forceinline__ bool read_tags(Cursor& c, V& v, int side, bool is_null, uint32_t& nt) {
+    nt = 0;
+    c.ws();
+    if (c.peek() == ']') { ++c.p; return true; }
+    for (;;) {
+        if (!c.expect('"')) return false;
+        GuidSink gs;
+        if (!read_string(c, gs) || !gs.ok()) return false;
+        v.tag(side, is_null, gs.tag());
+        ++nt;
+        c.ws();
+        const int ch = c.get();
+        if (ch == ']') return true;
+        if (ch != ',') return false;
+    }
+}
+
+// One ORSetMsg<string>: {"addSet":{"e":[guid,...],...},"removeSet":{...},"nullAddGuid":[...],
+// "nullRemoveGuid":[...]}, members in any order, each exactly once, none null (Merge would throw).
+// W: unescape element strings in place (pass 2).
+template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c, uint8_t* wbase, V& v) {
+    if (!c.expect('{')) return false;
+    int seen = 0;
+    c.ws();
+    if (c.peek() == '}') {
+        ++c.p;
+    } else {
+        for (;;) {
+            if (!c.expect('"')) return false;
+            PropSink ps;
+            if (!read_string(c, ps)) return false;
+            const int which = ps.which();
+            if (which < 0 || (seen >> which & 1)) return false;
+            seen |= 1 << which;
+            if (!c.expect(':')) return false;
+            c.ws();
+            if (which >= 2) {
+                if (c.peek() != '[') return false;  // `null` included
+                ++c.p;
+                uint32_t nt;
+                if (!read_tags(c, v, which - 2, true, nt)) return false;
+            } else {
+                if (c.peek() != '{') return false;
+                ++c.p;
+                c.ws();
+                if (c.peek() == '}') {
+                    ++c.p;
+                } else {
+                    for (;;) {
+                        c.ws();
+                        const uint64_t npos = c.p;
+                        if (c.peek() != '"') return false;
+                        ++c.p;
+                        const uint64_t noff = c.p;
+                        NameSink ns;
+                        if (W) ns.w = wbase + noff;
+                        if (!read_string(c, ns)) return false;
+                        if (!c.expect(':')) return false;
+                        c.ws();
+                        if (c.peek() != '[') return false;  // a null tag set, or not an array
+                        ++c.p;
+                        v.entry(which, npos, noff, ns.len, ns.h);
+                        uint32_t nt;
+                        if (!read_tags(c, v, which, false, nt)) return false;
+                        v.entry_end(which, c.p, nt);
+                        c.ws();
+                        const int ch = c.get();
+                        if (ch == '}') break;
+                        if (ch != ',') return false;
+                    }
+                }
+            }
+            c.ws();
+            const int ch = c.get();
+            if (ch == '}') break;
+            if (ch != ',') return false;
+        }
+    }
+    c.ws();
+    return seen == 15 && c.p == c.end;
+}
+
+struct CountVis {
+    uint64_t base;
+    uint32_t n_add = 0, n_rem = 0, nt = 0;
+    unsigned long long estate = kNone;
+    __device__ void entry(int side, uint64_t, uint64_t, uint32_t, uint64_t) {
+        n_add += side == 0;
+        n_rem += side != 0;
+    }
+    __device__ void tag(int, bool, const Tag16&) { ++nt; }
+    __device__ void entry_end(int side, uint64_t pos, uint32_t ntags) {
+        if (side == 0 && ntags == 0 && estate == kNone) estate = (unsigned long long)(pos - base) << 2 | kKindState;
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void k_ow_count(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t m0,
+                                                     uint64_t m1, unsigned long long* __restrict__ ne, unsigned long long* __restrict__ nt,
+                                                     uint32_t* __restrict__ na, unsigned long long* __restrict__ err) {
+    const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= m1) return;
+    const uint64_t b = off[m];
+    Cursor c(bytes, b, off[m + 1]);
+    CountVis v{b};
+    unsigned long long e = v.estate;
+    if (!parse_orset<false>(c, nullptr, v)) {
+        const unsigned long long s = (unsigned long long)(c.p - b) << 2 | kKindInval;
+        e = s;
+    }
+    if (v.estate < e) e = v.estate;
+    // the entries before a syntax error are kept: a repeated name before it is reported first
+    ne[m] = v.n_add + v.n_rem;
+    nt[m] = v.nt;
+    na[m] = v.n_add;
+    err[m] = e;
+}
+
+__global__ void k_ow_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) off[i] += base;
+}
+
+struct Entries {  // entry e: sort key, string (offset into the payload, length | side << 31), message, error position
+    unsigned long long* key;
+    uint32_t* val;
+    unsigned long long* noff;
+    uint32_t* msg;
+    uint32_t* meta;
+    uint32_t* pos;
+};
+
+struct EmitVis {
+    Entries E;
+    unsigned long long* tref;
+    Tag16* tval;
+    uint64_t base, e_add, e_rem, t, cur = 0;  // next addSet / removeSet entry, next tag
+    uint32_t m, set;
+    uint64_t kmask;
+    __device__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h) {
+        cur = side ? e_rem++ : e_add++;
+        E.key[cur] = name_key(set, h) & kmask;
+        E.val[cur] = (uint32_t)cur;
+        E.noff[cur] = noff;
+        E.msg[cur] = m;
+        E.meta[cur] = len | (uint32_t)side << 31;
+        E.pos[cur] = (uint32_t)(npos - base);
+    }
+    __device__ void tag(int side, bool is_null, const Tag16& g) {
+        tref[t] = is_null ? (1ull << 63 | (unsigned long long)side << 62 | m) : cur;
+        tval[t] = g;
+        ++t;
+    }
+    __device__ void entry_end(int, uint64_t, uint32_t) {}
+};
+
+__global__ __launch_bounds__(kBlock) void k_ow_emit(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+                                                    uint64_t n, const unsigned long long* __restrict__ eoff, const unsigned long long* __restrict__ toff,
+                                                    const uint32_t* __restrict__ na, Entries E, unsigned long long* __restrict__ tref,
+                                                    Tag16* __restrict__ tval, uint64_t kmask) {
+    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m >= n) return;
+    const uint64_t b = off[m];
+    EmitVis v{E, tref, tval, b, eoff[m], eoff[m] + na[m], toff[m], 0, (uint32_t)m, mset[m], kmask};
+    Cursor c(bytes, b, off[m + 1]);
+    parse_orset<true>(c, bytes, v);  // validity was recorded by pass 1; the same prefix is emitted
+}
+
+__device__ __forceinline__ bool same_bytes(const uint8_t* a, const uint8_t* b, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+__device__ __forceinline__ bool same_name(const Entries& E, const uint32_t* mset, const uint8_t* bytes, uint32_t a, uint32_t b) {
+    const uint32_t la = E.meta[a] & 0x7FFFFFFFu, lb = E.meta[b] & 0x7FFFFFFFu;
+    return la == lb && mset[E.msg[a]] == mset[E.msg[b]] && same_bytes(bytes + E.noff[a], bytes + E.noff[b], la);
+}
+
+__global__ void k_ow_head(const unsigned long long* __restrict__ skey, uint64_t n, uint32_t* __restrict__ hs) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) hs[i] = (i == 0 || skey[i] != skey[i - 1]) ? (uint32_t)i : 0u;
+}
+
+// A run of equal hashes holding two different strings (a collision) is marked impure.
+__global__ void k_ow_link(Entries E, const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ sval,
+                          const uint32_t* __restrict__ seg, uint64_t n, uint8_t* __restrict__ impure) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || seg[i] == i) return;
+    if (!same_name(E, mset, bytes, sval[i], sval[i - 1])) impure[seg[i]] = 1;
+}
+
+__device__ __forceinline__ void report_dup(const Entries& E, uint32_t e, unsigned long long* err) {
+    atomicMin(err + E.msg[e], (unsigned long long)E.pos[e] << 2 | kKindInval);
+}
+
+// label[i] = sorted index of the first entry with the same (set, string).  Pure runs: the run's head
+// (stable sort = commit order), and a repeat within one map of one message is adjacent to its twin.
+// Impure runs (hash collision): a scan of the run before i.
+__global__ void k_ow_label(Entries E, const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ sval,
+                           const uint32_t* __restrict__ seg, const uint8_t* __restrict__ impure, uint64_t n, uint32_t* __restrict__ label,
+                           unsigned long long* __restrict__ err) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = seg[i], e = sval[i];
+    if (!impure[s]) {
+        label[i] = s;
+        if (i > s) {
+            const uint32_t p = sval[i - 1];
+            if (E.msg[p] == E.msg[e] && (E.meta[p] >> 31) == (E.meta[e] >> 31)) report_dup(E, e, err);
+        }
+        return;
+    }
+    uint32_t lab = (uint32_t)i;
+    bool dup = false;
+    for (uint32_t j = s; j < i; ++j) {
+        const uint32_t q = sval[j];
+        if (!same_name(E, mset, bytes, e, q)) continue;
+        if (lab == i) lab = j;
+        dup |= E.msg[q] == E.msg[e] && (E.meta[q] >> 31) == (E.meta[e] >> 31);
+    }
+    label[i] = lab;
+    if (dup) report_dup(E, e, err);
+}
+
+__global__ void k_ow_first_bad(const unsigned long long* __restrict__ err, uint64_t n, unsigned long long* __restrict__ status) {
+    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (m < n && err[m] != kNone) atomicMin(status, (unsigned long long)m);
+}
+
+// ---- element table ----------------------------------------------------------------------------------
+struct Names {
+    unsigned long long* tab;
+    uint64_t mask;
+    uint32_t *set, *id, *gen, *len;
+    unsigned long long *off, *key;
+    uint8_t* pool;
+    uint32_t* set_gen;
+    uint32_t* next_id;
+};
+
+__device__ __forceinline__ void tab_insert(const Names& N, uint64_t key, uint32_t g) {
+    const unsigned long long word = (key >> 32) << 32 | (unsigned long long)(g + 1);
+    for (uint64_t s = key & N.mask;; s = (s + 1) & N.mask)
+        if (atomicCAS(N.tab + s, 0ull, word) == 0ull) return;
+}
+
+__device__ __forceinline__ uint32_t tab_find(const Names& N, uint64_t key, uint32_t set, const uint8_t* name, uint32_t len) {
+    const uint32_t tag = (uint32_t)(key >> 32), gen = N.set_gen[set];
+    for (uint64_t s = key & N.mask;; s = (s + 1) & N.mask) {
+        const unsigned long long w = N.tab[s];
+        if (w == 0) return kNoName;
+        if ((uint32_t)(w >> 32) != tag) continue;
+        const uint32_t g = (uint32_t)w - 1;
+        if (N.set[g] != set || N.gen[g] != gen || N.len[g] != len || !same_bytes(N.pool + N.off[g], name, len)) continue;
+        return N.id[g];
+    }
+}
+
+__global__ void k_names_rebuild(Names N, uint64_t n_names) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g < n_names && N.gen[g] == N.set_gen[N.set[g]]) tab_insert(N, N.key[g], (uint32_t)g);
+}
+
+__global__ void k_sets_update(Names N, const uint32_t* __restrict__ set, const uint32_t* __restrict__ next, const uint8_t* __restrict__ cleared, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (cleared[i]) N.set_gen[set[i]] += 1;
+    N.next_id[set[i]] = next[i];
+}
+
+__global__ void k_names_put(Names N, uint64_t g0, uint64_t pool0, const uint32_t* __restrict__ nset, const uint32_t* __restrict__ nid,
+                            const uint64_t* __restrict__ off, uint64_t n, uint64_t kmask) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t g = g0 + i;
+    const uint32_t set = nset[i], len = (uint32_t)(off[i + 1] - off[i]);
+    const uint8_t* b = N.pool + pool0 + off[i];
+    uint64_t h = kFnvBasis;
+    for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * kFnvPrime;
+    const uint64_t key = name_key(set, h) & kmask;
+    N.set[g] = set;
+    N.id[g] = nid[i];
+    N.gen[g] = N.set_gen[set];
+    N.len[g] = len;
+    N.off[g] = pool0 + off[i];
+    N.key[g] = key;
+    tab_insert(N, key, (uint32_t)g);
+}
+
+// commit: each live group head looks its string up; new strings are queued as (set << 32 | entry).
+__global__ void k_ow_resolve(Entries E, const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ skey,
+                             const uint32_t* __restrict__ sval, const uint32_t* __restrict__ label, uint64_t n, uint64_t limit, Names N,
+                             uint32_t* __restrict__ gid, unsigned long long* __restrict__ newk, uint32_t* __restrict__ newv,
+                             unsigned long long* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || label[i] != i) return;
+    const uint32_t e = sval[i], m = E.msg[e];
+    if (m >= limit) { gid[i] = kDead; return; }
+    const uint32_t set = mset[m];
+    const uint32_t id = tab_find(N, skey[i], set, bytes + E.noff[e], E.meta[e] & 0x7FFFFFFFu);
+    if (id != kNoName) { gid[i] = id; return; }
+    const unsigned long long k = atomicAdd(status + 1, 1ull);
+    newk[k] = (unsigned long long)set << 32 | e;
+    newv[k] = (uint32_t)i;
+}
+
+__device__ __forceinline__ uint64_t set_begin(const unsigned long long* snk, uint64_t n, uint32_t set) {
+    uint64_t lo = 0, hi = n;
+    const unsigned long long x = (unsigned long long)set << 32;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (snk[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// New strings sorted by (set, first entry): the r-th new string of a set takes next_id + r.
+__global__ void k_ow_assign(Entries E, const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ skey,
+                            const unsigned long long* __restrict__ snk, const uint32_t* __restrict__ snv, uint64_t nnew, uint64_t g0, Names N,
+                            uint32_t* __restrict__ gid, unsigned long long* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nnew) return;
+    const uint32_t set = (uint32_t)(snk[k] >> 32);
+    const uint64_t r = k - set_begin(snk, nnew, set);
+    const uint64_t id = (uint64_t)N.next_id[set] + r;
+    if (id >= JG_NULL_ELEM - 1) atomicOr(status + 3, 1ull);
+    const uint32_t i = snv[k], e = (uint32_t)(snk[k] & 0xFFFFFFFFull), len = E.meta[e] & 0x7FFFFFFFu;
+    gid[i] = (uint32_t)id;
+    const uint64_t g = g0 + k;
+    const unsigned long long p = atomicAdd(status + 2, (unsigned long long)len);
+    const uint8_t* src = bytes + E.noff[e];
+    for (uint32_t q = 0; q < len; ++q) N.pool[p + q] = src[q];
+    N.set[g] = set;
+    N.id[g] = (uint32_t)id;
+    N.gen[g] = N.set_gen[set];
+    N.len[g] = len;
+    N.off[g] = p;
+    N.key[g] = skey[i];
+    tab_insert(N, skey[i], (uint32_t)g);
+}
+
+__global__ void k_ow_next_ids(const unsigned long long* __restrict__ snk, uint64_t nnew, Names N) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nnew) return;
+    const uint32_t set = (uint32_t)(snk[k] >> 32);
+    if (k + 1 < nnew && (uint32_t)(snk[k + 1] >> 32) == set) return;  // not the set's last new string
+    N.next_id[set] += (uint32_t)(k + 1 - set_begin(snk, nnew, set));
+}
+
+__global__ void k_ow_entry_ids(const uint32_t* __restrict__ sval, const uint32_t* __restrict__ label, const uint32_t* __restrict__ gid, uint64_t n,
+                               uint32_t* __restrict__ eid) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) eid[sval[i]] = gid[label[i]];
+}
+
+// Record keys of every tag (kNone beyond the limit) and its side (0 add, 1 tombstone).
+__global__ void k_ow_rec_keys(Entries E, const uint32_t* __restrict__ mset, const unsigned long long* __restrict__ tref, const uint32_t* __restrict__ eid,
+                              uint64_t nt, uint64_t limit, unsigned long long* __restrict__ rkey, uint8_t* __restrict__ rside) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= nt) return;
+    const unsigned long long r = tref[t];
+    uint32_t m, id, side;
+    bool live;
+    if (r >> 63) {  // a null tag set: no string to intern (kDead == JG_NULL_ELEM: test the limit only)
+        m = (uint32_t)r;
+        side = (uint32_t)(r >> 62 & 1);
+        id = JG_NULL_ELEM;
+        live = m < limit;
+    } else {
+        const uint32_t e = (uint32_t)r;
+        m = E.msg[e];
+        side = E.meta[e] >> 31;
+        id = eid[e];
+        live = m < limit && id != kDead;
+    }
+    rkey[t] = live ? ((unsigned long long)mset[m] << 32 | id) : kNone;
+    rside[t] = (uint8_t)side;
+}
+
+__device__ __forceinline__ uint64_t rec_hash(unsigned long long k, const Tag16& g, uint32_t side) {
+    return mix64(k ^ mix64(g.lo + side) ^ (g.hi * 0x9E3779B97F4A7C15ull));
+}
+
+// Distinct records: insert-if-absent into an open-addressing table of record indices (exact compare on a
+// hash match); the first copy of each record is appended to its side's output (wave-aggregated counter).
+__global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* __restrict__ rkey, const uint8_t* __restrict__ rside,
+                                                     const Tag16* __restrict__ tval, uint64_t nt, unsigned long long* __restrict__ tab, uint64_t mask,
+                                                     unsigned long long* __restrict__ dk0, Tag16* __restrict__ dt0, unsigned long long* __restrict__ dk1,
+                                                     Tag16* __restrict__ dt1, unsigned long long* __restrict__ counts) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool fresh = false;
+    uint32_t side = 0;
+    unsigned long long k = kNone;
+    Tag16 g{0, 0};
+    if (t < nt) {
+        k = rkey[t];
+        side = rside[t];
+        g = tval[t];
+    }
+    if (k != kNone) {
+        const uint64_t h = rec_hash(k, g, side);
+        const unsigned long long word = (h >> 32) << 32 | (t + 1);
+        for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+            const unsigned long long w = atomicCAS(tab + s, 0ull, word);
+            if (w == 0) { fresh = true; break; }
+            if ((w >> 32) != (h >> 32)) continue;
+            const uint64_t u = (w & 0xFFFFFFFFull) - 1;
+            const Tag16 o = tval[u];
+            if (rkey[u] == k && rside[u] == side && o.lo == g.lo && o.hi == g.hi) break;
+        }
+    }
+    const uint32_t lane = __lane_id();
+    for (uint32_t sd = 0; sd < 2; ++sd) {
+        const bool mine = fresh && side == sd;
+        const unsigned long long b = __ballot(mine);
+        if (!b) continue;
+        const uint32_t leader = __ffsll((long long)b) - 1;
+        unsigned long long base = 0;
+        if (lane == leader) base = atomicAdd(counts + sd, (unsigned long long)__popcll(b));
+        base = __shfl(base, (int)leader);
+        if (mine) {
+            const unsigned long long pos = base + __popcll(b & ((1ull << lane) - 1));
+            (sd ? dk1 : dk0)[pos] = k;
+            (sd ? dt1 : dt0)[pos] = g;
+        }
+    }
+}
+
+__global__ void k_iota(uint32_t* __restrict__ p, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+// which: 0 tag.hi, 1 tag.lo, 2 key — the radix key of pass `which` through the current permutation
+__global__ void k_gather_radix(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ perm, uint64_t n,
+                               int which, unsigned long long* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = perm[i];
+    out[i] = which == 2 ? dk[p] : which == 1 ? dt[p].lo : dt[p].hi;
+}
+__global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ perm, uint64_t n,
+                              unsigned long long* __restrict__ ok, Tag16* __restrict__ ot) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t p = perm[i];
+    ok[i] = dk[p];
+    ot[i] = dt[p];
+}
+
+uint64_t pow2_at_least(uint64_t x) {
+    uint64_t p = 1024;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+int bits_for(uint64_t x) {
+    int b = 1;
+    while (b < 32 && (1ull << b) <= x) ++b;
+    return b;
+}
+
+}  // namespace
+
+// Element table + open wave of one store.
+struct jg_orset_wire {
+    // element table
+    jg::DevBuf tab, nset, nid, ngen, nlen, noff, nkey, pool, set_gen, next_id;
+    uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
+    // open wave: payload, offsets, set per message, per-message counts / errors
+    jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff;
+    uint64_t wn = 0, wnb = 0, cap_msgs = 0, cap_bytes = 0;
+    uint32_t max_set = 0;
+    bool open = false, checked = false, any_set = false;
+    uint64_t first_bad = kNone, n_ent = 0, n_tag = 0;
+    // entries, groups, tags, records
+    jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, skey, sval, hs, seg, impure, label, gid, eid;
+    jg::DevBuf tref, tval, rkey, rside, dtab, dk[2], dt[2], rk, rk2, perm, perm2;
+    jg::DevBuf newk, newv, snk, snv, status, cub;
+    // ids issued by the last commit: names [g0, g1), pool bytes [p0, p1)
+    uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;
+    // string-hash mask: all bits; tests narrow it (JANUS_TEST_NAME_HASH_BITS) to force collisions
+    uint64_t kmask = ~0ull;
+};
+
+namespace {
+
+void ensure(jg::DevBuf& b, size_t bytes) {
+    if (b.bytes < bytes) b.alloc(bytes + bytes / 4 + 256);
+}
+
+// Grow to `need` bytes keeping the first `keep` bytes; the new tail is zeroed when `zero`.
+void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero = false) {
+    if (b.bytes >= need) return;
+    jg::DevBuf nb;
+    nb.alloc(need + need / 2);
+    if (zero) JG_HIP(hipMemsetAsync(nb.p, 0, nb.bytes, ctx->stream));
+    keep = std::min(keep, b.p ? b.bytes : 0);
+    if (keep) JG_HIP(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    std::swap(nb.p, b.p);
+    std::swap(nb.bytes, b.bytes);
+}
+
+jg_orset_wire* wire_of(jg_orset* s) {
+    if (!s->wire) {
+        s->wire = new jg_orset_wire();
+        s->wire->status.alloc(64);
+        if (const char* e = std::getenv("JANUS_TEST_NAME_HASH_BITS")) {
+            const int bits = std::atoi(e);
+            if (bits > 0 && bits < 64) s->wire->kmask = (1ull << bits) - 1;
+        }
+    }
+    return s->wire;
+}
+
+Names names_of(jg_orset_wire* w) {
+    return Names{w->tab.as<unsigned long long>(), w->tab_cap - 1, w->nset.as<uint32_t>(), w->nid.as<uint32_t>(), w->ngen.as<uint32_t>(),
+                 w->nlen.as<uint32_t>(), w->noff.as<unsigned long long>(), w->nkey.as<unsigned long long>(), w->pool.as<uint8_t>(),
+                 w->set_gen.as<uint32_t>(), w->next_id.as<uint32_t>()};
+}
+
+void ensure_sets(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_sets) {
+    if (n_sets <= w->set_cap) return;
+    const uint64_t cap = std::max<uint64_t>(n_sets + n_sets / 2, 1024);
+    grow_keep(ctx, w->set_gen, cap * 4, w->set_cap * 4, true);
+    grow_keep(ctx, w->next_id, cap * 4, w->set_cap * 4, true);
+    w->set_cap = w->set_gen.bytes / 4;
+}
+
+// Room for `incoming` more names with `pool_bytes` more pool bytes; the table keeps load <= 1/2 (a
+// rebuild keeps live names only).
+void ensure_names(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t pool_bytes) {
+    const uint64_t total = w->n_names + incoming;
+    JG_REQUIRE(total < 0xFFFFFFF0ull, JG_ESTATE, "OR-Set element table: more than 2^32 names");
+    if (total > w->name_cap) {
+        const uint64_t cap = std::max<uint64_t>(total + total / 2, 4096);
+        grow_keep(ctx, w->nset, cap * 4, w->n_names * 4);
+        grow_keep(ctx, w->nid, cap * 4, w->n_names * 4);
+        grow_keep(ctx, w->ngen, cap * 4, w->n_names * 4);
+        grow_keep(ctx, w->nlen, cap * 4, w->n_names * 4);
+        grow_keep(ctx, w->noff, cap * 8, w->n_names * 8);
+        grow_keep(ctx, w->nkey, cap * 8, w->n_names * 8);
+        w->name_cap = std::min({w->nset.bytes / 4, w->nid.bytes / 4, w->ngen.bytes / 4, w->nlen.bytes / 4, w->noff.bytes / 8, w->nkey.bytes / 8});
+    }
+    if (w->pool_used + pool_bytes > w->pool_cap) {
+        grow_keep(ctx, w->pool, std::max<uint64_t>(w->pool_used + pool_bytes, 1 << 20), w->pool_used);
+        w->pool_cap = w->pool.bytes;
+    }
+    if (w->tab_cap == 0 || 2 * total > w->tab_cap) {
+        const uint64_t cap = pow2_at_least(4 * total);
+        w->tab.alloc(cap * 8);
+        w->tab_cap = cap;
+        JG_HIP(hipMemsetAsync(w->tab.p, 0, cap * 8, ctx->stream));
+        if (w->n_names) {
+            hipLaunchKernelGGL(k_names_rebuild, dim3(blocks_for(w->n_names)), dim3(kBlock), 0, ctx->stream, names_of(w), w->n_names);
+            JG_HIP(hipGetLastError());
+        }
+    }
+}
+
+unsigned long long* status_words(jg_orset_wire* w) { return w->status.as<unsigned long long>(); }
+
+void read_words(jg_ctx* ctx, const unsigned long long* d, unsigned long long* h, int n) {
+    JG_HIP(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+void* cub_temp(jg_orset_wire* w, size_t bytes) {
+    ensure(w->cub, bytes);
+    return w->cub.p;
+}
+
+template <class K, class V>
+void sort_pairs(jg_ctx* ctx, jg_orset_wire* w, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, int end_bit) {
+    if (n == 0) return;
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, kin, kout, vin, vout, (int)n, 0, end_bit, ctx->stream));
+    JG_HIP(hipcub::DeviceRadixSort::SortPairs(cub_temp(w, temp), temp, kin, kout, vin, vout, (int)n, 0, end_bit, ctx->stream));
+}
+
+void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
+    if (msgs > w->cap_msgs) {
+        const uint64_t cap = std::max<uint64_t>(msgs + msgs / 2, 1024), m = w->wn;
+        grow_keep(ctx, w->off, (cap + 1) * 8, (m + 1) * 8);
+        grow_keep(ctx, w->mset, cap * 4, m * 4);
+        grow_keep(ctx, w->ne, (cap + 1) * 8, m * 8);
+        grow_keep(ctx, w->nt, (cap + 1) * 8, m * 8);
+        grow_keep(ctx, w->na, cap * 4, m * 4);
+        grow_keep(ctx, w->err, cap * 8, m * 8);
+        w->cap_msgs = cap;
+    }
+    if (bytes > w->cap_bytes) {
+        const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 1 << 16);
+        grow_keep(ctx, w->bytes, ((cap + 15) & ~15ull) + 16, w->wnb);  // the cursor reads aligned 16-byte windows
+        w->cap_bytes = cap;
+    }
+}
+
+Entries entries_of(jg_orset_wire* w) {
+    return Entries{w->ekey.as<unsigned long long>(), w->eval.as<uint32_t>(), w->enoff.as<unsigned long long>(), w->emsg.as<uint32_t>(),
+                   w->emeta.as<uint32_t>(), w->epos.as<uint32_t>()};
+}
+
+// Passes 2 + grouping over the whole wave; sets w->first_bad.  Returns the first bad message's code.
+int check_wave(jg_orset* s, jg_orset_wire* w) {
+    jg_ctx* ctx = s->ctx;
+    const uint64_t n = w->wn;
+    w->checked = true;
+    w->first_bad = kNone;
+    w->n_ent = w->n_tag = 0;
+    if (n == 0) return JG_OK;
+    // offsets: exclusive sums with a zero sentinel at [n]
+    JG_HIP(hipMemsetAsync(w->ne.as<unsigned long long>() + n, 0, 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->nt.as<unsigned long long>() + n, 0, 8, ctx->stream));
+    ensure(w->eoff, (n + 1) * 8);
+    ensure(w->toff, (n + 1) * 8);
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, w->ne.as<unsigned long long>(), w->eoff.as<unsigned long long>(), (int)(n + 1), ctx->stream));
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(cub_temp(w, temp), temp, w->ne.as<unsigned long long>(), w->eoff.as<unsigned long long>(), (int)(n + 1),
+                                            ctx->stream));
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(cub_temp(w, temp), temp, w->nt.as<unsigned long long>(), w->toff.as<unsigned long long>(), (int)(n + 1),
+                                            ctx->stream));
+    unsigned long long tot[2];
+    JG_HIP(hipMemcpyAsync(&tot[0], w->eoff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipMemcpyAsync(&tot[1], w->toff.as<unsigned long long>() + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    const uint64_t ne = tot[0], nt = tot[1];
+    JG_REQUIRE(ne < 0x7FFFFFF0ull && nt < 0x7FFFFFF0ull, JG_EINVAL, "jg_orset_wave: %llu entries / %llu tags exceed one wave (2^31)",
+               (unsigned long long)ne, (unsigned long long)nt);
+    w->n_ent = ne;
+    w->n_tag = nt;
+    ensure(w->ekey, ne * 8 + 8);
+    ensure(w->eval, ne * 4 + 4);
+    ensure(w->enoff, ne * 8 + 8);
+    ensure(w->emsg, ne * 4 + 4);
+    ensure(w->emeta, ne * 4 + 4);
+    ensure(w->epos, ne * 4 + 4);
+    ensure(w->tref, nt * 8 + 8);
+    ensure(w->tval, nt * 16 + 16);
+    const Entries E = entries_of(w);
+    hipLaunchKernelGGL(k_ow_emit, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), w->mset.as<uint32_t>(),
+                       n, w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(), w->na.as<uint32_t>(), E,
+                       w->tref.as<unsigned long long>(), w->tval.as<Tag16>(), w->kmask);
+    JG_HIP(hipGetLastError());
+    if (ne) {
+        ensure(w->skey, ne * 8);
+        ensure(w->sval, ne * 4);
+        ensure(w->hs, ne * 4);
+        ensure(w->seg, ne * 4);
+        ensure(w->impure, ne);
+        ensure(w->label, ne * 4);
+        sort_pairs(ctx, w, E.key, w->skey.as<unsigned long long>(), E.val, w->sval.as<uint32_t>(), ne, 64);
+        hipLaunchKernelGGL(k_ow_head, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->skey.as<unsigned long long>(), ne, w->hs.as<uint32_t>());
+        JG_HIP(hipGetLastError());
+        temp = 0;
+        JG_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::InclusiveScan(cub_temp(w, temp), temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne,
+                                                 ctx->stream));
+        JG_HIP(hipMemsetAsync(w->impure.p, 0, ne, ctx->stream));
+        hipLaunchKernelGGL(k_ow_link, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+                           w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), ne, w->impure.as<uint8_t>());
+        JG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ow_label, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+                           w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), w->impure.as<uint8_t>(), ne, w->label.as<uint32_t>(),
+                           w->err.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+    }
+    unsigned long long* st = status_words(w);
+    JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
+    hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
+    JG_HIP(hipGetLastError());
+    unsigned long long bad;
+    read_words(ctx, st, &bad, 1);
+    if (bad == kNone) return JG_OK;
+    unsigned long long e;
+    JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    w->first_bad = bad;
+    return (e & 3) == kKindState ? JG_ESTATE : JG_EINVAL;
+}
+
+// Sort one side's distinct records by (key, tag.lo, tag.hi) (three stable LSD passes) into a dense stream.
+void sort_side(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out) {
+    jg::set_dense(ctx, out, n);
+    if (n == 0) return;
+    ensure(w->rk, n * 8);
+    ensure(w->rk2, n * 8);
+    ensure(w->perm, n * 4);
+    ensure(w->perm2, n * 4);
+    const auto* dk = w->dk[sd].as<unsigned long long>();
+    const auto* dt = w->dt[sd].as<Tag16>();
+    uint32_t* p = w->perm.as<uint32_t>();
+    uint32_t* q = w->perm2.as<uint32_t>();
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, p, n);
+    for (int which = 0; which < 3; ++which) {
+        hipLaunchKernelGGL(k_gather_radix, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, which, w->rk.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        sort_pairs(ctx, w, w->rk.as<unsigned long long>(), w->rk2.as<unsigned long long>(), p, q, n, which == 2 ? key_bits : 64);
+        std::swap(p, q);
+    }
+    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, out.key.as<unsigned long long>(),
+                       out.tag.as<Tag16>());
+    JG_HIP(hipGetLastError());
+}
+
+void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
+    jg_ctx* ctx = s->ctx;
+    const uint64_t ne = w->n_ent, nt = w->n_tag;
+    w->g0 = w->g1 = w->n_names;
+    w->p0 = w->p1 = w->pool_used;
+    if (limit == 0 || (ne == 0 && nt == 0)) return;
+    ensure_sets(ctx, w, (uint64_t)w->max_set + 1);
+    ensure_names(ctx, w, 0, 0);
+    unsigned long long* st = status_words(w);
+    const Entries E = entries_of(w);
+    ensure(w->gid, ne * 4 + 4);
+    ensure(w->eid, ne * 4 + 4);
+    uint64_t nnew = 0;
+    if (ne) {
+        ensure(w->newk, ne * 8);
+        ensure(w->newv, ne * 4);
+        JG_HIP(hipMemsetAsync(st, 0, 64, ctx->stream));
+        hipLaunchKernelGGL(k_ow_resolve, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+                           w->skey.as<unsigned long long>(), w->sval.as<uint32_t>(), w->label.as<uint32_t>(), ne, limit, names_of(w),
+                           w->gid.as<uint32_t>(), w->newk.as<unsigned long long>(), w->newv.as<uint32_t>(), st);
+        JG_HIP(hipGetLastError());
+        unsigned long long h[2];
+        read_words(ctx, st, h, 2);
+        nnew = h[1];
+    }
+    if (nnew) {
+        ensure_names(ctx, w, nnew, w->wnb);
+        ensure(w->snk, nnew * 8);
+        ensure(w->snv, nnew * 4);
+        sort_pairs(ctx, w, w->newk.as<unsigned long long>(), w->snk.as<unsigned long long>(), w->newv.as<uint32_t>(), w->snv.as<uint32_t>(), nnew,
+                   32 + bits_for(w->max_set));
+        const unsigned long long init[4] = {0, 0, w->pool_used, 0};
+        JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_ow_assign, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, E, w->bytes.as<uint8_t>(), w->skey.as<unsigned long long>(),
+                           w->snk.as<unsigned long long>(), w->snv.as<uint32_t>(), nnew, w->n_names, names_of(w), w->gid.as<uint32_t>(), st);
+        JG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ow_next_ids, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, w->snk.as<unsigned long long>(), nnew, names_of(w));
+        JG_HIP(hipGetLastError());
+        unsigned long long h[4];
+        read_words(ctx, st, h, 4);
+        JG_REQUIRE(h[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
+        w->n_names += nnew;
+        w->pool_used = h[2];
+        w->g1 = w->n_names;
+        w->p1 = w->pool_used;
+    }
+    if (ne) {
+        hipLaunchKernelGGL(k_ow_entry_ids, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->sval.as<uint32_t>(), w->label.as<uint32_t>(),
+                           w->gid.as<uint32_t>(), ne, w->eid.as<uint32_t>());
+        JG_HIP(hipGetLastError());
+    }
+    // tag records: keys, de-duplication, sort, union into the store
+    ensure(w->rkey, nt * 8 + 8);
+    ensure(w->rside, nt + 1);
+    const uint64_t tcap = pow2_at_least(2 * nt);
+    ensure(w->dtab, tcap * 8);
+    for (int sd = 0; sd < 2; ++sd) {
+        ensure(w->dk[sd], nt * 8 + 8);
+        ensure(w->dt[sd], nt * 16 + 16);
+    }
+    hipLaunchKernelGGL(k_ow_rec_keys, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->tref.as<unsigned long long>(),
+                       w->eid.as<uint32_t>(), nt, limit, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>());
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemsetAsync(w->dtab.p, 0, tcap * 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
+    hipLaunchKernelGGL(k_ow_dedup, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>(),
+                       w->tval.as<Tag16>(), nt, w->dtab.as<unsigned long long>(), tcap - 1, w->dk[0].as<unsigned long long>(), w->dt[0].as<Tag16>(),
+                       w->dk[1].as<unsigned long long>(), w->dt[1].as<Tag16>(), st + 4);
+    JG_HIP(hipGetLastError());
+    unsigned long long cnt[2];
+    read_words(ctx, st + 4, cnt, 2);
+    if (cnt[0] + cnt[1] == 0) return;
+    jg_orset tmp;
+    tmp.ctx = ctx;
+    const int key_bits = 32 + bits_for(w->max_set);
+    sort_side(ctx, w, 0, cnt[0], key_bits, tmp.add);
+    sort_side(ctx, w, 1, cnt[1], key_bits, tmp.rem);
+    jg::orset_merge_store(s, &tmp);
+}
+
+void close_wave(jg_orset_wire* w) {
+    w->open = false;
+    w->checked = false;
+    w->wn = w->wnb = 0;
+    w->max_set = 0;
+    w->first_bad = kNone;
+}
+
+}  // namespace
+
+namespace jg {
+void orset_wire_free(jg_orset_wire* w) { delete w; }
+}  // namespace jg
+
+extern "C" {
+
+int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const uint32_t* next_id, const uint8_t* cleared, uint64_t n_names,
+                        const uint32_t* name_set, const uint32_t* name_id, const uint64_t* off, const uint8_t* bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_names_sync: store is NULL");
+        JG_REQUIRE((n_sets == 0 || (set && next_id && cleared)) && (n_names == 0 || (name_set && name_id && off && bytes)), JG_EINVAL,
+                   "jg_orset_names_sync: NULL argument");
+        JG_REQUIRE(n_names == 0 || off[0] == 0, JG_EINVAL, "jg_orset_names_sync: off[0] must be 0");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = wire_of(s);
+        JG_REQUIRE(!w->open, JG_EINVAL, "jg_orset_names_sync: a wave is open");
+        uint64_t mx = 0;
+        for (uint64_t i = 0; i < n_sets; ++i) mx = std::max<uint64_t>(mx, (uint64_t)set[i] + 1);
+        for (uint64_t i = 0; i < n_names; ++i) {
+            JG_REQUIRE(off[i + 1] >= off[i] && off[i + 1] - off[i] < 0x7FFFFFFFull, JG_EINVAL, "jg_orset_names_sync: bad offsets at name %llu",
+                       (unsigned long long)i);
+            JG_REQUIRE(name_id[i] < JG_NULL_ELEM - 1, JG_EINVAL, "jg_orset_names_sync: id %u out of range", name_id[i]);
+            mx = std::max<uint64_t>(mx, (uint64_t)name_set[i] + 1);
+        }
+        if (mx == 0) return;
+        ensure_sets(ctx, w, mx);
+        const uint64_t nb = n_names ? off[n_names] : 0;
+        ensure_names(ctx, w, n_names, nb);
+        const size_t need = n_sets * 9 + n_names * 8 + (n_names + 1) * 8 + 64;
+        char* stage = static_cast<char*>(jg::scratch(ctx, ctx->scratch, need));
+        auto* d_set = reinterpret_cast<uint32_t*>(stage);
+        auto* d_next = d_set + n_sets;
+        auto* d_nset = d_next + n_sets;
+        auto* d_nid = d_nset + n_names;
+        auto* d_off = reinterpret_cast<uint64_t*>(stage + (((n_sets * 8 + n_names * 8) + 15) & ~15ull));
+        auto* d_clr = reinterpret_cast<uint8_t*>(d_off + n_names + 1);
+        if (n_sets) {
+            JG_HIP(hipMemcpyAsync(d_set, set, n_sets * 4, hipMemcpyHostToDevice, ctx->stream));
+            JG_HIP(hipMemcpyAsync(d_next, next_id, n_sets * 4, hipMemcpyHostToDevice, ctx->stream));
+            JG_HIP(hipMemcpyAsync(d_clr, cleared, n_sets, hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL(k_sets_update, dim3(blocks_for(n_sets)), dim3(kBlock), 0, ctx->stream, names_of(w), d_set, d_next, d_clr, n_sets);
+            JG_HIP(hipGetLastError());
+        }
+        if (n_names) {
+            JG_HIP(hipMemcpyAsync(d_nset, name_set, n_names * 4, hipMemcpyHostToDevice, ctx->stream));
+            JG_HIP(hipMemcpyAsync(d_nid, name_id, n_names * 4, hipMemcpyHostToDevice, ctx->stream));
+            JG_HIP(hipMemcpyAsync(d_off, off, (n_names + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+            if (nb) JG_HIP(hipMemcpyAsync(w->pool.as<uint8_t>() + w->pool_used, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL(k_names_put, dim3(blocks_for(n_names)), dim3(kBlock), 0, ctx->stream, names_of(w), w->n_names, w->pool_used, d_nset, d_nid,
+                               d_off, n_names, w->kmask);
+            JG_HIP(hipGetLastError());
+        }
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        w->n_names += n_names;
+        w->pool_used += nb;
+    });
+}
+
+int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_begin: store is NULL");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = wire_of(s);
+        close_wave(w);
+        grow_wave(ctx, w, std::max<uint64_t>(cap_msgs, 1), std::max<uint64_t>(cap_bytes, 1));
+        JG_HIP(hipMemsetAsync(w->off.p, 0, 8, ctx->stream));  // off[0] = 0
+        w->open = true;
+    });
+}
+
+int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_append: no open wave (jg_orset_wave_begin)");
+        jg_orset_wire* w = s->wire;
+        JG_REQUIRE(!w->checked, JG_EINVAL, "jg_orset_wave_append: the wave was already checked");
+        if (n == 0) return;
+        JG_REQUIRE(set && off && bytes, JG_EINVAL, "jg_orset_wave_append: NULL argument");
+        JG_REQUIRE(off[0] == 0, JG_EINVAL, "jg_orset_wave_append: off[0] must be 0");
+        JG_REQUIRE(w->wn + n < 0x7FFFFFF0ull, JG_EINVAL, "jg_orset_wave_append: at most 2^31 messages per wave");
+        uint32_t mx = w->max_set;
+        for (uint64_t i = 0; i < n; ++i) {
+            JG_REQUIRE(off[i + 1] >= off[i], JG_EINVAL, "jg_orset_wave_append: offsets decrease at message %llu", (unsigned long long)i);
+            JG_REQUIRE(set[i] < 0xFFFFFFF0u, JG_EINVAL, "jg_orset_wave_append: set id %u out of range", set[i]);
+            mx = std::max(mx, set[i]);
+        }
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        const uint64_t m0 = w->wn, b0 = w->wnb, nb = off[n];
+        grow_wave(ctx, w, m0 + n, b0 + nb);
+        if (nb) JG_HIP(hipMemcpyAsync(w->bytes.as<uint8_t>() + b0, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(w->off.as<uint64_t>() + m0 + 1, off + 1, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(w->mset.as<uint32_t>() + m0, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        if (b0) hipLaunchKernelGGL(k_ow_rebase, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>() + m0 + 1, n, b0);
+        hipLaunchKernelGGL(k_ow_count, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), m0, m0 + n,
+                           w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->err.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        w->wn = m0 + n;
+        w->wnb = b0 + nb;
+        w->max_set = mx;
+        w->any_set = true;
+    });
+}
+
+int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
+    if (bad_msg) *bad_msg = UINT64_MAX;
+    return jg::guard([&] {
+        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_check: no open wave (jg_orset_wave_begin)");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = s->wire;
+        if (!w->checked) check_wave(s, w);
+        if (w->first_bad == kNone) return;
+        if (bad_msg) *bad_msg = w->first_bad;
+        unsigned long long e;
+        JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + w->first_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        const bool state = (e & 3) == kKindState;
+        jg::fail(state ? JG_ESTATE : JG_EINVAL, "OR-Set state message %llu is rejected by ORSetMsg.Decode / Merge (%s at byte %llu)",
+                 (unsigned long long)w->first_bad, state ? "an empty add tag set" : "JsonException", (unsigned long long)(e >> 2));
+    });
+}
+
+int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
+    return jg::guard([&] {
+        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_commit: no open wave (jg_orset_wave_begin)");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = s->wire;
+        if (!w->checked) check_wave(s, w);
+        JG_REQUIRE(limit <= w->wn, JG_EINVAL, "jg_orset_wave_commit: limit %llu beyond the wave (%llu messages)", (unsigned long long)limit,
+                   (unsigned long long)w->wn);
+        JG_REQUIRE(w->first_bad == kNone || limit <= w->first_bad, JG_EINVAL, "jg_orset_wave_commit: limit %llu passes the bad message %llu",
+                   (unsigned long long)limit, (unsigned long long)w->first_bad);
+        try {
+            commit_wave(s, w, limit);
+        } catch (...) {
+            close_wave(w);
+            throw;
+        }
+        close_wave(w);
+    });
+}
+
+int jg_orset_wave_abort(jg_orset* s) {
+    return jg::guard([&] {
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_abort: store is NULL");
+        jg::ensure_device(s->ctx);
+        JG_HIP(hipStreamSynchronize(s->ctx->stream));
+        if (s->wire) {
+            close_wave(s->wire);
+            s->wire->g0 = s->wire->g1 = s->wire->n_names;
+            s->wire->p0 = s->wire->p1 = s->wire->pool_used;
+        }
+    });
+}
+
+int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes) {
+    return jg::guard([&] {
+        JG_REQUIRE(s && n_names && n_bytes, JG_EINVAL, "jg_orset_wave_names: NULL argument");
+        jg_orset_wire* w = s->wire;
+        const uint64_t n = w ? w->g1 - w->g0 : 0, nb = w ? w->p1 - w->p0 : 0;
+        *n_names = n;
+        *n_bytes = nb;
+        if (!set || n == 0) return;
+        JG_REQUIRE(id && off && (bytes || nb == 0), JG_EINVAL, "jg_orset_wave_names: NULL buffer");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        std::vector<uint32_t> len(n);
+        std::vector<unsigned long long> po(n);
+        std::vector<uint8_t> pool(nb);
+        JG_HIP(hipMemcpyAsync(set, w->nset.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipMemcpyAsync(id, w->nid.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipMemcpyAsync(len.data(), w->nlen.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipMemcpyAsync(po.data(), w->noff.as<unsigned long long>() + w->g0, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (nb) JG_HIP(hipMemcpyAsync(pool.data(), w->pool.as<uint8_t>() + w->p0, nb, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        off[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            off[i + 1] = off[i] + len[i];
+            if (len[i]) std::copy(pool.begin() + (po[i] - w->p0), pool.begin() + (po[i] - w->p0) + len[i], bytes + off[i]);
+        }
+    });
+}
+
+int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+    if (bad_msg) *bad_msg = UINT64_MAX;
+    if (!s || (n && (!set || !off || !bytes)))
+        return jg::guard([&] { jg::fail(JG_EINVAL, "jg_orset_merge_json: NULL argument"); });
+    int rc = jg_orset_wave_begin(s, n, n ? off[n] : 0);
+    if (rc == JG_OK) rc = jg_orset_wave_append(s, n, set, off, bytes);
+    if (rc == JG_OK) rc = jg_orset_wave_check(s, bad_msg);
+    if (rc != JG_OK) {
+        char keep[1024];
+        jg_last_error(keep, sizeof keep);
+        jg_orset_wave_abort(s);
+        return jg::guard([&] { jg::fail(rc, "%s", keep); });
+    }
+    return jg_orset_wave_commit(s, n);
+}
+
+}  // extern "C"

@@ -33,6 +33,8 @@ EXPORTS = [
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
     "jg_orset_lookup_all", "jg_pnc_encode_json",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
+    "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
+    "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -90,6 +92,14 @@ _SIGS = {
     "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
     "jg_orset_merge_device": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_read_sets": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
+    "jg_orset_names_sync": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_wave_begin": ([_vp, _u64, _u64], C.c_int),
+    "jg_orset_wave_append": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_orset_wave_check": ([_vp, C.POINTER(_u64)], C.c_int),
+    "jg_orset_wave_commit": ([_vp, _u64], C.c_int),
+    "jg_orset_wave_abort": ([_vp], C.c_int),
+    "jg_orset_wave_names": ([_vp, C.POINTER(_u64), C.POINTER(_u64), _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_merge_json": ([_vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -428,6 +438,56 @@ class ORSetStore:
         a, r = np.empty(max(1, int(ao[-1])), REC_DTYPE), np.empty(max(1, int(ro[-1])), REC_DTYPE)
         _check(load().jg_orset_read_sets(self._h, s.size, _ptr(s), _ptr(ao), _ptr(a), a.size, _ptr(ro), _ptr(r), r.size))
         return [(a[int(ao[i]):int(ao[i + 1])], r[int(ro[i]):int(ro[i + 1])]) for i in range(s.size)]
+
+    # ---- wire-format apply (jg_orset_wave_*, csrc/orset_wire.hip) ----
+    def names_sync(self, sets=(), next_ids=(), cleared=(), names=()) -> None:
+        """jg_orset_names_sync: per-set (next id, Clear flag), then live names [(set, id, bytes)]."""
+        s, nx, cl = _arr(sets, np.uint32), _arr(next_ids, np.uint32), _arr(cleared, np.uint8)
+        ns = _arr([x[0] for x in names], np.uint32)
+        ni = _arr([x[1] for x in names], np.uint32)
+        data, off = pack_wave([x[2] for x in names])
+        data = data if data.size else np.zeros(16, np.uint8)
+        _check(load().jg_orset_names_sync(self._h, s.size, _ptr(s), _ptr(nx), _ptr(cl), ns.size, _ptr(ns), _ptr(ni), _ptr(off), _ptr(data)))
+
+    def merge_json(self, set_ids, msgs) -> None:
+        """Apply ORSetMsg payloads (list of bytes) of sets set_ids (jg_orset_merge_json): all or nothing."""
+        data, off = pack_wave(msgs)
+        s = _arr(set_ids, np.uint32)
+        data = data if data.size else np.zeros(16, np.uint8)
+        bad = _u64(0)
+        rc = load().jg_orset_merge_json(self._h, s.size, _ptr(s), _ptr(off), _ptr(data), C.byref(bad))
+        _check(rc, bad.value)
+
+    def wave(self, chunks, limit=None):
+        """Streamed wave: chunks = [(set_ids, msgs)]; check, then commit(limit or the first bad message).
+        Returns (check code, bad message or None)."""
+        n = sum(len(c[1]) for c in chunks)
+        keep = []
+        _check(load().jg_orset_wave_begin(self._h, n, 0))
+        for set_ids, msgs in chunks:
+            data, off = pack_wave(msgs)
+            s = _arr(set_ids, np.uint32)
+            data = data if data.size else np.zeros(16, np.uint8)
+            keep.append((s, data, off))
+            _check(load().jg_orset_wave_append(self._h, s.size, _ptr(s), _ptr(off), _ptr(data)))
+        bad = _u64(0)
+        rc = load().jg_orset_wave_check(self._h, C.byref(bad))
+        first_bad = None if bad.value == 2**64 - 1 else bad.value
+        lim = (n if first_bad is None else first_bad) if limit is None else limit
+        _check(load().jg_orset_wave_commit(self._h, lim))
+        return rc, first_bad
+
+    def wave_names(self):
+        """Element ids the last commit issued: list of (set, id, bytes), sorted by (set, id)."""
+        n, nb = _u64(), _u64()
+        _check(load().jg_orset_wave_names(self._h, C.byref(n), C.byref(nb), None, None, None, None))
+        if n.value == 0:
+            return []
+        s, i = np.empty(n.value, np.uint32), np.empty(n.value, np.uint32)
+        off, b = np.empty(n.value + 1, np.uint64), np.empty(max(1, nb.value), np.uint8)
+        _check(load().jg_orset_wave_names(self._h, C.byref(n), C.byref(nb), _ptr(s), _ptr(i), _ptr(off), _ptr(b)))
+        raw = b.tobytes()
+        return [(int(s[k]), int(i[k]), raw[int(off[k]):int(off[k + 1])]) for k in range(n.value)]
 
     def lookup_all(self, set_ids):
         """ORSet.LookupAll of each set (jg_orset_lookup_all): list of uint32 arrays of elem ids."""

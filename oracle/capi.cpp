@@ -358,6 +358,39 @@ int64_t orc_json_encode_pnc(uint64_t n, const uint64_t* lo, const uint64_t* hi, 
     return (int64_t)s.size();
 }
 
+// ORSetMsg<string>.Decode (ORSet.cs:56-63) of one payload, flattened for tests in ORSet.Merge's walk
+// order (ORSet.cs:255-282): addSet entries in Dictionary order, removeSet entries, then the null add and
+// null remove sets, each as [u8 side][u8 is_null][u32 name_len][name bytes][u32 n_tags][n_tags x (u64 lo,
+// u64 hi)].  Returns the bytes written (or needed, if cap is short: nothing is written), -1 if Decode
+// throws (JsonException).
+int64_t orc_json_decode_orset(const char* bytes, uint64_t len, uint8_t* out, uint64_t cap) {
+    ORSetMsg m;
+    try {
+        m = json::DecodeORSet(std::string_view(bytes, len));
+    } catch (const json::JsonException&) {
+        return -1;
+    }
+    std::string o;
+    auto u32 = [&](uint32_t v) { o.append(reinterpret_cast<const char*>(&v), 4); };
+    auto entry = [&](uint8_t side, uint8_t is_null, const std::string& name, const GuidSet& tags) {
+        o.push_back((char)side);
+        o.push_back((char)is_null);
+        u32((uint32_t)name.size());
+        o += name;
+        u32((uint32_t)tags.size());
+        for (const Guid& g : tags) {
+            o.append(reinterpret_cast<const char*>(&g.lo), 8);
+            o.append(reinterpret_cast<const char*>(&g.hi), 8);
+        }
+    };
+    for (const auto& kv : m.addSet) entry(0, 0, kv.first, kv.second);
+    for (const auto& kv : m.removeSet) entry(1, 0, kv.first, kv.second);
+    entry(0, 1, std::string(), m.nullAddGuid);
+    entry(1, 1, std::string(), m.nullRemoveGuid);
+    if (o.size() <= cap) std::memcpy(out, o.data(), o.size());
+    return (int64_t)o.size();
+}
+
 // 1 if the payload is accepted by PNCounterMsg.Decode at width eb (the wire contract), else 0.
 int orc_json_accepts_pnc(const char* bytes, uint64_t len, uint32_t eb) {
     try {

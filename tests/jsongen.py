@@ -108,3 +108,93 @@ CONTRACT = [
     (b'{"pVector":[],"nVector":{}}', False, False),
     (b'\xef\xbb\xbf{"pVector":{},"nVector":{}}', False, False),
 ]
+
+
+# ---- ORSetMsg<string> payloads (ORSet.cs:56-69) ------------------------------------------------------
+_ORSET_MEMBERS = ("addSet", "removeSet", "nullAddGuid", "nullRemoveGuid")
+
+
+def json_str(s: str, mode: str = "default") -> str:
+    """A JSON string literal for s.  default: JavaScriptEncoder.Default's shape (printable ASCII except
+    " & ' + < > ` \\ kept, every other UTF-16 unit as \\uXXXX); raw: UTF-8 kept, only what JSON requires
+    escaped; all: every character as \\uXXXX (surrogate pairs above U+FFFF)."""
+    out = []
+    for ch in s:
+        c = ord(ch)
+        units = [c] if c < 0x10000 else [0xD800 | (c - 0x10000) >> 10, 0xDC00 | ((c - 0x10000) & 0x3FF)]
+        if mode == "all":
+            out.extend(f"\\u{u:04X}" for u in units)
+        elif mode == "raw":
+            if ch == '"':
+                out.append('\\"')
+            elif ch == "\\":
+                out.append("\\\\")
+            elif c < 0x20:
+                out.append({8: "\\b", 9: "\\t", 10: "\\n", 12: "\\f", 13: "\\r"}.get(c, f"\\u{c:04x}"))
+            else:
+                out.append(ch)
+        else:
+            if 0x20 <= c < 0x7F and ch not in "\"&'+<>`\\":
+                out.append(ch)
+            elif ch == "\\":
+                out.append("\\\\")
+            else:
+                out.extend(f"\\u{u:04X}" for u in units)
+    return '"' + "".join(out) + '"'
+
+
+def encode_orset(add, rem, nadd=(), nrem=(), mode="default", ws="", order=None, upper=False) -> bytes:
+    """add / rem: list of (element str, [(lo, hi) tags]); nadd / nrem: null tag lists.  ws is put
+    between tokens; order permutes the four members; upper prints Guid hex upper-case."""
+    def g(t):
+        s = guid_d(*t)
+        return json_str(s.upper() if upper else s, "raw" if mode == "all" else mode) if mode != "all" else json_str(s, "all")
+
+    def tags(ts):
+        return "[" + ws + ("," + ws).join(g(t) for t in ts) + ws + "]"
+
+    def dmap(m):
+        return "{" + ws + ("," + ws).join(json_str(e, mode) + ws + ":" + ws + tags(ts) for e, ts in m) + ws + "}"
+
+    vals = {"addSet": dmap(add), "removeSet": dmap(rem), "nullAddGuid": tags(nadd), "nullRemoveGuid": tags(nrem)}
+    names = order or _ORSET_MEMBERS
+    body = ("," + ws).join(json_str(k, "raw") + ws + ":" + ws + vals[k] for k in names)
+    return (ws + "{" + ws + body + ws + "}" + ws).encode()
+
+
+class ORSetCluster:
+    """Valid ORSetMsg states of many sets: each set has a growing pool of element strings (ASCII words,
+    escapes-needing text, non-BMP characters, the empty string) and per-element tag pools; a state lists
+    a random subset of the set's elements with non-empty add tag sets, tombstones drawn from them, and
+    optional null tag sets."""
+
+    WORDS = ["a", "bb", "x y", "q\"uote", "back\\slash", "tab\tnl\n", "café", "中文", "emoji\U0001F600", "", "<&'+>`",
+             "ctl\u0001", "ÿĀ", "z" * 40]
+
+    def __init__(self, rng, n_sets, grow=0.3):
+        self.rng, self.grow = rng, grow
+        self.elems = [[] for _ in range(n_sets)]
+        self.tags = [{} for _ in range(n_sets)]
+        self.null_tags = [random_guids(rng, 3) for _ in range(n_sets)]
+
+    def _new_elem(self, s):
+        rng = self.rng
+        k = len(self.elems[s])
+        base = self.WORDS[int(rng.integers(0, len(self.WORDS)))]
+        e = base + ("" if k == 0 and base == "" else f"#{k}")
+        self.elems[s].append(e)
+        self.tags[s][e] = random_guids(rng, int(rng.integers(1, 4)))
+        return e
+
+    def state(self, s):
+        rng = self.rng
+        if not self.elems[s] or rng.random() < self.grow:
+            self._new_elem(s)
+        es = self.elems[s]
+        pick = [e for e in es if rng.random() < 0.7] or [es[-1]]
+        rng.shuffle(pick)
+        add = [(e, [t for t in self.tags[s][e] if rng.random() < 0.8] or self.tags[s][e][:1]) for e in pick]
+        rem = [(e, ts[: int(rng.integers(0, len(ts) + 1))]) for e, ts in add if rng.random() < 0.3]
+        nadd = self.null_tags[s][: int(rng.integers(0, 4))]
+        nrem = nadd[: int(rng.integers(0, len(nadd) + 1))]
+        return add, rem, nadd, nrem

@@ -28,6 +28,7 @@ _SIGS = {
     "orc_bench_orset_merge": ([_u64, _u32, _u32, _u32, _u32, _u32, _u64, _i32, _i32], C.c_double),
     "orc_json_encode_pnc": ([_u64, _vp, _vp, _vp, _vp, _u32, _vp, _u64], C.c_int64),
     "orc_json_accepts_pnc": ([C.c_char_p, _u64, _u32], C.c_int),
+    "orc_json_decode_orset": ([C.c_char_p, _u64, _vp, _u64], C.c_int64),
     "orc_pnc_apply_json": ([_u64, _u32, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
 }
 
@@ -189,3 +190,57 @@ def pnc_apply_json(P, N, cols, ncols, key_idx, msgs, eb):
     bad = _u64(0)
     rc = lib().orc_pnc_apply_json(n_keys, R, eb, _p(P), _p(N), _p(cols), _p(ncols), len(msgs), _p(k), _p(off), data, C.byref(bad))
     return P, N, cols, ncols, (None if bad.value == 2**64 - 1 else bad.value), rc
+
+
+def json_decode_orset(payload: bytes):
+    """ORSetMsg.Decode of one payload in Merge's walk order: list of (side, is_null, name bytes, [(lo, hi)]),
+    or None if Decode throws."""
+    n = lib().orc_json_decode_orset(payload, len(payload), None, 0)
+    if n < 0:
+        return None
+    buf = np.empty(max(1, n), np.uint8)
+    assert lib().orc_json_decode_orset(payload, len(payload), _p(buf), n) == n
+    raw, at, out = buf.tobytes()[:n], 0, []
+    while at < n:
+        side, is_null = raw[at], raw[at + 1]
+        ln = int.from_bytes(raw[at + 2:at + 6], "little")
+        name = raw[at + 6:at + 6 + ln]
+        at += 6 + ln
+        nt = int.from_bytes(raw[at:at + 4], "little")
+        at += 4
+        tags = np.frombuffer(raw[at:at + 16 * nt], np.uint64).reshape(nt, 2) if nt else np.zeros((0, 2), np.uint64)
+        at += 16 * nt
+        out.append((side, bool(is_null), name, [(int(a), int(b)) for a, b in tags]))
+    return out
+
+
+def orset_apply_json(set_ids, msgs, names=None):
+    """The stable-apply loop over ORSetMsg payloads (SafeCRDT.ApplyUpdateStable -> Decode -> Merge in
+    commit order) with element strings interned per set at first insertion (ids never reused).
+    names: {set: {name bytes: id}} carried between calls (updated in place), with "next" ids in
+    names[("next", set)].  Returns (add records, tombstone records, first bad message or None, its
+    code: "EINVAL" for a Decode error, "ESTATE" for an empty add tag set), records sorted."""
+    names = {} if names is None else names
+    add, rem = set(), set()
+    bad, code = None, None
+    for m, (sid, p) in enumerate(zip(set_ids, msgs)):
+        d = json_decode_orset(p)
+        if d is None:
+            bad, code = m, "EINVAL"
+            break
+        if any(side == 0 and not is_null and not tags for side, is_null, _, tags in d):
+            bad, code = m, "ESTATE"
+            break
+        tab = names.setdefault(int(sid), {})
+        for side, is_null, name, tags in d:
+            if is_null:
+                eid = NULL_ELEM
+            else:
+                if name not in tab:
+                    tab[name] = names.get(("next", int(sid)), 0)
+                    names[("next", int(sid))] = tab[name] + 1
+                eid = tab[name]
+            for lo, hi in tags:
+                (rem if side else add).add((int(sid) << 32 | eid, lo, hi))
+    mk = lambda s: np.array(sorted(s), dtype=REC_DTYPE) if s else np.zeros(0, REC_DTYPE)
+    return mk(add), mk(rem), bad, code

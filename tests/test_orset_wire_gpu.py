@@ -1,0 +1,192 @@
+"""GPU parity of the OR-Set wire path (jg_orset_wave_* / jg_orset_merge_json, csrc/orset_wire.hip).
+
+ORSetMsg<string> payloads are decoded, their element strings interned and the states merged on the
+device; the oracle is the restated ORSetMsg.Decode (oracle/json.hpp, ORSet.cs:56-63) driven through
+tests/oracle_ref.orset_apply_json: Decode + Merge in commit order, element ids issued per set at first
+insertion.  Comparisons are exact: the store's record streams, the ids each wave issued (set, id,
+string), and the first rejected message with its code.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import janus_gpu as jg
+import jsongen as J
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+G1, G2, G3 = (0x1122334455667788, 0x99AABBCCDDEEFF00), (0x0102030405060708, 0x0A0B0C0D0E0F1011), (7, 9)
+_A, _B = J.guid_d(*G1), J.guid_d(*G2)
+
+
+def _model_names(model, before):
+    """New (set, id, bytes) entries of the oracle's interning since `before` (a copy), sorted."""
+    out = []
+    for s, tab in model.items():
+        if isinstance(s, tuple):
+            continue
+        old = before.get(s, {})
+        out.extend((s, i, n) for n, i in tab.items() if n not in old)
+    return sorted(out)
+
+
+def _copy(model):
+    return {k: (dict(v) if isinstance(v, dict) else v) for k, v in model.items()}
+
+
+def _union(acc, recs):
+    return np.unique(np.concatenate([acc, recs])) if len(recs) else acc
+
+
+def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3):
+    rng = np.random.default_rng(seed)
+    cl = J.ORSetCluster(rng, n_sets)
+    s = jg.ORSetStore(ctx)
+    model = {}
+    acc_a, acc_r = np.zeros(0, orc.REC_DTYPE), np.zeros(0, orc.REC_DTYPE)
+    try:
+        for w in range(waves):
+            sets, msgs = [], []
+            for i in range(per_wave):
+                sid = int(rng.integers(0, n_sets))
+                a, r, na, nr = cl.state(sid)
+                mode = modes[i % len(modes)]
+                msgs.append(J.encode_orset(a, r, na, nr, mode=mode, ws=" \t\r\n" if i % 7 == 3 else "",
+                                           order=list(reversed(J._ORSET_MEMBERS)) if i % 5 == 2 else None, upper=i % 11 == 4))
+                sets.append(sid)
+            before = _copy(model)
+            ea, er, bad, _ = orc.orset_apply_json(sets, msgs, model)
+            assert bad is None
+            acc_a, acc_r = _union(acc_a, ea), _union(acc_r, er)
+            cut = sorted(set(int(x) for x in rng.integers(0, len(msgs), chunks - 1)))
+            bounds = [0] + cut + [len(msgs)]
+            rc, first_bad = s.wave([(sets[b:e], msgs[b:e]) for b, e in zip(bounds, bounds[1:])])
+            assert rc == jg.JG_OK and first_bad is None
+            assert s.wave_names() == _model_names(model, before)
+            ga, gr = s.read()
+            assert np.array_equal(ga, acc_a) and np.array_equal(gr, acc_r)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("seed,n_sets,waves,per_wave", [(1, 3, 3, 40), (2, 64, 3, 600), (3, 500, 2, 3000)])
+def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave):
+    _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default", "raw", "all"))
+
+
+def test_hash_collisions_take_the_exact_path(ctx, monkeypatch):
+    """With the string hash narrowed to 3 bits every run of equal hashes mixes strings: labels, duplicate
+    detection and the element table must still compare strings byte for byte."""
+    monkeypatch.setenv("JANUS_TEST_NAME_HASH_BITS", "3")
+    _run_waves(ctx, 4, 6, 3, 120, modes=("default", "raw"))
+
+
+def test_names_sync_and_clear(ctx):
+    s = jg.ORSetStore(ctx)
+    try:
+        # host-issued names (ORSet.Add ops) registered first: the wave resolves to them
+        s.names_sync(sets=[0, 1], next_ids=[2, 1], cleared=[0, 0], names=[(0, 0, b"x"), (0, 1, "é".encode()), (1, 0, b"x")])
+        m = [J.encode_orset([("é", [G1]), ("new", [G2])], [("x", [G3])]), J.encode_orset([("x", [G1])], [], [G2])]
+        s.merge_json([0, 1], m)
+        assert s.wave_names() == [(0, 2, b"new")]
+        ga, gr = s.read()
+        exp_a = sorted([(0 << 32 | 1, *G1), (0 << 32 | 2, *G2), (1 << 32 | 0, *G1), (1 << 32 | jg.NULL_ELEM, *G2)])
+        assert [tuple(int(v) for v in r) for r in ga] == exp_a
+        assert [tuple(int(v) for v in r) for r in gr] == [(0 << 32 | 0, *G3)]
+        # Clear of set 0: its strings are dropped, ids keep growing; set 1 keeps "x"
+        s.names_sync(sets=[0], next_ids=[3], cleared=[1])
+        s.merge_json([0, 1, 0], [J.encode_orset([("x", [G2])], []), J.encode_orset([("x", [G3])], []),
+                                 J.encode_orset([("new", [G3]), ("x", [G1])], [])])
+        assert s.wave_names() == [(0, 3, b"x"), (0, 4, b"new")]
+        ga, _ = s.read()
+        keys = {int(r["key"]) for r in ga}
+        assert {0 << 32 | 3, 0 << 32 | 4, 1 << 32 | 0} <= keys
+    finally:
+        s.close()
+
+
+_GOOD = J.encode_orset([("a", [G1])], [("a", [G1])], [G2], [])
+# (payload, expected code or None): the ORSetMsg wire contract of oracle/json.hpp, plus the engine's
+# empty-add-set limit (JG_ESTATE) and the reader's error order
+_CASES = [
+    (J.encode_orset([("a", [G1, G1, G2])], []), None),                     # repeated tag in one array: one record
+    (J.encode_orset([], [], [], []), None),
+    (J.encode_orset([("a", [G1])], [("a", [])]), None),                    # empty tombstone set is fine
+    (J.encode_orset([("a", [G1])], [], [], [], mode="all"), None),         # escaped names and Guids
+    (b'{"add\\u0053et":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', None),
+    (J.encode_orset([("a", [G1])], [], upper=True, ws="\r\n\t "), None),
+    (J.encode_orset([("a", [])], []), jg.JG_ESTATE),
+    (J.encode_orset([("a", [G1]), ("b", [])], []), jg.JG_ESTATE),
+    (J.encode_orset([("a", [G1]), ("a", [G2])], []), jg.JG_EINVAL),
+    (J.encode_orset([("a", [G1])], [("b", [G1]), ("b", [])]), jg.JG_EINVAL),
+    (J.encode_orset([("a", [G1])], [], mode="all")[:-1] + b',"a":[]}', jg.JG_EINVAL),
+    (J.encode_orset([("a", []), ("a", [G1])], []), jg.JG_ESTATE),          # the empty set is met first
+    (J.encode_orset([("a", [G1]), ("a", [])], []), jg.JG_EINVAL),          # the repeat is met first
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":null,"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":null},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[],"x":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{},"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]} x', jg.JG_EINVAL),
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]', jg.JG_EINVAL),
+    (b'{"addSet":{"\xff":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"\\ud800":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A[:-1].encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A.replace("-", "x", 1).encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A.encode() + b'",]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a\x01":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":["' + _B.encode() + b'"],"nullRemoveGuid":null}', jg.JG_EINVAL),
+    (b'', jg.JG_EINVAL),
+]
+
+
+@pytest.mark.parametrize("idx", range(len(_CASES)))
+def test_contract_case_in_a_wave(ctx, idx):
+    """Case payload at position 3 of a 6-message wave: the first bad message and its code, then the
+    prefix before it merges exactly as the oracle's loop leaves the store."""
+    payload, code = _CASES[idx]
+    dec = orc.json_decode_orset(payload)
+    if code is None:
+        assert dec is not None
+    elif code == jg.JG_EINVAL:
+        assert dec is None  # the oracle's Decode rejects it too
+    msgs = [_GOOD, J.encode_orset([("b", [G2])], []), _GOOD, payload, J.encode_orset([("c", [G3])], []), _GOOD]
+    sets = [0, 1, 2, 0, 1, 2]
+    s = jg.ORSetStore(ctx)
+    try:
+        rc, bad = s.wave([(sets[:2], msgs[:2]), (sets[2:], msgs[2:])])
+        assert rc == (code or jg.JG_OK)
+        assert bad == (None if code is None else 3)
+        lim = 6 if code is None else 3
+        ea, er, _, _ = orc.orset_apply_json(sets[:lim], msgs[:lim])
+        ga, gr = s.read()
+        assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+        # one-shot form: all or nothing
+        t = jg.ORSetStore(ctx)
+        try:
+            if code is None:
+                t.merge_json(sets, msgs)
+                assert all(np.array_equal(x, y) for x, y in zip(t.read(), s.read()))
+            else:
+                with pytest.raises(jg.JanusError) as ei:
+                    t.merge_json(sets, msgs)
+                assert ei.value.code == code and ei.value.bad_msg == 3
+                assert [len(x) for x in t.read()] == [0, 0]
+        finally:
+            t.close()
+    finally:
+        s.close()
+
+
+def test_empty_and_all_bad_waves(ctx):
+    s = jg.ORSetStore(ctx)
+    try:
+        s.merge_json([], [])
+        assert [len(x) for x in s.read()] == [0, 0]
+        rc, bad = s.wave([([5], [b"{"])])
+        assert rc == jg.JG_EINVAL and bad == 0
+        assert [len(x) for x in s.read()] == [0, 0] and s.wave_names() == []
+    finally:
+        s.close()
