@@ -1,6 +1,7 @@
 // janus_host.cpp — see janus_host.hpp.
 #include "janus_host.hpp"
 
+#include <cstdio>
 #include <cstring>
 
 #include <algorithm>
@@ -23,12 +24,6 @@ std::string last_error() {
     jg_last_error(buf, sizeof buf);
     return buf;
 }
-bool rec_less(const jg_tagrec& a, const jg_tagrec& b) {
-    if (a.key != b.key) return a.key < b.key;
-    if (a.tag_lo != b.tag_lo) return a.tag_lo < b.tag_lo;
-    return a.tag_hi < b.tag_hi;
-}
-bool rec_eq(const jg_tagrec& a, const jg_tagrec& b) { return a.key == b.key && a.tag_lo == b.tag_lo && a.tag_hi == b.tag_hi; }
 }  // namespace
 
 void GpuStableStore::check(int rc) const {
@@ -43,8 +38,7 @@ GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas,
 }
 
 GpuStableStore::~GpuStableStore() {
-    for (auto& c : chunks_)
-        if (c.first) jg_host_free(c.first);
+    for (auto& a : arenas_) jg_host_free(a.first);
     if (orset_) jg_orset_destroy(orset_);
     if (pnc_) jg_pnc_destroy(pnc_);
     if (ctx_) jg_close(ctx_);
@@ -85,8 +79,10 @@ const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want
     return *r;
 }
 
-uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e, bool create) {
+uint32_t GpuStableStore::elem_id(uint32_t set, const std::optional<std::string>& e, bool create) {
     if (!e) return JG_NULL_ELEM;
+    SetKey& s = sets_[set];
+    for (; s.indexed < s.names.size(); ++s.indexed) s.elems.emplace(s.names[s.indexed], s.indexed);  // ids a wave issued
     auto it = s.elems.find(*e);
     if (it != s.elems.end()) return it->second;
     if (!create) return JG_NULL_ELEM - 1;  // never allocated: no records carry it
@@ -95,6 +91,8 @@ uint32_t GpuStableStore::elem_id(SetKey& s, const std::optional<std::string>& e,
     if (id >= JG_NULL_ELEM - 1) throw EngineError(JG_ESTATE, "too many elements in one OR-Set");
     s.elems.emplace(*e, id);
     s.names.push_back(*e);
+    s.indexed = (uint32_t)s.names.size();
+    pending_names_[set].ids.push_back(id);
     return id;
 }
 
@@ -218,18 +216,75 @@ WorkerPool& GpuStableStore::pool() {
     return *pool_;
 }
 
-char* GpuStableStore::chunk_buffer(size_t c, size_t bytes) {
-    if (chunks_.size() <= c) chunks_.resize(c + 1, {nullptr, 0});
-    auto& s = chunks_[c];
-    if (s.second < bytes) {
-        if (s.first) jg_host_free(s.first);
-        s = {nullptr, 0};
-        void* p = nullptr;
-        const size_t want = bytes + bytes / 4 + 4096;
-        check(jg_host_alloc(ctx_, want, &p));
-        s = {static_cast<char*>(p), want};
+void GpuStableStore::flush_names() {
+    if (pending_names_.empty()) return;
+    std::vector<uint32_t> set, next, nset, nid;
+    std::vector<uint8_t> cleared, bytes;
+    std::vector<uint64_t> off{0};
+    for (const auto& kv : pending_names_) {
+        const SetKey& sk = sets_[kv.first];
+        set.push_back(kv.first);
+        next.push_back((uint32_t)sk.names.size());
+        cleared.push_back(kv.second.cleared ? 1 : 0);
+        for (uint32_t id : kv.second.ids) {
+            const std::string& nm = sk.names[id];
+            nset.push_back(kv.first);
+            nid.push_back(id);
+            bytes.insert(bytes.end(), nm.begin(), nm.end());
+            off.push_back(bytes.size());
+        }
     }
-    return s.first;
+    if (bytes.empty()) bytes.push_back(0);
+    check(jg_orset_names_sync(orset_, set.size(), set.data(), next.data(), cleared.data(), nid.size(), nset.data(), nid.data(), off.data(),
+                              bytes.data()));
+    pending_names_.clear();
+}
+
+// The element ids the last wave issued (sorted by set, then id) appended to the host tables, the sets
+// split over the workers in contiguous ranges.
+void GpuStableStore::take_wave_names() {
+    uint64_t n = 0, nb = 0;
+    check(jg_orset_wave_names(orset_, &n, &nb, nullptr, nullptr, nullptr, nullptr));
+    if (n == 0) return;
+    std::vector<uint32_t> set(n), id(n);
+    std::vector<uint64_t> off(n + 1);
+    std::vector<uint8_t> bytes(std::max<uint64_t>(nb, 1));
+    check(jg_orset_wave_names(orset_, &n, &nb, set.data(), id.data(), off.data(), bytes.data()));
+    std::vector<int> bad(pool().size(), 0);
+    parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+        while (b < n && b > 0 && set[b - 1] == set[b]) ++b;  // that set belongs to the previous worker
+        while (e < n && e > 0 && set[e - 1] == set[e]) ++e;
+        for (size_t i = b; i < e; ++i) {
+            SetKey& sk = sets_[set[i]];
+            if (id[i] != sk.names.size()) { bad[t] = 1; return; }
+            sk.names.emplace_back(reinterpret_cast<const char*>(bytes.data()) + off[i], off[i + 1] - off[i]);  // elems: lazily
+        }
+    });
+    for (int b : bad)
+        if (b) throw EngineError(JG_ESTATE, "element ids of the engine and the host tables disagree");
+}
+
+// Pinned staging for wave chunks: arenas carved front to back each wave and kept for the next; a wave
+// bigger than all arenas adds one as large as the pool so far (the pool doubles), so a steady stream of
+// waves stops allocating pinned memory (hipHostMalloc costs ~0.3 ms per MB) after its first few waves.
+char* GpuStableStore::stage(size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    while (arena_i_ < arenas_.size() && arena_off_ + bytes > arenas_[arena_i_].second) {
+        ++arena_i_;
+        arena_off_ = 0;
+    }
+    if (arena_i_ == arenas_.size()) {
+        size_t total = 0;
+        for (const auto& a : arenas_) total += a.second;
+        const size_t cap = std::max({bytes, total, size_t(64) << 20});
+        void* p = nullptr;
+        check(jg_host_alloc(ctx_, cap, &p));
+        arenas_.emplace_back(static_cast<char*>(p), cap);
+        arena_off_ = 0;
+    }
+    char* r = arenas_[arena_i_].first + arena_off_;
+    arena_off_ += bytes;
+    return r;
 }
 
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
@@ -270,33 +325,39 @@ void GpuStableStore::ReceivedBlock(const std::vector<UpdateMessage>& block) {
 std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const NetworkProtocol*>& msgs,
                                                  std::unordered_map<uint64_t, uint64_t>* tracker, double t0) {
     flush_registrations();
+    flush_names();
+    arena_i_ = arena_off_ = 0;  // the previous wave's staged chunks are no longer referenced
     const size_t n = msgs.size();
     WorkerPool& wp = pool();
     const int T = wp.size();
     phase_s_[0] = wall_s() - t0;
     constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1;
-    static const size_t chunk_msgs = [] {
+    // Chunks of ~48 MB of payload (sized from the previous wave's bytes per message): the staging
+    // buffers stay few and reusable, and the first chunk's upload starts early.
+    static const size_t chunk_env = [] {
         const char* e = std::getenv("JANUS_WAVE_CHUNK");
-        return e ? std::max<size_t>(1, std::strtoull(e, nullptr, 10)) : size_t{131072};
+        return e ? std::max<size_t>(1, std::strtoull(e, nullptr, 10)) : size_t{0};
     }();
+    const size_t chunk_msgs = chunk_env ? chunk_env : std::clamp<size_t>((size_t)((48u << 20) / std::max(avg_msg_bytes_, 64.0)), 8192, 131072);
 
-    // The wave is streamed in chunks of commit order: classify + gather chunk c on the host workers
-    // while the engine uploads and scans chunk c-1 (jg_pnc_wave_append returns once queued).
-    // A chunk's pinned buffer: [payload | pad 16 | off (m+1) u64 | rows u32]; it stays untouched
-    // until the wave is committed or aborted.
-    std::vector<uint32_t> cls(n);
+    // Both kinds of states are uploaded undecoded and streamed in chunks of commit order: the host
+    // workers classify + gather chunk c (per kind, into its pinned buffer) while the engine uploads and
+    // runs the validation pass of chunk c-1 (the append calls return once queued).  A chunk's pinned
+    // buffer: [payload | pad 16 | off (m+1) u64 | rows or set ids u32]; untouched until commit / abort.
+    // cls[i]: PNC row, kSet (sid[i] = the set), or kSkip (create / keyspace / unknown uid, :133-136).
+    std::vector<uint32_t> cls(n), sid(n);
     struct Chunk { size_t m; char* buf; uint64_t* off; uint32_t* rows; uint8_t* bytes; };
-    std::vector<Chunk> chunks;
-    std::vector<uint64_t> where;  // PNC message (wave order) -> commit index
-    std::vector<size_t> cnt(T), nbytes(T), mbase(T + 1), bbase(T + 1);
+    std::vector<Chunk> chunks[2];
+    std::vector<uint64_t> where[2];  // message of a kind (wave order) -> commit index
+    std::vector<size_t> cnt(2 * T), nbytes(2 * T), mbase(2 * (T + 1)), bbase(2 * (T + 1));
     const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
-    bool open = false;
+    bool open[2] = {false, false};
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
         const size_t c0 = c * chunk_msgs, c1 = std::min(n, c0 + chunk_msgs);
         const double ta = wall_s();
         parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
-            size_t k = 0, bytes = 0;
+            size_t k[2] = {0, 0}, bytes[2] = {0, 0};
             for (size_t i = c0 + b; i < c0 + e; ++i) {
                 if (i + 16 < c0 + e) __builtin_prefetch(msgs[i + 16]);
                 if (i + 8 < c0 + e) uids_.prefetch(msgs[i + 8]->uid);
@@ -304,197 +365,124 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                 uint32_t cl = kSkip;
                 if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
                     if (const KeyRef* kr = uids_.find(u.uid)) {                                  // :136
-                        if (kr->type == CrdtType::PNCounter) { cl = kr->idx; ++k; bytes += u.message.size(); }
-                        else cl = kSet;
+                        const int kind = kr->type == CrdtType::PNCounter ? 0 : 1;
+                        if (kind == 0) cl = kr->idx;
+                        else { cl = kSet; sid[i] = kr->idx; }
+                        ++k[kind];
+                        bytes[kind] += u.message.size();
                     }
                 }
                 cls[i] = cl;
             }
-            cnt[t] = k;
-            nbytes[t] = bytes;
-        });
-        for (int t = 0; t < T; ++t) { mbase[t + 1] = mbase[t] + cnt[t]; bbase[t + 1] = bbase[t] + nbytes[t]; }
-        const size_t m = mbase[T], nb = bbase[T], nb_pad = (nb + 15) & ~size_t(15);
-        const double tb = wall_s();
-        t_classify += tb - ta;
-        if (m == 0) continue;
-        char* buf = chunk_buffer(chunks.size(), nb_pad + (m + 1) * 8 + m * 4 + 64);
-        Chunk ch{m, buf, reinterpret_cast<uint64_t*>(buf + nb_pad), nullptr, reinterpret_cast<uint8_t*>(buf)};
-        ch.rows = reinterpret_cast<uint32_t*>(ch.off + m + 1);
-        const size_t w0 = where.size();
-        where.resize(w0 + m);
-        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
-            size_t j = mbase[t];
-            uint64_t o = bbase[t];
-            for (size_t i = c0 + b; i < c0 + e; ++i) {
-                if (i + 8 < c0 + e) __builtin_prefetch(msgs[i + 8]->message.data());
-                if (cls[i] >= kSet) continue;
-                const std::string& p = msgs[i]->message;
-                std::memcpy(ch.bytes + o, p.data(), p.size());
-                ch.off[j] = o;
-                ch.rows[j] = cls[i];
-                where[w0 + j] = i;
-                o += p.size();
-                ++j;
+            for (int kind = 0; kind < 2; ++kind) {
+                cnt[kind * T + t] = k[kind];
+                nbytes[kind * T + t] = bytes[kind];
             }
         });
-        ch.off[m] = nb;
+        size_t m[2], nb[2];
+        for (int kind = 0; kind < 2; ++kind) {
+            size_t* mb = &mbase[kind * (T + 1)];
+            size_t* bb = &bbase[kind * (T + 1)];
+            mb[0] = bb[0] = 0;
+            for (int t = 0; t < T; ++t) { mb[t + 1] = mb[t] + cnt[kind * T + t]; bb[t + 1] = bb[t] + nbytes[kind * T + t]; }
+            m[kind] = mb[T];
+            nb[kind] = bb[T];
+        }
+        const double tb = wall_s();
+        t_classify += tb - ta;
+        Chunk ch[2];
+        size_t w0[2];
+        for (int kind = 0; kind < 2; ++kind) {
+            if (m[kind] == 0) continue;
+            const size_t nb_pad = (nb[kind] + 15) & ~size_t(15);
+            char* buf = stage(nb_pad + (m[kind] + 1) * 8 + m[kind] * 4 + 64);
+            ch[kind] = Chunk{m[kind], buf, reinterpret_cast<uint64_t*>(buf + nb_pad), nullptr, reinterpret_cast<uint8_t*>(buf)};
+            ch[kind].rows = reinterpret_cast<uint32_t*>(ch[kind].off + m[kind] + 1);
+            w0[kind] = where[kind].size();
+            where[kind].resize(w0[kind] + m[kind]);
+        }
+        const double tg = wall_s();
+        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
+            size_t j[2] = {mbase[t], mbase[(T + 1) + t]};
+            uint64_t o[2] = {bbase[t], bbase[(T + 1) + t]};
+            for (size_t i = c0 + b; i < c0 + e; ++i) {
+                if (i + 8 < c0 + e) __builtin_prefetch(msgs[i + 8]->message.data());
+                if (cls[i] == kSkip) continue;
+                const int kind = cls[i] == kSet ? 1 : 0;
+                const std::string& p = msgs[i]->message;
+                Chunk& k = ch[kind];
+                std::memcpy(k.bytes + o[kind], p.data(), p.size());
+                k.off[j[kind]] = o[kind];
+                k.rows[j[kind]] = kind ? sid[i] : cls[i];
+                where[kind][w0[kind] + j[kind]] = i;
+                o[kind] += p.size();
+                ++j[kind];
+            }
+        });
         t_gather += wall_s() - tb;
-        if (!open) {
-            check(jg_pnc_wave_begin(pnc_, std::max<size_t>(m * n_chunks, 1), std::max<size_t>(nb * n_chunks, 1)));
-            open = true;
+        if (std::getenv("JANUS_TRACE_WAVE"))
+            std::fprintf(stderr, "chunk %zu: classify %.2f ms, buffers %.2f ms, gather %.2f ms (%zu + %zu msgs, %zu + %zu bytes)\n", c,
+                         1e3 * (tb - ta), 1e3 * (tg - tb), 1e3 * (wall_s() - tg), m[0], m[1], nb[0], nb[1]);
+        for (int kind = 0; kind < 2; ++kind) {
+            if (m[kind] == 0) continue;
+            ch[kind].off[m[kind]] = nb[kind];
+            if (!open[kind]) {
+                const uint64_t cap_m = std::max<size_t>(m[kind] * n_chunks, 1), cap_b = std::max<size_t>(nb[kind] * n_chunks, 1);
+                check(kind ? jg_orset_wave_begin(orset_, cap_m, cap_b) : jg_pnc_wave_begin(pnc_, cap_m, cap_b));
+                open[kind] = true;
+            }
+            const int rc = kind ? jg_orset_wave_append(orset_, m[kind], ch[kind].rows, ch[kind].off, ch[kind].bytes)
+                                : jg_pnc_wave_append(pnc_, m[kind], ch[kind].rows, ch[kind].off, ch[kind].bytes);
+            if (rc != JG_OK) {
+                const std::string why = last_error();
+                if (open[0]) jg_pnc_wave_abort(pnc_);
+                if (open[1]) jg_orset_wave_abort(orset_);
+                throw EngineError(rc, why);
+            }
+            chunks[kind].push_back(ch[kind]);
         }
-        const int rc = jg_pnc_wave_append(pnc_, m, ch.rows, ch.off, ch.bytes);
-        if (rc != JG_OK) {
-            jg_pnc_wave_abort(pnc_);
-            check(rc);
-        }
-        chunks.push_back(ch);
     }
     phase_s_[1] = t_classify;
     phase_s_[2] = t_classify + t_gather;
+    {
+        size_t tot_m = 0, tot_b = 0;
+        for (int kind = 0; kind < 2; ++kind)
+            for (const Chunk& ch : chunks[kind]) { tot_m += ch.m; tot_b += (size_t)ch.off[ch.m]; }
+        if (tot_m) avg_msg_bytes_ = (double)tot_b / (double)tot_m;
+    }
 
-    // OR-Set states: one parse per payload, straight into element interning and records (no decoded
-    // ORSetState).  Sets are independent, so the states are grouped by set (stable: commit order
-    // within a set) and the sets split into contiguous id ranges over the workers; each worker interns
-    // its sets' elements in commit order and keeps each set's distinct records (a full-state message
-    // repeats most of them), sorted.  Worker outputs concatenated in worker order are sorted by
-    // (set, elem, tag).  A payload the reader rejects cuts the wave at the first one in commit order:
-    // the records of later states are dropped and the element ids they issued are withdrawn.
-    std::vector<size_t> set_msgs;
-    for (size_t i = 0; i < n; ++i)
-        if (cls[i] == kSet) set_msgs.push_back(i);
-    std::vector<size_t> first_bad(T, SIZE_MAX);
-    std::vector<int> bad_code(T, JG_OK);
-    std::vector<std::string> why(T);
-    std::vector<std::vector<jg_tagrec>> wadd(T), wrem(T);
-    auto rollback = [](SetKey& sk, size_t names0) {  // withdraw the ids issued since names0
-        for (size_t q = names0; q < sk.names.size(); ++q) sk.elems.erase(sk.names[q]);
-        sk.names.resize(names0);
-    };
-    std::vector<uint32_t> names_at_start(next_set_);
-    for (uint32_t q = 0; q < next_set_; ++q) names_at_start[q] = (uint32_t)sets_[q].names.size();
-    const double to0 = wall_s();
-    auto intern_pass = [&](size_t n_set) {  // the first n_set OR-Set states (commit order)
-        std::vector<uint32_t> set_of(n_set);
-        for (size_t j = 0; j < n_set; ++j) set_of[j] = uids_.find(msgs[set_msgs[j]]->uid)->idx;
-        std::vector<uint32_t> first(next_set_ + 1, 0);  // counting sort by set id
-        for (size_t j = 0; j < n_set; ++j) ++first[set_of[j] + 1];
-        for (uint32_t q = 0; q < next_set_; ++q) first[q + 1] += first[q];
-        std::vector<uint32_t> grouped(n_set);
-        {
-            std::vector<uint32_t> at(first.begin(), first.end() - 1);
-            for (size_t j = 0; j < n_set; ++j) grouped[at[set_of[j]]++] = (uint32_t)j;
-        }
-        // worker t takes the sets whose grouped messages start in [n_set*t/T, n_set*(t+1)/T)
-        parallel_ranges(wp, n_set, [&](size_t b, size_t e, int t) {
-            if (b >= e) return;
-            // whole sets only: start at the first set beginning at or after b, end at the first set at or after e
-            uint32_t s0 = set_of[grouped[b]], s1 = e < n_set ? set_of[grouped[e]] : next_set_;
-            if (b > 0 && set_of[grouped[b - 1]] == s0) ++s0;  // that set belongs to the previous worker
-            if (e < n_set && set_of[grouped[e - 1]] == s1) ++s1;
-            // A full-state message repeats most of its set's records: each set's records pass a per-side
-            // hash set before they are stored, so only distinct records are kept and sorted.
-            struct RecSet {
-                std::vector<jg_tagrec> slot;
-                std::vector<uint32_t> gen;  // slot is live iff gen == cur (O(1) reset per set)
-                uint32_t cur = 1;
-                size_t n = 0;
-                static uint64_t h(const jg_tagrec& r) {
-                    uint64_t x = r.key * 0x9E3779B97F4A7C15ull ^ r.tag_lo ^ (r.tag_hi * 0xBF58476D1CE4E5B9ull);
-                    x ^= x >> 31;
-                    x *= 0x94D049BB133111EBull;
-                    return x ^ (x >> 29);
-                }
-                void reset() {
-                    if (++cur == 0) { std::fill(gen.begin(), gen.end(), 0u); cur = 1; }
-                    n = 0;
-                }
-                bool insert(const jg_tagrec& r) {  // true if new
-                    if ((n + 1) * 2 > slot.size()) grow();
-                    const size_t mask = slot.size() - 1;
-                    for (size_t i = h(r) & mask;; i = (i + 1) & mask) {
-                        if (gen[i] != cur) { gen[i] = cur; slot[i] = r; ++n; return true; }
-                        if (rec_eq(slot[i], r)) return false;
-                    }
-                }
-                void grow() {
-                    std::vector<jg_tagrec> old;
-                    std::vector<uint32_t> og;
-                    old.swap(slot);
-                    og.swap(gen);
-                    const size_t sz = old.empty() ? 1024 : old.size() * 2;
-                    slot.assign(sz, jg_tagrec{0, 0, 0});
-                    gen.assign(sz, 0u);
-                    const uint32_t was = cur;
-                    cur = 1;
-                    n = 0;
-                    for (size_t i = 0; i < old.size(); ++i)
-                        if (og[i] == was) insert(old[i]);
-                }
-            };
-            struct Ctx {
-                GpuStableStore* self;
-                SetKey* sk;
-                uint64_t hi;
-                std::vector<jg_tagrec>* out[2];
-                RecSet seen[2];
-            } c{this, nullptr, 0, {&wadd[t], &wrem[t]}, {}};
-            for (uint32_t sid = s0; sid < s1 && sid < next_set_; ++sid) {
-                if (first[sid] == first[sid + 1]) continue;
-                c.sk = &sets_[sid];
-                c.hi = (uint64_t)sid << 32;
-                c.seen[0].reset();
-                c.seen[1].reset();
-                const size_t a0 = wadd[t].size(), r0 = wrem[t].size();
-                for (uint32_t x = first[sid]; x < first[sid + 1]; ++x) {
-                    const size_t i = set_msgs[grouped[x]];
-                    const size_t names0 = c.sk->names.size();
-                    try {
-                        wire::ScanORSetMsg(msgs[i]->message,
-                                           [](void* p, int side, std::string_view name, bool is_null, const Guid* tags, size_t nt) {
-                                               Ctx& k = *static_cast<Ctx*>(p);
-                                               if (side == 0 && !is_null && nt == 0)
-                                                   throw EngineError(JG_ESTATE, "empty add tag set (not produced by ORSet.Add)");
-                                               const uint64_t key = k.hi | (is_null ? JG_NULL_ELEM : k.self->elem_id(*k.sk, std::string(name), true));
-                                               for (size_t q = 0; q < nt; ++q) {
-                                                   const jg_tagrec r{key, tags[q].lo, tags[q].hi};
-                                                   if (k.seen[side].insert(r)) k.out[side]->push_back(r);
-                                               }
-                                           },
-                                           &c);
-                    } catch (const EngineError& err) {
-                        // the reference's loop stops at this state; later states of this set come after it
-                        rollback(*c.sk, names0);
-                        if (i < first_bad[t]) { first_bad[t] = i; why[t] = err.what(); bad_code[t] = err.code; }
-                        break;
-                    }
-                }
-                auto dedup = [](std::vector<jg_tagrec>& v, size_t from) {
-                    std::sort(v.begin() + from, v.end(), rec_less);
-                    v.erase(std::unique(v.begin() + from, v.end(), rec_eq), v.end());
-                };
-                dedup(wadd[t], a0);
-                dedup(wrem[t], r0);
-            }
-        });
-    };
-    intern_pass(set_msgs.size());
+    // OR-Set states: end the device validation; the first rejected state cuts the wave (the reference's
+    // loop stops at the state whose Decode / Merge throws).
     size_t cut = n;
     int cut_code = JG_OK;
     std::string cut_why;
-    for (int t = 0; t < T; ++t)
-        if (first_bad[t] < cut) { cut = first_bad[t]; cut_why = why[t]; cut_code = bad_code[t]; }
+    const double to0 = wall_s();
+    if (open[1]) {
+        uint64_t bad = UINT64_MAX;
+        const int rc = jg_orset_wave_check(orset_, &bad);
+        if (rc != JG_OK) {
+            const std::string why = last_error();
+            if (bad == UINT64_MAX) {
+                if (open[0]) jg_pnc_wave_abort(pnc_);
+                jg_orset_wave_abort(orset_);
+                throw EngineError(rc, why);
+            }
+            cut = where[1][bad];
+            cut_code = rc;
+            cut_why = why;
+        }
+    }
+    const double to1 = wall_s();
     phase_s_[3] = wall_s() - t0;
 
     const double t1 = wall_s();
     // Re-stream the first `limit` PNC messages (the reference's loop applied the messages before the
-    // one that threw; the engine's waves are all or nothing).
+    // one that threw; the engine's PN-Counter waves are all or nothing).
     auto submit_prefix = [&](size_t limit) {
         if (limit == 0) return;
         check(jg_pnc_wave_begin(pnc_, limit, 1));
         size_t left = limit;
-        for (const Chunk& ch : chunks) {
+        for (const Chunk& ch : chunks[0]) {
             if (!left) break;
             const size_t k = std::min(left, ch.m);
             check(jg_pnc_wave_append(pnc_, k, ch.rows, ch.off, ch.bytes));
@@ -502,16 +490,19 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         }
         check(jg_pnc_wave_commit(pnc_, nullptr));
     };
-    if (open) {
+    if (open[0]) {
         if (cut < n) {  // an OR-Set state before some of these PNC states was rejected
             check(jg_pnc_wave_abort(pnc_));
-            submit_prefix((size_t)(std::lower_bound(where.begin(), where.end(), (uint64_t)cut) - where.begin()));
+            submit_prefix((size_t)(std::lower_bound(where[0].begin(), where[0].end(), (uint64_t)cut) - where[0].begin()));
         } else {
             uint64_t bad = UINT64_MAX;
             const int rc = jg_pnc_wave_commit(pnc_, &bad);
             if (rc != JG_OK) {
-                if (bad == UINT64_MAX) check(rc);
-                cut = where[bad];
+                if (bad == UINT64_MAX) {
+                    if (open[1]) jg_orset_wave_abort(orset_);
+                    check(rc);
+                }
+                cut = where[0][bad];
                 cut_code = rc;
                 cut_why = last_error();
                 submit_prefix(bad);
@@ -519,37 +510,20 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         }
     }
     pnc_bytes_ = 0;
-    for (const Chunk& ch : chunks) pnc_bytes_ += ch.off[ch.m];
+    for (const Chunk& ch : chunks[0]) pnc_bytes_ += ch.off[ch.m];
 
-    // A cut (a rejected OR-Set or PN-Counter state) before some OR-Set state: redo the OR-Set part over
-    // the states before it, from the element tables as they were.
-    if (!set_msgs.empty() && set_msgs.back() >= cut) {
-        for (uint32_t q = 0; q < next_set_; ++q) rollback(sets_[q], names_at_start[q]);
-        for (int t = 0; t < T; ++t) { wadd[t].clear(); wrem[t].clear(); first_bad[t] = SIZE_MAX; }
-        size_t n_set = 0;
-        while (n_set < set_msgs.size() && set_msgs[n_set] < cut) ++n_set;
-        intern_pass(n_set);
-    }
-    std::vector<jg_tagrec> adds, rems;
-    {
-        size_t na = 0, nr = 0;
-        for (int t = 0; t < T; ++t) { na += wadd[t].size(); nr += wrem[t].size(); }
-        adds.reserve(na);
-        rems.reserve(nr);
-        for (int t = 0; t < T; ++t) {
-            adds.insert(adds.end(), wadd[t].begin(), wadd[t].end());
-            rems.insert(rems.end(), wrem[t].begin(), wrem[t].end());
-        }
-    }
-    const double to1 = wall_s();
-    double to2 = to1;
-    if (!adds.empty() || !rems.empty()) {
-        to2 = wall_s();
-        check(jg_orset_merge(orset_, adds.data(), adds.size(), rems.data(), rems.size()));
+    // OR-Set states before the cut: element strings interned in commit order, records unioned into the
+    // store (device); then the ids the wave issued join the host tables.
+    double to2 = wall_s(), to3 = to2;
+    if (open[1]) {
+        const uint64_t limit = (uint64_t)(std::lower_bound(where[1].begin(), where[1].end(), (uint64_t)cut) - where[1].begin());
+        check(jg_orset_wave_commit(orset_, limit));
+        to3 = wall_s();
+        take_wave_names();
     }
     orset_phase_s_[0] = to1 - to0;
-    orset_phase_s_[1] = to2 - to1;
-    orset_phase_s_[2] = wall_s() - to2;
+    orset_phase_s_[1] = to3 - to2;
+    orset_phase_s_[2] = wall_s() - to3;
     std::vector<uint64_t> completed;
     if (tracker)
         for (size_t i = 0; i < cut; ++i) {
@@ -594,9 +568,15 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) 
             // carries (Contains is false, ORSet.cs:174); Clear empties the Dictionaries, so elements
             // added afterwards take new, larger ids in their new insertion order (ORSet.cs:192-198)
             uint32_t id = 0;
-            if (op.opId == 1) id = elem_id(sk, op.elem, true);
-            else if (op.opId == 2) id = elem_id(sk, op.elem, false);
-            else sk.elems.clear();
+            if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
+            else if (op.opId == 2) id = elem_id(kr.idx, op.elem, false);
+            else {
+                sk.elems.clear();
+                sk.indexed = (uint32_t)sk.names.size();  // every id issued so far is dead
+                PendingNames& pn = pending_names_[kr.idx];
+                pn.cleared = true;
+                pn.ids.clear();
+            }
             oelem.push_back(id);
             oop.push_back((uint8_t)op.opId);
             olo.push_back(op.tag.lo);
@@ -624,7 +604,7 @@ int64_t GpuStableStore::QueryStablePNC(const Guid& uid) {
 
 bool GpuStableStore::QueryStableORSet(const Guid& uid, const std::optional<std::string>& elem) {
     const uint32_t set = ref(uid, CrdtType::ORSet).idx;
-    const uint32_t id = elem_id(sets_[set], elem, false);
+    const uint32_t id = elem_id(set, elem, false);
     uint8_t out = 0;
     check(jg_orset_contains(orset_, &set, &id, 1, &out));
     return out != 0;

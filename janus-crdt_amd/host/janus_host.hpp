@@ -212,17 +212,25 @@ class GpuStableStore {
         size_t n_ = 0;
     };
     struct SetKey {
-        std::unordered_map<std::string, uint32_t> elems;  // live interning (reset by Clear)
+        std::unordered_map<std::string, uint32_t> elems;  // live interning (reset by Clear), indexed lazily:
+        uint32_t indexed = 0;                              // names[indexed..] are live but not in elems yet
         std::vector<std::string> names;                   // id -> element, every id ever issued
     };
-    uint32_t elem_id(SetKey& s, const std::optional<std::string>& e, bool create);
+    uint32_t elem_id(uint32_t set, const std::optional<std::string>& e, bool create);
+    // Interning changes made here (ORSet.Add of a new element, Clear) that the engine's element table
+    // (the wave path, jg_orset_names_sync) has not seen yet, per set: cleared since the last sync, and
+    // the ids issued since then (or since the Clear).
+    struct PendingNames { bool cleared = false; std::vector<uint32_t> ids; };
+    std::unordered_map<uint32_t, PendingNames> pending_names_;
+    void flush_names();
+    void take_wave_names();  // ids the last OR-Set wave issued -> SetKey tables
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
     void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
     // The body of ApplyCommitted / ReceivedBlock over the flattened messages (commit order).
     std::vector<uint64_t> apply_msgs(const std::vector<const NetworkProtocol*>& msgs, std::unordered_map<uint64_t, uint64_t>* tracker,
                                      double t0);
-    char* chunk_buffer(size_t c, size_t bytes);  // pinned staging of wave chunk c (jg_host_alloc), grown on demand
+    char* stage(size_t bytes);  // pinned staging of one wave chunk (jg_host_alloc arenas, reused wave after wave)
     WorkerPool& pool();                     // persistent host workers (host_threads())
 
     jg_ctx* ctx_ = nullptr;
@@ -232,10 +240,12 @@ class GpuStableStore {
     uint32_t next_row_ = 0, next_set_ = 0;
     double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0}, orset_phase_s_[3] = {0, 0, 0};
     uint64_t pnc_bytes_ = 0;
+    double avg_msg_bytes_ = 357.0;          // bytes per state message of the last wave (chunk sizing)
     UidTable uids_;
     std::vector<uint32_t> reg_rows_;        // CreateSafeCRDT registrations not yet sent
     std::vector<jg_guid> reg_guids_;
-    std::vector<std::pair<char*, size_t>> chunks_;  // pinned chunk buffers, reused wave after wave
+    std::vector<std::pair<char*, size_t>> arenas_;  // pinned staging arenas (base, bytes)
+    size_t arena_i_ = 0, arena_off_ = 0;            // carve position of the current wave
     std::unique_ptr<WorkerPool> pool_;
     std::vector<SetKey> sets_;
     std::vector<NetworkProtocol> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167)
