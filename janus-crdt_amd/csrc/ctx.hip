@@ -45,6 +45,11 @@ void DevBuf::release() {
 
 void ensure_device(jg_ctx* ctx) { JG_HIP(hipSetDevice(ctx->device)); }
 
+void upload_done(jg_ctx* ctx) {
+    JG_HIP(hipEventRecord(ctx->copied, ctx->copy));
+    JG_HIP(hipStreamWaitEvent(ctx->stream, ctx->copied, 0));
+}
+
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes) {
     if (b.bytes < bytes) {
         JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block may still be in use
@@ -82,6 +87,8 @@ int jg_open(int device, jg_ctx** out) {
         try {
             JG_HIP(hipSetDevice(device));
             JG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            JG_HIP(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
+            JG_HIP(hipEventCreateWithFlags(&c->copied, hipEventDisableTiming));
             c->flags.alloc(256);
             JG_HIP(hipMemset(c->flags.p, 0, 256));
         } catch (...) {
@@ -97,11 +104,14 @@ int jg_close(jg_ctx* ctx) {
         if (!ctx) return;
         jg::ensure_device(ctx);
         (void)hipStreamSynchronize(ctx->stream);
+        if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
         ctx->scratch.release();
         ctx->scratch2.release();
         ctx->scratch3.release();
         ctx->flags.release();
         (void)hipStreamDestroy(ctx->stream);
+        if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
+        if (ctx->copied) (void)hipEventDestroy(ctx->copied);
         delete ctx;
     });
 }

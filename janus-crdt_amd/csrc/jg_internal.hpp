@@ -76,6 +76,8 @@ struct jg_ctx {
     jg::DevBuf scratch2;
     jg::DevBuf scratch3;
     jg::DevBuf flags;    // small zero-initialised status words (error flags)
+    hipStream_t copy = nullptr;    // wave uploads: chunk k+1's H2D overlaps chunk k's parse on `stream`
+    hipEvent_t copied = nullptr;
 };
 
 struct jg_pnc {
@@ -142,6 +144,11 @@ struct jg_orset {
 namespace jg {
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
+// After H2D copies queued on ctx->copy: make ctx->stream wait for them (stream order for the kernels
+// that read the uploaded chunk).  The copies start once ctx->stream has passed `order` (an event-free
+// way to keep the copy stream behind buffer reallocations on the compute stream: callers reallocate only
+// after synchronising ctx->stream).
+void upload_done(jg_ctx* ctx);
 void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
 // Dense chunk metadata for a stream whose n records sit contiguously in slots [0, n) (async).
 void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n);

@@ -6,15 +6,16 @@
 // state at a time inside HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160).  The store's records are
 // (set << 32 | element id, 16-byte tag), so element STRINGS must become ids first.  A wave is:
 //
-//   pass 1  k_ow_count   one thread per message: full parse + validation (the accepted form of
-//                        oracle/json.hpp, which host/wire.cpp's reader also follows); counts entries and
-//                        tags; the byte position of the first error it sees: a syntax error (JG_EINVAL) or
-//                        an empty add tag set (JG_ESTATE — the host reader reports it at that entry).
-//   scan    entry / tag offsets per message (hipcub).
-//   pass 2  k_ow_emit    parse again: one entry per (message, map, element) with a 64-bit hash of its
-//                        unescaped string (escaped strings are unescaped in place), one record per tag;
-//                        entries are numbered in commit order with addSet entries before removeSet ones
-//                        (Merge walks addSet first, ORSet.cs:255-279).
+//   pass 1  k_ow_parse   one thread per message, launched per uploaded chunk: full parse + validation (the
+//                        accepted form of oracle/json.hpp, which host/wire.cpp's reader also follows); the
+//                        byte position of the first error: a syntax error (JG_EINVAL) or an empty add tag
+//                        set (JG_ESTATE — the host reader reports it at that entry); one entry per
+//                        (message, map, element) with a 64-bit hash of its unescaped string (escaped
+//                        strings unescaped in place) and one record per tag, into regions addressed by
+//                        the message's byte offset (no wave-wide prefix needed yet).
+//   compact scan of the per-message counts (hipcub), then k_ow_compact: entries numbered in commit order
+//                        with addSet entries before removeSet ones (Merge walks addSet first,
+//                        ORSet.cs:255-279).
 //   sort    entries by (set, string) hash, stable (hipcub radix sort): commit order within a hash.
 //   group   k_ow_link / k_ow_label label every entry with the first entry of its string in the set,
 //                        strings compared byte for byte (a hash collision only takes a slower path).  The
@@ -243,6 +244,7 @@ template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c
             } else {
                 if (c.peek() != '{') return false;
                 ++c.p;
+                v.map(which);
                 c.ws();
                 if (c.peek() == '}') {
                     ++c.p;
@@ -281,38 +283,70 @@ template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c
     return seen == 15 && c.p == c.end;
 }
 
-struct CountVis {
-    uint64_t base;
-    uint32_t n_add = 0, n_rem = 0, nt = 0;
+// Pass 1 writes each message's entries and tags into SPARSE regions addressed by its byte offset, so
+// no prefix over the wave is needed before parsing: an entry needs >= 5 payload bytes after an 11-byte
+// `{"addSet":{` prefix and a tag >= 38 bytes, so message m's entries fit in slots [ceil(off/4),
+// ceil(off_next/4)) and its tags in [ceil(off/32), ceil(off_next/32)) whatever the payload holds.
+// check() compacts them in commit order (k_ow_compact).
+constexpr uint64_t kEntryDiv = 4, kTagDiv = 32;
+
+struct Sparse {  // entry slots: sort key, string offset, length | side << 31, error position; tag slots
+    unsigned long long* key;
+    unsigned long long* noff;
+    uint32_t* meta;
+    uint32_t* pos;
+    unsigned long long* tref;  // null << 63 | side << 62 | the entry's parse-order ordinal in its message
+    Tag16* tval;
+};
+
+struct ParseVis {
+    Sparse S;
+    uint64_t base, es, ts, kmask;  // message byte offset; first entry / tag slot
+    uint32_t set, n_add = 0, n_rem = 0, nt = 0, cur = 0;
+    bool rem_first = false, add_seen = false;
     unsigned long long estate = kNone;
-    __device__ void entry(int side, uint64_t, uint64_t, uint32_t, uint64_t) {
+    __device__ __forceinline__ void map(int which) {
+        if (which == 0) add_seen = true;
+        else if (!add_seen) rem_first = true;
+    }
+    __device__ __forceinline__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h) {
+        cur = n_add + n_rem;
+        const uint64_t e = es + cur;
+        S.key[e] = name_key(set, h) & kmask;
+        S.noff[e] = noff;
+        S.meta[e] = len | (uint32_t)side << 31;
+        S.pos[e] = (uint32_t)(npos - base);
         n_add += side == 0;
         n_rem += side != 0;
     }
-    __device__ void tag(int, bool, const Tag16&) { ++nt; }
-    __device__ void entry_end(int side, uint64_t pos, uint32_t ntags) {
+    __device__ __forceinline__ void tag(int side, bool is_null, const Tag16& g) {
+        S.tref[ts + nt] = (unsigned long long)is_null << 63 | (unsigned long long)side << 62 | cur;
+        S.tval[ts + nt] = g;
+        ++nt;
+    }
+    __device__ __forceinline__ void entry_end(int side, uint64_t pos, uint32_t ntags) {
         if (side == 0 && ntags == 0 && estate == kNone) estate = (unsigned long long)(pos - base) << 2 | kKindState;
     }
 };
 
-__global__ __launch_bounds__(kBlock) void k_ow_count(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t m0,
-                                                     uint64_t m1, unsigned long long* __restrict__ ne, unsigned long long* __restrict__ nt,
-                                                     uint32_t* __restrict__ na, unsigned long long* __restrict__ err) {
+// One thread per message: parse + validate (first error position: syntax or empty add tag set), element
+// strings hashed (escaped ones unescaped in place), entries and tags into the sparse regions.  The
+// entries before a syntax error are kept: a repeated name before it is reported first.
+__global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+                                                     uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, unsigned long long* __restrict__ ne,
+                                                     unsigned long long* __restrict__ nt, uint32_t* __restrict__ na,
+                                                     unsigned long long* __restrict__ err) {
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (m >= m1) return;
     const uint64_t b = off[m];
+    ParseVis v{S, b, (b + kEntryDiv - 1) / kEntryDiv, (b + kTagDiv - 1) / kTagDiv, kmask, mset[m]};
     Cursor c(bytes, b, off[m + 1]);
-    CountVis v{b};
-    unsigned long long e = v.estate;
-    if (!parse_orset<false>(c, nullptr, v)) {
-        const unsigned long long s = (unsigned long long)(c.p - b) << 2 | kKindInval;
-        e = s;
-    }
+    unsigned long long e = kNone;
+    if (!parse_orset<true>(c, bytes, v)) e = (unsigned long long)(c.p - b) << 2 | kKindInval;
     if (v.estate < e) e = v.estate;
-    // the entries before a syntax error are kept: a repeated name before it is reported first
     ne[m] = v.n_add + v.n_rem;
     nt[m] = v.nt;
-    na[m] = v.n_add;
+    na[m] = v.n_add | (v.rem_first ? 0x80000000u : 0u);
     err[m] = e;
 }
 
@@ -330,40 +364,34 @@ struct Entries {  // entry e: sort key, string (offset into the payload, length 
     uint32_t* pos;
 };
 
-struct EmitVis {
-    Entries E;
-    unsigned long long* tref;
-    Tag16* tval;
-    uint64_t base, e_add, e_rem, t, cur = 0;  // next addSet / removeSet entry, next tag
-    uint32_t m, set;
-    uint64_t kmask;
-    __device__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h) {
-        cur = side ? e_rem++ : e_add++;
-        E.key[cur] = name_key(set, h) & kmask;
-        E.val[cur] = (uint32_t)cur;
-        E.noff[cur] = noff;
-        E.msg[cur] = m;
-        E.meta[cur] = len | (uint32_t)side << 31;
-        E.pos[cur] = (uint32_t)(npos - base);
-    }
-    __device__ void tag(int side, bool is_null, const Tag16& g) {
-        tref[t] = is_null ? (1ull << 63 | (unsigned long long)side << 62 | m) : cur;
-        tval[t] = g;
-        ++t;
-    }
-    __device__ void entry_end(int, uint64_t, uint32_t) {}
-};
-
-__global__ __launch_bounds__(kBlock) void k_ow_emit(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
-                                                    uint64_t n, const unsigned long long* __restrict__ eoff, const unsigned long long* __restrict__ toff,
-                                                    const uint32_t* __restrict__ na, Entries E, unsigned long long* __restrict__ tref,
-                                                    Tag16* __restrict__ tval, uint64_t kmask) {
+// Sparse -> dense in commit order: entry ordinal = addSet entries first, then removeSet (Merge's walk),
+// whatever the member order of the payload.  One thread per message.
+__global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restrict__ off, uint64_t n, const unsigned long long* __restrict__ ne,
+                                                       const unsigned long long* __restrict__ nt, const uint32_t* __restrict__ na,
+                                                       const unsigned long long* __restrict__ eoff, const unsigned long long* __restrict__ toff,
+                                                       Sparse S, Entries E, unsigned long long* __restrict__ tref, Tag16* __restrict__ tval) {
     const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (m >= n) return;
-    const uint64_t b = off[m];
-    EmitVis v{E, tref, tval, b, eoff[m], eoff[m] + na[m], toff[m], 0, (uint32_t)m, mset[m], kmask};
-    Cursor c(bytes, b, off[m + 1]);
-    parse_orset<true>(c, bytes, v);  // validity was recorded by pass 1; the same prefix is emitted
+    const uint64_t b = off[m], es = (b + kEntryDiv - 1) / kEntryDiv, ts = (b + kTagDiv - 1) / kTagDiv;
+    const uint32_t cnt = (uint32_t)ne[m], n_add = na[m] & 0x7FFFFFFFu, n_rem = cnt - n_add;
+    const bool rem_first = (na[m] >> 31) != 0;
+    const uint64_t e0 = eoff[m], t0 = toff[m];
+    auto canon = [&](uint32_t q) -> uint32_t { return !rem_first ? q : (q < n_rem ? n_add + q : q - n_rem); };
+    for (uint32_t q = 0; q < cnt; ++q) {
+        const uint64_t e = e0 + canon(q);
+        E.key[e] = S.key[es + q];
+        E.val[e] = (uint32_t)e;
+        E.noff[e] = S.noff[es + q];
+        E.msg[e] = (uint32_t)m;
+        E.meta[e] = S.meta[es + q];
+        E.pos[e] = S.pos[es + q];
+    }
+    const uint32_t k = (uint32_t)nt[m];
+    for (uint32_t q = 0; q < k; ++q) {
+        const unsigned long long r = S.tref[ts + q];
+        tref[t0 + q] = (r >> 63) ? (r & (3ull << 62)) | m : e0 + canon((uint32_t)r);
+        tval[t0 + q] = S.tval[ts + q];
+    }
 }
 
 __device__ __forceinline__ bool same_bytes(const uint8_t* a, const uint8_t* b, uint32_t n) {
@@ -676,6 +704,7 @@ struct jg_orset_wire {
     uint64_t first_bad = kNone, n_ent = 0, n_tag = 0;
     // entries, groups, tags, records
     jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, skey, sval, hs, seg, impure, label, gid, eid;
+    jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
     jg::DevBuf tref, tval, rkey, rside, dtab, dk[2], dt[2], rk, rk2, perm, perm2;
     jg::DevBuf newk, newv, snk, snv, status, cub;
     // ids issued by the last commit: names [g0, g1), pool bytes [p0, p1)
@@ -794,8 +823,21 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
     if (bytes > w->cap_bytes) {
         const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 1 << 16);
         grow_keep(ctx, w->bytes, ((cap + 15) & ~15ull) + 16, w->wnb);  // the cursor reads aligned 16-byte windows
+        const uint64_t es = cap / kEntryDiv + 2, ts = cap / kTagDiv + 2;
+        const uint64_t ke = (w->wnb + kEntryDiv - 1) / kEntryDiv + 1, kt = (w->wnb + kTagDiv - 1) / kTagDiv + 1;  // slots in use
+        grow_keep(ctx, w->sp_key, es * 8, ke * 8);
+        grow_keep(ctx, w->sp_noff, es * 8, ke * 8);
+        grow_keep(ctx, w->sp_meta, es * 4, ke * 4);
+        grow_keep(ctx, w->sp_pos, es * 4, ke * 4);
+        grow_keep(ctx, w->sp_tref, ts * 8, kt * 8);
+        grow_keep(ctx, w->sp_tval, ts * 16, kt * 16);
         w->cap_bytes = cap;
     }
+}
+
+Sparse sparse_of(jg_orset_wire* w) {
+    return Sparse{w->sp_key.as<unsigned long long>(), w->sp_noff.as<unsigned long long>(), w->sp_meta.as<uint32_t>(), w->sp_pos.as<uint32_t>(),
+                  w->sp_tref.as<unsigned long long>(), w->sp_tval.as<Tag16>()};
 }
 
 Entries entries_of(jg_orset_wire* w) {
@@ -840,9 +882,9 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     ensure(w->tref, nt * 8 + 8);
     ensure(w->tval, nt * 16 + 16);
     const Entries E = entries_of(w);
-    hipLaunchKernelGGL(k_ow_emit, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), w->mset.as<uint32_t>(),
-                       n, w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(), w->na.as<uint32_t>(), E,
-                       w->tref.as<unsigned long long>(), w->tval.as<Tag16>(), w->kmask);
+    hipLaunchKernelGGL(k_ow_compact, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>(), n, w->ne.as<unsigned long long>(),
+                       w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(),
+                       sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
     JG_HIP(hipGetLastError());
     if (ne) {
         ensure(w->skey, ne * 8);
@@ -1090,8 +1132,9 @@ int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uin
         JG_HIP(hipMemcpyAsync(w->off.as<uint64_t>() + m0 + 1, off + 1, n * 8, hipMemcpyHostToDevice, ctx->stream));
         JG_HIP(hipMemcpyAsync(w->mset.as<uint32_t>() + m0, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
         if (b0) hipLaunchKernelGGL(k_ow_rebase, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>() + m0 + 1, n, b0);
-        hipLaunchKernelGGL(k_ow_count, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), m0, m0 + n,
-                           w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->err.as<unsigned long long>());
+        hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(),
+                           w->mset.as<uint32_t>(), m0, m0 + n, sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
+                           w->na.as<uint32_t>(), w->err.as<unsigned long long>());
         JG_HIP(hipGetLastError());
         w->wn = m0 + n;
         w->wnb = b0 + nb;
