@@ -199,6 +199,49 @@ template <class S> __device__ __forceinline__ bool read_string(Cursor& c, S& s) 
     }
 }
 
+// The common case of a tag string, decoded without the byte loop: [p, p + 37) holds exactly the
+// 36-character "D" form with hex digits and the closing quote.  Eleven independent dword loads cover it
+// (the payload buffer's 16-byte tail pad keeps them in bounds), v_alignbyte shifts them to p, and every
+// digit is checked and decoded at a fixed position.  Anything else (an escape, a bad digit, a string
+// running past the payload) returns false before the cursor moves, and the byte-wise GuidSink path
+// then reads the same bytes and reports the same error position.
+__device__ __forceinline__ bool guid_fast(const uint8_t* __restrict__ base, uint64_t p, uint64_t end, Tag16& t) {
+    if (p + 37 > end) return false;
+    const uint64_t a = p & ~3ull;
+    const uint32_t s = (uint32_t)(p - a);
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(base + a);
+    uint32_t raw[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) raw[i] = d[i];
+    uint32_t w[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) w[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], s);
+    uint32_t bad = 0;
+    auto byte = [&](int k) -> uint32_t { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; };
+    auto hx = [&](int k) -> uint32_t {
+        const uint32_t b = byte(k), dg = b - '0', lt = (b | 0x20u) - 'a';
+        const bool isd = dg < 10u;
+        bad |= (uint32_t)(!isd && lt >= 6u);
+        return isd ? dg : lt + 10u;
+    };
+    bad |= (byte(8) ^ '-') | (byte(13) ^ '-') | (byte(18) ^ '-') | (byte(23) ^ '-') | (byte(36) ^ '"');
+    uint32_t va = 0, vb = 0, vc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) va = va << 4 | hx(k);
+#pragma unroll
+    for (int k = 9; k < 13; ++k) vb = vb << 4 | hx(k);
+#pragma unroll
+    for (int k = 14; k < 18; ++k) vc = vc << 4 | hx(k);
+    unsigned long long hi = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // GuidSink's order: byte j/2 of hi, high nibble first
+        const int k = j < 4 ? 19 + j : 20 + j;
+        hi |= (unsigned long long)hx(k) << (8 * (j >> 1) + ((j & 1) ? 0 : 4));
+    }
+    t = Tag16{(unsigned long long)va | (unsigned long long)vb << 32 | (unsigned long long)vc << 48, hi};
+    return bad == 0;
+}
+
 // A tag array after its '['.  Null tag sets (nullAddGuid / nullRemoveGuid) report is_null.
 template <class V> __device__ __forceinline__ bool read_tags(Cursor& c, V& v, int side, bool is_null, uint32_t& nt) {
     nt = 0;
@@ -206,6 +249,17 @@ template <class V> __device__ __forceinline__ bool read_tags(Cursor& c, V& v, in
     if (c.peek() == ']') { ++c.p; return true; }
     for (;;) {
         if (!c.expect('"')) return false;
+        Tag16 g;
+        if (guid_fast(c.base, c.p, c.end, g)) {
+            c.p += 37;
+            v.tag(side, is_null, g);
+            ++nt;
+            c.ws();
+            const int ch = c.get();
+            if (ch == ']') return true;
+            if (ch != ',') return false;
+            continue;
+        }
         GuidSink gs;
         if (!read_string(c, gs) || !gs.ok()) return false;
         v.tag(side, is_null, gs.tag());
@@ -365,19 +419,22 @@ struct Entries {  // entry e: sort key, string (offset into the payload, length 
 };
 
 // Sparse -> dense in commit order: entry ordinal = addSet entries first, then removeSet (Merge's walk),
-// whatever the member order of the payload.  One thread per message.
+// whatever the member order of the payload.  One wave per message, lanes over its entries and tags (a
+// message's slots are contiguous on both sides: coalesced copies).
+constexpr int kCompactMsgs = kBlock / 64;
 __global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restrict__ off, uint64_t n, const unsigned long long* __restrict__ ne,
                                                        const unsigned long long* __restrict__ nt, const uint32_t* __restrict__ na,
                                                        const unsigned long long* __restrict__ eoff, const unsigned long long* __restrict__ toff,
                                                        Sparse S, Entries E, unsigned long long* __restrict__ tref, Tag16* __restrict__ tval) {
-    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t m = (uint64_t)blockIdx.x * kCompactMsgs + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
     if (m >= n) return;
     const uint64_t b = off[m], es = (b + kEntryDiv - 1) / kEntryDiv, ts = (b + kTagDiv - 1) / kTagDiv;
     const uint32_t cnt = (uint32_t)ne[m], n_add = na[m] & 0x7FFFFFFFu, n_rem = cnt - n_add;
     const bool rem_first = (na[m] >> 31) != 0;
     const uint64_t e0 = eoff[m], t0 = toff[m];
     auto canon = [&](uint32_t q) -> uint32_t { return !rem_first ? q : (q < n_rem ? n_add + q : q - n_rem); };
-    for (uint32_t q = 0; q < cnt; ++q) {
+    for (uint32_t q = lane; q < cnt; q += 64) {
         const uint64_t e = e0 + canon(q);
         E.key[e] = S.key[es + q];
         E.val[e] = (uint32_t)e;
@@ -387,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restric
         E.pos[e] = S.pos[es + q];
     }
     const uint32_t k = (uint32_t)nt[m];
-    for (uint32_t q = 0; q < k; ++q) {
+    for (uint32_t q = lane; q < k; q += 64) {
         const unsigned long long r = S.tref[ts + q];
         tref[t0 + q] = (r >> 63) ? (r & (3ull << 62)) | m : e0 + canon((uint32_t)r);
         tval[t0 + q] = S.tval[ts + q];
@@ -882,7 +939,7 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     ensure(w->tref, nt * 8 + 8);
     ensure(w->tval, nt * 16 + 16);
     const Entries E = entries_of(w);
-    hipLaunchKernelGGL(k_ow_compact, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>(), n, w->ne.as<unsigned long long>(),
+    hipLaunchKernelGGL(k_ow_compact, dim3((unsigned)((n + kCompactMsgs - 1) / kCompactMsgs)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>(), n, w->ne.as<unsigned long long>(),
                        w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(),
                        sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
     JG_HIP(hipGetLastError());

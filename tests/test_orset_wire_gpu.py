@@ -139,6 +139,13 @@ _CASES = [
     (b'{"addSet":{"a\x01":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
     (b'{"addSet":{},"removeSet":{},"nullAddGuid":["' + _B.encode() + b'"],"nullRemoveGuid":null}', jg.JG_EINVAL),
     (b'', jg.JG_EINVAL),
+    # the fixed-position Guid decoder's fall-backs: a bad last digit, one digit too many, the payload
+    # ending right after / inside a tag
+    (b'{"addSet":{"a":["' + _A[:-1].encode() + b'g"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A.encode() + b'0"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A.encode() + b'"', jg.JG_EINVAL),
+    (b'{"addSet":{"a":["' + _A[:20].encode(), jg.JG_EINVAL),
+    (b'{"addSet":{},"removeSet":{},"nullAddGuid":["' + _B.upper().encode() + b'"],"nullRemoveGuid":[]}', None),
 ]
 
 
