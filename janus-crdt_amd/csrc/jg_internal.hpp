@@ -145,9 +145,9 @@ namespace jg {
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 // After H2D copies queued on ctx->copy: make ctx->stream wait for them (stream order for the kernels
-// that read the uploaded chunk).  The copies start once ctx->stream has passed `order` (an event-free
-// way to keep the copy stream behind buffer reallocations on the compute stream: callers reallocate only
-// after synchronising ctx->stream).
+// that read the uploaded chunk).  Callers keep the copy stream off buffers the compute stream may still
+// use: they synchronise ctx->stream before the first upload of a wave, and ctx->copy before
+// reallocating an upload target.
 void upload_done(jg_ctx* ctx);
 void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
 // Dense chunk metadata for a stream whose n records sit contiguously in slots [0, n) (async).

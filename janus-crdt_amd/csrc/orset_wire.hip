@@ -779,6 +779,7 @@ void ensure(jg::DevBuf& b, size_t bytes) {
 // Grow to `need` bytes keeping the first `keep` bytes; the new tail is zeroed when `zero`.
 void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero = false) {
     if (b.bytes >= need) return;
+    if (ctx->copy) JG_HIP(hipStreamSynchronize(ctx->copy));  // uploads still landing in the old block
     jg::DevBuf nb;
     nb.alloc(need + need / 2);
     if (zero) JG_HIP(hipMemsetAsync(nb.p, 0, nb.bytes, ctx->stream));
@@ -1162,6 +1163,8 @@ int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
         close_wave(w);
         grow_wave(ctx, w, std::max<uint64_t>(cap_msgs, 1), std::max<uint64_t>(cap_bytes, 1));
         JG_HIP(hipMemsetAsync(w->off.p, 0, 8, ctx->stream));  // off[0] = 0
+        // the uploads run on ctx->copy: the previous wave's kernels must be done with these buffers
+        JG_HIP(hipStreamSynchronize(ctx->stream));
         w->open = true;
     });
 }
@@ -1185,9 +1188,11 @@ int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uin
         jg::ensure_device(ctx);
         const uint64_t m0 = w->wn, b0 = w->wnb, nb = off[n];
         grow_wave(ctx, w, m0 + n, b0 + nb);
-        if (nb) JG_HIP(hipMemcpyAsync(w->bytes.as<uint8_t>() + b0, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
-        JG_HIP(hipMemcpyAsync(w->off.as<uint64_t>() + m0 + 1, off + 1, n * 8, hipMemcpyHostToDevice, ctx->stream));
-        JG_HIP(hipMemcpyAsync(w->mset.as<uint32_t>() + m0, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        // chunk k+1's upload (copy stream) overlaps chunk k's parse (compute stream)
+        if (nb) JG_HIP(hipMemcpyAsync(w->bytes.as<uint8_t>() + b0, bytes, nb, hipMemcpyHostToDevice, ctx->copy));
+        JG_HIP(hipMemcpyAsync(w->off.as<uint64_t>() + m0 + 1, off + 1, n * 8, hipMemcpyHostToDevice, ctx->copy));
+        JG_HIP(hipMemcpyAsync(w->mset.as<uint32_t>() + m0, set, n * 4, hipMemcpyHostToDevice, ctx->copy));
+        jg::upload_done(ctx);
         if (b0) hipLaunchKernelGGL(k_ow_rebase, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>() + m0 + 1, n, b0);
         hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(),
                            w->mset.as<uint32_t>(), m0, m0 + n, sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
@@ -1245,6 +1250,7 @@ int jg_orset_wave_abort(jg_orset* s) {
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_abort: store is NULL");
         jg::ensure_device(s->ctx);
         JG_HIP(hipStreamSynchronize(s->ctx->stream));
+        JG_HIP(hipStreamSynchronize(s->ctx->copy));  // the caller's chunk buffers are released after this
         if (s->wire) {
             close_wave(s->wire);
             s->wire->g0 = s->wire->g1 = s->wire->n_names;
