@@ -579,15 +579,32 @@ __global__ void k_ow_resolve(Entries E, const uint32_t* __restrict__ mset, const
                              uint32_t* __restrict__ gid, unsigned long long* __restrict__ newk, uint32_t* __restrict__ newv,
                              unsigned long long* __restrict__ status) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n || label[i] != i) return;
-    const uint32_t e = sval[i], m = E.msg[e];
-    if (m >= limit) { gid[i] = kDead; return; }
-    const uint32_t set = mset[m];
-    const uint32_t id = tab_find(N, skey[i], set, bytes + E.noff[e], E.meta[e] & 0x7FFFFFFFu);
-    if (id != kNoName) { gid[i] = id; return; }
-    const unsigned long long k = atomicAdd(status + 1, 1ull);
-    newk[k] = (unsigned long long)set << 32 | e;
-    newv[k] = (uint32_t)i;
+    bool fresh = false;
+    uint32_t e = 0, set = 0;
+    if (i < n && label[i] == i) {
+        e = sval[i];
+        const uint32_t m = E.msg[e];
+        if (m >= limit) {
+            gid[i] = kDead;
+        } else {
+            set = mset[m];
+            const uint32_t id = tab_find(N, skey[i], set, bytes + E.noff[e], E.meta[e] & 0x7FFFFFFFu);
+            if (id != kNoName) gid[i] = id;
+            else fresh = true;
+        }
+    }
+    // new strings: one atomic per wave for their slots (their order is fixed later by the sort)
+    const unsigned long long b = __ballot(fresh);
+    if (!b) return;
+    const uint32_t lane = __lane_id(), leader = __ffsll((long long)b) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(status + 1, (unsigned long long)__popcll(b));
+    base = __shfl(base, (int)leader);
+    if (fresh) {
+        const unsigned long long k = base + __popcll(b & ((1ull << lane) - 1));
+        newk[k] = (unsigned long long)set << 32 | e;
+        newv[k] = (uint32_t)i;
+    }
 }
 
 __device__ __forceinline__ uint64_t set_begin(const unsigned long long* snk, uint64_t n, uint32_t set) {
@@ -688,8 +705,13 @@ __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* _
         const uint64_t h = rec_hash(k, g, side);
         const unsigned long long word = (h >> 32) << 32 | (t + 1);
         for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-            const unsigned long long w = atomicCAS(tab + s, 0ull, word);
-            if (w == 0) { fresh = true; break; }
+            // most records repeat one seen earlier in the wave: a plain load settles those without an
+            // atomic (a slot never changes once set; a stale 0 only sends us to the CAS)
+            unsigned long long w = tab[s];
+            if (w == 0) {
+                w = atomicCAS(tab + s, 0ull, word);
+                if (w == 0) { fresh = true; break; }
+            }
             if ((w >> 32) != (h >> 32)) continue;
             const uint64_t u = (w & 0xFFFFFFFFull) - 1;
             const Tag16 o = tval[u];
@@ -764,6 +786,7 @@ struct jg_orset_wire {
     jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
     jg::DevBuf tref, tval, rkey, rside, dtab, dk[2], dt[2], rk, rk2, perm, perm2;
     jg::DevBuf newk, newv, snk, snv, status, cub;
+    jg_orset* recs = nullptr;  // a committed wave's records, sorted (the merge source), reused
     // ids issued by the last commit: names [g0, g1), pool bytes [p0, p1)
     uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;
     // string-hash mask: all bits; tests narrow it (JANUS_TEST_NAME_HASH_BITS) to force collisions
@@ -1077,12 +1100,14 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     unsigned long long cnt[2];
     read_words(ctx, st + 4, cnt, 2);
     if (cnt[0] + cnt[1] == 0) return;
-    jg_orset tmp;
-    tmp.ctx = ctx;
+    if (!w->recs) {  // the wave's sorted records: kept across waves (no allocation per commit)
+        w->recs = new jg_orset();
+        w->recs->ctx = ctx;
+    }
     const int key_bits = 32 + bits_for(w->max_set);
-    sort_side(ctx, w, 0, cnt[0], key_bits, tmp.add);
-    sort_side(ctx, w, 1, cnt[1], key_bits, tmp.rem);
-    jg::orset_merge_store(s, &tmp);
+    sort_side(ctx, w, 0, cnt[0], key_bits, w->recs->add);
+    sort_side(ctx, w, 1, cnt[1], key_bits, w->recs->rem);
+    jg::orset_merge_store(s, w->recs);
 }
 
 void close_wave(jg_orset_wire* w) {
@@ -1096,7 +1121,10 @@ void close_wave(jg_orset_wire* w) {
 }  // namespace
 
 namespace jg {
-void orset_wire_free(jg_orset_wire* w) { delete w; }
+void orset_wire_free(jg_orset_wire* w) {
+    if (w) delete w->recs;
+    delete w;
+}
 }  // namespace jg
 
 extern "C" {
