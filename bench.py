@@ -298,6 +298,81 @@ def bench_c1(local):
     return json.loads(out.stdout.strip().splitlines()[-1]) if out.stdout.strip() else {"error": out.stderr[-500:]}
 
 
+DIGEST_MSGS, DIGEST_PER_UPDATE = 1_000_000, 1000  # one C5-sized wave, clientBatchSize-sized UpdateMessages
+# VALU instructions per 64-byte block of the k_sha_msgs loop (compress + window shift, gfx950 ISA count of
+# csrc/digest.hip) and the chip's VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
+SHA_VALU_PER_BLOCK, VALU_LANE_OPS = 1650, 256 * 4 * 32 * 2.4e9
+
+
+def digest_wave(n, seed):
+    """n PNCounterMsg-sized payloads (340..375 bytes, ~357 B like the C5 wave's JSON states), back to back."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(340, 376, n).astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(32, 127, int(off[-1]), dtype=np.uint8)
+    return data, off
+
+
+def bench_digest(jg, ctx, sync, rank, steps, warmup):
+    """UpdateMessage.ComputeDigest for one wave resident in HBM: 1M payloads in 1000
+    UpdateMessages of 1000 (jg_wave_update_digests: k_sha_msgs + k_sha_updates + 32 KB of digests D2H)."""
+    import numpy as np
+    data, off = digest_wave(DIGEST_MSGS, SEED + 31 + rank)
+    first = np.arange(0, DIGEST_MSGS + 1, DIGEST_PER_UPDATE, dtype=np.uint64)
+    w = jg.Wave(ctx, DIGEST_MSGS, data.size)
+    try:
+        w.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data, off=off)
+        wall, ev = timed(ctx, sync, lambda: w.update_digests(first), steps, warmup)
+        # the same payloads as one-state UpdateMessages: the second level shrinks to one block per update,
+        # so this call's time is essentially k_sha_msgs (the first level) alone
+        single = np.arange(0, DIGEST_MSGS + 1, dtype=np.uint64)
+        wall1, ev1 = timed(ctx, sync, lambda: w.update_digests(single), steps, warmup)
+    finally:
+        w.close()
+    blocks = int(((off[1:] - off[:-1] + 72) // 64).sum())
+    kern, kern1 = ev / steps, ev1 / steps
+    chain = int((32 * DIGEST_PER_UPDATE + 72) // 64) if DIGEST_PER_UPDATE <= 32768 else None
+    return {"workload": f"UpdateMessage.ComputeDigest: {DIGEST_MSGS} payloads of 340-375 B resident in HBM, "
+                        f"{DIGEST_MSGS // DIGEST_PER_UPDATE} UpdateMessages of {DIGEST_PER_UPDATE}",
+            "msgs_per_s": DIGEST_MSGS / (wall / steps), "ms_per_wave": wall / steps * 1e3,
+            "payload_GBps": data.size / (wall / steps) / 1e9, "event_ms": kern * 1e3, "sha_blocks": blocks,
+            "one_state_updates": {"msgs_per_s": DIGEST_MSGS / (wall1 / steps), "event_ms": kern1 * 1e3},
+            "second_level_chain_blocks": chain,
+            "roofline": {"bound": "valu", "achieved": blocks / kern1 / 1e9, "unit": "Gblocks/s",
+                         "peak": VALU_LANE_OPS / SHA_VALU_PER_BLOCK / 1e9,
+                         "frac": blocks / kern1 / (VALU_LANE_OPS / SHA_VALU_PER_BLOCK),
+                         "scope": "first level (k_sha_msgs) from the one-state-update call; the 1000-state call adds the "
+                                  "second level, a serial chain of second_level_chain_blocks SHA-256 blocks per "
+                                  "UpdateMessage (latency-bound, DESIGN.md section 4)"}}
+
+
+def cpu_digest_baseline():
+    """The oracle's scalar SHA-256 (port) and hashlib / OpenSSL (the primitive .NET 6's SHA256.HashData calls
+    on Linux) over the first 50k payloads of the same wave, 1 thread."""
+    import hashlib
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ref as orc
+    n = 50_000
+    data, off = digest_wave(n, SEED + 31)
+    first = np.arange(0, n + 1, DIGEST_PER_UPDATE, dtype=np.uint64)
+    t = orc.lib().orc_bench_update_digests(n, off.ctypes.data, data.ctypes.data, first.size - 1, first.ctypes.data, 3)
+    buf = data.tobytes()
+    t0 = time.perf_counter()
+    for u in range(first.size - 1):
+        toSign = bytearray(32768)
+        for j, i in enumerate(range(int(first[u]), int(first[u + 1]))):
+            toSign[32 * j:32 * j + 32] = hashlib.sha256(buf[off[i]:off[i + 1]]).digest()
+        hashlib.sha256(toSign).digest()
+    t_ssl = time.perf_counter() - t0
+    return {"msgs_per_s": n / t, "cores": 1, "kind": "port",
+            "sample": f"oracle UpdateMessage.ComputeDigest (scalar FIPS 180-4 restatement) over the first {n} payloads, median of 3",
+            "openssl": {"msgs_per_s": n / t_ssl, "cores": 1,
+                        "sample": "the same with Python hashlib (OpenSSL SHA-256, SHA extensions where the CPU has them)"}}
+
+
 def cpu_baseline():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as orc
@@ -329,7 +404,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange"], default="all")
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnc-shape", choices=sorted(PNC_SHAPES), default="c2",
                     help="per-GPU PN-Counter shard: c2 = BASELINE configs[1] (default), c4 = 1/8 of configs[3]")
@@ -356,6 +431,13 @@ def main():
             res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
         except Exception as e:  # noqa: BLE001
             res["exchange"] = {"error": repr(e)[:500]}
+    if args.workload in ("all", "digest"):
+        try:
+            res["digest"] = bench_digest(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                res["digest"]["cpu_baseline"] = cpu_digest_baseline()
+        except Exception as e:  # noqa: BLE001
+            res["digest"] = {"error": repr(e)[:500]}
     ctx.close()
 
     cpu = None
@@ -413,6 +495,8 @@ def main():
                          "dtype": "u64+u128 records", "config": {"workload": line["orset"]["workload"]}})
     if "exchange" in res:
         line["exchange"] = res["exchange"]
+    if "digest" in res:
+        line["update_digests"] = res["digest"]
     if apply_loop is not None:
         line["apply_loop"] = apply_loop
     if apply_orset is not None:

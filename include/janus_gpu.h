@@ -268,6 +268,23 @@ int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_coun
                           const void* d_add_tag, const void* d_rem_key, const void* d_rem_tag);
 
 /* ---------------------------------------------------------------------------------------------
+ * UpdateMessage digests (csrc/digest.hip) — replaces UpdateMessage.ComputeDigest
+ * (BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:32-55), run by `new UpdateMessage(list)` (:25-30) for
+ * every batch the client batcher submits (SafeCRDTManager.ActualPropagateSyncMsg, SafeCRDTManager.cs:165-198).
+ * ------------------------------------------------------------------------------------------- */
+/* n NetworkProtocol.message payloads: payload i = bytes[off[i], off[i+1]) (off[0] = 0), a C# null when
+ * is_null != NULL && is_null[i] (hashed as 32 zero bytes, :41-42).  n_updates UpdateMessages: update u
+ * holds payloads [first[u], first[u+1]) (first[0] = 0, first[n_updates] = n).  digest[32u..32u+32) =
+ * SHA256(SHA256(payload) for each payload of u ‖ zeros up to ArrayPool<byte>.Shared.Rent(32 * count)
+ * .Length) — the .NET 6 bucket length (oracle/digest.hpp).  msg_digest (optional, n * 32 bytes) receives
+ * each payload's SHA256 (zeros for null).  Synchronous; JG_EINVAL on malformed offsets. */
+int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, const uint8_t* is_null, uint64_t n_updates,
+                      const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);
+/* The same over a wave already in device memory (jg_wave_upload; no null payloads): first[n_updates]
+ * must equal the wave's message count. */
+int jg_wave_update_digests(const jg_wave* wave, uint64_t n_updates, const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);
+
+/* ---------------------------------------------------------------------------------------------
  * Synthetic workloads (bench / size-independent parity): device-side counter-based generators,
  * defined in DESIGN.md §Synthetic inputs and mirrored on the host by the test oracle.
  * ------------------------------------------------------------------------------------------- */

@@ -96,6 +96,15 @@ struct jg_pnc {
     bool wopen = false;
 };
 
+// Device-resident wave of encoded state messages (json.hip jg_wave_*; digest.hip reads it too).
+struct jg_wave {
+    jg_ctx* ctx;
+    uint64_t cap_msgs, cap_bytes;
+    uint64_t n = 0, n_bytes = 0;
+    uint32_t max_key = 0;
+    jg::DevBuf bytes, off, keys;
+};
+
 struct jg_rows {
     jg_ctx* ctx;
     uint64_t n_rows;

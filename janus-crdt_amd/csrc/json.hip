@@ -568,14 +568,6 @@ void check_wave_host(const jg_pnc* p, uint64_t n, const uint32_t* key_idx, const
 }  // namespace
 
 // Device-resident wave of encoded state messages (bench / pre-staged waves).
-struct jg_wave {
-    jg_ctx* ctx;
-    uint64_t cap_msgs, cap_bytes;
-    uint64_t n = 0, n_bytes = 0;
-    uint32_t max_key = 0;
-    jg::DevBuf bytes, off, keys;
-};
-
 extern "C" {
 
 int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid* replica, uint32_t* col_out) {

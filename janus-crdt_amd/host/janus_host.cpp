@@ -747,7 +747,9 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         }
         c0 = c1;
     }
-    // 4. Submitted UpdateMessages and the remaining queue carry the snapshots.
+    // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
+    //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).
+    const size_t s0 = submitted.size();
     for (Flush& f : flushes) {
         UpdateMessage um;
         for (auto& e : f.msgs) {
@@ -756,11 +758,30 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         }
         submitted.push_back(std::move(um));
     }
+    ComputeDigests(ctx_, submitted, s0);
     for (size_t j = head; j < q.size(); ++j) {
         if (q[j].second != kOld) q[j].first.message = snap[(size_t)q[j].second];
         batch_queue_.push_back(std::move(q[j].first));
     }
     return result;
+}
+
+void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first) {
+    if (first >= msgs.size()) return;
+    std::vector<uint64_t> off{0}, upd{0};
+    for (size_t u = first; u < msgs.size(); ++u) {
+        for (const auto& np : msgs[u].update) off.push_back(off.back() + np.message.size());
+        upd.push_back(off.size() - 1);
+    }
+    std::string bytes;
+    bytes.reserve(off.back());
+    for (size_t u = first; u < msgs.size(); ++u)
+        for (const auto& np : msgs[u].update) bytes += np.message;
+    std::vector<uint8_t> dig(32 * (msgs.size() - first));
+    const int rc = jg_update_digests(ctx, off.size() - 1, off.data(), reinterpret_cast<const uint8_t*>(bytes.data()), nullptr, upd.size() - 1,
+                            upd.data(), nullptr, dig.data());
+    if (rc != JG_OK) throw EngineError(rc, last_error());
+    for (size_t u = first; u < msgs.size(); ++u) std::memcpy(msgs[u].digest.data(), dig.data() + 32 * (u - first), 32);
 }
 
 std::vector<std::optional<std::string>> GpuStableStore::QueryStableLookupAll(const Guid& uid) {

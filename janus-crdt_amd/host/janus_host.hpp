@@ -19,6 +19,7 @@
 // undecoded (jg_pnc_merge_json); OR-Set payloads are decoded here (wire.hpp) and merged as records.
 #pragma once
 
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <optional>
@@ -67,7 +68,12 @@ struct NetworkProtocol {
 };
 struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
     std::vector<NetworkProtocol> update;
+    std::array<uint8_t, 32> digest{};  // ComputeDigest() (:32-55), filled where the batch is created
 };
+
+// `new UpdateMessage(list)` computes its digest (DAGUpdateMessage.cs:25-30): ComputeDigest of every
+// message in msgs[first..] in ONE device call (jg_update_digests).
+void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first = 0);
 
 struct EngineError : std::runtime_error {
     int code;

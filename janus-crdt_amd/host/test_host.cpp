@@ -13,11 +13,13 @@
 // are applied there, and QueryProspective plus every op result must match too.
 // Exit 0 = parity; prints the first mismatch otherwise.
 #include <cstdio>
+#include <cstring>
 #include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <memory>
 
+#include "digest.hpp"
 #include "janus_host.hpp"
 #include "json.hpp"
 #include "oracle.hpp"
@@ -80,6 +82,19 @@ const char* same_batches(const std::vector<janus::UpdateMessage>& g, const std::
                 return "OR-Set payload state";
             }
         }
+        // UpdateMessage.ComputeDigest (DAGUpdateMessage.cs:32-55) over the payload bytes: the reference's
+        // bytes where they are byte-exact (PN-Counter), the GPU's own bytes for OR-Set snapshots (whose
+        // tag order within an element is canonical, not HashSet order)
+        std::vector<const uint8_t*> ptr;
+        std::vector<uint64_t> len;
+        for (size_t j = 0; j < g[i].update.size(); ++j) {
+            const std::string& m = o[i].update[j].message.type == oracle::CrdtType::PNCounter ? o[i].update[j].bytes : g[i].update[j].message;
+            ptr.push_back(reinterpret_cast<const uint8_t*>(m.data()));
+            len.push_back(m.size());
+        }
+        uint8_t want[32];
+        oracle::update_digest(ptr.size(), ptr.data(), len.data(), nullptr, want);
+        if (std::memcmp(want, g[i].digest.data(), 32) != 0) return "UpdateMessage digest";
     }
     return nullptr;
 }

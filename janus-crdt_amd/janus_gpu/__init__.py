@@ -35,6 +35,7 @@ EXPORTS = [
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
+    "jg_update_digests", "jg_wave_update_digests",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -77,6 +78,8 @@ _SIGS = {
     "jg_pnc_merge_json": ([_vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_wave_create": ([_vp, _u64, _u64, C.POINTER(_vp)], C.c_int),
     "jg_wave_destroy": ([_vp], C.c_int),
+    "jg_update_digests": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_wave_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_wave_upload": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_host_alloc": ([_vp, _u64, C.POINTER(_vp)], C.c_int),
@@ -366,10 +369,35 @@ class Wave:
         data, off = _arr(data, np.uint8), _arr(off, np.uint64)
         _check(load().jg_wave_upload(self._h, k.size, _ptr(k), _ptr(off), _ptr(data)))
 
+    def update_digests(self, first, msg_digests: bool = False):
+        """UpdateMessage.ComputeDigest for updates [first[u], first[u+1]) of this wave (jg_wave_update_digests):
+        returns digests u8[n_updates, 32] (and the per-message SHA-256s u8[n, 32] if msg_digests)."""
+        first = _arr(first, np.uint64)
+        nu = first.size - 1
+        dig = np.zeros((max(nu, 0), 32), np.uint8)
+        md = np.zeros((int(first[-1]), 32), np.uint8) if msg_digests else None
+        _check(load().jg_wave_update_digests(self._h, nu, _ptr(first), _ptr(md), _ptr(dig)))
+        return (dig, md) if msg_digests else dig
+
     def close(self) -> None:
         if self._h:
             _check(load().jg_wave_destroy(self._h))
             self._h = _vp()
+
+
+def update_digests(ctx: Context, msgs, first, msg_digests: bool = False):
+    """UpdateMessage.ComputeDigest (DAGUpdateMessage.cs:32-55) on the device (jg_update_digests).
+    msgs: NetworkProtocol.message payloads (bytes, or None for a C# null); update u holds
+    msgs[first[u]:first[u+1]].  Returns digests u8[n_updates, 32] (and u8[n, 32] per message)."""
+    is_null = np.array([m is None for m in msgs], np.uint8)
+    data, off = pack_wave([b"" if m is None else m for m in msgs])
+    first = _arr(first, np.uint64)
+    nu = first.size - 1
+    dig = np.zeros((max(nu, 0), 32), np.uint8)
+    md = np.zeros((len(msgs), 32), np.uint8) if msg_digests else None
+    _check(load().jg_update_digests(ctx.handle, len(msgs), _ptr(off), _ptr(data), _ptr(is_null) if is_null.any() else None, nu,
+                                    _ptr(first), _ptr(md), _ptr(dig)))
+    return (dig, md) if msg_digests else dig
 
 
 def records(key=None, tag_lo=None, tag_hi=None, n: int = 0) -> np.ndarray:

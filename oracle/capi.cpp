@@ -473,3 +473,41 @@ int orc_pnc_apply_json(uint64_t n_keys, uint32_t R, uint32_t eb, void* P, void* 
 }
 
 }  // extern "C"
+
+// ---- UpdateMessage.ComputeDigest (digest.hpp; DAGUpdateMessage.cs:32-55) -----------------------
+#include "digest.hpp"
+
+extern "C" {
+
+// SHA256 of n payloads: payload i = bytes[off[i], off[i+1]); out = n * 32 bytes.
+void orc_sha256_batch(uint64_t n, const uint64_t* off, const uint8_t* bytes, uint8_t* out) {
+    for (uint64_t i = 0; i < n; ++i) sha256(bytes + off[i], off[i + 1] - off[i], out + 32 * i);
+}
+
+// n_updates UpdateMessages over n payloads (update u = payloads [first[u], first[u+1])); is_null may be
+// NULL; msg_digest (n * 32, optional) and digest (n_updates * 32).
+void orc_update_digests(uint64_t n, const uint64_t* off, const uint8_t* bytes, const uint8_t* is_null, uint64_t n_updates,
+                        const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
+    std::vector<const uint8_t*> ptr(n);
+    std::vector<uint64_t> len(n);
+    for (uint64_t i = 0; i < n; ++i) { ptr[i] = bytes + off[i]; len[i] = off[i + 1] - off[i]; }
+    for (uint64_t u = 0; u < n_updates; ++u) {
+        uint64_t a = first[u], c = first[u + 1] - a;
+        update_digest(c, ptr.data() + a, len.data() + a, is_null ? is_null + a : nullptr, digest + 32 * u,
+                      msg_digest ? msg_digest + 32 * a : nullptr);
+    }
+}
+
+// CPU baseline: seconds for orc_update_digests over the same inputs (median of reps, 1 thread).
+double orc_bench_update_digests(uint64_t n, const uint64_t* off, const uint8_t* bytes, uint64_t n_updates, const uint64_t* first, int reps) {
+    std::vector<uint8_t> out(32 * (n_updates ? n_updates : 1));
+    std::vector<double> t;
+    for (int r = 0; r < reps; ++r) {
+        auto t0 = std::chrono::steady_clock::now();
+        orc_update_digests(n, off, bytes, nullptr, n_updates, first, nullptr, out.data());
+        t.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
+    return median_of(t);
+}
+
+}  // extern "C"

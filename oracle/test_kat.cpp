@@ -9,6 +9,7 @@
 #include <functional>
 #include <sstream>
 
+#include "digest.hpp"
 #include "json.hpp"
 #include "oracle.hpp"
 
@@ -535,6 +536,47 @@ TEST(SafeCRDTManager_ApplySkipsCreateAndEmpty) {  // SafeCRDTManager.cs:133-134
     CHECK_EQ(a.QueryStable().i, 0);
     sm.HandleAfterConsensusUpdates({{UpdateMessage{{real}}}});
     CHECK_EQ(a.QueryStable().i, 9);
+}
+
+// ---- SHA-256 (FIPS 180-4 / NIST example vectors) and UpdateMessage.ComputeDigest ----------------
+std::string hex(const uint8_t* d, size_t n) { static const char* x = "0123456789abcdef"; std::string s; for (size_t i = 0; i < n; ++i) { s += x[d[i] >> 4]; s += x[d[i] & 15]; } return s; }
+std::string sha_hex(const std::string& m) { uint8_t o[32]; sha256((const uint8_t*)m.data(), m.size(), o); return hex(o, 32); }
+TEST(SHA256_NistVectors) {  // FIPS 180-4 examples (NIST CSRC "SHA256.pdf", SHA2 additional vectors)
+    CHECK_EQ(sha_hex(""), std::string("e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"));
+    CHECK_EQ(sha_hex("abc"), std::string("ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"));
+    CHECK_EQ(sha_hex("abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq"),
+             std::string("248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"));
+    CHECK_EQ(sha_hex("abcdefghbcdefghicdefghijdefghijkefghijklfghijklmghijklmnhijklmnoijklmnopjklmnopqklmnopqrlmnopqrsmnopqrstnopqrstu"),
+             std::string("cf5b16a778af8380036ce59e7b0492370b249b11e8f07a51afac45037afee9d1"));
+    CHECK_EQ(sha_hex(std::string(1000000, 'a')), std::string("cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"));
+}
+TEST(ArrayPoolRentLength) {  // .NET 6 TlsOverPerCoreLockedStacksArrayPool buckets (digest.hpp header)
+    CHECK_EQ(array_pool_rent_length(0), 0ull);
+    CHECK_EQ(array_pool_rent_length(1), 16ull);
+    CHECK_EQ(array_pool_rent_length(32), 32ull);
+    CHECK_EQ(array_pool_rent_length(96), 128ull);
+    CHECK_EQ(array_pool_rent_length(32000), 32768ull);
+    CHECK_EQ(array_pool_rent_length(1ull << 20), 1ull << 20);
+    CHECK_EQ(array_pool_rent_length((1ull << 20) + 32), (1ull << 20) + 32);
+}
+TEST(UpdateMessage_ComputeDigest) {  // DAGUpdateMessage.cs:32-55
+    // one message: toSign = its 32-byte digest exactly (Rent(32) = 32)
+    std::string m = "{\"pVector\":{},\"nVector\":{}}";
+    const uint8_t* p = (const uint8_t*)m.data(); uint64_t len = m.size();
+    uint8_t d1[32], inner[32], want[32];
+    update_digest(1, &p, &len, nullptr, d1);
+    sha256(p, len, inner); sha256(inner, 32, want);
+    CHECK_EQ(hex(d1, 32), hex(want, 32));
+    // three messages, the middle one null: 96 bytes rented as 128, zeros for null and the padding
+    const uint8_t* ps[3] = {p, p, p}; uint64_t ls[3] = {len, 0, len}; uint8_t nul[3] = {0, 1, 0};
+    uint8_t buf[128] = {0};
+    sha256(p, len, buf); sha256(p, len, buf + 64);
+    sha256(buf, 128, want);
+    update_digest(3, ps, ls, nul, d1);
+    CHECK_EQ(hex(d1, 32), hex(want, 32));
+    // empty update list: Rent(0) is the empty array
+    update_digest(0, nullptr, nullptr, nullptr, d1);
+    CHECK_EQ(hex(d1, 32), sha_hex(""));
 }
 
 }  // namespace

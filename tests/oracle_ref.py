@@ -29,6 +29,9 @@ _SIGS = {
     "orc_json_encode_pnc": ([_u64, _vp, _vp, _vp, _vp, _u32, _vp, _u64], C.c_int64),
     "orc_json_accepts_pnc": ([C.c_char_p, _u64, _u32], C.c_int),
     "orc_json_decode_orset": ([C.c_char_p, _u64, _vp, _u64], C.c_int64),
+    "orc_sha256_batch": ([_u64, _vp, _vp, _vp], None),
+    "orc_update_digests": ([_u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp], None),
+    "orc_bench_update_digests": ([_u64, _vp, _vp, _u64, _vp, _i32], C.c_double),
     "orc_pnc_apply_json": ([_u64, _u32, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
 }
 
@@ -244,3 +247,30 @@ def orset_apply_json(set_ids, msgs, names=None):
                 (rem if side else add).add((int(sid) << 32 | eid, lo, hi))
     mk = lambda s: np.array(sorted(s), dtype=REC_DTYPE) if s else np.zeros(0, REC_DTYPE)
     return mk(add), mk(rem), bad, code
+
+
+# ---- UpdateMessage.ComputeDigest (oracle/digest.hpp) ----
+def _pack(msgs):
+    off = np.zeros(len(msgs) + 1, np.uint64)
+    off[1:] = np.cumsum([0 if m is None else len(m) for m in msgs], dtype=np.uint64) if msgs else []
+    data = np.frombuffer(b"".join(b"" if m is None else m for m in msgs) + b"\0", np.uint8)
+    return data, off
+
+
+def sha256_batch(msgs) -> np.ndarray:
+    data, off = _pack(msgs)
+    out = np.zeros((len(msgs), 32), np.uint8)
+    lib().orc_sha256_batch(len(msgs), _p(off), _p(data), _p(out))
+    return out
+
+
+def update_digests(msgs, first):
+    """(digests u8[n_updates, 32], per-message u8[n, 32]) for updates msgs[first[u]:first[u+1]]."""
+    data, off = _pack(msgs)
+    is_null = np.array([m is None for m in msgs] or [False], np.uint8)
+    first = np.ascontiguousarray(first, np.uint64)
+    nu = first.size - 1
+    dig = np.zeros((max(nu, 0), 32), np.uint8)
+    md = np.zeros((len(msgs), 32), np.uint8)
+    lib().orc_update_digests(len(msgs), _p(off), _p(data), _p(is_null), nu, _p(first), _p(md), _p(dig))
+    return dig, md

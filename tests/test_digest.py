@@ -1,0 +1,165 @@
+"""UpdateMessage.ComputeDigest (BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:32-55).
+
+CPU tests pin the oracle (oracle/digest.hpp) against hashlib and the committed golden fixture
+(tests/golden/update_digests.npz, made by hashlib alone); GPU tests compare the HIP kernels
+(jg_update_digests / jg_wave_update_digests) byte for byte with both.  Integer/byte work: bit-exact."""
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_ref as orc
+
+GOLD = Path(__file__).resolve().parent / "golden" / "update_digests.npz"
+
+
+def rent_length(n: int) -> int:  # .NET 6 ArrayPool<byte>.Shared.Rent(n).Length
+    return 0 if n == 0 else (n if n > 1 << 20 else max(16, 1 << (n - 1).bit_length()))
+
+
+def py_digest(msgs) -> bytes:
+    buf = bytearray(rent_length(32 * len(msgs)))
+    for i, m in enumerate(msgs):
+        if m is not None:
+            buf[32 * i:32 * i + 32] = hashlib.sha256(m).digest()
+    return hashlib.sha256(bytes(buf)).digest()
+
+
+def golden():
+    z = np.load(GOLD)
+    data, off, nul = z["data"].tobytes(), z["off"], z["is_null"]
+    msgs = [None if nul[i] else data[off[i]:off[i + 1]] for i in range(off.size - 1)]
+    return msgs, z["first"], z["digest"], z["msg_digest"]
+
+
+def random_msgs(rng, n, lo=0, hi=700, null_every=0):
+    out = []
+    for i in range(n):
+        if null_every and i % null_every == null_every - 1:
+            out.append(None)
+        else:
+            out.append(rng.integers(0, 256, int(rng.integers(lo, hi + 1))).astype(np.uint8).tobytes())
+    return out
+
+
+# ---------------------------------------------------------------- CPU: the oracle
+def test_oracle_sha256_matches_hashlib():
+    rng = np.random.default_rng(1)
+    msgs = [bytes(rng.integers(0, 256, n).astype(np.uint8)) for n in list(range(0, 200)) + [1000, 4097, 70001]]
+    got = orc.sha256_batch(msgs)
+    for m, g in zip(msgs, got):
+        assert g.tobytes() == hashlib.sha256(m).digest()
+
+
+def test_oracle_against_golden():
+    msgs, first, digest, msg_digest = golden()
+    d, md = orc.update_digests(msgs, first)
+    assert np.array_equal(d, digest)
+    assert np.array_equal(md, msg_digest)
+
+
+def test_oracle_rent_boundary():
+    # 32768 payloads = exactly 2^20 digest bytes (pooled bucket); 32769 -> above the pool (exact length)
+    rng = np.random.default_rng(2)
+    msgs = random_msgs(rng, 32769, 0, 8)
+    for cnt in (32768, 32769):
+        d, _ = orc.update_digests(msgs[:cnt], [0, cnt])
+        assert d[0].tobytes() == py_digest(msgs[:cnt])
+
+
+# ---------------------------------------------------------------- GPU: the HIP kernels
+@pytest.mark.gpu
+def test_gpu_golden(ctx):
+    import janus_gpu as jg
+    msgs, first, digest, msg_digest = golden()
+    d, md = jg.update_digests(ctx, msgs, first, msg_digests=True)
+    assert np.array_equal(d, digest)
+    assert np.array_equal(md, msg_digest)
+
+
+@pytest.mark.gpu
+def test_gpu_every_length_and_alignment(ctx):
+    # every length 0..300 (all padding cases: 55/56/63/64/119/120 ...) at every start offset mod 16
+    import janus_gpu as jg
+    rng = np.random.default_rng(3)
+    msgs = []
+    for n in range(0, 301):
+        msgs.append(rng.integers(0, 256, n).astype(np.uint8).tobytes())
+        msgs.append(rng.integers(0, 256, int(rng.integers(0, 16))).astype(np.uint8).tobytes())  # shifts the next start
+    d, md = jg.update_digests(ctx, msgs, [0, len(msgs)], msg_digests=True)
+    for m, g in zip(msgs, md):
+        assert g.tobytes() == hashlib.sha256(m).digest(), len(m)
+    assert d[0].tobytes() == py_digest(msgs)
+
+
+@pytest.mark.gpu
+def test_gpu_updates_nulls_and_empty(ctx):
+    import janus_gpu as jg
+    rng = np.random.default_rng(4)
+    msgs = random_msgs(rng, 2600, 0, 1500, null_every=7)
+    sizes = [0, 1, 1, 2, 3, 4, 5, 31, 32, 33, 64, 1000, 0, 1424]
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    assert first[-1] == len(msgs)
+    d, md = jg.update_digests(ctx, msgs, first, msg_digests=True)
+    ed, emd = orc.update_digests(msgs, first)
+    assert np.array_equal(md, emd)
+    assert np.array_equal(d, ed)
+    for u in range(len(sizes)):
+        assert d[u].tobytes() == py_digest(msgs[first[u]:first[u + 1]])
+
+
+@pytest.mark.gpu
+def test_gpu_no_updates_and_all_null(ctx):
+    import janus_gpu as jg
+    d = jg.update_digests(ctx, [], [0])
+    assert d.shape == (0, 32)
+    d = jg.update_digests(ctx, [None, None, None], [0, 3])
+    assert d[0].tobytes() == hashlib.sha256(bytes(128)).digest()
+    d = jg.update_digests(ctx, [b""], [0, 1])
+    assert d[0].tobytes() == hashlib.sha256(hashlib.sha256(b"").digest()).digest()
+
+
+@pytest.mark.gpu
+def test_gpu_rent_boundary(ctx):
+    import janus_gpu as jg
+    rng = np.random.default_rng(5)
+    msgs = random_msgs(rng, 32769, 0, 40)
+    d = jg.update_digests(ctx, msgs, [0, 32768, 32768, 32769])  # second update empty
+    assert d[0].tobytes() == py_digest(msgs[:32768])
+    assert d[1].tobytes() == hashlib.sha256(b"").digest()
+    assert d[2].tobytes() == py_digest(msgs[32768:])
+    d = jg.update_digests(ctx, msgs, [0, 32769])
+    assert d[0].tobytes() == py_digest(msgs)
+
+
+@pytest.mark.gpu
+def test_gpu_bad_arguments(ctx):
+    import janus_gpu as jg
+    with pytest.raises(jg.JanusError):
+        jg.update_digests(ctx, [b"a", b"b"], [0, 1])      # first[-1] != payload count
+    with pytest.raises(jg.JanusError):
+        jg.update_digests(ctx, [b"a", b"b"], [0, 2, 1])   # decreasing
+
+
+@pytest.mark.gpu
+def test_gpu_wave_resident_pnc_payloads(ctx):
+    # the wave path over PNCounterMsg JSON payloads (what SafeCRDT.Update ships), 1000 per UpdateMessage
+    import janus_gpu as jg
+    rng = np.random.default_rng(6)
+    msgs = []
+    for i in range(5000):
+        g = ["%032x" % int(rng.integers(0, 2**63)) for _ in range(5)]
+        body = ",".join('"%s-%s-%s-%s-%s":%d' % (x[:8], x[8:12], x[12:16], x[16:20], x[20:], rng.integers(0, 2**31)) for x in g)
+        msgs.append(('{"pVector":{%s},"nVector":{%s}}' % (body, body[:len(body) // 2].rsplit(",", 1)[0])).encode())
+    w = jg.Wave(ctx, len(msgs), sum(map(len, msgs)))
+    try:
+        w.upload(np.zeros(len(msgs), np.uint32), msgs=msgs)
+        first = np.arange(0, 5001, 1000, dtype=np.uint64)
+        d, md = w.update_digests(first, msg_digests=True)
+    finally:
+        w.close()
+    for m, g in zip(msgs, md):
+        assert g.tobytes() == hashlib.sha256(m).digest()
+    for u in range(5):
+        assert d[u].tobytes() == py_digest(msgs[1000 * u:1000 * (u + 1)])
