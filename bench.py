@@ -301,7 +301,7 @@ def bench_c1(local):
 DIGEST_MSGS, DIGEST_PER_UPDATE = 1_000_000, 1000  # one C5-sized wave, clientBatchSize-sized UpdateMessages
 # VALU instructions per 64-byte block of the k_sha_msgs loop (compress + window shift, gfx950 ISA count of
 # csrc/digest.hip) and the chip's VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
-SHA_VALU_PER_BLOCK, VALU_LANE_OPS = 1650, 256 * 4 * 32 * 2.4e9
+SHA_VALU_PER_BLOCK, VALU_LANE_OPS = 1693, 256 * 4 * 32 * 2.4e9
 
 
 def digest_wave(n, seed):
@@ -325,10 +325,11 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
     try:
         w.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data, off=off)
         wall, ev = timed(ctx, sync, lambda: w.update_digests(first), steps, warmup)
-        # the same payloads as one-state UpdateMessages: the second level shrinks to one block per update,
-        # so this call's time is essentially k_sha_msgs (the first level) alone
-        single = np.arange(0, DIGEST_MSGS + 1, dtype=np.uint64)
-        wall1, ev1 = timed(ctx, sync, lambda: w.update_digests(single), steps, warmup)
+        # the first level alone (k_sha_msgs, digest bytes into device memory: jg_wave_sha256)
+        import torch
+        dout = torch.empty(DIGEST_MSGS * 32, dtype=torch.uint8, device=torch.device("cuda", ctx.device))
+        wall1, ev1 = timed(ctx, sync, lambda: w.sha256_device(dout.data_ptr(), async_=True), steps, warmup)
+        del dout
     finally:
         w.close()
     blocks = int(((off[1:] - off[:-1] + 72) // 64).sum())
@@ -338,14 +339,15 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
                         f"{DIGEST_MSGS // DIGEST_PER_UPDATE} UpdateMessages of {DIGEST_PER_UPDATE}",
             "msgs_per_s": DIGEST_MSGS / (wall / steps), "ms_per_wave": wall / steps * 1e3,
             "payload_GBps": data.size / (wall / steps) / 1e9, "event_ms": kern * 1e3, "sha_blocks": blocks,
-            "one_state_updates": {"msgs_per_s": DIGEST_MSGS / (wall1 / steps), "event_ms": kern1 * 1e3},
+            "first_level": {"kernel": "k_sha_msgs", "msgs_per_s": DIGEST_MSGS / (wall1 / steps), "event_ms": kern1 * 1e3,
+                            "payload_GBps": data.size / kern1 / 1e9},
             "second_level_chain_blocks": chain,
             "roofline": {"bound": "valu", "achieved": blocks / kern1 / 1e9, "unit": "Gblocks/s",
                          "peak": VALU_LANE_OPS / SHA_VALU_PER_BLOCK / 1e9,
                          "frac": blocks / kern1 / (VALU_LANE_OPS / SHA_VALU_PER_BLOCK),
-                         "scope": "first level (k_sha_msgs) from the one-state-update call; the 1000-state call adds the "
-                                  "second level, a serial chain of second_level_chain_blocks SHA-256 blocks per "
-                                  "UpdateMessage (latency-bound, DESIGN.md section 4)"}}
+                         "scope": "first level (k_sha_msgs, jg_wave_sha256); the full call adds the second level, a "
+                                  "serial chain of second_level_chain_blocks SHA-256 blocks per UpdateMessage "
+                                  "(latency-bound, DESIGN.md section 4)"}}
 
 
 def cpu_digest_baseline():
@@ -413,7 +415,7 @@ def main():
     world, rank, local = dist_env()
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-    if world > 1 or args.workload in ("all", "exchange"):
+    if world > 1 or args.workload in ("all", "exchange", "digest"):
         # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
         # instance (torch's libraries also name the runtime by an unversioned soname)
         import torch  # noqa: F401

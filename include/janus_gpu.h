@@ -283,6 +283,10 @@ int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_
 /* The same over a wave already in device memory (jg_wave_upload; no null payloads): first[n_updates]
  * must equal the wave's message count. */
 int jg_wave_update_digests(const jg_wave* wave, uint64_t n_updates, const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);
+/* SHA256.HashData of every payload of a device-resident wave (the per-message hashes ComputeDigest takes,
+ * DAGUpdateMessage.cs:43) into DEVICE memory d_out (wave count * 32 bytes, digest bytes), for a consumer
+ * on the device; async != 0 returns once queued on the context's stream (jg_fence waits). */
+int jg_wave_sha256(const jg_wave* wave, void* d_out, uint8_t async);
 
 /* ---------------------------------------------------------------------------------------------
  * Synthetic workloads (bench / size-independent parity): device-side counter-based generators,

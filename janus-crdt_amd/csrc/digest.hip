@@ -84,7 +84,9 @@ __device__ __forceinline__ void sha_init(uint32_t H[8]) {
     H[4] = 0x510e527f; H[5] = 0x9b05688c; H[6] = 0x1f83d9ab; H[7] = 0x5be0cd19;
 }
 
-// One lane per payload: D[8i..8i+8) = SHA-256 state words of payload i (zeros for a null payload).
+// One lane per payload: D[8i..8i+8) = SHA-256 state words of payload i (zeros for a null payload);
+// kBytes: the digest bytes instead (big-endian words, what SHA256.HashData returns).
+template <bool kBytes>
 __global__ void __launch_bounds__(kBlock) k_sha_msgs(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                      const uint8_t* __restrict__ is_null, uint64_t n, uint4* __restrict__ D) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -142,6 +144,10 @@ __global__ void __launch_bounds__(kBlock) k_sha_msgs(const uint8_t* __restrict__
             W[15] = (uint32_t)(len << 3);
         }
         compress(H, W);
+    }
+    if (kBytes) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) H[k] = bswap(H[k]);
     }
     D[2 * i] = make_uint4(H[0], H[1], H[2], H[3]);
     D[2 * i + 1] = make_uint4(H[4], H[5], H[6], H[7]);
@@ -308,7 +314,7 @@ void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, con
     auto* KW = reinterpret_cast<uint4*>(s + ((n * 32 + n_upd * 32 + hb.size() * 8 + 255) & ~255ull));
     hipStream_t st = ctx->stream;
     JG_HIP(hipMemcpyAsync(d_first, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, st));
-    if (n) k_sha_msgs<<<grid_for(n), kBlock, 0, st>>>(d_bytes, d_off, d_null, n, D);
+    if (n) k_sha_msgs<false><<<grid_for(n), kBlock, 0, st>>>(d_bytes, d_off, d_null, n, D);
     if (n_upd) {
         k_sha_expand<<<grid_for(B), kBlock, 0, st>>>(D, d_first, d_boff, n_upd, KW);
         k_sha_chain<<<grid_for(n_upd), kBlock, 0, st>>>(KW, d_boff, n_upd, out);
@@ -357,6 +363,18 @@ int jg_wave_update_digests(const jg_wave* w, uint64_t n_updates, const uint64_t*
         check_first(w->n, n_updates, first);
         jg::ensure_device(w->ctx);
         run_digests(w->ctx, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n, n_updates, first, msg_digest, digest);
+    });
+}
+
+int jg_wave_sha256(const jg_wave* w, void* d_out, uint8_t async) {
+    return jg::guard([&] {
+        JG_REQUIRE(w && (d_out || w->n == 0), JG_EINVAL, "jg_wave_sha256: NULL argument");
+        jg::ensure_device(w->ctx);
+        hipStream_t st = w->ctx->stream;
+        if (w->n) k_sha_msgs<true><<<grid_for(w->n), kBlock, 0, st>>>(w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n,
+                                                                      static_cast<uint4*>(d_out));
+        JG_HIP(hipGetLastError());
+        if (!async) JG_HIP(hipStreamSynchronize(st));
     });
 }
 

@@ -35,7 +35,7 @@ EXPORTS = [
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
-    "jg_update_digests", "jg_wave_update_digests",
+    "jg_update_digests", "jg_wave_update_digests", "jg_wave_sha256",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -80,6 +80,7 @@ _SIGS = {
     "jg_wave_destroy": ([_vp], C.c_int),
     "jg_update_digests": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_wave_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_wave_sha256": ([_vp, _vp, C.c_uint8], C.c_int),
     "jg_wave_upload": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_host_alloc": ([_vp, _u64, C.POINTER(_vp)], C.c_int),
@@ -378,6 +379,10 @@ class Wave:
         md = np.zeros((int(first[-1]), 32), np.uint8) if msg_digests else None
         _check(load().jg_wave_update_digests(self._h, nu, _ptr(first), _ptr(md), _ptr(dig)))
         return (dig, md) if msg_digests else dig
+
+    def sha256_device(self, d_out: int, async_: bool = False) -> None:
+        """SHA-256 of every payload into device memory at address d_out (jg_wave_sha256)."""
+        _check(load().jg_wave_sha256(self._h, _vp(d_out), 1 if async_ else 0))
 
     def close(self) -> None:
         if self._h:

@@ -163,3 +163,22 @@ def test_gpu_wave_resident_pnc_payloads(ctx):
         assert g.tobytes() == hashlib.sha256(m).digest()
     for u in range(5):
         assert d[u].tobytes() == py_digest(msgs[1000 * u:1000 * (u + 1)])
+
+
+@pytest.mark.gpu
+def test_gpu_wave_sha256_device_output(ctx):
+    # jg_wave_sha256: per-payload SHA256.HashData into device memory (digest bytes)
+    import torch
+    import janus_gpu as jg
+    rng = np.random.default_rng(7)
+    msgs = random_msgs(rng, 3000, 0, 900)
+    w = jg.Wave(ctx, len(msgs), sum(map(len, msgs)))
+    try:
+        w.upload(np.zeros(len(msgs), np.uint32), msgs=msgs)
+        out = torch.zeros(len(msgs) * 32, dtype=torch.uint8, device=torch.device("cuda", ctx.device))
+        w.sha256_device(out.data_ptr())
+        got = out.cpu().numpy().reshape(-1, 32)
+    finally:
+        w.close()
+    for m, g in zip(msgs, got):
+        assert g.tobytes() == hashlib.sha256(m).digest()
