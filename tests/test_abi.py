@@ -63,3 +63,10 @@ def test_no_device_fails_loudly():
 def test_missing_library_raises(tmp_path):
     with pytest.raises(FileNotFoundError):
         jg.load(tmp_path / "nope.so")
+
+
+def test_integration_binds_every_entry_point():
+    # INTEGRATION.md carries the C# [DllImport] declaration a maintainer adds for each ABI function
+    text = (ROOT / "INTEGRATION.md").read_text()
+    missing = [n for n in header_functions() if f"extern int {n}(" not in text]
+    assert not missing, missing
