@@ -11,6 +11,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
     python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload pnc-orset > "$OUT/bench_trace.json" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_exch" -o run --output-format csv -- \
     python3 bench.py --steps 16 --warmup 2 --no-cpu-baseline --workload exchange > "$OUT/bench_trace_exch.json" || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_digest" -o run --output-format csv -- \
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload digest > "$OUT/bench_trace_digest.json" || exit 1
 for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $C -d "$OUT/pmc_$C" -o run --output-format csv -- \
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload pnc-orset > "$OUT/bench_pmc_$C.json" || exit 1
