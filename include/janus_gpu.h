@@ -9,9 +9,11 @@
  *     no exception or abort crosses the ABI;
  *   - calls are synchronous (return after the work is complete) unless they take `async` != 0,
  *     in which case jg_fence(ctx) waits for them;
- *   - one writer per store handle at a time (the reference serialises its stable apply with a
- *     SemaphoreSlim and its prospective merges with lock(crdt)), concurrent readers allowed;
- *     each context owns one HIP stream on one device.
+ *   - thread-safe per context: every call holds its context's lock for its duration (the context's
+ *     scratch buffers and HIP stream are shared by all of its handles), so concurrent callers — the
+ *     reference's receiver threads merging prospective copies under lock(crdt), readers querying —
+ *     are serialised per context; use one context per thread for parallel device work.  Each context
+ *     owns one HIP stream (plus a copy stream for wave uploads) on one device.
  *
  * Reference interfaces each entry point replaces are cited per function (paths relative to the
  * reference root, MSRG/Janus-CRDT @ 2025-03-10).

@@ -118,6 +118,7 @@ int jg_close(jg_ctx* ctx) {
 
 int jg_fence(jg_ctx* ctx) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx, JG_EINVAL, "jg_fence: ctx is NULL");
         jg::ensure_device(ctx);
         JG_HIP(hipStreamSynchronize(ctx->stream));
@@ -126,6 +127,7 @@ int jg_fence(jg_ctx* ctx) {
 
 int jg_stream(jg_ctx* ctx, void** s) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && s, JG_EINVAL, "jg_stream: NULL argument");
         *s = (void*)ctx->stream;
     });

@@ -336,6 +336,7 @@ extern "C" {
 int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, const uint8_t* is_null, uint64_t n_updates,
                       const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && off && first && (digest || n_updates == 0), JG_EINVAL, "jg_update_digests: NULL argument");
         JG_REQUIRE(n < 0xFFFFFFFFull * kBlock, JG_EINVAL, "jg_update_digests: too many payloads");
         JG_REQUIRE(off[0] == 0, JG_EINVAL, "jg_update_digests: off[0] must be 0");
@@ -359,6 +360,7 @@ int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_
 
 int jg_wave_update_digests(const jg_wave* w, uint64_t n_updates, const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(w);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(w && first && (digest || n_updates == 0), JG_EINVAL, "jg_wave_update_digests: NULL argument");
         check_first(w->n, n_updates, first);
         jg::ensure_device(w->ctx);
@@ -368,6 +370,7 @@ int jg_wave_update_digests(const jg_wave* w, uint64_t n_updates, const uint64_t*
 
 int jg_wave_sha256(const jg_wave* w, void* d_out, uint8_t async) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(w);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(w && (d_out || w->n == 0), JG_EINVAL, "jg_wave_sha256: NULL argument");
         jg::ensure_device(w->ctx);
         hipStream_t st = w->ctx->stream;

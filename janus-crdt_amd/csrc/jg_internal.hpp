@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <new>
 #include <string>
 
@@ -78,6 +79,11 @@ struct jg_ctx {
     jg::DevBuf flags;    // small zero-initialised status words (error flags)
     hipStream_t copy = nullptr;    // wave uploads: chunk k+1's H2D overlaps chunk k's parse on `stream`
     hipEvent_t copied = nullptr;
+    // Every entry point that reaches this context holds `mu` for the call: the scratch buffers and the
+    // streams are shared by all of the context's handles, so concurrent callers (the reference's
+    // receiver threads merging prospective copies, readers querying) are serialised here.  Recursive:
+    // one-shot entry points reuse the streamed ones on the same thread.
+    std::recursive_mutex mu;
 };
 
 struct jg_pnc {
@@ -151,6 +157,9 @@ struct jg_orset {
 };
 
 namespace jg {
+using CtxLock = std::unique_lock<std::recursive_mutex>;
+inline CtxLock lock(jg_ctx* c) { return c ? CtxLock(c->mu) : CtxLock(); }
+template <class H> inline CtxLock lock(const H* h) { return lock(h ? h->ctx : nullptr); }
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 // After H2D copies queued on ctx->copy: make ctx->stream wait for them (stream order for the kernels

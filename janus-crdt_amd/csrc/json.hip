@@ -572,6 +572,7 @@ extern "C" {
 
 int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid* replica, uint32_t* col_out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_intern: store is NULL");
         if (n == 0) return;
         JG_REQUIRE(key_idx && replica && col_out, JG_EINVAL, "jg_pnc_intern: NULL argument");
@@ -611,6 +612,7 @@ int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid*
 
 int jg_pnc_columns(jg_pnc* p, uint64_t n, const uint32_t* key_idx, jg_guid* replicas, uint32_t* ncols) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_columns: store is NULL");
         if (n == 0) return;
         JG_REQUIRE(key_idx && replicas && ncols, JG_EINVAL, "jg_pnc_columns: NULL argument");
@@ -635,6 +637,7 @@ int jg_pnc_columns(jg_pnc* p, uint64_t n, const uint32_t* key_idx, jg_guid* repl
 
 int jg_wave_create(jg_ctx* ctx, uint64_t cap_msgs, uint64_t cap_bytes, jg_wave** out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && out, JG_EINVAL, "jg_wave_create: NULL argument");
         JG_REQUIRE(cap_msgs < 0xFFFFFFFFull, JG_EINVAL, "jg_wave_create: at most 2^32-2 messages per wave");
         jg::ensure_device(ctx);
@@ -656,6 +659,7 @@ int jg_wave_create(jg_ctx* ctx, uint64_t cap_msgs, uint64_t cap_bytes, jg_wave**
 
 int jg_wave_destroy(jg_wave* w) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(w);  // calls on one context are serialised (shared scratch, stream)
         if (!w) return;
         jg::ensure_device(w->ctx);
         JG_HIP(hipStreamSynchronize(w->ctx->stream));
@@ -665,6 +669,7 @@ int jg_wave_destroy(jg_wave* w) {
 
 int jg_wave_upload(jg_wave* w, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(w);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(w && key_idx && off && (bytes || n == 0), JG_EINVAL, "jg_wave_upload: NULL argument");
         JG_REQUIRE(n <= w->cap_msgs && off[n] <= w->cap_bytes, JG_EINVAL, "jg_wave_upload: wave exceeds the capacity");
         JG_REQUIRE(off[0] == 0, JG_EINVAL, "jg_wave_upload: off[0] must be 0");
@@ -687,6 +692,7 @@ int jg_wave_upload(jg_wave* w, uint64_t n, const uint32_t* key_idx, const uint64
 
 int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         if (bad_msg) *bad_msg = UINT64_MAX;
         JG_REQUIRE(p && w, JG_EINVAL, "jg_pnc_merge_wave: NULL argument");
         JG_REQUIRE(p->ctx == w->ctx, JG_EINVAL, "jg_pnc_merge_wave: wave and store belong to different contexts");
@@ -700,6 +706,7 @@ int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
 
 int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_begin: store is NULL");
         jg_ctx* ctx = p->ctx;
         jg::ensure_device(ctx);
@@ -718,6 +725,7 @@ int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
 
 int jg_pnc_wave_append(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_append: no open wave (jg_pnc_wave_begin)");
         if (n == 0) return;
         JG_REQUIRE(key_idx && off && bytes, JG_EINVAL, "jg_pnc_wave_append: NULL argument");
@@ -746,6 +754,7 @@ int jg_pnc_wave_append(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uin
 
 int jg_pnc_wave_commit(jg_pnc* p, uint64_t* bad_msg) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         if (bad_msg) *bad_msg = UINT64_MAX;
         JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_commit: no open wave (jg_pnc_wave_begin)");
         jg::ensure_device(p->ctx);
@@ -757,6 +766,7 @@ int jg_pnc_wave_commit(jg_pnc* p, uint64_t* bad_msg) {
 
 int jg_pnc_wave_abort(jg_pnc* p) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_abort: store is NULL");
         jg::ensure_device(p->ctx);
         JG_HIP(hipStreamSynchronize(p->ctx->stream));  // pass A only read the wave: nothing to undo
@@ -765,6 +775,7 @@ int jg_pnc_wave_abort(jg_pnc* p) {
 }
 
 int jg_pnc_merge_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+    auto lk_ = jg::lock(p);  // the whole begin/append/commit sequence under the context lock
     if (bad_msg) *bad_msg = UINT64_MAX;
     if (p && n && off) {
         int rc = jg_pnc_wave_begin(p, n, off[n]);
@@ -785,6 +796,7 @@ int jg_pnc_merge_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint
 
 int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && out, JG_EINVAL, "jg_host_alloc: NULL argument");
         jg::ensure_device(ctx);
         *out = nullptr;
@@ -801,6 +813,7 @@ int jg_host_free(void* p) {
 
 int jg_pnc_encode_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p && off, JG_EINVAL, "jg_pnc_encode_json: NULL argument");
         off[0] = 0;
         if (n == 0) return;

@@ -554,6 +554,7 @@ extern "C" {
 
 int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && out, JG_EINVAL, "jg_orset_create: NULL argument");
         jg::ensure_device(ctx);
         auto* s = new jg_orset();
@@ -575,6 +576,7 @@ int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** 
 
 int jg_orset_destroy(jg_orset* s) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         if (!s) return;
         jg::ensure_device(s->ctx);
         JG_HIP(hipStreamSynchronize(s->ctx->stream));
@@ -584,6 +586,7 @@ int jg_orset_destroy(jg_orset* s) {
 
 int jg_orset_load(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_load: store is NULL");
         JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_load: NULL records");
         jg::ensure_device(s->ctx);
@@ -596,6 +599,7 @@ int jg_orset_load(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_ta
 
 int jg_orset_size(jg_orset* s, uint64_t* n_add, uint64_t* n_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_size: store is NULL");
         jg::ensure_device(s->ctx);
         if (s->counts_pending) check_err_flag(s->ctx, "jg_orset_size");
@@ -607,6 +611,7 @@ int jg_orset_size(jg_orset* s, uint64_t* n_add, uint64_t* n_rem) {
 
 int jg_orset_read(jg_orset* s, jg_tagrec* add, uint64_t cap_add, jg_tagrec* rem, uint64_t cap_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_read: store is NULL");
         jg::ensure_device(s->ctx);
         jg::sync_counts(s);
@@ -620,6 +625,7 @@ int jg_orset_read(jg_orset* s, jg_tagrec* add, uint64_t cap_add, jg_tagrec* rem,
 
 int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_merge: store is NULL");
         JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_merge: NULL records");
         jg_ctx* ctx = s->ctx;
@@ -634,6 +640,7 @@ int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_t
 
 int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(dst);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(dst && src && dst != src, JG_EINVAL, "jg_orset_merge_store: bad stores");
         JG_REQUIRE(dst->ctx == src->ctx, JG_EINVAL, "jg_orset_merge_store: stores belong to different contexts");
         jg::ensure_device(dst->ctx);
@@ -644,6 +651,7 @@ int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
 
 int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int async) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(a);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(a && b && out, JG_EINVAL, "jg_orset_union: NULL store");
         JG_REQUIRE(out != a && out != b, JG_EINVAL, "jg_orset_union: out may not alias an input");
         JG_REQUIRE(a->ctx == b->ctx && a->ctx == out->ctx, JG_EINVAL, "jg_orset_union: stores belong to different contexts");
@@ -662,6 +670,7 @@ int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int asyn
 int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
                        const uint64_t* tag_hi, uint8_t* result) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_apply_ops: store is NULL");
         if (n_ops == 0) return;
         JG_REQUIRE(set && elem && op && tag_lo && tag_hi && result, JG_EINVAL, "jg_orset_apply_ops: NULL argument");
@@ -676,6 +685,7 @@ int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const u
 
 int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, uint64_t n, uint8_t* out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_contains: store is NULL");
         if (n == 0) return;
         JG_REQUIRE(set && elem && out, JG_EINVAL, "jg_orset_contains: NULL argument");
@@ -698,6 +708,7 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
 int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* add_off, jg_tagrec* add, uint64_t cap_add, uint64_t* rem_off,
                        jg_tagrec* rem, uint64_t cap_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && add_off && rem_off, JG_EINVAL, "jg_orset_read_sets: NULL argument");
         add_off[0] = rem_off[0] = 0;
         if (n == 0) return;
@@ -734,6 +745,7 @@ int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* a
 
 int jg_orset_lookup_all(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* off, uint32_t* elems, uint64_t cap) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && off, JG_EINVAL, "jg_orset_lookup_all: NULL argument");
         off[0] = 0;
         if (n == 0) return;

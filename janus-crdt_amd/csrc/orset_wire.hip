@@ -1132,6 +1132,7 @@ extern "C" {
 int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const uint32_t* next_id, const uint8_t* cleared, uint64_t n_names,
                         const uint32_t* name_set, const uint32_t* name_id, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_names_sync: store is NULL");
         JG_REQUIRE((n_sets == 0 || (set && next_id && cleared)) && (n_names == 0 || (name_set && name_id && off && bytes)), JG_EINVAL,
                    "jg_orset_names_sync: NULL argument");
@@ -1184,6 +1185,7 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
 
 int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_begin: store is NULL");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -1199,6 +1201,7 @@ int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
 
 int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_append: no open wave (jg_orset_wave_begin)");
         jg_orset_wire* w = s->wire;
         JG_REQUIRE(!w->checked, JG_EINVAL, "jg_orset_wave_append: the wave was already checked");
@@ -1236,6 +1239,7 @@ int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uin
 int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
     if (bad_msg) *bad_msg = UINT64_MAX;
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_check: no open wave (jg_orset_wave_begin)");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -1254,6 +1258,7 @@ int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
 
 int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_commit: no open wave (jg_orset_wave_begin)");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -1275,6 +1280,7 @@ int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
 
 int jg_orset_wave_abort(jg_orset* s) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_abort: store is NULL");
         jg::ensure_device(s->ctx);
         JG_HIP(hipStreamSynchronize(s->ctx->stream));
@@ -1289,6 +1295,7 @@ int jg_orset_wave_abort(jg_orset* s) {
 
 int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && n_names && n_bytes, JG_EINVAL, "jg_orset_wave_names: NULL argument");
         jg_orset_wire* w = s->wire;
         const uint64_t n = w ? w->g1 - w->g0 : 0, nb = w ? w->p1 - w->p0 : 0;
@@ -1316,6 +1323,7 @@ int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint3
 }
 
 int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg) {
+    auto lk_ = jg::lock(s);  // the whole begin/append/check/commit sequence under the context lock
     if (bad_msg) *bad_msg = UINT64_MAX;
     if (!s || (n && (!set || !off || !bytes)))
         return jg::guard([&] { jg::fail(JG_EINVAL, "jg_orset_merge_json: NULL argument"); });

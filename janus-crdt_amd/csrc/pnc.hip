@@ -375,6 +375,7 @@ extern "C" {
 
 int jg_pnc_create(jg_ctx* ctx, uint64_t n_keys, uint32_t n_replicas, uint32_t elem_bytes, jg_pnc** out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && out, JG_EINVAL, "jg_pnc_create: NULL argument");
         JG_REQUIRE(elem_bytes == 4 || elem_bytes == 8, JG_EINVAL, "jg_pnc_create: elem_bytes must be 4 or 8");
         JG_REQUIRE(n_replicas > 0 && n_keys > 0, JG_EINVAL, "jg_pnc_create: empty shape");
@@ -399,6 +400,7 @@ int jg_pnc_create(jg_ctx* ctx, uint64_t n_keys, uint32_t n_replicas, uint32_t el
 
 int jg_pnc_destroy(jg_pnc* p) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         if (!p) return;
         jg::ensure_device(p->ctx);
         JG_HIP(hipStreamSynchronize(p->ctx->stream));
@@ -408,6 +410,7 @@ int jg_pnc_destroy(jg_pnc* p) {
 
 int jg_pnc_write_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_write_rows");
         JG_REQUIRE(P && N, JG_EINVAL, "jg_pnc_write_rows: NULL rows");
         if (n_rows == 0) return;
@@ -432,6 +435,7 @@ int jg_pnc_write_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const
 
 int jg_pnc_read_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, void* P, void* N) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_read_rows");
         JG_REQUIRE(P && N, JG_EINVAL, "jg_pnc_read_rows: NULL rows");
         if (n_rows == 0) return;
@@ -456,6 +460,7 @@ int jg_pnc_read_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, void* 
 
 int jg_pnc_merge_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_merge_rows");
         JG_REQUIRE(P && N, JG_EINVAL, "jg_pnc_merge_rows: NULL rows");
         if (n_rows == 0) return;
@@ -476,6 +481,7 @@ int jg_pnc_merge_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const
 
 int jg_pnc_apply_ops(jg_pnc* p, uint64_t n_ops, const uint32_t* key, const uint32_t* col, const int64_t* delta, const uint8_t* is_n) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_apply_ops");
         if (n_ops == 0) return;
         JG_REQUIRE(key && col && delta && is_n, JG_EINVAL, "jg_pnc_apply_ops: NULL argument");
@@ -507,6 +513,7 @@ int jg_pnc_apply_ops(jg_pnc* p, uint64_t n_ops, const uint32_t* key, const uint3
 
 int jg_pnc_values(jg_pnc* p, const uint32_t* key_idx, uint64_t n, int64_t* out, uint8_t* overflow) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_values");
         JG_REQUIRE(out && overflow, JG_EINVAL, "jg_pnc_values: NULL output");
         if (n == 0) return;
@@ -534,6 +541,7 @@ int jg_pnc_values(jg_pnc* p, const uint32_t* key_idx, uint64_t n, int64_t* out, 
 
 int jg_rows_create(jg_ctx* ctx, uint64_t n_rows, uint32_t n_replicas, uint32_t elem_bytes, jg_rows** out) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(ctx && out, JG_EINVAL, "jg_rows_create: NULL argument");
         JG_REQUIRE(elem_bytes == 4 || elem_bytes == 8, JG_EINVAL, "jg_rows_create: elem_bytes must be 4 or 8");
         JG_REQUIRE(n_rows > 0 && n_replicas > 0, JG_EINVAL, "jg_rows_create: empty shape");
@@ -554,6 +562,7 @@ int jg_rows_create(jg_ctx* ctx, uint64_t n_rows, uint32_t n_replicas, uint32_t e
 
 int jg_rows_destroy(jg_rows* r) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(r);  // calls on one context are serialised (shared scratch, stream)
         if (!r) return;
         jg::ensure_device(r->ctx);
         JG_HIP(hipStreamSynchronize(r->ctx->stream));
@@ -563,6 +572,7 @@ int jg_rows_destroy(jg_rows* r) {
 
 int jg_rows_upload(jg_rows* r, const uint32_t* key_idx, const void* P, const void* N) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(r);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(r && P && N, JG_EINVAL, "jg_rows_upload: NULL argument");
         jg_ctx* ctx = r->ctx;
         jg::ensure_device(ctx);
@@ -585,6 +595,7 @@ int jg_rows_upload(jg_rows* r, const uint32_t* key_idx, const void* P, const voi
 
 int jg_pnc_merge_batch(jg_pnc* p, const jg_rows* r, int async) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         check_store(p, "jg_pnc_merge_batch");
         JG_REQUIRE(r, JG_EINVAL, "jg_pnc_merge_batch: rows is NULL");
         JG_REQUIRE(r->ctx == p->ctx, JG_EINVAL, "jg_pnc_merge_batch: rows and store belong to different contexts");

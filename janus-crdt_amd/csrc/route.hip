@@ -303,6 +303,7 @@ extern "C" {
 
 int jg_rows_route(const jg_rows* r, uint32_t world, uint64_t* counts, void* d_keys, void* d_P, void* d_N, uint64_t cap_rows) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(r);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_rows_route";
         JG_REQUIRE(r && counts, JG_EINVAL, "%s: NULL argument", fn);
         JG_REQUIRE(world >= 1 && world <= kMaxWorld, JG_EINVAL, "%s: world %u outside [1, %u]", fn, world, kMaxWorld);
@@ -323,6 +324,7 @@ int jg_rows_route(const jg_rows* r, uint32_t world, uint64_t* counts, void* d_ke
 
 int jg_pnc_merge_device(jg_pnc* p, uint64_t n_rows, const void* d_keys, const void* d_P, const void* d_N) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_pnc_merge_device";
         JG_REQUIRE(p, JG_EINVAL, "%s: store is NULL", fn);
         if (n_rows == 0) return;
@@ -352,6 +354,7 @@ int jg_pnc_merge_device(jg_pnc* p, uint64_t n_rows, const void* d_keys, const vo
 int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* rem_counts, void* d_add_key, void* d_add_tag,
                    uint64_t cap_add, void* d_rem_key, void* d_rem_tag, uint64_t cap_rem) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_orset_route";
         JG_REQUIRE(s && add_counts && rem_counts, JG_EINVAL, "%s: NULL argument", fn);
         JG_REQUIRE(world >= 1 && world <= kMaxWorld, JG_EINVAL, "%s: world %u outside [1, %u]", fn, world, kMaxWorld);
@@ -373,6 +376,7 @@ int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* 
 int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const void* d_add_key,
                           const void* d_add_tag, const void* d_rem_key, const void* d_rem_tag) {
     return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_orset_merge_device";
         JG_REQUIRE(s && (n_runs == 0 || (add_counts && rem_counts)), JG_EINVAL, "%s: NULL argument", fn);
         jg_ctx* ctx = s->ctx;
