@@ -81,6 +81,7 @@ const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want
 
 uint32_t GpuStableStore::elem_id(uint32_t set, const std::optional<std::string>& e, bool create) {
     if (!e) return JG_NULL_ELEM;
+    materialize_names();
     SetKey& s = sets_[set];
     for (; s.indexed < s.names.size(); ++s.indexed) s.elems.emplace(s.names[s.indexed], s.indexed);  // ids a wave issued
     auto it = s.elems.find(*e);
@@ -218,6 +219,7 @@ WorkerPool& GpuStableStore::pool() {
 
 void GpuStableStore::flush_names() {
     if (pending_names_.empty()) return;
+    materialize_names();
     std::vector<uint32_t> set, next, nset, nid;
     std::vector<uint8_t> cleared, bytes;
     std::vector<uint64_t> off{0};
@@ -240,28 +242,42 @@ void GpuStableStore::flush_names() {
     pending_names_.clear();
 }
 
-// The element ids the last wave issued (sorted by set, then id) appended to the host tables, the sets
-// split over the workers in contiguous ranges.
+// The element ids the last wave issued (sorted by set, then id), copied out of the engine; they join the
+// host tables in materialize_names.
 void GpuStableStore::take_wave_names() {
     uint64_t n = 0, nb = 0;
     check(jg_orset_wave_names(orset_, &n, &nb, nullptr, nullptr, nullptr, nullptr));
     if (n == 0) return;
-    std::vector<uint32_t> set(n), id(n);
-    std::vector<uint64_t> off(n + 1);
-    std::vector<uint8_t> bytes(std::max<uint64_t>(nb, 1));
-    check(jg_orset_wave_names(orset_, &n, &nb, set.data(), id.data(), off.data(), bytes.data()));
-    std::vector<int> bad(pool().size(), 0);
-    parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
-        while (b < n && b > 0 && set[b - 1] == set[b]) ++b;  // that set belongs to the previous worker
-        while (e < n && e > 0 && set[e - 1] == set[e]) ++e;
-        for (size_t i = b; i < e; ++i) {
-            SetKey& sk = sets_[set[i]];
-            if (id[i] != sk.names.size()) { bad[t] = 1; return; }
-            sk.names.emplace_back(reinterpret_cast<const char*>(bytes.data()) + off[i], off[i + 1] - off[i]);  // elems: lazily
-        }
-    });
-    for (int b : bad)
-        if (b) throw EngineError(JG_ESTATE, "element ids of the engine and the host tables disagree");
+    WaveNames w;
+    w.set.resize(n);
+    w.id.resize(n);
+    w.off.resize(n + 1);
+    w.bytes.resize(std::max<uint64_t>(nb, 1));
+    check(jg_orset_wave_names(orset_, &n, &nb, w.set.data(), w.id.data(), w.off.data(), w.bytes.data()));
+    wave_names_.push_back(std::move(w));
+}
+
+// Pending wave names appended to the SetKey tables, wave after wave, the sets split over the workers in
+// contiguous ranges.
+void GpuStableStore::materialize_names() {
+    if (wave_names_.empty()) return;
+    for (const WaveNames& w : wave_names_) {
+        const size_t n = w.set.size();
+        const std::vector<uint32_t>& set = w.set;
+        std::vector<int> bad(pool().size(), 0);
+        parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+            while (b < n && b > 0 && set[b - 1] == set[b]) ++b;  // that set belongs to the previous worker
+            while (e < n && e > 0 && set[e - 1] == set[e]) ++e;
+            for (size_t i = b; i < e; ++i) {
+                SetKey& sk = sets_[set[i]];
+                if (w.id[i] != sk.names.size()) { bad[t] = 1; return; }
+                sk.names.emplace_back(reinterpret_cast<const char*>(w.bytes.data()) + w.off[i], w.off[i + 1] - w.off[i]);  // elems: lazily
+            }
+        });
+        for (int x : bad)
+            if (x) throw EngineError(JG_ESTATE, "element ids of the engine and the host tables disagree");
+    }
+    wave_names_.clear();
 }
 
 // Pinned staging for wave chunks: arenas carved front to back each wave and kept for the next; a wave
@@ -538,6 +554,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
 }
 
 std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) {
+    materialize_names();
     std::vector<uint8_t> result(ops.size(), 1);
     std::vector<uint32_t> pkey, pcol;
     std::vector<int64_t> pdelta;
@@ -626,6 +643,7 @@ std::vector<std::string> GpuStableStore::EncodePNCStates(const std::vector<Guid>
 }
 
 std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids) {
+    materialize_names();
     std::vector<uint32_t> sets;
     sets.reserve(uids.size());
     for (const Guid& u : uids) sets.push_back(ref(u, CrdtType::ORSet).idx);
@@ -785,6 +803,7 @@ void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first)
 }
 
 std::vector<std::optional<std::string>> GpuStableStore::QueryStableLookupAll(const Guid& uid) {
+    materialize_names();
     const uint32_t set = ref(uid, CrdtType::ORSet).idx;
     uint64_t off[2] = {0, 0};
     check(jg_orset_lookup_all(orset_, 1, &set, off, nullptr, 0));

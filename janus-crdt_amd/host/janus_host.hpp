@@ -229,7 +229,13 @@ class GpuStableStore {
     struct PendingNames { bool cleared = false; std::vector<uint32_t> ids; };
     std::unordered_map<uint32_t, PendingNames> pending_names_;
     void flush_names();
-    void take_wave_names();  // ids the last OR-Set wave issued -> SetKey tables
+    // Ids the last OR-Set wave issued: copied from the engine right after the commit (the engine keeps
+    // only the last commit's), appended to the SetKey tables on first use by anything that reads names
+    // (interning for ops, encode, LookupAll, the name sync) — not on the apply path.
+    struct WaveNames { std::vector<uint32_t> set, id; std::vector<uint64_t> off; std::vector<uint8_t> bytes; };
+    std::vector<WaveNames> wave_names_;
+    void take_wave_names();
+    void materialize_names();
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
     void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
