@@ -182,3 +182,33 @@ def test_gpu_wave_sha256_device_output(ctx):
         w.close()
     for m, g in zip(msgs, got):
         assert g.tobytes() == hashlib.sha256(m).digest()
+
+
+@pytest.mark.gpu
+def test_gpu_full_wave_sampled(ctx):
+    # full C5 size (1M payloads of 340-375 B, 1000 UpdateMessages of 1000, as bench.py): every update
+    # digest is computed on the device; three updates and 2000 payload hashes are recomputed by hashlib
+    import torch
+    import janus_gpu as jg
+    rng = np.random.default_rng(8)
+    n, per = 1_000_000, 1000
+    lens = rng.integers(340, 376, n).astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = rng.integers(32, 127, int(off[-1]), dtype=np.uint8)
+    first = np.arange(0, n + 1, per, dtype=np.uint64)
+    w = jg.Wave(ctx, n, data.size)
+    try:
+        w.upload(np.zeros(n, np.uint32), data=data, off=off)
+        d = w.update_digests(first)
+        out = torch.zeros(n * 32, dtype=torch.uint8, device=torch.device("cuda", ctx.device))
+        w.sha256_device(out.data_ptr())
+        md = out.cpu().numpy().reshape(-1, 32)
+    finally:
+        w.close()
+    buf = data.tobytes()
+    msg = lambda i: buf[int(off[i]):int(off[i + 1])]  # noqa: E731
+    for u in (0, 499, 999):
+        assert d[u].tobytes() == py_digest([msg(i) for i in range(u * per, (u + 1) * per)])
+    for i in rng.integers(0, n, 2000):
+        assert md[i].tobytes() == hashlib.sha256(msg(i)).digest()
