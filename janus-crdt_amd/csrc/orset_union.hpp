@@ -24,6 +24,13 @@ constexpr int kQShift = 9;  // LUT granularity: one entry per 512 ranks
 struct Tag { unsigned long long lo, hi; };
 
 __device__ __forceinline__ Tag ld_tag(const uint4* p) { return __builtin_bit_cast(Tag, *p); }
+typedef unsigned int nt_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Tag ld_tag_nt(const uint4* p) {
+    return __builtin_bit_cast(Tag, __builtin_nontemporal_load(reinterpret_cast<const nt_v4u*>(p)));
+}
+__device__ __forceinline__ void st_tag_nt(uint4* p, uint4 v) {
+    __builtin_nontemporal_store(__builtin_bit_cast(nt_v4u, v), reinterpret_cast<nt_v4u*>(p));
+}
 __device__ __forceinline__ uint4 to_u4(Tag t) { return __builtin_bit_cast(uint4, t); }
 
 // Branch-free lexicographic compare on (key, tag.lo, tag.hi), unsigned.
@@ -173,8 +180,8 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
             uint64_t slot;
             if (s < kSeg) slot = (uint64_t)((from_a ? ca : cb) + s) * (uint64_t)(from_a ? a.C : b.C) + (r - s_off[side][s]);
             else slot = slot_of(from_a ? a : b, r);  // > 64 tiny chunks under one tile (drop-filtered input)
-            rk[it] = (from_a ? a.key : b.key)[slot];
-            const Tag t = ld_tag((from_a ? a.tag : b.tag) + slot);
+            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + slot);  // each record is read once
+            const Tag t = ld_tag_nt((from_a ? a.tag : b.tag) + slot);
             rlo[it] = t.lo;
             rhi[it] = t.hi;
         }
@@ -285,9 +292,9 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     }
     __syncthreads();
     const uint64_t base = tile * (uint64_t)kTile;
-    for (int x = tid; x < block_total; x += kOB) {
-        ok[base + x] = s_key[x];
-        ot[base + x] = s_tag[x];
+    for (int x = tid; x < block_total; x += kOB) {  // written once, read by a later launch: non-temporal
+        __builtin_nontemporal_store(s_key[x], ok + base + x);
+        st_tag_nt(ot + base + x, s_tag[x]);
     }
     if (tid == 0) ocnt[tile] = (uint32_t)block_total;
 }
