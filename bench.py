@@ -299,6 +299,7 @@ def bench_c1(local):
 
 
 DIGEST_MSGS, DIGEST_PER_UPDATE = 1_000_000, 1000  # one C5-sized wave, clientBatchSize-sized UpdateMessages
+DIGEST_PIPE = 8  # waves per pipelined call
 # VALU instructions per 64-byte block of the k_sha_msgs loop (compress + window shift, gfx950 ISA count of
 # csrc/digest.hip) and the chip's VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
 SHA_VALU_PER_BLOCK, VALU_LANE_OPS = 1693, 256 * 4 * 32 * 2.4e9
@@ -330,6 +331,9 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
         dout = torch.empty(DIGEST_MSGS * 32, dtype=torch.uint8, device=torch.device("cuda", ctx.device))
         wall1, ev1 = timed(ctx, sync, lambda: w.sha256_device(dout.data_ptr(), async_=True), steps, warmup)
         del dout
+        # pipelined: DIGEST_PIPE waves in one jg_waves_update_digests call (wave k's chains on the
+        # context's second stream beside wave k+1's first level); the same resident wave listed each time
+        wall_p, ev_p = timed(ctx, sync, lambda: jg.waves_update_digests([w] * DIGEST_PIPE, [first] * DIGEST_PIPE), steps, warmup)
     finally:
         w.close()
     blocks = int(((off[1:] - off[:-1] + 72) // 64).sum())
@@ -342,6 +346,9 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
             "first_level": {"kernel": "k_sha_msgs", "msgs_per_s": DIGEST_MSGS / (wall1 / steps), "event_ms": kern1 * 1e3,
                             "payload_GBps": data.size / kern1 / 1e9},
             "second_level_chain_blocks": chain,
+            "pipelined": {"api": "jg_waves_update_digests", "waves_per_call": DIGEST_PIPE,
+                          "msgs_per_s": DIGEST_MSGS * DIGEST_PIPE / (wall_p / steps),
+                          "ms_per_wave": wall_p / steps / DIGEST_PIPE * 1e3},
             "roofline": {"bound": "valu", "achieved": blocks / kern1 / 1e9, "unit": "Gblocks/s",
                          "peak": VALU_LANE_OPS / SHA_VALU_PER_BLOCK / 1e9,
                          "frac": blocks / kern1 / (VALU_LANE_OPS / SHA_VALU_PER_BLOCK),

@@ -285,6 +285,15 @@ int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_
 /* The same over a wave already in device memory (jg_wave_upload; no null payloads): first[n_updates]
  * must equal the wave's message count. */
 int jg_wave_update_digests(const jg_wave* wave, uint64_t n_updates, const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);
+/* The same for n_waves device-resident waves of one context in ONE call, pipelined: wave k+1's
+ * per-payload hashes run while wave k's UpdateMessage chains (the serial second level) run on a second
+ * stream.  Wave k: n_updates[k] UpdateMessages over payloads first[k][u].. (rules as above, first[k]
+ * [n_updates[k]] = that wave's count), digests into digest[k] (n_updates[k] * 32 bytes).  A wave may
+ * appear more than once.  Synchronous; JG_EINVAL (nothing computed) when any wave's arguments are
+ * malformed or the waves belong to different contexts.  The batched form of the per-batch
+ * ComputeDigest calls the batcher makes (SafeCRDTManager.cs:165-198 → DAGUpdateMessage.cs:25-30). */
+int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const uint64_t* n_updates, const uint64_t* const* first,
+                            uint8_t* const* digest);
 /* SHA256.HashData of every payload of a device-resident wave (the per-message hashes ComputeDigest takes,
  * DAGUpdateMessage.cs:43) into DEVICE memory d_out (wave count * 32 bytes, digest bytes), for a consumer
  * on the device; async != 0 returns once queued on the context's stream (jg_fence waits). */

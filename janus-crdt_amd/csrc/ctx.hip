@@ -89,6 +89,11 @@ int jg_open(int device, jg_ctx** out) {
             JG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             JG_HIP(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
             JG_HIP(hipEventCreateWithFlags(&c->copied, hipEventDisableTiming));
+            JG_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            for (int s = 0; s < 2; ++s) {
+                JG_HIP(hipEventCreateWithFlags(&c->level1_done[s], hipEventDisableTiming));
+                JG_HIP(hipEventCreateWithFlags(&c->chain_free[s], hipEventDisableTiming));
+            }
             c->flags.alloc(256);
             JG_HIP(hipMemset(c->flags.p, 0, 256));
         } catch (...) {
@@ -105,6 +110,7 @@ int jg_close(jg_ctx* ctx) {
         jg::ensure_device(ctx);
         (void)hipStreamSynchronize(ctx->stream);
         if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
+        if (ctx->side) (void)hipStreamSynchronize(ctx->side);
         ctx->scratch.release();
         ctx->scratch2.release();
         ctx->scratch3.release();
@@ -112,6 +118,11 @@ int jg_close(jg_ctx* ctx) {
         (void)hipStreamDestroy(ctx->stream);
         if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
         if (ctx->copied) (void)hipEventDestroy(ctx->copied);
+        if (ctx->side) (void)hipStreamDestroy(ctx->side);
+        for (int s = 0; s < 2; ++s) {
+            if (ctx->level1_done[s]) (void)hipEventDestroy(ctx->level1_done[s]);
+            if (ctx->chain_free[s]) (void)hipEventDestroy(ctx->chain_free[s]);
+        }
         delete ctx;
     });
 }

@@ -288,16 +288,13 @@ void check_first(uint64_t n, uint64_t n_upd, const uint64_t* first) {
                (unsigned long long)first[n_upd], (unsigned long long)n);
 }
 
-// Both levels on device buffers already in place (d_bytes: payloads; d_off: n+1 offsets); results to host.
-void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, const uint8_t* d_null, uint64_t n, uint64_t n_upd,
-                 const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
-    std::vector<uint64_t> hb(2 * (n_upd + 1));  // first[] then boff[] (second-level block offsets)
-    uint64_t* boff = hb.data() + n_upd + 1;
-    std::memcpy(hb.data(), first, (n_upd + 1) * 8);
+// boff[u] = first second-level block of update u: 32 * count bytes rounded up to the ArrayPool bucket
+// (rent_length) plus the 72-byte SHA-256 tail, in 64-byte blocks.  Returns the total block count.
+uint64_t chain_offsets(const uint64_t* first, uint64_t n_upd, uint64_t* boff) {
     boff[0] = 0;
     for (uint64_t u = 0; u < n_upd; ++u) {
         const uint64_t c = first[u + 1] - first[u];
-        uint64_t L = c * 32;  // ArrayPool bucket length (rent_length)
+        uint64_t L = c * 32;
         if (c && L <= (1ull << 20)) {
             uint64_t p = 32;
             while (p < L) p <<= 1;
@@ -305,7 +302,17 @@ void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, con
         }
         boff[u + 1] = boff[u] + ((L + 72) >> 6);
     }
-    const uint64_t B = boff[n_upd];
+    return boff[n_upd];
+}
+
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+// Both levels on device buffers already in place (d_bytes: payloads; d_off: n+1 offsets); results to host.
+void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, const uint8_t* d_null, uint64_t n, uint64_t n_upd,
+                 const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
+    std::vector<uint64_t> hb(2 * (n_upd + 1));  // first[] then boff[] (second-level block offsets)
+    std::memcpy(hb.data(), first, (n_upd + 1) * 8);
+    const uint64_t B = chain_offsets(first, n_upd, hb.data() + n_upd + 1);
     char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, n * 32 + n_upd * 32 + hb.size() * 8 + B * 256 + 512));
     auto* D = reinterpret_cast<uint4*>(s);
     auto* out = reinterpret_cast<uint4*>(s + n * 32);
@@ -365,6 +372,73 @@ int jg_wave_update_digests(const jg_wave* w, uint64_t n_updates, const uint64_t*
         check_first(w->n, n_updates, first);
         jg::ensure_device(w->ctx);
         run_digests(w->ctx, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n, n_updates, first, msg_digest, digest);
+    });
+}
+
+int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const uint64_t* n_updates, const uint64_t* const* first,
+                            uint8_t* const* digest) {
+    return jg::guard([&] {
+        JG_REQUIRE(n_waves == 0 || (waves && n_updates && first && digest), JG_EINVAL, "jg_waves_update_digests: NULL argument");
+        if (n_waves == 0) return;
+        jg_ctx* ctx = waves[0] ? waves[0]->ctx : nullptr;
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, streams)
+        JG_REQUIRE(ctx, JG_EINVAL, "jg_waves_update_digests: wave 0 is NULL");
+        // host metadata of every wave, [first (nu+1) | boff (nu+1)] back to back, uploaded once; the
+        // digests of every wave land in one device array (one D2H at the end, no pageable copy inside the
+        // pipeline that would block the host until the chain before it finished)
+        std::vector<uint64_t> moff(n_waves + 1, 0), ooff(n_waves + 1, 0), blocks(n_waves);
+        for (uint64_t k = 0; k < n_waves; ++k) {
+            const jg_wave* w = waves[k];
+            const uint64_t nu = n_updates[k];
+            JG_REQUIRE(w && w->ctx == ctx, JG_EINVAL, "jg_waves_update_digests: wave %llu is NULL or on another context", (unsigned long long)k);
+            JG_REQUIRE(first[k] && (digest[k] || nu == 0), JG_EINVAL, "jg_waves_update_digests: NULL first/digest for wave %llu",
+                       (unsigned long long)k);
+            check_first(w->n, nu, first[k]);
+            moff[k + 1] = moff[k] + 2 * (nu + 1);
+            ooff[k + 1] = ooff[k] + nu * 32;
+        }
+        std::vector<uint64_t> hm(moff[n_waves]);
+        uint64_t slot = 0;  // one slot: first-level digests D then the second level's KW blocks
+        for (uint64_t k = 0; k < n_waves; ++k) {
+            const uint64_t nu = n_updates[k];
+            std::memcpy(&hm[moff[k]], first[k], (nu + 1) * 8);
+            blocks[k] = chain_offsets(first[k], nu, &hm[moff[k] + nu + 1]);
+            slot = std::max(slot, align256(waves[k]->n * 32) + blocks[k] * 256);
+        }
+        slot = align256(slot);
+        const uint64_t m_bytes = align256(hm.size() * 8), o_bytes = align256(ooff[n_waves]);
+        jg::ensure_device(ctx);
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, m_bytes + o_bytes + 2 * slot + 256));
+        auto* d_meta = reinterpret_cast<uint64_t*>(s);
+        char* d_out = s + m_bytes;
+        hipStream_t st = ctx->stream, sd = ctx->side;
+        JG_HIP(hipMemcpyAsync(d_meta, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
+        // wave k: first level + schedules on `stream` into slot k&1 (after wave k-2's chain released it),
+        // its chain on `side`; wave k+1's first level overlaps wave k's chain
+        for (uint64_t k = 0; k < n_waves; ++k) {
+            const jg_wave* w = waves[k];
+            const uint64_t nu = n_updates[k];
+            const int sl = (int)(k & 1);
+            char* base = s + m_bytes + o_bytes + sl * slot;
+            auto* D = reinterpret_cast<uint4*>(base);
+            auto* KW = reinterpret_cast<uint4*>(base + align256(w->n * 32));
+            const uint64_t* d_first = d_meta + moff[k];
+            const uint64_t* d_boff = d_first + nu + 1;
+            if (k >= 2) JG_HIP(hipStreamWaitEvent(st, ctx->chain_free[sl], 0));
+            if (w->n) k_sha_msgs<false><<<grid_for(w->n), kBlock, 0, st>>>(w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n, D);
+            if (nu) k_sha_expand<<<grid_for(blocks[k]), kBlock, 0, st>>>(D, d_first, d_boff, nu, KW);
+            JG_HIP(hipEventRecord(ctx->level1_done[sl], st));
+            JG_HIP(hipStreamWaitEvent(sd, ctx->level1_done[sl], 0));
+            if (nu) k_sha_chain<<<grid_for(nu), kBlock, 0, sd>>>(KW, d_boff, nu, reinterpret_cast<uint4*>(d_out + ooff[k]));
+            JG_HIP(hipEventRecord(ctx->chain_free[sl], sd));
+        }
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipStreamWaitEvent(st, ctx->chain_free[(n_waves - 1) & 1], 0));  // the last chain (side is in order)
+        std::vector<uint8_t> out(ooff[n_waves]);
+        if (!out.empty()) JG_HIP(hipMemcpyAsync(out.data(), d_out, out.size(), hipMemcpyDeviceToHost, st));
+        JG_HIP(hipStreamSynchronize(st));
+        for (uint64_t k = 0; k < n_waves; ++k)
+            if (n_updates[k]) std::memcpy(digest[k], out.data() + ooff[k], n_updates[k] * 32);
     });
 }
 

@@ -35,7 +35,7 @@ EXPORTS = [
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
-    "jg_update_digests", "jg_wave_update_digests", "jg_wave_sha256",
+    "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -80,6 +80,7 @@ _SIGS = {
     "jg_wave_destroy": ([_vp], C.c_int),
     "jg_update_digests": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_wave_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_waves_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_wave_sha256": ([_vp, _vp, C.c_uint8], C.c_int),
     "jg_wave_upload": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
@@ -388,6 +389,23 @@ class Wave:
         if self._h:
             _check(load().jg_wave_destroy(self._h))
             self._h = _vp()
+
+
+def waves_update_digests(waves, firsts):
+    """UpdateMessage.ComputeDigest over several device-resident waves in one pipelined call
+    (jg_waves_update_digests): wave k's UpdateMessages are firsts[k] (as in Wave.update_digests).
+    Returns one u8[n_updates_k, 32] array per wave."""
+    firsts = [_arr(f, np.uint64) for f in firsts]
+    n = len(waves)
+    if len(firsts) != n:
+        raise ValueError("waves_update_digests: one first[] per wave")
+    nu = np.array([f.size - 1 for f in firsts], np.uint64)
+    digs = [np.zeros((int(k), 32), np.uint8) for k in nu]
+    hw = (_vp * max(n, 1))(*[w._h for w in waves])
+    fp = (_vp * max(n, 1))(*[_vp(f.ctypes.data) for f in firsts])
+    dp = (_vp * max(n, 1))(*[_vp(d.ctypes.data) for d in digs])
+    _check(load().jg_waves_update_digests(hw, n, _ptr(nu), fp, dp))
+    return digs
 
 
 def update_digests(ctx: Context, msgs, first, msg_digests: bool = False):

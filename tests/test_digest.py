@@ -212,3 +212,38 @@ def test_gpu_full_wave_sampled(ctx):
         assert d[u].tobytes() == py_digest([msg(i) for i in range(u * per, (u + 1) * per)])
     for i in rng.integers(0, n, 2000):
         assert md[i].tobytes() == hashlib.sha256(msg(i)).digest()
+
+
+@pytest.mark.gpu
+def test_gpu_waves_pipelined(ctx):
+    # jg_waves_update_digests: five waves of different sizes and UpdateMessage splits in one pipelined
+    # call (wave k+1's first level beside wave k's chain; slots reused from wave 2 on), one wave listed
+    # twice, one with no UpdateMessages and one with empty UpdateMessages: byte for byte vs hashlib and
+    # vs the single-wave call
+    import janus_gpu as jg
+    rng = np.random.default_rng(9)
+    sizes = [3000, 1, 2500, 4000, 700]
+    msgs = [random_msgs(rng, n, 0, 600) for n in sizes]
+    firsts = [np.array([0, 1000, 1000, 2999, 3000]), np.array([0, 1]), np.array([0, 2500]),
+              np.arange(0, 4001, 100), np.array([0, 0, 700, 700])]
+    waves = []
+    try:
+        for m in msgs:
+            w = jg.Wave(ctx, len(m), max(1, sum(map(len, m))))
+            w.upload(np.zeros(len(m), np.uint32), msgs=m)
+            waves.append(w)
+        order = [0, 1, 2, 3, 4, 0]
+        got = jg.waves_update_digests([waves[k] for k in order], [firsts[k] for k in order])
+        single = [waves[k].update_digests(firsts[k]) for k in range(len(waves))]
+        assert jg.waves_update_digests([], []) == []
+        assert jg.waves_update_digests([waves[1]], [np.array([0])])[0].shape == (0, 32)
+        with pytest.raises(jg.JanusError):
+            jg.waves_update_digests([waves[0], waves[1]], [firsts[0], np.array([0, 2])])  # first[-1] != count
+    finally:
+        for w in waves:
+            w.close()
+    for j, k in enumerate(order):
+        f = firsts[k]
+        assert np.array_equal(got[j], single[k])
+        for u in range(f.size - 1):
+            assert got[j][u].tobytes() == py_digest(msgs[k][int(f[u]):int(f[u + 1])])
