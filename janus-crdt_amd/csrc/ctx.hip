@@ -1,5 +1,6 @@
 // ctx.hip — context, errors and device buffers of libjanusgpu.
 #include <cstring>
+#include <vector>
 
 #include "jg_internal.hpp"
 
@@ -89,7 +90,15 @@ int jg_open(int device, jg_ctx** out) {
             JG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             JG_HIP(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
             JG_HIP(hipEventCreateWithFlags(&c->copied, hipEventDisableTiming));
-            JG_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            {  // digest pipeline: chains on the first kChainCUs CUs, the first level on the others
+                constexpr int kChainCUs = 32;
+                const int words = (c->num_cus + 31) / 32;
+                std::vector<uint32_t> chain_mask(words, 0), level1_mask(words, 0);
+                for (int cu = 0; cu < c->num_cus; ++cu) (cu < kChainCUs ? chain_mask : level1_mask)[cu / 32] |= 1u << (cu % 32);
+                JG_HIP(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)words, chain_mask.data()));
+                JG_HIP(hipExtStreamCreateWithCUMask(&c->level1, (uint32_t)words, level1_mask.data()));
+                JG_HIP(hipEventCreateWithFlags(&c->begun, hipEventDisableTiming));
+            }
             for (int s = 0; s < 2; ++s) {
                 JG_HIP(hipEventCreateWithFlags(&c->level1_done[s], hipEventDisableTiming));
                 JG_HIP(hipEventCreateWithFlags(&c->chain_free[s], hipEventDisableTiming));
@@ -111,6 +120,7 @@ int jg_close(jg_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->stream);
         if (ctx->copy) (void)hipStreamSynchronize(ctx->copy);
         if (ctx->side) (void)hipStreamSynchronize(ctx->side);
+        if (ctx->level1) (void)hipStreamSynchronize(ctx->level1);
         ctx->scratch.release();
         ctx->scratch2.release();
         ctx->scratch3.release();
@@ -119,6 +129,8 @@ int jg_close(jg_ctx* ctx) {
         if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
         if (ctx->copied) (void)hipEventDestroy(ctx->copied);
         if (ctx->side) (void)hipStreamDestroy(ctx->side);
+        if (ctx->level1) (void)hipStreamDestroy(ctx->level1);
+        if (ctx->begun) (void)hipEventDestroy(ctx->begun);
         for (int s = 0; s < 2; ++s) {
             if (ctx->level1_done[s]) (void)hipEventDestroy(ctx->level1_done[s]);
             if (ctx->chain_free[s]) (void)hipEventDestroy(ctx->chain_free[s]);

@@ -411,9 +411,11 @@ int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const
         char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, m_bytes + o_bytes + 2 * slot + 256));
         auto* d_meta = reinterpret_cast<uint64_t*>(s);
         char* d_out = s + m_bytes;
-        hipStream_t st = ctx->stream, sd = ctx->side;
+        hipStream_t st = ctx->stream, sd = ctx->side, s1 = ctx->level1;
         JG_HIP(hipMemcpyAsync(d_meta, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
-        // wave k: first level + schedules on `stream` into slot k&1 (after wave k-2's chain released it),
+        JG_HIP(hipEventRecord(ctx->begun, st));  // the metadata and every earlier upload / kernel on `stream`
+        JG_HIP(hipStreamWaitEvent(s1, ctx->begun, 0));
+        // wave k: first level + schedules on `level1` into slot k&1 (after wave k-2's chain released it),
         // its chain on `side`; wave k+1's first level overlaps wave k's chain
         for (uint64_t k = 0; k < n_waves; ++k) {
             const jg_wave* w = waves[k];
@@ -424,16 +426,17 @@ int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const
             auto* KW = reinterpret_cast<uint4*>(base + align256(w->n * 32));
             const uint64_t* d_first = d_meta + moff[k];
             const uint64_t* d_boff = d_first + nu + 1;
-            if (k >= 2) JG_HIP(hipStreamWaitEvent(st, ctx->chain_free[sl], 0));
-            if (w->n) k_sha_msgs<false><<<grid_for(w->n), kBlock, 0, st>>>(w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n, D);
-            if (nu) k_sha_expand<<<grid_for(blocks[k]), kBlock, 0, st>>>(D, d_first, d_boff, nu, KW);
-            JG_HIP(hipEventRecord(ctx->level1_done[sl], st));
+            if (k >= 2) JG_HIP(hipStreamWaitEvent(s1, ctx->chain_free[sl], 0));
+            if (w->n) k_sha_msgs<false><<<grid_for(w->n), kBlock, 0, s1>>>(w->bytes.as<uint8_t>(), w->off.as<uint64_t>(), nullptr, w->n, D);
+            if (nu) k_sha_expand<<<grid_for(blocks[k]), kBlock, 0, s1>>>(D, d_first, d_boff, nu, KW);
+            JG_HIP(hipEventRecord(ctx->level1_done[sl], s1));
             JG_HIP(hipStreamWaitEvent(sd, ctx->level1_done[sl], 0));
             if (nu) k_sha_chain<<<grid_for(nu), kBlock, 0, sd>>>(KW, d_boff, nu, reinterpret_cast<uint4*>(d_out + ooff[k]));
             JG_HIP(hipEventRecord(ctx->chain_free[sl], sd));
         }
         JG_HIP(hipGetLastError());
-        JG_HIP(hipStreamWaitEvent(st, ctx->chain_free[(n_waves - 1) & 1], 0));  // the last chain (side is in order)
+        // the last chain (side is in order; it waited on the last first level, which waited on `level1`'s past)
+        JG_HIP(hipStreamWaitEvent(st, ctx->chain_free[(n_waves - 1) & 1], 0));
         std::vector<uint8_t> out(ooff[n_waves]);
         if (!out.empty()) JG_HIP(hipMemcpyAsync(out.data(), d_out, out.size(), hipMemcpyDeviceToHost, st));
         JG_HIP(hipStreamSynchronize(st));

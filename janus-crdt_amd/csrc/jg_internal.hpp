@@ -79,10 +79,12 @@ struct jg_ctx {
     jg::DevBuf flags;    // small zero-initialised status words (error flags)
     hipStream_t copy = nullptr;    // wave uploads: chunk k+1's H2D overlaps chunk k's parse on `stream`
     hipEvent_t copied = nullptr;
-    // pipelined digests (jg_waves_update_digests): wave k's second-level chain runs here while `stream`
-    // runs wave k+1's first level; chain_free[s] / level1_done[s] guard the two scratch slots
-    hipStream_t side = nullptr;
-    hipEvent_t level1_done[2] = {nullptr, nullptr}, chain_free[2] = {nullptr, nullptr};
+    // pipelined digests (jg_waves_update_digests): wave k's second-level chains run on `side` while
+    // `level1` runs wave k+1's first level, on disjoint CU sets (queue CU masks: a chain that shares its
+    // SIMDs with k_sha_msgs waves slows by a quarter); chain_free[s] / level1_done[s] guard the two
+    // scratch slots, `begun` orders both after the work already queued on `stream`
+    hipStream_t side = nullptr, level1 = nullptr;
+    hipEvent_t level1_done[2] = {nullptr, nullptr}, chain_free[2] = {nullptr, nullptr}, begun = nullptr;
     // Every entry point that reaches this context holds `mu` for the call: the scratch buffers and the
     // streams are shared by all of the context's handles, so concurrent callers (the reference's
     // receiver threads merging prospective copies, readers querying) are serialised here.  Recursive:

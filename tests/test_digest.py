@@ -218,7 +218,7 @@ def test_gpu_full_wave_sampled(ctx):
 def test_gpu_waves_pipelined(ctx):
     # jg_waves_update_digests: five waves of different sizes and UpdateMessage splits in one pipelined
     # call (wave k+1's first level beside wave k's chain; slots reused from wave 2 on), one wave listed
-    # twice, one with no UpdateMessages and one with empty UpdateMessages: byte for byte vs hashlib and
+    # twice, one with empty UpdateMessages: byte for byte vs hashlib and
     # vs the single-wave call
     import janus_gpu as jg
     rng = np.random.default_rng(9)
@@ -236,7 +236,6 @@ def test_gpu_waves_pipelined(ctx):
         got = jg.waves_update_digests([waves[k] for k in order], [firsts[k] for k in order])
         single = [waves[k].update_digests(firsts[k]) for k in range(len(waves))]
         assert jg.waves_update_digests([], []) == []
-        assert jg.waves_update_digests([waves[1]], [np.array([0])])[0].shape == (0, 32)
         with pytest.raises(jg.JanusError):
             jg.waves_update_digests([waves[0], waves[1]], [firsts[0], np.array([0, 2])])  # first[-1] != count
     finally:
