@@ -95,8 +95,17 @@ int jg_open(int device, jg_ctx** out) {
                 const int words = (c->num_cus + 31) / 32;
                 std::vector<uint32_t> chain_mask(words, 0), level1_mask(words, 0);
                 for (int cu = 0; cu < c->num_cus; ++cu) (cu < kChainCUs ? chain_mask : level1_mask)[cu / 32] |= 1u << (cu % 32);
-                JG_HIP(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)words, chain_mask.data()));
-                JG_HIP(hipExtStreamCreateWithCUMask(&c->level1, (uint32_t)words, level1_mask.data()));
+                // a queue that refuses a CU mask still runs the pipeline, only with shared SIMDs
+                if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)words, chain_mask.data()) != hipSuccess) {
+                    (void)hipGetLastError();
+                    c->side = nullptr;
+                    JG_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                }
+                if (hipExtStreamCreateWithCUMask(&c->level1, (uint32_t)words, level1_mask.data()) != hipSuccess) {
+                    (void)hipGetLastError();
+                    c->level1 = nullptr;
+                    JG_HIP(hipStreamCreateWithFlags(&c->level1, hipStreamNonBlocking));
+                }
                 JG_HIP(hipEventCreateWithFlags(&c->begun, hipEventDisableTiming));
             }
             for (int s = 0; s < 2; ++s) {
