@@ -258,7 +258,7 @@ __device__ __forceinline__ void load_kw(uint4 dst[16], const uint4* __restrict__
 // block compresses), which keeps the chain on its VALU dependency path instead of the load latency.
 __global__ void __launch_bounds__(kBlock) k_sha_chain(const uint4* __restrict__ KW, const uint64_t* __restrict__ boff, uint64_t n_upd,
                                                       uint4* __restrict__ out) {
-    const uint64_t u = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= n_upd) return;
     const uint64_t b0 = boff[u], b1 = boff[u + 1];
     uint32_t H[8];
@@ -279,6 +279,9 @@ __global__ void __launch_bounds__(kBlock) k_sha_chain(const uint4* __restrict__ 
 }
 
 uint32_t grid_for(uint64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
+// k_sha_chain: one wave per workgroup, so the few chain waves spread over as many CUs as there are waves
+constexpr uint32_t kChainBlock = 64;
+uint32_t chain_grid(uint64_t n) { return (uint32_t)((n + kChainBlock - 1) / kChainBlock); }
 
 void check_first(uint64_t n, uint64_t n_upd, const uint64_t* first) {
     JG_REQUIRE(first[0] == 0, JG_EINVAL, "update digests: first[0] must be 0");
@@ -324,7 +327,7 @@ void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, con
     if (n) k_sha_msgs<false><<<grid_for(n), kBlock, 0, st>>>(d_bytes, d_off, d_null, n, D);
     if (n_upd) {
         k_sha_expand<<<grid_for(B), kBlock, 0, st>>>(D, d_first, d_boff, n_upd, KW);
-        k_sha_chain<<<grid_for(n_upd), kBlock, 0, st>>>(KW, d_boff, n_upd, out);
+        k_sha_chain<<<chain_grid(n_upd), kChainBlock, 0, st>>>(KW, d_boff, n_upd, out);
     }
     JG_HIP(hipGetLastError());
     if (digest && n_upd) JG_HIP(hipMemcpyAsync(digest, out, n_upd * 32, hipMemcpyDeviceToHost, st));
@@ -431,7 +434,7 @@ int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const
             if (nu) k_sha_expand<<<grid_for(blocks[k]), kBlock, 0, s1>>>(D, d_first, d_boff, nu, KW);
             JG_HIP(hipEventRecord(ctx->level1_done[sl], s1));
             JG_HIP(hipStreamWaitEvent(sd, ctx->level1_done[sl], 0));
-            if (nu) k_sha_chain<<<grid_for(nu), kBlock, 0, sd>>>(KW, d_boff, nu, reinterpret_cast<uint4*>(d_out + ooff[k]));
+            if (nu) k_sha_chain<<<chain_grid(nu), kChainBlock, 0, sd>>>(KW, d_boff, nu, reinterpret_cast<uint4*>(d_out + ooff[k]));
             JG_HIP(hipEventRecord(ctx->chain_free[sl], sd));
         }
         JG_HIP(hipGetLastError());
