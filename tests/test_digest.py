@@ -246,3 +246,10 @@ def test_gpu_waves_pipelined(ctx):
         assert np.array_equal(got[j], single[k])
         for u in range(f.size - 1):
             assert got[j][u].tobytes() == py_digest(msgs[k][int(f[u]):int(f[u + 1])])
+
+
+def test_waves_update_digests_argument_check():
+    # host-side check of the pipelined binding: one first[] per wave (raised before the library is called)
+    import janus_gpu as jg
+    with pytest.raises(ValueError):
+        jg.waves_update_digests([object(), object()], [np.array([0])])
