@@ -322,9 +322,12 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
     import numpy as np
     data, off = digest_wave(DIGEST_MSGS, SEED + 31 + rank)
     first = np.arange(0, DIGEST_MSGS + 1, DIGEST_PER_UPDATE, dtype=np.uint64)
+    data2, off2 = digest_wave(DIGEST_MSGS, SEED + 97 + rank)  # a second, distinct resident wave (pipelined leg)
     w = jg.Wave(ctx, DIGEST_MSGS, data.size)
+    w2 = jg.Wave(ctx, DIGEST_MSGS, data2.size)
     try:
         w.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data, off=off)
+        w2.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data2, off=off2)
         wall, ev = timed(ctx, sync, lambda: w.update_digests(first), steps, warmup)
         # the first level alone (k_sha_msgs, digest bytes into device memory: jg_wave_sha256)
         import torch
@@ -332,10 +335,13 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
         wall1, ev1 = timed(ctx, sync, lambda: w.sha256_device(dout.data_ptr(), async_=True), steps, warmup)
         del dout
         # pipelined: DIGEST_PIPE waves in one jg_waves_update_digests call (wave k's chains on the
-        # context's second stream beside wave k+1's first level); the same resident wave listed each time
-        wall_p, ev_p = timed(ctx, sync, lambda: jg.waves_update_digests([w] * DIGEST_PIPE, [first] * DIGEST_PIPE), steps, warmup)
+        # context's second stream beside wave k+1's first level); two distinct resident waves alternate, so
+        # wave k+1's first level does not re-read the bytes wave k just streamed through the caches
+        pipe = [w, w2] * (DIGEST_PIPE // 2)
+        wall_p, ev_p = timed(ctx, sync, lambda: jg.waves_update_digests(pipe, [first] * DIGEST_PIPE), steps, warmup)
     finally:
         w.close()
+        w2.close()
     blocks = int(((off[1:] - off[:-1] + 72) // 64).sum())
     kern, kern1 = ev / steps, ev1 / steps
     chain = int((32 * DIGEST_PER_UPDATE + 72) // 64) if DIGEST_PER_UPDATE <= 32768 else None

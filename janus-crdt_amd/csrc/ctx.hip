@@ -53,7 +53,9 @@ void upload_done(jg_ctx* ctx) {
 
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes) {
     if (b.bytes < bytes) {
-        JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block may still be in use
+        JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block may still be in use, also by the digest
+        if (ctx->side) JG_HIP(hipStreamSynchronize(ctx->side));      // pipeline's streams (scratch3)
+        if (ctx->level1) JG_HIP(hipStreamSynchronize(ctx->level1));
         b.alloc(bytes + bytes / 4);
     }
     return b.p;
@@ -90,22 +92,32 @@ int jg_open(int device, jg_ctx** out) {
             JG_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             JG_HIP(hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking));
             JG_HIP(hipEventCreateWithFlags(&c->copied, hipEventDisableTiming));
-            {  // digest pipeline: chains on the first kChainCUs CUs, the first level on the others
-                constexpr int kChainCUs = 32;
+            {  // digest pipeline: chains on the first num_cus/8 CUs, the first level on the others.  The
+               // split needs both sets non-empty and the first level the larger one; a small device or
+               // partition (a CPX partition has 32 CUs) gets plain streams that share every CU.  CU-masked
+               // queues are created blocking (hipStreamDefault) — no library path uses the null stream,
+               // so that only orders them against other null-stream work of the process.
+                const int chain_cus = c->num_cus / 8;
                 const int words = (c->num_cus + 31) / 32;
-                std::vector<uint32_t> chain_mask(words, 0), level1_mask(words, 0);
-                for (int cu = 0; cu < c->num_cus; ++cu) (cu < kChainCUs ? chain_mask : level1_mask)[cu / 32] |= 1u << (cu % 32);
-                // a queue that refuses a CU mask still runs the pipeline, only with shared SIMDs
-                if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)words, chain_mask.data()) != hipSuccess) {
-                    (void)hipGetLastError();
-                    c->side = nullptr;
-                    JG_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+                bool masked = chain_cus >= 1 && c->num_cus - chain_cus >= 4 * chain_cus;
+                if (masked) {
+                    std::vector<uint32_t> chain_mask(words, 0), level1_mask(words, 0);
+                    for (int cu = 0; cu < c->num_cus; ++cu) (cu < chain_cus ? chain_mask : level1_mask)[cu / 32] |= 1u << (cu % 32);
+                    // a queue that refuses a CU mask still runs the pipeline, only with shared SIMDs
+                    if (hipExtStreamCreateWithCUMask(&c->side, (uint32_t)words, chain_mask.data()) != hipSuccess ||
+                        hipExtStreamCreateWithCUMask(&c->level1, (uint32_t)words, level1_mask.data()) != hipSuccess) {
+                        (void)hipGetLastError();
+                        if (c->side) (void)hipStreamDestroy(c->side);
+                        if (c->level1) (void)hipStreamDestroy(c->level1);
+                        c->side = c->level1 = nullptr;
+                        masked = false;
+                    }
                 }
-                if (hipExtStreamCreateWithCUMask(&c->level1, (uint32_t)words, level1_mask.data()) != hipSuccess) {
-                    (void)hipGetLastError();
-                    c->level1 = nullptr;
+                if (!masked) {
+                    JG_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
                     JG_HIP(hipStreamCreateWithFlags(&c->level1, hipStreamNonBlocking));
                 }
+                c->cu_masked = masked;
                 JG_HIP(hipEventCreateWithFlags(&c->begun, hipEventDisableTiming));
             }
             for (int s = 0; s < 2; ++s) {

@@ -415,6 +415,18 @@ int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const
         auto* d_meta = reinterpret_cast<uint64_t*>(s);
         char* d_out = s + m_bytes;
         hipStream_t st = ctx->stream, sd = ctx->side, s1 = ctx->level1;
+        // a failure below leaves work queued on `side` / `level1` writing the scratch slots: drain both
+        // before the error leaves the call (the next user of scratch3 orders itself on `stream` only)
+        struct Drain {
+            hipStream_t a, b;
+            bool armed = true;
+            ~Drain() {
+                if (!armed) return;
+                (void)hipStreamSynchronize(a);
+                (void)hipStreamSynchronize(b);
+                (void)hipGetLastError();
+            }
+        } drain{sd, s1};
         JG_HIP(hipMemcpyAsync(d_meta, hm.data(), hm.size() * 8, hipMemcpyHostToDevice, st));
         JG_HIP(hipEventRecord(ctx->begun, st));  // the metadata and every earlier upload / kernel on `stream`
         JG_HIP(hipStreamWaitEvent(s1, ctx->begun, 0));
@@ -443,6 +455,7 @@ int jg_waves_update_digests(const jg_wave* const* waves, uint64_t n_waves, const
         std::vector<uint8_t> out(ooff[n_waves]);
         if (!out.empty()) JG_HIP(hipMemcpyAsync(out.data(), d_out, out.size(), hipMemcpyDeviceToHost, st));
         JG_HIP(hipStreamSynchronize(st));
+        drain.armed = false;  // `stream` waited on the last chain, which waited on every earlier launch
         for (uint64_t k = 0; k < n_waves; ++k)
             if (n_updates[k]) std::memcpy(digest[k], out.data() + ooff[k], n_updates[k] * 32);
     });

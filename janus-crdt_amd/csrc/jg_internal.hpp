@@ -84,6 +84,7 @@ struct jg_ctx {
     // SIMDs with k_sha_msgs waves slows by a quarter); chain_free[s] / level1_done[s] guard the two
     // scratch slots, `begun` orders both after the work already queued on `stream`
     hipStream_t side = nullptr, level1 = nullptr;
+    bool cu_masked = false;  // side / level1 hold disjoint CU sets (false: plain streams sharing every CU)
     hipEvent_t level1_done[2] = {nullptr, nullptr}, chain_free[2] = {nullptr, nullptr}, begun = nullptr;
     // Every entry point that reaches this context holds `mu` for the call: the scratch buffers and the
     // streams are shared by all of the context's handles, so concurrent callers (the reference's

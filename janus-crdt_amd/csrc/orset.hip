@@ -28,7 +28,7 @@
 
 namespace {
 
-// Tile shape chosen by measurement (tools/tune_orset_lookback.hip; profiles/r01/tune_orset_*.txt):
+// Tile shape chosen by measurement (tools/tune_orset.hip; profiles/r01/tune_orset_*.txt):
 // 512 x 6 = 3072 records per tile, 74 KB LDS, 2 workgroups per CU.
 constexpr int kOB = 512;   // threads per workgroup
 constexpr int kItems = 6;  // records per thread per tile

@@ -4,7 +4,7 @@
 // C slots: chunk c holds ranks [off[c], off[c+1]) in slots [c*C, c*C + cnt[c]).  A union tile writes
 // its output straight into its own chunk, so no workgroup ever waits on another: the contiguous
 // layout needed a decoupled look-back that measured 32-36 % of every tile and 57 % more kernel time
-// (tools/tune_orset_lookback.hip).  Readers translate rank -> slot with a lookup table:
+// (the look-back tool was removed in round 2; DESIGN.md §4 keeps its numbers).  Readers translate rank -> slot with a lookup table:
 // lut[q] = the last chunk starting at or before rank q * 512, so the chunk of rank r lies in
 // [lut[r >> 9], lut[(r >> 9) + 1]] — usually one candidate, a short binary search when a Clear left
 // empty chunks behind.

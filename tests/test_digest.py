@@ -248,6 +248,36 @@ def test_gpu_waves_pipelined(ctx):
             assert got[j][u].tobytes() == py_digest(msgs[k][int(f[u]):int(f[u + 1])])
 
 
+@pytest.mark.gpu
+def test_gpu_waves_pipelined_large(ctx):
+    # Four large distinct waves (200k payloads, 200 UpdateMessages each) in one pipelined call: the kernels
+    # run long enough that wave k+2's first level overwrites the slot wave k's chain may still read unless
+    # the chain_free / level1_done events order them.  Each wave's digests equal its single-wave call.
+    import janus_gpu as jg
+    rng = np.random.default_rng(77)
+    n, per = 200_000, 1000
+    first = np.arange(0, n + 1, per, dtype=np.uint64)
+    waves, single = [], []
+    try:
+        for k in range(4):
+            lens = rng.integers(300, 420, n).astype(np.uint64)
+            off = np.zeros(n + 1, np.uint64)
+            off[1:] = np.cumsum(lens)
+            data = rng.integers(32, 127, int(off[-1]), dtype=np.uint8)
+            w = jg.Wave(ctx, n, data.size)
+            w.upload(np.zeros(n, np.uint32), data=data, off=off)
+            waves.append(w)
+            single.append(w.update_digests(first))
+        order = [0, 1, 2, 3, 1, 0]
+        got = jg.waves_update_digests([waves[k] for k in order], [first] * len(order))
+    finally:
+        for w in waves:
+            w.close()
+    for j, k in enumerate(order):
+        assert np.array_equal(got[j], single[k]), f"pipelined wave {j} (wave {k}) differs from its single-wave digests"
+    assert not np.array_equal(single[0], single[1])
+
+
 def test_waves_update_digests_argument_check():
     # host-side check of the pipelined binding: one first[] per wave (raised before the library is called)
     import janus_gpu as jg
