@@ -35,7 +35,7 @@ PNC_BYTES_PER_CELL = 6 * PNC_EB  # read A.P A.N B.P B.N, write A.P A.N
 
 ORSET_GROUPS, ORSET_E = 10_000_000, 10          # 1M sets x 10 elems
 ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV = 10, 5, 2, 1
-REC_BYTES = 24
+REC_BYTES = 28  # OR-Set record in HBM: key 8 B + tag 16 B + arrival ordinal 4 B (jg_tagrec.ord)
 
 
 def shard_keys(total_keys: int, rank: int, world: int) -> tuple[int, int]:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 1
+#define JG_ABI_VERSION 2
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -49,11 +49,20 @@ typedef struct jg_orset jg_orset; /* OR-Set store: sorted add and tombstone tag 
 
 /* One OR-Set tag record: key = (uint64_t)set << 32 | elem, tag = 16 opaque bytes (a C# Guid:
  * tag_lo = bytes 0..7, tag_hi = bytes 8..15, little-endian).  Streams are sorted strictly
- * increasing by (key, tag_lo, tag_hi), unsigned.  24 bytes, 8-byte aligned. */
+ * increasing by (key, tag_lo, tag_hi), unsigned.
+ * ord = the record's ARRIVAL ORDINAL, which carries the reference's enumeration order: a HashSet<Guid>
+ * enumerates in first-insertion order (ORSet.cs:138-149 Add, :165/178/259/272/281 UnionWith, :182/263/276
+ * the copy constructor; nothing removes a single tag), so the tags of one (set, elem) in one stream
+ * enumerate in ascending (ord, tag_lo, tag_hi), and a removeSet Dictionary enumerates its elements in
+ * ascending (min ord of the element's tombstones, elem) — the element's first insertion.  The addSet
+ * Dictionary enumerates in ascending elem id (ids are interned at first insertion).  Only the relative
+ * order of ords within one stream of one set is meaningful: the engine renumbers them (order kept) and
+ * returns its own values; input ords must be < 2^32.  32 bytes, 8-byte aligned. */
 typedef struct jg_tagrec {
     uint64_t key;
     uint64_t tag_lo;
     uint64_t tag_hi;
+    uint64_t ord;
 } jg_tagrec;
 
 /* ---------------------------------------------------------------------------------------------
@@ -261,13 +270,14 @@ int jg_rows_route(const jg_rows* rows, uint32_t world, uint64_t* counts, void* d
  * may repeat; all or nothing (JG_EINVAL if any key >= n_keys, nothing merged). */
 int jg_pnc_merge_device(jg_pnc* pnc, uint64_t n_rows, const void* d_keys, const void* d_P, const void* d_N);
 /* Stable partition of both record streams of a store by owner rank (set id % world; set ids
- * rewritten to set / world): keys (8 B) and tags (16 B, jg_tagrec order) per stream. */
+ * rewritten to set / world): keys (8 B), tags (16 B, jg_tagrec order) and ords (uint32_t) per stream. */
 int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* rem_counts, void* d_add_key, void* d_add_tag,
-                   uint64_t cap_add, void* d_rem_key, void* d_rem_tag, uint64_t cap_rem);
+                   void* d_add_ord, uint64_t cap_add, void* d_rem_key, void* d_rem_tag, void* d_rem_ord, uint64_t cap_rem);
 /* ORSet.Merge of n_runs received runs (run r = add_counts[r] adds and rem_counts[r] tombstones,
- * stored run after run; each sorted strictly increasing, JG_ESTATE otherwise) into the store. */
+ * stored run after run; each sorted strictly increasing, JG_ESTATE otherwise) into the store, in run
+ * order: run r is the r-th state merged (its ords order its own records, jg_tagrec.ord). */
 int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const void* d_add_key,
-                          const void* d_add_tag, const void* d_rem_key, const void* d_rem_tag);
+                          const void* d_add_tag, const void* d_add_ord, const void* d_rem_key, const void* d_rem_tag, const void* d_rem_ord);
 
 /* ---------------------------------------------------------------------------------------------
  * UpdateMessage digests (csrc/digest.hip) — replaces UpdateMessage.ComputeDigest

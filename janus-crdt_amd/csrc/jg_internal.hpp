@@ -129,11 +129,13 @@ struct jg_rows {
 };
 
 // One sorted tag-record stream in the CHUNKED layout (orset_union.hpp): structure of arrays
-// key[slot] (8 B) and tag[slot] (16 B); chunk c holds ranks [off[c], off[c+1]) in slots
-// [c*kChunk, c*kChunk + cnt[c]); lut[q] = the last chunk starting at or before rank q*512.
+// key[slot] (8 B), tag[slot] (16 B) and ord[slot] (4 B, the arrival ordinal: jg_tagrec.ord); chunk c
+// holds ranks [off[c], off[c+1]) in slots [c*kChunk, c*kChunk + cnt[c]); lut[q] = the last chunk
+// starting at or before rank q*512.
 constexpr uint32_t kChunk = 3072;  // = one union tile (orset.hip kOB * kItems)
 struct jg_stream_soa {
-    jg::DevBuf key, tag;  // cap_chunks * kChunk slots
+    jg::DevBuf key, tag, ord;  // cap_chunks * kChunk slots
+    uint64_t next = 0;         // every record's ord < next (host copy; a union's B records land at next + ord)
     jg::DevBuf cnt;       // uint32 [cap_chunks]
     jg::DevBuf off;       // uint64 [cap_chunks + 1]
     jg::DevBuf lut;       // uint32 [(cap_chunks * kChunk >> 9) + 2]
@@ -181,7 +183,10 @@ void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n);
 void pnc_merge_indexed(jg_pnc* p, const void* BP, const void* BN, const uint32_t* d_keys, uint64_t n_rows);
 // orset.hip: merge n_runs sorted, duplicate-free runs (device SoA, run after run) into the store.
 void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const unsigned long long* add_key,
-                      const uint4* add_tag, const unsigned long long* rem_key, const uint4* rem_tag);
+                      const uint4* add_tag, const uint32_t* add_ord, const unsigned long long* rem_key, const uint4* rem_tag,
+                      const uint32_t* rem_ord);
+// orset.hip: largest ord + 1 of n device ords (0 if n == 0), synchronous.
+uint64_t ord_span(jg_ctx* ctx, const uint32_t* ord, uint64_t n);
 // orset.hip: s = s ∪ src (both streams), synchronous, src's streams may be dense or chunked.
-void orset_merge_store(jg_orset* s, const jg_orset* src);
+void orset_merge_store(jg_orset* s, jg_orset* src);
 }  // namespace jg

@@ -17,7 +17,10 @@
 //   Roofline: HBM.  Reads 24 B per input record, writes 24 B per output record.
 // ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams
 // (rank space), then SetEquals of the two sorted runs.
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <set>
 #include <unordered_map>
@@ -43,7 +46,16 @@ using jgk::rec_lt;
 using jgk::View;
 
 View view(const jg_stream_soa& s) {
-    return View{s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.off.as<uint64_t>(), s.lut.as<uint32_t>(), s.n, s.nch, kChunk, s.dense ? 1u : 0u};
+    return View{s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.ord.as<uint32_t>(), s.off.as<uint64_t>(), s.lut.as<uint32_t>(), s.n, s.nch,
+                kChunk, s.dense ? 1u : 0u};
+}
+
+// Ords are 32-bit on the device: a union's output needs A.next + B.next below this (renumber() first
+// otherwise).  Tests lower it (JANUS_TEST_ORD_LIMIT) to exercise the renumbering.
+uint64_t ord_limit() {
+    const char* e = std::getenv("JANUS_TEST_ORD_LIMIT");
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v > 0 && v < 0xFFFFFFFFull ? v : 0xFFFFFFFFull;
 }
 
 // Strictly increasing check of a DENSE stream: err |= 1 at the first non-increasing neighbour pair.
@@ -54,14 +66,59 @@ __global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* 
     }
 }
 
-// Host AoS records -> dense SoA stream.
-__global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in, uint64_t n, unsigned long long* __restrict__ k,
-                                                uint4* __restrict__ t) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
-        const jg_tagrec r = in[i];
-        k[i] = r.key;
-        t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
+// Largest ord + 1 into span[0] (atomicMax per wave; span zeroed by the caller).
+__device__ __forceinline__ void wave_span(uint32_t mine, unsigned long long* span) {
+    unsigned long long v = (unsigned long long)mine + 1ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(v, d, 64);
+        v = o > v ? o : v;
     }
+    if ((threadIdx.x & 63) == 0 && v) atomicMax(span, v);
+}
+
+// Host AoS records -> dense SoA stream; err |= 2 for an ord >= 2^32, span[0] = largest ord + 1.
+__global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in, uint64_t n, unsigned long long* __restrict__ k,
+                                                uint4* __restrict__ t, uint32_t* __restrict__ o, unsigned* err, unsigned long long* span) {
+    const uint64_t stride = (uint64_t)gridDim.x * kOB;
+    const uint64_t n_pad = (n + stride - 1) / stride * stride;  // every lane of a wave reaches wave_span
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n_pad; i += stride) {
+        uint32_t mine = 0;
+        bool any = false;
+        if (i < n) {
+            const jg_tagrec r = in[i];
+            k[i] = r.key;
+            t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
+            if (r.ord > 0xFFFFFFFFull) atomicOr(err, 2u);
+            mine = (uint32_t)r.ord;
+            o[i] = mine;
+            any = true;
+        }
+        wave_span(any ? mine : 0u, span);
+    }
+}
+
+__global__ __launch_bounds__(kOB) void k_ord_span(const uint32_t* __restrict__ o, uint64_t n, unsigned long long* span) {
+    const uint64_t stride = (uint64_t)gridDim.x * kOB;
+    const uint64_t n_pad = (n + stride - 1) / stride * stride;
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n_pad; i += stride) wave_span(i < n ? o[i] : 0u, span);
+}
+
+// Renumbering (order kept): ranks -> (ord, rank) pairs, sorted by ord (stable: ties stay in rank =
+// (key, tag) order), then ord[slot of sorted[i].rank] = i.
+__global__ __launch_bounds__(kOB) void k_ord_by_rank(View v, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ ko, uint32_t* __restrict__ vr) {
+    const uint64_t slots = (uint64_t)v.nch * v.C;
+    for (uint64_t x = (uint64_t)blockIdx.x * kOB + threadIdx.x; x < slots; x += (uint64_t)gridDim.x * kOB) {
+        const uint64_t c = x / v.C, j = x - c * v.C;
+        if (j < cnt[c]) {
+            const uint64_t r = v.off[c] + j;
+            ko[r] = v.ord[x];
+            vr[r] = (uint32_t)r;
+        }
+    }
+}
+__global__ __launch_bounds__(kOB) void k_ord_scatter(View v, uint32_t* __restrict__ ord, const uint32_t* __restrict__ sr, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) ord[jgk::slot_of(v, sr[i])] = (uint32_t)i;
 }
 // Chunked SoA stream -> AoS records in rank order (walks slots; skips each chunk's unused tail).
 __global__ __launch_bounds__(kOB) void k_pack(View v, const uint32_t* __restrict__ cnt, jg_tagrec* __restrict__ out) {
@@ -70,7 +127,7 @@ __global__ __launch_bounds__(kOB) void k_pack(View v, const uint32_t* __restrict
         const uint64_t c = x / v.C, j = x - c * v.C;
         if (j < cnt[c]) {
             const Tag g = ld_tag(v.tag + x);
-            out[v.off[c] + j] = jg_tagrec{v.key[x], g.lo, g.hi};
+            out[v.off[c] + j] = jg_tagrec{v.key[x], g.lo, g.hi, v.ord[x]};
         }
     }
 }
@@ -185,7 +242,7 @@ __global__ __launch_bounds__(kOB) void k_gather_ranges(View v, const uint64_t* _
         for (uint64_t j = 0; j < len[i]; ++j) {
             const uint64_t x = jgk::slot_of(v, src_off[i] + j);
             const Tag g = ld_tag(v.tag + x);
-            dst[dst_off[i] + j] = jg_tagrec{v.key[x], g.lo, g.hi};
+            dst[dst_off[i] + j] = jg_tagrec{v.key[x], g.lo, g.hi, v.ord[x]};
         }
     }
 }
@@ -205,12 +262,50 @@ size_t union_ws_bytes(uint64_t total) {
     return ((p * 8 + 255) & ~(size_t)255) + ((p * 8 + 255) & ~(size_t)255);
 }
 
+// Renumber a stream's ords to 0..n-1 in the same order (ties keep rank order); next = n.  Synchronous
+// on ctx->stream; needs the stream's count (no pending union).
+void renumber(jg_ctx* ctx, jg_stream_soa& s) {
+    if (s.n == 0) { s.next = 0; return; }
+    JG_REQUIRE(s.n < 0xFFFFFFFFull, JG_ESTATE, "OR-Set stream of %llu records exceeds the 32-bit ordinal range", (unsigned long long)s.n);
+    const uint64_t n = s.n;
+    jg::DevBuf buf;
+    size_t temp = 0;
+    uint32_t* nul = nullptr;
+    JG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, nul, nul, nul, nul, (int)n, 0, 32, ctx->stream));
+    const size_t a4 = (n * 4 + 255) & ~(size_t)255;
+    buf.alloc(4 * a4 + temp + 256);
+    auto* k0 = buf.as<uint32_t>();
+    auto* v0 = reinterpret_cast<uint32_t*>(buf.as<char>() + a4);
+    auto* k1 = reinterpret_cast<uint32_t*>(buf.as<char>() + 2 * a4);
+    auto* v1 = reinterpret_cast<uint32_t*>(buf.as<char>() + 3 * a4);
+    void* tmp = buf.as<char>() + 4 * a4;
+    const View v = view(s);
+    hipLaunchKernelGGL(k_ord_by_rank, dim3(grid_for(ctx, (uint64_t)s.nch * kChunk, 16)), dim3(kOB), 0, ctx->stream, v, s.cnt.as<uint32_t>(), k0, v0);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, temp, k0, k1, v0, v1, (int)n, 0, 32, ctx->stream));
+    hipLaunchKernelGGL(k_ord_scatter, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, v, s.ord.as<uint32_t>(), v1, n);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    s.next = n;
+}
+
+// Make room for out = a ∪ b: out's ords reach a.next + b.next.
+void ensure_ord_room(jg_ctx* ctx, jg_stream_soa& a, jg_stream_soa& b) {
+    if (a.next + b.next <= ord_limit()) return;
+    renumber(ctx, a);
+    if (a.next + b.next > ord_limit()) renumber(ctx, b);
+    JG_REQUIRE(a.next + b.next <= ord_limit(), JG_ESTATE, "OR-Set union of %llu + %llu records exceeds the 32-bit ordinal range",
+               (unsigned long long)a.n, (unsigned long long)b.n);
+}
+
 // Union of two streams into `out` (chunk capacity ensured here).  Async on ctx->stream; the output
-// record count lands in *d_count (device) and out.n is left for sync_counts.
+// record count lands in *d_count (device) and out.n is left for sync_counts.  Ords: see k_union
+// (the caller ensured a.next + b.next fits, ensure_ord_room).
 void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws,
                   jgk::Drop drop) {
     const uint64_t total = a.n + b.n;
     out.reserve_records(total);
+    out.next = a.next + b.next;
     if (total == 0) {
         jg::set_dense(ctx, out, 0);
         JG_HIP(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), ctx->stream));
@@ -225,7 +320,7 @@ void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, j
                        ctx->stream, va, vb, n_tiles + 1, part, pchunk);
     JG_HIP(hipGetLastError());
     hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, va, vb, part, pchunk,
-                       out.key.as<unsigned long long>(), out.tag.as<uint4>(), out.cnt.as<uint32_t>(), drop);
+                       out.key.as<unsigned long long>(), out.tag.as<uint4>(), out.ord.as<uint32_t>(), (uint32_t)a.next, out.cnt.as<uint32_t>(), drop);
     JG_HIP(hipGetLastError());
     hipLaunchKernelGGL(jgk::k_finish, dim3((unsigned)((n_tiles + 1023) / 1024)), dim3(1024), 0, ctx->stream, out.cnt.as<uint32_t>(),
                        (uint32_t)n_tiles, out.off.as<uint64_t>(), out.lut.as<uint32_t>(), (total >> jgk::kQShift) + 2, d_count);
@@ -234,9 +329,12 @@ void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, j
     out.dense = false;
 }
 
-// Union of both streams of two stores into `oa`/`orr`; counts to counted->counts.
-void union_store(jg_ctx* ctx, const jg_orset* a, const jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted,
+// Union of both streams of two stores into `oa`/`orr`; counts to counted->counts.  Stream counts must
+// be current (no pending union on a or b).
+void union_store(jg_ctx* ctx, jg_orset* a, jg_orset* b, jg_stream_soa& oa, jg_stream_soa& orr, jg_orset* counted,
                  jgk::Drop drop = {nullptr, 0}) {
+    ensure_ord_room(ctx, a->add, b->add);
+    ensure_ord_room(ctx, a->rem, b->rem);
     unsigned long long* d = counted->counts.as<unsigned long long>();
     const size_t ws_add = union_ws_bytes(a->add.n + b->add.n);
     char* ws = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, ws_add + union_ws_bytes(a->rem.n + b->rem.n)));
@@ -252,6 +350,7 @@ void check_err_flag(jg_ctx* ctx, const char* fn) {
     if (h) {
         JG_HIP(hipMemsetAsync(ctx->flags.p, 0, sizeof h, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
+        if (h & 2u) jg::fail(JG_EINVAL, "%s: a record's ord is not below 2^32", fn);
         jg::fail(JG_ESTATE, "%s: device reported a broken precondition (flag %u)", fn, h);
     }
 }
@@ -259,15 +358,22 @@ void check_err_flag(jg_ctx* ctx, const char* fn) {
 void upload_stream(jg_ctx* ctx, jg_stream_soa& s, const jg_tagrec* recs, uint64_t n, const char* fn) {
     s.reserve_records(n);
     jg::set_dense(ctx, s, n);
+    s.next = 0;
     if (n == 0) return;
     auto* st = static_cast<jg_tagrec*>(jg::scratch(ctx, ctx->scratch2, n * sizeof(jg_tagrec)));
+    auto* span = reinterpret_cast<unsigned long long*>(ctx->flags.as<char>() + 64);
     JG_HIP(hipMemcpyAsync(st, recs, n * sizeof(jg_tagrec), hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL(k_unpack, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st, n, s.key.as<unsigned long long>(), s.tag.as<uint4>());
+    JG_HIP(hipMemsetAsync(span, 0, 8, ctx->stream));
+    hipLaunchKernelGGL(k_unpack, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st, n, s.key.as<unsigned long long>(), s.tag.as<uint4>(),
+                       s.ord.as<uint32_t>(), ctx->flags.as<unsigned>(), span);
     JG_HIP(hipGetLastError());
     hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, s.key.as<unsigned long long>(),
                        s.tag.as<uint4>(), n, ctx->flags.as<unsigned>());
     JG_HIP(hipGetLastError());
-    check_err_flag(ctx, fn);
+    unsigned long long h = 0;
+    JG_HIP(hipMemcpyAsync(&h, span, 8, hipMemcpyDeviceToHost, ctx->stream));
+    check_err_flag(ctx, fn);  // synchronises: h is valid after it
+    s.next = h;
 }
 
 void download_stream(jg_ctx* ctx, const jg_stream_soa& s, jg_tagrec* out) {
@@ -280,7 +386,7 @@ void download_stream(jg_ctx* ctx, const jg_stream_soa& s, jg_tagrec* out) {
 }
 
 // In-place merge: s = (s minus the records of sets flagged in `drop`) ∪ src.
-void merge_into(jg_orset* s, const jg_orset* src, bool async, jgk::Drop drop = {nullptr, 0}) {
+void merge_into(jg_orset* s, jg_orset* src, bool async, jgk::Drop drop = {nullptr, 0}) {
     jg_ctx* ctx = s->ctx;
     jg::sync_counts(s);
     union_store(ctx, s, src, s->spare_add, s->spare_rem, s, drop);
@@ -345,12 +451,33 @@ Runs fetch_runs(jg_orset* s, const std::vector<unsigned long long>& keys) {
     return r;
 }
 
-using TagSet = std::set<std::pair<uint64_t, uint64_t>>;
+using TagKey = std::pair<uint64_t, uint64_t>;
+
+// One element's tag sets while a batch of ops runs: the enumeration order (existing records by
+// (ord, tag), then the batch's own in the order it appended them) and membership.
+struct ElemState {
+    std::vector<TagKey> add, rem;
+    std::set<TagKey> add_has, rem_has;
+};
+
+void load_group(const jg_tagrec* b, const jg_tagrec* e, std::vector<TagKey>& order, std::set<TagKey>& has) {
+    std::vector<jg_tagrec> g(b, e);
+    std::sort(g.begin(), g.end(), [](const jg_tagrec& x, const jg_tagrec& y) {
+        return x.ord != y.ord ? x.ord < y.ord : x.tag_lo != y.tag_lo ? x.tag_lo < y.tag_lo : x.tag_hi < y.tag_hi;
+    });
+    for (const auto& r : g) {
+        order.emplace_back(r.tag_lo, r.tag_hi);
+        has.emplace(r.tag_lo, r.tag_hi);
+    }
+}
 
 // ORSet.Add / Remove / Clear (ORSet.cs:134-198) in op order per set.  Host-side sequential
 // semantics over the store's runs of every element a Remove touches (gathered from the device),
 // then ONE device union: (store minus the sets Cleared in the batch) ∪ (records added after each
-// set's last Clear).
+// set's last Clear).  Ords of the batch's records count from 0 in op order (the union puts them after
+// the store's): an Add's tag is appended to its element's HashSet (:145-149); a Remove appends the
+// element's add tags it lacks to the tombstone set, in the add set's enumeration order (UnionWith /
+// the copy constructor of addSet[item], :175-183).
 void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
                const uint64_t* tag_hi, uint8_t* result) {
     std::vector<uint64_t> order(n_ops);
@@ -365,7 +492,7 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
 
     std::vector<jg_tagrec> dadd, drem;
     std::vector<uint32_t> cleared;
-    struct ElemState { TagSet add, rem; };
+    uint64_t next_a = 0, next_r = 0;  // batch ords (op order within a set; sets are independent)
     for (uint64_t g = 0; g < n_ops;) {
         const uint32_t sid = set[order[g]];
         uint64_t h = g;
@@ -381,26 +508,32 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
             auto nk = std::lower_bound(need.begin(), need.end(), key);
             if (!was_cleared && nk != need.end() && *nk == key) {
                 const size_t q = nk - need.begin();
-                for (uint64_t j = runs.add_off[q]; j < runs.add_off[q + 1]; ++j) es.add.emplace(runs.add[j].tag_lo, runs.add[j].tag_hi);
-                for (uint64_t j = runs.rem_off[q]; j < runs.rem_off[q + 1]; ++j) es.rem.emplace(runs.rem[j].tag_lo, runs.rem[j].tag_hi);
+                load_group(runs.add.data() + runs.add_off[q], runs.add.data() + runs.add_off[q + 1], es.add, es.add_has);
+                load_group(runs.rem.data() + runs.rem_off[q], runs.rem.data() + runs.rem_off[q + 1], es.rem, es.rem_has);
             }
             return st.emplace(e, std::move(es)).first->second;
         };
         for (uint64_t x = g; x < h; ++x) {
             const uint64_t i = order[x];
             const unsigned long long key = ((unsigned long long)sid << 32) | elem[i];
-            if (op[i] == 1) {  // Add: a fresh tag (ORSet.cs:134-153)
-                state(elem[i]).add.emplace(tag_lo[i], tag_hi[i]);
-                sa.push_back(jg_tagrec{key, tag_lo[i], tag_hi[i]});
+            if (op[i] == 1) {  // Add: a fresh tag (ORSet.cs:134-153); HashSet.Add keeps a present tag where it is
+                ElemState& es = state(elem[i]);
+                const TagKey t{tag_lo[i], tag_hi[i]};
+                if (es.add_has.insert(t).second) {
+                    es.add.push_back(t);
+                    sa.push_back(jg_tagrec{key, t.first, t.second, next_a++});
+                }
                 result[i] = 1;
             } else if (op[i] == 2) {  // Remove: if Contains, tombstone every observed tag (ORSet.cs:161-186)
                 ElemState& es = state(elem[i]);
-                const bool present = elem[i] == JG_NULL_ELEM ? es.add != es.rem : !es.add.empty() && (es.rem.empty() || es.add != es.rem);
+                const bool present =
+                    elem[i] == JG_NULL_ELEM ? es.add_has != es.rem_has : !es.add.empty() && (es.rem.empty() || es.add_has != es.rem_has);
                 if (present)
-                    for (const auto& t : es.add) {
-                        es.rem.insert(t);
-                        sr.push_back(jg_tagrec{key, t.first, t.second});
-                    }
+                    for (const TagKey& t : es.add)
+                        if (es.rem_has.insert(t).second) {
+                            es.rem.push_back(t);
+                            sr.push_back(jg_tagrec{key, t.first, t.second, next_r++});
+                        }
                 result[i] = present ? 1 : 0;
             } else {  // Clear (ORSet.cs:192-198)
                 st.clear();
@@ -415,14 +548,12 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
         drem.insert(drem.end(), sr.begin(), sr.end());
         g = h;
     }
+    // the batch's records carry no duplicate (key, tag): the ElemStates filtered them
     auto lt = [](const jg_tagrec& a, const jg_tagrec& b) {
         return a.key != b.key ? a.key < b.key : a.tag_lo != b.tag_lo ? a.tag_lo < b.tag_lo : a.tag_hi < b.tag_hi;
     };
-    auto eq = [](const jg_tagrec& a, const jg_tagrec& b) { return a.key == b.key && a.tag_lo == b.tag_lo && a.tag_hi == b.tag_hi; };
     std::sort(dadd.begin(), dadd.end(), lt);
-    dadd.erase(std::unique(dadd.begin(), dadd.end(), eq), dadd.end());
     std::sort(drem.begin(), drem.end(), lt);
-    drem.erase(std::unique(drem.begin(), drem.end(), eq), drem.end());
 
     jg_ctx* ctx = s->ctx;
     jg::DevBuf drop;
@@ -436,6 +567,7 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
         d = jgk::Drop{drop.as<unsigned>(), (uint32_t)bits.size()};
     }
     if (dadd.empty() && drem.empty() && cleared.empty()) return;
+    JG_REQUIRE(next_a < 0xFFFFFFFFull && next_r < 0xFFFFFFFFull, JG_EINVAL, "jg_orset_apply_ops: too many records in one batch");
     jg_orset tmp;
     tmp.ctx = ctx;
     upload_stream(ctx, tmp.add, dadd.data(), dadd.size(), "jg_orset_apply_ops(add)");
@@ -452,6 +584,8 @@ void jg_stream_soa::swap(jg_stream_soa& o) {
     };
     swap_buf(key, o.key);
     swap_buf(tag, o.tag);
+    swap_buf(ord, o.ord);
+    std::swap(next, o.next);
     swap_buf(cnt, o.cnt);
     swap_buf(off, o.off);
     swap_buf(lut, o.lut);
@@ -467,6 +601,7 @@ void jg_stream_soa::reserve_records(uint64_t records) {
     const uint64_t slots = c * kChunk;
     key.alloc(slots * 8);
     tag.alloc(slots * 16);
+    ord.alloc(slots * 4);
     cnt.alloc((c ? c : 1) * 4);
     off.alloc((c + 1) * 8);
     lut.alloc(((slots >> jgk::kQShift) + 2) * 4);
@@ -500,9 +635,24 @@ void sync_counts(jg_orset* s) {
 // owner, sorted and duplicate-free (a stable partition of a sorted stream; the set-id rewrite is
 // monotone within one owner).  Each run is copied into a dense stream and checked, the runs are
 // unioned pairwise (log2(n_runs) levels), and the result is merged into the store: the same
-// ORSet.Merge per set as jg_orset_merge, from device memory.
+// ORSet.Merge per set as jg_orset_merge, from device memory.  Run r's ords order its records among
+// themselves; run r is merged after runs 0..r-1 (the tree keeps the left operand first), so a tag
+// new to the store enumerates by (first run holding it, its ord there).
+uint64_t ord_span(jg_ctx* ctx, const uint32_t* ord, uint64_t n) {
+    if (n == 0) return 0;
+    auto* span = reinterpret_cast<unsigned long long*>(ctx->flags.as<char>() + 64);
+    JG_HIP(hipMemsetAsync(span, 0, 8, ctx->stream));
+    hipLaunchKernelGGL(k_ord_span, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, ord, n, span);
+    JG_HIP(hipGetLastError());
+    unsigned long long h = 0;
+    JG_HIP(hipMemcpyAsync(&h, span, 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    return h;
+}
+
 void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const unsigned long long* add_key,
-                      const uint4* add_tag, const unsigned long long* rem_key, const uint4* rem_tag) {
+                      const uint4* add_tag, const uint32_t* add_ord, const unsigned long long* rem_key, const uint4* rem_tag,
+                      const uint32_t* rem_ord) {
     jg_ctx* ctx = s->ctx;
     sync_counts(s);
     auto fresh = [ctx] {
@@ -511,11 +661,14 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
         t->counts.alloc(16);
         return t;
     };
-    auto fill = [ctx](jg_stream_soa& st, const unsigned long long* k, const uint4* t, uint64_t n) {
+    auto fill = [ctx](jg_stream_soa& st, const unsigned long long* k, const uint4* t, const uint32_t* o, uint64_t n) {
         set_dense(ctx, st, n);
+        st.next = 0;
         if (n == 0) return;
         JG_HIP(hipMemcpyAsync(st.key.p, k, n * 8, hipMemcpyDeviceToDevice, ctx->stream));
         JG_HIP(hipMemcpyAsync(st.tag.p, t, n * 16, hipMemcpyDeviceToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(st.ord.p, o, n * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        st.next = ord_span(ctx, st.ord.as<uint32_t>(), n);
         hipLaunchKernelGGL(k_check_sorted, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, st.key.as<unsigned long long>(),
                            st.tag.as<uint4>(), n, ctx->flags.as<unsigned>());
         JG_HIP(hipGetLastError());
@@ -525,8 +678,8 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
     for (uint32_t r = 0; r < n_runs; ++r) {
         if (add_counts[r] + rem_counts[r] > 0) {
             auto t = fresh();
-            fill(t->add, add_key + ao, add_tag + ao, add_counts[r]);
-            fill(t->rem, rem_key + ro, rem_tag + ro, rem_counts[r]);
+            fill(t->add, add_key + ao, add_tag + ao, add_ord + ao, add_counts[r]);
+            fill(t->rem, rem_key + ro, rem_tag + ro, rem_ord + ro, rem_counts[r]);
             level.push_back(std::move(t));
         }
         ao += add_counts[r];
@@ -547,7 +700,7 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
     if (!level.empty()) merge_into(s, level[0].get(), false);
 }
 
-void orset_merge_store(jg_orset* s, const jg_orset* src) { merge_into(s, src, false); }
+void orset_merge_store(jg_orset* s, jg_orset* src) { merge_into(s, src, false); }
 }  // namespace jg
 
 extern "C" {
@@ -645,7 +798,7 @@ int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
         JG_REQUIRE(dst->ctx == src->ctx, JG_EINVAL, "jg_orset_merge_store: stores belong to different contexts");
         jg::ensure_device(dst->ctx);
         jg::sync_counts(const_cast<jg_orset*>(src));
-        merge_into(dst, src, async == 0 ? false : true);
+        merge_into(dst, const_cast<jg_orset*>(src), async == 0 ? false : true);  // renumbering may touch src's ords (order kept)
     });
 }
 
@@ -659,7 +812,7 @@ int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int asyn
         jg::ensure_device(ctx);
         jg::sync_counts(const_cast<jg_orset*>(a));
         jg::sync_counts(const_cast<jg_orset*>(b));
-        union_store(ctx, a, b, out->add, out->rem, out);
+        union_store(ctx, const_cast<jg_orset*>(a), const_cast<jg_orset*>(b), out->add, out->rem, out);  // renumbering keeps order
         if (!async) {
             check_err_flag(ctx, "jg_orset_union");
             jg::sync_counts(out);

@@ -45,6 +45,7 @@ __device__ __forceinline__ bool rec_eq(unsigned long long ka, Tag ta, unsigned l
 struct View {
     const unsigned long long* key;
     const uint4* tag;
+    const uint32_t* ord;  // arrival ordinals (jg_tagrec.ord); only the union reads them
     const uint64_t* off;  // [nch + 1]
     const uint32_t* lut;  // [(n >> kQShift) + 2]
     uint64_t n;
@@ -130,10 +131,13 @@ __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_pa
 }
 
 // One tile: A ranks [i0, i1), B ranks [j0, j1) -> chunk `tile` of the output (capacity kOB*kItems).
+// Ordinals: an A record keeps its ord, a B record takes b_base + its ord (b_base = A's next: a tag new
+// to A's HashSet is appended after every tag A holds, in B's order — UnionWith / the copy constructor,
+// ORSet.cs:255-282).  A B record equal to an A record is dropped, so the A record's ord stays.
 template <int kOB, int kItems>
 __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* __restrict__ part, const uint32_t* __restrict__ pchunk,
-                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ ocnt,
-                                               Drop drop) {
+                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ oord,
+                                               uint32_t b_base, uint32_t* __restrict__ ocnt, Drop drop) {
     constexpr int kTile = kOB * kItems;
     constexpr int kSeg = 64;  // chunks a tile's A (or B) range may span before the slow path
     __shared__ unsigned long long s_key[kTile];
@@ -167,6 +171,9 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     __syncthreads();
 
     // ---- stage the tile in LDS; every load issued before the first LDS write ----
+    // The ordinals stay in registers (staging index x = it * kOB + tid): keys + tags fill the LDS of two
+    // workgroups per CU, so ords only pass through LDS after the merge (below).
+    uint32_t rord[kItems];
     {
         unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
 #pragma unroll
@@ -184,6 +191,7 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
             const Tag t = ld_tag_nt((from_a ? a.tag : b.tag) + slot);
             rlo[it] = t.lo;
             rhi[it] = t.hi;
+            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + slot) + (from_a ? 0u : b_base);
         }
         unsigned long long pk = 0;
         Tag pt{0, 0};
@@ -238,14 +246,16 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     Tag ta{0, 0}, tb{0, 0};
     if (ai < nA) { ka = s_key[ai]; ta = __builtin_bit_cast(Tag, s_tag[ai]); }
     if (bi < nB) { kb = s_key[nA + bi]; tb = __builtin_bit_cast(Tag, s_tag[nA + bi]); }
-    // the merged records stay in registers for the compaction (no second LDS gather)
+    // the merged records stay in registers for the compaction (no second LDS gather); src = staging index
     unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
+    int src[kItems];
     unsigned keep = 0;
 #pragma unroll
     for (int it = 0; it < kItems; ++it) {
-        rk[it] = 0; rlo[it] = 0; rhi[it] = 0;
+        rk[it] = 0; rlo[it] = 0; rhi[it] = 0; src[it] = 0;
         if (it < my_n) {
             const bool take_a = ai < nA && (bi >= nB || !rec_lt(kb, tb, ka, ta));
+            src[it] = take_a ? ai : nA + bi;
             if (take_a) {
                 rk[it] = ka; rlo[it] = ta.lo; rhi[it] = ta.hi;
                 hp = !dropped(drop, ka);
@@ -280,6 +290,21 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
         block_total += v;
     }
     const int my_off = wbase + incl - cnt;
+    const uint64_t base = tile * (uint64_t)kTile;
+
+    // ---- ordinals: registers -> LDS by staging index -> each kept output's ord -> compacted, stored ----
+    // (the scan's barrier ended every merge-phase LDS read; the key area is free, then the tag area)
+    uint32_t* s_ord_in = reinterpret_cast<uint32_t*>(s_tag);  // 12 KB of the tag area
+    uint32_t* s_ord_out = reinterpret_cast<uint32_t*>(s_key);  // 12 KB of the key area
+#pragma unroll
+    for (int it = 0; it < kItems; ++it) s_ord_in[it * kOB + tid] = rord[it];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kItems; ++it)
+        if (keep & (1u << it)) s_ord_out[my_off + __popc(keep & ((1u << it) - 1u))] = s_ord_in[src[it]];
+    __syncthreads();
+    for (int x = tid; x < block_total; x += kOB) __builtin_nontemporal_store(s_ord_out[x], oord + base + x);
+    __syncthreads();
 
     // ---- compact the kept records through LDS, store coalesced into this tile's chunk ----
 #pragma unroll
@@ -291,7 +316,6 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
         }
     }
     __syncthreads();
-    const uint64_t base = tile * (uint64_t)kTile;
     for (int x = tid; x < block_total; x += kOB) {  // written once, read by a later launch: non-temporal
         __builtin_nontemporal_store(s_key[x], ok + base + x);
         st_tag_nt(ot + base + x, s_tag[x]);

@@ -686,16 +686,21 @@ __device__ __forceinline__ uint64_t rec_hash(unsigned long long k, const Tag16& 
 }
 
 // Distinct records: insert-if-absent into an open-addressing table of record indices (exact compare on a
-// hash match); the first copy of each record is appended to its side's output (wave-aggregated counter).
+// hash match); the copy that wins the slot is appended to its side's output (wave-aggregated counter)
+// with its table slot, and every copy lowers the slot's mint to its tag index: mint = the record's
+// FIRST occurrence in commit order = its arrival ordinal (a HashSet keeps a tag where it was first
+// inserted; tag indices run message after message, each message in its arrays' order).
 __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* __restrict__ rkey, const uint8_t* __restrict__ rside,
                                                      const Tag16* __restrict__ tval, uint64_t nt, unsigned long long* __restrict__ tab, uint64_t mask,
-                                                     unsigned long long* __restrict__ dk0, Tag16* __restrict__ dt0, unsigned long long* __restrict__ dk1,
-                                                     Tag16* __restrict__ dt1, unsigned long long* __restrict__ counts) {
+                                                     uint32_t* __restrict__ mint, unsigned long long* __restrict__ dk0, Tag16* __restrict__ dt0,
+                                                     uint32_t* __restrict__ ds0, unsigned long long* __restrict__ dk1, Tag16* __restrict__ dt1,
+                                                     uint32_t* __restrict__ ds1, unsigned long long* __restrict__ counts) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool fresh = false;
     uint32_t side = 0;
     unsigned long long k = kNone;
     Tag16 g{0, 0};
+    uint64_t slot = 0;
     if (t < nt) {
         k = rkey[t];
         side = rside[t];
@@ -710,13 +715,14 @@ __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* _
             unsigned long long w = tab[s];
             if (w == 0) {
                 w = atomicCAS(tab + s, 0ull, word);
-                if (w == 0) { fresh = true; break; }
+                if (w == 0) { fresh = true; slot = s; break; }
             }
             if ((w >> 32) != (h >> 32)) continue;
             const uint64_t u = (w & 0xFFFFFFFFull) - 1;
             const Tag16 o = tval[u];
-            if (rkey[u] == k && rside[u] == side && o.lo == g.lo && o.hi == g.hi) break;
+            if (rkey[u] == k && rside[u] == side && o.lo == g.lo && o.hi == g.hi) { slot = s; break; }
         }
+        atomicMin(mint + slot, (uint32_t)t);
     }
     const uint32_t lane = __lane_id();
     for (uint32_t sd = 0; sd < 2; ++sd) {
@@ -731,6 +737,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* _
             const unsigned long long pos = base + __popcll(b & ((1ull << lane) - 1));
             (sd ? dk1 : dk0)[pos] = k;
             (sd ? dt1 : dt0)[pos] = g;
+            (sd ? ds1 : ds0)[pos] = (uint32_t)slot;
         }
     }
 }
@@ -747,13 +754,15 @@ __global__ void k_gather_radix(const unsigned long long* __restrict__ dk, const 
     const uint32_t p = perm[i];
     out[i] = which == 2 ? dk[p] : which == 1 ? dt[p].lo : dt[p].hi;
 }
-__global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ perm, uint64_t n,
-                              unsigned long long* __restrict__ ok, Tag16* __restrict__ ot) {
+__global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ ds,
+                              const uint32_t* __restrict__ mint, const uint32_t* __restrict__ perm, uint64_t n, unsigned long long* __restrict__ ok,
+                              Tag16* __restrict__ ot, uint32_t* __restrict__ oo) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = perm[i];
     ok[i] = dk[p];
     ot[i] = dt[p];
+    oo[i] = mint[ds[p]];
 }
 
 uint64_t pow2_at_least(uint64_t x) {
@@ -784,7 +793,7 @@ struct jg_orset_wire {
     // entries, groups, tags, records
     jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, skey, sval, hs, seg, impure, label, gid, eid;
     jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
-    jg::DevBuf tref, tval, rkey, rside, dtab, dk[2], dt[2], rk, rk2, perm, perm2;
+    jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm, perm2;
     jg::DevBuf newk, newv, snk, snv, status, cub;
     jg_orset* recs = nullptr;  // a committed wave's records, sorted (the merge source), reused
     // ids issued by the last commit: names [g0, g1), pool bytes [p0, p1)
@@ -1004,9 +1013,11 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     return (e & 3) == kKindState ? JG_ESTATE : JG_EINVAL;
 }
 
-// Sort one side's distinct records by (key, tag.lo, tag.hi) (three stable LSD passes) into a dense stream.
-void sort_side(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out) {
+// Sort one side's distinct records by (key, tag.lo, tag.hi) (three stable LSD passes) into a dense stream;
+// ords = first tag index in the wave (< nt = the stream's next).
+void sort_side(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, uint64_t nt, jg_stream_soa& out) {
     jg::set_dense(ctx, out, n);
+    out.next = nt;
     if (n == 0) return;
     ensure(w->rk, n * 8);
     ensure(w->rk2, n * 8);
@@ -1023,8 +1034,8 @@ void sort_side(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, 
         sort_pairs(ctx, w, w->rk.as<unsigned long long>(), w->rk2.as<unsigned long long>(), p, q, n, which == 2 ? key_bits : 64);
         std::swap(p, q);
     }
-    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, out.key.as<unsigned long long>(),
-                       out.tag.as<Tag16>());
+    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), w->dmin.as<uint32_t>(), p,
+                       n, out.key.as<unsigned long long>(), out.tag.as<Tag16>(), out.ord.as<uint32_t>());
     JG_HIP(hipGetLastError());
 }
 
@@ -1084,18 +1095,22 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     ensure(w->rside, nt + 1);
     const uint64_t tcap = pow2_at_least(2 * nt);
     ensure(w->dtab, tcap * 8);
+    ensure(w->dmin, tcap * 4);
     for (int sd = 0; sd < 2; ++sd) {
         ensure(w->dk[sd], nt * 8 + 8);
         ensure(w->dt[sd], nt * 16 + 16);
+        ensure(w->ds[sd], nt * 4 + 4);
     }
     hipLaunchKernelGGL(k_ow_rec_keys, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->tref.as<unsigned long long>(),
                        w->eid.as<uint32_t>(), nt, limit, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>());
     JG_HIP(hipGetLastError());
     JG_HIP(hipMemsetAsync(w->dtab.p, 0, tcap * 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->dmin.p, 0xFF, tcap * 4, ctx->stream));
     JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
     hipLaunchKernelGGL(k_ow_dedup, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>(),
-                       w->tval.as<Tag16>(), nt, w->dtab.as<unsigned long long>(), tcap - 1, w->dk[0].as<unsigned long long>(), w->dt[0].as<Tag16>(),
-                       w->dk[1].as<unsigned long long>(), w->dt[1].as<Tag16>(), st + 4);
+                       w->tval.as<Tag16>(), nt, w->dtab.as<unsigned long long>(), tcap - 1, w->dmin.as<uint32_t>(), w->dk[0].as<unsigned long long>(),
+                       w->dt[0].as<Tag16>(), w->ds[0].as<uint32_t>(), w->dk[1].as<unsigned long long>(), w->dt[1].as<Tag16>(), w->ds[1].as<uint32_t>(),
+                       st + 4);
     JG_HIP(hipGetLastError());
     unsigned long long cnt[2];
     read_words(ctx, st + 4, cnt, 2);
@@ -1105,8 +1120,8 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         w->recs->ctx = ctx;
     }
     const int key_bits = 32 + bits_for(w->max_set);
-    sort_side(ctx, w, 0, cnt[0], key_bits, w->recs->add);
-    sort_side(ctx, w, 1, cnt[1], key_bits, w->recs->rem);
+    sort_side(ctx, w, 0, cnt[0], key_bits, nt, w->recs->add);
+    sort_side(ctx, w, 1, cnt[1], key_bits, nt, w->recs->rem);
     jg::orset_merge_store(s, w->recs);
 }
 

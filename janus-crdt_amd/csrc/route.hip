@@ -164,8 +164,10 @@ struct RowMover {
 struct RecMover {
     const unsigned long long* key;
     const uint4* tag;
+    const uint32_t* ord;
     unsigned long long* okey;
     uint4* otag;
+    uint32_t* oord;
     uint32_t world;
     __device__ __forceinline__ void move(uint64_t s0, uint32_t cnt, const uint64_t* dst, int, int) const {
         const uint32_t i = threadIdx.x;
@@ -174,6 +176,7 @@ struct RecMover {
             const unsigned long long set = k >> 32;
             okey[dst[i]] = ((set / world) << 32) | (k & 0xFFFFFFFFull);
             otag[dst[i]] = tag[s0 + i];
+            oord[dst[i]] = ord[s0 + i];
         }
     }
 };
@@ -284,7 +287,7 @@ void route_rows(jg_ctx* ctx, const jg_rows* r, uint32_t world, uint64_t* counts,
     JG_HIP(hipGetLastError());
 }
 
-void route_stream(jg_ctx* ctx, const jg_stream_soa& s, uint32_t world, uint64_t* counts, void* dk, void* dt) {
+void route_stream(jg_ctx* ctx, const jg_stream_soa& s, uint32_t world, uint64_t* counts, void* dk, void* dt, void* dord) {
     if (s.n == 0 || s.nch == 0) {
         std::fill(counts, counts + world, 0ull);
         return;
@@ -292,7 +295,8 @@ void route_stream(jg_ctx* ctx, const jg_stream_soa& s, uint32_t world, uint64_t*
     const RecOwner own{s.key.as<unsigned long long>(), world};
     const Tiles tl{s.n, s.cnt.as<uint32_t>(), kChunk};
     const uint64_t* pos = route_plan(ctx, own, tl, s.nch, world, counts);
-    const RecMover mv{s.key.as<unsigned long long>(), s.tag.as<uint4>(), (unsigned long long*)dk, (uint4*)dt, world};
+    const RecMover mv{s.key.as<unsigned long long>(), s.tag.as<uint4>(), s.ord.as<uint32_t>(), (unsigned long long*)dk, (uint4*)dt,
+                      (uint32_t*)dord, world};
     hipLaunchKernelGGL((k_route_scatter<RecOwner, RecMover>), dim3(s.nch), dim3(kRB), 0, ctx->stream, own, tl, s.nch, pos, mv);
     JG_HIP(hipGetLastError());
 }
@@ -352,7 +356,7 @@ int jg_pnc_merge_device(jg_pnc* p, uint64_t n_rows, const void* d_keys, const vo
 }
 
 int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* rem_counts, void* d_add_key, void* d_add_tag,
-                   uint64_t cap_add, void* d_rem_key, void* d_rem_tag, uint64_t cap_rem) {
+                   void* d_add_ord, uint64_t cap_add, void* d_rem_key, void* d_rem_tag, void* d_rem_ord, uint64_t cap_rem) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_orset_route";
@@ -365,16 +369,18 @@ int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* 
                    (unsigned long long)cap_add, (unsigned long long)cap_rem, (unsigned long long)s->add.n, (unsigned long long)s->rem.n);
         check_dev(ctx, d_add_key, s->add.n * 8, fn, "d_add_key");
         check_dev(ctx, d_add_tag, s->add.n * 16, fn, "d_add_tag");
+        check_dev(ctx, d_add_ord, s->add.n * 4, fn, "d_add_ord");
         check_dev(ctx, d_rem_key, s->rem.n * 8, fn, "d_rem_key");
         check_dev(ctx, d_rem_tag, s->rem.n * 16, fn, "d_rem_tag");
-        route_stream(ctx, s->add, world, add_counts, d_add_key, d_add_tag);
-        route_stream(ctx, s->rem, world, rem_counts, d_rem_key, d_rem_tag);
+        check_dev(ctx, d_rem_ord, s->rem.n * 4, fn, "d_rem_ord");
+        route_stream(ctx, s->add, world, add_counts, d_add_key, d_add_tag, d_add_ord);
+        route_stream(ctx, s->rem, world, rem_counts, d_rem_key, d_rem_tag, d_rem_ord);
         JG_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
 
 int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const void* d_add_key,
-                          const void* d_add_tag, const void* d_rem_key, const void* d_rem_tag) {
+                          const void* d_add_tag, const void* d_add_ord, const void* d_rem_key, const void* d_rem_tag, const void* d_rem_ord) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         const char* fn = "jg_orset_merge_device";
@@ -388,10 +394,12 @@ int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_coun
         }
         check_dev(ctx, d_add_key, na * 8, fn, "d_add_key");
         check_dev(ctx, d_add_tag, na * 16, fn, "d_add_tag");
+        check_dev(ctx, d_add_ord, na * 4, fn, "d_add_ord");
         check_dev(ctx, d_rem_key, nr * 8, fn, "d_rem_key");
         check_dev(ctx, d_rem_tag, nr * 16, fn, "d_rem_tag");
+        check_dev(ctx, d_rem_ord, nr * 4, fn, "d_rem_ord");
         jg::orset_merge_runs(s, n_runs, add_counts, rem_counts, (const unsigned long long*)d_add_key, (const uint4*)d_add_tag,
-                             (const unsigned long long*)d_rem_key, (const uint4*)d_rem_tag);
+                             (const uint32_t*)d_add_ord, (const unsigned long long*)d_rem_key, (const uint4*)d_rem_tag, (const uint32_t*)d_rem_ord);
     });
 }
 

@@ -31,9 +31,10 @@ __global__ __launch_bounds__(kB) void k_synth_pnc(T* __restrict__ out, uint64_t 
     }
 }
 
-// record i of a stream with `per` tags u in [u0, u0+per) per group, groups in order.
-__global__ __launch_bounds__(kB) void k_synth_orset(unsigned long long* __restrict__ key, uint4* __restrict__ tag, uint64_t n, uint32_t E,
-                                                    uint32_t per, uint32_t u0, unsigned long long seed) {
+// record i of a stream with `per` tags u in [u0, u0+per) per group, groups in order; arrival ord = i
+// (the stream arrived in its canonical order).
+__global__ __launch_bounds__(kB) void k_synth_orset(unsigned long long* __restrict__ key, uint4* __restrict__ tag, uint32_t* __restrict__ ord,
+                                                    uint64_t n, uint32_t E, uint32_t per, uint32_t u0, unsigned long long seed) {
     for (uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kB) {
         const uint64_t g = i / per;
         const unsigned long long u = u0 + (i % per);
@@ -42,6 +43,7 @@ __global__ __launch_bounds__(kB) void k_synth_orset(unsigned long long* __restri
         key[i] = ((g / E) << 32) | (g % E);
         const unsigned long long t0 = (u << 56) | (h1 >> 8);
         tag[i] = make_uint4((unsigned)t0, (unsigned)(t0 >> 32), (unsigned)h2, (unsigned)(h2 >> 32));
+        ord[i] = (uint32_t)i;
     }
 }
 
@@ -95,14 +97,17 @@ int jg_synth_orset(jg_orset* s, uint64_t seed, uint64_t n_groups, uint32_t elems
         jg::ensure_device(ctx);
         jg::sync_counts(s);
         const uint64_t na = n_groups * add_per_group, nr = n_groups * rem_per_group;
+        JG_REQUIRE(na < 0xFFFFFFFFull && nr < 0xFFFFFFFFull, JG_EINVAL, "jg_synth_orset: a stream of 2^32 records or more");
         jg::set_dense(ctx, s->add, na);
         jg::set_dense(ctx, s->rem, nr);
+        s->add.next = na;
+        s->rem.next = nr;
         if (na)
             hipLaunchKernelGGL(k_synth_orset, dim3(grid_for(ctx, na)), dim3(kB), 0, ctx->stream, s->add.key.as<unsigned long long>(),
-                               s->add.tag.as<uint4>(), na, elems_per_set, add_per_group, add_u0, (unsigned long long)seed);
+                               s->add.tag.as<uint4>(), s->add.ord.as<uint32_t>(), na, elems_per_set, add_per_group, add_u0, (unsigned long long)seed);
         if (nr)
             hipLaunchKernelGGL(k_synth_orset, dim3(grid_for(ctx, nr)), dim3(kB), 0, ctx->stream, s->rem.key.as<unsigned long long>(),
-                               s->rem.tag.as<uint4>(), nr, elems_per_set, rem_per_group, rem_u0, (unsigned long long)seed);
+                               s->rem.tag.as<uint4>(), s->rem.ord.as<uint32_t>(), nr, elems_per_set, rem_per_group, rem_u0, (unsigned long long)seed);
         JG_HIP(hipGetLastError());
         JG_HIP(hipStreamSynchronize(ctx->stream));
     });

@@ -657,21 +657,37 @@ std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Gui
     for (size_t i = 0; i < n; ++i) {
         const SetKey& sk = sets_[sets[i]];
         ORSetState st;
-        // records are sorted by (elem id, tag): one run per element, ascending id = insertion order
-        auto fill = [&](const jg_tagrec* b, const jg_tagrec* e, std::vector<std::pair<std::string, std::vector<Guid>>>& dict,
-                        std::vector<Guid>& nulls) {
-            for (const jg_tagrec* x = b; x < e;) {
+        // records come sorted by (elem id, tag): one run per element.  Tags enumerate in ascending
+        // (ord, tag) (HashSet<Guid> insertion order); addSet elements in ascending id (= the add
+        // Dictionary's insertion order); removeSet elements by their first tombstone's ord (= when the
+        // element entered the remove Dictionary), ties by id; null last (its own HashSet member).
+        auto fill = [&](jg_tagrec* b, jg_tagrec* e, std::vector<std::pair<std::string, std::vector<Guid>>>& dict, std::vector<Guid>& nulls,
+                        bool by_first_ord) {
+            struct Run { jg_tagrec* b; jg_tagrec* e; uint32_t id; uint64_t first; };
+            std::vector<Run> runs;
+            for (jg_tagrec* x = b; x < e;) {
                 const uint32_t id = (uint32_t)x->key;
-                const jg_tagrec* y = x;
-                std::vector<Guid> tags;
-                for (; y < e && (uint32_t)y->key == id; ++y) tags.push_back(Guid{y->tag_lo, y->tag_hi});
-                if (id == JG_NULL_ELEM) nulls = std::move(tags);
-                else dict.emplace_back(sk.names.at(id), std::move(tags));
+                jg_tagrec* y = x;
+                uint64_t first = UINT64_MAX;
+                for (; y < e && (uint32_t)y->key == id; ++y) first = std::min(first, y->ord);
+                std::sort(x, y, [](const jg_tagrec& p, const jg_tagrec& q) {
+                    return p.ord != q.ord ? p.ord < q.ord : p.tag_lo != q.tag_lo ? p.tag_lo < q.tag_lo : p.tag_hi < q.tag_hi;
+                });
+                runs.push_back(Run{x, y, id, first});
                 x = y;
             }
+            if (by_first_ord)
+                std::stable_sort(runs.begin(), runs.end(), [](const Run& p, const Run& q) { return p.first < q.first; });
+            for (const Run& r : runs) {
+                std::vector<Guid> tags;
+                tags.reserve(r.e - r.b);
+                for (const jg_tagrec* x = r.b; x < r.e; ++x) tags.push_back(Guid{x->tag_lo, x->tag_hi});
+                if (r.id == JG_NULL_ELEM) nulls = std::move(tags);
+                else dict.emplace_back(sk.names.at(r.id), std::move(tags));
+            }
         };
-        fill(a.data() + ao[i], a.data() + ao[i + 1], st.addSet, st.nullAddGuid);
-        fill(r.data() + ro[i], r.data() + ro[i + 1], st.removeSet, st.nullRemoveGuid);
+        fill(a.data() + ao[i], a.data() + ao[i + 1], st.addSet, st.nullAddGuid, false);
+        fill(r.data() + ro[i], r.data() + ro[i + 1], st.removeSet, st.nullRemoveGuid, true);
         out.push_back(wire::EncodeORSetMsg(st));
     }
     return out;

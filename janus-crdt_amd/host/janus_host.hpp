@@ -156,10 +156,9 @@ class GpuStableStore {
     // each op's bool result; validation failures throw before anything is applied.
     std::vector<uint8_t> SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize, std::vector<UpdateMessage>& submitted,
                                              std::unordered_map<uint64_t, uint64_t>& tracker);
-    // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys from the device store (jg_orset_read_sets):
-    // elements in Dictionary insertion order (= ascending interned id), tags of an element in the
-    // store's canonical (sorted) order — the reference's HashSet enumeration order is not kept, so the
-    // bytes decode to the same state rather than matching byte for byte.
+    // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys from the device store (jg_orset_read_sets),
+    // byte for byte the reference's: Dictionary and HashSet enumeration orders come from the records'
+    // arrival ordinals (jg_tagrec.ord; addSet elements in ascending interned id).
     std::vector<std::string> EncodeORSetStates(const std::vector<Guid>& uids);
     // Identity of the next message SubmitClientUpdates creates (NetworkProtocol.seq; the reference keys
     // its safe-update tracker by message object, so identities only need to be unique per process).

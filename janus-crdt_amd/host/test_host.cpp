@@ -45,29 +45,10 @@ struct Rng {
     uint64_t below(uint64_t n) { return next() % n; }
 };
 
-// An ORSetMsg as a comparable value: addSet in Dictionary order with each HashSet as a sorted set;
-// removeSet as a map (its Dictionary order is first-Remove order, which the device store does not
-// keep; nothing observable depends on it); the null tag sets as sorted sets.
-std::string canonical_orset(const std::string& bytes) {
-    janus::ORSetState st = janus::wire::DecodeORSetMsg(bytes);
-    auto tags = [](std::vector<janus::Guid> v) {
-        std::sort(v.begin(), v.end(), [](const janus::Guid& a, const janus::Guid& b) { return a.lo != b.lo ? a.lo < b.lo : a.hi < b.hi; });
-        std::string o;
-        for (const auto& g : v) janus::wire::AppendGuidD(o, g);
-        return o;
-    };
-    std::string out = "A:";
-    for (const auto& e : st.addSet) out += e.first + "=" + tags(e.second) + ";";
-    std::map<std::string, std::string> rem;
-    for (const auto& e : st.removeSet) rem[e.first] = tags(e.second);
-    out += "R:";
-    for (const auto& e : rem) out += e.first + "=" + e.second + ";";
-    return out + "NA:" + tags(st.nullAddGuid) + "NR:" + tags(st.nullRemoveGuid);
-}
-
 // The GPU producer's batches against what the oracle node submitted: same UpdateMessages, same
-// NetworkProtocols (uid, seq) in the same order; PN-Counter payloads byte for byte, OR-Set payloads
-// as the same state (canonical_orset).  Returns nullptr on a match.
+// NetworkProtocols (uid, seq) in the same order, every payload byte for byte (PN-Counter and OR-Set:
+// Dictionary and HashSet enumeration orders included), and each UpdateMessage's digest equal to the
+// digest of the reference's bytes.  Returns nullptr on a match.
 const char* same_batches(const std::vector<janus::UpdateMessage>& g, const std::vector<oracle::UpdateMessage>& o) {
     if (g.size() != o.size()) return "number of UpdateMessages";
     for (size_t i = 0; i < g.size(); ++i) {
@@ -76,19 +57,14 @@ const char* same_batches(const std::vector<janus::UpdateMessage>& g, const std::
             const auto& a = g[i].update[j];
             const auto& b = o[i].update[j];
             if (!(a.uid == G(b.uid)) || a.seq != b.seq) return "message order / identity";
-            if (b.message.type == oracle::CrdtType::PNCounter) {
-                if (a.message != b.bytes) return "PN-Counter payload bytes";
-            } else if (canonical_orset(a.message) != canonical_orset(b.bytes)) {
-                return "OR-Set payload state";
-            }
+            if (a.message != b.bytes)
+                return b.message.type == oracle::CrdtType::PNCounter ? "PN-Counter payload bytes" : "OR-Set payload bytes";
         }
-        // UpdateMessage.ComputeDigest (DAGUpdateMessage.cs:32-55) over the payload bytes: the reference's
-        // bytes where they are byte-exact (PN-Counter), the GPU's own bytes for OR-Set snapshots (whose
-        // tag order within an element is canonical, not HashSet order)
+        // UpdateMessage.ComputeDigest (DAGUpdateMessage.cs:32-55) over the reference's payload bytes
         std::vector<const uint8_t*> ptr;
         std::vector<uint64_t> len;
         for (size_t j = 0; j < g[i].update.size(); ++j) {
-            const std::string& m = o[i].update[j].message.type == oracle::CrdtType::PNCounter ? o[i].update[j].bytes : g[i].update[j].message;
+            const std::string& m = o[i].update[j].bytes;
             ptr.push_back(reinterpret_cast<const uint8_t*>(m.data()));
             len.push_back(m.size());
         }

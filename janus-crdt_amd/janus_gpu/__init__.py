@@ -17,7 +17,7 @@ LIB_PATH = Path(os.environ.get("JANUS_GPU_LIB", _PKG / "lib" / "libjanusgpu.so")
 
 JG_OK, JG_EINVAL, JG_ENOMEM, JG_EOVERFLOW, JG_ETYPE, JG_EHIP, JG_ESTATE = range(7)
 NULL_ELEM = 0xFFFFFFFF
-REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8")])  # jg_tagrec
+REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8"), ("ord", "<u8")])  # jg_tagrec
 
 # Every entry point include/janus_gpu.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -94,8 +94,8 @@ _SIGS = {
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
-    "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
-    "jg_orset_merge_device": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_orset_merge_device": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_read_sets": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _u64], C.c_int),
     "jg_orset_names_sync": ([_vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_wave_begin": ([_vp, _u64, _u64], C.c_int),
@@ -423,10 +423,12 @@ def update_digests(ctx: Context, msgs, first, msg_digests: bool = False):
     return (dig, md) if msg_digests else dig
 
 
-def records(key=None, tag_lo=None, tag_hi=None, n: int = 0) -> np.ndarray:
+def records(key=None, tag_lo=None, tag_hi=None, n: int = 0, ord=None) -> np.ndarray:
+    """jg_tagrec array; ord (arrival ordinal) defaults to the record's index."""
     r = np.zeros(n if key is None else len(key), REC_DTYPE)
     if key is not None:
         r["key"], r["tag_lo"], r["tag_hi"] = key, tag_lo, tag_hi
+    r["ord"] = np.arange(r.size, dtype=np.uint64) if ord is None else ord
     return r
 
 
@@ -549,19 +551,24 @@ class ORSetStore:
         _check(load().jg_orset_lookup_all(self._h, s.size, _ptr(s), _ptr(off), _ptr(out), out.size))
         return [out[int(off[i]):int(off[i + 1])] for i in range(s.size)]
 
-    def route(self, world: int, d_add_key: int, d_add_tag: int, cap_add: int, d_rem_key: int, d_rem_tag: int, cap_rem: int):
+    def route(self, world: int, d_add_key: int, d_add_tag: int, d_add_ord: int, cap_add: int, d_rem_key: int, d_rem_tag: int,
+              d_rem_ord: int, cap_rem: int):
         """jg_orset_route: both streams partitioned by owner rank (set % world, set ids rewritten to
-        set // world) into caller DEVICE buffers; returns (add counts, tombstone counts) per rank."""
+        set // world) into caller DEVICE buffers (keys, tags, uint32 ords); returns (add counts,
+        tombstone counts) per rank."""
         ca, cr = np.zeros(world, np.uint64), np.zeros(world, np.uint64)
-        _check(load().jg_orset_route(self._h, world, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, cap_add, d_rem_key, d_rem_tag, cap_rem))
+        _check(load().jg_orset_route(self._h, world, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, d_add_ord, cap_add, d_rem_key, d_rem_tag,
+                                     d_rem_ord, cap_rem))
         return ca, cr
 
-    def merge_device(self, add_counts, rem_counts, d_add_key: int, d_add_tag: int, d_rem_key: int, d_rem_tag: int) -> None:
+    def merge_device(self, add_counts, rem_counts, d_add_key: int, d_add_tag: int, d_add_ord: int, d_rem_key: int, d_rem_tag: int,
+                     d_rem_ord: int) -> None:
         """jg_orset_merge_device: merge received runs (run r = add_counts[r] / rem_counts[r] records,
-        stored run after run in caller DEVICE buffers)."""
+        stored run after run in caller DEVICE buffers), in run order."""
         ca, cr = _arr(add_counts, np.uint64), _arr(rem_counts, np.uint64)
         assert ca.size == cr.size
-        _check(load().jg_orset_merge_device(self._h, ca.size, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, d_rem_key, d_rem_tag))
+        _check(load().jg_orset_merge_device(self._h, ca.size, _ptr(ca), _ptr(cr), d_add_key, d_add_tag, d_add_ord, d_rem_key, d_rem_tag,
+                                            d_rem_ord))
 
     def synth(self, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0) -> None:
         _check(load().jg_synth_orset(self._h, seed, n_groups, elems_per_set, add_per_group, add_u0, rem_per_group, rem_u0))

@@ -95,13 +95,14 @@ def exchange_orset(store: jg.ORSetStore, received: jg.ORSetStore, ex: Exchange |
     na, nr = received.size()
     ak, rk = _empty(torch, (na,), torch.int64, device), _empty(torch, (nr,), torch.int64, device)
     at, rt = _empty(torch, (na, 2), torch.int64, device), _empty(torch, (nr, 2), torch.int64, device)
-    sa, sr = received.route(world, ak.data_ptr(), at.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), nr)
+    ao, ro = _empty(torch, (na,), torch.int32, device), _empty(torch, (nr,), torch.int32, device)
+    sa, sr = received.route(world, ak.data_ptr(), at.data_ptr(), ao.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), ro.data_ptr(), nr)
     if ex is None:
         ga, gr = sa, sr
     else:
         ga, gr = ex.counts(sa), ex.counts(sr)
-        ak, at = ex.runs(ak, sa, ga), ex.runs(at, sa, ga)
-        rk, rt = ex.runs(rk, sr, gr), ex.runs(rt, sr, gr)
+        ak, at, ao = ex.runs(ak, sa, ga), ex.runs(at, sa, ga), ex.runs(ao, sa, ga)
+        rk, rt, ro = ex.runs(rk, sr, gr), ex.runs(rt, sr, gr), ex.runs(ro, sr, gr)
         ex.sync()
-    store.merge_device(ga, gr, ak.data_ptr(), at.data_ptr(), rk.data_ptr(), rt.data_ptr())
+    store.merge_device(ga, gr, ak.data_ptr(), at.data_ptr(), ao.data_ptr(), rk.data_ptr(), rt.data_ptr(), ro.data_ptr())
     return {"sent": (sa, sr), "received": (ga, gr)}

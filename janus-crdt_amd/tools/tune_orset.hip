@@ -45,6 +45,7 @@ __global__ void k_sum(View v, const uint32_t* cnt, unsigned long long* out) {
 struct Stream {
     unsigned long long* key = nullptr;
     uint4* tag = nullptr;
+    uint32_t* ord = nullptr;
     uint32_t* cnt = nullptr;
     uint64_t* off = nullptr;
     uint32_t* lut = nullptr;
@@ -52,11 +53,11 @@ struct Stream {
     uint32_t nch = 0, C = 0, dense = 1;
     void alloc(unsigned long long cap_slots, uint32_t chunk) {
         const unsigned long long ch = cap_slots / chunk + 2;
-        CK(hipMalloc(&key, (ch * chunk) * 8)); CK(hipMalloc(&tag, (ch * chunk) * 16));
+        CK(hipMalloc(&key, (ch * chunk) * 8)); CK(hipMalloc(&tag, (ch * chunk) * 16)); CK(hipMalloc(&ord, (ch * chunk) * 4));
         CK(hipMalloc(&cnt, ch * 4)); CK(hipMalloc(&off, (ch + 1) * 8)); CK(hipMalloc(&lut, (((ch * chunk) >> jgk::kQShift) + 2) * 4));
         C = chunk;
     }
-    View view() const { return View{key, tag, off, lut, n, nch, C, dense}; }
+    View view() const { return View{key, tag, ord, off, lut, n, nch, C, dense}; }
     void set_dense(unsigned long long nn, hipStream_t s) {
         n = nn; nch = (uint32_t)((nn + C - 1) / C); dense = 1;
         const unsigned long long nlut = (nn >> jgk::kQShift) + 2;
@@ -81,7 +82,8 @@ Times run(Stream& a, Stream& b, Stream& o, hipStream_t s) {
     CK(hipEventRecord(e[0], s));
     hipLaunchKernelGGL((jgk::k_partition<T, L>), dim3((unsigned)(((nt + 1) * L + 255) / 256)), dim3(256), 0, s, va, vb, nt + 1, part, pch);
     CK(hipEventRecord(e[1], s));
-    hipLaunchKernelGGL((jgk::k_union<OB, IT>), dim3((unsigned)nt), dim3(OB), 0, s, va, vb, part, pch, o.key, o.tag, o.cnt, jgk::Drop{nullptr, 0});
+    hipLaunchKernelGGL((jgk::k_union<OB, IT>), dim3((unsigned)nt), dim3(OB), 0, s, va, vb, part, pch, o.key, o.tag, o.ord, (uint32_t)a.n, o.cnt,
+                       jgk::Drop{nullptr, 0});
     CK(hipEventRecord(e[2], s));
     hipLaunchKernelGGL(jgk::k_finish, dim3((unsigned)((nt + 1023) / 1024)), dim3(1024), 0, s, o.cnt, (uint32_t)nt, o.off, o.lut,
                        (total >> jgk::kQShift) + 2, d_cnt);

@@ -19,7 +19,10 @@ namespace {
 
 constexpr uint32_t kNullElem = 0xFFFFFFFFu;  // elem id of C# null (ORSet.cs:136-140)
 
-struct Rec { uint64_t key, t0, t1; };  // key = set << 32 | elem; tag = {t0, t1} (16 opaque bytes)
+// key = set << 32 | elem; tag = {t0, t1} (16 opaque bytes); ord = arrival ordinal (jg_tagrec.ord:
+// tags of one (set, elem) enumerate in ascending (ord, tag); remove-Dictionary elements by their
+// smallest ord, ties by elem; add-Dictionary elements by elem id)
+struct Rec { uint64_t key, t0, t1, ord; };
 
 // Column c of key k is replica Guid {k+1, c+1}: unique per (key, replica) like the reference's
 // per-instance Guid.NewGuid() (PNCounters.cs:75).
@@ -81,26 +84,46 @@ inline Elem elem_of(uint32_t e) { return e == kNullElem ? Elem() : Elem(std::to_
 inline uint32_t elem_id(const std::string& s) { return (uint32_t)std::stoul(s); }
 inline Guid tag_of(const Rec& r) { Guid g; g.lo = r.t0; g.hi = r.t1; return g; }
 
+// ORSet objects from records: each set's add Dictionary filled in ascending elem id, its remove
+// Dictionary in ascending (smallest ord, elem), every HashSet in ascending (ord, tag) — the order the
+// engine's records encode (jg_tagrec.ord).
 void build_sets(std::map<uint32_t, ORSet>& sets, const Rec* A, uint64_t nA, const Rec* Rm, uint64_t nR) {
-    for (uint64_t i = 0; i < nA; ++i) {
-        uint32_t s = (uint32_t)(A[i].key >> 32), e = (uint32_t)A[i].key;
-        sets[s].AddTag(elem_of(e), tag_of(A[i]));
+    auto tag_order = [](const Rec& a, const Rec& b) {
+        return a.key != b.key ? a.key < b.key : a.ord != b.ord ? a.ord < b.ord : a.t0 != b.t0 ? a.t0 < b.t0 : a.t1 < b.t1;
+    };
+    std::vector<Rec> add(A, A + nA), rem(Rm, Rm + nR);
+    std::sort(add.begin(), add.end(), tag_order);  // by (set, elem): ascending id, then HashSet order
+    for (const Rec& r : add) sets[(uint32_t)(r.key >> 32)].AddTag(elem_of((uint32_t)r.key), tag_of(r));
+    std::sort(rem.begin(), rem.end(), tag_order);
+    std::unordered_map<uint64_t, uint64_t> first;  // key -> smallest ord
+    for (const Rec& r : rem) {
+        auto it = first.find(r.key);
+        if (it == first.end()) first.emplace(r.key, r.ord);
     }
-    for (uint64_t i = 0; i < nR; ++i) {
-        uint32_t s = (uint32_t)(Rm[i].key >> 32), e = (uint32_t)Rm[i].key;
-        ORSet& o = sets[s];
-        if (e == kNullElem) o.mutNullRem().insert(tag_of(Rm[i]));
-        else o.mutRemoveSet()[std::to_string(e)].insert(tag_of(Rm[i]));
+    std::stable_sort(rem.begin(), rem.end(), [&](const Rec& a, const Rec& b) {
+        const uint32_t sa = (uint32_t)(a.key >> 32), sb = (uint32_t)(b.key >> 32);
+        if (sa != sb) return sa < sb;
+        const uint64_t fa = first.at(a.key), fb = first.at(b.key);
+        return fa != fb ? fa < fb : (uint32_t)a.key < (uint32_t)b.key;
+    });
+    for (const Rec& r : rem) {
+        ORSet& o = sets[(uint32_t)(r.key >> 32)];
+        const uint32_t e = (uint32_t)r.key;
+        if (e == kNullElem) o.mutNullRem().insert(tag_of(r));
+        else o.mutRemoveSet()[std::to_string(e)].insert(tag_of(r));
     }
 }
 
+// Records of ORSet objects, sorted by (key, t0, t1); ord = the record's position in its set's
+// enumeration (Dictionary entries in order, each HashSet in order, then the null set).
 void export_sets(const std::map<uint32_t, ORSet>& sets, std::vector<Rec>& add, std::vector<Rec>& rem) {
     for (const auto& kv : sets) {
         uint64_t s = (uint64_t)kv.first << 32;
-        for (const auto& e : kv.second.addSet()) for (const auto& g : e.second) add.push_back(Rec{s | elem_id(e.first), g.lo, g.hi});
-        for (const auto& e : kv.second.removeSet()) for (const auto& g : e.second) rem.push_back(Rec{s | elem_id(e.first), g.lo, g.hi});
-        for (const auto& g : kv.second.nullAdd()) add.push_back(Rec{s | kNullElem, g.lo, g.hi});
-        for (const auto& g : kv.second.nullRem()) rem.push_back(Rec{s | kNullElem, g.lo, g.hi});
+        uint64_t oa = 0, orr = 0;
+        for (const auto& e : kv.second.addSet()) for (const auto& g : e.second) add.push_back(Rec{s | elem_id(e.first), g.lo, g.hi, oa++});
+        for (const auto& e : kv.second.removeSet()) for (const auto& g : e.second) rem.push_back(Rec{s | elem_id(e.first), g.lo, g.hi, orr++});
+        for (const auto& g : kv.second.nullAdd()) add.push_back(Rec{s | kNullElem, g.lo, g.hi, oa++});
+        for (const auto& g : kv.second.nullRem()) rem.push_back(Rec{s | kNullElem, g.lo, g.hi, orr++});
     }
     auto lt = [](const Rec& a, const Rec& b) { return a.key != b.key ? a.key < b.key : a.t0 != b.t0 ? a.t0 < b.t0 : a.t1 < b.t1; };
     std::sort(add.begin(), add.end(), lt);
@@ -127,6 +150,7 @@ inline Rec synth_orset_rec(uint64_t seed, uint64_t g, uint32_t u, uint32_t elems
     r.key = ((g / elems_per_set) << 32) | (g % elems_per_set);
     r.t0 = ((uint64_t)u << 56) | (h1 >> 8);
     r.t1 = h2;
+    r.ord = 0;  // set by the caller: the record's index in its stream (synth.hip)
     return r;
 }
 
@@ -155,6 +179,7 @@ void orc_synth_orset(uint64_t seed, uint64_t first, uint64_t n, uint32_t elems_p
     for (uint64_t i = 0; i < n; ++i) {
         uint64_t r = first + i;
         out[i] = synth_orset_rec(seed, r / per_group, u0 + (uint32_t)(r % per_group), elems_per_set);
+        out[i].ord = r;
     }
 }
 

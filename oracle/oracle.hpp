@@ -14,7 +14,7 @@
 //   Dictionary<Guid,int>          -> OrderedDict<Guid,T>   (hash map + insertion-ordered entries;
 //                                    .NET Dictionary enumerates in insertion order while no entry
 //                                    is removed, and the reference never removes single entries)
-//   HashSet<Guid>                 -> GuidSet (std::unordered_set<Guid>)
+//   HashSet<Guid>                 -> GuidSet (insertion-ordered: entries array + hash index)
 //   Dictionary<T,HashSet<Guid>>   -> OrderedDict<std::string, GuidSet>
 //   C# int '+=' (unchecked)       -> wrapping add (two's complement)
 //   LINQ Sum (checked)            -> exact prefix sums; any prefix outside T's range = overflow
@@ -25,6 +25,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <initializer_list>
 #include <map>
 #include <memory>
 #include <optional>
@@ -73,13 +74,42 @@ struct GuidGen {
     }
 };
 
-using GuidSet = std::unordered_set<Guid, GuidHash>;
+// HashSet<Guid> with .NET's enumeration order.  A .NET 6 HashSet<T> keeps its entries in an array
+// filled front to back; Add appends (when the value is new), enumeration walks that array, and only
+// Remove (a free list) could reorder later additions — the reference never removes a single tag:
+// ORSet.cs only calls Add (:138,145,149), UnionWith (:165,178,259,272,281-282), the copy constructor
+// (:182,263,276; HashSet(IEnumerable) of a HashSet copies the entry array, so the order carries over)
+// and Clear (:196-197, which resets the array).  System.Text.Json fills a deserialised HashSet with
+// Add in array order (duplicates ignored) and serialises it in enumeration order.  So the order is
+// first-insertion order, which this class keeps: a vector of entries plus a hash index.
+class GuidSet {
+  public:
+    GuidSet() = default;
+    GuidSet(std::initializer_list<Guid> l) { for (const auto& g : l) insert(g); }
+    bool insert(const Guid& g) {  // HashSet.Add: false (and no change) when present
+        if (!idx_.insert(g).second) return false;
+        items_.push_back(g);
+        return true;
+    }
+    size_t count(const Guid& g) const { return idx_.count(g); }
+    size_t size() const { return items_.size(); }
+    bool empty() const { return items_.empty(); }
+    void clear() { items_.clear(); idx_.clear(); }
+    std::vector<Guid>::const_iterator begin() const { return items_.begin(); }
+    std::vector<Guid>::const_iterator end() const { return items_.end(); }
+    const std::vector<Guid>& items() const { return items_; }
 
-inline bool SetEquals(const GuidSet& a, const GuidSet& b) {  // HashSet<T>.SetEquals
+  private:
+    std::vector<Guid> items_;
+    std::unordered_set<Guid, GuidHash> idx_;
+};
+
+inline bool SetEquals(const GuidSet& a, const GuidSet& b) {  // HashSet<T>.SetEquals (order-free)
     if (a.size() != b.size()) return false;
     for (const auto& g : a) if (!b.count(g)) return false;
     return true;
 }
+// HashSet<T>.UnionWith: src's elements in src's enumeration order, each appended if new.
 inline void UnionWith(GuidSet& dst, const GuidSet& src) { for (const auto& g : src) dst.insert(g); }
 
 // ---------------------------------------------------------------------------------------------

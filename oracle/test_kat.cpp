@@ -350,6 +350,33 @@ TEST(Json_ORSetEscapesAndRoundTrip) {  // ORSet.cs:56-69; JavaScriptEncoder.Defa
     CHECK_THROWS<json::JsonException>([&] { json::DecodeORSet("{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[]}"); }, __LINE__);
     CHECK_THROWS<json::JsonException>([&] { json::DecodeORSet("{\"addSet\":{\"\\ud800\":[]},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"); }, __LINE__);
 }
+// HashSet<Guid> / Dictionary enumeration order on the wire (.NET 6 HashSet: entries array, Add appends,
+// nothing removes single tags; oracle.hpp GuidSet header).  Tags chosen so that insertion order is
+// not their sorted order; removeSet's Dictionary order is first-Remove order, not addSet's.
+TEST(Json_ORSetEnumerationOrder) {  // ORSet.cs:134-186, 253-283, 305-308; encoded as SafeCRDT.cs:49 ships it
+    const Guid t3{3, 0}, t1{1, 0}, t2{2, 0}, t9{9, 0};
+    auto q = [](const Guid& g) { return "\"" + json::GuidD(g) + "\""; };
+    ORSet s;
+    s.AddTag(S("b"), t3); s.AddTag(S("a"), t1); s.AddTag(S("b"), t2); s.AddTag(NUL, t9); s.AddTag(NUL, t1);
+    CHECK(s.Remove(S("b")));  // removeSet["b"] = new HashSet(addSet["b"]): [t3, t2]
+    CHECK(s.Remove(S("a")));  // removeSet["a"] appended after "b"
+    const std::string e = json::EncodeORSet(s.GetLastSynchronizedUpdate());
+    CHECK_EQ(e, "{\"addSet\":{\"b\":[" + q(t3) + "," + q(t2) + "],\"a\":[" + q(t1) + "]},\"removeSet\":{\"b\":[" + q(t3) + "," + q(t2) +
+                    "],\"a\":[" + q(t1) + "]},\"nullAddGuid\":[" + q(t9) + "," + q(t1) + "],\"nullRemoveGuid\":[]}");
+    // Merge: UnionWith appends the received tags the local set lacks, in the received order; new keys
+    // are appended to the Dictionaries in the received Dictionary's order
+    ORSet r;
+    r.AddTag(S("a"), t9); r.AddTag(S("b"), t2);
+    r.ApplySynchronizedUpdate(json::DecodeORSet(e));
+    CHECK_EQ(json::EncodeORSet(r.GetLastSynchronizedUpdate()),
+             "{\"addSet\":{\"a\":[" + q(t9) + "," + q(t1) + "],\"b\":[" + q(t2) + "," + q(t3) + "]},\"removeSet\":{\"b\":[" + q(t3) + "," +
+                 q(t2) + "],\"a\":[" + q(t1) + "]},\"nullAddGuid\":[" + q(t9) + "," + q(t1) + "],\"nullRemoveGuid\":[]}");
+    // Clear resets both Dictionaries and their order
+    r.Clear();
+    r.AddTag(S("b"), t1); r.AddTag(S("a"), t3);
+    CHECK_EQ(json::EncodeORSet(r.GetLastSynchronizedUpdate()),
+             "{\"addSet\":{\"b\":[" + q(t1) + "],\"a\":[" + q(t3) + "]},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}");
+}
 // Semantics note n4 (SetEquals, not "add \ rem non-empty"), pinned by ORSet.cs:216.
 TEST(ORSet_SetEqualsNotDifference) {
     ORSet s;

@@ -4,10 +4,14 @@ import numpy as np
 from oracle_ref import NULL_ELEM, REC_DTYPE
 
 
-def recs(keys, lo, hi):
-    r = np.empty(len(keys), REC_DTYPE)
+def recs(keys, lo, hi, rng=None):
+    """Records sorted by (key, tag_lo, tag_hi), duplicate-free; ord = a random arrival order (rng), else
+    the canonical order."""
+    r = np.zeros(len(keys), REC_DTYPE)
     r["key"], r["tag_lo"], r["tag_hi"] = keys, lo, hi
-    return np.unique(r)  # sorted by (key, tag_lo, tag_hi), duplicate-free
+    r = np.unique(r)
+    r["ord"] = rng.permutation(r.size).astype(np.uint64) if rng is not None else np.arange(r.size, dtype=np.uint64)
+    return r
 
 
 def random_orset_pair(rng, n_sets=8, n_elems=6, pool=12, p_l=0.5, p_r=0.5, p_rem=0.4, p_full_rem=0.2,
@@ -39,7 +43,7 @@ def random_orset_pair(rng, n_sets=8, n_elems=6, pool=12, p_l=0.5, p_r=0.5, p_rem
         for lst in out[side][:2]:
             if lst:
                 a = np.array(lst, dtype=object)
-                res.append(recs(a[:, 0].astype(np.uint64), a[:, 1].astype(np.uint64), a[:, 2].astype(np.uint64)))
+                res.append(recs(a[:, 0].astype(np.uint64), a[:, 1].astype(np.uint64), a[:, 2].astype(np.uint64), rng))
             else:
                 res.append(np.empty(0, REC_DTYPE))
     return tuple(res)  # La, Lr, Ra, Rr

@@ -9,7 +9,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parent.parent
 LIB = ROOT / "oracle" / "build" / "liboracle.so"
-REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8")])
+REC_DTYPE = np.dtype([("key", "<u8"), ("tag_lo", "<u8"), ("tag_hi", "<u8"), ("ord", "<u8")])  # jg_tagrec
 NULL_ELEM = 0xFFFFFFFF
 
 _vp, _u64, _u32, _i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
@@ -109,6 +109,62 @@ def pnc_apply_ops(P, N, key, col, delta, is_n):
 # ---- OR-Set ----
 def _recs(a):
     return np.ascontiguousarray(a, REC_DTYPE)
+
+
+def canon(r) -> np.ndarray:
+    """(key, tag_lo, tag_hi) rows of a record stream, in its stored (canonical, sorted) order."""
+    r = _recs(r)
+    return np.stack([r["key"], r["tag_lo"], r["tag_hi"]], 1) if r.size else np.zeros((0, 3), np.uint64)
+
+
+def enum_view(r, rem: bool) -> np.ndarray:
+    """The reference's enumeration order of one record stream (jg_tagrec.ord): (key, tag_lo, tag_hi) rows,
+    sets ascending; within a set the Dictionary's elements — add stream: ascending elem id; tombstone
+    stream: ascending smallest ord (first insertion into removeSet), then elem — each element's tags by
+    (ord, tag); the null element's HashSet last."""
+    r = _recs(r)
+    if r.size == 0:
+        return np.zeros((0, 3), np.uint64)
+    key, lo, hi, o = r["key"], r["tag_lo"], r["tag_hi"], r["ord"]
+    elem, sid = key & np.uint64(0xFFFFFFFF), key >> np.uint64(32)
+    isnull = (elem == np.uint64(NULL_ELEM)).astype(np.uint8)
+    if rem:
+        uk, inv = np.unique(key, return_inverse=True)
+        first = np.full(uk.size, np.iinfo(np.uint64).max, np.uint64)
+        np.minimum.at(first, inv, o)
+        grp = first[inv]
+    else:
+        grp = elem
+    idx = np.lexsort((hi, lo, o, elem, grp, isnull, sid))
+    return np.stack([key[idx], lo[idx], hi[idx]], 1)
+
+
+def same_stream(g, e, rem: bool) -> bool:
+    """Same records and the same enumeration order (ords may differ in value, not in order)."""
+    return np.array_equal(canon(g), canon(e)) and np.array_equal(enum_view(g, rem), enum_view(e, rem))
+
+
+def same_orset(ga, gr, ea, er) -> bool:
+    return same_stream(ga, ea, False) and same_stream(gr, er, True)
+
+
+def enum_is_canonical(r, rem: bool) -> bool:
+    """O(n) check that a stream's enumeration order is its canonical (sorted) order: ords increase
+    within every element and, for tombstones, elements' first ords increase within every set."""
+    r = _recs(r)
+    if r.size < 2:
+        return True
+    key, o = r["key"], r["ord"]
+    same = key[1:] == key[:-1]
+    if not np.all(~same | (o[1:] > o[:-1])):
+        return False
+    if not rem:
+        return True
+    head = np.concatenate([[True], ~same])
+    hk, ho = key[head], o[head]  # each element's first record = its smallest ord (ords increase within it)
+    hs = hk >> np.uint64(32)
+    notnull = (hk[1:] & np.uint64(0xFFFFFFFF)) != np.uint64(NULL_ELEM)
+    return bool(np.all((hs[1:] != hs[:-1]) | ~notnull | (ho[1:] > ho[:-1])))
 
 
 def orset_merge(La, Lr, Ra, Rr):
@@ -217,14 +273,17 @@ def json_decode_orset(payload: bytes):
     return out
 
 
-def orset_apply_json(set_ids, msgs, names=None):
+def orset_apply_json(set_ids, msgs, names=None, state=None):
     """The stable-apply loop over ORSetMsg payloads (SafeCRDT.ApplyUpdateStable -> Decode -> Merge in
     commit order) with element strings interned per set at first insertion (ids never reused).
     names: {set: {name bytes: id}} carried between calls (updated in place), with "next" ids in
-    names[("next", set)].  Returns (add records, tombstone records, first bad message or None, its
-    code: "EINVAL" for a Decode error, "ESTATE" for an empty add tag set), records sorted."""
+    names[("next", set)].  state: {(side, key): {tag: None}} — the Dictionaries and HashSets in their
+    insertion order (Merge appends new keys and UnionWith appends new tags, ORSet.cs:255-282) — carried
+    between calls (updated in place) when given.  Returns (add records, tombstone records, first bad
+    message or None, its code: "EINVAL" for a Decode error, "ESTATE" for an empty add tag set): the whole
+    state, sorted, ord = the record's position in its stream's enumeration."""
     names = {} if names is None else names
-    add, rem = set(), set()
+    state = {} if state is None else state
     bad, code = None, None
     for m, (sid, p) in enumerate(zip(set_ids, msgs)):
         d = json_decode_orset(p)
@@ -243,10 +302,15 @@ def orset_apply_json(set_ids, msgs, names=None):
                     tab[name] = names.get(("next", int(sid)), 0)
                     names[("next", int(sid))] = tab[name] + 1
                 eid = tab[name]
-            for lo, hi in tags:
-                (rem if side else add).add((int(sid) << 32 | eid, lo, hi))
-    mk = lambda s: np.array(sorted(s), dtype=REC_DTYPE) if s else np.zeros(0, REC_DTYPE)
-    return mk(add), mk(rem), bad, code
+            hs = state.setdefault((side, int(sid) << 32 | eid), {})
+            for t in tags:
+                hs.setdefault(t)
+    out = ([], [])
+    for (side, key), hs in state.items():  # dict order = first insertion, across sets
+        for lo, hi in hs:
+            out[side].append((key, lo, hi, len(out[side])))
+    mk = lambda v: np.sort(np.array(v, dtype=REC_DTYPE), order=["key", "tag_lo", "tag_hi"]) if v else np.zeros(0, REC_DTYPE)
+    return mk(out[0]), mk(out[1]), bad, code
 
 
 # ---- UpdateMessage.ComputeDigest (oracle/digest.hpp) ----

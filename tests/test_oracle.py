@@ -123,8 +123,8 @@ def test_orset_merge_bridge_is_union():
     rng = np.random.default_rng(11)
     La, Lr, Ra, Rr = random_orset_pair(rng)
     oa, orr = orc.orset_merge(La, Lr, Ra, Rr)
-    assert np.array_equal(oa, np.unique(np.concatenate([La, Ra])))
-    assert np.array_equal(orr, np.unique(np.concatenate([Lr, Rr])))
+    assert np.array_equal(orc.canon(oa), np.unique(np.concatenate([orc.canon(La), orc.canon(Ra)]), axis=0))
+    assert np.array_equal(orc.canon(orr), np.unique(np.concatenate([orc.canon(Lr), orc.canon(Rr)]), axis=0))
 
 
 def test_orset_contains_bridge_rule():
@@ -146,7 +146,7 @@ def test_orset_contains_bridge_rule():
 def test_orset_lookup_all_order():
     # Add-only keys first (insertion order), then keys in both with differing sets, null last.
     def rec(s, e, t):
-        return ((s << 32) | e, t, 0)
+        return ((s << 32) | e, t, 0, 0)
 
     add = np.array([rec(0, 1, 5), rec(0, 2, 6), rec(0, 3, 7), rec(0, 3, 8), rec(0, orc.NULL_ELEM, 9)], orc.REC_DTYPE)
     rem = np.array([rec(0, 1, 5), rec(0, 3, 7)], orc.REC_DTYPE)
@@ -187,6 +187,7 @@ def test_synth_orset_formula():
         assert int(got[i]["key"]) == ((g // 10) << 32) | (g % 10)
         assert int(got[i]["tag_lo"]) == (u << 56) | (h1 >> 8)
         assert int(got[i]["tag_hi"]) == h2
+        assert int(got[i]["ord"]) == r  # arrival ordinal = the record's index in its stream
 
 
 # ---------------------------------------------------------------- golden fixtures
@@ -217,3 +218,34 @@ def test_orset_apply_ops_bridge_reference_sequence():
     assert sorted(orc.orset_lookup_all(a, r, 0)) == [2, 3]
     a2, r2, res2 = orc.orset_apply_ops(a, r, [0, 0], [0, 1], [3, 1], [0, 9], [0, 0])
     assert list(res2) == [1, 1] and list(orc.orset_lookup_all(a2, r2, 0)) == [1] and r2.size == 0
+
+
+# ---------------------------------------------------------------- enumeration order (jg_tagrec.ord)
+def test_orset_merge_bridge_enumeration_order():
+    """HashSet / Dictionary insertion order through the record bridge (oracle_ref.enum_view): Merge
+    appends R's new tags after L's in R's order, and R's new tombstone elements after L's in R's
+    Dictionary order (ORSet.cs:255-282; oracle/oracle.hpp GuidSet)."""
+    def rec(e, t, o):
+        return (e, t, 0, o)
+
+    La = np.array([rec(1, 5, 0), rec(1, 6, 1), rec(2, 7, 2)], orc.REC_DTYPE)   # 1: [5, 6]; 2: [7]
+    Lr = np.array([rec(2, 7, 0)], orc.REC_DTYPE)                               # removeSet: 2
+    Ra = np.array([rec(1, 4, 1), rec(1, 6, 2), rec(1, 9, 0)], orc.REC_DTYPE)   # 1: [9, 4, 6]
+    Rr = np.array([rec(1, 4, 1), rec(1, 9, 0), rec(3, 1, 5)], orc.REC_DTYPE)   # removeSet: 1 [9, 4], then 3
+    oa, orr = orc.orset_merge(La, Lr, Ra, Rr)
+    assert [(int(k), int(t)) for k, t, _ in orc.enum_view(oa, False)] == [(1, 5), (1, 6), (1, 9), (1, 4), (2, 7)]
+    assert [(int(k), int(t)) for k, t, _ in orc.enum_view(orr, True)] == [(2, 7), (1, 9), (1, 4), (3, 1)]
+    # the helpers agree with an explicit canonical ordering
+    assert orc.same_orset(oa, orr, oa, orr) and not orc.same_stream(oa, Ra, False)
+
+
+def test_orset_apply_json_enumeration_order():
+    """The Python wire oracle keeps first-insertion order across messages (UnionWith appends)."""
+    import jsongen as J
+    g = [(i, 0) for i in range(1, 6)]
+    m1 = J.encode_orset([("x", [g[2], g[0]])], [("x", [g[0]])])
+    m2 = J.encode_orset([("y", [g[4]]), ("x", [g[1], g[0]])], [("y", [g[4]]), ("x", [g[2]])])
+    ea, er, bad, _ = orc.orset_apply_json([0, 0], [m1, m2])
+    assert bad is None
+    assert [(int(k), int(t)) for k, t, _ in orc.enum_view(ea, False)] == [(0, 3), (0, 1), (0, 2), (1, 5)]
+    assert [(int(k), int(t)) for k, t, _ in orc.enum_view(er, True)] == [(0, 1), (0, 3), (1, 5)]

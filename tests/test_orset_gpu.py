@@ -1,7 +1,9 @@
 """GPU parity of the OR-Set path (through the C ABI) against the oracle.
 
 Oracle = dictionary-faithful ORSet<string?> (oracle/oracle.hpp) pinned by the reference's
-ORSetTests.cs known answers; comparisons are exact on canonical (sorted) record streams.
+ORSetTests.cs known answers; comparisons are exact on canonical (sorted) record streams AND on the
+reference's enumeration order (HashSet / Dictionary insertion order carried by jg_tagrec.ord:
+oracle_ref.same_orset).
 """
 from pathlib import Path
 
@@ -37,15 +39,17 @@ def test_union_matches_oracle(ctx, seed, n_sets, n_elems, pool):
     try:
         jg.ORSetStore.union(a, b, out)
         ga, gr = out.read()
-        assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+        assert orc.same_orset(ga, gr, ea, er)
         s, e = _queries(n_sets, min(n_elems, 40))
         assert np.array_equal(out.contains(s, e), orc.orset_contains(ea, er, s, e))
         # in-place merge of a device store and of host records give the same state
         a.merge_store(b)
-        assert all(np.array_equal(x, y) for x, y in zip(a.read(), (ea, er)))
+        assert orc.same_orset(*a.read(), ea, er)
+        # the other direction: R <- L (same records, the other enumeration order)
+        fa, fr = orc.orset_merge(Ra, Rr, La, Lr)
         c = _store(ctx, Ra, Rr)
         c.merge(La, Lr)
-        assert all(np.array_equal(x, y) for x, y in zip(c.read(), (ea, er)))
+        assert orc.same_orset(*c.read(), fa, fr)
         c.close()
     finally:
         for h in (a, b, out):
@@ -64,15 +68,17 @@ def test_union_duplicates_and_tiles(ctx, n):
     A = _interleaved(n, 0, 2)
     B = _interleaved(n, 1, 2)
     empty = np.empty(0, jg.REC_DTYPE)
-    cases = [(A, A), (A, B), (A, np.unique(np.concatenate([A[::2], B[: n // 2]]))), (A, empty), (empty, B)]
+    mix = np.unique(np.concatenate([A[::2], B[: n // 2]]))
+    mix["ord"] = np.random.default_rng(n).permutation(mix.size)
+    cases = [(A, A), (A, B), (A, mix), (A, empty), (empty, B)]
     for x, y in cases:
-        exp = np.unique(np.concatenate([x, y]))
+        exp, _ = orc.orset_merge(x, empty, y, empty)
         a, b = _store(ctx, x, empty), _store(ctx, y, empty)
         out = jg.ORSetStore(ctx, len(x) + len(y), 0)
         try:
             jg.ORSetStore.union(a, b, out)
             ga, gr = out.read()
-            assert np.array_equal(ga, exp) and gr.size == 0
+            assert orc.same_stream(ga, exp, False) and gr.size == 0
         finally:
             for h in (a, b, out):
                 h.close()
@@ -84,16 +90,15 @@ def test_equal_keys_long_runs(ctx):
     lo = rng.integers(0, 1 << 62, 40_000, dtype=np.uint64)
     hi = rng.integers(0, 1 << 62, 40_000, dtype=np.uint64)
     key = np.full(40_000, (5 << 32) | 3, np.uint64)
-    A = recs(key[:25_000], lo[:25_000], hi[:25_000])
-    B = recs(key[15_000:], lo[15_000:], hi[15_000:])
-    exp = np.unique(np.concatenate([A, B]))
+    A = recs(key[:25_000], lo[:25_000], hi[:25_000], rng)
+    B = recs(key[15_000:], lo[15_000:], hi[15_000:], rng)
+    ea, er = orc.orset_merge(A, A[:100], B, B[:50])
     a, b = _store(ctx, A, A[:100]), _store(ctx, B, B[:50])
     out = jg.ORSetStore(ctx, len(A) + len(B), 150)
     try:
         jg.ORSetStore.union(a, b, out)
         ga, gr = out.read()
-        assert np.array_equal(ga, exp)
-        assert np.array_equal(gr, np.unique(np.concatenate([A[:100], B[:50]])))
+        assert orc.same_orset(ga, gr, ea, er)  # one HashSet of 35k tags: its whole enumeration order
         assert out.contains([5], [3])[0] == 1
     finally:
         for h in (a, b, out):
@@ -103,7 +108,7 @@ def test_equal_keys_long_runs(ctx):
 def test_reference_scenarios_on_gpu(ctx):
     """ORSetTests.cs:102-129 (Multiple) and :314-328 (MergeNull) replayed as record states."""
     def rec(s, e, t):
-        return ((s << 32) | e, t, 7)
+        return ((s << 32) | e, t, 7, 0)
 
     NUL = jg.NULL_ELEM
     # set1 = {1: t1}, set2 = {2: t2}; set1 <- set2  => 1, 2 present
@@ -128,15 +133,19 @@ def test_reference_scenarios_on_gpu(ctx):
 
 
 def test_unsorted_or_duplicate_input_rejected(ctx):
-    a = np.array([(5, 1, 1), (4, 1, 1)], jg.REC_DTYPE)
-    d = np.array([(5, 1, 1), (5, 1, 1)], jg.REC_DTYPE)
+    a = np.array([(5, 1, 1, 0), (4, 1, 1, 1)], jg.REC_DTYPE)
+    d = np.array([(5, 1, 1, 0), (5, 1, 1, 1)], jg.REC_DTYPE)
     s = jg.ORSetStore(ctx, 4, 4)
     try:
         for bad in (a, d):
             with pytest.raises(jg.JanusError) as e:
                 s.load(bad, np.empty(0, jg.REC_DTYPE))
             assert e.value.code == jg.JG_ESTATE
-        s.load(np.sort(a), np.empty(0, jg.REC_DTYPE))  # the store stays usable
+        big = np.array([(5, 1, 1, 1 << 32)], jg.REC_DTYPE)  # ords are 32-bit on the device
+        with pytest.raises(jg.JanusError) as e:
+            s.load(big, np.empty(0, jg.REC_DTYPE))
+        assert e.value.code == jg.JG_EINVAL
+        s.load(np.sort(a, order=["key", "tag_lo", "tag_hi"]), np.empty(0, jg.REC_DTYPE))  # the store stays usable
         assert s.size() == (2, 0)
     finally:
         s.close()
@@ -148,7 +157,7 @@ def test_golden_fixture(ctx):
     try:
         s.merge(z["Ra"], z["Rr"])
         ga, gr = s.read()
-        assert np.array_equal(ga, z["out_add"]) and np.array_equal(gr, z["out_rem"])
+        assert orc.same_orset(ga, gr, z["out_add"], z["out_rem"])
         assert np.array_equal(s.contains(z["q_set"], z["q_elem"]), z["contains"])
     finally:
         s.close()
@@ -178,10 +187,14 @@ def test_full_size_c3(ctx):
         jg.ORSetStore.union(L, R, out)
         assert out.size() == (150_000_000, 30_000_000)
         ga, gr = out.read()
-        assert np.array_equal(gr, orc.synth_orset(seed, 0, 30_000_000, E, 3, 0))
+        # records in closed form; enumeration order: L's tags (ords kept), then R's new ones (ords after
+        # L's), which is ascending u = canonical order within every element
+        assert np.array_equal(orc.canon(gr), orc.canon(orc.synth_orset(seed, 0, 30_000_000, E, 3, 0)))
+        assert orc.enum_is_canonical(gr, True)
         del gr
         for lo in range(0, 150_000_000, 25_000_000):
-            assert np.array_equal(ga[lo:lo + 25_000_000], orc.synth_orset(seed, lo, 25_000_000, E, 15, 0)), lo
+            assert np.array_equal(orc.canon(ga[lo:lo + 25_000_000]), orc.canon(orc.synth_orset(seed, lo, 25_000_000, E, 15, 0))), lo
+        assert orc.enum_is_canonical(ga, False)
         del ga
         rng = np.random.default_rng(3)
         sets = rng.integers(0, G // E, 100_000).astype(np.uint32)
@@ -215,7 +228,7 @@ def test_apply_ops_match_oracle(ctx, seed, n_sets, n_elems, n_ops, p_clear):
     finally:
         s.close()
     assert np.array_equal(gres, eres)
-    assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+    assert orc.same_orset(ga, gr, ea, er)
 
 
 def test_apply_ops_rejects_bad_op(ctx):
@@ -232,7 +245,7 @@ def test_apply_ops_rejects_bad_op(ctx):
 def _rand_recs(rng, n, n_sets, n_elems, tag_pool):
     key = (rng.integers(0, n_sets, n).astype(np.uint64) << np.uint64(32)) | rng.integers(0, n_elems, n).astype(np.uint64)
     t = rng.integers(0, tag_pool, n).astype(np.uint64)
-    return recs(key, t * np.uint64(0x9E3779B97F4A7C15), t)
+    return recs(key, t * np.uint64(0x9E3779B97F4A7C15), t, rng)
 
 
 def test_chunked_chain_and_mass_clear(ctx):
@@ -257,9 +270,9 @@ def test_chunked_chain_and_mass_clear(ctx):
                 s.merge_store(src)
                 src.close()
             d.merge(xa, xr)
-            acc_a, acc_r = np.unique(np.concatenate([acc_a, xa])), np.unique(np.concatenate([acc_r, xr]))
+            acc_a, acc_r = orc.orset_merge(acc_a, acc_r, xa, xr)
             ga, gr = s.read()
-            assert np.array_equal(ga, acc_a) and np.array_equal(gr, acc_r), step
+            assert orc.same_orset(ga, gr, acc_a, acc_r), step
         # Clear sets 20..379 through the op path: most of the stream's chunks become empty
         sets = np.arange(20, 380, dtype=np.uint32)
         ops = np.full(len(sets), 3, np.uint8)
@@ -267,7 +280,7 @@ def test_chunked_chain_and_mass_clear(ctx):
         ea, er, eres = orc.orset_apply_ops(acc_a, acc_r, sets, sets * 0, ops, zero, zero)
         assert np.array_equal(s.apply_ops(sets, sets * 0, ops, zero, zero), eres)
         ga, gr = s.read()
-        assert np.array_equal(ga, ea) and np.array_equal(gr, er)
+        assert orc.same_orset(ga, gr, ea, er)
         q_s = rng.integers(0, n_sets, 5000).astype(np.uint32)
         q_e = rng.integers(0, n_elems, 5000).astype(np.uint32)
         assert np.array_equal(s.contains(q_s, q_e), orc.orset_contains(ea, er, q_s, q_e))
@@ -275,14 +288,14 @@ def test_chunked_chain_and_mass_clear(ctx):
         out = jg.ORSetStore(ctx, 0, 0)
         jg.ORSetStore.union(d, s, out)
         ua, ur = out.read()
-        assert np.array_equal(ua, np.unique(np.concatenate([acc_a, ea]))) and np.array_equal(ur, np.unique(np.concatenate([acc_r, er])))
+        assert orc.same_orset(ua, ur, *orc.orset_merge(acc_a, acc_r, ea, er))
         jg.ORSetStore.union(s, s, out)
         ua, ur = out.read()
-        assert np.array_equal(ua, ea) and np.array_equal(ur, er)
+        assert orc.same_orset(ua, ur, ea, er)
         xa = _rand_recs(rng, 30_000, n_sets, n_elems, pool)
         s.merge(xa, empty)
         ga, _ = s.read()
-        assert np.array_equal(ga, np.unique(np.concatenate([ea, xa])))
+        assert orc.same_stream(ga, orc.orset_merge(ea, er, xa, empty)[0], False)
         out.close()
     finally:
         s.close()
@@ -327,3 +340,70 @@ def test_read_sets_matches_full_read(ctx, n_sets):
             assert np.array_equal(ga, ea) and np.array_equal(gr, er), sid
     finally:
         s.close()
+
+
+def test_ord_renumbering_keeps_order(ctx, monkeypatch):
+    """Device ords are 32-bit: a union whose ords would pass the limit renumbers its inputs first (order
+    kept, ties by record order).  With the limit lowered to force a renumbering on most merges, a chain
+    of merges (host records, device stores, op batches) still enumerates exactly like the oracle."""
+    monkeypatch.setenv("JANUS_TEST_ORD_LIMIT", "9000")
+    rng = np.random.default_rng(31)
+    n_sets, n_elems, pool = 30, 8, 40
+    empty = np.empty(0, jg.REC_DTYPE)
+    acc_a, acc_r = empty, empty
+    s = jg.ORSetStore(ctx, 0, 0)
+    try:
+        for step in range(10):
+            xa = _rand_recs(rng, 2500, n_sets, n_elems, pool)
+            xr = _rand_recs(rng, 900, n_sets, n_elems, pool)
+            xa["ord"] = xa["ord"] + np.uint64(step * 500)  # ords far from 0: spans add up quickly
+            if step % 3 == 0:
+                src = _store(ctx, xa, xr)
+                s.merge_store(src)
+                src.close()
+            else:
+                s.merge(xa, xr)
+            acc_a, acc_r = orc.orset_merge(acc_a, acc_r, xa, xr)
+            if step % 4 == 3:  # a batch of ops between merges
+                n_ops = 200
+                sets = rng.integers(0, n_sets, n_ops).astype(np.uint32)
+                elems = rng.integers(0, n_elems, n_ops).astype(np.uint32)
+                ops = np.where(rng.random(n_ops) < 0.5, 1, 2).astype(np.uint8)
+                lo = rng.integers(1, 1 << 63, n_ops, dtype=np.uint64)
+                hi = rng.integers(1, 1 << 63, n_ops, dtype=np.uint64)
+                acc_a, acc_r, eres = orc.orset_apply_ops(acc_a, acc_r, sets, elems, ops, lo, hi)
+                assert np.array_equal(s.apply_ops(sets, elems, ops, lo, hi), eres)
+            ga, gr = s.read()
+            assert orc.same_orset(ga, gr, acc_a, acc_r), step
+            assert int(ga["ord"].max()) < 9000 and int(gr["ord"].max()) < 9000
+    finally:
+        s.close()
+
+
+def test_enumeration_order_scenario(ctx):
+    """The oracle's Json_ORSetEnumerationOrder KAT (oracle/test_kat.cpp) on the device: tags enumerate in
+    insertion order, not sorted; the tombstone Dictionary in first-Remove order; Merge appends."""
+    K = lambda e: (0 << 32) | e  # noqa: E731
+    b, a, NUL = 1, 0, jg.NULL_ELEM
+    t3, t1, t2, t9 = (3, 0), (1, 0), (2, 0), (9, 0)
+    s = jg.ORSetStore(ctx, 0, 0)
+    r = jg.ORSetStore(ctx, 0, 0)
+    try:
+        # s: Add(b,t3) Add(a,t1) Add(b,t2) Add(null,t9) Add(null,t1); Remove(b); Remove(a)
+        res = s.apply_ops([0] * 7, [b, a, b, NUL, NUL, b, a], [1, 1, 1, 1, 1, 2, 2],
+                          [t3[0], t1[0], t2[0], t9[0], t1[0], 0, 0], [0] * 7)
+        assert list(res) == [1] * 7
+        ga, gr = s.read()
+        va, vr = orc.enum_view(ga, False), orc.enum_view(gr, True)
+        assert [(int(k), int(lo)) for k, lo, _ in va] == [(K(a), 1), (K(b), 3), (K(b), 2), (K(NUL), 9), (K(NUL), 1)]
+        assert [(int(k), int(lo)) for k, lo, _ in vr] == [(K(b), 3), (K(b), 2), (K(a), 1)]
+        # r: Add(a,t9) Add(b,t2); then merge s's state: a gets t1 appended, b gets t3 appended
+        r.apply_ops([0, 0], [a, b], [1, 1], [t9[0], t2[0]], [0, 0])
+        r.merge_store(s)
+        ga, gr = r.read()
+        va, vr = orc.enum_view(ga, False), orc.enum_view(gr, True)
+        assert [(int(k), int(lo)) for k, lo, _ in va] == [(K(a), 9), (K(a), 1), (K(b), 2), (K(b), 3), (K(NUL), 9), (K(NUL), 1)]
+        assert [(int(k), int(lo)) for k, lo, _ in vr] == [(K(b), 3), (K(b), 2), (K(a), 1)]
+    finally:
+        s.close()
+        r.close()

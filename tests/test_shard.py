@@ -82,7 +82,7 @@ def _worker(rank, world, port, q):
         sa, ra_ = ref.route_records(Ra, world)
         sr, rr_ = ref.route_records(Rr, world)
         ga, gr = ex.counts(sa), ex.counts(sr)
-        view = lambda x: torch.from_numpy(x.view(np.int64).reshape(-1, 3))
+        view = lambda x: torch.from_numpy(x.view(np.int64).reshape(-1, 4))
         ia = ex.runs(view(ra_), sa, ga).numpy().reshape(-1).view(orc.REC_DTYPE)
         ir = ex.runs(view(rr_), sr, gr).numpy().reshape(-1).view(orc.REC_DTYPE)
         ma, mr = ref.shard_records(La, world, rank), ref.shard_records(Lr, world, rank)
@@ -93,7 +93,7 @@ def _worker(rank, world, port, q):
         ea, er = La, Lr
         for a, r in recv:
             ea, er = orc.orset_merge(ea, er, a, r)
-        ok_orset = np.array_equal(ma, ref.shard_records(ea, world, rank)) and np.array_equal(mr, ref.shard_records(er, world, rank))
+        ok_orset = orc.same_orset(ma, mr, ref.shard_records(ea, world, rank), ref.shard_records(er, world, rank))
         q.put((rank, ok_pnc, ok_counts, ok_orset, ""))
     except Exception as e:  # report, do not hang the parent
         q.put((rank, False, False, False, repr(e)))

@@ -158,17 +158,27 @@ def _route_store(ctx, add, rem, world):
     na, nr = len(add), len(rem)
     ak, rk = torch.empty(na, dtype=torch.int64, device=dev), torch.empty(nr, dtype=torch.int64, device=dev)
     at, rt = torch.empty((na, 2), dtype=torch.int64, device=dev), torch.empty((nr, 2), dtype=torch.int64, device=dev)
-    ca, cr = src.route(world, ak.data_ptr(), at.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), nr)
+    ao, ro = torch.empty(na, dtype=torch.int32, device=dev), torch.empty(nr, dtype=torch.int32, device=dev)
+    ca, cr = src.route(world, ak.data_ptr(), at.data_ptr(), ao.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), ro.data_ptr(), nr)
     src.close()
 
-    def recs(k, t):
+    def recs(k, t, o):
         r = np.empty(k.shape[0], jg.REC_DTYPE)
         r["key"] = k.cpu().numpy().view(np.uint64)
         tt = t.cpu().numpy().view(np.uint64).reshape(-1, 2)
         r["tag_lo"], r["tag_hi"] = tt[:, 0], tt[:, 1]
+        r["ord"] = o.cpu().numpy().view(np.uint32)
         return r
 
-    return ca, cr, recs(ak, at), recs(rk, rt)
+    return ca, cr, recs(ak, at, ao), recs(rk, rt, ro)
+
+
+def _dev_recs(recs, dev):
+    """A record array as the (key, tag, ord) device buffers jg_orset_merge_device reads."""
+    k = torch.from_numpy(recs["key"].view(np.int64).copy()).to(dev)
+    t = torch.from_numpy(np.stack([recs["tag_lo"], recs["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+    o = torch.from_numpy(recs["ord"].astype(np.uint32).view(np.int32).copy()).to(dev)
+    return k, t, o
 
 
 @pytest.mark.parametrize("world", [1, 3, 8])
@@ -194,7 +204,8 @@ def test_orset_route_of_a_union_output(ctx):
     dev = _dev(ctx)
     ak, rk = torch.empty(na, dtype=torch.int64, device=dev), torch.empty(nr, dtype=torch.int64, device=dev)
     at, rt = torch.empty((na, 2), dtype=torch.int64, device=dev), torch.empty((nr, 2), dtype=torch.int64, device=dev)
-    ca, cr = a.route(5, ak.data_ptr(), at.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), nr)
+    ao, ro = torch.empty(na, dtype=torch.int32, device=dev), torch.empty(nr, dtype=torch.int32, device=dev)
+    ca, cr = a.route(5, ak.data_ptr(), at.data_ptr(), ao.data_ptr(), na, rk.data_ptr(), rt.data_ptr(), ro.data_ptr(), nr)
     ea, er = orc.orset_merge(La, Lr, Ra, Rr)
     assert np.array_equal(ca, ref.route_records(ea, 5)[0]) and np.array_equal(cr, ref.route_records(er, 5)[0])
     assert np.array_equal(ak.cpu().numpy().view(np.uint64), ref.route_records(ea, 5)[1]["key"])
@@ -224,15 +235,13 @@ def test_orset_sharded_keyspace_in_one_process(ctx, world):
             cnt_a.append(int(ca[d]))
             cnt_r.append(int(cr[d]))
         A, Rm = np.concatenate(runs_a), np.concatenate(runs_r)
-        ak = torch.from_numpy(A["key"].view(np.int64).copy()).to(dev)
-        at = torch.from_numpy(np.stack([A["tag_lo"], A["tag_hi"]], 1).view(np.int64).copy()).to(dev)
-        rk = torch.from_numpy(Rm["key"].view(np.int64).copy()).to(dev)
-        rt = torch.from_numpy(np.stack([Rm["tag_lo"], Rm["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+        ak, at, ao = _dev_recs(A, dev)
+        rk, rt, ro = _dev_recs(Rm, dev)
         torch.cuda.synchronize(dev)
-        s.merge_device(cnt_a, cnt_r, ak.data_ptr(), at.data_ptr(), rk.data_ptr(), rt.data_ptr())
+        s.merge_device(cnt_a, cnt_r, ak.data_ptr(), at.data_ptr(), ao.data_ptr(), rk.data_ptr(), rt.data_ptr(), ro.data_ptr())
         ga, gr = s.read()
         s.close()
-        assert np.array_equal(ga, ref.shard_records(ea, world, d)) and np.array_equal(gr, ref.shard_records(er, world, d))
+        assert orc.same_orset(ga, gr, ref.shard_records(ea, world, d), ref.shard_records(er, world, d))
 
 
 def test_orset_merge_device_rejects_unsorted_run(ctx):
@@ -242,12 +251,11 @@ def test_orset_merge_device_rejects_unsorted_run(ctx):
     s.load(La, Lr)
     bad = Ra[::-1].copy()
     dev = _dev(ctx)
-    ak = torch.from_numpy(bad["key"].view(np.int64).copy()).to(dev)
-    at = torch.from_numpy(np.stack([bad["tag_lo"], bad["tag_hi"]], 1).view(np.int64).copy()).to(dev)
+    ak, at, ao = _dev_recs(bad, dev)
     e0 = torch.empty(0, dtype=torch.int64, device=dev)
     torch.cuda.synchronize(dev)
     with pytest.raises(jg.JanusError) as e:
-        s.merge_device([len(bad)], [0], ak.data_ptr(), at.data_ptr(), e0.data_ptr(), e0.data_ptr())
+        s.merge_device([len(bad)], [0], ak.data_ptr(), at.data_ptr(), ao.data_ptr(), e0.data_ptr(), e0.data_ptr(), e0.data_ptr())
     assert e.value.code == jg.JG_ESTATE
     ga, gr = s.read()  # unchanged
     assert np.array_equal(ga, La) and np.array_equal(gr, Lr)
@@ -305,7 +313,7 @@ def _two_rank_worker(rank, world, port, q):
             ea, er = La, Lr
             for a, r in recv:
                 ea, er = orc_.orset_merge(ea, er, a, r)
-            ok_orset = np.array_equal(ga, ref_.shard_records(ea, world, rank)) and np.array_equal(gr, ref_.shard_records(er, world, rank))
+            ok_orset = orc_.same_orset(ga, gr, ref_.shard_records(ea, world, rank), ref_.shard_records(er, world, rank))
             for h in (s, rows, o, src):
                 h.close()
         q.put((rank, ok_pnc, ok_orset, ""))
