@@ -7,8 +7,11 @@ jg_pnc_merge_batch over the whole batch = 640M cell merges (P and N).  The OR-Se
 1M sets, 100M adds + 20M tombstones per side) runs in the same job and is reported under "orset".
 
 Multi-GPU (`torch.distributed.run --nproc-per-node N`): one process per GPU, the keyspace is
-hash-sharded so every rank merges its own fixed 10M-key shard (weak scaling); the data path has no
-collective.  torch.distributed only provides the barrier and the max-over-ranks of the timings.
+hash-sharded; the data path has no collective, torch.distributed only provides the barrier and the
+max-over-ranks of the timings.  At N > 1 the PN-Counter workload is BASELINE configs[3] (C4: 200M keys
+x 128 replicas over 8 GPUs): by default every rank merges its own 25M x 128 shard (weak scaling,
+--scaling weak); --scaling strong splits a fixed 200M-key keyspace over the N ranks (N >= 4: the
+819.2 GB of A and B do not fit fewer MI355X).  The OR-Set leg keeps a C3-shaped shard per rank.
 
 Timing: W untimed warmup steps, then K steps bracketed by barrier + device sync on both sides; the
 wall time is max over ranks.  The kernel's own average duration comes from HIP events recorded on
@@ -82,6 +85,13 @@ class Sync:
         t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
+
+    def sum_int(self, x: int) -> int:
+        if not self.dist:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.int64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return int(t.item())
 
     def close(self):
         if self.dist:
@@ -171,24 +181,43 @@ def _orset_traffic():
     return a[0] + r[0] if a and r else None
 
 
-# Per-GPU PN-Counter shard: C2 (BASELINE configs[1]) by default; "c4" = one GPU's share of
-# configs[3] (200M keys x 128 replicas over 8 GPUs = 25M x 128 per GPU, 102.4 GB resident per GPU).
+# Per-GPU PN-Counter shard: C2 (BASELINE configs[1]) at N = 1; "c4" = one GPU's share of configs[3]
+# (200M keys x 128 replicas over 8 GPUs = 25M x 128 per GPU, 102.4 GB resident per GPU), the default
+# at N > 1.  Strong scaling splits C4_TOTAL_KEYS over the ranks instead.
 PNC_SHAPES = {"c2": (PNC_KEYS, PNC_R), "c4": (25_000_000, 128)}
+C4_TOTAL_KEYS = 200_000_000
+WORKLOAD_NAMES = {
+    "c2": "PNCounter batch merge (BASELINE configs[1]: 10M keys x 64 replicas, int64 P/N)",
+    "c4": "PNCounter batch merge (BASELINE configs[3] per-GPU shard: 25M keys x 128 replicas, int64 P/N; 200M keys over 8 GPUs)",
+    "c4-strong": "PNCounter batch merge (BASELINE configs[3]: 200M keys x 128 replicas, int64 P/N, split over the GPUs)",
+}
 
 
-def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2"):
+def pnc_shard(shape: str, scaling: str, rank: int, world: int) -> tuple[int, int, int]:
+    """(first global key, keys on this rank, replicas).  weak: every rank owns a full shard of `shape`;
+    strong: the C4 keyspace (200M keys) split into `world` contiguous ranges."""
+    if scaling == "strong":
+        base, extra = divmod(C4_TOTAL_KEYS, world)
+        n = base + (1 if rank < extra else 0)
+        return rank * base + min(rank, extra), n, PNC_SHAPES["c4"][1]
     keys, R = PNC_SHAPES[shape]
-    key0, n_keys = shard_keys(keys, rank, world)
+    key0, n = shard_keys(keys, rank, world)
+    return key0, n, R
+
+
+def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2", scaling="weak"):
+    key0, n_keys, R = pnc_shard(shape, scaling, rank, world)
     store = jg.PNCStore(ctx, n_keys, R, PNC_EB)
     rows = jg.Rows(ctx, n_keys, R, PNC_EB)
     store.synth(SEED + rank)
-    rows.synth(SEED + rank, key0=0)
+    rows.synth(SEED + rank, key0=0)  # per-rank seed: every shard holds its own synthetic keys
     wall, ev = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, warmup)
     store.close()
     rows.close()
     cells = n_keys * R
+    keys_total = sync.sum_int(n_keys)
     return {"wall_s": wall, "event_s": ev, "cells_per_rank": cells, "bytes_per_launch": cells * PNC_BYTES_PER_CELL,
-            "keys": n_keys, "R": R}
+            "keys": n_keys, "keys_total": keys_total, "cells_total": keys_total * R, "R": R}
 
 
 def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
@@ -421,11 +450,18 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pnc-shape", choices=sorted(PNC_SHAPES), default="c2",
-                    help="per-GPU PN-Counter shard: c2 = BASELINE configs[1] (default), c4 = 1/8 of configs[3]")
+    ap.add_argument("--pnc-shape", choices=["auto"] + sorted(PNC_SHAPES), default="auto",
+                    help="per-GPU PN-Counter shard: c2 = BASELINE configs[1], c4 = 1/8 of configs[3]; "
+                         "auto (default) = c2 on one GPU, c4 on N > 1")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: a fixed shard per GPU; strong: configs[3]'s 200M keys split over N >= 4 GPUs")
     args = ap.parse_args()
 
     world, rank, local = dist_env()
+    if args.pnc_shape == "auto":
+        args.pnc_shape = "c2" if world == 1 and args.scaling == "weak" else "c4"
+    if args.scaling == "strong" and world < 4:
+        sys.exit("--scaling strong needs N >= 4: configs[3]'s 200M keys x 128 replicas (A + B = 819.2 GB) do not fit fewer MI355X")
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
     if world > 1 or args.workload in ("all", "exchange", "digest"):
@@ -438,7 +474,7 @@ def main():
 
     res = {}
     if args.workload in ("all", "pnc", "pnc-orset"):
-        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape)
+        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape, args.scaling)
     if args.workload in ("all", "orset", "pnc-orset"):
         res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
     if args.workload in ("all", "exchange"):
@@ -466,7 +502,7 @@ def main():
         return
 
     line = {"metric": "replica-key merges/sec + achieved HBM GB/s (PNCounter & ORSet)", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+            "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "data": "synthetic (seeded counter-based generators, DESIGN.md)"}
     if "pnc" in res:
         p = res["pnc"]
@@ -474,17 +510,16 @@ def main():
         kern = p["event_s"] / args.steps
         achieved = p["bytes_per_launch"] / kern / 1e9
         traffic = load_traffic("pnc_merge_dense") if args.pnc_shape == "c2" else None  # PMC pass exists for C2 only
+        total_cells = p["cells_total"]
         line.update({
-            "value": world * p["cells_per_rank"] / step,
+            "value": total_cells / step,
             "unit": "replica-key merges/s",
             "ms_per_step": step * 1e3,
             "dtype": "int64",
-            "config": {"workload": ("PNCounter batch merge (BASELINE configs[1]: 10M keys x 64 replicas, int64 P/N)"
-                                    if args.pnc_shape == "c2" else
-                                    "PNCounter batch merge (BASELINE configs[3] per-GPU shard: 25M keys x 128 replicas, int64 P/N)"),
-                       "keys_per_gpu": p["keys"], "replicas": p["R"], "elem_bytes": PNC_EB,
+            "config": {"workload": WORKLOAD_NAMES["c4-strong" if args.scaling == "strong" else args.pnc_shape],
+                       "keys_per_gpu": p["keys"], "total_keys": p["keys_total"], "replicas": p["R"], "elem_bytes": PNC_EB,
                        "parallelism": f"keyspace-sharded x{world}, no data-path collective"},
-            "hbm_GBps": world * p["bytes_per_launch"] / step / 1e9,
+            "hbm_GBps": total_cells * PNC_BYTES_PER_CELL / step / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic[0] if traffic else None,

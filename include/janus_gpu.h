@@ -234,7 +234,9 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
  * validation (element names repeated inside one map need the whole wave): JG_OK, or the code of the
  * first message the reference's Decode/Merge would throw on — JG_EINVAL (JsonException: not an
  * ORSetMsg in the accepted form of oracle/json.hpp, a null member or tag set, an element repeated in
- * one map) or JG_ESTATE (an empty add tag set, which ORSet.Add never produces) — with *bad_msg = its
+ * one map) or JG_ESTATE (an element whose add or tombstone tag set is empty: Add always inserts a tag and
+ * Remove copies a non-empty add set, so no reference state holds one, and the record layout has no
+ * record to carry the Dictionary key it would add) — with *bad_msg = its
  * wave index (UINT64_MAX if none).  commit merges messages [0, limit) (limit <= *bad_msg): interns
  * their new element strings in commit order and unions their tag records into the store; the wave
  * closes.  abort closes the wave with nothing applied. */

@@ -8,8 +8,9 @@
 //
 //   pass 1  k_ow_parse   one thread per message, launched per uploaded chunk: full parse + validation (the
 //                        accepted form of oracle/json.hpp, which host/wire.cpp's reader also follows); the
-//                        byte position of the first error: a syntax error (JG_EINVAL) or an empty add tag
-//                        set (JG_ESTATE — the host reader reports it at that entry); one entry per
+//                        byte position of the first error: a syntax error (JG_EINVAL) or an element with an
+//                        empty add or tombstone tag set (JG_ESTATE: no ORSet op produces one, and the
+//                        record layout cannot hold the Dictionary key it would add); one entry per
 //                        (message, map, element) with a 64-bit hash of its unescaped string (escaped
 //                        strings unescaped in place) and one record per tag, into regions addressed by
 //                        the message's byte offset (no wave-wide prefix needed yet).
@@ -379,11 +380,11 @@ struct ParseVis {
         ++nt;
     }
     __device__ __forceinline__ void entry_end(int side, uint64_t pos, uint32_t ntags) {
-        if (side == 0 && ntags == 0 && estate == kNone) estate = (unsigned long long)(pos - base) << 2 | kKindState;
+        if (ntags == 0 && estate == kNone) estate = (unsigned long long)(pos - base) << 2 | kKindState;  // add or tombstone
     }
 };
 
-// One thread per message: parse + validate (first error position: syntax or empty add tag set), element
+// One thread per message: parse + validate (first error position: syntax or empty tag set), element
 // strings hashed (escaped ones unescaped in place), entries and tags into the sparse regions.  The
 // entries before a syntax error are kept: a repeated name before it is reported first.
 __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
@@ -1267,7 +1268,7 @@ int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
         JG_HIP(hipStreamSynchronize(ctx->stream));
         const bool state = (e & 3) == kKindState;
         jg::fail(state ? JG_ESTATE : JG_EINVAL, "OR-Set state message %llu is rejected by ORSetMsg.Decode / Merge (%s at byte %llu)",
-                 (unsigned long long)w->first_bad, state ? "an empty add tag set" : "JsonException", (unsigned long long)(e >> 2));
+                 (unsigned long long)w->first_bad, state ? "an element with an empty tag set" : "JsonException", (unsigned long long)(e >> 2));
     });
 }
 

@@ -194,7 +194,7 @@ class ORSetCluster:
         pick = [e for e in es if rng.random() < 0.7] or [es[-1]]
         rng.shuffle(pick)
         add = [(e, [t for t in self.tags[s][e] if rng.random() < 0.8] or self.tags[s][e][:1]) for e in pick]
-        rem = [(e, ts[: int(rng.integers(0, len(ts) + 1))]) for e, ts in add if rng.random() < 0.3]
+        rem = [(e, ts[: int(rng.integers(1, len(ts) + 1))]) for e, ts in add if rng.random() < 0.3]  # Remove copies a non-empty set
         nadd = self.null_tags[s][: int(rng.integers(0, 4))]
         nrem = nadd[: int(rng.integers(0, len(nadd) + 1))]
         return add, rem, nadd, nrem

@@ -280,7 +280,7 @@ def orset_apply_json(set_ids, msgs, names=None, state=None):
     names[("next", set)].  state: {(side, key): {tag: None}} — the Dictionaries and HashSets in their
     insertion order (Merge appends new keys and UnionWith appends new tags, ORSet.cs:255-282) — carried
     between calls (updated in place) when given.  Returns (add records, tombstone records, first bad
-    message or None, its code: "EINVAL" for a Decode error, "ESTATE" for an empty add tag set): the whole
+    message or None, its code: "EINVAL" for a Decode error, "ESTATE" for an element's empty tag set): the whole
     state, sorted, ord = the record's position in its stream's enumeration."""
     names = {} if names is None else names
     state = {} if state is None else state
@@ -290,7 +290,7 @@ def orset_apply_json(set_ids, msgs, names=None, state=None):
         if d is None:
             bad, code = m, "EINVAL"
             break
-        if any(side == 0 and not is_null and not tags for side, is_null, _, tags in d):
+        if any(not is_null and not tags for side, is_null, _, tags in d):  # an element with an empty tag set
             bad, code = m, "ESTATE"
             break
         tab = names.setdefault(int(sid), {})

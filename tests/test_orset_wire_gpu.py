@@ -103,11 +103,11 @@ def test_names_sync_and_clear(ctx):
 
 _GOOD = J.encode_orset([("a", [G1])], [("a", [G1])], [G2], [])
 # (payload, expected code or None): the ORSetMsg wire contract of oracle/json.hpp, plus the engine's
-# empty-add-set limit (JG_ESTATE) and the reader's error order
+# empty-tag-set limit (JG_ESTATE, add or tombstone side) and the reader's error order
 _CASES = [
     (J.encode_orset([("a", [G1, G1, G2])], []), None),                     # repeated tag in one array: one record
     (J.encode_orset([], [], [], []), None),
-    (J.encode_orset([("a", [G1])], [("a", [])]), None),                    # empty tombstone set is fine
+    (J.encode_orset([("a", [G1])], [("a", [])]), jg.JG_ESTATE),            # empty tombstone set: no record holds its key
     (J.encode_orset([("a", [G1])], [], [], [], mode="all"), None),         # escaped names and Guids
     (b'{"add\\u0053et":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', None),
     (J.encode_orset([("a", [G1])], [], upper=True, ws="\r\n\t "), None),

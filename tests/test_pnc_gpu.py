@@ -245,6 +245,39 @@ def test_full_size_c2_properties(ctx):
     assert np.array_equal(P1, P2) and np.array_equal(N1, N2)
 
 
+def test_full_size_c4_shard_properties(ctx):
+    """BASELINE config C4 (200M keys x 128 replicas over 8 GPUs): one GPU's shard, 25M keys x 128 replicas
+    int64 — A and B resident, 102.4 GB — merged on the device; 3.2G cells per array, so cell offsets pass
+    2^32 (64-bit indexing).  Sampled rows (first, last, random) exactly against the oracle, Get on them
+    against the oracle's checked sums, then idempotence."""
+    seed, n_keys, R = 0x4A414E5553 + 7, 25_000_000, 128
+    s = jg.PNCStore(ctx, n_keys, R, 8)
+    b = jg.Rows(ctx, n_keys, R, 8)
+    try:
+        s.synth(seed)
+        b.synth(seed)
+        s.merge_batch(b)
+        rng = np.random.default_rng(4)
+        keys = np.unique(np.concatenate([rng.integers(0, n_keys, 2000), [0, 1, n_keys // 2, n_keys - 2, n_keys - 1]])).astype(np.uint32)
+        P1, N1 = s.read_rows(keys)
+        v1, o1 = s.values(keys)
+        s.merge_batch(b)
+        P2, N2 = s.read_rows(keys)
+    finally:
+        s.close()
+        b.close()
+    check = np.concatenate([np.arange(200), np.arange(keys.size - 5, keys.size)])
+    for i in check:
+        k = int(keys[i])
+        AP, AN = orc.synth_pnc(seed, 0, k, 1, R, 8), orc.synth_pnc(seed, 1, k, 1, R, 8)
+        BP, BN = orc.synth_pnc(seed, 2, k, 1, R, 8), orc.synth_pnc(seed, 3, k, 1, R, 8)
+        eP, eN = orc.pnc_merge(AP, AN, BP, BN)
+        assert np.array_equal(P1[i], eP[0]) and np.array_equal(N1[i], eN[0]), k
+        ev, eo = orc.pnc_values(eP, eN)
+        assert v1[i] == ev[0] and o1[i] == eo[0], k
+    assert np.array_equal(P1, P2) and np.array_equal(N1, N2)
+
+
 def test_errors_are_codes(ctx):
     with pytest.raises(jg.JanusError) as e:
         jg.PNCStore(ctx, 10, 4, 3)
