@@ -1,18 +1,28 @@
-// bench_apply.cpp — committed-batch apply loop throughput.
+// bench_apply.cpp — committed-batch apply loop of the banking replay.
 //
-// Synthetic DAG-committed waves shaped like the reference's banking workload
-// (BFT-CRDT-Client/BankingBenchmark.cs/BankingBenchmarkRunner.cs:135-163, BankingWorload.cs): 4 nodes,
-// PN-Counter accounts, every client update ships the FULL state of its account as seen by its node
-// (SafeCRDT.cs:52), packed clientBatchSize = 1000 states per UpdateMessage (JanusService.cs:29) and
-// 100 UpdateMessages per block (DAG.cs:25).  A wave holds `msgs` state messages.
+// Client side, restated from the reference's banking benchmark: BankingBenchmarkRunner.cs:135-163 picks
+// an op by opsRatio (benchmark_config_example.json: [0.25 view, 0.25 deposit, 0.5 transfer-or-withdraw])
+// and an account (uniform, or N(n/2, n/6) clamped: :208-226); BankingWorload.cs turns each into
+//   View      "gp"                                            -> no state shipped          (:30-60)
+//   Deposit   "i"  Next(1000), non-safe                      -> 1 state                  (:62-92)
+//   Transfer  "d"  Next(100) safe on the account, then "i" non-safe on the other account
+//                                                            -> 2 states                 (:94-133)
+//   Withdraw  "gs" read, then "d" Next(100) safe             -> 1 state                  (:156-203)
+// and every "d" is Update(1, ...) = Increment (PNCounterCommand.cs:48-50): N columns stay 0.
+// Node side: each client thread talks to one server (:64-79, threads round-robin over servers); the
+// node applies the op to its prospective copy and ships the FULL state (SafeCRDT.cs:39-62: the node's
+// own counter plus the other nodes' counters it merged; here every node has seen every other node's
+// latest value), and its batcher ActualPropagateSyncMsg (SafeCRDTManager.cs:165-198, clientBatchSize
+// 1000, JanusService.cs:29) keeps safe states individually and compacts non-safe ones to the last state
+// per account; the 100 ms timer flushes every queue at the end of a wave.  100 UpdateMessages per block
+// (DAG.cs:25).  A wave is `ops` client ops (1M: BASELINE configs[4]).
 //
-// Every state travels as the reference ships it: NetworkProtocol.message = PNCounterMsg JSON
-// (SafeCRDT.cs:49, PNCounters.cs:46-49).
-// GPU: janus::GpuStableStore::ApplyCommitted (classify + gather the payloads into pinned staging +
-// ONE jg_pnc_merge_json: decode, replica interning and merge on the device).  CPU baseline: the
-// oracle's SafeCRDTManager.HandleAfterConsensusUpdates (dictionary-faithful restatement of
-// SafeCRDTManager.cs:109-160: Decode + Merge per message, one thread like the reference's serialized
-// apply task) on the first `cpu_msgs` messages of the same wave.
+// GPU: janus::GpuStableStore::ApplyCommitted with the safe-update tracker (classify + gather into
+// pinned staging + the streamed jg_pnc_wave_*: decode, replica interning and merge on the device).
+// CPU baseline: the oracle's SafeCRDTManager.HandleAfterConsensusUpdates (Decode + Merge per message,
+// one thread like the reference's serialized apply task) on the first `cpu_msgs` messages of each wave.
+// --parity: the oracle applies EVERY wave in full; after each wave every owned account's stable Get and
+// the safe-update completions (origins, in commit order) must equal the oracle's (exit 1 otherwise).
 // Prints one JSON object.
 #include <chrono>
 #include <cmath>
@@ -21,6 +31,7 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <unordered_map>
 
 #include "janus_host.hpp"
 #include "oracle.hpp"
@@ -30,25 +41,20 @@ namespace {
 
 double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 
-struct Wave {
-    std::vector<std::vector<janus::UpdateMessage>> gpu;
-    std::vector<std::vector<oracle::UpdateMessage>> cpu;  // first cpu_msgs messages only
-    uint64_t n = 0;
-};
-
 }  // namespace
 
 int main(int argc, char** argv) {
-    uint64_t accounts = 1000000, msgs = 1000000, cpu_msgs = 100000;
-    int waves = 5, nodes = 4, device = 0;
+    uint64_t accounts = 1000000, ops = 1000000, cpu_msgs = 100000;
+    int waves = 3, nodes = 4, device = 0, batch = 1000, threads_per_node = 3;  // 12 client threads (config example)
     uint32_t rank = 0, world = 1;
-    bool normal = false;
+    bool normal = false, parity = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--accounts") && i + 1 < argc) accounts = std::strtoull(argv[++i], nullptr, 10);
-        else if (!std::strcmp(argv[i], "--msgs") && i + 1 < argc) msgs = std::strtoull(argv[++i], nullptr, 10);
+        else if (!std::strcmp(argv[i], "--ops") && i + 1 < argc) ops = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--cpu-msgs") && i + 1 < argc) cpu_msgs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--normal")) normal = true;
+        else if (!std::strcmp(argv[i], "--parity")) parity = true;
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) world = (uint32_t)std::atoi(argv[++i]);
@@ -56,8 +62,9 @@ int main(int argc, char** argv) {
     const uint32_t R = nodes + 1;  // the stable copy's own replica + one prospective replica per node
     std::mt19937_64 rng(0x4A414E5553ull);
     oracle::GuidGen gen(7);
+    auto G = [](const oracle::Guid& g) { return janus::Guid{g.lo, g.hi}; };
 
-    // accounts: key uid, per-node prospective replica Guids, stable replica Guid
+    // accounts: key uid, stable replica Guid (column 0), per-node prospective replica Guids
     std::vector<oracle::Guid> uid(accounts), stable(accounts), rep(accounts * nodes);
     for (uint64_t k = 0; k < accounts; ++k) {
         uid[k] = gen.next();
@@ -65,7 +72,6 @@ int main(int argc, char** argv) {
         for (int n = 0; n < nodes; ++n) rep[k * nodes + n] = gen.next();
     }
     janus::GpuStableStore gpu(device, (uint32_t)accounts, R, 4);
-    auto G = [](const oracle::Guid& g) { return janus::Guid{g.lo, g.hi}; };
     // key-space shard of this rank (every rank sees the whole wave and skips the uids it does not own)
     std::vector<uint8_t> mine(accounts);
     uint64_t owned = 0;
@@ -73,96 +79,200 @@ int main(int argc, char** argv) {
         mine[k] = janus::GpuStableStore::ShardOf(G(uid[k]), world) == rank;
         if (mine[k]) { gpu.CreateSafeCRDT(G(uid[k]), janus::CrdtType::PNCounter, G(stable[k])); ++owned; }
     }
-    uint64_t applied = 0;
-    oracle::SafeCRDTManager cpu(1000, 1);
-    if (cpu_msgs)
-        for (uint64_t k = 0; k < accounts; ++k) cpu.CreateSafeCRDT("acct" + std::to_string(k), oracle::CrdtType::PNCounter, uid[k]);
+    const bool run_cpu = parity || cpu_msgs > 0;
+    oracle::SafeCRDTManager cpu(batch, 1);
+    std::vector<oracle::SafeCRDT*> cref(accounts, nullptr);
+    if (run_cpu)
+        for (uint64_t k = 0; k < accounts; ++k)
+            if (mine[k]) {
+                oracle::SafeCRDT& sc = cpu.CreateSafeCRDT("acct" + std::to_string(k), oracle::CrdtType::PNCounter, uid[k]);
+                sc.pncStable->pnc = oracle::PNCounter<int32_t>(stable[k]);  // the stable instance's own replica (column 0)
+                cref[k] = &sc;
+            }
 
-    // per (account, node) counters: a node's state of an account = its own P/N plus what it merged
-    std::vector<int32_t> P(accounts * nodes, 0), N(accounts * nodes, 0);
+    std::vector<int32_t> P(accounts * nodes, 0), N(accounts * nodes, 0);  // N stays 0: "d" is Increment
     std::normal_distribution<double> nd(accounts / 2.0, accounts / 6.0);
-    auto pick = [&]() -> uint64_t {
+    auto account = [&]() -> uint64_t {  // GetRandomAccount (BankingBenchmarkRunner.cs:208-226)
         if (!normal) return rng() % accounts;
         const double x = std::round(nd(rng));
         return (uint64_t)std::max(0.0, std::min(x, (double)accounts - 1));
     };
+    struct Queued { janus::NetworkProtocol np; bool safe; };
+    std::vector<std::vector<Queued>> q(nodes);
+    std::unordered_map<uint64_t, uint64_t> tracker_g, tracker_c;  // safe-update tracker: seq -> client origin
+    uint64_t seq = 1;
 
     double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
-    uint64_t gpu_n = 0, cpu_n = 0, payload = 0, payload_timed = 0, shard_bytes = 0;
-    for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
-        Wave wave;
-        std::vector<janus::UpdateMessage> block;
-        std::vector<oracle::UpdateMessage> cblock;
-        janus::UpdateMessage um;
-        oracle::UpdateMessage cum;
-        for (uint64_t m = 0; m < msgs; ++m) {
-            const uint64_t k = pick();
-            const int n = (int)(rng() % nodes);
-            const uint64_t op = rng() % 4;  // view / deposit / transfer / withdraw (BankingBenchmarkRunner.cs:140-160)
-            const int32_t amt = (int32_t)(op == 1 ? rng() % 1000 : rng() % 100);
-            if (op == 0) { --m; continue; }           // a read ships no state
-            P[k * nodes + n] += amt;                   // "i" and "d" are both Increment (PNCounterCommand.cs:42-51)
-            if (rng() % 8 == 0) N[k * nodes + n] += amt / 3;
+    uint64_t gpu_n = 0, cpu_n = 0, payload_timed = 0, shard_bytes = 0, applied = 0, n_safe = 0, n_states = 0, n_done = 0;
+    bool ok = true;
+    std::string why;
+    for (int w = 0; w < waves + 1 && ok; ++w) {  // wave 0 = warmup
+        std::vector<janus::UpdateMessage> ums;
+        auto flush = [&](int n) {  // ActualPropagateSyncMsg's drain (SafeCRDTManager.cs:170-196)
+            std::vector<janus::NetworkProtocol> safe, appeared;
+            std::unordered_map<janus::Guid, size_t, janus::GuidHash> pos;
+            size_t at = 0;
+            for (; at < q[n].size(); ++at) {
+                if (!((int)safe.size() < batch)) { ++at; break; }  // dequeued, then dropped (:175)
+                Queued& e = q[n][at];
+                if (!e.safe) {
+                    auto it = pos.find(e.np.uid);
+                    if (it == pos.end()) { pos.emplace(e.np.uid, appeared.size()); appeared.push_back(std::move(e.np)); }
+                    else appeared[it->second] = std::move(e.np);
+                } else {
+                    safe.push_back(std::move(e.np));
+                }
+            }
+            q[n].erase(q[n].begin(), q[n].begin() + (long)at);
+            for (auto& a : appeared) safe.push_back(std::move(a));
+            if (!safe.empty()) ums.push_back(janus::UpdateMessage{std::move(safe)});
+        };
+        // SafeCRDT.Update on node n: Increment its own column, ship the full state, queue it
+        auto update = [&](int n, uint64_t k, int32_t amt, bool safe, uint64_t origin) {
+            P[k * nodes + n] += amt;
             janus::NetworkProtocol np;
             np.uid = G(uid[k]);
-            np.seq = m;
-            {   // the node's full state: every replica it has seen, encoded (GetLastSynchronizedUpdate().Encode())
-                janus::Guid g[16];
-                int64_t pv[16], nv[16];
-                for (int j = 0; j < nodes; ++j) { g[j] = G(rep[k * nodes + j]); pv[j] = P[k * nodes + j]; nv[j] = N[k * nodes + j]; }
-                janus::wire::AppendPNCounterMsg(np.message, g, pv, nv, nodes);
+            np.seq = seq++;
+            janus::Guid g[16];
+            int64_t pv[16], nv[16];
+            for (int j = 0; j < nodes; ++j) { g[j] = G(rep[k * nodes + j]); pv[j] = P[k * nodes + j]; nv[j] = N[k * nodes + j]; }
+            janus::wire::AppendPNCounterMsg(np.message, g, pv, nv, nodes);
+            if (safe) {  // SafeCRDT.cs:55-56: tracked when safe and the origin is a client
+                tracker_g[np.seq] = origin;
+                tracker_c[np.seq] = origin;
+                if (w > 0) ++n_safe;
             }
-            payload += np.message.size();
-            if (w > 0 && mine[k]) ++applied;
-            if (m < cpu_msgs && w > 0) {
-                oracle::NetworkProtocol cp;
-                cp.uid = uid[k];
-                cp.seq = m;
-                cp.bytes = np.message;  // the oracle decodes it in ApplyUpdateStable (oracle/json.hpp)
-                cum.update.push_back(std::move(cp));
-                if (cum.update.size() == 1000) { cblock.push_back(std::move(cum)); cum = oracle::UpdateMessage(); }
-                if (cblock.size() == 100) { wave.cpu.push_back(std::move(cblock)); cblock.clear(); }
+            if (w > 0) ++n_states;
+            q[n].push_back(Queued{std::move(np), safe});
+            if ((int)q[n].size() >= batch) flush(n);
+        };
+        for (uint64_t o = 0; o < ops; ++o) {
+            const int thread = (int)(rng() % (uint64_t)(nodes * threads_per_node));
+            const int n = thread % nodes;                  // client thread i talks to server i mod nodes
+            const uint64_t origin = 1 + (uint64_t)thread;  // the client connection notified on completion
+            const uint64_t r = rng() % 4;                  // PickRandomOptionByRatio over [0.25, 0.25, 0.5]
+            const uint64_t acct = account();
+            if (r == 0) continue;                                                        // ViewBalance: "gp"
+            if (r == 1) { update(n, acct, (int32_t)(rng() % 1000), false, origin); continue; }  // Deposit: "i"
+            if (rng() % 2 == 0) {                                                        // Transfer
+                const uint64_t other = account();
+                const int32_t amt = (int32_t)(rng() % 100);
+                update(n, acct, amt, true, origin);                                      // "d" safe (= Increment)
+                update(n, other, amt, false, origin);                                    // then "i" non-safe
+            } else {
+                update(n, acct, (int32_t)(rng() % 100), true, origin);                   // Withdraw: "gs", then "d" safe
             }
-            um.update.push_back(std::move(np));
-            if (um.update.size() == 1000) { block.push_back(std::move(um)); um = janus::UpdateMessage(); }
-            if (block.size() == 100) { wave.gpu.push_back(std::move(block)); block.clear(); }
         }
-        if (!um.update.empty()) block.push_back(std::move(um));
-        if (!block.empty()) wave.gpu.push_back(std::move(block));
-        if (!cum.update.empty()) cblock.push_back(std::move(cum));
-        if (!cblock.empty()) wave.cpu.push_back(std::move(cblock));
-
-        const uint64_t wave_payload = payload;
-        payload = 0;
+        for (int n = 0; n < nodes; ++n) flush(n);  // the 100 ms timer at the end of the wave
+        std::vector<std::vector<janus::UpdateMessage>> wave(1);
+        uint64_t wave_msgs = 0, wave_payload = 0;
+        for (auto& um : ums) {
+            wave_msgs += um.update.size();
+            for (const auto& np : um.update) wave_payload += np.message.size();
+            if (wave.back().size() == 100) wave.emplace_back();
+            wave.back().push_back(std::move(um));
+        }
+        // the oracle's copy of the wave (all of it for parity, else the first cpu_msgs messages)
+        std::vector<std::vector<oracle::UpdateMessage>> cwave;
+        if (run_cpu && w > 0) {
+            uint64_t left = parity ? UINT64_MAX : cpu_msgs;
+            for (const auto& blk : wave) {
+                if (!left) break;
+                cwave.emplace_back();
+                for (const auto& um : blk) {
+                    if (!left) break;
+                    oracle::UpdateMessage cu;
+                    for (const auto& np : um.update) {
+                        if (!left) break;
+                        oracle::NetworkProtocol cp;
+                        cp.uid = oracle::Guid{np.uid.lo, np.uid.hi};
+                        cp.seq = np.seq;
+                        cp.bytes = np.message;  // decoded by the stable copy's codec (oracle/json.hpp)
+                        cu.update.push_back(std::move(cp));
+                        --left;
+                    }
+                    cwave.back().push_back(std::move(cu));
+                }
+            }
+        }
         const double t0 = now_s();
-        gpu.ApplyCommitted(wave.gpu, nullptr);
+        const std::vector<uint64_t> done = gpu.ApplyCommitted(wave, &tracker_g);
         const double t1 = now_s();
-        if (w > 0) {
-            gpu_s += t1 - t0;
-            host_s += gpu.last_apply_host_s();
-            engine_s += gpu.last_apply_engine_s();
-            for (int q = 0; q < 4; ++q) ph[q] += gpu.last_apply_phases_s()[q];
-            gpu_n += msgs;
-            payload_timed += wave_payload;
-            shard_bytes += gpu.last_apply_pnc_bytes();
-            if (!cpu_msgs) continue;
-            const double c0 = now_s();
-            cpu.HandleAfterConsensusUpdates(wave.cpu);
-            cpu_s += now_s() - c0;
-            cpu_n += std::min(msgs, cpu_msgs);
+        if (w == 0) {
+            if (parity) {  // the warmup wave reaches the oracle too (untimed), so states stay in step
+                std::vector<std::vector<oracle::UpdateMessage>> all;
+                for (const auto& blk : wave) {
+                    all.emplace_back();
+                    for (const auto& um : blk) {
+                        oracle::UpdateMessage cu;
+                        for (const auto& np : um.update) {
+                            oracle::NetworkProtocol cp;
+                            cp.uid = oracle::Guid{np.uid.lo, np.uid.hi};
+                            cp.seq = np.seq;
+                            cp.bytes = np.message;
+                            cu.update.push_back(std::move(cp));
+                        }
+                        all.back().push_back(std::move(cu));
+                    }
+                }
+                cpu.safeUpdateTracker = tracker_c;
+                cpu.notified.clear();
+                cpu.HandleAfterConsensusUpdates(all);
+                tracker_c = cpu.safeUpdateTracker;
+            }
+            continue;
+        }
+        gpu_s += t1 - t0;
+        host_s += gpu.last_apply_host_s();
+        engine_s += gpu.last_apply_engine_s();
+        for (int p = 0; p < 4; ++p) ph[p] += gpu.last_apply_phases_s()[p];
+        gpu_n += wave_msgs;
+        payload_timed += wave_payload;
+        shard_bytes += gpu.last_apply_pnc_bytes();
+        n_done += done.size();
+        for (const auto& blk : wave)
+            for (const auto& um : blk)
+                for (const auto& np : um.update) applied += janus::GpuStableStore::ShardOf(np.uid, world) == rank;
+        if (!run_cpu) continue;
+        cpu.safeUpdateTracker = tracker_c;
+        cpu.notified.clear();
+        const double c0 = now_s();
+        cpu.HandleAfterConsensusUpdates(cwave);
+        cpu_s += now_s() - c0;
+        tracker_c = cpu.safeUpdateTracker;
+        uint64_t cn = 0;
+        for (const auto& blk : cwave)
+            for (const auto& um : blk) cn += um.update.size();
+        cpu_n += cn;
+        if (!parity) continue;
+        // every owned account's stable Get, and the completions in commit order (unowned uids are
+        // skipped on both sides, SafeCRDTManager.cs:136)
+        if (done != cpu.notified) { ok = false; why = "safe-update completions differ"; }
+        for (uint64_t k = 0; k < accounts && ok; ++k) {
+            if (!mine[k]) continue;
+            if (gpu.QueryStablePNC(G(uid[k])) != cref[k]->QueryStable().i) { ok = false; why = "account " + std::to_string(k) + " differs"; }
         }
     }
+    if (parity) {
+        std::printf("{\"parity\": %s, \"why\": \"%s\", \"waves\": %d, \"msgs_per_wave\": %.1f, \"safe_per_wave\": %.1f, \"completed_per_wave\": %.1f, "
+                    "\"owned_accounts\": %llu}\n",
+                    ok ? "true" : "false", why.c_str(), waves, (double)gpu_n / waves, (double)n_safe / waves, (double)n_done / waves,
+                    (unsigned long long)owned);
+        return ok ? 0 : 1;
+    }
     const double bytes = (double)payload_timed;  // JSON payload bytes uploaded and decoded
-    std::printf("{\"workload\": \"committed-batch apply (C5 banking-shaped, %s accounts %llu, %d nodes, %llu PNCounterMsg JSON states per wave)\", "
-                "\"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"payload_bytes_per_msg\": %.1f, \"host_ms_per_wave\": %.3f, "
-                "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, \"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], "
-                "\"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
-                "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, \"kind\": \"port\", "
+    std::printf("{\"workload\": \"C5 banking replay (BankingWorload.cs ops: view/deposit/transfer/withdraw at opsRatio [0.25, 0.25, 0.5], "
+                "every d an Increment; %s accounts %llu; %d nodes, clientBatchSize %d with state compaction; committed waves of %llu client ops)\", "
+                "\"waves\": %d, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
+                "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, \"host_ms_per_wave\": %.3f, "
+                "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, "
+                "\"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
+                "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %.1f, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
-                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s,
-                1e3 * gpu_s / waves, bytes / gpu_n, 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, shard_bytes / engine_s / 1e9,
-                janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves, 1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves,
-                rank, world, (unsigned long long)owned, (double)applied / waves, cpu_s > 0 ? cpu_n / cpu_s : 0.0,
-                (unsigned long long)std::min(msgs, cpu_msgs));
+                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, gpu_n / gpu_s,
+                (double)ops * waves / gpu_s, 1e3 * gpu_s / waves, (double)gpu_n / waves, (double)n_states / waves, (double)n_safe / waves,
+                bytes / std::max<uint64_t>(gpu_n, 1), 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, shard_bytes / engine_s / 1e9,
+                janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves, 1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves, rank,
+                world, (unsigned long long)owned, (double)applied / waves, cpu_s > 0 ? cpu_n / cpu_s : 0.0, (double)cpu_n / waves);
     return 0;
 }

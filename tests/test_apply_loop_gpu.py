@@ -31,10 +31,36 @@ def test_sharded_apply_covers_the_wave_once():
     import json
     res = []
     for r in range(2):
-        out = subprocess.run([str(BENCH), "--accounts", "20000", "--msgs", "50000", "--waves", "2", "--cpu-msgs", "0",
+        out = subprocess.run([str(BENCH), "--accounts", "20000", "--ops", "50000", "--waves", "2", "--cpu-msgs", "0",
                               "--rank", str(r), "--world", "2"], capture_output=True, text=True, timeout=110)
         assert out.returncode == 0, out.stderr
         res.append(json.loads(out.stdout.strip().splitlines()[-1]))
     assert res[0]["owned_accounts"] + res[1]["owned_accounts"] == 20000
     assert min(x["owned_accounts"] for x in res) > 9000  # balanced hash split
-    assert res[0]["applied_msgs_per_wave"] + res[1]["applied_msgs_per_wave"] == 50000
+    assert res[0]["state_msgs_per_wave"] == res[1]["state_msgs_per_wave"]  # both ranks saw the same waves
+    assert res[0]["applied_msgs_per_wave"] + res[1]["applied_msgs_per_wave"] == res[0]["state_msgs_per_wave"]
+
+
+@pytest.mark.parametrize("args", [
+    ["--accounts", "1000000", "--ops", "1000000", "--waves", "1"],             # C5: one 1M-op wave, 1M accounts
+    ["--accounts", "100", "--ops", "200000", "--waves", "2", "--normal"],     # the paper's 100 accounts, N(n/2, n/6)
+    ["--accounts", "5000", "--ops", "100000", "--waves", "2", "--rank", "1", "--world", "3"],  # one key-space shard
+])
+def test_banking_replay_matches_oracle(args):
+    """C5 parity (BankingWorload.cs ops through the node batchers): after every committed wave, every owned
+    account's stable Get and the safe-update completions in commit order equal the oracle's
+    HandleAfterConsensusUpdates over the same wave."""
+    import json
+    out = subprocess.run([str(BENCH), "--parity"] + args, capture_output=True, text=True, timeout=280)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and res["parity"], (res, out.stderr[-2000:])
+    assert res["safe_per_wave"] > 0 and res["completed_per_wave"] > 0
+
+
+def test_c1_replay_matches_oracle():
+    """BASELINE configs[0] (C1: PNCWorkload, 100 keys, opsRatio [0.25, 0.25, 0.5], safeRatio 0.5) through the
+    node batchers: every key's stable Get equals the oracle's after the committed waves."""
+    import json
+    out = subprocess.run([str(BIN.parent / "bench_c1"), "--ops", "300000", "--waves", "2"], capture_output=True, text=True, timeout=200)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and res["parity_vs_oracle"] is True, res
