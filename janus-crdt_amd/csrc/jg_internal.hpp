@@ -101,8 +101,9 @@ struct jg_pnc {
     jg::DevBuf P, N;
     // replica table (json.hip): [n_keys x R] 16-byte Guids + [n_keys] column counts, first use only
     jg::DevBuf cols, ncols;
-    // per-key occurrence counters of the batch being merged (k_claim_*), zero between calls; first use
-    jg::DevBuf claim;
+    // grouped indexed merge (k_group_*): per-key list head of the batch being merged (0xFFFFFFFF between
+    // calls) and a next[] link per received row; first use
+    jg::DevBuf head, next;
     // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list
     jg::DevBuf wbytes, woff, wrows, wstat;
     uint64_t wn = 0, wnb = 0;

@@ -109,64 +109,72 @@ __global__ __launch_bounds__(kBlock) void k_merge_indexed_rows(typename Elem<EB>
     }
 }
 
-// Duplicate-aware scatter-max, three passes over the batch's keys.  Keys that occur ONCE in the batch
-// (the common case) are merged with plain 16-B vector loads / max / stores — atomics run at ~1.3 TB/s
-// of added bytes on MI355X, plain stores at ~6 TB/s (MI355X_MICROARCH.md, atomics table); only rows
-// of repeated keys take the per-cell atomicMax path.  ABSENT (the width's minimum) needs no test on
-// the vector path: max(a, ABSENT) = a.
-__global__ __launch_bounds__(kBlock) void k_claim_count(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ claim) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) atomicAdd(claim + keys[i], 1u);
+// Duplicate-aware scatter-max with no atomics on the data, three passes over the batch's keys (a
+// committed wave folds several states of one key, SafeCRDTManager.cs:122-146).  Pass 1 (k_group_link)
+// links each key's rows into a list: next[m] = the key's previous head, head[key] = m (one atomicExch
+// per row).  Pass 2 (k_merge_grouped): the head row of every key loads its A row once, max-folds every
+// B row of the key in registers — each B row's load issued together with its next[] link, so a key
+// held k times costs k - 1 dependent hops — and stores A once; the other rows of the key do nothing.
+// Pass 3 (k_group_reset) restores the touched heads.  Atomics ran at ~1.3 TB/s of added bytes on
+// MI355X against ~6 TB/s for plain stores (MI355X_MICROARCH.md, atomics table), and random 4-B atomics
+// ~17x slower again: a per-cell atomicMax for repeated keys (39 % of the rows of a uniform batch of n
+// rows over 2n keys) and an occurrence counter per row both measured slower (tools/tune_grouped.hip,
+// DESIGN.md §4).  ABSENT (the width's minimum) needs no test: max(a, ABSENT) = a.
+constexpr uint32_t kNil = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(kBlock) void k_group_link(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ head,
+                                                       uint32_t* __restrict__ next) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        next[i] = atomicExch(head + keys[i], (uint32_t)i);
 }
-__global__ __launch_bounds__(kBlock) void k_claim_reset(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ claim) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) claim[keys[i]] = 0;
+__global__ __launch_bounds__(kBlock) void k_group_reset(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ head) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) head[keys[i]] = kNil;
 }
 
-// One wave per received row, U rows in flight; the row (R x EB bytes) is a whole number of 16-B vectors.
-template <int EB>
-__global__ __launch_bounds__(kBlock) void k_merge_claimed(typename Elem<EB>::T* __restrict__ AP, typename Elem<EB>::T* __restrict__ AN,
+// One wave per received row, U rows in flight; the row (R x EB bytes) is a whole number of 16-B vectors
+// and each lane owns the same vector slot(s) of every row it touches.
+template <int EB, int U>
+__global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* __restrict__ AP, typename Elem<EB>::T* __restrict__ AN,
                                                           const typename Elem<EB>::T* __restrict__ BP,
                                                           const typename Elem<EB>::T* __restrict__ BN, const uint32_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ claim, uint64_t n_rows, uint32_t R) {
-    using T = typename Elem<EB>::T;
-    constexpr int U = 4;
-    const T absent = EB == 4 ? (T)INT32_MIN : (T)INT64_MIN;
+                                                          const uint32_t* __restrict__ head, const uint32_t* __restrict__ next, uint64_t n_rows,
+                                                          uint32_t R) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nv = R * EB / 16;  // vectors per array row
     const uint64_t n_waves = ((uint64_t)gridDim.x * kBlock) >> 6;
     for (uint64_t m0 = (((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> 6) * U; m0 < n_rows; m0 += n_waves * U) {
         uint64_t key[U];
-        bool once[U];
+        bool lead[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t m = m0 + u;
             key[u] = m < n_rows ? keys[m] : 0;
-            once[u] = m < n_rows && claim[key[u]] == 1;
+            lead[u] = m < n_rows && head[key[u]] == (uint32_t)m;
         }
         for (uint32_t v = lane; v < 2 * nv; v += 64) {
             const bool isP = v < nv;
             const uint32_t w = isP ? v : v - nv;
+            const auto* B = isP ? BP : BN;
+            auto* A = isP ? AP : AN;
             uint4 a[U], b[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                if (once[u]) {
-                    const uint4* src = reinterpret_cast<const uint4*>((isP ? BP : BN) + (m0 + u) * R) + w;
-                    const uint4* dst = reinterpret_cast<const uint4*>((isP ? AP : AN) + key[u] * R) + w;
-                    b[u] = nt_load(src);
-                    a[u] = *dst;
+                if (lead[u]) {
+                    b[u] = nt_load(reinterpret_cast<const uint4*>(B + (m0 + u) * R) + w);
+                    a[u] = *(reinterpret_cast<const uint4*>(A + key[u] * R) + w);
                 }
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (once[u]) *(reinterpret_cast<uint4*>((isP ? AP : AN) + key[u] * R) + w) = vmax<EB>(a[u], b[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint64_t m = m0 + u;
-            if (m >= n_rows || once[u]) continue;
-            for (uint32_t c = lane; c < R; c += 64) {  // a key repeated in the batch: order-free atomics
-                const T p = BP[m * R + c], q = BN[m * R + c];
-                if (p != absent) atomicMax(AP + key[u] * R + c, p);
-                if (q != absent) atomicMax(AN + key[u] * R + c, q);
+            for (int u = 0; u < U; ++u) {
+                if (!lead[u]) continue;
+                a[u] = vmax<EB>(a[u], b[u]);
+                for (uint32_t cur = next[m0 + u]; cur != kNil;) {  // the key's other rows
+                    const uint4 bb = nt_load(reinterpret_cast<const uint4*>(B + (uint64_t)cur * R) + w);
+                    const uint32_t nx = next[cur];
+                    a[u] = vmax<EB>(a[u], bb);
+                    cur = nx;
+                }
+                *(reinterpret_cast<uint4*>(A + key[u] * R) + w) = a[u];
             }
         }
     }
@@ -306,19 +314,25 @@ void launch_merge_dense(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void
     JG_HIP(hipGetLastError());
 }
 
+// The store's per-key list heads (kNil between calls) and a next[] link per received row (grown to the
+// largest batch).
+struct Groups { uint32_t* head; uint32_t* next; };
+
 void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void* BP, const void* BN, const uint32_t* keys,
-                          uint64_t n_rows, uint32_t R, uint32_t* claim = nullptr) {
-    if (claim && R >= 32 && ((uint64_t)R * eb) % 16 == 0) {
+                          uint64_t n_rows, uint32_t R, const Groups* g = nullptr) {
+    if (g && R >= 32 && ((uint64_t)R * eb) % 16 == 0) {
+        JG_REQUIRE(n_rows < kNil, JG_EINVAL, "merge: %llu rows exceed one grouped launch", (unsigned long long)n_rows);
         const unsigned gk = grid_for(ctx, n_rows, 16);
-        hipLaunchKernelGGL(k_claim_count, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, claim);
-        const unsigned grid = grid_for(ctx, (n_rows + 3) / 4 * 64, 16);
+        hipLaunchKernelGGL(k_group_link, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, g->head, g->next);
+        constexpr int U = 4;  // rows in flight per wave (U = 8 measured slower, tools/tune_grouped.hip)
+        const unsigned grid = grid_for(ctx, (n_rows + U - 1) / U * 64, 16);
         if (eb == 8)
-            hipLaunchKernelGGL(k_merge_claimed<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, (long long*)AP, (long long*)AN,
-                               (const long long*)BP, (const long long*)BN, keys, claim, n_rows, R);
+            hipLaunchKernelGGL((k_merge_grouped<8, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (long long*)AP, (long long*)AN,
+                               (const long long*)BP, (const long long*)BN, keys, g->head, g->next, n_rows, R);
         else
-            hipLaunchKernelGGL(k_merge_claimed<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, (int*)AP, (int*)AN, (const int*)BP,
-                               (const int*)BN, keys, claim, n_rows, R);
-        hipLaunchKernelGGL(k_claim_reset, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, claim);
+            hipLaunchKernelGGL((k_merge_grouped<4, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (int*)AP, (int*)AN, (const int*)BP,
+                               (const int*)BN, keys, g->head, g->next, n_rows, R);
+        hipLaunchKernelGGL(k_group_reset, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, g->head);
         JG_HIP(hipGetLastError());
         return;
     }
@@ -343,14 +357,20 @@ void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const vo
     JG_HIP(hipGetLastError());
 }
 
-// The store's claim counters (zeroed on first use; every claimed merge resets what it counted).
-uint32_t* claim_of(jg_pnc* p) {
+// The store's group state for a batch of n_rows (allocated on first use; every grouped merge restores
+// the heads it touched).  nullptr when rows are too narrow for the vector path.
+const Groups* groups_of(jg_pnc* p, uint64_t n_rows, Groups& g) {
     if (p->R < 32 || ((uint64_t)p->R * p->eb) % 16 != 0) return nullptr;
-    if (!p->claim.p) {
-        p->claim.alloc(p->n_keys * 4);
-        JG_HIP(hipMemsetAsync(p->claim.p, 0, p->n_keys * 4, p->ctx->stream));
+    if (!p->head.p) {
+        p->head.alloc(p->n_keys * 4);
+        JG_HIP(hipMemsetAsync(p->head.p, 0xFF, p->n_keys * 4, p->ctx->stream));
     }
-    return p->claim.as<uint32_t>();
+    if (p->next.bytes < n_rows * 4) {
+        JG_HIP(hipStreamSynchronize(p->ctx->stream));  // an earlier launch may still read the old links
+        p->next.alloc(n_rows * 4 + n_rows);
+    }
+    g = Groups{p->head.as<uint32_t>(), p->next.as<uint32_t>()};
+    return &g;
 }
 
 void launch_rows_copy(jg_ctx* ctx, uint32_t eb, void* dst, const void* src, const uint32_t* keys, uint64_t n_rows, uint32_t R,
@@ -368,7 +388,8 @@ void launch_rows_copy(jg_ctx* ctx, uint32_t eb, void* dst, const void* src, cons
 }  // namespace
 
 void jg::pnc_merge_indexed(jg_pnc* p, const void* BP, const void* BN, const uint32_t* d_keys, uint64_t n_rows) {
-    launch_merge_indexed(p->ctx, p->eb, p->P.p, p->N.p, BP, BN, d_keys, n_rows, p->R, claim_of(p));
+    Groups g;
+    launch_merge_indexed(p->ctx, p->eb, p->P.p, p->N.p, BP, BN, d_keys, n_rows, p->R, groups_of(p, n_rows, g));
 }
 
 extern "C" {
@@ -473,7 +494,8 @@ int jg_pnc_merge_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const
         void* st = jg::scratch(ctx, ctx->scratch2, 2 * bytes);
         JG_HIP(hipMemcpyAsync(st, P, bytes, hipMemcpyHostToDevice, ctx->stream));
         JG_HIP(hipMemcpyAsync((char*)st + bytes, N, bytes, hipMemcpyHostToDevice, ctx->stream));
-        if (dk) launch_merge_indexed(ctx, p->eb, p->P.p, p->N.p, st, (char*)st + bytes, dk, n_rows, p->R, claim_of(p));
+        Groups g;
+        if (dk) launch_merge_indexed(ctx, p->eb, p->P.p, p->N.p, st, (char*)st + bytes, dk, n_rows, p->R, groups_of(p, n_rows, g));
         else launch_merge_dense(ctx, p->eb, p->P.p, p->N.p, st, (char*)st + bytes, n_rows * p->R);
         JG_HIP(hipStreamSynchronize(ctx->stream));
     });
@@ -606,7 +628,8 @@ int jg_pnc_merge_batch(jg_pnc* p, const jg_rows* r, int async) {
         if (r->has_keys) {
             JG_REQUIRE(r->max_key < p->n_keys, JG_EINVAL, "jg_pnc_merge_batch: batch addresses key %u >= n_keys %llu", r->max_key,
                        (unsigned long long)p->n_keys);
-            launch_merge_indexed(ctx, p->eb, p->P.p, p->N.p, r->P.p, r->N.p, r->keys.as<uint32_t>(), r->n_rows, p->R, claim_of(p));
+            Groups g;
+            launch_merge_indexed(ctx, p->eb, p->P.p, p->N.p, r->P.p, r->N.p, r->keys.as<uint32_t>(), r->n_rows, p->R, groups_of(p, r->n_rows, g));
         } else {
             JG_REQUIRE(r->n_rows <= p->n_keys, JG_EINVAL, "jg_pnc_merge_batch: identity batch of %llu rows > n_keys",
                        (unsigned long long)r->n_rows);

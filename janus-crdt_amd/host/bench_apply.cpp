@@ -99,7 +99,8 @@ int main(int argc, char** argv) {
     };
     struct Queued { janus::NetworkProtocol np; bool safe; };
     std::vector<std::vector<Queued>> q(nodes);
-    std::unordered_map<uint64_t, uint64_t> tracker_g, tracker_c;  // safe-update tracker: seq -> client origin
+    janus::SafeUpdateTracker tracker_g;                   // safe-update tracker: seq -> client origin (GPU node)
+    std::unordered_map<uint64_t, uint64_t> tracker_c;    // the oracle node's
     uint64_t seq = 1;
 
     double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
@@ -138,7 +139,7 @@ int main(int argc, char** argv) {
             for (int j = 0; j < nodes; ++j) { g[j] = G(rep[k * nodes + j]); pv[j] = P[k * nodes + j]; nv[j] = N[k * nodes + j]; }
             janus::wire::AppendPNCounterMsg(np.message, g, pv, nv, nodes);
             if (safe) {  // SafeCRDT.cs:55-56: tracked when safe and the origin is a client
-                tracker_g[np.seq] = origin;
+                tracker_g.add(np.seq, origin);
                 tracker_c[np.seq] = origin;
                 if (w > 0) ++n_safe;
             }

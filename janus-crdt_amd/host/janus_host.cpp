@@ -303,8 +303,76 @@ char* GpuStableStore::stage(size_t bytes) {
     return r;
 }
 
-std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
-                                                     std::unordered_map<uint64_t, uint64_t>* tracker) {
+namespace {
+inline size_t seq_hash(uint64_t x) {
+    x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33;
+    return (size_t)x;
+}
+}  // namespace
+
+bool SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
+    if (seq == 0 || seq == kTomb) return false;
+    if ((used_ + 1) * 2 > slots_.size()) grow();
+    const size_t mask = slots_.size() - 1;
+    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+        const uint64_t k = slots_[i].key.load(std::memory_order_relaxed);
+        if (k == seq) return false;
+        if (k == 0) {
+            slots_[i].val = origin;
+            slots_[i].key.store(seq, std::memory_order_release);
+            ++used_;
+            n_.fetch_add(1, std::memory_order_relaxed);
+            return true;
+        }
+    }
+}
+
+bool SafeUpdateTracker::contains(uint64_t seq) const {
+    if (slots_.empty() || seq == 0 || seq == kTomb) return false;
+    const size_t mask = slots_.size() - 1;
+    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+        const uint64_t k = slots_[i].key.load(std::memory_order_acquire);
+        if (k == seq) return true;
+        if (k == 0) return false;
+    }
+}
+
+bool SafeUpdateTracker::take(uint64_t seq, uint64_t* origin) {
+    if (slots_.empty() || seq == 0 || seq == kTomb) return false;
+    const size_t mask = slots_.size() - 1;
+    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+        uint64_t k = slots_[i].key.load(std::memory_order_acquire);
+        if (k == 0) return false;
+        if (k != seq) continue;
+        const uint64_t v = slots_[i].val;
+        if (!slots_[i].key.compare_exchange_strong(k, kTomb, std::memory_order_acq_rel)) return false;  // another take won
+        n_.fetch_sub(1, std::memory_order_relaxed);
+        if (origin) *origin = v;
+        return true;
+    }
+}
+
+std::vector<std::pair<uint64_t, uint64_t>> SafeUpdateTracker::items() const {
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    for (const Slot& s : slots_) {
+        const uint64_t k = s.key.load(std::memory_order_acquire);
+        if (k != 0 && k != kTomb) out.emplace_back(k, s.val);
+    }
+    return out;
+}
+
+void SafeUpdateTracker::grow() {  // rehash the live entries (tombstones dropped), single-threaded
+    std::vector<std::pair<uint64_t, uint64_t>> live = items();
+    size_t cap = 1024;
+    while (cap < 4 * (live.size() + 1)) cap <<= 1;
+    std::vector<Slot> fresh(cap);
+    slots_.swap(fresh);
+    used_ = 0;
+    n_.store(0, std::memory_order_relaxed);
+    for (const auto& kv : live) add(kv.first, kv.second);
+}
+
+std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker) {
     const double t0 = wall_s();
     std::vector<const NetworkProtocol*> msgs;
     size_t n_msgs = 0;
@@ -338,8 +406,7 @@ void GpuStableStore::ReceivedBlock(const std::vector<UpdateMessage>& block) {
     throw ApplyError(JG_EINVAL, "The given key was not present in the dictionary. (unknown CRDT uid)", cut, {});
 }
 
-std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const NetworkProtocol*>& msgs,
-                                                 std::unordered_map<uint64_t, uint64_t>* tracker, double t0) {
+std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const NetworkProtocol*>& msgs, SafeUpdateTracker* tracker, double t0) {
     flush_registrations();
     flush_names();
     arena_i_ = arena_off_ = 0;  // the previous wave's staged chunks are no longer referenced
@@ -540,13 +607,18 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     orset_phase_s_[0] = to1 - to0;
     orset_phase_s_[1] = to3 - to2;
     orset_phase_s_[2] = wall_s() - to3;
+    // safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) of the applied prefix, in
+    // commit order: the workers take contiguous ranges, their lists concatenate in worker order
     std::vector<uint64_t> completed;
-    if (tracker)
-        for (size_t i = 0; i < cut; ++i) {
-            if (cls[i] == kSkip) continue;
-            auto tr = tracker->find(msgs[i]->seq);
-            if (tr != tracker->end()) { completed.push_back(tr->second); tracker->erase(tr); }
-        }
+    if (tracker && tracker->size()) {
+        std::vector<std::vector<uint64_t>> part(T);
+        parallel_ranges(wp, cut, [&](size_t b, size_t e, int t) {
+            uint64_t o;
+            for (size_t i = b; i < e; ++i)
+                if (cls[i] != kSkip && tracker->take(msgs[i]->seq, &o)) part[t].push_back(o);
+        });
+        for (auto& p : part) completed.insert(completed.end(), p.begin(), p.end());
+    }
     host_s_ = t1 - t0;
     engine_s_ = wall_s() - t1;
     if (cut < n) throw ApplyError(cut_code, cut_why, cut, std::move(completed));
@@ -695,7 +767,7 @@ std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Gui
 
 std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize,
                                                          std::vector<UpdateMessage>& submitted,
-                                                         std::unordered_map<uint64_t, uint64_t>& tracker) {
+                                                         SafeUpdateTracker& tracker) {
     const size_t n = ups.size();
     for (const ClientUpdate& u : ups) {  // the wrappers' checks, before anything is applied or queued
         const KeyRef* kr = uids_.find(u.op.uid);
@@ -718,7 +790,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         np.uid = ups[i].op.uid;
         np.syncMsgType = NetworkProtocol::CRDTMsg;
         np.seq = next_seq_++;
-        if (ups[i].isSafe && ups[i].origin != 0) tracker[np.seq] = ups[i].origin;  // SafeCRDT.cs:55-56
+        if (ups[i].isSafe && ups[i].origin != 0) tracker.add(np.seq, ups[i].origin);  // SafeCRDT.cs:55-56
         q.emplace_back(std::move(np), (int64_t)i);
         if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
             std::vector<std::pair<NetworkProtocol, int64_t>> safe, appeared;
@@ -726,7 +798,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             while (head < q.size()) {
                 auto e = std::move(q[head++]);                       // TryDequeue first ...
                 if (!((int)safe.size() < clientBatchSize)) break;     // ... so this one is lost (:175)
-                if (!tracker.count(e.first.seq)) {
+                if (!tracker.contains(e.first.seq)) {
                     auto it = pos.find(e.first.uid);
                     if (it == pos.end()) { pos.emplace(e.first.uid, appeared.size()); appeared.push_back(std::move(e)); }
                     else appeared[it->second] = std::move(e);        // last state wins, position kept

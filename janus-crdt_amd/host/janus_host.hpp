@@ -20,6 +20,7 @@
 #pragma once
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <optional>
@@ -75,6 +76,35 @@ struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
 // message in msgs[first..] in ONE device call (jg_update_digests).
 void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first = 0);
 
+// SafeCRDTManager.safeUpdateTracker (SafeCRDTManager.cs:33, a ConcurrentDictionary<NetworkProtocol,
+// (Connection, uint)>): message identity (NetworkProtocol.seq, >= 1) -> client origin.  TryAdd / ContainsKey
+// from one thread (the batcher); TryRemove (take) from many threads at once — the apply loop removes a
+// wave's completed messages in parallel (open addressing; a removed slot becomes a tombstone, so
+// concurrent takes of different keys never move an entry).
+class SafeUpdateTracker {
+  public:
+    SafeUpdateTracker() = default;
+    template <class It> SafeUpdateTracker(It b, It e) { for (; b != e; ++b) add(b->first, b->second); }
+    SafeUpdateTracker(const SafeUpdateTracker& o) { for (const auto& kv : o.items()) add(kv.first, kv.second); }
+    SafeUpdateTracker& operator=(const SafeUpdateTracker& o) {
+        if (this != &o) { slots_.clear(); n_ = used_ = 0; for (const auto& kv : o.items()) add(kv.first, kv.second); }
+        return *this;
+    }
+    bool add(uint64_t seq, uint64_t origin);          // TryAdd: false if present (seq 0 is not a message)
+    bool contains(uint64_t seq) const;
+    bool take(uint64_t seq, uint64_t* origin);        // TryRemove; safe against concurrent take()s
+    size_t size() const { return n_.load(std::memory_order_relaxed); }
+    std::vector<std::pair<uint64_t, uint64_t>> items() const;  // live entries (any order)
+
+  private:
+    struct Slot { std::atomic<uint64_t> key{0}; uint64_t val = 0; };  // key 0 empty, kTomb removed
+    static constexpr uint64_t kTomb = ~0ull;
+    void grow();
+    std::vector<Slot> slots_;
+    std::atomic<size_t> n_{0};
+    size_t used_ = 0;  // live + tombstones
+};
+
 struct EngineError : std::runtime_error {
     int code;
     EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
@@ -126,8 +156,7 @@ class GpuStableStore {
     // ONE jg_orset_merge, then report the safe updates that completed, in commit order (:141-142).
     // `tracker` maps message seq -> client origin; matched entries are removed like
     // ConcurrentDictionary.TryRemove.  A rejected payload throws ApplyError after applying the prefix.
-    std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates,
-                                         std::unordered_map<uint64_t, uint64_t>* tracker = nullptr);
+    std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker = nullptr);
 
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
     // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the
@@ -155,7 +184,7 @@ class GpuStableStore {
     // (or stay queued) are encoded — on the device, after applying the ops up to that point.  Returns
     // each op's bool result; validation failures throw before anything is applied.
     std::vector<uint8_t> SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize, std::vector<UpdateMessage>& submitted,
-                                             std::unordered_map<uint64_t, uint64_t>& tracker);
+                                             SafeUpdateTracker& tracker);
     // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys from the device store (jg_orset_read_sets),
     // byte for byte the reference's: Dictionary and HashSet enumeration orders come from the records'
     // arrival ordinals (jg_tagrec.ord; addSet elements in ascending interned id).
@@ -239,8 +268,7 @@ class GpuStableStore {
     void check(int rc) const;
     void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
     // The body of ApplyCommitted / ReceivedBlock over the flattened messages (commit order).
-    std::vector<uint64_t> apply_msgs(const std::vector<const NetworkProtocol*>& msgs, std::unordered_map<uint64_t, uint64_t>* tracker,
-                                     double t0);
+    std::vector<uint64_t> apply_msgs(const std::vector<const NetworkProtocol*>& msgs, SafeUpdateTracker* tracker, double t0);
     char* stage(size_t bytes);  // pinned staging of one wave chunk (jg_host_alloc arenas, reused wave after wave)
     WorkerPool& pool();                     // persistent host workers (host_threads())
 

@@ -88,7 +88,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     janus::GpuStableStore gpu_p(0, n_pnc + 1, 8, eb);  // node 0's PROSPECTIVE copies (ApplyOp + block-receipt merges)
     gpu_p.SetNextMessageSeq(nodes[0]->nextSeq);
     std::vector<janus::ClientUpdate> pending;           // node 0's client updates since the last wave
-    std::unordered_map<uint64_t, uint64_t> tracker_p;   // node 0's safe messages, as produced on the GPU
+    janus::SafeUpdateTracker tracker_p;   // node 0's safe messages, as produced on the GPU
     std::vector<uint8_t> pending_res;                   // the oracle's results for them
     std::vector<std::string> keys;
     for (int k = 0; k < n_pnc + n_set; ++k) {
@@ -141,7 +141,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         pending.clear();
         pending_res.clear();
         for (size_t src = 1; src < jw.size(); ++src) gpu_p.ReceivedBlock(jw[src]);  // one block per other node
-        std::unordered_map<uint64_t, uint64_t> tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
+        janus::SafeUpdateTracker tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
         const size_t before = nodes[0]->notified.size();
         for (auto& n : nodes) n->HandleAfterConsensusUpdates(wave);
         auto done = gpu.ApplyCommitted(jw, &tracker);
@@ -325,7 +325,7 @@ int bad_wave() {
         for (auto& um : wave[0])
             for (auto& np : um.update)
                 if (seen++ == bad_at) np.bytes = bad_at == 9 ? "{\"pVector\":{}}" : "{\"addSet\":null}";
-        std::unordered_map<uint64_t, uint64_t> tracker(node.safeUpdateTracker.begin(), node.safeUpdateTracker.end());
+        janus::SafeUpdateTracker tracker(node.safeUpdateTracker.begin(), node.safeUpdateTracker.end());
         const size_t before = node.notified.size();
         bool othrew = false;
         try { node.HandleAfterConsensusUpdates(wave); } catch (const oracle::json::JsonException&) { othrew = true; }
@@ -356,7 +356,8 @@ int bad_wave() {
         }
         // keep the oracle and the GPU in step for the next round: the reference node's tracker keeps
         // the entries of messages it never applied; so does ours.
-        node.safeUpdateTracker = std::unordered_map<uint64_t, uint64_t>(tracker.begin(), tracker.end());
+        const auto left = tracker.items();
+        node.safeUpdateTracker = std::unordered_map<uint64_t, uint64_t>(left.begin(), left.end());
     }
     return 0;
 }

@@ -54,19 +54,25 @@ def test_merge_indexed_repeated_keys(ctx, eb):
 @pytest.mark.parametrize("eb", [4, 8])
 @pytest.mark.parametrize("R", [32, 64, 130])
 def test_merge_indexed_unique_and_repeated_rows(ctx, eb, R):
-    """The duplicate-aware path (R x width a whole number of 16-B vectors, R >= 32): keys seen once
-    in a batch take the plain vector RMW, repeated keys the atomics; the per-key claim counters are
-    reset, so a second batch over the same keys merges exactly too."""
+    """The grouped path (R x width a whole number of 16-B vectors, R >= 32): every key's rows are folded
+    by its list head (one A row load and store; a key seen once is its own list); heads are reset, so the
+    next batch over the same keys merges exactly too.  Round 3 mixes unique, 7-, 64-, 65- and 400-row keys
+    in one batch."""
     rng = np.random.default_rng(R * 10 + eb)
     n_keys, M = 20_000, 6_000
     AP, AN = random_pnc(rng, n_keys, R, eb, absent=False), random_pnc(rng, n_keys, R, eb, absent=False)
     s = jg.PNCStore(ctx, n_keys, R, eb)
     eP, eN = AP, AN
+    mixed = np.concatenate([np.arange(2000, 4000), np.repeat(np.arange(10), 7), np.repeat([77, 78], 64), np.repeat([5000], 65),
+                            np.repeat([6000], 400)])
     try:
         s.write_rows(AP, AN)
-        for rnd in range(3):
-            BP, BN = random_pnc(rng, M, R, eb), random_pnc(rng, M, R, eb)
-            keys = rng.integers(0, n_keys if rnd != 1 else 50, M).astype(np.uint32)  # mostly unique / hot keys
+        for rnd in range(4):
+            if rnd == 3:
+                keys = rng.permutation(mixed).astype(np.uint32)
+            else:
+                keys = rng.integers(0, n_keys if rnd != 1 else 50, M).astype(np.uint32)  # mostly unique / hot keys
+            BP, BN = random_pnc(rng, keys.size, R, eb), random_pnc(rng, keys.size, R, eb)
             s.merge_rows(BP, BN, keys)
             eP, eN = orc.pnc_merge(eP, eN, BP, BN, keys)
         P, N = s.read_rows()
