@@ -275,6 +275,66 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
                            "torch.distributed all_to_all_single over RCCL (xGMI)")}
 
 
+JSON_MSGS, JSON_KEYS, JSON_R, JSON_EB, JSON_NODES = 1_000_000, 1_000_000, 5, 4, 4  # one C5 wave, device-resident
+
+
+def json_wave(seed, n=JSON_MSGS, n_keys=JSON_KEYS):
+    """C5-shaped PNCounterMsg states (compact System.Text.Json form): message m is the state of key keys[m]
+    as one of JSON_NODES nodes knows it, naming 1..JSON_NODES replicas of that key with int32 values.
+    Replica Guids per key come from 4096 pools (Guids need only be distinct within a key's row)."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    from jsongen import encode_pnc, random_guids
+    rng = np.random.default_rng(seed)
+    T, V = 4096, 8
+    pools = [random_guids(rng, JSON_NODES) for _ in range(T)]
+    var = [[encode_pnc(pools[t][: 1 + (v % JSON_NODES)], list(rng.integers(0, 2**31 - 1, JSON_NODES)),
+                       list(rng.integers(0, 2**31 - 1, JSON_NODES))) for v in range(V)] for t in range(T)]
+    keys = rng.integers(0, n_keys, n).astype(np.uint32)
+    pick = rng.integers(0, V, n)
+    msgs = [var[k % T][v] for k, v in zip(keys.tolist(), pick.tolist())]
+    lens = np.fromiter((len(x) for x in msgs), np.uint64, n)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    data = np.frombuffer(b"".join(msgs), np.uint8)
+    entries = int(sum(2 * (1 + (v % JSON_NODES)) for v in pick.tolist()))
+    return keys, data, off, entries
+
+
+def bench_json(jg, ctx, sync, rank, steps, warmup):
+    """The committed-wave apply from wire bytes (json.hip: k_scan + k_resolve + k_apply) on one C5 wave
+    resident in HBM (jg_wave_upload once, jg_pnc_merge_wave per step): steady state (every replica known:
+    scan + apply) and a cold wave (every message names replicas its row has not seen: scan + sort +
+    resolve + apply).  Algorithmic bytes per message: its payload, offset (8 B) and row index (4 B), per
+    entry one int32 cell read + written."""
+    keys, data, off, entries = json_wave(SEED + 53 + rank)
+    w = jg.Wave(ctx, JSON_MSGS, data.size)
+    warm = jg.PNCStore(ctx, JSON_KEYS, JSON_R, JSON_EB)
+    try:
+        w.upload(keys, data=data, off=off)
+        wall, ev = timed(ctx, sync, lambda: warm.merge_wave(w), steps, warmup)
+        cold_ms = []
+        for _ in range(2):
+            cold = jg.PNCStore(ctx, JSON_KEYS, JSON_R, JSON_EB)
+            t0 = time.perf_counter()
+            cold.merge_wave(w)
+            cold_ms.append((time.perf_counter() - t0) * 1e3)
+            cold.close()
+    finally:
+        warm.close()
+        w.close()
+    alg = data.size + 12 * JSON_MSGS + 2 * JSON_EB * entries
+    kern = ev / steps
+    return {"workload": f"PNCounterMsg wave from wire bytes (C5 shape: {JSON_MSGS} states of {JSON_KEYS} accounts, "
+                        f"{JSON_R - 1}-node replicas, int32), resident in HBM, steady state (replicas known)",
+            "msgs_per_s": JSON_MSGS / (wall / steps), "ms_per_wave": wall / steps * 1e3, "event_ms": kern * 1e3,
+            "payload_bytes": int(data.size), "engine_payload_GBps": data.size / kern / 1e9,
+            "cold_wave_ms": min(cold_ms), "json_group": int(os.environ.get("JANUS_JSON_GROUP", "8")),
+            "roofline": {"bound": "hbm", "achieved": alg / kern / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / kern / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_wave": alg,
+                         "scope": "jg_pnc_merge_wave (k_scan + k_apply, status reads) per step"}}
+
+
 def bench_apply_loop(sync, rank, world, local):
     """C5 committed-batch apply (the banking replay, BankingWorload.cs ops through the
     node batchers, 1M client ops per committed wave) through the C++ host mirror, on every rank.  Every
@@ -450,7 +510,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest"], default="all")
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest", "json"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnc-shape", choices=["auto"] + sorted(PNC_SHAPES), default="auto",
                     help="per-GPU PN-Counter shard: c2 = BASELINE configs[1], c4 = 1/8 of configs[3]; "
@@ -466,7 +526,7 @@ def main():
         sys.exit("--scaling strong needs N >= 4: configs[3]'s 200M keys x 128 replicas (A + B = 819.2 GB) do not fit fewer MI355X")
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-    if world > 1 or args.workload in ("all", "exchange", "digest"):
+    if world > 1 or args.workload in ("all", "exchange", "digest", "json"):
         # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
         # instance (torch's libraries also name the runtime by an unversioned soname)
         import torch  # noqa: F401
@@ -484,6 +544,11 @@ def main():
             res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
         except Exception as e:  # noqa: BLE001
             res["exchange"] = {"error": repr(e)[:500]}
+    if args.workload in ("all", "json"):
+        try:
+            res["json"] = bench_json(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
+        except Exception as e:  # noqa: BLE001
+            res["json"] = {"error": repr(e)[:500]}
     if args.workload in ("all", "digest"):
         try:
             res["digest"] = bench_digest(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
@@ -549,6 +614,8 @@ def main():
         line["exchange"] = res["exchange"]
     if "digest" in res:
         line["update_digests"] = res["digest"]
+    if "json" in res:
+        line["json_apply"] = res["json"]
     if apply_loop is not None:
         line["apply_loop"] = apply_loop
     if apply_orset is not None:

@@ -104,8 +104,9 @@ struct jg_pnc {
     // grouped indexed merge (k_group_*): per-key list head of the batch being merged (0xFFFFFFFF between
     // calls) and a next[] link per received row; first use
     jg::DevBuf head, next;
-    // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list
-    jg::DevBuf wbytes, woff, wrows, wstat;
+    // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list; pass A's
+    // resolved entries per message and its list of messages pass B must parse again (json.hip)
+    jg::DevBuf wbytes, woff, wrows, wstat, wemit, wslow;
     uint64_t wn = 0, wnb = 0;
     bool wopen = false;
 };

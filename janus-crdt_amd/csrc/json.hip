@@ -6,7 +6,8 @@
 // message at a time inside HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160).  Here a whole
 // wave of PNCounterMsg JSON payloads is uploaded once and decoded, interned and merged on the GPU:
 //
-//   pass A  k_scan      one thread per message: full parse + validation (the wire contract of
+//   pass A  k_scan      a group of lanes per message (json_wave.hpp; the serial parser for payloads
+//                       not in the compact form): full parse + validation (the wire contract of
 //                       oracle/json.hpp), every Guid looked up in its row's replica table (read-only);
 //                       a Guid repeated among a vector's known replicas is an error; a message naming a
 //                       replica its row has not seen is DEFERRED (row << 32 | msg appended to a list).
@@ -17,12 +18,13 @@
 //                       order) to the row's table: first-insertion order = the stable Dictionary's
 //                       enumeration order.  A full row or a Guid repeated in one vector rolls the
 //                       appended columns back and fails the call.
-//   pass B  k_apply     one thread per message: parse again, every Guid now resolves, atomicMax into
+//   pass B  k_apply     a group of lanes per message: parse again, every Guid now resolves, atomicMax into
 //                       P / N (messages of one wave may repeat a key; max is order-free).
 //
-// Parsing is byte-serial per thread through a 16-byte window register (one aligned global load per
-// 16 bytes), so a message costs ~len/16 loads; the bound of the end-to-end call is the PCIe upload of
-// the payload, not the parse.
+// The serial parser (scan_one / apply_one, the fallback) is byte-serial per thread through a 16-byte
+// window register; the group parse loads a message's windows side by side and checks its tokens in
+// parallel (json_wave.hpp).  The bound of the end-to-end call is the PCIe upload of the payload
+// (DESIGN.md §4).
 //
 // Replica table (jg_pnc::cols / ncols, allocated on first use): [n_keys x R] Guids + [n_keys] counts.
 // P and N share one column per replica: the reference keeps two dictionaries whose key orders coincide
@@ -194,14 +196,21 @@ struct ScanVis {
     }
 };
 
+// Pass A's per-message output (json_wave.hpp writes it for the payloads it proves compact): a u16
+// entry count (kReparse: pass B parses the message again), a u16 code per entry (column | vector << 15),
+// then the entries' values at +32.  Entries in token order; at most kEmitMax.
+constexpr uint32_t kEmitMax = 14;
+constexpr uint16_t kReparse = 0xFFFF;
+__host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kEmitMax * eb; }
+
+// Serial pass-A body for one message (one lane): the definitive parse.  A message it accepts goes to
+// the deferred list (a replica its row has not seen) or to the `slow` list (pass B parses it again).
 template <int EB>
-__global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 const uint32_t* __restrict__ rows, uint64_t m0, uint64_t m1, Table t,
-                                                 unsigned long long* __restrict__ status /* [0] first bad, [1] n deferred */,
-                                                 unsigned long long* __restrict__ deferred) {
-    const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= m1) return;
+__device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ rows, uint64_t m,
+                         const Table& t, unsigned long long* __restrict__ status, unsigned long long* __restrict__ deferred,
+                         uint8_t* __restrict__ emit, unsigned long long* __restrict__ slow) {
     const uint32_t row = rows[m];
+    *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = kReparse;
     Cursor c(bytes, off[m], off[m + 1]);
     ScanVis vis{t.cols + (uint64_t)row * t.R, t.ncols[row]};
     if (!parse_pnc<EB>(c, vis)) {
@@ -211,6 +220,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
     if (vis.miss) {
         const unsigned long long at = atomicAdd(status + 1, 1ull);
         deferred[at] = (unsigned long long)row << 32 | m;
+    } else {
+        const unsigned long long at = atomicAdd(status + 3, 1ull);
+        slow[at] = m;
     }
 }
 
@@ -220,15 +232,23 @@ __global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) 
     if (i < n) off[i] += base;
 }
 
-// Pass C visitor: exclusive owner of the row; appends new Guids.
+// Pass C visitor: exclusive owner of the row; appends new Guids.  Merge visits every pVector entry
+// before any nVector entry (PNCounters.cs:133-143): one parse covers both when pVector comes first in
+// the text (every Encode'd state); an nVector ahead of its pVector is skipped and visited by a second
+// parse (`only` = 1) once the pVector is in.
 struct ResolveVis {
     Guid16* row;
     uint32_t* ncol;
     uint32_t R;
     Mask256 m;
     uint32_t err = UINT32_MAX;
-    __device__ void begin_vector(int) { m.clear(); }
-    __device__ bool entry(int, uint32_t pos, const Guid16& g, long long) {
+    bool p_seen = false, n_skipped = false;
+    __device__ void begin_vector(int which) {
+        m.clear();
+        if (which == 0) p_seen = true;
+    }
+    __device__ bool entry(int which, uint32_t pos, const Guid16& g, long long) {
+        if (which == 1 && !p_seen) { n_skipped = true; return true; }
         uint32_t c = find_col(row, *ncol, g, pos);
         if (c == UINT32_MAX) {
             if (*ncol >= R) { err = kErrFull; return false; }
@@ -240,28 +260,35 @@ struct ResolveVis {
     }
 };
 
-// One thread per sorted deferred entry; segment heads (first entry of a row) walk their row's
+// One message of a row's walk (serial): new Guids appended to the row; returns an error code or UINT32_MAX.
+template <int EB>
+__device__ uint32_t resolve_msg(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, uint64_t m, Guid16* row, uint32_t* ncol,
+                                uint32_t R) {
+    ResolveVis vis{row, ncol, R};
+    Cursor c(bytes, off[m], off[m + 1]);
+    bool ok = parse_pnc<EB>(c, vis);
+    if (ok && vis.n_skipped) {
+        Cursor c2(bytes, off[m], off[m + 1]);
+        ok = parse_pnc<EB>(c2, vis, 1);
+    }
+    return ok ? UINT32_MAX : vis.err == UINT32_MAX ? kErrInternal : vis.err;
+}
+
+// Serial pass C for sorted deferred entry i: a segment head (first entry of a row) walks its row's
 // messages in commit order.  saved[i] = the head's ncols before the walk (for roll-back).
 template <int EB>
-__global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                    const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
-                                                    uint32_t* __restrict__ saved, unsigned long long* __restrict__ status) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= nd) return;
+__device__ void resolve_one(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const unsigned long long* __restrict__ keys,
+                            uint64_t nd, uint64_t i, const Table& t, uint32_t* __restrict__ saved, unsigned long long* __restrict__ status) {
     const uint32_t row = (uint32_t)(keys[i] >> 32);
     if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;
     uint32_t* ncol = t.ncols + row;
     saved[i] = *ncol;
-    ResolveVis vis{t.cols + (uint64_t)row * t.R, ncol, t.R};
     for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
         const uint64_t m = (uint32_t)keys[j];
-        // Merge visits every pVector entry before any nVector entry (PNCounters.cs:133-143)
-        for (int which = 0; which < 2; ++which) {
-            Cursor c(bytes, off[m], off[m + 1]);
-            if (!parse_pnc<EB>(c, vis, which)) {
-                atomicMin(status + 2, (unsigned long long)m << 2 | (vis.err == UINT32_MAX ? kErrInternal : vis.err));
-                return;
-            }
+        const uint32_t err = resolve_msg<EB>(bytes, off, m, t.cols + (uint64_t)row * t.R, ncol, t.R);
+        if (err != UINT32_MAX) {
+            atomicMin(status + 2, (unsigned long long)m << 2 | err);
+            return;
         }
     }
 }
@@ -294,18 +321,17 @@ struct ApplyVis {
 };
 
 template <int EB>
-__global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ rows, uint64_t n, Table t, void* P, void* N,
-                                                  unsigned long long* __restrict__ status) {
+__device__ void apply_one(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ rows, uint64_t m,
+                          const Table& t, void* P, void* N, unsigned long long* __restrict__ status) {
     using T = typename ApplyVis<EB>::T;
-    const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= n) return;
     const uint32_t row = rows[m];
     const uint64_t base = (uint64_t)row * t.R;
     Cursor c(bytes, off[m], off[m + 1]);
     ApplyVis<EB> vis{static_cast<T*>(P) + base, static_cast<T*>(N) + base, t.cols + base, t.ncols[row]};
     if (!parse_pnc<EB>(c, vis)) atomicMin(status + 2, (unsigned long long)m << 2 | kErrInternal);
 }
+
+#include "json_wave.hpp"
 
 // jg_pnc_intern: entries (row, guid) in order; keys = row << 32 | i sorted; segment heads walk.
 __global__ __launch_bounds__(kBlock) void k_intern(const unsigned long long* __restrict__ keys, uint64_t n, const Guid16* __restrict__ g,
@@ -452,7 +478,7 @@ unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n,
     return out;
 }
 
-struct Status { unsigned long long first_bad, n_deferred, resolve_bad, pad; };
+struct Status { unsigned long long first_bad, n_deferred, resolve_bad, n_slow; };
 
 Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     Status s;
@@ -482,11 +508,14 @@ void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep) {
     std::swap(nb.bytes, b.bytes);
 }
 
-// Wave-level device scratch: status words, the deferred list and its roll-back slots (n messages).
+// Wave-level device scratch: status words, the deferred list and its roll-back slots (n messages),
+// pass A's per-message entries and its list of messages for pass B to parse again.
 struct WaveScratch {
     unsigned long long* status;
     unsigned long long* deferred;
     uint32_t* saved;
+    uint8_t* emit;
+    unsigned long long* slow;
 };
 
 // Room for n messages; growing keeps the status words and the first `keep` deferred entries (a
@@ -495,10 +524,13 @@ struct WaveScratch {
 WaveScratch wave_scratch(jg_pnc* p, uint64_t n, uint64_t keep = 0) {
     const size_t need = 64 + n * 8 + n * 4 + 256;
     if (p->wstat.bytes < need) grow_keep(p->ctx, p->wstat, need, p->wstat.p ? 64 + keep * 8 : 0);
+    grow_keep(p->ctx, p->wemit, n * emit_stride(p->eb) + 256, keep * emit_stride(p->eb));
+    grow_keep(p->ctx, p->wslow, n * 8 + 256, keep * 8);
     n = (p->wstat.bytes - 64 - 256) / 12;  // the capacity actually there
     char* s = p->wstat.as<char>();
     return WaveScratch{reinterpret_cast<unsigned long long*>(s), reinterpret_cast<unsigned long long*>(s + 64),
-                       reinterpret_cast<uint32_t*>(s + 64 + ((n * 8 + 15) & ~15ull))};
+                       reinterpret_cast<uint32_t*>(s + 64 + ((n * 8 + 15) & ~15ull)), p->wemit.as<uint8_t>(),
+                       p->wslow.as<unsigned long long>()};
 }
 
 void reset_status(jg_ctx* ctx, unsigned long long* status) {
@@ -510,9 +542,9 @@ void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
                  const WaveScratch& w) {
     if (m1 <= m0) return;
     const Table t = table_of(p);
-    const unsigned g = blocks_for(m1 - m0);
-    if (p->eb == 8) hipLaunchKernelGGL(k_scan<8>, dim3(g), dim3(kBlock), 0, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred);
-    else hipLaunchKernelGGL(k_scan<4>, dim3(g), dim3(kBlock), 0, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred);
+    const int G = json_group();
+    if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.slow);
+    else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.slow);
     JG_HIP(hipGetLastError());
 }
 
@@ -523,12 +555,15 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     const Table t = table_of(p);
     Status st = read_status(ctx, w.status);
     if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
+    unsigned long long* sorted_deferred = nullptr;
     if (st.n_deferred) {
         const uint64_t nd = st.n_deferred;
         unsigned long long* sorted = sort_keys(ctx, w.deferred, nd, p->n_keys);
+        sorted_deferred = sorted;
         const unsigned gd = blocks_for(nd);
-        if (p->eb == 8) hipLaunchKernelGGL(k_resolve<8>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
-        else hipLaunchKernelGGL(k_resolve<4>, dim3(gd), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
+        const int G = json_group();
+        if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
+        else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
         JG_HIP(hipGetLastError());
         st = read_status(ctx, w.status);
         if (st.resolve_bad != ~0ull) {
@@ -538,10 +573,21 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
             fail_msg(st.resolve_bad, bad_msg, "state message");
         }
     }
-    const unsigned g = blocks_for(n);
-    if (p->eb == 8) hipLaunchKernelGGL(k_apply<8>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, w.status);
-    else hipLaunchKernelGGL(k_apply<4>, dim3(g), dim3(kBlock), 0, ctx->stream, bytes, off, rows, n, t, p->P.p, p->N.p, w.status);
+    // pass B: pass A's resolved entries, then the messages it left to parse again (deferred: now every
+    // replica resolves; slow: not in the compact form).  max is order-free.
+    const int G = json_group();
+    const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
+    if (p->eb == 8) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
+    else hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
     JG_HIP(hipGetLastError());
+    const unsigned long long* lists[2] = {st.n_deferred ? sorted_deferred : nullptr, w.slow};
+    const uint64_t counts[2] = {st.n_deferred, st.n_slow};
+    for (int l = 0; l < 2; ++l) {
+        if (!counts[l]) continue;
+        if (p->eb == 8) launch_apply_g<8>(G, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        else launch_apply_g<4>(G, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        JG_HIP(hipGetLastError());
+    }
     st = read_status(ctx, w.status);
     if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
 }

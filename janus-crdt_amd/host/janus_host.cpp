@@ -303,18 +303,11 @@ char* GpuStableStore::stage(size_t bytes) {
     return r;
 }
 
-namespace {
-inline size_t seq_hash(uint64_t x) {
-    x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33;
-    return (size_t)x;
-}
-}  // namespace
-
 bool SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
     if (seq == 0 || seq == kTomb) return false;
     if ((used_ + 1) * 2 > slots_.size()) grow();
     const size_t mask = slots_.size() - 1;
-    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+    for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
         const uint64_t k = slots_[i].key.load(std::memory_order_relaxed);
         if (k == seq) return false;
         if (k == 0) {
@@ -330,23 +323,22 @@ bool SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
 bool SafeUpdateTracker::contains(uint64_t seq) const {
     if (slots_.empty() || seq == 0 || seq == kTomb) return false;
     const size_t mask = slots_.size() - 1;
-    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+    for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
         const uint64_t k = slots_[i].key.load(std::memory_order_acquire);
         if (k == seq) return true;
         if (k == 0) return false;
     }
 }
 
-bool SafeUpdateTracker::take(uint64_t seq, uint64_t* origin) {
+bool SafeUpdateTracker::claim(uint64_t seq, uint64_t* origin) {
     if (slots_.empty() || seq == 0 || seq == kTomb) return false;
     const size_t mask = slots_.size() - 1;
-    for (size_t i = seq_hash(seq) & mask;; i = (i + 1) & mask) {
+    for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
         uint64_t k = slots_[i].key.load(std::memory_order_acquire);
         if (k == 0) return false;
         if (k != seq) continue;
         const uint64_t v = slots_[i].val;
         if (!slots_[i].key.compare_exchange_strong(k, kTomb, std::memory_order_acq_rel)) return false;  // another take won
-        n_.fetch_sub(1, std::memory_order_relaxed);
         if (origin) *origin = v;
         return true;
     }
@@ -428,10 +420,15 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     // runs the validation pass of chunk c-1 (the append calls return once queued).  A chunk's pinned
     // buffer: [payload | pad 16 | off (m+1) u64 | rows or set ids u32]; untouched until commit / abort.
     // cls[i]: PNC row, kSet (sid[i] = the set), or kSkip (create / keyspace / unknown uid, :133-136).
-    std::vector<uint32_t> cls(n), sid(n);
+    if (cls_.size() < n) cls_.resize(n), sid_.resize(n);  // wave scratch kept across waves (no page faults)
+    uint32_t* cls = cls_.data();
+    uint32_t* sid = sid_.data();
     struct Chunk { size_t m; char* buf; uint64_t* off; uint32_t* rows; uint8_t* bytes; };
     std::vector<Chunk> chunks[2];
-    std::vector<uint64_t> where[2];  // message of a kind (wave order) -> commit index
+    // where_[kind][j]: commit index of the kind's j-th message (wave order); nw[kind] entries
+    size_t nw[2] = {0, 0};
+    for (auto& w : where_)
+        if (w.size() < n) w.resize(n);
     std::vector<size_t> cnt(2 * T), nbytes(2 * T), mbase(2 * (T + 1)), bbase(2 * (T + 1));
     const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
     bool open[2] = {false, false};
@@ -481,8 +478,8 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             char* buf = stage(nb_pad + (m[kind] + 1) * 8 + m[kind] * 4 + 64);
             ch[kind] = Chunk{m[kind], buf, reinterpret_cast<uint64_t*>(buf + nb_pad), nullptr, reinterpret_cast<uint8_t*>(buf)};
             ch[kind].rows = reinterpret_cast<uint32_t*>(ch[kind].off + m[kind] + 1);
-            w0[kind] = where[kind].size();
-            where[kind].resize(w0[kind] + m[kind]);
+            w0[kind] = nw[kind];
+            nw[kind] += m[kind];
         }
         const double tg = wall_s();
         parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
@@ -497,15 +494,13 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                 std::memcpy(k.bytes + o[kind], p.data(), p.size());
                 k.off[j[kind]] = o[kind];
                 k.rows[j[kind]] = kind ? sid[i] : cls[i];
-                where[kind][w0[kind] + j[kind]] = i;
+                where_[kind][w0[kind] + j[kind]] = i;
                 o[kind] += p.size();
                 ++j[kind];
             }
         });
         t_gather += wall_s() - tb;
-        if (std::getenv("JANUS_TRACE_WAVE"))
-            std::fprintf(stderr, "chunk %zu: classify %.2f ms, buffers %.2f ms, gather %.2f ms (%zu + %zu msgs, %zu + %zu bytes)\n", c,
-                         1e3 * (tb - ta), 1e3 * (tg - tb), 1e3 * (wall_s() - tg), m[0], m[1], nb[0], nb[1]);
+        const double tq = wall_s();
         for (int kind = 0; kind < 2; ++kind) {
             if (m[kind] == 0) continue;
             ch[kind].off[m[kind]] = nb[kind];
@@ -524,6 +519,9 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             }
             chunks[kind].push_back(ch[kind]);
         }
+        if (std::getenv("JANUS_TRACE_WAVE"))
+            std::fprintf(stderr, "chunk %zu: classify %.2f ms, buffers %.2f ms, gather %.2f ms, append %.2f ms (%zu + %zu msgs, %zu + %zu bytes)\n",
+                         c, 1e3 * (tb - ta), 1e3 * (tg - tb), 1e3 * (tq - tg), 1e3 * (wall_s() - tq), m[0], m[1], nb[0], nb[1]);
     }
     phase_s_[1] = t_classify;
     phase_s_[2] = t_classify + t_gather;
@@ -534,93 +532,133 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         if (tot_m) avg_msg_bytes_ = (double)tot_b / (double)tot_m;
     }
 
-    // OR-Set states: end the device validation; the first rejected state cuts the wave (the reference's
-    // loop stops at the state whose Decode / Merge throws).
     size_t cut = n;
     int cut_code = JG_OK;
     std::string cut_why;
-    const double to0 = wall_s();
-    if (open[1]) {
-        uint64_t bad = UINT64_MAX;
-        const int rc = jg_orset_wave_check(orset_, &bad);
-        if (rc != JG_OK) {
-            const std::string why = last_error();
-            if (bad == UINT64_MAX) {
-                if (open[0]) jg_pnc_wave_abort(pnc_);
-                jg_orset_wave_abort(orset_);
-                throw EngineError(rc, why);
-            }
-            cut = where[1][bad];
-            cut_code = rc;
-            cut_why = why;
+    double to0 = 0, to1 = 0, t1 = 0;
+    // The safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) are claimed by the
+    // workers while the caller runs the device side below (validation, commit): one random tracker probe
+    // per message, hidden behind the GPU.  Worker t > 0 sweeps a contiguous range, so concatenating the
+    // claims in worker order keeps commit order; claims at or past the cut are put back afterwards.
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> part(T);  // (message, origin)
+    const bool sweep = tracker && tracker->size();
+    auto sweep_range = [&](size_t b, size_t e, int t) {
+        uint64_t o;
+        for (size_t i = b; i < e; ++i) {
+            if (i + 8 < e && cls[i + 8] != kSkip) tracker->prefetch(msgs[i + 8]->seq);
+            if (cls[i] != kSkip && tracker->claim(msgs[i]->seq, &o)) part[t].emplace_back(i, o);
         }
-    }
-    const double to1 = wall_s();
-    phase_s_[3] = wall_s() - t0;
-
-    const double t1 = wall_s();
-    // Re-stream the first `limit` PNC messages (the reference's loop applied the messages before the
-    // one that threw; the engine's PN-Counter waves are all or nothing).
-    auto submit_prefix = [&](size_t limit) {
-        if (limit == 0) return;
-        check(jg_pnc_wave_begin(pnc_, limit, 1));
-        size_t left = limit;
-        for (const Chunk& ch : chunks[0]) {
-            if (!left) break;
-            const size_t k = std::min(left, ch.m);
-            check(jg_pnc_wave_append(pnc_, k, ch.rows, ch.off, ch.bytes));
-            left -= k;
-        }
-        check(jg_pnc_wave_commit(pnc_, nullptr));
     };
-    if (open[0]) {
-        if (cut < n) {  // an OR-Set state before some of these PNC states was rejected
-            check(jg_pnc_wave_abort(pnc_));
-            submit_prefix((size_t)(std::lower_bound(where[0].begin(), where[0].end(), (uint64_t)cut) - where[0].begin()));
-        } else {
+    auto device_side = [&] {
+        // OR-Set states: end the device validation; the first rejected state cuts the wave (the reference's
+        // loop stops at the state whose Decode / Merge throws).
+        to0 = wall_s();
+        if (open[1]) {
             uint64_t bad = UINT64_MAX;
-            const int rc = jg_pnc_wave_commit(pnc_, &bad);
+            const int rc = jg_orset_wave_check(orset_, &bad);
             if (rc != JG_OK) {
+                const std::string why = last_error();
                 if (bad == UINT64_MAX) {
-                    if (open[1]) jg_orset_wave_abort(orset_);
-                    check(rc);
+                    if (open[0]) jg_pnc_wave_abort(pnc_);
+                    jg_orset_wave_abort(orset_);
+                    throw EngineError(rc, why);
                 }
-                cut = where[0][bad];
+                cut = where_[1][bad];
                 cut_code = rc;
-                cut_why = last_error();
-                submit_prefix(bad);
+                cut_why = why;
             }
         }
-    }
-    pnc_bytes_ = 0;
-    for (const Chunk& ch : chunks[0]) pnc_bytes_ += ch.off[ch.m];
+        to1 = wall_s();
+        phase_s_[3] = wall_s() - t0;
 
-    // OR-Set states before the cut: element strings interned in commit order, records unioned into the
-    // store (device); then the ids the wave issued join the host tables.
-    double to2 = wall_s(), to3 = to2;
-    if (open[1]) {
-        const uint64_t limit = (uint64_t)(std::lower_bound(where[1].begin(), where[1].end(), (uint64_t)cut) - where[1].begin());
-        check(jg_orset_wave_commit(orset_, limit));
-        to3 = wall_s();
-        take_wave_names();
-    }
-    orset_phase_s_[0] = to1 - to0;
-    orset_phase_s_[1] = to3 - to2;
-    orset_phase_s_[2] = wall_s() - to3;
-    // safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) of the applied prefix, in
-    // commit order: the workers take contiguous ranges, their lists concatenate in worker order
-    std::vector<uint64_t> completed;
-    if (tracker && tracker->size()) {
-        std::vector<std::vector<uint64_t>> part(T);
-        parallel_ranges(wp, cut, [&](size_t b, size_t e, int t) {
-            uint64_t o;
-            for (size_t i = b; i < e; ++i)
-                if (cls[i] != kSkip && tracker->take(msgs[i]->seq, &o)) part[t].push_back(o);
+        t1 = wall_s();
+        // Re-stream the first `limit` PNC messages (the reference's loop applied the messages before the
+        // one that threw; the engine's PN-Counter waves are all or nothing).
+        auto submit_prefix = [&](size_t limit) {
+            if (limit == 0) return;
+            check(jg_pnc_wave_begin(pnc_, limit, 1));
+            size_t left = limit;
+            for (const Chunk& ch : chunks[0]) {
+                if (!left) break;
+                const size_t k = std::min(left, ch.m);
+                check(jg_pnc_wave_append(pnc_, k, ch.rows, ch.off, ch.bytes));
+                left -= k;
+            }
+            check(jg_pnc_wave_commit(pnc_, nullptr));
+        };
+        if (open[0]) {
+            if (cut < n) {  // an OR-Set state before some of these PNC states was rejected
+                check(jg_pnc_wave_abort(pnc_));
+                submit_prefix((size_t)(std::lower_bound(where_[0].begin(), where_[0].begin() + nw[0], (uint64_t)cut) - where_[0].begin()));
+            } else {
+                uint64_t bad = UINT64_MAX;
+                const int rc = jg_pnc_wave_commit(pnc_, &bad);
+                if (rc != JG_OK) {
+                    if (bad == UINT64_MAX) {
+                        if (open[1]) jg_orset_wave_abort(orset_);
+                        check(rc);
+                    }
+                    cut = where_[0][bad];
+                    cut_code = rc;
+                    cut_why = last_error();
+                    submit_prefix(bad);
+                }
+            }
+        }
+        pnc_bytes_ = 0;
+        for (const Chunk& ch : chunks[0]) pnc_bytes_ += ch.off[ch.m];
+
+        // OR-Set states before the cut: element strings interned in commit order, records unioned into the
+        // store (device); then the ids the wave issued join the host tables.
+        double to2 = wall_s(), to3 = to2;
+        if (open[1]) {
+            const uint64_t limit = (uint64_t)(std::lower_bound(where_[1].begin(), where_[1].begin() + nw[1], (uint64_t)cut) - where_[1].begin());
+            check(jg_orset_wave_commit(orset_, limit));
+            to3 = wall_s();
+            take_wave_names();
+        }
+        orset_phase_s_[0] = to1 - to0;
+        orset_phase_s_[1] = to3 - to2;
+        orset_phase_s_[2] = wall_s() - to3;
+    };
+    const double tt = wall_s();
+    double t_sweep = 0;
+    if (sweep && T > 1 && n >= 8192) {
+        std::exception_ptr err;
+        wp.run([&](int t) {
+            if (t == 0) {
+                try { device_side(); } catch (...) { err = std::current_exception(); }
+                return;
+            }
+            const double ts = wall_s();
+            sweep_range(n * (t - 1) / (T - 1), n * t / (T - 1), t);
+            if (t == 1) t_sweep = wall_s() - ts;
         });
-        for (auto& p : part) completed.insert(completed.end(), p.begin(), p.end());
+        if (err) {  // nothing of the wave counts as applied: every claim goes back
+            for (const auto& p : part)
+                for (const auto& [i, o] : p) tracker->add(msgs[i]->seq, o);
+            std::rethrow_exception(err);
+        }
+    } else {
+        device_side();
+        if (sweep) sweep_range(0, cut, 0);
+    }
+    std::vector<uint64_t> completed;
+    if (sweep) {
+        size_t kept = 0;
+        for (const auto& p : part)
+            for (const auto& [i, o] : p) {
+                if (i < cut) completed.push_back(o), ++kept;
+                else tracker->add(msgs[i]->seq, o);  // past the cut: not applied, still pending
+            }
+        tracker->settle(kept);
     }
     host_s_ = t1 - t0;
     engine_s_ = wall_s() - t1;
+    if (std::getenv("JANUS_TRACE_WAVE"))
+        std::fprintf(stderr, "wave: device side %.2f ms (orset check %.2f commit %.2f names %.2f), completion sweep %.2f ms (worker 1), total %.2f ms\n",
+                     1e3 * (wall_s() - tt), 1e3 * orset_phase_s_[0], 1e3 * orset_phase_s_[1], 1e3 * orset_phase_s_[2], 1e3 * t_sweep,
+                     1e3 * (wall_s() - tt));
     if (cut < n) throw ApplyError(cut_code, cut_why, cut, std::move(completed));
     return completed;
 }

@@ -92,13 +92,28 @@ class SafeUpdateTracker {
     }
     bool add(uint64_t seq, uint64_t origin);          // TryAdd: false if present (seq 0 is not a message)
     bool contains(uint64_t seq) const;
-    bool take(uint64_t seq, uint64_t* origin);        // TryRemove; safe against concurrent take()s
+    bool take(uint64_t seq, uint64_t* origin) {       // TryRemove; safe against concurrent take()s
+        if (!claim(seq, origin)) return false;
+        n_.fetch_sub(1, std::memory_order_relaxed);
+        return true;
+    }
+    // take() without the size update, for parallel sweeps (one shared counter decremented per take
+    // serialised 16 workers to ~90 ns a take); settle(k) afterwards with the number claimed
+    bool claim(uint64_t seq, uint64_t* origin);
+    void settle(size_t k) { n_.fetch_sub(k, std::memory_order_relaxed); }
+    void prefetch(uint64_t seq) const {
+        if (!slots_.empty()) __builtin_prefetch(&slots_[seq_slot(seq) & (slots_.size() - 1)]);
+    }
     size_t size() const { return n_.load(std::memory_order_relaxed); }
     std::vector<std::pair<uint64_t, uint64_t>> items() const;  // live entries (any order)
 
   private:
     struct Slot { std::atomic<uint64_t> key{0}; uint64_t val = 0; };  // key 0 empty, kTomb removed
     static constexpr uint64_t kTomb = ~0ull;
+    static size_t seq_slot(uint64_t x) {
+        x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33;
+        return (size_t)x;
+    }
     void grow();
     std::vector<Slot> slots_;
     std::atomic<size_t> n_{0};
@@ -285,6 +300,8 @@ class GpuStableStore {
     std::vector<jg_guid> reg_guids_;
     std::vector<std::pair<char*, size_t>> arenas_;  // pinned staging arenas (base, bytes)
     size_t arena_i_ = 0, arena_off_ = 0;            // carve position of the current wave
+    std::vector<uint32_t> cls_, sid_;               // apply_msgs scratch: per message class / set id
+    std::vector<uint64_t> where_[2];                //   and per kind, the commit index of its messages
     std::unique_ptr<WorkerPool> pool_;
     std::vector<SetKey> sets_;
     std::vector<NetworkProtocol> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167)

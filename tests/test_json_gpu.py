@@ -52,8 +52,13 @@ class Pair:
         self.s.close()
 
 
+GROUPS = ["1", "8", "16", "32", "64"]  # JANUS_JSON_GROUP: lanes per message (1 = the serial parser)
+
+
+@pytest.mark.parametrize("group", GROUPS)
 @pytest.mark.parametrize("eb", [4, 8])
-def test_decode_contract_on_device(ctx, eb):
+def test_decode_contract_on_device(ctx, eb, group, monkeypatch):
+    monkeypatch.setenv("JANUS_JSON_GROUP", group)
     for i, (payload, ok4, ok8) in enumerate(CONTRACT):
         ok = ok4 if eb == 4 else ok8
         pr = Pair(ctx, 2, 4, eb, [(7, 7), (8, 8)])
@@ -69,8 +74,10 @@ def test_decode_contract_on_device(ctx, eb):
         pr.close()
 
 
+@pytest.mark.parametrize("group", ["1", "16"])
 @pytest.mark.parametrize("eb,R,pool", [(4, 8, 6), (8, 8, 6), (4, 64, 40), (8, 200, 150)])
-def test_random_waves_match_oracle(ctx, eb, R, pool):
+def test_random_waves_match_oracle(ctx, eb, R, pool, group, monkeypatch):
+    monkeypatch.setenv("JANUS_JSON_GROUP", group)
     rng = np.random.default_rng(R * 10 + eb)
     n_keys = 40
     stable = random_guids(rng, n_keys)
@@ -85,6 +92,79 @@ def test_random_waves_match_oracle(ctx, eb, R, pool):
         pr.s.merge_json(keys, msgs)
         pr.check()
     pr.close()
+
+
+def _mutants(rng, cl, keys, n):
+    """Near-compact payloads: one byte replaced, deleted or inserted, vectors swapped, a space added."""
+    alpha = b'"{},:-0123456789abcdefABCDEF xnpV\\'
+    out = []
+    for _ in range(n):
+        k = int(keys[int(rng.integers(0, len(keys)))])
+        m = bytearray(cl.message(k))
+        op = int(rng.integers(0, 5))
+        i = int(rng.integers(0, len(m)))
+        if op == 0:
+            m[i] = alpha[int(rng.integers(0, len(alpha)))]
+        elif op == 1:
+            del m[i]
+        elif op == 2:
+            m.insert(i, alpha[int(rng.integers(0, len(alpha)))])
+        elif op == 3:
+            s_ = bytes(m)
+            j = s_.index(b',"nVector"')
+            m = bytearray(b'{' + s_[j + 1:-1] + b',' + s_[1:j] + b'}')
+        else:
+            m.insert(i, ord(" "))
+        out.append((k, bytes(m)))
+    return out
+
+
+@pytest.mark.parametrize("group", GROUPS[1:])
+@pytest.mark.parametrize("eb", [4, 8])
+def test_group_parse_near_compact(ctx, eb, group, monkeypatch):
+    """The group parse (json_wave.hpp) proves a payload compact or hands it to the serial parser:
+    single-byte mutations of reference-shaped states (every token position), vector swaps and stray
+    whitespace are accepted or rejected exactly as the oracle's Decode does, and a store fed through the
+    group parse ends bit-identical to one fed through the serial parser (JANUS_JSON_GROUP=1).  Mutated
+    Guids may sit in one vector only, a state no reference node produces (the shared column order of
+    DESIGN.md §2 then differs from the oracle's P order), so the state check is serial-vs-group."""
+    rng = np.random.default_rng(int(group) * 7 + eb)
+    n_keys, R = 6, 64
+    stable = random_guids(rng, n_keys)
+    ga = _guid_arr(stable)
+    stores = {}
+    for G in (group, "1"):
+        stores[G] = jg.PNCStore(ctx, n_keys, R, eb)
+        stores[G].intern(np.arange(n_keys, dtype=np.uint32), ga["lo"], ga["hi"])
+    cl = Cluster(rng, n_keys, 6, eb, stable)
+    keys = np.arange(n_keys, dtype=np.uint32)
+    dt = np.int32 if eb == 4 else np.int64
+    z = np.zeros((n_keys, R), dt)
+    cols0 = np.zeros((n_keys, R), orc.GUID_DTYPE)
+    n_bad = 0
+    for k, msg in _mutants(rng, cl, keys, 160):
+        wave = (np.array([k, k], np.uint32), [cl.message(k), msg])
+        *_, bad, rc = orc.pnc_apply_json(z, z, cols0, np.zeros(n_keys, np.uint32), np.array([k], np.uint32), [msg], eb)
+        n_bad += bad is not None
+        for G, st in stores.items():
+            monkeypatch.setenv("JANUS_JSON_GROUP", G)
+            if bad is None:
+                st.merge_json(*wave)
+            else:
+                with pytest.raises(jg.JanusError) as e:
+                    st.merge_json(*wave)
+                assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 1, (G, msg)
+    a, b = stores[group], stores["1"]
+    for x, y in zip(a.read_rows(), b.read_rows()):
+        assert np.array_equal(x, y)
+    ga_, na = a.columns(keys)
+    gb_, nb = b.columns(keys)
+    assert np.array_equal(na, nb)
+    for k in range(n_keys):
+        assert np.array_equal(ga_[k, : na[k]], gb_[k, : nb[k]]), f"replica order differs at key {k}"
+    assert 20 < n_bad < 160  # both outcomes exercised
+    a.close()
+    b.close()
 
 
 def test_wild_values_and_vector_orders(ctx):
