@@ -203,8 +203,11 @@ constexpr uint32_t kEmitMax = 14;
 constexpr uint16_t kReparse = 0xFFFF;
 __host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kEmitMax * eb; }
 
-// Serial pass-A body for one message (one lane): the definitive parse.  A message it accepts goes to
-// the deferred list (a replica its row has not seen) or to the `slow` list (pass B parses it again).
+// deferred[m] (pass A): row << 32 | m for a message naming a replica its row has not seen, else this.
+constexpr unsigned long long kNotDeferred = ~0ull;
+
+// Serial pass-A body for one message (one lane): the definitive parse.  A message it accepts is marked
+// deferred (a replica its row has not seen) or goes to the `slow` list (pass B parses it again).
 template <int EB>
 __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ rows, uint64_t m,
                          const Table& t, unsigned long long* __restrict__ status, unsigned long long* __restrict__ deferred,
@@ -217,9 +220,9 @@ __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __re
         atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         return;
     }
+    deferred[m] = vis.miss ? (unsigned long long)row << 32 | m : kNotDeferred;
     if (vis.miss) {
-        const unsigned long long at = atomicAdd(status + 1, 1ull);
-        deferred[at] = (unsigned long long)row << 32 | m;
+        atomicAdd(status + 1, 1ull);
     } else {
         const unsigned long long at = atomicAdd(status + 3, 1ull);
         slow[at] = m;
@@ -463,6 +466,33 @@ void ensure_table(jg_pnc* p) {
 
 Table table_of(jg_pnc* p) { return Table{p->cols.as<Guid16>(), p->ncols.as<uint32_t>(), p->R}; }
 
+struct IsDeferred {
+    __host__ __device__ bool operator()(const unsigned long long& k) const { return k != kNotDeferred; }
+};
+
+// The nd deferred messages of pass A's per-message marks (n of them), compacted and sorted by (row,
+// message): commit order within each row.  Marks instead of an appended list: a cold wave defers
+// every message, and one counter taking a returning atomic per wave serialised 125k waves (4x pass A).
+unsigned long long* deferred_sorted(jg_ctx* ctx, const unsigned long long* marks, uint64_t n, uint64_t nd, uint64_t n_keys) {
+    JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "sort: %llu entries exceed one radix sort", (unsigned long long)n);
+    int row_bits = 1;
+    while (row_bits < 32 && (1ull << row_bits) < n_keys) ++row_bits;
+    const int end_bit = 32 + row_bits;
+    size_t tsel = 0, tsort = 0;
+    using ull = unsigned long long;
+    JG_HIP(hipcub::DeviceSelect::If(nullptr, tsel, marks, (ull*)nullptr, (int*)nullptr, (int)n, IsDeferred(), ctx->stream));
+    JG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tsort, (ull*)nullptr, (ull*)nullptr, (int)nd, 0, end_bit, ctx->stream));
+    const size_t a = (nd * 8 + 255) & ~255ull;
+    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, 2 * a + 256 + std::max(tsel, tsort) + 256));
+    ull* list = reinterpret_cast<ull*>(s);
+    ull* out = reinterpret_cast<ull*>(s + a);
+    int* cnt = reinterpret_cast<int*>(s + 2 * a);
+    void* tmp = s + 2 * a + 256;
+    JG_HIP(hipcub::DeviceSelect::If(tmp, tsel, marks, list, cnt, (int)n, IsDeferred(), ctx->stream));
+    JG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tsort, list, out, (int)nd, 0, end_bit, ctx->stream));
+    return out;
+}
+
 // Sort `n` 64-bit keys (row << 32 | index) in place through ctx scratch.  end_bit covers the row bits.
 unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n, uint64_t n_keys) {
     JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "sort: %llu entries exceed one radix sort", (unsigned long long)n);
@@ -508,7 +538,7 @@ void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep) {
     std::swap(nb.bytes, b.bytes);
 }
 
-// Wave-level device scratch: status words, the deferred list and its roll-back slots (n messages),
+// Wave-level device scratch: status words, pass A's deferred marks and the roll-back slots (n messages),
 // pass A's per-message entries and its list of messages for pass B to parse again.
 struct WaveScratch {
     unsigned long long* status;
@@ -558,7 +588,7 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     unsigned long long* sorted_deferred = nullptr;
     if (st.n_deferred) {
         const uint64_t nd = st.n_deferred;
-        unsigned long long* sorted = sort_keys(ctx, w.deferred, nd, p->n_keys);
+        unsigned long long* sorted = deferred_sorted(ctx, w.deferred, n, nd, p->n_keys);
         sorted_deferred = sorted;
         const unsigned gd = blocks_for(nd);
         const int G = json_group();

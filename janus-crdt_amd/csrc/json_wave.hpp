@@ -51,57 +51,95 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ bool same(const Guid16& a, const Guid16& b) { return a.lo == b.lo && a.hi == b.hi; }
 
-__device__ __forceinline__ bool lds_guid(const uint8_t* s, Guid16& g) {  // s[0..35], read_guid's layout
-    uint32_t v = 0;
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { const int h = hexv(s[i]); ok &= h >= 0; v = v << 4 | (uint32_t)(h & 15); }
-    unsigned long long lo = v;
-    v = 0;
-#pragma unroll
-    for (int i = 9; i < 13; ++i) { const int h = hexv(s[i]); ok &= h >= 0; v = v << 4 | (uint32_t)(h & 15); }
-    lo |= (unsigned long long)v << 32;
-    v = 0;
-#pragma unroll
-    for (int i = 14; i < 18; ++i) { const int h = hexv(s[i]); ok &= h >= 0; v = v << 4 | (uint32_t)(h & 15); }
-    lo |= (unsigned long long)v << 48;
-    ok &= s[8] == '-' && s[13] == '-' && s[18] == '-' && s[23] == '-';
-    unsigned long long hi = 0;
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const int at = 19 + 2 * b + (b >= 2 ? 1 : 0);
-        const int h = hexv(s[at]), l = hexv(s[at + 1]);
-        ok &= h >= 0 && l >= 0;
-        hi |= (unsigned long long)((h & 15) << 4 | (l & 15)) << (8 * b);
-    }
-    g.lo = lo;
-    g.hi = hi;
-    return ok;
+// *counter += the wave's lanes with `want`: one non-returning atomic per wave (the wave does not wait
+// on it).  Every lane of the wave calls it.
+__device__ __forceinline__ void wave_count(bool want, unsigned long long* counter) {
+    const unsigned long long mask = __ballot(want);
+    if (mask && (int)(threadIdx.x & 63) == __ffsll((long long)mask) - 1) atomicAdd(counter, (unsigned long long)__popcll(mask));
 }
 
-// read_int's grammar and width limits over s[p, L); *t = the first byte after the number.
+// ---- SWAR over 4 ASCII bytes (byte 0 = the first character): 0x80 in each byte where a test holds --
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu); }
+__device__ __forceinline__ uint32_t ge_bytes(uint32_t x7, uint32_t a) { return ((x7 | 0x80808080u) - a * 0x01010101u) & 0x80808080u; }
+__device__ __forceinline__ uint32_t le_bytes(uint32_t x7, uint32_t b) { return ((b * 0x01010101u | 0x80808080u) - x7) & 0x80808080u; }
+__device__ __forceinline__ uint32_t digit_bytes(uint32_t x) {  // '0'..'9'
+    const uint32_t x7 = x & 0x7F7F7F7Fu;
+    return ge_bytes(x7, 0x30) & le_bytes(x7, 0x39) & ~x;
+}
+__device__ __forceinline__ uint32_t bits4(uint32_t c) {  // 0x80 flags of bytes 0..3 -> bits 0..3
+    return ((c >> 7) & 1u) | ((c >> 14) & 2u) | ((c >> 21) & 4u) | ((c >> 28) & 8u);
+}
+// 4 hex characters (hexv's alphabet: 0-9 a-f A-F) -> byte j = value of character j
+__device__ __forceinline__ uint32_t hex4(uint32_t x, uint32_t& nib) {  // 1 if all four are hex
+    const uint32_t x7 = x & 0x7F7F7F7Fu, l7 = x7 | 0x20202020u;
+    const uint32_t dig = ge_bytes(x7, 0x30) & le_bytes(x7, 0x39);
+    const uint32_t af = ge_bytes(l7, 0x61) & le_bytes(l7, 0x66);
+    nib = (x & 0x0F0F0F0Fu) + (af >> 7) * 9u;
+    return ((dig | af) & ~x & 0x80808080u) == 0x80808080u ? 1u : 0u;
+}
+__device__ __forceinline__ uint32_t hex_pairs(uint32_t nib) {  // byte 0 = c0 c1, byte 2 = c2 c3
+    return ((nib & 0x000F000Fu) << 4) | ((nib >> 8) & 0x000F000Fu);
+}
+__device__ __forceinline__ uint32_t hex_be16(uint32_t nib) {  // the 4 characters as one hex number
+    const uint32_t t = hex_pairs(nib);
+    return ((t & 0xFFu) << 8) | (t >> 16);
+}
+__device__ __forceinline__ uint32_t hex_le16(uint32_t nib) {  // two hex-pair bytes, the first at the low address
+    const uint32_t t = hex_pairs(nib);
+    return (t & 0xFFu) | ((t >> 8) & 0xFF00u);
+}
+
+// K words of LDS bytes [q, q + 4K) at any alignment: K + 1 aligned reads, realigned in registers.
+template <int K>
+__device__ __forceinline__ void lds_words(const uint8_t* base, uint32_t q, uint32_t (&X)[K]) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(base) + (q >> 2);
+    const uint32_t sh = q & 3;
+    uint32_t W[K + 1];
+#pragma unroll
+    for (int i = 0; i <= K; ++i) W[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < K; ++i) X[i] = __builtin_amdgcn_alignbyte(W[i + 1], W[i], sh);
+}
+
+// `<36-char Guid>":<int>` at LDS byte q (the byte after the opening quote), read_guid's and read_int's
+// grammar without whitespace; *tend = offset from q of the byte after the number.
 template <int EB>
-__device__ __forceinline__ bool lds_int(const uint8_t* s, uint32_t p, uint32_t L, long long& out, uint32_t* t) {
-    bool neg = false;
-    if (p < L && s[p] == '-') { neg = true; ++p; }
-    if (p >= L || s[p] < '0' || s[p] > '9') return false;
+__device__ __forceinline__ bool entry_at(const uint8_t* base, uint32_t q, Guid16& g, long long& out, uint32_t* tend) {
+    uint32_t X[15];  // characters 0..59
+    lds_words<15>(base, q, X);
+    uint32_t n0, n1, nb, nc, nd, n6, n7, n8;
+    const uint32_t B = __builtin_amdgcn_alignbyte(X[3], X[2], 1);  // characters 9..12
+    const uint32_t C = __builtin_amdgcn_alignbyte(X[4], X[3], 2);  // 14..17
+    const uint32_t D = __builtin_amdgcn_alignbyte(X[5], X[4], 3);  // 19..22
+    bool ok = (hex4(X[0], n0) & hex4(X[1], n1) & hex4(B, nb) & hex4(C, nc) & hex4(D, nd) & hex4(X[6], n6) & hex4(X[7], n7) &
+               hex4(X[8], n8)) != 0;
+    ok &= (X[2] & 0xFFu) == '-' && ((X[3] >> 8) & 0xFFu) == '-' && ((X[4] >> 16) & 0xFFu) == '-' && (X[5] >> 24) == '-';
+    ok &= (X[9] & 0xFFFFu) == ('"' | ':' << 8);
+    g.lo = (unsigned long long)(hex_be16(n0) << 16 | hex_be16(n1)) | (unsigned long long)hex_be16(nb) << 32 |
+           (unsigned long long)hex_be16(nc) << 48;
+    g.hi = (unsigned long long)(hex_le16(nd) | hex_le16(n6) << 16) | (unsigned long long)(hex_le16(n7) | hex_le16(n8) << 16) << 32;
+    // -?(0|[1-9][0-9]*) from character 38; more digits than the width can hold never pass the limit
+    const uint32_t neg = ((X[9] >> 16) & 0xFFu) == '-' ? 1u : 0u;
+    uint32_t Y[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Y[k] = __builtin_amdgcn_alignbyte(X[10 + k], X[9 + k], 2 + neg);
+    uint32_t dm = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dm |= bits4(digit_bytes(Y[k])) << (4 * k);
+    const uint32_t run = (uint32_t)__builtin_ctz(~dm);
+    constexpr uint32_t kMaxDigits = EB == 4 ? 10 : 19;
+    ok &= run >= 1 && run <= kMaxDigits && !((Y[0] & 0xFFu) == '0' && run > 1);
     unsigned long long mag = 0;
-    if (s[p] == '0') {
-        ++p;
-        if (p < L && s[p] >= '0' && s[p] <= '9') return false;  // leading zero
-    } else {
-        while (p < L && s[p] >= '0' && s[p] <= '9') {
-            const unsigned d = (unsigned)(s[p] - '0');
-            if (mag > (~0ull - d) / 10) return false;
-            mag = mag * 10 + d;
-            ++p;
-        }
+#pragma unroll
+    for (uint32_t j = 0; j < kMaxDigits; ++j) {
+        const uint32_t d = (Y[j >> 2] >> (8 * (j & 3))) & 0xFu;
+        mag = j < run ? mag * 10 + d : mag;
     }
     const unsigned long long lim = EB == 4 ? (neg ? 0x80000000ull : 0x7FFFFFFFull) : (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
-    if (mag > lim) return false;
+    ok &= mag <= lim;
     out = neg ? (long long)(0ull - mag) : (long long)mag;
-    *t = p;
-    return true;
+    *tend = 38 + neg + run;
+    return ok;
 }
 
 __device__ __forceinline__ bool lds_name_tail(const uint8_t* s) {  // s = the byte after 'p' / 'n': Vector":{
@@ -188,19 +226,23 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
             const uint32_t w = u * G + g;
             if (u * G * 16 >= a + L) break;  // group-uniform
             if (w * 16 < a + L) sh.buf[grp][w] = v[u];
-            const uint32_t last = v[u].w >> 24;
-            uint32_t prev = __shfl_up(last, 1, G);
+            // token starts: '"' right after '{' or ','; o = those two bytes, carried across words and lanes
+            const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            uint32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = zero_bytes(wv[i] ^ 0x7B7B7B7Bu) | zero_bytes(wv[i] ^ 0x2C2C2C2Cu);
+            uint32_t prev = __shfl_up(o[3], 1, G);
             if (g == 0) prev = carry;
-            carry = __shfl(last, G - 1, G);
-            const int base = (int)(16 * w) - (int)a;  // message position of byte 0 of this window
+            carry = __shfl(o[3], G - 1, G);
             uint32_t cm = 0;
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t word = j < 4 ? v[u].x : j < 8 ? v[u].y : j < 12 ? v[u].z : v[u].w;
-                const uint32_t ch = (word >> ((j & 3) * 8)) & 0xFF;
-                if (ch == '"' && (prev == '{' || prev == ',') && base + j >= 1 && base + j < (int)L) cm |= 1u << j;
-                prev = ch;
+            for (int i = 0; i < 4; ++i) {
+                cm |= bits4(zero_bytes(wv[i] ^ 0x22222222u) & (o[i] << 8 | prev >> 24)) << (4 * i);
+                prev = o[i];
             }
+            const int base = (int)(16 * w) - (int)a;  // message position of byte 0 of this window
+            const int jlo = base >= 1 ? 0 : 1 - base, jhi = (int)L - base;  // bytes j with 1 <= base + j < L
+            cm &= jlo >= 16 || jhi <= 0 ? 0u : ((jhi >= 16 ? 0xFFFFu : (1u << jhi) - 1u) & ~((1u << jlo) - 1u));
             const uint32_t cnt = __popc(cm);
             uint32_t incl = cnt;
 #pragma unroll
@@ -260,8 +302,10 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
             if (k == 0 || p + 41 > L) { bad = true; continue; }
             Guid16 eg;
             long long val;
-            uint32_t t;
-            if (!lds_guid(c + p + 1, eg) || c[p + 37] != '"' || c[p + 38] != ':' || !lds_int<EB>(c, p + 39, L, val, &t) || t >= L) {
+            uint32_t tr;
+            const bool ok = entry_at<EB>(reinterpret_cast<const uint8_t*>(sh.buf[grp]), a + p + 1, eg, val, &tr);
+            const uint32_t t = p + 1 + tr;
+            if (!ok || t >= L) {
                 bad = true;
                 continue;
             }
@@ -322,18 +366,16 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             }
         }
         wave_sync();
+        const uint32_t f = sh.flags[grp];
+        const bool defer = g == 0 && fast && !(f & kDup) && (f & kMiss);
+        wave_count(defer, status + 1);
+        if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
         if (g == 0 && live) {
             if (!fast) {
                 scan_one<EB>(bytes, off, rows, m, t, status, deferred, emit, slow);
             } else {
-                const uint32_t f = sh.flags[grp];
                 *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = (f & (kDup | kMiss)) ? kReparse : (uint16_t)(gp.nt - 2);
-                if (f & kDup) {
-                    atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
-                } else if (f & kMiss) {
-                    const unsigned long long at = atomicAdd(status + 1, 1ull);
-                    deferred[at] = (unsigned long long)rc.row << 32 | m;
-                }
+                if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
             }
         }
     }
@@ -427,9 +469,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ 
             if (g == 0) {
                 uint32_t err = UINT32_MAX;
                 if (fast) {
-                    Mask256 seen;
+                    uint32_t* seen = sh.mask[grp];  // zeroed by group_parse; 256 bits per vector
                     for (uint32_t k = 1; k < gp.nt && err == UINT32_MAX; ++k) {
-                        if (k == gp.kn) { seen.clear(); continue; }
+                        if (k == gp.kn) continue;
                         const Guid16 x = sh.eg[grp][k];
                         uint32_t col = cached_col<G>(sh.cols[grp], gcols, nc, x, k < gp.kn ? k - 1 : k - gp.kn - 1);
                         if (col == UINT32_MAX) {
@@ -438,7 +480,9 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ 
                             gcols[col] = x;
                             if (col < (uint32_t)G) sh.cols[grp][col] = x;
                         }
-                        if (seen.test_set(col)) err = kErrSyntax;  // repeated Guid in one vector
+                        const uint32_t bit = 1u << (col & 31), wi = (k < gp.kn ? 0u : 8u) + (col >> 5);
+                        if (seen[wi] & bit) err = kErrSyntax;  // repeated Guid in one vector
+                        seen[wi] |= bit;
                     }
                 } else {
                     t.ncols[row] = nc;
