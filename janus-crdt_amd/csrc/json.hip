@@ -207,7 +207,8 @@ __host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kE
 constexpr unsigned long long kNotDeferred = ~0ull;
 
 // Serial pass-A body for one message (one lane): the definitive parse.  A message it accepts is marked
-// deferred (a replica its row has not seen) or goes to the `slow` list (pass B parses it again).
+// deferred (a replica its row has not seen) or, given a `slow` list, appended to it (pass B parses it
+// again); k_scan_slow passes none: its messages are on the list already.
 template <int EB>
 __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ rows, uint64_t m,
                          const Table& t, unsigned long long* __restrict__ status, unsigned long long* __restrict__ deferred,
@@ -223,7 +224,7 @@ __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __re
     deferred[m] = vis.miss ? (unsigned long long)row << 32 | m : kNotDeferred;
     if (vis.miss) {
         atomicAdd(status + 1, 1ull);
-    } else {
+    } else if (slow) {
         const unsigned long long at = atomicAdd(status + 3, 1ull);
         slow[at] = m;
     }
@@ -583,6 +584,12 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
                  uint64_t* bad_msg) {
     jg_ctx* ctx = p->ctx;
     const Table t = table_of(p);
+    const int G = json_group();
+    if (G > 1) {  // the payloads the group parse left to the serial parser (count read on the device)
+        if (p->eb == 8) hipLaunchKernelGGL(k_scan_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
+        else hipLaunchKernelGGL(k_scan_slow<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
+        JG_HIP(hipGetLastError());
+    }
     Status st = read_status(ctx, w.status);
     if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
     unsigned long long* sorted_deferred = nullptr;
@@ -591,7 +598,6 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         unsigned long long* sorted = deferred_sorted(ctx, w.deferred, n, nd, p->n_keys);
         sorted_deferred = sorted;
         const unsigned gd = blocks_for(nd);
-        const int G = json_group();
         if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
         else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
         JG_HIP(hipGetLastError());
@@ -605,17 +611,17 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     }
     // pass B: pass A's resolved entries, then the messages it left to parse again (deferred: now every
     // replica resolves; slow: not in the compact form).  max is order-free.
-    const int G = json_group();
     const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
     if (p->eb == 8) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
     else hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
     JG_HIP(hipGetLastError());
     const unsigned long long* lists[2] = {st.n_deferred ? sorted_deferred : nullptr, w.slow};
     const uint64_t counts[2] = {st.n_deferred, st.n_slow};
-    for (int l = 0; l < 2; ++l) {
+    for (int l = 0; l < 2; ++l) {  // deferred: the group parse (non-compact ones are on the slow list too); slow: serial
         if (!counts[l]) continue;
-        if (p->eb == 8) launch_apply_g<8>(G, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
-        else launch_apply_g<4>(G, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        const int Gl = l == 0 ? G : 1;
+        if (p->eb == 8) launch_apply_g<8>(Gl, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        else launch_apply_g<4>(Gl, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
         JG_HIP(hipGetLastError());
     }
     st = read_status(ctx, w.status);

@@ -21,9 +21,10 @@
 // A group never spans two waves, so the phases are separated by wave-level syncs, not block
 // barriers: every wave runs its groups at its own pace.
 //
-// Any payload the chain does not prove (whitespace, nVector first, > kGroupBytes, or malformed) is
-// handed whole to the serial parser (scan_one / apply_one) on the group's first lane: the fast path
-// accepts a subset of what the serial parser accepts, with identical entries, and never rejects.
+// Any payload the chain does not prove (whitespace, nVector first, > kGroupBytes, or malformed) goes
+// to the `slow` list, which the serial parser (scan_one / apply_one, one lane per message) handles in
+// kernels of its own, so the group kernels carry none of its registers: the fast path accepts a subset
+// of what the serial parser accepts, with identical entries, and never rejects.
 #pragma once
 
 constexpr uint32_t kGroupBytes = 512;              // LDS bytes per message: payload + its 16-B alignment offset
@@ -31,12 +32,12 @@ constexpr uint32_t kGroupTok = 16;                 // token slots (an entry span
 constexpr uint32_t kCompactMin = 27;               // {"pVector":{},"nVector":{}}
 enum : uint32_t { kSlow = 1, kMiss = 2, kDup = 4, kFail = 8 };
 
-template <int G>
+template <int G, bool EG = false>
 struct GroupShared {
     static constexpr int kGroups = kBlock / G;
     uint4 buf[kGroups][kGroupBytes / 16];
     Guid16 cols[kGroups][G];                       // the row's first G replica columns
-    Guid16 eg[kGroups][kGroupTok];                 // pass C: the entries' Guids by token
+    Guid16 eg[EG ? kGroups : 1][EG ? kGroupTok : 1];  // pass C: the entries' Guids by token
     uint16_t tok[kGroups][kGroupTok];
     uint32_t mask[kGroups][16];                    // pass A: columns seen, 256 bits per vector
     uint32_t ntok[kGroups], kn[kGroups], nn[kGroups], flags[kGroups];
@@ -50,6 +51,19 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ bool same(const Guid16& a, const Guid16& b) { return a.lo == b.lo && a.hi == b.hi; }
+
+// Lanes with `want` get consecutive slots of *counter, one returning atomic per wave (rare paths only:
+// a counter every wave waits on serialises the grid).  Every lane of the wave calls it.
+__device__ __forceinline__ unsigned long long wave_slot(bool want, unsigned long long* counter) {
+    const unsigned long long mask = __ballot(want);
+    if (!mask) return 0;
+    const int leader = __ffsll((long long)mask) - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    unsigned long long base = 0;
+    if ((int)lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+    base = __shfl(base, leader);
+    return base + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
+}
 
 // *counter += the wave's lanes with `want`: one non-returning atomic per wave (the wave does not wait
 // on it).  Every lane of the wave calls it.
@@ -195,7 +209,7 @@ __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16
 // Phases 1-3 for message m on every lane of the group; on return sh.flags[grp] & kSlow is clear iff
 // the payload is proven compact, and the row cache is in sh.cols.  STORE_EG: entry Guids to sh.eg.
 template <int EB, int G, bool STORE_EG>
-__device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+__device__ __forceinline__ void group_parse(GroupShared<G, STORE_EG>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                             uint64_t m, bool live, const RowCache& rc, GroupParse<EB, G>& gp) {
     constexpr uint32_t NW = (kGroupBytes / 16 + G - 1) / G;  // windows per lane
     const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
                                                  unsigned long long* __restrict__ deferred, uint8_t* __restrict__ emit,
                                                  unsigned long long* __restrict__ slow) {
     using T = typename ApplyVis<EB>::T;
-    if constexpr (G == 1) {
+    if constexpr (G == 1) {  // every accepted message not deferred also goes to the slow list
         const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
         if (m < m1) scan_one<EB>(bytes, off, rows, m, t, status, deferred, emit, slow);
     } else {
@@ -370,15 +384,26 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const bool defer = g == 0 && fast && !(f & kDup) && (f & kMiss);
         wave_count(defer, status + 1);
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
-        if (g == 0 && live) {
-            if (!fast) {
-                scan_one<EB>(bytes, off, rows, m, t, status, deferred, emit, slow);
-            } else {
-                *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = (f & (kDup | kMiss)) ? kReparse : (uint16_t)(gp.nt - 2);
-                if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
-            }
+        const bool to_slow = g == 0 && live && !fast;
+        const unsigned long long at = wave_slot(to_slow, status + 3);
+        if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
+        if (g == 0 && fast) {
+            *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = (f & (kDup | kMiss)) ? kReparse : (uint16_t)(gp.nt - 2);
+            if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
     }
+}
+
+// Pass A for the payloads the group parse did not prove compact: the serial parser, one lane per
+// message of the slow list (count in status[3], read on the device).
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_scan_slow(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                      const uint32_t* __restrict__ rows, Table t, unsigned long long* __restrict__ status,
+                                                      unsigned long long* __restrict__ deferred, uint8_t* __restrict__ emit,
+                                                      const unsigned long long* __restrict__ slow) {
+    const unsigned long long n = status[3];
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        scan_one<EB>(bytes, off, rows, slow[i], t, status, deferred, emit, nullptr);
 }
 
 // Pass B for the entries pass A resolved: kEmitLanes lanes per message, one entry each.
@@ -402,7 +427,8 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
 }
 
 // Pass B for the messages pass A left (list entries: [row << 32 |] message): parse again, every Guid now
-// resolves, max into the cells.
+// resolves, max into the cells.  G > 1 (the deferred list) skips payloads it cannot prove compact:
+// those are on the slow list, which the serial kernel (G == 1) applies.
 template <int EB, int G>
 __global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                   const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ list, uint64_t n,
@@ -432,8 +458,6 @@ __global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ by
                 if (col == UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | kErrInternal);
                 else atomicMax(static_cast<T*>(vv ? N : P) + base + col, (T)gp.ev[u]);
             }
-        } else if (live && g == 0) {
-            apply_one<EB>(bytes, off, rows, m, t, P, N, status);
         }
     }
 }
@@ -451,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ 
         const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
         if (i < nd) resolve_one<EB>(bytes, off, keys, nd, i, t, saved, status);
     } else {
-        __shared__ GroupShared<G> sh;
+        __shared__ GroupShared<G, true> sh;
         const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
         const uint64_t i = (uint64_t)blockIdx.x * GroupShared<G>::kGroups + grp;
         const uint32_t row = i < nd ? (uint32_t)(keys[i] >> 32) : 0;
