@@ -83,13 +83,14 @@ __device__ __forceinline__ bool dropped(const Drop& d, unsigned long long key) {
 }
 
 // Merge-path split of output tile boundary w (diagonal d = w*C in merged order): the number of A
-// records among the first d (A first on ties).  L lanes cooperate on one boundary with an
+// records among the first d (A first on ties).  C must be a multiple of 512 (aligned coarse probes).  L lanes cooperate on one boundary with an
 // (L+1)-ary search (L = 1: plain binary search); tags are read only when keys tie.  Also records
 // the chunk holding the first A and B rank of the tile (saves the tile one dependent lookup).
 template <int C, int L>
 __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_parts, uint64_t* __restrict__ part,
                                                    uint32_t* __restrict__ pchunk) {
     static_assert(L >= 1 && L <= 64 && 64 % L == 0, "lanes per boundary must divide the wave");
+    static_assert(C % 512 == 0, "tile boundaries on 512-rank multiples");
     const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     const uint64_t w = gt / L;
     const int gl = (int)(gt % L);
@@ -103,8 +104,12 @@ __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_pa
         const uint64_t W = hi - lo;
         const bool valid = lo < hi;
         bool fail = false;
+        uint64_t m = lo + ((uint64_t)(gl + 1) * W) / (L + 1);
+        // wide ranges probe 512-aligned A ranks only (m stays in (lo, hi): W / 2 >= 512); d is a multiple
+        // of C = 6 * 512, so the B rank d - 1 - m is 511 mod 512 too: every boundary's coarse probes hit
+        // the same n / 512 lines of each stream (L2 / MALL reuse across boundaries)
+        if (L == 1 && W > 1024) m &= ~511ull;
         if (valid) {
-            const uint64_t m = lo + ((uint64_t)(gl + 1) * W) / (L + 1);
             const uint64_t sa = slot_of(a, m), sb = slot_of(b, d - 1 - m);
             const unsigned long long ka = a.key[sa], kb = b.key[sb];
             fail = ka != kb ? kb < ka : rec_lt(kb, ld_tag(b.tag + sb), ka, ld_tag(a.tag + sa));
@@ -112,7 +117,10 @@ __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_pa
         const unsigned long long fm = __ballot(fail);
         const unsigned long long mine = L == 64 ? fm : (fm >> gbase) & ((1ull << (L & 63)) - 1);
         if (valid) {
-            if (mine == 0) {
+            if (L == 1) {
+                if (mine == 0) lo = m + 1;
+                else hi = m;
+            } else if (mine == 0) {
                 lo = lo + ((uint64_t)L * W) / (L + 1) + 1;
             } else {
                 const uint64_t k = (uint64_t)(__ffsll((long long)mine) - 1);
