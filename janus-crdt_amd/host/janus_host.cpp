@@ -208,8 +208,21 @@ int GpuStableStore::host_threads() {
         const int v = std::atoi(e);
         if (v >= 1) return v;
     }
-    const unsigned hw = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));
+    unsigned cap = std::thread::hardware_concurrency();
+    cap = std::min(cap ? cap : 1u, 16u);
+    // A cgroup CPU quota (cgroup v2 cpu.max "quota period", e.g. 16 CPUs of time on a 256-CPU host)
+    // throttles every thread of the process once exceeded: leave two CPUs for the caller's other
+    // threads and the HIP runtime's.
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long long period = 0;
+        if (std::fscanf(f, "%31s %llu", q, &period) == 2 && std::strcmp(q, "max") != 0 && period) {
+            const unsigned long long cpus = std::strtoull(q, nullptr, 10) / period;
+            if (cpus >= 1) cap = std::min<unsigned>(cap, (unsigned)std::max<unsigned long long>(1, cpus > 4 ? cpus - 2 : cpus));
+        }
+        std::fclose(f);
+    }
+    return (int)std::max(1u, cap);
 }
 
 WorkerPool& GpuStableStore::pool() {
