@@ -65,12 +65,6 @@ __device__ __forceinline__ unsigned long long wave_slot(bool want, unsigned long
     return base + (unsigned long long)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
-// *counter += the wave's lanes with `want`: one non-returning atomic per wave (the wave does not wait
-// on it).  Every lane of the wave calls it.
-__device__ __forceinline__ void wave_count(bool want, unsigned long long* counter) {
-    const unsigned long long mask = __ballot(want);
-    if (mask && (int)(threadIdx.x & 63) == __ffsll((long long)mask) - 1) atomicAdd(counter, (unsigned long long)__popcll(mask));
-}
 
 // ---- SWAR over 4 ASCII bytes (byte 0 = the first character): 0x80 in each byte where a test holds --
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) { return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu); }
@@ -382,7 +376,6 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         wave_sync();
         const uint32_t f = sh.flags[grp];
         const bool defer = g == 0 && fast && !(f & kDup) && (f & kMiss);
-        wave_count(defer, status + 1);
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
         const bool to_slow = g == 0 && live && !fast;
         const unsigned long long at = wave_slot(to_slow, status + 3);
