@@ -173,11 +173,15 @@ __device__ __forceinline__ uint32_t find_col(const Guid16* row, uint32_t n, cons
 struct Mask256 {
     unsigned long long w0 = 0, w1 = 0, w2 = 0, w3 = 0;
     __device__ void clear() { w0 = w1 = w2 = w3 = 0; }
-    __device__ bool test_set(uint32_t c) {  // returns the old bit
+    __device__ bool test_set(uint32_t c) {  // returns the old bit (no address taken: stays in registers)
         const unsigned long long b = 1ull << (c & 63);
-        unsigned long long* w = c < 64 ? &w0 : c < 128 ? &w1 : c < 192 ? &w2 : &w3;
-        const bool old = (*w & b) != 0;
-        *w |= b;
+        bool old;
+        switch (c >> 6) {
+            case 0: old = (w0 & b) != 0; w0 |= b; break;
+            case 1: old = (w1 & b) != 0; w1 |= b; break;
+            case 2: old = (w2 & b) != 0; w2 |= b; break;
+            default: old = (w3 & b) != 0; w3 |= b; break;
+        }
         return old;
     }
 };
@@ -523,7 +527,7 @@ unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n,
     return out;
 }
 
-struct Status { unsigned long long first_bad, n_deferred, resolve_bad, n_slow; };
+struct Status { unsigned long long first_bad, n_deferred, resolve_bad, n_slow, n_resume; };
 
 Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     Status s;
@@ -579,7 +583,7 @@ WaveScratch wave_scratch(jg_pnc* p, uint64_t n, uint64_t keep = 0) {
 }
 
 void reset_status(jg_ctx* ctx, unsigned long long* status) {
-    static const Status init{~0ull, 0, ~0ull, 0};
+    static const Status init{~0ull, 0, ~0ull, 0, 0};
     JG_HIP(hipMemcpyAsync(status, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
 }
 
@@ -613,10 +617,17 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         unsigned long long* sorted = sort_deferred(ctx, dl, nd);
         sorted_deferred = sorted;
         const unsigned gd = blocks_for(nd);
-        if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
-        else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status);
+        // the resume list reuses pass A's deferral marks (dead once compacted)
+        if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status, w.deferred);
+        else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status, w.deferred);
         JG_HIP(hipGetLastError());
         st = read_status(ctx, w.status);
+        if (st.n_resume && st.resolve_bad == ~0ull) {  // walks the group parse handed to the serial parser
+            if (p->eb == 8) hipLaunchKernelGGL(k_resolve_resume<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred);
+            else hipLaunchKernelGGL(k_resolve_resume<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred);
+            JG_HIP(hipGetLastError());
+            st = read_status(ctx, w.status);
+        }
         if (st.resolve_bad != ~0ull) {
             hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, w.saved);
             JG_HIP(hipGetLastError());

@@ -458,12 +458,15 @@ __global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ by
 // Pass C (new replicas appended in commit order).  One group per sorted deferred entry; the group of a
 // row's first entry walks the row's messages in commit order: each compact message is parsed by the
 // group, then its first lane appends the unknown Guids in token order (every pVector entry before any
-// nVector entry, PNCounters.cs:133-143), keeping the row's first G columns in LDS; other messages go
-// through the serial ResolveVis on that lane.  saved[i] = ncols before the walk (for roll-back).
+// nVector entry, PNCounters.cs:133-143), keeping the row's first G columns in LDS.  At a message it
+// cannot prove compact the group hands the rest of the row's walk to k_resolve_resume (the serial
+// ResolveVis; list in `resume`, count in status[4]), so it carries none of the serial parser's
+// registers.  saved[i] = ncols before the walk (for roll-back).
 template <int EB, int G>
 __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                     const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
-                                                    uint32_t* __restrict__ saved, unsigned long long* __restrict__ status) {
+                                                    uint32_t* __restrict__ saved, unsigned long long* __restrict__ status,
+                                                    unsigned long long* __restrict__ resume) {
     if constexpr (G == 1) {
         const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
         if (i < nd) resolve_one<EB>(bytes, off, keys, nd, i, t, saved, status);
@@ -501,15 +504,12 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ 
                         if (seen[wi] & bit) err = kErrSyntax;  // repeated Guid in one vector
                         seen[wi] |= bit;
                     }
-                } else {
+                } else {  // the serial walk takes over from message j
                     t.ncols[row] = nc;
-                    err = resolve_msg<EB>(bytes, off, m, gcols, t.ncols + row, t.R);
-                    const uint32_t nc2 = t.ncols[row];
-                    for (uint32_t col = nc; col < nc2 && col < (uint32_t)G; ++col) sh.cols[grp][col] = gcols[col];
-                    nc = nc2;
+                    resume[atomicAdd(status + 4, 1ull)] = j;
                 }
                 if (err != UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | err);
-                sh.flags[grp] = err != UINT32_MAX ? kFail : 0;
+                sh.flags[grp] = err != UINT32_MAX || !fast ? kFail : 0;
                 sh.ntok[grp] = nc;
             }
             wave_sync();
@@ -517,6 +517,27 @@ __global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ 
             if (sh.flags[grp] & kFail) return;
         }
         if (g == 0) t.ncols[row] = nc;
+    }
+}
+
+// The rest of a row's walk from a message the group parse handed over (serial ResolveVis, one lane).
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_resolve_resume(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                           const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
+                                                           unsigned long long* __restrict__ status,
+                                                           const unsigned long long* __restrict__ resume) {
+    const unsigned long long nr = status[4];
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nr; r += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t j0 = resume[r];
+        const uint32_t row = (uint32_t)(keys[j0] >> 32);
+        for (uint64_t j = j0; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
+            const uint64_t m = (uint32_t)keys[j];
+            const uint32_t err = resolve_msg<EB>(bytes, off, m, t.cols + (uint64_t)row * t.R, t.ncols + row, t.R);
+            if (err != UINT32_MAX) {
+                atomicMin(status + 2, (unsigned long long)m << 2 | err);
+                break;
+            }
+        }
     }
 }
 
@@ -530,16 +551,16 @@ inline unsigned json_blocks(uint64_t n, int G) { return (unsigned)((n * (uint64_
 
 template <int EB>
 void launch_resolve_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_t* off, const unsigned long long* keys, uint64_t nd,
-                      const Table& t, uint32_t* saved, unsigned long long* status) {
+                      const Table& t, uint32_t* saved, unsigned long long* status, unsigned long long* resume) {
     const unsigned gr = json_blocks(nd, G);
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_resolve<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        case 4: hipLaunchKernelGGL((k_resolve<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        case 16: hipLaunchKernelGGL((k_resolve<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        case 8: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        case 32: hipLaunchKernelGGL((k_resolve<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        case 64: hipLaunchKernelGGL((k_resolve<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
-        default: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status); break;
+        case 1: hipLaunchKernelGGL((k_resolve<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        case 4: hipLaunchKernelGGL((k_resolve<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        case 16: hipLaunchKernelGGL((k_resolve<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        case 8: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        case 32: hipLaunchKernelGGL((k_resolve<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        case 64: hipLaunchKernelGGL((k_resolve<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+        default: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
     }
 }
 
