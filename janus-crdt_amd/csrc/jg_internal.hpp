@@ -106,7 +106,7 @@ struct jg_pnc {
     jg::DevBuf head, next;
     // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list; pass A's
     // resolved entries per message and its list of messages pass B must parse again (json.hip)
-    jg::DevBuf wbytes, woff, wrows, wstat, wemit, wslow;
+    jg::DevBuf wbytes, woff, wrows, wstat, wemit, wguid, wslow;
     uint64_t wn = 0, wnb = 0;
     bool wopen = false;
 };

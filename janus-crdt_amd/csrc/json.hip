@@ -205,6 +205,7 @@ struct ScanVis {
 // then the entries' values at +32.  Entries in token order; at most kEmitMax.
 constexpr uint32_t kEmitMax = 14;
 constexpr uint16_t kReparse = 0xFFFF;
+constexpr uint32_t kNeedsCols = 0x4000;  // count flag: a deferred record whose columns pass C resolves
 __host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kEmitMax * eb; }
 
 // deferred[m] (pass A): row << 32 | m for a message naming a replica its row has not seen, else this.
@@ -564,6 +565,7 @@ struct WaveScratch {
     unsigned long long* deferred;
     uint32_t* saved;
     uint8_t* emit;
+    Guid16* eguid;  // [n x kEmitMax] entry Guids of the deferred compact messages
     unsigned long long* slow;
 };
 
@@ -575,10 +577,11 @@ WaveScratch wave_scratch(jg_pnc* p, uint64_t n, uint64_t keep = 0) {
     if (p->wstat.bytes < need) grow_keep(p->ctx, p->wstat, need, p->wstat.p ? 64 + keep * 8 : 0);
     grow_keep(p->ctx, p->wemit, n * emit_stride(p->eb) + 256, keep * emit_stride(p->eb));
     grow_keep(p->ctx, p->wslow, n * 8 + 256, keep * 8);
+    grow_keep(p->ctx, p->wguid, n * kEmitMax * sizeof(Guid16) + 256, keep * kEmitMax * sizeof(Guid16));
     n = (p->wstat.bytes - 64 - 256) / 12;  // the capacity actually there
     char* s = p->wstat.as<char>();
     return WaveScratch{reinterpret_cast<unsigned long long*>(s), reinterpret_cast<unsigned long long*>(s + 64),
-                       reinterpret_cast<uint32_t*>(s + 64 + ((n * 8 + 15) & ~15ull)), p->wemit.as<uint8_t>(),
+                       reinterpret_cast<uint32_t*>(s + 64 + ((n * 8 + 15) & ~15ull)), p->wemit.as<uint8_t>(), p->wguid.as<Guid16>(),
                        p->wslow.as<unsigned long long>()};
 }
 
@@ -592,8 +595,8 @@ void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     if (m1 <= m0) return;
     const Table t = table_of(p);
     const int G = json_group();
-    if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.slow);
-    else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.slow);
+    if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow);
+    else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow);
     JG_HIP(hipGetLastError());
 }
 
@@ -618,13 +621,15 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         sorted_deferred = sorted;
         const unsigned gd = blocks_for(nd);
         // the resume list reuses pass A's deferral marks (dead once compacted)
-        if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status, w.deferred);
-        else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.saved, w.status, w.deferred);
+        if (p->eb == 8) launch_resolve_g<8>(G, ctx->stream, bytes, off, sorted, nd, t, w.emit, w.eguid, w.saved, w.status, w.deferred);
+        else launch_resolve_g<4>(G, ctx->stream, bytes, off, sorted, nd, t, w.emit, w.eguid, w.saved, w.status, w.deferred);
         JG_HIP(hipGetLastError());
         st = read_status(ctx, w.status);
         if (st.n_resume && st.resolve_bad == ~0ull) {  // walks the group parse handed to the serial parser
-            if (p->eb == 8) hipLaunchKernelGGL(k_resolve_resume<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred);
-            else hipLaunchKernelGGL(k_resolve_resume<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred);
+            if (p->eb == 8)
+                hipLaunchKernelGGL(k_resolve_resume<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred, w.emit, w.eguid);
+            else
+                hipLaunchKernelGGL(k_resolve_resume<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, sorted, nd, t, w.status, w.deferred, w.emit, w.eguid);
             JG_HIP(hipGetLastError());
             st = read_status(ctx, w.status);
         }
@@ -635,19 +640,20 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
             fail_msg(st.resolve_bad, bad_msg, "state message");
         }
     }
-    // pass B: pass A's resolved entries, then the messages it left to parse again (deferred: now every
-    // replica resolves; slow: not in the compact form).  max is order-free.
+    // pass B: pass A's records (resolved by pass C where deferred), then the messages left to the serial
+    // parser (slow: not in the compact form; with JANUS_JSON_GROUP=1 also the deferred ones).  max is
+    // order-free.
     const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
     if (p->eb == 8) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
     else hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
     JG_HIP(hipGetLastError());
     const unsigned long long* lists[2] = {st.n_deferred ? sorted_deferred : nullptr, w.slow};
     const uint64_t counts[2] = {st.n_deferred, st.n_slow};
-    for (int l = 0; l < 2; ++l) {  // deferred: the group parse (non-compact ones are on the slow list too); slow: serial
+    for (int l = G > 1 ? 1 : 0; l < 2; ++l) {
         if (!counts[l]) continue;
-        const int Gl = l == 0 ? G : 1;
-        if (p->eb == 8) launch_apply_g<8>(Gl, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
-        else launch_apply_g<4>(Gl, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        const unsigned gl = blocks_for(counts[l]);
+        if (p->eb == 8) hipLaunchKernelGGL(k_apply_list<8>, dim3(gl), dim3(kBlock), 0, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
+        else hipLaunchKernelGGL(k_apply_list<4>, dim3(gl), dim3(kBlock), 0, ctx->stream, bytes, off, rows, lists[l], counts[l], t, p->P.p, p->N.p, w.status);
         JG_HIP(hipGetLastError());
     }
     st = read_status(ctx, w.status);

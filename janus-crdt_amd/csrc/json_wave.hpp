@@ -339,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
                                                  const uint32_t* __restrict__ rows, uint64_t m0, uint64_t m1, Table t,
                                                  unsigned long long* __restrict__ status /* [0] first bad, [1] n deferred, [3] n slow */,
                                                  unsigned long long* __restrict__ deferred, uint8_t* __restrict__ emit,
-                                                 unsigned long long* __restrict__ slow) {
+                                                 Guid16* __restrict__ eguid, unsigned long long* __restrict__ slow) {
     using T = typename ApplyVis<EB>::T;
     if constexpr (G == 1) {  // every accepted message not deferred also goes to the slow list
         const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -375,13 +375,28 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         }
         wave_sync();
         const uint32_t f = sh.flags[grp];
-        const bool defer = g == 0 && fast && !(f & kDup) && (f & kMiss);
+        const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
+        if (deferred_msg) {  // pass C resolves the columns from these Guids, pass B then applies the record
+            uint8_t* h = emit + m * emit_stride(EB);
+#pragma unroll
+            for (int u = 0; u < GroupParse<EB, G>::TPL; ++u) {
+                if (!gp.has[u]) continue;
+                const uint32_t k = g + u * G;
+                const uint32_t vv = k < gp.kn ? 0 : 1;
+                const uint32_t e = vv ? k - 2 : k - 1;
+                eguid[m * kEmitMax + e] = gp.eg[u];
+                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(0x7FFF | vv << 15);
+                reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
+            }
+        }
+        const bool defer = g == 0 && deferred_msg;
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
         const bool to_slow = g == 0 && live && !fast;
         const unsigned long long at = wave_slot(to_slow, status + 3);
         if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
         if (g == 0 && fast) {
-            *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = (f & (kDup | kMiss)) ? kReparse : (uint16_t)(gp.nt - 2);
+            *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
+                (f & kDup) ? kReparse : (uint16_t)((gp.nt - 2) | ((f & kMiss) ? kNeedsCols : 0u));
             if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
     }
@@ -413,129 +428,134 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
     if (m >= n) return;
     const uint8_t* h = emit + m * emit_stride(EB);
     const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
-    if (cnt == kReparse || e >= cnt) return;
+    if (cnt == kReparse || (cnt & kNeedsCols) || e >= cnt) return;
     const uint32_t code = reinterpret_cast<const uint16_t*>(h)[1 + e];
     const T v = reinterpret_cast<const T*>(h + 32)[e];
     atomicMax(static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF), v);
 }
 
-// Pass B for the messages pass A left (list entries: [row << 32 |] message): parse again, every Guid now
-// resolves, max into the cells.  G > 1 (the deferred list) skips payloads it cannot prove compact:
-// those are on the slow list, which the serial kernel (G == 1) applies.
-template <int EB, int G>
-__global__ __launch_bounds__(kBlock) void k_apply(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ list, uint64_t n,
-                                                  Table t, void* P, void* N, unsigned long long* __restrict__ status) {
-    if constexpr (G == 1) {
-        const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-        if (i < n) apply_one<EB>(bytes, off, rows, (uint32_t)list[i], t, P, N, status);
-    } else {
-        using T = typename ApplyVis<EB>::T;
-        __shared__ GroupShared<G> sh;
-        const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
-        const uint64_t i = (uint64_t)blockIdx.x * GroupShared<G>::kGroups + grp;
-        const bool live = i < n;
-        const uint64_t m = live ? (uint32_t)list[i] : 0;
-        const RowCache rc = row_cache(t, rows, m, live, g);
-        GroupParse<EB, G> gp;
-        group_parse<EB, G, false>(sh, bytes, off, m, live, rc, gp);
-        const bool fast = live && !(sh.flags[grp] & kSlow);
-        if (fast) {
-            const uint64_t base = (uint64_t)rc.row * t.R;
-#pragma unroll
-            for (int u = 0; u < GroupParse<EB, G>::TPL; ++u) {
-                if (!gp.has[u]) continue;
-                const uint32_t k = g + u * G;
-                const uint32_t vv = k < gp.kn ? 0 : 1;
-                const uint32_t col = cached_col<G>(sh.cols[grp], t.cols + base, rc.nc, gp.eg[u], vv ? k - gp.kn - 1 : k - 1);
-                if (col == UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | kErrInternal);
-                else atomicMax(static_cast<T*>(vv ? N : P) + base + col, (T)gp.ev[u]);
-            }
-        }
-    }
+// Pass B for the messages left to the serial parser (list entries: [row << 32 |] message): parse again,
+// every Guid now resolves, max into the cells.  With the group parse (G > 1) that is the slow list:
+// compact deferred messages are applied from their resolved records by k_apply_emit.
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_apply_list(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ list,
+                                                       uint64_t n, Table t, void* P, void* N, unsigned long long* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) apply_one<EB>(bytes, off, rows, (uint32_t)list[i], t, P, N, status);
 }
 
-// Pass C (new replicas appended in commit order).  One group per sorted deferred entry; the group of a
-// row's first entry walks the row's messages in commit order: each compact message is parsed by the
-// group, then its first lane appends the unknown Guids in token order (every pVector entry before any
-// nVector entry, PNCounters.cs:133-143), keeping the row's first G columns in LDS.  At a message it
-// cannot prove compact the group hands the rest of the row's walk to k_resolve_resume (the serial
-// ResolveVis; list in `resume`, count in status[4]), so it carries none of the serial parser's
-// registers.  saved[i] = ncols before the walk (for roll-back).
-template <int EB, int G>
-__global__ __launch_bounds__(kBlock) void k_resolve(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                    const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
-                                                    uint32_t* __restrict__ saved, unsigned long long* __restrict__ status,
-                                                    unsigned long long* __restrict__ resume) {
-    if constexpr (G == 1) {
-        const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-        if (i < nd) resolve_one<EB>(bytes, off, keys, nd, i, t, saved, status);
-    } else {
-        __shared__ GroupShared<G, true> sh;
-        const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
-        const uint64_t i = (uint64_t)blockIdx.x * GroupShared<G>::kGroups + grp;
-        const uint32_t row = i < nd ? (uint32_t)(keys[i] >> 32) : 0;
-        if (i >= nd || (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row)) return;  // not a segment head (group-uniform)
-        Guid16* gcols = t.cols + (uint64_t)row * t.R;
-        uint32_t nc = t.ncols[row];  // every lane tracks the count (lane 0 appends, then broadcasts)
-        if (g == 0) saved[i] = nc;
-        if (g < nc) sh.cols[grp][g] = gcols[g];
-        RowCache none;
-        for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
-            const uint64_t m = (uint32_t)keys[j];
-            GroupParse<EB, G> gp;
-            group_parse<EB, G, true>(sh, bytes, off, m, true, none, gp);
-            const bool fast = !(sh.flags[grp] & kSlow);
+// Pass C (new replicas appended in commit order) from pass A's records: no payload is parsed again.
+// One group of kEmitLanes lanes per sorted deferred entry; the group of a row's first entry walks the
+// row's deferred messages in commit order: the lanes stage a message's entry Guids in LDS, the first
+// lane finds or appends each in token order (every pVector entry before any nVector entry,
+// PNCounters.cs:133-143) against the row's first columns cached in LDS, checks repeats within a vector,
+// and writes the columns into the record for pass B.  At a message the group parse did not prove
+// compact (record kReparse) the rest of the walk goes to k_resolve_resume (serial ResolveVis).  G == 1
+// (JANUS_JSON_GROUP=1): the serial walk throughout.  saved[i] = ncols before the walk (for roll-back).
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_resolve_serial(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                           const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
+                                                           uint32_t* __restrict__ saved, unsigned long long* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < nd) resolve_one<EB>(bytes, off, keys, nd, i, t, saved, status);
+}
+
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_resolve_emit(const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
+                                                         uint8_t* __restrict__ emit, const Guid16* __restrict__ eguid,
+                                                         uint32_t* __restrict__ saved, unsigned long long* __restrict__ status,
+                                                         unsigned long long* __restrict__ resume) {
+    constexpr uint32_t L = kEmitLanes;
+    constexpr int kGroups = kBlock / L;
+    __shared__ Guid16 cache[kGroups][L];  // the row's first L columns
+    __shared__ Guid16 eg[kGroups][kEmitMax];
+    __shared__ uint32_t seen[kGroups][16];  // columns met per vector, 256 bits each
+    __shared__ uint32_t bc[kGroups];
+    const uint32_t grp = threadIdx.x / L, g = threadIdx.x % L;
+    const uint64_t i = (uint64_t)blockIdx.x * kGroups + grp;
+    const uint32_t row = i < nd ? (uint32_t)(keys[i] >> 32) : 0;
+    if (i >= nd || (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row)) return;  // not a segment head (group-uniform)
+    Guid16* gcols = t.cols + (uint64_t)row * t.R;
+    uint32_t nc = t.ncols[row];
+    if (g == 0) saved[i] = nc;
+    if (g < nc) cache[grp][g] = gcols[g];
+    for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
+        const uint64_t m = (uint32_t)keys[j];
+        uint8_t* h = emit + m * emit_stride(EB);
+        const uint32_t hdr = *reinterpret_cast<const uint16_t*>(h);
+        if (hdr == kReparse) {  // not compact: the serial walk takes over from message j
             if (g == 0) {
-                uint32_t err = UINT32_MAX;
-                if (fast) {
-                    uint32_t* seen = sh.mask[grp];  // zeroed by group_parse; 256 bits per vector
-                    for (uint32_t k = 1; k < gp.nt && err == UINT32_MAX; ++k) {
-                        if (k == gp.kn) continue;
-                        const Guid16 x = sh.eg[grp][k];
-                        uint32_t col = cached_col<G>(sh.cols[grp], gcols, nc, x, k < gp.kn ? k - 1 : k - gp.kn - 1);
-                        if (col == UINT32_MAX) {
-                            if (nc >= t.R) { err = kErrFull; break; }
-                            col = nc++;
-                            gcols[col] = x;
-                            if (col < (uint32_t)G) sh.cols[grp][col] = x;
-                        }
-                        const uint32_t bit = 1u << (col & 31), wi = (k < gp.kn ? 0u : 8u) + (col >> 5);
-                        if (seen[wi] & bit) err = kErrSyntax;  // repeated Guid in one vector
-                        seen[wi] |= bit;
-                    }
-                } else {  // the serial walk takes over from message j
-                    t.ncols[row] = nc;
-                    resume[atomicAdd(status + 4, 1ull)] = j;
-                }
-                if (err != UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | err);
-                sh.flags[grp] = err != UINT32_MAX || !fast ? kFail : 0;
-                sh.ntok[grp] = nc;
+                t.ncols[row] = nc;
+                resume[atomicAdd(status + 4, 1ull)] = j;
             }
-            wave_sync();
-            nc = sh.ntok[grp];
-            if (sh.flags[grp] & kFail) return;
+            return;
         }
-        if (g == 0) t.ncols[row] = nc;
+        const uint32_t cnt = hdr & ~kNeedsCols;
+        if (g < cnt) eg[grp][g] = eguid[m * kEmitMax + g];
+        seen[grp][g] = 0;  // L == 16 lanes clear the 16 words
+        wave_sync();
+        if (g == 0) {
+            uint16_t* codes = reinterpret_cast<uint16_t*>(h) + 1;
+            uint32_t err = UINT32_MAX, pos = 0, pv = 0;
+            for (uint32_t e = 0; e < cnt; ++e) {
+                const uint32_t vv = codes[e] >> 15;
+                pos = e == 0 || vv != pv ? 0 : pos + 1;  // position within its vector (find_col's hint)
+                pv = vv;
+                const Guid16 x = eg[grp][e];
+                uint32_t col = cached_col<L>(cache[grp], gcols, nc, x, pos);
+                if (col == UINT32_MAX) {
+                    if (nc >= t.R) { err = kErrFull; break; }
+                    col = nc++;
+                    gcols[col] = x;
+                    if (col < L) cache[grp][col] = x;
+                }
+                const uint32_t bit = 1u << (col & 31), wi = vv * 8 + (col >> 5);
+                if (seen[grp][wi] & bit) { err = kErrSyntax; break; }  // repeated Guid in one vector
+                seen[grp][wi] |= bit;
+                codes[e] = (uint16_t)(col | vv << 15);
+            }
+            *reinterpret_cast<uint16_t*>(h) = (uint16_t)cnt;  // resolved: pass B applies the record
+            if (err != UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | err);
+            bc[grp] = err != UINT32_MAX ? ~0u : nc;
+        }
+        wave_sync();
+        const uint32_t b = bc[grp];
+        if (b == ~0u) return;
+        nc = b;
     }
+    if (g == 0) t.ncols[row] = nc;
 }
 
-// The rest of a row's walk from a message the group parse handed over (serial ResolveVis, one lane).
+// The rest of a row's walk from a message k_resolve_emit handed over (serial ResolveVis, one lane).  A
+// compact message further on in the walk still has its record to resolve: its columns are looked up
+// once its Guids are in the row, so pass B applies it from the record.
 template <int EB>
 __global__ __launch_bounds__(kBlock) void k_resolve_resume(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
                                                            unsigned long long* __restrict__ status,
-                                                           const unsigned long long* __restrict__ resume) {
+                                                           const unsigned long long* __restrict__ resume, uint8_t* __restrict__ emit,
+                                                           const Guid16* __restrict__ eguid) {
     const unsigned long long nr = status[4];
     for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nr; r += (uint64_t)gridDim.x * kBlock) {
         const uint64_t j0 = resume[r];
         const uint32_t row = (uint32_t)(keys[j0] >> 32);
+        Guid16* gcols = t.cols + (uint64_t)row * t.R;
         for (uint64_t j = j0; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
             const uint64_t m = (uint32_t)keys[j];
-            const uint32_t err = resolve_msg<EB>(bytes, off, m, t.cols + (uint64_t)row * t.R, t.ncols + row, t.R);
+            const uint32_t err = resolve_msg<EB>(bytes, off, m, gcols, t.ncols + row, t.R);
             if (err != UINT32_MAX) {
                 atomicMin(status + 2, (unsigned long long)m << 2 | err);
                 break;
+            }
+            uint16_t* h = reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB));
+            if (h[0] != kReparse && (h[0] & kNeedsCols)) {
+                const uint32_t cnt = h[0] & ~kNeedsCols;
+                for (uint32_t e = 0; e < cnt; ++e) {
+                    const uint32_t col = find_col(gcols, t.ncols[row], eguid[m * kEmitMax + e], UINT32_MAX);
+                    h[1 + e] = (uint16_t)((col & 0x7FFF) | (h[1 + e] & 0x8000));
+                }
+                h[0] = (uint16_t)cnt;
             }
         }
     }
@@ -551,45 +571,29 @@ inline unsigned json_blocks(uint64_t n, int G) { return (unsigned)((n * (uint64_
 
 template <int EB>
 void launch_resolve_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_t* off, const unsigned long long* keys, uint64_t nd,
-                      const Table& t, uint32_t* saved, unsigned long long* status, unsigned long long* resume) {
-    const unsigned gr = json_blocks(nd, G);
-    switch (G) {
-        case 1: hipLaunchKernelGGL((k_resolve<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        case 4: hipLaunchKernelGGL((k_resolve<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        case 16: hipLaunchKernelGGL((k_resolve<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        case 8: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        case 32: hipLaunchKernelGGL((k_resolve<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        case 64: hipLaunchKernelGGL((k_resolve<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
-        default: hipLaunchKernelGGL((k_resolve<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status, resume); break;
+                      const Table& t, uint8_t* emit, const Guid16* eguid, uint32_t* saved, unsigned long long* status,
+                      unsigned long long* resume) {
+    if (G == 1) {
+        hipLaunchKernelGGL(k_resolve_serial<EB>, dim3(json_blocks(nd, 1)), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status);
+    } else {
+        hipLaunchKernelGGL(k_resolve_emit<EB>, dim3(json_blocks(nd, kEmitLanes)), dim3(kBlock), 0, st, keys, nd, t, emit, eguid, saved, status,
+                           resume);
     }
 }
 
 template <int EB>
 void launch_scan_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1,
-                   const Table& t, unsigned long long* status, unsigned long long* deferred, uint8_t* emit, unsigned long long* slow) {
+                   const Table& t, unsigned long long* status, unsigned long long* deferred, uint8_t* emit, Guid16* eguid,
+                   unsigned long long* slow) {
     const unsigned gr = json_blocks(m1 - m0, G);
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_scan<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        case 4: hipLaunchKernelGGL((k_scan<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        case 16: hipLaunchKernelGGL((k_scan<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        case 8: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        case 32: hipLaunchKernelGGL((k_scan<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        case 64: hipLaunchKernelGGL((k_scan<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
-        default: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, slow); break;
+        case 1: hipLaunchKernelGGL((k_scan<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 4: hipLaunchKernelGGL((k_scan<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 16: hipLaunchKernelGGL((k_scan<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 8: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 32: hipLaunchKernelGGL((k_scan<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 64: hipLaunchKernelGGL((k_scan<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        default: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
     }
 }
 
-template <int EB>
-void launch_apply_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, const unsigned long long* list,
-                    uint64_t n, const Table& t, void* P, void* N, unsigned long long* status) {
-    const unsigned gr = json_blocks(n, G);
-    switch (G) {
-        case 1: hipLaunchKernelGGL((k_apply<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        case 4: hipLaunchKernelGGL((k_apply<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        case 16: hipLaunchKernelGGL((k_apply<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        case 8: hipLaunchKernelGGL((k_apply<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        case 32: hipLaunchKernelGGL((k_apply<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        case 64: hipLaunchKernelGGL((k_apply<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-        default: hipLaunchKernelGGL((k_apply<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, list, n, t, P, N, status); break;
-    }
-}

@@ -74,11 +74,15 @@ def test_decode_contract_on_device(ctx, eb, group, monkeypatch):
         pr.close()
 
 
-@pytest.mark.parametrize("group", ["1", "16"])
+@pytest.mark.parametrize("ws", [0.0, 0.3])
+@pytest.mark.parametrize("group", ["1", "8", "16"])
 @pytest.mark.parametrize("eb,R,pool", [(4, 8, 6), (8, 8, 6), (4, 64, 40), (8, 200, 150)])
-def test_random_waves_match_oracle(ctx, eb, R, pool, group, monkeypatch):
+def test_random_waves_match_oracle(ctx, eb, R, pool, group, ws, monkeypatch):
+    """ws: the fraction of states written with a space after every ':' (valid, not the compact form), so
+    one row's walk mixes group-parsed and serially parsed messages: pass C hands a walk to the serial
+    resume kernel, which also resolves the records of the compact messages after it."""
     monkeypatch.setenv("JANUS_JSON_GROUP", group)
-    rng = np.random.default_rng(R * 10 + eb)
+    rng = np.random.default_rng(R * 10 + eb + int(ws * 100))
     n_keys = 40
     stable = random_guids(rng, n_keys)
     pr = Pair(ctx, n_keys, R, eb, stable)
@@ -87,6 +91,7 @@ def test_random_waves_match_oracle(ctx, eb, R, pool, group, monkeypatch):
         n = int(rng.integers(1, 1500))
         keys = rng.integers(0, n_keys, n).astype(np.uint32)
         msgs = [cl.message(int(k), grow=0.05 if R > 8 else 0.3) for k in keys]
+        msgs = [m.replace(b'":', b'": ') if rng.random() < ws else m for m in msgs]
         bad, rc = pr.oracle(keys, msgs)
         assert bad is None and rc == 0
         pr.s.merge_json(keys, msgs)
