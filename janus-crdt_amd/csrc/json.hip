@@ -6,25 +6,31 @@
 // message at a time inside HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160).  Here a whole
 // wave of PNCounterMsg JSON payloads is uploaded once and decoded, interned and merged on the GPU:
 //
-//   pass A  k_scan      a group of lanes per message (json_wave.hpp; the serial parser for payloads
-//                       not in the compact form): full parse + validation (the wire contract of
-//                       oracle/json.hpp), every Guid looked up in its row's replica table (read-only);
-//                       a Guid repeated among a vector's known replicas is an error; a message naming a
-//                       replica its row has not seen is DEFERRED (row << 32 | msg appended to a list).
-//   host     one 16-byte D2H: first bad message, deferred count.  A bad message = nothing is written.
+//   pass A  k_scan      8 lanes per message (json_wave.hpp) prove the payload is the compact form
+//                       System.Text.Json writes and check it against the wire contract of
+//                       oracle/json.hpp; every Guid is looked up in its row's replica table (read-only);
+//                       a Guid repeated among a vector's known replicas is an error.  Each message
+//                       leaves a record: its entries' columns and values (pass B applies it), or, when
+//                       it names a replica its row has not seen (DEFERRED, marked per message), the
+//                       entries' Guids and values with the columns still open.  Payloads not in the
+//                       compact form go to the slow list: k_scan_slow runs the serial parser on them.
+//   host     deferral marks compacted (hipcub select, count written beside the status) and one
+//            D2H of the status words: first bad message, deferred count.  A bad message = nothing
+//            is written.
 //   sort     hipcub radix sort of the deferred list -> messages grouped by row in commit order.
-//   pass C   k_resolve   one thread per row segment walks its deferred messages in commit order and
-//                       appends the new replica Guids (pVector entries first, then nVector — Merge's
-//                       order) to the row's table: first-insertion order = the stable Dictionary's
-//                       enumeration order.  A full row or a Guid repeated in one vector rolls the
-//                       appended columns back and fails the call.
-//   pass B  k_apply     a group of lanes per message: parse again, every Guid now resolves, atomicMax into
-//                       P / N (messages of one wave may repeat a key; max is order-free).
+//   pass C   k_resolve_emit  one group per row segment walks the row's deferred records in commit
+//                       order and appends the new replica Guids (pVector entries first, then nVector —
+//                       Merge's order) to the row's table: first-insertion order = the stable
+//                       Dictionary's enumeration order; the columns go back into the records.  A walk
+//                       reaching a non-compact message continues serially (k_resolve_resume).  A full
+//                       row or a Guid repeated in one vector rolls the appended columns back and fails
+//                       the call.
+//   pass B  k_apply_emit  one lane per record entry, atomicMax into P / N (messages of one wave may
+//                       repeat a key; max is order-free); k_apply_list parses the slow list again.
 //
-// The serial parser (scan_one / apply_one, the fallback) is byte-serial per thread through a 16-byte
-// window register; the group parse loads a message's windows side by side and checks its tokens in
-// parallel (json_wave.hpp).  The bound of the end-to-end call is the PCIe upload of the payload
-// (DESIGN.md §4).
+// JANUS_JSON_GROUP=1 runs the serial parser (scan_one / resolve_one / apply_one: byte-serial per thread
+// through a 16-byte window register) for every message: the reference the group path is tested
+// against.  The bound of the end-to-end call is the PCIe upload of the payload.
 //
 // Replica table (jg_pnc::cols / ncols, allocated on first use): [n_keys x R] Guids + [n_keys] counts.
 // P and N share one column per replica: the reference keeps two dictionaries whose key orders coincide
