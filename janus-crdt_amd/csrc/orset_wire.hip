@@ -574,11 +574,12 @@ __global__ void k_names_put(Names N, uint64_t g0, uint64_t pool0, const uint32_t
     tab_insert(N, key, (uint32_t)g);
 }
 
-// commit: each live group head looks its string up; new strings are queued as (set << 32 | entry).
+// commit: each live group head looks its string up; new strings are marked (set << 32 | entry) at their
+// sorted index.  Marks, not a wave-aggregated counter: every wave that met a new string took a returning
+// atomic on one address, which serialised the grid there.
 __global__ void k_ow_resolve(Entries E, const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ skey,
                              const uint32_t* __restrict__ sval, const uint32_t* __restrict__ label, uint64_t n, uint64_t limit, Names N,
-                             uint32_t* __restrict__ gid, unsigned long long* __restrict__ newk, uint32_t* __restrict__ newv,
-                             unsigned long long* __restrict__ status) {
+                             uint32_t* __restrict__ gid, unsigned long long* __restrict__ newk) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool fresh = false;
     uint32_t e = 0, set = 0;
@@ -594,18 +595,15 @@ __global__ void k_ow_resolve(Entries E, const uint32_t* __restrict__ mset, const
             else fresh = true;
         }
     }
-    // new strings: one atomic per wave for their slots (their order is fixed later by the sort)
-    const unsigned long long b = __ballot(fresh);
-    if (!b) return;
-    const uint32_t lane = __lane_id(), leader = __ffsll((long long)b) - 1;
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(status + 1, (unsigned long long)__popcll(b));
-    base = __shfl(base, (int)leader);
-    if (fresh) {
-        const unsigned long long k = base + __popcll(b & ((1ull << lane) - 1));
-        newk[k] = (unsigned long long)set << 32 | e;
-        newv[k] = (uint32_t)i;
-    }
+    // new strings: marked in place (compacted by select_marked; their order is fixed later by the sort)
+    if (i < n) newk[i] = fresh ? (unsigned long long)set << 32 | e : kNone;
+}
+
+// Keys of the compacted new-string marks (count on the device).
+__global__ void k_ow_gather_new(const unsigned long long* __restrict__ newk, const uint32_t* __restrict__ idx,
+                                const unsigned long long* __restrict__ count, unsigned long long* __restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < *count) out[j] = newk[idx[j]];
 }
 
 __device__ __forceinline__ uint64_t set_begin(const unsigned long long* snk, uint64_t n, uint32_t set) {
@@ -687,15 +685,14 @@ __device__ __forceinline__ uint64_t rec_hash(unsigned long long k, const Tag16& 
 }
 
 // Distinct records: insert-if-absent into an open-addressing table of record indices (exact compare on a
-// hash match); the copy that wins the slot is appended to its side's output (wave-aggregated counter)
-// with its table slot, and every copy lowers the slot's mint to its tag index: mint = the record's
+// hash match); the copy that wins the slot marks itself with its side (fsel = 1 + side, compacted per
+// side afterwards: a wave-aggregated counter per side had every wave wait on one of two addresses) and
+// its table slot, and every copy lowers the slot's mint to its tag index: mint = the record's
 // FIRST occurrence in commit order = its arrival ordinal (a HashSet keeps a tag where it was first
 // inserted; tag indices run message after message, each message in its arrays' order).
 __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* __restrict__ rkey, const uint8_t* __restrict__ rside,
                                                      const Tag16* __restrict__ tval, uint64_t nt, unsigned long long* __restrict__ tab, uint64_t mask,
-                                                     uint32_t* __restrict__ mint, unsigned long long* __restrict__ dk0, Tag16* __restrict__ dt0,
-                                                     uint32_t* __restrict__ ds0, unsigned long long* __restrict__ dk1, Tag16* __restrict__ dt1,
-                                                     uint32_t* __restrict__ ds1, unsigned long long* __restrict__ counts) {
+                                                     uint32_t* __restrict__ mint, uint8_t* __restrict__ fsel, uint32_t* __restrict__ fslot) {
     const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool fresh = false;
     uint32_t side = 0;
@@ -723,25 +720,37 @@ __global__ __launch_bounds__(kBlock) void k_ow_dedup(const unsigned long long* _
             const Tag16 o = tval[u];
             if (rkey[u] == k && rside[u] == side && o.lo == g.lo && o.hi == g.hi) { slot = s; break; }
         }
-        atomicMin(mint + slot, (uint32_t)t);
+        // most copies arrive after the first (lower tag index, earlier block) has set the slot: a plain
+        // read settles them without an atomic on what is often a hot address
+        if (mint[slot] > (uint32_t)t) atomicMin(mint + slot, (uint32_t)t);
     }
-    const uint32_t lane = __lane_id();
-    for (uint32_t sd = 0; sd < 2; ++sd) {
-        const bool mine = fresh && side == sd;
-        const unsigned long long b = __ballot(mine);
-        if (!b) continue;
-        const uint32_t leader = __ffsll((long long)b) - 1;
-        unsigned long long base = 0;
-        if (lane == leader) base = atomicAdd(counts + sd, (unsigned long long)__popcll(b));
-        base = __shfl(base, (int)leader);
-        if (mine) {
-            const unsigned long long pos = base + __popcll(b & ((1ull << lane) - 1));
-            (sd ? dk1 : dk0)[pos] = k;
-            (sd ? dt1 : dt0)[pos] = g;
-            (sd ? ds1 : ds0)[pos] = (uint32_t)slot;
-        }
+    if (t < nt) {
+        fsel[t] = fresh ? (uint8_t)(1 + side) : (uint8_t)0;
+        fslot[t] = (uint32_t)slot;
     }
 }
+
+// The distinct records of one side, compacted (select_marked) in tag order: keys, tags, table slots.
+__global__ void k_ow_gather_side(const uint32_t* __restrict__ idx, const unsigned long long* __restrict__ count,
+                                 const unsigned long long* __restrict__ rkey, const Tag16* __restrict__ tval, const uint32_t* __restrict__ fslot,
+                                 unsigned long long* __restrict__ dk, Tag16* __restrict__ dt, uint32_t* __restrict__ ds) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *count) return;
+    const uint32_t t = idx[j];
+    dk[j] = rkey[t];
+    dt[j] = tval[t];
+    ds[j] = fslot[t];
+}
+
+struct IsNewAt {
+    const unsigned long long* k;
+    __host__ __device__ bool operator()(const uint32_t& i) const { return k[i] != kNone; }
+};
+struct OnSide {
+    const uint8_t* fsel;
+    uint8_t want;
+    __host__ __device__ bool operator()(const uint32_t& t) const { return fsel[t] == want; }
+};
 
 __global__ void k_iota(uint32_t* __restrict__ p, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -796,6 +805,7 @@ struct jg_orset_wire {
     jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
     jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm, perm2;
     jg::DevBuf newk, newv, snk, snv, status, cub;
+    jg::DevBuf cnk, fsel, fslot, fidx;  // commit: compacted new-string keys; dedup marks, slots, compacted indices
     jg_orset* recs = nullptr;  // a committed wave's records, sorted (the merge source), reused
     // ids issued by the last commit: names [g0, g1), pool bytes [p0, p1)
     uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;
@@ -898,6 +908,14 @@ void sort_pairs(jg_ctx* ctx, jg_orset_wire* w, const K* kin, K* kout, const V* v
     size_t temp = 0;
     JG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, kin, kout, vin, vout, (int)n, 0, end_bit, ctx->stream));
     JG_HIP(hipcub::DeviceRadixSort::SortPairs(cub_temp(w, temp), temp, kin, kout, vin, vout, (int)n, 0, end_bit, ctx->stream));
+}
+
+// Indices i in [0, n) with pred(i), in order, into idx; their number into *count (device).
+template <class Pred> void select_marked(jg_ctx* ctx, jg_orset_wire* w, Pred pred, uint64_t n, uint32_t* idx, unsigned long long* count) {
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceSelect::If(nullptr, temp, it, idx, count, (int)n, pred, ctx->stream));
+    JG_HIP(hipcub::DeviceSelect::If(cub_temp(w, temp), temp, it, idx, count, (int)n, pred, ctx->stream));
 }
 
 void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
@@ -1059,7 +1077,14 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         JG_HIP(hipMemsetAsync(st, 0, 64, ctx->stream));
         hipLaunchKernelGGL(k_ow_resolve, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
                            w->skey.as<unsigned long long>(), w->sval.as<uint32_t>(), w->label.as<uint32_t>(), ne, limit, names_of(w),
-                           w->gid.as<uint32_t>(), w->newk.as<unsigned long long>(), w->newv.as<uint32_t>(), st);
+                           w->gid.as<uint32_t>(), w->newk.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        // the marked sorted indices compacted (count into st[1]) and their keys gathered; the sort below
+        // orders them by (set, first entry)
+        ensure(w->cnk, ne * 8);
+        select_marked(ctx, w, IsNewAt{w->newk.as<unsigned long long>()}, ne, w->newv.as<uint32_t>(), st + 1);
+        hipLaunchKernelGGL(k_ow_gather_new, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->newk.as<unsigned long long>(),
+                           w->newv.as<uint32_t>(), st + 1, w->cnk.as<unsigned long long>());
         JG_HIP(hipGetLastError());
         unsigned long long h[2];
         read_words(ctx, st, h, 2);
@@ -1069,7 +1094,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         ensure_names(ctx, w, nnew, w->wnb);
         ensure(w->snk, nnew * 8);
         ensure(w->snv, nnew * 4);
-        sort_pairs(ctx, w, w->newk.as<unsigned long long>(), w->snk.as<unsigned long long>(), w->newv.as<uint32_t>(), w->snv.as<uint32_t>(), nnew,
+        sort_pairs(ctx, w, w->cnk.as<unsigned long long>(), w->snk.as<unsigned long long>(), w->newv.as<uint32_t>(), w->snv.as<uint32_t>(), nnew,
                    32 + bits_for(w->max_set));
         const unsigned long long init[4] = {0, 0, w->pool_used, 0};
         JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
@@ -1108,11 +1133,20 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     JG_HIP(hipMemsetAsync(w->dtab.p, 0, tcap * 8, ctx->stream));
     JG_HIP(hipMemsetAsync(w->dmin.p, 0xFF, tcap * 4, ctx->stream));
     JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
+    ensure(w->fsel, nt + 1);
+    ensure(w->fslot, nt * 4 + 4);
+    ensure(w->fidx, nt * 4 + 4);
     hipLaunchKernelGGL(k_ow_dedup, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>(),
-                       w->tval.as<Tag16>(), nt, w->dtab.as<unsigned long long>(), tcap - 1, w->dmin.as<uint32_t>(), w->dk[0].as<unsigned long long>(),
-                       w->dt[0].as<Tag16>(), w->ds[0].as<uint32_t>(), w->dk[1].as<unsigned long long>(), w->dt[1].as<Tag16>(), w->ds[1].as<uint32_t>(),
-                       st + 4);
+                       w->tval.as<Tag16>(), nt, w->dtab.as<unsigned long long>(), tcap - 1, w->dmin.as<uint32_t>(), w->fsel.as<uint8_t>(),
+                       w->fslot.as<uint32_t>());
     JG_HIP(hipGetLastError());
+    for (int sd = 0; sd < 2; ++sd) {  // each side's distinct records, compacted in tag order
+        select_marked(ctx, w, OnSide{w->fsel.as<uint8_t>(), (uint8_t)(1 + sd)}, nt, w->fidx.as<uint32_t>(), st + 4 + sd);
+        hipLaunchKernelGGL(k_ow_gather_side, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, w->fidx.as<uint32_t>(), st + 4 + sd,
+                           w->rkey.as<unsigned long long>(), w->tval.as<Tag16>(), w->fslot.as<uint32_t>(), w->dk[sd].as<unsigned long long>(),
+                           w->dt[sd].as<Tag16>(), w->ds[sd].as<uint32_t>());
+        JG_HIP(hipGetLastError());
+    }
     unsigned long long cnt[2];
     read_words(ctx, st + 4, cnt, 2);
     if (cnt[0] + cnt[1] == 0) return;
