@@ -431,7 +431,10 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
     if (cnt == kReparse || (cnt & kNeedsCols) || e >= cnt) return;
     const uint32_t code = reinterpret_cast<const uint16_t*>(h)[1 + e];
     const T v = reinterpret_cast<const T*>(h + 32)[e];
-    atomicMax(static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF), v);
+    T* cell = static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF);
+    // a wave repeats hot keys (C1: 100 keys, ~3000 states each): most values do not raise the cell, and
+    // a plain read settles those without an atomic on a hot address
+    if (*cell < v) atomicMax(cell, v);
 }
 
 // Pass B for the messages left to the serial parser (list entries: [row << 32 |] message): parse again,

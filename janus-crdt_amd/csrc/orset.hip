@@ -66,42 +66,43 @@ __global__ __launch_bounds__(kOB) void k_check_sorted(const unsigned long long* 
     }
 }
 
-// Largest ord + 1 into span[0] (atomicMax per wave; span zeroed by the caller).
-__device__ __forceinline__ void wave_span(uint32_t mine, unsigned long long* span) {
-    unsigned long long v = (unsigned long long)mine + 1ull;
+// Largest ord + 1 over the block into span[0]: one atomicMax per block at the end of its grid-stride
+// loop (span zeroed by the caller).  Every thread of the block calls it once.
+__device__ __forceinline__ void block_span(unsigned long long v, unsigned long long* span) {
+    __shared__ unsigned long long wmax[kOB / 64];
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         const unsigned long long o = __shfl_xor(v, d, 64);
         v = o > v ? o : v;
     }
-    if ((threadIdx.x & 63) == 0 && v) atomicMax(span, v);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kOB / 64; ++w) v = wmax[w] > v ? wmax[w] : v;
+        if (v) atomicMax(span, v);
+    }
 }
 
 // Host AoS records -> dense SoA stream; err |= 2 for an ord >= 2^32, span[0] = largest ord + 1.
 __global__ __launch_bounds__(kOB) void k_unpack(const jg_tagrec* __restrict__ in, uint64_t n, unsigned long long* __restrict__ k,
                                                 uint4* __restrict__ t, uint32_t* __restrict__ o, unsigned* err, unsigned long long* span) {
-    const uint64_t stride = (uint64_t)gridDim.x * kOB;
-    const uint64_t n_pad = (n + stride - 1) / stride * stride;  // every lane of a wave reaches wave_span
-    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n_pad; i += stride) {
-        uint32_t mine = 0;
-        bool any = false;
-        if (i < n) {
-            const jg_tagrec r = in[i];
-            k[i] = r.key;
-            t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
-            if (r.ord > 0xFFFFFFFFull) atomicOr(err, 2u);
-            mine = (uint32_t)r.ord;
-            o[i] = mine;
-            any = true;
-        }
-        wave_span(any ? mine : 0u, span);
+    unsigned long long mx = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB) {
+        const jg_tagrec r = in[i];
+        k[i] = r.key;
+        t[i] = to_u4(Tag{r.tag_lo, r.tag_hi});
+        if (r.ord > 0xFFFFFFFFull) atomicOr(err, 2u);
+        o[i] = (uint32_t)r.ord;
+        mx = std::max<unsigned long long>(mx, (unsigned long long)(uint32_t)r.ord + 1ull);
     }
+    block_span(mx, span);
 }
 
 __global__ __launch_bounds__(kOB) void k_ord_span(const uint32_t* __restrict__ o, uint64_t n, unsigned long long* span) {
-    const uint64_t stride = (uint64_t)gridDim.x * kOB;
-    const uint64_t n_pad = (n + stride - 1) / stride * stride;
-    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n_pad; i += stride) wave_span(i < n ? o[i] : 0u, span);
+    unsigned long long mx = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kOB + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kOB)
+        mx = std::max<unsigned long long>(mx, (unsigned long long)o[i] + 1ull);
+    block_span(mx, span);
 }
 
 // Renumbering (order kept): ranks -> (ord, rank) pairs, sorted by ord (stable: ties stay in rank =
