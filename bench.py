@@ -261,7 +261,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
         last = {}
         wall, _ = timed(ctx, sync, lambda: last.update(shard.exchange_pnc(store, rows, ex, dev)), steps, warmup)
         # the owner-side merge alone (jg_pnc_merge_batch with key indices: k_group_link + k_merge_grouped +
-        # k_group_reset) on a batch of the same shape with keys in this rank's shard
+        # the list heads reset) on a batch of the same shape with keys in this rank's shard
         lkeys = keys % EXCH_KEYS
         rows.upload(zeros, zeros, lkeys)
         rows.synth(SEED + 11 + rank)
@@ -271,7 +271,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
         rows.close()
     row_bytes = 4 + 2 * PNC_R * PNC_EB
     distinct = int(np.unique(lkeys).size)
-    merge_alg = EXCH_ROWS * row_bytes + distinct * 2 * PNC_R * PNC_EB  # every row read; each distinct key's A row read + written once
+    merge_alg = EXCH_ROWS * row_bytes + distinct * 4 * PNC_R * PNC_EB  # every row read; each distinct key's A row (P, N) read + written once
     merge_s = ev_m / steps
     sent = last["sent"].astype(np.int64)
     remote = int(sent.sum() - sent[rank]) if world > 1 else 0
@@ -279,7 +279,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
                         f"uniform over {world} x {EXCH_KEYS} keys): route + all-to-all + merge from device memory",
             "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
             "xgmi_bytes_per_rank": remote * row_bytes, "row_bytes": row_bytes,
-            "merge": {"kernels": "k_group_link + k_merge_grouped<8,4> + k_group_reset", "ms": merge_s * 1e3,
+            "merge": {"kernels": "k_group_link + k_merge_grouped<8,4>", "ms": merge_s * 1e3,
                       "distinct_keys": distinct,
                       "roofline": {"bound": "hbm", "achieved": merge_alg / merge_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": merge_alg / merge_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": merge_alg}},

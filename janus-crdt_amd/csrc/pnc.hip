@@ -115,7 +115,9 @@ __global__ __launch_bounds__(kBlock) void k_merge_indexed_rows(typename Elem<EB>
 // per row).  Pass 2 (k_merge_grouped): the head row of every key loads its A row once, max-folds every
 // B row of the key in registers — each B row's load issued together with its next[] link, so a key
 // held k times costs k - 1 dependent hops — and stores A once; the other rows of the key do nothing.
-// Pass 3 (k_group_reset) restores the touched heads.  Atomics ran at ~1.3 TB/s of added bytes on
+// The list head also restores head[key] to kNil once it has claimed the key (any row reading head
+// later sees kNil, not itself: only the head row ever matched), so no reset pass runs.  Atomics ran
+// at ~1.3 TB/s of added bytes on
 // MI355X against ~6 TB/s for plain stores (MI355X_MICROARCH.md, atomics table), and random 4-B atomics
 // ~17x slower again: a per-cell atomicMax for repeated keys (39 % of the rows of a uniform batch of n
 // rows over 2n keys) and an occurrence counter per row both measured slower (tools/tune_grouped.hip,
@@ -127,9 +129,6 @@ __global__ __launch_bounds__(kBlock) void k_group_link(const uint32_t* __restric
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
         next[i] = atomicExch(head + keys[i], (uint32_t)i);
 }
-__global__ __launch_bounds__(kBlock) void k_group_reset(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ head) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) head[keys[i]] = kNil;
-}
 
 // One wave per received row, U rows in flight; the row (R x EB bytes) is a whole number of 16-B vectors
 // and each lane owns the same vector slot(s) of every row it touches.
@@ -137,7 +136,7 @@ template <int EB, int U>
 __global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* __restrict__ AP, typename Elem<EB>::T* __restrict__ AN,
                                                           const typename Elem<EB>::T* __restrict__ BP,
                                                           const typename Elem<EB>::T* __restrict__ BN, const uint32_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ head, const uint32_t* __restrict__ next, uint64_t n_rows,
+                                                          uint32_t* __restrict__ head, const uint32_t* __restrict__ next, uint64_t n_rows,
                                                           uint32_t R) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nv = R * EB / 16;  // vectors per array row
@@ -150,6 +149,11 @@ __global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* 
             const uint64_t m = m0 + u;
             key[u] = m < n_rows ? keys[m] : 0;
             lead[u] = m < n_rows && head[key[u]] == (uint32_t)m;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (lead[u]) head[key[u]] = kNil;  // the key is claimed: ready for the next batch
         }
         for (uint32_t v = lane; v < 2 * nv; v += 64) {
             const bool isP = v < nv;
@@ -332,7 +336,7 @@ void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const vo
         else
             hipLaunchKernelGGL((k_merge_grouped<4, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (int*)AP, (int*)AN, (const int*)BP,
                                (const int*)BN, keys, g->head, g->next, n_rows, R);
-        hipLaunchKernelGGL(k_group_reset, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, g->head);
+
         JG_HIP(hipGetLastError());
         return;
     }
