@@ -172,7 +172,8 @@ __global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* 
             for (int u = 0; u < U; ++u) {
                 if (!lead[u]) continue;
                 a[u] = vmax<EB>(a[u], b[u]);
-                for (uint32_t cur = next[m0 + u]; cur != kNil;) {  // the key's other rows
+                uint64_t hops = 0;  // a list holds at most n_rows - 1 more rows: a bound every walk reaches
+                for (uint32_t cur = next[m0 + u]; cur != kNil && ++hops < n_rows;) {  // the key's other rows
                     const uint4 bb = nt_load(reinterpret_cast<const uint4*>(B + (uint64_t)cur * R) + w);
                     const uint32_t nx = next[cur];
                     a[u] = vmax<EB>(a[u], bb);
