@@ -379,14 +379,22 @@ void SafeUpdateTracker::grow() {  // rehash the live entries (tombstones dropped
 
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker) {
     const double t0 = wall_s();
-    std::vector<const NetworkProtocol*> msgs;
-    size_t n_msgs = 0;
+    // the wave's messages in commit order: block offsets first, then the blocks filled in parallel into
+    // a buffer kept across waves (a fresh 8 MB vector per 1M-message wave cost its page faults)
+    blocks_.clear();
     for (const auto& list : updates)
-        for (const auto& block : list) n_msgs += block.update.size();
-    msgs.reserve(n_msgs);
-    for (const auto& list : updates)
-        for (const auto& block : list)
-            for (const auto& u : block.update) msgs.push_back(&u);
+        for (const auto& block : list) blocks_.push_back(&block);
+    block_off_.resize(blocks_.size() + 1);
+    block_off_[0] = 0;
+    for (size_t b = 0; b < blocks_.size(); ++b) block_off_[b + 1] = block_off_[b] + blocks_[b]->update.size();
+    std::vector<const NetworkProtocol*>& msgs = msgs_;
+    msgs.resize(block_off_.back());
+    parallel_ranges(pool(), blocks_.size(), [&](size_t b0, size_t b1, int) {
+        for (size_t b = b0; b < b1; ++b) {
+            const NetworkProtocol* u = blocks_[b]->update.data();
+            for (size_t i = block_off_[b], e = block_off_[b + 1]; i < e; ++i) msgs[i] = u++;
+        }
+    });
     return apply_msgs(msgs, tracker, t0);
 }
 
@@ -445,6 +453,22 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     std::vector<size_t> cnt(2 * T), nbytes(2 * T), mbase(2 * (T + 1)), bbase(2 * (T + 1));
     const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
     bool open[2] = {false, false};
+    // The safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) are claimed in the
+    // classify pass, which already has each message in cache: (message, origin) per (chunk, worker),
+    // so concatenating the lists in that order keeps commit order; claims at or past the cut go back.
+    const bool sweep = tracker && tracker->size();
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> part(sweep ? n_chunks * T : 0);
+    struct GiveBack {  // any throw before the cut is known: nothing of the wave counts as applied
+        const std::vector<std::vector<std::pair<uint64_t, uint64_t>>>& part;
+        const NetworkProtocol* const* msgs;
+        SafeUpdateTracker* tracker;
+        bool armed = true;
+        ~GiveBack() {
+            if (armed)
+                for (const auto& p : part)
+                    for (const auto& [i, o] : p) tracker->add(msgs[i]->seq, o);
+        }
+    } give_back{part, msgs.data(), tracker};
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
         const size_t c0 = c * chunk_msgs, c1 = std::min(n, c0 + chunk_msgs);
@@ -453,7 +477,10 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             size_t k[2] = {0, 0}, bytes[2] = {0, 0};
             for (size_t i = c0 + b; i < c0 + e; ++i) {
                 if (i + 16 < c0 + e) __builtin_prefetch(msgs[i + 16]);
-                if (i + 8 < c0 + e) uids_.prefetch(msgs[i + 8]->uid);
+                if (i + 8 < c0 + e) {
+                    uids_.prefetch(msgs[i + 8]->uid);
+                    if (sweep) tracker->prefetch(msgs[i + 8]->seq);
+                }
                 const NetworkProtocol& u = *msgs[i];
                 uint32_t cl = kSkip;
                 if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
@@ -466,6 +493,8 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                     }
                 }
                 cls[i] = cl;
+                uint64_t o;
+                if (sweep && cl != kSkip && tracker->claim(u.seq, &o)) part[c * T + t].emplace_back(i, o);
             }
             for (int kind = 0; kind < 2; ++kind) {
                 cnt[kind * T + t] = k[kind];
@@ -549,19 +578,6 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     int cut_code = JG_OK;
     std::string cut_why;
     double to0 = 0, to1 = 0, t1 = 0;
-    // The safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) are claimed by the
-    // workers while the caller runs the device side below (validation, commit): one random tracker probe
-    // per message, hidden behind the GPU.  Worker t > 0 sweeps a contiguous range, so concatenating the
-    // claims in worker order keeps commit order; claims at or past the cut are put back afterwards.
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> part(T);  // (message, origin)
-    const bool sweep = tracker && tracker->size();
-    auto sweep_range = [&](size_t b, size_t e, int t) {
-        uint64_t o;
-        for (size_t i = b; i < e; ++i) {
-            if (i + 8 < e && cls[i + 8] != kSkip) tracker->prefetch(msgs[i + 8]->seq);
-            if (cls[i] != kSkip && tracker->claim(msgs[i]->seq, &o)) part[t].emplace_back(i, o);
-        }
-    };
     auto device_side = [&] {
         // OR-Set states: end the device validation; the first rejected state cuts the wave (the reference's
         // loop stops at the state whose Decode / Merge throws).
@@ -635,27 +651,8 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         orset_phase_s_[2] = wall_s() - to3;
     };
     const double tt = wall_s();
-    double t_sweep = 0;
-    if (sweep && T > 1 && n >= 8192) {
-        std::exception_ptr err;
-        wp.run([&](int t) {
-            if (t == 0) {
-                try { device_side(); } catch (...) { err = std::current_exception(); }
-                return;
-            }
-            const double ts = wall_s();
-            sweep_range(n * (t - 1) / (T - 1), n * t / (T - 1), t);
-            if (t == 1) t_sweep = wall_s() - ts;
-        });
-        if (err) {  // nothing of the wave counts as applied: every claim goes back
-            for (const auto& p : part)
-                for (const auto& [i, o] : p) tracker->add(msgs[i]->seq, o);
-            std::rethrow_exception(err);
-        }
-    } else {
-        device_side();
-        if (sweep) sweep_range(0, cut, 0);
-    }
+    device_side();
+    give_back.armed = false;
     std::vector<uint64_t> completed;
     if (sweep) {
         size_t kept = 0;
@@ -669,9 +666,8 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     host_s_ = t1 - t0;
     engine_s_ = wall_s() - t1;
     if (std::getenv("JANUS_TRACE_WAVE"))
-        std::fprintf(stderr, "wave: device side %.2f ms (orset check %.2f commit %.2f names %.2f), completion sweep %.2f ms (worker 1), total %.2f ms\n",
-                     1e3 * (wall_s() - tt), 1e3 * orset_phase_s_[0], 1e3 * orset_phase_s_[1], 1e3 * orset_phase_s_[2], 1e3 * t_sweep,
-                     1e3 * (wall_s() - tt));
+        std::fprintf(stderr, "wave: device side %.2f ms (orset check %.2f commit %.2f names %.2f)\n", 1e3 * (wall_s() - tt),
+                     1e3 * orset_phase_s_[0], 1e3 * orset_phase_s_[1], 1e3 * orset_phase_s_[2]);
     if (cut < n) throw ApplyError(cut_code, cut_why, cut, std::move(completed));
     return completed;
 }

@@ -301,6 +301,9 @@ class GpuStableStore {
     std::vector<std::pair<char*, size_t>> arenas_;  // pinned staging arenas (base, bytes)
     size_t arena_i_ = 0, arena_off_ = 0;            // carve position of the current wave
     std::vector<uint32_t> cls_, sid_;               // apply_msgs scratch: per message class / set id
+    std::vector<const UpdateMessage*> blocks_;      // ApplyCommitted scratch: the wave's blocks, their
+    std::vector<size_t> block_off_;                 //   first message, the messages in commit order
+    std::vector<const NetworkProtocol*> msgs_;
     std::vector<uint64_t> where_[2];                //   and per kind, the commit index of its messages
     std::unique_ptr<WorkerPool> pool_;
     std::vector<SetKey> sets_;
