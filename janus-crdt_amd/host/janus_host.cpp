@@ -479,7 +479,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                 if (i + 16 < c0 + e) __builtin_prefetch(msgs[i + 16]);
                 if (i + 8 < c0 + e) {
                     uids_.prefetch(msgs[i + 8]->uid);
-                    if (sweep) tracker->prefetch(msgs[i + 8]->seq);
+                    if (sweep) tracker->prefetch_claim(msgs[i + 8]->seq);
                 }
                 const NetworkProtocol& u = *msgs[i];
                 uint32_t cl = kSkip;

@@ -104,6 +104,11 @@ class SafeUpdateTracker {
     void prefetch(uint64_t seq) const {
         if (!slots_.empty()) __builtin_prefetch(&slots_[seq_slot(seq) & (slots_.size() - 1)]);
     }
+    // the line in exclusive state, for a claim() that will tombstone it (its CAS then needs no ownership
+    // request of its own; measured ~110 ns a claim with a shared-state prefetch, 14 workers)
+    void prefetch_claim(uint64_t seq) const {
+        if (!slots_.empty()) __builtin_prefetch(&slots_[seq_slot(seq) & (slots_.size() - 1)], 1);
+    }
     size_t size() const { return n_.load(std::memory_order_relaxed); }
     std::vector<std::pair<uint64_t, uint64_t>> items() const;  // live entries (any order)
 
