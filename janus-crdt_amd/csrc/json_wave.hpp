@@ -32,15 +32,15 @@ constexpr uint32_t kGroupTok = 16;                 // token slots (an entry span
 constexpr uint32_t kCompactMin = 27;               // {"pVector":{},"nVector":{}}
 enum : uint32_t { kSlow = 1, kMiss = 2, kDup = 4, kFail = 8 };
 
-template <int G, bool EG = false>
+template <int G>
 struct GroupShared {
     static constexpr int kGroups = kBlock / G;
     uint4 buf[kGroups][kGroupBytes / 16];
     Guid16 cols[kGroups][G];                       // the row's first G replica columns
-    Guid16 eg[EG ? kGroups : 1][EG ? kGroupTok : 1];  // pass C: the entries' Guids by token
     uint16_t tok[kGroups][kGroupTok];
     uint32_t mask[kGroups][16];                    // pass A: columns seen, 256 bits per vector
     uint32_t ntok[kGroups], kn[kGroups], nn[kGroups], flags[kGroups];
+    uint32_t geo[kGroups], row[kGroups], nc[kGroups];  // alignment offset | length << 4; the row, its columns
 };
 
 // LDS written by some lanes of a wave, then read by others: order them (a group never spans waves).
@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t hex4(uint32_t x, uint32_t& nib) {  // 1 if a
     const uint32_t x7 = x & 0x7F7F7F7Fu, l7 = x7 | 0x20202020u;
     const uint32_t dig = ge_bytes(x7, 0x30) & le_bytes(x7, 0x39);
     const uint32_t af = ge_bytes(l7, 0x61) & le_bytes(l7, 0x66);
-    nib = (x & 0x0F0F0F0Fu) + (af >> 7) * 9u;
+    nib = (x & 0x0F0F0F0Fu) + ((af >> 7) | (af >> 4));  // + 9 per letter (no multiply: bits 0 and 3)
     return ((dig | af) & ~x & 0x80808080u) == 0x80808080u ? 1u : 0u;
 }
 __device__ __forceinline__ uint32_t hex_pairs(uint32_t nib) {  // byte 0 = c0 c1, byte 2 = c2 c3
@@ -137,12 +137,21 @@ __device__ __forceinline__ bool entry_at(const uint8_t* base, uint32_t q, Guid16
     const uint32_t run = (uint32_t)__builtin_ctz(~dm);
     constexpr uint32_t kMaxDigits = EB == 4 ? 10 : 19;
     ok &= run >= 1 && run <= kMaxDigits && !((Y[0] & 0xFFu) == '0' && run > 1);
+    // digits while any lane of the wave still has one (magnitudes of a few digits are the common
+    // case); the first 7 in 24-bit multiply-adds (full rate: < 10^7), the rest in 64 bits
     unsigned long long mag = 0;
+    uint32_t m24 = 0;
 #pragma unroll
     for (uint32_t j = 0; j < kMaxDigits; ++j) {
+        if (!__builtin_amdgcn_ballot_w64(j < run)) break;  // wave-uniform
         const uint32_t d = (Y[j >> 2] >> (8 * (j & 3))) & 0xFu;
-        mag = j < run ? mag * 10 + d : mag;
+        if (j < 7) m24 = j < run ? __umul24(m24, 10u) + d : m24;
+        else {
+            if (j == 7) mag = m24;
+            mag = j < run ? mag * 10 + d : mag;
+        }
     }
+    if (run < 8) mag = m24;
     const unsigned long long lim = EB == 4 ? (neg ? 0x80000000ull : 0x7FFFFFFFull) : (neg ? 0x8000000000000000ull : 0x7FFFFFFFFFFFFFFFull);
     ok &= mag <= lim;
     out = neg ? (long long)(0ull - mag) : (long long)mag;
@@ -155,15 +164,19 @@ __device__ __forceinline__ bool lds_name_tail(const uint8_t* s) {  // s = the by
            s[8] == '{';
 }
 
-// A group's parse result: token k's entry (if any) on lane k mod G, slot k / G.
+// A wave's parse result.  The tokens of the wave's 64 / G groups, in group order, are dealt over its
+// 64 lanes: round u of a lane holds wave token lane + 64u, tg = its group << 16 | its index there.
+// (Dealt over the group's own G lanes, ~7 tokens per message took two rounds on 8 lanes whenever
+// one message of the wave had more than 8.)
 template <int EB, int G>
 struct GroupParse {
-    static constexpr int TPL = (kGroupTok + G - 1) / G;  // token slots per lane
-    static_assert(TPL * G >= (int)kGroupTok, "every token slot must have a lane: an unchecked token would pass the chain");
-    Guid16 eg[TPL];
-    long long ev[TPL];
-    bool has[TPL];
-    uint32_t kn, nt;
+    static constexpr int kRounds = (kGroupTok + G - 1) / G;
+    static_assert(64 % G == 0 && kRounds * 64 >= (64 / G) * (int)kGroupTok,
+                  "every token of the wave must have a lane: an unchecked token would pass the chain");
+    Guid16 eg[kRounds];
+    long long ev[kRounds];
+    uint32_t tg[kRounds];
+    bool has[kRounds];
 };
 
 // The group's row: its column count and first G columns, loaded before the payload so that both
@@ -201,9 +214,9 @@ __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16
 }
 
 // Phases 1-3 for message m on every lane of the group; on return sh.flags[grp] & kSlow is clear iff
-// the payload is proven compact, and the row cache is in sh.cols.  STORE_EG: entry Guids to sh.eg.
-template <int EB, int G, bool STORE_EG>
-__device__ __forceinline__ void group_parse(GroupShared<G, STORE_EG>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+// the payload is proven compact, and the row cache is in sh.cols / sh.row / sh.nc.
+template <int EB, int G>
+__device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                             uint64_t m, bool live, const RowCache& rc, GroupParse<EB, G>& gp) {
     constexpr uint32_t NW = (kGroupBytes / 16 + G - 1) / G;  // windows per lane
     const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
@@ -269,17 +282,20 @@ __device__ __forceinline__ void group_parse(GroupShared<G, STORE_EG>& sh, const 
         }
     }
     const bool go = fit && ntok <= kGroupTok && ntok >= 2;  // group-uniform
+    const uint32_t nt = go ? ntok : 0;
     if (g == 0) {
         sh.flags[grp] = go ? 0 : kSlow;
         sh.kn[grp] = 0;
         sh.nn[grp] = 0;
+        sh.ntok[grp] = nt;
+        sh.geo[grp] = a | L << 4;
+        sh.row[grp] = rc.row;
+        sh.nc[grp] = rc.nc;
     }
     for (uint32_t i = g; i < 16; i += G) sh.mask[grp][i] = 0;
     wave_sync();
     // phase 2: the "nVector" token
     const uint8_t* c = reinterpret_cast<const uint8_t*>(sh.buf[grp]) + a;
-    const uint32_t nt = go ? ntok : 0;
-    gp.nt = nt;
     for (uint32_t k = g; k < nt; k += G) {
         const uint32_t p = sh.tok[grp][k];
         if (p + 1 < L && c[p + 1] == 'n') {
@@ -288,48 +304,55 @@ __device__ __forceinline__ void group_parse(GroupShared<G, STORE_EG>& sh, const 
         }
     }
     wave_sync();
-    // phase 3: each token checked, the chain from token 0 to the closing brace
-    const uint32_t kn = sh.kn[grp];
-    gp.kn = kn;
-    bool bad = go && (sh.nn[grp] != 1 || kn == 0 || c[0] != '{');
+    // phase 3: each token checked (dealt over the wave), the chain from token 0 to the closing brace
+    constexpr uint32_t GW = 64 / G;  // groups per wave
+    const uint32_t lane = threadIdx.x & 63, wg0 = (threadIdx.x >> 6) * GW;
+    uint32_t base[GW + 1];
+    base[0] = 0;
 #pragma unroll
-    for (int u = 0; u < GroupParse<EB, G>::TPL; ++u) {
+    for (uint32_t j = 0; j < GW; ++j) base[j + 1] = base[j] + sh.ntok[wg0 + j];
+#pragma unroll
+    for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
         gp.has[u] = false;
-        const uint32_t k = g + u * G;
-        if (!go || bad || k >= nt) continue;
-        const uint32_t p = sh.tok[grp][k];
-        const uint32_t pn = k + 1 < nt ? sh.tok[grp][k + 1] : UINT32_MAX;
-        const int c1 = p + 1 < L ? c[p + 1] : -1;
-        uint32_t e = UINT32_MAX, next = UINT32_MAX;  // the '}' closing this token's vector / the next token's start
-        if (c1 == 'p' || c1 == 'n') {                // property name
-            if (p + 12 > L || !lds_name_tail(c + p + 2) || (c1 == 'p' && (k != 0 || p != 1))) { bad = true; continue; }
-            const uint32_t q = p + 11;
-            if (c[q] == '}') e = q;
-            else next = q;
-        } else {  // "<guid>":<int>
-            if (k == 0 || p + 41 > L) { bad = true; continue; }
-            Guid16 eg;
-            long long val;
-            uint32_t tr;
-            const bool ok = entry_at<EB>(reinterpret_cast<const uint8_t*>(sh.buf[grp]), a + p + 1, eg, val, &tr);
-            const uint32_t t = p + 1 + tr;
-            if (!ok || t >= L) {
-                bad = true;
-                continue;
+        gp.tg[u] = 0;
+        const uint32_t tw = lane + 64u * (uint32_t)u;
+        if (tw >= base[GW]) continue;
+        uint32_t j = 0, bj = 0;
+#pragma unroll
+        for (uint32_t i = 1; i < GW; ++i)
+            if (tw >= base[i]) { j = i; bj = base[i]; }
+        const uint32_t gq = wg0 + j, k = tw - bj;
+        const uint32_t geo = sh.geo[gq], aq = geo & 15u, Lq = geo >> 4, ntq = sh.ntok[gq], kn = sh.kn[gq];
+        const uint8_t* cq = reinterpret_cast<const uint8_t*>(sh.buf[gq]) + aq;
+        bool bad = k == 0 && (sh.nn[gq] != 1 || kn == 0 || cq[0] != '{');
+        do {
+            const uint32_t p = sh.tok[gq][k];
+            const uint32_t pn = k + 1 < ntq ? sh.tok[gq][k + 1] : UINT32_MAX;
+            const int c1 = p + 1 < Lq ? cq[p + 1] : -1;
+            uint32_t e = UINT32_MAX, next = UINT32_MAX;  // the '}' closing this token's vector / the next token's start
+            if (c1 == 'p' || c1 == 'n') {                // property name
+                if (p + 12 > Lq || !lds_name_tail(cq + p + 2) || (c1 == 'p' && (k != 0 || p != 1))) { bad = true; break; }
+                const uint32_t q = p + 11;
+                if (cq[q] == '}') e = q;
+                else next = q;
+            } else {  // "<guid>":<int>
+                if (k == 0 || p + 41 > Lq) { bad = true; break; }
+                uint32_t tr;
+                const bool ok = entry_at<EB>(reinterpret_cast<const uint8_t*>(sh.buf[gq]), aq + p + 1, gp.eg[u], gp.ev[u], &tr);
+                const uint32_t t = p + 1 + tr;
+                if (!ok || t >= Lq) { bad = true; break; }
+                if (cq[t] == ',') next = t + 1;
+                else if (cq[t] == '}') e = t;
+                else { bad = true; break; }
+                gp.has[u] = true;
+                gp.tg[u] = gq << 16 | k;
             }
-            if (c[t] == ',') next = t + 1;
-            else if (c[t] == '}') e = t;
-            else { bad = true; continue; }
-            gp.has[u] = true;
-            gp.eg[u] = eg;
-            gp.ev[u] = val;
-            if (STORE_EG) sh.eg[grp][k] = eg;
-        }
-        if (next != UINT32_MAX) bad |= pn != next || k + 1 == kn;               // another entry of this vector
-        else if (k < kn) bad |= e + 2 >= L || c[e + 1] != ',' || pn != e + 2 || k + 1 != kn;  // pVector ends, nVector next
-        else bad |= e + 2 != L || c[e + 1] != '}' || k + 1 != nt;              // nVector ends the message
+            if (next != UINT32_MAX) bad |= pn != next || k + 1 == kn;                 // another entry of this vector
+            else if (k < kn) bad |= e + 2 >= Lq || cq[e + 1] != ',' || pn != e + 2 || k + 1 != kn;  // pVector ends, nVector next
+            else bad |= e + 2 != Lq || cq[e + 1] != '}' || k + 1 != ntq;            // nVector ends the message
+        } while (false);
+        if (bad) atomicOr(&sh.flags[gq], (uint32_t)kSlow);
     }
-    if (bad) atomicOr(&sh.flags[grp], (uint32_t)kSlow);
     wave_sync();
 }
 
@@ -351,44 +374,46 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const bool live = m < m1;
         const RowCache rc = row_cache(t, rows, m, live, g);
         GroupParse<EB, G> gp;
-        group_parse<EB, G, false>(sh, bytes, off, m, live, rc, gp);
-        const bool fast = live && !(sh.flags[grp] & kSlow);
-        if (fast) {
-            const Guid16* gcols = t.cols + (uint64_t)rc.row * t.R;
+        group_parse<EB, G>(sh, bytes, off, m, live, rc, gp);
+        // each parsed entry (on the lane its token was dealt to): its column, repeat check, emit slot
 #pragma unroll
-            for (int u = 0; u < GroupParse<EB, G>::TPL; ++u) {
-                if (!gp.has[u]) continue;
-                const uint32_t k = g + u * G;
-                const uint32_t vv = k < gp.kn ? 0 : 1;
-                const uint32_t col = cached_col<G>(sh.cols[grp], gcols, rc.nc, gp.eg[u], vv ? k - gp.kn - 1 : k - 1);
-                if (col == UINT32_MAX) {
-                    atomicOr(&sh.flags[grp], (uint32_t)kMiss);
-                } else {
-                    const uint32_t bit = 1u << (col & 31);
-                    if (atomicOr(&sh.mask[grp][vv * 8 + (col >> 5)], bit) & bit) atomicOr(&sh.flags[grp], (uint32_t)kDup);
-                    const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
-                    uint8_t* h = emit + m * emit_stride(EB);
-                    reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(col | vv << 15);
-                    reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
-                }
-            }
-        }
-        wave_sync();
-        const uint32_t f = sh.flags[grp];
-        const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
-        if (deferred_msg) {  // pass C resolves the columns from these Guids, pass B then applies the record
-            uint8_t* h = emit + m * emit_stride(EB);
-#pragma unroll
-            for (int u = 0; u < GroupParse<EB, G>::TPL; ++u) {
-                if (!gp.has[u]) continue;
-                const uint32_t k = g + u * G;
-                const uint32_t vv = k < gp.kn ? 0 : 1;
-                const uint32_t e = vv ? k - 2 : k - 1;
-                eguid[m * kEmitMax + e] = gp.eg[u];
-                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(0x7FFF | vv << 15);
+        for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
+            const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
+            if (!gp.has[u] || (sh.flags[gq] & kSlow)) continue;
+            const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
+            const uint32_t kn = sh.kn[gq], rq = sh.row[gq];
+            const uint32_t vv = k < kn ? 0 : 1;
+            const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, sh.nc[gq], gp.eg[u], vv ? k - kn - 1 : k - 1);
+            if (col == UINT32_MAX) {
+                atomicOr(&sh.flags[gq], (uint32_t)kMiss);
+            } else {
+                const uint32_t bit = 1u << (col & 31);
+                if (atomicOr(&sh.mask[gq][vv * 8 + (col >> 5)], bit) & bit) atomicOr(&sh.flags[gq], (uint32_t)kDup);
+                const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
+                uint8_t* h = emit + mq * emit_stride(EB);
+                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(col | vv << 15);
                 reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
             }
         }
+        wave_sync();
+        // messages with an unknown replica: pass C resolves the columns from these Guids, pass B then
+        // applies the record
+#pragma unroll
+        for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
+            const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
+            const uint32_t fq = sh.flags[gq];
+            if (!gp.has[u] || (fq & (kSlow | kDup)) || !(fq & kMiss)) continue;
+            const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
+            const uint32_t vv = k < sh.kn[gq] ? 0 : 1;
+            const uint32_t e = vv ? k - 2 : k - 1;
+            uint8_t* h = emit + mq * emit_stride(EB);
+            eguid[mq * kEmitMax + e] = gp.eg[u];
+            reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(0x7FFF | vv << 15);
+            reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
+        }
+        const uint32_t f = sh.flags[grp];
+        const bool fast = live && !(f & kSlow);
+        const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
         const bool defer = g == 0 && deferred_msg;
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
         const bool to_slow = g == 0 && live && !fast;
@@ -396,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
-                (f & kDup) ? kReparse : (uint16_t)((gp.nt - 2) | ((f & kMiss) ? kNeedsCols : 0u));
+                (f & kDup) ? kReparse : (uint16_t)((sh.ntok[grp] - 2) | ((f & kMiss) ? kNeedsCols : 0u));
             if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
     }
