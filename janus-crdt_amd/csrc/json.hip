@@ -233,6 +233,7 @@ __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __re
         return;
     }
     deferred[m] = vis.miss ? (unsigned long long)row << 32 | m : kNotDeferred;  // counted by select_deferred
+    if (vis.miss) status[1] = 1;  // any deferral: the guarded tail of finish_wave stands down
     if (!vis.miss && slow) {
         const unsigned long long at = atomicAdd(status + 3, 1ull);
         slow[at] = m;
@@ -612,10 +613,28 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     jg_ctx* ctx = p->ctx;
     const Table t = table_of(p);
     const int G = json_group();
+    const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
     if (G > 1) {  // the payloads the group parse left to the serial parser (count read on the device)
         if (p->eb == 8) hipLaunchKernelGGL(k_scan_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
         else hipLaunchKernelGGL(k_scan_slow<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
         JG_HIP(hipGetLastError());
+        // The steady state (every payload valid, every replica known): pass B right away, guarded on the
+        // device by pass A's status, so the wave costs one status read.  If pass A failed or deferred a
+        // message both launches are no-ops and the full path below runs (all or nothing).
+        if (p->eb == 8) {
+            hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
+            hipLaunchKernelGGL(k_apply_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, w.slow, t, p->P.p, p->N.p, w.status);
+        } else {
+            hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
+            hipLaunchKernelGGL(k_apply_slow<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, w.slow, t, p->P.p, p->N.p, w.status);
+        }
+        JG_HIP(hipGetLastError());
+        const Status st = read_status(ctx, w.status);
+        if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
+        if (!st.n_deferred) {
+            if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
+            return;
+        }
     }
     DeferredLists dl = select_deferred(ctx, w.deferred, n, p->n_keys, w.status + 1);
     Status st = read_status(ctx, w.status);
@@ -649,9 +668,8 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     // pass B: pass A's records (resolved by pass C where deferred), then the messages left to the serial
     // parser (slow: not in the compact form; with JANUS_JSON_GROUP=1 also the deferred ones).  max is
     // order-free.
-    const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
-    if (p->eb == 8) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
-    else hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p);
+    if (p->eb == 8) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, nullptr);
+    else hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, nullptr);
     JG_HIP(hipGetLastError());
     const unsigned long long* lists[2] = {st.n_deferred ? sorted_deferred : nullptr, w.slow};
     const uint64_t counts[2] = {st.n_deferred, st.n_slow};

@@ -416,6 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
         const bool defer = g == 0 && deferred_msg;
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
+        if (defer) status[1] = 1;  // any deferral (select_deferred later overwrites it with the count)
         const bool to_slow = g == 0 && live && !fast;
         const unsigned long long at = wave_slot(to_slow, status + 3);
         if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
@@ -445,12 +446,12 @@ static_assert(kEmitMax <= kEmitLanes && kGroupTok - 2 <= kEmitMax, "an entry slo
 
 template <int EB>
 __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict__ emit, const uint32_t* __restrict__ rows, uint64_t n,
-                                                       uint32_t R, void* P, void* N) {
+                                                       uint32_t R, void* P, void* N, const unsigned long long* __restrict__ guard) {
     using T = typename ApplyVis<EB>::T;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint64_t m = tid / kEmitLanes;
     const uint32_t e = (uint32_t)(tid % kEmitLanes);
-    if (m >= n) return;
+    if (m >= n || (guard && (guard[0] != ~0ull || guard[1] != 0))) return;  // guard: pass A failed or deferred
     const uint8_t* h = emit + m * emit_stride(EB);
     const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
     if (cnt == kReparse || (cnt & kNeedsCols) || e >= cnt) return;
@@ -471,6 +472,18 @@ __global__ __launch_bounds__(kBlock) void k_apply_list(const uint8_t* __restrict
                                                        uint64_t n, Table t, void* P, void* N, unsigned long long* __restrict__ status) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) apply_one<EB>(bytes, off, rows, (uint32_t)list[i], t, P, N, status);
+}
+
+// k_apply_list over the slow list with its count read on the device (status[3]), guarded like
+// k_apply_emit: a no-op unless pass A accepted every message and deferred none.
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_apply_slow(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                       const uint32_t* __restrict__ rows, const unsigned long long* __restrict__ list,
+                                                       Table t, void* P, void* N, unsigned long long* __restrict__ status) {
+    if (status[0] != ~0ull || status[1] != 0) return;
+    const unsigned long long n = status[3];
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        apply_one<EB>(bytes, off, rows, (uint32_t)list[i], t, P, N, status);
 }
 
 // Pass C (new replicas appended in commit order) from pass A's records: no payload is parsed again.
