@@ -30,6 +30,7 @@
 constexpr uint32_t kGroupBytes = 512;              // LDS bytes per message: payload + its 16-B alignment offset
 constexpr uint32_t kGroupTok = 16;                 // token slots (an entry spans >= 41 bytes, a name 11)
 constexpr uint32_t kCompactMin = 27;               // {"pVector":{},"nVector":{}}
+constexpr uint32_t kMaskCols = 64;                 // pass A's repeat check covers columns < 64 (else: serial parser)
 enum : uint32_t { kSlow = 1, kMiss = 2, kDup = 4, kFail = 8 };
 
 template <int G>
@@ -38,7 +39,7 @@ struct GroupShared {
     uint4 buf[kGroups][kGroupBytes / 16];
     Guid16 cols[kGroups][G];                       // the row's first G replica columns
     uint16_t tok[kGroups][kGroupTok];
-    uint32_t mask[kGroups][16];                    // pass A: columns seen, 256 bits per vector
+    uint32_t mask[kGroups][2 * kMaskCols / 32];    // pass A: columns seen per vector (LDS: 7 workgroups per CU, not 6)
     uint32_t ntok[kGroups], kn[kGroups], nn[kGroups], flags[kGroups];
     uint32_t geo[kGroups], row[kGroups], nc[kGroups];  // alignment offset | length << 4; the row, its columns
 };
@@ -292,7 +293,7 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
         sh.row[grp] = rc.row;
         sh.nc[grp] = rc.nc;
     }
-    for (uint32_t i = g; i < 16; i += G) sh.mask[grp][i] = 0;
+    for (uint32_t i = g; i < 2 * kMaskCols / 32; i += G) sh.mask[grp][i] = 0;
     wave_sync();
     // phase 2: the "nVector" token
     const uint8_t* c = reinterpret_cast<const uint8_t*>(sh.buf[grp]) + a;
@@ -386,9 +387,11 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, sh.nc[gq], gp.eg[u], vv ? k - kn - 1 : k - 1);
             if (col == UINT32_MAX) {
                 atomicOr(&sh.flags[gq], (uint32_t)kMiss);
+            } else if (col >= kMaskCols) {
+                atomicOr(&sh.flags[gq], (uint32_t)kSlow);  // past the repeat mask: the serial parser decides
             } else {
                 const uint32_t bit = 1u << (col & 31);
-                if (atomicOr(&sh.mask[gq][vv * 8 + (col >> 5)], bit) & bit) atomicOr(&sh.flags[gq], (uint32_t)kDup);
+                if (atomicOr(&sh.mask[gq][vv * (kMaskCols / 32) + (col >> 5)], bit) & bit) atomicOr(&sh.flags[gq], (uint32_t)kDup);
                 const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
                 uint8_t* h = emit + mq * emit_stride(EB);
                 reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(col | vv << 15);

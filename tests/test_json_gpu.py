@@ -99,6 +99,48 @@ def test_random_waves_match_oracle(ctx, eb, R, pool, group, ws, monkeypatch):
     pr.close()
 
 
+@pytest.mark.parametrize("group", ["8", "16"])
+@pytest.mark.parametrize("eb", [4, 8])
+def test_columns_past_the_repeat_mask(ctx, eb, group, monkeypatch):
+    """Compact states naming columns >= 64 (kMaskCols): the group parse hands them to the serial parser,
+    which applies them, or rejects a repeated Guid in one vector (all or nothing)."""
+    monkeypatch.setenv("JANUS_JSON_GROUP", group)
+    rng = np.random.default_rng(640 + eb)
+    stable = random_guids(rng, 2)
+    reps = random_guids(rng, 90)
+    pr = Pair(ctx, 2, 128, eb, stable)
+    # wave 1: 90 new replicas on key 1, 10 per compact state (appended in commit order)
+    keys = np.ones(9, np.uint32)
+    msgs = [encode_pnc(reps[10 * i:10 * i + 10], [int(v) for v in rng.integers(0, 1000, 10)], [None] * 10) for i in range(9)]
+    assert pr.oracle(keys, msgs) == (None, 0)
+    pr.s.merge_json(keys, msgs)
+    pr.check()
+    # wave 2: states mixing columns below and past 64, in both vectors
+    msgs = []
+    for _ in range(200):
+        pick = sorted(int(x) for x in rng.choice(90, 12, replace=False))
+        g = [reps[i] for i in pick]
+        pv = [int(v) if rng.random() < 0.7 else None for v in rng.integers(0, 5000, 12)]
+        nv = [int(v) if rng.random() < 0.5 else None for v in rng.integers(0, 5000, 12)]
+        msgs.append(encode_pnc(g, pv, nv))
+    keys = np.ones(len(msgs), np.uint32)
+    assert pr.oracle(keys, msgs) == (None, 0)
+    pr.s.merge_json(keys, msgs)
+    pr.check()
+    # wave 3: a repeated Guid at a column past 64 rejects the wave; nothing is applied
+    dup = encode_pnc([reps[80], reps[3], reps[80]], [5, 6, 7], [None] * 3)
+    keys = np.ones(3, np.uint32)
+    wave = [msgs[0], dup, msgs[1]]
+    bad, rc = pr.oracle(keys, wave)
+    assert bad == 1
+    with pytest.raises(jg.JanusError) as e:
+        pr.s.merge_json(keys, wave)
+    assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 1
+    P, N = pr.s.read_rows()
+    assert np.array_equal(P, pr.P) and np.array_equal(N, pr.N), "a rejected wave changed the store"
+    pr.close()
+
+
 def _mutants(rng, cl, keys, n):
     """Near-compact payloads: one byte replaced, deleted or inserted, vectors swapped, a space added."""
     alpha = b'"{},:-0123456789abcdefABCDEF xnpV\\'
