@@ -95,6 +95,104 @@ __global__ __launch_bounds__(256) void k_grouped(long long* AP, long long* AN, c
     }
 }
 
+// pipelined head-only: the next iteration's keys and list heads are loaded while this iteration's rows
+// fold (the keys -> head -> rows chain otherwise leaves a wave with nothing in flight for two round trips)
+template <int U>
+__global__ __launch_bounds__(256) void k_grouped_pipe(long long* AP, long long* AN, const long long* BP, const long long* BN,
+                                                      const uint32_t* keys, const uint32_t* head, const uint32_t* next, uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t step = (((uint64_t)gridDim.x * 256) >> 6) * U;
+    const bool isP = lane < NV;
+    const uint32_t w = isP ? lane : lane - NV;
+    const long long* B = isP ? BP : BN;
+    long long* A = isP ? AP : AN;
+    uint64_t m0 = (((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6) * U;
+    uint64_t key[U];
+    bool lead[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        key[u] = m0 + u < n ? keys[m0 + u] : 0;
+        lead[u] = m0 + u < n && head[key[u]] == (uint32_t)(m0 + u);
+    }
+    for (; m0 < n; m0 += step) {
+        uint4 a[U], b[U];
+        uint32_t nx0[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lead[u]) {
+                b[u] = ntl(reinterpret_cast<const uint4*>(B + (m0 + u) * R) + w);
+                a[u] = *(reinterpret_cast<const uint4*>(A + key[u] * R) + w);
+                nx0[u] = next[m0 + u];
+            }
+        const uint64_t m1 = m0 + step;
+        uint64_t nkey[U];
+        bool nlead[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nkey[u] = m1 + u < n ? keys[m1 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) nlead[u] = m1 + u < n && head[nkey[u]] == (uint32_t)(m1 + u);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!lead[u]) continue;
+            a[u] = vmax8(a[u], b[u]);
+            for (uint32_t cur = nx0[u]; cur != kNil;) {
+                const uint4 bb = ntl(reinterpret_cast<const uint4*>(B + (uint64_t)cur * R) + w);
+                const uint32_t nx = next[cur];
+                a[u] = vmax8(a[u], bb);
+                cur = nx;
+            }
+            *(reinterpret_cast<uint4*>(A + key[u] * R) + w) = a[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { key[u] = nkey[u]; lead[u] = nlead[u]; }
+    }
+}
+
+// lead flags from a pass of their own (head[key] == m, then head reset), so the merge's chain is
+// (keys, flag) -> rows: one dependent round trip fewer per iteration
+__global__ void k_lead(const uint32_t* keys, uint64_t n, const uint32_t* head, uint8_t* lead) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        lead[i] = head[keys[i]] == (uint32_t)i;
+}
+template <int U>
+__global__ __launch_bounds__(256) void k_grouped_flag(long long* AP, long long* AN, const long long* BP, const long long* BN,
+                                                      const uint32_t* keys, const uint8_t* leadf, const uint32_t* next, uint64_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * 256) >> 6;
+    const bool isP = lane < NV;
+    const uint32_t w = isP ? lane : lane - NV;
+    const long long* B = isP ? BP : BN;
+    long long* A = isP ? AP : AN;
+    for (uint64_t m0 = (((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6) * U; m0 < n; m0 += nw * U) {
+        uint64_t key[U];
+        bool lead[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            key[u] = m0 + u < n ? keys[m0 + u] : 0;
+            lead[u] = m0 + u < n && leadf[m0 + u];
+        }
+        uint4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lead[u]) {
+                b[u] = ntl(reinterpret_cast<const uint4*>(B + (m0 + u) * R) + w);
+                a[u] = *(reinterpret_cast<const uint4*>(A + key[u] * R) + w);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!lead[u]) continue;
+            a[u] = vmax8(a[u], b[u]);
+            for (uint32_t cur = next[m0 + u]; cur != kNil;) {
+                const uint4 bb = ntl(reinterpret_cast<const uint4*>(B + (uint64_t)cur * R) + w);
+                const uint32_t nx = next[cur];
+                a[u] = vmax8(a[u], bb);
+                cur = nx;
+            }
+            *(reinterpret_cast<uint4*>(A + key[u] * R) + w) = a[u];
+        }
+    }
+}
+
 // sort-based: rows sorted by key (sk, sr); one wave per sorted position, U in flight; a segment head
 // folds its segment's rows (independent loads, no pointer chase)
 template <int U, bool NTS>
@@ -180,7 +278,11 @@ int main() {
 
     // kind: 0 head-only U4 (production), 1 head-only U8, 2 count+head U4, 3 sorted U4, 4 sorted U8, 5 sorted U4 nt-store
     struct Var { const char* name; int kind; };
-    const Var vars[] = {{"head-only U4", 0}, {"head-only U8", 1}, {"count+head U4", 2}, {"sorted U4", 3}, {"sorted U8", 4}, {"sorted U4 nt-store", 5}};
+    const Var vars[] = {{"head-only U4", 0}, {"head-only U8", 1}, {"count+head U4", 2}, {"sorted U4", 3}, {"sorted U8", 4}, {"sorted U4 nt-store", 5},
+                        {"pipelined U4", 6}, {"pipelined U2", 7}, {"lead-flag U4", 8}, {"head-only U4 32/CU", 9}};
+    constexpr int kVars = 10;
+    uint8_t* leadf;
+    CK(hipMalloc(&leadf, n));
     for (int dist = 0; dist < 2; ++dist) {
         std::vector<uint32_t> hk(n);
         std::mt19937_64 g(7 + dist);
@@ -193,8 +295,8 @@ int main() {
         }
         CK(hipMemcpy(keys, hk.data(), n * 4, hipMemcpyHostToDevice));
         std::printf("== keys %s\n", dist == 0 ? "uniform over 2M (39%% of rows repeat a key)" : "a permutation (every key once)");
-        std::vector<std::vector<float>> t(6);
-        std::vector<unsigned long long> chk(6);
+        std::vector<std::vector<float>> t(kVars);
+        std::vector<unsigned long long> chk(kVars);
         for (int round = 0; round < 7; ++round)
             for (const Var& v : vars) {
                 CK(hipMemcpy(AP, A0P, cells * 8, hipMemcpyDeviceToDevice));
@@ -210,6 +312,21 @@ int main() {
                     hipLaunchKernelGGL(k_link<true>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
                     hipLaunchKernelGGL((k_grouped<4, false, true>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
                     hipLaunchKernelGGL(k_reset<true>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                } else if (v.kind == 6 || v.kind == 7) {
+                    hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
+                    if (v.kind == 6) hipLaunchKernelGGL((k_grouped_pipe<4>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, head, next, n);
+                    else hipLaunchKernelGGL((k_grouped_pipe<2>), dim3(grid(2)), dim3(256), 0, 0, AP, AN, BP, BN, keys, head, next, n);
+                    hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                } else if (v.kind == 8) {
+                    hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
+                    hipLaunchKernelGGL(k_lead, dim3(gk), dim3(256), 0, 0, keys, n, head, leadf);
+                    hipLaunchKernelGGL((k_grouped_flag<4>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, leadf, next, n);
+                    hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                } else if (v.kind == 9) {
+                    hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
+                    const unsigned g9 = (unsigned)std::min<uint64_t>((n + 3) / 4 * 64 / 256, (uint64_t)num_cus * 32);
+                    hipLaunchKernelGGL((k_grouped<4, false, false>), dim3(g9), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
+                    hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
                 } else {
                     CK(hipcub::DeviceRadixSort::SortPairs(dtemp, temp, keys, sk, rows, sr, (int)n, 0, 21));
                     if (v.kind == 3) hipLaunchKernelGGL((k_sorted<4, false>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, sk, sr, n);
