@@ -279,8 +279,9 @@ int main() {
     // kind: 0 head-only U4 (production), 1 head-only U8, 2 count+head U4, 3 sorted U4, 4 sorted U8, 5 sorted U4 nt-store
     struct Var { const char* name; int kind; };
     const Var vars[] = {{"head-only U4", 0}, {"head-only U8", 1}, {"count+head U4", 2}, {"sorted U4", 3}, {"sorted U8", 4}, {"sorted U4 nt-store", 5},
-                        {"pipelined U4", 6}, {"pipelined U2", 7}, {"lead-flag U4", 8}, {"head-only U4 32/CU", 9}};
-    constexpr int kVars = 10;
+                        {"pipelined U4", 6}, {"pipelined U2", 7}, {"lead-flag U4", 8}, {"head-only U4 32/CU", 9},
+                        {"head-only U4 nt-store", 10}, {"head-only U2 nt-store", 11}};
+    constexpr int kVars = 12;
     uint8_t* leadf;
     CK(hipMalloc(&leadf, n));
     for (int dist = 0; dist < 2; ++dist) {
@@ -321,6 +322,11 @@ int main() {
                     hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
                     hipLaunchKernelGGL(k_lead, dim3(gk), dim3(256), 0, 0, keys, n, head, leadf);
                     hipLaunchKernelGGL((k_grouped_flag<4>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, leadf, next, n);
+                    hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                } else if (v.kind == 10 || v.kind == 11) {
+                    hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
+                    if (v.kind == 10) hipLaunchKernelGGL((k_grouped<4, true, false>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
+                    else hipLaunchKernelGGL((k_grouped<2, true, false>), dim3(grid(2)), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
                     hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
                 } else if (v.kind == 9) {
                     hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);

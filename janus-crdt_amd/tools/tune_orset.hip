@@ -119,7 +119,7 @@ void bench(const char* title, Stream& a, Stream& b, Stream& o, hipStream_t s, co
     std::vector<std::vector<Times>> t(vs.size());
     for (int r = 0; r < rounds; ++r)
         for (size_t k = 0; k < vs.size(); ++k) t[k].push_back(vs[k].fn(a, b, o, s));
-    const double bytes = (double)(a.n + b.n + rc) * 24;
+    const double bytes = (double)(a.n + b.n + rc) * 28;  // key 8 + tag 16 + ord 4
     for (size_t k = 0; k < vs.size(); ++k) {
         auto med = [&](float Times::*f) { std::vector<float> x; for (auto& y : t[k]) x.push_back(y.*f); std::sort(x.begin(), x.end()); return x[x.size() / 2]; };
         const double p = med(&Times::part), u = med(&Times::uni), f = med(&Times::fin);
