@@ -338,6 +338,16 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
         w.close()
     alg = data.size + 12 * JSON_MSGS + 2 * JSON_EB * entries
     kern = ev / steps
+    # the parse is instruction-bound, not HBM-bound: VALU wave instructions per wave (PMC SQ_INSTS_VALU of
+    # k_scan + k_apply_emit, profiles/pmc_*.json) against the chip's issue rate (one wave instruction per
+    # SIMD every 2 cycles: 256 CUs x 4 SIMDs x 0.5 x 2.4 GHz)
+    sv, av = load_traffic("json_scan_valu"), load_traffic("json_apply_emit_valu")
+    valu = None
+    if sv and av:
+        insts, peak = sv[0] + av[0], VALU_LANE_OPS / 64
+        valu = {"bound": "valu", "achieved": insts / kern / 1e12, "peak": peak / 1e12, "unit": "T wave-instructions/s",
+                "frac": insts / kern / peak, "valu_insts_per_wave": insts, "source": sv[1],
+                "scope": "k_scan + k_apply_emit VALU instructions over the jg_pnc_merge_wave event time"}
     return {"workload": f"PNCounterMsg wave from wire bytes (C5 shape: {JSON_MSGS} states of {JSON_KEYS} accounts, "
                         f"{JSON_R - 1}-node replicas, int32), resident in HBM, steady state (replicas known)",
             "msgs_per_s": JSON_MSGS / (wall / steps), "ms_per_wave": wall / steps * 1e3, "event_ms": kern * 1e3,
@@ -345,7 +355,8 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
             "cold_wave_ms": min(cold_ms), "json_group": int(os.environ.get("JANUS_JSON_GROUP", "8")),
             "roofline": {"bound": "hbm", "achieved": alg / kern / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / kern / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_wave": alg,
-                         "scope": "jg_pnc_merge_wave (k_scan + k_apply, status reads) per step"}}
+                         "scope": "jg_pnc_merge_wave (k_scan + k_apply, status reads) per step"},
+            "roofline_valu": valu}
 
 
 def bench_apply_loop(sync, rank, world, local):
