@@ -130,6 +130,60 @@ int main(int argc, char** argv) {
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         return std::make_pair(s, claimed.load());
     };
+    // classify (uid + claim, pf 8) then gather into one staging buffer (the product's two passes), vs one
+    // pass that classifies and copies each payload into a per-worker buffer, then a streaming copy of the
+    // per-worker buffers into the staging buffer at their prefix offsets
+    std::vector<char> stage(400u << 20);
+    std::vector<std::vector<char>> priv(T, std::vector<char>(64u << 20));
+    auto gather = [&](bool fused) {
+        fill_tracker();
+        std::vector<size_t> bytes(T + 1, 0);
+        const auto t0 = std::chrono::steady_clock::now();
+        auto pass1 = [&](int t) {
+            const size_t b = n * t / T, e = n * (t + 1) / T;
+            size_t o = 0;
+            for (size_t i = b; i < e; ++i) {
+                if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
+                if (i + 8 < e) {
+                    __builtin_prefetch(&ut[ghash(msgs[i + 8]->uid) & (us - 1)]);
+                    __builtin_prefetch(&tt[sslot(msgs[i + 8]->seq) & (ts - 1)], 1);
+                    if (fused) __builtin_prefetch(msgs[i + 8]->message.data());
+                }
+                const NP& m = *msgs[i];
+                const USlot* sl = find(m.uid);
+                cls[i] = sl ? sl->idx : ~0u;
+                uint64_t og;
+                claim(m.seq, &og);
+                if (fused) { std::memcpy(priv[t].data() + o, m.message.data(), m.message.size()); }
+                o += m.message.size();
+            }
+            bytes[t + 1] = o;
+        };
+        auto pass2 = [&](int t) {
+            size_t at = 0;
+            for (int u = 0; u < t; ++u) at += bytes[u + 1];
+            if (fused) { std::memcpy(stage.data() + at, priv[t].data(), bytes[t + 1]); return; }
+            const size_t b = n * t / T, e = n * (t + 1) / T;
+            for (size_t i = b; i < e; ++i) {
+                if (i + 8 < e) __builtin_prefetch(msgs[i + 8]->message.data());
+                const std::string& p = msgs[i]->message;
+                std::memcpy(stage.data() + at, p.data(), p.size());
+                at += p.size();
+            }
+        };
+        double t1s = 0;
+        for (int ph = 0; ph < 2; ++ph) {
+            std::vector<std::thread> th;
+            for (int t = 0; t < T; ++t) th.emplace_back([&, t, ph] { ph == 0 ? pass1(t) : pass2(t); });
+            for (auto& x : th) x.join();
+            if (ph == 0) t1s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("%-30s %7.2f ms (pass 1 %.2f, pass 2 %.2f)\n", fused ? "fused classify+gather" : "classify, then gather", s * 1e3, t1s * 1e3,
+                    (s - t1s) * 1e3);
+    };
+    for (int rep = 0; rep < 3; ++rep) { gather(false); gather(true); }
+    if (argc > 3) return 0;
     struct V { const char* name; int mode; size_t pf; bool relaxed; };
     const V vs[] = {{"read NP only", 0, 8, false},        {"uid, no prefetch", 1, 8, false},    {"uid, pf 8", 5, 8, false},
                     {"uid+claim, no prefetch", 3, 8, false}, {"uid+claim, pf 8 (product)", 7, 8, false},
