@@ -1,6 +1,9 @@
 // janus_host.cpp — see janus_host.hpp.
 #include "janus_host.hpp"
 
+#include <emmintrin.h>
+#include <sys/mman.h>
+
 #include <cstdio>
 #include <cstring>
 
@@ -44,6 +47,19 @@ GpuStableStore::~GpuStableStore() {
     if (ctx_) jg_close(ctx_);
 }
 
+void* table_alloc(size_t bytes) {
+    if (bytes < TableAlloc<char>::kHuge) return ::operator new(bytes, std::align_val_t(64));
+    const size_t b = (bytes + TableAlloc<char>::kHuge - 1) & ~(TableAlloc<char>::kHuge - 1);
+    void* p = std::aligned_alloc(TableAlloc<char>::kHuge, b);
+    if (!p) throw std::bad_alloc();
+    (void)madvise(p, b, MADV_HUGEPAGE);  // advisory: without THP support the table works the same
+    return p;
+}
+void table_free(void* p, size_t bytes) {
+    if (bytes < TableAlloc<char>::kHuge) ::operator delete(p, std::align_val_t(64));
+    else std::free(p);
+}
+
 const GpuStableStore::KeyRef* GpuStableStore::UidTable::find(const Guid& g) const {
     if (slots_.empty()) return nullptr;
     const size_t mask = slots_.size() - 1;
@@ -65,7 +81,7 @@ bool GpuStableStore::UidTable::insert(const Guid& g, KeyRef v) {
 }
 
 void GpuStableStore::UidTable::grow() {
-    std::vector<Slot> old = std::move(slots_);
+    std::vector<Slot, TableAlloc<Slot>> old = std::move(slots_);
     slots_.assign(old.empty() ? 1024 : old.size() * 2, Slot{});
     n_ = 0;
     for (const Slot& s : old)
@@ -186,6 +202,51 @@ class WorkerPool {
 };
 
 namespace {
+// One worker's contiguous output range in a pinned staging buffer, written with non-temporal stores in
+// whole 64-B lines: the staging is read once by the H2D copy engine, so a line written through the cache
+// costs a read for ownership first.  Bytes are collected into `line` until it is full; a payload part
+// that starts on an empty, aligned line streams straight from the source.  The range's first and last
+// partial lines (shared with the neighbouring workers' ranges) are written with ordinary stores.
+class LineStream {
+  public:
+    LineStream(char* base, size_t pos) : base_(base), pos_(pos) {}
+    void put(const char* src, size_t n) {
+        if (head_) {  // up to the range's first line boundary: ordinary stores
+            const size_t c = std::min(n, (64 - (pos_ & 63)) & 63);
+            std::memcpy(base_ + pos_, src, c);
+            pos_ += c, src += c, n -= c;
+            if ((pos_ & 63) == 0) head_ = false;
+            if (head_ || n == 0) return;
+        }
+        if (fill_) {
+            const size_t c = std::min(n, 64 - fill_);
+            std::memcpy(line_ + fill_, src, c);
+            fill_ += c, pos_ += c, src += c, n -= c;
+            if (fill_ < 64) return;
+            stream(base_ + pos_ - 64, line_);
+            fill_ = 0;
+        }
+        for (; n >= 64; pos_ += 64, src += 64, n -= 64) stream(base_ + pos_, src);
+        std::memcpy(line_, src, n);
+        fill_ = n, pos_ += n;
+    }
+    void finish() {  // the range's last partial line, then order the streamed lines before the join
+        if (fill_) std::memcpy(base_ + pos_ - fill_, line_, fill_);
+        _mm_sfence();
+    }
+
+  private:
+    static void stream(char* dst, const char* src) {
+        for (int k = 0; k < 4; ++k)
+            _mm_stream_si128(reinterpret_cast<__m128i*>(dst) + k, _mm_loadu_si128(reinterpret_cast<const __m128i*>(src) + k));
+    }
+    char* base_;
+    size_t pos_;
+    bool head_ = true;
+    size_t fill_ = 0;
+    alignas(64) char line_[64];
+};
+
 // Static contiguous split of [0, n) over the pool's workers: fn(begin, end, worker).  Worker t's
 // range precedes worker t+1's, so per-worker results concatenated in worker order keep message order.
 template <class F> void parallel_ranges(WorkerPool& pool, size_t n, F&& fn) {
@@ -371,7 +432,7 @@ void SafeUpdateTracker::grow() {  // rehash the live entries (tombstones dropped
     std::vector<std::pair<uint64_t, uint64_t>> live = items();
     size_t cap = 1024;
     while (cap < 4 * (live.size() + 1)) cap <<= 1;
-    std::vector<Slot> fresh(cap);
+    std::vector<Slot, TableAlloc<Slot>> fresh(cap);
     slots_.swap(fresh);
     used_ = 0;
     n_.store(0, std::memory_order_relaxed);
@@ -513,7 +574,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         }
         const double tb = wall_s();
         t_classify += tb - ta;
-        Chunk ch[2];
+        Chunk ch[2] = {};
         size_t w0[2];
         for (int kind = 0; kind < 2; ++kind) {
             if (m[kind] == 0) continue;
@@ -528,19 +589,22 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
             size_t j[2] = {mbase[t], mbase[(T + 1) + t]};
             uint64_t o[2] = {bbase[t], bbase[(T + 1) + t]};
+            LineStream out[2] = {LineStream(reinterpret_cast<char*>(ch[0].bytes), o[0]), LineStream(reinterpret_cast<char*>(ch[1].bytes), o[1])};
             for (size_t i = c0 + b; i < c0 + e; ++i) {
                 if (i + 8 < c0 + e) __builtin_prefetch(msgs[i + 8]->message.data());
                 if (cls[i] == kSkip) continue;
                 const int kind = cls[i] == kSet ? 1 : 0;
                 const std::string& p = msgs[i]->message;
                 Chunk& k = ch[kind];
-                std::memcpy(k.bytes + o[kind], p.data(), p.size());
+                out[kind].put(p.data(), p.size());
                 k.off[j[kind]] = o[kind];
                 k.rows[j[kind]] = kind ? sid[i] : cls[i];
                 where_[kind][w0[kind] + j[kind]] = i;
                 o[kind] += p.size();
                 ++j[kind];
             }
+            out[0].finish();
+            out[1].finish();
         });
         t_gather += wall_s() - tb;
         const double tq = wall_s();

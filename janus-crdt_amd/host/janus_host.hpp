@@ -76,6 +76,24 @@ struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
 // message in msgs[first..] in ONE device call (jg_update_digests).
 void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first = 0);
 
+// Storage of the apply loop's random-access tables (uid table, safe-update tracker: one random line per
+// message each): 2 MiB-aligned and marked for transparent huge pages once at least 2 MiB, so a lookup's
+// line does not also miss the TLB (a 1M-key uid table spans 64 MB).
+template <class T> struct TableAlloc {
+    using value_type = T;
+    static constexpr size_t kHuge = size_t(2) << 20;
+    TableAlloc() = default;
+    template <class U> TableAlloc(const TableAlloc<U>&) {}
+    T* allocate(size_t n);
+    void deallocate(T* p, size_t n);
+    template <class U> bool operator==(const TableAlloc<U>&) const { return true; }
+    template <class U> bool operator!=(const TableAlloc<U>&) const { return false; }
+};
+void* table_alloc(size_t bytes);
+void table_free(void* p, size_t bytes);
+template <class T> T* TableAlloc<T>::allocate(size_t n) { return static_cast<T*>(table_alloc(n * sizeof(T))); }
+template <class T> void TableAlloc<T>::deallocate(T* p, size_t n) { table_free(p, n * sizeof(T)); }
+
 // SafeCRDTManager.safeUpdateTracker (SafeCRDTManager.cs:33, a ConcurrentDictionary<NetworkProtocol,
 // (Connection, uint)>): message identity (NetworkProtocol.seq, >= 1) -> client origin.  TryAdd / ContainsKey
 // from one thread (the batcher); TryRemove (take) from many threads at once — the apply loop removes a
@@ -120,7 +138,7 @@ class SafeUpdateTracker {
         return (size_t)x;
     }
     void grow();
-    std::vector<Slot> slots_;
+    std::vector<Slot, TableAlloc<Slot>> slots_;
     std::atomic<size_t> n_{0};
     size_t used_ = 0;  // live + tombstones
 };
@@ -262,7 +280,7 @@ class GpuStableStore {
             uint8_t used = 0;
         };
         void grow();
-        std::vector<Slot> slots_;
+        std::vector<Slot, TableAlloc<Slot>> slots_;
         size_t n_ = 0;
     };
     struct SetKey {
