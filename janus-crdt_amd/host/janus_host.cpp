@@ -591,7 +591,10 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             uint64_t o[2] = {bbase[t], bbase[(T + 1) + t]};
             LineStream out[2] = {LineStream(reinterpret_cast<char*>(ch[0].bytes), o[0]), LineStream(reinterpret_cast<char*>(ch[1].bytes), o[1])};
             for (size_t i = c0 + b; i < c0 + e; ++i) {
-                if (i + 8 < c0 + e) __builtin_prefetch(msgs[i + 8]->message.data());
+                if (i + 8 < c0 + e) {  // every line of the payload 8 messages ahead (one prefetch left the rest to miss)
+                    const std::string& q = msgs[i + 8]->message;
+                    for (size_t x = 0; x < q.size(); x += 64) __builtin_prefetch(q.data() + x);
+                }
                 if (cls[i] == kSkip) continue;
                 const int kind = cls[i] == kSet ? 1 : 0;
                 const std::string& p = msgs[i]->message;
