@@ -451,10 +451,14 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
     for (size_t b = 0; b < blocks_.size(); ++b) block_off_[b + 1] = block_off_[b] + blocks_[b]->update.size();
     std::vector<const NetworkProtocol*>& msgs = msgs_;
     msgs.resize(block_off_.back());
-    parallel_ranges(pool(), blocks_.size(), [&](size_t b0, size_t b1, int) {
-        for (size_t b = b0; b < b1; ++b) {
-            const NetworkProtocol* u = blocks_[b]->update.data();
-            for (size_t i = block_off_[b], e = block_off_[b + 1]; i < e; ++i) msgs[i] = u++;
+    // split by messages, not blocks (a wave is ~1000 blocks of ~1000 messages: split by block count it
+    // ran on one thread, 0.8 ms per 1M-message wave)
+    parallel_ranges(pool(), msgs.size(), [&](size_t i0, size_t i1, int) {
+        if (i0 >= i1) return;
+        size_t b = (size_t)(std::upper_bound(block_off_.begin(), block_off_.end(), i0) - block_off_.begin()) - 1;
+        for (size_t i = i0; i < i1; ++b) {
+            const NetworkProtocol* u = blocks_[b]->update.data() + (i - block_off_[b]);
+            for (const size_t e = std::min(i1, block_off_[b + 1]); i < e; ++i) msgs[i] = u++;
         }
     });
     return apply_msgs(msgs, tracker, t0);
@@ -512,14 +516,18 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     size_t nw[2] = {0, 0};
     for (auto& w : where_)
         if (w.size() < n) w.resize(n);
-    std::vector<size_t> cnt(2 * T), nbytes(2 * T), mbase(2 * (T + 1)), bbase(2 * (T + 1));
     const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
+    // Work inside a chunk is dealt in tasks of kTask messages from a shared counter (a static split made
+    // every phase wait for the slowest of 16 workers on a shared host); per-task counts keep commit order.
+    constexpr size_t kTask = 2048;
+    const size_t max_tasks = (chunk_msgs + kTask - 1) / kTask;
+    std::vector<size_t> tcnt(2 * max_tasks), tbytes(2 * max_tasks), tmbase(2 * (max_tasks + 1)), tbbase(2 * (max_tasks + 1));
     bool open[2] = {false, false};
     // The safe-update completions (safeUpdateTracker.TryRemove + notify, :141-142) are claimed in the
-    // classify pass, which already has each message in cache: (message, origin) per (chunk, worker),
-    // so concatenating the lists in that order keeps commit order; claims at or past the cut go back.
+    // classify pass, which already has each message in cache: (message, origin) per (chunk, task), so
+    // concatenating the lists in that order keeps commit order; claims at or past the cut go back.
     const bool sweep = tracker && tracker->size();
-    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> part(sweep ? n_chunks * T : 0);
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> part(sweep ? n_chunks * max_tasks : 0);
     struct GiveBack {  // any throw before the cut is known: nothing of the wave counts as applied
         const std::vector<std::vector<std::pair<uint64_t, uint64_t>>>& part;
         const NetworkProtocol* const* msgs;
@@ -531,46 +539,96 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                     for (const auto& [i, o] : p) tracker->add(msgs[i]->seq, o);
         }
     } give_back{part, msgs.data(), tracker};
+    // Chunk c's engine append runs on the caller (worker 0) at the start of chunk c+1's classify, while
+    // the other workers already classify; its error is rethrown once the phase has joined.
+    Chunk pend[2] = {};
+    size_t pend_m[2] = {0, 0}, pend_nb[2] = {0, 0};
+    int append_rc = JG_OK;
+    std::string append_why;
+    auto append = [&] {
+        for (int kind = 0; kind < 2 && append_rc == JG_OK; ++kind) {
+            if (pend_m[kind] == 0) continue;
+            pend[kind].off[pend_m[kind]] = pend_nb[kind];
+            int rc = JG_OK;
+            if (!open[kind]) {
+                const uint64_t cap_m = std::max<size_t>(pend_m[kind] * n_chunks, 1), cap_b = std::max<size_t>(pend_nb[kind] * n_chunks, 1);
+                rc = kind ? jg_orset_wave_begin(orset_, cap_m, cap_b) : jg_pnc_wave_begin(pnc_, cap_m, cap_b);
+                if (rc == JG_OK) open[kind] = true;
+            }
+            if (rc == JG_OK)
+                rc = kind ? jg_orset_wave_append(orset_, pend_m[kind], pend[kind].rows, pend[kind].off, pend[kind].bytes)
+                          : jg_pnc_wave_append(pnc_, pend_m[kind], pend[kind].rows, pend[kind].off, pend[kind].bytes);
+            if (rc != JG_OK) {
+                append_rc = rc;
+                append_why = last_error();
+                break;
+            }
+            chunks[kind].push_back(pend[kind]);
+        }
+        pend_m[0] = pend_m[1] = 0;
+    };
+    auto append_failed = [&] {
+        if (append_rc == JG_OK) return;
+        if (open[0]) jg_pnc_wave_abort(pnc_);
+        if (open[1]) jg_orset_wave_abort(orset_);
+        throw EngineError(append_rc, append_why);
+    };
+    static const size_t min_par = [] {  // below this many messages a chunk runs on the caller alone
+        const char* e = std::getenv("JANUS_HOST_PAR_MIN");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{8192};
+    }();
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
         const size_t c0 = c * chunk_msgs, c1 = std::min(n, c0 + chunk_msgs);
+        const size_t ntask = (c1 - c0 + kTask - 1) / kTask;
+        const bool par = T > 1 && c1 - c0 >= min_par;
+        auto run = [&](const std::function<void(int)>& fn) {
+            if (par) wp.run(fn);
+            else fn(0);
+        };
         const double ta = wall_s();
-        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
-            size_t k[2] = {0, 0}, bytes[2] = {0, 0};
-            for (size_t i = c0 + b; i < c0 + e; ++i) {
-                if (i + 16 < c0 + e) __builtin_prefetch(msgs[i + 16]);
-                if (i + 8 < c0 + e) {
-                    uids_.prefetch(msgs[i + 8]->uid);
-                    if (sweep) tracker->prefetch_claim(msgs[i + 8]->seq);
-                }
-                const NetworkProtocol& u = *msgs[i];
-                uint32_t cl = kSkip;
-                if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
-                    if (const KeyRef* kr = uids_.find(u.uid)) {                                  // :136
-                        const int kind = kr->type == CrdtType::PNCounter ? 0 : 1;
-                        if (kind == 0) cl = kr->idx;
-                        else { cl = kSet; sid[i] = kr->idx; }
-                        ++k[kind];
-                        bytes[kind] += u.message.size();
+        std::atomic<size_t> next{0};
+        run([&](int t) {
+            if (t == 0) append();  // the previous chunk's upload + pass A, queued
+            for (size_t q; (q = next.fetch_add(1, std::memory_order_relaxed)) < ntask;) {
+                const size_t e = std::min(c1, c0 + (q + 1) * kTask);
+                size_t k[2] = {0, 0}, bytes[2] = {0, 0};
+                for (size_t i = c0 + q * kTask; i < e; ++i) {
+                    if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
+                    if (i + 8 < e) {
+                        uids_.prefetch(msgs[i + 8]->uid);
+                        if (sweep) tracker->prefetch_claim(msgs[i + 8]->seq);
                     }
+                    const NetworkProtocol& u = *msgs[i];
+                    uint32_t cl = kSkip;
+                    if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
+                        if (const KeyRef* kr = uids_.find(u.uid)) {                                  // :136
+                            const int kind = kr->type == CrdtType::PNCounter ? 0 : 1;
+                            if (kind == 0) cl = kr->idx;
+                            else { cl = kSet; sid[i] = kr->idx; }
+                            ++k[kind];
+                            bytes[kind] += u.message.size();
+                        }
+                    }
+                    cls[i] = cl;
+                    uint64_t o;
+                    if (sweep && cl != kSkip && tracker->claim(u.seq, &o)) part[c * max_tasks + q].emplace_back(i, o);
                 }
-                cls[i] = cl;
-                uint64_t o;
-                if (sweep && cl != kSkip && tracker->claim(u.seq, &o)) part[c * T + t].emplace_back(i, o);
-            }
-            for (int kind = 0; kind < 2; ++kind) {
-                cnt[kind * T + t] = k[kind];
-                nbytes[kind * T + t] = bytes[kind];
+                for (int kind = 0; kind < 2; ++kind) {
+                    tcnt[kind * max_tasks + q] = k[kind];
+                    tbytes[kind * max_tasks + q] = bytes[kind];
+                }
             }
         });
+        append_failed();
         size_t m[2], nb[2];
         for (int kind = 0; kind < 2; ++kind) {
-            size_t* mb = &mbase[kind * (T + 1)];
-            size_t* bb = &bbase[kind * (T + 1)];
+            size_t* mb = &tmbase[kind * (max_tasks + 1)];
+            size_t* bb = &tbbase[kind * (max_tasks + 1)];
             mb[0] = bb[0] = 0;
-            for (int t = 0; t < T; ++t) { mb[t + 1] = mb[t] + cnt[kind * T + t]; bb[t + 1] = bb[t] + nbytes[kind * T + t]; }
-            m[kind] = mb[T];
-            nb[kind] = bb[T];
+            for (size_t q = 0; q < ntask; ++q) { mb[q + 1] = mb[q] + tcnt[kind * max_tasks + q]; bb[q + 1] = bb[q] + tbytes[kind * max_tasks + q]; }
+            m[kind] = mb[ntask];
+            nb[kind] = bb[ntask];
         }
         const double tb = wall_s();
         t_classify += tb - ta;
@@ -586,53 +644,45 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             nw[kind] += m[kind];
         }
         const double tg = wall_s();
-        parallel_ranges(wp, c1 - c0, [&](size_t b, size_t e, int t) {
-            size_t j[2] = {mbase[t], mbase[(T + 1) + t]};
-            uint64_t o[2] = {bbase[t], bbase[(T + 1) + t]};
-            LineStream out[2] = {LineStream(reinterpret_cast<char*>(ch[0].bytes), o[0]), LineStream(reinterpret_cast<char*>(ch[1].bytes), o[1])};
-            for (size_t i = c0 + b; i < c0 + e; ++i) {
-                if (i + 8 < c0 + e) {  // every line of the payload 8 messages ahead (one prefetch left the rest to miss)
-                    const std::string& q = msgs[i + 8]->message;
-                    for (size_t x = 0; x < q.size(); x += 64) __builtin_prefetch(q.data() + x);
+        next.store(0, std::memory_order_relaxed);
+        run([&](int) {
+            for (size_t q; (q = next.fetch_add(1, std::memory_order_relaxed)) < ntask;) {
+                const size_t e = std::min(c1, c0 + (q + 1) * kTask);
+                size_t j[2] = {tmbase[q], tmbase[(max_tasks + 1) + q]};
+                uint64_t o[2] = {tbbase[q], tbbase[(max_tasks + 1) + q]};
+                LineStream out[2] = {LineStream(reinterpret_cast<char*>(ch[0].bytes), o[0]), LineStream(reinterpret_cast<char*>(ch[1].bytes), o[1])};
+                for (size_t i = c0 + q * kTask; i < e; ++i) {
+                    if (i + 8 < e) {  // every line of the payload 8 messages ahead (one prefetch left the rest to miss)
+                        const std::string& pq = msgs[i + 8]->message;
+                        for (size_t x = 0; x < pq.size(); x += 64) __builtin_prefetch(pq.data() + x);
+                    }
+                    if (cls[i] == kSkip) continue;
+                    const int kind = cls[i] == kSet ? 1 : 0;
+                    const std::string& p = msgs[i]->message;
+                    Chunk& k = ch[kind];
+                    out[kind].put(p.data(), p.size());
+                    k.off[j[kind]] = o[kind];
+                    k.rows[j[kind]] = kind ? sid[i] : cls[i];
+                    where_[kind][w0[kind] + j[kind]] = i;
+                    o[kind] += p.size();
+                    ++j[kind];
                 }
-                if (cls[i] == kSkip) continue;
-                const int kind = cls[i] == kSet ? 1 : 0;
-                const std::string& p = msgs[i]->message;
-                Chunk& k = ch[kind];
-                out[kind].put(p.data(), p.size());
-                k.off[j[kind]] = o[kind];
-                k.rows[j[kind]] = kind ? sid[i] : cls[i];
-                where_[kind][w0[kind] + j[kind]] = i;
-                o[kind] += p.size();
-                ++j[kind];
+                out[0].finish();
+                out[1].finish();
             }
-            out[0].finish();
-            out[1].finish();
         });
-        t_gather += wall_s() - tb;
-        const double tq = wall_s();
+        t_gather += wall_s() - tg;
         for (int kind = 0; kind < 2; ++kind) {
-            if (m[kind] == 0) continue;
-            ch[kind].off[m[kind]] = nb[kind];
-            if (!open[kind]) {
-                const uint64_t cap_m = std::max<size_t>(m[kind] * n_chunks, 1), cap_b = std::max<size_t>(nb[kind] * n_chunks, 1);
-                check(kind ? jg_orset_wave_begin(orset_, cap_m, cap_b) : jg_pnc_wave_begin(pnc_, cap_m, cap_b));
-                open[kind] = true;
-            }
-            const int rc = kind ? jg_orset_wave_append(orset_, m[kind], ch[kind].rows, ch[kind].off, ch[kind].bytes)
-                                : jg_pnc_wave_append(pnc_, m[kind], ch[kind].rows, ch[kind].off, ch[kind].bytes);
-            if (rc != JG_OK) {
-                const std::string why = last_error();
-                if (open[0]) jg_pnc_wave_abort(pnc_);
-                if (open[1]) jg_orset_wave_abort(orset_);
-                throw EngineError(rc, why);
-            }
-            chunks[kind].push_back(ch[kind]);
+            pend[kind] = ch[kind];
+            pend_m[kind] = m[kind];
+            pend_nb[kind] = nb[kind];
         }
         if (std::getenv("JANUS_TRACE_WAVE"))
-            std::fprintf(stderr, "chunk %zu: classify %.2f ms, buffers %.2f ms, gather %.2f ms, append %.2f ms (%zu + %zu msgs, %zu + %zu bytes)\n",
-                         c, 1e3 * (tb - ta), 1e3 * (tg - tb), 1e3 * (tq - tg), 1e3 * (wall_s() - tq), m[0], m[1], nb[0], nb[1]);
+            std::fprintf(stderr, "chunk %zu: classify (+ previous append) %.2f ms, buffers %.2f ms, gather %.2f ms (%zu + %zu msgs, %zu + %zu bytes)\n", c,
+                         1e3 * (tb - ta), 1e3 * (tg - tb), 1e3 * (wall_s() - tg), m[0], m[1], nb[0], nb[1]);
     }
+    append();  // the last chunk
+    append_failed();
     phase_s_[1] = t_classify;
     phase_s_[2] = t_classify + t_gather;
     {
