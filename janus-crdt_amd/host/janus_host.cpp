@@ -516,7 +516,14 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     size_t nw[2] = {0, 0};
     for (auto& w : where_)
         if (w.size() < n) w.resize(n);
-    const size_t n_chunks = (n + chunk_msgs - 1) / chunk_msgs;
+    // Chunk boundaries: full chunks, then the remainder, whose last kTail messages form a chunk of their
+    // own — the last chunk's upload and pass A are the part of the engine that no host work overlaps.
+    constexpr size_t kTail = 16384;
+    std::vector<size_t> cb{0};
+    for (size_t c0 = chunk_msgs; c0 < n; c0 += chunk_msgs) cb.push_back(c0);
+    if (n > cb.back() + 2 * kTail) cb.push_back(n - kTail);
+    if (n > 0) cb.push_back(n);
+    const size_t n_chunks = cb.size() - 1;
     // Work inside a chunk is dealt in tasks of kTask messages from a shared counter (a static split made
     // every phase wait for the slowest of 16 workers on a shared host); per-task counts keep commit order.
     constexpr size_t kTask = 2048;
@@ -579,7 +586,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     }();
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
-        const size_t c0 = c * chunk_msgs, c1 = std::min(n, c0 + chunk_msgs);
+        const size_t c0 = cb[c], c1 = cb[c + 1];
         const size_t ntask = (c1 - c0 + kTask - 1) / kTask;
         const bool par = T > 1 && c1 - c0 >= min_par;
         auto run = [&](const std::function<void(int)>& fn) {
