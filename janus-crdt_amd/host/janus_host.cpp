@@ -516,12 +516,12 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     size_t nw[2] = {0, 0};
     for (auto& w : where_)
         if (w.size() < n) w.resize(n);
-    // Chunk boundaries: full chunks, then the remainder, whose last kTail messages form a chunk of their
+    // Chunk boundaries: full chunks, then the remainder, whose last `tail` messages form a chunk of their
     // own — the last chunk's upload and pass A are the part of the engine that no host work overlaps.
-    constexpr size_t kTail = 16384;
+    const size_t tail = std::max<size_t>(1, std::min<size_t>(16384, chunk_msgs / 8));
     std::vector<size_t> cb{0};
     for (size_t c0 = chunk_msgs; c0 < n; c0 += chunk_msgs) cb.push_back(c0);
-    if (n > cb.back() + 2 * kTail) cb.push_back(n - kTail);
+    if (n > cb.back() + 2 * tail) cb.push_back(n - tail);
     if (n > 0) cb.push_back(n);
     const size_t n_chunks = cb.size() - 1;
     // Work inside a chunk is dealt in tasks of kTask messages from a shared counter (a static split made
@@ -796,7 +796,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
             for (size_t k; (k = next.fetch_add(1, std::memory_order_relaxed)) < whole;)
                 for (size_t x = 0; x < part[k].size(); ++x) completed[at[k] + x] = part[k][x].second;
         };
-        if (T > 1 && at[whole] >= 65536) wp.run(copy);
+        if (T > 1 && at[whole] >= 8 * min_par) wp.run(copy);
         else copy(0);
         size_t kept = at[whole];
         for (size_t k = whole; k < np; ++k)

@@ -21,6 +21,22 @@ def test_committed_waves_match_oracle():
         assert check in out.stdout
 
 
+def test_committed_waves_match_oracle_chunked():
+    """The same 4-node parity run with waves cut into 5-message chunks and every phase on the worker
+    pool (JANUS_WAVE_CHUNK / JANUS_HOST_PAR_MIN): many chunks per wave, the dealt classify / gather tasks,
+    chunk appends overlapped with the next chunk's classify, the split-off tail chunk, the parallel
+    completion list, and the rejected-payload cut landing inside a multi-chunk wave."""
+    import os
+    env = dict(os.environ, JANUS_WAVE_CHUNK="5", JANUS_HOST_PAR_MIN="1")
+    out = subprocess.run([str(BIN)], capture_output=True, text=True, timeout=110, env=env)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "FAIL" not in out.stdout
+    assert out.stdout.count("PASS case") == 5
+    for check in ("codec cross-check", "bad-payload wave", "unknown uid"):
+        assert check in out.stdout
+
+
 BENCH = BIN.parent / "bench_apply"
 
 
