@@ -452,9 +452,13 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
                                                        uint32_t R, void* P, void* N, const unsigned long long* __restrict__ guard) {
     using T = typename ApplyVis<EB>::T;
     const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint64_t m = tid / kEmitLanes;
     const uint32_t e = (uint32_t)(tid % kEmitLanes);
-    if (m >= n || (guard && (guard[0] != ~0ull || guard[1] != 0))) return;  // guard: pass A failed or deferred
+    if (tid / kEmitLanes >= n || (guard && (guard[0] != ~0ull || guard[1] != 0))) return;  // guard: pass A failed or deferred
+    // newest message first: a key's states grow along the wave (counters only increase), so its largest
+    // value usually lands first and the older states' reads below settle without an atomic (max is
+    // order-free; C1's 100 hot keys, ~3000 states each per wave: 292 us of serialised atomics in
+    // commit order)
+    const uint64_t m = n - 1 - tid / kEmitLanes;
     const uint8_t* h = emit + m * emit_stride(EB);
     const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
     if (cnt == kReparse || (cnt & kNeedsCols) || e >= cnt) return;
