@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
         for (int n = 0; n < nodes; ++n) rep[k * nodes + n] = gen.next();
     }
     janus::GpuStableStore gpu(device, (uint32_t)accounts, R, 4);
+    gpu.SetShard(rank, world);  // non-owned states skipped from the uid alone
     // key-space shard of this rank (every rank sees the whole wave and skips the uids it does not own)
     std::vector<uint8_t> mine(accounts);
     uint64_t owned = 0;

@@ -47,6 +47,7 @@ int main(int argc, char** argv) {
     std::vector<oracle::Guid> uid(sets);
     for (auto& u : uid) u = gen.next();
     janus::GpuStableStore gpu(device, 1, 1, 4);
+    gpu.SetShard(rank, world);  // non-owned states skipped from the uid alone
     std::vector<uint8_t> mine(sets);
     uint64_t owned = 0;
     for (uint64_t k = 0; k < sets; ++k) {

@@ -115,6 +115,7 @@ uint32_t GpuStableStore::elem_id(uint32_t set, const std::optional<std::string>&
 
 void GpuStableStore::CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid) {
     if (uids_.find(uid)) return;
+    if (shard_world_ > 1 && ShardOf(uid, shard_world_) != shard_rank_) foreign_keys_ = true;
     if (type == CrdtType::PNCounter) {
         if (next_row_ >= max_keys_) throw EngineError(JG_ESTATE, "PNCounter store full");
         const uint32_t row = next_row_++;
@@ -584,6 +585,8 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
         const char* e = std::getenv("JANUS_HOST_PAR_MIN");
         return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{8192};
     }();
+    // states of other shards' uids are skipped from the uid alone (SetShard), before any table line
+    const uint32_t sw = shard_world_ > 1 && !foreign_keys_ ? shard_world_ : 1, sr = shard_rank_;
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
         const size_t c0 = cb[c], c1 = cb[c + 1];
@@ -602,13 +605,14 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                 size_t k[2] = {0, 0}, bytes[2] = {0, 0};
                 for (size_t i = c0 + q * kTask; i < e; ++i) {
                     if (i + 16 < e) __builtin_prefetch(msgs[i + 16]);
-                    if (i + 8 < e) {
+                    if (i + 8 < e && (sw == 1 || ShardOf(msgs[i + 8]->uid, sw) == sr)) {
                         uids_.prefetch(msgs[i + 8]->uid);
                         if (sweep) tracker->prefetch_claim(msgs[i + 8]->seq);
                     }
                     const NetworkProtocol& u = *msgs[i];
                     uint32_t cl = kSkip;
-                    if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty()) {  // :133-134
+                    if (u.syncMsgType != NetworkProtocol::ManagerMsg_Create && !u.uid.is_empty() &&  // :133-134
+                        (sw == 1 || ShardOf(u.uid, sw) == sr)) {
                         if (const KeyRef* kr = uids_.find(u.uid)) {                                  // :136
                             const int kind = kr->type == CrdtType::PNCounter ? 0 : 1;
                             if (kind == 0) cl = kr->idx;
@@ -659,7 +663,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                 uint64_t o[2] = {tbbase[q], tbbase[(max_tasks + 1) + q]};
                 LineStream out[2] = {LineStream(reinterpret_cast<char*>(ch[0].bytes), o[0]), LineStream(reinterpret_cast<char*>(ch[1].bytes), o[1])};
                 for (size_t i = c0 + q * kTask; i < e; ++i) {
-                    if (i + 8 < e) {  // every line of the payload 8 messages ahead (one prefetch left the rest to miss)
+                    if (i + 8 < e && cls[i + 8] != kSkip) {  // every line of the payload 8 messages ahead (one prefetch left the rest to miss)
                         const std::string& pq = msgs[i + 8]->message;
                         for (size_t x = 0; x < pq.size(); x += 64) __builtin_prefetch(pq.data() + x);
                     }

@@ -248,6 +248,11 @@ class GpuStableStore {
     static uint32_t ShardOf(const Guid& uid, uint32_t world) {
         return world <= 1 ? 0u : (uint32_t)((GuidHash()(uid) >> 7) % world);
     }
+    // Declare this store the shard `rank` of `world`: the apply loop then skips a state of another
+    // shard's uid from the uid alone (ShardOf), without the uid-table and safe-update-tracker lookups —
+    // the same skip the table lookup would make, since a shard registers only the uids it owns.  A
+    // CreateSafeCRDT of a uid outside the shard turns the shortcut off (the table decides again).
+    void SetShard(uint32_t rank, uint32_t world) { shard_rank_ = rank, shard_world_ = world; }
 
     jg_ctx* ctx() const { return ctx_; }
     jg_pnc* pnc() const { return pnc_; }
@@ -324,6 +329,8 @@ class GpuStableStore {
     std::vector<std::pair<char*, size_t>> arenas_;  // pinned staging arenas (base, bytes)
     size_t arena_i_ = 0, arena_off_ = 0;            // carve position of the current wave
     std::vector<uint32_t> cls_, sid_;               // apply_msgs scratch: per message class / set id
+    uint32_t shard_rank_ = 0, shard_world_ = 1;
+    bool foreign_keys_ = false;  // a uid outside the declared shard was registered
     std::vector<const UpdateMessage*> blocks_;      // ApplyCommitted scratch: the wave's blocks, their
     std::vector<size_t> block_off_;                 //   first message, the messages in commit order
     std::vector<const NetworkProtocol*> msgs_;
