@@ -462,6 +462,7 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
             for (const size_t e = std::min(i1, block_off_[b + 1]); i < e; ++i) msgs[i] = u++;
         }
     });
+    if (std::getenv("JANUS_TRACE_WAVE")) std::fprintf(stderr, "wave: flatten %.2f ms\n", 1e3 * (wall_s() - t0));
     return apply_msgs(msgs, tracker, t0);
 }
 
@@ -494,6 +495,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     WorkerPool& wp = pool();
     const int T = wp.size();
     phase_s_[0] = wall_s() - t0;
+    if (std::getenv("JANUS_TRACE_WAVE")) std::fprintf(stderr, "wave: setup %.2f ms\n", 1e3 * phase_s_[0]);
     constexpr uint32_t kSkip = UINT32_MAX, kSet = UINT32_MAX - 1;
     // Chunks of ~48 MB of payload (sized from the previous wave's bytes per message): the staging
     // buffers stay few and reusable, and the first chunk's upload starts early.
