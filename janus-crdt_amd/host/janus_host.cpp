@@ -380,7 +380,45 @@ char* GpuStableStore::stage(size_t bytes) {
 }
 
 bool SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
+    if (seq == 0 || seq == kTomb || contains(seq)) return false;
+    if (ring_.empty()) {
+        std::vector<Slot, TableAlloc<Slot>> fresh(kRing0);
+        ring_.swap(fresh);
+    }
+    Slot& r = ring_[seq & (ring_.size() - 1)];
+    if (r.key.load(std::memory_order_relaxed) == 0) {
+        r.val = origin;
+        r.key.store(seq, std::memory_order_release);
+        n_.fetch_add(1, std::memory_order_relaxed);
+        return true;
+    }
+    table_add(seq, origin);  // the ring slot holds another live seq
+    if (++spill_ > ring_.size() / 16) grow_ring();
+    return true;
+}
+
+bool SafeUpdateTracker::contains(uint64_t seq) const {
     if (seq == 0 || seq == kTomb) return false;
+    if (!ring_.empty() && ring_[seq & (ring_.size() - 1)].key.load(std::memory_order_acquire) == seq) return true;
+    return table_contains(seq);
+}
+
+bool SafeUpdateTracker::claim(uint64_t seq, uint64_t* origin) {
+    if (seq == 0 || seq == kTomb) return false;
+    if (!ring_.empty()) {
+        Slot& r = ring_[seq & (ring_.size() - 1)];
+        uint64_t k = r.key.load(std::memory_order_acquire);
+        if (k == seq) {
+            const uint64_t v = r.val;
+            if (!r.key.compare_exchange_strong(k, 0, std::memory_order_acq_rel)) return false;  // another take won
+            if (origin) *origin = v;
+            return true;
+        }
+    }
+    return used_ ? table_claim(seq, origin) : false;
+}
+
+bool SafeUpdateTracker::table_add(uint64_t seq, uint64_t origin) {
     if ((used_ + 1) * 2 > slots_.size()) grow();
     const size_t mask = slots_.size() - 1;
     for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
@@ -396,8 +434,8 @@ bool SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
     }
 }
 
-bool SafeUpdateTracker::contains(uint64_t seq) const {
-    if (slots_.empty() || seq == 0 || seq == kTomb) return false;
+bool SafeUpdateTracker::table_contains(uint64_t seq) const {
+    if (slots_.empty()) return false;
     const size_t mask = slots_.size() - 1;
     for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
         const uint64_t k = slots_[i].key.load(std::memory_order_acquire);
@@ -406,8 +444,8 @@ bool SafeUpdateTracker::contains(uint64_t seq) const {
     }
 }
 
-bool SafeUpdateTracker::claim(uint64_t seq, uint64_t* origin) {
-    if (slots_.empty() || seq == 0 || seq == kTomb) return false;
+bool SafeUpdateTracker::table_claim(uint64_t seq, uint64_t* origin) {
+    if (slots_.empty()) return false;
     const size_t mask = slots_.size() - 1;
     for (size_t i = seq_slot(seq) & mask;; i = (i + 1) & mask) {
         uint64_t k = slots_[i].key.load(std::memory_order_acquire);
@@ -422,6 +460,10 @@ bool SafeUpdateTracker::claim(uint64_t seq, uint64_t* origin) {
 
 std::vector<std::pair<uint64_t, uint64_t>> SafeUpdateTracker::items() const {
     std::vector<std::pair<uint64_t, uint64_t>> out;
+    for (const Slot& s : ring_) {
+        const uint64_t k = s.key.load(std::memory_order_acquire);
+        if (k != 0) out.emplace_back(k, s.val);
+    }
     for (const Slot& s : slots_) {
         const uint64_t k = s.key.load(std::memory_order_acquire);
         if (k != 0 && k != kTomb) out.emplace_back(k, s.val);
@@ -429,15 +471,40 @@ std::vector<std::pair<uint64_t, uint64_t>> SafeUpdateTracker::items() const {
     return out;
 }
 
-void SafeUpdateTracker::grow() {  // rehash the live entries (tombstones dropped), single-threaded
-    std::vector<std::pair<uint64_t, uint64_t>> live = items();
+void SafeUpdateTracker::grow() {  // rehash the table's live entries (tombstones dropped), single-threaded
+    std::vector<std::pair<uint64_t, uint64_t>> live;
+    for (const Slot& s : slots_) {
+        const uint64_t k = s.key.load(std::memory_order_acquire);
+        if (k != 0 && k != kTomb) live.emplace_back(k, s.val);
+    }
     size_t cap = 1024;
     while (cap < 4 * (live.size() + 1)) cap <<= 1;
     std::vector<Slot, TableAlloc<Slot>> fresh(cap);
     slots_.swap(fresh);
     used_ = 0;
-    n_.store(0, std::memory_order_relaxed);
-    for (const auto& kv : live) add(kv.first, kv.second);
+    n_.fetch_sub(live.size(), std::memory_order_relaxed);  // table_add counts them again
+    for (const auto& kv : live) table_add(kv.first, kv.second);
+}
+
+void SafeUpdateTracker::grow_ring() {  // twice the ring; every live entry placed again, single-threaded
+    const std::vector<std::pair<uint64_t, uint64_t>> live = items();
+    const size_t pending = n_.load(std::memory_order_relaxed) - live.size();  // claimed, not settled yet
+    const size_t cap = ring_.size() * 2;
+    clear();
+    n_.store(pending, std::memory_order_relaxed);
+    std::vector<Slot, TableAlloc<Slot>> fresh(cap);
+    ring_.swap(fresh);
+    for (const auto& kv : live) {
+        Slot& r = ring_[kv.first & (cap - 1)];
+        if (r.key.load(std::memory_order_relaxed) == 0) {
+            r.val = kv.second;
+            r.key.store(kv.first, std::memory_order_relaxed);
+            n_.fetch_add(1, std::memory_order_relaxed);
+        } else {
+            table_add(kv.first, kv.second);
+            ++spill_;
+        }
+    }
 }
 
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker) {
@@ -589,6 +656,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     }();
     // states of other shards' uids are skipped from the uid alone (SetShard), before any table line
     const uint32_t sw = shard_world_ > 1 && !foreign_keys_ ? shard_world_ : 1, sr = shard_rank_;
+    std::vector<std::vector<size_t>> cand(T);  // per worker: the current task's messages that may be tracked
     double t_classify = 0, t_gather = 0;
     for (size_t c = 0; c < n_chunks; ++c) {
         const size_t c0 = cb[c], c1 = cb[c + 1];
@@ -624,9 +692,16 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
                         }
                     }
                     cls[i] = cl;
-                    uint64_t o;
-                    if (sweep && cl != kSkip && tracker->claim(u.seq, &o)) part[c * max_tasks + q].emplace_back(i, o);
+                    if (sweep && cl != kSkip && tracker->maybe(u.seq)) cand[t].push_back(i);
                 }
+                // the task's claims after its lookups: each claim is a locked compare-exchange, which
+                // drains the core's outstanding loads — inside the loop above it stalled every
+                // prefetched lookup behind it (the loop ran 2-3x slower with claims in it)
+                for (const size_t i : cand[t]) {
+                    uint64_t o;
+                    if (tracker->claim(msgs[i]->seq, &o)) part[c * max_tasks + q].emplace_back(i, o);
+                }
+                cand[t].clear();
                 for (int kind = 0; kind < 2; ++kind) {
                     tcnt[kind * max_tasks + q] = k[kind];
                     tbytes[kind * max_tasks + q] = bytes[kind];

@@ -97,15 +97,23 @@ template <class T> void TableAlloc<T>::deallocate(T* p, size_t n) { table_free(p
 // SafeCRDTManager.safeUpdateTracker (SafeCRDTManager.cs:33, a ConcurrentDictionary<NetworkProtocol,
 // (Connection, uint)>): message identity (NetworkProtocol.seq, >= 1) -> client origin.  TryAdd / ContainsKey
 // from one thread (the batcher); TryRemove (take) from many threads at once — the apply loop removes a
-// wave's completed messages in parallel (open addressing; a removed slot becomes a tombstone, so
-// concurrent takes of different keys never move an entry).
+// wave's completed messages in parallel.  Message identities are issued in order and a committed wave
+// carries them roughly in that order, so the entries live in a ring indexed by seq itself (slot =
+// seq mod ring size: a wave's claims walk the ring nearly sequentially instead of one random line
+// each; a claim empties its slot); a seq whose ring slot holds another live seq goes to an
+// open-addressing table (a removed slot there becomes a tombstone, so concurrent takes of different
+// keys never move an entry), and the ring doubles once that table holds 1/16 of its size.
 class SafeUpdateTracker {
   public:
     SafeUpdateTracker() = default;
     template <class It> SafeUpdateTracker(It b, It e) { for (; b != e; ++b) add(b->first, b->second); }
     SafeUpdateTracker(const SafeUpdateTracker& o) { for (const auto& kv : o.items()) add(kv.first, kv.second); }
     SafeUpdateTracker& operator=(const SafeUpdateTracker& o) {
-        if (this != &o) { slots_.clear(); n_ = used_ = 0; for (const auto& kv : o.items()) add(kv.first, kv.second); }
+        if (this != &o) {
+            std::vector<std::pair<uint64_t, uint64_t>> kv = o.items();
+            clear();
+            for (const auto& e : kv) add(e.first, e.second);
+        }
         return *this;
     }
     bool add(uint64_t seq, uint64_t origin);          // TryAdd: false if present (seq 0 is not a message)
@@ -118,29 +126,43 @@ class SafeUpdateTracker {
     // take() without the size update, for parallel sweeps (one shared counter decremented per take
     // serialised 16 workers to ~90 ns a take); settle(k) afterwards with the number claimed
     bool claim(uint64_t seq, uint64_t* origin);
+    // false only if seq is certainly not tracked: a plain load of its ring slot (no locked instruction),
+    // for callers that batch their claims
+    bool maybe(uint64_t seq) const {
+        if (used_) return true;
+        return !ring_.empty() && ring_[seq & (ring_.size() - 1)].key.load(std::memory_order_relaxed) == seq;
+    }
     void settle(size_t k) { n_.fetch_sub(k, std::memory_order_relaxed); }
     void prefetch(uint64_t seq) const {
-        if (!slots_.empty()) __builtin_prefetch(&slots_[seq_slot(seq) & (slots_.size() - 1)]);
+        if (!ring_.empty()) __builtin_prefetch(&ring_[seq & (ring_.size() - 1)]);
     }
-    // the line in exclusive state, for a claim() that will tombstone it (its CAS then needs no ownership
-    // request of its own; measured ~110 ns a claim with a shared-state prefetch, 14 workers)
+    // the line in exclusive state, for a claim() that will empty it (its CAS then needs no ownership
+    // request of its own)
     void prefetch_claim(uint64_t seq) const {
-        if (!slots_.empty()) __builtin_prefetch(&slots_[seq_slot(seq) & (slots_.size() - 1)], 1);
+        if (!ring_.empty()) __builtin_prefetch(&ring_[seq & (ring_.size() - 1)], 1);
     }
     size_t size() const { return n_.load(std::memory_order_relaxed); }
     std::vector<std::pair<uint64_t, uint64_t>> items() const;  // live entries (any order)
 
   private:
-    struct Slot { std::atomic<uint64_t> key{0}; uint64_t val = 0; };  // key 0 empty, kTomb removed
+    struct Slot { std::atomic<uint64_t> key{0}; uint64_t val = 0; };  // key 0 empty; kTomb removed (table only)
     static constexpr uint64_t kTomb = ~0ull;
+    static constexpr size_t kRing0 = size_t(1) << 20;
     static size_t seq_slot(uint64_t x) {
         x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33;
         return (size_t)x;
     }
-    void grow();
+    void clear() { ring_.clear(); slots_.clear(); n_ = 0; used_ = 0; spill_ = 0; }
+    bool table_add(uint64_t seq, uint64_t origin);
+    bool table_contains(uint64_t seq) const;
+    bool table_claim(uint64_t seq, uint64_t* origin);
+    void grow();       // the table: rehash its live entries (tombstones dropped), single-threaded
+    void grow_ring();  // twice the ring, every live entry placed again, single-threaded
+    std::vector<Slot, TableAlloc<Slot>> ring_;
     std::vector<Slot, TableAlloc<Slot>> slots_;
     std::atomic<size_t> n_{0};
-    size_t used_ = 0;  // live + tombstones
+    size_t used_ = 0;   // table: live + tombstones
+    size_t spill_ = 0;  // table entries added since the ring was (re)built
 };
 
 struct EngineError : std::runtime_error {
