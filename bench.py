@@ -369,7 +369,7 @@ def bench_apply_loop(sync, rank, world, local):
     import subprocess
     exe = ROOT / "janus-crdt_amd" / "build" / "bench_apply"
     cpu_msgs = "100000" if world == 1 else "0"
-    out = subprocess.run([str(exe), "--accounts", "1000000", "--ops", "1000000", "--waves", "2", "--cpu-msgs", cpu_msgs,
+    out = subprocess.run([str(exe), "--accounts", "1000000", "--ops", "1000000", "--waves", "3", "--cpu-msgs", cpu_msgs,
                           "--device", str(local), "--rank", str(rank), "--world", str(world)],
                          capture_output=True, text=True, timeout=240)
     ok = out.returncode == 0

@@ -379,6 +379,9 @@ std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vect
     block_off_[0] = 0;
     for (size_t b = 0; b < blocks_.size(); ++b) block_off_[b + 1] = block_off_[b] + blocks_[b]->update.size();
     std::vector<const NetworkProtocol*>& msgs = msgs_;
+    // wave scratch grows with headroom: an exact fit reallocated (and page-faulted in) 8 MB whenever a
+    // wave held a few more messages than the largest before it
+    if (msgs.capacity() < block_off_.back()) msgs.reserve(block_off_.back() + block_off_.back() / 4);
     msgs.resize(block_off_.back());
     // split by messages, not blocks (a wave is ~1000 blocks of ~1000 messages: split by block count it
     // ran on one thread, 0.8 ms per 1M-message wave)
@@ -438,7 +441,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     // runs the validation pass of chunk c-1 (the append calls return once queued).  A chunk's pinned
     // buffer: [payload | pad 16 | off (m+1) u64 | rows or set ids u32]; untouched until commit / abort.
     // cls[i]: PNC row, kSet (sid[i] = the set), or kSkip (create / keyspace / unknown uid, :133-136).
-    if (cls_.size() < n) cls_.resize(n), sid_.resize(n);  // wave scratch kept across waves (no page faults)
+    if (cls_.size() < n) cls_.resize(n + n / 4), sid_.resize(n + n / 4);  // kept across waves, with headroom (no page faults)
     uint32_t* cls = cls_.data();
     uint32_t* sid = sid_.data();
     struct Chunk { size_t m; char* buf; uint64_t* off; uint32_t* rows; uint8_t* bytes; };
@@ -446,7 +449,7 @@ std::vector<uint64_t> GpuStableStore::apply_msgs(const std::vector<const Network
     // where_[kind][j]: commit index of the kind's j-th message (wave order); nw[kind] entries
     size_t nw[2] = {0, 0};
     for (auto& w : where_)
-        if (w.size() < n) w.resize(n);
+        if (w.size() < n) w.resize(n + n / 4);
     // Chunk boundaries: full chunks, then the remainder, whose last `tail` messages form a chunk of their
     // own — the last chunk's upload and pass A are the part of the engine that no host work overlaps.
     const size_t tail = std::max<size_t>(1, std::min<size_t>(16384, chunk_msgs / 8));
