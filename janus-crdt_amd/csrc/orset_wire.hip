@@ -17,7 +17,8 @@
 //   compact scan of the per-message counts (hipcub), then k_ow_compact: entries numbered in commit order
 //                        with addSet entries before removeSet ones (Merge walks addSet first,
 //                        ORSet.cs:255-279).
-//   sort    entries by (set, string) hash, stable (hipcub radix sort): commit order within a hash.
+//   sort    entries by the low 32 bits of their (set, string) hash, stable (hipcub radix sort): commit
+//                        order within a hash.
 //   group   k_ow_link / k_ow_label label every entry with the first entry of its string in the set,
 //                        strings compared byte for byte (a hash collision only takes a slower path).  The
 //                        same string twice in one map of one message is Decode's duplicate-key error
@@ -417,6 +418,8 @@ struct Entries {  // entry e: sort key, string (offset into the payload, length 
     uint32_t* msg;
     uint32_t* meta;
     uint32_t* pos;
+    unsigned long long* pfx;  // the string's first 8 bytes (zero past its end): k_ow_link compares short strings here
+    uint32_t* set;            // the message's set
 };
 
 // Sparse -> dense in commit order: entry ordinal = addSet entries first, then removeSet (Merge's walk),
@@ -426,7 +429,8 @@ constexpr int kCompactMsgs = kBlock / 64;
 __global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restrict__ off, uint64_t n, const unsigned long long* __restrict__ ne,
                                                        const unsigned long long* __restrict__ nt, const uint32_t* __restrict__ na,
                                                        const unsigned long long* __restrict__ eoff, const unsigned long long* __restrict__ toff,
-                                                       Sparse S, Entries E, unsigned long long* __restrict__ tref, Tag16* __restrict__ tval) {
+                                                       const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, Sparse S, Entries E,
+                                                       unsigned long long* __restrict__ tref, Tag16* __restrict__ tval) {
     const uint64_t m = (uint64_t)blockIdx.x * kCompactMsgs + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     if (m >= n) return;
@@ -435,14 +439,21 @@ __global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restric
     const bool rem_first = (na[m] >> 31) != 0;
     const uint64_t e0 = eoff[m], t0 = toff[m];
     auto canon = [&](uint32_t q) -> uint32_t { return !rem_first ? q : (q < n_rem ? n_add + q : q - n_rem); };
+    const uint32_t set = mset[m];
     for (uint32_t q = lane; q < cnt; q += 64) {
         const uint64_t e = e0 + canon(q);
+        const unsigned long long no = S.noff[es + q];
+        const uint32_t meta = S.meta[es + q], len = meta & 0x7FFFFFFFu;
+        unsigned long long pf = 0;
+        for (uint32_t k = 0; k < 8 && k < len; ++k) pf |= (unsigned long long)bytes[no + k] << (8 * k);
         E.key[e] = S.key[es + q];
         E.val[e] = (uint32_t)e;
-        E.noff[e] = S.noff[es + q];
+        E.noff[e] = no;
         E.msg[e] = (uint32_t)m;
-        E.meta[e] = S.meta[es + q];
+        E.meta[e] = meta;
         E.pos[e] = S.pos[es + q];
+        E.pfx[e] = pf;
+        E.set[e] = set;
     }
     const uint32_t k = (uint32_t)nt[m];
     for (uint32_t q = lane; q < k; q += 64) {
@@ -460,12 +471,17 @@ __device__ __forceinline__ bool same_bytes(const uint8_t* a, const uint8_t* b, u
 
 __device__ __forceinline__ bool same_name(const Entries& E, const uint32_t* mset, const uint8_t* bytes, uint32_t a, uint32_t b) {
     const uint32_t la = E.meta[a] & 0x7FFFFFFFu, lb = E.meta[b] & 0x7FFFFFFFu;
-    return la == lb && mset[E.msg[a]] == mset[E.msg[b]] && same_bytes(bytes + E.noff[a], bytes + E.noff[b], la);
+    if (la != lb || E.set[a] != E.set[b] || E.pfx[a] != E.pfx[b]) return false;
+    return la <= 8 || same_bytes(bytes + E.noff[a] + 8, bytes + E.noff[b] + 8, la - 8);
 }
 
-__global__ void k_ow_head(const unsigned long long* __restrict__ skey, uint64_t n, uint32_t* __restrict__ hs) {
+// Entries are sorted on the low sort_bits (32) of their 64-bit (set, string) key (half the radix passes
+// of the full key); a run is one value of those bits, so two strings whose keys differ only above them
+// share a run, which k_ow_link marks impure like any other collision.  Each entry keeps its full key for
+// the element table.
+__global__ void k_ow_head(const unsigned long long* __restrict__ skey, uint64_t n, unsigned long long run_mask, uint32_t* __restrict__ hs) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) hs[i] = (i == 0 || skey[i] != skey[i - 1]) ? (uint32_t)i : 0u;
+    if (i < n) hs[i] = (i == 0 || ((skey[i] ^ skey[i - 1]) & run_mask) != 0) ? (uint32_t)i : 0u;
 }
 
 // A run of equal hashes holding two different strings (a collision) is marked impure.
@@ -801,7 +817,7 @@ struct jg_orset_wire {
     bool open = false, checked = false, any_set = false;
     uint64_t first_bad = kNone, n_ent = 0, n_tag = 0;
     // entries, groups, tags, records
-    jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, skey, sval, hs, seg, impure, label, gid, eid;
+    jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, epfx, eset, skey, sval, hs, seg, impure, label, gid, eid;
     jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
     jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm, perm2;
     jg::DevBuf newk, newv, snk, snv, status, cub;
@@ -811,6 +827,8 @@ struct jg_orset_wire {
     uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;
     // string-hash mask: all bits; tests narrow it (JANUS_TEST_NAME_HASH_BITS) to force collisions
     uint64_t kmask = ~0ull;
+    // key bits the entry sort orders on; tests narrow it (JANUS_TEST_ENTRY_SORT_BITS) so runs mix full keys
+    int sort_bits = 32;
 };
 
 namespace {
@@ -840,6 +858,10 @@ jg_orset_wire* wire_of(jg_orset* s) {
         if (const char* e = std::getenv("JANUS_TEST_NAME_HASH_BITS")) {
             const int bits = std::atoi(e);
             if (bits > 0 && bits < 64) s->wire->kmask = (1ull << bits) - 1;
+        }
+        if (const char* e = std::getenv("JANUS_TEST_ENTRY_SORT_BITS")) {
+            const int bits = std::atoi(e);
+            if (bits > 0 && bits <= 64) s->wire->sort_bits = bits;
         }
     }
     return s->wire;
@@ -951,7 +973,7 @@ Sparse sparse_of(jg_orset_wire* w) {
 
 Entries entries_of(jg_orset_wire* w) {
     return Entries{w->ekey.as<unsigned long long>(), w->eval.as<uint32_t>(), w->enoff.as<unsigned long long>(), w->emsg.as<uint32_t>(),
-                   w->emeta.as<uint32_t>(), w->epos.as<uint32_t>()};
+                   w->emeta.as<uint32_t>(), w->epos.as<uint32_t>(), w->epfx.as<unsigned long long>(), w->eset.as<uint32_t>()};
 }
 
 // Passes 2 + grouping over the whole wave; sets w->first_bad.  Returns the first bad message's code.
@@ -988,12 +1010,14 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     ensure(w->emsg, ne * 4 + 4);
     ensure(w->emeta, ne * 4 + 4);
     ensure(w->epos, ne * 4 + 4);
+    ensure(w->epfx, ne * 8 + 8);
+    ensure(w->eset, ne * 4 + 4);
     ensure(w->tref, nt * 8 + 8);
     ensure(w->tval, nt * 16 + 16);
     const Entries E = entries_of(w);
     hipLaunchKernelGGL(k_ow_compact, dim3((unsigned)((n + kCompactMsgs - 1) / kCompactMsgs)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>(), n, w->ne.as<unsigned long long>(),
                        w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(),
-                       sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
+                       w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(), sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
     JG_HIP(hipGetLastError());
     if (ne) {
         ensure(w->skey, ne * 8);
@@ -1002,8 +1026,10 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         ensure(w->seg, ne * 4);
         ensure(w->impure, ne);
         ensure(w->label, ne * 4);
-        sort_pairs(ctx, w, E.key, w->skey.as<unsigned long long>(), E.val, w->sval.as<uint32_t>(), ne, 64);
-        hipLaunchKernelGGL(k_ow_head, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->skey.as<unsigned long long>(), ne, w->hs.as<uint32_t>());
+        sort_pairs(ctx, w, E.key, w->skey.as<unsigned long long>(), E.val, w->sval.as<uint32_t>(), ne, w->sort_bits);
+        const unsigned long long run_mask = w->sort_bits >= 64 ? ~0ull : (1ull << w->sort_bits) - 1;
+        hipLaunchKernelGGL(k_ow_head, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->skey.as<unsigned long long>(), ne, run_mask,
+                           w->hs.as<uint32_t>());
         JG_HIP(hipGetLastError());
         temp = 0;
         JG_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne, ctx->stream));

@@ -77,6 +77,13 @@ def test_hash_collisions_take_the_exact_path(ctx, monkeypatch):
     _run_waves(ctx, 4, 6, 3, 120, modes=("default", "raw"))
 
 
+def test_entry_runs_mixing_full_keys(ctx, monkeypatch):
+    """With the entry sort narrowed to 4 key bits every run holds strings whose full keys differ: the run is
+    labelled string by string and each string is looked up under its own full key."""
+    monkeypatch.setenv("JANUS_TEST_ENTRY_SORT_BITS", "4")
+    _run_waves(ctx, 5, 6, 3, 120, modes=("default", "raw"))
+
+
 def test_names_sync_and_clear(ctx):
     s = jg.ORSetStore(ctx)
     try:
