@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 2
+#define JG_ABI_VERSION 3
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -251,6 +251,91 @@ int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint3
 /* One-shot: begin + append(all) + check, then commit(n) if every message is good; else nothing is
  * applied and the check's code is returned with *bad_msg (the jg_pnc_merge_json contract). */
 int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg);
+
+/* ---------------------------------------------------------------------------------------------
+ * The committed-wave apply loop (csrc/node.hip) — SafeCRDTManager.HandleAfterConsensusUpdates
+ * (BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:109-160) as ONE call per committed wave (SURVEY.md §8b B2's
+ * jg_apply_batch).  Inside the library: the walk in commit order, the skip of creation and key-space
+ * messages (:133-134), the uid lookup safeCRDTsIndexedByuid.TryGetValue (:136) in a device hash table,
+ * Decode + Merge of every state (SafeCRDT.ApplyUpdateStable, BFT-CRDT/SafeCRDTs/SafeCRDT.cs:80-83) on the
+ * device, and safeUpdateTracker.TryRemove (:141-142) in a device table.  The library's host workers only
+ * gather the payloads into page-locked staging, chunk by chunk, while the device parses the chunk before.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct jg_node jg_node;        /* one copy (stable or prospective) of a node's keyspace          */
+typedef struct jg_tracker jg_tracker;  /* SafeCRDTManager.safeUpdateTracker (SafeCRDTManager.cs:33)     */
+
+/* A node's copy of its keys over a PN-Counter store and an OR-Set store of one context (either NULL if the
+ * node holds no key of that type).  The stores stay owned by the caller and must outlive the node. */
+int jg_node_create(jg_pnc* pnc, jg_orset* orset, jg_node** out);
+int jg_node_destroy(jg_node* node);
+/* SafeCRDTManager.CreateSafeCRDT (SafeCRDTManager.cs:61-101) -> safeCRDTsIndexedByuid[uid] = sc (:73, :98):
+ * key uid[i] is a PNCounter (type 0) at row idx[i] of the node's store, or an ORSet (type 1) at set id
+ * idx[i].  All or nothing: JG_EINVAL for Guid.Empty, a uid registered twice, a row >= the store's n_keys,
+ * a set id >= 2^31 - 16, or a type whose store the node lacks.  (The PNCounter constructor's own replica
+ * column is jg_pnc_intern's, as before.) */
+int jg_node_register(jg_node* node, uint64_t n, const jg_guid* uid, const uint8_t* type, const uint32_t* idx);
+/* Key-space sharding over the GPUs of a node: the owner rank of a key is
+ * jg_shard_of(uid, world) (a hash of the 16 uid bytes).  A node declared shard `rank` of `world` leaves
+ * another shard's states out of its gather from the uid alone — no upload, no lookup; the uid table would
+ * skip them the same way (:136), since such a node registers only its own keys.  Registering a uid of
+ * another shard turns the shortcut off (the table decides every state again); each jg_node_set_shard
+ * rescans the registered uids.  world 1 = no sharding. */
+int jg_node_set_shard(jg_node* node, uint32_t rank, uint32_t world);
+int jg_shard_of(const jg_guid* uid, uint32_t world, uint32_t* rank);
+
+int jg_tracker_create(jg_ctx* ctx, jg_tracker** out);
+int jg_tracker_destroy(jg_tracker* t);
+/* ConcurrentDictionary.TryAdd of SafeCRDT.Update (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:55-56: a safe update with a
+ * client origin): seq[i] (>= 1, < UINT64_MAX) identifies the NetworkProtocol object, origin[i] (!= 0) the
+ * (Connection, id) to notify.  Thread-safe without the context lock (the reference's client threads add
+ * while the apply task runs) and cheap: buffered, the device table takes the adds at the next call that
+ * reads the tracker.  An identity already tracked keeps its entry. */
+int jg_tracker_add(jg_tracker* t, uint64_t n, const uint64_t* seq, const uint64_t* origin);
+int jg_tracker_size(jg_tracker* t, uint64_t* n);
+/* ContainsKey: out[i] = 1 while seq[i] is tracked. */
+int jg_tracker_contains(jg_tracker* t, uint64_t n, const uint64_t* seq, uint8_t* out);
+
+/* A committed wave in commit order (Consensus.Commit's List<List<UpdateMessage>>, Consensus.cs:123-134,
+ * flattened: list, block, update): message i is NetworkProtocol{uid[i], syncMsgType type[i]
+ * (0 ManagerMsg_Create, 1 CRDTMsg), message} (MergeSharp/MergeSharp/proto/SyncProtocol.cs:12-62) with
+ * identity seq[i] (0 = never tracked; seq NULL = all 0).  Payloads either contiguous (off[n + 1], off[0] = 0,
+ * bytes) or scattered (off NULL: message i = ptr[i][0 .. len[i])).  Contiguous payloads in page-locked
+ * memory (jg_host_alloc) are uploaded from there without a host copy. */
+typedef struct jg_commit {
+    uint64_t n;
+    const jg_guid* uid;
+    const uint8_t* type;
+    const uint64_t* seq;
+    const uint64_t* off;
+    const uint8_t* bytes;
+    const uint8_t* const* ptr;
+    const uint32_t* len;
+} jg_commit;
+
+/* HandleAfterConsensusUpdates over one committed wave.  completed[0 .. *n_completed) = the origins of the
+ * safe updates the wave completed (their tracker entries removed), in commit order — the
+ * safeUpdateCompleteClientNotifier calls; completed needs room for n entries (NULL: count only); tracker
+ * may be NULL.  A state its key's Decode / Merge rejects stops the loop there, as the reference's apply
+ * Task faults at it: every message before *stopped_at was applied and its completions reported, nothing
+ * from it on, and the call returns the rejection's code (JG_EINVAL: JsonException; JG_ESTATE: an OR-Set
+ * element with an empty tag set, or a key out of replica columns) — the one entry point that applies a
+ * prefix on error.  JG_OK with *stopped_at = UINT64_MAX otherwise. */
+int jg_apply_committed(jg_node* node, jg_tracker* tracker, const jg_commit* wave, uint64_t* completed, uint64_t* n_completed,
+                       uint64_t* stopped_at);
+/* ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/DAGConnectionManager.cs:40-50,
+ * MergeSharp/MergeSharp/ReplicationManager.cs:290-344) on a node's PROSPECTIVE copy: the same without a
+ * tracker; a CRDT state of an uid the node never registered stops the block there with JG_EINVAL
+ * (KeyNotFoundException, RM:329).  The shard shortcut does not apply. */
+int jg_apply_block(jg_node* node, const jg_commit* wave, uint64_t* stopped_at);
+/* Figures of the node's last apply call.  Host: seconds gathering payloads into staging, waiting for the
+ * device after the last chunk was queued, the whole call.  Device: kernel time of the wave (hipEvents
+ * around each chunk's kernels and around the final phase, on the context's stream).  Messages and
+ * payload bytes uploaded, messages applied (registered CRDT states before the cut), chunks. */
+typedef struct jg_apply_stats {
+    double gather_s, device_wait_s, total_s, device_busy_s;
+    uint64_t msgs_uploaded, bytes_uploaded, msgs_applied, chunks;
+} jg_apply_stats;
+int jg_node_last_stats(jg_node* node, jg_apply_stats* out);
 
 /* ---------------------------------------------------------------------------------------------
  * Cross-shard exchange (csrc/route.hip).  The keyspace of a node is sharded over

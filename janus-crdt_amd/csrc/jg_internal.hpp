@@ -14,6 +14,10 @@
 
 namespace jg {
 
+// Row / set id of a message of another kind in a node wave (csrc/node.hip): the PN-Counter and OR-Set
+// passes run over the same uploaded wave and skip each other's messages.
+constexpr uint32_t kSkipIdx = 0xFFFFFFFFu;
+
 // ---- errors ------------------------------------------------------------------------------------
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void clear_error();
@@ -191,4 +195,18 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
 uint64_t ord_span(jg_ctx* ctx, const uint32_t* ord, uint64_t n);
 // orset.hip: s = s ∪ src (both streams), synchronous, src's streams may be dense or chunked.
 void orset_merge_store(jg_orset* s, jg_orset* src);
+
+// Node waves (node.hip): one upload of every kind's messages; rows / mset = the message's row / set id
+// or kSkipIdx.  json.hip (PN-Counter):
+void pnc_node_begin(jg_pnc* p, uint64_t n);
+void pnc_node_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1);
+int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
+int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
+// orset_wire.hip (OR-Set):
+void orset_node_begin(jg_orset* s, uint8_t* bytes, uint64_t* off, uint32_t* mset, uint64_t n, uint64_t nbytes, uint32_t max_set);
+void orset_node_parse(jg_orset* s, uint64_t m0, uint64_t m1);
+int orset_node_check(jg_orset* s, uint64_t n, uint64_t nbytes, uint64_t* bad, std::string* why);
+void orset_node_commit(jg_orset* s, uint64_t limit);
+void orset_node_abort(jg_orset* s);
+void orset_node_no_names(jg_orset* s);
 }  // namespace jg

@@ -225,6 +225,11 @@ __device__ void scan_one(const uint8_t* __restrict__ bytes, const uint64_t* __re
                          const Table& t, unsigned long long* __restrict__ status, unsigned long long* __restrict__ deferred,
                          uint8_t* __restrict__ emit, unsigned long long* __restrict__ slow) {
     const uint32_t row = rows[m];
+    if (row == jg::kSkipIdx) {  // another kind's message in a node wave (csrc/node.hip): no entries
+        *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = 0;
+        deferred[m] = kNotDeferred;
+        return;
+    }
     *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = kReparse;
     Cursor c(bytes, off[m], off[m + 1]);
     ScanVis vis{t.cols + (uint64_t)row * t.R, t.ncols[row]};
@@ -704,6 +709,49 @@ void check_wave_host(const jg_pnc* p, uint64_t n, const uint32_t* key_idx, const
 }
 
 }  // namespace
+
+// ---- node waves (csrc/node.hip) ------------------------------------------------------------------
+// The node uploads every kind's messages of a committed wave once, classifies them on the device and
+// drives this path over its own buffers: rows[m] = the message's row, or kSkipIdx for another kind's.
+namespace jg {
+
+void pnc_node_begin(jg_pnc* p, uint64_t n) {
+    ensure_table(p);
+    reset_status(p->ctx, wave_scratch(p, n).status);
+    p->wn = n;  // the node wave's capacity (no jg_pnc_wave_* wave is open while a node wave runs)
+}
+
+void pnc_node_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1) {
+    launch_scan(p, bytes, off, rows, m0, m1, wave_scratch(p, p->wn));
+}
+
+// The rest of the wave over messages [0, n) (pass A ran on all of them), all or nothing: JG_OK, or the
+// code of the first rejected message (*bad, why) with nothing applied.  Other failures throw.
+int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why) {
+    *bad = UINT64_MAX;
+    if (n == 0) return JG_OK;
+    try {
+        finish_wave(p, bytes, off, rows, n, wave_scratch(p, p->wn), bad);
+        return JG_OK;
+    } catch (const Error& e) {
+        if (*bad == UINT64_MAX) throw;
+        *why = e.msg;
+        return e.code;
+    }
+}
+
+// Pass A again over [0, n) only, then the rest: the prefix of a wave cut at n (the reference's loop
+// applied the messages before the one that threw).
+int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why) {
+    *bad = UINT64_MAX;
+    if (n == 0) return JG_OK;
+    const WaveScratch w = wave_scratch(p, p->wn);
+    reset_status(p->ctx, w.status);
+    launch_scan(p, bytes, off, rows, 0, n, w);
+    return pnc_node_finish(p, bytes, off, rows, n, bad, why);
+}
+
+}  // namespace jg
 
 // Device-resident wave of encoded state messages (bench / pre-staged waves).
 extern "C" {

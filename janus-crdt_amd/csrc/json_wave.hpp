@@ -372,7 +372,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         __shared__ GroupShared<G> sh;
         const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
         const uint64_t m = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + grp;
-        const bool live = m < m1;
+        // a node wave (csrc/node.hip) holds every kind's messages: those of other kinds carry kSkipIdx
+        const bool skip = m < m1 && rows[m] == jg::kSkipIdx;
+        const bool live = m < m1 && !skip;
         const RowCache rc = row_cache(t, rows, m, live, g);
         GroupParse<EB, G> gp;
         group_parse<EB, G>(sh, bytes, off, m, live, rc, gp);
@@ -423,6 +425,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const bool to_slow = g == 0 && live && !fast;
         const unsigned long long at = wave_slot(to_slow, status + 3);
         if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
+        if (g == 0 && skip) {  // no entries, not deferred
+            *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = 0;
+            deferred[m] = kNotDeferred;
+        }
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
                 (f & kDup) ? kReparse : (uint16_t)((sh.ntok[grp] - 2) | ((f & kMiss) ? kNeedsCols : 0u));

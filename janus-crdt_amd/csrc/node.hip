@@ -1,0 +1,913 @@
+// node.hip — the committed-wave apply loop behind the C ABI (SURVEY.md §8a A13, §8b B2 jg_apply_batch).
+//
+// SafeCRDTManager.HandleAfterConsensusUpdates (BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:109-160) walks a
+// committed wave message by message: skip ManagerMsg_Create and Guid.Empty (:133-134), look the uid up in
+// safeCRDTsIndexedByuid (:136), ApplyUpdateStable = Decode + Merge (SafeCRDT.cs:80-83), then
+// safeUpdateTracker.TryRemove + notify (:141-142).  jg_apply_committed does the whole wave in one call:
+//
+//   host        the library's workers gather chunk c (payloads, uids, identities, types) into pinned
+//               staging with non-temporal line stores while the device works on chunk c-1 — the only
+//               per-message host work left (no table is touched on the host);
+//   copy        the chunk's H2D on the context's copy stream;
+//   k_classify  one lane per message: the skip rule, uid -> (type, row / set id) in the device uid table
+//               (32-B slots, linear probing: one line per lookup), the tracker slot of the message's
+//               identity and a first-occurrence claim on it (atomicMin of the commit index);
+//   passes      the PN-Counter pass A (json_wave.hpp) and the OR-Set parse (orset_wire.hip) over the
+//               chunk, each skipping the other kind's messages (row / set id kSkipIdx);
+//   end         OR-Set check -> first rejected state (the cut); PN-Counter commit (all or nothing, the
+//               prefix re-run when something cut the wave); OR-Set commit up to the cut; k_complete: a
+//               message before the cut that claimed its identity first turns the tracker entry into a
+//               tombstone and reports the origin; origins compacted in commit order (hipcub select).
+//
+// Uid table: open addressing over 32-B slots {uid lo, uid hi, type << 31 | idx}, (0, 0) = empty (Guid.Empty
+// is never a key, :134); load <= 1/2.  The library keeps the authoritative copy on the host (registration
+// is rare: key creation) and uploads the slots a registration touched before the next wave.
+// Tracker: open addressing over 16-B slots {identity, origin}, 0 = empty, ~0 = removed (a tombstone:
+// concurrent probes never see an entry move); rebuilt without tombstones when live + removed pass 1/2.
+#include <hipcub/hipcub.hpp>
+
+#include <chrono>
+#include <memory>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "host_pool.hpp"
+#include "jg_internal.hpp"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr unsigned long long kTomb = ~0ull;
+constexpr uint32_t kOrSetBit = 0x80000000u;
+
+unsigned blocks_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, (n + kBlock - 1) / kBlock); }
+uint64_t pow2_at_least(uint64_t x, uint64_t lo = 1024) {
+    uint64_t p = lo;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+struct UidSlot {
+    unsigned long long lo, hi;
+    uint32_t val, pad0;
+    unsigned long long pad1;
+};
+static_assert(sizeof(UidSlot) == 32, "one uid slot = half a 64-B line");
+struct TrackSlot { unsigned long long key, origin; };
+struct Guid16 { unsigned long long lo, hi; };
+
+__host__ __device__ __forceinline__ uint64_t uid_hash(uint64_t lo, uint64_t hi) {
+    uint64_t x = lo ^ (hi * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t shard_of(uint64_t lo, uint64_t hi, uint32_t world) {
+    return world <= 1 ? 0u : (uint32_t)((uid_hash(lo, hi) >> 7) % world);
+}
+__host__ __device__ __forceinline__ uint64_t seq_hash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 33);
+}
+
+struct DevUids { const UidSlot* tab; uint64_t mask; };
+struct DevTrack { TrackSlot* tab; uint32_t* claim; uint64_t mask; };
+
+__global__ void k_uid_scatter(UidSlot* __restrict__ tab, const uint32_t* __restrict__ at, const UidSlot* __restrict__ v, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) tab[at[i]] = v[i];
+}
+
+// TryAdd of pending (identity, origin) pairs: an identity already present keeps its entry; *count += added.
+__global__ __launch_bounds__(kBlock) void k_track_insert(DevTrack t, const unsigned long long* __restrict__ pairs, uint64_t n,
+                                                         unsigned long long* __restrict__ count) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    bool added = false;
+    if (i < n) {
+        const unsigned long long k = pairs[2 * i];
+        for (uint64_t s = seq_hash(k) & t.mask;; s = (s + 1) & t.mask) {
+            unsigned long long w = t.tab[s].key;
+            if (w == 0) {
+                w = atomicCAS(&t.tab[s].key, 0ull, k);
+                if (w == 0) {
+                    t.tab[s].origin = pairs[2 * i + 1];
+                    added = true;
+                    break;
+                }
+            }
+            if (w == k) break;
+        }
+    }
+    __shared__ uint32_t c;
+    if (threadIdx.x == 0) c = 0;
+    __syncthreads();
+    if (added) atomicAdd(&c, 1u);
+    __syncthreads();
+    if (threadIdx.x == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
+// Live entries of the old table into the new one (tombstones dropped).
+__global__ void k_track_rehash(const TrackSlot* __restrict__ old, uint64_t old_cap, DevTrack t) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= old_cap) return;
+    const TrackSlot e = old[i];
+    if (e.key == 0 || e.key == kTomb) return;
+    for (uint64_t s = seq_hash(e.key) & t.mask;; s = (s + 1) & t.mask)
+        if (atomicCAS(&t.tab[s].key, 0ull, e.key) == 0ull) {
+            t.tab[s].origin = e.origin;
+            return;
+        }
+}
+
+__global__ void k_track_lookup(DevTrack t, const unsigned long long* __restrict__ seq, uint64_t n, uint8_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = seq[i];
+    uint8_t r = 0;
+    if (k != 0 && k != kTomb && t.tab)
+        for (uint64_t s = seq_hash(k) & t.mask;; s = (s + 1) & t.mask) {
+            const unsigned long long w = t.tab[s].key;
+            if (w == 0) break;
+            if (w == k) { r = 1; break; }
+        }
+    out[i] = r;
+}
+
+__global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) off[i] += base;
+}
+
+// Per message of [m0, m1): the loop's skip rule (:133-134), the uid lookup (:136), the tracker slot of its
+// identity and a first-occurrence claim.  status[0] = first CRDT state of an unknown uid (block mode).
+__global__ __launch_bounds__(kBlock) void k_classify(const Guid16* __restrict__ uid, const uint8_t* __restrict__ type,
+                                                     const unsigned long long* __restrict__ seq, uint64_t m0, uint64_t m1, DevUids u,
+                                                     DevTrack t, uint32_t* __restrict__ rows, uint32_t* __restrict__ mset,
+                                                     uint32_t* __restrict__ tslot, unsigned long long* __restrict__ status) {
+    const uint64_t i = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m1) return;
+    uint32_t r = jg::kSkipIdx, s = jg::kSkipIdx, ts = kNoSlot;
+    const Guid16 g = uid[i];
+    if (type[i] != 0 && (g.lo | g.hi) != 0) {  // CRDTMsg of a key (not ManagerMsg_Create, not the key space)
+        uint32_t v = kNoSlot;
+        for (uint64_t q = uid_hash(g.lo, g.hi) & u.mask;; q = (q + 1) & u.mask) {
+            const UidSlot e = u.tab[q];
+            if ((e.lo | e.hi) == 0) break;
+            if (e.lo == g.lo && e.hi == g.hi) { v = e.val; break; }
+        }
+        if (v == kNoSlot) {
+            atomicMin(status, (unsigned long long)i);  // TryGetValue false: skipped (:136); KeyNotFound in RM:329
+        } else {
+            if (v & kOrSetBit) s = v & ~kOrSetBit;
+            else r = v;
+            const unsigned long long k = seq[i];
+            if (t.tab && k != 0 && k != kTomb)
+                for (uint64_t q = seq_hash(k) & t.mask;; q = (q + 1) & t.mask) {
+                    const unsigned long long w = t.tab[q].key;
+                    if (w == 0) break;
+                    if (w == k) {
+                        ts = (uint32_t)q;
+                        if (t.claim[q] > (uint32_t)i) atomicMin(&t.claim[q], (uint32_t)i);
+                        break;
+                    }
+                }
+        }
+    }
+    rows[i] = r;
+    mset[i] = s;
+    tslot[i] = ts;
+}
+
+// Messages before the cut: the first occurrence of a tracked identity removes the entry (TryRemove) and
+// reports its origin (the notifier call); every other message reports 0.
+__global__ void k_complete(const uint32_t* __restrict__ tslot, uint64_t cut, DevTrack t, unsigned long long* __restrict__ origin) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= cut) return;
+    const uint32_t ts = tslot[i];
+    unsigned long long o = 0;
+    if (ts != kNoSlot && t.claim[ts] == (uint32_t)i) {
+        o = t.tab[ts].origin;
+        t.tab[ts].key = kTomb;
+    }
+    origin[i] = o;
+}
+
+__global__ void k_claim_reset(const uint32_t* __restrict__ tslot, uint64_t n, uint32_t* __restrict__ claim) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && tslot[i] != kNoSlot) claim[tslot[i]] = 0xFFFFFFFFu;
+}
+
+__global__ void k_count_sub(unsigned long long* __restrict__ count, const unsigned long long* __restrict__ sub) { *count -= *sub; }
+
+// Messages before the cut that reached a registered key (the states the loop applied) into *out.
+__global__ __launch_bounds__(kBlock) void k_count_applied(const uint32_t* __restrict__ rows, const uint32_t* __restrict__ mset, uint64_t cut,
+                                                          unsigned long long* __restrict__ out) {
+    uint32_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < cut; i += (uint64_t)gridDim.x * kBlock)
+        c += (rows[i] != jg::kSkipIdx || mset[i] != jg::kSkipIdx) ? 1u : 0u;
+    __shared__ uint32_t s;
+    if (threadIdx.x == 0) s = 0;
+    __syncthreads();
+    atomicAdd(&s, c);
+    __syncthreads();
+    if (threadIdx.x == 0 && s) atomicAdd(out, (unsigned long long)s);
+}
+
+struct NonZero {
+    __host__ __device__ bool operator()(const unsigned long long& x) const { return x != 0; }
+};
+
+void ensure(jg::DevBuf& b, size_t bytes) {
+    if (b.bytes < bytes) b.alloc(bytes + bytes / 4 + 256);
+}
+
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+
+}  // namespace
+
+struct jg_tracker {
+    jg_ctx* ctx;
+    // jg_tracker_add runs on the callers' threads (SafeCRDT.Update), not under the context lock: it appends
+    // (identity, origin) pairs to page-locked buffer `cur` under pend_mu; a flush uploads that buffer
+    // (async, stream-ordered before the wave's classify) and switches to the other one, whose own upload
+    // finished before the call that queued it returned (every call that flushes ends with a stream sync).
+    std::mutex pend_mu;
+    struct Pin { unsigned long long* p = nullptr; size_t cap = 0, n = 0; } pin[2];
+    int cur = 0;
+    jg::DevBuf tab, claim, count, dpairs;
+    uint64_t cap = 0;
+    uint64_t used = 0;  // live + tombstones, an upper bound (TryAdd of a present identity counted too)
+
+    ~jg_tracker() {
+        for (Pin& b : pin)
+            if (b.p) (void)hipHostFree(b.p);
+    }
+    DevTrack dev() const { return DevTrack{tab.as<TrackSlot>(), claim.as<uint32_t>(), cap ? cap - 1 : 0}; }
+
+    void append(uint64_t n, const uint64_t* seq, const uint64_t* origin) {  // under pend_mu
+        Pin& b = pin[cur];
+        if (b.n + n > b.cap) {
+            const size_t nc = std::max<size_t>({2 * b.cap, b.n + n, 4096});
+            void* p = nullptr;
+            JG_HIP(hipHostMalloc(&p, nc * 16, hipHostMallocDefault));
+            if (b.n) std::memcpy(p, b.p, b.n * 16);
+            if (b.p) (void)hipHostFree(b.p);
+            b.p = static_cast<unsigned long long*>(p);
+            b.cap = nc;
+        }
+        for (uint64_t i = 0; i < n; ++i) {
+            b.p[2 * (b.n + i)] = seq[i];
+            b.p[2 * (b.n + i) + 1] = origin[i];
+        }
+        b.n += n;
+    }
+
+    // The pending adds into the device table, queued on the context's stream (under the context lock).
+    void flush() {
+        Pin* b;
+        {
+            std::lock_guard<std::mutex> g(pend_mu);
+            b = &pin[cur];
+            cur ^= 1;
+            pin[cur].n = 0;
+        }
+        if (!count.p) {
+            count.alloc(8);
+            JG_HIP(hipMemsetAsync(count.p, 0, 8, ctx->stream));
+        }
+        const uint64_t np = b->n;
+        if (np == 0) return;
+        if (cap == 0 || 2 * (used + np) > cap) {  // rebuild without tombstones
+            unsigned long long live = 0;
+            if (cap) {
+                JG_HIP(hipMemcpyAsync(&live, count.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+                JG_HIP(hipStreamSynchronize(ctx->stream));
+            }
+            const uint64_t ncap = pow2_at_least(4 * (live + np), 4096);
+            jg::DevBuf nt, nc;
+            nt.alloc(ncap * sizeof(TrackSlot));
+            nc.alloc(ncap * 4);
+            JG_HIP(hipMemsetAsync(nt.p, 0, nt.bytes, ctx->stream));
+            JG_HIP(hipMemsetAsync(nc.p, 0xFF, nc.bytes, ctx->stream));
+            const DevTrack nd{nt.as<TrackSlot>(), nc.as<uint32_t>(), ncap - 1};
+            if (cap) hipLaunchKernelGGL(k_track_rehash, dim3(blocks_for(cap)), dim3(kBlock), 0, ctx->stream, tab.as<TrackSlot>(), cap, nd);
+            JG_HIP(hipGetLastError());
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            std::swap(tab.p, nt.p);
+            std::swap(tab.bytes, nt.bytes);
+            std::swap(claim.p, nc.p);
+            std::swap(claim.bytes, nc.bytes);
+            cap = ncap;
+            used = live;
+        }
+        ensure(dpairs, np * 16);
+        JG_HIP(hipMemcpyAsync(dpairs.p, b->p, np * 16, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_track_insert, dim3(blocks_for(np)), dim3(kBlock), 0, ctx->stream, dev(), dpairs.as<unsigned long long>(), np,
+                           count.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        used += np;
+    }
+};
+
+struct jg_node {
+    jg_ctx* ctx;
+    jg_pnc* pnc;
+    jg_orset* orset;
+    // uid table: host copy (authoritative) + device copy
+    std::vector<UidSlot> htab;
+    uint64_t n_keys = 0, n_pnc = 0, n_orset = 0;
+    uint32_t max_set = 0;
+    jg::DevBuf dtab;
+    bool upload_all = true;
+    std::vector<uint32_t> dirty;
+    // key-space shard (jg_node_set_shard)
+    uint32_t shard_rank = 0, shard_world = 1;
+    bool foreign = false;
+    // the wave on the device
+    jg::DevBuf bytes, off, uid, seq, type, rows, mset, tslot, origin, done, status, cub;
+    // pinned staging arenas, carved front to back each wave and kept
+    std::vector<std::pair<char*, size_t>> arenas;
+    size_t arena_i = 0, arena_off = 0;
+    std::unique_ptr<jg::WorkerPool> pool;
+    double avg_msg_bytes = 357.0;
+    std::vector<uint64_t> dmap;  // device index -> commit index (when the shard shortcut dropped messages)
+    jg_apply_stats stats{};
+    std::vector<hipEvent_t> ev;  // pairs around each chunk's kernels and the final phase (device_busy_s)
+
+    ~jg_node() {
+        for (auto& a : arenas) (void)hipHostFree(a.first);
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+    hipEvent_t event(size_t k) {
+        while (ev.size() <= k) {
+            hipEvent_t e;
+            JG_HIP(hipEventCreate(&e));
+            ev.push_back(e);
+        }
+        return ev[k];
+    }
+    jg::WorkerPool& workers() {
+        const int want = jg::host_threads();
+        if (!pool || pool->size() != want) pool = std::make_unique<jg::WorkerPool>(want);
+        return *pool;
+    }
+    char* stage(size_t n) {
+        n = (n + 255) & ~size_t(255);
+        while (arena_i < arenas.size() && arena_off + n > arenas[arena_i].second) {
+            ++arena_i;
+            arena_off = 0;
+        }
+        if (arena_i == arenas.size()) {  // a bigger wave: one more arena as large as the pool so far
+            size_t total = 0;
+            for (const auto& a : arenas) total += a.second;
+            const size_t cap = std::max({n, total, size_t(64) << 20});
+            void* p = nullptr;
+            JG_HIP(hipHostMalloc(&p, cap, hipHostMallocDefault));
+            arenas.emplace_back(static_cast<char*>(p), cap);
+            arena_off = 0;
+        }
+        char* r = arenas[arena_i].first + arena_off;
+        arena_off += n;
+        return r;
+    }
+    bool insert(const UidSlot& e) {  // host table; false if present
+        const uint64_t mask = htab.size() - 1;
+        for (uint64_t q = uid_hash(e.lo, e.hi) & mask;; q = (q + 1) & mask) {
+            UidSlot& s = htab[q];
+            if ((s.lo | s.hi) == 0) {
+                s = e;
+                if (!upload_all) dirty.push_back((uint32_t)q);
+                return true;
+            }
+            if (s.lo == e.lo && s.hi == e.hi) return false;
+        }
+    }
+    const UidSlot* find(uint64_t lo, uint64_t hi) const {
+        if (htab.empty()) return nullptr;
+        const uint64_t mask = htab.size() - 1;
+        for (uint64_t q = uid_hash(lo, hi) & mask;; q = (q + 1) & mask) {
+            const UidSlot& s = htab[q];
+            if ((s.lo | s.hi) == 0) return nullptr;
+            if (s.lo == lo && s.hi == hi) return &s;
+        }
+    }
+    void grow(uint64_t total) {
+        if (!htab.empty() && 2 * total <= htab.size()) return;
+        std::vector<UidSlot> old;
+        old.swap(htab);
+        htab.assign(pow2_at_least(4 * total), UidSlot{0, 0, 0, 0, 0});
+        upload_all = true;
+        dirty.clear();
+        for (const UidSlot& s : old)
+            if ((s.lo | s.hi) != 0) insert(s);
+    }
+    void sync_table() {  // the registrations since the last wave, to the device
+        if (upload_all) {
+            if (htab.empty()) grow(1);
+            dtab.alloc(htab.size() * sizeof(UidSlot));
+            JG_HIP(hipMemcpyAsync(dtab.p, htab.data(), dtab.bytes, hipMemcpyHostToDevice, ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            upload_all = false;
+            dirty.clear();
+            return;
+        }
+        if (dirty.empty()) return;
+        const uint64_t n = dirty.size();
+        std::vector<UidSlot> v(n);
+        for (uint64_t i = 0; i < n; ++i) v[i] = htab[dirty[i]];
+        char* st = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 36 + 512));
+        auto* dat = reinterpret_cast<uint32_t*>(st);
+        auto* dv = reinterpret_cast<UidSlot*>(st + ((n * 4 + 255) & ~255ull));
+        JG_HIP(hipMemcpyAsync(dat, dirty.data(), n * 4, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(dv, v.data(), n * sizeof(UidSlot), hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_uid_scatter, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dtab.as<UidSlot>(), dat, dv, n);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        dirty.clear();
+    }
+    bool shortcut() const { return shard_world > 1 && !foreign; }
+};
+
+namespace {
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// The apply loop over one wave (jg_apply_committed / jg_apply_block).
+void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
+    const double t_begin = now_s();
+    jg_ctx* ctx = nd->ctx;
+    const uint64_t n = w->n;
+    JG_REQUIRE(n < 0x7FFFFFF0ull, JG_EINVAL, "jg_apply: at most 2^31 - 16 messages per wave");
+    JG_REQUIRE(n == 0 || (w->uid && w->type && (w->off ? w->bytes != nullptr || w->off[n] == 0 : (w->ptr && w->len))), JG_EINVAL,
+               "jg_apply: NULL array in the wave");
+    if (w->off) {
+        JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");
+        for (uint64_t i = 0; i < n; ++i) JG_REQUIRE(w->off[i + 1] >= w->off[i], JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)i);
+    }
+    nd->stats = jg_apply_stats{};
+    if (nd->orset) jg::orset_node_no_names(nd->orset);
+    nd->sync_table();
+    if (tr) tr->flush();
+    nd->arena_i = nd->arena_off = 0;  // the previous wave's chunks are no longer referenced
+    nd->dmap.clear();
+    if (n == 0) {
+        *stopped_at = UINT64_MAX;
+        return;
+    }
+    jg::WorkerPool& pool = nd->workers();
+    const bool filter = !block_mode && nd->shortcut();
+    const uint32_t rank = nd->shard_rank, world = nd->shard_world;
+    auto pay = [&](uint64_t i) -> const uint8_t* { return w->off ? w->bytes + w->off[i] : w->ptr[i]; };
+    auto plen = [&](uint64_t i) -> uint64_t { return w->off ? w->off[i + 1] - w->off[i] : w->len[i]; };
+    auto keep = [&](uint64_t i) { return !filter || shard_of(w->uid[i].lo, w->uid[i].hi, world) == rank; };
+
+    // chunks: ~48 MB of payload each (sized from the previous wave's bytes per message), the last 16k
+    // messages a chunk of their own (its upload + passes are the part no host work overlaps)
+    // (read per call: tests narrow them)
+    const char* ce = std::getenv("JANUS_WAVE_CHUNK");
+    const size_t chunk_env = ce ? std::max<size_t>(1, std::strtoull(ce, nullptr, 10)) : size_t{0};
+    const char* pe = std::getenv("JANUS_HOST_PAR_MIN");  // below this many messages a chunk is gathered on the caller alone
+    const size_t min_par = pe ? (size_t)std::strtoull(pe, nullptr, 10) : size_t{8192};
+    const size_t chunk_msgs = chunk_env ? chunk_env : std::clamp<size_t>((size_t)((48u << 20) / std::max(nd->avg_msg_bytes, 64.0)), 8192, 131072);
+    const size_t tail = std::max<size_t>(1, std::min<size_t>(16384, chunk_msgs / 8));
+    // a small first chunk: the first upload starts after ~0.1 ms of gathering instead of a full chunk's
+    std::vector<uint64_t> cb{0};
+    const uint64_t first = n > 4 * tail ? tail : chunk_msgs;
+    for (uint64_t c0 = first; c0 < n; c0 += chunk_msgs) cb.push_back(c0);
+    if (n > cb.back() + 2 * tail) cb.push_back(n - tail);
+    cb.push_back(n);
+    const size_t n_chunks = cb.size() - 1;
+    constexpr size_t kTask = 2048;
+
+    // capacity for the whole wave (payload bytes: an upper bound when the shard shortcut drops states)
+    uint64_t total_bytes = 0;
+    if (w->off) {
+        total_bytes = w->off[n];
+    } else {
+        const size_t ntask = (n + kTask - 1) / kTask;
+        std::vector<uint64_t> part(ntask);
+        jg::deal(pool, n >= min_par, ntask, [&](size_t q, int) {
+            uint64_t b = 0;
+            for (uint64_t i = q * kTask, e = std::min<uint64_t>(n, (q + 1) * kTask); i < e; ++i) b += w->len[i];
+            part[q] = b;
+        });
+        for (uint64_t b : part) total_bytes += b;
+    }
+    ensure(nd->bytes, ((total_bytes + 15) & ~15ull) + 64);  // the parsers read aligned 16-byte windows
+    ensure(nd->off, (n + 1) * 8);
+    ensure(nd->uid, n * 16);
+    ensure(nd->seq, n * 8);
+    ensure(nd->type, n);
+    ensure(nd->rows, n * 4);
+    ensure(nd->mset, n * 4);
+    ensure(nd->tslot, n * 4);
+    ensure(nd->status, 64);
+    uint8_t* d_bytes = nd->bytes.as<uint8_t>();
+    uint64_t* d_off = nd->off.as<uint64_t>();
+    uint32_t* d_rows = nd->rows.as<uint32_t>();
+    uint32_t* d_mset = nd->mset.as<uint32_t>();
+    unsigned long long* d_status = nd->status.as<unsigned long long>();
+    const bool do_pnc = nd->pnc && nd->n_pnc > 0, do_orset = nd->orset && nd->n_orset > 0;
+    const DevUids du{nd->dtab.as<UidSlot>(), nd->htab.size() - 1};
+    const DevTrack dt = tr && tr->cap ? tr->dev() : DevTrack{nullptr, nullptr, 0};
+    // the copy stream must not overwrite buffers the previous call's kernels still read
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    JG_HIP(hipMemsetAsync(d_off, 0, 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(d_status, 0xFF, 64, ctx->stream));
+    if (do_pnc) jg::pnc_node_begin(nd->pnc, n);
+    if (do_orset) jg::orset_node_begin(nd->orset, d_bytes, d_off, d_mset, n, total_bytes, nd->max_set);
+    const bool direct = w->off && !filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
+    if (filter) nd->dmap.resize(n);
+
+    double t_gather = 0;
+    uint64_t m0 = 0, b0 = 0;
+    size_t n_ev = 0;  // event pairs recorded
+    const size_t max_tasks = (chunk_msgs + kTask - 1) / kTask + 1;
+    std::vector<uint64_t> tcnt(max_tasks + 1), tbytes(max_tasks + 1);
+    try {
+        for (size_t c = 0; c < n_chunks; ++c) {
+            const uint64_t c0 = cb[c], c1 = cb[c + 1];
+            const size_t ntask = (size_t)((c1 - c0 + kTask - 1) / kTask);
+            const bool par = c1 - c0 >= min_par;
+            const double tg = now_s();
+            // pass 1: kept messages and their bytes per task
+            jg::deal(pool, par, ntask, [&](size_t q, int) {
+                uint64_t k = 0, b = 0;
+                for (uint64_t i = c0 + q * kTask, e = std::min(c1, c0 + (q + 1) * kTask); i < e; ++i)
+                    if (keep(i)) ++k, b += plen(i);
+                tcnt[q + 1] = k;
+                tbytes[q + 1] = b;
+            });
+            tcnt[0] = tbytes[0] = 0;
+            for (size_t q = 0; q < ntask; ++q) tcnt[q + 1] += tcnt[q], tbytes[q + 1] += tbytes[q];
+            const uint64_t m = tcnt[ntask], nb = tbytes[ntask];
+            if (m == 0) {
+                t_gather += now_s() - tg;
+                continue;
+            }
+            const uint64_t nb_pad = direct ? 0 : (nb + 15) & ~15ull;
+            char* buf = nd->stage(nb_pad + (m + 1) * 8 + m * 16 + m * 8 + m + 64);
+            auto* soff = reinterpret_cast<uint64_t*>(buf + nb_pad);
+            auto* suid = reinterpret_cast<jg_guid*>(soff + m + 1);
+            auto* sseq = reinterpret_cast<uint64_t*>(suid + m);
+            auto* stype = reinterpret_cast<uint8_t*>(sseq + m);
+            soff[0] = 0;
+            // pass 2: payloads (non-temporal lines), chunk-relative end offsets, uids, identities, types
+            jg::deal(pool, par, ntask, [&](size_t q, int) {
+                uint64_t j = tcnt[q], o = tbytes[q];
+                jg::LineStream out(buf, o);
+                const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
+                for (uint64_t i = c0 + q * kTask; i < e; ++i) {
+                    if (!direct && i + 8 < e) {  // every line of the payload 8 messages ahead
+                        const uint8_t* pq = pay(i + 8);
+                        for (uint64_t x = 0, L = plen(i + 8); x < L; x += 64) __builtin_prefetch(pq + x);
+                    }
+                    if (!keep(i)) continue;
+                    const uint64_t L = plen(i);
+                    if (!direct) out.put(reinterpret_cast<const char*>(pay(i)), L);
+                    o += L;
+                    soff[j + 1] = o;
+                    suid[j] = w->uid[i];
+                    sseq[j] = w->seq ? w->seq[i] : 0;
+                    stype[j] = w->type[i];
+                    if (filter) nd->dmap[m0 + j] = i;
+                    ++j;
+                }
+                if (!direct) out.finish();
+            });
+            t_gather += now_s() - tg;
+            // upload (copy stream), then classify and both parses of the chunk (compute stream)
+            const uint8_t* src = direct ? w->bytes + w->off[c0] : reinterpret_cast<const uint8_t*>(buf);
+            if (nb) JG_HIP(hipMemcpyAsync(d_bytes + b0, src, nb, hipMemcpyHostToDevice, ctx->copy));
+            JG_HIP(hipMemcpyAsync(d_off + m0 + 1, soff + 1, m * 8, hipMemcpyHostToDevice, ctx->copy));
+            JG_HIP(hipMemcpyAsync(nd->uid.as<jg_guid>() + m0, suid, m * 16, hipMemcpyHostToDevice, ctx->copy));
+            JG_HIP(hipMemcpyAsync(nd->seq.as<uint64_t>() + m0, sseq, m * 8, hipMemcpyHostToDevice, ctx->copy));
+            JG_HIP(hipMemcpyAsync(nd->type.as<uint8_t>() + m0, stype, m, hipMemcpyHostToDevice, ctx->copy));
+            jg::upload_done(ctx);
+            JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));
+            if (b0) hipLaunchKernelGGL(k_rebase, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d_off + m0 + 1, m, b0);
+            hipLaunchKernelGGL(k_classify, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, nd->uid.as<Guid16>(), nd->type.as<uint8_t>(),
+                               nd->seq.as<unsigned long long>(), m0, m0 + m, du, dt, d_rows, d_mset, nd->tslot.as<uint32_t>(), d_status);
+            JG_HIP(hipGetLastError());
+            if (do_pnc) jg::pnc_node_scan(nd->pnc, d_bytes, d_off, d_rows, m0, m0 + m);
+            if (do_orset) jg::orset_node_parse(nd->orset, m0, m0 + m);
+            JG_HIP(hipEventRecord(nd->event(2 * n_ev + 1), ctx->stream));
+            ++n_ev;
+            m0 += m;
+            b0 += nb;
+            ++nd->stats.chunks;
+        }
+    } catch (...) {
+        (void)hipStreamSynchronize(ctx->copy);
+        (void)hipStreamSynchronize(ctx->stream);
+        if (do_orset) jg::orset_node_abort(nd->orset);
+        throw;
+    }
+    const uint64_t nn = m0;  // messages on the device
+    nd->stats.gather_s = t_gather;
+    nd->stats.msgs_uploaded = nn;
+    nd->stats.bytes_uploaded = b0;
+    if (nn) nd->avg_msg_bytes = (double)b0 / (double)nn;
+    const double t_dev = now_s();
+
+    // the cut: the first state the reference's loop would throw at
+    JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));  // the final phase's kernels start after the chunks'
+    uint64_t cut = nn;
+    int code = JG_OK;
+    std::string why;
+    try {
+        if (block_mode) {
+            unsigned long long unk;
+            JG_HIP(hipMemcpyAsync(&unk, d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            if (unk < nn) {
+                cut = unk;
+                code = JG_EINVAL;
+                why = "The given key was not present in the dictionary (a CRDT state of an uid the node does not hold)";
+            }
+        }
+        if (do_orset) {
+            uint64_t bad = UINT64_MAX;
+            std::string w2;
+            const int rc = jg::orset_node_check(nd->orset, nn, b0, &bad, &w2);  // over the messages uploaded
+            if (rc != JG_OK) {
+                if (bad == UINT64_MAX) jg::fail(rc, "%s", w2.c_str());
+                if (bad < cut) cut = bad, code = rc, why = w2;
+            }
+        }
+        if (do_pnc) {
+            uint64_t bad = UINT64_MAX;
+            std::string w3;
+            int rc = cut < nn ? jg::pnc_node_prefix(nd->pnc, d_bytes, d_off, d_rows, cut, &bad, &w3)
+                              : jg::pnc_node_finish(nd->pnc, d_bytes, d_off, d_rows, nn, &bad, &w3);
+            if (rc != JG_OK) {
+                cut = bad, code = rc, why = w3;
+                rc = jg::pnc_node_prefix(nd->pnc, d_bytes, d_off, d_rows, cut, &bad, &w3);
+                if (rc != JG_OK) jg::fail(JG_EHIP, "jg_apply: the prefix before message %llu failed again: %s", (unsigned long long)cut, w3.c_str());
+            }
+        }
+        if (do_orset) jg::orset_node_commit(nd->orset, cut);
+    } catch (...) {
+        if (do_orset) jg::orset_node_abort(nd->orset);
+        throw;
+    }
+
+    // safe-update completions of the messages before the cut, in commit order
+    uint64_t ndone = 0;
+    JG_HIP(hipMemsetAsync(d_status + 2, 0, 8, ctx->stream));
+    if (cut) hipLaunchKernelGGL(k_count_applied, dim3((unsigned)std::min<uint64_t>(1024, blocks_for(cut))), dim3(kBlock), 0, ctx->stream, d_rows, d_mset, cut,
+                                d_status + 2);
+    JG_HIP(hipGetLastError());
+    if (dt.tab && cut > 0) {
+        ensure(nd->origin, nn * 8 + 8);
+        ensure(nd->done, nn * 8 + 8);
+        auto* d_origin = nd->origin.as<unsigned long long>();
+        auto* d_done = nd->done.as<unsigned long long>();
+        hipLaunchKernelGGL(k_complete, dim3(blocks_for(cut)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), cut, dt, d_origin);
+        hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
+        JG_HIP(hipGetLastError());
+        size_t temp = 0;
+        JG_HIP(hipcub::DeviceSelect::If(nullptr, temp, d_origin, d_done, d_status + 1, (int)cut, NonZero(), ctx->stream));
+        ensure(nd->cub, temp + 256);
+        JG_HIP(hipcub::DeviceSelect::If(nd->cub.p, temp, d_origin, d_done, d_status + 1, (int)cut, NonZero(), ctx->stream));
+        hipLaunchKernelGGL(k_count_sub, dim3(1), dim3(1), 0, ctx->stream, tr->count.as<unsigned long long>(), d_status + 1);
+        JG_HIP(hipGetLastError());
+        unsigned long long k = 0;
+        JG_HIP(hipMemcpyAsync(&k, d_status + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        ndone = k;
+        if (completed && k) {
+            JG_HIP(hipMemcpyAsync(completed, d_done, k * 8, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    } else if (dt.tab) {
+        hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    JG_HIP(hipEventRecord(nd->event(2 * n_ev + 1), ctx->stream));
+    unsigned long long applied = 0;
+    JG_HIP(hipMemcpyAsync(&applied, d_status + 2, 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    nd->stats.msgs_applied = applied;
+    double busy = 0;
+    for (size_t k = 0; k <= n_ev; ++k) {
+        float ms = 0;
+        JG_HIP(hipEventElapsedTime(&ms, nd->ev[2 * k], nd->ev[2 * k + 1]));
+        busy += ms * 1e-3;
+    }
+    nd->stats.device_busy_s = busy;
+    if (n_completed) *n_completed = ndone;
+    *stopped_at = cut < nn ? (filter ? nd->dmap[cut] : cut) : UINT64_MAX;
+    const double t_end = now_s();
+    nd->stats.device_wait_s = t_end - t_dev;
+    nd->stats.total_s = t_end - t_begin;
+    if (code != JG_OK) jg::fail(code, "%s (commit index %llu)", why.c_str(), (unsigned long long)*stopped_at);
+}
+
+}  // namespace
+
+extern "C" {
+
+int jg_node_create(jg_pnc* pnc, jg_orset* orset, jg_node** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(out && (pnc || orset), JG_EINVAL, "jg_node_create: NULL argument (one store at least)");
+        JG_REQUIRE(!pnc || !orset || pnc->ctx == orset->ctx, JG_EINVAL, "jg_node_create: the stores belong to different contexts");
+        jg_ctx* ctx = pnc ? pnc->ctx : orset->ctx;
+        auto lk_ = jg::lock(ctx);
+        jg::ensure_device(ctx);
+        auto* nd = new jg_node();
+        nd->ctx = ctx;
+        nd->pnc = pnc;
+        nd->orset = orset;
+        *out = nd;
+    });
+}
+
+int jg_node_destroy(jg_node* nd) {
+    return jg::guard([&] {
+        if (!nd) return;
+        auto lk_ = jg::lock(nd->ctx);
+        jg::ensure_device(nd->ctx);
+        JG_HIP(hipStreamSynchronize(nd->ctx->stream));
+        JG_HIP(hipStreamSynchronize(nd->ctx->copy));
+        delete nd;
+    });
+}
+
+int jg_node_register(jg_node* nd, uint64_t n, const jg_guid* uid, const uint8_t* type, const uint32_t* idx) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd, JG_EINVAL, "jg_node_register: node is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(uid && type && idx, JG_EINVAL, "jg_node_register: NULL argument");
+        std::unordered_set<uint64_t> batch;  // repeats inside the call (hash of the uid; exact check below)
+        for (uint64_t i = 0; i < n; ++i) {
+            JG_REQUIRE((uid[i].lo | uid[i].hi) != 0, JG_EINVAL, "jg_node_register: entry %llu is Guid.Empty (the key space itself)", (unsigned long long)i);
+            JG_REQUIRE(type[i] <= 1, JG_EINVAL, "jg_node_register: entry %llu: type %u (0 PNCounter, 1 ORSet)", (unsigned long long)i, type[i]);
+            if (type[i] == 0) {
+                JG_REQUIRE(nd->pnc, JG_EINVAL, "jg_node_register: entry %llu is a PNCounter but the node has no PN-Counter store", (unsigned long long)i);
+                JG_REQUIRE(idx[i] < nd->pnc->n_keys, JG_EINVAL, "jg_node_register: entry %llu: row %u >= n_keys %llu", (unsigned long long)i, idx[i],
+                           (unsigned long long)nd->pnc->n_keys);
+            } else {
+                JG_REQUIRE(nd->orset, JG_EINVAL, "jg_node_register: entry %llu is an ORSet but the node has no OR-Set store", (unsigned long long)i);
+                JG_REQUIRE(idx[i] < 0x7FFFFFF0u, JG_EINVAL, "jg_node_register: entry %llu: set id %u out of range", (unsigned long long)i, idx[i]);
+            }
+            JG_REQUIRE(!nd->find(uid[i].lo, uid[i].hi), JG_EINVAL, "jg_node_register: entry %llu: uid already registered", (unsigned long long)i);
+            if (!batch.insert(uid_hash(uid[i].lo, uid[i].hi)).second)
+                for (uint64_t j = 0; j < i; ++j)
+                    JG_REQUIRE(!(uid[j].lo == uid[i].lo && uid[j].hi == uid[i].hi), JG_EINVAL, "jg_node_register: entry %llu repeats entry %llu",
+                               (unsigned long long)i, (unsigned long long)j);
+        }
+        nd->grow(nd->n_keys + n);
+        for (uint64_t i = 0; i < n; ++i) {
+            nd->insert(UidSlot{uid[i].lo, uid[i].hi, type[i] ? (idx[i] | kOrSetBit) : idx[i], 0, 0});
+            if (type[i]) ++nd->n_orset, nd->max_set = std::max(nd->max_set, idx[i]);
+            else ++nd->n_pnc;
+            if (nd->shard_world > 1 && shard_of(uid[i].lo, uid[i].hi, nd->shard_world) != nd->shard_rank) nd->foreign = true;
+        }
+        nd->n_keys += n;
+    });
+}
+
+int jg_node_set_shard(jg_node* nd, uint32_t rank, uint32_t world) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd && world >= 1 && rank < world, JG_EINVAL, "jg_node_set_shard: need rank < world");
+        nd->shard_rank = rank;
+        nd->shard_world = world;
+        nd->foreign = false;
+        if (world > 1)
+            for (const UidSlot& s : nd->htab)
+                if ((s.lo | s.hi) != 0 && shard_of(s.lo, s.hi, world) != rank) {
+                    nd->foreign = true;  // a registered key of another shard: the table decides again
+                    break;
+                }
+    });
+}
+
+int jg_shard_of(const jg_guid* uid, uint32_t world, uint32_t* rank) {
+    return jg::guard([&] {
+        JG_REQUIRE(uid && rank && world >= 1, JG_EINVAL, "jg_shard_of: bad argument");
+        *rank = shard_of(uid->lo, uid->hi, world);
+    });
+}
+
+int jg_node_last_stats(jg_node* nd, jg_apply_stats* out) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd && out, JG_EINVAL, "jg_node_last_stats: NULL argument");
+        *out = nd->stats;
+    });
+}
+
+int jg_tracker_create(jg_ctx* ctx, jg_tracker** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && out, JG_EINVAL, "jg_tracker_create: NULL argument");
+        auto lk_ = jg::lock(ctx);
+        jg::ensure_device(ctx);
+        auto* t = new jg_tracker();
+        t->ctx = ctx;
+        *out = t;
+    });
+}
+
+int jg_tracker_destroy(jg_tracker* t) {
+    return jg::guard([&] {
+        if (!t) return;
+        auto lk_ = jg::lock(t->ctx);
+        jg::ensure_device(t->ctx);
+        JG_HIP(hipStreamSynchronize(t->ctx->stream));
+        delete t;
+    });
+}
+
+int jg_tracker_add(jg_tracker* t, uint64_t n, const uint64_t* seq, const uint64_t* origin) {
+    return jg::guard([&] {
+        JG_REQUIRE(t, JG_EINVAL, "jg_tracker_add: tracker is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(seq && origin, JG_EINVAL, "jg_tracker_add: NULL argument");
+        for (uint64_t i = 0; i < n; ++i) {
+            JG_REQUIRE(seq[i] != 0 && seq[i] != kTomb, JG_EINVAL, "jg_tracker_add: identity %llu is reserved", (unsigned long long)seq[i]);
+            JG_REQUIRE(origin[i] != 0, JG_EINVAL, "jg_tracker_add: origin 0 is the default connection (never tracked, SafeCRDT.cs:55)");
+        }
+        std::lock_guard<std::mutex> g(t->pend_mu);
+        t->append(n, seq, origin);
+    });
+}
+
+int jg_tracker_size(jg_tracker* t, uint64_t* n) {
+    return jg::guard([&] {
+        JG_REQUIRE(t && n, JG_EINVAL, "jg_tracker_size: NULL argument");
+        auto lk_ = jg::lock(t->ctx);
+        jg::ensure_device(t->ctx);
+        t->flush();
+        unsigned long long c = 0;
+        JG_HIP(hipMemcpyAsync(&c, t->count.p, 8, hipMemcpyDeviceToHost, t->ctx->stream));
+        JG_HIP(hipStreamSynchronize(t->ctx->stream));
+        *n = c;
+    });
+}
+
+int jg_tracker_contains(jg_tracker* t, uint64_t n, const uint64_t* seq, uint8_t* out) {
+    return jg::guard([&] {
+        JG_REQUIRE(t, JG_EINVAL, "jg_tracker_contains: tracker is NULL");
+        if (n == 0) return;
+        JG_REQUIRE(seq && out, JG_EINVAL, "jg_tracker_contains: NULL argument");
+        auto lk_ = jg::lock(t->ctx);
+        jg_ctx* ctx = t->ctx;
+        jg::ensure_device(ctx);
+        t->flush();
+        char* st = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 9 + 512));
+        auto* ds = reinterpret_cast<unsigned long long*>(st);
+        auto* dout = reinterpret_cast<uint8_t*>(st + ((n * 8 + 255) & ~255ull));
+        JG_HIP(hipMemcpyAsync(ds, seq, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_track_lookup, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, t->dev(), ds, n, dout);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_apply_committed(jg_node* nd, jg_tracker* tr, const jg_commit* wave, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
+    uint64_t dummy = 0;
+    if (!stopped_at) stopped_at = &dummy;
+    *stopped_at = UINT64_MAX;
+    if (n_completed) *n_completed = 0;
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd && wave, JG_EINVAL, "jg_apply_committed: NULL argument");
+        JG_REQUIRE(!tr || tr->ctx == nd->ctx, JG_EINVAL, "jg_apply_committed: the tracker belongs to another context");
+        jg::ensure_device(nd->ctx);
+        apply_wave(nd, tr, wave, false, completed, n_completed, stopped_at);
+    });
+}
+
+int jg_apply_block(jg_node* nd, const jg_commit* wave, uint64_t* stopped_at) {
+    uint64_t dummy = 0;
+    if (!stopped_at) stopped_at = &dummy;
+    *stopped_at = UINT64_MAX;
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd && wave, JG_EINVAL, "jg_apply_block: NULL argument");
+        jg::ensure_device(nd->ctx);
+        apply_wave(nd, nullptr, wave, true, nullptr, nullptr, stopped_at);
+    });
+}
+
+}  // extern "C"

@@ -394,6 +394,12 @@ __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes
                                                      unsigned long long* __restrict__ err) {
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (m >= m1) return;
+    if (mset[m] == jg::kSkipIdx) {  // another kind's message in a node wave (csrc/node.hip)
+        ne[m] = nt[m] = 0;
+        na[m] = 0;
+        err[m] = kNone;
+        return;
+    }
     const uint64_t b = off[m];
     ParseVis v{S, b, (b + kEntryDiv - 1) / kEntryDiv, (b + kTagDiv - 1) / kTagDiv, kmask, mset[m]};
     Cursor c(bytes, b, off[m + 1]);
@@ -812,6 +818,12 @@ struct jg_orset_wire {
     uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
     // open wave: payload, offsets, set per message, per-message counts / errors
     jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff;
+    // the wave's payload / offsets / set ids: the buffers above (jg_orset_wave_*), or a node's
+    // (csrc/node.hip: every kind's messages uploaded once, set id kSkipIdx for another kind's)
+    uint8_t* vbytes = nullptr;
+    uint64_t* voff = nullptr;
+    uint32_t* vmset = nullptr;
+    bool external = false;
     uint64_t wn = 0, wnb = 0, cap_msgs = 0, cap_bytes = 0;
     uint32_t max_set = 0;
     bool open = false, checked = false, any_set = false;
@@ -941,10 +953,9 @@ template <class Pred> void select_marked(jg_ctx* ctx, jg_orset_wire* w, Pred pre
 }
 
 void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
+    const uint64_t m = w->wn;
     if (msgs > w->cap_msgs) {
-        const uint64_t cap = std::max<uint64_t>(msgs + msgs / 2, 1024), m = w->wn;
-        grow_keep(ctx, w->off, (cap + 1) * 8, (m + 1) * 8);
-        grow_keep(ctx, w->mset, cap * 4, m * 4);
+        const uint64_t cap = std::max<uint64_t>(msgs + msgs / 2, 1024);
         grow_keep(ctx, w->ne, (cap + 1) * 8, m * 8);
         grow_keep(ctx, w->nt, (cap + 1) * 8, m * 8);
         grow_keep(ctx, w->na, cap * 4, m * 4);
@@ -953,7 +964,6 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
     }
     if (bytes > w->cap_bytes) {
         const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 1 << 16);
-        grow_keep(ctx, w->bytes, ((cap + 15) & ~15ull) + 16, w->wnb);  // the cursor reads aligned 16-byte windows
         const uint64_t es = cap / kEntryDiv + 2, ts = cap / kTagDiv + 2;
         const uint64_t ke = (w->wnb + kEntryDiv - 1) / kEntryDiv + 1, kt = (w->wnb + kTagDiv - 1) / kTagDiv + 1;  // slots in use
         grow_keep(ctx, w->sp_key, es * 8, ke * 8);
@@ -964,6 +974,20 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
         grow_keep(ctx, w->sp_tval, ts * 16, kt * 16);
         w->cap_bytes = cap;
     }
+    if (w->external) return;  // a node's buffers
+    // the store's own upload targets (sized on their own: a node wave grows only the arrays above)
+    if (w->off.bytes < (msgs + 1) * 8 || w->mset.bytes < msgs * 4) {
+        const uint64_t cap = std::max<uint64_t>(msgs + msgs / 2, 1024);
+        grow_keep(ctx, w->off, (cap + 1) * 8, (m + 1) * 8);
+        grow_keep(ctx, w->mset, cap * 4, m * 4);
+    }
+    if (w->bytes.bytes < ((bytes + 15) & ~15ull) + 16) {
+        const uint64_t cap = std::max<uint64_t>(bytes + bytes / 2, 1 << 16);
+        grow_keep(ctx, w->bytes, ((cap + 15) & ~15ull) + 16, w->wnb);  // the cursor reads aligned 16-byte windows
+    }
+    w->vbytes = w->bytes.as<uint8_t>();
+    w->voff = w->off.as<uint64_t>();
+    w->vmset = w->mset.as<uint32_t>();
 }
 
 Sparse sparse_of(jg_orset_wire* w) {
@@ -974,6 +998,15 @@ Sparse sparse_of(jg_orset_wire* w) {
 Entries entries_of(jg_orset_wire* w) {
     return Entries{w->ekey.as<unsigned long long>(), w->eval.as<uint32_t>(), w->enoff.as<unsigned long long>(), w->emsg.as<uint32_t>(),
                    w->emeta.as<uint32_t>(), w->epos.as<uint32_t>(), w->epfx.as<unsigned long long>(), w->eset.as<uint32_t>()};
+}
+
+// Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
+void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
+    if (m1 <= m0) return;
+    hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(m1 - m0)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff, w->vmset, m0, m1, sparse_of(w),
+                       w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
+                       w->err.as<unsigned long long>());
+    JG_HIP(hipGetLastError());
 }
 
 // Passes 2 + grouping over the whole wave; sets w->first_bad.  Returns the first bad message's code.
@@ -1015,9 +1048,9 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     ensure(w->tref, nt * 8 + 8);
     ensure(w->tval, nt * 16 + 16);
     const Entries E = entries_of(w);
-    hipLaunchKernelGGL(k_ow_compact, dim3((unsigned)((n + kCompactMsgs - 1) / kCompactMsgs)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>(), n, w->ne.as<unsigned long long>(),
+    hipLaunchKernelGGL(k_ow_compact, dim3((unsigned)((n + kCompactMsgs - 1) / kCompactMsgs)), dim3(kBlock), 0, ctx->stream, w->voff, n, w->ne.as<unsigned long long>(),
                        w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->eoff.as<unsigned long long>(), w->toff.as<unsigned long long>(),
-                       w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(), sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
+                       w->vmset, w->vbytes, sparse_of(w), E, w->tref.as<unsigned long long>(), w->tval.as<Tag16>());
     JG_HIP(hipGetLastError());
     if (ne) {
         ensure(w->skey, ne * 8);
@@ -1036,10 +1069,10 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         JG_HIP(hipcub::DeviceScan::InclusiveScan(cub_temp(w, temp), temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne,
                                                  ctx->stream));
         JG_HIP(hipMemsetAsync(w->impure.p, 0, ne, ctx->stream));
-        hipLaunchKernelGGL(k_ow_link, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+        hipLaunchKernelGGL(k_ow_link, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes,
                            w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), ne, w->impure.as<uint8_t>());
         JG_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_ow_label, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+        hipLaunchKernelGGL(k_ow_label, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes,
                            w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), w->impure.as<uint8_t>(), ne, w->label.as<uint32_t>(),
                            w->err.as<unsigned long long>());
         JG_HIP(hipGetLastError());
@@ -1101,7 +1134,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         ensure(w->newk, ne * 8);
         ensure(w->newv, ne * 4);
         JG_HIP(hipMemsetAsync(st, 0, 64, ctx->stream));
-        hipLaunchKernelGGL(k_ow_resolve, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->bytes.as<uint8_t>(),
+        hipLaunchKernelGGL(k_ow_resolve, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes,
                            w->skey.as<unsigned long long>(), w->sval.as<uint32_t>(), w->label.as<uint32_t>(), ne, limit, names_of(w),
                            w->gid.as<uint32_t>(), w->newk.as<unsigned long long>());
         JG_HIP(hipGetLastError());
@@ -1124,7 +1157,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
                    32 + bits_for(w->max_set));
         const unsigned long long init[4] = {0, 0, w->pool_used, 0};
         JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_ow_assign, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, E, w->bytes.as<uint8_t>(), w->skey.as<unsigned long long>(),
+        hipLaunchKernelGGL(k_ow_assign, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, E, w->vbytes, w->skey.as<unsigned long long>(),
                            w->snk.as<unsigned long long>(), w->snv.as<uint32_t>(), nnew, w->n_names, names_of(w), w->gid.as<uint32_t>(), st);
         JG_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_ow_next_ids, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, w->snk.as<unsigned long long>(), nnew, names_of(w));
@@ -1153,7 +1186,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         ensure(w->dt[sd], nt * 16 + 16);
         ensure(w->ds[sd], nt * 4 + 4);
     }
-    hipLaunchKernelGGL(k_ow_rec_keys, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, E, w->mset.as<uint32_t>(), w->tref.as<unsigned long long>(),
+    hipLaunchKernelGGL(k_ow_rec_keys, dim3(blocks_for(nt)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->tref.as<unsigned long long>(),
                        w->eid.as<uint32_t>(), nt, limit, w->rkey.as<unsigned long long>(), w->rside.as<uint8_t>());
     JG_HIP(hipGetLastError());
     JG_HIP(hipMemsetAsync(w->dtab.p, 0, tcap * 8, ctx->stream));
@@ -1188,6 +1221,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
 
 void close_wave(jg_orset_wire* w) {
     w->open = false;
+    w->external = false;
     w->checked = false;
     w->wn = w->wnb = 0;
     w->max_set = 0;
@@ -1197,6 +1231,56 @@ void close_wave(jg_orset_wire* w) {
 }  // namespace
 
 namespace jg {
+// ---- node waves (csrc/node.hip): the node's buffers hold every kind's messages; mset[m] = kSkipIdx for
+// another kind's.  begin sizes the per-message arrays for n messages / nbytes payload bytes.
+void orset_node_begin(jg_orset* s, uint8_t* bytes, uint64_t* off, uint32_t* mset, uint64_t n, uint64_t nbytes, uint32_t max_set) {
+    jg_ctx* ctx = s->ctx;
+    jg_orset_wire* w = wire_of(s);
+    close_wave(w);
+    w->external = true;
+    w->vbytes = bytes;
+    w->voff = off;
+    w->vmset = mset;
+    grow_wave(ctx, w, std::max<uint64_t>(n, 1), std::max<uint64_t>(nbytes, 1));
+    w->wn = n;
+    w->wnb = nbytes;
+    w->max_set = max_set;
+    w->any_set = true;
+    w->open = true;
+}
+void orset_node_parse(jg_orset* s, uint64_t m0, uint64_t m1) { launch_parse(s->ctx, s->wire, m0, m1); }
+// JG_OK, or the code of the first rejected message (*bad, why).
+int orset_node_check(jg_orset* s, uint64_t n, uint64_t nbytes, uint64_t* bad, std::string* why) {
+    *bad = UINT64_MAX;
+    s->wire->wn = n;
+    s->wire->wnb = nbytes;
+    const int rc = jg_orset_wave_check(s, bad);
+    if (rc != JG_OK) {
+        char buf[1024];
+        jg_last_error(buf, sizeof buf);
+        *why = buf;
+    }
+    return rc;
+}
+void orset_node_commit(jg_orset* s, uint64_t limit) {
+    const int rc = jg_orset_wave_commit(s, limit);
+    if (rc != JG_OK) {
+        char buf[1024];
+        jg_last_error(buf, sizeof buf);
+        fail(rc, "%s", buf);
+    }
+}
+void orset_node_abort(jg_orset* s) {
+    if (s->wire) close_wave(s->wire);
+}
+// No element ids issued yet by this call (jg_orset_wave_names reports the last commit's: a node call that
+// ends before committing must not leave the previous call's there).
+void orset_node_no_names(jg_orset* s) {
+    if (!s->wire) return;
+    s->wire->g0 = s->wire->g1 = s->wire->n_names;
+    s->wire->p0 = s->wire->p1 = s->wire->pool_used;
+}
+
 void orset_wire_free(jg_orset_wire* w) {
     if (w) delete w->recs;
     delete w;
@@ -1301,10 +1385,7 @@ int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uin
         JG_HIP(hipMemcpyAsync(w->mset.as<uint32_t>() + m0, set, n * 4, hipMemcpyHostToDevice, ctx->copy));
         jg::upload_done(ctx);
         if (b0) hipLaunchKernelGGL(k_ow_rebase, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->off.as<uint64_t>() + m0 + 1, n, b0);
-        hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->bytes.as<uint8_t>(), w->off.as<uint64_t>(),
-                           w->mset.as<uint32_t>(), m0, m0 + n, sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
-                           w->na.as<uint32_t>(), w->err.as<unsigned long long>());
-        JG_HIP(hipGetLastError());
+        launch_parse(ctx, w, m0, m0 + n);
         w->wn = m0 + n;
         w->wnb = b0 + nb;
         w->max_set = mx;

@@ -17,8 +17,9 @@
 // per account; the 100 ms timer flushes every queue at the end of a wave.  100 UpdateMessages per block
 // (DAG.cs:25).  A wave is `ops` client ops (1M: BASELINE configs[4]).
 //
-// GPU: janus::GpuStableStore::ApplyCommitted with the safe-update tracker (classify + gather into
-// pinned staging + the streamed jg_pnc_wave_*: decode, replica interning and merge on the device).
+// GPU: janus::GpuStableStore::ApplyCommitted = the wave flattened into the jg_commit arrays (the C# caller's
+// share) + ONE jg_apply_committed (the library: gather into pinned staging, uid lookup, safe-update tracker,
+// decode, replica interning and merge; csrc/node.hip).
 // CPU baseline: the oracle's SafeCRDTManager.HandleAfterConsensusUpdates (Decode + Merge per message,
 // one thread like the reference's serialized apply task) on the first `cpu_msgs` messages of each wave.
 // --parity: the oracle applies EVERY wave in full; after each wave every owned account's stable Get and
@@ -33,6 +34,7 @@
 #include <string>
 #include <unordered_map>
 
+#include "host_pool.hpp"
 #include "janus_host.hpp"
 #include "oracle.hpp"
 #include "wire.hpp"
@@ -100,12 +102,12 @@ int main(int argc, char** argv) {
     };
     struct Queued { janus::NetworkProtocol np; bool safe; };
     std::vector<std::vector<Queued>> q(nodes);
-    janus::SafeUpdateTracker tracker_g;                   // safe-update tracker: seq -> client origin (GPU node)
+    janus::SafeUpdateTracker tracker_g(gpu.ctx());       // safe-update tracker: seq -> client origin (GPU node, on the device)
     std::unordered_map<uint64_t, uint64_t> tracker_c;    // the oracle node's
     uint64_t seq = 1;
 
-    double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, ph[4] = {0, 0, 0, 0};
-    uint64_t gpu_n = 0, cpu_n = 0, payload_timed = 0, shard_bytes = 0, applied = 0, n_safe = 0, n_states = 0, n_done = 0;
+    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0;
+    uint64_t gpu_n = 0, cpu_n = 0, payload_timed = 0, up_bytes = 0, up_msgs = 0, applied = 0, n_safe = 0, n_states = 0, n_done = 0;
     bool ok = true;
     std::string why;
     for (int w = 0; w < waves + 1 && ok; ++w) {  // wave 0 = warmup
@@ -225,16 +227,18 @@ int main(int argc, char** argv) {
             continue;
         }
         gpu_s += t1 - t0;
-        host_s += gpu.last_apply_host_s();
-        engine_s += gpu.last_apply_engine_s();
-        for (int p = 0; p < 4; ++p) ph[p] += gpu.last_apply_phases_s()[p];
+        const jg_apply_stats& st = gpu.last_apply_stats();
+        flat_s += gpu.last_flatten_s();
+        gather_s += st.gather_s;
+        wait_s += st.device_wait_s;
+        lib_s += st.total_s;
+        busy_s += st.device_busy_s;
+        up_bytes += st.bytes_uploaded;
+        up_msgs += st.msgs_uploaded;
+        applied += st.msgs_applied;  // counted by the library: states that reached a registered key
         gpu_n += wave_msgs;
         payload_timed += wave_payload;
-        shard_bytes += gpu.last_apply_pnc_bytes();
         n_done += done.size();
-        for (const auto& blk : wave)
-            for (const auto& um : blk)
-                for (const auto& np : um.update) applied += janus::GpuStableStore::ShardOf(np.uid, world) == rank;
         if (!run_cpu) continue;
         cpu.safeUpdateTracker = tracker_c;
         cpu.notified.clear();
@@ -262,19 +266,24 @@ int main(int argc, char** argv) {
                     (unsigned long long)owned);
         return ok ? 0 : 1;
     }
-    const double bytes = (double)payload_timed;  // JSON payload bytes uploaded and decoded
+    const double W = waves;
+    // per uploaded message the library moves its payload, 8 B offset, 16 B uid, 8 B identity, 1 B type
+    const double pcie_bytes = (double)up_bytes + 33.0 * (double)up_msgs;
     std::printf("{\"workload\": \"C5 banking replay (BankingWorload.cs ops: view/deposit/transfer/withdraw at opsRatio [0.25, 0.25, 0.5], "
                 "every d an Increment; %s accounts %llu; %d nodes, clientBatchSize %d with state compaction; committed waves of %llu client ops)\", "
                 "\"waves\": %d, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
-                "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, \"host_ms_per_wave\": %.3f, "
-                "\"engine_ms_per_wave\": %.3f, \"engine_msgs_per_s\": %.1f, \"engine_payload_GBps\": %.2f, \"host_threads\": %d, "
-                "\"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
+                "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"completed_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, "
+                "\"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
+                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
+                "\"uploaded_msgs_per_wave\": %.1f, \"uploaded_bytes_per_wave\": %.1f, \"pcie_GBps\": %.2f, \"engine_payload_GBps\": %.2f, "
+                "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %.1f, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
                 normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, gpu_n / gpu_s,
-                (double)ops * waves / gpu_s, 1e3 * gpu_s / waves, (double)gpu_n / waves, (double)n_states / waves, (double)n_safe / waves,
-                bytes / std::max<uint64_t>(gpu_n, 1), 1e3 * host_s / waves, 1e3 * engine_s / waves, gpu_n / engine_s, shard_bytes / engine_s / 1e9,
-                janus::GpuStableStore::host_threads(), 1e3 * ph[0] / waves, 1e3 * ph[1] / waves, 1e3 * ph[2] / waves, 1e3 * ph[3] / waves, rank,
-                world, (unsigned long long)owned, (double)applied / waves, cpu_s > 0 ? cpu_n / cpu_s : 0.0, (double)cpu_n / waves);
+                (double)ops * waves / gpu_s, 1e3 * gpu_s / W, (double)gpu_n / W, (double)n_states / W, (double)n_safe / W, (double)n_done / W,
+                (double)payload_timed / std::max<uint64_t>(gpu_n, 1), 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W,
+                1e3 * busy_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
+                (double)up_bytes / std::max(busy_s, 1e-12) / 1e9, jg::host_threads(), rank, world, (unsigned long long)owned,
+                (double)applied / W, cpu_s > 0 ? cpu_n / cpu_s : 0.0, (double)cpu_n / W);
     return 0;
 }

@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_pool.hpp"
 #include "janus_host.hpp"
 #include "oracle.hpp"
 #include "wire.hpp"
@@ -28,14 +29,12 @@ double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock:
 
 int main(int argc, char** argv) {
     uint64_t sets = 100000, msgs = 200000, cpu_msgs = 20000;
-    bool probe = false;
     int waves = 3, nodes = 4, device = 0;
     uint32_t rank = 0, world = 1;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--sets") && i + 1 < argc) sets = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--msgs") && i + 1 < argc) msgs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--cpu-msgs") && i + 1 < argc) cpu_msgs = std::strtoull(argv[++i], nullptr, 10);
-        else if (!std::strcmp(argv[i], "--probe-copy")) probe = true;
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
@@ -61,7 +60,8 @@ int main(int argc, char** argv) {
     static const char chars[] = "abcdefghijklmnorqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";  // sic (BenchmarkWorkload.cs:151)
     // per (set, node): the node's elements since its last Clear, one tag each
     std::vector<janus::ORSetState> st(sets * nodes);
-    double gpu_s = 0, host_s = 0, engine_s = 0, cpu_s = 0, oph[3] = {0, 0, 0}, hph[4] = {0, 0, 0, 0};
+    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0;
+    uint64_t up_bytes = 0, up_msgs = 0, applied = 0;
     uint64_t gpu_n = 0, cpu_n = 0, payload = 0, recs = 0;
     const int warm = 2;  // warm-up waves: the staging buffers reach their size, the tables their load
     for (int w = 0; w < waves + warm; ++w) {
@@ -111,44 +111,20 @@ int main(int argc, char** argv) {
         if (!cum.update.empty()) cblock.push_back(std::move(cum));
         if (!cblock.empty()) cwave.push_back(std::move(cblock));
 
-        if (probe) {  // host copy rate of this wave's payloads (diagnostic)
-            std::vector<const std::string*> ps;
-            for (auto& b : wave)
-                for (auto& u : b)
-                    for (auto& np : u.update) ps.push_back(&np.message);
-            std::vector<char> dst(wave_payload + 64);
-            jg_ctx* pctx = nullptr;
-            void* pinned = nullptr;
-            jg_open(device, &pctx);
-            jg_host_alloc(pctx, wave_payload + 64, &pinned);
-            for (int T : {1, 4, 16, -16}) {
-                const double a = now_s();
-                std::vector<std::thread> th;
-                char* out = T < 0 ? static_cast<char*>(pinned) : dst.data();
-                const int TT = T < 0 ? -T : T;
-                for (int t = 0; t < TT; ++t)
-                    th.emplace_back([&, t, TT, out] {
-                        const size_t b = ps.size() * t / TT, e = ps.size() * (t + 1) / TT;
-                        size_t o = 0;
-                        for (size_t i = 0; i < b; ++i) o += ps[i]->size();
-                        for (size_t i = b; i < e; ++i) { std::memcpy(out + o, ps[i]->data(), ps[i]->size()); o += ps[i]->size(); }
-                    });
-                for (auto& x : th) x.join();
-                std::fprintf(stderr, "probe wave %d threads %d%s: %.2f ms (%.1f GB/s)\n", w, TT, T < 0 ? " pinned" : "", 1e3 * (now_s() - a),
-                             wave_payload / (now_s() - a) / 1e9);
-            }
-            jg_host_free(pinned);
-            jg_close(pctx);
-        }
         const double t0 = now_s();
         gpu.ApplyCommitted(wave, nullptr);
         const double t1 = now_s();
         if (w < warm) continue;
         gpu_s += t1 - t0;
-        host_s += gpu.last_apply_host_s();
-        engine_s += gpu.last_apply_engine_s();
-        for (int q = 0; q < 3; ++q) oph[q] += gpu.last_apply_orset_phases_s()[q];
-        for (int q = 0; q < 4; ++q) hph[q] += gpu.last_apply_phases_s()[q];
+        const jg_apply_stats& st = gpu.last_apply_stats();
+        flat_s += gpu.last_flatten_s();
+        gather_s += st.gather_s;
+        wait_s += st.device_wait_s;
+        lib_s += st.total_s;
+        busy_s += st.device_busy_s;
+        up_bytes += st.bytes_uploaded;
+        up_msgs += st.msgs_uploaded;
+        applied += st.msgs_applied;
         gpu_n += msgs;
         payload += wave_payload;
         recs += wave_recs;
@@ -158,17 +134,20 @@ int main(int argc, char** argv) {
         cpu_s += now_s() - c0;
         cpu_n += std::min(msgs, cpu_msgs);
     }
+    const double W = waves;
+    const double pcie_bytes = (double)up_bytes + 33.0 * (double)up_msgs;
     std::printf("{\"workload\": \"committed-batch apply (OR-Set, ORSetWorkload-shaped: random 5-char adds, Clear at 50, %llu sets, %d nodes, "
                 "%llu ORSetMsg JSON states per wave)\", \"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"payload_bytes_per_msg\": %.1f, "
-                "\"tag_records_per_msg\": %.2f, \"host_ms_per_wave\": %.3f, \"engine_ms_per_wave\": %.3f, "
-                "\"orset_ms_per_wave\": {\"validate\": %.3f, \"commit\": %.3f, \"host_names\": %.3f}, \"host_phase_ms\": [%.2f, %.2f, %.2f, %.2f], "
-                "\"host_threads\": %d, \"rank\": %u, "
-                "\"world\": %u, \"owned_sets\": %llu, \"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, "
+                "\"tag_records_per_msg\": %.2f, \"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
+                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
+                "\"uploaded_msgs_per_wave\": %.1f, \"uploaded_bytes_per_wave\": %.1f, \"pcie_GBps\": %.2f, \"engine_payload_GBps\": %.2f, "
+                "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_sets\": %llu, \"applied_msgs_per_wave\": %.1f, "
+                "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, "
                 "\"kind\": \"port\", \"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + ORSet.Merge per message\"}}\n",
-                (unsigned long long)sets, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s, 1e3 * gpu_s / waves, (double)payload / gpu_n,
-                (double)recs / gpu_n, 1e3 * host_s / waves, 1e3 * engine_s / waves, 1e3 * oph[0] / waves, 1e3 * oph[1] / waves, 1e3 * oph[2] / waves, 1e3 * hph[0] / waves, 1e3 * hph[1] / waves,
-                1e3 * hph[2] / waves, 1e3 * hph[3] / waves,
-                janus::GpuStableStore::host_threads(), rank, world,
-                (unsigned long long)owned, cpu_s > 0 ? cpu_n / cpu_s : 0.0, (unsigned long long)std::min(msgs, cpu_msgs));
+                (unsigned long long)sets, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s, 1e3 * gpu_s / W, (double)payload / gpu_n,
+                (double)recs / gpu_n, 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W, 1e3 * busy_s / W,
+                1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
+                (double)up_bytes / std::max(busy_s, 1e-12) / 1e9, jg::host_threads(), rank, world, (unsigned long long)owned, (double)applied / W,
+                cpu_s > 0 ? cpu_n / cpu_s : 0.0, (unsigned long long)std::min(msgs, cpu_msgs));
     return 0;
 }

@@ -15,8 +15,10 @@
 // id (null -> JG_NULL_ELEM) here.
 //
 // Committed states arrive as the reference ships them: NetworkProtocol.message = the encoded
-// PropagationMessage bytes (System.Text.Json, SafeCRDT.cs:49).  PN-Counter payloads go to the GPU
-// undecoded (jg_pnc_merge_json); OR-Set payloads are decoded here (wire.hpp) and merged as records.
+// PropagationMessage bytes (System.Text.Json, SafeCRDT.cs:49).  A committed wave is flattened here into
+// the C ABI's jg_commit arrays and applied by ONE jg_apply_committed call (csrc/node.hip): the uid lookup,
+// the safe-update tracker and both kinds' decode + merge run inside the library — exactly the call the
+// C# HandleAfterConsensusUpdates makes.
 #pragma once
 
 #include <array>
@@ -32,9 +34,12 @@
 
 #include "janus_gpu.h"
 
+namespace jg {
+class WorkerPool;
+}
+
 namespace janus {
 
-class WorkerPool;
 
 struct Guid {
     uint64_t lo = 0, hi = 0;
@@ -76,93 +81,22 @@ struct UpdateMessage {  // BFT-CRDT/DAGConsensus/DAGUpdateMessage.cs:16-55
 // message in msgs[first..] in ONE device call (jg_update_digests).
 void ComputeDigests(jg_ctx* ctx, std::vector<UpdateMessage>& msgs, size_t first = 0);
 
-// Storage of the apply loop's random-access tables (uid table, safe-update tracker: one random line per
-// message each): 2 MiB-aligned and marked for transparent huge pages once at least 2 MiB, so a lookup's
-// line does not also miss the TLB (a 1M-key uid table spans 64 MB).
-template <class T> struct TableAlloc {
-    using value_type = T;
-    static constexpr size_t kHuge = size_t(2) << 20;
-    TableAlloc() = default;
-    template <class U> TableAlloc(const TableAlloc<U>&) {}
-    T* allocate(size_t n);
-    void deallocate(T* p, size_t n);
-    template <class U> bool operator==(const TableAlloc<U>&) const { return true; }
-    template <class U> bool operator!=(const TableAlloc<U>&) const { return false; }
-};
-void* table_alloc(size_t bytes);
-void table_free(void* p, size_t bytes);
-template <class T> T* TableAlloc<T>::allocate(size_t n) { return static_cast<T*>(table_alloc(n * sizeof(T))); }
-template <class T> void TableAlloc<T>::deallocate(T* p, size_t n) { table_free(p, n * sizeof(T)); }
-
 // SafeCRDTManager.safeUpdateTracker (SafeCRDTManager.cs:33, a ConcurrentDictionary<NetworkProtocol,
-// (Connection, uint)>): message identity (NetworkProtocol.seq, >= 1) -> client origin.  TryAdd / ContainsKey
-// from one thread (the batcher); TryRemove (take) from many threads at once — the apply loop removes a
-// wave's completed messages in parallel.  Message identities are issued in order and a committed wave
-// carries them roughly in that order, so the entries live in a ring indexed by seq itself (slot =
-// seq mod ring size: a wave's claims walk the ring nearly sequentially instead of one random line
-// each; a claim empties its slot); a seq whose ring slot holds another live seq goes to an
-// open-addressing table (a removed slot there becomes a tombstone, so concurrent takes of different
-// keys never move an entry), and the ring doubles once that table holds 1/16 of its size.
+// (Connection, uint)>): message identity (NetworkProtocol.seq, >= 1) -> client origin, held by the library
+// on the device (jg_tracker); the apply loop removes a wave's completed entries there.
 class SafeUpdateTracker {
   public:
-    SafeUpdateTracker() = default;
-    template <class It> SafeUpdateTracker(It b, It e) { for (; b != e; ++b) add(b->first, b->second); }
-    SafeUpdateTracker(const SafeUpdateTracker& o) { for (const auto& kv : o.items()) add(kv.first, kv.second); }
-    SafeUpdateTracker& operator=(const SafeUpdateTracker& o) {
-        if (this != &o) {
-            std::vector<std::pair<uint64_t, uint64_t>> kv = o.items();
-            clear();
-            for (const auto& e : kv) add(e.first, e.second);
-        }
-        return *this;
-    }
-    bool add(uint64_t seq, uint64_t origin);          // TryAdd: false if present (seq 0 is not a message)
-    bool contains(uint64_t seq) const;
-    bool take(uint64_t seq, uint64_t* origin) {       // TryRemove; safe against concurrent take()s
-        if (!claim(seq, origin)) return false;
-        n_.fetch_sub(1, std::memory_order_relaxed);
-        return true;
-    }
-    // take() without the size update, for parallel sweeps (one shared counter decremented per take
-    // serialised 16 workers to ~90 ns a take); settle(k) afterwards with the number claimed
-    bool claim(uint64_t seq, uint64_t* origin);
-    // false only if seq is certainly not tracked: a plain load of its ring slot (no locked instruction),
-    // for callers that batch their claims
-    bool maybe(uint64_t seq) const {
-        if (used_) return true;
-        return !ring_.empty() && ring_[seq & (ring_.size() - 1)].key.load(std::memory_order_relaxed) == seq;
-    }
-    void settle(size_t k) { n_.fetch_sub(k, std::memory_order_relaxed); }
-    void prefetch(uint64_t seq) const {
-        if (!ring_.empty()) __builtin_prefetch(&ring_[seq & (ring_.size() - 1)]);
-    }
-    // the line in exclusive state, for a claim() that will empty it (its CAS then needs no ownership
-    // request of its own)
-    void prefetch_claim(uint64_t seq) const {
-        if (!ring_.empty()) __builtin_prefetch(&ring_[seq & (ring_.size() - 1)], 1);
-    }
-    size_t size() const { return n_.load(std::memory_order_relaxed); }
-    std::vector<std::pair<uint64_t, uint64_t>> items() const;  // live entries (any order)
+    explicit SafeUpdateTracker(jg_ctx* ctx);
+    ~SafeUpdateTracker();
+    SafeUpdateTracker(const SafeUpdateTracker&) = delete;
+    SafeUpdateTracker& operator=(const SafeUpdateTracker&) = delete;
+    void add(uint64_t seq, uint64_t origin);  // TryAdd (SafeCRDT.cs:55-56)
+    bool contains(uint64_t seq) const;         // ContainsKey
+    size_t size() const;
+    jg_tracker* handle() const { return t_; }
 
   private:
-    struct Slot { std::atomic<uint64_t> key{0}; uint64_t val = 0; };  // key 0 empty; kTomb removed (table only)
-    static constexpr uint64_t kTomb = ~0ull;
-    static constexpr size_t kRing0 = size_t(1) << 20;
-    static size_t seq_slot(uint64_t x) {
-        x ^= x >> 33; x *= 0xFF51AFD7ED558CCDull; x ^= x >> 33;
-        return (size_t)x;
-    }
-    void clear() { ring_.clear(); slots_.clear(); n_ = 0; used_ = 0; spill_ = 0; }
-    bool table_add(uint64_t seq, uint64_t origin);
-    bool table_contains(uint64_t seq) const;
-    bool table_claim(uint64_t seq, uint64_t* origin);
-    void grow();       // the table: rehash its live entries (tombstones dropped), single-threaded
-    void grow_ring();  // twice the ring, every live entry placed again, single-threaded
-    std::vector<Slot, TableAlloc<Slot>> ring_;
-    std::vector<Slot, TableAlloc<Slot>> slots_;
-    std::atomic<size_t> n_{0};
-    size_t used_ = 0;   // table: live + tombstones
-    size_t spill_ = 0;  // table entries added since the ring was (re)built
+    jg_tracker* t_ = nullptr;
 };
 
 struct EngineError : std::runtime_error {
@@ -210,17 +144,16 @@ class GpuStableStore {
     // PNCounter's own replica Guid takes column 0 with value 0 (PNCounters.cs:73-81).
     void CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid = Guid{});
 
-    // HandleAfterConsensusUpdates: walk the committed wave in order, skip ManagerMsg_Create and
-    // Guid.Empty (:133-134) and unknown uids (:136), gather the PN-Counter payloads into one pinned
-    // staging buffer for ONE jg_pnc_merge_json, decode the OR-Set payloads into one record batch for
-    // ONE jg_orset_merge, then report the safe updates that completed, in commit order (:141-142).
-    // `tracker` maps message seq -> client origin; matched entries are removed like
-    // ConcurrentDictionary.TryRemove.  A rejected payload throws ApplyError after applying the prefix.
+    // HandleAfterConsensusUpdates (SafeCRDTManager.cs:109-160): the committed wave flattened in commit
+    // order into the jg_commit arrays (uid, syncMsgType, identity, payload pointer + length) and applied by
+    // ONE jg_apply_committed: unknown uids, ManagerMsg_Create and Guid.Empty skipped (:133-136), every state
+    // decoded and merged, the safe updates that completed reported in commit order with their tracker
+    // entries removed (:141-142).  A rejected payload throws ApplyError after the prefix was applied.
     std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker = nullptr);
 
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
     // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the
-    // PROSPECTIVE merge of one received block, one batched engine call per CRDT type.  Creation
+    // PROSPECTIVE merge of one received block, one jg_apply_block call.  Creation
     // messages (RM:300-302) and the key-space set (Guid.Empty) are not CRDT states of this store and
     // are skipped; a CRDT state of an unknown uid throws ApplyError(JG_EINVAL) after merging the
     // states before it (KeyNotFoundException at RM:329); a rejected payload throws like ApplyCommitted.
@@ -263,53 +196,27 @@ class GpuStableStore {
     // ORSetWrapper's enumeration / ORSet.LookupAll (ORSet.cs:204-227) in the reference's order.
     std::vector<std::optional<std::string>> QueryStableLookupAll(const Guid& uid);
 
-    // Key-space sharding over `world` GPUs: the shard owning `uid`.  Every rank
-    // registers only the keys it owns and applies the same committed waves: states of keys it does
-    // not own are skipped exactly like the reference skips unknown uids (SafeCRDTManager.cs:136), so
-    // no state crosses GPUs and the data path needs no collective.
-    static uint32_t ShardOf(const Guid& uid, uint32_t world) {
-        return world <= 1 ? 0u : (uint32_t)((GuidHash()(uid) >> 7) % world);
-    }
-    // Declare this store the shard `rank` of `world`: the apply loop then skips a state of another
-    // shard's uid from the uid alone (ShardOf), without the uid-table and safe-update-tracker lookups —
-    // the same skip the table lookup would make, since a shard registers only the uids it owns.  A
-    // CreateSafeCRDT of a uid outside the shard turns the shortcut off (the table decides again).
-    void SetShard(uint32_t rank, uint32_t world) { shard_rank_ = rank, shard_world_ = world; }
+    // Key-space sharding over `world` GPUs: the shard owning `uid` (jg_shard_of).
+    // Every rank registers only the keys it owns and applies the same committed waves: states of keys
+    // it does not own are skipped exactly like the reference skips unknown uids (SafeCRDTManager.cs:136),
+    // so no state crosses GPUs and the data path needs no collective.
+    static uint32_t ShardOf(const Guid& uid, uint32_t world);
+    // Declare this store the shard `rank` of `world` (jg_node_set_shard): the library's gather then leaves
+    // another shard's states out from the uid alone.
+    void SetShard(uint32_t rank, uint32_t world);
 
     jg_ctx* ctx() const { return ctx_; }
     jg_pnc* pnc() const { return pnc_; }
     uint32_t pnc_row(const Guid& uid) const { return ref(uid, CrdtType::PNCounter).idx; }
-    static int host_threads();  // host workers: JANUS_HOST_THREADS, else min(16, hardware threads)
-    // Wall time of the last ApplyCommitted: host work (classify, gather into pinned staging, OR-Set
-    // decode; JANUS_HOST_THREADS workers) vs the engine calls (H2D + kernels).
-    double last_apply_host_s() const { return host_s_; }
-    double last_apply_engine_s() const { return engine_s_; }
-    uint64_t last_apply_pnc_bytes() const { return pnc_bytes_; }
-    // Cumulative host time at the end of: flatten, classify, gather, OR-Set decode.
-    const double* last_apply_phases_s() const { return phase_s_; }
-    // OR-Set part of the last ApplyCommitted: element interning, record sort, engine merge call.
-    const double* last_apply_orset_phases_s() const { return orset_phase_s_; }
+    // The library's figures for the last ApplyCommitted / ReceivedBlock (jg_node_last_stats), plus the
+    // host mirror's own flatten of the wave into the jg_commit arrays.
+    const jg_apply_stats& last_apply_stats() const { return stats_; }
+    double last_flatten_s() const { return flatten_s_; }
+    uint64_t last_apply_msgs() const { return last_msgs_; }
 
   private:
-    struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id
-    // uid -> KeyRef, open addressing with linear probing: one cache line per lookup on the apply path.
-    class UidTable {
-      public:
-        const KeyRef* find(const Guid& g) const;
-        bool insert(const Guid& g, KeyRef v);  // false if present
-        void prefetch(const Guid& g) const {
-            if (!slots_.empty()) __builtin_prefetch(&slots_[GuidHash()(g) & (slots_.size() - 1)]);
-        }
-      private:
-        struct alignas(32) Slot {  // one cache line holds two slots: a lookup touches one line
-            Guid key;
-            KeyRef val{CrdtType::PNCounter, 0};
-            uint8_t used = 0;
-        };
-        void grow();
-        std::vector<Slot, TableAlloc<Slot>> slots_;
-        size_t n_ = 0;
-    };
+    struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id (queries, ops)
+    std::unordered_map<Guid, KeyRef, GuidHash> uids_;
     struct SetKey {
         std::unordered_map<std::string, uint32_t> elems;  // live interning (reset by Clear), indexed lazily:
         uint32_t indexed = 0;                              // names[indexed..] are live but not in elems yet
@@ -331,35 +238,36 @@ class GpuStableStore {
     void materialize_names();
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;
-    void flush_registrations();             // pending CreateSafeCRDT replica Guids -> jg_pnc_intern
-    // The body of ApplyCommitted / ReceivedBlock over the flattened messages (commit order).
-    std::vector<uint64_t> apply_msgs(const std::vector<const NetworkProtocol*>& msgs, SafeUpdateTracker* tracker, double t0);
-    char* stage(size_t bytes);  // pinned staging of one wave chunk (jg_host_alloc arenas, reused wave after wave)
-    WorkerPool& pool();                     // persistent host workers (host_threads())
+    void flush_registrations();  // pending CreateSafeCRDT registrations -> jg_node_register + jg_pnc_intern
+    // ApplyCommitted / ReceivedBlock: flatten the messages into the jg_commit arrays, one library call.
+    std::vector<uint64_t> apply(const std::vector<const UpdateMessage*>& blocks, SafeUpdateTracker* tracker, bool block_mode);
+    jg::WorkerPool& pool();  // persistent host workers for the flatten
 
     jg_ctx* ctx_ = nullptr;
     jg_pnc* pnc_ = nullptr;
     jg_orset* orset_ = nullptr;
+    jg_node* node_ = nullptr;
     uint32_t max_keys_, R_, eb_;
     uint32_t next_row_ = 0, next_set_ = 0;
-    double host_s_ = 0, engine_s_ = 0, phase_s_[4] = {0, 0, 0, 0}, orset_phase_s_[3] = {0, 0, 0};
-    uint64_t pnc_bytes_ = 0;
-    double avg_msg_bytes_ = 357.0;          // bytes per state message of the last wave (chunk sizing)
-    UidTable uids_;
-    std::vector<uint32_t> reg_rows_;        // CreateSafeCRDT registrations not yet sent
+    std::vector<uint32_t> reg_rows_;  // CreateSafeCRDT registrations not yet sent: PNC stable replica Guids
     std::vector<jg_guid> reg_guids_;
-    std::vector<std::pair<char*, size_t>> arenas_;  // pinned staging arenas (base, bytes)
-    size_t arena_i_ = 0, arena_off_ = 0;            // carve position of the current wave
-    std::vector<uint32_t> cls_, sid_;               // apply_msgs scratch: per message class / set id
-    uint32_t shard_rank_ = 0, shard_world_ = 1;
-    bool foreign_keys_ = false;  // a uid outside the declared shard was registered
-    std::vector<const UpdateMessage*> blocks_;      // ApplyCommitted scratch: the wave's blocks, their
-    std::vector<size_t> block_off_;                 //   first message, the messages in commit order
-    std::vector<const NetworkProtocol*> msgs_;
-    std::vector<uint64_t> where_[2];                //   and per kind, the commit index of its messages
-    std::unique_ptr<WorkerPool> pool_;
+    std::vector<jg_guid> reg_uid_;    // ... and the node's uid table entries
+    std::vector<uint8_t> reg_type_;
+    std::vector<uint32_t> reg_idx_;
+    // the flattened wave (kept across waves: a fresh 40 MB per 1M-message wave cost its page faults)
+    std::vector<size_t> block_off_;
+    std::vector<jg_guid> w_uid_;
+    std::vector<uint8_t> w_type_;
+    std::vector<uint64_t> w_seq_;
+    std::vector<const uint8_t*> w_ptr_;
+    std::vector<uint32_t> w_len_;
+    std::vector<uint64_t> w_done_;  // the library's completions
+    jg_apply_stats stats_{};
+    double flatten_s_ = 0;
+    uint64_t last_msgs_ = 0;
+    std::unique_ptr<jg::WorkerPool> pool_;
     std::vector<SetKey> sets_;
-    std::vector<NetworkProtocol> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167)
+    std::vector<std::pair<NetworkProtocol, bool>> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167): message, tracked
     double last_submit_ms_ = 0;                 // lastSumittedTime
     uint64_t next_seq_ = 1;                     // message identity for the safe-update tracker
 };

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <map>
 #include <memory>
+#include <unordered_set>
 
 #include "digest.hpp"
 #include "janus_host.hpp"
@@ -88,7 +89,9 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
     janus::GpuStableStore gpu_p(0, n_pnc + 1, 8, eb);  // node 0's PROSPECTIVE copies (ApplyOp + block-receipt merges)
     gpu_p.SetNextMessageSeq(nodes[0]->nextSeq);
     std::vector<janus::ClientUpdate> pending;           // node 0's client updates since the last wave
-    janus::SafeUpdateTracker tracker_p;   // node 0's safe messages, as produced on the GPU
+    janus::SafeUpdateTracker tracker_p(gpu_p.ctx());  // node 0's safe messages, as produced on the GPU
+    janus::SafeUpdateTracker tracker(gpu.ctx());      // node 0's safeUpdateTracker, as the stable apply loop sees it
+    std::unordered_set<uint64_t> tracked;             // identities already added to `tracker`
     std::vector<uint8_t> pending_res;                   // the oracle's results for them
     std::vector<std::string> keys;
     for (int k = 0; k < n_pnc + n_set; ++k) {
@@ -141,12 +144,18 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         pending.clear();
         pending_res.clear();
         for (size_t src = 1; src < jw.size(); ++src) gpu_p.ReceivedBlock(jw[src]);  // one block per other node
-        janus::SafeUpdateTracker tracker(nodes[0]->safeUpdateTracker.begin(), nodes[0]->safeUpdateTracker.end());
+        // SafeCRDT.Update's TryAdd of node 0's safe messages since the last wave (SafeCRDT.cs:55-56)
+        for (const auto& kv : nodes[0]->safeUpdateTracker)
+            if (tracked.insert(kv.first).second) tracker.add(kv.first, kv.second);
         const size_t before = nodes[0]->notified.size();
         for (auto& n : nodes) n->HandleAfterConsensusUpdates(wave);
         auto done = gpu.ApplyCommitted(jw, &tracker);
         std::vector<uint64_t> exp(nodes[0]->notified.begin() + before, nodes[0]->notified.end());
         if (done != exp) { std::printf("FAIL safe-update notifications differ (%zu vs %zu)\n", done.size(), exp.size()); return 1; }
+        if (tracker.size() != nodes[0]->safeUpdateTracker.size()) {
+            std::printf("FAIL safe-update tracker holds %zu entries, the oracle's %zu\n", tracker.size(), nodes[0]->safeUpdateTracker.size());
+            return 1;
+        }
         n_done += done.size();
         ++n_waves;
         // the encoded states (GetLastSynchronizedUpdate().Encode()) of every PN-Counter, byte for byte
@@ -306,6 +315,8 @@ int codec_cross_check() {
 int bad_wave() {
     oracle::SafeCRDTManager node(1, 5);
     janus::GpuStableStore gpu(0, 8, 6, 4);
+    janus::SafeUpdateTracker tracker(gpu.ctx());
+    std::unordered_set<uint64_t> tracked;
     std::vector<oracle::SafeCRDT*> keys;
     for (int k = 0; k < 4; ++k) {
         oracle::SafeCRDT& sc = node.CreateSafeCRDT("k" + std::to_string(k), k < 2 ? oracle::CrdtType::PNCounter : oracle::CrdtType::ORSet);
@@ -325,7 +336,8 @@ int bad_wave() {
         for (auto& um : wave[0])
             for (auto& np : um.update)
                 if (seen++ == bad_at) np.bytes = bad_at == 9 ? "{\"pVector\":{}}" : "{\"addSet\":null}";
-        janus::SafeUpdateTracker tracker(node.safeUpdateTracker.begin(), node.safeUpdateTracker.end());
+        for (const auto& kv : node.safeUpdateTracker)
+            if (tracked.insert(kv.first).second) tracker.add(kv.first, kv.second);
         const size_t before = node.notified.size();
         bool othrew = false;
         try { node.HandleAfterConsensusUpdates(wave); } catch (const oracle::json::JsonException&) { othrew = true; }
@@ -354,10 +366,10 @@ int bad_wave() {
                 }
             }
         }
-        // keep the oracle and the GPU in step for the next round: the reference node's tracker keeps
-        // the entries of messages it never applied; so does ours.
-        const auto left = tracker.items();
-        node.safeUpdateTracker = std::unordered_map<uint64_t, uint64_t>(left.begin(), left.end());
+        // the reference node's tracker keeps the entries of messages it never applied; so must ours
+        if (tracker.size() != node.safeUpdateTracker.size()) { std::printf("FAIL bad wave: tracker sizes differ\n"); return 1; }
+        for (const auto& kv : node.safeUpdateTracker)
+            if (!tracker.contains(kv.first)) { std::printf("FAIL bad wave: entry %llu lost\n", (unsigned long long)kv.first); return 1; }
     }
     return 0;
 }

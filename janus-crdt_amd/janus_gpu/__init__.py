@@ -36,6 +36,9 @@ EXPORTS = [
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
     "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256",
+    "jg_node_create", "jg_node_destroy", "jg_node_register", "jg_node_set_shard", "jg_shard_of", "jg_node_last_stats",
+    "jg_tracker_create", "jg_tracker_destroy", "jg_tracker_add", "jg_tracker_size", "jg_tracker_contains",
+    "jg_apply_committed", "jg_apply_block",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -105,6 +108,19 @@ _SIGS = {
     "jg_orset_wave_abort": ([_vp], C.c_int),
     "jg_orset_wave_names": ([_vp, C.POINTER(_u64), C.POINTER(_u64), _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_merge_json": ([_vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
+    "jg_node_create": ([_vp, _vp, C.POINTER(_vp)], C.c_int),
+    "jg_node_destroy": ([_vp], C.c_int),
+    "jg_node_register": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_node_set_shard": ([_vp, _u32, _u32], C.c_int),
+    "jg_shard_of": ([_vp, _u32, C.POINTER(_u32)], C.c_int),
+    "jg_node_last_stats": ([_vp, _vp], C.c_int),
+    "jg_tracker_create": ([_vp, C.POINTER(_vp)], C.c_int),
+    "jg_tracker_destroy": ([_vp], C.c_int),
+    "jg_tracker_add": ([_vp, _u64, _vp, _vp], C.c_int),
+    "jg_tracker_size": ([_vp, C.POINTER(_u64)], C.c_int),
+    "jg_tracker_contains": ([_vp, _u64, _vp, _vp], C.c_int),
+    "jg_apply_committed": ([_vp, _vp, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)], C.c_int),
+    "jg_apply_block": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -576,4 +592,114 @@ class ORSetStore:
     def close(self) -> None:
         if self._h:
             _check(load().jg_orset_destroy(self._h))
+            self._h = _vp()
+
+
+# ---- the committed-wave apply loop (csrc/node.hip) -------------------------------------------------------
+class Commit(C.Structure):
+    """jg_commit: a committed wave in commit order (contiguous payloads: off + bytes)."""
+    _fields_ = [("n", _u64), ("uid", _vp), ("type", _vp), ("seq", _vp), ("off", _vp), ("bytes", _vp), ("ptr", _vp), ("len", _vp)]
+
+
+class ApplyStats(C.Structure):
+    """jg_apply_stats."""
+    _fields_ = [("gather_s", C.c_double), ("device_wait_s", C.c_double), ("total_s", C.c_double), ("device_busy_s", C.c_double),
+                ("msgs_uploaded", _u64), ("bytes_uploaded", _u64), ("msgs_applied", _u64), ("chunks", _u64)]
+
+
+def shard_of(lo: int, hi: int, world: int) -> int:
+    """jg_shard_of: the owner rank of key uid (lo, hi) among `world` GPUs."""
+    g = np.zeros(1, GUID_DTYPE)
+    g["lo"], g["hi"] = lo, hi
+    r = _u32()
+    _check(load().jg_shard_of(_ptr(g), world, C.byref(r)))
+    return r.value
+
+
+class Tracker:
+    """SafeCRDTManager.safeUpdateTracker on the device (jg_tracker)."""
+
+    def __init__(self, ctx: Context):
+        self._h = _vp()
+        _check(load().jg_tracker_create(ctx.handle, C.byref(self._h)))
+
+    def add(self, seq, origin) -> None:
+        s, o = _arr(seq, np.uint64), _arr(origin, np.uint64)
+        _check(load().jg_tracker_add(self._h, s.size, _ptr(s), _ptr(o)))
+
+    def size(self) -> int:
+        n = _u64()
+        _check(load().jg_tracker_size(self._h, C.byref(n)))
+        return n.value
+
+    def contains(self, seq) -> np.ndarray:
+        s = _arr(seq, np.uint64)
+        out = np.zeros(s.size, np.uint8)
+        _check(load().jg_tracker_contains(self._h, s.size, _ptr(s), _ptr(out)))
+        return out
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_tracker_destroy(self._h))
+            self._h = _vp()
+
+
+class Node:
+    """A node's copy of its keys (jg_node) over a PN-Counter and/or an OR-Set store."""
+
+    def __init__(self, pnc: PNCStore | None = None, orset: ORSetStore | None = None):
+        self._h = _vp()
+        self._stores = (pnc, orset)  # keep them alive
+        _check(load().jg_node_create(pnc._h if pnc else None, orset._h if orset else None, C.byref(self._h)))
+
+    def register(self, lo, hi, types, idx) -> None:
+        g = np.empty(np.size(lo), GUID_DTYPE)
+        g["lo"], g["hi"] = lo, hi
+        t, i = _arr(types, np.uint8), _arr(idx, np.uint32)
+        _check(load().jg_node_register(self._h, g.size, _ptr(g), _ptr(t), _ptr(i)))
+
+    def set_shard(self, rank: int, world: int) -> None:
+        _check(load().jg_node_set_shard(self._h, rank, world))
+
+    def _commit(self, lo, hi, types, seqs, msgs=None, data=None, off=None):
+        if msgs is not None:
+            data, off = pack_wave(msgs)
+        g = np.empty(np.size(lo), GUID_DTYPE)
+        g["lo"], g["hi"] = lo, hi
+        t = _arr(types, np.uint8)
+        s = None if seqs is None else _arr(seqs, np.uint64)
+        data = _arr(data, np.uint8)
+        data = data if data.size else np.zeros(16, np.uint8)
+        off = _arr(off, np.uint64)
+        keep = (g, t, s, data, off)
+        c = Commit(g.size, _ptr(g), _ptr(t), _ptr(s), _ptr(off), _ptr(data), None, None)
+        return c, keep
+
+    def apply_committed(self, tracker: Tracker | None, lo, hi, types, seqs, msgs=None, data=None, off=None):
+        """jg_apply_committed: returns (completed origins in commit order, stopped_at or None, code)."""
+        c, keep = self._commit(lo, hi, types, seqs, msgs, data, off)
+        done = np.zeros(max(1, c.n), np.uint64)
+        nd, at = _u64(), _u64()
+        rc = load().jg_apply_committed(self._h, tracker._h if tracker else None, C.byref(c), _ptr(done), C.byref(nd), C.byref(at))
+        if rc != JG_OK and at.value == 2**64 - 1:
+            _check(rc)
+        return done[: nd.value].copy(), (None if at.value == 2**64 - 1 else at.value), rc
+
+    def apply_block(self, lo, hi, types, msgs=None, data=None, off=None):
+        """jg_apply_block: returns (stopped_at or None, code)."""
+        c, keep = self._commit(lo, hi, types, None, msgs, data, off)
+        at = _u64()
+        rc = load().jg_apply_block(self._h, C.byref(c), C.byref(at))
+        if rc != JG_OK and at.value == 2**64 - 1:
+            _check(rc)
+        return (None if at.value == 2**64 - 1 else at.value), rc
+
+    def stats(self) -> dict:
+        st = ApplyStats()
+        _check(load().jg_node_last_stats(self._h, C.byref(st)))
+        return {k: getattr(st, k) for k, _ in ApplyStats._fields_}
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_node_destroy(self._h))
             self._h = _vp()

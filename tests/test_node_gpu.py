@@ -1,0 +1,322 @@
+"""GPU parity of the committed-wave apply loop behind the C ABI (jg_apply_committed / jg_apply_block,
+csrc/node.hip) against the oracle.
+
+The checker restates SafeCRDTManager.HandleAfterConsensusUpdates (BFT-CRDT/CRDTManagers/
+SafeCRDTManager.cs:109-160) over the oracle's per-type stable-apply loops (tests/oracle_ref.py:
+pnc_apply_json = Decode + PNCounter.Merge, orset_apply_json = Decode + ORSet.Merge): skip
+ManagerMsg_Create and Guid.Empty (:133-134) and unknown uids (:136), stop at the first state a Decode /
+Merge rejects (the apply Task faults there), and TryRemove each applied message's identity from the
+tracker, notifying its origin in commit order (:141-142).  Comparisons are exact: every PN-Counter row
+(values and replica columns), the OR-Set record streams with their enumeration order, the completed
+origins in order, the cut, and the entries left in the tracker.
+"""
+import numpy as np
+import pytest
+
+import janus_gpu as jg
+import jsongen as J
+import oracle_ref as orc
+
+pytestmark = pytest.mark.gpu
+
+R, EB = 6, 4
+
+
+class Model:
+    """The oracle node: PN-Counter rows, OR-Set model, uid table, tracker."""
+
+    def __init__(self, n_pnc, rng):
+        self.P = np.zeros((n_pnc, R), np.int32)
+        self.N = np.zeros((n_pnc, R), np.int32)
+        self.cols = np.zeros((n_pnc, R), jg.GUID_DTYPE)
+        self.ncols = np.zeros(n_pnc, np.uint32)
+        own = J.random_guids(rng, n_pnc)  # the stable instance's own replica (column 0, PNCounters.cs:73-81)
+        for k, g in enumerate(own):
+            self.cols[k, 0] = g
+            self.ncols[k] = 1
+        self.own = own
+        self.names, self.state = {}, {}
+        self.keys = {}  # uid -> (type, idx)
+        self.tracker = {}  # seq -> origin (insertion order = dict order)
+
+    def apply(self, wave, block=False):
+        """wave: list of (uid, type, seq, payload).  Returns (completed origins, cut or None)."""
+        live = []  # (commit index, type, idx, payload)
+        cut = None
+        for i, (uid, t, seq, p) in enumerate(wave):
+            if t == 0 or uid == (0, 0):
+                continue
+            if uid not in self.keys:
+                if block:
+                    cut = i
+                    break
+                continue
+            kt, idx = self.keys[uid]
+            ok = orc.json_accepts_pnc(p, EB) if kt == 0 else (
+                (d := orc.json_decode_orset(p)) is not None and all(is_null or tags for _, is_null, _, tags in d))
+            if not ok:
+                cut = i
+                break
+            live.append((i, kt, idx, p, seq))
+        pm = [(idx, p) for _, kt, idx, p, _ in live if kt == 0]
+        if pm:
+            self.P, self.N, self.cols, self.ncols, bad, rc = orc.pnc_apply_json(self.P, self.N, self.cols, self.ncols,
+                                                                                [x[0] for x in pm], [x[1] for x in pm], EB)
+            assert bad is None, "the model's acceptance check disagrees with the oracle's loop"
+        om = [(idx, p) for _, kt, idx, p, _ in live if kt == 1]
+        ea, er, bad, _ = orc.orset_apply_json([x[0] for x in om], [x[1] for x in om], self.names, self.state)
+        assert bad is None
+        self.orset = (ea, er)
+        done = [self.tracker.pop(seq) for _, _, _, _, seq in live if seq in self.tracker]
+        return done, cut
+
+
+def _setup(ctx, rng, n_pnc, n_set):
+    pnc = jg.PNCStore(ctx, n_pnc, R, EB)
+    st = jg.ORSetStore(ctx)
+    node = jg.Node(pnc, st)
+    tr = jg.Tracker(ctx)
+    m = Model(n_pnc, rng)
+    pnc.intern(np.arange(n_pnc), [g[0] for g in m.own], [g[1] for g in m.own])
+    uids = J.random_guids(rng, n_pnc + n_set)
+    types = [0] * n_pnc + [1] * n_set
+    idx = list(range(n_pnc)) + list(range(n_set))
+    node.register([u[0] for u in uids], [u[1] for u in uids], types, idx)
+    for u, t, i in zip(uids, types, idx):
+        m.keys[u] = (t, i)
+    return pnc, st, node, tr, m, uids
+
+
+def _wave(rng, m, uids, n_pnc, n_set, n, pcl, ocl, seq0, bad_at=None, extras=True):
+    """n messages: PN-Counter and OR-Set states of registered keys, plus (extras) creation messages,
+    key-space (Guid.Empty) messages and states of unknown uids.  Half the states are tracked; some
+    identities repeat inside the wave (only the first occurrence completes)."""
+    wave, seqs = [], []
+    for i in range(n):
+        r = rng.random()
+        if extras and r < 0.03:
+            wave.append(((int(rng.integers(1, 2**62)), 5), 1, 0, b'{"pVector":{},"nVector":{}}'))  # unknown uid
+            continue
+        if extras and r < 0.05:
+            wave.append((uids[int(rng.integers(0, len(uids)))], 0, 0, b"junk: ManagerMsg_Create"))  # creation message
+            continue
+        if extras and r < 0.06:
+            wave.append(((0, 0), 1, 0, b"key space"))  # Guid.Empty (the replicated key-space set)
+            continue
+        k = int(rng.integers(0, n_pnc + n_set))
+        if k < n_pnc:
+            p = pcl.message(k)
+        else:
+            sid = k - n_pnc
+            a, rr, na, nr = ocl.state(sid)
+            p = J.encode_orset(a, rr, na, nr)
+        seq = 0
+        if rng.random() < 0.5:
+            if seqs and rng.random() < 0.05:
+                seq = seqs[int(rng.integers(0, len(seqs)))]  # the same message object committed twice
+            else:
+                seq = seq0 + i + 1
+                seqs.append(seq)
+                origin = int(rng.integers(1, 1000))
+                m.tracker[seq] = origin
+        wave.append((uids[k], 1, seq, p))
+    if bad_at is not None:
+        u, t, s, _ = wave[bad_at]
+        wave[bad_at] = (uids[0], 1, s, b'{"pVector":{}}')  # a PNCounterMsg Decode rejects (missing nVector)
+    return wave
+
+
+def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=False, block=False, shard=None):
+    rng = np.random.default_rng(seed)
+    if chunk and monkeypatch:
+        monkeypatch.setenv("JANUS_WAVE_CHUNK", str(chunk))
+        monkeypatch.setenv("JANUS_HOST_PAR_MIN", "1")
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, n_pnc, n_set)
+    if shard:
+        node.set_shard(*shard)
+    pcl = J.Cluster(rng, n_pnc, R - 1, EB, stable=None)
+    ocl = J.ORSetCluster(rng, n_set)
+    added = set()
+    try:
+        for w in range(waves):
+            bad_at = int(rng.integers(0, n)) if bad else None
+            wave = _wave(rng, m, uids, n_pnc, n_set, n, pcl, ocl, seq0=w * 10 * n, bad_at=bad_at, extras=not block)
+            new = [(s, o) for s, o in m.tracker.items() if s not in added]
+            if new:
+                tr.add([s for s, _ in new], [o for _, o in new])
+                added.update(s for s, _ in new)
+            exp_done, exp_cut = m.apply(wave, block=block)
+            lo = [x[0][0] for x in wave]
+            hi = [x[0][1] for x in wave]
+            types = [x[1] for x in wave]
+            seqs = [x[2] for x in wave]
+            msgs = [x[3] for x in wave]
+            if block:
+                cut, rc = node.apply_block(lo, hi, types, msgs)
+                done = []
+            else:
+                done, cut, rc = node.apply_committed(tr, lo, hi, types, seqs, msgs)
+            assert cut == exp_cut, (cut, exp_cut)
+            assert (rc == jg.JG_OK) == (exp_cut is None)
+            assert list(done) == exp_done
+            P, N = pnc.read_rows()
+            assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+            g, nc = pnc.columns(np.arange(n_pnc))
+            assert np.array_equal(nc, m.ncols)
+            assert all(np.array_equal(g[k, :nc[k]], m.cols[k, :nc[k]]) for k in range(n_pnc))
+            ga, gr = st.read()
+            assert orc.same_orset(ga, gr, *m.orset)
+            if not block:
+                assert tr.size() == len(m.tracker)
+                left = list(m.tracker)
+                if left:
+                    assert tr.contains(left).all()
+            s = node.stats()
+            assert s["msgs_applied"] == sum(1 for i, (u, t, _, _) in enumerate(wave)
+                                            if t != 0 and u in m.keys and (exp_cut is None or i < exp_cut))
+            st.names_sync()  # nothing pending: the store's element table is the wave path's own
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()
+
+
+@pytest.mark.parametrize("seed,n_pnc,n_set,waves,n", [(1, 20, 8, 3, 300), (2, 200, 60, 3, 4000), (3, 3000, 500, 2, 30000)])
+def test_mixed_waves_match_oracle(ctx, seed, n_pnc, n_set, waves, n):
+    _run(ctx, seed, n_pnc, n_set, waves, n)
+
+
+def test_mixed_waves_many_chunks(ctx, monkeypatch):
+    """Waves cut into 97-message chunks gathered by every worker: chunk-relative offsets rebased, classify
+    and both parses per chunk, completions across chunks."""
+    _run(ctx, 5, 150, 40, 3, 2500, chunk=97, monkeypatch=monkeypatch)
+
+
+@pytest.mark.parametrize("chunk", [None, 61])
+def test_rejected_state_cuts_the_wave(ctx, monkeypatch, chunk):
+    """A state Decode rejects stops the loop there: the prefix is applied (both kinds) and its completions
+    reported, nothing after it, and the tracker keeps the entries of the messages not applied."""
+    _run(ctx, 7, 80, 30, 4, 1500, chunk=chunk, monkeypatch=monkeypatch, bad=True)
+
+
+def test_block_receipt_unknown_uid(ctx):
+    """jg_apply_block (ReplicationManager.ReceivedUpdateSyncMsg): a CRDT state of an unknown uid stops the
+    block there with JG_EINVAL (KeyNotFoundException), after the states before it."""
+    rng = np.random.default_rng(11)
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, 30, 10)
+    pcl = J.Cluster(rng, 30, R - 1, EB, stable=None)
+    try:
+        wave = [(uids[k], 1, 0, pcl.message(k)) for k in rng.integers(0, 30, 200).tolist()]
+        wave[120] = ((123, 456), 1, 0, b'{"pVector":{},"nVector":{}}')
+        exp_done, exp_cut = m.apply(wave, block=True)
+        cut, rc = node.apply_block([x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], [x[3] for x in wave])
+        assert cut == exp_cut == 120 and rc == jg.JG_EINVAL
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()
+
+
+def test_shard_shortcut_matches_the_table(ctx):
+    """A node declared shard r of w gathers only its shard's states (jg_shard_of): the same result as the
+    uid table's skip.  A registered uid of another shard turns the shortcut off, and set_shard rescans."""
+    rng = np.random.default_rng(13)
+    world = 3
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, 40, 12)
+    try:
+        mine = [u for u in uids if jg.shard_of(u[0], u[1], world) == 1]
+        assert 0 < len(mine) < len(uids)
+        node.set_shard(1, world)  # foreign uids are registered: the shortcut stays off
+        pcl = J.Cluster(rng, 40, R - 1, EB, stable=None)
+        ocl = J.ORSetCluster(rng, 12)
+        wave = _wave(rng, m, uids, 40, 12, 800, pcl, ocl, seq0=0)
+        exp_done, exp_cut = m.apply(wave)
+        done, cut, rc = node.apply_committed(None, [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], None,
+                                             [x[3] for x in wave])
+        assert cut is None and rc == jg.JG_OK
+        s = node.stats()
+        assert s["msgs_uploaded"] == len(wave)  # the table decided
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()
+    # a node that holds only its shard's keys: the gather drops the other shards' states
+    rng = np.random.default_rng(14)
+    pnc = jg.PNCStore(ctx, 40, R, EB)
+    node = jg.Node(pnc, None)
+    try:
+        keys = J.random_guids(rng, 120)
+        own = [k for k in keys if jg.shard_of(k[0], k[1], world) == 2][:40]
+        node.register([k[0] for k in own], [k[1] for k in own], [0] * len(own), list(range(len(own))))
+        node.set_shard(2, world)
+        msgs, lo, hi = [], [], []
+        for i in range(600):
+            k = keys[int(rng.integers(0, len(keys)))]
+            lo.append(k[0])
+            hi.append(k[1])
+            msgs.append(J.encode_pnc([(5, 7)], [i], [0]))
+        done, cut, rc = node.apply_committed(None, lo, hi, [1] * len(msgs), None, msgs)
+        assert cut is None
+        s = node.stats()
+        kept = sum(1 for a, b in zip(lo, hi) if jg.shard_of(a, b, world) == 2)
+        assert s["msgs_uploaded"] == kept < len(msgs)
+        mine = {k: i for i, k in enumerate(own)}
+        exp = np.zeros(len(own), np.int64)
+        for a, b, i in zip(lo, hi, range(600)):
+            if (a, b) in mine:
+                exp[mine[(a, b)]] = max(exp[mine[(a, b)]], i)
+        assert s["msgs_applied"] == sum(1 for a, b in zip(lo, hi) if (a, b) in mine)
+        v, o = pnc.values(np.arange(len(own)))
+        assert np.array_equal(v, exp)
+    finally:
+        node.close()
+        pnc.close()
+
+
+def test_tracker_add_contains_and_growth(ctx):
+    """TryAdd / ContainsKey / Count of the device tracker, an identity added twice kept once, and the
+    table rebuilt (tombstones dropped) as waves complete and new entries arrive."""
+    tr = jg.Tracker(ctx)
+    pnc = jg.PNCStore(ctx, 4, R, EB)
+    node = jg.Node(pnc, None)
+    try:
+        tr.add([5, 6, 7], [50, 60, 70])
+        tr.add([6], [99])  # TryAdd of a present identity: false, the first origin stays
+        assert tr.size() == 3
+        assert list(tr.contains([5, 6, 7, 8])) == [1, 1, 1, 0]
+        u = (0xABC, 0xDEF)
+        node.register([u[0]], [u[1]], [0], [0])
+        live = {5: 50, 6: 60, 7: 70}
+        seq = 100
+        for w in range(6):
+            new = list(range(seq, seq + 20000))
+            seq += 20000
+            tr.add(new, [s % 997 + 1 for s in new])
+            live.update({s: s % 997 + 1 for s in new})
+            take = [s for i, s in enumerate(list(live)) if i % 3 != 1]
+            msgs = [J.encode_pnc([(1, 2)], [1], [0])] * len(take)
+            done, cut, rc = node.apply_committed(tr, [u[0]] * len(take), [u[1]] * len(take), [1] * len(take), take, msgs)
+            assert list(done) == [live.pop(s) for s in take]
+            assert tr.size() == len(live)
+        rest = list(live)
+        assert tr.contains(rest).all() and not tr.contains(take).any()
+    finally:
+        node.close()
+        pnc.close()
+        tr.close()
+
+
+def test_register_rejects_bad_keys(ctx):
+    pnc = jg.PNCStore(ctx, 4, R, EB)
+    node = jg.Node(pnc, None)
+    try:
+        node.register([1], [2], [0], [0])
+        for lo, hi, t, i in ([0], [0], [0], [1]), ([1], [2], [0], [1]), ([3], [4], [0], [4]), ([3], [4], [1], [0]), ([3, 3], [4, 4], [0, 0], [1, 2]):
+            with pytest.raises(jg.JanusError) as e:
+                node.register(lo, hi, t, i)
+            assert e.value.code == jg.JG_EINVAL
+        node.register([3], [4], [0], [1])  # nothing of the rejected calls was registered
+    finally:
+        node.close()
+        pnc.close()
