@@ -79,6 +79,14 @@ class Sync:
         if self.dist:
             self.dist.barrier()
 
+    def broadcast_bytes(self, b: bytes) -> bytes:
+        """Rank 0's bytes on every rank (the RCCL unique id of the library's own communicator)."""
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
     def max(self, x: float) -> float:
         if not self.dist:
             return x
@@ -241,15 +249,13 @@ EXCH_KEYS, EXCH_ROWS = 2_000_000, 1_000_000  # per rank: owned shard, received b
 
 def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
     """Cross-shard exchange: every rank receives a batch of EXCH_ROWS PN-Counter
-    rows whose keys are uniform over the WHOLE keyspace (world x EXCH_KEYS), routes it on its GPU
-    (jg_rows_route), exchanges the runs with one RCCL all-to-all per buffer over xGMI, and merges what
-    it owns from device memory (jg_pnc_merge_device).  At world 1 there is nothing to exchange: route +
-    merge only."""
+    rows whose keys are uniform over the WHOLE keyspace (world x EXCH_KEYS) and makes one
+    jg_pnc_exchange on the library's own RCCL communicator (csrc/comm.hip): route on its GPU, counts
+    all-gather, grouped ncclSend/ncclRecv of the runs over xGMI, merge of what it owns from device memory.
+    At world 1 the runs stay on the device (route + copy + merge)."""
     import numpy as np
-    import torch
-    from janus_gpu import shard
-    dev = torch.device("cuda", local)
-    ex = shard.Exchange(dev) if world > 1 else None
+    uid = sync.broadcast_bytes(jg.comm_unique_id() if rank == 0 else b"")
+    comm = jg.Comm(ctx, rank, world, uid)
     store = jg.PNCStore(ctx, EXCH_KEYS, PNC_R, PNC_EB)
     rows = jg.Rows(ctx, EXCH_ROWS, PNC_R, PNC_EB)
     try:
@@ -259,7 +265,10 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
         rows.upload(zeros, zeros, keys)   # the key indices; values synthesised on the device next
         rows.synth(SEED + 11 + rank)
         last = {}
-        wall, _ = timed(ctx, sync, lambda: last.update(shard.exchange_pnc(store, rows, ex, dev)), steps, warmup)
+        wall, _ = timed(ctx, sync, lambda: last.update(comm.exchange_pnc(store, rows)), steps, warmup)
+        st = comm.stats()
+        phases = {"route_ms": st.route_s * 1e3, "counts_and_runs_ms": st.exchange_s * 1e3, "merge_ms": st.merge_s * 1e3,
+                  "link_bytes_sent": int(st.bytes_sent), "link_bytes_received": int(st.bytes_received)}
         # the owner-side merge alone (jg_pnc_merge_batch with key indices: k_group_link + k_merge_grouped +
         # the list heads reset) on a batch of the same shape with keys in this rank's shard
         lkeys = keys % EXCH_KEYS
@@ -269,6 +278,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
     finally:
         store.close()
         rows.close()
+        comm.close()
     row_bytes = 4 + 2 * PNC_R * PNC_EB
     distinct = int(np.unique(lkeys).size)
     merge_alg = EXCH_ROWS * row_bytes + distinct * 4 * PNC_R * PNC_EB  # every row read; each distinct key's A row (P, N) read + written once
@@ -276,16 +286,14 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
     sent = last["sent"].astype(np.int64)
     remote = int(sent.sum() - sent[rank]) if world > 1 else 0
     return {"workload": f"cross-shard exchange: {EXCH_ROWS} received PN-Counter rows per rank (64 replicas, int64, keys "
-                        f"uniform over {world} x {EXCH_KEYS} keys): route + all-to-all + merge from device memory",
+                        f"uniform over {world} x {EXCH_KEYS} keys): jg_pnc_exchange = route + RCCL send/recv + merge",
             "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
-            "xgmi_bytes_per_rank": remote * row_bytes, "row_bytes": row_bytes,
+            "xgmi_bytes_per_rank": remote * row_bytes, "row_bytes": row_bytes, "last_step": phases,
             "merge": {"kernels": "k_group_link + k_merge_grouped<8,4>", "ms": merge_s * 1e3,
                       "distinct_keys": distinct,
                       "roofline": {"bound": "hbm", "achieved": merge_alg / merge_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": merge_alg / merge_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": merge_alg}},
-            "collective": ("none (world 1)" if world == 1 else
-                           "torch.distributed all_to_all_single, host-staged (gloo rehearsal)" if ex.staged else
-                           "torch.distributed all_to_all_single over RCCL (xGMI)")}
+            "collective": f"library RCCL communicator (jg_comm), world {world}: ncclAllGather of the counts + grouped ncclSend/ncclRecv"}
 
 
 JSON_MSGS, JSON_KEYS, JSON_R, JSON_EB, JSON_NODES = 1_000_000, 1_000_000, 5, 4, 4  # one C5 wave, device-resident

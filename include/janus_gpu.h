@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 3
+#define JG_ABI_VERSION 4
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -365,6 +365,35 @@ int jg_orset_route(jg_orset* s, uint32_t world, uint64_t* add_counts, uint64_t* 
  * order: run r is the r-th state merged (its ords order its own records, jg_tagrec.ord). */
 int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, const uint64_t* rem_counts, const void* d_add_key,
                           const void* d_add_tag, const void* d_add_ord, const void* d_rem_key, const void* d_rem_tag, const void* d_rem_ord);
+
+/* The exchange itself, inside the library over RCCL (csrc/comm.hip): one communicator per process (one
+ * rank per GPU of the node), then one call per received batch does route -> all-gather of the counts ->
+ * grouped ncclSend/ncclRecv of every run over the xGMI peer links (this rank's own run by a device copy)
+ * -> merge of the received runs in source-rank order.  Collective: every rank of the communicator makes
+ * the same exchange call (a rank with nothing received passes an empty batch / store). */
+typedef struct jg_comm jg_comm;
+/* ncclGetUniqueId into id[128]: made by one rank and handed to the others over the caller's own channel. */
+int jg_comm_unique_id(uint8_t* id);
+/* ncclCommInitRank on ctx's device: blocks until all `world` ranks have joined with the same id. */
+int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, jg_comm** out);
+int jg_comm_destroy(jg_comm* comm);
+/* PNCounter.Merge (PNCounters.cs:131-144) of a received batch on the owners of its keys: rows is this
+ * rank's batch in GLOBAL keys (row key k goes to rank k % world as local key k / world), store this
+ * rank's shard (rows NULL: this rank sends nothing).  sent[world] / received[world] (optional): rows per
+ * destination / per source. */
+int jg_pnc_exchange(jg_comm* comm, jg_pnc* store, const jg_rows* rows, uint64_t* sent, uint64_t* received);
+/* ORSet.Merge (ORSet.cs:253-283) of a received state (global set ids: set s goes to rank s % world as
+ * s / world) on the owners: the runs merged into store in source-rank order (jg_orset_merge_device).
+ * Per-destination / per-source record counts of both streams (optional, world entries each). */
+int jg_orset_exchange(jg_comm* comm, jg_orset* store, jg_orset* received, uint64_t* sent_add, uint64_t* sent_rem, uint64_t* recv_add,
+                      uint64_t* recv_rem);
+/* Figures of the communicator's last exchange: device seconds of route, counts + runs, merge (hipEvents on
+ * the context's stream); bytes that left / reached this rank over the links; records merged. */
+typedef struct jg_exchange_stats {
+    double route_s, exchange_s, merge_s;
+    uint64_t bytes_sent, bytes_received, records_received;
+} jg_exchange_stats;
+int jg_comm_last_stats(jg_comm* comm, jg_exchange_stats* out);
 
 /* ---------------------------------------------------------------------------------------------
  * UpdateMessage digests (csrc/digest.hip) — replaces UpdateMessage.ComputeDigest

@@ -52,6 +52,17 @@ struct Guid16 { unsigned long long lo, hi; };
 
 using jgw::Cursor;  // byte cursor with a 16-byte aligned window (wire_cursor.hpp)
 using jgw::hexv;
+using jgw::wave_sync;  // SWAR / LDS helpers shared with orset_wire.hip
+using jgw::zero_bytes;
+using jgw::ge_bytes;
+using jgw::le_bytes;
+using jgw::digit_bytes;
+using jgw::bits4;
+using jgw::hex4;
+using jgw::hex_pairs;
+using jgw::hex_be16;
+using jgw::hex_le16;
+using jgw::lds_words;
 
 // 36-char "D" Guid (Guid.ToString() layout: b3b2b1b0-b5b4-b7b6-b8b9-b10..b15) + the closing quote.
 __device__ __forceinline__ bool read_guid(Cursor& c, Guid16& g) {

@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "jg_internal.hpp"
@@ -391,9 +392,9 @@ struct ParseVis {
 __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                      uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, unsigned long long* __restrict__ ne,
                                                      unsigned long long* __restrict__ nt, uint32_t* __restrict__ na,
-                                                     unsigned long long* __restrict__ err) {
+                                                     unsigned long long* __restrict__ err, const uint8_t* __restrict__ slow) {
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (m >= m1) return;
+    if (m >= m1 || (slow && !slow[m])) return;  // slow: the messages k_ow_group left to the serial parse
     if (mset[m] == jg::kSkipIdx) {  // another kind's message in a node wave (csrc/node.hip)
         ne[m] = nt[m] = 0;
         na[m] = 0;
@@ -411,6 +412,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes
     na[m] = v.n_add | (v.rem_first ? 0x80000000u : 0u);
     err[m] = e;
 }
+
+#include "orset_group.hpp"
 
 __global__ void k_ow_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -817,7 +820,7 @@ struct jg_orset_wire {
     jg::DevBuf tab, nset, nid, ngen, nlen, noff, nkey, pool, set_gen, next_id;
     uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
     // open wave: payload, offsets, set per message, per-message counts / errors
-    jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff;
+    jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff, slow;  // slow: k_ow_group's per-message flags
     // the wave's payload / offsets / set ids: the buffers above (jg_orset_wave_*), or a node's
     // (csrc/node.hip: every kind's messages uploaded once, set id kSkipIdx for another kind's)
     uint8_t* vbytes = nullptr;
@@ -960,6 +963,7 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
         grow_keep(ctx, w->nt, (cap + 1) * 8, m * 8);
         grow_keep(ctx, w->na, cap * 4, m * 4);
         grow_keep(ctx, w->err, cap * 8, m * 8);
+        grow_keep(ctx, w->slow, cap, m);
         w->cap_msgs = cap;
     }
     if (bytes > w->cap_bytes) {
@@ -1001,11 +1005,28 @@ Entries entries_of(jg_orset_wire* w) {
 }
 
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
+// One wave per message (k_ow_group, orset_group.hpp), then the serial parse of the messages it left;
+// JANUS_ORSET_PARSE=serial runs the serial parse alone, =group the group parse alone (read per chunk: tests
+// switch it).
 void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
     if (m1 <= m0) return;
-    hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(m1 - m0)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff, w->vmset, m0, m1, sparse_of(w),
-                       w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
-                       w->err.as<unsigned long long>());
+    const char* e = std::getenv("JANUS_ORSET_PARSE");
+    const bool serial = e && std::strcmp(e, "serial") == 0, strict = e && std::strcmp(e, "group") == 0;
+    uint8_t* slow = nullptr;
+    if (!serial) {
+        slow = w->slow.as<uint8_t>();
+        hipLaunchKernelGGL(k_ow_group, dim3((unsigned)((m1 - m0 + kOgWaves - 1) / kOgWaves)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff,
+                           w->vmset, m0, m1, sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
+                           w->na.as<uint32_t>(), w->err.as<unsigned long long>(), slow);
+        JG_HIP(hipGetLastError());
+    }
+    if (strict)
+        hipLaunchKernelGGL(k_ow_reject_slow, dim3(blocks_for(m1 - m0)), dim3(kBlock), 0, ctx->stream, slow, m0, m1, w->ne.as<unsigned long long>(),
+                           w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->err.as<unsigned long long>());
+    else
+        hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(m1 - m0)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff, w->vmset, m0, m1,
+                           sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
+                           w->err.as<unsigned long long>(), slow);
     JG_HIP(hipGetLastError());
 }
 

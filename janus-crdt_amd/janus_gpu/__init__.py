@@ -39,6 +39,7 @@ EXPORTS = [
     "jg_node_create", "jg_node_destroy", "jg_node_register", "jg_node_set_shard", "jg_shard_of", "jg_node_last_stats",
     "jg_tracker_create", "jg_tracker_destroy", "jg_tracker_add", "jg_tracker_size", "jg_tracker_contains",
     "jg_apply_committed", "jg_apply_block",
+    "jg_comm_unique_id", "jg_comm_init", "jg_comm_destroy", "jg_pnc_exchange", "jg_orset_exchange", "jg_comm_last_stats",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -121,6 +122,12 @@ _SIGS = {
     "jg_tracker_contains": ([_vp, _u64, _vp, _vp], C.c_int),
     "jg_apply_committed": ([_vp, _vp, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)], C.c_int),
     "jg_apply_block": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
+    "jg_comm_unique_id": ([_vp], C.c_int),
+    "jg_comm_init": ([_vp, _u32, _u32, _vp, C.POINTER(_vp)], C.c_int),
+    "jg_comm_destroy": ([_vp], C.c_int),
+    "jg_pnc_exchange": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_exchange": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_comm_last_stats": ([_vp, _vp], C.c_int),
 }
 GUID_DTYPE = np.dtype([("lo", "<u8"), ("hi", "<u8")])  # jg_guid
 
@@ -703,3 +710,55 @@ class Node:
         if self._h:
             _check(load().jg_node_destroy(self._h))
             self._h = _vp()
+
+
+class ExchangeStats(C.Structure):
+    """jg_exchange_stats: device seconds of route / counts + runs / merge, link bytes, records merged."""
+    _fields_ = [("route_s", C.c_double), ("exchange_s", C.c_double), ("merge_s", C.c_double),
+                ("bytes_sent", C.c_uint64), ("bytes_received", C.c_uint64), ("records_received", C.c_uint64)]
+
+
+def comm_unique_id() -> bytes:
+    """jg_comm_unique_id: a fresh 128-byte RCCL unique id (made by one rank, handed to the others)."""
+    buf = (C.c_uint8 * 128)()
+    _check(load().jg_comm_unique_id(C.cast(buf, _vp)))
+    return bytes(buf)
+
+
+class Comm:
+    """The library's own RCCL communicator (jg_comm_init, csrc/comm.hip): one per process, one rank per GPU.
+    exchange_pnc / exchange_orset route a received batch / state by owner, move the runs over RCCL and
+    merge what this rank owns — the whole cross-shard exchange inside the library."""
+
+    def __init__(self, ctx: Context, rank: int, world: int, uid: bytes):
+        assert len(uid) == 128
+        self._h = _vp()
+        self.rank, self.world = rank, world
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(load().jg_comm_init(ctx.handle, rank, world, C.cast(buf, _vp), C.byref(self._h)))
+
+    def exchange_pnc(self, store, rows):
+        sent, got = np.zeros(self.world, np.uint64), np.zeros(self.world, np.uint64)
+        _check(load().jg_pnc_exchange(self._h, store._h, rows._h if rows is not None else None, _ptr(sent), _ptr(got)))
+        return {"sent": sent, "received": got}
+
+    def exchange_orset(self, store, received):
+        v = [np.zeros(self.world, np.uint64) for _ in range(4)]
+        _check(load().jg_orset_exchange(self._h, store._h, received._h, *(_ptr(x) for x in v)))
+        return {"sent": (v[0], v[1]), "received": (v[2], v[3])}
+
+    def stats(self) -> ExchangeStats:
+        st = ExchangeStats()
+        _check(load().jg_comm_last_stats(self._h, C.cast(C.byref(st), _vp)))
+        return st
+
+    def close(self) -> None:
+        if self._h:
+            _check(load().jg_comm_destroy(self._h))
+            self._h = _vp()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

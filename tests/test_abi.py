@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(str(jg.LIB_PATH))
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.jg_abi_version() == 3  # v3: the committed-wave apply loop (jg_node, jg_tracker, jg_apply_committed)
+    assert lib.jg_abi_version() == 4  # v4: the RCCL exchange inside the library (jg_comm, jg_pnc_exchange, jg_orset_exchange)
 
 
 def test_library_is_gfx950_only():

@@ -65,9 +65,125 @@ def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3)
         s.close()
 
 
+PARSE = ["group", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
+
+
+@pytest.mark.parametrize("parse", PARSE)
 @pytest.mark.parametrize("seed,n_sets,waves,per_wave", [(1, 3, 3, 40), (2, 64, 3, 600), (3, 500, 2, 3000)])
-def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave):
+def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave, parse, monkeypatch):
+    monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
     _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default", "raw", "all"))
+
+
+@pytest.mark.parametrize("parse", ["group", "default"])
+def test_compact_waves_match_oracle(ctx, parse, monkeypatch):
+    """Reference-shaped compact states only (ASCII names, no whitespace, members in the encoder's order):
+    every message takes the group parse (JANUS_ORSET_PARSE=group rejects any message it leaves)."""
+    if parse == "group":
+        monkeypatch.setenv("JANUS_ORSET_PARSE", "group")
+    rng = np.random.default_rng(11)
+    s = jg.ORSetStore(ctx)
+    model, state = {}, {}
+    try:
+        for w in range(3):
+            sets, msgs = [], []
+            for i in range(2000):
+                sid = int(rng.integers(0, 50))
+                nel = int(rng.integers(0, 40))
+                add = [(f"e{sid}_{j}", J.random_guids(rng, int(rng.integers(1, 3)))) for j in range(nel)]
+                rem = [(e, ts[:1]) for e, ts in add if rng.random() < 0.3]
+                na = J.random_guids(rng, int(rng.integers(0, 3)))
+                nr = na[:int(rng.integers(0, len(na) + 1))]
+                msgs.append(J.encode_orset(add, rem, na, nr, upper=i % 9 == 4))
+                sets.append(sid)
+            before = _copy(model)
+            ea, er, bad, _ = orc.orset_apply_json(sets, msgs, model, state)
+            assert bad is None
+            rc, first_bad = s.wave([(sets[:700], msgs[:700]), (sets[700:], msgs[700:])])
+            assert rc == jg.JG_OK and first_bad is None
+            assert s.wave_names() == _model_names(model, before)
+            ga, gr = s.read()
+            assert orc.same_orset(ga, gr, ea, er)
+    finally:
+        s.close()
+
+
+def _mutants(rng, base, n):
+    """Single-byte edits of a payload: replace, delete or insert one byte at a random position."""
+    alphabet = b'"{}[]:, \\a0-Gf\x00\xc3\t'
+    out = []
+    for _ in range(n):
+        p = int(rng.integers(0, len(base)))
+        ch = bytes([alphabet[int(rng.integers(0, len(alphabet)))]])
+        kind = int(rng.integers(0, 3))
+        out.append(base[:p] + ch + base[p + 1:] if kind == 0 else base[:p] + base[p + 1:] if kind == 1 else base[:p] + ch + base[p:])
+    return out
+
+
+def test_group_parse_mutants_equal_serial(ctx, monkeypatch):
+    """Single-byte mutants of compact reference-shaped states, each merged on its own (one-shot calls, all or
+    nothing) into a store per parse mode: the group parse (which proves a payload compact or hands it to the
+    serial parse) ends with the same error codes, first bad messages, element ids and records as the serial
+    parse alone.  Mutants that stay valid (a changed hex digit, name byte...) are merged by both."""
+    rng = np.random.default_rng(12)
+    bases = [J.encode_orset([("abcde", [G1]), ("x", [G2, G3])], [("x", [G2])], [G3], []),
+             J.encode_orset([], [], [], []),
+             J.encode_orset([("k", [G1])], [], [G2], [G2]),
+             J.encode_orset([(f"n{j}", [G1, G2]) for j in range(6)], [("n1", [G1])], [], [G3])]
+    muts = [m for b in bases for m in _mutants(rng, b, 160)] + bases
+    results = {}
+    for mode in PARSE:
+        monkeypatch.setenv("JANUS_ORSET_PARSE", mode)
+        s = jg.ORSetStore(ctx)
+        try:
+            codes = []
+            for i, m in enumerate(muts):
+                try:
+                    s.merge_json([i], [m])
+                    codes.append((0, None))
+                except jg.JanusError as e:
+                    codes.append((e.code, e.bad_msg))
+            results[mode] = (codes, s.read())
+        finally:
+            s.close()
+    (cg, rg), (cs, rs) = results["group"], results["serial"]
+    assert cg == cs
+    assert all(np.array_equal(x, y) for x, y in zip(rg, rs))
+    assert sum(c == (0, None) for c in cg) > len(bases)  # some mutants stayed valid
+    # the unmutated bases are compact: the group parse alone takes them
+    monkeypatch.setenv("JANUS_ORSET_PARSE", "group")
+    s = jg.ORSetStore(ctx)
+    try:
+        s.merge_json(list(range(len(bases))), bases)
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("parse", PARSE)
+def test_group_parse_size_limits(ctx, parse, monkeypatch):
+    """States around the group parse's limits (4096 bytes with the 16-byte alignment offset, 192 string
+    tokens): the ones past them take the serial parse, with the same result as the oracle."""
+    monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
+    rng = np.random.default_rng(13)
+    msgs, sets = [], []
+    for nel in (60, 75, 80, 84, 85, 86, 90, 95, 120):  # "eNN":[guid] = 47-48 bytes per element
+        add = [(f"e{j:02d}", J.random_guids(rng, 1)) for j in range(nel)]
+        msgs.append(J.encode_orset(add, [], [], []))
+        sets.append(len(sets))
+    for nt in (90, 95, 100, 110):  # null tags: 39 bytes each, one token each
+        msgs.append(J.encode_orset([], [], J.random_guids(rng, nt), []))
+        sets.append(len(sets))
+    assert min(len(m) for m in msgs) < 4080 < max(len(m) for m in msgs)
+    ea, er, bad, _ = orc.orset_apply_json(sets, msgs)
+    assert bad is None
+    s = jg.ORSetStore(ctx)
+    try:
+        rc, first_bad = s.wave([(sets, msgs)])
+        assert rc == jg.JG_OK and first_bad is None
+        ga, gr = s.read()
+        assert orc.same_orset(ga, gr, ea, er)
+    finally:
+        s.close()
 
 
 def test_hash_collisions_take_the_exact_path(ctx, monkeypatch):
@@ -150,10 +266,12 @@ _CASES = [
 ]
 
 
+@pytest.mark.parametrize("parse", PARSE)
 @pytest.mark.parametrize("idx", range(len(_CASES)))
-def test_contract_case_in_a_wave(ctx, idx):
+def test_contract_case_in_a_wave(ctx, idx, parse, monkeypatch):
     """Case payload at position 3 of a 6-message wave: the first bad message and its code, then the
     prefix before it merges exactly as the oracle's loop leaves the store."""
+    monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
     payload, code = _CASES[idx]
     dec = orc.json_decode_orset(payload)
     if code is None:

@@ -395,3 +395,69 @@ def test_rccl_exchange_world1():
             p.kill()
     assert not err, err
     assert ok
+
+
+# ---- the exchange inside the library (jg_comm over RCCL, csrc/comm.hip) at world size 1 ----
+def test_native_exchange_world1(ctx):
+    """jg_pnc_exchange / jg_orset_exchange on a one-rank communicator: route, RCCL counts all-gather, the
+    rank's own run copied into place, merge — bit-exact against the oracle's Merge of the whole batch."""
+    rng = np.random.default_rng(21)
+    K, R, n = 700, 64, 4000
+    AP, AN = random_pnc(rng, K, R, 8, absent=False, lo=0), random_pnc(rng, K, R, 8, absent=False, lo=0)
+    k, P, N = rng.integers(0, K, n).astype(np.uint32), random_pnc(rng, n, R, 8), random_pnc(rng, n, R, 8)
+    La, Lr, Ra, Rr = random_orset_pair(rng, n_sets=60, n_elems=20, pool=10)
+    with jg.Comm(ctx, 0, 1, jg.comm_unique_id()) as cm:
+        s = jg.PNCStore(ctx, K, R, 8)
+        rows = jg.Rows(ctx, n, R, 8)
+        o, src = jg.ORSetStore(ctx, 0, 0), jg.ORSetStore(ctx, 0, 0)
+        try:
+            s.write_rows(AP, AN)
+            rows.upload(P, N, k)
+            out = cm.exchange_pnc(s, rows)
+            assert out["sent"].tolist() == [n] and out["received"].tolist() == [n]
+            st = cm.stats()
+            assert st.records_received == n and st.bytes_sent == 0 and st.bytes_received == 0
+            gP, gN = s.read_rows()
+            eP, eN = orc.pnc_merge(AP, AN, P, N, k)
+            assert np.array_equal(gP, eP) and np.array_equal(gN, eN)
+            # a batch of another shape is rejected before anything moves
+            bad = jg.Rows(ctx, 10, 32, 8)
+            try:
+                with pytest.raises(jg.JanusError) as ei:
+                    cm.exchange_pnc(s, bad)
+                assert ei.value.code == jg.JG_EINVAL
+            finally:
+                bad.close()
+            o.load(La, Lr)
+            src.load(Ra, Rr)
+            out = cm.exchange_orset(o, src)
+            assert out["received"][0].tolist() == [len(Ra)] and out["received"][1].tolist() == [len(Rr)]
+            ga, gr = o.read()
+            ea, er = orc.orset_merge(La, Lr, Ra, Rr)
+            assert orc.same_orset(ga, gr, ea, er)
+            with pytest.raises(jg.JanusError):
+                cm.exchange_orset(o, o)
+        finally:
+            for h in (s, rows, o, src):
+                h.close()
+
+
+def test_native_exchange_of_empty_batches(ctx):
+    with jg.Comm(ctx, 0, 1, jg.comm_unique_id()) as cm:
+        s = jg.PNCStore(ctx, 10, 8, 4)
+        o, src = jg.ORSetStore(ctx, 0, 0), jg.ORSetStore(ctx, 0, 0)
+        try:
+            assert cm.exchange_pnc(s, None)["received"].tolist() == [0]  # a rank that received nothing
+            assert cm.exchange_orset(o, src)["received"][0].tolist() == [0]
+            assert [len(x) for x in o.read()] == [0, 0]
+        finally:
+            for h in (s, o, src):
+                h.close()
+
+
+def test_comm_init_rejects_bad_ranks(ctx):
+    uid = jg.comm_unique_id()
+    for rank, world in ((1, 1), (0, 0), (0, 65)):
+        with pytest.raises(jg.JanusError) as ei:
+            jg.Comm(ctx, rank, world, uid)
+        assert ei.value.code == jg.JG_EINVAL
