@@ -228,19 +228,33 @@ def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2", scaling="we
             "keys": n_keys, "keys_total": keys_total, "cells_total": keys_total * R, "R": R}
 
 
-def bench_orset(jg, ctx, sync, rank, world, steps, warmup):
+ORSET_STRONG_SHARDS = 8  # strong scaling: the C3 shape x 8 shards (80M (set, elem) groups) split over the ranks
+
+
+def orset_groups(scaling: str, rank: int, world: int) -> int:
+    """(set, elem) groups on this rank.  weak: a full C3 shard per rank (1M sets); strong: C3 x 8 shards
+    split into `world` parts ("the same for OR-Set with the C3 shape x 8 shards")."""
+    if scaling != "strong":
+        return ORSET_GROUPS
+    total = ORSET_STRONG_SHARDS * ORSET_GROUPS
+    base, extra = divmod(total // ORSET_E, world)  # whole sets per rank
+    return (base + (1 if rank < extra else 0)) * ORSET_E
+
+
+def bench_orset(jg, ctx, sync, rank, world, steps, warmup, scaling="weak"):
+    groups = orset_groups(scaling, rank, world)
     L = jg.ORSetStore(ctx, 0, 0)
     R = jg.ORSetStore(ctx, 0, 0)
-    na, nr = ORSET_GROUPS * ORSET_ADD, ORSET_GROUPS * ORSET_REM
+    na, nr = groups * ORSET_ADD, groups * ORSET_REM
     out = jg.ORSetStore(ctx, 2 * na, 2 * nr)
-    L.synth(SEED + rank, ORSET_GROUPS, ORSET_E, ORSET_ADD, 0, ORSET_REM, 0)
-    R.synth(SEED + rank, ORSET_GROUPS, ORSET_E, ORSET_ADD, ORSET_ADD - ORSET_ADD_OV, ORSET_REM, ORSET_REM - ORSET_REM_OV)
+    L.synth(SEED + rank, groups, ORSET_E, ORSET_ADD, 0, ORSET_REM, 0)
+    R.synth(SEED + rank, groups, ORSET_E, ORSET_ADD, ORSET_ADD - ORSET_ADD_OV, ORSET_REM, ORSET_REM - ORSET_REM_OV)
     wall, ev = timed(ctx, sync, lambda: jg.ORSetStore.union(L, R, out, async_=True), steps, warmup)
     ua, ur = out.size()
     for h in (L, R, out):
         h.close()
     consumed = 2 * (na + nr)
-    return {"wall_s": wall, "event_s": ev, "records_per_rank": consumed, "out": [ua, ur],
+    return {"wall_s": wall, "event_s": ev, "records_per_rank": consumed, "records_total": sync.sum_int(consumed), "groups": groups, "out": [ua, ur],
             "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
 
 
@@ -367,6 +381,32 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
             "roofline_valu": valu}
 
 
+PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link, per direction (MI355X_MICROARCH.md)
+
+
+def apply_roofline(res):
+    """Roofline of an apply-loop leg.  The committed wave's payloads live in host memory (the reference's
+    byte[] messages), so every byte the library uploads (payload + per-message uid / identity / type /
+    offset) must cross the host link once: the wave is bounded by PCIe, and `frac` is that link's share.
+    Beside it: the device share (uploaded bytes / kernel time of the wave, against HBM) and the host
+    share (the library's gather into page-locked staging)."""
+    if "error" in res or not res.get("uploaded_bytes_per_wave"):
+        return None
+    up = float(res["uploaded_bytes_per_wave"])
+    wave_s = res["ms_per_wave"] / 1e3
+    busy_s = res["device_busy_ms_per_wave"] / 1e3
+    gather_s = res["gather_ms_per_wave"] / 1e3
+    ach = up / wave_s / 1e9
+    return {"bound": "pcie", "achieved": ach, "peak": PCIE_PEAK_GBS, "unit": "GB/s", "frac": ach / PCIE_PEAK_GBS, "traffic": None,
+            "bytes_per_wave": up, "ideal_ms_per_wave": up / PCIE_PEAK_GBS / 1e6,
+            "scope": "bytes the library uploads per wave (payloads + per-message arrays) / wave time",
+            "device_share": {"bound": "hbm", "achieved": up / busy_s / 1e9 if busy_s else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": up / busy_s / 1e9 / HBM_PEAK_GBS if busy_s else None, "busy_ms_per_wave": busy_s * 1e3,
+                             "scope": "uploaded bytes / kernel time of the wave (hipEvents around each chunk's kernels and the final phase)"},
+            "host_share": {"gather_ms_per_wave": gather_s * 1e3, "gather_GBps": up / gather_s / 1e9 if gather_s else None,
+                           "scope": "the library's workers gathering payloads into page-locked staging (overlaps the uploads)"}}
+
+
 def bench_apply_loop(sync, rank, world, local):
     """C5 committed-batch apply (the banking replay, BankingWorload.cs ops through the
     node batchers, 1M client ops per committed wave) through the C++ host mirror, on every rank.  Every
@@ -386,7 +426,7 @@ def bench_apply_loop(sync, rank, world, local):
     if world > 1 and ok:
         res = {"workload": res["workload"] + f", key-space sharded x{world}", "scaling": "strong",
                "msgs_per_s": res["state_msgs_per_wave"] / (worst_ms / 1e3), "client_ops_per_s": 1_000_000 / (worst_ms / 1e3),
-               "ms_per_wave": worst_ms,
+               "ms_per_wave": worst_ms, "rank0_roofline": apply_roofline(res),
                "rank0": {k: res[k] for k in ("ms_per_wave", "host_ms_per_wave", "engine_ms_per_wave", "owned_accounts",
                                                "applied_msgs_per_wave")}}
     return res
@@ -406,7 +446,8 @@ def bench_apply_orset(sync, rank, world, local):
     worst_ms = sync.max(res["ms_per_wave"] if ok else float("inf"))
     if world > 1 and ok:
         res = {"workload": res["workload"] + f", key-space sharded x{world}", "scaling": "strong",
-               "msgs_per_s": 200_000 / (worst_ms / 1e3), "ms_per_wave": worst_ms, "rank0_ms_per_wave": res["ms_per_wave"]}
+               "msgs_per_s": 200_000 / (worst_ms / 1e3), "ms_per_wave": worst_ms, "rank0_ms_per_wave": res["ms_per_wave"],
+               "rank0_roofline": apply_roofline(res)}
     return res
 
 
@@ -570,7 +611,7 @@ def main():
     if args.workload in ("all", "pnc", "pnc-orset"):
         res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape, args.scaling)
     if args.workload in ("all", "orset", "pnc-orset"):
-        res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup)
+        res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup, args.scaling)
     if args.workload in ("all", "exchange"):
         try:  # a failure here must not cost the headline line
             res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
@@ -596,6 +637,9 @@ def main():
     apply_loop = bench_apply_loop(sync, rank, world, local) if args.workload == "all" else None
     apply_orset = bench_apply_orset(sync, rank, world, local) if args.workload == "all" else None
     apply_c1 = bench_c1(local) if args.workload == "all" and world == 1 else None
+    for leg in (apply_loop, apply_orset, apply_c1):
+        if leg is not None and "error" not in leg and "scaling" not in leg:
+            leg["roofline"] = apply_roofline(leg)
     sync.close()
     if rank != 0:
         return
@@ -629,8 +673,11 @@ def main():
         o = res["orset"]
         ost = o["wall_s"] / max(1, args.steps // 2)
         line["orset"] = {
-            "workload": "ORSet batch merge (BASELINE configs[2]: 1M sets, 100M adds + 20M tombstones per side)",
-            "value": world * o["records_per_rank"] / ost, "unit": "tag records merged/s",
+            "workload": ("ORSet batch merge (BASELINE configs[2]: 1M sets, 100M adds + 20M tombstones per side)" if args.scaling != "strong" else
+                         f"ORSet batch merge (BASELINE configs[2] shape x {ORSET_STRONG_SHARDS} shards: {ORSET_STRONG_SHARDS}M sets, "
+                         f"{ORSET_STRONG_SHARDS * 100}M adds + {ORSET_STRONG_SHARDS * 20}M tombstones per side, split over {world} GPUs)"),
+            "scaling": args.scaling, "groups_per_rank": o["groups"],
+            "value": o["records_total"] / ost, "unit": "tag records merged/s",
             "ms_per_step": ost * 1e3, "out_records": o["out"],
             "hbm_GBps": world * o["bytes_per_step"] / ost / 1e9,
             "roofline": {"bound": "hbm", "achieved": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9,

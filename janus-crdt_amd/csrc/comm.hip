@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -84,9 +85,12 @@ void gather_counts(jg_comm* c, const uint64_t* send, uint32_t k, std::vector<uin
 }
 
 // Buffer b of element size `es` per record: the runs sent (grouped by destination, counts `sc`) and received
-// (grouped by source, counts `rc`), exchanged in the caller's open group.
-void post_runs(jg_comm* c, const char* send, char* recv, size_t es, const uint64_t* sc, const uint64_t* rc, uint32_t stride) {
+// (grouped by source, counts `rc`), exchanged in the caller's open group.  `layout` (default sc) gives the
+// send buffer's run sizes when sc leaves a run out (a zero count: not sent, not copied).
+void post_runs(jg_comm* c, const char* send, char* recv, size_t es, const uint64_t* sc, const uint64_t* rc, uint32_t stride,
+               const uint64_t* layout = nullptr) {
     jg_ctx* ctx = c->ctx;
+    if (!layout) layout = sc;
     uint64_t so = 0, ro = 0;
     for (uint32_t p = 0; p < c->world; ++p) {
         const uint64_t ns = sc[(size_t)p * stride], nr = rc[(size_t)p * stride];
@@ -96,9 +100,16 @@ void post_runs(jg_comm* c, const char* send, char* recv, size_t es, const uint64
             if (ns) JG_NCCL(ncclSend(send + so * es, ns * es, ncclUint8, (int)p, c->nc, ctx->stream));
             if (nr) JG_NCCL(ncclRecv(recv + ro * es, nr * es, ncclUint8, (int)p, c->nc, ctx->stream));
         }
-        so += ns;
+        so += layout[(size_t)p * stride];
         ro += nr;
     }
+}
+
+// JANUS_TEST_EXCHANGE_FULL=1: a one-rank communicator takes the whole route / all-gather / run path too
+// (tests on a one-GPU box; read per call).
+bool full_path() {
+    const char* e = std::getenv("JANUS_TEST_EXCHANGE_FULL");
+    return e && e[0] == '1';
 }
 
 hipEvent_t event(jg_comm* c, int i) {
@@ -173,6 +184,16 @@ int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* se
         jg::ensure_device(ctx);
         const uint32_t W = c->world;
         const uint64_t n = rows ? rows->n_rows : 0, rb = (uint64_t)store->R * store->eb;
+        if (W == 1 && !full_path()) {  // every key is this rank's and local key = global key: the batch merges in place
+            JG_HIP(hipEventRecord(event(c, 0), ctx->stream));
+            if (rows) check_rc(jg_pnc_merge_batch(store, rows, 0));
+            JG_HIP(hipEventRecord(event(c, 3), ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            c->stats = jg_exchange_stats{0, 0, elapsed_ms(c, 0, 3) * 1e-3, 0, 0, n};
+            if (sent) sent[0] = n;
+            if (received) received[0] = n;
+            return;
+        }
         ensure(c->sbuf[0], n * 4 + 16);
         ensure(c->sbuf[1], n * rb + 16);
         ensure(c->sbuf[2], n * rb + 16);
@@ -181,24 +202,35 @@ int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* se
         if (rows) check_rc(jg_rows_route(rows, W, sc.data(), c->sbuf[0].p, c->sbuf[1].p, c->sbuf[2].p, n));
         JG_HIP(hipEventRecord(event(c, 1), ctx->stream));
         gather_counts(c, sc.data(), 1, rc);
+        // max is order-free: this rank's own run merges straight from the send buffers, the peers' runs
+        // land back to back in the receive buffers (rc with the own entry zeroed)
+        const uint64_t own = sc[c->rank];
+        uint64_t own_at = 0;
+        for (uint32_t p = 0; p < c->rank; ++p) own_at += sc[p];
+        std::vector<uint64_t> sc2 = sc, rc2 = rc;
+        sc2[c->rank] = rc2[c->rank] = 0;
         uint64_t nr = 0;
-        for (uint64_t x : rc) nr += x;
+        for (uint64_t x : rc2) nr += x;
         ensure(c->rbuf[0], nr * 4 + 16);
         ensure(c->rbuf[1], nr * rb + 16);
         ensure(c->rbuf[2], nr * rb + 16);
         JG_NCCL(ncclGroupStart());
-        post_runs(c, c->sbuf[0].as<char>(), c->rbuf[0].as<char>(), 4, sc.data(), rc.data(), 1);
-        post_runs(c, c->sbuf[1].as<char>(), c->rbuf[1].as<char>(), rb, sc.data(), rc.data(), 1);
-        post_runs(c, c->sbuf[2].as<char>(), c->rbuf[2].as<char>(), rb, sc.data(), rc.data(), 1);
+        post_runs(c, c->sbuf[0].as<char>(), c->rbuf[0].as<char>(), 4, sc2.data(), rc2.data(), 1, sc.data());
+        post_runs(c, c->sbuf[1].as<char>(), c->rbuf[1].as<char>(), rb, sc2.data(), rc2.data(), 1, sc.data());
+        post_runs(c, c->sbuf[2].as<char>(), c->rbuf[2].as<char>(), rb, sc2.data(), rc2.data(), 1, sc.data());
         JG_NCCL(ncclGroupEnd());
         JG_HIP(hipEventRecord(event(c, 2), ctx->stream));
-        check_rc(jg_pnc_merge_device(store, nr, c->rbuf[0].p, c->rbuf[1].p, c->rbuf[2].p));
+        if (own)
+            check_rc(jg_pnc_merge_device(store, own, c->sbuf[0].as<char>() + own_at * 4, c->sbuf[1].as<char>() + own_at * rb,
+                                         c->sbuf[2].as<char>() + own_at * rb));
+        if (nr) check_rc(jg_pnc_merge_device(store, nr, c->rbuf[0].p, c->rbuf[1].p, c->rbuf[2].p));
+        nr += own;
         JG_HIP(hipEventRecord(event(c, 3), ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
         uint64_t off_rank = 0;
         for (uint32_t p = 0; p < W; ++p) off_rank += p == c->rank ? 0 : sc[p];
         c->stats = jg_exchange_stats{elapsed_ms(c, 0, 1) * 1e-3, elapsed_ms(c, 1, 2) * 1e-3, elapsed_ms(c, 2, 3) * 1e-3, off_rank * (4 + 2 * rb),
-                                     (nr - rc[c->rank]) * (4 + 2 * rb), nr};
+                                     (nr - own) * (4 + 2 * rb), nr};
         if (sent) std::copy(sc.begin(), sc.end(), sent);
         if (received) std::copy(rc.begin(), rc.end(), received);
     });
@@ -216,6 +248,18 @@ int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t*
         const uint32_t W = c->world;
         jg::sync_counts(received);
         const uint64_t na = received->add.n, nrm = received->rem.n;
+        if (W == 1 && !full_path()) {  // set id = local id: ORSet.Merge of the received state in place
+            JG_HIP(hipEventRecord(event(c, 0), ctx->stream));
+            check_rc(jg_orset_merge_store(store, received, 0));
+            JG_HIP(hipEventRecord(event(c, 3), ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            c->stats = jg_exchange_stats{0, 0, elapsed_ms(c, 0, 3) * 1e-3, 0, 0, na + nrm};
+            if (sent_add) sent_add[0] = na;
+            if (sent_rem) sent_rem[0] = nrm;
+            if (recv_add) recv_add[0] = na;
+            if (recv_rem) recv_rem[0] = nrm;
+            return;
+        }
         const size_t es[6] = {8, 16, 4, 8, 16, 4};  // key, tag, ord of the add stream, then of the tombstones
         for (int i = 0; i < 6; ++i) ensure(c->sbuf[i], (i < 3 ? na : nrm) * es[i] + 16);
         JG_HIP(hipEventRecord(event(c, 0), ctx->stream));

@@ -61,3 +61,15 @@ def test_weak_scaling_shards_and_max_over_ranks(world):
     assert strong[0][0] == 0 and strong[-1][1] == 200_000_000
     assert all(a1 == b0 for (_, a1), (b0, _) in zip(strong, strong[1:]))
     assert all(x[6] == 128 and x[7] == 200_000_000 for x in res)  # every rank saw the summed key count
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 5, 8])
+def test_orset_strong_split_is_whole_sets_of_c3_times_8(world):
+    """--scaling strong for the OR-Set leg: the C3 shape x 8 shards (80M (set, elem) groups) split into
+    whole sets over the ranks, together exactly the total; weak keeps one C3 shard per rank."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    parts = [bench.orset_groups("strong", r, world) for r in range(world)]
+    assert sum(parts) == bench.ORSET_STRONG_SHARDS * bench.ORSET_GROUPS
+    assert all(p % bench.ORSET_E == 0 for p in parts) and max(parts) - min(parts) <= bench.ORSET_E
+    assert all(bench.orset_groups("weak", r, world) == bench.ORSET_GROUPS for r in range(world))

@@ -65,7 +65,7 @@ def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3)
         s.close()
 
 
-PARSE = ["group", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
+PARSE = ["auto", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
 
 
 @pytest.mark.parametrize("parse", PARSE)
@@ -146,7 +146,7 @@ def test_group_parse_mutants_equal_serial(ctx, monkeypatch):
             results[mode] = (codes, s.read())
         finally:
             s.close()
-    (cg, rg), (cs, rs) = results["group"], results["serial"]
+    (cg, rg), (cs, rs) = results["auto"], results["serial"]
     assert cg == cs
     assert all(np.array_equal(x, y) for x, y in zip(rg, rs))
     assert sum(c == (0, None) for c in cg) > len(bases)  # some mutants stayed valid

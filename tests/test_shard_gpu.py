@@ -398,9 +398,12 @@ def test_rccl_exchange_world1():
 
 
 # ---- the exchange inside the library (jg_comm over RCCL, csrc/comm.hip) at world size 1 ----
-def test_native_exchange_world1(ctx):
-    """jg_pnc_exchange / jg_orset_exchange on a one-rank communicator: route, RCCL counts all-gather, the
-    rank's own run copied into place, merge — bit-exact against the oracle's Merge of the whole batch."""
+@pytest.mark.parametrize("full", ["0", "1"])
+def test_native_exchange_world1(ctx, full, monkeypatch):
+    """jg_pnc_exchange / jg_orset_exchange on a one-rank communicator — the in-place merge a single rank takes,
+    and (JANUS_TEST_EXCHANGE_FULL=1) the whole multi-rank path: route, RCCL counts all-gather, the rank's own
+    run, merge — bit-exact against the oracle's Merge of the whole batch either way."""
+    monkeypatch.setenv("JANUS_TEST_EXCHANGE_FULL", full)
     rng = np.random.default_rng(21)
     K, R, n = 700, 64, 4000
     AP, AN = random_pnc(rng, K, R, 8, absent=False, lo=0), random_pnc(rng, K, R, 8, absent=False, lo=0)
