@@ -218,8 +218,12 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
                 if (ok && q < ecap) {
                     unsigned long long h = kFnvBasis;
                     for (uint32_t i = 0; i < n; ++i) h = (h ^ c[s + 1 + i]) * kFnvPrime;
+                    uint32_t X[2];
+                    jgw::lds_words<2>(lds, a + (uint32_t)s + 1, X);
+                    const unsigned long long pf = ((unsigned long long)X[1] << 32 | X[0]) & (n >= 8 ? ~0ull : (1ull << (8 * n)) - 1ull);
                     S.key[es + q] = name_key(set, h) & kmask;
                     S.noff[es + q] = b + (uint64_t)s + 1;
+                    S.pfx[es + q] = pf;
                     S.meta[es + q] = n | sec << 31;
                     S.pos[es + q] = (uint32_t)s;
                 }

@@ -114,15 +114,16 @@ struct GuidSink {  // Guid.Parse of the "D" form (what Guid's JSON converter acc
     __device__ Tag16 tag() const { return Tag16{(unsigned long long)va | (unsigned long long)vb << 32 | (unsigned long long)vc << 48, hi}; }
 };
 
-struct NameSink {  // FNV-1a of the unescaped bytes; with w set, the bytes after the first escape are
-                   // written back at the string's start (unescaping never lengthens a string)
-    unsigned long long h = kFnvBasis;
+struct NameSink {  // FNV-1a of the unescaped bytes and the first 8 of them; with w set, the bytes after the
+                   // first escape are written back at the string's start (unescaping never lengthens a string)
+    unsigned long long h = kFnvBasis, pf = 0;
     uint32_t len = 0;
     uint8_t* w = nullptr;
     bool shifted = false;
     __device__ void esc() { shifted = w != nullptr; }
     __device__ void put(int b) {
         h = (h ^ (uint32_t)b) * kFnvPrime;
+        if (len < 8) pf |= (unsigned long long)(uint8_t)b << (8 * len);
         if (shifted) w[len] = (uint8_t)b;
         ++len;
     }
@@ -319,7 +320,7 @@ template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c
                         c.ws();
                         if (c.peek() != '[') return false;  // a null tag set, or not an array
                         ++c.p;
-                        v.entry(which, npos, noff, ns.len, ns.h);
+                        v.entry(which, npos, noff, ns.len, ns.h, ns.pf);
                         uint32_t nt;
                         if (!read_tags(c, v, which, false, nt)) return false;
                         v.entry_end(which, c.p, nt);
@@ -347,9 +348,11 @@ template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c
 // check() compacts them in commit order (k_ow_compact).
 constexpr uint64_t kEntryDiv = 4, kTagDiv = 32;
 
-struct Sparse {  // entry slots: sort key, string offset, length | side << 31, error position; tag slots
+struct Sparse {  // entry slots: sort key, string offset, length | side << 31, error position, the string's
+                 // first 8 bytes (zero past its end); tag slots
     unsigned long long* key;
     unsigned long long* noff;
+    unsigned long long* pfx;
     uint32_t* meta;
     uint32_t* pos;
     unsigned long long* tref;  // null << 63 | side << 62 | the entry's parse-order ordinal in its message
@@ -366,11 +369,12 @@ struct ParseVis {
         if (which == 0) add_seen = true;
         else if (!add_seen) rem_first = true;
     }
-    __device__ __forceinline__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h) {
+    __device__ __forceinline__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h, uint64_t pf) {
         cur = n_add + n_rem;
         const uint64_t e = es + cur;
         S.key[e] = name_key(set, h) & kmask;
         S.noff[e] = noff;
+        S.pfx[e] = pf;
         S.meta[e] = len | (uint32_t)side << 31;
         S.pos[e] = (uint32_t)(npos - base);
         n_add += side == 0;
@@ -452,16 +456,14 @@ __global__ __launch_bounds__(kBlock) void k_ow_compact(const uint64_t* __restric
     for (uint32_t q = lane; q < cnt; q += 64) {
         const uint64_t e = e0 + canon(q);
         const unsigned long long no = S.noff[es + q];
-        const uint32_t meta = S.meta[es + q], len = meta & 0x7FFFFFFFu;
-        unsigned long long pf = 0;
-        for (uint32_t k = 0; k < 8 && k < len; ++k) pf |= (unsigned long long)bytes[no + k] << (8 * k);
+        const uint32_t meta = S.meta[es + q];
         E.key[e] = S.key[es + q];
         E.val[e] = (uint32_t)e;
         E.noff[e] = no;
         E.msg[e] = (uint32_t)m;
         E.meta[e] = meta;
         E.pos[e] = S.pos[es + q];
-        E.pfx[e] = pf;
+        E.pfx[e] = S.pfx[es + q];
         E.set[e] = set;
     }
     const uint32_t k = (uint32_t)nt[m];
@@ -789,6 +791,34 @@ __global__ void k_gather_radix(const unsigned long long* __restrict__ dk, const 
     const uint32_t p = perm[i];
     out[i] = which == 2 ? dk[p] : which == 1 ? dt[p].lo : dt[p].hi;
 }
+// Records sorted by key alone: each run of equal keys (one element's new tags, a handful) put in (tag.lo,
+// tag.hi) order by its head thread (insertion sort over the permutation); a run longer than kRunFix
+// raises *long_run and the caller sorts the whole side by all three words instead.
+constexpr uint32_t kRunFix = 64;
+__global__ void k_fix_runs(const unsigned long long* __restrict__ skey, const Tag16* __restrict__ dt, uint32_t* __restrict__ perm, uint64_t n,
+                           unsigned long long* __restrict__ long_run) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || (i > 0 && skey[i] == skey[i - 1])) return;
+    uint64_t j = i + 1;
+    while (j < n && skey[j] == skey[i] && j - i <= kRunFix) ++j;
+    if (j - i > kRunFix) {
+        atomicOr(long_run, 1ull);
+        return;
+    }
+    for (uint64_t a = i + 1; a < j; ++a) {
+        const uint32_t x = perm[a];
+        const Tag16 tx = dt[x];
+        uint64_t b = a;
+        while (b > i) {
+            const Tag16 ty = dt[perm[b - 1]];
+            if (ty.lo < tx.lo || (ty.lo == tx.lo && ty.hi <= tx.hi)) break;
+            perm[b] = perm[b - 1];
+            --b;
+        }
+        perm[b] = x;
+    }
+}
+
 __global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ ds,
                               const uint32_t* __restrict__ mint, const uint32_t* __restrict__ perm, uint64_t n, unsigned long long* __restrict__ ok,
                               Tag16* __restrict__ ot, uint32_t* __restrict__ oo) {
@@ -833,8 +863,8 @@ struct jg_orset_wire {
     uint64_t first_bad = kNone, n_ent = 0, n_tag = 0;
     // entries, groups, tags, records
     jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, epfx, eset, skey, sval, hs, seg, impure, label, gid, eid;
-    jg::DevBuf sp_key, sp_noff, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
-    jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm, perm2;
+    jg::DevBuf sp_key, sp_noff, sp_pfx, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
+    jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm[2], perm2[2];
     jg::DevBuf newk, newv, snk, snv, status, cub;
     jg::DevBuf cnk, fsel, fslot, fidx;  // commit: compacted new-string keys; dedup marks, slots, compacted indices
     jg_orset* recs = nullptr;  // a committed wave's records, sorted (the merge source), reused
@@ -972,6 +1002,7 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
         const uint64_t ke = (w->wnb + kEntryDiv - 1) / kEntryDiv + 1, kt = (w->wnb + kTagDiv - 1) / kTagDiv + 1;  // slots in use
         grow_keep(ctx, w->sp_key, es * 8, ke * 8);
         grow_keep(ctx, w->sp_noff, es * 8, ke * 8);
+        grow_keep(ctx, w->sp_pfx, es * 8, ke * 8);
         grow_keep(ctx, w->sp_meta, es * 4, ke * 4);
         grow_keep(ctx, w->sp_pos, es * 4, ke * 4);
         grow_keep(ctx, w->sp_tref, ts * 8, kt * 8);
@@ -995,7 +1026,8 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
 }
 
 Sparse sparse_of(jg_orset_wire* w) {
-    return Sparse{w->sp_key.as<unsigned long long>(), w->sp_noff.as<unsigned long long>(), w->sp_meta.as<uint32_t>(), w->sp_pos.as<uint32_t>(),
+    return Sparse{w->sp_key.as<unsigned long long>(), w->sp_noff.as<unsigned long long>(), w->sp_pfx.as<unsigned long long>(),
+                  w->sp_meta.as<uint32_t>(), w->sp_pos.as<uint32_t>(),
                   w->sp_tref.as<unsigned long long>(), w->sp_tval.as<Tag16>()};
 }
 
@@ -1112,26 +1144,48 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     return (e & 3) == kKindState ? JG_ESTATE : JG_EINVAL;
 }
 
-// Sort one side's distinct records by (key, tag.lo, tag.hi) (three stable LSD passes) into a dense stream;
-// ords = first tag index in the wave (< nt = the stream's next).
-void sort_side(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, uint64_t nt, jg_stream_soa& out) {
+// Sort one side's distinct records by (key, tag.lo, tag.hi) into a dense stream; ords = first tag index in the
+// wave (< nt = the stream's next).  begin: one radix sort by key, then each key's few tags ordered in place
+// (k_fix_runs), queued without a wait — *long_run (device) flags a key with more than kRunFix new tags;
+// end (after the caller read both sides' flags in one sync): such a side is sorted again by all three words
+// (three stable LSD passes), then the records are gathered in order.
+void sort_side_begin(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, uint64_t nt, jg_stream_soa& out,
+                     unsigned long long* long_run) {
     jg::set_dense(ctx, out, n);
     out.next = nt;
+    JG_HIP(hipMemsetAsync(long_run, 0, 8, ctx->stream));
     if (n == 0) return;
     ensure(w->rk, n * 8);
     ensure(w->rk2, n * 8);
-    ensure(w->perm, n * 4);
-    ensure(w->perm2, n * 4);
+    ensure(w->perm[sd], n * 4);
+    ensure(w->perm2[sd], n * 4);
     const auto* dk = w->dk[sd].as<unsigned long long>();
     const auto* dt = w->dt[sd].as<Tag16>();
-    uint32_t* p = w->perm.as<uint32_t>();
-    uint32_t* q = w->perm2.as<uint32_t>();
+    uint32_t* p = w->perm[sd].as<uint32_t>();
+    uint32_t* q = w->perm2[sd].as<uint32_t>();
     hipLaunchKernelGGL(k_iota, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, p, n);
-    for (int which = 0; which < 3; ++which) {
-        hipLaunchKernelGGL(k_gather_radix, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, which, w->rk.as<unsigned long long>());
-        JG_HIP(hipGetLastError());
-        sort_pairs(ctx, w, w->rk.as<unsigned long long>(), w->rk2.as<unsigned long long>(), p, q, n, which == 2 ? key_bits : 64);
-        std::swap(p, q);
+    hipLaunchKernelGGL(k_gather_radix, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, 2, w->rk.as<unsigned long long>());
+    JG_HIP(hipGetLastError());
+    sort_pairs(ctx, w, w->rk.as<unsigned long long>(), w->rk2.as<unsigned long long>(), p, q, n, key_bits);
+    hipLaunchKernelGGL(k_fix_runs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->rk2.as<unsigned long long>(), dt, q, n, long_run);
+    JG_HIP(hipGetLastError());
+}
+
+void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out, bool long_run) {
+    if (n == 0) return;
+    const auto* dk = w->dk[sd].as<unsigned long long>();
+    const auto* dt = w->dt[sd].as<Tag16>();
+    uint32_t* p = w->perm2[sd].as<uint32_t>();  // the key sort's output, runs fixed
+    if (long_run) {
+        p = w->perm[sd].as<uint32_t>();
+        uint32_t* q = w->perm2[sd].as<uint32_t>();
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, p, n);
+        for (int which = 0; which < 3; ++which) {
+            hipLaunchKernelGGL(k_gather_radix, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, p, n, which, w->rk.as<unsigned long long>());
+            JG_HIP(hipGetLastError());
+            sort_pairs(ctx, w, w->rk.as<unsigned long long>(), w->rk2.as<unsigned long long>(), p, q, n, which == 2 ? key_bits : 64);
+            std::swap(p, q);
+        }
     }
     hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), w->dmin.as<uint32_t>(), p,
                        n, out.key.as<unsigned long long>(), out.tag.as<Tag16>(), out.ord.as<uint32_t>());
@@ -1235,8 +1289,15 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         w->recs->ctx = ctx;
     }
     const int key_bits = 32 + bits_for(w->max_set);
-    sort_side(ctx, w, 0, cnt[0], key_bits, nt, w->recs->add);
-    sort_side(ctx, w, 1, cnt[1], key_bits, nt, w->recs->rem);
+    const uint64_t nmax = std::max(cnt[0], cnt[1]);  // the radix-key buffers serve both sides: sized once,
+    ensure(w->rk, nmax * 8);                           // so no reallocation frees one that queued work reads
+    ensure(w->rk2, nmax * 8);
+    sort_side_begin(ctx, w, 0, cnt[0], key_bits, nt, w->recs->add, st + 6);
+    sort_side_begin(ctx, w, 1, cnt[1], key_bits, nt, w->recs->rem, st + 7);
+    unsigned long long long_run[2];
+    read_words(ctx, st + 6, long_run, 2);
+    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0);
+    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0);
     jg::orset_merge_store(s, w->recs);
 }
 

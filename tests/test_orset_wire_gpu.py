@@ -316,3 +316,24 @@ def test_empty_and_all_bad_waves(ctx):
         assert [len(x) for x in s.read()] == [0, 0] and s.wave_names() == []
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("n_tags", [3, 64, 65, 300])
+def test_element_with_many_new_tags(ctx, n_tags):
+    """The commit sorts a wave's new records by key and orders each key's tags in place; an element with more
+    than 64 new tags in one wave takes the full three-word sort.  Both must give the oracle's records."""
+    rng = np.random.default_rng(14 + n_tags)
+    big = J.random_guids(rng, n_tags)
+    msgs = [J.encode_orset([("big", big), ("x", J.random_guids(rng, 2))], [("x", big[:1])]),
+            J.encode_orset([("big", big[: n_tags // 2] + J.random_guids(rng, 5))], [("big", big[:7])], J.random_guids(rng, 70), []),
+            J.encode_orset([("y", J.random_guids(rng, 1))], [])]
+    sets = [3, 3, 4]
+    ea, er, bad, _ = orc.orset_apply_json(sets, msgs)
+    assert bad is None
+    s = jg.ORSetStore(ctx)
+    try:
+        s.merge_json(sets, msgs)
+        ga, gr = s.read()
+        assert orc.same_orset(ga, gr, ea, er)
+    finally:
+        s.close()
