@@ -90,7 +90,7 @@ __device__ __forceinline__ uint32_t og_prefix_le(unsigned long long ballot, uint
 }
 
 __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                     const uint32_t* __restrict__ mset, uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask,
+                                                     const uint32_t* __restrict__ mset, uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, uint64_t salt,
                                                      unsigned long long* __restrict__ ne, unsigned long long* __restrict__ nt,
                                                      uint32_t* __restrict__ na, unsigned long long* __restrict__ err, uint8_t* __restrict__ slow) {
     __shared__ OgShared sh;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
                     uint32_t X[2];
                     jgw::lds_words<2>(lds, a + (uint32_t)s + 1, X);
                     const unsigned long long pf = ((unsigned long long)X[1] << 32 | X[0]) & (n >= 8 ? ~0ull : (1ull << (8 * n)) - 1ull);
-                    S.key[es + q] = name_key(set, h) & kmask;
+                    S.key[es + q] = name_key(set, h, salt) & kmask;
                     S.noff[es + q] = b + (uint64_t)s + 1;
                     S.pfx[es + q] = pf;
                     S.meta[es + q] = n | sec << 31;

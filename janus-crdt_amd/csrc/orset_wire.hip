@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <random>
 #include <vector>
 
 #include "jg_internal.hpp"
@@ -65,7 +66,11 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 constexpr uint64_t kFnvBasis = 0xcbf29ce484222325ull, kFnvPrime = 0x100000001b3ull;
-__device__ __forceinline__ uint64_t name_key(uint32_t set, uint64_t fnv) { return mix64(fnv ^ mix64((uint64_t)set + 0x9E3779B97F4A7C15ull)); }
+// (set, string) key of an element name: the string's FNV-1a mixed with its set and the store's random salt
+// (drawn at the store's first wave), so a peer cannot aim names at one value of the sort's low 32 bits
+__device__ __forceinline__ uint64_t name_key(uint32_t set, uint64_t fnv, uint64_t salt) {
+    return mix64(fnv ^ mix64((uint64_t)set + salt));
+}
 
 // ---- string sinks: read_string feeds each unescaped UTF-8 byte to put(), esc() at a backslash -------
 __constant__ char kProp[4][16] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
@@ -361,7 +366,7 @@ struct Sparse {  // entry slots: sort key, string offset, length | side << 31, e
 
 struct ParseVis {
     Sparse S;
-    uint64_t base, es, ts, kmask;  // message byte offset; first entry / tag slot
+    uint64_t base, es, ts, kmask, salt;  // message byte offset; first entry / tag slot
     uint32_t set, n_add = 0, n_rem = 0, nt = 0, cur = 0;
     bool rem_first = false, add_seen = false;
     unsigned long long estate = kNone;
@@ -372,7 +377,7 @@ struct ParseVis {
     __device__ __forceinline__ void entry(int side, uint64_t npos, uint64_t noff, uint32_t len, uint64_t h, uint64_t pf) {
         cur = n_add + n_rem;
         const uint64_t e = es + cur;
-        S.key[e] = name_key(set, h) & kmask;
+        S.key[e] = name_key(set, h, salt) & kmask;
         S.noff[e] = noff;
         S.pfx[e] = pf;
         S.meta[e] = len | (uint32_t)side << 31;
@@ -394,7 +399,7 @@ struct ParseVis {
 // strings hashed (escaped ones unescaped in place), entries and tags into the sparse regions.  The
 // entries before a syntax error are kept: a repeated name before it is reported first.
 __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
-                                                     uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, unsigned long long* __restrict__ ne,
+                                                     uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, uint64_t salt, unsigned long long* __restrict__ ne,
                                                      unsigned long long* __restrict__ nt, uint32_t* __restrict__ na,
                                                      unsigned long long* __restrict__ err, const uint8_t* __restrict__ slow) {
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_parse(uint8_t* __restrict__ bytes
         return;
     }
     const uint64_t b = off[m];
-    ParseVis v{S, b, (b + kEntryDiv - 1) / kEntryDiv, (b + kTagDiv - 1) / kTagDiv, kmask, mset[m]};
+    ParseVis v{S, b, (b + kEntryDiv - 1) / kEntryDiv, (b + kTagDiv - 1) / kTagDiv, kmask, salt, mset[m]};
     Cursor c(bytes, b, off[m + 1]);
     unsigned long long e = kNone;
     if (!parse_orset<true>(c, bytes, v)) e = (unsigned long long)(c.p - b) << 2 | kKindInval;
@@ -510,9 +515,12 @@ __device__ __forceinline__ void report_dup(const Entries& E, uint32_t e, unsigne
 // label[i] = sorted index of the first entry with the same (set, string).  Pure runs: the run's head
 // (stable sort = commit order), and a repeat within one map of one message is adjacent to its twin.
 // Impure runs (hash collision): a scan of the run before i.
+// An impure run is scanned entry by entry (O(L) per entry); past scan_limit entries into such a run the
+// kernel raises *long_run instead, and the caller sorts the entries again on their full 64-bit keys (runs
+// then mix only strings whose whole keys collide) and labels once more without a limit.
 __global__ void k_ow_label(Entries E, const uint32_t* __restrict__ mset, const uint8_t* __restrict__ bytes, const uint32_t* __restrict__ sval,
                            const uint32_t* __restrict__ seg, const uint8_t* __restrict__ impure, uint64_t n, uint32_t* __restrict__ label,
-                           unsigned long long* __restrict__ err) {
+                           unsigned long long* __restrict__ err, uint32_t scan_limit, unsigned long long* __restrict__ long_run) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t s = seg[i], e = sval[i];
@@ -524,17 +532,24 @@ __global__ void k_ow_label(Entries E, const uint32_t* __restrict__ mset, const u
         }
         return;
     }
+    if (i - s > scan_limit) {
+        *long_run = 1;
+        return;
+    }
     uint32_t lab = (uint32_t)i;
     bool dup = false;
+    const unsigned long long ke = E.key[e];
     for (uint32_t j = s; j < i; ++j) {
         const uint32_t q = sval[j];
-        if (!same_name(E, mset, bytes, e, q)) continue;
+        if (E.key[q] != ke || !same_name(E, mset, bytes, e, q)) continue;  // whole keys first: bytes only on a full match
         if (lab == i) lab = j;
         dup |= E.msg[q] == E.msg[e] && (E.meta[q] >> 31) == (E.meta[e] >> 31);
     }
     label[i] = lab;
     if (dup) report_dup(E, e, err);
 }
+
+constexpr uint32_t kImpureScan = 64;  // entries of an impure run labelled by a scan before the full-key re-sort
 
 __global__ void k_ow_first_bad(const unsigned long long* __restrict__ err, uint64_t n, unsigned long long* __restrict__ status) {
     const uint64_t m = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -583,7 +598,7 @@ __global__ void k_sets_update(Names N, const uint32_t* __restrict__ set, const u
 }
 
 __global__ void k_names_put(Names N, uint64_t g0, uint64_t pool0, const uint32_t* __restrict__ nset, const uint32_t* __restrict__ nid,
-                            const uint64_t* __restrict__ off, uint64_t n, uint64_t kmask) {
+                            const uint64_t* __restrict__ off, uint64_t n, uint64_t kmask, uint64_t salt) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint64_t g = g0 + i;
@@ -591,7 +606,7 @@ __global__ void k_names_put(Names N, uint64_t g0, uint64_t pool0, const uint32_t
     const uint8_t* b = N.pool + pool0 + off[i];
     uint64_t h = kFnvBasis;
     for (uint32_t k = 0; k < len; ++k) h = (h ^ b[k]) * kFnvPrime;
-    const uint64_t key = name_key(set, h) & kmask;
+    const uint64_t key = name_key(set, h, salt) & kmask;
     N.set[g] = set;
     N.id[g] = nid[i];
     N.gen[g] = N.set_gen[set];
@@ -872,8 +887,10 @@ struct jg_orset_wire {
     uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;
     // string-hash mask: all bits; tests narrow it (JANUS_TEST_NAME_HASH_BITS) to force collisions
     uint64_t kmask = ~0ull;
+    uint64_t salt = 0;  // name_key's per-store salt (random, drawn at first use)
     // key bits the entry sort orders on; tests narrow it (JANUS_TEST_ENTRY_SORT_BITS) so runs mix full keys
     int sort_bits = 32;
+    uint64_t resorts = 0;  // waves whose entries were sorted again on full keys (a long impure run)
 };
 
 namespace {
@@ -900,6 +917,8 @@ jg_orset_wire* wire_of(jg_orset* s) {
     if (!s->wire) {
         s->wire = new jg_orset_wire();
         s->wire->status.alloc(64);
+        std::random_device rd;
+        s->wire->salt = ((uint64_t)rd() << 32 ^ rd()) | 1;
         if (const char* e = std::getenv("JANUS_TEST_NAME_HASH_BITS")) {
             const int bits = std::atoi(e);
             if (bits > 0 && bits < 64) s->wire->kmask = (1ull << bits) - 1;
@@ -1048,7 +1067,7 @@ void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
     if (!serial) {
         slow = w->slow.as<uint8_t>();
         hipLaunchKernelGGL(k_ow_group, dim3((unsigned)((m1 - m0 + kOgWaves - 1) / kOgWaves)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff,
-                           w->vmset, m0, m1, sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
+                           w->vmset, m0, m1, sparse_of(w), w->kmask, w->salt, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(),
                            w->na.as<uint32_t>(), w->err.as<unsigned long long>(), slow);
         JG_HIP(hipGetLastError());
     }
@@ -1057,7 +1076,7 @@ void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
                            w->nt.as<unsigned long long>(), w->na.as<uint32_t>(), w->err.as<unsigned long long>());
     else
         hipLaunchKernelGGL(k_ow_parse, dim3(blocks_for(m1 - m0)), dim3(kBlock), 0, ctx->stream, w->vbytes, w->voff, w->vmset, m0, m1,
-                           sparse_of(w), w->kmask, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
+                           sparse_of(w), w->kmask, w->salt, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
                            w->err.as<unsigned long long>(), slow);
     JG_HIP(hipGetLastError());
 }
@@ -1125,17 +1144,42 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         hipLaunchKernelGGL(k_ow_link, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes,
                            w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), ne, w->impure.as<uint8_t>());
         JG_HIP(hipGetLastError());
+        JG_HIP(hipMemsetAsync(status_words(w) + 1, 0, 8, ctx->stream));
         hipLaunchKernelGGL(k_ow_label, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes,
                            w->sval.as<uint32_t>(), w->seg.as<uint32_t>(), w->impure.as<uint8_t>(), ne, w->label.as<uint32_t>(),
-                           w->err.as<unsigned long long>());
+                           w->err.as<unsigned long long>(), kImpureScan, status_words(w) + 1);
         JG_HIP(hipGetLastError());
     }
     unsigned long long* st = status_words(w);
     JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
     hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
     JG_HIP(hipGetLastError());
-    unsigned long long bad;
-    read_words(ctx, st, &bad, 1);
+    unsigned long long words[2] = {kNone, 0};
+    read_words(ctx, st, words, ne ? 2 : 1);
+    if (words[1]) {  // a long impure run: entries again by their whole 64-bit keys, then label without a limit
+        const Entries E = entries_of(w);
+        sort_pairs(ctx, w, E.key, w->skey.as<unsigned long long>(), E.val, w->sval.as<uint32_t>(), ne, 64);
+        hipLaunchKernelGGL(k_ow_head, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->skey.as<unsigned long long>(), ne, ~0ull,
+                           w->hs.as<uint32_t>());
+        JG_HIP(hipGetLastError());
+        size_t temp = 0;
+        JG_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::InclusiveScan(cub_temp(w, temp), temp, w->hs.as<uint32_t>(), w->seg.as<uint32_t>(), hipcub::Max(), (int)ne,
+                                                 ctx->stream));
+        JG_HIP(hipMemsetAsync(w->impure.p, 0, ne, ctx->stream));
+        hipLaunchKernelGGL(k_ow_link, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes, w->sval.as<uint32_t>(),
+                           w->seg.as<uint32_t>(), ne, w->impure.as<uint8_t>());
+        hipLaunchKernelGGL(k_ow_label, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, E, w->vmset, w->vbytes, w->sval.as<uint32_t>(),
+                           w->seg.as<uint32_t>(), w->impure.as<uint8_t>(), ne, w->label.as<uint32_t>(), w->err.as<unsigned long long>(),
+                           UINT32_MAX, st + 1);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
+        hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
+        JG_HIP(hipGetLastError());
+        read_words(ctx, st, words, 1);
+        ++w->resorts;
+    }
+    const unsigned long long bad = words[0];
     if (bad == kNone) return JG_OK;
     unsigned long long e;
     JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + bad, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1416,7 +1460,7 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
             JG_HIP(hipMemcpyAsync(d_off, off, (n_names + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
             if (nb) JG_HIP(hipMemcpyAsync(w->pool.as<uint8_t>() + w->pool_used, bytes, nb, hipMemcpyHostToDevice, ctx->stream));
             hipLaunchKernelGGL(k_names_put, dim3(blocks_for(n_names)), dim3(kBlock), 0, ctx->stream, names_of(w), w->n_names, w->pool_used, d_nset, d_nid,
-                               d_off, n_names, w->kmask);
+                               d_off, n_names, w->kmask, w->salt);
             JG_HIP(hipGetLastError());
         }
         JG_HIP(hipStreamSynchronize(ctx->stream));

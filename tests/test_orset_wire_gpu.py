@@ -337,3 +337,29 @@ def test_element_with_many_new_tags(ctx, n_tags):
         assert orc.same_orset(ga, gr, ea, er)
     finally:
         s.close()
+
+
+def test_hot_name_in_long_impure_runs(ctx, monkeypatch):
+    """A name repeated thousands of times in a run that also holds other strings (the entry sort narrowed to 4
+    key bits, so every run mixes strings): labelling scans an impure run only up to 64 entries, then the wave's
+    entries are sorted again on their whole keys — linear work, the oracle's result."""
+    import time
+    monkeypatch.setenv("JANUS_TEST_ENTRY_SORT_BITS", "4")
+    rng = np.random.default_rng(15)
+    hot = J.random_guids(rng, 1)
+    msgs, sets = [], []
+    for i in range(6000):
+        others = [(f"o{int(rng.integers(0, 40))}", J.random_guids(rng, 1))]
+        msgs.append(J.encode_orset([("hot", hot)] + others, []))
+        sets.append(0)
+    s = jg.ORSetStore(ctx)
+    try:
+        t0 = time.perf_counter()
+        s.merge_json(sets, msgs)
+        dt = time.perf_counter() - t0
+        ga, gr = s.read()
+        ea, er, bad, _ = orc.orset_apply_json(sets, msgs)
+        assert bad is None and orc.same_orset(ga, gr, ea, er)
+        assert dt < 5.0, dt
+    finally:
+        s.close()
