@@ -226,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
                     S.pfx[es + q] = pf;
                     S.meta[es + q] = n | sec << 31;
                     S.pos[es + q] = (uint32_t)s;
+                    S.set[es + q] = set;
                 }
             } else if (nbrk) {  // "nullRemoveGuid"
                 ok = nsub == 1 && og_name_is(c, s + 1, n, "nullRemoveGuid", 14) && (ga == kGlArr || (last && ga == kGlEndEmpty));

@@ -1,0 +1,277 @@
+// orset_tables.hpp — the OR-Set wave's string and record tables, filled chunk by chunk (included by
+// orset_wire.hip only).
+//
+// A wave's commit needs, for every element string of every set, the first entry that names it (its id is
+// issued in first-insertion order, ORSet.cs:255-279 / the Dictionaries' order), and, for every distinct tag
+// record, its first occurrence (the arrival ordinal: HashSet<Guid>.UnionWith keeps a tag where it first
+// entered).  Sorting the wave's entries and de-duplicating its records after the last chunk made the
+// commit a ~2.3 ms tail behind the uploads on the ORSetWorkload wave (200k states, 4.6M entries, 4.6M tag
+// references, ~0.4M distinct records).  Here three small kernels run after each chunk's parse, while the
+// next chunk is still being gathered and uploaded:
+//
+//   k_ow_strings   one wave per message, one lane per entry: the (set, string) goes into an open-addressing
+//                  table (exact byte compare on a hash match; slot = the string's id for this wave), the
+//                  slot keeps the smallest canonical entry index (atomicMin; entry slots are ordered like
+//                  commit order), and a string named twice in one map of one message is Decode's
+//                  duplicate-key error at the second name (the messages' entries compared in LDS).
+//   k_ow_rkeys     each tag reference's record identity without its tag: (string slot, side), or
+//                  (set, side) for a null tag set.
+//   k_ow_rins      each tag reference into the record table (exact compare of identity + tag), the slot
+//                  keeping the smallest tag index = the record's arrival ordinal.
+//
+// The commit then resolves only the distinct strings against the element table and sorts only the
+// distinct records.  A table that runs out of probes (more distinct strings / records than it was sized
+// for, or tests narrowing the hashes) or a message with more than kDupScan entries raises the overflow
+// word, and the wave falls back to the sort-based check and commit (k_ow_compact ... k_ow_dedup), which
+// reads the same sparse regions.  Messages past the commit limit are in the tables too; the commit keeps
+// the strings and records whose first occurrence lies before the limit (entry / tag slots are ordered
+// like messages).
+#pragma once
+
+constexpr uint32_t kNoSid = 0xFFFFFFFFu;
+constexpr uint32_t kProbeCap = 256;  // probes before a table insert gives up (the wave falls back)
+constexpr uint32_t kDupScan = 512;   // entries per message the in-wave duplicate check holds in LDS
+constexpr int kTabWaves = kBlock / 64;
+
+struct StrTab {
+    unsigned long long* word;  // (key >> 32) << 32 | (entry slot + 1) of the string's first inserter; 0 = empty
+    uint32_t* first;           // smallest canonical entry index naming the string
+    uint64_t mask;
+};
+struct RecTab {
+    unsigned long long* word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
+    uint32_t* mint;            // smallest tag slot holding the record (arrival ordinal)
+    uint64_t mask;
+};
+
+__device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* bytes, uint64_t a, uint32_t set_a, unsigned long long key_a,
+                                            uint32_t len_a, unsigned long long pfx_a, uint64_t noff_a, uint64_t b) {
+    if (S.set[b] != set_a || S.key[b] != key_a || (S.meta[b] & 0x7FFFFFFFu) != len_a || S.pfx[b] != pfx_a) return false;
+    return len_a <= 8 || same_bytes(bytes + S.noff[b] + 8, bytes + noff_a + 8, len_a - 8);
+}
+
+__global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+                                                       const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ ne,
+                                                       const uint32_t* __restrict__ na, uint64_t m0, uint64_t m1, StrTab T,
+                                                       unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow) {
+    __shared__ uint32_t sh[kTabWaves][kDupScan];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
+    if (m >= m1) return;  // one message per wave: no workgroup barrier below
+    const uint32_t set = mset[m];
+    if (set == jg::kSkipIdx) return;
+    const uint32_t cnt = (uint32_t)ne[m];
+    if (cnt == 0) return;
+    const uint64_t es = (off[m] + kEntryDiv - 1) / kEntryDiv;
+    const uint32_t n_add = na[m] & 0x7FFFFFFFu, n_rem = cnt - n_add;
+    const bool rem_first = (na[m] >> 31) != 0;
+    bool over = false;
+    for (uint32_t q = lane; q < cnt; q += 64) {
+        const uint64_t slot = es + q;
+        const unsigned long long key = S.key[slot], pfx = S.pfx[slot];
+        const uint32_t meta = S.meta[slot], len = meta & 0x7FFFFFFFu;
+        const uint64_t noff = S.noff[slot];
+        const unsigned long long word = (key >> 32) << 32 | (slot + 1);
+        uint32_t sid = kNoSid;
+        uint64_t p = key & T.mask;
+        for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
+            unsigned long long w = T.word[p];
+            if (w == 0) {
+                w = atomicCAS(T.word + p, 0ull, word);
+                if (w == 0) {
+                    sid = (uint32_t)p;
+                    break;
+                }
+            }
+            if ((w >> 32) != (key >> 32)) continue;
+            if (same_string(S, bytes, slot, set, key, len, pfx, noff, (w & 0xFFFFFFFFull) - 1)) {
+                sid = (uint32_t)p;
+                break;
+            }
+        }
+        if (sid == kNoSid) {
+            over = true;
+        } else {
+            const uint32_t c = (uint32_t)es + (!rem_first ? q : (q < n_rem ? n_add + q : q - n_rem));  // canonical: addSet first
+            if (T.first[sid] > c) atomicMin(T.first + sid, c);
+        }
+        S.sid[slot] = sid;
+        if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
+    }
+    if (cnt > kDupScan) over = true;  // the duplicate check below would miss pairs: the sort path decides
+    if (__ballot(over) != 0) {
+        if (lane == 0) *overflow = 1;
+        return;
+    }
+    jgw::wave_sync();
+    // Decode's duplicate key: a (string, side) an earlier entry of this message already named (error at the
+    // later name; the message's error is the smallest position, k_ow_first_bad)
+    for (uint32_t q = lane; q < cnt; q += 64) {
+        const uint32_t x = sh[wv][q];
+        for (uint32_t p = 0; p < q; ++p)
+            if (sh[wv][p] == x) {
+                atomicMin(err + m, (unsigned long long)S.pos[es + q] << 2 | kKindInval);
+                break;
+            }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ow_rkeys(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+                                                     const unsigned long long* __restrict__ nt, uint64_t m0, uint64_t m1) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
+    if (m >= m1) return;
+    const uint32_t set = mset[m];
+    if (set == jg::kSkipIdx) return;
+    const uint32_t k = (uint32_t)nt[m];
+    const uint64_t es = (off[m] + kEntryDiv - 1) / kEntryDiv, ts = (off[m] + kTagDiv - 1) / kTagDiv;
+    for (uint32_t q = lane; q < k; q += 64) {
+        const unsigned long long r = S.tref[ts + q];
+        const unsigned long long side = r >> 62 & 1;
+        unsigned long long id;
+        if (r >> 63) {
+            id = 1ull << 63 | (unsigned long long)set << 1 | side;
+        } else {
+            const uint32_t sid = S.sid[es + (uint32_t)r];
+            id = sid == kNoSid ? kNone : ((unsigned long long)sid << 1 | side);
+        }
+        S.trk[ts + q] = id;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+                                                    const unsigned long long* __restrict__ nt, uint64_t m0, uint64_t m1, RecTab T,
+                                                    unsigned long long* __restrict__ overflow) {
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
+    if (m >= m1) return;
+    if (mset[m] == jg::kSkipIdx) return;
+    const uint32_t k = (uint32_t)nt[m];
+    const uint64_t ts = (off[m] + kTagDiv - 1) / kTagDiv;
+    bool over = false;
+    for (uint32_t q = lane; q < k; q += 64) {
+        const uint64_t t = ts + q;
+        const unsigned long long id = S.trk[t];
+        if (id == kNone) continue;  // its string found no slot: the overflow word is up already
+        const Tag16 g = S.tval[t];
+        const uint64_t h = rec_hash(id, g, 0);
+        const unsigned long long word = (h >> 32) << 32 | (t + 1);
+        uint64_t p = h & T.mask, slot = ~0ull;
+        for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
+            // most references repeat a record seen earlier in the wave: a plain load settles those
+            unsigned long long w = T.word[p];
+            if (w == 0) {
+                w = atomicCAS(T.word + p, 0ull, word);
+                if (w == 0) {
+                    slot = p;
+                    break;
+                }
+            }
+            if ((w >> 32) != (h >> 32)) continue;
+            const uint64_t u = (w & 0xFFFFFFFFull) - 1;
+            const Tag16 o = S.tval[u];
+            if (S.trk[u] == id && o.lo == g.lo && o.hi == g.hi) {
+                slot = p;
+                break;
+            }
+        }
+        if (slot == ~0ull) {
+            over = true;
+            continue;
+        }
+        if (T.mint[slot] > (uint32_t)t) atomicMin(T.mint + slot, (uint32_t)t);
+    }
+    if (__ballot(over) != 0 && lane == 0) *overflow = 1;
+}
+
+// ---- commit from the tables ----------------------------------------------------------------------------
+struct StrLive {  // a string whose first entry lies before the commit limit
+    const unsigned long long* word;
+    const uint32_t* first;
+    uint32_t lim;
+    __host__ __device__ bool operator()(const uint32_t& s) const { return word[s] != 0 && first[s] < lim; }
+};
+struct RecLive {  // a record of side `side` whose first occurrence lies before the commit limit
+    const unsigned long long* word;
+    const uint32_t* mint;
+    const unsigned long long* trk;
+    uint32_t lim, side;
+    __host__ __device__ bool operator()(const uint32_t& s) const {
+        const unsigned long long w = word[s];
+        return w != 0 && mint[s] < lim && (uint32_t)(trk[(w & 0xFFFFFFFFull) - 1] & 1) == side;
+    }
+};
+
+// Each live string looked up in the set's element table: sid_id[sid] = its id, or a new string marked
+// (set << 32 | first entry, to be sorted: ids go in first-insertion order per set).
+__global__ void k_ow_sresolve(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, const uint32_t* __restrict__ live,
+                              const unsigned long long* __restrict__ count, Names N, uint32_t* __restrict__ sid_id,
+                              unsigned long long* __restrict__ newk) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= *count) return;
+    const uint32_t sid = live[i];
+    const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+    const uint32_t set = S.set[ref];
+    const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], S.meta[ref] & 0x7FFFFFFFu);
+    sid_id[sid] = id;
+    newk[i] = id != kNoName ? kNone : ((unsigned long long)set << 32 | T.first[sid]);
+}
+
+__global__ void k_ow_gather_newsid(const unsigned long long* __restrict__ newk, const uint32_t* __restrict__ live,
+                                   const uint32_t* __restrict__ idx, const unsigned long long* __restrict__ count,
+                                   unsigned long long* __restrict__ keys, uint32_t* __restrict__ sids) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *count) return;
+    keys[j] = newk[idx[j]];
+    sids[j] = live[idx[j]];
+}
+
+// New strings sorted by (set, first entry): the r-th new string of a set takes next_id + r (k_ow_assign's
+// rule, from the string slots).
+__global__ void k_ow_sassign(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, const unsigned long long* __restrict__ snk,
+                             const uint32_t* __restrict__ snv, uint64_t nnew, uint64_t g0, Names N, uint32_t* __restrict__ sid_id,
+                             unsigned long long* __restrict__ status) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= nnew) return;
+    const uint32_t set = (uint32_t)(snk[k] >> 32);
+    const uint64_t r = k - set_begin(snk, nnew, set);
+    const uint64_t id = (uint64_t)N.next_id[set] + r;
+    if (id >= JG_NULL_ELEM - 1) atomicOr(status + 3, 1ull);
+    const uint32_t sid = snv[k];
+    const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+    const uint32_t len = S.meta[ref] & 0x7FFFFFFFu;
+    sid_id[sid] = (uint32_t)id;
+    const uint64_t g = g0 + k;
+    const unsigned long long p = atomicAdd(status + 2, (unsigned long long)len);
+    const uint8_t* src = bytes + S.noff[ref];
+    for (uint32_t q = 0; q < len; ++q) N.pool[p + q] = src[q];
+    N.set[g] = set;
+    N.id[g] = (uint32_t)id;
+    N.gen[g] = N.set_gen[set];
+    N.len[g] = len;
+    N.off[g] = p;
+    N.key[g] = S.key[ref];
+    tab_insert(N, S.key[ref], (uint32_t)g);
+}
+
+// One side's live records (their table slots, compacted): store keys, tags, and the slot (its mint is the ord).
+__global__ void k_ow_rgather(Sparse S, StrTab ST, RecTab RT, const uint32_t* __restrict__ sid_id, const uint32_t* __restrict__ idx,
+                             const unsigned long long* __restrict__ count, unsigned long long* __restrict__ dk, Tag16* __restrict__ dt,
+                             uint32_t* __restrict__ ds) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *count) return;
+    const uint32_t slot = idx[j];
+    const uint64_t u = (RT.word[slot] & 0xFFFFFFFFull) - 1;
+    const unsigned long long id = S.trk[u];
+    unsigned long long key;
+    if (id >> 63) {
+        key = ((id >> 1) & 0xFFFFFFFFull) << 32 | JG_NULL_ELEM;
+    } else {
+        const uint32_t sid = (uint32_t)(id >> 1);
+        const uint64_t ref = (ST.word[sid] & 0xFFFFFFFFull) - 1;
+        key = (unsigned long long)S.set[ref] << 32 | sid_id[sid];
+    }
+    dk[j] = key;
+    dt[j] = S.tval[u];
+    ds[j] = slot;
+}

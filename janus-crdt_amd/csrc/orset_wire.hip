@@ -360,8 +360,12 @@ struct Sparse {  // entry slots: sort key, string offset, length | side << 31, e
     unsigned long long* pfx;
     uint32_t* meta;
     uint32_t* pos;
+    uint32_t* set;             // the message's set
+    uint32_t* sid;             // the string's slot in the wave's string table (k_ow_strings)
     unsigned long long* tref;  // null << 63 | side << 62 | the entry's parse-order ordinal in its message
     Tag16* tval;
+    unsigned long long* trk;   // the record's identity without its tag (k_ow_rkeys): sid << 1 | side, or
+                               // 1 << 63 | set << 1 | side for a null tag set
 };
 
 struct ParseVis {
@@ -382,6 +386,7 @@ struct ParseVis {
         S.pfx[e] = pf;
         S.meta[e] = len | (uint32_t)side << 31;
         S.pos[e] = (uint32_t)(npos - base);
+        S.set[e] = set;
         n_add += side == 0;
         n_rem += side != 0;
     }
@@ -845,6 +850,8 @@ __global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const T
     oo[i] = mint[ds[p]];
 }
 
+#include "orset_tables.hpp"
+
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t p = 1024;
     while (p < x) p <<= 1;
@@ -878,7 +885,7 @@ struct jg_orset_wire {
     uint64_t first_bad = kNone, n_ent = 0, n_tag = 0;
     // entries, groups, tags, records
     jg::DevBuf ekey, eval, enoff, emsg, emeta, epos, epfx, eset, skey, sval, hs, seg, impure, label, gid, eid;
-    jg::DevBuf sp_key, sp_noff, sp_pfx, sp_meta, sp_pos, sp_tref, sp_tval;  // pass 1's sparse regions (by byte offset)
+    jg::DevBuf sp_key, sp_noff, sp_pfx, sp_meta, sp_pos, sp_set, sp_sid, sp_tref, sp_tval, sp_trk;  // pass 1's sparse regions (by byte offset)
     jg::DevBuf tref, tval, rkey, rside, dtab, dmin, dk[2], dt[2], ds[2], rk, rk2, perm[2], perm2[2];
     jg::DevBuf newk, newv, snk, snv, status, cub;
     jg::DevBuf cnk, fsel, fslot, fidx;  // commit: compacted new-string keys; dedup marks, slots, compacted indices
@@ -891,6 +898,12 @@ struct jg_orset_wire {
     // key bits the entry sort orders on; tests narrow it (JANUS_TEST_ENTRY_SORT_BITS) so runs mix full keys
     int sort_bits = 32;
     uint64_t resorts = 0;  // waves whose entries were sorted again on full keys (a long impure run)
+    // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
+    // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
+    jg::DevBuf st_word, st_first, rt_word, rt_mint, sid_id, ovf;
+    uint64_t st_cap = 0, rt_cap = 0;
+    bool tables = false, tables_ok = false;
+    uint64_t waves_fast = 0, waves_sorted = 0;  // commits from the tables / by the sort path (tests read them)
 };
 
 namespace {
@@ -1024,6 +1037,9 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
         grow_keep(ctx, w->sp_pfx, es * 8, ke * 8);
         grow_keep(ctx, w->sp_meta, es * 4, ke * 4);
         grow_keep(ctx, w->sp_pos, es * 4, ke * 4);
+        grow_keep(ctx, w->sp_set, es * 4, ke * 4);
+        grow_keep(ctx, w->sp_sid, es * 4, ke * 4);
+        grow_keep(ctx, w->sp_trk, ts * 8, kt * 8);
         grow_keep(ctx, w->sp_tref, ts * 8, kt * 8);
         grow_keep(ctx, w->sp_tval, ts * 16, kt * 16);
         w->cap_bytes = cap;
@@ -1046,8 +1062,8 @@ void grow_wave(jg_ctx* ctx, jg_orset_wire* w, uint64_t msgs, uint64_t bytes) {
 
 Sparse sparse_of(jg_orset_wire* w) {
     return Sparse{w->sp_key.as<unsigned long long>(), w->sp_noff.as<unsigned long long>(), w->sp_pfx.as<unsigned long long>(),
-                  w->sp_meta.as<uint32_t>(), w->sp_pos.as<uint32_t>(),
-                  w->sp_tref.as<unsigned long long>(), w->sp_tval.as<Tag16>()};
+                  w->sp_meta.as<uint32_t>(), w->sp_pos.as<uint32_t>(), w->sp_set.as<uint32_t>(), w->sp_sid.as<uint32_t>(),
+                  w->sp_tref.as<unsigned long long>(), w->sp_tval.as<Tag16>(), w->sp_trk.as<unsigned long long>()};
 }
 
 Entries entries_of(jg_orset_wire* w) {
@@ -1056,6 +1072,53 @@ Entries entries_of(jg_orset_wire* w) {
 }
 
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
+StrTab str_tab(jg_orset_wire* w) { return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1}; }
+RecTab rec_tab(jg_orset_wire* w) { return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1}; }
+
+// A wave opens: size and clear its string / record tables (queued on the compute stream, ahead of the first
+// chunk's parse).  A compact entry needs >= 43 payload bytes ("":["<guid>"]) and a tag reference >= 38, so
+// nbytes / 40 and nbytes / 38 bound the distinct strings and records; a streamed wave sized by its message
+// count alone gets 16 strings / 32 records per message and falls back to the sort path if it holds more.
+// JANUS_ORSET_TAIL=sort runs the sort path alone (read per wave: tests switch it).
+void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbytes) {
+    const char* e = std::getenv("JANUS_ORSET_TAIL");
+    w->tables = !(e && std::strcmp(e, "sort") == 0) && nbytes / kEntryDiv + 2 < 0xFFFFFFFFull && nbytes / kTagDiv + 2 < 0xFFFFFFFFull;
+    w->tables_ok = false;
+    if (!w->tables) return;
+    const uint64_t lim = 1ull << 30;  // slot ids < 2^31 (k_ow_strings packs the side above them); hipcub counts in int
+    const uint64_t sc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, 2 * std::max(nbytes / 40, n_msgs * 16) + 64)));
+    const uint64_t rc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, 2 * std::max(nbytes / 38, n_msgs * 32) + 64)));
+    if (w->st_cap < sc) {
+        w->st_word.alloc(sc * 8);
+        w->st_first.alloc(sc * 4);
+        w->sid_id.alloc(sc * 4);
+        w->st_cap = sc;
+    }
+    if (w->rt_cap < rc) {
+        w->rt_word.alloc(rc * 8);
+        w->rt_mint.alloc(rc * 4);
+        w->rt_cap = rc;
+    }
+    if (!w->ovf.p) w->ovf.alloc(8);
+    JG_HIP(hipMemsetAsync(w->st_word.p, 0, w->st_cap * 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->st_first.p, 0xFF, w->st_cap * 4, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->rt_word.p, 0, w->rt_cap * 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->rt_mint.p, 0xFF, w->rt_cap * 4, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->ovf.p, 0, 8, ctx->stream));
+}
+
+// The chunk's strings and records into the wave's tables (after its parse, same stream).
+void launch_tables(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
+    const dim3 grid((unsigned)((m1 - m0 + kTabWaves - 1) / kTabWaves));
+    const Sparse S = sparse_of(w);
+    auto* ovf = w->ovf.as<unsigned long long>();
+    hipLaunchKernelGGL(k_ow_strings, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->vbytes, w->ne.as<unsigned long long>(),
+                       w->na.as<uint32_t>(), m0, m1, str_tab(w), w->err.as<unsigned long long>(), ovf);
+    hipLaunchKernelGGL(k_ow_rkeys, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1);
+    hipLaunchKernelGGL(k_ow_rins, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1, rec_tab(w), ovf);
+    JG_HIP(hipGetLastError());
+}
+
 // One wave per message (k_ow_group, orset_group.hpp), then the serial parse of the messages it left;
 // JANUS_ORSET_PARSE=serial runs the serial parse alone, =group the group parse alone (read per chunk: tests
 // switch it).
@@ -1079,6 +1142,7 @@ void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
                            sparse_of(w), w->kmask, w->salt, w->ne.as<unsigned long long>(), w->nt.as<unsigned long long>(), w->na.as<uint32_t>(),
                            w->err.as<unsigned long long>(), slow);
     JG_HIP(hipGetLastError());
+    if (w->tables) launch_tables(ctx, w, m0, m1);
 }
 
 // Passes 2 + grouping over the whole wave; sets w->first_bad.  Returns the first bad message's code.
@@ -1088,7 +1152,28 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     w->checked = true;
     w->first_bad = kNone;
     w->n_ent = w->n_tag = 0;
+    w->tables_ok = false;
     if (n == 0) return JG_OK;
+    if (w->tables) {  // the chunks filled the tables (and reported repeated names): the first bad message is all
+        unsigned long long* st = status_words(w);  // that is left, unless a table overflowed
+        JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
+        hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(st + 1, w->ovf.p, 8, hipMemcpyDeviceToDevice, ctx->stream));
+        unsigned long long h[2];
+        read_words(ctx, st, h, 2);
+        const char* e = std::getenv("JANUS_ORSET_TAIL");  // =tables (tests): no fall-back, an overflow is an error
+        JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
+        if (h[1] == 0) {
+            w->tables_ok = true;
+            if (h[0] == kNone) return JG_OK;
+            unsigned long long e;
+            JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + h[0], 8, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            w->first_bad = h[0];
+            return (e & 3) == kKindState ? JG_ESTATE : JG_EINVAL;
+        }
+    }
     // offsets: exclusive sums with a zero sentinel at [n]
     JG_HIP(hipMemsetAsync(w->ne.as<unsigned long long>() + n, 0, 8, ctx->stream));
     JG_HIP(hipMemsetAsync(w->nt.as<unsigned long long>() + n, 0, 8, ctx->stream));
@@ -1215,7 +1300,7 @@ void sort_side_begin(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_
     JG_HIP(hipGetLastError());
 }
 
-void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out, bool long_run) {
+void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out, bool long_run, const uint32_t* mint) {
     if (n == 0) return;
     const auto* dk = w->dk[sd].as<unsigned long long>();
     const auto* dt = w->dt[sd].as<Tag16>();
@@ -1231,13 +1316,123 @@ void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bi
             std::swap(p, q);
         }
     }
-    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), w->dmin.as<uint32_t>(), p,
+    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), mint, p,
                        n, out.key.as<unsigned long long>(), out.tag.as<Tag16>(), out.ord.as<uint32_t>());
     JG_HIP(hipGetLastError());
 }
 
+// Commit from the wave's tables: the distinct strings whose first entry lies before the limit resolved against
+// the element table (new ones take ids in (set, first entry) order), the distinct records before the limit
+// keyed, sorted and unioned into the store; ords = first tag slot (ordered like commit order, < next).
+void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
+    jg_ctx* ctx = s->ctx;
+    const uint64_t n = w->wn;
+    uint64_t lim_off = w->wnb;
+    if (limit < n) {  // the limit message's byte offset
+        JG_HIP(hipMemcpyAsync(&lim_off, w->voff + limit, 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    const uint32_t csi_lim = limit < n ? (uint32_t)((lim_off + kEntryDiv - 1) / kEntryDiv) : 0xFFFFFFFFu;
+    const uint32_t t_lim = limit < n ? (uint32_t)((lim_off + kTagDiv - 1) / kTagDiv) : 0xFFFFFFFFu;
+    const uint64_t t_next = (w->wnb + kTagDiv - 1) / kTagDiv + 1;  // every tag slot of the wave is below this
+    ensure_sets(ctx, w, (uint64_t)w->max_set + 1);
+    ensure_names(ctx, w, 0, 0);
+    unsigned long long* st = status_words(w);
+    const Sparse S = sparse_of(w);
+    const StrTab ST = str_tab(w);
+    const RecTab RT = rec_tab(w);
+    // live strings
+    ensure(w->newv, w->st_cap * 4);
+    JG_HIP(hipMemsetAsync(st, 0, 64, ctx->stream));
+    select_marked(ctx, w, StrLive{ST.word, ST.first, csi_lim}, w->st_cap, w->newv.as<uint32_t>(), st + 1);
+    unsigned long long h[2];
+    read_words(ctx, st, h, 2);
+    const uint64_t ns = h[1];
+    if (ns) {
+        ensure(w->newk, ns * 8);
+        ensure(w->fidx, ns * 4);
+        ensure(w->cnk, ns * 8);
+        ensure(w->gid, ns * 4);
+        hipLaunchKernelGGL(k_ow_sresolve, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, w->newv.as<uint32_t>(), st + 1,
+                           names_of(w), w->sid_id.as<uint32_t>(), w->newk.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        select_marked(ctx, w, IsNewAt{w->newk.as<unsigned long long>()}, ns, w->fidx.as<uint32_t>(), st + 5);
+        hipLaunchKernelGGL(k_ow_gather_newsid, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, w->newk.as<unsigned long long>(),
+                           w->newv.as<uint32_t>(), w->fidx.as<uint32_t>(), st + 5, w->cnk.as<unsigned long long>(), w->gid.as<uint32_t>());
+        JG_HIP(hipGetLastError());
+        unsigned long long c5;
+        read_words(ctx, st + 5, &c5, 1);
+        const uint64_t nnew = c5;
+        if (nnew) {
+            ensure_names(ctx, w, nnew, w->wnb);
+            ensure(w->snk, nnew * 8);
+            ensure(w->snv, nnew * 4);
+            sort_pairs(ctx, w, w->cnk.as<unsigned long long>(), w->snk.as<unsigned long long>(), w->gid.as<uint32_t>(), w->snv.as<uint32_t>(), nnew,
+                       32 + bits_for(w->max_set));
+            const unsigned long long init[4] = {0, 0, w->pool_used, 0};
+            JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL(k_ow_sassign, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, w->snk.as<unsigned long long>(),
+                               w->snv.as<uint32_t>(), nnew, w->n_names, names_of(w), w->sid_id.as<uint32_t>(), st);
+            JG_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_ow_next_ids, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, w->snk.as<unsigned long long>(), nnew,
+                               names_of(w));
+            JG_HIP(hipGetLastError());
+            unsigned long long hh[4];
+            read_words(ctx, st, hh, 4);
+            JG_REQUIRE(hh[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
+            w->n_names += nnew;
+            w->pool_used = hh[2];
+            w->g1 = w->n_names;
+            w->p1 = w->pool_used;
+        }
+    }
+    // live records, per side
+    ensure(w->fidx, w->rt_cap * 4);
+    ensure(w->fslot, w->rt_cap * 4);
+    JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
+    select_marked(ctx, w, RecLive{RT.word, RT.mint, S.trk, t_lim, 0}, w->rt_cap, w->fidx.as<uint32_t>(), st + 4);
+    select_marked(ctx, w, RecLive{RT.word, RT.mint, S.trk, t_lim, 1}, w->rt_cap, w->fslot.as<uint32_t>(), st + 5);
+    unsigned long long cnt[2];
+    read_words(ctx, st + 4, cnt, 2);
+    if (cnt[0] + cnt[1] == 0) return;
+    for (int sd = 0; sd < 2; ++sd) {
+        ensure(w->dk[sd], cnt[sd] * 8 + 8);
+        ensure(w->dt[sd], cnt[sd] * 16 + 16);
+        ensure(w->ds[sd], cnt[sd] * 4 + 4);
+        if (cnt[sd] == 0) continue;
+        hipLaunchKernelGGL(k_ow_rgather, dim3(blocks_for(cnt[sd])), dim3(kBlock), 0, ctx->stream, S, ST, RT, w->sid_id.as<uint32_t>(),
+                           (sd ? w->fslot : w->fidx).as<uint32_t>(), st + 4 + sd, w->dk[sd].as<unsigned long long>(), w->dt[sd].as<Tag16>(),
+                           w->ds[sd].as<uint32_t>());
+        JG_HIP(hipGetLastError());
+    }
+    if (!w->recs) {
+        w->recs = new jg_orset();
+        w->recs->ctx = ctx;
+    }
+    const int key_bits = 32 + bits_for(w->max_set);
+    const uint64_t nmax = std::max(cnt[0], cnt[1]);
+    ensure(w->rk, nmax * 8);
+    ensure(w->rk2, nmax * 8);
+    sort_side_begin(ctx, w, 0, cnt[0], key_bits, t_next, w->recs->add, st + 6);
+    sort_side_begin(ctx, w, 1, cnt[1], key_bits, t_next, w->recs->rem, st + 7);
+    unsigned long long long_run[2];
+    read_words(ctx, st + 6, long_run, 2);
+    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, RT.mint);
+    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, RT.mint);
+    jg::orset_merge_store(s, w->recs);
+}
+
 void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     jg_ctx* ctx = s->ctx;
+    w->g0 = w->g1 = w->n_names;
+    w->p0 = w->p1 = w->pool_used;
+    if (limit == 0) return;
+    if (w->tables_ok) {
+        ++w->waves_fast;
+        commit_tables(s, w, limit);
+        return;
+    }
+    ++w->waves_sorted;
     const uint64_t ne = w->n_ent, nt = w->n_tag;
     w->g0 = w->g1 = w->n_names;
     w->p0 = w->p1 = w->pool_used;
@@ -1340,8 +1535,8 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     sort_side_begin(ctx, w, 1, cnt[1], key_bits, nt, w->recs->rem, st + 7);
     unsigned long long long_run[2];
     read_words(ctx, st + 6, long_run, 2);
-    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0);
-    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0);
+    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, w->dmin.as<uint32_t>());
+    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, w->dmin.as<uint32_t>());
     jg::orset_merge_store(s, w->recs);
 }
 
@@ -1368,6 +1563,7 @@ void orset_node_begin(jg_orset* s, uint8_t* bytes, uint64_t* off, uint32_t* mset
     w->voff = off;
     w->vmset = mset;
     grow_wave(ctx, w, std::max<uint64_t>(n, 1), std::max<uint64_t>(nbytes, 1));
+    tables_begin(ctx, w, n, nbytes);
     w->wn = n;
     w->wnb = nbytes;
     w->max_set = max_set;
@@ -1478,6 +1674,7 @@ int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
         jg_orset_wire* w = wire_of(s);
         close_wave(w);
         grow_wave(ctx, w, std::max<uint64_t>(cap_msgs, 1), std::max<uint64_t>(cap_bytes, 1));
+        tables_begin(ctx, w, cap_msgs, cap_bytes);
         JG_HIP(hipMemsetAsync(w->off.p, 0, 8, ctx->stream));  // off[0] = 0
         // the uploads run on ctx->copy: the previous wave's kernels must be done with these buffers
         JG_HIP(hipStreamSynchronize(ctx->stream));

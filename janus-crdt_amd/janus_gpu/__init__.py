@@ -539,7 +539,7 @@ class ORSetStore:
         Returns (check code, bad message or None)."""
         n = sum(len(c[1]) for c in chunks)
         keep = []
-        _check(load().jg_orset_wave_begin(self._h, n, 0))
+        _check(load().jg_orset_wave_begin(self._h, n, sum(len(m) for c in chunks for m in c[1])))
         for set_ids, msgs in chunks:
             data, off = pack_wave(msgs)
             s = _arr(set_ids, np.uint32)

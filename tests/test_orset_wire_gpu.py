@@ -65,20 +65,26 @@ def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3)
         s.close()
 
 
+TAIL = ["tables", "sort"]  # JANUS_ORSET_TAIL: the per-chunk string / record tables (strict: no fall-back), or the sort path
 PARSE = ["auto", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
 
 
+@pytest.mark.parametrize("tail", TAIL)
 @pytest.mark.parametrize("parse", PARSE)
 @pytest.mark.parametrize("seed,n_sets,waves,per_wave", [(1, 3, 3, 40), (2, 64, 3, 600), (3, 500, 2, 3000)])
-def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave, parse, monkeypatch):
+def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave, parse, tail, monkeypatch):
     monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
+    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
     _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default", "raw", "all"))
 
 
+@pytest.mark.parametrize("tail", TAIL)
 @pytest.mark.parametrize("parse", ["group", "default"])
-def test_compact_waves_match_oracle(ctx, parse, monkeypatch):
+def test_compact_waves_match_oracle(ctx, parse, tail, monkeypatch):
     """Reference-shaped compact states only (ASCII names, no whitespace, members in the encoder's order):
-    every message takes the group parse (JANUS_ORSET_PARSE=group rejects any message it leaves)."""
+    every message takes the group parse (JANUS_ORSET_PARSE=group rejects any message it leaves), and
+    with JANUS_ORSET_TAIL=tables every wave commits from the per-chunk tables."""
+    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
     if parse == "group":
         monkeypatch.setenv("JANUS_ORSET_PARSE", "group")
     rng = np.random.default_rng(11)
@@ -132,8 +138,9 @@ def test_group_parse_mutants_equal_serial(ctx, monkeypatch):
              J.encode_orset([(f"n{j}", [G1, G2]) for j in range(6)], [("n1", [G1])], [], [G3])]
     muts = [m for b in bases for m in _mutants(rng, b, 160)] + bases
     results = {}
-    for mode in PARSE:
+    for mode, tail in (("auto", "tables"), ("serial", "sort")):
         monkeypatch.setenv("JANUS_ORSET_PARSE", mode)
+        monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
         s = jg.ORSetStore(ctx)
         try:
             codes = []
@@ -193,10 +200,12 @@ def test_hash_collisions_take_the_exact_path(ctx, monkeypatch):
     _run_waves(ctx, 4, 6, 3, 120, modes=("default", "raw"))
 
 
-def test_entry_runs_mixing_full_keys(ctx, monkeypatch):
+@pytest.mark.parametrize("tail", ["auto", "sort"])
+def test_entry_runs_mixing_full_keys(ctx, tail, monkeypatch):
     """With the entry sort narrowed to 4 key bits every run holds strings whose full keys differ: the run is
     labelled string by string and each string is looked up under its own full key."""
     monkeypatch.setenv("JANUS_TEST_ENTRY_SORT_BITS", "4")
+    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
     _run_waves(ctx, 5, 6, 3, 120, modes=("default", "raw"))
 
 
@@ -266,12 +275,14 @@ _CASES = [
 ]
 
 
+@pytest.mark.parametrize("tail", TAIL)
 @pytest.mark.parametrize("parse", PARSE)
 @pytest.mark.parametrize("idx", range(len(_CASES)))
-def test_contract_case_in_a_wave(ctx, idx, parse, monkeypatch):
+def test_contract_case_in_a_wave(ctx, idx, parse, tail, monkeypatch):
     """Case payload at position 3 of a 6-message wave: the first bad message and its code, then the
     prefix before it merges exactly as the oracle's loop leaves the store."""
     monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
+    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
     payload, code = _CASES[idx]
     dec = orc.json_decode_orset(payload)
     if code is None:
@@ -342,8 +353,10 @@ def test_element_with_many_new_tags(ctx, n_tags):
 def test_hot_name_in_long_impure_runs(ctx, monkeypatch):
     """A name repeated thousands of times in a run that also holds other strings (the entry sort narrowed to 4
     key bits, so every run mixes strings): labelling scans an impure run only up to 64 entries, then the wave's
-    entries are sorted again on their whole keys — linear work, the oracle's result."""
+    entries are sorted again on their whole keys — linear work, the oracle's result.  (The sort path's
+    labelling: JANUS_ORSET_TAIL=sort.)"""
     import time
+    monkeypatch.setenv("JANUS_ORSET_TAIL", "sort")
     monkeypatch.setenv("JANUS_TEST_ENTRY_SORT_BITS", "4")
     rng = np.random.default_rng(15)
     hot = J.random_guids(rng, 1)
