@@ -33,16 +33,54 @@ constexpr uint32_t kProbeCap = 256;  // probes before a table insert gives up (t
 constexpr uint32_t kDupScan = 512;   // entries per message the in-wave duplicate check holds in LDS
 constexpr int kTabWaves = kBlock / 64;
 
+// The slots a table's inserts claimed, appended as they are claimed, so the commit walks these instead of the
+// whole table: kLists sub-lists of sub_cap entries (list j of workgroup blockIdx % kLists, count n[j]) —
+// one counter took every wave's append and serialised the insert kernels (360 us per 32k-state chunk).
+constexpr uint32_t kLists = 16;
+constexpr uint32_t kCountStride = 32;  // counters 256 B apart: atomics on one L2 line serialise
 struct StrTab {
     unsigned long long* word;  // (key >> 32) << 32 | (entry slot + 1) of the string's first inserter; 0 = empty
     uint32_t* first;           // smallest canonical entry index naming the string
     uint64_t mask;
+    uint32_t* list;
+    unsigned long long* n;
+    uint64_t sub_cap;
 };
 struct RecTab {
     unsigned long long* word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
     uint32_t* mint;            // smallest tag slot holding the record (arrival ordinal)
     uint64_t mask;
+    uint32_t* list;
+    unsigned long long* n;
+    uint64_t sub_cap;
 };
+
+// Lanes that claimed a slot append it to their workgroup's sub-list: one atomic per wave (claims are a few
+// per message).  A full sub-list raises the overflow word (the wave takes the sort path).
+__device__ __forceinline__ void list_append(bool fresh, uint32_t slot, uint32_t* list, unsigned long long* n, uint64_t sub_cap,
+                                            unsigned long long* overflow) {
+    const unsigned long long b = __ballot(fresh);
+    if (!b) return;
+    const uint32_t lane = threadIdx.x & 63, j = blockIdx.x % kLists;
+    const int leader = __ffsll((long long)b) - 1;
+    unsigned long long base = 0;
+    if ((int)lane == leader) base = atomicAdd(n + j * kCountStride, (unsigned long long)__popcll(b));
+    base = __shfl(base, leader);
+    const unsigned long long at = base + __popcll(b & ((1ull << lane) - 1ull));
+    if (!fresh) return;
+    if (at < sub_cap) list[j * sub_cap + at] = slot;
+    else *overflow = 1;
+}
+
+// The sub-lists packed back to back (offs[j] = where sub-list j starts; offs[kLists] = the total).
+__global__ void k_list_pack(const uint32_t* __restrict__ list, uint64_t sub_cap, const unsigned long long* __restrict__ offs,
+                            uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= offs[kLists]) return;
+    uint32_t j = 0;
+    while (offs[j + 1] <= i) ++j;
+    out[i] = list[j * sub_cap + (i - offs[j])];
+}
 
 __device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* bytes, uint64_t a, uint32_t set_a, unsigned long long key_a,
                                             uint32_t len_a, unsigned long long pfx_a, uint64_t noff_a, uint64_t b) {
@@ -66,13 +104,16 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
     const uint32_t n_add = na[m] & 0x7FFFFFFFu, n_rem = cnt - n_add;
     const bool rem_first = (na[m] >> 31) != 0;
     bool over = false;
-    for (uint32_t q = lane; q < cnt; q += 64) {
+    for (uint32_t q0 = 0; q0 < cnt; q0 += 64) {  // wave-uniform bounds: list_append's ballot needs every lane
+        const uint32_t q = q0 + lane;
+        bool fresh = false;
+        uint32_t sid = kNoSid;
+        if (q < cnt) {
         const uint64_t slot = es + q;
         const unsigned long long key = S.key[slot], pfx = S.pfx[slot];
         const uint32_t meta = S.meta[slot], len = meta & 0x7FFFFFFFu;
         const uint64_t noff = S.noff[slot];
         const unsigned long long word = (key >> 32) << 32 | (slot + 1);
-        uint32_t sid = kNoSid;
         uint64_t p = key & T.mask;
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
             unsigned long long w = T.word[p];
@@ -80,6 +121,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                 w = atomicCAS(T.word + p, 0ull, word);
                 if (w == 0) {
                     sid = (uint32_t)p;
+                    fresh = true;
                     break;
                 }
             }
@@ -97,6 +139,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         }
         S.sid[slot] = sid;
         if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
+        }
+        list_append(fresh, sid, T.list, T.n, T.sub_cap, overflow);
     }
     if (cnt > kDupScan) over = true;  // the duplicate check below would miss pairs: the sort path decides
     if (__ballot(over) != 0) {
@@ -149,14 +193,17 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
     const uint32_t k = (uint32_t)nt[m];
     const uint64_t ts = (off[m] + kTagDiv - 1) / kTagDiv;
     bool over = false;
-    for (uint32_t q = lane; q < k; q += 64) {
+    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+        const uint32_t q = q0 + lane;
         const uint64_t t = ts + q;
-        const unsigned long long id = S.trk[t];
-        if (id == kNone) continue;  // its string found no slot: the overflow word is up already
+        const unsigned long long id = q < k ? S.trk[t] : kNone;
+        bool fresh = false;
+        uint64_t slot = ~0ull;
+        if (id != kNone) {  // kNone: its string found no slot (the overflow word is up already), or past the message
         const Tag16 g = S.tval[t];
         const uint64_t h = rec_hash(id, g, 0);
         const unsigned long long word = (h >> 32) << 32 | (t + 1);
-        uint64_t p = h & T.mask, slot = ~0ull;
+        uint64_t p = h & T.mask;
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
             // most references repeat a record seen earlier in the wave: a plain load settles those
             unsigned long long w = T.word[p];
@@ -164,6 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
                 w = atomicCAS(T.word + p, 0ull, word);
                 if (w == 0) {
                     slot = p;
+                    fresh = true;
                     break;
                 }
             }
@@ -175,41 +223,39 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
                 break;
             }
         }
-        if (slot == ~0ull) {
-            over = true;
-            continue;
+        if (slot == ~0ull) over = true;
+        else if (T.mint[slot] > (uint32_t)t) atomicMin(T.mint + slot, (uint32_t)t);
         }
-        if (T.mint[slot] > (uint32_t)t) atomicMin(T.mint + slot, (uint32_t)t);
+        list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow);
     }
     if (__ballot(over) != 0 && lane == 0) *overflow = 1;
 }
 
 // ---- commit from the tables ----------------------------------------------------------------------------
-struct StrLive {  // a string whose first entry lies before the commit limit
-    const unsigned long long* word;
-    const uint32_t* first;
-    uint32_t lim;
-    __host__ __device__ bool operator()(const uint32_t& s) const { return word[s] != 0 && first[s] < lim; }
-};
-struct RecLive {  // a record of side `side` whose first occurrence lies before the commit limit
+struct RecLive {  // list entry i: a record of side `side` whose first occurrence lies before the commit limit
+    const uint32_t* list;
     const unsigned long long* word;
     const uint32_t* mint;
     const unsigned long long* trk;
     uint32_t lim, side;
-    __host__ __device__ bool operator()(const uint32_t& s) const {
-        const unsigned long long w = word[s];
-        return w != 0 && mint[s] < lim && (uint32_t)(trk[(w & 0xFFFFFFFFull) - 1] & 1) == side;
+    __host__ __device__ bool operator()(const uint32_t& i) const {
+        const uint32_t s = list[i];
+        return mint[s] < lim && (uint32_t)(trk[(word[s] & 0xFFFFFFFFull) - 1] & 1) == side;
     }
 };
 
-// Each live string looked up in the set's element table: sid_id[sid] = its id, or a new string marked
-// (set << 32 | first entry, to be sorted: ids go in first-insertion order per set).
-__global__ void k_ow_sresolve(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, const uint32_t* __restrict__ live,
-                              const unsigned long long* __restrict__ count, Names N, uint32_t* __restrict__ sid_id,
-                              unsigned long long* __restrict__ newk) {
+// Each string of the table's list whose first entry lies before the limit, looked up in the set's element
+// table: sid_id[sid] = its id, or a new string marked (set << 32 | first entry, to be sorted: ids go in
+// first-insertion order per set).
+__global__ void k_ow_sresolve(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, uint64_t count, uint32_t lim, Names N,
+                              uint32_t* __restrict__ sid_id, unsigned long long* __restrict__ newk) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= *count) return;
-    const uint32_t sid = live[i];
+    if (i >= count) return;
+    const uint32_t sid = T.list[i];
+    if (T.first[sid] >= lim) {
+        newk[i] = kNone;
+        return;
+    }
     const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
     const uint32_t set = S.set[ref];
     const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], S.meta[ref] & 0x7FFFFFFFu);
@@ -228,13 +274,16 @@ __global__ void k_ow_gather_newsid(const unsigned long long* __restrict__ newk, 
 
 // New strings sorted by (set, first entry): the r-th new string of a set takes next_id + r (k_ow_assign's
 // rule, from the string slots).
+// snk / snv: the wave's listed strings sorted by that key, the known ones (kNone) last; status[1] counts the
+// new ones (the caller learns it at its next read, no sync here).
 __global__ void k_ow_sassign(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, const unsigned long long* __restrict__ snk,
-                             const uint32_t* __restrict__ snv, uint64_t nnew, uint64_t g0, Names N, uint32_t* __restrict__ sid_id,
+                             const uint32_t* __restrict__ snv, uint64_t ns, uint64_t g0, Names N, uint32_t* __restrict__ sid_id,
                              unsigned long long* __restrict__ status) {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= nnew) return;
+    if (k >= ns || snk[k] == kNone) return;
+    if (k + 1 == ns || snk[k + 1] == kNone) status[1] = k + 1;  // the last new string: their count
     const uint32_t set = (uint32_t)(snk[k] >> 32);
-    const uint64_t r = k - set_begin(snk, nnew, set);
+    const uint64_t r = k - set_begin(snk, ns, set);
     const uint64_t id = (uint64_t)N.next_id[set] + r;
     if (id >= JG_NULL_ELEM - 1) atomicOr(status + 3, 1ull);
     const uint32_t sid = snv[k];
@@ -260,7 +309,7 @@ __global__ void k_ow_rgather(Sparse S, StrTab ST, RecTab RT, const uint32_t* __r
                              uint32_t* __restrict__ ds) {
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= *count) return;
-    const uint32_t slot = idx[j];
+    const uint32_t slot = RT.list[idx[j]];
     const uint64_t u = (RT.word[slot] & 0xFFFFFFFFull) - 1;
     const unsigned long long id = S.trk[u];
     unsigned long long key;
@@ -274,4 +323,13 @@ __global__ void k_ow_rgather(Sparse S, StrTab ST, RecTab RT, const uint32_t* __r
     dk[j] = key;
     dt[j] = S.tval[u];
     ds[j] = slot;
+}
+
+// next_id of every set that took new strings (the sorted list's last new string of each set); kNone = known.
+__global__ void k_ow_snext_ids(const unsigned long long* __restrict__ snk, uint64_t ns, Names N) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= ns || snk[k] == kNone) return;
+    const uint32_t set = (uint32_t)(snk[k] >> 32);
+    if (k + 1 < ns && snk[k + 1] != kNone && (uint32_t)(snk[k + 1] >> 32) == set) return;  // not the set's last new string
+    N.next_id[set] += (uint32_t)(k + 1 - set_begin(snk, ns, set));
 }

@@ -900,9 +900,11 @@ struct jg_orset_wire {
     uint64_t resorts = 0;  // waves whose entries were sorted again on full keys (a long impure run)
     // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
-    jg::DevBuf st_word, st_first, rt_word, rt_mint, sid_id, ovf;
+    jg::DevBuf st_word, st_first, st_list, rt_word, rt_mint, rt_list, sid_id, ovf;  // ovf: overflow word, sub-list counts
+    jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
     uint64_t st_cap = 0, rt_cap = 0;
     bool tables = false, tables_ok = false;
+    std::vector<unsigned long long> lc;  // host copy of ovf (overflow word, sub-list counts) taken by the check
     uint64_t waves_fast = 0, waves_sorted = 0;  // commits from the tables / by the sort path (tests read them)
 };
 
@@ -1072,8 +1074,14 @@ Entries entries_of(jg_orset_wire* w) {
 }
 
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
-StrTab str_tab(jg_orset_wire* w) { return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1}; }
-RecTab rec_tab(jg_orset_wire* w) { return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1}; }
+StrTab str_tab(jg_orset_wire* w) {
+    return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
+                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8};
+}
+RecTab rec_tab(jg_orset_wire* w) {
+    return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
+                  w->ovf.as<unsigned long long>() + (1 + kLists) * kCountStride, w->rt_cap / 8};
+}
 
 // A wave opens: size and clear its string / record tables (queued on the compute stream, ahead of the first
 // chunk's parse).  A compact entry needs >= 43 payload bytes ("":["<guid>"]) and a tag reference >= 38, so
@@ -1091,20 +1099,22 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     if (w->st_cap < sc) {
         w->st_word.alloc(sc * 8);
         w->st_first.alloc(sc * 4);
+        w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
         w->st_cap = sc;
     }
     if (w->rt_cap < rc) {
         w->rt_word.alloc(rc * 8);
         w->rt_mint.alloc(rc * 4);
+        w->rt_list.alloc((rc / 8) * kLists * 4);
         w->rt_cap = rc;
     }
-    if (!w->ovf.p) w->ovf.alloc(8);
+    if (!w->ovf.p) w->ovf.alloc((1 + 2 * kLists) * kCountStride * 8);
     JG_HIP(hipMemsetAsync(w->st_word.p, 0, w->st_cap * 8, ctx->stream));
     JG_HIP(hipMemsetAsync(w->st_first.p, 0xFF, w->st_cap * 4, ctx->stream));
     JG_HIP(hipMemsetAsync(w->rt_word.p, 0, w->rt_cap * 8, ctx->stream));
     JG_HIP(hipMemsetAsync(w->rt_mint.p, 0xFF, w->rt_cap * 4, ctx->stream));
-    JG_HIP(hipMemsetAsync(w->ovf.p, 0, 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(w->ovf.p, 0, (1 + 2 * kLists) * kCountStride * 8, ctx->stream));  // overflow, sub-list counts
 }
 
 // The chunk's strings and records into the wave's tables (after its parse, same stream).
@@ -1159,9 +1169,12 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
         hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
         JG_HIP(hipGetLastError());
-        JG_HIP(hipMemcpyAsync(st + 1, w->ovf.p, 8, hipMemcpyDeviceToDevice, ctx->stream));
+        // the overflow word and the tables' sub-list counts (the commit's) come back with the first bad message
+        w->lc.resize((1 + 2 * kLists) * kCountStride);
+        JG_HIP(hipMemcpyAsync(w->lc.data(), w->ovf.p, w->lc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
         unsigned long long h[2];
-        read_words(ctx, st, h, 2);
+        read_words(ctx, st, h, 1);
+        h[1] = w->lc[0];
         const char* e = std::getenv("JANUS_ORSET_TAIL");  // =tables (tests): no fall-back, an overflow is an error
         JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
         if (h[1] == 0) {
@@ -1339,61 +1352,65 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     ensure_names(ctx, w, 0, 0);
     unsigned long long* st = status_words(w);
     const Sparse S = sparse_of(w);
-    const StrTab ST = str_tab(w);
-    const RecTab RT = rec_tab(w);
-    // live strings
-    ensure(w->newv, w->st_cap * 4);
-    JG_HIP(hipMemsetAsync(st, 0, 64, ctx->stream));
-    select_marked(ctx, w, StrLive{ST.word, ST.first, csi_lim}, w->st_cap, w->newv.as<uint32_t>(), st + 1);
-    unsigned long long h[2];
-    read_words(ctx, st, h, 2);
-    const uint64_t ns = h[1];
-    if (ns) {
-        ensure(w->newk, ns * 8);
-        ensure(w->fidx, ns * 4);
-        ensure(w->cnk, ns * 8);
-        ensure(w->gid, ns * 4);
-        hipLaunchKernelGGL(k_ow_sresolve, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, w->newv.as<uint32_t>(), st + 1,
-                           names_of(w), w->sid_id.as<uint32_t>(), w->newk.as<unsigned long long>());
-        JG_HIP(hipGetLastError());
-        select_marked(ctx, w, IsNewAt{w->newk.as<unsigned long long>()}, ns, w->fidx.as<uint32_t>(), st + 5);
-        hipLaunchKernelGGL(k_ow_gather_newsid, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, w->newk.as<unsigned long long>(),
-                           w->newv.as<uint32_t>(), w->fidx.as<uint32_t>(), st + 5, w->cnk.as<unsigned long long>(), w->gid.as<uint32_t>());
-        JG_HIP(hipGetLastError());
-        unsigned long long c5;
-        read_words(ctx, st + 5, &c5, 1);
-        const uint64_t nnew = c5;
-        if (nnew) {
-            ensure_names(ctx, w, nnew, w->wnb);
-            ensure(w->snk, nnew * 8);
-            ensure(w->snv, nnew * 4);
-            sort_pairs(ctx, w, w->cnk.as<unsigned long long>(), w->snk.as<unsigned long long>(), w->gid.as<uint32_t>(), w->snv.as<uint32_t>(), nnew,
-                       32 + bits_for(w->max_set));
-            const unsigned long long init[4] = {0, 0, w->pool_used, 0};
-            JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL(k_ow_sassign, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, w->snk.as<unsigned long long>(),
-                               w->snv.as<uint32_t>(), nnew, w->n_names, names_of(w), w->sid_id.as<uint32_t>(), st);
-            JG_HIP(hipGetLastError());
-            hipLaunchKernelGGL(k_ow_next_ids, dim3(blocks_for(nnew)), dim3(kBlock), 0, ctx->stream, w->snk.as<unsigned long long>(), nnew,
-                               names_of(w));
-            JG_HIP(hipGetLastError());
-            unsigned long long hh[4];
-            read_words(ctx, st, hh, 4);
-            JG_REQUIRE(hh[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
-            w->n_names += nnew;
-            w->pool_used = hh[2];
-            w->g1 = w->n_names;
-            w->p1 = w->pool_used;
-        }
+    StrTab ST = str_tab(w);
+    RecTab RT = rec_tab(w);
+    // the wave's strings (the table's list; those first named past the limit are skipped)
+    // the sub-lists packed into one list each (offsets from the counts: one read, one pack launch per table)
+    const std::vector<unsigned long long>& lc = w->lc;  // read by the check with the first bad message
+    unsigned long long offs[2][kLists + 1];
+    for (int t = 0; t < 2; ++t) {
+        offs[t][0] = 0;
+        for (uint32_t j = 0; j < kLists; ++j) offs[t][j + 1] = offs[t][j] + lc[(1 + t * kLists + j) * kCountStride];
     }
-    // live records, per side
-    ensure(w->fidx, w->rt_cap * 4);
-    ensure(w->fslot, w->rt_cap * 4);
+    const uint64_t ns = offs[0][kLists], nrec = offs[1][kLists];
+    ensure(w->loffs, sizeof offs);
+    ensure(w->st_packed, ns * 4 + 4);
+    ensure(w->rt_packed, nrec * 4 + 4);
+    JG_HIP(hipMemcpyAsync(w->loffs.p, offs, sizeof offs, hipMemcpyHostToDevice, ctx->stream));
+    const auto* doffs = w->loffs.as<unsigned long long>();
+    if (ns)
+        hipLaunchKernelGGL(k_list_pack, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, ST.list, ST.sub_cap, doffs, w->st_packed.as<uint32_t>());
+    if (nrec)
+        hipLaunchKernelGGL(k_list_pack, dim3(blocks_for(nrec)), dim3(kBlock), 0, ctx->stream, RT.list, RT.sub_cap, doffs + kLists + 1,
+                           w->rt_packed.as<uint32_t>());
+    JG_HIP(hipGetLastError());
+    ST.list = w->st_packed.as<uint32_t>();  // the commit kernels read the packed lists
+    RT.list = w->rt_packed.as<uint32_t>();
+    // strings: each looked up (new ones keyed by (set, first entry), known ones kNone), all sorted by that key
+    // (known last), new ids assigned in that order; no host round trip until the record counts are read
+    const unsigned long long init[4] = {0, 0, w->pool_used, 0};
+    JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+    if (ns) {
+        ensure_names(ctx, w, ns, w->wnb);  // room for every listed string (an upper bound of the new ones)
+        ensure(w->newk, ns * 8);
+        ensure(w->snk, ns * 8);
+        ensure(w->snv, ns * 4);
+        hipLaunchKernelGGL(k_ow_sresolve, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, ns, csi_lim, names_of(w),
+                           w->sid_id.as<uint32_t>(), w->newk.as<unsigned long long>());
+        JG_HIP(hipGetLastError());
+        sort_pairs(ctx, w, w->newk.as<unsigned long long>(), w->snk.as<unsigned long long>(), ST.list, w->snv.as<uint32_t>(), ns, 64);
+        hipLaunchKernelGGL(k_ow_sassign, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, w->snk.as<unsigned long long>(),
+                           w->snv.as<uint32_t>(), ns, w->n_names, names_of(w), w->sid_id.as<uint32_t>(), st);
+        JG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_ow_snext_ids, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, w->snk.as<unsigned long long>(), ns, names_of(w));
+        JG_HIP(hipGetLastError());
+    }
+    // the wave's records (the table's list), per side, first occurring before the limit
+    ensure(w->fidx, nrec * 4 + 4);
+    ensure(w->fslot, nrec * 4 + 4);
     JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
-    select_marked(ctx, w, RecLive{RT.word, RT.mint, S.trk, t_lim, 0}, w->rt_cap, w->fidx.as<uint32_t>(), st + 4);
-    select_marked(ctx, w, RecLive{RT.word, RT.mint, S.trk, t_lim, 1}, w->rt_cap, w->fslot.as<uint32_t>(), st + 5);
-    unsigned long long cnt[2];
-    read_words(ctx, st + 4, cnt, 2);
+    if (nrec) {
+        select_marked(ctx, w, RecLive{RT.list, RT.word, RT.mint, S.trk, t_lim, 0}, nrec, w->fidx.as<uint32_t>(), st + 4);
+        select_marked(ctx, w, RecLive{RT.list, RT.word, RT.mint, S.trk, t_lim, 1}, nrec, w->fslot.as<uint32_t>(), st + 5);
+    }
+    unsigned long long hh[6];  // [1] new strings, [2] pool bytes used, [3] id overflow, [4] [5] records per side
+    read_words(ctx, st, hh, 6);
+    JG_REQUIRE(hh[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
+    w->n_names += hh[1];
+    w->pool_used = hh[2];
+    w->g1 = w->n_names;
+    w->p1 = w->pool_used;
+    const unsigned long long cnt[2] = {hh[4], hh[5]};
     if (cnt[0] + cnt[1] == 0) return;
     for (int sd = 0; sd < 2; ++sd) {
         ensure(w->dk[sd], cnt[sd] * 8 + 8);
