@@ -268,6 +268,8 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
     all-gather, grouped ncclSend/ncclRecv of the runs over xGMI, merge of what it owns from device memory.
     At world 1 the runs stay on the device (route + copy + merge)."""
     import numpy as np
+    if world > 1 and os.environ.get("JANUS_BENCH_BACKEND", "nccl") != "nccl":
+        return bench_exchange_staged(jg, ctx, sync, rank, world, local, steps, warmup)
     uid = sync.broadcast_bytes(jg.comm_unique_id() if rank == 0 else b"")
     comm = jg.Comm(ctx, rank, world, uid)
     store = jg.PNCStore(ctx, EXCH_KEYS, PNC_R, PNC_EB)
@@ -308,6 +310,32 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
                       "roofline": {"bound": "hbm", "achieved": merge_alg / merge_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                    "frac": merge_alg / merge_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": merge_alg}},
             "collective": f"library RCCL communicator (jg_comm), world {world}: ncclAllGather of the counts + grouped ncclSend/ncclRecv"}
+
+
+def bench_exchange_staged(jg, ctx, sync, rank, world, local, steps, warmup):
+    """The exchange rehearsed with several ranks on ONE device over gloo (JANUS_BENCH_BACKEND=gloo; RCCL cannot
+    put two ranks on one GPU): janus_gpu/shard.py's host-staged all-to-all around the same route / merge
+    kernels.  Correctness only — the time says nothing about xGMI."""
+    import numpy as np
+    import torch
+    from janus_gpu import shard
+    dev = torch.device("cuda", local)
+    ex = shard.Exchange(dev)
+    store = jg.PNCStore(ctx, EXCH_KEYS, PNC_R, PNC_EB)
+    rows = jg.Rows(ctx, EXCH_ROWS, PNC_R, PNC_EB)
+    try:
+        store.synth(SEED + 7 + rank)
+        keys = np.random.default_rng(SEED + rank).integers(0, world * EXCH_KEYS, EXCH_ROWS, dtype=np.uint32)
+        zeros = np.zeros((EXCH_ROWS, PNC_R), np.int64)
+        rows.upload(zeros, zeros, keys)
+        rows.synth(SEED + 11 + rank)
+        wall, _ = timed(ctx, sync, lambda: shard.exchange_pnc(store, rows, ex, dev), steps, warmup)
+    finally:
+        store.close()
+        rows.close()
+    return {"workload": f"cross-shard exchange rehearsal: {world} ranks on one device, host-staged gloo all-to-all",
+            "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
+            "collective": "torch.distributed all_to_all_single over gloo (rehearsal, not xGMI)"}
 
 
 JSON_MSGS, JSON_KEYS, JSON_R, JSON_EB, JSON_NODES = 1_000_000, 1_000_000, 5, 4, 4  # one C5 wave, device-resident
@@ -397,7 +425,7 @@ def apply_roofline(res):
     busy_s = res["device_busy_ms_per_wave"] / 1e3
     gather_s = res["gather_ms_per_wave"] / 1e3
     ach = up / wave_s / 1e9
-    return {"bound": "pcie", "achieved": ach, "peak": PCIE_PEAK_GBS, "unit": "GB/s", "frac": ach / PCIE_PEAK_GBS, "traffic": None,
+    out = {"bound": "pcie", "achieved": ach, "peak": PCIE_PEAK_GBS, "unit": "GB/s", "frac": ach / PCIE_PEAK_GBS, "traffic": None,
             "bytes_per_wave": up, "ideal_ms_per_wave": up / PCIE_PEAK_GBS / 1e6,
             "scope": "bytes the library uploads per wave (payloads + per-message arrays) / wave time",
             "device_share": {"bound": "hbm", "achieved": up / busy_s / 1e9 if busy_s else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -405,6 +433,12 @@ def apply_roofline(res):
                              "scope": "uploaded bytes / kernel time of the wave (hipEvents around each chunk's kernels and the final phase)"},
             "host_share": {"gather_ms_per_wave": gather_s * 1e3, "gather_GBps": up / gather_s / 1e9 if gather_s else None,
                            "scope": "the library's workers gathering payloads into page-locked staging (overlaps the uploads)"}}
+    chunk_s = res.get("chunk_busy_ms_per_wave", 0) / 1e3
+    if chunk_s:  # the per-chunk kernels: classify + the payload decode (k_scan / k_ow_group + the OR-Set tables)
+        out["decode"] = {"bound": "hbm", "achieved": up / chunk_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": up / chunk_s / 1e9 / HBM_PEAK_GBS, "busy_ms_per_wave": chunk_s * 1e3,
+                         "scope": "uploaded bytes / kernel time of the per-chunk classify + parse kernels (hipEvents, chunk_busy_s)"}
+    return out
 
 
 def bench_apply_loop(sync, rank, world, local):
@@ -684,7 +718,9 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
                          "traffic": _orset_traffic(),
-                         "scope": "whole step: adds + tombstones, each k_partition + k_union + k_finish"},
+                         "frac_24B": o["bytes_per_step"] * 24 / 28 / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
+                         "scope": "whole step: adds + tombstones, each k_partition + k_union + k_finish; 28-B records (key, tag, "
+                                  "arrival ordinal); frac_24B = the same time in SURVEY.md D3's 24-B unit (DESIGN.md section 5)"},
         }
         if "value" not in line:
             line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,

@@ -329,11 +329,13 @@ int jg_apply_committed(jg_node* node, jg_tracker* tracker, const jg_commit* wave
 int jg_apply_block(jg_node* node, const jg_commit* wave, uint64_t* stopped_at);
 /* Figures of the node's last apply call.  Host: seconds gathering payloads into staging, waiting for the
  * device after the last chunk was queued, the whole call.  Device: kernel time of the wave (hipEvents
- * around each chunk's kernels and around the final phase, on the context's stream).  Messages and
- * payload bytes uploaded, messages applied (registered CRDT states before the cut), chunks. */
+ * around each chunk's kernels and around the final phase, on the context's stream) = chunk_busy_s (the
+ * per-chunk classify + parse kernels: the payload decode) + tail_busy_s (after the last chunk).  Messages
+ * and payload bytes uploaded, messages applied (registered CRDT states before the cut), chunks. */
 typedef struct jg_apply_stats {
     double gather_s, device_wait_s, total_s, device_busy_s;
     uint64_t msgs_uploaded, bytes_uploaded, msgs_applied, chunks;
+    double chunk_busy_s, tail_busy_s;
 } jg_apply_stats;
 int jg_node_last_stats(jg_node* node, jg_apply_stats* out);
 

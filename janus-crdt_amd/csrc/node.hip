@@ -710,8 +710,10 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         float ms = 0;
         JG_HIP(hipEventElapsedTime(&ms, nd->ev[2 * k], nd->ev[2 * k + 1]));
         busy += ms * 1e-3;
+        if (k == n_ev) nd->stats.tail_busy_s = ms * 1e-3;  // the final phase's pair
     }
     nd->stats.device_busy_s = busy;
+    nd->stats.chunk_busy_s = busy - nd->stats.tail_busy_s;
     if (n_completed) *n_completed = ndone;
     *stopped_at = cut < nn ? (filter ? nd->dmap[cut] : cut) : UINT64_MAX;
     const double t_end = now_s();
