@@ -461,8 +461,8 @@ def bench_apply_loop(sync, rank, world, local):
         res = {"workload": res["workload"] + f", key-space sharded x{world}", "scaling": "strong",
                "msgs_per_s": res["state_msgs_per_wave"] / (worst_ms / 1e3), "client_ops_per_s": 1_000_000 / (worst_ms / 1e3),
                "ms_per_wave": worst_ms, "rank0_roofline": apply_roofline(res),
-               "rank0": {k: res[k] for k in ("ms_per_wave", "host_ms_per_wave", "engine_ms_per_wave", "owned_accounts",
-                                               "applied_msgs_per_wave")}}
+               "rank0": {k: res.get(k) for k in ("ms_per_wave", "host_ms_per_wave", "device_busy_ms_per_wave", "device_wait_ms_per_wave",
+                                                   "owned_accounts", "applied_msgs_per_wave")}}
     return res
 
 
@@ -668,12 +668,18 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
-    apply_loop = bench_apply_loop(sync, rank, world, local) if args.workload == "all" else None
-    apply_orset = bench_apply_orset(sync, rank, world, local) if args.workload == "all" else None
-    apply_c1 = bench_c1(local) if args.workload == "all" and world == 1 else None
+    def guarded(fn, *a):  # a leg's failure must not cost the headline line (each leg's collective runs on every
+        try:              # rank before anything in it can raise: sync.max takes inf for a failed run)
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001
+            return {"error": repr(e)[:500]}
+
+    apply_loop = guarded(bench_apply_loop, sync, rank, world, local) if args.workload == "all" else None
+    apply_orset = guarded(bench_apply_orset, sync, rank, world, local) if args.workload == "all" else None
+    apply_c1 = guarded(bench_c1, local) if args.workload == "all" and world == 1 else None
     for leg in (apply_loop, apply_orset, apply_c1):
         if leg is not None and "error" not in leg and "scaling" not in leg:
-            leg["roofline"] = apply_roofline(leg)
+            leg["roofline"] = guarded(apply_roofline, leg)
     sync.close()
     if rank != 0:
         return
