@@ -8,13 +8,14 @@
 // run of its records; Dictionary membership of elem = the run being non-empty.
 //
 // ORSet.Merge (ORSet.cs:253-283) over a keyspace of sets = per-stream sorted set UNION:
-//   k_partition : merge-path split of every tile boundary (one wave, 64-ary search, each).
+//   k_partition_gallop2 : merge-path split of every tile boundary of both streams in one launch (a
+//                 guess in proportion, galloped and binary-searched from there, one thread each).
 //   k_union     : one tile per workgroup.  Stage the tile's slices of A and B in LDS, merge (A first
 //                 on ties), drop a B record equal to the A record before it in merged order (the only
 //                 way a duplicate can appear, since each input is duplicate-free), compact through a
 //                 block scan, write the tile into ITS OWN output chunk.  No inter-workgroup traffic.
-//   k_finish    : the output's chunk offsets and rank -> chunk table (one small launch).
-//   Roofline: HBM.  Reads 24 B per input record, writes 24 B per output record.
+//   k_finish2   : both outputs' chunk offsets and rank -> chunk tables (one small launch).
+//   Roofline: HBM.  Reads 28 B per input record, writes 28 B per output record (key, tag, ord).
 // ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams
 // (rank space), then SetEquals of the two sorted runs.
 #include <hipcub/hipcub.hpp>
@@ -39,7 +40,6 @@ constexpr int kOB = 512;   // threads per workgroup
 constexpr int kItems = 6;  // records per thread per tile
 constexpr int kTile = kOB * kItems;
 static_assert(kTile == (int)kChunk, "a union tile fills exactly one stream chunk");
-constexpr int kPartLanes = 1;  // lanes per tile boundary in k_partition (tools/tune_orset.hip)
 
 using jgk::Tag;
 using jgk::ld_tag;
@@ -301,34 +301,56 @@ void ensure_ord_room(jg_ctx* ctx, jg_stream_soa& a, jg_stream_soa& b) {
                (unsigned long long)a.n, (unsigned long long)b.n);
 }
 
-// Union of two streams into `out` (chunk capacity ensured here).  Async on ctx->stream; the output
-// record count lands in *d_count (device) and out.n is left for sync_counts.  Ords: see k_union
-// (the caller ensured a.next + b.next fits, ensure_ord_room).
-void launch_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count, char* ws,
-                  jgk::Drop drop) {
-    const uint64_t total = a.n + b.n;
-    out.reserve_records(total);
+// One stream's union into `out` (chunk capacity ensured here), launched in three steps shared with the
+// store's other stream: boundaries (k_partition_gallop2, both streams), the tiles (k_union, per stream),
+// offsets + rank table (k_finish2, both streams).  Async on ctx->stream; the output record count lands
+// in *d_count (device) and out.n is left for sync_counts.  Ords: see k_union (the caller ensured
+// a.next + b.next fits, ensure_ord_room).
+struct UnionLaunch {
+    View va{}, vb{};
+    jg_stream_soa* out = nullptr;
+    uint64_t total = 0, n_tiles = 0;
+    uint64_t* part = nullptr;
+    uint32_t* pchunk = nullptr;
+    unsigned long long* d_count = nullptr;
+    uint32_t b_base = 0;
+    jgk::PartJob part_job() const { return jgk::PartJob{va, vb, n_tiles ? n_tiles + 1 : 0, part, pchunk}; }
+    jgk::FinishJob finish_job() const {
+        return jgk::FinishJob{out->cnt.as<uint32_t>(), (uint32_t)n_tiles, out->off.as<uint64_t>(), out->lut.as<uint32_t>(),
+                              (total >> jgk::kQShift) + 2, d_count};
+    }
+};
+
+UnionLaunch prepare_union(jg_ctx* ctx, const jg_stream_soa& a, const jg_stream_soa& b, jg_stream_soa& out, unsigned long long* d_count,
+                          char* ws) {
+    UnionLaunch u;
+    u.total = a.n + b.n;
+    out.reserve_records(u.total);
     out.next = a.next + b.next;
-    if (total == 0) {
+    u.out = &out;
+    u.d_count = d_count;
+    u.b_base = (uint32_t)a.next;
+    if (u.total == 0) {
         jg::set_dense(ctx, out, 0);
         JG_HIP(hipMemsetAsync(d_count, 0, sizeof(unsigned long long), ctx->stream));
-        return;
+        return u;
     }
-    const uint64_t n_tiles = tiles_for(total);
-    JG_REQUIRE(n_tiles < 0xFFFFFFFFull, JG_EINVAL, "union: %llu records exceed the chunk index range", (unsigned long long)total);
-    auto* part = reinterpret_cast<uint64_t*>(ws);
-    auto* pchunk = reinterpret_cast<uint32_t*>(ws + (((n_tiles + 1) * 8 + 255) & ~(size_t)255));
-    const View va = view(a), vb = view(b);
-    hipLaunchKernelGGL((jgk::k_partition<kTile, kPartLanes>), dim3((unsigned)(((n_tiles + 1) * kPartLanes + 255) / 256)), dim3(256), 0,
-                       ctx->stream, va, vb, n_tiles + 1, part, pchunk);
+    u.n_tiles = tiles_for(u.total);
+    JG_REQUIRE(u.n_tiles < 0xFFFFFFFFull, JG_EINVAL, "union: %llu records exceed the chunk index range", (unsigned long long)u.total);
+    u.part = reinterpret_cast<uint64_t*>(ws);
+    u.pchunk = reinterpret_cast<uint32_t*>(ws + (((u.n_tiles + 1) * 8 + 255) & ~(size_t)255));
+    u.va = view(a);
+    u.vb = view(b);
+    return u;
+}
+
+void launch_tiles(jg_ctx* ctx, UnionLaunch& u, jgk::Drop drop) {
+    if (u.n_tiles == 0) return;
+    jg_stream_soa& out = *u.out;
+    hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)u.n_tiles), dim3(kOB), 0, ctx->stream, u.va, u.vb, u.part, u.pchunk,
+                       out.key.as<unsigned long long>(), out.tag.as<uint4>(), out.ord.as<uint32_t>(), u.b_base, out.cnt.as<uint32_t>(), drop);
     JG_HIP(hipGetLastError());
-    hipLaunchKernelGGL((jgk::k_union<kOB, kItems>), dim3((unsigned)n_tiles), dim3(kOB), 0, ctx->stream, va, vb, part, pchunk,
-                       out.key.as<unsigned long long>(), out.tag.as<uint4>(), out.ord.as<uint32_t>(), (uint32_t)a.next, out.cnt.as<uint32_t>(), drop);
-    JG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(jgk::k_finish, dim3((unsigned)((n_tiles + 1023) / 1024)), dim3(1024), 0, ctx->stream, out.cnt.as<uint32_t>(),
-                       (uint32_t)n_tiles, out.off.as<uint64_t>(), out.lut.as<uint32_t>(), (total >> jgk::kQShift) + 2, d_count);
-    JG_HIP(hipGetLastError());
-    out.nch = (uint32_t)n_tiles;
+    out.nch = (uint32_t)u.n_tiles;
     out.dense = false;
 }
 
@@ -341,8 +363,27 @@ void union_store(jg_ctx* ctx, jg_orset* a, jg_orset* b, jg_stream_soa& oa, jg_st
     unsigned long long* d = counted->counts.as<unsigned long long>();
     const size_t ws_add = union_ws_bytes(a->add.n + b->add.n);
     char* ws = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, ws_add + union_ws_bytes(a->rem.n + b->rem.n)));
-    launch_union(ctx, a->add, b->add, oa, d, ws, drop);
-    launch_union(ctx, a->rem, b->rem, orr, d + 1, ws + ws_add, drop);
+    UnionLaunch ua = prepare_union(ctx, a->add, b->add, oa, d, ws);
+    UnionLaunch ur = prepare_union(ctx, a->rem, b->rem, orr, d + 1, ws + ws_add);
+    const jgk::PartJob pa = ua.part_job(), pr = ur.part_job();
+    const uint64_t parts = pa.n_parts + pr.n_parts;
+    if (parts) {
+        hipLaunchKernelGGL((jgk::k_partition_gallop2<kTile>), dim3((unsigned)((parts + 255) / 256)), dim3(256), 0, ctx->stream, pa, pr);
+        JG_HIP(hipGetLastError());
+    }
+    launch_tiles(ctx, ua, drop);
+    launch_tiles(ctx, ur, drop);
+    if (ua.n_tiles && ur.n_tiles) {
+        hipLaunchKernelGGL(jgk::k_finish2, dim3(jgk::finish_blocks((uint32_t)ua.n_tiles) + jgk::finish_blocks((uint32_t)ur.n_tiles)), dim3(1024), 0,
+                           ctx->stream, ua.finish_job(), ur.finish_job());
+    } else {
+        for (UnionLaunch* u : {&ua, &ur})
+            if (u->n_tiles)
+                hipLaunchKernelGGL(jgk::k_finish, dim3(jgk::finish_blocks((uint32_t)u->n_tiles)), dim3(1024), 0, ctx->stream,
+                                   u->out->cnt.as<uint32_t>(), (uint32_t)u->n_tiles, u->out->off.as<uint64_t>(), u->out->lut.as<uint32_t>(),
+                                   (u->total >> jgk::kQShift) + 2, u->d_count);
+    }
+    JG_HIP(hipGetLastError());
     counted->counts_pending = true;
 }
 

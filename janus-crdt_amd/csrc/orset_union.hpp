@@ -138,89 +138,110 @@ __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_pa
     }
 }
 
-// One tile: A ranks [i0, i1), B ranks [j0, j1) -> chunk `tile` of the output (capacity kOB*kItems).
-// Ordinals: an A record keeps its ord, a B record takes b_base + its ord (b_base = A's next: a tag new
-// to A's HashSet is appended after every tag A holds, in B's order — UnionWith / the copy constructor,
-// ORSet.cs:255-282).  A B record equal to an A record is dropped, so the A record's ord stays.
+// Merge-path predicate at split candidate m of diagonal d: A[m] <= B[d-1-m] (A first on ties).
+__device__ __forceinline__ bool mp_le(const View& a, const View& b, uint64_t d, uint64_t m) {
+    const uint64_t sa = slot_of(a, m), sb = slot_of(b, d - 1 - m);
+    const unsigned long long ka = a.key[sa], kb = b.key[sb];
+    return !(ka != kb ? kb < ka : rec_lt(kb, ld_tag(b.tag + sb), ka, ld_tag(a.tag + sa)));
+}
+
+// k_partition from a guess: the split of diagonal d is first guessed in proportion (d * |A| / total),
+// then bracketed by probes at distances 1, 2, 4, ... <= kGallop from the guess, then binary-searched
+// inside the bracket (or inside what is left of the range when the gallop did not close it, with
+// k_partition's 512-aligned wide probes).  Exact for any input; streams that interleave evenly need
+// about 2 log2(|split - guess|) dependent probes instead of log2(min(|A|, |B|)).
+template <int C>
+__device__ __forceinline__ void gallop_split(const View& a, const View& b, uint64_t w, uint64_t* __restrict__ part, uint32_t* __restrict__ pchunk) {
+    constexpr uint64_t kGallop = 1024;
+    const uint64_t total = a.n + b.n;
+    const uint64_t d = w * C < total ? w * C : total;
+    uint64_t lo = d > b.n ? d - b.n : 0, hi = d < a.n ? d : a.n;  // the split lies in [lo, hi]
+    if (lo < hi) {
+        uint64_t g = (uint64_t)((double)d * (double)a.n / (double)total);
+        g = g < lo ? lo : g >= hi ? hi - 1 : g;
+        if (mp_le(a, b, d, g)) {  // split > g
+            lo = g + 1;
+            for (uint64_t step = 1; step <= kGallop; step <<= 1) {
+                const uint64_t m = g + step;
+                if (m >= hi) break;
+                if (mp_le(a, b, d, m)) lo = m + 1;
+                else { hi = m; break; }
+            }
+        } else {  // split <= g
+            hi = g;
+            for (uint64_t step = 1; step <= kGallop && step <= g - lo; step <<= 1) {
+                const uint64_t m = g - step;
+                if (mp_le(a, b, d, m)) { lo = m + 1; break; }
+                hi = m;
+            }
+        }
+        while (lo < hi) {
+            const uint64_t W = hi - lo;
+            uint64_t m = lo + W / 2;
+            if (W > 1024) m &= ~511ull;  // wide leftovers: k_partition's shared 512-aligned probes
+            if (mp_le(a, b, d, m)) lo = m + 1;
+            else hi = m;
+        }
+    }
+    part[w] = lo;
+    const uint64_t j = d - lo;
+    pchunk[2 * w] = lo < a.n ? chunk_of(a, lo) : a.nch;
+    pchunk[2 * w + 1] = j < b.n ? chunk_of(b, j) : b.nch;
+}
+
+// One union's tile boundaries: n_parts = tiles + 1 (none for an empty union).
+struct PartJob {
+    View a, b;
+    uint64_t n_parts;
+    uint64_t* part;
+    uint32_t* pchunk;
+};
+
+template <int C>
+__global__ __launch_bounds__(256) void k_partition_gallop(View a, View b, uint64_t n_parts, uint64_t* __restrict__ part,
+                                                          uint32_t* __restrict__ pchunk) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w < n_parts) gallop_split<C>(a, b, w, part, pchunk);
+}
+
+// Both streams' boundaries (adds, tombstones) in one launch: the two searches are latency-bound and
+// overlap instead of running back to back.
+template <int C>
+__global__ __launch_bounds__(256) void k_partition_gallop2(PartJob j0, PartJob j1) {
+    const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (w < j0.n_parts) gallop_split<C>(j0.a, j0.b, w, j0.part, j0.pchunk);
+    else if (w - j0.n_parts < j1.n_parts) gallop_split<C>(j1.a, j1.b, w - j0.n_parts, j1.part, j1.pchunk);
+}
+
+// LDS of one union tile.
 template <int kOB, int kItems>
-__global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* __restrict__ part, const uint32_t* __restrict__ pchunk,
-                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ oord,
-                                               uint32_t b_base, uint32_t* __restrict__ ocnt, Drop drop) {
+struct UnionShared {
+    static constexpr int kTile = kOB * kItems;
+    static constexpr int kSeg = 64;  // chunks a tile's A (or B) range may span before the slow path
+    unsigned long long key[kTile];
+    uint4 tag[kTile];
+    uint64_t off[2][kSeg + 1];  // chunk boundaries around the A (0) and B (1) ranges
+    unsigned long long prev_key;
+    uint4 prev_tag;
+    int has_prev;
+    int wsum[kOB / 64];
+};
+
+// Merge, compaction and stores of one tile whose records are staged in LDS (A ranks [0, nA), B ranks
+// [nA, n)), with their ordinals in registers (staging index it * kOB + tid) and the A record before the
+// tile in sh.prev_*.  Ordinals: an A record keeps its ord, a B record arrives with b_base added (b_base
+// = A's next: a tag new to A's HashSet is appended after every tag A holds, in B's order — UnionWith /
+// the copy constructor, ORSet.cs:255-282).  A B record equal to an A record is dropped, so the A
+// record's ord stays.  Ends with every LDS read done (the caller may restage after a barrier).
+template <int kOB, int kItems>
+__device__ __forceinline__ void union_tile(UnionShared<kOB, kItems>& sh, int nA, int nB, uint64_t tile, const uint32_t (&rord)[kItems],
+                                           unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ oord,
+                                           uint32_t* __restrict__ ocnt, const Drop& drop) {
     constexpr int kTile = kOB * kItems;
-    constexpr int kSeg = 64;  // chunks a tile's A (or B) range may span before the slow path
-    __shared__ unsigned long long s_key[kTile];
-    __shared__ uint4 s_tag[kTile];
-    __shared__ uint64_t s_off[2][kSeg + 1];  // chunk boundaries around the A (0) and B (1) ranges
-    __shared__ unsigned long long s_prev_key;
-    __shared__ uint4 s_prev_tag;
-    __shared__ int s_has_prev;
-    __shared__ int s_wsum[kOB / 64];
-
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t tile = blockIdx.x;
-    const uint64_t total_in = a.n + b.n;
-    const uint64_t d0 = tile * kTile;
-    const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
-    const uint64_t i0 = part[tile], i1 = part[tile + 1];
-    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
-    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0), n = nA + nB;
-    const uint32_t ca = pchunk[2 * tile], cb = pchunk[2 * tile + 1];
-
-    // ---- chunk boundaries around the tile's A and B ranges (waves 0 and 1) ----
-    if (wid == 0) {
-        const uint32_t c = ca + lane;
-        s_off[0][lane] = c <= a.nch ? a.off[c] : a.n;
-        if (lane == 0) s_off[0][kSeg] = ca + kSeg <= a.nch ? a.off[ca + kSeg] : a.n;
-    } else if (wid == 1) {
-        const uint32_t c = cb + lane;
-        s_off[1][lane] = c <= b.nch ? b.off[c] : b.n;
-        if (lane == 0) s_off[1][kSeg] = cb + kSeg <= b.nch ? b.off[cb + kSeg] : b.n;
-    }
-    __syncthreads();
-
-    // ---- stage the tile in LDS; every load issued before the first LDS write ----
-    // The ordinals stay in registers (staging index x = it * kOB + tid): keys + tags fill the LDS of two
-    // workgroups per CU, so ords only pass through LDS after the merge (below).
-    uint32_t rord[kItems];
-    {
-        unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {
-            const int x = min(it * kOB + tid, n - 1);  // clamped: unconditional loads (n >= 1)
-            const bool from_a = x < nA;
-            const uint64_t r = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
-            const int side = from_a ? 0 : 1;
-            int s = 0;
-            while (s < kSeg && s_off[side][s + 1] <= r) ++s;
-            uint64_t slot;
-            if (s < kSeg) slot = (uint64_t)((from_a ? ca : cb) + s) * (uint64_t)(from_a ? a.C : b.C) + (r - s_off[side][s]);
-            else slot = slot_of(from_a ? a : b, r);  // > 64 tiny chunks under one tile (drop-filtered input)
-            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + slot);  // each record is read once
-            const Tag t = ld_tag_nt((from_a ? a.tag : b.tag) + slot);
-            rlo[it] = t.lo;
-            rhi[it] = t.hi;
-            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + slot) + (from_a ? 0u : b_base);
-        }
-        unsigned long long pk = 0;
-        Tag pt{0, 0};
-        if (tid == 0 && i0 > 0) {  // the A record before the tile (duplicate check at the seam)
-            const uint64_t ps = slot_of(a, i0 - 1);
-            pk = a.key[ps];
-            pt = ld_tag(a.tag + ps);
-        }
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
-            const int x = it * kOB + tid;
-            s_key[x] = rk[it];
-            s_tag[x] = to_u4(Tag{rlo[it], rhi[it]});
-        }
-        if (tid == 0) {
-            s_has_prev = i0 > 0 && !dropped(drop, pk);
-            s_prev_key = pk;
-            s_prev_tag = to_u4(pt);
-        }
-    }
-    __syncthreads();
+    const int n = nA + nB;
+    unsigned long long* s_key = sh.key;
+    uint4* s_tag = sh.tag;
 
     // ---- per-thread merge path + serial merge of kItems outputs ----
     // The search compares keys and reads the two 16-B tags from LDS only when the keys tie (LDS
@@ -247,7 +268,7 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     unsigned long long pk;
     Tag pt;
     if (ai > 0) { pk = s_key[ai - 1]; pt = __builtin_bit_cast(Tag, s_tag[ai - 1]); hp = !dropped(drop, pk); }
-    else { hp = s_has_prev != 0; pk = s_prev_key; pt = __builtin_bit_cast(Tag, s_prev_tag); }
+    else { hp = sh.has_prev != 0; pk = sh.prev_key; pt = __builtin_bit_cast(Tag, sh.prev_tag); }
 
     const int my_n = n - diag < kItems ? n - diag : kItems;
     unsigned long long ka = 0, kb = 0;
@@ -288,12 +309,12 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
         const int y = __shfl_up(incl, dd, 64);
         if (lane >= dd) incl += y;
     }
-    if (lane == 63) s_wsum[wid] = incl;
+    if (lane == 63) sh.wsum[wid] = incl;
     __syncthreads();
     int wbase = 0, block_total = 0;
 #pragma unroll
     for (int w = 0; w < kOB / 64; ++w) {
-        const int v = s_wsum[w];
+        const int v = sh.wsum[w];
         if (w < wid) wbase += v;
         block_total += v;
     }
@@ -331,19 +352,200 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     if (tid == 0) ocnt[tile] = (uint32_t)block_total;
 }
 
+// One tile: A ranks [i0, i1), B ranks [j0, j1) -> chunk `tile` of the output (capacity kOB*kItems).
+template <int kOB, int kItems>
+__global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* __restrict__ part, const uint32_t* __restrict__ pchunk,
+                                               unsigned long long* __restrict__ ok, uint4* __restrict__ ot, uint32_t* __restrict__ oord,
+                                               uint32_t b_base, uint32_t* __restrict__ ocnt, Drop drop) {
+    using SH = UnionShared<kOB, kItems>;
+    constexpr int kTile = SH::kTile, kSeg = SH::kSeg;
+    __shared__ SH sh;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t tile = blockIdx.x;
+    const uint64_t total_in = a.n + b.n;
+    const uint64_t d0 = tile * kTile;
+    const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
+    const uint64_t i0 = part[tile], i1 = part[tile + 1];
+    const uint64_t j0 = d0 - i0, j1 = d1 - i1;
+    const int nA = (int)(i1 - i0), nB = (int)(j1 - j0), n = nA + nB;
+    const uint32_t ca = pchunk[2 * tile], cb = pchunk[2 * tile + 1];
+
+    // ---- chunk boundaries around the tile's A and B ranges (waves 0 and 1) ----
+    if (wid == 0) {
+        const uint32_t c = ca + lane;
+        sh.off[0][lane] = c <= a.nch ? a.off[c] : a.n;
+        if (lane == 0) sh.off[0][kSeg] = ca + kSeg <= a.nch ? a.off[ca + kSeg] : a.n;
+    } else if (wid == 1) {
+        const uint32_t c = cb + lane;
+        sh.off[1][lane] = c <= b.nch ? b.off[c] : b.n;
+        if (lane == 0) sh.off[1][kSeg] = cb + kSeg <= b.nch ? b.off[cb + kSeg] : b.n;
+    }
+    __syncthreads();
+
+    // ---- stage the tile in LDS; every load issued before the first LDS write ----
+    // The ordinals stay in registers (staging index x = it * kOB + tid): keys + tags fill the LDS of two
+    // workgroups per CU, so ords only pass through LDS after the merge (union_tile).
+    uint32_t rord[kItems];
+    {
+        unsigned long long rk[kItems], rlo[kItems], rhi[kItems];  // scalar arrays: stay in VGPRs
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {
+            const int x = min(it * kOB + tid, n - 1);  // clamped: unconditional loads (n >= 1)
+            const bool from_a = x < nA;
+            const uint64_t r = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
+            const int side = from_a ? 0 : 1;
+            int s = 0;
+            while (s < kSeg && sh.off[side][s + 1] <= r) ++s;
+            uint64_t slot;
+            if (s < kSeg) slot = (uint64_t)((from_a ? ca : cb) + s) * (uint64_t)(from_a ? a.C : b.C) + (r - sh.off[side][s]);
+            else slot = slot_of(from_a ? a : b, r);  // > 64 tiny chunks under one tile (drop-filtered input)
+            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + slot);  // each record is read once
+            const Tag t = ld_tag_nt((from_a ? a.tag : b.tag) + slot);
+            rlo[it] = t.lo;
+            rhi[it] = t.hi;
+            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + slot) + (from_a ? 0u : b_base);
+        }
+        unsigned long long pk = 0;
+        Tag pt{0, 0};
+        if (tid == 0 && i0 > 0) {  // the A record before the tile (duplicate check at the seam)
+            const uint64_t ps = slot_of(a, i0 - 1);
+            pk = a.key[ps];
+            pt = ld_tag(a.tag + ps);
+        }
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {  // slots >= n get a duplicate; never read
+            const int x = it * kOB + tid;
+            sh.key[x] = rk[it];
+            sh.tag[x] = to_u4(Tag{rlo[it], rhi[it]});
+        }
+        if (tid == 0) {
+            sh.has_prev = i0 > 0 && !dropped(drop, pk);
+            sh.prev_key = pk;
+            sh.prev_tag = to_u4(pt);
+        }
+    }
+    __syncthreads();
+    union_tile<kOB, kItems>(sh, nA, nB, tile, rord, ok, ot, oord, ocnt, drop);
+}
+
+// Persistent variant for DENSE inputs (slot = rank): workgroup g walks tiles g, g + G, g + 2G, ... and
+// issues the loads of its next tile's records into registers right after staging the current tile in
+// LDS, so they are in flight while the current tile merges, compacts and stores (the one-tile kernel
+// has no load in flight during those phases; two workgroups per CU fit the LDS).  Tile bounds come one
+// iteration ahead of the loads that need them.
+template <int kOB, int kItems>
+__global__ __launch_bounds__(kOB) void k_union_pf(View a, View b, const uint64_t* __restrict__ part, unsigned long long* __restrict__ ok,
+                                                  uint4* __restrict__ ot, uint32_t* __restrict__ oord, uint32_t b_base,
+                                                  uint32_t* __restrict__ ocnt, Drop drop, uint64_t n_tiles) {
+    using SH = UnionShared<kOB, kItems>;
+    constexpr int kTile = SH::kTile;
+    __shared__ SH sh;
+    const int tid = threadIdx.x;
+    const uint64_t total_in = a.n + b.n;
+    const uint64_t G = gridDim.x;
+    uint64_t tile = blockIdx.x;
+    if (tile >= n_tiles) return;
+
+    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
+    uint32_t rord[kItems];
+    unsigned long long pk = 0;
+    Tag pt{0, 0};
+    // loads of tile t's records (and, on thread 0, the A record before it)
+    auto issue = [&](uint64_t t, uint64_t i0, uint64_t i1) {
+        const uint64_t d0 = t * kTile;
+        const uint64_t j0 = d0 - i0;
+        const int nA = (int)(i1 - i0);
+        const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
+        const int n = (int)(d1 - d0);
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {
+            const int x = min(it * kOB + tid, n - 1);
+            const bool from_a = x < nA;
+            const uint64_t r = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
+            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + r);
+            const Tag tg = ld_tag_nt((from_a ? a.tag : b.tag) + r);
+            rlo[it] = tg.lo;
+            rhi[it] = tg.hi;
+            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + r) + (from_a ? 0u : b_base);
+        }
+        if (tid == 0 && i0 > 0) {
+            pk = a.key[i0 - 1];
+            pt = ld_tag(a.tag + i0 - 1);
+        }
+    };
+    uint64_t i0 = part[tile], i1 = part[tile + 1];
+    issue(tile, i0, i1);
+    uint64_t nt = tile + G;
+    uint64_t n0 = nt < n_tiles ? part[nt] : 0, n1 = nt < n_tiles ? part[nt + 1] : 0;
+    for (;;) {
+        const uint64_t d0 = tile * kTile;
+        const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
+        const int nA = (int)(i1 - i0), n = (int)(d1 - d0);
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) {
+            const int x = it * kOB + tid;
+            sh.key[x] = rk[it];
+            sh.tag[x] = to_u4(Tag{rlo[it], rhi[it]});
+        }
+        if (tid == 0) {
+            sh.has_prev = i0 > 0 && !dropped(drop, pk);
+            sh.prev_key = pk;
+            sh.prev_tag = to_u4(pt);
+        }
+        uint32_t cord[kItems];
+#pragma unroll
+        for (int it = 0; it < kItems; ++it) cord[it] = rord[it];
+        __syncthreads();
+        const uint64_t cur = tile;
+        const bool more = nt < n_tiles;
+        if (more) {
+            issue(nt, n0, n1);  // in flight during this tile's merge and stores
+            i0 = n0;
+            i1 = n1;
+            const uint64_t nn = nt + G;
+            n0 = nn < n_tiles ? part[nn] : 0;
+            n1 = nn < n_tiles ? part[nn + 1] : 0;
+        }
+        union_tile<kOB, kItems>(sh, nA, n - nA, cur, cord, ok, ot, oord, ocnt, drop);
+        if (!more) break;
+        tile = nt;
+        nt += G;
+        __syncthreads();  // every store of this tile read its LDS before the next staging
+    }
+}
+
 // After a union: off = exclusive scan of the tiles' counts (off[nch] = *total = the record count)
-// and the rank -> chunk table, in one launch of ceil(nch / 1024) workgroups.  Each workgroup sums
-// the counts before its 1024 chunks itself (coalesced, L2-resident), so no workgroup waits on
-// another.  lut[q] = the chunk holding rank q*512; entries past the last record name the last chunk
-// (nlut = (n_bound >> kQShift) + 2 for a bound n_bound >= n).
-__global__ __launch_bounds__(1024) void k_finish(const uint32_t* __restrict__ cnt, uint32_t nch, uint64_t* __restrict__ off,
-                                                 uint32_t* __restrict__ lut, uint64_t nlut, unsigned long long* __restrict__ total) {
+// and the rank -> chunk table, in ceil(nch / 1024) workgroups.  Each workgroup sums the counts before
+// its 1024 chunks itself (coalesced 16-B loads, 16 in flight per thread: a one-count-per-iteration
+// loop was a chain of up to 64 dependent L2 round trips, 26 us per C3 add union), so no workgroup
+// waits on another.  lut[q] = the chunk holding rank q*512; entries past the last record name the
+// last chunk (nlut = (n_bound >> kQShift) + 2 for a bound n_bound >= n).
+struct FinishJob {
+    const uint32_t* cnt;  // 16-B aligned
+    uint32_t nch;
+    uint64_t* off;
+    uint32_t* lut;
+    uint64_t nlut;
+    unsigned long long* total;
+};
+__host__ __device__ inline unsigned finish_blocks(uint32_t nch) { return (nch + 1023) / 1024; }
+
+__device__ __forceinline__ void finish_block(const FinishJob& j, uint32_t blk, uint32_t nblk) {
     __shared__ uint64_t s_w[16];
     __shared__ uint64_t s_base, s_n;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t c0 = blockIdx.x * 1024u;
+    const uint32_t c0 = blk * 1024u;  // a multiple of 4
     uint64_t pre = 0;
-    for (uint32_t i = tid; i < c0; i += 1024) pre += cnt[i];
+    {
+        const uint4* c4 = reinterpret_cast<const uint4*>(j.cnt);
+        const uint32_t n4 = c0 / 4;
+#pragma unroll 16
+        for (uint32_t i = tid; i < n4; i += 1024) {
+            const uint4 v = c4[i];
+            pre += (uint64_t)v.x + v.y + v.z + v.w;
+        }
+    }
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) pre += __shfl_xor(pre, dd, 64);
     if (lane == 0) s_w[wid] = pre;
@@ -354,8 +556,9 @@ __global__ __launch_bounds__(1024) void k_finish(const uint32_t* __restrict__ cn
         s_base = t;
     }
     __syncthreads();
+    const uint32_t nch = j.nch;
     const uint32_t c = c0 + tid;
-    const uint64_t v = c < nch ? cnt[c] : 0;
+    const uint64_t v = c < nch ? j.cnt[c] : 0;
     uint64_t incl = v;
 #pragma unroll
     for (int dd = 1; dd < 64; dd <<= 1) {
@@ -368,21 +571,33 @@ __global__ __launch_bounds__(1024) void k_finish(const uint32_t* __restrict__ cn
     for (int w = 0; w < wid; ++w) wb += s_w[w];
     const uint64_t o = wb + incl - v;
     if (c < nch) {
-        off[c] = o;
+        j.off[c] = o;
         constexpr uint64_t Q = 1ull << kQShift;
-        for (uint64_t q = (o + Q - 1) >> kQShift; (q << kQShift) < o + v; ++q) lut[q] = c;
+        for (uint64_t q = (o + Q - 1) >> kQShift; (q << kQShift) < o + v; ++q) j.lut[q] = c;
     }
     if (c + 1 == nch) {  // the last chunk's thread: totals
-        off[nch] = o + v;
-        *total = o + v;
+        j.off[nch] = o + v;
+        *j.total = o + v;
     }
-    if (blockIdx.x == gridDim.x - 1) {  // tail of the table: ranks at or past the end
+    if (blk == nblk - 1) {  // tail of the table: ranks at or past the end
         __syncthreads();
         if (c + 1 == nch) s_n = o + v;
         __syncthreads();
         const uint64_t n = s_n;
-        for (uint64_t q = ((n + (1ull << kQShift) - 1) >> kQShift) + tid; q < nlut; q += 1024) lut[q] = nch - 1;
+        for (uint64_t q = ((n + (1ull << kQShift) - 1) >> kQShift) + tid; q < j.nlut; q += 1024) j.lut[q] = nch - 1;
     }
+}
+
+__global__ __launch_bounds__(1024) void k_finish(const uint32_t* __restrict__ cnt, uint32_t nch, uint64_t* __restrict__ off,
+                                                 uint32_t* __restrict__ lut, uint64_t nlut, unsigned long long* __restrict__ total) {
+    finish_block(FinishJob{cnt, nch, off, lut, nlut, total}, blockIdx.x, gridDim.x);
+}
+
+// Both streams' finishes in one launch: blocks [0, nb0) finish j0, the rest j1 (nch > 0 for each).
+__global__ __launch_bounds__(1024) void k_finish2(FinishJob j0, FinishJob j1) {
+    const uint32_t nb0 = finish_blocks(j0.nch);
+    if (blockIdx.x < nb0) finish_block(j0, blockIdx.x, nb0);
+    else finish_block(j1, blockIdx.x - nb0, gridDim.x - nb0);
 }
 
 // Metadata of a dense stream: chunk c = ranks [c*C, min((c+1)*C, n)).

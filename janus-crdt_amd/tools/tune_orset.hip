@@ -98,6 +98,43 @@ Times run(Stream& a, Stream& b, Stream& o, hipStream_t s) {
     return t;
 }
 
+// MODE bit 0: k_partition_gallop instead of k_partition; bit 1: persistent k_union_pf (dense inputs) with
+// PF workgroups per CU.
+template <int MODE, int PF>
+Times run2(Stream& a, Stream& b, Stream& o, hipStream_t s) {
+    constexpr int OB = 512, IT = 6, T = OB * IT;
+    const unsigned long long total = a.n + b.n, nt = (total + T - 1) / T;
+    uint64_t* part = (uint64_t*)ws;
+    uint32_t* pch = (uint32_t*)(ws + (((nt + 1) * 8 + 255) & ~255ull));
+    hipEvent_t e[4];
+    for (auto& x : e) CK(hipEventCreate(&x));
+    const View va = a.view(), vb = b.view();
+    CK(hipEventRecord(e[0], s));
+    if (MODE & 1) hipLaunchKernelGGL((jgk::k_partition_gallop<T>), dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, s, va, vb, nt + 1, part, pch);
+    else hipLaunchKernelGGL((jgk::k_partition<T, 1>), dim3((unsigned)((nt + 1 + 255) / 256)), dim3(256), 0, s, va, vb, nt + 1, part, pch);
+    CK(hipEventRecord(e[1], s));
+    if ((MODE & 2) && a.dense && b.dense) {
+        const unsigned g = (unsigned)std::min<unsigned long long>(nt, (unsigned long long)num_cus * PF);
+        hipLaunchKernelGGL((jgk::k_union_pf<OB, IT>), dim3(g), dim3(OB), 0, s, va, vb, part, o.key, o.tag, o.ord, (uint32_t)a.n, o.cnt,
+                           jgk::Drop{nullptr, 0}, nt);
+    } else {
+        hipLaunchKernelGGL((jgk::k_union<OB, IT>), dim3((unsigned)nt), dim3(OB), 0, s, va, vb, part, pch, o.key, o.tag, o.ord, (uint32_t)a.n, o.cnt,
+                           jgk::Drop{nullptr, 0});
+    }
+    CK(hipEventRecord(e[2], s));
+    hipLaunchKernelGGL(jgk::k_finish, dim3((unsigned)((nt + 1023) / 1024)), dim3(1024), 0, s, o.cnt, (uint32_t)nt, o.off, o.lut,
+                       (total >> jgk::kQShift) + 2, d_cnt);
+    CK(hipEventRecord(e[3], s));
+    CK(hipEventSynchronize(e[3]));
+    CK(hipGetLastError());
+    Times t;
+    CK(hipEventElapsedTime(&t.part, e[0], e[1])); CK(hipEventElapsedTime(&t.uni, e[1], e[2])); CK(hipEventElapsedTime(&t.fin, e[2], e[3]));
+    for (auto& x : e) CK(hipEventDestroy(x));
+    CK(hipMemcpy(&o.n, d_cnt, 8, hipMemcpyDeviceToHost));
+    o.nch = (uint32_t)nt; o.C = T; o.dense = 0;
+    return t;
+}
+
 struct Var { const char* name; Times (*fn)(Stream&, Stream&, Stream&, hipStream_t); };
 
 unsigned long long checksum(const Stream& o) {
@@ -144,10 +181,8 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
 
     const std::vector<Var> shapes = {
-        {"OB512 IT6 L1 (prod)", run<512, 6, 1>},  {"OB512 IT6 L4", run<512, 6, 4>},   {"OB512 IT6 L8", run<512, 6, 8>},
-        {"OB512 IT6 L16", run<512, 6, 16>},       {"OB512 IT6 L64", run<512, 6, 64>}, {"OB256 IT12 L1", run<256, 12, 1>},
-        {"OB1024 IT3 L1", run<1024, 3, 1>},       {"OB256 IT8 L1", run<256, 8, 1>},   {"OB256 IT6 L1", run<256, 6, 1>},
-        {"OB512 IT4 L1", run<512, 4, 1>},         {"OB512 IT8 L1", run<512, 8, 1>},
+        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"gallop", run2<1, 2>},    {"pf 2/CU", run2<2, 2>},   {"gallop+pf 2/CU", run2<3, 2>},
+        {"pf 1/CU", run2<2, 1>},                  {"gallop+pf 4/CU", run2<3, 4>}, {"OB512 IT6 L1 (prod) again", run<512, 6, 1>},
     };
     bench("dense x dense (C3 adds)", a, b, o, s, shapes, rounds);
 
@@ -159,9 +194,21 @@ int main(int argc, char** argv) {
     b2.set_dense(n, s);
     CK(hipStreamSynchronize(s));
     const std::vector<Var> ch = {
-        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"OB512 IT6 L4", run<512, 6, 4>}, {"OB512 IT6 L8", run<512, 6, 8>},
-        {"OB512 IT6 L16", run<512, 6, 16>},
+        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"gallop", run2<1, 2>},
     };
+    // the C3 tombstone stream: 20M + 20M records (u in [0, 2) and [1, 3)), dense x dense
+    Stream ra, rb, ro;
+    const unsigned long long nr = G * 2;
+    ra.alloc(nr, 3072); rb.alloc(nr, 3072); ro.alloc(2 * nr + 8192, 1024);
+    hipLaunchKernelGGL(k_gen, dim3(4096), dim3(256), 0, s, ra.key, ra.tag, nr, 2u, 0u, 10u, 0x52454Dull);
+    hipLaunchKernelGGL(k_gen, dim3(4096), dim3(256), 0, s, rb.key, rb.tag, nr, 2u, 1u, 10u, 0x52454Dull);
+    ra.set_dense(nr, s);
+    rb.set_dense(nr, s);
+    CK(hipStreamSynchronize(s));
+    const std::vector<Var> tv = {
+        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"gallop", run2<1, 2>}, {"pf 2/CU", run2<2, 2>}, {"gallop+pf 2/CU", run2<3, 2>},
+    };
+    bench("dense x dense (C3 tombstones)", ra, rb, ro, s, tv, rounds);
     bench("chunked x dense (store = previous union output)", o, b2, o2, s, ch, rounds);
     return 0;
 }
