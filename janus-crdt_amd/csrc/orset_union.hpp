@@ -429,92 +429,6 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
     union_tile<kOB, kItems>(sh, nA, nB, tile, rord, ok, ot, oord, ocnt, drop);
 }
 
-// Persistent variant for DENSE inputs (slot = rank): workgroup g walks tiles g, g + G, g + 2G, ... and
-// issues the loads of its next tile's records into registers right after staging the current tile in
-// LDS, so they are in flight while the current tile merges, compacts and stores (the one-tile kernel
-// has no load in flight during those phases; two workgroups per CU fit the LDS).  Tile bounds come one
-// iteration ahead of the loads that need them.
-template <int kOB, int kItems>
-__global__ __launch_bounds__(kOB) void k_union_pf(View a, View b, const uint64_t* __restrict__ part, unsigned long long* __restrict__ ok,
-                                                  uint4* __restrict__ ot, uint32_t* __restrict__ oord, uint32_t b_base,
-                                                  uint32_t* __restrict__ ocnt, Drop drop, uint64_t n_tiles) {
-    using SH = UnionShared<kOB, kItems>;
-    constexpr int kTile = SH::kTile;
-    __shared__ SH sh;
-    const int tid = threadIdx.x;
-    const uint64_t total_in = a.n + b.n;
-    const uint64_t G = gridDim.x;
-    uint64_t tile = blockIdx.x;
-    if (tile >= n_tiles) return;
-
-    unsigned long long rk[kItems], rlo[kItems], rhi[kItems];
-    uint32_t rord[kItems];
-    unsigned long long pk = 0;
-    Tag pt{0, 0};
-    // loads of tile t's records (and, on thread 0, the A record before it)
-    auto issue = [&](uint64_t t, uint64_t i0, uint64_t i1) {
-        const uint64_t d0 = t * kTile;
-        const uint64_t j0 = d0 - i0;
-        const int nA = (int)(i1 - i0);
-        const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
-        const int n = (int)(d1 - d0);
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {
-            const int x = min(it * kOB + tid, n - 1);
-            const bool from_a = x < nA;
-            const uint64_t r = from_a ? i0 + (uint64_t)x : j0 + (uint64_t)(x - nA);
-            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + r);
-            const Tag tg = ld_tag_nt((from_a ? a.tag : b.tag) + r);
-            rlo[it] = tg.lo;
-            rhi[it] = tg.hi;
-            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + r) + (from_a ? 0u : b_base);
-        }
-        if (tid == 0 && i0 > 0) {
-            pk = a.key[i0 - 1];
-            pt = ld_tag(a.tag + i0 - 1);
-        }
-    };
-    uint64_t i0 = part[tile], i1 = part[tile + 1];
-    issue(tile, i0, i1);
-    uint64_t nt = tile + G;
-    uint64_t n0 = nt < n_tiles ? part[nt] : 0, n1 = nt < n_tiles ? part[nt + 1] : 0;
-    for (;;) {
-        const uint64_t d0 = tile * kTile;
-        const uint64_t d1 = d0 + kTile < total_in ? d0 + kTile : total_in;
-        const int nA = (int)(i1 - i0), n = (int)(d1 - d0);
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) {
-            const int x = it * kOB + tid;
-            sh.key[x] = rk[it];
-            sh.tag[x] = to_u4(Tag{rlo[it], rhi[it]});
-        }
-        if (tid == 0) {
-            sh.has_prev = i0 > 0 && !dropped(drop, pk);
-            sh.prev_key = pk;
-            sh.prev_tag = to_u4(pt);
-        }
-        uint32_t cord[kItems];
-#pragma unroll
-        for (int it = 0; it < kItems; ++it) cord[it] = rord[it];
-        __syncthreads();
-        const uint64_t cur = tile;
-        const bool more = nt < n_tiles;
-        if (more) {
-            issue(nt, n0, n1);  // in flight during this tile's merge and stores
-            i0 = n0;
-            i1 = n1;
-            const uint64_t nn = nt + G;
-            n0 = nn < n_tiles ? part[nn] : 0;
-            n1 = nn < n_tiles ? part[nn + 1] : 0;
-        }
-        union_tile<kOB, kItems>(sh, nA, n - nA, cur, cord, ok, ot, oord, ocnt, drop);
-        if (!more) break;
-        tile = nt;
-        nt += G;
-        __syncthreads();  // every store of this tile read its LDS before the next staging
-    }
-}
-
 // After a union: off = exclusive scan of the tiles' counts (off[nch] = *total = the record count)
 // and the rank -> chunk table, in ceil(nch / 1024) workgroups.  Each workgroup sums the counts before
 // its 1024 chunks itself (coalesced 16-B loads, 16 in flight per thread: a one-count-per-iteration
