@@ -233,6 +233,92 @@ __global__ __launch_bounds__(256) void k_sorted(long long* AP, long long* AN, co
     }
 }
 
+// Generation-tagged heads: head64[key] = gen << 32 | row, so a head left from an earlier batch reads as
+// empty and no reset write is needed (the lead's head[key] = kNil store was one random write per
+// distinct key).
+__global__ void k_link_gen(const uint32_t* keys, uint64_t n, unsigned long long* head64, uint32_t* next, unsigned long long gen) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const unsigned long long old = atomicExch(head64 + keys[i], gen << 32 | i);
+        next[i] = (old >> 32) == gen ? (uint32_t)old : kNil;
+    }
+}
+template <int U>
+__global__ __launch_bounds__(256) void k_grouped_gen(long long* AP, long long* AN, const long long* BP, const long long* BN, const uint32_t* keys,
+                                                     const unsigned long long* head64, const uint32_t* next, uint64_t n, unsigned long long gen) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * 256) >> 6;
+    const bool isP = lane < NV;
+    const uint32_t w = isP ? lane : lane - NV;
+    const long long* B = isP ? BP : BN;
+    long long* A = isP ? AP : AN;
+    for (uint64_t m0 = (((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6) * U; m0 < n; m0 += nw * U) {
+        uint64_t key[U];
+        bool lead[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t m = m0 + u;
+            key[u] = m < n ? keys[m] : 0;
+            lead[u] = m < n && head64[key[u]] == (gen << 32 | m);
+        }
+        uint4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lead[u]) {
+                b[u] = ntl(reinterpret_cast<const uint4*>(B + (m0 + u) * R) + w);
+                a[u] = *(reinterpret_cast<const uint4*>(A + key[u] * R) + w);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!lead[u]) continue;
+            a[u] = vmax8(a[u], b[u]);
+            for (uint32_t cur = next[m0 + u]; cur != kNil;) {
+                const uint4 bb = ntl(reinterpret_cast<const uint4*>(B + (uint64_t)cur * R) + w);
+                const uint32_t nx = next[cur];
+                a[u] = vmax8(a[u], bb);
+                cur = nx;
+            }
+            *(reinterpret_cast<uint4*>(A + key[u] * R) + w) = a[u];
+        }
+    }
+}
+
+// Ceilings of the access pattern (not merges): each lead row (precomputed flags) reads its B row and its
+// key's A row and writes the A row back (RMW = 0) — the grouped merge minus its list walks — or only
+// gathers the A row into a sequential output (RMW = 1, the guide's "random whole-row gather").
+template <int U, int KIND>
+__global__ __launch_bounds__(256) void k_ceiling(long long* AP, long long* AN, const long long* BP, const long long* BN, const uint32_t* keys,
+                                                 const uint8_t* leadf, uint64_t n, long long* OP, long long* ON) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * 256) >> 6;
+    const bool isP = lane < NV;
+    const uint32_t w = isP ? lane : lane - NV;
+    const long long* B = isP ? BP : BN;
+    long long* A = isP ? AP : AN;
+    long long* O = isP ? OP : ON;
+    for (uint64_t m0 = (((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6) * U; m0 < n; m0 += nw * U) {
+        uint64_t key[U];
+        bool lead[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            key[u] = m0 + u < n ? keys[m0 + u] : 0;
+            lead[u] = m0 + u < n && leadf[m0 + u];
+        }
+        uint4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (lead[u]) {
+                if (KIND == 0) b[u] = ntl(reinterpret_cast<const uint4*>(B + (m0 + u) * R) + w);
+                a[u] = *(reinterpret_cast<const uint4*>(A + key[u] * R) + w);
+            }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!lead[u]) continue;
+            if (KIND == 0) *(reinterpret_cast<uint4*>(A + key[u] * R) + w) = vmax8(a[u], b[u]);
+            else nts(reinterpret_cast<uint4*>(O + (m0 + u) * R) + w, a[u]);
+        }
+    }
+}
+
 __global__ void k_sum(const unsigned long long* a, uint64_t n, unsigned long long* out) {
     unsigned long long s = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) s += a[i] * (i | 1);
@@ -280,10 +366,17 @@ int main() {
     struct Var { const char* name; int kind; };
     const Var vars[] = {{"head-only U4", 0}, {"head-only U8", 1}, {"count+head U4", 2}, {"sorted U4", 3}, {"sorted U8", 4}, {"sorted U4 nt-store", 5},
                         {"pipelined U4", 6}, {"pipelined U2", 7}, {"lead-flag U4", 8}, {"head-only U4 32/CU", 9},
-                        {"head-only U4 nt-store", 10}, {"head-only U2 nt-store", 11}};
-    constexpr int kVars = 12;
+                        {"head-only U4 nt-store", 10}, {"head-only U2 nt-store", 11}, {"ceiling: lead RMW, no lists", 12},
+                        {"ceiling: lead A gather only", 13}, {"gen-tagged heads U4", 14}};
+    constexpr int kVars = 15;
+    unsigned long long* head64;
+    CK(hipMalloc(&head64, n_keys * 8));
+    CK(hipMemset(head64, 0, n_keys * 8));
+    unsigned long long gen = 0;
     uint8_t* leadf;
     CK(hipMalloc(&leadf, n));
+    long long *OP, *ON;  // gather-only ceiling's output
+    CK(hipMalloc(&OP, n * R * 8)); CK(hipMalloc(&ON, n * R * 8));
     for (int dist = 0; dist < 2; ++dist) {
         std::vector<uint32_t> hk(n);
         std::mt19937_64 g(7 + dist);
@@ -328,6 +421,19 @@ int main() {
                     if (v.kind == 10) hipLaunchKernelGGL((k_grouped<4, true, false>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
                     else hipLaunchKernelGGL((k_grouped<2, true, false>), dim3(grid(2)), dim3(256), 0, 0, AP, AN, BP, BN, keys, claim, head, next, n);
                     hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                } else if (v.kind == 14) {
+                    ++gen;
+                    hipLaunchKernelGGL(k_link_gen, dim3(gk), dim3(256), 0, 0, keys, n, head64, next, gen);
+                    hipLaunchKernelGGL((k_grouped_gen<4>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, head64, next, n, gen);
+                } else if (v.kind == 12 || v.kind == 13) {  // flags computed outside the timed region
+                    CK(hipEventRecord(e1, 0));
+                    hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
+                    hipLaunchKernelGGL(k_lead, dim3(gk), dim3(256), 0, 0, keys, n, head, leadf);
+                    hipLaunchKernelGGL(k_reset<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head);
+                    CK(hipDeviceSynchronize());
+                    CK(hipEventRecord(e0, 0));
+                    if (v.kind == 12) hipLaunchKernelGGL((k_ceiling<4, 0>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, leadf, n, A0P, A0N);
+                    else hipLaunchKernelGGL((k_ceiling<4, 1>), dim3(grid(4)), dim3(256), 0, 0, AP, AN, BP, BN, keys, leadf, n, OP, ON);
                 } else if (v.kind == 9) {
                     hipLaunchKernelGGL(k_link<false>, dim3(gk), dim3(256), 0, 0, keys, n, claim, head, next);
                     const unsigned g9 = (unsigned)std::min<uint64_t>((n + 3) / 4 * 64 / 256, (uint64_t)num_cus * 32);
@@ -353,8 +459,9 @@ int main() {
         for (const Var& v : vars) {
             auto x = t[v.kind];
             std::sort(x.begin(), x.end());
-            std::printf("%-22s median %.3f ms  min %.3f  checksum %016llx%s\n", v.name, x[x.size() / 2], x[0], chk[v.kind],
-                        chk[v.kind] == chk[0] ? "" : "  MISMATCH");
+            const bool ceil = v.kind >= 12;
+            std::printf("%-28s median %.3f ms  min %.3f  %s %016llx%s\n", v.name, x[x.size() / 2], x[0], ceil ? "(no merge) sum" : "checksum", chk[v.kind],
+                        ceil || chk[v.kind] == chk[0] ? "" : "  MISMATCH");
         }
     }
     return 0;
