@@ -308,7 +308,11 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
             "merge": {"kernels": "k_group_link + k_merge_grouped<8,4>", "ms": merge_s * 1e3,
                       "distinct_keys": distinct,
                       "roofline": {"bound": "hbm", "achieved": merge_alg / merge_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                   "frac": merge_alg / merge_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": merge_alg}},
+                                   "frac": merge_alg / merge_s / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": merge_alg,
+                                   "pattern_ceiling": {"GBps": GROUPED_CEILING_GBS, "frac": merge_alg / merge_s / 1e9 / GROUPED_CEILING_GBS,
+                                                       "source": "profiles/r03/tune_grouped_ceiling.txt",
+                                                       "scope": "the same random 1-KB A-row read-modify-write + B-row read per distinct key "
+                                                                "with no lists, no link and no merge arithmetic (tools/tune_grouped.hip k_ceiling)"}}},
             "collective": f"library RCCL communicator (jg_comm), world {world}: ncclAllGather of the counts + grouped ncclSend/ncclRecv"}
 
 
@@ -410,6 +414,12 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
 
 
 PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link, per direction (MI355X_MICROARCH.md)
+# One hipMemcpyAsync of 48-MB chunks from page-locked memory, measured on the box: 56.0-56.5 GB/s; split over
+# two copy queues, SDMA off (blit kernels) or pulled by a kernel it is no faster (profiles/r03/tune_h2d.txt).
+PCIE_MEASURED_GBS = 56.5
+# The grouped merge's access pattern alone (random 1-KB A-row read-modify-write + one B-row read per distinct
+# key, 787k of 2M keys): 2.42 GB in 0.466 ms on the box (profiles/r03/tune_grouped_ceiling.txt).
+GROUPED_CEILING_GBS = 5190.0
 
 
 def apply_roofline(res):
@@ -427,6 +437,8 @@ def apply_roofline(res):
     ach = up / wave_s / 1e9
     out = {"bound": "pcie", "achieved": ach, "peak": PCIE_PEAK_GBS, "unit": "GB/s", "frac": ach / PCIE_PEAK_GBS, "traffic": None,
             "bytes_per_wave": up, "ideal_ms_per_wave": up / PCIE_PEAK_GBS / 1e6,
+            "measured_link": {"GBps": PCIE_MEASURED_GBS, "frac": ach / PCIE_MEASURED_GBS, "ideal_ms_per_wave": up / PCIE_MEASURED_GBS / 1e6,
+                              "source": "profiles/r03/tune_h2d.txt (one hipMemcpyAsync per 48-MB chunk from page-locked memory)"},
             "scope": "bytes the library uploads per wave (payloads + per-message arrays) / wave time",
             "device_share": {"bound": "hbm", "achieved": up / busy_s / 1e9 if busy_s else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": up / busy_s / 1e9 / HBM_PEAK_GBS if busy_s else None, "busy_ms_per_wave": busy_s * 1e3,
