@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 4
+#define JG_ABI_VERSION 5
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -331,11 +331,15 @@ int jg_apply_block(jg_node* node, const jg_commit* wave, uint64_t* stopped_at);
  * device after the last chunk was queued, the whole call.  Device: kernel time of the wave (hipEvents
  * around each chunk's kernels and around the final phase, on the context's stream) = chunk_busy_s (the
  * per-chunk classify + parse kernels: the payload decode) + tail_busy_s (after the last chunk).  Messages
- * and payload bytes uploaded, messages applied (registered CRDT states before the cut), chunks. */
+ * and payload bytes uploaded, messages applied (registered CRDT states before the cut), chunks.  Host
+ * phases (ABI v5, appended): setup_s (registrations and tracker adds to the device, buffers sized, the
+ * previous call's kernels drained) and loop_s (the chunk loop: gathers + queueing the uploads and kernels);
+ * total_s = setup_s + loop_s + device_wait_s + argument checks. */
 typedef struct jg_apply_stats {
     double gather_s, device_wait_s, total_s, device_busy_s;
     uint64_t msgs_uploaded, bytes_uploaded, msgs_applied, chunks;
     double chunk_busy_s, tail_busy_s;
+    double setup_s, loop_s;
 } jg_apply_stats;
 int jg_node_last_stats(jg_node* node, jg_apply_stats* out);
 

@@ -139,9 +139,23 @@ __global__ void k_track_lookup(DevTrack t, const unsigned long long* __restrict_
     out[i] = r;
 }
 
-__global__ void k_rebase(uint64_t* __restrict__ off, uint64_t n, uint64_t base) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) off[i] += base;
+// A chunk's per-message arrays arrive as ONE upload (the staging layout: end offsets [m + 1] from 0, uids
+// [m], identities [m], types [m], back to back) and are scattered here into the wave's arrays, offsets
+// rebased to the chunk's first payload byte: one copy per chunk instead of four (each copy on the queue
+// cost ~8-17 us of gap on top of its bytes: ~60 us per 131k-message chunk, 6 % of its upload).
+__global__ __launch_bounds__(kBlock) void k_unstage(const uint8_t* __restrict__ meta, uint64_t m, uint64_t m0, uint64_t b0,
+                                                    uint64_t* __restrict__ off, Guid16* __restrict__ uid, uint64_t* __restrict__ seq,
+                                                    uint8_t* __restrict__ type) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= m) return;
+    const auto* soff = reinterpret_cast<const uint64_t*>(meta);
+    const auto* suid = reinterpret_cast<const uint64_t*>(soff + m + 1);  // 8-B aligned: two words per uid
+    const auto* sseq = suid + 2 * m;
+    const auto* stype = reinterpret_cast<const uint8_t*>(sseq + m);
+    off[m0 + 1 + j] = soff[j + 1] + b0;
+    uid[m0 + j] = Guid16{suid[2 * j], suid[2 * j + 1]};
+    seq[m0 + j] = sseq[j];
+    type[m0 + j] = stype[j];
 }
 
 // Per message of [m0, m1): the loop's skip rule (:133-134), the uid lookup (:136), the tracker slot of its
@@ -241,6 +255,7 @@ struct jg_tracker {
     struct Pin { unsigned long long* p = nullptr; size_t cap = 0, n = 0; } pin[2];
     int cur = 0;
     jg::DevBuf tab, claim, count, dpairs;
+    jg::DevBuf spare_tab, spare_claim;  // the other pair of a rebuild (tables are rebuilt into it, then swapped)
     uint64_t cap = 0;
     uint64_t used = 0;  // live + tombstones, an upper bound (TryAdd of a present identity counted too)
 
@@ -283,26 +298,28 @@ struct jg_tracker {
         }
         const uint64_t np = b->n;
         if (np == 0) return;
-        if (cap == 0 || 2 * (used + np) > cap) {  // rebuild without tombstones
+        if (cap == 0 || 2 * (used + np) > cap) {  // rebuild without tombstones, into the spare table
             unsigned long long live = 0;
             if (cap) {
                 JG_HIP(hipMemcpyAsync(&live, count.p, 8, hipMemcpyDeviceToHost, ctx->stream));
                 JG_HIP(hipStreamSynchronize(ctx->stream));
             }
             const uint64_t ncap = pow2_at_least(4 * (live + np), 4096);
-            jg::DevBuf nt, nc;
-            nt.alloc(ncap * sizeof(TrackSlot));
-            nc.alloc(ncap * 4);
-            JG_HIP(hipMemsetAsync(nt.p, 0, nt.bytes, ctx->stream));
-            JG_HIP(hipMemsetAsync(nc.p, 0xFF, nc.bytes, ctx->stream));
-            const DevTrack nd{nt.as<TrackSlot>(), nc.as<uint32_t>(), ncap - 1};
+            // the spare is the table before the last rebuild: reused while it is large enough (a steady
+            // wave stream rebuilds every wave or two at the same capacity; hipMalloc + hipFree of the
+            // tables cost ~0.7 ms of a C5 wave's setup), freed-and-grown otherwise.  Stream order keeps
+            // the rehash reading the old table before anything clears it.
+            if (spare_tab.bytes < ncap * sizeof(TrackSlot)) spare_tab.alloc(ncap * sizeof(TrackSlot));
+            if (spare_claim.bytes < ncap * 4) spare_claim.alloc(ncap * 4);
+            JG_HIP(hipMemsetAsync(spare_tab.p, 0, ncap * sizeof(TrackSlot), ctx->stream));
+            JG_HIP(hipMemsetAsync(spare_claim.p, 0xFF, ncap * 4, ctx->stream));
+            const DevTrack nd{spare_tab.as<TrackSlot>(), spare_claim.as<uint32_t>(), ncap - 1};
             if (cap) hipLaunchKernelGGL(k_track_rehash, dim3(blocks_for(cap)), dim3(kBlock), 0, ctx->stream, tab.as<TrackSlot>(), cap, nd);
             JG_HIP(hipGetLastError());
-            JG_HIP(hipStreamSynchronize(ctx->stream));
-            std::swap(tab.p, nt.p);
-            std::swap(tab.bytes, nt.bytes);
-            std::swap(claim.p, nc.p);
-            std::swap(claim.bytes, nc.bytes);
+            std::swap(tab.p, spare_tab.p);
+            std::swap(tab.bytes, spare_tab.bytes);
+            std::swap(claim.p, spare_claim.p);
+            std::swap(claim.bytes, spare_claim.bytes);
             cap = ncap;
             used = live;
         }
@@ -331,6 +348,7 @@ struct jg_node {
     bool foreign = false;
     // the wave on the device
     jg::DevBuf bytes, off, uid, seq, type, rows, mset, tslot, origin, done, status, cub;
+    jg::DevBuf meta;  // the wave's per-message arrays as uploaded, chunk after chunk (k_unstage)
     // pinned staging arenas, carved front to back each wave and kept
     std::vector<std::pair<char*, size_t>> arenas;
     size_t arena_i = 0, arena_off = 0;
@@ -339,10 +357,12 @@ struct jg_node {
     std::vector<uint64_t> dmap;  // device index -> commit index (when the shard shortcut dropped messages)
     jg_apply_stats stats{};
     std::vector<hipEvent_t> ev;  // pairs around each chunk's kernels and the final phase (device_busy_s)
+    hipEvent_t drained = nullptr;  // the compute stream's tail when a wave starts (the copy queue waits on it)
 
     ~jg_node() {
         for (auto& a : arenas) (void)hipHostFree(a.first);
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+        if (drained) (void)hipEventDestroy(drained);
     }
     hipEvent_t event(size_t k) {
         while (ev.size() <= k) {
@@ -458,9 +478,14 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         for (uint64_t i = 0; i < n; ++i) JG_REQUIRE(w->off[i + 1] >= w->off[i], JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)i);
     }
     nd->stats = jg_apply_stats{};
+    static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;  // setup phases to stderr
+    double tp[8] = {now_s()};
     if (nd->orset) jg::orset_node_no_names(nd->orset);
+    tp[1] = now_s();
     nd->sync_table();
+    tp[2] = now_s();
     if (tr) tr->flush();
+    tp[3] = now_s();
     nd->arena_i = nd->arena_off = 0;  // the previous wave's chunks are no longer referenced
     nd->dmap.clear();
     if (n == 0) {
@@ -497,15 +522,17 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     if (w->off) {
         total_bytes = w->off[n];
     } else {
-        const size_t ntask = (n + kTask - 1) / kTask;
+        const uint64_t per = std::max<uint64_t>(65536, (n + 63) / 64);  // few large tasks: this pass only sums lengths
+        const size_t ntask = (size_t)((n + per - 1) / per);
         std::vector<uint64_t> part(ntask);
         jg::deal(pool, n >= min_par, ntask, [&](size_t q, int) {
             uint64_t b = 0;
-            for (uint64_t i = q * kTask, e = std::min<uint64_t>(n, (q + 1) * kTask); i < e; ++i) b += w->len[i];
+            for (uint64_t i = q * per, e = std::min<uint64_t>(n, (q + 1) * per); i < e; ++i) b += w->len[i];
             part[q] = b;
         });
         for (uint64_t b : part) total_bytes += b;
     }
+    tp[4] = now_s();
     ensure(nd->bytes, ((total_bytes + 15) & ~15ull) + 64);  // the parsers read aligned 16-byte windows
     ensure(nd->off, (n + 1) * 8);
     ensure(nd->uid, n * 16);
@@ -515,6 +542,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     ensure(nd->mset, n * 4);
     ensure(nd->tslot, n * 4);
     ensure(nd->status, 64);
+    ensure(nd->meta, n * 33 + 72 * (n_chunks + 1));  // per chunk: 33 m + 8 bytes, 64-B aligned
     uint8_t* d_bytes = nd->bytes.as<uint8_t>();
     uint64_t* d_off = nd->off.as<uint64_t>();
     uint32_t* d_rows = nd->rows.as<uint32_t>();
@@ -523,17 +551,30 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     const bool do_pnc = nd->pnc && nd->n_pnc > 0, do_orset = nd->orset && nd->n_orset > 0;
     const DevUids du{nd->dtab.as<UidSlot>(), nd->htab.size() - 1};
     const DevTrack dt = tr && tr->cap ? tr->dev() : DevTrack{nullptr, nullptr, 0};
-    // the copy stream must not overwrite buffers the previous call's kernels still read
-    JG_HIP(hipStreamSynchronize(ctx->stream));
+    // the copy queue must not overwrite buffers kernels queued earlier on the compute stream still read:
+    // it waits for the stream's tail on the device (a host sync here also waited for the tracker adds
+    // just queued, 0.3-0.4 ms of every C5 wave before the first gather)
+    if (!nd->drained) JG_HIP(hipEventCreateWithFlags(&nd->drained, hipEventDisableTiming));
+    JG_HIP(hipEventRecord(nd->drained, ctx->stream));
+    JG_HIP(hipStreamWaitEvent(ctx->copy, nd->drained, 0));
+    tp[5] = now_s();
     JG_HIP(hipMemsetAsync(d_off, 0, 8, ctx->stream));
     JG_HIP(hipMemsetAsync(d_status, 0xFF, 64, ctx->stream));
     if (do_pnc) jg::pnc_node_begin(nd->pnc, n);
+    tp[6] = now_s();
     if (do_orset) jg::orset_node_begin(nd->orset, d_bytes, d_off, d_mset, n, total_bytes, nd->max_set);
+    tp[7] = now_s();
+    if (trace)
+        std::fprintf(stderr, "apply setup: checks %.0f us, names %.0f, uid table %.0f, tracker adds %.0f, sizes %.0f, buffers %.0f, pnc begin %.0f, orset begin %.0f\n",
+                     (tp[0] - t_begin) * 1e6, (tp[1] - tp[0]) * 1e6, (tp[2] - tp[1]) * 1e6, (tp[3] - tp[2]) * 1e6, (tp[4] - tp[3]) * 1e6,
+                     (tp[5] - tp[4]) * 1e6, (tp[6] - tp[5]) * 1e6, (tp[7] - tp[6]) * 1e6);
     const bool direct = w->off && !filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
     if (filter) nd->dmap.resize(n);
 
     double t_gather = 0;
-    uint64_t m0 = 0, b0 = 0;
+    const double t_loop = now_s();
+    nd->stats.setup_s = t_loop - t_begin;
+    uint64_t m0 = 0, b0 = 0, mo = 0;
     size_t n_ev = 0;  // event pairs recorded
     const size_t max_tasks = (chunk_msgs + kTask - 1) / kTask + 1;
     std::vector<uint64_t> tcnt(max_tasks + 1), tbytes(max_tasks + 1);
@@ -592,13 +633,14 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             // upload (copy stream), then classify and both parses of the chunk (compute stream)
             const uint8_t* src = direct ? w->bytes + w->off[c0] : reinterpret_cast<const uint8_t*>(buf);
             if (nb) JG_HIP(hipMemcpyAsync(d_bytes + b0, src, nb, hipMemcpyHostToDevice, ctx->copy));
-            JG_HIP(hipMemcpyAsync(d_off + m0 + 1, soff + 1, m * 8, hipMemcpyHostToDevice, ctx->copy));
-            JG_HIP(hipMemcpyAsync(nd->uid.as<jg_guid>() + m0, suid, m * 16, hipMemcpyHostToDevice, ctx->copy));
-            JG_HIP(hipMemcpyAsync(nd->seq.as<uint64_t>() + m0, sseq, m * 8, hipMemcpyHostToDevice, ctx->copy));
-            JG_HIP(hipMemcpyAsync(nd->type.as<uint8_t>() + m0, stype, m, hipMemcpyHostToDevice, ctx->copy));
+            const uint64_t meta_bytes = (m + 1) * 8 + m * 25;  // offsets, uids (16), identities (8), types (1)
+            uint8_t* d_meta = nd->meta.as<uint8_t>() + mo;
+            JG_HIP(hipMemcpyAsync(d_meta, soff, meta_bytes, hipMemcpyHostToDevice, ctx->copy));
+            mo += (meta_bytes + 63) & ~63ull;
             jg::upload_done(ctx);
             JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));
-            if (b0) hipLaunchKernelGGL(k_rebase, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d_off + m0 + 1, m, b0);
+            hipLaunchKernelGGL(k_unstage, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d_meta, m, m0, b0, d_off, nd->uid.as<Guid16>(),
+                               nd->seq.as<uint64_t>(), nd->type.as<uint8_t>());
             hipLaunchKernelGGL(k_classify, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, nd->uid.as<Guid16>(), nd->type.as<uint8_t>(),
                                nd->seq.as<unsigned long long>(), m0, m0 + m, du, dt, d_rows, d_mset, nd->tslot.as<uint32_t>(), d_status);
             JG_HIP(hipGetLastError());
@@ -622,6 +664,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     nd->stats.bytes_uploaded = b0;
     if (nn) nd->avg_msg_bytes = (double)b0 / (double)nn;
     const double t_dev = now_s();
+    nd->stats.loop_s = t_dev - t_loop;
 
     // the cut: the first state the reference's loop would throw at
     JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));  // the final phase's kernels start after the chunks'

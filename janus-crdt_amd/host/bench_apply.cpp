@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
     std::unordered_map<uint64_t, uint64_t> tracker_c;    // the oracle node's
     uint64_t seq = 1;
 
-    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0, chunk_s = 0;
+    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0, chunk_s = 0, setup_s = 0, loop_s = 0;
     uint64_t gpu_n = 0, cpu_n = 0, payload_timed = 0, up_bytes = 0, up_msgs = 0, applied = 0, n_safe = 0, n_states = 0, n_done = 0;
     bool ok = true;
     std::string why;
@@ -234,6 +234,8 @@ int main(int argc, char** argv) {
         lib_s += st.total_s;
         busy_s += st.device_busy_s;
         chunk_s += st.chunk_busy_s;
+        setup_s += st.setup_s;
+        loop_s += st.loop_s;
         up_bytes += st.bytes_uploaded;
         up_msgs += st.msgs_uploaded;
         applied += st.msgs_applied;  // counted by the library: states that reached a registered key
@@ -275,7 +277,7 @@ int main(int argc, char** argv) {
                 "\"waves\": %d, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
                 "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"completed_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, "
                 "\"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
-                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
+                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
                 "\"uploaded_msgs_per_wave\": %.1f, \"uploaded_bytes_per_wave\": %.1f, \"pcie_GBps\": %.2f, \"engine_payload_GBps\": %.2f, "
                 "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %.1f, \"cores\": 1, \"kind\": \"port\", "
@@ -283,7 +285,7 @@ int main(int argc, char** argv) {
                 normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, gpu_n / gpu_s,
                 (double)ops * waves / gpu_s, 1e3 * gpu_s / W, (double)gpu_n / W, (double)n_states / W, (double)n_safe / W, (double)n_done / W,
                 (double)payload_timed / std::max<uint64_t>(gpu_n, 1), 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W,
-                1e3 * busy_s / W, 1e3 * chunk_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
+                1e3 * busy_s / W, 1e3 * chunk_s / W, 1e3 * setup_s / W, 1e3 * loop_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
                 (double)up_bytes / std::max(busy_s, 1e-12) / 1e9, jg::host_threads(), rank, world, (unsigned long long)owned,
                 (double)applied / W, cpu_s > 0 ? cpu_n / cpu_s : 0.0, (double)cpu_n / W);
     return 0;

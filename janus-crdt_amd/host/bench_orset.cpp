@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
     static const char chars[] = "abcdefghijklmnorqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789";  // sic (BenchmarkWorkload.cs:151)
     // per (set, node): the node's elements since its last Clear, one tag each
     std::vector<janus::ORSetState> st(sets * nodes);
-    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0, chunk_s = 0;
+    double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0, chunk_s = 0, setup_s = 0, loop_s = 0;
     uint64_t up_bytes = 0, up_msgs = 0, applied = 0;
     uint64_t gpu_n = 0, cpu_n = 0, payload = 0, recs = 0;
     const int warm = 2;  // warm-up waves: the staging buffers reach their size, the tables their load
@@ -123,6 +123,8 @@ int main(int argc, char** argv) {
         lib_s += st.total_s;
         busy_s += st.device_busy_s;
         chunk_s += st.chunk_busy_s;
+        setup_s += st.setup_s;
+        loop_s += st.loop_s;
         up_bytes += st.bytes_uploaded;
         up_msgs += st.msgs_uploaded;
         applied += st.msgs_applied;
@@ -140,14 +142,14 @@ int main(int argc, char** argv) {
     std::printf("{\"workload\": \"committed-batch apply (OR-Set, ORSetWorkload-shaped: random 5-char adds, Clear at 50, %llu sets, %d nodes, "
                 "%llu ORSetMsg JSON states per wave)\", \"waves\": %d, \"msgs_per_s\": %.1f, \"ms_per_wave\": %.3f, \"payload_bytes_per_msg\": %.1f, "
                 "\"tag_records_per_msg\": %.2f, \"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
-                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
+                "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
                 "\"uploaded_msgs_per_wave\": %.1f, \"uploaded_bytes_per_wave\": %.1f, \"pcie_GBps\": %.2f, \"engine_payload_GBps\": %.2f, "
                 "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_sets\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %llu, \"cores\": 1, "
                 "\"kind\": \"port\", \"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + ORSet.Merge per message\"}}\n",
                 (unsigned long long)sets, nodes, (unsigned long long)msgs, waves, gpu_n / gpu_s, 1e3 * gpu_s / W, (double)payload / gpu_n,
                 (double)recs / gpu_n, 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W, 1e3 * busy_s / W,
-                1e3 * chunk_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
+                1e3 * chunk_s / W, 1e3 * setup_s / W, 1e3 * loop_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,
                 (double)up_bytes / std::max(busy_s, 1e-12) / 1e9, jg::host_threads(), rank, world, (unsigned long long)owned, (double)applied / W,
                 cpu_s > 0 ? cpu_n / cpu_s : 0.0, (unsigned long long)std::min(msgs, cpu_msgs));
     return 0;

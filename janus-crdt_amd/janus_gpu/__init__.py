@@ -612,7 +612,8 @@ class ApplyStats(C.Structure):
     """jg_apply_stats."""
     _fields_ = [("gather_s", C.c_double), ("device_wait_s", C.c_double), ("total_s", C.c_double), ("device_busy_s", C.c_double),
                 ("msgs_uploaded", _u64), ("bytes_uploaded", _u64), ("msgs_applied", _u64), ("chunks", _u64),
-                ("chunk_busy_s", C.c_double), ("tail_busy_s", C.c_double)]
+                ("chunk_busy_s", C.c_double), ("tail_busy_s", C.c_double),
+                ("setup_s", C.c_double), ("loop_s", C.c_double)]
 
 
 def shard_of(lo: int, hi: int, world: int) -> int:
