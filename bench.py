@@ -137,12 +137,30 @@ class HipEvents:
             self.hip.hipEventDestroy(e)
 
 
-def timed(ctx, sync, fn, steps, warmup):
-    """Run fn() warmup+steps times; returns (max-over-ranks wall seconds, event seconds) of the K steps."""
+def timed(ctx, sync, fn, steps, warmup, min_warm_s=0.0, info=None):
+    """Run fn() warmup+steps times; returns (max-over-ranks wall seconds, event seconds) of the K steps.
+    min_warm_s: after the W warmup steps, more untimed steps until about that much warmup time has passed
+    (the same count on every rank: fn may hold a collective).  Short HBM-bound steps keep getting faster
+    for tens of milliseconds of sustained traffic (the C3 union: 2.07 -> 1.71 ms per add union over its
+    first 5 steps, profiles/r03), so a leg of ~2 ms steps is timed once that ramp is over; info["warmup"]
+    receives the count actually run."""
     ev = HipEvents(ctx.stream())
+    t_w = time.perf_counter()
     for _ in range(warmup):
         fn()
     ctx.fence()
+    done = warmup
+    if min_warm_s > 0:
+        el = time.perf_counter() - t_w
+        per = el / max(warmup, 1)
+        extra = 0 if el >= min_warm_s or per <= 0 else min(500, int((min_warm_s - el) / per) + 1)
+        extra = int(sync.max(float(extra)))
+        for _ in range(extra):
+            fn()
+        ctx.fence()
+        done += extra
+    if info is not None:
+        info["warmup"] = done
     sync.barrier()
     ctx.fence()
     t0 = time.perf_counter()
@@ -228,6 +246,7 @@ def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2", scaling="we
             "keys": n_keys, "keys_total": keys_total, "cells_total": keys_total * R, "R": R}
 
 
+SIDE_WARM_S = 0.1  # untimed warmup of the side legs (OR-Set, exchange, JSON, digests): at least this long
 ORSET_STRONG_SHARDS = 8  # strong scaling: the C3 shape x 8 shards (80M (set, elem) groups) split over the ranks
 
 
@@ -249,12 +268,14 @@ def bench_orset(jg, ctx, sync, rank, world, steps, warmup, scaling="weak"):
     out = jg.ORSetStore(ctx, 2 * na, 2 * nr)
     L.synth(SEED + rank, groups, ORSET_E, ORSET_ADD, 0, ORSET_REM, 0)
     R.synth(SEED + rank, groups, ORSET_E, ORSET_ADD, ORSET_ADD - ORSET_ADD_OV, ORSET_REM, ORSET_REM - ORSET_REM_OV)
-    wall, ev = timed(ctx, sync, lambda: jg.ORSetStore.union(L, R, out, async_=True), steps, warmup)
+    wi = {}
+    wall, ev = timed(ctx, sync, lambda: jg.ORSetStore.union(L, R, out, async_=True), steps, max(warmup, 1), SIDE_WARM_S, wi)
     ua, ur = out.size()
     for h in (L, R, out):
         h.close()
     consumed = 2 * (na + nr)
     return {"wall_s": wall, "event_s": ev, "records_per_rank": consumed, "records_total": sync.sum_int(consumed), "groups": groups, "out": [ua, ur],
+            "warmup": wi["warmup"],
             "bytes_per_step": consumed * REC_BYTES + (ua + ur) * REC_BYTES}
 
 
@@ -281,7 +302,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
         rows.upload(zeros, zeros, keys)   # the key indices; values synthesised on the device next
         rows.synth(SEED + 11 + rank)
         last = {}
-        wall, _ = timed(ctx, sync, lambda: last.update(comm.exchange_pnc(store, rows)), steps, warmup)
+        wall, _ = timed(ctx, sync, lambda: last.update(comm.exchange_pnc(store, rows)), steps, max(warmup, 1), SIDE_WARM_S)
         st = comm.stats()
         phases = {"route_ms": st.route_s * 1e3, "counts_and_runs_ms": st.exchange_s * 1e3, "merge_ms": st.merge_s * 1e3,
                   "link_bytes_sent": int(st.bytes_sent), "link_bytes_received": int(st.bytes_received)}
@@ -290,7 +311,7 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
         lkeys = keys % EXCH_KEYS
         rows.upload(zeros, zeros, lkeys)
         rows.synth(SEED + 11 + rank)
-        _, ev_m = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, warmup)
+        _, ev_m = timed(ctx, sync, lambda: store.merge_batch(rows, async_=True), steps, max(warmup, 1), SIDE_WARM_S)
     finally:
         store.close()
         rows.close()
@@ -379,7 +400,7 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
     warm = jg.PNCStore(ctx, JSON_KEYS, JSON_R, JSON_EB)
     try:
         w.upload(keys, data=data, off=off)
-        wall, ev = timed(ctx, sync, lambda: warm.merge_wave(w), steps, warmup)
+        wall, ev = timed(ctx, sync, lambda: warm.merge_wave(w), steps, max(warmup, 1), SIDE_WARM_S)
         cold_ms = []
         for _ in range(2):
             cold = jg.PNCStore(ctx, JSON_KEYS, JSON_R, JSON_EB)
@@ -538,17 +559,17 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
     try:
         w.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data, off=off)
         w2.upload(np.zeros(DIGEST_MSGS, np.uint32), data=data2, off=off2)
-        wall, ev = timed(ctx, sync, lambda: w.update_digests(first), steps, warmup)
+        wall, ev = timed(ctx, sync, lambda: w.update_digests(first), steps, max(warmup, 1), SIDE_WARM_S)
         # the first level alone (k_sha_msgs, digest bytes into device memory: jg_wave_sha256)
         import torch
         dout = torch.empty(DIGEST_MSGS * 32, dtype=torch.uint8, device=torch.device("cuda", ctx.device))
-        wall1, ev1 = timed(ctx, sync, lambda: w.sha256_device(dout.data_ptr(), async_=True), steps, warmup)
+        wall1, ev1 = timed(ctx, sync, lambda: w.sha256_device(dout.data_ptr(), async_=True), steps, max(warmup, 1), SIDE_WARM_S)
         del dout
         # pipelined: DIGEST_PIPE waves in one jg_waves_update_digests call (wave k's chains on the
         # context's second stream beside wave k+1's first level); two distinct resident waves alternate, so
         # wave k+1's first level does not re-read the bytes wave k just streamed through the caches
         pipe = [w, w2] * (DIGEST_PIPE // 2)
-        wall_p, ev_p = timed(ctx, sync, lambda: jg.waves_update_digests(pipe, [first] * DIGEST_PIPE), steps, warmup)
+        wall_p, ev_p = timed(ctx, sync, lambda: jg.waves_update_digests(pipe, [first] * DIGEST_PIPE), steps, max(warmup, 1), SIDE_WARM_S)
     finally:
         w.close()
         w2.close()
@@ -730,14 +751,15 @@ def main():
                          f"{ORSET_STRONG_SHARDS * 100}M adds + {ORSET_STRONG_SHARDS * 20}M tombstones per side, split over {world} GPUs)"),
             "scaling": args.scaling, "groups_per_rank": o["groups"],
             "value": o["records_total"] / ost, "unit": "tag records merged/s",
-            "ms_per_step": ost * 1e3, "out_records": o["out"],
+            "ms_per_step": ost * 1e3, "out_records": o["out"], "steps": max(1, args.steps // 2), "warmup": o["warmup"],
             "hbm_GBps": world * o["bytes_per_step"] / ost / 1e9,
             "roofline": {"bound": "hbm", "achieved": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": o["bytes_per_step"] / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
                          "traffic": _orset_traffic(),
                          "frac_24B": o["bytes_per_step"] * 24 / 28 / (o["event_s"] / max(1, args.steps // 2)) / 1e9 / HBM_PEAK_GBS,
-                         "scope": "whole step: adds + tombstones, each k_partition + k_union + k_finish; 28-B records (key, tag, "
+                         "scope": "whole step: both streams' boundaries (k_partition_gallop2), the add and tombstone unions (k_union), "
+                                  "both finishes (k_finish2); 28-B records (key, tag, "
                                   "arrival ordinal); frac_24B = the same time in SURVEY.md D3's 24-B unit (DESIGN.md section 5)"},
         }
         if "value" not in line:
