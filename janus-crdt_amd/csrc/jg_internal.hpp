@@ -105,9 +105,10 @@ struct jg_pnc {
     jg::DevBuf P, N;
     // replica table (json.hip): [n_keys x R] 16-byte Guids + [n_keys] column counts, first use only
     jg::DevBuf cols, ncols;
-    // grouped indexed merge (k_group_*): per-key list head of the batch being merged (0xFFFFFFFF between
-    // calls) and a next[] link per received row; first use
+    // grouped indexed merge (k_group_*): per-key list head of the batch being merged (gen << 32 | row,
+    // generation-tagged: no reset between calls) and a next[] link per received row; first use
     jg::DevBuf head, next;
+    unsigned long long head_gen = 0;  // generation of the last grouped batch (heads hold gen << 32 | row)
     // open streamed wave (jg_pnc_wave_*): payload, offsets, rows, status + deferred list; pass A's
     // resolved entries per message and its list of messages pass B must parse again (json.hip)
     jg::DevBuf wbytes, woff, wrows, wstat, wemit, wguid, wslow;

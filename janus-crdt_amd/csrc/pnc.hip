@@ -109,25 +109,27 @@ __global__ __launch_bounds__(kBlock) void k_merge_indexed_rows(typename Elem<EB>
     }
 }
 
-// Duplicate-aware scatter-max with no atomics on the data, three passes over the batch's keys (a
-// committed wave folds several states of one key, SafeCRDTManager.cs:122-146).  Pass 1 (k_group_link)
-// links each key's rows into a list: next[m] = the key's previous head, head[key] = m (one atomicExch
-// per row).  Pass 2 (k_merge_grouped): the head row of every key loads its A row once, max-folds every
-// B row of the key in registers — each B row's load issued together with its next[] link, so a key
-// held k times costs k - 1 dependent hops — and stores A once; the other rows of the key do nothing.
-// The list head also restores head[key] to kNil once it has claimed the key (any row reading head
-// later sees kNil, not itself: only the head row ever matched), so no reset pass runs.  Atomics ran
-// at ~1.3 TB/s of added bytes on
-// MI355X against ~6 TB/s for plain stores (MI355X_MICROARCH.md, atomics table), and random 4-B atomics
-// ~17x slower again: a per-cell atomicMax for repeated keys (39 % of the rows of a uniform batch of n
-// rows over 2n keys) and an occurrence counter per row both measured slower (tools/tune_grouped.hip,
-// DESIGN.md §4).  ABSENT (the width's minimum) needs no test: max(a, ABSENT) = a.
+// Duplicate-aware scatter-max with no atomics on the data, two passes over the batch's keys (a committed
+// wave folds several states of one key, SafeCRDTManager.cs:122-146).  Pass 1 (k_group_link) links each
+// key's rows into a list: next[m] = the key's previous head, head[key] = gen << 32 | m (one atomicExch per
+// row).  Pass 2 (k_merge_grouped): the head row of every key loads its A row once, max-folds every B row of
+// the key in registers — each B row's load issued together with its next[] link, so a key held k times
+// costs k - 1 dependent hops — and stores A once; the other rows of the key do nothing.  Heads carry the
+// batch's generation: a head left by an earlier batch reads as empty, so nothing resets them (the list
+// head's `head[key] = kNil` store was one more random write per distinct key: 0.578 -> 0.566 ms per 1M rows,
+// tools/tune_grouped.hip).  Atomics ran at ~1.3 TB/s of added bytes on MI355X against ~6 TB/s for plain
+// stores (MI355X_MICROARCH.md, atomics table), and random 4-B atomics ~17x slower again: a per-cell
+// atomicMax for repeated keys (39 % of the rows of a uniform batch of n rows over 2n keys) and an
+// occurrence count per row both measured slower (tools/tune_grouped.hip).  ABSENT (the
+// width's minimum) needs no test: max(a, ABSENT) = a.
 constexpr uint32_t kNil = 0xFFFFFFFFu;
 
-__global__ __launch_bounds__(kBlock) void k_group_link(const uint32_t* __restrict__ keys, uint64_t n, uint32_t* __restrict__ head,
-                                                       uint32_t* __restrict__ next) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-        next[i] = atomicExch(head + keys[i], (uint32_t)i);
+__global__ __launch_bounds__(kBlock) void k_group_link(const uint32_t* __restrict__ keys, uint64_t n, unsigned long long* __restrict__ head,
+                                                       uint32_t* __restrict__ next, unsigned long long gen) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const unsigned long long old = atomicExch(head + keys[i], gen << 32 | i);
+        next[i] = (old >> 32) == gen ? (uint32_t)old : kNil;
+    }
 }
 
 // One wave per received row, U rows in flight; the row (R x EB bytes) is a whole number of 16-B vectors
@@ -136,8 +138,8 @@ template <int EB, int U>
 __global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* __restrict__ AP, typename Elem<EB>::T* __restrict__ AN,
                                                           const typename Elem<EB>::T* __restrict__ BP,
                                                           const typename Elem<EB>::T* __restrict__ BN, const uint32_t* __restrict__ keys,
-                                                          uint32_t* __restrict__ head, const uint32_t* __restrict__ next, uint64_t n_rows,
-                                                          uint32_t R) {
+                                                          const unsigned long long* __restrict__ head, const uint32_t* __restrict__ next,
+                                                          uint64_t n_rows, uint32_t R, unsigned long long gen) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nv = R * EB / 16;  // vectors per array row
     const uint64_t n_waves = ((uint64_t)gridDim.x * kBlock) >> 6;
@@ -148,12 +150,7 @@ __global__ __launch_bounds__(kBlock) void k_merge_grouped(typename Elem<EB>::T* 
         for (int u = 0; u < U; ++u) {
             const uint64_t m = m0 + u;
             key[u] = m < n_rows ? keys[m] : 0;
-            lead[u] = m < n_rows && head[key[u]] == (uint32_t)m;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (lead[u]) head[key[u]] = kNil;  // the key is claimed: ready for the next batch
+            lead[u] = m < n_rows && head[key[u]] == (gen << 32 | m);
         }
         for (uint32_t v = lane; v < 2 * nv; v += 64) {
             const bool isP = v < nv;
@@ -319,25 +316,24 @@ void launch_merge_dense(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void
     JG_HIP(hipGetLastError());
 }
 
-// The store's per-key list heads (kNil between calls) and a next[] link per received row (grown to the
-// largest batch).
-struct Groups { uint32_t* head; uint32_t* next; };
+// The store's per-key list heads (generation-tagged) and a next[] link per received row (grown to the
+// largest batch); gen = this batch's generation.
+struct Groups { unsigned long long* head; uint32_t* next; unsigned long long gen; };
 
 void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const void* BP, const void* BN, const uint32_t* keys,
                           uint64_t n_rows, uint32_t R, const Groups* g = nullptr) {
     if (g && R >= 32 && ((uint64_t)R * eb) % 16 == 0) {
         JG_REQUIRE(n_rows < kNil, JG_EINVAL, "merge: %llu rows exceed one grouped launch", (unsigned long long)n_rows);
         const unsigned gk = grid_for(ctx, n_rows, 16);
-        hipLaunchKernelGGL(k_group_link, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, g->head, g->next);
+        hipLaunchKernelGGL(k_group_link, dim3(gk), dim3(kBlock), 0, ctx->stream, keys, n_rows, g->head, g->next, g->gen);
         constexpr int U = 4;  // rows in flight per wave (U = 8 measured slower, tools/tune_grouped.hip)
         const unsigned grid = grid_for(ctx, (n_rows + U - 1) / U * 64, 16);
         if (eb == 8)
             hipLaunchKernelGGL((k_merge_grouped<8, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (long long*)AP, (long long*)AN,
-                               (const long long*)BP, (const long long*)BN, keys, g->head, g->next, n_rows, R);
+                               (const long long*)BP, (const long long*)BN, keys, g->head, g->next, n_rows, R, g->gen);
         else
             hipLaunchKernelGGL((k_merge_grouped<4, U>), dim3(grid), dim3(kBlock), 0, ctx->stream, (int*)AP, (int*)AN, (const int*)BP,
-                               (const int*)BN, keys, g->head, g->next, n_rows, R);
-
+                               (const int*)BN, keys, g->head, g->next, n_rows, R, g->gen);
         JG_HIP(hipGetLastError());
         return;
     }
@@ -362,19 +358,22 @@ void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const vo
     JG_HIP(hipGetLastError());
 }
 
-// The store's group state for a batch of n_rows (allocated on first use; every grouped merge restores
-// the heads it touched).  nullptr when rows are too narrow for the vector path.
+// The store's group state for a batch of n_rows (allocated on first use; each grouped merge takes the next
+// generation, and the heads are cleared once every 2^32 - 1 batches).  nullptr when rows are too narrow
+// for the vector path.
 const Groups* groups_of(jg_pnc* p, uint64_t n_rows, Groups& g) {
     if (p->R < 32 || ((uint64_t)p->R * p->eb) % 16 != 0) return nullptr;
-    if (!p->head.p) {
-        p->head.alloc(p->n_keys * 4);
-        JG_HIP(hipMemsetAsync(p->head.p, 0xFF, p->n_keys * 4, p->ctx->stream));
+    if (!p->head.p || p->head_gen == 0xFFFFFFFFull) {
+        if (!p->head.p) p->head.alloc(p->n_keys * 8);
+        JG_HIP(hipMemsetAsync(p->head.p, 0, p->n_keys * 8, p->ctx->stream));
+        p->head_gen = 0;
     }
+    ++p->head_gen;
     if (p->next.bytes < n_rows * 4) {
         JG_HIP(hipStreamSynchronize(p->ctx->stream));  // an earlier launch may still read the old links
         p->next.alloc(n_rows * 4 + n_rows);
     }
-    g = Groups{p->head.as<uint32_t>(), p->next.as<uint32_t>()};
+    g = Groups{p->head.as<unsigned long long>(), p->next.as<uint32_t>(), p->head_gen};
     return &g;
 }
 
