@@ -60,7 +60,7 @@ int main(int argc, char** argv) {
     std::vector<std::vector<Queued>> q(nodes);
     uint64_t seq = 1;
 
-    double gpu_s = 0, cpu_s = 0, up_bytes = 0, busy_s = 0, gather_s = 0, chunk_s = 0;
+    double gpu_s = 0, cpu_s = 0, up_bytes = 0, busy_s = 0, gather_s = 0, chunk_s = 0, setup_s = 0, loop_s = 0, wait_s = 0, lib_s = 0;
     uint64_t n_msgs = 0, n_updates = 0, n_ops = 0;
     for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
         std::vector<janus::UpdateMessage> ums;
@@ -140,6 +140,10 @@ int main(int argc, char** argv) {
         up_bytes += (double)st.bytes_uploaded;
         busy_s += st.device_busy_s;
         chunk_s += st.chunk_busy_s;
+        setup_s += st.setup_s;
+        loop_s += st.loop_s;
+        wait_s += st.device_wait_s;
+        lib_s += st.total_s;
         gather_s += st.gather_s;
         gpu_s += t1 - t0;
         cpu_s += t2 - t1;
@@ -155,11 +159,11 @@ int main(int argc, char** argv) {
     std::printf("{\"workload\": \"C1: PNCWorkload-shaped client ops (%llu keys round-robin, opsRatio [0.25, 0.25, 0.5], safeRatio 0.5, "
                 "Next(1,100)), %d nodes, clientBatchSize %d with state compaction, committed waves of %llu client ops\", \"waves\": %d, "
                 "\"state_msgs_per_wave\": %.1f, \"client_updates_per_wave\": %.1f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, "
-                "\"ms_per_wave\": %.3f, \"uploaded_bytes_per_wave\": %.1f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
+                "\"ms_per_wave\": %.3f, \"uploaded_bytes_per_wave\": %.1f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"device_wait_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
                 "\"parity_vs_oracle\": %s, \"cpu_baseline\": {\"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, "
                 "\"ms_per_wave\": %.3f, \"cores\": 1, \"kind\": \"port\", \"sample\": \"oracle HandleAfterConsensusUpdates on the same waves\"}}\n",
                 (unsigned long long)keys, nodes, batch, (unsigned long long)updates, waves, (double)n_msgs / waves, (double)n_updates / waves,
-                n_msgs / gpu_s, n_ops / gpu_s, 1e3 * gpu_s / waves, up_bytes / waves, 1e3 * busy_s / waves, 1e3 * chunk_s / waves, 1e3 * gather_s / waves, cpu ? (parity ? "true" : "false") : "null", cpu ? n_msgs / cpu_s : 0.0,
+                n_msgs / gpu_s, n_ops / gpu_s, 1e3 * gpu_s / waves, up_bytes / waves, 1e3 * busy_s / waves, 1e3 * chunk_s / waves, 1e3 * lib_s / waves, 1e3 * setup_s / waves, 1e3 * loop_s / waves, 1e3 * wait_s / waves, 1e3 * gather_s / waves, cpu ? (parity ? "true" : "false") : "null", cpu ? n_msgs / cpu_s : 0.0,
                 cpu ? n_ops / cpu_s : 0.0, cpu ? 1e3 * cpu_s / waves : 0.0);
     return parity ? 0 : 1;
 }
