@@ -499,6 +499,21 @@ def bench_apply_loop(sync, rank, world, local):
     return res
 
 
+def bench_apply_direct(local):
+    """The C5 wave of bench_apply_loop as a transport that receives its blocks into page-locked memory
+    (jg_host_alloc) would hand it over: the payloads back to back there, laid out outside the timed region
+    (that copy is the receive path's), then the same jg_apply_committed, which uploads them in place (the
+    library's `direct` path, no gather).  One GPU only: the shard shortcut gathers (it drops other shards'
+    states on the host)."""
+    import subprocess
+    exe = ROOT / "janus-crdt_amd" / "build" / "bench_apply"
+    out = subprocess.run([str(exe), "--accounts", "1000000", "--ops", "1000000", "--waves", "3", "--cpu-msgs", "0",
+                          "--device", str(local), "--direct"], capture_output=True, text=True, timeout=240)
+    if out.returncode != 0:
+        return {"error": out.stderr[-500:]}
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
 def bench_apply_orset(sync, rank, world, local):
     """The committed-batch apply loop for OR-Set states (ORSetWorkload-shaped, host/bench_orset.cpp):
     2000 sets, 4 nodes, 200k full-state ORSetMsg payloads per wave, through the host mirror (host
@@ -710,7 +725,8 @@ def main():
     apply_loop = guarded(bench_apply_loop, sync, rank, world, local) if args.workload == "all" else None
     apply_orset = guarded(bench_apply_orset, sync, rank, world, local) if args.workload == "all" else None
     apply_c1 = guarded(bench_c1, local) if args.workload == "all" and world == 1 else None
-    for leg in (apply_loop, apply_orset, apply_c1):
+    apply_direct = guarded(bench_apply_direct, local) if args.workload == "all" and world == 1 else None
+    for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
         if leg is not None and "error" not in leg and "scaling" not in leg:
             leg["roofline"] = guarded(apply_roofline, leg)
     sync.close()
@@ -777,6 +793,8 @@ def main():
         line["apply_loop_orset"] = apply_orset
     if apply_c1 is not None:
         line["apply_loop_c1"] = apply_c1
+    if apply_direct is not None:
+        line["apply_loop_direct"] = apply_direct
     line["cpu_baseline"] = cpu
     print(json.dumps(line), flush=True)
 

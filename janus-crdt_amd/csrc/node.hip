@@ -26,6 +26,7 @@
 // concurrent probes never see an entry move); rebuilt without tombstones when live + removed pass 1/2.
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <chrono>
 #include <memory>
 #include <string>
@@ -473,10 +474,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     JG_REQUIRE(n < 0x7FFFFFF0ull, JG_EINVAL, "jg_apply: at most 2^31 - 16 messages per wave");
     JG_REQUIRE(n == 0 || (w->uid && w->type && (w->off ? w->bytes != nullptr || w->off[n] == 0 : (w->ptr && w->len))), JG_EINVAL,
                "jg_apply: NULL array in the wave");
-    if (w->off) {
-        JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");
-        for (uint64_t i = 0; i < n; ++i) JG_REQUIRE(w->off[i + 1] >= w->off[i], JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)i);
-    }
+    if (w->off) JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");  // monotonicity: checked by the chunks' first pass
     nd->stats = jg_apply_stats{};
     static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;  // setup phases to stderr
     double tp[8] = {now_s()};
@@ -584,14 +582,26 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             const size_t ntask = (size_t)((c1 - c0 + kTask - 1) / kTask);
             const bool par = c1 - c0 >= min_par;
             const double tg = now_s();
-            // pass 1: kept messages and their bytes per task
+            // pass 1: kept messages and their bytes per task (and, for contiguous payloads, that the offsets
+            // never decrease: the wave is rejected before anything of it is applied)
+            std::atomic<uint64_t> bad_off{UINT64_MAX};
             jg::deal(pool, par, ntask, [&](size_t q, int) {
                 uint64_t k = 0, b = 0;
-                for (uint64_t i = c0 + q * kTask, e = std::min(c1, c0 + (q + 1) * kTask); i < e; ++i)
+                const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
+                for (uint64_t i = c0 + q * kTask; i < e; ++i)
                     if (keep(i)) ++k, b += plen(i);
+                if (w->off)
+                    for (uint64_t i = c0 + q * kTask; i < e; ++i)
+                        if (w->off[i + 1] < w->off[i]) {
+                            uint64_t cur = bad_off.load();
+                            while (i < cur && !bad_off.compare_exchange_weak(cur, i)) {
+                            }
+                            break;
+                        }
                 tcnt[q + 1] = k;
                 tbytes[q + 1] = b;
             });
+            JG_REQUIRE(bad_off.load() == UINT64_MAX, JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)bad_off.load());
             tcnt[0] = tbytes[0] = 0;
             for (size_t q = 0; q < ntask; ++q) tcnt[q + 1] += tcnt[q], tbytes[q + 1] += tbytes[q];
             const uint64_t m = tcnt[ntask], nb = tbytes[ntask];
@@ -653,6 +663,9 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             ++nd->stats.chunks;
         }
     } catch (...) {
+        // a wave rejected mid-loop (offsets checked chunk by chunk): nothing was applied, but the chunks
+        // already classified took first-occurrence claims on tracker slots; release them for the next wave
+        if (dt.tab && m0) hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(m0)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), m0, dt.claim);
         (void)hipStreamSynchronize(ctx->copy);
         (void)hipStreamSynchronize(ctx->stream);
         if (do_orset) jg::orset_node_abort(nd->orset);

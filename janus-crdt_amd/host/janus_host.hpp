@@ -151,6 +151,13 @@ class GpuStableStore {
     // entries removed (:141-142).  A rejected payload throws ApplyError after the prefix was applied.
     std::vector<uint64_t> ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker = nullptr);
 
+    // The same apply for a wave a transport received into page-locked memory: PackCommitted
+    // lays the wave out as such a receive path would (payloads back to back in jg_host_alloc memory + offsets),
+    // ApplyPacked applies it with ONE jg_apply_committed that uploads the payloads in place (the library's
+    // `direct` path: no gather into its staging).  Same results as ApplyCommitted on the same wave.
+    void PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates);
+    std::vector<uint64_t> ApplyPacked(SafeUpdateTracker* tracker = nullptr);
+
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
     // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the
     // PROSPECTIVE merge of one received block, one jg_apply_block call.  Creation
@@ -241,6 +248,8 @@ class GpuStableStore {
     void flush_registrations();  // pending CreateSafeCRDT registrations -> jg_node_register + jg_pnc_intern
     // ApplyCommitted / ReceivedBlock: flatten the messages into the jg_commit arrays, one library call.
     std::vector<uint64_t> apply(const std::vector<const UpdateMessage*>& blocks, SafeUpdateTracker* tracker, bool block_mode);
+    size_t index_blocks(const std::vector<const UpdateMessage*>& blocks);  // block_off_ + the flattened arrays' room
+    std::vector<uint64_t> run_wave(const jg_commit& wave, SafeUpdateTracker* tracker, bool block_mode);
     jg::WorkerPool& pool();  // persistent host workers for the flatten
 
     jg_ctx* ctx_ = nullptr;
@@ -262,6 +271,10 @@ class GpuStableStore {
     std::vector<const uint8_t*> w_ptr_;
     std::vector<uint32_t> w_len_;
     std::vector<uint64_t> w_done_;  // the library's completions
+    std::vector<uint64_t> p_off_;   // PackCommitted: payload offsets into p_bytes_ (page-locked, jg_host_alloc)
+    uint8_t* p_bytes_ = nullptr;
+    size_t p_cap_ = 0;
+    uint64_t p_n_ = 0;
     jg_apply_stats stats_{};
     double flatten_s_ = 0;
     uint64_t last_msgs_ = 0;

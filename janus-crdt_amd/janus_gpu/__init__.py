@@ -653,6 +653,24 @@ class Tracker:
             self._h = _vp()
 
 
+class PinnedBytes:
+    """Page-locked host bytes (jg_host_alloc): a wave whose payloads sit here uploads without the library's
+    gather (the `direct` path of jg_apply_committed)."""
+
+    def __init__(self, ctx: Context, data):
+        src = _arr(data, np.uint8)
+        self._p = _vp()
+        self.size = max(16, src.size)
+        _check(load().jg_host_alloc(ctx.handle, self.size, C.byref(self._p)))
+        self.array = np.ctypeslib.as_array(C.cast(self._p, C.POINTER(C.c_uint8)), shape=(self.size,))
+        self.array[: src.size] = src
+
+    def close(self) -> None:
+        if self._p:
+            _check(load().jg_host_free(self._p))
+            self._p = _vp()
+
+
 class Node:
     """A node's copy of its keys (jg_node) over a PN-Counter and/or an OR-Set store."""
 
@@ -670,7 +688,7 @@ class Node:
     def set_shard(self, rank: int, world: int) -> None:
         _check(load().jg_node_set_shard(self._h, rank, world))
 
-    def _commit(self, lo, hi, types, seqs, msgs=None, data=None, off=None):
+    def _commit(self, lo, hi, types, seqs, msgs=None, data=None, off=None, pinned=None):
         if msgs is not None:
             data, off = pack_wave(msgs)
         g = np.empty(np.size(lo), GUID_DTYPE)
@@ -679,14 +697,24 @@ class Node:
         s = None if seqs is None else _arr(seqs, np.uint64)
         data = _arr(data, np.uint8)
         data = data if data.size else np.zeros(16, np.uint8)
+        if pinned is not None:  # payloads in page-locked memory: the library uploads them in place
+            data = PinnedBytes(pinned, data)
         off = _arr(off, np.uint64)
         keep = (g, t, s, data, off)
-        c = Commit(g.size, _ptr(g), _ptr(t), _ptr(s), _ptr(off), _ptr(data), None, None)
+        c = Commit(g.size, _ptr(g), _ptr(t), _ptr(s), _ptr(off), data._p if pinned is not None else _ptr(data), None, None)
         return c, keep
 
-    def apply_committed(self, tracker: Tracker | None, lo, hi, types, seqs, msgs=None, data=None, off=None):
-        """jg_apply_committed: returns (completed origins in commit order, stopped_at or None, code)."""
-        c, keep = self._commit(lo, hi, types, seqs, msgs, data, off)
+    def apply_committed(self, tracker: Tracker | None, lo, hi, types, seqs, msgs=None, data=None, off=None, pinned=None):
+        """jg_apply_committed: returns (completed origins in commit order, stopped_at or None, code).  pinned: a
+        Context whose page-locked memory carries the payloads (the library's direct upload, no gather)."""
+        c, keep = self._commit(lo, hi, types, seqs, msgs, data, off, pinned)
+        try:
+            return self._apply(tracker, c)
+        finally:
+            if pinned is not None:
+                keep[3].close()
+
+    def _apply(self, tracker, c):
         done = np.zeros(max(1, c.n), np.uint64)
         nd, at = _u64(), _u64()
         rc = load().jg_apply_committed(self._h, tracker._h if tracker else None, C.byref(c), _ptr(done), C.byref(nd), C.byref(at))

@@ -126,7 +126,7 @@ def _wave(rng, m, uids, n_pnc, n_set, n, pcl, ocl, seq0, bad_at=None, extras=Tru
     return wave
 
 
-def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=False, block=False, shard=None):
+def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=False, block=False, shard=None, pinned=False):
     rng = np.random.default_rng(seed)
     if chunk and monkeypatch:
         monkeypatch.setenv("JANUS_WAVE_CHUNK", str(chunk))
@@ -155,7 +155,7 @@ def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=Fa
                 cut, rc = node.apply_block(lo, hi, types, msgs)
                 done = []
             else:
-                done, cut, rc = node.apply_committed(tr, lo, hi, types, seqs, msgs)
+                done, cut, rc = node.apply_committed(tr, lo, hi, types, seqs, msgs, pinned=ctx if pinned else None)
             assert cut == exp_cut, (cut, exp_cut)
             assert (rc == jg.JG_OK) == (exp_cut is None)
             assert list(done) == exp_done
@@ -189,6 +189,16 @@ def test_mixed_waves_many_chunks(ctx, monkeypatch):
     """Waves cut into 97-message chunks gathered by every worker: chunk-relative offsets rebased, classify
     and both parses per chunk, completions across chunks."""
     _run(ctx, 5, 150, 40, 3, 2500, chunk=97, monkeypatch=monkeypatch)
+
+
+@pytest.mark.parametrize("chunk,bad", [(None, False), (83, False), (61, True)])
+def test_direct_upload_from_pinned_payloads(ctx, monkeypatch, chunk, bad):
+    """Payloads the caller holds in page-locked memory (jg_host_alloc) are uploaded in place, chunk by chunk
+    (no gather into the library's staging): the same stores, completions and cut as the gathered path."""
+    if chunk:
+        _run(ctx, 11, 120, 40, 3, 2000, chunk=chunk, monkeypatch=monkeypatch, bad=bad, pinned=True)
+    else:
+        _run(ctx, 13, 200, 60, 3, 4000, bad=bad, pinned=True)
 
 
 @pytest.mark.parametrize("chunk", [None, 61])
@@ -320,3 +330,42 @@ def test_register_rejects_bad_keys(ctx):
     finally:
         node.close()
         pnc.close()
+
+
+def test_decreasing_offsets_reject_the_wave(ctx, monkeypatch):
+    """Contiguous payload offsets that decrease inside a later chunk (checked by each chunk's first pass)
+    reject the whole wave with JG_EINVAL before anything of it is applied; the tracker claims the chunks
+    already classified took are released, so the same wave with correct offsets then applies exactly as
+    the oracle's loop does (completions included)."""
+    monkeypatch.setenv("JANUS_WAVE_CHUNK", "50")
+    monkeypatch.setenv("JANUS_HOST_PAR_MIN", "1")
+    rng = np.random.default_rng(17)
+    n_pnc, n_set, n = 60, 20, 400
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, n_pnc, n_set)
+    try:
+        pcl = J.Cluster(rng, n_pnc, R - 1, EB, stable=None)
+        ocl = J.ORSetCluster(rng, n_set)
+        wave = _wave(rng, m, uids, n_pnc, n_set, n, pcl, ocl, seq0=0, extras=False)
+        tr.add(list(m.tracker), list(m.tracker.values()))
+        lo, hi = [x[0][0] for x in wave], [x[0][1] for x in wave]
+        types, seqs = [x[1] for x in wave], [x[2] for x in wave]
+        data, off = jg.pack_wave([x[3] for x in wave])
+        bad = np.array(off, np.uint64).copy()
+        bad[301] = bad[300] - 1  # message 300 (chunk 6 of 50-message chunks) ends before it starts
+        with pytest.raises(jg.JanusError) as e:
+            node.apply_committed(tr, lo, hi, types, seqs, data=data, off=bad)
+        assert e.value.code == jg.JG_EINVAL and "offsets decrease at message 300" in str(e.value)
+        P0, N0 = pnc.read_rows()
+        assert np.array_equal(P0, m.P) and np.array_equal(N0, m.N)  # nothing applied
+        exp_done, exp_cut = m.apply(wave)
+        done, cut, rc = node.apply_committed(tr, lo, hi, types, seqs, data=data, off=off)
+        assert rc == jg.JG_OK and cut is None and exp_cut is None
+        assert list(done) == exp_done
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+        ga, gr = st.read()
+        assert orc.same_orset(ga, gr, *m.orset)
+        assert tr.size() == len(m.tracker)
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()
