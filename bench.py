@@ -246,7 +246,8 @@ def bench_pnc(jg, ctx, sync, rank, world, steps, warmup, shape="c2", scaling="we
             "keys": n_keys, "keys_total": keys_total, "cells_total": keys_total * R, "R": R}
 
 
-SIDE_WARM_S = 0.1  # untimed warmup of the side legs (OR-Set, exchange, JSON, digests): at least this long
+# untimed warmup of the side legs (OR-Set, exchange, JSON, digests): at least this long
+SIDE_WARM_S = float(os.environ.get("JANUS_BENCH_SIDE_WARM_S", "0.1"))
 ORSET_STRONG_SHARDS = 8  # strong scaling: the C3 shape x 8 shards (80M (set, elem) groups) split over the ranks
 
 

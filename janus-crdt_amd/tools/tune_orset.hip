@@ -140,9 +140,12 @@ struct Stream {
     uint32_t* lut = nullptr;
     unsigned long long n = 0;
     uint32_t nch = 0, C = 0, dense = 1;
-    void alloc(unsigned long long cap_slots, uint32_t chunk) {
+    // shift: the arrays start `shift` records into their allocations (tests whether streams whose ranks
+    // line up at the same large-power-of-two address offsets contend for the same HBM channels)
+    void alloc(unsigned long long cap_slots, uint32_t chunk, unsigned long long shift = 0) {
         const unsigned long long ch = cap_slots / chunk + 2;
-        CK(hipMalloc(&key, (ch * chunk) * 8)); CK(hipMalloc(&tag, (ch * chunk) * 16)); CK(hipMalloc(&ord, (ch * chunk) * 4));
+        CK(hipMalloc(&key, (ch * chunk + shift) * 8)); CK(hipMalloc(&tag, (ch * chunk + shift) * 16)); CK(hipMalloc(&ord, (ch * chunk + shift) * 4));
+        key += shift; tag += shift; ord += shift;
         CK(hipMalloc(&cnt, ch * 4)); CK(hipMalloc(&off, (ch + 1) * 8)); CK(hipMalloc(&lut, (((ch * chunk) >> jgk::kQShift) + 2) * 4));
         C = chunk;
     }
@@ -270,10 +273,21 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
 
     const std::vector<Var> shapes = {
-        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"gallop", run2<1, 2>},    {"pf 2/CU", run2<2, 2>},   {"gallop+pf 2/CU", run2<3, 2>},
-        {"pf 1/CU", run2<2, 1>},                  {"gallop+pf 4/CU", run2<3, 4>}, {"OB512 IT6 L1 (prod) again", run<512, 6, 1>},
+        {"OB512 IT6 L1 (prod)", run<512, 6, 1>}, {"gallop", run2<1, 2>}, {"OB512 IT6 L1 (prod) again", run<512, 6, 1>},
     };
     bench("dense x dense (C3 adds)", a, b, o, s, shapes, rounds);
+    {  // the same inputs with B's arrays (and then the output's) started at odd record offsets
+        Stream bs, os_;
+        bs.alloc(n, 3072, 1573);
+        os_.alloc(2 * n + 8192, 1024, 777);
+        hipLaunchKernelGGL(k_gen, dim3(4096), dim3(256), 0, s, bs.key, bs.tag, n, 10u, 5u, 10u, 0x4A414E5553ull);
+        bs.set_dense(n, s);
+        CK(hipStreamSynchronize(s));
+        const std::vector<Var> pv = {{"prod", run<512, 6, 1>}, {"prod again", run<512, 6, 1>}};
+        bench("dense x dense, B shifted 1573 records", a, bs, o, s, pv, rounds);
+        bench("dense x dense, B shifted 1573, out 777", a, bs, os_, s, pv, rounds);
+        bench("dense x dense, unshifted (control)", a, b, o, s, pv, rounds);
+    }
 
     // chunked store: A' = A u B from the production shape, then A' u B2 with B2 a fresh dense batch
     run<512, 6, 1>(a, b, o, s);
