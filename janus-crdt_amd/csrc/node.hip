@@ -602,6 +602,8 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
                 tbytes[q + 1] = b;
             });
             JG_REQUIRE(bad_off.load() == UINT64_MAX, JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)bad_off.load());
+            // monotone on [0, c1] and within off[n]: every chunk so far fits the buffers sized from off[n]
+            JG_REQUIRE(!w->off || w->off[c1] <= w->off[n], JG_EINVAL, "jg_apply: offsets decrease after message %llu", (unsigned long long)(c1 - 1));
             tcnt[0] = tbytes[0] = 0;
             for (size_t q = 0; q < ntask; ++q) tcnt[q + 1] += tcnt[q], tbytes[q + 1] += tbytes[q];
             const uint64_t m = tcnt[ntask], nb = tbytes[ntask];
