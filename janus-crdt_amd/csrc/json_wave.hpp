@@ -110,9 +110,12 @@ __device__ __forceinline__ bool entry_at(const uint8_t* base, uint32_t q, Guid16
     return ok;
 }
 
-__device__ __forceinline__ bool lds_name_tail(const uint8_t* s) {  // s = the byte after 'p' / 'n': Vector":{
-    return s[0] == 'V' && s[1] == 'e' && s[2] == 'c' && s[3] == 't' && s[4] == 'o' && s[5] == 'r' && s[6] == '"' && s[7] == ':' &&
-           s[8] == '{';
+// `Vector":{` at LDS byte q (the byte after 'p' / 'n'): three realigned words instead of nine byte reads.
+__device__ __forceinline__ bool lds_name_tail(const uint8_t* base, uint32_t q) {
+    uint32_t X[3];
+    lds_words<3>(base, q, X);
+    return X[0] == ('V' | 'e' << 8 | 'c' << 16 | (uint32_t)'t' << 24) && X[1] == ('o' | 'r' << 8 | '"' << 16 | (uint32_t)':' << 24) &&
+           (X[2] & 0xFFu) == '{';
 }
 
 // A wave's parse result.  The tokens of the wave's 64 / G groups, in group order, are dealt over its
@@ -190,48 +193,43 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
         }
     }
     if (rc.has && g < rc.nc) sh.cols[grp][g] = rc.cg;
-    uint32_t ntok = 0;
+    // token starts = the even-numbered quotes: in the compact form every string (the two property names,
+    // each entry's Guid) is one pair of quotes with no escapes inside, so quote 2k opens token k.  A stray or
+    // escaped quote shifts the pairing, and the token chain of phase 3 then fails: slow list (the serial
+    // parser decides).  (The round-2 scan tested each quote's previous byte for '{' or ',' instead: two more
+    // SWAR tests per word and a carried byte between lanes, ~40 VALU per window.)
+    uint32_t nq = 0;  // quotes before this window, over the group
     if (fit) {
-        uint32_t carry = 0;
 #pragma unroll
         for (uint32_t u = 0; u < NW; ++u) {
             const uint32_t w = u * G + g;
             if (u * G * 16 >= a + L) break;  // group-uniform
             if (w * 16 < a + L) sh.buf[grp][w] = v[u];
-            // token starts: '"' right after '{' or ','; o = those two bytes, carried across words and lanes
-            const uint32_t wv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            uint32_t o[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[i] = zero_bytes(wv[i] ^ 0x7B7B7B7Bu) | zero_bytes(wv[i] ^ 0x2C2C2C2Cu);
-            uint32_t prev = __shfl_up(o[3], 1, G);
-            if (g == 0) prev = carry;
-            carry = __shfl(o[3], G - 1, G);
-            uint32_t cm = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                cm |= bits4(zero_bytes(wv[i] ^ 0x22222222u) & (o[i] << 8 | prev >> 24)) << (4 * i);
-                prev = o[i];
-            }
+            uint32_t qm = bits4(zero_bytes(v[u].x ^ 0x22222222u)) | bits4(zero_bytes(v[u].y ^ 0x22222222u)) << 4 |
+                          bits4(zero_bytes(v[u].z ^ 0x22222222u)) << 8 | bits4(zero_bytes(v[u].w ^ 0x22222222u)) << 12;
             const int base = (int)(16 * w) - (int)a;  // message position of byte 0 of this window
             const int jlo = base >= 1 ? 0 : 1 - base, jhi = (int)L - base;  // bytes j with 1 <= base + j < L
-            cm &= jlo >= 16 || jhi <= 0 ? 0u : ((jhi >= 16 ? 0xFFFFu : (1u << jhi) - 1u) & ~((1u << jlo) - 1u));
-            const uint32_t cnt = __popc(cm);
+            qm &= jlo >= 16 || jhi <= 0 ? 0u : ((jhi >= 16 ? 0xFFFFu : (1u << jhi) - 1u) & ~((1u << jlo) - 1u));
+            const uint32_t cnt = __popc(qm);
             uint32_t incl = cnt;
 #pragma unroll
             for (int d = 1; d < G; d <<= 1) {
                 const uint32_t y = __shfl_up(incl, d, G);
                 if (g >= (uint32_t)d) incl += y;
             }
-            uint32_t k = ntok + incl - cnt;
-            while (cm) {
-                const int j = __ffs(cm) - 1;
-                cm &= cm - 1;
-                if (k < kGroupTok) sh.tok[grp][k] = (uint16_t)(base + j);
-                ++k;
+            uint32_t q = nq + incl - cnt;  // index of this lane's first quote in the window
+            if (q & 1) qm &= qm - 1, ++q;  // an odd quote closes a string: start from the next one
+            while (qm) {  // every other quote from here opens a token
+                const int j = __ffs(qm) - 1;
+                if ((q >> 1) < kGroupTok) sh.tok[grp][q >> 1] = (uint16_t)(base + j);
+                qm &= qm - 1;
+                qm &= qm - 1;  // skip the closing quote
+                q += 2;
             }
-            ntok += __shfl(incl, G - 1, G);
+            nq += __shfl(incl, G - 1, G);
         }
     }
+    const uint32_t ntok = (nq & 1) ? kGroupTok + 1 : nq >> 1;  // an unpaired quote: not the compact form
     const bool go = fit && ntok <= kGroupTok && ntok >= 2;  // group-uniform
     const uint32_t nt = go ? ntok : 0;
     if (g == 0) {
@@ -282,7 +280,10 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
             const int c1 = p + 1 < Lq ? cq[p + 1] : -1;
             uint32_t e = UINT32_MAX, next = UINT32_MAX;  // the '}' closing this token's vector / the next token's start
             if (c1 == 'p' || c1 == 'n') {                // property name
-                if (p + 12 > Lq || !lds_name_tail(cq + p + 2) || (c1 == 'p' && (k != 0 || p != 1))) { bad = true; break; }
+                if (p + 12 > Lq || !lds_name_tail(reinterpret_cast<const uint8_t*>(sh.buf[gq]), aq + p + 2) || (c1 == 'p' && (k != 0 || p != 1))) {
+                    bad = true;
+                    break;
+                }
                 const uint32_t q = p + 11;
                 if (cq[q] == '}') e = q;
                 else next = q;
