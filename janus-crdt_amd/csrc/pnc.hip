@@ -12,6 +12,8 @@
 //   k_apply_ops      Increment/Decrement (PNCounters.cs:97-112): wrapping atomic adds.
 //   k_values         PNCounter.Get (PNCounters.cs:87-90): one wave per key, exact prefix sums in
 //                    column order to reproduce the checked LINQ Sum's OverflowException.
+#include <cstdlib>
+
 #include "jg_internal.hpp"
 
 namespace {
@@ -364,9 +366,13 @@ void launch_merge_indexed(jg_ctx* ctx, uint32_t eb, void* AP, void* AN, const vo
 const Groups* groups_of(jg_pnc* p, uint64_t n_rows, Groups& g) {
     if (p->R < 32 || ((uint64_t)p->R * p->eb) % 16 != 0) return nullptr;
     if (!p->head.p || p->head_gen == 0xFFFFFFFFull) {
-        if (!p->head.p) p->head.alloc(p->n_keys * 8);
+        const bool first = !p->head.p;
+        if (first) p->head.alloc(p->n_keys * 8);
         JG_HIP(hipMemsetAsync(p->head.p, 0, p->n_keys * 8, p->ctx->stream));
         p->head_gen = 0;
+        // JANUS_TEST_HEAD_GEN: a new store's first generation (tests run batches across the wrap)
+        const char* e = first ? std::getenv("JANUS_TEST_HEAD_GEN") : nullptr;
+        if (e) p->head_gen = std::strtoull(e, nullptr, 10) & 0xFFFFFFFFull;
     }
     ++p->head_gen;
     if (p->next.bytes < n_rows * 4) {

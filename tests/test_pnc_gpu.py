@@ -81,6 +81,29 @@ def test_merge_indexed_unique_and_repeated_rows(ctx, eb, R):
     assert np.array_equal(P, eP) and np.array_equal(N, eN)
 
 
+def test_grouped_heads_across_the_generation_wrap(ctx, monkeypatch):
+    """Grouped-merge list heads carry the batch generation (gen << 32 | row); after 2^32 - 1 batches the heads
+    are cleared and the generation restarts.  A store whose first generation is set just below the wrap
+    (JANUS_TEST_HEAD_GEN) merges batches of repeated keys before, at and after it exactly."""
+    monkeypatch.setenv("JANUS_TEST_HEAD_GEN", str(2**32 - 3))
+    rng = np.random.default_rng(91)
+    n_keys, R, eb, M = 5000, 64, 8, 3000
+    AP, AN = random_pnc(rng, n_keys, R, eb, absent=False), random_pnc(rng, n_keys, R, eb, absent=False)
+    s = jg.PNCStore(ctx, n_keys, R, eb)
+    eP, eN = AP, AN
+    try:
+        s.write_rows(AP, AN)
+        for rnd in range(6):  # generations 2^32-2, 2^32-1, then 1, 2, 3, 4 after the clear
+            keys = rng.integers(0, 400 if rnd % 2 else n_keys, M).astype(np.uint32)
+            BP, BN = random_pnc(rng, M, R, eb), random_pnc(rng, M, R, eb)
+            s.merge_rows(BP, BN, keys)
+            eP, eN = orc.pnc_merge(eP, eN, BP, BN, keys)
+            P, N = s.read_rows()
+            assert np.array_equal(P, eP) and np.array_equal(N, eN), rnd
+    finally:
+        s.close()
+
+
 @pytest.mark.parametrize("eb", [4, 8])
 def test_merge_batch_device_rows(ctx, eb):
     rng = np.random.default_rng(21)
