@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 5
+#define JG_ABI_VERSION 6
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -248,6 +248,14 @@ int jg_orset_wave_abort(jg_orset* s);
 /* The element ids the last commit issued, sorted by (set, id): name i = bytes[off[i], off[i+1]) got id
  * id[i] in set set[i].  set / id / off / bytes NULL = size query (*n_names, *n_bytes). */
 int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes);
+/* The store's names log: every name the element table took, in the order it took them (commits and
+ * jg_orset_names_sync alike; never reordered, cleared names stay in it).  Names [from, *to) with *to = the
+ * log's length now: name i - from = bytes[off[i], off[i+1]) with id id[i] in set set[i] (the caller skips
+ * the ones it synced itself).  set / id / off / bytes NULL = size query (*to, *n_bytes).  A caller that only
+ * needs the ids when it next interns or reads a name pulls them then, several waves at once, instead of
+ * after every wave (jg_orset_wave_names) — the ORSetWorkload wave's ~0.7 ms of host copying leaves the
+ * apply loop (replaces nothing in the reference: its names live in the C# Dictionaries, ORSet.cs:83-88). */
+int jg_orset_names_since(jg_orset* s, uint64_t from, uint64_t* to, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes);
 /* One-shot: begin + append(all) + check, then commit(n) if every message is good; else nothing is
  * applied and the check's code is returned with *bad_msg (the jg_pnc_merge_json contract). */
 int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes, uint64_t* bad_msg);
@@ -380,9 +388,31 @@ int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_coun
 typedef struct jg_comm jg_comm;
 /* ncclGetUniqueId into id[128]: made by one rank and handed to the others over the caller's own channel. */
 int jg_comm_unique_id(uint8_t* id);
-/* ncclCommInitRank on ctx's device: blocks until all `world` ranks have joined with the same id. */
+/* A non-blocking RCCL communicator (ncclCommInitRankConfig, blocking = 0) on ctx's device: returns once all
+ * `world` ranks have joined with the same id, or JG_EHIP after JANUS_COMM_TIMEOUT_S seconds (default 120)
+ * with the half-made communicator aborted.  Every exchange on it polls against the same deadline: a rank that
+ * never posts its half, or an RCCL async error, aborts the communicator and returns JG_EHIP (every later
+ * call on it then fails at once) instead of hanging. */
 int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, jg_comm** out);
+/* The host transport: the same exchange with the counts and the runs moved by the caller's all-to-all-v over
+ * host memory — send holds the runs for peers 0..world-1 back to back (send_bytes[p] each), recv receives
+ * the peers' runs back to back (recv_bytes[p] each, known in advance); returns 0 on success.  For ranks that
+ * RCCL cannot serve (several ranks on one GPU, or shards moved over the caller's own links). */
+typedef int (*jg_alltoallv_fn)(void* user, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes);
+int jg_comm_init_host(jg_ctx* ctx, uint32_t rank, uint32_t world, jg_alltoallv_fn fn, void* user, jg_comm** out);
 int jg_comm_destroy(jg_comm* comm);
+/* The exchange's plan (pure host arithmetic, what every exchange call follows): counts[(src * world + dst) * k
+ * + j] = records source src routes to destination dst in buffer j (the all-gathered route counts).  For this
+ * rank and each peer p, buffer j (index p * k + j): send[send_off .. + send_n) goes to p (the send buffer
+ * holds every destination's run in rank order) and recv[recv_off .. + recv_n) comes from p (the peers' runs
+ * back to back in source-rank order).  skip_own: the own run is neither sent nor received (the PN-Counter
+ * exchange merges it from the send buffer).  world <= 64. */
+int jg_exchange_plan(uint32_t rank, uint32_t world, uint32_t k, const uint64_t* counts, uint8_t skip_own, uint64_t* send_off, uint64_t* send_n,
+                     uint64_t* recv_off, uint64_t* recv_n);
+/* The one owner rule (SafeCRDTManager.cs:136's routing, sharded): a key registered by the rank
+ * jg_shard_of(uid, world) names as its owner, with that rank's local index `local`, has the global key
+ * local * world + owner — the id the exchange routes by (owner = global % world, local = global / world). */
+int jg_global_key(const jg_guid* uid, uint32_t world, uint32_t local, uint32_t* global);
 /* PNCounter.Merge (PNCounters.cs:131-144) of a received batch on the owners of its keys: rows is this
  * rank's batch in GLOBAL keys (row key k goes to rank k % world as local key k / world), store this
  * rank's shard (rows NULL: this rank sends nothing).  sent[world] / received[world] (optional): rows per

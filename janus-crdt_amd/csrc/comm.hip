@@ -1,61 +1,232 @@
-// comm.hip — the cross-shard exchange inside the library, over RCCL.
+// comm.hip — the cross-shard exchange inside the library.
 //
-// The keyspace of a node is sharded over its GPUs, one process per GPU (csrc/route.hip: global key k
-// belongs to rank k % world, where it is local key k / world).  A received batch that lands on a rank that
-// does not own all of its keys still has to reach PNCounter.Merge (MergeSharp/MergeSharp/CRDTs/
-// PNCounters.cs:131-144) / ORSet.Merge (ORSet.cs:253-283) on each key's owner.  One call does it all on the
-// context's stream:
+// The keyspace of a node is sharded over its GPUs, one process per GPU (jg_internal.hpp's owner rule:
+// global key k belongs to rank owner_of_key(k) = k % world, where it is local key k / world).  A received
+// batch that lands on a rank that does not own all of its keys still has to reach PNCounter.Merge
+// (MergeSharp/MergeSharp/CRDTs/PNCounters.cs:131-144) / ORSet.Merge (ORSet.cs:253-283) on each key's
+// owner — the routing the reference does by uid lookup on every receiver (safeCRDTsIndexedByuid[u.uid],
+// BFT-CRDT/CRDTManagers/SafeCRDTManager.cs:136, fed by ConnectionManager.ReceivedBlock,
+// BFT-CRDT/Network/DAGConnectionManager.cs:40-50).  One call does it all on the context's stream:
 //
 //   route     the stable partition by owner (k_route_hist / k_route_scan / k_route_scatter) into the
 //             communicator's send buffers; per-destination counts to the host
-//   counts    ncclAllGather of every rank's count vector (world^2 words): each rank learns what every
-//             source sends it and sizes its receive buffers
-//   runs      one ncclGroupStart/End holding an ncclSend + ncclRecv per peer and buffer — RCCL over the
-//             xGMI peer links; this rank's own run is a device-to-device copy into its place
+//   counts    an all-gather of every rank's count vector (world^2 words): each rank learns what every
+//             source sends it
+//   plan      jg_exchange_plan (host, pure): every peer's send run and receive slot per buffer
+//   runs      one group of send + receive per peer and buffer; this rank's own run by a device copy
 //   merge     the received runs, in source-rank order, merged from device memory (jg_pnc_merge_device's
-//             scatter-max / jg_orset_merge_device's run unions)
+//             grouped fold / jg_orset_merge_device's run unions)
+//
+// Two transports carry the counts and the runs:
+//   RCCL      (jg_comm_init) ncclAllGather + grouped ncclSend / ncclRecv over the xGMI peer links.  The
+//             communicator is NON-BLOCKING (ncclConfig_t.blocking = 0): init, every group and every wait
+//             for the stream poll ncclCommGetAsyncError against a deadline (JANUS_COMM_TIMEOUT_S, default
+//             120 s); past it the communicator is aborted (ncclCommAbort) and the call returns JG_EHIP
+//             instead of hanging — a peer that never joins or dies mid-exchange costs a bounded wait.
+//   host      (jg_comm_init_host) the caller's all-to-all-v callback over page-locked host memory: the same
+//             route / plan / merge code at world > 1 where RCCL cannot run (RCCL refuses two ranks on one
+//             GPU), e.g. ranks sharing a device in a test, or a caller that moves shards over its own links.
 //
 // The 128-byte ncclUniqueId is created by one rank (jg_comm_unique_id) and handed to the others by the
 // caller over whatever channel it already has (the C# node's TCP links, torch.distributed in the bench).
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "jg_internal.hpp"
 
-#define JG_NCCL(call)                                                                                             \
-    do {                                                                                                          \
-        ncclResult_t r_ = (call);                                                                                 \
-        if (r_ != ncclSuccess) ::jg::fail(JG_EHIP, "%s failed: %s (%s:%d)", #call, ncclGetErrorString(r_), __FILE__, \
-                                          __LINE__);                                                              \
-    } while (0)
-
 static_assert(sizeof(ncclUniqueId) == 128, "the ABI passes the unique id as 128 bytes");
+
+// Abort of a hung RCCL communicator from outside the blocked call (ncclCommAbort is meant to be called from
+// another thread to stop uncompleted operations): armed for the duration of every exchange on the RCCL
+// transport, it aborts the communicator when the deadline passes and the call is still in RCCL.
+struct Watchdog {
+    std::mutex m;
+    std::condition_variable cv;
+    std::chrono::steady_clock::time_point until{};
+    bool armed = false, quit = false, fired = false;
+    std::thread th;
+};
 
 struct jg_comm {
     jg_ctx* ctx = nullptr;
-    ncclComm_t nc = nullptr;
+    ncclComm_t nc = nullptr;               // RCCL transport (nullptr: host transport, or aborted)
+    std::mutex abort_mu;                   // one abort, from the call's thread or the watchdog
+    std::unique_ptr<Watchdog> dog;
+    jg_alltoallv_fn host_fn = nullptr;     // host transport
+    void* host_user = nullptr;
+    bool rccl = false;                     // the RCCL transport (else the host transport)
+    std::atomic<bool> broken{false};       // aborted after a timeout / async error: every call fails
     uint32_t rank = 0, world = 1;
+    double timeout_s = 120;
     jg::DevBuf dcounts;                    // [world] mine, then [world x world] gathered
     jg::DevBuf sbuf[6], rbuf[6];           // route output / receive buffers (PN-Counter uses 0..2)
     std::vector<uint64_t> hcounts;
+    uint8_t* pin = nullptr;                // host transport staging (page-locked)
+    size_t pin_cap = 0;
     jg_exchange_stats stats{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     ~jg_comm() {
+        if (dog) {
+            {
+                std::lock_guard<std::mutex> g(dog->m);
+                dog->quit = true;
+            }
+            dog->cv.notify_all();
+            if (dog->th.joinable()) dog->th.join();
+        }
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
-        if (nc) (void)ncclCommDestroy(nc);
+        if (pin) (void)hipHostFree(pin);
     }
 };
 
 namespace {
 
+using Clock = std::chrono::steady_clock;
+
+#define JG_NCCL(c, call) nccl_check((c), (call), #call, __LINE__)
+
+bool trace_comm() {
+    static const bool t = std::getenv("JANUS_TRACE_COMM") != nullptr;
+    return t;
+}
+
+void abort_comm(jg_comm* c) {
+    std::lock_guard<std::mutex> g(c->abort_mu);
+    if (c->broken) return;
+    if (trace_comm()) std::fprintf(stderr, "jg_comm: aborting the communicator\n");
+    c->broken = true;
+    if (c->nc) (void)ncclCommAbort(c->nc);  // c->nc stays set: the handle is dead, c->broken says so
+    if (trace_comm()) std::fprintf(stderr, "jg_comm: aborted\n");
+}
+
+void start_watchdog(jg_comm* c) {
+    c->dog = std::make_unique<Watchdog>();
+    Watchdog* d = c->dog.get();
+    const int dev = c->ctx->device;
+    d->th = std::thread([c, d, dev] {
+        (void)hipSetDevice(dev);
+        std::unique_lock<std::mutex> lk(d->m);
+        for (;;) {
+            d->cv.wait(lk, [d] { return d->quit || d->armed; });
+            if (d->quit) return;
+            if (d->cv.wait_until(lk, d->until, [d] { return d->quit || !d->armed; })) {
+                if (d->quit) return;
+                continue;  // disarmed in time
+            }
+            d->fired = true;
+            d->armed = false;
+            lk.unlock();
+            abort_comm(c);  // the blocked RCCL call returns with an error; the call reports the timeout
+            lk.lock();
+        }
+    });
+}
+
+// Arms the watchdog for one exchange on the RCCL transport (no-op for the host transport).
+struct Armed {
+    jg_comm* c;
+    explicit Armed(jg_comm* cc) : c(cc) {
+        if (!c->dog) return;
+        std::lock_guard<std::mutex> g(c->dog->m);
+        c->dog->fired = false;
+        c->dog->until = std::chrono::steady_clock::now() + std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(c->timeout_s));
+        c->dog->armed = true;
+        c->dog->cv.notify_all();
+    }
+    ~Armed() {
+        if (!c->dog) return;
+        std::lock_guard<std::mutex> g(c->dog->m);
+        c->dog->armed = false;
+        c->dog->cv.notify_all();
+    }
+};
+
+// Poll the communicator until no operation is in progress (non-blocking RCCL), against the deadline.
+void nccl_settle(jg_comm* c, const char* what, int line) {
+    const auto end = Clock::now() + std::chrono::duration<double>(c->timeout_s);
+    for (;;) {
+        ncclResult_t a = ncclSuccess;
+        const ncclResult_t q = ncclCommGetAsyncError(c->nc, &a);
+        if (q != ncclSuccess) a = q;
+        if (a == ncclSuccess) return;
+        if (a != ncclInProgress) {
+            abort_comm(c);
+            jg::fail(JG_EHIP, "%s failed: %s (comm.hip:%d); the communicator was aborted", what, ncclGetErrorString(a), line);
+        }
+        if (Clock::now() > end) {
+            abort_comm(c);
+            jg::fail(JG_EHIP, "%s: no progress in %.0f s (a rank missing or stuck, comm.hip:%d); the communicator was aborted", what, c->timeout_s,
+                     line);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+void nccl_check(jg_comm* c, ncclResult_t r, const char* what, int line) {
+    if (r == ncclSuccess && !c->broken) return;
+    if (r == ncclInProgress && !c->broken) return nccl_settle(c, what, line);
+    const bool timed_out = c->broken;
+    abort_comm(c);
+    if (timed_out)
+        jg::fail(JG_EHIP, "%s: no progress in %.0f s (a rank missing or stuck, comm.hip:%d); the communicator was aborted", what, c->timeout_s, line);
+    jg::fail(JG_EHIP, "%s failed: %s (comm.hip:%d); the communicator was aborted", what, ncclGetErrorString(r), line);
+}
+
+// The context's stream drained: with RCCL work queued on it, polled against the deadline (a peer that never
+// posts its half of a send / receive leaves the RCCL kernel waiting forever; hipStreamSynchronize would too).
+void wait_stream(jg_comm* c) {
+    jg_ctx* ctx = c->ctx;
+    if (!c->rccl) {
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        return;
+    }
+    const auto end = Clock::now() + std::chrono::duration<double>(c->timeout_s);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(ctx->stream);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) JG_HIP(e);
+        JG_REQUIRE(!c->broken, JG_EHIP, "exchange: no progress in %.0f s (a rank missing or stuck); the communicator was aborted", c->timeout_s);
+        ncclResult_t a = ncclSuccess;
+        (void)ncclCommGetAsyncError(c->nc, &a);
+        if (a != ncclSuccess && a != ncclInProgress) {
+            abort_comm(c);
+            jg::fail(JG_EHIP, "exchange: RCCL reported %s; the communicator was aborted", ncclGetErrorString(a));
+        }
+        if (Clock::now() > end) {
+            abort_comm(c);
+            jg::fail(JG_EHIP, "exchange: the collective did not finish in %.0f s (a rank missing or stuck); the communicator was aborted",
+                     c->timeout_s);
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 void ensure(jg::DevBuf& b, size_t bytes) {
     if (b.bytes < bytes) b.alloc(bytes + bytes / 4 + 256);
+}
+
+uint8_t* pinned(jg_comm* c, size_t bytes) {
+    if (c->pin_cap < bytes) {
+        if (c->pin) JG_HIP(hipHostFree(c->pin));
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        void* p = nullptr;
+        JG_HIP(hipHostMalloc(&p, bytes + bytes / 4 + 256, hipHostMallocDefault));
+        c->pin = static_cast<uint8_t*>(p);
+        c->pin_cap = bytes + bytes / 4 + 256;
+    }
+    return c->pin;
 }
 
 // Re-raise the error a nested entry point of this library left in the thread's message.
@@ -66,43 +237,96 @@ void check_rc(int rc) {
     jg::fail(rc, "%s", msg);
 }
 
-// Every rank's per-destination counts (k words per destination) -> recv[src * k + j] = what src sends
-// this rank; the all-gather runs on the context's stream and the call waits for it.
-void gather_counts(jg_comm* c, const uint64_t* send, uint32_t k, std::vector<uint64_t>& recv) {
-    jg_ctx* ctx = c->ctx;
-    const uint32_t W = c->world;
-    ensure(c->dcounts, (size_t)(W + (size_t)W * W) * k * 8);
-    auto* mine = c->dcounts.as<uint64_t>();
-    auto* all = mine + (size_t)W * k;
-    JG_HIP(hipMemcpyAsync(mine, send, (size_t)W * k * 8, hipMemcpyHostToDevice, ctx->stream));
-    JG_NCCL(ncclAllGather(mine, all, (size_t)W * k, ncclUint64, c->nc, ctx->stream));
-    c->hcounts.resize((size_t)W * W * k);
-    JG_HIP(hipMemcpyAsync(c->hcounts.data(), all, c->hcounts.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
-    recv.assign((size_t)W * k, 0);
-    for (uint32_t src = 0; src < W; ++src)
-        for (uint32_t j = 0; j < k; ++j) recv[(size_t)src * k + j] = c->hcounts[((size_t)src * W + c->rank) * k + j];
+void host_xfer(jg_comm* c, const void* send, const uint64_t* sb, void* recv, const uint64_t* rb) {
+    const int r = c->host_fn(c->host_user, send, sb, recv, rb);
+    JG_REQUIRE(r == 0, JG_EHIP, "exchange: the host transport's all-to-all returned %d", r);
 }
 
-// Buffer b of element size `es` per record: the runs sent (grouped by destination, counts `sc`) and received
-// (grouped by source, counts `rc`), exchanged in the caller's open group.  `layout` (default sc) gives the
-// send buffer's run sizes when sc leaves a run out (a zero count: not sent, not copied).
-void post_runs(jg_comm* c, const char* send, char* recv, size_t es, const uint64_t* sc, const uint64_t* rc, uint32_t stride,
-               const uint64_t* layout = nullptr) {
+// Every rank's per-destination counts (k words per destination) -> all[src][dst][j] (src-major, world^2 k
+// words): what every source sends every destination.  The call waits for it.
+void gather_counts(jg_comm* c, const uint64_t* send, uint32_t k, std::vector<uint64_t>& all) {
     jg_ctx* ctx = c->ctx;
-    if (!layout) layout = sc;
-    uint64_t so = 0, ro = 0;
-    for (uint32_t p = 0; p < c->world; ++p) {
-        const uint64_t ns = sc[(size_t)p * stride], nr = rc[(size_t)p * stride];
-        if (p == c->rank) {
-            if (ns) JG_HIP(hipMemcpyAsync(recv + ro * es, send + so * es, ns * es, hipMemcpyDeviceToDevice, ctx->stream));
-        } else {
-            if (ns) JG_NCCL(ncclSend(send + so * es, ns * es, ncclUint8, (int)p, c->nc, ctx->stream));
-            if (nr) JG_NCCL(ncclRecv(recv + ro * es, nr * es, ncclUint8, (int)p, c->nc, ctx->stream));
-        }
-        so += layout[(size_t)p * stride];
-        ro += nr;
+    const uint32_t W = c->world;
+    all.resize((size_t)W * W * k);
+    if (c->host_fn) {  // an all-to-all-v carrying this rank's whole vector to every peer
+        std::vector<uint64_t> out((size_t)W * W * k), sb(W, (uint64_t)W * k * 8), rb(W, (uint64_t)W * k * 8);
+        for (uint32_t p = 0; p < W; ++p) std::memcpy(out.data() + (size_t)p * W * k, send, (size_t)W * k * 8);
+        host_xfer(c, out.data(), sb.data(), all.data(), rb.data());
+        return;
     }
+    ensure(c->dcounts, (size_t)(W + (size_t)W * W) * k * 8);
+    auto* mine = c->dcounts.as<uint64_t>();
+    auto* dall = mine + (size_t)W * k;
+    JG_HIP(hipMemcpyAsync(mine, send, (size_t)W * k * 8, hipMemcpyHostToDevice, ctx->stream));
+    JG_NCCL(c, ncclAllGather(mine, dall, (size_t)W * k, ncclUint64, c->nc, ctx->stream));
+    c->hcounts.resize(all.size());
+    JG_HIP(hipMemcpyAsync(c->hcounts.data(), dall, c->hcounts.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    wait_stream(c);
+    all = c->hcounts;
+}
+
+struct Plan {
+    std::vector<uint64_t> send_off, send_n, recv_off, recv_n;  // [world x k]: peer p, buffer j at p * k + j
+};
+
+Plan plan_of(jg_comm* c, const std::vector<uint64_t>& all, uint32_t k, bool skip_own) {
+    Plan pl;
+    const uint32_t W = c->world;
+    for (auto* v : {&pl.send_off, &pl.send_n, &pl.recv_off, &pl.recv_n}) v->resize((size_t)W * k);
+    check_rc(jg_exchange_plan(c->rank, W, k, all.data(), skip_own ? 1 : 0, pl.send_off.data(), pl.send_n.data(), pl.recv_off.data(),
+                              pl.recv_n.data()));
+    return pl;
+}
+
+// Buffer j's runs (element size es): peer p gets send[send_off .. + send_n) and this rank receives
+// recv[recv_off .. + recv_n) from it; the own run (p == rank) moves by a device copy.  RCCL: posted into the
+// caller's open group.  Host transport: staged through page-locked memory around one all-to-all-v.
+void post_runs(jg_comm* c, const Plan& pl, uint32_t k, uint32_t j, const char* send, char* recv, size_t es) {
+    jg_ctx* ctx = c->ctx;
+    const uint32_t W = c->world;
+    for (uint32_t p = 0; p < W; ++p) {
+        const size_t x = (size_t)p * k + j;
+        if (p == c->rank) {
+            JG_REQUIRE(pl.send_n[x] == pl.recv_n[x], JG_EHIP, "exchange plan: own run %llu sent, %llu received", (unsigned long long)pl.send_n[x],
+                       (unsigned long long)pl.recv_n[x]);
+            if (pl.send_n[x])
+                JG_HIP(hipMemcpyAsync(recv + pl.recv_off[x] * es, send + pl.send_off[x] * es, pl.send_n[x] * es, hipMemcpyDeviceToDevice, ctx->stream));
+        } else if (c->rccl) {
+            if (pl.send_n[x]) JG_NCCL(c, ncclSend(send + pl.send_off[x] * es, pl.send_n[x] * es, ncclUint8, (int)p, c->nc, ctx->stream));
+            if (pl.recv_n[x]) JG_NCCL(c, ncclRecv(recv + pl.recv_off[x] * es, pl.recv_n[x] * es, ncclUint8, (int)p, c->nc, ctx->stream));
+        }
+    }
+    if (c->rccl) return;
+    // host transport: peers' runs out through page-locked staging, one all-to-all-v, back in
+    std::vector<uint64_t> sb(W, 0), rb(W, 0);
+    uint64_t ts = 0, tr = 0;
+    for (uint32_t p = 0; p < W; ++p)
+        if (p != c->rank) sb[p] = pl.send_n[(size_t)p * k + j] * es, rb[p] = pl.recv_n[(size_t)p * k + j] * es, ts += sb[p], tr += rb[p];
+    uint8_t* h = pinned(c, ts + tr + 64);
+    uint8_t* hs = h;
+    uint8_t* hr = h + ((ts + 63) & ~63ull);
+    uint64_t o = 0;
+    for (uint32_t p = 0; p < W; ++p)
+        if (sb[p]) {
+            JG_HIP(hipMemcpyAsync(hs + o, send + pl.send_off[(size_t)p * k + j] * es, sb[p], hipMemcpyDeviceToHost, ctx->stream));
+            o += sb[p];
+        }
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    host_xfer(c, hs, sb.data(), hr, rb.data());
+    o = 0;
+    for (uint32_t p = 0; p < W; ++p)
+        if (rb[p]) {
+            JG_HIP(hipMemcpyAsync(recv + pl.recv_off[(size_t)p * k + j] * es, hr + o, rb[p], hipMemcpyHostToDevice, ctx->stream));
+            o += rb[p];
+        }
+    JG_HIP(hipStreamSynchronize(ctx->stream));  // the staging is reused by the next buffer
+}
+
+void group_start(jg_comm* c) {
+    if (c->rccl) JG_NCCL(c, ncclGroupStart());
+}
+void group_end(jg_comm* c) {
+    if (c->rccl) JG_NCCL(c, ncclGroupEnd());
 }
 
 // JANUS_TEST_EXCHANGE_FULL=1: a one-rank communicator takes the whole route / all-gather / run path too
@@ -123,15 +347,53 @@ float elapsed_ms(jg_comm* c, int a, int b) {
     return ms;
 }
 
+double timeout_from_env() {
+    const char* e = std::getenv("JANUS_COMM_TIMEOUT_S");
+    const double t = e ? std::atof(e) : 120.0;
+    return t > 0 ? t : 120.0;
+}
+
+jg_comm* usable(jg_comm* c, const char* fn) {
+    JG_REQUIRE(c, JG_EINVAL, "%s: NULL communicator", fn);
+    JG_REQUIRE(!c->broken, JG_EHIP, "%s: the communicator was aborted by an earlier failure; destroy it and join a new one", fn);
+    return c;
+}
+
 }  // namespace
 
 extern "C" {
+
+int jg_exchange_plan(uint32_t rank, uint32_t world, uint32_t k, const uint64_t* counts, uint8_t skip_own, uint64_t* send_off, uint64_t* send_n,
+                     uint64_t* recv_off, uint64_t* recv_n) {
+    return jg::guard([&] {
+        JG_REQUIRE(counts && send_off && send_n && recv_off && recv_n, JG_EINVAL, "jg_exchange_plan: NULL argument");
+        JG_REQUIRE(world >= 1 && world <= 64 && rank < world && k >= 1, JG_EINVAL, "jg_exchange_plan: need rank < world <= 64, k >= 1");
+        const uint32_t W = world;
+        auto cnt = [&](uint32_t src, uint32_t dst, uint32_t j) { return counts[((size_t)src * W + dst) * k + j]; };
+        for (uint32_t j = 0; j < k; ++j) {
+            // send buffer j holds every destination's run, destinations in rank order (the route's stable
+            // partition); receive buffer j takes the peers' runs back to back in source-rank order
+            uint64_t so = 0, ro = 0;
+            for (uint32_t p = 0; p < W; ++p) {
+                const size_t x = (size_t)p * k + j;
+                const bool own_skipped = skip_own && p == rank;
+                send_off[x] = so;
+                send_n[x] = own_skipped ? 0 : cnt(rank, p, j);
+                recv_off[x] = ro;
+                recv_n[x] = own_skipped ? 0 : cnt(p, rank, j);
+                so += cnt(rank, p, j);
+                ro += recv_n[x];
+            }
+        }
+    });
+}
 
 int jg_comm_unique_id(uint8_t* id) {
     return jg::guard([&] {
         JG_REQUIRE(id, JG_EINVAL, "jg_comm_unique_id: NULL argument");
         ncclUniqueId u;
-        JG_NCCL(ncclGetUniqueId(&u));
+        const ncclResult_t r = ncclGetUniqueId(&u);
+        JG_REQUIRE(r == ncclSuccess, JG_EHIP, "ncclGetUniqueId failed: %s", ncclGetErrorString(r));
         std::memcpy(id, &u, sizeof u);
     });
 }
@@ -146,9 +408,69 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         c->ctx = ctx;
         c->rank = rank;
         c->world = world;
+        c->timeout_s = timeout_from_env();
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof u);
-        JG_NCCL(ncclCommInitRank(&c->nc, (int)world, u, (int)rank));
+        // The rendezvous waits for every rank inside ncclCommInitRank (this RCCL blocks there even for a
+        // non-blocking config), so it runs on a thread of its own and this call waits for it against the
+        // deadline.  A rank that never joins leaves that thread in the rendezvous: it is abandoned (it destroys
+        // a communicator that completes after all) and the call returns JG_EHIP.
+        struct Job {
+            std::mutex m;
+            std::condition_variable cv;
+            bool done = false, abandoned = false;
+            ncclResult_t r = ncclSuccess;
+            ncclComm_t nc = nullptr;
+        };
+        auto job = std::make_shared<Job>();
+        const int dev = ctx->device;
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRank (rank %u of %u)\n", rank, world);
+        std::thread([job, u, rank, world, dev] {
+            (void)hipSetDevice(dev);
+            ncclComm_t nc = nullptr;
+            const ncclResult_t r = ncclCommInitRank(&nc, (int)world, u, (int)rank);
+            std::lock_guard<std::mutex> g(job->m);
+            if (job->abandoned) {
+                if (nc) (void)ncclCommAbort(nc);
+                return;
+            }
+            job->r = r;
+            job->nc = nc;
+            job->done = true;
+            job->cv.notify_all();
+        }).detach();
+        {
+            std::unique_lock<std::mutex> g(job->m);
+            const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(c->timeout_s));
+            if (!job->cv.wait_until(g, end, [&] { return job->done; })) {
+                job->abandoned = true;
+                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous timed out\n");
+                jg::fail(JG_EHIP, "jg_comm_init: not every rank joined in %.0f s (rank %u of %u); JANUS_COMM_TIMEOUT_S sets the wait", c->timeout_s,
+                         rank, world);
+            }
+        }
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRank returned %s\n", ncclGetErrorString(job->r));
+        JG_REQUIRE(job->r == ncclSuccess, JG_EHIP, "ncclCommInitRank failed: %s", ncclGetErrorString(job->r));
+        c->nc = job->nc;
+        c->rccl = true;
+        start_watchdog(c.get());
+        *out = c.release();
+    });
+}
+
+int jg_comm_init_host(jg_ctx* ctx, uint32_t rank, uint32_t world, jg_alltoallv_fn fn, void* user, jg_comm** out) {
+    return jg::guard([&] {
+        JG_REQUIRE(ctx && fn && out, JG_EINVAL, "jg_comm_init_host: NULL argument");
+        JG_REQUIRE(world >= 1 && world <= 64 && rank < world, JG_EINVAL, "jg_comm_init_host: need rank < world <= 64 (rank %u, world %u)", rank,
+                   world);
+        auto lk_ = jg::lock(ctx);
+        jg::ensure_device(ctx);
+        auto c = std::make_unique<jg_comm>();
+        c->ctx = ctx;
+        c->rank = rank;
+        c->world = world;
+        c->host_fn = fn;
+        c->host_user = user;
         *out = c.release();
     });
 }
@@ -156,10 +478,17 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
 int jg_comm_destroy(jg_comm* c) {
     return jg::guard([&] {
         if (!c) return;
+        std::unique_ptr<jg_comm> own(c);
         auto lk_ = jg::lock(c->ctx);
         jg::ensure_device(c->ctx);
-        JG_HIP(hipStreamSynchronize(c->ctx->stream));
-        delete c;
+        if (c->broken) return;  // aborted: its queued work was cancelled with it
+        Armed armed_(c);
+        wait_stream(c);
+        if (c->nc && !c->broken) {
+            const ncclResult_t r = ncclCommDestroy(c->nc);
+            if (r == ncclInProgress) nccl_settle(c, "ncclCommDestroy", __LINE__);
+            c->nc = nullptr;
+        }
     });
 }
 
@@ -173,7 +502,8 @@ int jg_comm_last_stats(jg_comm* c, jg_exchange_stats* out) {
 
 int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* sent, uint64_t* received) {
     return jg::guard([&] {
-        JG_REQUIRE(c && store, JG_EINVAL, "jg_pnc_exchange: NULL argument");
+        usable(c, "jg_pnc_exchange");
+        JG_REQUIRE(store, JG_EINVAL, "jg_pnc_exchange: NULL argument");
         JG_REQUIRE(store->ctx == c->ctx && (!rows || rows->ctx == c->ctx), JG_EINVAL,
                    "jg_pnc_exchange: the store and the batch must be on the communicator's context");
         JG_REQUIRE(!rows || (store->R == rows->R && store->eb == rows->eb), JG_EINVAL,
@@ -194,52 +524,51 @@ int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* se
             if (received) received[0] = n;
             return;
         }
+        Armed armed_(c);  // RCCL: a call stuck past the deadline is aborted from the watchdog
         ensure(c->sbuf[0], n * 4 + 16);
         ensure(c->sbuf[1], n * rb + 16);
         ensure(c->sbuf[2], n * rb + 16);
         JG_HIP(hipEventRecord(event(c, 0), ctx->stream));
-        std::vector<uint64_t> sc(W), rc;
+        std::vector<uint64_t> sc(W, 0), all;
         if (rows) check_rc(jg_rows_route(rows, W, sc.data(), c->sbuf[0].p, c->sbuf[1].p, c->sbuf[2].p, n));
         JG_HIP(hipEventRecord(event(c, 1), ctx->stream));
-        gather_counts(c, sc.data(), 1, rc);
-        // max is order-free: this rank's own run merges straight from the send buffers, the peers' runs
-        // land back to back in the receive buffers (rc with the own entry zeroed)
-        const uint64_t own = sc[c->rank];
-        uint64_t own_at = 0;
-        for (uint32_t p = 0; p < c->rank; ++p) own_at += sc[p];
-        std::vector<uint64_t> sc2 = sc, rc2 = rc;
-        sc2[c->rank] = rc2[c->rank] = 0;
+        gather_counts(c, sc.data(), 1, all);
+        // max is order-free: this rank's own run merges straight from the send buffers (skip_own), the peers'
+        // runs land back to back in the receive buffers
+        const Plan pl = plan_of(c, all, 1, true);
+        const uint64_t own = sc[c->rank], own_at = pl.send_off[c->rank];
         uint64_t nr = 0;
-        for (uint64_t x : rc2) nr += x;
+        for (uint32_t p = 0; p < W; ++p) nr += pl.recv_n[p];
         ensure(c->rbuf[0], nr * 4 + 16);
         ensure(c->rbuf[1], nr * rb + 16);
         ensure(c->rbuf[2], nr * rb + 16);
-        JG_NCCL(ncclGroupStart());
-        post_runs(c, c->sbuf[0].as<char>(), c->rbuf[0].as<char>(), 4, sc2.data(), rc2.data(), 1, sc.data());
-        post_runs(c, c->sbuf[1].as<char>(), c->rbuf[1].as<char>(), rb, sc2.data(), rc2.data(), 1, sc.data());
-        post_runs(c, c->sbuf[2].as<char>(), c->rbuf[2].as<char>(), rb, sc2.data(), rc2.data(), 1, sc.data());
-        JG_NCCL(ncclGroupEnd());
+        const size_t es[3] = {4, rb, rb};
+        group_start(c);
+        for (uint32_t b = 0; b < 3; ++b) post_runs(c, pl, 1, 0, c->sbuf[b].as<char>(), c->rbuf[b].as<char>(), es[b]);
+        group_end(c);
         JG_HIP(hipEventRecord(event(c, 2), ctx->stream));
+        if (c->rccl) wait_stream(c);  // RCCL: the runs are in before the merges' own host syncs (bounded wait)
         if (own)
             check_rc(jg_pnc_merge_device(store, own, c->sbuf[0].as<char>() + own_at * 4, c->sbuf[1].as<char>() + own_at * rb,
                                          c->sbuf[2].as<char>() + own_at * rb));
         if (nr) check_rc(jg_pnc_merge_device(store, nr, c->rbuf[0].p, c->rbuf[1].p, c->rbuf[2].p));
-        nr += own;
         JG_HIP(hipEventRecord(event(c, 3), ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        wait_stream(c);
         uint64_t off_rank = 0;
-        for (uint32_t p = 0; p < W; ++p) off_rank += p == c->rank ? 0 : sc[p];
+        for (uint32_t p = 0; p < W; ++p) off_rank += pl.send_n[p];
         c->stats = jg_exchange_stats{elapsed_ms(c, 0, 1) * 1e-3, elapsed_ms(c, 1, 2) * 1e-3, elapsed_ms(c, 2, 3) * 1e-3, off_rank * (4 + 2 * rb),
-                                     (nr - own) * (4 + 2 * rb), nr};
+                                     nr * (4 + 2 * rb), nr + own};
         if (sent) std::copy(sc.begin(), sc.end(), sent);
-        if (received) std::copy(rc.begin(), rc.end(), received);
+        if (received)
+            for (uint32_t p = 0; p < W; ++p) received[p] = all[(size_t)p * W + c->rank];
     });
 }
 
 int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t* sent_add, uint64_t* sent_rem, uint64_t* recv_add,
                       uint64_t* recv_rem) {
     return jg::guard([&] {
-        JG_REQUIRE(c && store && received, JG_EINVAL, "jg_orset_exchange: NULL argument");
+        usable(c, "jg_orset_exchange");
+        JG_REQUIRE(store && received, JG_EINVAL, "jg_orset_exchange: NULL argument");
         JG_REQUIRE(store->ctx == c->ctx && received->ctx == c->ctx, JG_EINVAL, "jg_orset_exchange: the stores must be on the communicator's context");
         JG_REQUIRE(store != received, JG_EINVAL, "jg_orset_exchange: the received state cannot be the store itself");
         auto lk_ = jg::lock(c->ctx);
@@ -260,6 +589,7 @@ int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t*
             if (recv_rem) recv_rem[0] = nrm;
             return;
         }
+        Armed armed_(c);  // RCCL: a call stuck past the deadline is aborted from the watchdog
         const size_t es[6] = {8, 16, 4, 8, 16, 4};  // key, tag, ord of the add stream, then of the tombstones
         for (int i = 0; i < 6; ++i) ensure(c->sbuf[i], (i < 3 ? na : nrm) * es[i] + 16);
         JG_HIP(hipEventRecord(event(c, 0), ctx->stream));
@@ -267,22 +597,25 @@ int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t*
         check_rc(jg_orset_route(received, W, sa.data(), sr.data(), c->sbuf[0].p, c->sbuf[1].p, c->sbuf[2].p, na, c->sbuf[3].p, c->sbuf[4].p,
                                 c->sbuf[5].p, nrm));
         JG_HIP(hipEventRecord(event(c, 1), ctx->stream));
-        std::vector<uint64_t> sc(2 * (size_t)W), rc;
+        std::vector<uint64_t> sc(2 * (size_t)W), all;
         for (uint32_t p = 0; p < W; ++p) sc[2 * p] = sa[p], sc[2 * p + 1] = sr[p];
-        gather_counts(c, sc.data(), 2, rc);
+        gather_counts(c, sc.data(), 2, all);
+        // the union keeps source-rank order (arrival ordinals), so the own run takes its place among the
+        // received ones (no skip)
+        const Plan pl = plan_of(c, all, 2, false);
         std::vector<uint64_t> ra(W), rr(W);
         uint64_t ta = 0, tr = 0;
-        for (uint32_t p = 0; p < W; ++p) ra[p] = rc[2 * p], rr[p] = rc[2 * p + 1], ta += ra[p], tr += rr[p];
+        for (uint32_t p = 0; p < W; ++p) ra[p] = pl.recv_n[2 * p], rr[p] = pl.recv_n[2 * p + 1], ta += ra[p], tr += rr[p];
         for (int i = 0; i < 6; ++i) ensure(c->rbuf[i], (i < 3 ? ta : tr) * es[i] + 16);
-        JG_NCCL(ncclGroupStart());
-        for (int i = 0; i < 6; ++i)
-            post_runs(c, c->sbuf[i].as<char>(), c->rbuf[i].as<char>(), es[i], sc.data() + (i < 3 ? 0 : 1), rc.data() + (i < 3 ? 0 : 1), 2);
-        JG_NCCL(ncclGroupEnd());
+        group_start(c);
+        for (int i = 0; i < 6; ++i) post_runs(c, pl, 2, i < 3 ? 0 : 1, c->sbuf[i].as<char>(), c->rbuf[i].as<char>(), es[i]);
+        group_end(c);
         JG_HIP(hipEventRecord(event(c, 2), ctx->stream));
+        if (c->rccl) wait_stream(c);  // RCCL: the runs are in before the merge's host reads (bounded wait)
         check_rc(jg_orset_merge_device(store, W, ra.data(), rr.data(), c->rbuf[0].p, c->rbuf[1].p, c->rbuf[2].p, c->rbuf[3].p, c->rbuf[4].p,
                                        c->rbuf[5].p));
         JG_HIP(hipEventRecord(event(c, 3), ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        wait_stream(c);
         constexpr uint64_t kRec = 28;  // key + tag + ord
         uint64_t out = 0;
         for (uint32_t p = 0; p < W; ++p) out += p == c->rank ? 0 : sa[p] + sr[p];

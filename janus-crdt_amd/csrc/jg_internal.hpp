@@ -18,6 +18,24 @@ namespace jg {
 // passes run over the same uploaded wave and skip each other's messages.
 constexpr uint32_t kSkipIdx = 0xFFFFFFFFu;
 
+// ---- the one owner rule of a sharded node -------------------
+// A key uid belongs to rank shard_of_uid(uid, world) (the apply loop's shard shortcut, jg_shard_of); its
+// global key (PN-Counter row / OR-Set set id in the node's key space) is local x world + owner
+// (jg_global_key), so the exchange's routing rule owner_of_key(global) = global % world (route.hip, comm.hip)
+// names the same rank, and the owner stores it as local key global / world.
+__host__ __device__ __forceinline__ uint64_t uid_hash(uint64_t lo, uint64_t hi) {
+    uint64_t x = lo ^ (hi * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 31;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 29;
+    return x;
+}
+__host__ __device__ __forceinline__ uint32_t shard_of_uid(uint64_t lo, uint64_t hi, uint32_t world) {
+    return world <= 1 ? 0u : (uint32_t)((uid_hash(lo, hi) >> 7) % world);
+}
+__host__ __device__ __forceinline__ uint32_t owner_of_key(uint64_t global_key, uint32_t world) { return (uint32_t)(global_key % world); }
+__host__ __device__ __forceinline__ uint64_t local_of_key(uint64_t global_key, uint32_t world) { return global_key / world; }
+
 // ---- errors ------------------------------------------------------------------------------------
 void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void clear_error();
@@ -180,8 +198,11 @@ void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling th
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 // After H2D copies queued on ctx->copy: make ctx->stream wait for them (stream order for the kernels
 // that read the uploaded chunk).  Callers keep the copy stream off buffers the compute stream may still
-// use: they synchronise ctx->stream before the first upload of a wave, and ctx->copy before
-// reallocating an upload target.
+// use: before a wave's first upload they record an event at the compute stream's tail (after every setup
+// launch of the wave) and make ctx->copy wait on it on the device (node.hip `drained`; the one-shot
+// jg_*_wave_append paths synchronise ctx->stream instead), and they synchronise ctx->copy before
+// reallocating an upload target (grow_keep) — the same rule covers the D2H copies of issued OR-Set names
+// that a commit queues on ctx->copy.
 void upload_done(jg_ctx* ctx);
 void sync_counts(jg_orset* s);   // fold a pending async count into the host copy
 // Dense chunk metadata for a stream whose n records sit contiguously in slots [0, n) (async).
@@ -196,6 +217,8 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
 uint64_t ord_span(jg_ctx* ctx, const uint32_t* ord, uint64_t n);
 // orset.hip: s = s ∪ src (both streams), synchronous, src's streams may be dense or chunked.
 void orset_merge_store(jg_orset* s, jg_orset* src);
+// orset.hip: room in the store's union targets for that many more records (no sync; skipped while counts are pending).
+void orset_reserve_union(jg_orset* s, uint64_t add_in, uint64_t rem_in);
 
 // Node waves (node.hip): one upload of every kind's messages; rows / mset = the message's row / set id
 // or kSkipIdx.  json.hip (PN-Counter):

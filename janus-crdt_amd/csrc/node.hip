@@ -59,16 +59,8 @@ static_assert(sizeof(UidSlot) == 32, "one uid slot = half a 64-B line");
 struct TrackSlot { unsigned long long key, origin; };
 struct Guid16 { unsigned long long lo, hi; };
 
-__host__ __device__ __forceinline__ uint64_t uid_hash(uint64_t lo, uint64_t hi) {
-    uint64_t x = lo ^ (hi * 0x9E3779B97F4A7C15ull);
-    x ^= x >> 31;
-    x *= 0xBF58476D1CE4E5B9ull;
-    x ^= x >> 29;
-    return x;
-}
-__host__ __device__ __forceinline__ uint32_t shard_of(uint64_t lo, uint64_t hi, uint32_t world) {
-    return world <= 1 ? 0u : (uint32_t)((uid_hash(lo, hi) >> 7) % world);
-}
+using jg::uid_hash;
+__host__ __device__ __forceinline__ uint32_t shard_of(uint64_t lo, uint64_t hi, uint32_t world) { return jg::shard_of_uid(lo, hi, world); }
 __host__ __device__ __forceinline__ uint64_t seq_hash(uint64_t x) {
     x ^= x >> 33;
     x *= 0xFF51AFD7ED558CCDull;
@@ -85,25 +77,40 @@ __global__ void k_uid_scatter(UidSlot* __restrict__ tab, const uint32_t* __restr
     if (i < n) tab[at[i]] = v[i];
 }
 
-// TryAdd of pending (identity, origin) pairs: an identity already present keeps its entry; *count += added.
+// TryAdd of pending (identity, origin) pairs, in add order: an identity already present keeps its entry,
+// and an identity added twice in one batch keeps the origin of its FIRST add (ConcurrentDictionary.TryAdd,
+// SafeCRDT.cs:55; ADVICE r03: whichever lane won the CAS used to keep its origin).  Pass 1 inserts the keys;
+// every pair whose slot is new in this batch (origin still 0: origins are never 0, jg_tracker_add) claims it
+// with atomicMin of its pair index in the slot's claim word (all 0xFFFFFFFF between waves); pass 2
+// (k_track_origin) lets the smallest index write the origin and resets the claim.  *count += added.
 __global__ __launch_bounds__(kBlock) void k_track_insert(DevTrack t, const unsigned long long* __restrict__ pairs, uint64_t n,
-                                                         unsigned long long* __restrict__ count) {
+                                                         uint32_t* __restrict__ slot_of, unsigned long long* __restrict__ count) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     bool added = false;
     if (i < n) {
         const unsigned long long k = pairs[2 * i];
+        uint32_t slot = kNoSlot;
         for (uint64_t s = seq_hash(k) & t.mask;; s = (s + 1) & t.mask) {
             unsigned long long w = t.tab[s].key;
             if (w == 0) {
                 w = atomicCAS(&t.tab[s].key, 0ull, k);
                 if (w == 0) {
-                    t.tab[s].origin = pairs[2 * i + 1];
                     added = true;
+                    slot = (uint32_t)s;
                     break;
                 }
             }
-            if (w == k) break;
+            if (w == k) {
+                slot = (uint32_t)s;
+                break;
+            }
         }
+        if (t.tab[slot].origin == 0) {  // new in this batch (an entry of an earlier batch has its origin)
+            atomicMin(&t.claim[slot], (uint32_t)i);
+        } else {
+            slot = kNoSlot;
+        }
+        slot_of[i] = slot;
     }
     __shared__ uint32_t c;
     if (threadIdx.x == 0) c = 0;
@@ -111,6 +118,15 @@ __global__ __launch_bounds__(kBlock) void k_track_insert(DevTrack t, const unsig
     if (added) atomicAdd(&c, 1u);
     __syncthreads();
     if (threadIdx.x == 0 && c) atomicAdd(count, (unsigned long long)c);
+}
+
+__global__ void k_track_origin(DevTrack t, const unsigned long long* __restrict__ pairs, const uint32_t* __restrict__ slot_of, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot_of[i];
+    if (s == kNoSlot || t.claim[s] != (uint32_t)i) return;
+    t.tab[s].origin = pairs[2 * i + 1];
+    t.claim[s] = 0xFFFFFFFFu;
 }
 
 // Live entries of the old table into the new one (tombstones dropped).
@@ -250,10 +266,17 @@ struct jg_tracker {
     jg_ctx* ctx;
     // jg_tracker_add runs on the callers' threads (SafeCRDT.Update), not under the context lock: it appends
     // (identity, origin) pairs to page-locked buffer `cur` under pend_mu; a flush uploads that buffer
-    // (async, stream-ordered before the wave's classify) and switches to the other one, whose own upload
-    // finished before the call that queued it returned (every call that flushes ends with a stream sync).
+    // (async, stream-ordered before the wave's classify), records the buffer's event after the copy and
+    // switches to the other one.  A buffer is written or reallocated only after its event completed (the
+    // first append after a switch waits on it): no call has to end with a stream sync for the pair of
+    // buffers to be safe (an empty wave returned after a flush without one).
     std::mutex pend_mu;
-    struct Pin { unsigned long long* p = nullptr; size_t cap = 0, n = 0; } pin[2];
+    struct Pin {
+        unsigned long long* p = nullptr;
+        size_t cap = 0, n = 0;
+        hipEvent_t up = nullptr;  // recorded after the buffer's last upload
+        bool wait = false;        // the upload may still be queued: wait on `up` before touching p
+    } pin[2];
     int cur = 0;
     jg::DevBuf tab, claim, count, dpairs;
     jg::DevBuf spare_tab, spare_claim;  // the other pair of a rebuild (tables are rebuilt into it, then swapped)
@@ -261,13 +284,20 @@ struct jg_tracker {
     uint64_t used = 0;  // live + tombstones, an upper bound (TryAdd of a present identity counted too)
 
     ~jg_tracker() {
-        for (Pin& b : pin)
+        for (Pin& b : pin) {
+            if (b.up) (void)hipEventSynchronize(b.up);
             if (b.p) (void)hipHostFree(b.p);
+            if (b.up) (void)hipEventDestroy(b.up);
+        }
     }
     DevTrack dev() const { return DevTrack{tab.as<TrackSlot>(), claim.as<uint32_t>(), cap ? cap - 1 : 0}; }
 
     void append(uint64_t n, const uint64_t* seq, const uint64_t* origin) {  // under pend_mu
         Pin& b = pin[cur];
+        if (b.wait) {  // its last upload (queued by the flush before the one that switched to it) must be done
+            JG_HIP(hipEventSynchronize(b.up));
+            b.wait = false;
+        }
         if (b.n + n > b.cap) {
             const size_t nc = std::max<size_t>({2 * b.cap, b.n + n, 4096});
             void* p = nullptr;
@@ -292,6 +322,7 @@ struct jg_tracker {
             b = &pin[cur];
             cur ^= 1;
             pin[cur].n = 0;
+            pin[cur].wait = pin[cur].up != nullptr;  // appends to it wait for its previous upload first
         }
         if (!count.p) {
             count.alloc(8);
@@ -324,10 +355,14 @@ struct jg_tracker {
             cap = ncap;
             used = live;
         }
-        ensure(dpairs, np * 16);
+        ensure(dpairs, np * 20);  // pairs, then each pair's slot
         JG_HIP(hipMemcpyAsync(dpairs.p, b->p, np * 16, hipMemcpyHostToDevice, ctx->stream));
-        hipLaunchKernelGGL(k_track_insert, dim3(blocks_for(np)), dim3(kBlock), 0, ctx->stream, dev(), dpairs.as<unsigned long long>(), np,
+        if (!b->up) JG_HIP(hipEventCreateWithFlags(&b->up, hipEventDisableTiming));
+        JG_HIP(hipEventRecord(b->up, ctx->stream));
+        auto* slot_of = reinterpret_cast<uint32_t*>(dpairs.as<char>() + np * 16);
+        hipLaunchKernelGGL(k_track_insert, dim3(blocks_for(np)), dim3(kBlock), 0, ctx->stream, dev(), dpairs.as<unsigned long long>(), np, slot_of,
                            count.as<unsigned long long>());
+        hipLaunchKernelGGL(k_track_origin, dim3(blocks_for(np)), dim3(kBlock), 0, ctx->stream, dev(), dpairs.as<unsigned long long>(), slot_of, np);
         JG_HIP(hipGetLastError());
         used += np;
     }
@@ -683,6 +718,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
 
     // the cut: the first state the reference's loop would throw at
     JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));  // the final phase's kernels start after the chunks'
+    double te[6] = {now_s()};
     uint64_t cut = nn;
     int code = JG_OK;
     std::string why;
@@ -701,6 +737,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             uint64_t bad = UINT64_MAX;
             std::string w2;
             const int rc = jg::orset_node_check(nd->orset, nn, b0, &bad, &w2);  // over the messages uploaded
+            te[1] = now_s();
             if (rc != JG_OK) {
                 if (bad == UINT64_MAX) jg::fail(rc, "%s", w2.c_str());
                 if (bad < cut) cut = bad, code = rc, why = w2;
@@ -717,8 +754,17 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
                 if (rc != JG_OK) jg::fail(JG_EHIP, "jg_apply: the prefix before message %llu failed again: %s", (unsigned long long)cut, w3.c_str());
             }
         }
+        te[2] = now_s();
         if (do_orset) jg::orset_node_commit(nd->orset, cut);
+        te[3] = now_s();
     } catch (...) {
+        // an internal failure past the chunk loop (a check that could not name a message, a prefix that failed
+        // again, a device error): the classified chunks' first-occurrence claims are released as in the loop's
+        // catch, or a stale claim below the next wave's index would keep that safe update from completing
+        // (ADVICE r03).  The OR-Set commit's one data-dependent failure (a set's element ids running out) is
+        // ruled out by orset_node_check before the PN-Counter commit, so what is left here is a device error.
+        if (dt.tab && nn) hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
+        (void)hipStreamSynchronize(ctx->stream);
         if (do_orset) jg::orset_node_abort(nd->orset);
         throw;
     }
@@ -763,6 +809,10 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     JG_HIP(hipMemcpyAsync(&applied, d_status + 2, 8, hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
     nd->stats.msgs_applied = applied;
+    te[4] = now_s();
+    if (trace)
+        std::fprintf(stderr, "apply tail: orset check %.0f us, pnc finish %.0f, orset commit %.0f, completions %.0f (after the loop's last upload: %.0f us host)\n",
+                     (te[1] - te[0]) * 1e6, (te[2] - te[1]) * 1e6, (te[3] - te[2]) * 1e6, (te[4] - te[3]) * 1e6, (te[4] - te[0]) * 1e6);
     double busy = 0;
     for (size_t k = 0; k <= n_ev; ++k) {
         float ms = 0;
@@ -865,6 +915,15 @@ int jg_shard_of(const jg_guid* uid, uint32_t world, uint32_t* rank) {
     return jg::guard([&] {
         JG_REQUIRE(uid && rank && world >= 1, JG_EINVAL, "jg_shard_of: bad argument");
         *rank = shard_of(uid->lo, uid->hi, world);
+    });
+}
+
+int jg_global_key(const jg_guid* uid, uint32_t world, uint32_t local, uint32_t* global) {
+    return jg::guard([&] {
+        JG_REQUIRE(uid && global && world >= 1, JG_EINVAL, "jg_global_key: bad argument");
+        const uint64_t g = (uint64_t)local * world + jg::shard_of_uid(uid->lo, uid->hi, world);
+        JG_REQUIRE(g < 0xFFFFFFF0ull, JG_EINVAL, "jg_global_key: local key %u x world %u leaves the 32-bit key space", local, world);
+        *global = (uint32_t)g;
     });
 }
 

@@ -658,16 +658,28 @@ void jg_stream_soa::reserve_records(uint64_t records) {
     // each in-place union: a growing stream takes twice what it needs, so it reallocates every few waves,
     // not every wave (hipFree + hipMalloc of the three arrays cost 0.24-0.88 ms of a 200k-state OR-Set wave,
     // JANUS_TRACE_MERGE)
-    if (cap_chunks) c = std::max<uint64_t>(2 * c, cap_chunks + cap_chunks / 2);
+    // (and on this device's HBM a small growing stream takes 4x what it needs: below 64M records the spare
+    // headroom costs < 8 GB, and each reallocation of the ORSetWorkload store cost ~2.3 ms of host time
+    // (hipMalloc + hipFree of the six arrays) — every second wave at 2x early on)
+    if (cap_chunks) c = std::max<uint64_t>((c * kChunk < (64ull << 20) ? 4 : 2) * c, cap_chunks + cap_chunks / 2);
     const uint64_t slots = c * kChunk;
-    key.alloc(slots * 8);
-    tag.alloc(slots * 16);
-    ord.alloc(slots * 4);
-    cnt.alloc((c ? c : 1) * 4);
-    off.alloc((c + 1) * 8);
-    lut.alloc(((slots >> jgk::kQShift) + 2) * 4);
+    // the new blocks first, then the old ones freed: hipMalloc does not wait for the device, hipFree does,
+    // so a reservation made while the device is still busy (orset_reserve_union, during a wave's uploads)
+    // costs the host that wait and not the device an idle gap behind it
+    jg::DevBuf nb[6];
+    nb[0].alloc(slots * 8);
+    nb[1].alloc(slots * 16);
+    nb[2].alloc(slots * 4);
+    nb[3].alloc((c ? c : 1) * 4);
+    nb[4].alloc((c + 1) * 8);
+    nb[5].alloc(((slots >> jgk::kQShift) + 2) * 4);
+    jg::DevBuf* cur[6] = {&key, &tag, &ord, &cnt, &off, &lut};
+    for (int i = 0; i < 6; ++i) {
+        std::swap(cur[i]->p, nb[i].p);
+        std::swap(cur[i]->bytes, nb[i].bytes);
+    }
     cap_chunks = c;
-}
+}  // the old blocks are freed here
 
 namespace jg {
 void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n) {
@@ -762,6 +774,15 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
 }
 
 void orset_merge_store(jg_orset* s, jg_orset* src) { merge_into(s, src, false); }
+
+// Room in the store's union targets for `add_in` / `rem_in` more records (merge_into reserves again if a
+// union turns out larger).  Called by a node wave while its uploads are in flight, so a growing store's
+// reallocation is not part of the commit behind the last upload.
+void orset_reserve_union(jg_orset* s, uint64_t add_in, uint64_t rem_in) {
+    if (s->counts_pending) return;  // the sizes are not known without a sync: the commit reserves
+    s->spare_add.reserve_records(s->add.n + add_in);
+    s->spare_rem.reserve_records(s->rem.n + rem_in);
+}
 }  // namespace jg
 
 extern "C" {

@@ -35,6 +35,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -871,6 +872,8 @@ struct jg_orset_wire {
     // element table
     jg::DevBuf tab, nset, nid, ngen, nlen, noff, nkey, pool, set_gen, next_id;
     uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
+    // an upper bound of every set's next element id (names_sync's next ids, plus every name a commit issued since)
+    uint64_t id_bound = 0;
     // open wave: payload, offsets, set per message, per-message counts / errors
     jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff, slow;  // slow: k_ow_group's per-message flags
     // the wave's payload / offsets / set ids: the buffers above (jg_orset_wave_*), or a node's
@@ -906,6 +909,30 @@ struct jg_orset_wire {
     bool tables = false, tables_ok = false;
     std::vector<unsigned long long> lc;  // host copy of ovf (overflow word, sub-list counts) taken by the check
     uint64_t waves_fast = 0, waves_sorted = 0;  // commits from the tables / by the sort path (tests read them)
+    uint64_t last_cnt[2] = {0, 0};  // distinct records (add, tombstone) the last commit merged: the next wave's estimate
+    // (names held, pool bytes used) after each commit / names_sync: where a names_since pull starts in the pool
+    std::vector<std::pair<uint64_t, uint64_t>> marks;
+    void mark() {
+        if (!marks.empty() && marks.back().first == n_names) return;
+        marks.emplace_back(n_names, pool_used);
+        if (marks.size() > 4096) marks.erase(marks.begin(), marks.begin() + 2048);
+    }
+    // the names a commit issued, copied into page-locked memory right behind the commit (one queue of copies,
+    // no wait): jg_orset_wave_names then waits on `ev` instead of five pageable copies and their syncs
+    // (~0.6 ms of every ORSetWorkload wave, the host mirror reads them after each wave)
+    struct NamesOut {
+        uint8_t* host = nullptr;
+        size_t cap = 0;
+        hipEvent_t ev = nullptr;
+        uint64_t g0 = 0, g1 = 0, p0 = 0, p1 = 0;  // what the queued copy holds (g0 == g1: nothing queued)
+        // or what jg_orset_names_since staged: names [since_from, since_to), pool [since_pool0, since_pool1)
+        uint64_t since_from = UINT64_MAX, since_to = 0, since_pool0 = 0, since_pool1 = 0, since_bytes = 0;
+    } nout;
+    ~jg_orset_wire() {
+        if (nout.ev) (void)hipEventSynchronize(nout.ev);
+        if (nout.host) (void)hipHostFree(nout.host);
+        if (nout.ev) (void)hipEventDestroy(nout.ev);
+    }
 };
 
 namespace {
@@ -996,6 +1023,47 @@ unsigned long long* status_words(jg_orset_wire* w) { return w->status.as<unsigne
 void read_words(jg_ctx* ctx, const unsigned long long* d, unsigned long long* h, int n) {
     JG_HIP(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+// Page-locked layout of a names copy: set [n] u32 | id [n] u32 | len [n] u32 | pad | pool offset [n] u64 | pool bytes.
+size_t names_out_bytes(uint64_t n, uint64_t nb) { return ((n * 12 + 15) & ~15ull) + n * 8 + nb; }
+
+// Queue the copy of the names [g0, g1) / pool bytes [p0, p1) the last commit issued (async on ctx->stream).
+void queue_names(jg_ctx* ctx, jg_orset_wire* w) {
+    auto& o = w->nout;
+    o.g0 = o.g1 = 0;
+    o.since_from = UINT64_MAX;  // the staging is about to hold this commit's names
+    const uint64_t n = w->g1 - w->g0, nb = w->p1 - w->p0;
+    if (n == 0) return;
+    const size_t need = names_out_bytes(n, nb);
+    if (o.cap < need) {
+        if (o.ev) JG_HIP(hipEventSynchronize(o.ev));  // no earlier copy may still land in the old block
+        if (o.host) JG_HIP(hipHostFree(o.host));
+        o.host = nullptr;
+        o.cap = 0;
+        void* p = nullptr;
+        JG_HIP(hipHostMalloc(&p, need + need / 2, hipHostMallocDefault));
+        o.host = static_cast<uint8_t*>(p);
+        o.cap = need + need / 2;
+    }
+    if (!o.ev) JG_HIP(hipEventCreateWithFlags(&o.ev, hipEventDisableTiming));
+    // on the copy queue (idle once a wave's uploads are in), behind the commit's kernels: the record sorts and
+    // the union behind them on ctx->stream do not wait for these copies.  The names arrays are only ever
+    // appended to past g1 / p1 or reallocated, and a reallocation (grow_keep) syncs the copy queue first.
+    hipStream_t q = ctx->copy ? ctx->copy : ctx->stream;
+    if (q != ctx->stream) {
+        JG_HIP(hipEventRecord(o.ev, ctx->stream));
+        JG_HIP(hipStreamWaitEvent(q, o.ev, 0));
+    }
+    uint8_t* h = o.host;
+    JG_HIP(hipMemcpyAsync(h, w->nset.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, q));
+    JG_HIP(hipMemcpyAsync(h + n * 4, w->nid.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, q));
+    JG_HIP(hipMemcpyAsync(h + n * 8, w->nlen.as<uint32_t>() + w->g0, n * 4, hipMemcpyDeviceToHost, q));
+    const size_t po = (n * 12 + 15) & ~15ull;
+    JG_HIP(hipMemcpyAsync(h + po, w->noff.as<unsigned long long>() + w->g0, n * 8, hipMemcpyDeviceToHost, q));
+    if (nb) JG_HIP(hipMemcpyAsync(h + po + n * 8, w->pool.as<uint8_t>() + w->p0, nb, hipMemcpyDeviceToHost, q));
+    JG_HIP(hipEventRecord(o.ev, q));
+    o.g0 = w->g0, o.g1 = w->g1, o.p0 = w->p0, o.p1 = w->p1;
 }
 
 void* cub_temp(jg_orset_wire* w, size_t bytes) {
@@ -1179,6 +1247,13 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
         if (h[1] == 0) {
             w->tables_ok = true;
+            // a set's element ids cannot run out in this wave's commit: every set's next id is at most the
+            // names issued so far, and the wave adds at most one per distinct (set, string) — checked here,
+            // before a node wave commits anything (the commit's own check then never fires mid-wave)
+            uint64_t ns = 0;
+            for (uint32_t j = 0; j < kLists; ++j) ns += w->lc[(1 + j) * kCountStride];
+            JG_REQUIRE(w->id_bound + ns <= JG_NULL_ELEM - 1, JG_ESTATE, "jg_orset_wave: element ids up to %llu issued + %llu names in this wave pass an OR-Set's 2^32 - 2 ids",
+                       (unsigned long long)w->id_bound, (unsigned long long)ns);
             if (h[0] == kNone) return JG_OK;
             unsigned long long e;
             JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + h[0], 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1205,6 +1280,8 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     const uint64_t ne = tot[0], nt = tot[1];
     JG_REQUIRE(ne < 0x7FFFFFF0ull && nt < 0x7FFFFFF0ull, JG_EINVAL, "jg_orset_wave: %llu entries / %llu tags exceed one wave (2^31)",
                (unsigned long long)ne, (unsigned long long)nt);
+    JG_REQUIRE(w->id_bound + ne <= JG_NULL_ELEM - 1, JG_ESTATE, "jg_orset_wave: element ids up to %llu issued + %llu entries in this wave pass an OR-Set's 2^32 - 2 ids",
+               (unsigned long long)w->id_bound, (unsigned long long)ne);
     w->n_ent = ne;
     w->n_tag = nt;
     ensure(w->ekey, ne * 8 + 8);
@@ -1340,6 +1417,9 @@ void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bi
 void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     jg_ctx* ctx = s->ctx;
     const uint64_t n = w->wn;
+    static const bool tr = std::getenv("JANUS_TRACE_MERGE") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e6; };
+    double tc[5] = {tr ? now() : 0};
     uint64_t lim_off = w->wnb;
     if (limit < n) {  // the limit message's byte offset
         JG_HIP(hipMemcpyAsync(&lim_off, w->voff + limit, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1404,13 +1484,19 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         select_marked(ctx, w, RecLive{RT.list, RT.word, RT.mint, S.trk, t_lim, 1}, nrec, w->fslot.as<uint32_t>(), st + 5);
     }
     unsigned long long hh[6];  // [1] new strings, [2] pool bytes used, [3] id overflow, [4] [5] records per side
+    if (tr) tc[1] = now();
     read_words(ctx, st, hh, 6);
+    if (tr) tc[2] = now();
     JG_REQUIRE(hh[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
     w->n_names += hh[1];
+    w->id_bound += hh[1];
     w->pool_used = hh[2];
     w->g1 = w->n_names;
     w->p1 = w->pool_used;
+    queue_names(ctx, w);
+    w->mark();
     const unsigned long long cnt[2] = {hh[4], hh[5]};
+    w->last_cnt[0] = cnt[0], w->last_cnt[1] = cnt[1];
     if (cnt[0] + cnt[1] == 0) return;
     for (int sd = 0; sd < 2; ++sd) {
         ensure(w->dk[sd], cnt[sd] * 8 + 8);
@@ -1434,9 +1520,15 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     sort_side_begin(ctx, w, 1, cnt[1], key_bits, t_next, w->recs->rem, st + 7);
     unsigned long long long_run[2];
     read_words(ctx, st + 6, long_run, 2);
+    if (tr) tc[3] = now();
     sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, RT.mint);
     sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, RT.mint);
     jg::orset_merge_store(s, w->recs);
+    if (tr) {
+        tc[4] = now();
+        std::fprintf(stderr, "commit_tables: strings queued %.0f us, counts read %.0f, record sorts + long-run read %.0f, union %.0f (%llu strings, %llu + %llu records)\n",
+                     tc[1] - tc[0], tc[2] - tc[1], tc[3] - tc[2], tc[4] - tc[3], (unsigned long long)ns, cnt[0], cnt[1]);
+    }
 }
 
 void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
@@ -1497,9 +1589,12 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
         read_words(ctx, st, h, 4);
         JG_REQUIRE(h[3] == 0, JG_ESTATE, "jg_orset_wave_commit: too many elements in one OR-Set (2^32 - 2 ids)");
         w->n_names += nnew;
+        w->id_bound += nnew;
         w->pool_used = h[2];
         w->g1 = w->n_names;
         w->p1 = w->pool_used;
+        queue_names(ctx, w);
+        w->mark();
     }
     if (ne) {
         hipLaunchKernelGGL(k_ow_entry_ids, dim3(blocks_for(ne)), dim3(kBlock), 0, ctx->stream, w->sval.as<uint32_t>(), w->label.as<uint32_t>(),
@@ -1539,6 +1634,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     }
     unsigned long long cnt[2];
     read_words(ctx, st + 4, cnt, 2);
+    w->last_cnt[0] = cnt[0], w->last_cnt[1] = cnt[1];
     if (cnt[0] + cnt[1] == 0) return;
     if (!w->recs) {  // the wave's sorted records: kept across waves (no allocation per commit)
         w->recs = new jg_orset();
@@ -1593,6 +1689,13 @@ int orset_node_check(jg_orset* s, uint64_t n, uint64_t nbytes, uint64_t* bad, st
     *bad = UINT64_MAX;
     s->wire->wn = n;
     s->wire->wnb = nbytes;
+    // the union targets sized for the store plus twice the last wave's distinct records while this wave's
+    // uploads are still in flight (a growing store reallocates here, not behind the last upload)
+    const uint64_t* lc = s->wire->last_cnt;
+    static const bool tr = std::getenv("JANUS_TRACE_MERGE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    orset_reserve_union(s, 2 * lc[0] + 4096, 2 * lc[1] + 4096);
+    if (tr) std::fprintf(stderr, "orset_node_check: union targets reserved in %.0f us\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
     const int rc = jg_orset_wave_check(s, bad);
     if (rc != JG_OK) {
         char buf[1024];
@@ -1640,8 +1743,8 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
         jg::ensure_device(ctx);
         jg_orset_wire* w = wire_of(s);
         JG_REQUIRE(!w->open, JG_EINVAL, "jg_orset_names_sync: a wave is open");
-        uint64_t mx = 0;
-        for (uint64_t i = 0; i < n_sets; ++i) mx = std::max<uint64_t>(mx, (uint64_t)set[i] + 1);
+        uint64_t mx = 0, idb = 0;
+        for (uint64_t i = 0; i < n_sets; ++i) mx = std::max<uint64_t>(mx, (uint64_t)set[i] + 1), idb = std::max<uint64_t>(idb, next_id[i]);
         for (uint64_t i = 0; i < n_names; ++i) {
             JG_REQUIRE(off[i + 1] >= off[i] && off[i + 1] - off[i] < 0x7FFFFFFFull, JG_EINVAL, "jg_orset_names_sync: bad offsets at name %llu",
                        (unsigned long long)i);
@@ -1678,7 +1781,9 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
         }
         JG_HIP(hipStreamSynchronize(ctx->stream));
         w->n_names += n_names;
+        w->id_bound = std::max(w->id_bound, idb);
         w->pool_used += nb;
+        w->mark();
     });
 }
 
@@ -1802,6 +1907,22 @@ int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint3
         JG_REQUIRE(id && off && (bytes || nb == 0), JG_EINVAL, "jg_orset_wave_names: NULL buffer");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
+        const auto& o = w->nout;
+        if (o.g0 != o.g1 && o.g0 == w->g0 && o.g1 == w->g1 && o.p0 == w->p0 && o.p1 == w->p1) {  // queued by the commit
+            JG_HIP(hipEventSynchronize(o.ev));
+            const uint8_t* h = o.host;
+            const auto* hlen = reinterpret_cast<const uint32_t*>(h + n * 8);
+            const auto* hpo = reinterpret_cast<const unsigned long long*>(h + ((n * 12 + 15) & ~15ull));
+            const uint8_t* hpool = reinterpret_cast<const uint8_t*>(hpo + n);
+            std::memcpy(set, h, n * 4);
+            std::memcpy(id, h + n * 4, n * 4);
+            off[0] = 0;
+            for (uint64_t i = 0; i < n; ++i) {
+                off[i + 1] = off[i] + hlen[i];
+                if (hlen[i]) std::memcpy(bytes + off[i], hpool + (hpo[i] - w->p0), hlen[i]);
+            }
+            return;
+        }
         std::vector<uint32_t> len(n);
         std::vector<unsigned long long> po(n);
         std::vector<uint8_t> pool(nb);
@@ -1815,6 +1936,78 @@ int jg_orset_wave_names(jg_orset* s, uint64_t* n_names, uint64_t* n_bytes, uint3
         for (uint64_t i = 0; i < n; ++i) {
             off[i + 1] = off[i] + len[i];
             if (len[i]) std::copy(pool.begin() + (po[i] - w->p0), pool.begin() + (po[i] - w->p0) + len[i], bytes + off[i]);
+        }
+    });
+}
+
+int jg_orset_names_since(jg_orset* s, uint64_t from, uint64_t* to, uint64_t* n_bytes, uint32_t* set, uint32_t* id, uint64_t* off, uint8_t* bytes) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(s);
+        JG_REQUIRE(s && to && n_bytes, JG_EINVAL, "jg_orset_names_since: NULL argument");
+        jg_orset_wire* w = s->wire;
+        const uint64_t total = w ? w->n_names : 0;
+        JG_REQUIRE(from <= total, JG_EINVAL, "jg_orset_names_since: from %llu past the %llu names held", (unsigned long long)from,
+                   (unsigned long long)total);
+        *to = total;
+        *n_bytes = 0;
+        const uint64_t n = total - from;
+        if (n == 0) return;
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        auto& o = w->nout;
+        if (!(o.since_from == from && o.since_to == total && o.since_pool1 == w->pool_used)) {
+            // A commit's new names take their pool bytes by atomics (not in name order), so the bytes of names
+            // [from, total) lie in the pool range that starts at the last mark at or before `from` (every name
+            // past a mark was made after it) and ends at pool_used.  One queue of copies into page-locked
+            // staging, one wait; kept for the second call of a size query + fill.
+            uint64_t pool0 = 0;
+            for (auto it = w->marks.rbegin(); it != w->marks.rend(); ++it)
+                if (it->first <= from) { pool0 = it->second; break; }
+            const uint64_t nb = w->pool_used - pool0;
+            const size_t need = names_out_bytes(n, nb);
+            if (o.ev) JG_HIP(hipEventSynchronize(o.ev));
+            o.g0 = o.g1 = 0;  // the staging is reused here: a queued wave-names copy is gone
+            if (o.cap < need) {
+                if (o.host) JG_HIP(hipHostFree(o.host));
+                o.host = nullptr;
+                o.cap = 0;
+                void* p = nullptr;
+                JG_HIP(hipHostMalloc(&p, need + need / 2, hipHostMallocDefault));
+                o.host = static_cast<uint8_t*>(p);
+                o.cap = need + need / 2;
+            }
+            uint8_t* h = o.host;
+            const size_t po = (n * 12 + 15) & ~15ull;
+            JG_HIP(hipMemcpyAsync(h, w->nset.as<uint32_t>() + from, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipMemcpyAsync(h + n * 4, w->nid.as<uint32_t>() + from, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipMemcpyAsync(h + n * 8, w->nlen.as<uint32_t>() + from, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipMemcpyAsync(h + po, w->noff.as<unsigned long long>() + from, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+            if (nb) JG_HIP(hipMemcpyAsync(h + po + n * 8, w->pool.as<uint8_t>() + pool0, nb, hipMemcpyDeviceToHost, ctx->stream));
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            const auto* hlen = reinterpret_cast<const uint32_t*>(h + n * 8);
+            const auto* hpo = reinterpret_cast<const unsigned long long*>(h + po);
+            uint64_t sum = 0;
+            for (uint64_t i = 0; i < n; ++i) {
+                JG_REQUIRE(hpo[i] >= pool0 && hpo[i] + hlen[i] <= w->pool_used, JG_ESTATE,
+                           "jg_orset_names_since: name %llu's bytes lie outside the pool range of its log position", (unsigned long long)(from + i));
+                sum += hlen[i];
+            }
+            o.since_from = from, o.since_to = total, o.since_pool0 = pool0, o.since_pool1 = w->pool_used, o.since_bytes = sum;
+        }
+        *n_bytes = o.since_bytes;
+        if (!set) return;
+        JG_REQUIRE(id && off && (bytes || o.since_bytes == 0), JG_EINVAL, "jg_orset_names_since: NULL buffer");
+        const uint8_t* h = o.host;
+        const size_t po = (n * 12 + 15) & ~15ull;
+        const auto* hlen = reinterpret_cast<const uint32_t*>(h + n * 8);
+        const auto* hpo = reinterpret_cast<const unsigned long long*>(h + po);
+        const uint8_t* hpool = reinterpret_cast<const uint8_t*>(hpo + n);
+        std::memcpy(set, h, n * 4);
+        std::memcpy(id, h + n * 4, n * 4);
+        off[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            off[i + 1] = off[i] + hlen[i];
+            if (hlen[i]) std::memcpy(bytes + off[i], hpool + (hpo[i] - o.since_pool0), hlen[i]);
         }
     });
 }

@@ -372,7 +372,9 @@ const Groups* groups_of(jg_pnc* p, uint64_t n_rows, Groups& g) {
         p->head_gen = 0;
         // JANUS_TEST_HEAD_GEN: a new store's first generation (tests run batches across the wrap)
         const char* e = first ? std::getenv("JANUS_TEST_HEAD_GEN") : nullptr;
-        if (e) p->head_gen = std::strtoull(e, nullptr, 10) & 0xFFFFFFFFull;
+        // clamped below 2^32 - 1: the increment below then gives 1 .. 2^32 - 1, never 0 or 2^32 (a generation
+        // whose low 32 bits read 0 would make every head look old)
+        if (e) p->head_gen = std::min<unsigned long long>(std::strtoull(e, nullptr, 10), 0xFFFFFFFEull);
     }
     ++p->head_gen;
     if (p->next.bytes < n_rows * 4) {

@@ -45,13 +45,13 @@ struct Tiles {
 struct RowOwner {  // PN-Counter rows: key_idx (NULL = identity rows)
     const uint32_t* keys;
     uint32_t world;
-    __device__ __forceinline__ uint32_t owner(uint64_t s) const { return (keys ? keys[s] : (uint32_t)s) % world; }
+    __device__ __forceinline__ uint32_t owner(uint64_t s) const { return jg::owner_of_key(keys ? keys[s] : (uint32_t)s, world); }
 };
 
 struct RecOwner {  // OR-Set records: key = set << 32 | elem
     const unsigned long long* key;
     uint32_t world;
-    __device__ __forceinline__ uint32_t owner(uint64_t s) const { return (uint32_t)((key[s] >> 32) % world); }
+    __device__ __forceinline__ uint32_t owner(uint64_t s) const { return jg::owner_of_key(key[s] >> 32, world); }
 };
 
 template <class Own>
@@ -120,7 +120,7 @@ struct RowMover {
             for (uint32_t i0 = wv; i0 < cnt; i0 += kRW * U) {
                 if (lane < U && i0 + lane * kRW < cnt) {
                     const uint64_t s = s0 + i0 + lane * kRW;
-                    okeys[dst[i0 + lane * kRW]] = (keys ? keys[s] : (uint32_t)s) / world;
+                    okeys[dst[i0 + lane * kRW]] = (uint32_t)jg::local_of_key(keys ? keys[s] : (uint32_t)s, world);
                 }
                 for (uint32_t v = lane; v < 2 * nv; v += 64) {
                     const bool isP = v < nv;
@@ -144,7 +144,7 @@ struct RowMover {
         }
         for (uint32_t i = wv; i < cnt; i += kRW) {
             const uint64_t s = s0 + i, d = dst[i];
-            if (lane == 0) okeys[d] = (keys ? keys[s] : (uint32_t)s) / world;
+            if (lane == 0) okeys[d] = (uint32_t)jg::local_of_key(keys ? keys[s] : (uint32_t)s, world);
             {
                 using T = std::conditional_t<EB == 4, int, long long>;
                 const T* sp = reinterpret_cast<const T*>(P) + s * R;
@@ -174,7 +174,7 @@ struct RecMover {
         if (i < cnt) {
             const unsigned long long k = key[s0 + i];
             const unsigned long long set = k >> 32;
-            okey[dst[i]] = ((set / world) << 32) | (k & 0xFFFFFFFFull);
+            okey[dst[i]] = (jg::local_of_key(set, world) << 32) | (k & 0xFFFFFFFFull);
             otag[dst[i]] = tag[s0 + i];
             oord[dst[i]] = ord[s0 + i];
         }

@@ -180,45 +180,42 @@ void GpuStableStore::flush_names() {
     if (bytes.empty()) bytes.push_back(0);
     check(jg_orset_names_sync(orset_, set.size(), set.data(), next.data(), cleared.data(), nid.size(), nset.data(), nid.data(), off.data(),
                               bytes.data()));
+    names_seen_ += nid.size();  // caught up before the sync (materialize_names above): the log's new tail is ours
     pending_names_.clear();
 }
 
-// The element ids the last wave issued (sorted by set, then id), copied out of the engine; they join the
-// host tables in materialize_names.
-void GpuStableStore::take_wave_names() {
-    uint64_t n = 0, nb = 0;
-    check(jg_orset_wave_names(orset_, &n, &nb, nullptr, nullptr, nullptr, nullptr));
-    if (n == 0) return;
-    WaveNames w;
-    w.set.resize(n);
-    w.id.resize(n);
-    w.off.resize(n + 1);
-    w.bytes.resize(std::max<uint64_t>(nb, 1));
-    check(jg_orset_wave_names(orset_, &n, &nb, w.set.data(), w.id.data(), w.off.data(), w.bytes.data()));
-    wave_names_.push_back(std::move(w));
-}
-
-// Pending wave names appended to the SetKey tables, wave after wave, the sets split over the workers in
-// contiguous ranges.
+// The names the engine's waves issued since the last pull (its names log past names_seen_, several waves
+// at once), appended to the SetKey tables, the sets split over the workers in contiguous ranges.  The log
+// is in issue order: within a set, ids ascend.
 void GpuStableStore::materialize_names() {
-    if (wave_names_.empty()) return;
-    for (const WaveNames& w : wave_names_) {
-        const size_t n = w.set.size();
-        const std::vector<uint32_t>& set = w.set;
-        std::vector<int> bad(pool().size(), 0);
-        parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
-            while (b < n && b > 0 && set[b - 1] == set[b]) ++b;  // that set belongs to the previous worker
-            while (e < n && e > 0 && set[e - 1] == set[e]) ++e;
-            for (size_t i = b; i < e; ++i) {
-                SetKey& sk = sets_[set[i]];
-                if (w.id[i] != sk.names.size()) { bad[t] = 1; return; }
-                sk.names.emplace_back(reinterpret_cast<const char*>(w.bytes.data()) + w.off[i], w.off[i + 1] - w.off[i]);  // elems: lazily
-            }
-        });
-        for (int x : bad)
-            if (x) throw EngineError(JG_ESTATE, "element ids of the engine and the host tables disagree");
-    }
-    wave_names_.clear();
+    if (!orset_) return;
+    uint64_t to = 0, nb = 0;
+    check(jg_orset_names_since(orset_, names_seen_, &to, &nb, nullptr, nullptr, nullptr, nullptr));
+    if (to == names_seen_) return;
+    const uint64_t n = to - names_seen_;
+    std::vector<uint32_t> set(n), id(n);
+    std::vector<uint64_t> off(n + 1);
+    std::vector<uint8_t> bytes(std::max<uint64_t>(nb, 1));
+    check(jg_orset_names_since(orset_, names_seen_, &to, &nb, set.data(), id.data(), off.data(), bytes.data()));
+    // per set the log's ids ascend, but a set's names may interleave with other sets' across waves: group the
+    // log's entries by set (stable), then each worker appends whole sets
+    std::vector<uint32_t> order(n);
+    for (uint64_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return set[a] < set[b]; });
+    std::vector<int> bad(pool().size(), 0);
+    parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+        while (b < n && b > 0 && set[order[b - 1]] == set[order[b]]) ++b;  // that set belongs to the previous worker
+        while (e < n && e > 0 && set[order[e - 1]] == set[order[e]]) ++e;
+        for (size_t k = b; k < e; ++k) {
+            const uint32_t i = order[k];
+            SetKey& sk = sets_[set[i]];
+            if (id[i] != sk.names.size()) { bad[t] = 1; return; }
+            sk.names.emplace_back(reinterpret_cast<const char*>(bytes.data()) + off[i], off[i + 1] - off[i]);  // elems: lazily
+        }
+    });
+    for (int x : bad)
+        if (x) throw EngineError(JG_ESTATE, "element ids of the engine and the host tables disagree");
+    names_seen_ = to;
 }
 
 std::vector<uint64_t> GpuStableStore::ApplyCommitted(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker) {
@@ -328,9 +325,12 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
     const int rc = block_mode ? jg_apply_block(node_, &wave, &at)
                               : jg_apply_committed(node_, tracker ? tracker->handle() : nullptr, &wave, w_done_.data(), &n_done, &at);
     const std::string why = rc == JG_OK ? std::string() : last_error();
+    static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     jg_node_last_stats(node_, &stats_);
     std::vector<uint64_t> done(w_done_.begin(), w_done_.begin() + (ptrdiff_t)n_done);
-    take_wave_names();  // the element ids an OR-Set commit issued join the host tables lazily
+    if (trace) std::fprintf(stderr, "run_wave: stats + completions %.0f us\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
+    // the element ids an OR-Set commit issued join the host tables when something next reads names
     if (rc != JG_OK) {
         if (at == UINT64_MAX) throw EngineError(rc, why);
         throw ApplyError(rc, why, at, std::move(done));  // the prefix before `at` was applied

@@ -236,12 +236,11 @@ class GpuStableStore {
     struct PendingNames { bool cleared = false; std::vector<uint32_t> ids; };
     std::unordered_map<uint32_t, PendingNames> pending_names_;
     void flush_names();
-    // Ids the last OR-Set wave issued: copied from the engine right after the commit (the engine keeps
-    // only the last commit's), appended to the SetKey tables on first use by anything that reads names
-    // (interning for ops, encode, LookupAll, the name sync) — not on the apply path.
-    struct WaveNames { std::vector<uint32_t> set, id; std::vector<uint64_t> off; std::vector<uint8_t> bytes; };
-    std::vector<WaveNames> wave_names_;
-    void take_wave_names();
+    // Ids the OR-Set waves issued join the SetKey tables on first use by anything that reads names
+    // (interning for ops, encode, LookupAll, the name sync): pulled then from the engine's names log
+    // (jg_orset_names_since, every wave since the last pull at once) — nothing on the apply path.
+    // names_seen_ = the log length these tables cover (the names this mirror synced itself included).
+    uint64_t names_seen_ = 0;
     void materialize_names();
     const KeyRef& ref(const Guid& uid, CrdtType want) const;
     void check(int rc) const;

@@ -34,12 +34,13 @@ EXPORTS = [
     "jg_orset_lookup_all", "jg_pnc_encode_json",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
-    "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_merge_json",
+    "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
     "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256",
     "jg_node_create", "jg_node_destroy", "jg_node_register", "jg_node_set_shard", "jg_shard_of", "jg_node_last_stats",
     "jg_tracker_create", "jg_tracker_destroy", "jg_tracker_add", "jg_tracker_size", "jg_tracker_contains",
     "jg_apply_committed", "jg_apply_block",
     "jg_comm_unique_id", "jg_comm_init", "jg_comm_destroy", "jg_pnc_exchange", "jg_orset_exchange", "jg_comm_last_stats",
+    "jg_comm_init_host", "jg_exchange_plan", "jg_global_key",
 ]
 
 _u8p = C.POINTER(C.c_uint8)
@@ -108,6 +109,7 @@ _SIGS = {
     "jg_orset_wave_commit": ([_vp, _u64], C.c_int),
     "jg_orset_wave_abort": ([_vp], C.c_int),
     "jg_orset_wave_names": ([_vp, C.POINTER(_u64), C.POINTER(_u64), _vp, _vp, _vp, _vp], C.c_int),
+    "jg_orset_names_since": ([_vp, _u64, C.POINTER(_u64), C.POINTER(_u64), _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_merge_json": ([_vp, _u64, _vp, _vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_node_create": ([_vp, _vp, C.POINTER(_vp)], C.c_int),
     "jg_node_destroy": ([_vp], C.c_int),
@@ -124,6 +126,9 @@ _SIGS = {
     "jg_apply_block": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_comm_unique_id": ([_vp], C.c_int),
     "jg_comm_init": ([_vp, _u32, _u32, _vp, C.POINTER(_vp)], C.c_int),
+    "jg_comm_init_host": ([_vp, _u32, _u32, _vp, _vp, C.POINTER(_vp)], C.c_int),
+    "jg_exchange_plan": ([_u32, _u32, _u32, _vp, C.c_uint8, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_global_key": ([_vp, _u32, _u32, C.POINTER(_u32)], C.c_int),
     "jg_comm_destroy": ([_vp], C.c_int),
     "jg_pnc_exchange": ([_vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_exchange": ([_vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
@@ -565,6 +570,19 @@ class ORSetStore:
         raw = b.tobytes()
         return [(int(s[k]), int(i[k]), raw[int(off[k]):int(off[k + 1])]) for k in range(n.value)]
 
+    def names_since(self, start=0):
+        """The store's names log from `start`: (end, list of (set, id, bytes)) in the order the table took them."""
+        to, nb = _u64(), _u64()
+        _check(load().jg_orset_names_since(self._h, start, C.byref(to), C.byref(nb), None, None, None, None))
+        n = to.value - start
+        if n == 0:
+            return to.value, []
+        s, i = np.empty(n, np.uint32), np.empty(n, np.uint32)
+        off, b = np.empty(n + 1, np.uint64), np.empty(max(1, nb.value), np.uint8)
+        _check(load().jg_orset_names_since(self._h, start, C.byref(to), C.byref(nb), _ptr(s), _ptr(i), _ptr(off), _ptr(b)))
+        raw = b.tobytes()
+        return to.value, [(int(s[k]), int(i[k]), raw[int(off[k]):int(off[k + 1])]) for k in range(n)]
+
     def lookup_all(self, set_ids):
         """ORSet.LookupAll of each set (jg_orset_lookup_all): list of uint32 arrays of elem ids."""
         s = _arr(set_ids, np.uint32)
@@ -623,6 +641,27 @@ def shard_of(lo: int, hi: int, world: int) -> int:
     r = _u32()
     _check(load().jg_shard_of(_ptr(g), world, C.byref(r)))
     return r.value
+
+
+def global_key(lo: int, hi: int, world: int, local: int) -> int:
+    """jg_global_key: the global key (row / set id the exchange routes by) of key uid (lo, hi) registered with
+    local index `local` by its owner jg_shard_of(uid, world)."""
+    g = np.zeros(1, GUID_DTYPE)
+    g["lo"], g["hi"] = lo, hi
+    r = _u32()
+    _check(load().jg_global_key(_ptr(g), world, local, C.byref(r)))
+    return r.value
+
+
+def exchange_plan(rank: int, world: int, counts, skip_own: bool = False):
+    """jg_exchange_plan: counts[src, dst, j] (uint64, world x world x k) -> (send_off, send_n, recv_off, recv_n),
+    each [world, k] for this rank (pure host arithmetic: no device needed)."""
+    c = np.ascontiguousarray(counts, np.uint64)
+    assert c.ndim == 3 and c.shape[0] == c.shape[1] == world
+    k = c.shape[2]
+    out = [np.zeros((world, k), np.uint64) for _ in range(4)]
+    _check(load().jg_exchange_plan(rank, world, k, _ptr(c), 1 if skip_own else 0, *(_ptr(x) for x in out)))
+    return tuple(out)
 
 
 class Tracker:
@@ -748,6 +787,9 @@ class ExchangeStats(C.Structure):
                 ("bytes_sent", C.c_uint64), ("bytes_received", C.c_uint64), ("records_received", C.c_uint64)]
 
 
+_ALLTOALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.c_void_p, C.POINTER(C.c_uint64))
+
+
 def comm_unique_id() -> bytes:
     """jg_comm_unique_id: a fresh 128-byte RCCL unique id (made by one rank, handed to the others)."""
     buf = (C.c_uint8 * 128)()
@@ -760,10 +802,31 @@ class Comm:
     exchange_pnc / exchange_orset route a received batch / state by owner, move the runs over RCCL and
     merge what this rank owns — the whole cross-shard exchange inside the library."""
 
-    def __init__(self, ctx: Context, rank: int, world: int, uid: bytes):
-        assert len(uid) == 128
+    def __init__(self, ctx: Context, rank: int, world: int, uid: bytes | None = None, alltoallv=None):
+        """uid: the RCCL transport (jg_comm_init).  alltoallv: the host transport (jg_comm_init_host) —
+        alltoallv(send: bytes, send_bytes: list, recv_bytes: list) -> bytes of the peers' runs back to back."""
         self._h = _vp()
         self.rank, self.world = rank, world
+        if alltoallv is not None:
+            def cb(user, send, sb, recv, rb):
+                try:
+                    s_n = [sb[p] for p in range(world)]
+                    r_n = [rb[p] for p in range(world)]
+                    data = C.string_at(send, sum(s_n)) if sum(s_n) else b""
+                    got = alltoallv(data, s_n, r_n)
+                    if len(got) != sum(r_n):
+                        return 2
+                    if got:
+                        C.memmove(recv, got, len(got))
+                    return 0
+                except Exception:  # noqa: BLE001 — an exception cannot cross the C boundary
+                    import traceback
+                    traceback.print_exc()
+                    return 1
+            self._cb = _ALLTOALLV(cb)  # kept alive with the communicator
+            _check(load().jg_comm_init_host(ctx.handle, rank, world, C.cast(self._cb, _vp), None, C.byref(self._h)))
+            return
+        assert uid is not None and len(uid) == 128
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         _check(load().jg_comm_init(ctx.handle, rank, world, C.cast(buf, _vp), C.byref(self._h)))
 

@@ -23,6 +23,26 @@ import numpy as np
 import janus_gpu as jg
 
 
+def all_to_all_plan(counts, rank: int, skip_own: bool = False):
+    """The layout all_to_all_single gives the runs (what Exchange.runs moves): counts[src, dst, j] records
+    source src routes to destination dst in buffer j.  Returns (send_off, send_n, recv_off, recv_n), each
+    [world, k]: this rank's send buffer j holds every destination's run in rank order, its receive buffer j
+    the sources' runs back to back in rank order.  skip_own: the own run stays out of both (a PN-Counter
+    rank merges it from its send buffer).  csrc/comm.hip's jg_exchange_plan must equal this."""
+    c = np.asarray(counts, np.uint64)
+    world, k = c.shape[0], c.shape[2]
+    send_off = np.zeros((world, k), np.uint64)
+    send_off[1:] = np.cumsum(c[rank, :-1, :], axis=0)
+    send_n = c[rank].copy()
+    recv_n = c[:, rank, :].copy()
+    if skip_own:
+        send_n[rank] = 0
+        recv_n[rank] = 0
+    recv_off = np.zeros((world, k), np.uint64)
+    recv_off[1:] = np.cumsum(recv_n[:-1], axis=0)
+    return send_off, send_n, recv_off, recv_n
+
+
 class Exchange:
     """All-to-all of variable-size runs over a torch.distributed group (RCCL on the GPU box)."""
 

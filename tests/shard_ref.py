@@ -9,6 +9,16 @@ import numpy as np
 from oracle_ref import REC_DTYPE
 
 
+def owner_of_key(k, world):
+    """The rank that owns global key k (csrc/jg_internal.hpp owner_of_key)."""
+    return int(k) % world
+
+
+def local_of_key(k, world):
+    """Global key k's local key on its owner (csrc/jg_internal.hpp local_of_key)."""
+    return int(k) // world
+
+
 def route_rows(keys, P, N, world):
     """-> (counts[world], local keys, P, N) grouped by destination rank, batch order within a group."""
     keys = np.asarray(keys, np.uint32)

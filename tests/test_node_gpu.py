@@ -375,3 +375,90 @@ def test_decreasing_offsets_reject_the_wave(ctx, monkeypatch, drop):
     finally:
         for h in (node, tr, pnc, st):
             h.close()
+
+
+def test_tracker_adds_across_empty_waves(ctx):
+    """an empty wave flushes the pending tracker adds and returns; the next adds go into the other
+    page-locked buffer, the wave after that flushes them and reuses the first one.  Every add must reach the
+    device table intact (no buffer rewritten or freed while its upload is queued), in add order."""
+    tr = jg.Tracker(ctx)
+    pnc = jg.PNCStore(ctx, 4, R, EB)
+    node = jg.Node(pnc, None)
+    try:
+        u = (0x1234, 0x5678)
+        node.register([u[0]], [u[1]], [0], [0])
+        origin = {}
+        seq = 1
+        for rnd in range(4):
+            for _ in range(3):  # adds, then an empty wave (flushes them), twice over; the buffers alternate
+                new = list(range(seq, seq + 5000))
+                seq += 5000
+                tr.add(new, [s % 991 + 1 for s in new])
+                origin.update({s: s % 991 + 1 for s in new})
+                done, cut, rc = node.apply_committed(tr, [], [], [], [], [])
+                assert cut is None and rc == jg.JG_OK and len(done) == 0
+            take = sorted(origin)[::2]
+            msgs = [J.encode_pnc([(1, 2)], [1], [0])] * len(take)
+            done, cut, rc = node.apply_committed(tr, [u[0]] * len(take), [u[1]] * len(take), [1] * len(take), take, msgs)
+            assert cut is None and list(done) == [origin.pop(s) for s in take]
+            assert tr.size() == len(origin)
+    finally:
+        node.close()
+        pnc.close()
+        tr.close()
+
+
+def test_tracker_first_add_wins_within_a_batch(ctx):
+    """ConcurrentDictionary.TryAdd (SafeCRDT.cs:55): an identity added twice before one flush keeps the
+    origin of its first add, whichever device lane inserts it."""
+    tr = jg.Tracker(ctx)
+    pnc = jg.PNCStore(ctx, 4, R, EB)
+    node = jg.Node(pnc, None)
+    try:
+        u = (0x99, 0x77)
+        node.register([u[0]], [u[1]], [0], [0])
+        ids = list(range(1000, 1000 + 4096))
+        # each identity added 8 times in one batch (first origin = id % 13 + 1), interleaved
+        for r in range(8):
+            tr.add(ids, [i % 13 + 1 + 100 * r for i in ids])
+        tr.add([ids[0]], [777])  # a later batch: TryAdd of a present identity keeps the first origin too
+        msgs = [J.encode_pnc([(1, 2)], [1], [0])] * len(ids)
+        done, cut, rc = node.apply_committed(tr, [u[0]] * len(ids), [u[1]] * len(ids), [1] * len(ids), ids, msgs)
+        assert list(done) == [i % 13 + 1 for i in ids]
+        assert tr.size() == 0
+    finally:
+        node.close()
+        pnc.close()
+        tr.close()
+
+
+def test_orset_id_space_rejects_before_anything_commits(ctx):
+    """A wave whose new element names could run a set past 2^32 - 2 ids is rejected (JG_ESTATE) by the check,
+    before the PN-Counter commit: no PN-Counter row and no OR-Set record of the wave is applied, and the
+    tracker claims are released (the OR-Set commit used to fail after the PN-Counter one)."""
+    rng = np.random.default_rng(21)
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, 10, 2)
+    try:
+        pcl = J.Cluster(rng, 10, R - 1, EB, stable=None)
+        st.names_sync(sets=[0], next_ids=[0xFFFFFFFD], cleared=[0])
+        P0, N0 = pnc.read_rows()
+        a0, r0 = st.read()
+        tr.add([41], [9])
+        wave = [(uids[0], 1, 41, pcl.message(0)), (uids[10], 1, 0, J.encode_orset([("n1", [(1, 2)]), ("n2", [(3, 4)])], []))]
+        with pytest.raises(jg.JanusError) as e:
+            node.apply_committed(tr, [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], [x[2] for x in wave],
+                                 [x[3] for x in wave])
+        assert e.value.code == jg.JG_ESTATE
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, P0) and np.array_equal(N, N0)
+        a, r = st.read()
+        assert orc.same_orset(a, r, a0, r0)
+        # one new name still fits (id 2^32 - 3): the same PN-Counter message then completes its identity
+        wave[1] = (uids[10], 1, 0, J.encode_orset([("n1", [(1, 2)])], []))
+        done, cut, rc = node.apply_committed(tr, [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave],
+                                             [x[2] for x in wave], [x[3] for x in wave])
+        assert rc == jg.JG_OK and cut is None and list(done) == [9]
+        assert st.wave_names() == [(0, 0xFFFFFFFD, b"n1")]
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()

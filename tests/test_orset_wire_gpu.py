@@ -376,3 +376,48 @@ def test_hot_name_in_long_impure_runs(ctx, monkeypatch):
         assert dt < 5.0, dt
     finally:
         s.close()
+
+
+def test_names_log_holds_every_wave_and_sync(ctx):
+    """jg_orset_names_since: the store's names log is every wave's issued names (jg_orset_wave_names) and every
+    synced name, in the order the table took them; a pull from any point returns its tail."""
+    rng = np.random.default_rng(31)
+    cl = J.ORSetCluster(rng, 20)
+    s = jg.ORSetStore(ctx)
+    try:
+        log = []
+        for w in range(4):
+            sets = [int(x) for x in rng.integers(0, 20, 300)]
+            msgs = [J.encode_orset(*cl.state(k)) for k in sets]
+            rc, bad = s.wave([(sets[:150], msgs[:150]), (sets[150:], msgs[150:])])
+            assert rc == jg.JG_OK and bad is None
+            log += s.wave_names()
+            if w == 1:  # names a caller issued itself (ORSet.Add): appended to the log as synced
+                nxt = max(i for st_, i, _ in log if st_ == 3) + 1
+                s.names_sync(sets=[3], next_ids=[nxt + 2], cleared=[0], names=[(3, nxt, b"own-a"), (3, nxt + 1, b"own-b")])
+                log += [(3, nxt, b"own-a"), (3, nxt + 1, b"own-b")]
+        end, got = s.names_since(0)
+        assert end == len(log) and got == log
+        for k in (1, len(log) // 3, len(log) - 1, len(log)):
+            end, tail = s.names_since(k)
+            assert end == len(log) and tail == log[k:]
+        with pytest.raises(jg.JanusError):
+            s.names_since(len(log) + 1)
+    finally:
+        s.close()
+
+
+def test_element_id_space_limit(ctx):
+    """Ids are issued up to 2^32 - 3 (JG_NULL_ELEM - 1 is reserved): a wave that could pass it is rejected with
+    JG_ESTATE and nothing applied; one that fits commits."""
+    s = jg.ORSetStore(ctx)
+    try:
+        s.names_sync(sets=[0], next_ids=[0xFFFFFFFC], cleared=[0])
+        with pytest.raises(jg.JanusError) as e:
+            s.merge_json([0], [J.encode_orset([("a", [G1]), ("b", [G2]), ("c", [G3])], [])])
+        assert e.value.code == jg.JG_ESTATE
+        assert all(len(x) == 0 for x in s.read())
+        s.merge_json([0], [J.encode_orset([("a", [G1]), ("b", [G2])], [])])
+        assert s.wave_names() == [(0, 0xFFFFFFFC, b"a"), (0, 0xFFFFFFFD, b"b")]
+    finally:
+        s.close()

@@ -138,3 +138,62 @@ def test_route_rule_is_a_stable_partition():
         run = out[at: at + int(c[d])]
         assert np.array_equal(np.unique(run), run)    # each owner's run stays strictly increasing
         at += int(c[d])
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("k,skip_own", [(1, True), (1, False), (2, False)])
+def test_exchange_plan_matches_all_to_all_layout(world, k, skip_own):
+    """jg_exchange_plan (csrc/comm.hip, the plan every exchange call follows: RCCL or host transport) against
+    janus_gpu/shard.py's all_to_all_single layout on the same counts, then the whole exchange simulated: every
+    rank's runs copied where the plan says must land exactly the records routed to each rank, in source-rank
+    order (the order the OR-Set union keeps for arrival ordinals).  Pure host arithmetic: runs on CPU."""
+    sys.path.insert(0, str(ROOT / "janus-crdt_amd"))
+    import janus_gpu as jg
+    from janus_gpu.shard import all_to_all_plan
+    rng = np.random.default_rng(world * 10 + k)
+    counts = rng.integers(0, 50, (world, world, k)).astype(np.uint64)
+    counts[rng.random((world, world, k)) < 0.25] = 0  # empty runs, incl. own ones
+    counts[0] = 0  # a rank that sends nothing
+    plans = [jg.exchange_plan(r, world, counts, skip_own) for r in range(world)]
+    for r in range(world):
+        for a, b in zip(plans[r], all_to_all_plan(counts, r, skip_own)):
+            assert np.array_equal(a, b)
+    for j in range(k):
+        # send buffer of src: (src, dst, idx) records grouped by dst in rank order
+        send = [[(s_, d, i) for d in range(world) for i in range(int(counts[s_, d, j]))] for s_ in range(world)]
+        for d in range(world):
+            so, sn, ro, rn = (x[:, j] for x in plans[d])
+            recv = [None] * int(rn.sum())
+            for s_ in range(world):
+                s_off, s_n = plans[s_][0][d, j], plans[s_][1][d, j]
+                assert s_n == rn[s_], "what src sends dst must equal what dst receives from src"
+                if s_ == d and skip_own:
+                    assert s_n == 0
+                    continue
+                recv[int(ro[s_]):int(ro[s_] + rn[s_])] = send[s_][int(s_off):int(s_off + s_n)]
+            exp = [(s_, d, i) for s_ in range(world) if not (skip_own and s_ == d) for i in range(int(counts[s_, d, j]))]
+            assert recv == exp
+            if skip_own:  # the own run stays in the send buffer where the merge reads it
+                own = send[d][int(so[d]):int(so[d] + counts[d, d, j])]
+                assert own == [(d, d, i) for i in range(int(counts[d, d, j]))]
+
+
+def test_global_key_follows_shard_of():
+    """The one owner rule: a key registered by its owner jg_shard_of(uid, world) with local
+    index l has the global key l * world + owner, which the exchange routes to rank global % world as local
+    key global // world (csrc/jg_internal.hpp owner_of_key).  Pure host: runs on CPU."""
+    sys.path.insert(0, str(ROOT / "janus-crdt_amd"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import janus_gpu as jg
+    import shard_ref as ref
+    rng = np.random.default_rng(5)
+    uids = [(int(a), int(b)) for a, b in rng.integers(1, 2**63, (300, 2), dtype=np.int64)]
+    for world in range(1, 9):
+        nxt = [0] * world
+        for lo, hi in uids:
+            owner = jg.shard_of(lo, hi, world)
+            g = jg.global_key(lo, hi, world, nxt[owner])
+            assert g % world == owner and g // world == nxt[owner]
+            assert ref.owner_of_key(g, world) == owner and ref.local_of_key(g, world) == nxt[owner]
+            nxt[owner] += 1
+        assert sum(nxt) == len(uids)

@@ -464,3 +464,162 @@ def test_comm_init_rejects_bad_ranks(ctx):
         with pytest.raises(jg.JanusError) as ei:
             jg.Comm(ctx, rank, world, uid)
         assert ei.value.code == jg.JG_EINVAL
+
+
+# ---- one owner rule: the apply loop's jg_shard_of and the exchange's route agree ----
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_routes_follow_the_uid_owner(ctx, world):
+    """Keys registered by their owner jg_shard_of(uid, world) with global ids from jg_global_key (INTEGRATION.md
+    §5): jg_rows_route and jg_orset_route send every row / record of a key to exactly the rank jg_shard_of names
+    (the routing safeCRDTsIndexedByuid[u.uid] decides in the reference, SafeCRDTManager.cs:136), as its local id."""
+    rng = np.random.default_rng(40 + world)
+    uids = [(int(a), int(b)) for a, b in rng.integers(1, 2**63, (600, 2), dtype=np.int64)]
+    nxt = [0] * world
+    gkey, owner, local = [], [], []
+    for lo, hi in uids:
+        o = jg.shard_of(lo, hi, world)
+        gkey.append(jg.global_key(lo, hi, world, nxt[o]))
+        owner.append(o)
+        local.append(nxt[o])
+        nxt[o] += 1
+    gkey, owner, local = np.array(gkey, np.uint32), np.array(owner), np.array(local, np.uint32)
+    pick = rng.integers(0, len(uids), 5000)  # a batch of rows of these keys, repeats included
+    P, N = random_pnc(rng, len(pick), 64, 8), random_pnc(rng, len(pick), 64, 8)
+    counts, k, _, _ = _route_rows(ctx, gkey[pick], P, N, world, 8)
+    at = 0
+    for d in range(world):
+        mine = pick[owner[pick] == d]  # stable: batch order within the destination's run
+        assert counts[d] == len(mine)
+        assert np.array_equal(k[at:at + len(mine)], local[mine])
+        at += len(mine)
+    # OR-Set records of these keys (set id = global key), sorted as a store keeps them
+    recs = np.zeros(len(uids) * 3, jg.REC_DTYPE)
+    recs["key"] = (np.repeat(gkey.astype(np.uint64), 3) << np.uint64(32)) | np.tile(np.arange(3, dtype=np.uint64), len(uids))
+    recs["tag_lo"] = rng.integers(1, 2**62, len(recs))
+    recs["tag_hi"] = rng.integers(1, 2**62, len(recs))
+    recs = np.sort(recs, order=["key", "tag_lo", "tag_hi"])
+    recs["ord"] = np.arange(len(recs)) % 3
+    ca, _, ga, _ = _route_store(ctx, recs, recs[:0], world)
+    sets = (recs["key"] >> np.uint64(32)).astype(np.uint64)
+    at = 0
+    for d in range(world):
+        n_d = int(np.sum(sets % np.uint64(world) == d))
+        assert ca[d] == n_d
+        got_sets = (ga["key"][at:at + n_d] >> np.uint64(32)).astype(np.uint64)
+        exp_sets = sets[sets % np.uint64(world) == d] // np.uint64(world)
+        assert np.array_equal(got_sets, exp_sets)
+        at += n_d
+    idx = {int(g): i for i, g in enumerate(gkey)}
+    assert all(owner[idx[int(s)]] == int(s) % world for s in np.unique(sets))
+
+
+# ---- the RCCL communicator's deadline: a rank that never joins costs a bounded wait, not a hang ----
+def test_comm_init_without_peers_times_out():
+    """jg_comm_init(world 2, rank 0) with no rank 1: the non-blocking communicator's init polls against
+    JANUS_COMM_TIMEOUT_S (5 s here), aborts and returns JG_EHIP (run in a child process with its own limit)."""
+    import subprocess
+    import time
+    code = ("import sys, time; sys.path.insert(0, %r); import janus_gpu as jg\n"
+            "ctx = jg.Context(0)\nt = time.time()\n"
+            "try:\n    jg.Comm(ctx, 0, 2, jg.comm_unique_id())\nexcept jg.JanusError as e:\n"
+            "    print('ERR', e.code, round(time.time() - t, 1), flush=True)\nelse:\n    print('JOINED')\n"
+            "ctx.close()\n" % str(ROOT / "janus-crdt_amd"))
+    env = dict(os.environ, JANUS_COMM_TIMEOUT_S="5")
+    t = time.time()
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=90, env=env)
+    line = [x for x in out.stdout.splitlines() if x.startswith(("ERR", "JOINED"))]
+    assert line and line[0].startswith("ERR"), out.stdout + out.stderr[-3000:]
+    _, rc, secs = line[0].split()
+    assert int(rc) == jg.JG_EHIP
+    assert 4.0 <= float(secs) < 30 and time.time() - t < 90
+
+
+# ---- the library's own exchange at world > 1: the host transport over gloo, ranks sharing device 0 ----
+def _host_comm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    for p in (ROOT / "janus-crdt_amd", ROOT / "tests"):
+        sys.path.insert(0, str(p))
+    import torch as th
+    import torch.distributed as dist
+    import janus_gpu as jg_
+    import oracle_ref as orc_
+    import shard_ref as ref_
+    from gen import random_orset_pair as rop, random_pnc as rpnc
+    dist.init_process_group("gloo")
+
+    def a2a(send, sb, rb):  # the caller's all-to-all-v (gloo over host memory)
+        out = th.empty(sum(rb), dtype=th.uint8)
+        inp = th.frombuffer(bytearray(send), dtype=th.uint8) if send else th.empty(0, dtype=th.uint8)
+        dist.all_to_all_single(out, inp, [int(x) for x in rb], [int(x) for x in sb])
+        return out.numpy().tobytes()
+
+    try:
+        rng = np.random.default_rng(321)
+        K_local, R, n = 400, 64, 2500
+        G = K_local * world
+        AP, AN = rpnc(rng, G, R, 8, absent=False, lo=0), rpnc(rng, G, R, 8, absent=False, lo=0)
+        batches = [(rng.integers(0, G, n).astype(np.uint32), rpnc(rng, n, R, 8), rpnc(rng, n, R, 8)) for _ in range(world)]
+        batches[world - 1] = (batches[world - 1][0][:0], batches[world - 1][1][:0], batches[world - 1][2][:0])  # a rank sends nothing
+        La, Lr, _, _ = rop(rng, n_sets=30 * world, n_elems=5, pool=8)
+        recv = [rop(rng, n_sets=30 * world, n_elems=5, pool=8)[2:] for _ in range(world)]
+        with jg_.Context(0) as ctx:
+            cm = jg_.Comm(ctx, rank, world, alltoallv=a2a)
+            s = jg_.PNCStore(ctx, K_local, R, 8)
+            s.write_rows(ref_.shard_rows(AP, world, rank), ref_.shard_rows(AN, world, rank))
+            k, P, N = batches[rank]
+            rows = None
+            if len(k):
+                rows = jg_.Rows(ctx, len(k), R, 8)
+                rows.upload(P, N, k)
+            out = cm.exchange_pnc(s, rows)
+            gP, gN = s.read_rows()
+            eP, eN = AP, AN
+            for kk, PP, NN in batches:
+                if len(kk):
+                    eP, eN = orc_.pnc_merge(eP, eN, PP, NN, kk)
+            ok_pnc = np.array_equal(gP, ref_.shard_rows(eP, world, rank)) and np.array_equal(gN, ref_.shard_rows(eN, world, rank))
+            exp_recv = [int(np.sum(b[0] % world == rank)) for b in batches]
+            ok_counts = out["received"].tolist() == exp_recv and int(cm.stats().records_received) == sum(exp_recv)
+            o = jg_.ORSetStore(ctx, 0, 0)
+            o.load(ref_.shard_records(La, world, rank), ref_.shard_records(Lr, world, rank))
+            src = jg_.ORSetStore(ctx, 0, 0)
+            src.load(*recv[rank])
+            cm.exchange_orset(o, src)
+            ga, gr = o.read()
+            ea, er = La, Lr
+            for a, r in recv:  # ORSet.Merge of every rank's state in source-rank order
+                ea, er = orc_.orset_merge(ea, er, a, r)
+            ok_orset = orc_.same_orset(ga, gr, ref_.shard_records(ea, world, rank), ref_.shard_records(er, world, rank))
+            for h in (s, o, src, cm) + ((rows,) if rows is not None else ()):
+                h.close()
+        q.put((rank, ok_pnc and ok_counts, ok_orset, ""))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, False, False, traceback.format_exc()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_library_exchange_at_world_2_and_3_host_transport(world):
+    """jg_pnc_exchange / jg_orset_exchange of csrc/comm.hip at world > 1 — route, counts all-gather, the plan,
+    the runs, the merge — with the host transport (RCCL refuses two ranks on one GPU): every rank's shard equals
+    its slice of the oracle's Merge of every rank's batch (PNCounter.Merge; ORSet.Merge in source-rank order,
+    arrival ordinals included).  Only the transport differs from the RCCL path bench.py --gpus N runs."""
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_host_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted(q.get(timeout=110) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, ok_pnc, ok_orset, err in res:
+        assert not err, f"rank {rank}: {err}"
+        assert ok_pnc and ok_orset, (rank, ok_pnc, ok_orset)
