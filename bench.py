@@ -525,7 +525,9 @@ def bench_apply_direct(local):
                           "--device", str(local), "--direct"], capture_output=True, text=True, timeout=240)
     if out.returncode != 0:
         return {"error": out.stderr[-500:]}
-    return json.loads(out.stdout.strip().splitlines()[-1])
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    res.pop("cpu_baseline", None)  # not run here (--cpu-msgs 0): the gathered leg "apply_loop" carries it
+    return res
 
 
 def bench_apply_orset(sync, rank, world, local):
@@ -674,84 +676,8 @@ def cpu_baseline():
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest", "json"], default="all")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pnc-shape", choices=["auto"] + sorted(PNC_SHAPES), default="auto",
-                    help="per-GPU PN-Counter shard: c2 = BASELINE configs[1], c4 = 1/8 of configs[3]; "
-                         "auto (default) = c2 on one GPU, c4 on N > 1")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: a fixed shard per GPU; strong: configs[3]'s 200M keys split over N >= 4 GPUs")
-    args = ap.parse_args()
-
-    world, rank, local = dist_env()
-    if args.pnc_shape == "auto":
-        args.pnc_shape = "c2" if world == 1 and args.scaling == "weak" else "c4"
-    if args.scaling == "strong" and world < 4:
-        sys.exit("--scaling strong needs N >= 4: configs[3]'s 200M keys x 128 replicas (A + B = 819.2 GB) do not fit fewer MI355X")
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
-    if world > 1 or args.workload in ("all", "exchange", "digest", "json"):
-        # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
-        # instance (torch's libraries also name the runtime by an unversioned soname)
-        import torch  # noqa: F401
-    sync = Sync(world, local, os.environ.get("JANUS_BENCH_BACKEND", "nccl"))
-    import janus_gpu as jg
-    ctx = jg.Context(local)
-
-    res = {}
-    if args.workload in ("all", "pnc", "pnc-orset"):
-        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape, args.scaling)
-    if args.workload in ("all", "orset", "pnc-orset"):
-        res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup, args.scaling)
-    if args.workload in ("all", "exchange"):
-        try:  # a failure here must not cost the headline line
-            res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
-        except Exception as e:  # noqa: BLE001
-            res["exchange"] = {"error": repr(e)[:500]}
-    if args.workload in ("all", "json"):
-        try:
-            res["json"] = bench_json(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
-        except Exception as e:  # noqa: BLE001
-            res["json"] = {"error": repr(e)[:500]}
-    if args.workload in ("all", "digest"):
-        try:
-            res["digest"] = bench_digest(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
-            if rank == 0 and world == 1 and not args.no_cpu_baseline:
-                res["digest"]["cpu_baseline"] = cpu_digest_baseline()
-        except Exception as e:  # noqa: BLE001
-            res["digest"] = {"error": repr(e)[:500]}
-    ctx.close()
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline()
-    def guarded(fn, *a):  # a leg's failure must not cost the headline line (each leg's collective runs on every
-        try:              # rank before anything in it can raise: sync.max takes inf for a failed run)
-            return fn(*a)
-        except Exception as e:  # noqa: BLE001
-            return {"error": repr(e)[:500]}
-
-    apply_loop = guarded(bench_apply_loop, sync, rank, world, local) if args.workload == "all" else None
-    apply_orset = guarded(bench_apply_orset, sync, rank, world, local) if args.workload == "all" else None
-    apply_c1 = guarded(bench_c1, local) if args.workload == "all" and world == 1 else None
-    apply_direct = guarded(bench_apply_direct, local) if args.workload == "all" and world == 1 else None
-    for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
-        if leg is not None and "error" not in leg and "scaling" not in leg:
-            leg["roofline"] = guarded(apply_roofline, leg)
-    # the same OR-Set and C1 waves from page-locked payloads (one GPU: the shard shortcut gathers)
-    if apply_orset is not None and "error" not in apply_orset and world == 1:
-        apply_orset["from_pinned"] = guarded(run_direct, "bench_orset", ["--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "0"], local)
-    if apply_c1 is not None and "error" not in apply_c1:
-        apply_c1["from_pinned"] = guarded(run_direct, "bench_c1", ["--waves", "3", "--no-cpu"], local)
-    sync.close()
-    if rank != 0:
-        return
-
+def headline(args, world, res, cpu):
+    """The line's headline fields: the C2 PN-Counter step (metric, value, roofline) and the C3 OR-Set step."""
     line = {"metric": "replica-key merges/sec + achieved HBM GB/s (PNCounter & ORSet)", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": args.scaling,
             "vs_baseline": None, "data": "synthetic (seeded counter-based generators, DESIGN.md)"}
@@ -800,12 +726,96 @@ def main():
         if "value" not in line:
             line.update({"value": line["orset"]["value"], "unit": "tag records merged/s", "ms_per_step": ost * 1e3,
                          "dtype": "u64+u128 records", "config": {"workload": line["orset"]["workload"]}})
-    if "exchange" in res:
-        line["exchange"] = res["exchange"]
-    if "digest" in res:
-        line["update_digests"] = res["digest"]
-    if "json" in res:
-        line["json_apply"] = res["json"]
+    line["cpu_baseline"] = cpu
+    return line
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest", "json"], default="all")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pnc-shape", choices=["auto"] + sorted(PNC_SHAPES), default="auto",
+                    help="per-GPU PN-Counter shard: c2 = BASELINE configs[1], c4 = 1/8 of configs[3]; "
+                         "auto (default) = c2 on one GPU, c4 on N > 1")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: a fixed shard per GPU; strong: configs[3]'s 200M keys split over N >= 4 GPUs")
+    args = ap.parse_args()
+
+    world, rank, local = dist_env()
+    if args.pnc_shape == "auto":
+        args.pnc_shape = "c2" if world == 1 and args.scaling == "weak" else "c4"
+    if args.scaling == "strong" and world < 4:
+        sys.exit("--scaling strong needs N >= 4: configs[3]'s 200M keys x 128 replicas (A + B = 819.2 GB) do not fit fewer MI355X")
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+    if world > 1 or args.workload in ("all", "exchange", "digest", "json"):
+        # torch (device buffers + RCCL) is loaded before libjanusgpu so both bind ONE HIP runtime
+        # instance (torch's libraries also name the runtime by an unversioned soname)
+        import torch  # noqa: F401
+    sync = Sync(world, local, os.environ.get("JANUS_BENCH_BACKEND", "nccl"))
+    import janus_gpu as jg
+    ctx = jg.Context(local)
+
+    res = {}
+    if args.workload in ("all", "pnc", "pnc-orset"):
+        res["pnc"] = bench_pnc(jg, ctx, sync, rank, world, args.steps, args.warmup, args.pnc_shape, args.scaling)
+    if args.workload in ("all", "orset", "pnc-orset"):
+        res["orset"] = bench_orset(jg, ctx, sync, rank, world, max(1, args.steps // 2), args.warmup, args.scaling)
+    if world > 1 and rank == 0 and args.workload in ("all", "exchange") and ("pnc" in res or "orset" in res):
+        # the headline (PN-Counter + OR-Set) before the first world > 1 collective of the library's own
+        # communicator: whatever the exchange leg does, a line is out; the full line follows at the end
+        print(json.dumps(headline(args, world, res, None)), flush=True)
+    if args.workload in ("all", "exchange"):
+        try:  # a failure here must not cost the headline line
+            res["exchange"] = bench_exchange(jg, ctx, sync, rank, world, local, max(1, args.steps // 4), min(args.warmup, 2))
+        except Exception as e:  # noqa: BLE001
+            res["exchange"] = {"error": repr(e)[:500]}
+    if args.workload in ("all", "json"):
+        try:
+            res["json"] = bench_json(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
+        except Exception as e:  # noqa: BLE001
+            res["json"] = {"error": repr(e)[:500]}
+    if args.workload in ("all", "digest"):
+        try:
+            res["digest"] = bench_digest(jg, ctx, sync, rank, max(1, args.steps // 2), min(args.warmup, 2))
+            if rank == 0 and world == 1 and not args.no_cpu_baseline:
+                res["digest"]["cpu_baseline"] = cpu_digest_baseline()
+        except Exception as e:  # noqa: BLE001
+            res["digest"] = {"error": repr(e)[:500]}
+    ctx.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+    def guarded(fn, *a):  # a leg's failure must not cost the headline line (each leg's collective runs on every
+        try:              # rank before anything in it can raise: sync.max takes inf for a failed run)
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001
+            return {"error": repr(e)[:500]}
+
+    apply_loop = guarded(bench_apply_loop, sync, rank, world, local) if args.workload == "all" else None
+    apply_orset = guarded(bench_apply_orset, sync, rank, world, local) if args.workload == "all" else None
+    apply_c1 = guarded(bench_c1, local) if args.workload == "all" and world == 1 else None
+    apply_direct = guarded(bench_apply_direct, local) if args.workload == "all" and world == 1 else None
+    for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
+        if leg is not None and "error" not in leg and "scaling" not in leg:
+            leg["roofline"] = guarded(apply_roofline, leg)
+    # the same OR-Set and C1 waves from page-locked payloads (one GPU: the shard shortcut gathers)
+    if apply_orset is not None and "error" not in apply_orset and world == 1:
+        apply_orset["from_pinned"] = guarded(run_direct, "bench_orset", ["--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "0"], local)
+    if apply_c1 is not None and "error" not in apply_c1:
+        apply_c1["from_pinned"] = guarded(run_direct, "bench_c1", ["--waves", "3", "--no-cpu"], local)
+    sync.close()
+    if rank != 0:
+        return
+
+    line = headline(args, world, res, cpu)
+    orset_leg = line.pop("orset", None)
+    # the verbose apply-loop objects first, the compact legs (OR-Set step, exchange, JSON, digests) last: a
+    # reader that keeps only the line's tail still sees them
     if apply_loop is not None:
         line["apply_loop"] = apply_loop
     if apply_orset is not None:
@@ -815,6 +825,14 @@ def main():
     if apply_direct is not None:
         line["apply_loop_direct"] = apply_direct
     line["cpu_baseline"] = cpu
+    if "digest" in res:
+        line["update_digests"] = res["digest"]
+    if "json" in res:
+        line["json_apply"] = res["json"]
+    if "exchange" in res:
+        line["exchange"] = res["exchange"]
+    if orset_leg is not None:
+        line["orset"] = orset_leg
     print(json.dumps(line), flush=True)
 
 

@@ -28,6 +28,7 @@ void fail(int code, const char* fmt, ...) {
 
 void DevBuf::alloc(size_t n) {
     release();
+    own = true;
     if (n == 0) return;
     hipError_t e = hipMalloc(&p, n);
     if (e != hipSuccess) {
@@ -39,9 +40,10 @@ void DevBuf::alloc(size_t n) {
 }
 
 void DevBuf::release() {
-    if (p) (void)hipFree(p);
+    if (p && own) (void)hipFree(p);
     p = nullptr;
     bytes = 0;
+    own = true;
 }
 
 void ensure_device(jg_ctx* ctx) { JG_HIP(hipSetDevice(ctx->device)); }

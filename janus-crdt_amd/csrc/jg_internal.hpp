@@ -79,7 +79,14 @@ template <class F> int guard(F&& body) {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    bool own = true;       // false: a view into another DevBuf's block (never freed through this one)
     void alloc(size_t n);  // frees the old block; n == 0 leaves p null
+    void view(void* q, size_t n) {  // a non-owning view (the owner frees the block)
+        release();
+        p = q;
+        bytes = n;
+        own = false;
+    }
     void release();
     ~DevBuf() { release(); }
     DevBuf() = default;
@@ -159,6 +166,8 @@ struct jg_rows {
 // starting at or before rank q*512.
 constexpr uint32_t kChunk = 3072;  // = one union tile (orset.hip kOB * kItems)
 struct jg_stream_soa {
+    jg::DevBuf block;          // one device block holding the six arrays below (views into it): one hipMalloc and
+                               // one hipFree per reservation (hipFree costs ~0.2 ms of host time each on the box)
     jg::DevBuf key, tag, ord;  // cap_chunks * kChunk slots
     uint64_t next = 0;         // every record's ord < next (host copy; a union's B records land at next + ord)
     jg::DevBuf cnt;       // uint32 [cap_chunks]

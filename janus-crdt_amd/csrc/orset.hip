@@ -637,7 +637,9 @@ void jg_stream_soa::swap(jg_stream_soa& o) {
     auto swap_buf = [](jg::DevBuf& x, jg::DevBuf& y) {
         std::swap(x.p, y.p);
         std::swap(x.bytes, y.bytes);
+        std::swap(x.own, y.own);
     };
+    swap_buf(block, o.block);
     swap_buf(key, o.key);
     swap_buf(tag, o.tag);
     swap_buf(ord, o.ord);
@@ -663,23 +665,24 @@ void jg_stream_soa::reserve_records(uint64_t records) {
     // (hipMalloc + hipFree of the six arrays) — every second wave at 2x early on)
     if (cap_chunks) c = std::max<uint64_t>((c * kChunk < (64ull << 20) ? 4 : 2) * c, cap_chunks + cap_chunks / 2);
     const uint64_t slots = c * kChunk;
-    // the new blocks first, then the old ones freed: hipMalloc does not wait for the device, hipFree does,
-    // so a reservation made while the device is still busy (orset_reserve_union, during a wave's uploads)
-    // costs the host that wait and not the device an idle gap behind it
-    jg::DevBuf nb[6];
-    nb[0].alloc(slots * 8);
-    nb[1].alloc(slots * 16);
-    nb[2].alloc(slots * 4);
-    nb[3].alloc((c ? c : 1) * 4);
-    nb[4].alloc((c + 1) * 8);
-    nb[5].alloc(((slots >> jgk::kQShift) + 2) * 4);
+    // ONE block for the six arrays (hipFree costs ~0.2 ms of host time per call on the box: six per stream made
+    // a growing store's reservation ~2.3 ms), the new block first, then the old one freed: hipMalloc does not
+    // wait for the device, hipFree does, so a reservation made while the device is still busy
+    // (orset_reserve_union, during a wave's uploads) costs the host that wait, not the device an idle gap
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    const size_t sz[6] = {al(slots * 8), al(slots * 16), al(slots * 4), al((c ? c : 1) * 4), al((c + 1) * 8), al(((slots >> jgk::kQShift) + 2) * 4)};
+    jg::DevBuf nb;
+    nb.alloc(sz[0] + sz[1] + sz[2] + sz[3] + sz[4] + sz[5]);
+    std::swap(block.p, nb.p);
+    std::swap(block.bytes, nb.bytes);
     jg::DevBuf* cur[6] = {&key, &tag, &ord, &cnt, &off, &lut};
+    char* q = block.as<char>();
     for (int i = 0; i < 6; ++i) {
-        std::swap(cur[i]->p, nb[i].p);
-        std::swap(cur[i]->bytes, nb[i].bytes);
+        cur[i]->view(q, sz[i]);
+        q += sz[i];
     }
     cap_chunks = c;
-}  // the old blocks are freed here
+}  // the old block is freed here
 
 namespace jg {
 void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n) {

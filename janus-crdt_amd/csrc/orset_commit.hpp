@@ -1,0 +1,343 @@
+// orset_commit.hpp — the OR-Set wave commit from the tables, by set buckets (included by orset_wire.hip
+// after orset_tables.hpp).
+//
+// A committed wave (ORSet.Merge of every state before the cut, ORSet.cs:253-283) needs two orders:
+//   strings  the wave's new element strings get ids per set in first-insertion order (the add/remove
+//            Dictionaries' order, :255-279): sorted by (set, first entry);
+//   records  the wave's distinct tag records become a stream sorted by (set, element id, tag) that the
+//            union merges into the store.
+// Both orders are "by set, then a few hundred items of one set".  The round-3 commit sorted each list with a
+// device-wide radix sort (rocprim's merge sort at these sizes: ~20 launches each, ~0.75 ms of launches, syncs
+// and passes behind the last upload of the ORSetWorkload wave).  Here:
+//   k_cb_count    one lane per listed string / record: known strings resolved against the element table,
+//                 new strings and live records counted per set (one atomic per distinct set of a wave: the
+//                 lanes of a wave that share a set are folded first, so a hot set costs one atomic per wave)
+//                 with their place in the set's bucket;
+//   k_cb_scan     exclusive sums of the per-set counts (and of the new strings' bytes), totals and the
+//                 largest bucket — read back in the commit's one host sync;
+//   k_cb_scatter  every item into its bucket;
+//   k_cb_strings  one workgroup per set: the bucket sorted by first entry in LDS (bitonic), ids next_id + rank,
+//                 names appended in (set, first entry) order with their bytes placed by a prefix of lengths;
+//   k_cb_records  one workgroup per (side, set): the bucket sorted by (element id, tag) in LDS, written straight
+//                 into the dense stream the union reads (position = bucket offset + rank).
+// A bucket larger than the LDS sort holds (kCbMax) sends the wave to the radix path (commit_tables' own).
+#pragma once
+
+constexpr uint32_t kCbMax = 2048;  // items of one set / (side, set) the LDS sorts hold
+constexpr int kCbBlock = 256;
+
+struct Buckets {
+    uint32_t* scnt;              // [n_sets + 1] new strings per set -> exclusive offsets
+    unsigned long long* sbytes;  // [n_sets + 1] their bytes -> exclusive byte offsets
+    uint32_t* rcnt[2];           // [n_sets + 1] live records per set, per side -> exclusive offsets
+    uint32_t* spos;              // [ns] place of listed string i in its set's bucket (kDead: known / past the limit)
+    uint32_t* sset;              // [ns] its set
+    uint32_t* rpos;              // [nrec] place of listed record j in its (side, set) bucket (kDead: past the limit)
+    uint32_t* rset;              // [nrec] side << 31 | set
+    uint32_t* sitem;             // [new strings] list indices in bucket order
+    uint32_t* ritem[2];          // [live records of the side] list indices in bucket order
+    uint32_t n_sets;
+};
+
+// The lanes of a wave holding the same key (set, or side << 31 | set) take consecutive places from one atomic
+// on that key's counter; returns this lane's place.  Lanes with active = false take part in the ballots only.
+__device__ __forceinline__ uint32_t wave_fold_add(bool active, uint32_t key, uint32_t* counters, uint32_t ctr_index, unsigned long long* bytes,
+                                                  uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    unsigned long long todo = __ballot(active);
+    uint32_t place = kDead;
+    while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const uint32_t k = __shfl(key, leader);
+        const unsigned long long same = __ballot(active && key == k) & todo;
+        const uint32_t kidx = __shfl(ctr_index, leader);
+        uint32_t base = 0;
+        unsigned long long sum = 0;
+        if (bytes) {  // the group's bytes: a wave sum over the group's lanes
+            unsigned long long v = ((same >> lane) & 1) ? len : 0;
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            sum = v;
+        }
+        if ((int)lane == leader) {
+            base = atomicAdd(counters + kidx, (uint32_t)__popcll(same));
+            if (bytes) atomicAdd(bytes + kidx, sum);
+        }
+        base = __shfl(base, leader);
+        if ((same >> lane) & 1) place = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+        todo &= ~same;
+    }
+    return place;
+}
+
+__global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, RecTab R, uint64_t ns, uint64_t nrec,
+                                                     uint32_t s_lim, uint32_t t_lim, Names N, uint32_t* __restrict__ sid_id, Buckets B) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    // a workgroup's lanes are all strings or all records up to the boundary wave (ns need not be a multiple of 64:
+    // both folds run in every wave, each with its own lanes active)
+    bool s_new = false, r_live = false;
+    uint32_t s_set = 0, s_len = 0, r_key = 0, r_side = 0;
+    if (i < ns) {
+        const uint32_t sid = T.list[i];
+        if (T.first[sid] < s_lim) {
+            const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+            const uint32_t set = S.set[ref], len = S.meta[ref] & 0x7FFFFFFFu;
+            const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], len);
+            if (id != kNoName) {
+                sid_id[sid] = id;
+            } else {
+                s_new = true;
+                s_set = set;
+                s_len = len;
+            }
+        }
+    } else if (i - ns < nrec) {
+        const uint64_t j = i - ns;
+        const uint32_t slot = R.list[j];
+        if (R.mint[slot] < t_lim) {
+            const uint64_t u = (R.word[slot] & 0xFFFFFFFFull) - 1;
+            const unsigned long long id = S.trk[u];
+            r_side = (uint32_t)(id & 1);
+            const uint32_t set = (id >> 63) ? (uint32_t)((id >> 1) & 0xFFFFFFFFull) : S.set[(T.word[(uint32_t)(id >> 1)] & 0xFFFFFFFFull) - 1];
+            r_live = true;
+            r_key = r_side << 31 | set;
+        }
+    }
+    const uint32_t sp = wave_fold_add(s_new, s_set, B.scnt, s_set, B.sbytes, s_len);
+    const uint32_t r_set = r_key & 0x7FFFFFFFu;
+    // two record counters (per side): fold on side << 31 | set, count into that side's array
+    uint32_t rp = kDead;
+    {
+        const uint32_t lane = threadIdx.x & 63;
+        unsigned long long todo = __ballot(r_live);
+        while (todo) {
+            const int leader = __ffsll((long long)todo) - 1;
+            const uint32_t k = __shfl(r_key, leader);
+            const unsigned long long same = __ballot(r_live && r_key == k) & todo;
+            uint32_t base = 0;
+            if ((int)lane == leader) base = atomicAdd(B.rcnt[k >> 31] + (k & 0x7FFFFFFFu), (uint32_t)__popcll(same));
+            base = __shfl(base, leader);
+            if ((same >> lane) & 1) rp = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+            todo &= ~same;
+        }
+    }
+    if (i < ns) {
+        B.spos[i] = s_new ? sp : kDead;
+        B.sset[i] = s_set;
+    } else if (i - ns < nrec) {
+        B.rpos[i - ns] = r_live ? rp : kDead;
+        B.rset[i - ns] = r_key;
+    }
+    (void)r_set;
+}
+
+// Exclusive sums of the four per-set arrays in place (n + 1 entries each, the last one 0 before: the total
+// after), one workgroup per array, tiles of 1024 x 4 with a carried prefix; status[k] = total, status[4 + k]
+// = the largest entry.
+constexpr int kScanThreads = 1024, kScanItems = 4;
+template <class T> __device__ void scan_array(T* a, uint64_t n, unsigned long long* total, unsigned long long* maxv) {
+    __shared__ unsigned long long part[kScanThreads];
+    __shared__ unsigned long long carry_s;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) carry_s = 0;
+    unsigned long long mx = 0;
+    __syncthreads();
+    for (uint64_t base = 0; base < n; base += (uint64_t)kScanThreads * kScanItems) {
+        unsigned long long v[kScanItems], s = 0;
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t x = base + (uint64_t)t * kScanItems + q;
+            v[q] = x < n ? (unsigned long long)a[x] : 0ull;
+            mx = v[q] > mx ? v[q] : mx;
+            s += v[q];
+        }
+        part[t] = s;
+        __syncthreads();
+        for (int o = 1; o < kScanThreads; o <<= 1) {  // inclusive Hillis-Steele over the thread sums
+            const unsigned long long y = t >= (uint32_t)o ? part[t - o] : 0ull;
+            __syncthreads();
+            part[t] += y;
+            __syncthreads();
+        }
+        unsigned long long run = carry_s + (t ? part[t - 1] : 0ull);
+        for (int q = 0; q < kScanItems; ++q) {
+            const uint64_t x = base + (uint64_t)t * kScanItems + q;
+            if (x < n) a[x] = (T)run;
+            run += v[q];
+        }
+        __syncthreads();
+        if (t == kScanThreads - 1) carry_s += part[t];
+        __syncthreads();
+    }
+    // the largest entry (a block max through the same LDS)
+    part[t] = mx;
+    __syncthreads();
+    for (int o = kScanThreads / 2; o > 0; o >>= 1) {
+        if (t < (uint32_t)o && part[t + o] > part[t]) part[t] = part[t + o];
+        __syncthreads();
+    }
+    if (t == 0) {
+        *total = carry_s;
+        *maxv = part[0];
+    }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_cb_scan(Buckets B, uint64_t n, unsigned long long* __restrict__ status) {
+    switch (blockIdx.x) {
+        case 0: scan_array(B.scnt, n, status + 0, status + 4); break;
+        case 1: scan_array(B.sbytes, n, status + 1, status + 5); break;
+        case 2: scan_array(B.rcnt[0], n, status + 2, status + 6); break;
+        default: scan_array(B.rcnt[1], n, status + 3, status + 7); break;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cb_scatter(uint64_t ns, uint64_t nrec, Buckets B) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < ns) {
+        const uint32_t p = B.spos[i];
+        if (p != kDead) B.sitem[B.scnt[B.sset[i]] + p] = (uint32_t)i;
+    } else if (i - ns < nrec) {
+        const uint64_t j = i - ns;
+        const uint32_t p = B.rpos[j];
+        if (p != kDead) {
+            const uint32_t k = B.rset[j], sd = k >> 31;
+            B.ritem[sd][B.rcnt[sd][k & 0x7FFFFFFFu] + p] = (uint32_t)j;
+        }
+    }
+}
+
+// Bitonic sort of P (a power of two, <= kCbMax) slots by less(a, b) over an LDS permutation.
+template <class Less> __device__ void lds_bitonic(uint16_t* perm, uint32_t P, Less less) {
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t x = threadIdx.x; x < P / 2; x += blockDim.x) {
+                const uint32_t a = 2 * j * (x / j) + (x % j), b = a + j;
+                const bool up = (a & k) == 0;
+                const uint16_t pa = perm[a], pb = perm[b];
+                if (less(pb, pa) == up) {
+                    perm[a] = pb;
+                    perm[b] = pa;
+                }
+            }
+            __syncthreads();
+        }
+}
+
+__device__ __forceinline__ uint32_t pow2_ge(uint32_t x) {
+    uint32_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// One workgroup per set: its new strings by first entry; ids next_id + rank; names g0 + bucket offset + rank
+// with their bytes at pool0 + the set's byte offset + the prefix of lengths in rank order.
+__global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, Buckets B, uint64_t g0,
+                                                         uint64_t pool0, Names N, uint32_t* __restrict__ sid_id,
+                                                         unsigned long long* __restrict__ status) {
+    const uint32_t s = blockIdx.x;
+    const uint32_t o0 = B.scnt[s], cnt = B.scnt[s + 1] - o0;
+    if (cnt == 0) return;
+    __shared__ uint32_t key[kCbMax], item[kCbMax], lens[kCbMax];
+    __shared__ uint16_t perm[kCbMax];
+    __shared__ unsigned long long wsum[kCbBlock / 64];
+    const uint32_t P = pow2_ge(cnt);
+    for (uint32_t r = threadIdx.x; r < P; r += kCbBlock) {
+        if (r < cnt) {
+            const uint32_t i = B.sitem[o0 + r];
+            item[r] = i;
+            key[r] = T.first[T.list[i]];
+        }
+        perm[r] = (uint16_t)r;
+    }
+    __syncthreads();
+    lds_bitonic(perm, P, [&](uint16_t a, uint16_t b) {
+        const uint32_t ka = a < cnt ? key[a] : 0xFFFFFFFFu, kb = b < cnt ? key[b] : 0xFFFFFFFFu;
+        return ka != kb ? ka < kb : a < b;  // pads (index >= cnt) last
+    });
+    for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
+        const uint32_t sid = T.list[item[perm[r]]];
+        lens[r] = S.meta[(T.word[sid] & 0xFFFFFFFFull) - 1] & 0x7FFFFFFFu;
+    }
+    __syncthreads();
+    // exclusive prefix of the lengths in rank order (each thread a contiguous run, then the thread sums)
+    const uint32_t per = (cnt + kCbBlock - 1) / kCbBlock, r0 = threadIdx.x * per, r1 = min(cnt, r0 + per);
+    unsigned long long mine = 0;
+    for (uint32_t r = r0; r < r1; ++r) mine += lens[r];
+    unsigned long long incl = mine;  // inclusive scan over the threads: wave scan, then the wave totals
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    unsigned long long before = incl - mine;
+    for (uint32_t q = 0; q < wv; ++q) before += wsum[q];
+    const uint64_t pbase = pool0 + B.sbytes[s];
+    const uint32_t next = N.next_id[s], gen = N.set_gen[s];
+    for (uint32_t r = r0; r < r1; ++r) {
+        const uint32_t sid = T.list[item[perm[r]]];
+        const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+        const uint32_t len = lens[r];
+        const uint64_t id = (uint64_t)next + r;
+        if (id >= JG_NULL_ELEM - 1) atomicOr(status + 8, 1ull);
+        sid_id[sid] = (uint32_t)id;
+        const uint64_t g = g0 + o0 + r, p = pbase + before;
+        const uint8_t* src = bytes + S.noff[ref];
+        for (uint32_t q = 0; q < len; ++q) N.pool[p + q] = src[q];
+        before += len;
+        N.set[g] = s;
+        N.id[g] = (uint32_t)id;
+        N.gen[g] = gen;
+        N.len[g] = len;
+        N.off[g] = p;
+        N.key[g] = S.key[ref];
+        tab_insert(N, S.key[ref], (uint32_t)g);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) N.next_id[s] = next + cnt;
+}
+
+// One workgroup per (set, side): its live records by (element id, tag.lo, tag.hi) into the side's dense stream
+// at the bucket's offset; ord = the record's arrival ordinal (its first tag slot).
+__global__ __launch_bounds__(kCbBlock) void k_cb_records(Sparse S, StrTab T, RecTab R, Buckets B, const uint32_t* __restrict__ sid_id,
+                                                         unsigned long long* __restrict__ k0, Tag16* __restrict__ t0, uint32_t* __restrict__ o0_,
+                                                         unsigned long long* __restrict__ k1, Tag16* __restrict__ t1, uint32_t* __restrict__ o1_) {
+    const uint32_t s = blockIdx.x, sd = blockIdx.y;
+    const uint32_t* off = B.rcnt[sd];
+    const uint32_t o0 = off[s], cnt = off[s + 1] - o0;
+    if (cnt == 0) return;
+    __shared__ uint32_t elem[kCbMax], mint[kCbMax];
+    __shared__ unsigned long long lo[kCbMax], hi[kCbMax];
+    __shared__ uint16_t perm[kCbMax];
+    const uint32_t P = pow2_ge(cnt);
+    const uint32_t* items = B.ritem[sd];
+    for (uint32_t r = threadIdx.x; r < P; r += kCbBlock) {
+        if (r < cnt) {
+            const uint32_t slot = R.list[items[o0 + r]];
+            const uint64_t u = (R.word[slot] & 0xFFFFFFFFull) - 1;
+            const unsigned long long id = S.trk[u];
+            elem[r] = (id >> 63) ? JG_NULL_ELEM : sid_id[(uint32_t)(id >> 1)];
+            const Tag16 g = S.tval[u];
+            lo[r] = g.lo;
+            hi[r] = g.hi;
+            mint[r] = R.mint[slot];
+        }
+        perm[r] = (uint16_t)r;
+    }
+    __syncthreads();
+    lds_bitonic(perm, P, [&](uint16_t a, uint16_t b) {
+        const bool pa = a >= cnt, pb = b >= cnt;  // pads last
+        if (pa || pb) return !pa && pb ? true : (pa && pb ? a < b : false);
+        if (elem[a] != elem[b]) return elem[a] < elem[b];
+        if (lo[a] != lo[b]) return lo[a] < lo[b];
+        return hi[a] < hi[b];
+    });
+    unsigned long long* ok = sd ? k1 : k0;
+    Tag16* ot = sd ? t1 : t0;
+    uint32_t* oo = sd ? o1_ : o0_;
+    for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
+        const uint32_t x = perm[r];
+        ok[o0 + r] = (unsigned long long)s << 32 | elem[x];
+        ot[o0 + r] = Tag16{lo[x], hi[x]};
+        oo[o0 + r] = mint[x];
+    }
+}

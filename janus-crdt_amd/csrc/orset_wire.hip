@@ -852,6 +852,7 @@ __global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const T
 }
 
 #include "orset_tables.hpp"
+#include "orset_commit.hpp"
 
 uint64_t pow2_at_least(uint64_t x) {
     uint64_t p = 1024;
@@ -905,6 +906,8 @@ struct jg_orset_wire {
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
     jg::DevBuf st_word, st_first, st_list, rt_word, rt_mint, rt_list, sid_id, ovf;  // ovf: overflow word, sub-list counts
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
+    jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
+    uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
     uint64_t st_cap = 0, rt_cap = 0;
     bool tables = false, tables_ok = false;
     std::vector<unsigned long long> lc;  // host copy of ovf (overflow word, sub-list counts) taken by the check
@@ -958,7 +961,7 @@ void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero =
 jg_orset_wire* wire_of(jg_orset* s) {
     if (!s->wire) {
         s->wire = new jg_orset_wire();
-        s->wire->status.alloc(64);
+        s->wire->status.alloc(128);
         std::random_device rd;
         s->wire->salt = ((uint64_t)rd() << 32 ^ rd()) | 1;
         if (const char* e = std::getenv("JANUS_TEST_NAME_HASH_BITS")) {
@@ -1411,6 +1414,93 @@ void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bi
     JG_HIP(hipGetLastError());
 }
 
+// The bucket commit (orset_commit.hpp): false if a set's bucket is past the LDS sorts (or JANUS_ORSET_COMMIT=radix),
+// with nothing changed but the resolved ids of known strings (the radix path writes them again).
+bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTab& RT, uint64_t ns, uint64_t nrec, uint32_t csi_lim,
+                    uint32_t t_lim, uint64_t t_next) {
+    // JANUS_ORSET_COMMIT (read per wave: tests switch it): radix = the radix path alone; buckets = no fall-back (a
+    // wave the bucket path cannot take is an error)
+    const char* e = std::getenv("JANUS_ORSET_COMMIT");
+    if (e && std::strcmp(e, "radix") == 0) return false;
+    const bool strict = e && std::strcmp(e, "buckets") == 0;
+    jg_ctx* ctx = s->ctx;
+    const uint64_t n_sets = (uint64_t)w->max_set + 1;
+    // one count per set id up to the wave's largest: sparse set ids (far more ids than items) take the radix path
+    if (n_sets >= 0x7FFFFFFFull || ns + nrec >= 0xFFFFFFF0ull || n_sets > 4 * (ns + nrec) + (1u << 20)) {
+        JG_REQUIRE(!strict, JG_ESTATE, "OR-Set bucket commit: %llu set ids for %llu items (JANUS_ORSET_COMMIT=buckets)", (unsigned long long)n_sets,
+                   (unsigned long long)(ns + nrec));
+        return false;
+    }
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    const uint64_t c4 = al((n_sets + 1) * 4), c8 = al((n_sets + 1) * 8), s4 = al(ns * 4 + 4), r4 = al(nrec * 4 + 4);
+    ensure(w->cb, 3 * c4 + c8 + 3 * s4 + 4 * r4);
+    char* p = w->cb.as<char>();
+    Buckets B{};
+    B.scnt = reinterpret_cast<uint32_t*>(p);
+    B.rcnt[0] = reinterpret_cast<uint32_t*>(p + c4);
+    B.rcnt[1] = reinterpret_cast<uint32_t*>(p + 2 * c4);
+    B.sbytes = reinterpret_cast<unsigned long long*>(p + 3 * c4);
+    char* q = p + 3 * c4 + c8;
+    B.spos = reinterpret_cast<uint32_t*>(q);
+    B.sset = reinterpret_cast<uint32_t*>(q + s4);
+    B.sitem = reinterpret_cast<uint32_t*>(q + 2 * s4);
+    q += 3 * s4;
+    B.rpos = reinterpret_cast<uint32_t*>(q);
+    B.rset = reinterpret_cast<uint32_t*>(q + r4);
+    B.ritem[0] = reinterpret_cast<uint32_t*>(q + 2 * r4);
+    B.ritem[1] = reinterpret_cast<uint32_t*>(q + 3 * r4);
+    B.n_sets = (uint32_t)n_sets;
+    unsigned long long* st = status_words(w);
+    JG_HIP(hipMemsetAsync(p, 0, 3 * c4 + c8, ctx->stream));  // the four count arrays (and their trailing zeros)
+    JG_HIP(hipMemsetAsync(st, 0, 9 * 8, ctx->stream));
+    const Sparse S = sparse_of(w);
+    const Names N = names_of(w);
+    if (ns + nrec)
+        hipLaunchKernelGGL(k_cb_count, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, RT, ns, nrec, csi_lim, t_lim, N,
+                           w->sid_id.as<uint32_t>(), B);
+    hipLaunchKernelGGL(k_cb_scan, dim3(4), dim3(kScanThreads), 0, ctx->stream, B, n_sets + 1, st);
+    JG_HIP(hipGetLastError());
+    unsigned long long h[8];  // totals: new strings, their bytes, records per side; then the largest buckets
+    read_words(ctx, st, h, 8);
+    if (h[4] > kCbMax || h[6] > kCbMax || h[7] > kCbMax) {
+        JG_REQUIRE(!strict, JG_ESTATE, "OR-Set bucket commit: a set holds %llu new strings / %llu + %llu records of the wave (> %u, JANUS_ORSET_COMMIT=buckets)",
+                   h[4], h[6], h[7], kCbMax);
+        return false;
+    }
+    const uint64_t n_new = h[0], nb = h[1], cnt[2] = {h[2], h[3]};
+    if (ns + nrec) hipLaunchKernelGGL(k_cb_scatter, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, B);
+    if (n_new)
+        hipLaunchKernelGGL(k_cb_strings, dim3((unsigned)n_sets), dim3(kCbBlock), 0, ctx->stream, S, w->vbytes, ST, B, w->n_names, w->pool_used, N,
+                           w->sid_id.as<uint32_t>(), st);
+    JG_HIP(hipGetLastError());
+    ++w->waves_bucketed;
+    // ids issued (the check ruled out running past 2^32 - 2: id_bound), names in (set, first entry) order
+    w->n_names += n_new;
+    w->id_bound += n_new;
+    w->pool_used += nb;
+    w->g1 = w->n_names;
+    w->p1 = w->pool_used;
+    queue_names(ctx, w);
+    w->mark();
+    w->last_cnt[0] = cnt[0], w->last_cnt[1] = cnt[1];
+    if (cnt[0] + cnt[1] == 0) return true;
+    if (!w->recs) {
+        w->recs = new jg_orset();
+        w->recs->ctx = ctx;
+    }
+    jg::set_dense(ctx, w->recs->add, cnt[0]);
+    jg::set_dense(ctx, w->recs->rem, cnt[1]);
+    w->recs->add.next = w->recs->rem.next = t_next;
+    jg_stream_soa& a = w->recs->add;
+    jg_stream_soa& r = w->recs->rem;
+    hipLaunchKernelGGL(k_cb_records, dim3((unsigned)n_sets, 2), dim3(kCbBlock), 0, ctx->stream, S, ST, RT, B, w->sid_id.as<uint32_t>(),
+                       a.key.as<unsigned long long>(), a.tag.as<Tag16>(), a.ord.as<uint32_t>(), r.key.as<unsigned long long>(), r.tag.as<Tag16>(),
+                       r.ord.as<uint32_t>());
+    JG_HIP(hipGetLastError());
+    jg::orset_merge_store(s, w->recs);
+    return true;
+}
+
 // Commit from the wave's tables: the distinct strings whose first entry lies before the limit resolved against
 // the element table (new ones take ids in (set, first entry) order), the distinct records before the limit
 // keyed, sorted and unioned into the store; ords = first tag slot (ordered like commit order, < next).
@@ -1456,12 +1546,17 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     JG_HIP(hipGetLastError());
     ST.list = w->st_packed.as<uint32_t>();  // the commit kernels read the packed lists
     RT.list = w->rt_packed.as<uint32_t>();
+    if (ns) ensure_names(ctx, w, ns, w->wnb);  // room for every listed string (an upper bound of the new ones)
+    if (commit_buckets(s, w, ST, RT, ns, nrec, csi_lim, t_lim, t_next)) {
+        if (tr) std::fprintf(stderr, "commit_tables: bucket commit %.0f us (%llu strings, %llu records listed)\n", now() - tc[0],
+                             (unsigned long long)ns, (unsigned long long)nrec);
+        return;
+    }
     // strings: each looked up (new ones keyed by (set, first entry), known ones kNone), all sorted by that key
     // (known last), new ids assigned in that order; no host round trip until the record counts are read
     const unsigned long long init[4] = {0, 0, w->pool_used, 0};
     JG_HIP(hipMemcpyAsync(st, init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
     if (ns) {
-        ensure_names(ctx, w, ns, w->wnb);  // room for every listed string (an upper bound of the new ones)
         ensure(w->newk, ns * 8);
         ensure(w->snk, ns * 8);
         ensure(w->snv, ns * 4);

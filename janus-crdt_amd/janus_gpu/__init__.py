@@ -554,6 +554,11 @@ class ORSetStore:
         bad = _u64(0)
         rc = load().jg_orset_wave_check(self._h, C.byref(bad))
         first_bad = None if bad.value == 2**64 - 1 else bad.value
+        if rc != JG_OK and first_bad is None:  # the check itself failed (no message to cut at): nothing applies
+            buf = C.create_string_buffer(1024)
+            load().jg_last_error(buf, 1024)
+            load().jg_orset_wave_abort(self._h)
+            raise JanusError(rc, buf.value.decode(errors="replace"))
         lim = (n if first_bad is None else first_bad) if limit is None else limit
         _check(load().jg_orset_wave_commit(self._h, lim))
         return rc, first_bad

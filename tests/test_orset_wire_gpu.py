@@ -65,7 +65,14 @@ def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3)
         s.close()
 
 
-TAIL = ["tables", "sort"]  # JANUS_ORSET_TAIL: the per-chunk string / record tables (strict: no fall-back), or the sort path
+# JANUS_ORSET_TAIL: the per-chunk string / record tables (strict: no fall-back), committed by set buckets
+# (JANUS_ORSET_COMMIT=buckets, strict) or by the radix path; or the sort path
+TAIL = ["tables", "tables-radix", "sort"]
+
+
+def _tail(monkeypatch, tail):
+    monkeypatch.setenv("JANUS_ORSET_TAIL", "tables" if tail.startswith("tables") else tail)
+    monkeypatch.setenv("JANUS_ORSET_COMMIT", "radix" if tail == "tables-radix" else "buckets")
 PARSE = ["auto", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
 
 
@@ -74,7 +81,7 @@ PARSE = ["auto", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_grou
 @pytest.mark.parametrize("seed,n_sets,waves,per_wave", [(1, 3, 3, 40), (2, 64, 3, 600), (3, 500, 2, 3000)])
 def test_waves_match_oracle(ctx, seed, n_sets, waves, per_wave, parse, tail, monkeypatch):
     monkeypatch.setenv("JANUS_ORSET_PARSE", parse)
-    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
+    _tail(monkeypatch, tail)
     _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default", "raw", "all"))
 
 
@@ -84,7 +91,7 @@ def test_compact_waves_match_oracle(ctx, parse, tail, monkeypatch):
     """Reference-shaped compact states only (ASCII names, no whitespace, members in the encoder's order):
     every message takes the group parse (JANUS_ORSET_PARSE=group rejects any message it leaves), and
     with JANUS_ORSET_TAIL=tables every wave commits from the per-chunk tables."""
-    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
+    _tail(monkeypatch, tail)
     if parse == "group":
         monkeypatch.setenv("JANUS_ORSET_PARSE", "group")
     rng = np.random.default_rng(11)
@@ -419,5 +426,36 @@ def test_element_id_space_limit(ctx):
         assert all(len(x) == 0 for x in s.read())
         s.merge_json([0], [J.encode_orset([("a", [G1]), ("b", [G2])], [])])
         assert s.wave_names() == [(0, 0xFFFFFFFC, b"a"), (0, 0xFFFFFFFD, b"b")]
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("commit", ["buckets", "radix", "auto"])
+def test_big_set_buckets_fall_back(ctx, commit, monkeypatch):
+    """A set with more new names / records in one wave than the bucket commit's LDS sorts hold (2048) takes the
+    radix path (auto), is refused under JANUS_ORSET_COMMIT=buckets, and either way the ids and records equal
+    the oracle's."""
+    monkeypatch.setenv("JANUS_ORSET_TAIL", "tables")
+    monkeypatch.setenv("JANUS_ORSET_COMMIT", commit)
+    rng = np.random.default_rng(41)
+    # 60 states of 45 new names each, all of set 0 (spread over the tables' sub-lists), then a small set
+    big = [(f"b{j}", J.random_guids(rng, 1)) for j in range(2700)]
+    msgs = [J.encode_orset(big[k:k + 45], []) for k in range(0, 2700, 45)] + [J.encode_orset([("x", J.random_guids(rng, 2))], [])]
+    sets = [0] * 60 + [1]
+    model = {}
+    ea, er, bad, _ = orc.orset_apply_json(sets, msgs, model)
+    assert bad is None
+    s = jg.ORSetStore(ctx)
+    try:
+        if commit == "buckets":
+            with pytest.raises(jg.JanusError) as e:
+                s.wave([(sets[:30], msgs[:30]), (sets[30:], msgs[30:])])
+            assert e.value.code == jg.JG_ESTATE and "bucket" in str(e.value)
+            return
+        rc, first_bad = s.wave([(sets[:30], msgs[:30]), (sets[30:], msgs[30:])])
+        assert rc == jg.JG_OK and first_bad is None
+        ga, gr = s.read()
+        assert orc.same_orset(ga, gr, ea, er)
+        assert s.wave_names() == _model_names(model, {})
     finally:
         s.close()
