@@ -500,17 +500,19 @@ def bench_apply_loop(sync, rank, world, local):
     return res
 
 
-def run_direct(exe_name, args, local):
-    """One apply-loop bench binary with --direct (the wave laid out in page-locked memory, uploaded in place)."""
+def run_direct(exe_name, args, local, mode="--direct"):
+    """One apply-loop bench binary with --direct (the wave laid out in page-locked memory, uploaded in place) or
+    --arena (bench_apply: the caller's own copy of the wave into a jg_host_alloc arena, timed)."""
     import subprocess
-    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / exe_name)] + args + ["--device", str(local), "--direct"],
+    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / exe_name)] + args + ["--device", str(local), mode],
                          capture_output=True, text=True, timeout=240)
     if out.returncode != 0 or not out.stdout.strip():
         return {"error": out.stderr[-500:]}
     res = json.loads(out.stdout.strip().splitlines()[-1])
     res["roofline"] = apply_roofline(res)
-    return {k: res.get(k) for k in ("ms_per_wave", "msgs_per_s", "library_ms_per_wave", "setup_ms_per_wave", "loop_ms_per_wave",
-                                    "device_wait_ms_per_wave", "device_busy_ms_per_wave", "uploaded_bytes_per_wave", "roofline")}
+    return {k: res.get(k) for k in ("ms_per_wave", "msgs_per_s", "caller_flatten_ms_per_wave", "library_ms_per_wave", "setup_ms_per_wave",
+                                    "loop_ms_per_wave", "device_wait_ms_per_wave", "device_busy_ms_per_wave", "uploaded_bytes_per_wave",
+                                    "roofline")}
 
 
 def bench_apply_direct(local):
@@ -808,6 +810,11 @@ def main():
         apply_orset["from_pinned"] = guarded(run_direct, "bench_orset", ["--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "0"], local)
     if apply_c1 is not None and "error" not in apply_c1:
         apply_c1["from_pinned"] = guarded(run_direct, "bench_c1", ["--waves", "3", "--no-cpu"], local)
+    # what a C# caller without page-locked receive buffers pays: its own parallel copy of every
+    # committed byte[] into a jg_host_alloc arena (plain cached copies, Span.CopyTo), then the in-place upload
+    if apply_direct is not None and "error" not in apply_direct:
+        apply_direct["caller_arena"] = guarded(run_direct, "bench_apply", ["--accounts", "1000000", "--ops", "1000000", "--waves", "3",
+                                                                           "--cpu-msgs", "0"], local, "--arena")
     sync.close()
     if rank != 0:
         return

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "janus_gpu.h"
 
@@ -179,6 +180,11 @@ struct jg_stream_soa {
     bool dense = true;    // chunks full except the last (slot = rank): uploads and generated streams
     void reserve_records(uint64_t records);  // room for a dense stream or a union output of `records`
     void swap(jg_stream_soa& o);
+    std::vector<void*> retired;  // blocks of earlier reservations, freed with the stream (reserve_records)
+    jg_stream_soa() = default;
+    jg_stream_soa(const jg_stream_soa&) = delete;
+    jg_stream_soa& operator=(const jg_stream_soa&) = delete;
+    ~jg_stream_soa();
 };
 
 struct jg_orset_wire;  // orset_wire.hip: element table + open payload wave (first use only)

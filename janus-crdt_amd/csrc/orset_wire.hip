@@ -931,7 +931,9 @@ struct jg_orset_wire {
         // or what jg_orset_names_since staged: names [since_from, since_to), pool [since_pool0, since_pool1)
         uint64_t since_from = UINT64_MAX, since_to = 0, since_pool0 = 0, since_pool1 = 0, since_bytes = 0;
     } nout;
+    std::vector<void*> retired;  // blocks the element table outgrew (grow_keep), freed with the wire
     ~jg_orset_wire() {
+        for (void* p : retired) (void)hipFree(p);
         if (nout.ev) (void)hipEventSynchronize(nout.ev);
         if (nout.host) (void)hipHostFree(nout.host);
         if (nout.ev) (void)hipEventDestroy(nout.ev);
@@ -945,7 +947,9 @@ void ensure(jg::DevBuf& b, size_t bytes) {
 }
 
 // Grow to `need` bytes keeping the first `keep` bytes; the new tail is zeroed when `zero`.
-void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero = false) {
+// retire: the old block goes there instead of hipFree (the element table grows wave after wave, and each
+// hipFree costs ~0.2 ms of host time on the box: six arrays per growth); freed with the wire.
+void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero = false, std::vector<void*>* retire = nullptr) {
     if (b.bytes >= need) return;
     if (ctx->copy) JG_HIP(hipStreamSynchronize(ctx->copy));  // uploads still landing in the old block
     jg::DevBuf nb;
@@ -956,6 +960,11 @@ void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero =
     JG_HIP(hipStreamSynchronize(ctx->stream));
     std::swap(nb.p, b.p);
     std::swap(nb.bytes, b.bytes);
+    if (retire && nb.p) {
+        retire->push_back(nb.p);
+        nb.p = nullptr;
+        nb.bytes = 0;
+    }
 }
 
 jg_orset_wire* wire_of(jg_orset* s) {
@@ -985,8 +994,8 @@ Names names_of(jg_orset_wire* w) {
 void ensure_sets(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_sets) {
     if (n_sets <= w->set_cap) return;
     const uint64_t cap = std::max<uint64_t>(n_sets + n_sets / 2, 1024);
-    grow_keep(ctx, w->set_gen, cap * 4, w->set_cap * 4, true);
-    grow_keep(ctx, w->next_id, cap * 4, w->set_cap * 4, true);
+    grow_keep(ctx, w->set_gen, cap * 4, w->set_cap * 4, true, &w->retired);
+    grow_keep(ctx, w->next_id, cap * 4, w->set_cap * 4, true, &w->retired);
     w->set_cap = w->set_gen.bytes / 4;
 }
 
@@ -997,20 +1006,25 @@ void ensure_names(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t poo
     JG_REQUIRE(total < 0xFFFFFFF0ull, JG_ESTATE, "OR-Set element table: more than 2^32 names");
     if (total > w->name_cap) {
         const uint64_t cap = std::max<uint64_t>(total + total / 2, 4096);
-        grow_keep(ctx, w->nset, cap * 4, w->n_names * 4);
-        grow_keep(ctx, w->nid, cap * 4, w->n_names * 4);
-        grow_keep(ctx, w->ngen, cap * 4, w->n_names * 4);
-        grow_keep(ctx, w->nlen, cap * 4, w->n_names * 4);
-        grow_keep(ctx, w->noff, cap * 8, w->n_names * 8);
-        grow_keep(ctx, w->nkey, cap * 8, w->n_names * 8);
+        grow_keep(ctx, w->nset, cap * 4, w->n_names * 4, false, &w->retired);
+        grow_keep(ctx, w->nid, cap * 4, w->n_names * 4, false, &w->retired);
+        grow_keep(ctx, w->ngen, cap * 4, w->n_names * 4, false, &w->retired);
+        grow_keep(ctx, w->nlen, cap * 4, w->n_names * 4, false, &w->retired);
+        grow_keep(ctx, w->noff, cap * 8, w->n_names * 8, false, &w->retired);
+        grow_keep(ctx, w->nkey, cap * 8, w->n_names * 8, false, &w->retired);
         w->name_cap = std::min({w->nset.bytes / 4, w->nid.bytes / 4, w->ngen.bytes / 4, w->nlen.bytes / 4, w->noff.bytes / 8, w->nkey.bytes / 8});
     }
     if (w->pool_used + pool_bytes > w->pool_cap) {
-        grow_keep(ctx, w->pool, std::max<uint64_t>(w->pool_used + pool_bytes, 1 << 20), w->pool_used);
+        grow_keep(ctx, w->pool, std::max<uint64_t>(w->pool_used + pool_bytes, 1 << 20), w->pool_used, false, &w->retired);
         w->pool_cap = w->pool.bytes;
     }
     if (w->tab_cap == 0 || 2 * total > w->tab_cap) {
         const uint64_t cap = pow2_at_least(4 * total);
+        if (w->tab.p) {  // retired, not freed (see grow_keep)
+            w->retired.push_back(w->tab.p);
+            w->tab.p = nullptr;
+            w->tab.bytes = 0;
+        }
         w->tab.alloc(cap * 8);
         w->tab_cap = cap;
         JG_HIP(hipMemsetAsync(w->tab.p, 0, cap * 8, ctx->stream));

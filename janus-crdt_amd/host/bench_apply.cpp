@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     uint64_t accounts = 1000000, ops = 1000000, cpu_msgs = 100000;
     int waves = 3, nodes = 4, device = 0, batch = 1000, threads_per_node = 3;  // 12 client threads (config example)
     uint32_t rank = 0, world = 1;
-    bool normal = false, parity = false, direct = false;
+    bool normal = false, parity = false, direct = false, arena = false;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--accounts") && i + 1 < argc) accounts = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--ops") && i + 1 < argc) ops = std::strtoull(argv[++i], nullptr, 10);
@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--normal")) normal = true;
         else if (!std::strcmp(argv[i], "--parity")) parity = true;
         else if (!std::strcmp(argv[i], "--direct")) direct = true;  // the wave received into page-locked memory
+        else if (!std::strcmp(argv[i], "--arena")) direct = arena = true;  // the caller copies the wave into page-locked memory (timed)
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) world = (uint32_t)std::atoi(argv[++i]);
@@ -202,10 +203,12 @@ int main(int argc, char** argv) {
         }
         // --direct: the wave as a transport receiving its blocks into jg_host_alloc memory would hold it (laid
         // out untimed: that copy is the receive path's), applied by the library's in-place upload
+        // --arena: a C# caller without page-locked receive buffers copies each committed byte[] into a jg_host_alloc
+        // arena itself (parallel Span.CopyTo = plain cached copies), timed as the caller's cost
         const double tp = now_s();
-        if (direct) gpu.PackCommitted(wave);
-        const double t0 = now_s();
-        if (direct && w > 0) pack_s += t0 - tp;
+        if (direct) gpu.PackCommitted(wave, !arena);
+        const double t0 = arena ? tp : now_s();
+        if (direct && w > 0) pack_s += now_s() - tp;
         const std::vector<uint64_t> done = direct ? gpu.ApplyPacked(&tracker_g) : gpu.ApplyCommitted(wave, &tracker_g);
         const double t1 = now_s();
         if (w == 0) {
@@ -276,11 +279,12 @@ int main(int argc, char** argv) {
         return ok ? 0 : 1;
     }
     const double W = waves;
+    if (arena) flat_s = pack_s;  // the caller's copy into the arena is its flatten (inside ms_per_wave)
     // per uploaded message the library moves its payload, 8 B offset, 16 B uid, 8 B identity, 1 B type
     const double pcie_bytes = (double)up_bytes + 33.0 * (double)up_msgs;
     std::printf("{\"workload\": \"C5 banking replay (BankingWorload.cs ops: view/deposit/transfer/withdraw at opsRatio [0.25, 0.25, 0.5], "
                 "every d an Increment; %s accounts %llu; %d nodes, clientBatchSize %d with state compaction; committed waves of %llu client ops)\", "
-                "\"waves\": %d, \"direct\": %s, \"untimed_pack_ms_per_wave\": %.3f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
+                "\"waves\": %d, \"direct\": %s, \"arena\": %s, \"untimed_pack_ms_per_wave\": %.3f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
                 "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"completed_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, "
                 "\"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
                 "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
@@ -288,7 +292,7 @@ int main(int argc, char** argv) {
                 "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %.1f, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
-                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, direct ? "true" : "false", 1e3 * pack_s / W, gpu_n / gpu_s,
+                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, direct ? "true" : "false", arena ? "true" : "false", arena ? 0.0 : 1e3 * pack_s / W, gpu_n / gpu_s,
                 (double)ops * waves / gpu_s, 1e3 * gpu_s / W, (double)gpu_n / W, (double)n_states / W, (double)n_safe / W, (double)n_done / W,
                 (double)payload_timed / std::max<uint64_t>(gpu_n, 1), 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W,
                 1e3 * busy_s / W, 1e3 * chunk_s / W, 1e3 * setup_s / W, 1e3 * loop_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,

@@ -271,7 +271,7 @@ std::vector<uint64_t> GpuStableStore::apply(const std::vector<const UpdateMessag
     return run_wave(wave, tracker, block_mode);
 }
 
-void GpuStableStore::PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates) {
+void GpuStableStore::PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates, bool nontemporal) {
     std::vector<const UpdateMessage*> blocks;
     for (const auto& list : updates)
         for (const auto& block : list) blocks.push_back(&block);
@@ -301,10 +301,11 @@ void GpuStableStore::PackCommitted(const std::vector<std::vector<UpdateMessage>>
                 w_uid_[i] = jg_guid{u->uid.lo, u->uid.hi};
                 w_type_[i] = u->syncMsgType == NetworkProtocol::CRDTMsg ? 1 : 0;
                 w_seq_[i] = u->seq;
-                out.put(reinterpret_cast<const char*>(u->message.data()), u->message.size());
+                if (nontemporal) out.put(reinterpret_cast<const char*>(u->message.data()), u->message.size());
+                else std::memcpy(p_bytes_ + p_off_[i], u->message.data(), u->message.size());
             }
         }
-        out.finish();
+        if (nontemporal) out.finish();
     });
     p_n_ = n;
 }

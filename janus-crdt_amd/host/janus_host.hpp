@@ -155,7 +155,9 @@ class GpuStableStore {
     // lays the wave out as such a receive path would (payloads back to back in jg_host_alloc memory + offsets),
     // ApplyPacked applies it with ONE jg_apply_committed that uploads the payloads in place (the library's
     // `direct` path: no gather into its staging).  Same results as ApplyCommitted on the same wave.
-    void PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates);
+    // nontemporal = false: plain cached copies (what a C# caller's parallel Span.CopyTo does, INTEGRATION.md §3;
+    // the upload then snoops the dirty lines)
+    void PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates, bool nontemporal = true);
     std::vector<uint64_t> ApplyPacked(SafeUpdateTracker* tracker = nullptr);
 
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/

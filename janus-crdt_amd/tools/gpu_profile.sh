@@ -1,33 +1,53 @@
 #!/bin/bash
-# Profile the bench on the GPU box: kernel trace + stats of every bench leg, then one PMC pass per counter
-# group (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950; SQ_INSTS_VALU for the JSON leg's
-# instruction roofline), then the per-launch HBM byte summary (pmc_summary.py).
+# Profile the bench on the GPU box, in ONE lease with the final bench line: kernel trace + stats of every bench
+# leg (incl. the OR-Set apply loop from page-locked payloads), one PMC pass per counter group (FETCH_SIZE and
+# WRITE_SIZE do not fit one pass on gfx950; SQ instruction / wait counters; TCC atomics / hits), the per-launch
+# summary (pmc_summary.py), then the default bench line itself.
 # Usage: gpu_profile.sh <outdir> [round label]
 set -o pipefail
 OUT=${1:-gpurun_out/prof}
-LABEL=${2:-r03}
+LABEL=${2:-r04}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
+step() { echo "[$(date +%H:%M:%S)] $*"; }
 trace() {  # trace <name> <seconds> <command...>
     local name=$1 secs=$2
     shift 2
-    timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run --output-format csv -- "$@" > "$OUT/$name.out" || exit 1
+    step "trace $name"
+    timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run --output-format csv -- "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || exit 1
 }
-trace trace 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload pnc-orset
-trace trace_exch 300 python3 bench.py --steps 16 --warmup 2 --no-cpu-baseline --workload exchange
-trace trace_digest 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload digest
-trace trace_json 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload json
-trace trace_apply 300 janus-crdt_amd/build/bench_apply --accounts 1000000 --ops 1000000 --waves 3 --cpu-msgs 0 --device 0
-trace trace_orset_loop 300 janus-crdt_amd/build/bench_orset --sets 2000 --msgs 200000 --waves 3 --cpu-msgs 0 --device 0
+pass() {  # pass <name> <counters> <command...>
+    local name=$1 ctr=$2
+    shift 2
+    step "pmc $name ($ctr)"
+    timeout -s KILL 150 rocprofv3 --pmc "$ctr" -d "$OUT/$name" -o run --output-format csv -- "$@" > "$OUT/$name.out" 2> "$OUT/$name.err" || exit 1
+}
+PNC_ORSET="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload pnc-orset"
+EXCH="python3 bench.py --steps 16 --warmup 2 --no-cpu-baseline --workload exchange"
+JSON="python3 bench.py --steps 8 --warmup 1 --no-cpu-baseline --workload json"
+DIGEST="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload digest"
+APPLY="janus-crdt_amd/build/bench_apply --accounts 1000000 --ops 1000000 --waves 3 --cpu-msgs 0 --device 0"
+ORSET_LOOP="janus-crdt_amd/build/bench_orset --sets 2000 --msgs 200000 --waves 3 --cpu-msgs 0 --device 0 --direct"
+SQ=SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES
+SQ2=SQ_ACTIVE_INST_ANY,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_WAIT_INST_LDS
+TCC=TCC_ATOMIC_sum,TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum
+trace trace 300 $PNC_ORSET
+trace trace_exch 300 $EXCH
+trace trace_digest 300 $DIGEST
+trace trace_json 300 $JSON
+trace trace_apply 300 $APPLY
+trace trace_orset_loop 300 $ORSET_LOOP
 for C in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $C -d "$OUT/pmc_$C" -o run --output-format csv -- \
-        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload pnc-orset > "$OUT/bench_pmc_$C.json" || exit 1
-    timeout -s KILL 120 rocprofv3 --pmc $C -d "$OUT/pmc_exch_$C" -o run --output-format csv -- \
-        python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload exchange > "$OUT/bench_pmc_exch_$C.json" || exit 1
-    timeout -s KILL 120 rocprofv3 --pmc $C -d "$OUT/pmc_json_$C" -o run --output-format csv -- \
-        python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload json > "$OUT/bench_pmc_json_$C.json" || exit 1
+    pass pmc_$C $C python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload pnc-orset
+    pass pmc_exch_$C $C python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload exchange
+    pass pmc_json_$C $C python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload json
+    pass pmc_orset_loop_$C $C $ORSET_LOOP
 done
-timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU -d "$OUT/sq_json" -o run --output-format csv -- \
-    python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload json > "$OUT/bench_sq_json.json" || exit 1
-python3 janus-crdt_amd/tools/pmc_summary.py "$OUT" "$OUT/pmc_$LABEL.json" "$LABEL" || exit 1
+pass sq_json $SQ python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload json
+pass sq2_json $SQ2 python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload json
+pass sq_orset_loop $SQ $ORSET_LOOP
+pass sq2_orset_loop $SQ2 $ORSET_LOOP
+pass tcc_orset_loop $TCC $ORSET_LOOP
+step summary
+python3 janus-crdt_amd/tools/pmc_summary.py "$OUT" "$OUT/pmc_$LABEL.json" "$LABEL" > "$OUT/pmc_summary.out" || exit 1
 echo profile-done
