@@ -475,6 +475,33 @@ def apply_roofline(res):
     return out
 
 
+def orset_decode_counters():
+    """The bound of the OR-Set apply loop's device work, named by its PMC counters: the per-kernel summary of
+    bench_orset --direct in the newest profiles/pmc_*.json (janus-crdt_amd/tools/pmc_summary.py: HBM bytes,
+    VALU issue share, the share of wave cycles parked on memory, L2 hit rate and atomics per wave).  The
+    dominant kernel's bound is the loop's: hbm (>= 50 % of 8 TB/s), valu (>= 50 % of the issue rate), or
+    latency (waves parked on memory with neither near its peak)."""
+    best = None
+    for p in sorted((ROOT / "profiles").glob("pmc_*.json")):
+        try:
+            d = json.loads(p.read_text())
+        except (OSError, ValueError):
+            continue
+        if "orset_wire" in d:
+            best = (d["orset_wire"]["kernels"], p.name)
+    if not best:
+        return None
+    ks = best[0]
+    timed_ks = sorted(((k, v) for k, v in ks.items() if v.get("us_per_wave")), key=lambda kv: -kv[1]["us_per_wave"])
+    if not timed_ks:
+        return None
+    top, tv = timed_ks[0]
+    keep = ("us_per_wave", "bound", "hbm_GBps", "valu_issue_frac", "wait_mem_frac", "tcc_hit_rate", "tcc_atomics_per_wave")
+    return {"bound": tv["bound"], "dominant_kernel": top, "kernels_us_per_wave": sum(v["us_per_wave"] for _, v in timed_ks),
+            "kernels": {k: {f: v.get(f) for f in keep} for k, v in timed_ks[:8]}, "source": best[1],
+            "scope": "bench_orset --direct per-chunk parse + tables + commit kernels, counters per wave"}
+
+
 def bench_apply_loop(sync, rank, world, local):
     """C5 committed-batch apply (the banking replay, BankingWorload.cs ops through the
     node batchers, 1M client ops per committed wave) through the C++ host mirror, on every rank.  Every
@@ -510,6 +537,8 @@ def run_direct(exe_name, args, local, mode="--direct"):
         return {"error": out.stderr[-500:]}
     res = json.loads(out.stdout.strip().splitlines()[-1])
     res["roofline"] = apply_roofline(res)
+    if exe_name == "bench_orset" and res["roofline"]:
+        res["roofline"]["decode_counters"] = orset_decode_counters()
     return {k: res.get(k) for k in ("ms_per_wave", "msgs_per_s", "caller_flatten_ms_per_wave", "library_ms_per_wave", "setup_ms_per_wave",
                                     "loop_ms_per_wave", "device_wait_ms_per_wave", "device_busy_ms_per_wave", "uploaded_bytes_per_wave",
                                     "roofline")}
@@ -805,6 +834,8 @@ def main():
     for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
         if leg is not None and "error" not in leg and "scaling" not in leg:
             leg["roofline"] = guarded(apply_roofline, leg)
+    if apply_orset is not None and isinstance(apply_orset.get("roofline"), dict):
+        apply_orset["roofline"]["decode_counters"] = guarded(orset_decode_counters)
     # the same OR-Set and C1 waves from page-locked payloads (one GPU: the shard shortcut gathers)
     if apply_orset is not None and "error" not in apply_orset and world == 1:
         apply_orset["from_pinned"] = guarded(run_direct, "bench_orset", ["--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "0"], local)

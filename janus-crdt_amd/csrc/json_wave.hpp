@@ -36,13 +36,48 @@ enum : uint32_t { kSlow = 1, kMiss = 2, kDup = 4, kFail = 8 };
 template <int G>
 struct GroupShared {
     static constexpr int kGroups = kBlock / G;
-    uint4 buf[kGroups][kGroupBytes / 16];
+    // one spare window per message: the 8 messages of a wave start 4 LDS banks apart, so that the entry
+    // reads of phase 3 (lanes of different messages at similar offsets) do not all hit one bank
+    uint4 buf[kGroups][kGroupBytes / 16 + 1];
     Guid16 cols[kGroups][G];                       // the row's first G replica columns
     uint16_t tok[kGroups][kGroupTok];
     uint32_t mask[kGroups][2 * kMaskCols / 32];    // pass A: columns seen per vector (LDS: 7 workgroups per CU, not 6)
-    uint32_t ntok[kGroups], kn[kGroups], nn[kGroups], flags[kGroups];
+    uint32_t tk[kGroups];                          // tokens | the "nVector" token << 8 | "nVector" tokens seen << 16
+    uint32_t flags[kGroups];
     uint32_t geo[kGroups], row[kGroups], nc[kGroups];  // alignment offset | length << 4; the row, its columns
 };
+__device__ __forceinline__ uint32_t tk_ntok(uint32_t tk) { return tk & 0xFFu; }
+__device__ __forceinline__ uint32_t tk_kn(uint32_t tk) { return (tk >> 8) & 0xFFu; }
+__device__ __forceinline__ uint32_t tk_nn(uint32_t tk) { return tk >> 16; }
+
+// Inclusive prefix sum over the G lanes of a group (g = lane in group): row_shr DPP moves for groups inside
+// one 16-lane row (no LDS round trip, no address arithmetic), ds_bpermute shuffles past that.
+template <int D>
+__device__ __forceinline__ uint32_t dpp_shr(uint32_t x) {  // lane - D of the same 16-lane row, 0 past its start
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + D, 0xF, 0xF, true);
+}
+template <int G>
+__device__ __forceinline__ uint32_t group_scan(uint32_t x, uint32_t g) {
+    if constexpr (G <= 16) {
+        if constexpr (G > 1) { const uint32_t y = dpp_shr<1>(x); x += g >= 1 ? y : 0u; }
+        if constexpr (G > 2) { const uint32_t y = dpp_shr<2>(x); x += g >= 2 ? y : 0u; }
+        if constexpr (G > 4) { const uint32_t y = dpp_shr<4>(x); x += g >= 4 ? y : 0u; }
+        if constexpr (G > 8) { const uint32_t y = dpp_shr<8>(x); x += g >= 8 ? y : 0u; }
+    } else {
+#pragma unroll
+        for (int d = 1; d < G; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, G);
+            if (g >= (uint32_t)d) x += y;
+        }
+    }
+    return x;
+}
+// x of the group's last lane, on every lane of the group (ds_swizzle in bitmask mode within 32 lanes)
+template <int G>
+__device__ __forceinline__ uint32_t group_last(uint32_t x) {
+    if constexpr (G <= 32) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, (int)((0x1Fu & ~(uint32_t)(G - 1)) | (uint32_t)(G - 1) << 5));
+    else return __shfl(x, G - 1, G);
+}
 
 __device__ __forceinline__ bool same(const Guid16& a, const Guid16& b) { return a.lo == b.lo && a.hi == b.hi; }
 
@@ -64,29 +99,28 @@ __device__ __forceinline__ unsigned long long wave_slot(bool want, unsigned long
 // grammar without whitespace; *tend = offset from q of the byte after the number.
 template <int EB>
 __device__ __forceinline__ bool entry_at(const uint8_t* base, uint32_t q, Guid16& g, long long& out, uint32_t* tend) {
-    uint32_t X[15];  // characters 0..59
-    lds_words<15>(base, q, X);
-    uint32_t n0, n1, nb, nc, nd, n6, n7, n8;
-    const uint32_t B = __builtin_amdgcn_alignbyte(X[3], X[2], 1);  // characters 9..12
-    const uint32_t C = __builtin_amdgcn_alignbyte(X[4], X[3], 2);  // 14..17
-    const uint32_t D = __builtin_amdgcn_alignbyte(X[5], X[4], 3);  // 19..22
-    bool ok = (hex4(X[0], n0) & hex4(X[1], n1) & hex4(B, nb) & hex4(C, nc) & hex4(D, nd) & hex4(X[6], n6) & hex4(X[7], n7) &
-               hex4(X[8], n8)) != 0;
-    ok &= (X[2] & 0xFFu) == '-' && ((X[3] >> 8) & 0xFFu) == '-' && ((X[4] >> 16) & 0xFFu) == '-' && (X[5] >> 24) == '-';
+    constexpr uint32_t kMaxDigits = EB == 4 ? 10 : 19;
+    constexpr int kYW = (kMaxDigits + 1 + 3) / 4;  // words holding the longest run and the character after it
+    uint32_t X[10 + kYW];                           // characters 0 .. 40 + 4 kYW
+    lds_words<10 + kYW>(base, q, X);
+    bool ok = jgw::guid_d(X, g.lo, g.hi);
     ok &= (X[9] & 0xFFFFu) == ('"' | ':' << 8);
-    g.lo = (unsigned long long)(hex_be16(n0) << 16 | hex_be16(n1)) | (unsigned long long)hex_be16(nb) << 32 |
-           (unsigned long long)hex_be16(nc) << 48;
-    g.hi = (unsigned long long)(hex_le16(nd) | hex_le16(n6) << 16) | (unsigned long long)(hex_le16(n7) | hex_le16(n8) << 16) << 32;
     // -?(0|[1-9][0-9]*) from character 38; more digits than the width can hold never pass the limit
     const uint32_t neg = ((X[9] >> 16) & 0xFFu) == '-' ? 1u : 0u;
-    uint32_t Y[5];
+    uint32_t Y[kYW];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) Y[k] = __builtin_amdgcn_alignbyte(X[10 + k], X[9 + k], 2 + neg);
-    uint32_t dm = 0;
+    for (int k = 0; k < kYW; ++k) Y[k] = __builtin_amdgcn_alignbyte(X[10 + k], X[9 + k], 2 + neg);
+    // the run of digits ends at the first non-digit: its flag bit (8j + 7 of word j / 4) by find-first-set per
+    // word, 32 k added with saturation so that a word of four digits (no bit: ~0) never wins the min.  (A
+    // 20-bit digit mask built with bits4 took ~100 VALU per entry.)
+    uint32_t first = UINT32_MAX;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) dm |= bits4(digit_bytes(Y[k])) << (4 * k);
-    const uint32_t run = (uint32_t)__builtin_ctz(~dm);
-    constexpr uint32_t kMaxDigits = EB == 4 ? 10 : 19;
+    for (int k = 0; k < kYW; ++k) {
+        const uint32_t nd = ~digit_bytes(Y[k]) & 0x80808080u;
+        const uint32_t b = nd ? (uint32_t)__builtin_ctz(nd) : UINT32_MAX;
+        first = min(first, __builtin_elementwise_add_sat(b, 32u * (uint32_t)k));
+    }
+    const uint32_t run = first == UINT32_MAX ? 4u * kYW : (first - 7) >> 3;  // > kMaxDigits either way when all are digits
     ok &= run >= 1 && run <= kMaxDigits && !((Y[0] & 0xFFu) == '0' && run > 1);
     // digits while any lane of the wave still has one (magnitudes of a few digits are the common
     // case); the first 7 in 24-bit multiply-adds (full rate: < 10^7), the rest in 64 bits
@@ -118,15 +152,16 @@ __device__ __forceinline__ bool lds_name_tail(const uint8_t* base, uint32_t q) {
            (X[2] & 0xFFu) == '{';
 }
 
-// A wave's parse result.  The tokens of the wave's 64 / G groups, in group order, are dealt over its
-// 64 lanes: round u of a lane holds wave token lane + 64u, tg = its group << 16 | its index there.
-// (Dealt over the group's own G lanes, ~7 tokens per message took two rounds on 8 lanes whenever
-// one message of the wave had more than 8.)
+// A wave's parse result.  The entry tokens (every token but the two names) of the wave's 64 / G groups,
+// in group order, are dealt over its 64 lanes: round u of a lane holds wave entry lane + 64u, tg = its
+// group << 16 | its token index there.  The two names are checked by lanes 0 and 1 of their group.  (All
+// tokens dealt, C5's ~7 tokens per message overflowed the 64 lanes of 8 messages in ~10 % of the waves,
+// and those paid a second round of the entry parse for a handful of tokens.)
 template <int EB, int G>
 struct GroupParse {
-    static constexpr int kRounds = (kGroupTok + G - 1) / G;
-    static_assert(64 % G == 0 && kRounds * 64 >= (64 / G) * (int)kGroupTok,
-                  "every token of the wave must have a lane: an unchecked token would pass the chain");
+    static constexpr int kRounds = ((64 / G) * ((int)kGroupTok - 2) + 63) / 64;
+    static_assert(64 % G == 0 && G >= 2 && kRounds * 64 >= (64 / G) * ((int)kGroupTok - 2),
+                  "every entry of the wave must have a lane: an unchecked token would pass the chain");
     Guid16 eg[kRounds];
     long long ev[kRounds];
     uint32_t tg[kRounds];
@@ -205,18 +240,12 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
             const uint32_t w = u * G + g;
             if (u * G * 16 >= a + L) break;  // group-uniform
             if (w * 16 < a + L) sh.buf[grp][w] = v[u];
-            uint32_t qm = bits4(zero_bytes(v[u].x ^ 0x22222222u)) | bits4(zero_bytes(v[u].y ^ 0x22222222u)) << 4 |
-                          bits4(zero_bytes(v[u].z ^ 0x22222222u)) << 8 | bits4(zero_bytes(v[u].w ^ 0x22222222u)) << 12;
-            const int base = (int)(16 * w) - (int)a;  // message position of byte 0 of this window
-            const int jlo = base >= 1 ? 0 : 1 - base, jhi = (int)L - base;  // bytes j with 1 <= base + j < L
-            qm &= jlo >= 16 || jhi <= 0 ? 0u : ((jhi >= 16 ? 0xFFFFu : (1u << jhi) - 1u) & ~((1u << jlo) - 1u));
+            uint32_t qm = jgw::quote_mask16(v[u]);
+            const int base = (int)(16 * w) - (int)a;                     // message position of byte 0 of this window
+            const int lo = base >= 1 ? 0 : 1 - base, hi = min((int)L - base, 16);  // bytes j with 1 <= base + j < L
+            qm &= hi > lo ? ((1u << (hi - lo)) - 1u) << lo : 0u;
             const uint32_t cnt = __popc(qm);
-            uint32_t incl = cnt;
-#pragma unroll
-            for (int d = 1; d < G; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d, G);
-                if (g >= (uint32_t)d) incl += y;
-            }
+            const uint32_t incl = group_scan<G>(cnt, g);
             uint32_t q = nq + incl - cnt;  // index of this lane's first quote in the window
             if (q & 1) qm &= qm - 1, ++q;  // an odd quote closes a string: start from the next one
             while (qm) {  // every other quote from here opens a token
@@ -226,7 +255,7 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
                 qm &= qm - 1;  // skip the closing quote
                 q += 2;
             }
-            nq += __shfl(incl, G - 1, G);
+            nq += group_last<G>(incl);
         }
     }
     const uint32_t ntok = (nq & 1) ? kGroupTok + 1 : nq >> 1;  // an unpaired quote: not the compact form
@@ -234,32 +263,49 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
     const uint32_t nt = go ? ntok : 0;
     if (g == 0) {
         sh.flags[grp] = go ? 0 : kSlow;
-        sh.kn[grp] = 0;
-        sh.nn[grp] = 0;
-        sh.ntok[grp] = nt;
+        sh.tk[grp] = nt;
         sh.geo[grp] = a | L << 4;
         sh.row[grp] = rc.row;
         sh.nc[grp] = rc.nc;
     }
     for (uint32_t i = g; i < 2 * kMaskCols / 32; i += G) sh.mask[grp][i] = 0;
     wave_sync();
-    // phase 2: the "nVector" token
-    const uint8_t* c = reinterpret_cast<const uint8_t*>(sh.buf[grp]) + a;
+    // phase 2: the "nVector" token (index and count in one word: with one such token its index is exact)
+    const uint8_t* buf = reinterpret_cast<const uint8_t*>(sh.buf[grp]);
+    const uint8_t* c = buf + a;
     for (uint32_t k = g; k < nt; k += G) {
         const uint32_t p = sh.tok[grp][k];
-        if (p + 1 < L && c[p + 1] == 'n') {
-            sh.kn[grp] = k;
-            atomicAdd(&sh.nn[grp], 1u);
-        }
+        if (p + 1 < L && c[p + 1] == 'n') atomicAdd(&sh.tk[grp], 1u << 16 | k << 8);
     }
     wave_sync();
-    // phase 3: each token checked (dealt over the wave), the chain from token 0 to the closing brace
+    // phase 3: the chain from token 0 to the closing brace.  The two names on lanes 0 and 1 of the group
+    // ("pVector" opens the message at byte 1; "nVector" follows the pVector's '}'), each with what follows
+    // its '{' (the vector's first entry, or '}' and then the next name / the message's end) ...
+    if (nt && g < 2) {
+        const uint32_t tk = sh.tk[grp], kn = tk_kn(tk);
+        const uint32_t k = g ? min(kn, nt - 1) : 0;
+        const uint32_t p = sh.tok[grp][k];
+        bool bad = tk_nn(tk) != 1 || kn == 0 || p + 12 > L || c[p + 1] != (g ? 'n' : 'p') || (g == 0 && (p != 1 || c[0] != '{')) ||
+                   !lds_name_tail(buf, a + p + 2);
+        if (!bad) {
+            const uint32_t q = p + 11;  // the byte after the name's '{'
+            const uint32_t pn = k + 1 < nt ? sh.tok[grp][k + 1] : UINT32_MAX;
+            if (c[q] == '}') bad = g ? (q + 2 != L || c[q + 1] != '}' || k + 1 != nt)    // empty nVector ends the message
+                                     : (q + 2 >= L || c[q + 1] != ',' || pn != q + 2 || k + 1 != kn);  // empty pVector, then nVector
+            else bad = pn != q || k + 1 == kn;  // the vector's first entry starts right after '{'
+        }
+        if (bad) atomicOr(&sh.flags[grp], (uint32_t)kSlow);
+    }
+    // ... and every entry, dealt over the wave
     constexpr uint32_t GW = 64 / G;  // groups per wave
     const uint32_t lane = threadIdx.x & 63, wg0 = (threadIdx.x >> 6) * GW;
     uint32_t base[GW + 1];
     base[0] = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < GW; ++j) base[j + 1] = base[j] + sh.ntok[wg0 + j];
+    for (uint32_t j = 0; j < GW; ++j) {
+        const uint32_t t = tk_ntok(sh.tk[wg0 + j]);
+        base[j + 1] = base[j] + (t >= 2 ? t - 2 : 0u);
+    }
 #pragma unroll
     for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
         gp.has[u] = false;
@@ -270,38 +316,25 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
 #pragma unroll
         for (uint32_t i = 1; i < GW; ++i)
             if (tw >= base[i]) { j = i; bj = base[i]; }
-        const uint32_t gq = wg0 + j, k = tw - bj;
-        const uint32_t geo = sh.geo[gq], aq = geo & 15u, Lq = geo >> 4, ntq = sh.ntok[gq], kn = sh.kn[gq];
+        const uint32_t gq = wg0 + j, e = tw - bj;
+        const uint32_t geo = sh.geo[gq], aq = geo & 15u, Lq = geo >> 4, tkq = sh.tk[gq], ntq = tk_ntok(tkq), kn = tk_kn(tkq);
+        const uint32_t k = e + 1 + (e + 1 >= kn ? 1u : 0u);  // entry e's token: tokens 0 and kn are the names
         const uint8_t* cq = reinterpret_cast<const uint8_t*>(sh.buf[gq]) + aq;
-        bool bad = k == 0 && (sh.nn[gq] != 1 || kn == 0 || cq[0] != '{');
-        do {
+        bool bad = false;
+        do {  // "<guid>":<int>
             const uint32_t p = sh.tok[gq][k];
             const uint32_t pn = k + 1 < ntq ? sh.tok[gq][k + 1] : UINT32_MAX;
-            const int c1 = p + 1 < Lq ? cq[p + 1] : -1;
-            uint32_t e = UINT32_MAX, next = UINT32_MAX;  // the '}' closing this token's vector / the next token's start
-            if (c1 == 'p' || c1 == 'n') {                // property name
-                if (p + 12 > Lq || !lds_name_tail(reinterpret_cast<const uint8_t*>(sh.buf[gq]), aq + p + 2) || (c1 == 'p' && (k != 0 || p != 1))) {
-                    bad = true;
-                    break;
-                }
-                const uint32_t q = p + 11;
-                if (cq[q] == '}') e = q;
-                else next = q;
-            } else {  // "<guid>":<int>
-                if (k == 0 || p + 41 > Lq) { bad = true; break; }
-                uint32_t tr;
-                const bool ok = entry_at<EB>(reinterpret_cast<const uint8_t*>(sh.buf[gq]), aq + p + 1, gp.eg[u], gp.ev[u], &tr);
-                const uint32_t t = p + 1 + tr;
-                if (!ok || t >= Lq) { bad = true; break; }
-                if (cq[t] == ',') next = t + 1;
-                else if (cq[t] == '}') e = t;
-                else { bad = true; break; }
-                gp.has[u] = true;
-                gp.tg[u] = gq << 16 | k;
-            }
-            if (next != UINT32_MAX) bad |= pn != next || k + 1 == kn;                 // another entry of this vector
-            else if (k < kn) bad |= e + 2 >= Lq || cq[e + 1] != ',' || pn != e + 2 || k + 1 != kn;  // pVector ends, nVector next
-            else bad |= e + 2 != Lq || cq[e + 1] != '}' || k + 1 != ntq;            // nVector ends the message
+            if (p + 41 > Lq) { bad = true; break; }
+            uint32_t tr;
+            const bool ok = entry_at<EB>(reinterpret_cast<const uint8_t*>(sh.buf[gq]), aq + p + 1, gp.eg[u], gp.ev[u], &tr);
+            const uint32_t t = p + 1 + tr;
+            if (!ok || t >= Lq) { bad = true; break; }
+            gp.has[u] = true;
+            gp.tg[u] = gq << 16 | k;
+            if (cq[t] == ',') bad = pn != t + 1 || k + 1 == kn;                                   // another entry of this vector
+            else if (cq[t] != '}') bad = true;
+            else if (k < kn) bad = t + 2 >= Lq || cq[t + 1] != ',' || pn != t + 2 || k + 1 != kn;  // pVector ends, nVector next
+            else bad = t + 2 != Lq || cq[t + 1] != '}' || k + 1 != ntq;                        // nVector ends the message
         } while (false);
         if (bad) atomicOr(&sh.flags[gq], (uint32_t)kSlow);
     }
@@ -335,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
             if (!gp.has[u] || (sh.flags[gq] & kSlow)) continue;
             const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
-            const uint32_t kn = sh.kn[gq], rq = sh.row[gq];
+            const uint32_t kn = tk_kn(sh.tk[gq]), rq = sh.row[gq];
             const uint32_t vv = k < kn ? 0 : 1;
             const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, sh.nc[gq], gp.eg[u], vv ? k - kn - 1 : k - 1);
             if (col == UINT32_MAX) {
@@ -360,7 +393,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             const uint32_t fq = sh.flags[gq];
             if (!gp.has[u] || (fq & (kSlow | kDup)) || !(fq & kMiss)) continue;
             const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
-            const uint32_t vv = k < sh.kn[gq] ? 0 : 1;
+            const uint32_t vv = k < tk_kn(sh.tk[gq]) ? 0 : 1;
             const uint32_t e = vv ? k - 2 : k - 1;
             uint8_t* h = emit + mq * emit_stride(EB);
             eguid[mq * kEmitMax + e] = gp.eg[u];
@@ -382,7 +415,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         }
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
-                (f & kDup) ? kReparse : (uint16_t)((sh.ntok[grp] - 2) | ((f & kMiss) ? kNeedsCols : 0u));
+                (f & kDup) ? kReparse : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
             if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
     }

@@ -72,17 +72,7 @@ __device__ __forceinline__ bool og_name_is(const uint8_t* c, uint32_t p, uint32_
 __device__ __forceinline__ bool og_guid(const uint8_t* lds, uint32_t q, Tag16& t) {
     uint32_t X[9];
     jgw::lds_words<9>(lds, q, X);
-    uint32_t n0, n1, nb, nc, nd, n6, n7, n8;
-    const uint32_t B = __builtin_amdgcn_alignbyte(X[3], X[2], 1);  // characters 9..12
-    const uint32_t C = __builtin_amdgcn_alignbyte(X[4], X[3], 2);  // 14..17
-    const uint32_t D = __builtin_amdgcn_alignbyte(X[5], X[4], 3);  // 19..22
-    bool ok = (jgw::hex4(X[0], n0) & jgw::hex4(X[1], n1) & jgw::hex4(B, nb) & jgw::hex4(C, nc) & jgw::hex4(D, nd) & jgw::hex4(X[6], n6) &
-               jgw::hex4(X[7], n7) & jgw::hex4(X[8], n8)) != 0;
-    ok &= (X[2] & 0xFFu) == '-' && ((X[3] >> 8) & 0xFFu) == '-' && ((X[4] >> 16) & 0xFFu) == '-' && (X[5] >> 24) == '-';
-    t.lo = (unsigned long long)(jgw::hex_be16(n0) << 16 | jgw::hex_be16(n1)) | (unsigned long long)jgw::hex_be16(nb) << 32 |
-           (unsigned long long)jgw::hex_be16(nc) << 48;
-    t.hi = (unsigned long long)(jgw::hex_le16(nd) | jgw::hex_le16(n6) << 16) | (unsigned long long)(jgw::hex_le16(n7) | jgw::hex_le16(n8) << 16) << 32;
-    return ok;
+    return jgw::guid_d(X, t.lo, t.hi);
 }
 
 __device__ __forceinline__ uint32_t og_prefix_le(unsigned long long ballot, uint32_t lane) {  // set bits at lanes <= lane
@@ -133,25 +123,19 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
         const uint32_t w = u * 64 + lane;
         sh.buf[wv][w] = v[u];
         const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        uint32_t qm = 0, bm = 0;
+        uint32_t badb[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            qm |= jgw::bits4(jgw::zero_bytes(x[i] ^ 0x22222222u)) << (4 * i);
-            const uint32_t badb = (x[i] | jgw::le_bytes(x[i] & 0x7F7F7F7Fu, 0x1F) | jgw::zero_bytes(x[i] ^ 0x5C5C5C5Cu)) & 0x80808080u;
-            bm |= jgw::bits4(badb) << (4 * i);
-        }
+        for (int i = 0; i < 4; ++i)  // backslash, control or non-ASCII
+            badb[i] = (x[i] | jgw::le_bytes(x[i] & 0x7F7F7F7Fu, 0x1F) | jgw::zero_bytes(x[i] ^ 0x5C5C5C5Cu)) & 0x80808080u;
+        uint32_t qm = jgw::quote_mask16(v[u]);
+        const uint32_t bm = jgw::flags16(badb[0], badb[1], badb[2], badb[3]);
         // bytes of this window inside the message: span positions [a, a + L)
-        const int lo = (int)a - (int)(16 * w), hi = (int)span - (int)(16 * w);
-        const uint32_t in = hi <= 0 || lo >= 16 ? 0u : ((hi >= 16 ? 0xFFFFu : (1u << hi) - 1u) & ~(lo <= 0 ? 0u : (1u << lo) - 1u));
+        const int lo = max((int)a - (int)(16 * w), 0), hi = min((int)span - (int)(16 * w), 16);
+        const uint32_t in = hi > lo ? ((1u << (hi - lo)) - 1u) << lo : 0u;
         qm &= in;
         rej |= __ballot((bm & in) != 0) != 0;
         const uint32_t cnt = __popc(qm);
-        uint32_t incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if (lane >= (uint32_t)d) incl += y;
-        }
+        const uint32_t incl = jgw::wave_incl_scan(cnt);  // every lane of the wave is here (wave-uniform loop)
         uint32_t k = nq + incl - cnt;
         while (qm) {
             const int j = __ffs(qm) - 1;
@@ -159,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
             if (k < 2 * kOgTok) qp[k] = (uint16_t)(16 * w + j - a);
             ++k;
         }
-        nq += __shfl(incl, 63, 64);
+        nq += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
     const uint32_t ntok = nq >> 1;
     if (rej || (nq & 1) || ntok == 0 || ntok > kOgTok) {  // wave-uniform

@@ -92,6 +92,70 @@ __device__ __forceinline__ uint32_t hex_le16(uint32_t nib) {  // two hex-pair by
     const uint32_t t = hex_pairs(nib);
     return (t & 0xFFu) | ((t >> 8) & 0xFF00u);
 }
+// hex4 without the compare: 0x80 in each byte that is not a hex digit (0 when all four are), so that the
+// checks of a Guid's eight groups fold into one OR and one compare
+__device__ __forceinline__ uint32_t hex4_bad(uint32_t x, uint32_t& nib) {
+    const uint32_t x7 = x & 0x7F7F7F7Fu, l7 = x7 | 0x20202020u;
+    const uint32_t dig = ge_bytes(x7, 0x30) & le_bytes(x7, 0x39);
+    const uint32_t af = ge_bytes(l7, 0x61) & le_bytes(l7, 0x66);
+    nib = (x & 0x0F0F0F0Fu) + ((af >> 7) | (af >> 4));
+    return (~(dig | af) | x) & 0x80808080u;
+}
+
+// The 36-character "D" form in X[0..8] (characters 0..35, Guid.ToString() layout b3b2b1b0-b5b4-b7b6-b8b9-b10..b15)
+// in C#'s byte order (lo = bytes 0..7, hi = 8..15); true iff every digit is hex and the dashes sit at 8, 13, 18,
+// 23.  Digit pairs combine with one shift-or per group (byte 0 = characters 0-1, byte 2 = 2-3) and the bytes
+// land in place with one v_perm per half word pair.
+__device__ __forceinline__ bool guid_d(const uint32_t* X, unsigned long long& lo, unsigned long long& hi) {
+    uint32_t n[8];
+    const uint32_t bad = hex4_bad(X[0], n[0]) | hex4_bad(X[1], n[1]) | hex4_bad(__builtin_amdgcn_alignbyte(X[3], X[2], 1), n[2]) |
+                         hex4_bad(__builtin_amdgcn_alignbyte(X[4], X[3], 2), n[3]) | hex4_bad(__builtin_amdgcn_alignbyte(X[5], X[4], 3), n[4]) |
+                         hex4_bad(X[6], n[5]) | hex4_bad(X[7], n[6]) | hex4_bad(X[8], n[7]);
+    // characters 8, 13, 18, 23 gathered into one word
+    const uint32_t dashes = __builtin_amdgcn_perm(X[3], X[2], 0x0C0C0500u) | __builtin_amdgcn_perm(X[5], X[4], 0x07020C0Cu);
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = n[i] << 4 | n[i] >> 8;  // valid only where every digit is (< 16)
+    // group a big-endian into bytes 0..3, b and c big-endian into 4..5 / 6..7, the rest in text order
+    lo = (unsigned long long)__builtin_amdgcn_perm(t[0], t[1], 0x04060002u) | (unsigned long long)__builtin_amdgcn_perm(t[3], t[2], 0x04060002u) << 32;
+    hi = (unsigned long long)__builtin_amdgcn_perm(t[5], t[4], 0x06040200u) | (unsigned long long)__builtin_amdgcn_perm(t[7], t[6], 0x06040200u) << 32;
+    return bad == 0 && dashes == 0x2D2D2D2Du;
+}
+
+// ---- quote positions of a 16-byte window -----------------------------------------------------------------
+__device__ __forceinline__ uint32_t quote_flags(uint32_t x) {  // 0x80 in each byte equal to '"'
+    return ~((((x & 0x7F7F7F7Fu) ^ 0x22222222u) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+// 0x80 byte flags of a window's four words (bit 8k + 7 of word i) -> bit 4i + k: a 4x4 bit transpose (two delta
+// swaps) and one byte gather, 17 operations instead of 31 for four bits4
+__device__ __forceinline__ uint32_t flags16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3) {
+    uint32_t u = f0 >> 7 | f1 >> 6 | f2 >> 5 | f3 >> 4;  // bit 8k + i
+    uint32_t t = ((u >> 14) ^ u) & 0x00000C0Cu;  // swap the off-diagonal 2x2 blocks
+    u ^= t ^ (t << 14);
+    t = ((u >> 7) ^ u) & 0x000A000Au;  // then the off-diagonal bits inside each block: bit 8i + k
+    u ^= t ^ (t << 7);
+    u |= u >> 4;
+    return __builtin_amdgcn_perm(u, u, 0x0C0C0200u);  // bytes 0 and 2
+}
+// bit j = byte j of the window is '"'
+__device__ __forceinline__ uint32_t quote_mask16(uint4 v) {
+    return flags16(quote_flags(v.x), quote_flags(v.y), quote_flags(v.z), quote_flags(v.w));
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave: row_shr DPP moves inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry a row's total into the rows after it (no LDS, no address arithmetic; a
+// __shfl_up ladder costs a ds_bpermute and ~6 VALU per step).  Every lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t r = threadIdx.x & 15;
+    uint32_t y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true); x += r >= 1 ? y : 0u;  // row_shr:1
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true); x += r >= 2 ? y : 0u;  // row_shr:2
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true); x += r >= 4 ? y : 0u;  // row_shr:4
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true); x += r >= 8 ? y : 0u;  // row_shr:8
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); x += y;  // row_bcast:15 -> rows 1, 3
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); x += y;  // row_bcast:31 -> rows 2, 3
+    return x;
+}
 
 // K words of LDS bytes [q, q + 4K) at any alignment: K + 1 aligned reads, realigned in registers.
 template <int K>
