@@ -128,6 +128,7 @@ int jg_open(int device, jg_ctx** out) {
             }
             c->flags.alloc(256);
             JG_HIP(hipMemset(c->flags.p, 0, 256));
+            JG_HIP(hipHostMalloc(&c->hstat, 256, hipHostMallocDefault));
         } catch (...) {
             delete c;
             throw;
@@ -148,6 +149,7 @@ int jg_close(jg_ctx* ctx) {
         ctx->scratch2.release();
         ctx->scratch3.release();
         ctx->flags.release();
+        if (ctx->hstat) (void)hipHostFree(ctx->hstat);
         (void)hipStreamDestroy(ctx->stream);
         if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
         if (ctx->copied) (void)hipEventDestroy(ctx->copied);

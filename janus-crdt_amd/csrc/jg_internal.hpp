@@ -107,6 +107,7 @@ struct jg_ctx {
     jg::DevBuf scratch2;
     jg::DevBuf scratch3;
     jg::DevBuf flags;    // small zero-initialised status words (error flags)
+    void* hstat = nullptr;  // 256 page-locked bytes for small status reads (a pageable D2H is staged by the runtime)
     hipStream_t copy = nullptr;    // wave uploads: chunk k+1's H2D overlaps chunk k's parse on `stream`
     hipEvent_t copied = nullptr;
     // pipelined digests (jg_waves_update_digests): wave k's second-level chains run on `side` while

@@ -36,6 +36,7 @@
 // P and N share one column per replica: the reference keeps two dictionaries whose key orders coincide
 // for every state its nodes produce (constructor inserts self into both, Merge inserts new keys in
 // message order), which the shared order reproduces.
+#include <cstring>
 #include <hipcub/hipcub.hpp>
 
 #include "jg_internal.hpp"
@@ -553,10 +554,15 @@ unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n,
 
 struct Status { unsigned long long first_bad, n_deferred, resolve_bad, n_slow, n_resume; };
 
+static_assert(sizeof(Status) <= 256, "status fits the context's page-locked word");
+
+// Into the context's page-locked bytes: a pageable destination is staged by the runtime (a blit plus a host
+// copy per read; three reads per wave)
 Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     Status s;
-    JG_HIP(hipMemcpyAsync(&s, d, sizeof s, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipMemcpyAsync(ctx->hstat, d, sizeof s, hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
+    std::memcpy(&s, ctx->hstat, sizeof s);
     return s;
 }
 
@@ -608,9 +614,16 @@ WaveScratch wave_scratch(jg_pnc* p, uint64_t n, uint64_t keep = 0) {
                        p->wslow.as<unsigned long long>()};
 }
 
+__global__ void k_reset_status(unsigned long long* status) {
+    const unsigned long long init[5] = {~0ull, 0, ~0ull, 0, 0};  // Status{first_bad, n_deferred, resolve_bad, n_slow, n_resume}
+    if (threadIdx.x < 5) status[threadIdx.x] = init[threadIdx.x];
+}
+
+// a one-wave kernel instead of a copy from pageable host memory (staged by the runtime: a blit and a host
+// round trip in front of every wave's pass A)
 void reset_status(jg_ctx* ctx, unsigned long long* status) {
-    static const Status init{~0ull, 0, ~0ull, 0, 0};
-    JG_HIP(hipMemcpyAsync(status, &init, sizeof init, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_reset_status, dim3(1), dim3(64), 0, ctx->stream, status);
+    JG_HIP(hipGetLastError());
 }
 
 void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1,

@@ -207,7 +207,10 @@ __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16
 template <int EB, int G>
 __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                             uint64_t m, bool live, const RowCache& rc, GroupParse<EB, G>& gp) {
-    constexpr uint32_t NW = (kGroupBytes / 16 + G - 1) / G;  // windows per lane
+    // 32-byte windows (two aligned 16-byte loads per lane per round): at 8 lanes two rounds cover a message
+    // (16-byte windows took four, the fourth for the quarter of C5's messages past 384 bytes, and every round
+    // pays the group scan, the range mask and the token loop's set-up)
+    constexpr uint32_t NW = (kGroupBytes / 32 + G - 1) / G;  // windows per lane
     const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
     uint64_t beg = 0, len = 0;
     if (live) {
@@ -218,13 +221,14 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
     const bool fit = live && len >= kCompactMin && len + a <= kGroupBytes;
     const uint32_t L = fit ? (uint32_t)len : 0;
     // phase 1: every window load issued first, then stored to LDS and scanned for token starts
-    uint4 v[NW];
+    uint4 v[NW][2];
     if (fit) {
         const uint8_t* src = bytes + (beg & ~15ull);
 #pragma unroll
         for (uint32_t u = 0; u < NW; ++u) {
             const uint32_t w = u * G + g;
-            v[u] = w * 16 < a + L ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 16) : make_uint4(0, 0, 0, 0);
+            v[u][0] = 32 * w < a + L ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 32) : make_uint4(0, 0, 0, 0);
+            v[u][1] = 32 * w + 16 < a + L ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 32 + 16) : make_uint4(0, 0, 0, 0);
         }
     }
     if (rc.has && g < rc.nc) sh.cols[grp][g] = rc.cg;
@@ -238,12 +242,14 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
 #pragma unroll
         for (uint32_t u = 0; u < NW; ++u) {
             const uint32_t w = u * G + g;
-            if (u * G * 16 >= a + L) break;  // group-uniform
-            if (w * 16 < a + L) sh.buf[grp][w] = v[u];
-            uint32_t qm = jgw::quote_mask16(v[u]);
-            const int base = (int)(16 * w) - (int)a;                     // message position of byte 0 of this window
-            const int lo = base >= 1 ? 0 : 1 - base, hi = min((int)L - base, 16);  // bytes j with 1 <= base + j < L
-            qm &= hi > lo ? ((1u << (hi - lo)) - 1u) << lo : 0u;
+            if (u * G * 32 >= a + L) break;  // group-uniform
+            if (32 * w < a + L) sh.buf[grp][2 * w] = v[u][0];
+            if (32 * w + 16 < a + L) sh.buf[grp][2 * w + 1] = v[u][1];
+            uint32_t qm = jgw::quote_mask16(v[u][0]) | jgw::quote_mask16(v[u][1]) << 16;
+            const int base = (int)(32 * w) - (int)a;                     // message position of byte 0 of this window
+            const int lo = base >= 1 ? 0 : 1 - base, hi = min((int)L - base, 32);  // bytes j with 1 <= base + j < L
+            const uint32_t width = (uint32_t)(hi - lo);
+            qm &= hi > lo ? (width >= 32 ? ~0u : (1u << width) - 1u) << lo : 0u;
             const uint32_t cnt = __popc(qm);
             const uint32_t incl = group_scan<G>(cnt, g);
             uint32_t q = nq + incl - cnt;  // index of this lane's first quote in the window

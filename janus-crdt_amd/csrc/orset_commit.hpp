@@ -81,10 +81,12 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
         if (T.first[sid] < s_lim) {
             const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
             const uint32_t set = S.set[ref], len = S.meta[ref] & 0x7FFFFFFFu;
-            const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], len);
-            if (id != kNoName) {
-                sid_id[sid] = id;
-            } else {
+            uint32_t id = sid_id[sid];  // looked up when the chunk's k_ow_strings claimed the slot
+            if (id == kUnresolved) {
+                id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], len);
+                if (id != kNoName) sid_id[sid] = id;
+            }
+            if (id == kNoName) {
                 s_new = true;
                 s_set = set;
                 s_len = len;

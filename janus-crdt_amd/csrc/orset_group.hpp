@@ -28,7 +28,7 @@
 
 constexpr uint32_t kOgBytes = 4096;            // LDS bytes per message: payload + its 16-B alignment offset
 constexpr uint32_t kOgWin = kOgBytes / 16;     // windows per message
-constexpr uint32_t kOgRounds = kOgWin / 64;    // window rounds of the wave
+constexpr uint32_t kOgRounds = kOgBytes / 32 / 64;  // rounds of 32-byte windows (two 16-byte loads per lane)
 constexpr uint32_t kOgTok = 192;               // string tokens per message (a compact 4 KB state has < 190)
 constexpr uint32_t kOgTokRounds = kOgTok / 64;
 constexpr int kOgWaves = kBlock / 64;          // messages per workgroup
@@ -107,31 +107,40 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
     uint8_t* lds = reinterpret_cast<uint8_t*>(sh.buf[wv]);
     uint16_t* qp = sh.q[wv];
 
-    // phase 1: windows into LDS; quotes numbered; bytes the fast path does not take
-    uint4 v[kOgRounds];
+    // phase 1: windows into LDS; quotes numbered; bytes the fast path does not take.  32-byte windows: the
+    // ORSetWorkload state (~1.2 KB) is one round of the wave (16-byte windows took two, each paying the wave
+    // scan, the range masks and the token loop's set-up)
+    uint4 v[kOgRounds][2];
     const uint8_t* src = bytes + (b & ~15ull);
 #pragma unroll
     for (uint32_t u = 0; u < kOgRounds; ++u) {
         const uint32_t w = u * 64 + lane;
-        v[u] = w * 16 < span ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 16) : make_uint4(0, 0, 0, 0);
+        v[u][0] = 32 * w < span ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 32) : make_uint4(0, 0, 0, 0);
+        v[u][1] = 32 * w + 16 < span ? *reinterpret_cast<const uint4*>(src + (uint64_t)w * 32 + 16) : make_uint4(0, 0, 0, 0);
     }
     uint32_t nq = 0;
     bool rej = false;
 #pragma unroll
     for (uint32_t u = 0; u < kOgRounds; ++u) {
-        if (u * 64 * 16 >= span) break;  // wave-uniform
+        if (u * 64 * 32 >= span) break;  // wave-uniform
         const uint32_t w = u * 64 + lane;
-        sh.buf[wv][w] = v[u];
-        const uint32_t x[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-        uint32_t badb[4];
+        sh.buf[wv][2 * w] = v[u][0];
+        sh.buf[wv][2 * w + 1] = v[u][1];
+        uint32_t qm = 0, bm = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)  // backslash, control or non-ASCII
-            badb[i] = (x[i] | jgw::le_bytes(x[i] & 0x7F7F7F7Fu, 0x1F) | jgw::zero_bytes(x[i] ^ 0x5C5C5C5Cu)) & 0x80808080u;
-        uint32_t qm = jgw::quote_mask16(v[u]);
-        const uint32_t bm = jgw::flags16(badb[0], badb[1], badb[2], badb[3]);
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t x[4] = {v[u][h].x, v[u][h].y, v[u][h].z, v[u][h].w};
+            uint32_t badb[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)  // backslash, control or non-ASCII
+                badb[i] = (x[i] | jgw::le_bytes(x[i] & 0x7F7F7F7Fu, 0x1F) | jgw::zero_bytes(x[i] ^ 0x5C5C5C5Cu)) & 0x80808080u;
+            qm |= jgw::quote_mask16(v[u][h]) << (16 * h);
+            bm |= jgw::flags16(badb[0], badb[1], badb[2], badb[3]) << (16 * h);
+        }
         // bytes of this window inside the message: span positions [a, a + L)
-        const int lo = max((int)a - (int)(16 * w), 0), hi = min((int)span - (int)(16 * w), 16);
-        const uint32_t in = hi > lo ? ((1u << (hi - lo)) - 1u) << lo : 0u;
+        const int lo = max((int)a - (int)(32 * w), 0), hi = min((int)span - (int)(32 * w), 32);
+        const uint32_t width = (uint32_t)(hi - lo);
+        const uint32_t in = hi > lo ? (width >= 32 ? ~0u : (1u << width) - 1u) << lo : 0u;
         qm &= in;
         rej |= __ballot((bm & in) != 0) != 0;
         const uint32_t cnt = __popc(qm);
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__
         while (qm) {
             const int j = __ffs(qm) - 1;
             qm &= qm - 1;
-            if (k < 2 * kOgTok) qp[k] = (uint16_t)(16 * w + j - a);
+            if (k < 2 * kOgTok) qp[k] = (uint16_t)(32 * w + j - a);
             ++k;
         }
         nq += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);

@@ -29,6 +29,7 @@
 #pragma once
 
 constexpr uint32_t kNoSid = 0xFFFFFFFFu;
+constexpr uint32_t kUnresolved = 0xFFFFFFFEu;  // sid_id of a string not looked up at claim time (ids stay below it)
 constexpr uint32_t kProbeCap = 256;  // probes before a table insert gives up (the wave falls back)
 constexpr uint32_t kDupScan = 512;   // entries per message the in-wave duplicate check holds in LDS
 constexpr int kTabWaves = kBlock / 64;
@@ -88,10 +89,16 @@ __device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* byte
     return len_a <= 8 || same_bytes(bytes + S.noff[b] + 8, bytes + noff_a + 8, len_a - 8);
 }
 
+// The lane that claims a string's slot also looks the string up in the store's element table (N: committed
+// names, unchanged until the wave commits) and leaves the answer in sid_id[slot] (an id, kNoName for a new
+// string, kUnresolved when the table or the set's generation word does not exist yet): the commit's
+// per-string lookup — a chain of dependent random loads, 141 us behind the last upload of the ORSetWorkload
+// wave — runs here, under the next chunk's upload.
 __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                        const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ ne,
                                                        const uint32_t* __restrict__ na, uint64_t m0, uint64_t m1, StrTab T,
-                                                       unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow) {
+                                                       unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow,
+                                                       Names N, uint32_t set_lim, uint32_t* __restrict__ sid_id) {
     __shared__ uint32_t sh[kTabWaves][kDupScan];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                 if (w == 0) {
                     sid = (uint32_t)p;
                     fresh = true;
+                    sid_id[sid] = set < set_lim ? tab_find(N, key, set, bytes + noff, len) : kUnresolved;
                     break;
                 }
             }
@@ -261,15 +269,6 @@ __global__ void k_ow_sresolve(Sparse S, const uint8_t* __restrict__ bytes, StrTa
     const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], S.meta[ref] & 0x7FFFFFFFu);
     sid_id[sid] = id;
     newk[i] = id != kNoName ? kNone : ((unsigned long long)set << 32 | T.first[sid]);
-}
-
-__global__ void k_ow_gather_newsid(const unsigned long long* __restrict__ newk, const uint32_t* __restrict__ live,
-                                   const uint32_t* __restrict__ idx, const unsigned long long* __restrict__ count,
-                                   unsigned long long* __restrict__ keys, uint32_t* __restrict__ sids) {
-    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= *count) return;
-    keys[j] = newk[idx[j]];
-    sids[j] = live[idx[j]];
 }
 
 // New strings sorted by (set, first entry): the r-th new string of a set takes next_id + r (k_ow_assign's
