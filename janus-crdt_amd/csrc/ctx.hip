@@ -128,7 +128,7 @@ int jg_open(int device, jg_ctx** out) {
             }
             c->flags.alloc(256);
             JG_HIP(hipMemset(c->flags.p, 0, 256));
-            JG_HIP(hipHostMalloc(&c->hstat, 256, hipHostMallocDefault));
+            JG_HIP(hipHostMalloc(&c->hstat, jg::kPinBytes, hipHostMallocDefault));
         } catch (...) {
             delete c;
             throw;

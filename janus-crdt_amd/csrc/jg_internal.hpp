@@ -107,7 +107,10 @@ struct jg_ctx {
     jg::DevBuf scratch2;
     jg::DevBuf scratch3;
     jg::DevBuf flags;    // small zero-initialised status words (error flags)
-    void* hstat = nullptr;  // 256 page-locked bytes for small status reads (a pageable D2H is staged by the runtime)
+    // page-locked bytes for small status reads and writes (a pageable copy is staged by the runtime: a blit
+    // kernel plus a host copy, ~30-40 us of host gap per round trip): reads at [0, kPinRead), writes from
+    // kPinRead (jg::pin_get / pin_sync / pin_at)
+    void* hstat = nullptr;
     hipStream_t copy = nullptr;    // wave uploads: chunk k+1's H2D overlaps chunk k's parse on `stream`
     hipEvent_t copied = nullptr;
     // pipelined digests (jg_waves_update_digests): wave k's second-level chains run on `side` while
@@ -209,6 +212,16 @@ struct jg_orset {
 namespace jg {
 using CtxLock = std::unique_lock<std::recursive_mutex>;
 inline CtxLock lock(jg_ctx* c) { return c ? CtxLock(c->mu) : CtxLock(); }
+constexpr size_t kPinRead = 32 << 10, kPinBytes = 64 << 10;
+// Queue a small device -> host read into the context's page-locked bytes at `at` (< kPinRead); several reads
+// share one pin_sync, then pin_at reads them.  Calls on a context are serialised (ctx->mu), and every reader
+// syncs before it returns, so the bytes are free at the start of each call.
+inline void pin_get(jg_ctx* ctx, size_t at, const void* d, size_t n) {
+    if (at + n > kPinRead) fail(JG_EINVAL, "pin_get: %zu bytes at %zu exceed the page-locked read area", n, at);
+    JG_HIP(hipMemcpyAsync(static_cast<char*>(ctx->hstat) + at, d, n, hipMemcpyDeviceToHost, ctx->stream));
+}
+inline void pin_sync(jg_ctx* ctx) { JG_HIP(hipStreamSynchronize(ctx->stream)); }
+inline const void* pin_at(jg_ctx* ctx, size_t at) { return static_cast<const char*>(ctx->hstat) + at; }
 template <class H> inline CtxLock lock(const H* h) { return lock(h ? h->ctx : nullptr); }
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);

@@ -24,6 +24,7 @@
 // is rare: key creation) and uploads the slots a registration touched before the next wave.
 // Tracker: open addressing over 16-B slots {identity, origin}, 0 = empty, ~0 = removed (a tombstone:
 // concurrent probes never see an entry move); rebuilt without tombstones when live + removed pass 1/2.
+#include <cstring>
 #include <hipcub/hipcub.hpp>
 
 #include <atomic>
@@ -790,24 +791,26 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         hipLaunchKernelGGL(k_count_sub, dim3(1), dim3(1), 0, ctx->stream, tr->count.as<unsigned long long>(), d_status + 1);
         JG_HIP(hipGetLastError());
         unsigned long long k = 0;
-        JG_HIP(hipMemcpyAsync(&k, d_status + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        jg::pin_get(ctx, 0, d_status + 1, 16);  // the completions' count and the applied count
+        jg::pin_sync(ctx);
+        std::memcpy(&k, jg::pin_at(ctx, 0), 8);
         ndone = k;
         if (completed && k) {
             JG_HIP(hipMemcpyAsync(completed, d_done, k * 8, hipMemcpyDeviceToHost, ctx->stream));
             JG_HIP(hipStreamSynchronize(ctx->stream));
         }
-    } else if (dt.tab) {
-        hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
-        JG_HIP(hipGetLastError());
-        JG_HIP(hipStreamSynchronize(ctx->stream));
     } else {
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        if (dt.tab) {
+            hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
+            JG_HIP(hipGetLastError());
+        }
+        jg::pin_get(ctx, 8, d_status + 2, 8);  // the applied count with the final sync
+        jg::pin_sync(ctx);
     }
     JG_HIP(hipEventRecord(nd->event(2 * n_ev + 1), ctx->stream));
     unsigned long long applied = 0;
-    JG_HIP(hipMemcpyAsync(&applied, d_status + 2, 8, hipMemcpyDeviceToHost, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
+    JG_HIP(hipEventSynchronize(nd->event(2 * n_ev + 1)));
+    std::memcpy(&applied, jg::pin_at(ctx, 8), 8);
     nd->stats.msgs_applied = applied;
     te[4] = now_s();
     if (trace)

@@ -18,6 +18,7 @@
 //   Roofline: HBM.  Reads 28 B per input record, writes 28 B per output record (key, tag, ord).
 // ORSet.Contains (ORSet.cs:204-237): k_contains, binary search of each queried key in both streams
 // (rank space), then SetEquals of the two sorted runs.
+#include <cstring>
 #include <hipcub/hipcub.hpp>
 
 #include <chrono>
@@ -387,16 +388,21 @@ void union_store(jg_ctx* ctx, jg_orset* a, jg_orset* b, jg_stream_soa& oa, jg_st
     counted->counts_pending = true;
 }
 
-void check_err_flag(jg_ctx* ctx, const char* fn) {
-    unsigned h = 0;
-    JG_HIP(hipMemcpyAsync(&h, ctx->flags.p, sizeof h, hipMemcpyDeviceToHost, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
+void flag_failed(jg_ctx* ctx, unsigned h, const char* fn) {
     if (h) {
         JG_HIP(hipMemsetAsync(ctx->flags.p, 0, sizeof h, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
         if (h & 2u) jg::fail(JG_EINVAL, "%s: a record's ord is not below 2^32", fn);
         jg::fail(JG_ESTATE, "%s: device reported a broken precondition (flag %u)", fn, h);
     }
+}
+
+void check_err_flag(jg_ctx* ctx, const char* fn) {
+    jg::pin_get(ctx, 0, ctx->flags.p, sizeof(unsigned));
+    jg::pin_sync(ctx);
+    unsigned h;
+    std::memcpy(&h, jg::pin_at(ctx, 0), sizeof h);
+    flag_failed(ctx, h, fn);
 }
 
 void upload_stream(jg_ctx* ctx, jg_stream_soa& s, const jg_tagrec* recs, uint64_t n, const char* fn) {
@@ -448,9 +454,18 @@ void merge_into(jg_orset* s, jg_orset* src, bool async, jgk::Drop drop = {nullpt
                          t2 - t1, t3 - t2, now() - t3, (unsigned long long)s->add.n, (unsigned long long)src->add.n);
     s->add.swap(s->spare_add);
     s->rem.swap(s->spare_rem);
-    if (!async) {
-        check_err_flag(ctx, "jg_orset_merge");
-        jg::sync_counts(s);
+    if (!async) {  // the error flag and the union's counts in one page-locked round trip
+        jg::pin_get(ctx, 0, ctx->flags.p, sizeof(unsigned));
+        jg::pin_get(ctx, 64, s->counts.p, 16);
+        jg::pin_sync(ctx);
+        unsigned h;
+        std::memcpy(&h, jg::pin_at(ctx, 0), sizeof h);
+        flag_failed(ctx, h, "jg_orset_merge");
+        unsigned long long c[2];
+        std::memcpy(c, jg::pin_at(ctx, 64), sizeof c);
+        s->add.n = c[0];
+        s->rem.n = c[1];
+        s->counts_pending = false;
     }
 }
 
@@ -719,8 +734,9 @@ void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n) {
 void sync_counts(jg_orset* s) {
     if (!s->counts_pending) return;
     unsigned long long h[2];
-    JG_HIP(hipMemcpyAsync(h, s->counts.p, sizeof h, hipMemcpyDeviceToHost, s->ctx->stream));
-    JG_HIP(hipStreamSynchronize(s->ctx->stream));
+    jg::pin_get(s->ctx, 0, s->counts.p, sizeof h);
+    jg::pin_sync(s->ctx);
+    std::memcpy(h, jg::pin_at(s->ctx, 0), sizeof h);
     s->add.n = h[0];
     s->rem.n = h[1];
     s->counts_pending = false;

@@ -10,8 +10,8 @@
 // device-wide radix sort (rocprim's merge sort at these sizes: ~20 launches each, ~0.75 ms of launches, syncs
 // and passes behind the last upload of the ORSetWorkload wave).  Here:
 //   k_cb_count    one lane per listed string / record: known strings resolved against the element table,
-//                 new strings and live records counted per set (one atomic per distinct set of a wave: the
-//                 lanes of a wave that share a set are folded first, so a hot set costs one atomic per wave)
+//                 new strings and live records counted per set (the lanes of a wave that share a set are folded
+//                 for its first few keys, so a hot set costs one atomic per wave; the rest one atomic per lane)
 //                 with their place in the set's bucket;
 //   k_cb_scan     exclusive sums of the per-set counts (and of the new strings' bytes), totals and the
 //                 largest bucket — read back in the commit's one host sync;
@@ -41,12 +41,24 @@ struct Buckets {
 
 // The lanes of a wave holding the same key (set, or side << 31 | set) take consecutive places from one atomic
 // on that key's counter; returns this lane's place.  Lanes with active = false take part in the ballots only.
+// At most kFoldIters keys are folded (the first remaining lane's, in turn): a wave whose keys are mostly distinct
+// (the ORSetWorkload wave: 2000 sets, lists in claim order) then issues one atomic per remaining lane at once
+// instead of up to 64 serial rounds of ballot + shuffle + atomic (117 of the commit's 140 us), while a hot key
+// that fills most of a wave is still folded (it is the first remaining lane's key within a few rounds).
+constexpr int kFoldIters = 4;
 __device__ __forceinline__ uint32_t wave_fold_add(bool active, uint32_t key, uint32_t* counters, uint32_t ctr_index, unsigned long long* bytes,
                                                   uint32_t len) {
     const uint32_t lane = threadIdx.x & 63;
     unsigned long long todo = __ballot(active);
     uint32_t place = kDead;
-    while (todo) {
+    for (int it = 0; todo; ++it) {
+        if (it == kFoldIters) {  // wave-uniform
+            if ((todo >> lane) & 1) {
+                place = atomicAdd(counters + ctr_index, 1u);
+                if (bytes) atomicAdd(bytes + ctr_index, (unsigned long long)len);
+            }
+            break;
+        }
         const int leader = __ffsll((long long)todo) - 1;
         const uint32_t k = __shfl(key, leader);
         const unsigned long long same = __ballot(active && key == k) & todo;
@@ -111,7 +123,11 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
     {
         const uint32_t lane = threadIdx.x & 63;
         unsigned long long todo = __ballot(r_live);
-        while (todo) {
+        for (int it = 0; todo; ++it) {
+            if (it == kFoldIters) {  // wave-uniform: the rest one atomic per lane (wave_fold_add)
+                if ((todo >> lane) & 1) rp = atomicAdd(B.rcnt[r_key >> 31] + (r_key & 0x7FFFFFFFu), 1u);
+                break;
+            }
             const int leader = __ffsll((long long)todo) - 1;
             const uint32_t k = __shfl(r_key, leader);
             const unsigned long long same = __ballot(r_live && r_key == k) & todo;
@@ -223,6 +239,19 @@ template <class Less> __device__ void lds_bitonic(uint16_t* perm, uint32_t P, Le
         }
 }
 
+// The same permutation by counting for a bucket of at most one item per thread: item r's rank is the number of
+// items before it in the order (the order is total: ties broken by index).  A ~200-item bucket takes ~200 LDS
+// broadcast reads per thread instead of bitonic's 36 passes with a workgroup barrier each.
+template <class Less> __device__ void lds_rank_sort(uint16_t* perm, uint32_t cnt, Less less) {
+    const uint32_t r = threadIdx.x;
+    if (r < cnt) {
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < cnt; ++j) rank += less((uint16_t)j, (uint16_t)r) ? 1u : 0u;
+        perm[rank] = (uint16_t)r;
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ uint32_t pow2_ge(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
@@ -250,10 +279,12 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
         perm[r] = (uint16_t)r;
     }
     __syncthreads();
-    lds_bitonic(perm, P, [&](uint16_t a, uint16_t b) {
+    const auto by_first = [&](uint16_t a, uint16_t b) {
         const uint32_t ka = a < cnt ? key[a] : 0xFFFFFFFFu, kb = b < cnt ? key[b] : 0xFFFFFFFFu;
         return ka != kb ? ka < kb : a < b;  // pads (index >= cnt) last
-    });
+    };
+    if (cnt <= kCbBlock) lds_rank_sort(perm, cnt, by_first);
+    else lds_bitonic(perm, P, by_first);
     for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
         const uint32_t sid = T.list[item[perm[r]]];
         lens[r] = S.meta[(T.word[sid] & 0xFFFFFFFFull) - 1] & 0x7FFFFFFFu;
@@ -326,13 +357,15 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_records(Sparse S, StrTab T, Rec
         perm[r] = (uint16_t)r;
     }
     __syncthreads();
-    lds_bitonic(perm, P, [&](uint16_t a, uint16_t b) {
+    const auto by_record = [&](uint16_t a, uint16_t b) {
         const bool pa = a >= cnt, pb = b >= cnt;  // pads last
         if (pa || pb) return !pa && pb ? true : (pa && pb ? a < b : false);
         if (elem[a] != elem[b]) return elem[a] < elem[b];
         if (lo[a] != lo[b]) return lo[a] < lo[b];
-        return hi[a] < hi[b];
-    });
+        if (hi[a] != hi[b]) return hi[a] < hi[b];
+        return a < b;  // (never equal: the records are distinct) a total order for the rank count
+    };
+    lds_bitonic(perm, P, by_record);  // (a rank count over three-field keys measured slower here: 108 vs 64 us per wave)
     unsigned long long* ok = sd ? k1 : k0;
     Tag16* ot = sd ? t1 : t0;
     uint32_t* oo = sd ? o1_ : o0_;

@@ -1038,8 +1038,9 @@ void ensure_names(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t poo
 unsigned long long* status_words(jg_orset_wire* w) { return w->status.as<unsigned long long>(); }
 
 void read_words(jg_ctx* ctx, const unsigned long long* d, unsigned long long* h, int n) {
-    JG_HIP(hipMemcpyAsync(h, d, n * 8, hipMemcpyDeviceToHost, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
+    jg::pin_get(ctx, 0, d, n * 8);
+    jg::pin_sync(ctx);
+    std::memcpy(h, jg::pin_at(ctx, 0), n * 8);
 }
 
 // Page-locked layout of a names copy: set [n] u32 | id [n] u32 | len [n] u32 | pad | pool offset [n] u64 | pool bytes.
@@ -1258,11 +1259,15 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
         hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
         JG_HIP(hipGetLastError());
-        // the overflow word and the tables' sub-list counts (the commit's) come back with the first bad message
+        // the overflow word and the tables' sub-list counts (the commit's) come back with the first bad message:
+        // one round trip, page-locked
         w->lc.resize((1 + 2 * kLists) * kCountStride);
-        JG_HIP(hipMemcpyAsync(w->lc.data(), w->ovf.p, w->lc.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        jg::pin_get(ctx, 0, st, 8);
+        jg::pin_get(ctx, 64, w->ovf.p, w->lc.size() * 8);
+        jg::pin_sync(ctx);
+        std::memcpy(w->lc.data(), jg::pin_at(ctx, 64), w->lc.size() * 8);
         unsigned long long h[2];
-        read_words(ctx, st, h, 1);
+        std::memcpy(h, jg::pin_at(ctx, 0), 8);
         h[1] = w->lc[0];
         const char* e = std::getenv("JANUS_ORSET_TAIL");  // =tables (tests): no fall-back, an overflow is an error
         JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
@@ -1530,8 +1535,9 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     double tc[5] = {tr ? now() : 0};
     uint64_t lim_off = w->wnb;
     if (limit < n) {  // the limit message's byte offset
-        JG_HIP(hipMemcpyAsync(&lim_off, w->voff + limit, 8, hipMemcpyDeviceToHost, ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        jg::pin_get(ctx, 0, w->voff + limit, 8);
+        jg::pin_sync(ctx);
+        std::memcpy(&lim_off, jg::pin_at(ctx, 0), 8);
     }
     const uint32_t csi_lim = limit < n ? (uint32_t)((lim_off + kEntryDiv - 1) / kEntryDiv) : 0xFFFFFFFFu;
     const uint32_t t_lim = limit < n ? (uint32_t)((lim_off + kTagDiv - 1) / kTagDiv) : 0xFFFFFFFFu;
@@ -1554,7 +1560,12 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     ensure(w->loffs, sizeof offs);
     ensure(w->st_packed, ns * 4 + 4);
     ensure(w->rt_packed, nrec * 4 + 4);
-    JG_HIP(hipMemcpyAsync(w->loffs.p, offs, sizeof offs, hipMemcpyHostToDevice, ctx->stream));
+    // from the context's page-locked write area (a pageable source is staged by the runtime, a host round trip);
+    // nothing else writes there before this wave's commit has synced
+    static_assert(sizeof offs <= jg::kPinBytes - jg::kPinRead, "offsets fit the page-locked write area");
+    void* hoffs = static_cast<char*>(ctx->hstat) + jg::kPinRead;
+    std::memcpy(hoffs, offs, sizeof offs);
+    JG_HIP(hipMemcpyAsync(w->loffs.p, hoffs, sizeof offs, hipMemcpyHostToDevice, ctx->stream));
     const auto* doffs = w->loffs.as<unsigned long long>();
     if (ns)
         hipLaunchKernelGGL(k_list_pack, dim3(blocks_for(ns)), dim3(kBlock), 0, ctx->stream, ST.list, ST.sub_cap, doffs, w->st_packed.as<uint32_t>());
