@@ -220,7 +220,7 @@ inline void pin_get(jg_ctx* ctx, size_t at, const void* d, size_t n) {
     if (at + n > kPinRead) fail(JG_EINVAL, "pin_get: %zu bytes at %zu exceed the page-locked read area", n, at);
     JG_HIP(hipMemcpyAsync(static_cast<char*>(ctx->hstat) + at, d, n, hipMemcpyDeviceToHost, ctx->stream));
 }
-inline void pin_sync(jg_ctx* ctx) { JG_HIP(hipStreamSynchronize(ctx->stream)); }
+inline void pin_sync(jg_ctx* ctx) { JG_HIP(hipStreamSynchronize(ctx->stream)); }  // (polling measured no gain)
 inline const void* pin_at(jg_ctx* ctx, size_t at) { return static_cast<const char*>(ctx->hstat) + at; }
 template <class H> inline CtxLock lock(const H* h) { return lock(h ? h->ctx : nullptr); }
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread

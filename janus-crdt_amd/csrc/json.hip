@@ -560,9 +560,9 @@ static_assert(sizeof(Status) <= 256, "status fits the context's page-locked word
 // copy per read; three reads per wave)
 Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     Status s;
-    JG_HIP(hipMemcpyAsync(ctx->hstat, d, sizeof s, hipMemcpyDeviceToHost, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
-    std::memcpy(&s, ctx->hstat, sizeof s);
+    jg::pin_get(ctx, 0, d, sizeof s);
+    jg::pin_sync(ctx);
+    std::memcpy(&s, jg::pin_at(ctx, 0), sizeof s);
     return s;
 }
 

@@ -41,6 +41,7 @@ constexpr int kOB = 512;   // threads per workgroup
 constexpr int kItems = 6;  // records per thread per tile
 constexpr int kTile = kOB * kItems;
 static_assert(kTile == (int)kChunk, "a union tile fills exactly one stream chunk");
+constexpr uint64_t kFewParts = 4096;  // tile boundaries below which the union's partition takes 64 lanes each
 
 using jgk::Tag;
 using jgk::ld_tag;
@@ -369,7 +370,10 @@ void union_store(jg_ctx* ctx, jg_orset* a, jg_orset* b, jg_stream_soa& oa, jg_st
     const jgk::PartJob pa = ua.part_job(), pr = ur.part_job();
     const uint64_t parts = pa.n_parts + pr.n_parts;
     if (parts) {
-        hipLaunchKernelGGL((jgk::k_partition_gallop2<kTile>), dim3((unsigned)((parts + 255) / 256)), dim3(256), 0, ctx->stream, pa, pr);
+        if (parts <= kFewParts)  // a wave into a store: latency of the search, not throughput (orset_union.hpp)
+            hipLaunchKernelGGL((jgk::k_partition_lanes2<kTile, 64>), dim3((unsigned)((parts * 64 + 255) / 256)), dim3(256), 0, ctx->stream, pa, pr);
+        else
+            hipLaunchKernelGGL((jgk::k_partition_gallop2<kTile>), dim3((unsigned)((parts + 255) / 256)), dim3(256), 0, ctx->stream, pa, pr);
         JG_HIP(hipGetLastError());
     }
     launch_tiles(ctx, ua, drop);

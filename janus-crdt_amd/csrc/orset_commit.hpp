@@ -10,9 +10,9 @@
 // device-wide radix sort (rocprim's merge sort at these sizes: ~20 launches each, ~0.75 ms of launches, syncs
 // and passes behind the last upload of the ORSetWorkload wave).  Here:
 //   k_cb_count    one lane per listed string / record: known strings resolved against the element table,
-//                 new strings and live records counted per set (the lanes of a wave that share a set are folded
-//                 for its first few keys, so a hot set costs one atomic per wave; the rest one atomic per lane)
-//                 with their place in the set's bucket;
+//                 new strings and live records counted per set (one atomic per lane, all in flight together;
+//                 a hot set's lanes of a wave folded into one) with their place in the set's bucket (the
+//                 string's set and length, the record's side and set, stored beside the slots at claim time);
 //   k_cb_scan     exclusive sums of the per-set counts (and of the new strings' bytes), totals and the
 //                 largest bucket — read back in the commit's one host sync;
 //   k_cb_scatter  every item into its bucket;
@@ -39,105 +39,71 @@ struct Buckets {
     uint32_t n_sets;
 };
 
-// The lanes of a wave holding the same key (set, or side << 31 | set) take consecutive places from one atomic
-// on that key's counter; returns this lane's place.  Lanes with active = false take part in the ballots only.
-// At most kFoldIters keys are folded (the first remaining lane's, in turn): a wave whose keys are mostly distinct
-// (the ORSetWorkload wave: 2000 sets, lists in claim order) then issues one atomic per remaining lane at once
-// instead of up to 64 serial rounds of ballot + shuffle + atomic (117 of the commit's 140 us), while a hot key
-// that fills most of a wave is still folded (it is the first remaining lane's key within a few rounds).
-constexpr int kFoldIters = 4;
-__device__ __forceinline__ uint32_t wave_fold_add(bool active, uint32_t key, uint32_t* counters, uint32_t ctr_index, unsigned long long* bytes,
-                                                  uint32_t len) {
+// A place in the bucket of `cell` (the key's counter) for every active lane: one returning atomic per lane,
+// all of the wave's in flight together (one round trip), except that the lanes sharing the wave's first key
+// fold into one add of their count when there are many of them (a hot set: >= 8 lanes), so a wave of one hot set
+// costs one atomic on its counter, not 64.  Device-scope atomics execute at the memory side (MI355X_MICROARCH
+// "Global float atomics"; one word takes ~88 per us): the round-3 fold took every distinct key of a wave in turn,
+// a chain of up to 64 dependent ballot + atomic rounds per wave.  bcell (optional): add len there too.
+__device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32_t* cell, unsigned long long* bcell, uint32_t len) {
     const uint32_t lane = threadIdx.x & 63;
-    unsigned long long todo = __ballot(active);
-    uint32_t place = kDead;
-    for (int it = 0; todo; ++it) {
-        if (it == kFoldIters) {  // wave-uniform
-            if ((todo >> lane) & 1) {
-                place = atomicAdd(counters + ctr_index, 1u);
-                if (bytes) atomicAdd(bytes + ctr_index, (unsigned long long)len);
-            }
-            break;
-        }
-        const int leader = __ffsll((long long)todo) - 1;
-        const uint32_t k = __shfl(key, leader);
-        const unsigned long long same = __ballot(active && key == k) & todo;
-        const uint32_t kidx = __shfl(ctr_index, leader);
-        uint32_t base = 0;
-        unsigned long long sum = 0;
-        if (bytes) {  // the group's bytes: a wave sum over the group's lanes
-            unsigned long long v = ((same >> lane) & 1) ? len : 0;
-            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-            sum = v;
-        }
-        if ((int)lane == leader) {
-            base = atomicAdd(counters + kidx, (uint32_t)__popcll(same));
-            if (bytes) atomicAdd(bytes + kidx, sum);
-        }
-        base = __shfl(base, leader);
-        if ((same >> lane) & 1) place = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-        todo &= ~same;
+    const unsigned long long act = __ballot(active);
+    if (!act) return kDead;  // wave-uniform
+    const int leader = __ffsll((long long)act) - 1;
+    const uint32_t k0 = __shfl(key, leader);
+    const unsigned long long same = __ballot(active && key == k0);
+    const bool fold = __popcll(same) >= 8;  // wave-uniform
+    const bool member = fold && ((same >> lane) & 1);
+    uint32_t add = 0;
+    unsigned long long badd = 0;
+    if (active && !member) add = 1, badd = len;
+    if (fold && bcell) {  // the fold group's bytes: a wave sum of its lanes' lengths
+        unsigned long long v = member ? len : 0;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        badd = (int)lane == leader ? v : badd;
     }
-    return place;
+    if (member && (int)lane == leader) add = (uint32_t)__popcll(same);
+    uint32_t r = 0;
+    if (add) {
+        r = atomicAdd(cell, add);
+        if (bcell) atomicAdd(bcell, badd);
+    }
+    const uint32_t base = __shfl(r, leader);
+    return member ? base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull)) : (active ? r : kDead);
 }
 
 __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, RecTab R, uint64_t ns, uint64_t nrec,
                                                      uint32_t s_lim, uint32_t t_lim, Names N, uint32_t* __restrict__ sid_id, Buckets B) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     // a workgroup's lanes are all strings or all records up to the boundary wave (ns need not be a multiple of 64:
-    // both folds run in every wave, each with its own lanes active)
+    // both adds run in every wave, each with its own lanes active)
     bool s_new = false, r_live = false;
-    uint32_t s_set = 0, s_len = 0, r_key = 0, r_side = 0;
+    uint32_t s_set = 0, s_len = 0, r_key = 0;
     if (i < ns) {
         const uint32_t sid = T.list[i];
         if (T.first[sid] < s_lim) {
-            const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
-            const uint32_t set = S.set[ref], len = S.meta[ref] & 0x7FFFFFFFu;
+            const uint32_t set = T.set[sid];
             uint32_t id = sid_id[sid];  // looked up when the chunk's k_ow_strings claimed the slot
             if (id == kUnresolved) {
-                id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], len);
+                const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+                id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], T.len[sid]);
                 if (id != kNoName) sid_id[sid] = id;
             }
             if (id == kNoName) {
                 s_new = true;
                 s_set = set;
-                s_len = len;
+                s_len = T.len[sid];
             }
         }
     } else if (i - ns < nrec) {
-        const uint64_t j = i - ns;
-        const uint32_t slot = R.list[j];
+        const uint32_t slot = R.list[i - ns];
         if (R.mint[slot] < t_lim) {
-            const uint64_t u = (R.word[slot] & 0xFFFFFFFFull) - 1;
-            const unsigned long long id = S.trk[u];
-            r_side = (uint32_t)(id & 1);
-            const uint32_t set = (id >> 63) ? (uint32_t)((id >> 1) & 0xFFFFFFFFull) : S.set[(T.word[(uint32_t)(id >> 1)] & 0xFFFFFFFFull) - 1];
             r_live = true;
-            r_key = r_side << 31 | set;
+            r_key = R.key[slot];
         }
     }
-    const uint32_t sp = wave_fold_add(s_new, s_set, B.scnt, s_set, B.sbytes, s_len);
-    const uint32_t r_set = r_key & 0x7FFFFFFFu;
-    // two record counters (per side): fold on side << 31 | set, count into that side's array
-    uint32_t rp = kDead;
-    {
-        const uint32_t lane = threadIdx.x & 63;
-        unsigned long long todo = __ballot(r_live);
-        for (int it = 0; todo; ++it) {
-            if (it == kFoldIters) {  // wave-uniform: the rest one atomic per lane (wave_fold_add)
-                if ((todo >> lane) & 1) rp = atomicAdd(B.rcnt[r_key >> 31] + (r_key & 0x7FFFFFFFu), 1u);
-                break;
-            }
-            const int leader = __ffsll((long long)todo) - 1;
-            const uint32_t k = __shfl(r_key, leader);
-            const unsigned long long same = __ballot(r_live && r_key == k) & todo;
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(B.rcnt[k >> 31] + (k & 0x7FFFFFFFu), (uint32_t)__popcll(same));
-            base = __shfl(base, leader);
-            if ((same >> lane) & 1) rp = base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-            todo &= ~same;
-        }
-    }
+    const uint32_t sp = bucket_add(s_new, s_set, B.scnt + s_set, B.sbytes + s_set, s_len);
+    const uint32_t rp = bucket_add(r_live, r_key, B.rcnt[r_key >> 31] + (r_key & 0x7FFFFFFFu), nullptr, 0);
     if (i < ns) {
         B.spos[i] = s_new ? sp : kDead;
         B.sset[i] = s_set;
@@ -145,7 +111,6 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
         B.rpos[i - ns] = r_live ? rp : kDead;
         B.rset[i - ns] = r_key;
     }
-    (void)r_set;
 }
 
 // Exclusive sums of the four per-set arrays in place (n + 1 entries each, the last one 0 before: the total

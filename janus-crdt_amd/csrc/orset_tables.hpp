@@ -46,6 +46,8 @@ struct StrTab {
     uint32_t* list;
     unsigned long long* n;
     uint64_t sub_cap;
+    uint32_t* set;             // per claimed slot: the string's set and length (written by the claimant, so that the
+    uint32_t* len;             // commit reads them beside the slot instead of through the first entry)
 };
 struct RecTab {
     unsigned long long* word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
@@ -54,6 +56,7 @@ struct RecTab {
     uint32_t* list;
     unsigned long long* n;
     uint64_t sub_cap;
+    uint32_t* key;             // per claimed slot: side << 31 | set (the commit's bucket, without the string chain)
 };
 
 // Lanes that claimed a slot append it to their workgroup's sub-list: one atomic per wave (claims are a few
@@ -129,6 +132,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                 if (w == 0) {
                     sid = (uint32_t)p;
                     fresh = true;
+                    T.set[sid] = set;
+                    T.len[sid] = len;
                     sid_id[sid] = set < set_lim ? tab_find(N, key, set, bytes + noff, len) : kUnresolved;
                     break;
                 }
@@ -197,7 +202,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
     if (m >= m1) return;
-    if (mset[m] == jg::kSkipIdx) return;
+    const uint32_t set = mset[m];
+    if (set == jg::kSkipIdx) return;
     const uint32_t k = (uint32_t)nt[m];
     const uint64_t ts = (off[m] + kTagDiv - 1) / kTagDiv;
     bool over = false;
@@ -220,6 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
                 if (w == 0) {
                     slot = p;
                     fresh = true;
+                    T.key[slot] = (uint32_t)(id & 1) << 31 | set;  // the record's set is its message's
                     break;
                 }
             }

@@ -86,14 +86,13 @@ __device__ __forceinline__ bool dropped(const Drop& d, unsigned long long key) {
 // records among the first d (A first on ties).  C must be a multiple of 512 (aligned coarse probes).  L lanes cooperate on one boundary with an
 // (L+1)-ary search (L = 1: plain binary search); tags are read only when keys tie.  Also records
 // the chunk holding the first A and B rank of the tile (saves the tile one dependent lookup).
+// Boundary w of (a, b) on the L lanes of its group (gl = this lane's index in the group); every lane of the
+// wave calls it (ballots), inactive groups with w >= n_parts.
 template <int C, int L>
-__global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_parts, uint64_t* __restrict__ part,
-                                                   uint32_t* __restrict__ pchunk) {
+__device__ __forceinline__ void lanes_split(const View& a, const View& b, uint64_t n_parts, uint64_t* __restrict__ part,
+                                            uint32_t* __restrict__ pchunk, uint64_t w, int gl) {
     static_assert(L >= 1 && L <= 64 && 64 % L == 0, "lanes per boundary must divide the wave");
     static_assert(C % 512 == 0, "tile boundaries on 512-rank multiples");
-    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint64_t w = gt / L;
-    const int gl = (int)(gt % L);
     const int gbase = (int)(threadIdx.x & 63) - gl;  // first lane of this boundary's group
     const uint64_t total = a.n + b.n;
     const bool active = w < n_parts;
@@ -136,6 +135,13 @@ __global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_pa
         pchunk[2 * w] = i < a.n ? chunk_of(a, i) : a.nch;
         pchunk[2 * w + 1] = j < b.n ? chunk_of(b, j) : b.nch;
     }
+}
+
+template <int C, int L>
+__global__ __launch_bounds__(256) void k_partition(View a, View b, uint64_t n_parts, uint64_t* __restrict__ part,
+                                                   uint32_t* __restrict__ pchunk) {
+    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    lanes_split<C, L>(a, b, n_parts, part, pchunk, gt / L, (int)(gt % L));
 }
 
 // Merge-path predicate at split candidate m of diagonal d: A[m] <= B[d-1-m] (A first on ties).
@@ -211,6 +217,19 @@ __global__ __launch_bounds__(256) void k_partition_gallop2(PartJob j0, PartJob j
     const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (w < j0.n_parts) gallop_split<C>(j0.a, j0.b, w, j0.part, j0.pchunk);
     else if (w - j0.n_parts < j1.n_parts) gallop_split<C>(j1.a, j1.b, w - j0.n_parts, j1.part, j1.pchunk);
+}
+
+// Both streams' boundaries, L lanes per boundary ((L+1)-ary search: each round's L probes are independent).
+// For a union of few tiles (a committed wave into a store: a few hundred boundaries) the gallop's chain of
+// dependent probes — each a chunk lookup, a key and maybe a tag, ~16 probes — is the whole kernel (46 us);
+// 64 lanes per boundary take ~4 rounds.  Many boundaries (C3: 10^5) keep the gallop (one lane each).
+template <int C, int L>
+__global__ __launch_bounds__(256) void k_partition_lanes2(PartJob j0, PartJob j1) {
+    const uint64_t gt = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t w = gt / L;
+    const int gl = (int)(gt % L);
+    if (w < j0.n_parts) lanes_split<C, L>(j0.a, j0.b, j0.n_parts, j0.part, j0.pchunk, w, gl);
+    else lanes_split<C, L>(j1.a, j1.b, j1.n_parts, j1.part, j1.pchunk, w - j0.n_parts, gl);  // (w past both: inactive)
 }
 
 // LDS of one union tile.

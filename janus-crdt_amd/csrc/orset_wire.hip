@@ -905,6 +905,7 @@ struct jg_orset_wire {
     // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
     jg::DevBuf st_word, st_first, st_list, rt_word, rt_mint, rt_list, sid_id, ovf;  // ovf: overflow word, sub-list counts
+    jg::DevBuf st_set, st_len, rt_key;  // per claimed slot: the string's set and length, the record's side << 31 | set
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
     jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
@@ -1162,11 +1163,11 @@ Entries entries_of(jg_orset_wire* w) {
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
 StrTab str_tab(jg_orset_wire* w) {
     return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
-                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8};
+                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8, w->st_set.as<uint32_t>(), w->st_len.as<uint32_t>()};
 }
 RecTab rec_tab(jg_orset_wire* w) {
     return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
-                  w->ovf.as<unsigned long long>() + (1 + kLists) * kCountStride, w->rt_cap / 8};
+                  w->ovf.as<unsigned long long>() + (1 + kLists) * kCountStride, w->rt_cap / 8, w->rt_key.as<uint32_t>()};
 }
 
 // A wave opens: size and clear its string / record tables (queued on the compute stream, ahead of the first
@@ -1185,6 +1186,8 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     if (w->st_cap < sc) {
         w->st_word.alloc(sc * 8);
         w->st_first.alloc(sc * 4);
+        w->st_set.alloc(sc * 4);
+        w->st_len.alloc(sc * 4);
         w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
         w->st_cap = sc;
@@ -1192,6 +1195,7 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     if (w->rt_cap < rc) {
         w->rt_word.alloc(rc * 8);
         w->rt_mint.alloc(rc * 4);
+        w->rt_key.alloc(rc * 4);
         w->rt_list.alloc((rc / 8) * kLists * 4);
         w->rt_cap = rc;
     }
