@@ -10,14 +10,15 @@
 // device-wide radix sort (rocprim's merge sort at these sizes: ~20 launches each, ~0.75 ms of launches, syncs
 // and passes behind the last upload of the ORSetWorkload wave).  Here:
 //   k_cb_count    one lane per listed string / record: known strings resolved against the element table,
-//                 new strings and live records counted per set (one atomic per lane, all in flight together;
-//                 a hot set's lanes of a wave folded into one) with their place in the set's bucket (the
+//                 new strings (and their bytes) and live records counted per set (one atomic per run of a
+//                 wave's items with one set, all in flight together) with their place in the set's bucket (the
 //                 string's set and length, the record's side and set, stored beside the slots at claim time);
-//   k_cb_scan     exclusive sums of the per-set counts (and of the new strings' bytes), totals and the
-//                 largest bucket — read back in the commit's one host sync;
+//   k_cb_scan     exclusive sums of the per-set counts and of the new strings' bytes, totals and the largest
+//                 bucket — read back in the commit's one host sync;
 //   k_cb_scatter  every item into its bucket;
-//   k_cb_strings  one workgroup per set: the bucket sorted by first entry in LDS (bitonic), ids next_id + rank,
-//                 names appended in (set, first entry) order with their bytes placed by a prefix of lengths;
+//   k_cb_strings  one workgroup per set: the bucket sorted by first entry in LDS (a rank count, bitonic past
+//                 256), ids next_id + rank, names appended in (set, first entry) order with their bytes placed by
+//                 a prefix of lengths;
 //   k_cb_records  one workgroup per (side, set): the bucket sorted by (element id, tag) in LDS, written straight
 //                 into the dense stream the union reads (position = bucket offset + rank).
 // A bucket larger than the LDS sort holds (kCbMax) sends the wave to the radix path (commit_tables' own).
@@ -39,37 +40,51 @@ struct Buckets {
     uint32_t n_sets;
 };
 
-// A place in the bucket of `cell` (the key's counter) for every active lane: one returning atomic per lane,
-// all of the wave's in flight together (one round trip), except that the lanes sharing the wave's first key
-// fold into one add of their count when there are many of them (a hot set: >= 8 lanes), so a wave of one hot set
-// costs one atomic on its counter, not 64.  Device-scope atomics execute at the memory side (MI355X_MICROARCH
-// "Global float atomics"; one word takes ~88 per us): the round-3 fold took every distinct key of a wave in turn,
-// a chain of up to 64 dependent ballot + atomic rounds per wave.  bcell (optional): add len there too.
-__device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32_t* cell, unsigned long long* bcell, uint32_t len) {
+// A place in the bucket of `cell` (the key's counter) for every active lane, from one atomic per RUN of
+// consecutive active lanes with the same key, all of the wave's in flight together (one round trip).  The lists
+// hold each message's claims back to back (one wave per message appends them together) and a message is one
+// set, so a wave's 64 items are a few runs: ~8x fewer atomics than one per lane, and a hot set costs one per
+// wave.  Device-scope atomics execute at the memory side (MI355X_MICROARCH "Global float atomics"); the round-3
+// fold took every distinct key of a wave in turn, a chain of up to 64 dependent ballot + atomic rounds.
+__device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32_t* cell) {
     const uint32_t lane = threadIdx.x & 63;
     const unsigned long long act = __ballot(active);
     if (!act) return kDead;  // wave-uniform
-    const int leader = __ffsll((long long)act) - 1;
-    const uint32_t k0 = __shfl(key, leader);
-    const unsigned long long same = __ballot(active && key == k0);
-    const bool fold = __popcll(same) >= 8;  // wave-uniform
-    const bool member = fold && ((same >> lane) & 1);
-    uint32_t add = 0;
-    unsigned long long badd = 0;
-    if (active && !member) add = 1, badd = len;
-    if (fold && bcell) {  // the fold group's bytes: a wave sum of its lanes' lengths
-        unsigned long long v = member ? len : 0;
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        badd = (int)lane == leader ? v : badd;
-    }
-    if (member && (int)lane == leader) add = (uint32_t)__popcll(same);
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long breaks = heads | ~act;  // a run ends before the next head or inactive lane
+    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
+    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
     uint32_t r = 0;
-    if (add) {
-        r = atomicAdd(cell, add);
-        if (bcell) atomicAdd(bcell, badd);
+    if (head) r = atomicAdd(cell, end - lane);
+    const unsigned long long hm = heads & (lane == 63 ? ~0ull : (2ull << lane) - 1ull);
+    const uint32_t h = hm ? 63u - (uint32_t)__clzll(hm) : lane;  // this lane's run head (an inactive lane: itself)
+    const uint32_t base = (uint32_t)__shfl((int)r, (int)h);
+    return active ? base + (lane - h) : kDead;
+}
+
+// The bytes of each run of bucket_add (same runs: consecutive active lanes with one key) added to the key's
+// byte counter by the run's head, no return: an inclusive wave scan of the lengths, the head adds the scan at
+// the run's last lane minus the scan before it.  Lengths that could overflow the 32-bit scan (>= 2^25 each):
+// one add per lane.  Every lane of the wave calls it.
+__device__ __forceinline__ void run_bytes(bool active, uint32_t key, unsigned long long* cell, uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long act = __ballot(active);
+    if (!act) return;  // wave-uniform
+    const uint32_t v = active ? len : 0u;
+    if (__ballot(v >= (1u << 25))) {  // wave-uniform
+        if (active) atomicAdd(cell, (unsigned long long)len);
+        return;
     }
-    const uint32_t base = __shfl(r, leader);
-    return member ? base + (uint32_t)__popcll(same & ((1ull << lane) - 1ull)) : (active ? r : kDead);
+    const uint32_t incl = jgw::wave_incl_scan(v);
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
+    const unsigned long long breaks = __ballot(head) | ~act;
+    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
+    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
+    const uint32_t at_end = (uint32_t)__shfl((int)incl, (int)(end - 1));
+    if (head) atomicAdd(cell, (unsigned long long)(at_end - (incl - v)));
 }
 
 __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, RecTab R, uint64_t ns, uint64_t nrec,
@@ -81,18 +96,18 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
     uint32_t s_set = 0, s_len = 0, r_key = 0;
     if (i < ns) {
         const uint32_t sid = T.list[i];
+        const uint4 mt = T.meta[sid];  // {set, length, id looked up when the chunk's k_ow_strings claimed the slot}
         if (T.first[sid] < s_lim) {
-            const uint32_t set = T.set[sid];
-            uint32_t id = sid_id[sid];  // looked up when the chunk's k_ow_strings claimed the slot
+            uint32_t id = mt.z;
             if (id == kUnresolved) {
                 const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
-                id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], T.len[sid]);
+                id = tab_find(N, S.key[ref], mt.x, bytes + S.noff[ref], mt.y);
                 if (id != kNoName) sid_id[sid] = id;
             }
             if (id == kNoName) {
                 s_new = true;
-                s_set = set;
-                s_len = T.len[sid];
+                s_set = mt.x;
+                s_len = mt.y;
             }
         }
     } else if (i - ns < nrec) {
@@ -102,8 +117,9 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
             r_key = R.key[slot];
         }
     }
-    const uint32_t sp = bucket_add(s_new, s_set, B.scnt + s_set, B.sbytes + s_set, s_len);
-    const uint32_t rp = bucket_add(r_live, r_key, B.rcnt[r_key >> 31] + (r_key & 0x7FFFFFFFu), nullptr, 0);
+    const uint32_t sp = bucket_add(s_new, s_set, B.scnt + s_set);
+    run_bytes(s_new, s_set, B.sbytes + s_set, s_len);
+    const uint32_t rp = bucket_add(r_live, r_key, B.rcnt[r_key >> 31] + (r_key & 0x7FFFFFFFu));
     if (i < ns) {
         B.spos[i] = s_new ? sp : kDead;
         B.sset[i] = s_set;
@@ -251,8 +267,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
     if (cnt <= kCbBlock) lds_rank_sort(perm, cnt, by_first);
     else lds_bitonic(perm, P, by_first);
     for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
-        const uint32_t sid = T.list[item[perm[r]]];
-        lens[r] = S.meta[(T.word[sid] & 0xFFFFFFFFull) - 1] & 0x7FFFFFFFu;
+        lens[r] = T.meta[T.list[item[perm[r]]]].y;
     }
     __syncthreads();
     // exclusive prefix of the lengths in rank order (each thread a contiguous run, then the thread sums)

@@ -46,8 +46,8 @@ struct StrTab {
     uint32_t* list;
     unsigned long long* n;
     uint64_t sub_cap;
-    uint32_t* set;             // per claimed slot: the string's set and length (written by the claimant, so that the
-    uint32_t* len;             // commit reads them beside the slot instead of through the first entry)
+    uint4* meta;               // per claimed slot, written by the claimant: {set, length, id at claim time, 0} — one
+                               // 16-byte read for the commit instead of a chain through the first entry
 };
 struct RecTab {
     unsigned long long* word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
@@ -132,9 +132,9 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                 if (w == 0) {
                     sid = (uint32_t)p;
                     fresh = true;
-                    T.set[sid] = set;
-                    T.len[sid] = len;
-                    sid_id[sid] = set < set_lim ? tab_find(N, key, set, bytes + noff, len) : kUnresolved;
+                    const uint32_t id0 = set < set_lim ? tab_find(N, key, set, bytes + noff, len) : kUnresolved;
+                    sid_id[sid] = id0;
+                    T.meta[sid] = make_uint4(set, len, id0, 0u);
                     break;
                 }
             }

@@ -905,11 +905,12 @@ struct jg_orset_wire {
     // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
     jg::DevBuf st_word, st_first, st_list, rt_word, rt_mint, rt_list, sid_id, ovf;  // ovf: overflow word, sub-list counts
-    jg::DevBuf st_set, st_len, rt_key;  // per claimed slot: the string's set and length, the record's side << 31 | set
+    jg::DevBuf st_meta, rt_key;  // per claimed slot: the string's {set, length, id}, the record's side << 31 | set
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
     jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
-    uint64_t st_cap = 0, rt_cap = 0;
+    uint64_t st_cap = 0, rt_cap = 0;     // slots in use this wave (a power of two, <= the allocations)
+    uint64_t st_alloc = 0, rt_alloc = 0, seen_s = 0, seen_r = 0;  // allocated slots; the last checked wave's distinct strings / records
     bool tables = false, tables_ok = false;
     std::vector<unsigned long long> lc;  // host copy of ovf (overflow word, sub-list counts) taken by the check
     uint64_t waves_fast = 0, waves_sorted = 0;  // commits from the tables / by the sort path (tests read them)
@@ -1163,7 +1164,7 @@ Entries entries_of(jg_orset_wire* w) {
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
 StrTab str_tab(jg_orset_wire* w) {
     return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
-                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8, w->st_set.as<uint32_t>(), w->st_len.as<uint32_t>()};
+                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8, w->st_meta.as<uint4>()};
 }
 RecTab rec_tab(jg_orset_wire* w) {
     return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
@@ -1181,24 +1182,34 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     w->tables_ok = false;
     if (!w->tables) return;
     const uint64_t lim = 1ull << 30;  // slot ids < 2^31 (k_ow_strings packs the side above them); hipcub counts in int
-    const uint64_t sc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, 2 * std::max(nbytes / 40, n_msgs * 16) + 64)));
-    const uint64_t rc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, 2 * std::max(nbytes / 38, n_msgs * 32) + 64)));
-    if (w->st_cap < sc) {
+    const uint64_t bound_s = 2 * std::max(nbytes / 40, n_msgs * 16) + 64, bound_r = 2 * std::max(nbytes / 38, n_msgs * 32) + 64;
+    // The tables in use are sized from the previous wave's distinct strings / records, x4 (a quarter full at the
+    // same mix, half full at twice as many), below the certain bound: that bound gave the ORSetWorkload wave
+    // (~0.4M distinct strings and records) 16M-slot tables, ~0.5 GB probed at random, every probe a miss in
+    // the 256 MB MALL.  A wave past the smaller tables' room overflows into the sort path (correct, slower) and
+    // the next one sizes from the bound again.  JANUS_ORSET_TAIL=tables (no fall-back) keeps the bound.
+    const bool strict = e && std::strcmp(e, "tables") == 0;
+    const uint64_t want_s = w->seen_s && !strict ? std::min(bound_s, 4 * w->seen_s + 65536) : bound_s;
+    const uint64_t want_r = w->seen_r && !strict ? std::min(bound_r, 4 * w->seen_r + 65536) : bound_r;
+    const uint64_t sc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, want_s)));
+    const uint64_t rc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, want_r)));
+    if (w->st_alloc < sc) {  // allocations only grow; the active part is the first st_cap slots
         w->st_word.alloc(sc * 8);
         w->st_first.alloc(sc * 4);
-        w->st_set.alloc(sc * 4);
-        w->st_len.alloc(sc * 4);
+        w->st_meta.alloc(sc * 16);
         w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
-        w->st_cap = sc;
+        w->st_alloc = sc;
     }
-    if (w->rt_cap < rc) {
+    if (w->rt_alloc < rc) {
         w->rt_word.alloc(rc * 8);
         w->rt_mint.alloc(rc * 4);
         w->rt_key.alloc(rc * 4);
         w->rt_list.alloc((rc / 8) * kLists * 4);
-        w->rt_cap = rc;
+        w->rt_alloc = rc;
     }
+    w->st_cap = sc;
+    w->rt_cap = rc;
     if (!w->ovf.p) w->ovf.alloc((1 + 2 * kLists) * kCountStride * 8);
     JG_HIP(hipMemsetAsync(w->st_word.p, 0, w->st_cap * 8, ctx->stream));
     JG_HIP(hipMemsetAsync(w->st_first.p, 0xFF, w->st_cap * 4, ctx->stream));
@@ -1275,8 +1286,13 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         h[1] = w->lc[0];
         const char* e = std::getenv("JANUS_ORSET_TAIL");  // =tables (tests): no fall-back, an overflow is an error
         JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
+        w->seen_s = w->seen_r = 0;  // an overflowed wave: the next one sizes its tables from the bound
         if (h[1] == 0) {
             w->tables_ok = true;
+            for (uint32_t j = 0; j < kLists; ++j) {  // the next wave's table sizes (tables_begin)
+                w->seen_s += w->lc[(1 + j) * kCountStride];
+                w->seen_r += w->lc[(1 + kLists + j) * kCountStride];
+            }
             // a set's element ids cannot run out in this wave's commit: every set's next id is at most the
             // names issued so far, and the wave adds at most one per distinct (set, string) — checked here,
             // before a node wave commits anything (the commit's own check then never fires mid-wave)
