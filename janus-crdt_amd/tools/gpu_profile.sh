@@ -3,7 +3,7 @@
 # leg (incl. the OR-Set apply loop from page-locked payloads), one PMC pass per counter group (FETCH_SIZE and
 # WRITE_SIZE do not fit one pass on gfx950; SQ instruction / wait counters; TCC atomics / hits), the per-launch
 # summary (pmc_summary.py), then the default bench line itself.
-# Usage: gpu_profile.sh <outdir> [round label]
+# Usage: [WITH_BENCH=1] gpu_profile.sh <outdir> [round label]
 set -o pipefail
 OUT=${1:-gpurun_out/prof}
 LABEL=${2:-r04}
@@ -50,4 +50,10 @@ pass sq2_orset_loop $SQ2 $ORSET_LOOP
 pass tcc_orset_loop $TCC $ORSET_LOOP
 step summary
 python3 janus-crdt_amd/tools/pmc_summary.py "$OUT" "$OUT/pmc_$LABEL.json" "$LABEL" > "$OUT/pmc_summary.out" || exit 1
+# the default bench line in the same lease, reading the summary just made (its rooflines cite it)
+if [ -n "$WITH_BENCH" ]; then
+    step bench
+    mkdir -p profiles && cp "$OUT/pmc_$LABEL.json" "profiles/pmc_$LABEL.json"
+    timeout -k 10 600 python3 bench.py > "$OUT/bench_final.json" 2> "$OUT/bench_final.err" || exit 1
+fi
 echo profile-done

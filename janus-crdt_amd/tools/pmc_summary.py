@@ -90,11 +90,14 @@ def orset_loop(d: Path):
             continue
         ns = sum(dur.get(k, [])) / ORSET_LOOP_WAVES if dur.get(k) else None
         wc = c.get("SQ_WAVE_CYCLES") or 0
+        # FETCH_SIZE counts half of a wide streaming read (the 2x correction) but a random 64-byte line fetch
+        # once: these kernels probe tables at random, so the bytes lie between the two readings
         hbm = 2 * 1024 * c.get("FETCH_SIZE", 0) + 1024 * c.get("WRITE_SIZE", 0)
+        hbm_rand = 1024 * c.get("FETCH_SIZE", 0) + 1024 * c.get("WRITE_SIZE", 0)
         hit, miss = c.get("TCC_HIT_sum", 0), c.get("TCC_MISS_sum", 0)
         e = {"us_per_wave": ns / 1e3 if ns else None,
-             "hbm_bytes_per_wave": hbm, "tcc_ea_rdreq_per_wave": c.get("TCC_EA0_RDREQ_sum"),
-             "hbm_GBps": hbm / ns if ns else None,
+             "hbm_bytes_per_wave": hbm, "hbm_bytes_per_wave_random_lines": hbm_rand, "tcc_ea_rdreq_per_wave": c.get("TCC_EA0_RDREQ_sum"),
+             "hbm_GBps": hbm / ns if ns else None, "hbm_GBps_random_lines": hbm_rand / ns if ns else None,
              "valu_insts_per_wave": c.get("SQ_INSTS_VALU"), "salu_insts_per_wave": c.get("SQ_INSTS_SALU"),
              "lds_insts_per_wave": c.get("SQ_INSTS_LDS"), "vmem_insts_per_wave": c.get("SQ_INSTS_VMEM"),
              "valu_issue_frac": (c.get("SQ_INSTS_VALU", 0) / (ns * 1e-9) / VALU_WAVE_INSTS_PER_S) if ns else None,
@@ -103,9 +106,10 @@ def orset_loop(d: Path):
              "active_frac": c.get("SQ_ACTIVE_INST_ANY", 0) / wc if wc else None,
              "lds_conflict_frac": c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else None,
              "tcc_hit_rate": hit / (hit + miss) if hit + miss else None, "tcc_atomics_per_wave": c.get("TCC_ATOMIC_sum")}
-        # the bound the counters name: the HBM share of peak, the VALU issue share, or waves parked on memory
-        # with neither near its peak (latency: dependent random probes / atomics)
-        hf = (e["hbm_GBps"] or 0) / 8000.0
+        # the bound the counters name: the HBM share of peak (on the random-line reading: a random probe fetches
+        # its line once), the VALU issue share, or waves parked on memory with neither near its peak (latency:
+        # dependent random probes / atomics, the request rate of scattered lines)
+        hf = (e["hbm_GBps_random_lines"] or 0) / 8000.0
         vf = e["valu_issue_frac"] or 0
         wm = e["wait_mem_frac"] or 0
         e["bound"] = "hbm" if hf >= 0.5 else "valu" if vf >= 0.5 else "latency" if wm >= 0.5 else "mixed"
@@ -177,7 +181,8 @@ def main():
     if ol:
         res["orset_wire"] = {"_doc": "bench_orset --direct (ORSetWorkload-shaped waves of 200k states, 245 MB), per WAVE: every launch of the "
                                      "5-wave run / 5.  hbm_bytes: the streaming correction (2 x FETCH_SIZE + WRITE_SIZE), an upper bound for "
-                                     "random probes; bound: hbm if >= 50 % of 8 TB/s, valu if >= 50 % of the VALU issue rate, latency if "
+                                     "random probes, beside the random-line reading (1 x FETCH_SIZE + WRITE_SIZE); bound: hbm if the "
+                                     "random-line rate is >= 50 % of 8 TB/s, valu if >= 50 % of the VALU issue rate, latency if "
                                      "waves sit parked on memory (SQ_WAIT_ANY) >= 50 % of their cycles with neither near its peak.",
                              "kernels": ol}
     dst.write_text(json.dumps(res, indent=1) + "\n")
