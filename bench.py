@@ -340,13 +340,21 @@ def bench_exchange(jg, ctx, sync, rank, world, local, steps, warmup):
 
 def bench_exchange_staged(jg, ctx, sync, rank, world, local, steps, warmup):
     """The exchange rehearsed with several ranks on ONE device over gloo (JANUS_BENCH_BACKEND=gloo; RCCL cannot
-    put two ranks on one GPU): janus_gpu/shard.py's host-staged all-to-all around the same route / merge
-    kernels.  Correctness only — the time says nothing about xGMI."""
+    put two ranks on one GPU): the library's own jg_pnc_exchange (csrc/comm.hip: route kernels, the exchange
+    plan, the owner's merge) on its host transport (jg_comm_init_host), whose all-to-all-v is gloo's
+    all_to_all_single over host memory.  Correctness of the shipped path at world > 1 — the time says nothing
+    about xGMI."""
     import numpy as np
     import torch
-    from janus_gpu import shard
-    dev = torch.device("cuda", local)
-    ex = shard.Exchange(dev)
+    import torch.distributed as dist
+
+    def a2a(send, sb, rb):  # the caller's all-to-all-v (gloo over host memory)
+        out = torch.empty(sum(rb), dtype=torch.uint8)
+        inp = torch.frombuffer(bytearray(send), dtype=torch.uint8) if send else torch.empty(0, dtype=torch.uint8)
+        dist.all_to_all_single(out, inp, [int(x) for x in rb], [int(x) for x in sb])
+        return out.numpy().tobytes()
+
+    comm = jg.Comm(ctx, rank, world, alltoallv=a2a)
     store = jg.PNCStore(ctx, EXCH_KEYS, PNC_R, PNC_EB)
     rows = jg.Rows(ctx, EXCH_ROWS, PNC_R, PNC_EB)
     try:
@@ -355,13 +363,17 @@ def bench_exchange_staged(jg, ctx, sync, rank, world, local, steps, warmup):
         zeros = np.zeros((EXCH_ROWS, PNC_R), np.int64)
         rows.upload(zeros, zeros, keys)
         rows.synth(SEED + 11 + rank)
-        wall, _ = timed(ctx, sync, lambda: shard.exchange_pnc(store, rows, ex, dev), steps, warmup)
+        last = {}
+        wall, _ = timed(ctx, sync, lambda: last.update(comm.exchange_pnc(store, rows)), steps, warmup)
+        st = comm.stats()
     finally:
         store.close()
         rows.close()
-    return {"workload": f"cross-shard exchange rehearsal: {world} ranks on one device, host-staged gloo all-to-all",
+        comm.close()
+    return {"workload": f"cross-shard exchange rehearsal: {world} ranks on one device, the library's exchange on its host transport (gloo)",
             "rows_per_s": world * EXCH_ROWS / (wall / steps), "ms_per_step": wall / steps * 1e3,
-            "collective": "torch.distributed all_to_all_single over gloo (rehearsal, not xGMI)"}
+            "records_received_last_step": int(st.records_received), "received_per_source": [int(x) for x in last["received"]],
+            "collective": "jg_comm_init_host: the caller's all-to-all-v = torch.distributed all_to_all_single over gloo (rehearsal, not xGMI)"}
 
 
 JSON_MSGS, JSON_KEYS, JSON_R, JSON_EB, JSON_NODES = 1_000_000, 1_000_000, 5, 4, 4  # one C5 wave, device-resident
