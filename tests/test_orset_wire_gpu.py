@@ -459,3 +459,34 @@ def test_big_set_buckets_fall_back(ctx, commit, monkeypatch):
         assert s.wave_names() == _model_names(model, {})
     finally:
         s.close()
+
+
+def test_tables_sized_from_the_last_wave(ctx, monkeypatch):
+    """The default tail sizes a wave's string / record tables from the previous wave's distinct counts: a small
+    wave, then one with ~180k distinct strings (far past the small wave's room: the tables overflow and the wave
+    commits by the sort path), then another big one (sized from the bound again): every wave equals the
+    oracle."""
+    for v in ("JANUS_ORSET_TAIL", "JANUS_ORSET_COMMIT", "JANUS_ORSET_PARSE"):
+        monkeypatch.delenv(v, raising=False)
+    rng = np.random.default_rng(77)
+    s = jg.ORSetStore(ctx)
+    model, state = {}, {}
+    try:
+        for w, (n_msgs, n_names) in enumerate([(3, 2), (3000, 60), (3000, 60)]):
+            sets, msgs = [], []
+            for i in range(n_msgs):
+                sid = int(rng.integers(0, 400))
+                add = [(f"w{w}m{i}n{j}", J.random_guids(rng, 1)) for j in range(n_names)]
+                msgs.append(J.encode_orset(add, add[:1]))
+                sets.append(sid)
+            before = _copy(model)
+            ea, er, bad, _ = orc.orset_apply_json(sets, msgs, model, state)
+            assert bad is None
+            half = len(msgs) // 2
+            rc, first_bad = s.wave([(sets[:half], msgs[:half]), (sets[half:], msgs[half:])])
+            assert rc == jg.JG_OK and first_bad is None
+            assert s.wave_names() == _model_names(model, before)
+            ga, gr = s.read()
+            assert orc.same_orset(ga, gr, ea, er)
+    finally:
+        s.close()
