@@ -28,6 +28,15 @@ typedef unsigned int nt_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ Tag ld_tag_nt(const uint4* p) {
     return __builtin_bit_cast(Tag, __builtin_nontemporal_load(reinterpret_cast<const nt_v4u*>(p)));
 }
+// Streams' records read through global-address-space pointers: a pointer picked per lane between two
+// streams is otherwise generic (a FLAT load, which also counts on lgkmcnt).
+template <class T>
+using gptr = const __attribute__((address_space(1))) T*;
+template <class T>
+__device__ __forceinline__ gptr<T> as_global(const T* p) { return (gptr<T>)p; }
+__device__ __forceinline__ Tag ld_tag_nt(gptr<uint4> p) {
+    return __builtin_bit_cast(Tag, __builtin_nontemporal_load((gptr<nt_v4u>)p));
+}
 __device__ __forceinline__ void st_tag_nt(uint4* p, uint4 v) {
     __builtin_nontemporal_store(__builtin_bit_cast(nt_v4u, v), reinterpret_cast<nt_v4u*>(p));
 }
@@ -418,12 +427,13 @@ __global__ __launch_bounds__(kOB) void k_union(View a, View b, const uint64_t* _
             while (s < kSeg && sh.off[side][s + 1] <= r) ++s;
             uint64_t slot;
             if (s < kSeg) slot = (uint64_t)((from_a ? ca : cb) + s) * (uint64_t)(from_a ? a.C : b.C) + (r - sh.off[side][s]);
-            else slot = slot_of(from_a ? a : b, r);  // > 64 tiny chunks under one tile (drop-filtered input)
-            rk[it] = __builtin_nontemporal_load((from_a ? a.key : b.key) + slot);  // each record is read once
-            const Tag t = ld_tag_nt((from_a ? a.tag : b.tag) + slot);
+            else slot = from_a ? slot_of(a, r) : slot_of(b, r);  // > 64 tiny chunks under one tile (drop-filtered input); not
+                                                                 // slot_of(from_a ? a : b, r), which copies both Views to scratch
+            rk[it] = __builtin_nontemporal_load(as_global(from_a ? a.key : b.key) + slot);  // each record is read once
+            const Tag t = ld_tag_nt(as_global(from_a ? a.tag : b.tag) + slot);
             rlo[it] = t.lo;
             rhi[it] = t.hi;
-            rord[it] = __builtin_nontemporal_load((from_a ? a.ord : b.ord) + slot) + (from_a ? 0u : b_base);
+            rord[it] = __builtin_nontemporal_load(as_global(from_a ? a.ord : b.ord) + slot) + (from_a ? 0u : b_base);
         }
         unsigned long long pk = 0;
         Tag pt{0, 0};
