@@ -605,6 +605,12 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     const bool direct = w->off && !filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
     if (filter) nd->dmap.resize(n);
 
+    // trace mode: timing events on the copy queue before the first upload and after the last one
+    hipEvent_t up_ev[2] = {nullptr, nullptr};
+    if (trace) {
+        for (hipEvent_t& e : up_ev) JG_HIP(hipEventCreate(&e));
+        JG_HIP(hipEventRecord(up_ev[0], ctx->copy));
+    }
     double t_gather = 0;
     const double t_loop = now_s();
     nd->stats.setup_s = t_loop - t_begin;
@@ -710,6 +716,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         throw;
     }
     const uint64_t nn = m0;  // messages on the device
+    if (trace) JG_HIP(hipEventRecord(up_ev[1], ctx->copy));
     nd->stats.gather_s = t_gather;
     nd->stats.msgs_uploaded = nn;
     nd->stats.bytes_uploaded = b0;
@@ -813,9 +820,21 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     std::memcpy(&applied, jg::pin_at(ctx, 8), 8);
     nd->stats.msgs_applied = applied;
     te[4] = now_s();
-    if (trace)
+    if (trace) {
+        if (!do_orset) te[1] = te[0];
         std::fprintf(stderr, "apply tail: orset check %.0f us, pnc finish %.0f, orset commit %.0f, completions %.0f (after the loop's last upload: %.0f us host)\n",
                      (te[1] - te[0]) * 1e6, (te[2] - te[1]) * 1e6, (te[3] - te[2]) * 1e6, (te[4] - te[3]) * 1e6, (te[4] - te[0]) * 1e6);
+        // device clock: the copy queue from its first upload to the last one's end, and from there to the end of
+        // the wave's last kernel (the final phase's event pair)
+        float up_ms = 0, after_ms = 0, first_ms = 0;
+        JG_HIP(hipEventElapsedTime(&up_ms, up_ev[0], up_ev[1]));
+        JG_HIP(hipEventElapsedTime(&after_ms, up_ev[1], nd->ev[2 * n_ev + 1]));
+        JG_HIP(hipEventElapsedTime(&first_ms, up_ev[0], nd->ev[0]));
+        std::fprintf(stderr, "apply device: uploads %.0f us (%llu chunks, %.1f GB/s of payload over the span), first chunk's kernels at +%.0f us, "
+                     "last kernel %.0f us after the last upload\n",
+                     up_ms * 1e3, (unsigned long long)n_chunks, up_ms > 0 ? b0 / (up_ms * 1e-3) / 1e9 : 0.0, first_ms * 1e3, after_ms * 1e3);
+        for (hipEvent_t e : up_ev) (void)hipEventDestroy(e);
+    }
     double busy = 0;
     for (size_t k = 0; k <= n_ev; ++k) {
         float ms = 0;
