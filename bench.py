@@ -617,8 +617,13 @@ def bench_c1(local):
 DIGEST_MSGS, DIGEST_PER_UPDATE = 1_000_000, 1000  # one C5-sized wave, clientBatchSize-sized UpdateMessages
 DIGEST_PIPE = 8  # waves per pipelined call
 # VALU instructions per 64-byte block of the k_sha_msgs loop (compress + window shift, gfx950 ISA count of
-# csrc/digest.hip) and the chip's VALU issue rate: 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
+# csrc/digest.hip) and the chip's VALU issue rate if every one issued in 2 cycles: 256 CUs x 4
+# SIMDs x 32 lanes/clk x 2.4 GHz.  They do not: v_alignbit_b32 (576 per block) and v_add3_u32 (~240) take
+# ~4.3 cycles per wave64 instruction, v_bitop3_b32 ~2.5 (tools/valu_rate.hip).  The digest roofline's peak
+# is therefore the MEASURED issue ceiling of the same compression code on register-resident blocks at the
+# kernel's occupancy: 27.8-28.0 Gblocks/s (profiles/r04/valu_rate.txt; 4 and 5 waves per SIMD agree).
 SHA_VALU_PER_BLOCK, VALU_LANE_OPS = 1693, 256 * 4 * 32 * 2.4e9
+SHA_CEILING_BLOCKS_PER_S = 27.9e9
 
 
 def digest_wave(n, seed):
@@ -672,11 +677,14 @@ def bench_digest(jg, ctx, sync, rank, steps, warmup):
                           "msgs_per_s": DIGEST_MSGS * DIGEST_PIPE / (wall_p / steps),
                           "ms_per_wave": wall_p / steps / DIGEST_PIPE * 1e3},
             "roofline": {"bound": "valu", "achieved": blocks / kern1 / 1e9, "unit": "Gblocks/s",
-                         "peak": VALU_LANE_OPS / SHA_VALU_PER_BLOCK / 1e9,
-                         "frac": blocks / kern1 / (VALU_LANE_OPS / SHA_VALU_PER_BLOCK),
+                         "peak": SHA_CEILING_BLOCKS_PER_S / 1e9,
+                         "frac": blocks / kern1 / SHA_CEILING_BLOCKS_PER_S,
+                         "peak_source": "measured issue ceiling of csrc/sha256_device.hpp's compression, no memory traffic "
+                                        "(tools/valu_rate.hip, profiles/r04/valu_rate.txt)",
+                         "frac_of_2cycle_issue": blocks / kern1 / (VALU_LANE_OPS / SHA_VALU_PER_BLOCK),
                          "scope": "first level (k_sha_msgs, jg_wave_sha256); the full call adds the second level, a "
                                   "serial chain of second_level_chain_blocks SHA-256 blocks per UpdateMessage "
-                                  "(latency-bound, DESIGN.md section 4)"}}
+                                  "(one wave's issue latency, DESIGN.md section 4)"}}
 
 
 def cpu_digest_baseline():

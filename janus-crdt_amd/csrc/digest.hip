@@ -25,63 +25,36 @@
 #include <vector>
 
 #include "jg_internal.hpp"
+#include "sha256_device.hpp"
 
 namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
-__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
-// v_bitop3_b32 truth tables: bit (s0 << 2 | s1 << 1 | s2) of the immediate is the result for those input bits.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
-__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA); }
-__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8); }
+using jgsha::bswap;
+using jgsha::ch;
+using jgsha::compress;
+using jgsha::maj;
+using jgsha::rotr;
+using jgsha::sha_init;
+using jgsha::xor3;
 
-#define JG_SHA_ROUND(a, b, c, d, e, f, g, h, k, w)                                                     \
-    do {                                                                                                \
-        uint32_t t1_ = (h + (k) + (w)) + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g);       \
-        uint32_t t2_ = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);                         \
-        d += t1_;                                                                                       \
-        h = t1_ + t2_;                                                                                  \
-    } while (0)
-
-// FIPS 180-4 §6.2.2 on one block W[16] (consumed) into H[8].
-__device__ __forceinline__ void compress(uint32_t H[8], uint32_t W[16]) {
-    constexpr uint32_t K[64] = {
-        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-        0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-        0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-        0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-        0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-        0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-        0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-    uint32_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
-#pragma unroll
-    for (int t = 0; t < 64; t += 8) {
-        if (t >= 16) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int i = (t + j) & 15;
-                uint32_t w15 = W[(i + 1) & 15], w2 = W[(i + 14) & 15];
-                W[i] += xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3) + W[(i + 9) & 15] + xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            }
-        }
-        JG_SHA_ROUND(a, b, c, d, e, f, g, h, K[t + 0], W[(t + 0) & 15]);
-        JG_SHA_ROUND(h, a, b, c, d, e, f, g, K[t + 1], W[(t + 1) & 15]);
-        JG_SHA_ROUND(g, h, a, b, c, d, e, f, K[t + 2], W[(t + 2) & 15]);
-        JG_SHA_ROUND(f, g, h, a, b, c, d, e, K[t + 3], W[(t + 3) & 15]);
-        JG_SHA_ROUND(e, f, g, h, a, b, c, d, K[t + 4], W[(t + 4) & 15]);
-        JG_SHA_ROUND(d, e, f, g, h, a, b, c, K[t + 5], W[(t + 5) & 15]);
-        JG_SHA_ROUND(c, d, e, f, g, h, a, b, K[t + 6], W[(t + 6) & 15]);
-        JG_SHA_ROUND(b, c, d, e, f, g, h, a, K[t + 7], W[(t + 7) & 15]);
-    }
-    H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+// An 80-byte window of a payload as five 16-byte granules; dword i of it (i constant after unrolling).
+struct Win { uint4 g0, g1, g2, g3, g4; };
+__device__ __forceinline__ uint32_t win_dw(const Win& w, int i) {
+    const uint4 g = i < 4 ? w.g0 : i < 8 ? w.g1 : i < 12 ? w.g2 : i < 16 ? w.g3 : w.g4;
+    const int c = i & 3;
+    return c == 0 ? g.x : c == 1 ? g.y : c == 2 ? g.z : g.w;
 }
-
-__device__ __forceinline__ void sha_init(uint32_t H[8]) {
-    H[0] = 0x6a09e667; H[1] = 0xbb67ae85; H[2] = 0x3c6ef372; H[3] = 0xa54ff53a;
-    H[4] = 0x510e527f; H[5] = 0x9b05688c; H[6] = 0x1f83d9ab; H[7] = 0x5be0cd19;
+// Granule j of the aligned window at p, or zeros when it starts at or past `end` (then granule 0, which
+// holds payload bytes, is read instead: no address outside the payload's lines).
+__device__ __forceinline__ uint4 ld_granule(uintptr_t p, int j, uintptr_t end) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    using G = const __attribute__((address_space(1))) v4u*;
+    const uintptr_t a = p + 16 * j;
+    const bool in = a < end;
+    const v4u v = *(G)(in ? a : p);
+    return in ? make_uint4(v.x, v.y, v.z, v.w) : make_uint4(0, 0, 0, 0);
 }
 
 // One lane per payload: D[8i..8i+8) = SHA-256 state words of payload i (zeros for a null payload);
@@ -101,27 +74,35 @@ __global__ void __launch_bounds__(kBlock) k_sha_msgs(const uint8_t* __restrict__
     uint32_t H[8];
     sha_init(H);
     const uint64_t nblk = (len + 72) >> 6;  // message + 0x80 + 8-byte length, rounded up to blocks
+    // block b's five granules are loaded while block b - 1 compresses (its words are formed first): each
+    // wave's own ~1.7k VALU instructions hide the load.  The 80-byte window is five uint4 values picked by
+    // constant index (an array indexed through the per-lane select became a dynamic index: the compiler put
+    // it in LDS, one full wait per granule), loaded through a global pointer (an address rebuilt from an
+    // integer is generic: FLAT), without branches (a granule past the payload reads the block's first one
+    // and is zeroed, so nothing outside the wave's byte range is touched).
+    Win w;
+    auto load = [&](uint64_t q0) {
+        const uintptr_t p = (uintptr_t)(bytes + o0 + q0) & ~(uintptr_t)15;
+        w.g0 = ld_granule(p, 0, end);
+        w.g1 = ld_granule(p, 1, end);
+        w.g2 = ld_granule(p, 2, end);
+        w.g3 = ld_granule(p, 3, end);
+        w.g4 = ld_granule(p, 4, end);
+    };
+    if (len > 0) load(0);
     for (uint64_t b = 0; b < nblk; ++b) {
         const uint64_t q0 = b << 6;
         uint32_t W[16];
         if (q0 < len) {
-            const uintptr_t p = (uintptr_t)(bytes + o0 + q0);
-            const uint4* a = reinterpret_cast<const uint4*>(p & ~(uintptr_t)15);
-            const uint32_t s = (uint32_t)(p & 15);
-            uint32_t d[20];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if ((uintptr_t)(a + j) < end) v = a[j];
-                d[4 * j] = v.x; d[4 * j + 1] = v.y; d[4 * j + 2] = v.z; d[4 * j + 3] = v.w;
-            }
-            const uint32_t s4 = s >> 2, sb = s & 3;
+            const uint32_t s = (uint32_t)((uintptr_t)(bytes + o0 + q0) & 15);
+            const bool s1 = (s >> 2) & 1, s2 = (s >> 3) & 1;
+            const uint32_t sb = s & 3;
             uint32_t e[17];
 #pragma unroll
             for (int k = 0; k < 17; ++k) {
-                uint32_t lo = s4 & 1 ? d[k + 1] : d[k];
-                uint32_t hi = s4 & 1 ? d[k + 3] : d[k + 2];
-                e[k] = s4 & 2 ? hi : lo;
+                const uint32_t lo = s1 ? win_dw(w, k + 1) : win_dw(w, k);
+                const uint32_t hi = s1 ? win_dw(w, k + 3) : win_dw(w, k + 2);
+                e[k] = s2 ? hi : lo;
             }
 #pragma unroll
             for (int k = 0; k < 16; ++k) W[k] = __builtin_amdgcn_alignbyte(e[k + 1], e[k], sb);  // bytes q0+4k.. (LE)
@@ -134,6 +115,7 @@ __global__ void __launch_bounds__(kBlock) k_sha_msgs(const uint8_t* __restrict__
             }
 #pragma unroll
             for (int k = 0; k < 16; ++k) W[k] = bswap(W[k]);
+            if (q0 + 64 < len) load(q0 + 64);  // the next block holds payload bytes: its granules now
         } else {  // a block of padding only: 0x80 opens it when the payload filled the previous block
 #pragma unroll
             for (int k = 0; k < 16; ++k) W[k] = 0;
