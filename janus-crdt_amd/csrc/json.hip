@@ -18,7 +18,7 @@
 //            D2H of the status words: first bad message, deferred count.  A bad message = nothing
 //            is written.
 //   sort     hipcub radix sort of the deferred list -> messages grouped by row in commit order.
-//   pass C   k_resolve_emit  one group per row segment walks the row's deferred records in commit
+//   pass C   k_resolve_rows  one lane per row segment walks the row's deferred records in commit
 //                       order and appends the new replica Guids (pVector entries first, then nVector —
 //                       Merge's order) to the row's table: first-insertion order = the stable
 //                       Dictionary's enumeration order; the columns go back into the records.  A walk

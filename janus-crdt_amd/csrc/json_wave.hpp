@@ -490,13 +490,15 @@ __global__ __launch_bounds__(kBlock) void k_apply_slow(const uint8_t* __restrict
 }
 
 // Pass C (new replicas appended in commit order) from pass A's records: no payload is parsed again.
-// One group of kEmitLanes lanes per sorted deferred entry; the group of a row's first entry walks the
-// row's deferred messages in commit order: the lanes stage a message's entry Guids in LDS, the first
-// lane finds or appends each in token order (every pVector entry before any nVector entry,
-// PNCounters.cs:133-143) against the row's first columns cached in LDS, checks repeats within a vector,
-// and writes the columns into the record for pass B.  At a message the group parse did not prove
-// compact (record kReparse) the rest of the walk goes to k_resolve_resume (serial ResolveVis).  G == 1
-// (JANUS_JSON_GROUP=1): the serial walk throughout.  saved[i] = ncols before the walk (for roll-back).
+// One lane per sorted deferred entry; the lane of a row's first entry walks the row's deferred messages
+// in commit order, finds or appends each entry's Guid in token order (every pVector entry before any
+// nVector entry, PNCounters.cs:133-143) against the row's columns, checks repeats within a vector, and
+// writes the columns into the record for pass B.  At a message the group parse did not prove compact
+// (record kReparse) the rest of the walk goes to k_resolve_resume (serial ResolveVis).  G == 1
+// (JANUS_JSON_GROUP=1): the serial walk throughout (k_resolve_serial).  saved[i] = ncols before the walk
+// (for roll-back).  The walk is serial per row either way; round 3 gave each row a 16-lane group whose
+// first lane walked it (the others staged Guids into LDS): 16x the waves for the same serial work, 0.42 ms
+// of a C5 wave whose rows mostly meet a new replica, all of it after the wave's last upload.
 template <int EB>
 __global__ __launch_bounds__(kBlock) void k_resolve_serial(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                            const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
@@ -506,72 +508,54 @@ __global__ __launch_bounds__(kBlock) void k_resolve_serial(const uint8_t* __rest
 }
 
 template <int EB>
-__global__ __launch_bounds__(kBlock) void k_resolve_emit(const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
+__global__ __launch_bounds__(kBlock) void k_resolve_rows(const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
                                                          uint8_t* __restrict__ emit, const Guid16* __restrict__ eguid,
                                                          uint32_t* __restrict__ saved, unsigned long long* __restrict__ status,
                                                          unsigned long long* __restrict__ resume) {
-    constexpr uint32_t L = kEmitLanes;
-    constexpr int kGroups = kBlock / L;
-    __shared__ Guid16 cache[kGroups][L];  // the row's first L columns
-    __shared__ Guid16 eg[kGroups][kEmitMax];
-    __shared__ uint32_t seen[kGroups][16];  // columns met per vector, 256 bits each
-    __shared__ uint32_t bc[kGroups];
-    const uint32_t grp = threadIdx.x / L, g = threadIdx.x % L;
-    const uint64_t i = (uint64_t)blockIdx.x * kGroups + grp;
-    const uint32_t row = i < nd ? (uint32_t)(keys[i] >> 32) : 0;
-    if (i >= nd || (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row)) return;  // not a segment head (group-uniform)
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nd) return;
+    const uint32_t row = (uint32_t)(keys[i] >> 32);
+    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;  // not a segment head
     Guid16* gcols = t.cols + (uint64_t)row * t.R;
     uint32_t nc = t.ncols[row];
-    if (g == 0) saved[i] = nc;
-    if (g < nc) cache[grp][g] = gcols[g];
+    saved[i] = nc;
     for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
         const uint64_t m = (uint32_t)keys[j];
         uint8_t* h = emit + m * emit_stride(EB);
         const uint32_t hdr = *reinterpret_cast<const uint16_t*>(h);
         if (hdr == kReparse) {  // not compact: the serial walk takes over from message j
-            if (g == 0) {
-                t.ncols[row] = nc;
-                resume[atomicAdd(status + 4, 1ull)] = j;
-            }
+            t.ncols[row] = nc;
+            resume[atomicAdd(status + 4, 1ull)] = j;
             return;
         }
         const uint32_t cnt = hdr & ~kNeedsCols;
-        if (g < cnt) eg[grp][g] = eguid[m * kEmitMax + g];
-        seen[grp][g] = 0;  // L == 16 lanes clear the 16 words
-        wave_sync();
-        if (g == 0) {
-            uint16_t* codes = reinterpret_cast<uint16_t*>(h) + 1;
-            uint32_t err = UINT32_MAX, pos = 0, pv = 0;
-            for (uint32_t e = 0; e < cnt; ++e) {
-                const uint32_t vv = codes[e] >> 15;
-                pos = e == 0 || vv != pv ? 0 : pos + 1;  // position within its vector (find_col's hint)
-                pv = vv;
-                const Guid16 x = eg[grp][e];
-                uint32_t col = cached_col<L>(cache[grp], gcols, nc, x, pos);
-                if (col == UINT32_MAX) {
-                    if (nc >= t.R) { err = kErrFull; break; }
-                    col = nc++;
-                    gcols[col] = x;
-                    if (col < L) cache[grp][col] = x;
-                }
-                const uint32_t bit = 1u << (col & 31), wi = vv * 8 + (col >> 5);
-                if (seen[grp][wi] & bit) { err = kErrSyntax; break; }  // repeated Guid in one vector
-                seen[grp][wi] |= bit;
-                codes[e] = (uint16_t)(col | vv << 15);
+        uint16_t* codes = reinterpret_cast<uint16_t*>(h) + 1;
+        Mask256 seen[2];  // columns met per vector
+        uint32_t err = UINT32_MAX, pos = 0, pv = 0;
+        for (uint32_t e = 0; e < cnt; ++e) {
+            const uint32_t vv = codes[e] >> 15;
+            pos = e == 0 || vv != pv ? 0 : pos + 1;  // position within its vector (find_col's hint)
+            pv = vv;
+            const Guid16 x = eguid[m * kEmitMax + e];
+            uint32_t col = find_col(gcols, nc, x, pos);
+            if (col == UINT32_MAX) {
+                if (nc >= t.R) { err = kErrFull; break; }
+                col = nc++;
+                gcols[col] = x;
             }
-            *reinterpret_cast<uint16_t*>(h) = (uint16_t)cnt;  // resolved: pass B applies the record
-            if (err != UINT32_MAX) atomicMin(status + 2, (unsigned long long)m << 2 | err);
-            bc[grp] = err != UINT32_MAX ? ~0u : nc;
+            if (vv ? seen[1].test_set(col) : seen[0].test_set(col)) { err = kErrSyntax; break; }  // repeated Guid in one vector
+            codes[e] = (uint16_t)(col | vv << 15);
         }
-        wave_sync();
-        const uint32_t b = bc[grp];
-        if (b == ~0u) return;
-        nc = b;
+        *reinterpret_cast<uint16_t*>(h) = (uint16_t)cnt;  // resolved: pass B applies the record
+        if (err != UINT32_MAX) {
+            atomicMin(status + 2, (unsigned long long)m << 2 | err);
+            return;
+        }
     }
-    if (g == 0) t.ncols[row] = nc;
+    t.ncols[row] = nc;
 }
 
-// The rest of a row's walk from a message k_resolve_emit handed over (serial ResolveVis, one lane).  A
+// The rest of a row's walk from a message k_resolve_rows handed over (serial ResolveVis, one lane).  A
 // compact message further on in the walk still has its record to resolve: its columns are looked up
 // once its Guids are in the row, so pass B applies it from the record.
 template <int EB>
@@ -620,8 +604,7 @@ void launch_resolve_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_
     if (G == 1) {
         hipLaunchKernelGGL(k_resolve_serial<EB>, dim3(json_blocks(nd, 1)), dim3(kBlock), 0, st, bytes, off, keys, nd, t, saved, status);
     } else {
-        hipLaunchKernelGGL(k_resolve_emit<EB>, dim3(json_blocks(nd, kEmitLanes)), dim3(kBlock), 0, st, keys, nd, t, emit, eguid, saved, status,
-                           resume);
+        hipLaunchKernelGGL(k_resolve_rows<EB>, dim3(json_blocks(nd, 1)), dim3(kBlock), 0, st, keys, nd, t, emit, eguid, saved, status, resume);
     }
 }
 
