@@ -97,10 +97,10 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
     if (i < ns) {
         const uint32_t sid = T.list[i];
         const uint4 mt = T.meta[sid];  // {set, length, id looked up when the chunk's k_ow_strings claimed the slot}
-        if (T.first[sid] < s_lim) {
+        if (T.slot[sid].first < s_lim) {
             uint32_t id = mt.z;
             if (id == kUnresolved) {
-                const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+                const uint64_t ref = (T.slot[sid].word & 0xFFFFFFFFull) - 1;
                 id = tab_find(N, S.key[ref], mt.x, bytes + S.noff[ref], mt.y);
                 if (id != kNoName) sid_id[sid] = id;
             }
@@ -112,9 +112,9 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
         }
     } else if (i - ns < nrec) {
         const uint32_t slot = R.list[i - ns];
-        if (R.mint[slot] < t_lim) {
+        if (R.slot[slot].mint < t_lim) {
             r_live = true;
-            r_key = R.key[slot];
+            r_key = R.slot[slot].key;
         }
     }
     const uint32_t sp = bucket_add(s_new, s_set, B.scnt + s_set);
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
         if (r < cnt) {
             const uint32_t i = B.sitem[o0 + r];
             item[r] = i;
-            key[r] = T.first[T.list[i]];
+            key[r] = T.slot[T.list[i]].first;
         }
         perm[r] = (uint16_t)r;
     }
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
     const uint32_t next = N.next_id[s], gen = N.set_gen[s];
     for (uint32_t r = r0; r < r1; ++r) {
         const uint32_t sid = T.list[item[perm[r]]];
-        const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+        const uint64_t ref = (T.slot[sid].word & 0xFFFFFFFFull) - 1;
         const uint32_t len = lens[r];
         const uint64_t id = (uint64_t)next + r;
         if (id >= JG_NULL_ELEM - 1) atomicOr(status + 8, 1ull);
@@ -326,13 +326,13 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_records(Sparse S, StrTab T, Rec
     for (uint32_t r = threadIdx.x; r < P; r += kCbBlock) {
         if (r < cnt) {
             const uint32_t slot = R.list[items[o0 + r]];
-            const uint64_t u = (R.word[slot] & 0xFFFFFFFFull) - 1;
+            const uint64_t u = (R.slot[slot].word & 0xFFFFFFFFull) - 1;
             const unsigned long long id = S.trk[u];
             elem[r] = (id >> 63) ? JG_NULL_ELEM : sid_id[(uint32_t)(id >> 1)];
             const Tag16 g = S.tval[u];
             lo[r] = g.lo;
             hi[r] = g.hi;
-            mint[r] = R.mint[slot];
+            mint[r] = R.slot[slot].mint;
         }
         perm[r] = (uint16_t)r;
     }

@@ -39,9 +39,23 @@ constexpr int kTabWaves = kBlock / 64;
 // one counter took every wave's append and serialised the insert kernels (360 us per 32k-state chunk).
 constexpr uint32_t kLists = 16;
 constexpr uint32_t kCountStride = 32;  // counters 256 B apart: atomics on one L2 line serialise
+// One 16-byte slot per table entry: a probe's word and the field every probe that hits then updates share
+// one line (round 3 kept them in separate arrays: two scattered lines per entry / tag reference).  Cleared
+// to {0, ~0, 0} per wave (k_tab_clear).
+struct alignas(16) StrSlot {
+    unsigned long long word;  // (key >> 32) << 32 | (entry slot + 1) of the string's first inserter; 0 = empty
+    uint32_t first;           // smallest canonical entry index naming the string
+    uint32_t pad;
+};
+struct alignas(16) RecSlot {
+    unsigned long long word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
+    uint32_t mint;            // smallest tag slot holding the record (arrival ordinal)
+    uint32_t key;             // side << 31 | set, written by the claimant (the commit's bucket, without the string chain)
+};
+static_assert(sizeof(StrSlot) == 16 && sizeof(RecSlot) == 16, "one 16-byte slot");
+
 struct StrTab {
-    unsigned long long* word;  // (key >> 32) << 32 | (entry slot + 1) of the string's first inserter; 0 = empty
-    uint32_t* first;           // smallest canonical entry index naming the string
+    StrSlot* slot;
     uint64_t mask;
     uint32_t* list;
     unsigned long long* n;
@@ -50,14 +64,17 @@ struct StrTab {
                                // 16-byte read for the commit instead of a chain through the first entry
 };
 struct RecTab {
-    unsigned long long* word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
-    uint32_t* mint;            // smallest tag slot holding the record (arrival ordinal)
+    RecSlot* slot;
     uint64_t mask;
     uint32_t* list;
     unsigned long long* n;
     uint64_t sub_cap;
-    uint32_t* key;             // per claimed slot: side << 31 | set (the commit's bucket, without the string chain)
 };
+
+__global__ void k_tab_clear(uint4* __restrict__ slots, uint64_t n) {  // {word 0, ~0, 0}: empty, no first / mint yet
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        slots[i] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+}
 
 // Lanes that claimed a slot append it to their workgroup's sub-list: one atomic per wave (claims are a few
 // per message).  A full sub-list raises the overflow word (the wave takes the sort path).
@@ -126,9 +143,9 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         const unsigned long long word = (key >> 32) << 32 | (slot + 1);
         uint64_t p = key & T.mask;
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
-            unsigned long long w = T.word[p];
+            unsigned long long w = T.slot[p].word;
             if (w == 0) {
-                w = atomicCAS(T.word + p, 0ull, word);
+                w = atomicCAS(&T.slot[p].word, 0ull, word);
                 if (w == 0) {
                     sid = (uint32_t)p;
                     fresh = true;
@@ -148,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
             over = true;
         } else {
             const uint32_t c = (uint32_t)es + (!rem_first ? q : (q < n_rem ? n_add + q : q - n_rem));  // canonical: addSet first
-            if (T.first[sid] > c) atomicMin(T.first + sid, c);
+            if (T.slot[sid].first > c) atomicMin(&T.slot[sid].first, c);
         }
         S.sid[slot] = sid;
         if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
@@ -220,13 +237,13 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
         uint64_t p = h & T.mask;
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
             // most references repeat a record seen earlier in the wave: a plain load settles those
-            unsigned long long w = T.word[p];
+            unsigned long long w = T.slot[p].word;
             if (w == 0) {
-                w = atomicCAS(T.word + p, 0ull, word);
+                w = atomicCAS(&T.slot[p].word, 0ull, word);
                 if (w == 0) {
                     slot = p;
                     fresh = true;
-                    T.key[slot] = (uint32_t)(id & 1) << 31 | set;  // the record's set is its message's
+                    T.slot[slot].key = (uint32_t)(id & 1) << 31 | set;  // the record's set is its message's
                     break;
                 }
             }
@@ -239,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
             }
         }
         if (slot == ~0ull) over = true;
-        else if (T.mint[slot] > (uint32_t)t) atomicMin(T.mint + slot, (uint32_t)t);
+        else if (T.slot[slot].mint > (uint32_t)t) atomicMin(&T.slot[slot].mint, (uint32_t)t);
         }
         list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow);
     }
@@ -249,13 +266,12 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
 // ---- commit from the tables ----------------------------------------------------------------------------
 struct RecLive {  // list entry i: a record of side `side` whose first occurrence lies before the commit limit
     const uint32_t* list;
-    const unsigned long long* word;
-    const uint32_t* mint;
+    const RecSlot* slot;
     const unsigned long long* trk;
     uint32_t lim, side;
     __host__ __device__ bool operator()(const uint32_t& i) const {
-        const uint32_t s = list[i];
-        return mint[s] < lim && (uint32_t)(trk[(word[s] & 0xFFFFFFFFull) - 1] & 1) == side;
+        const RecSlot& e = slot[list[i]];
+        return e.mint < lim && (uint32_t)(trk[(e.word & 0xFFFFFFFFull) - 1] & 1) == side;
     }
 };
 
@@ -267,15 +283,15 @@ __global__ void k_ow_sresolve(Sparse S, const uint8_t* __restrict__ bytes, StrTa
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= count) return;
     const uint32_t sid = T.list[i];
-    if (T.first[sid] >= lim) {
+    if (T.slot[sid].first >= lim) {
         newk[i] = kNone;
         return;
     }
-    const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+    const uint64_t ref = (T.slot[sid].word & 0xFFFFFFFFull) - 1;
     const uint32_t set = S.set[ref];
     const uint32_t id = tab_find(N, S.key[ref], set, bytes + S.noff[ref], S.meta[ref] & 0x7FFFFFFFu);
     sid_id[sid] = id;
-    newk[i] = id != kNoName ? kNone : ((unsigned long long)set << 32 | T.first[sid]);
+    newk[i] = id != kNoName ? kNone : ((unsigned long long)set << 32 | T.slot[sid].first);
 }
 
 // New strings sorted by (set, first entry): the r-th new string of a set takes next_id + r (k_ow_assign's
@@ -293,7 +309,7 @@ __global__ void k_ow_sassign(Sparse S, const uint8_t* __restrict__ bytes, StrTab
     const uint64_t id = (uint64_t)N.next_id[set] + r;
     if (id >= JG_NULL_ELEM - 1) atomicOr(status + 3, 1ull);
     const uint32_t sid = snv[k];
-    const uint64_t ref = (T.word[sid] & 0xFFFFFFFFull) - 1;
+    const uint64_t ref = (T.slot[sid].word & 0xFFFFFFFFull) - 1;
     const uint32_t len = S.meta[ref] & 0x7FFFFFFFu;
     sid_id[sid] = (uint32_t)id;
     const uint64_t g = g0 + k;
@@ -316,14 +332,14 @@ __global__ void k_ow_rgather(Sparse S, StrTab ST, RecTab RT, const uint32_t* __r
     const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= *count) return;
     const uint32_t slot = RT.list[idx[j]];
-    const uint64_t u = (RT.word[slot] & 0xFFFFFFFFull) - 1;
+    const uint64_t u = (RT.slot[slot].word & 0xFFFFFFFFull) - 1;
     const unsigned long long id = S.trk[u];
     unsigned long long key;
     if (id >> 63) {
         key = ((id >> 1) & 0xFFFFFFFFull) << 32 | JG_NULL_ELEM;
     } else {
         const uint32_t sid = (uint32_t)(id >> 1);
-        const uint64_t ref = (ST.word[sid] & 0xFFFFFFFFull) - 1;
+        const uint64_t ref = (ST.slot[sid].word & 0xFFFFFFFFull) - 1;
         key = (unsigned long long)S.set[ref] << 32 | sid_id[sid];
     }
     dk[j] = key;

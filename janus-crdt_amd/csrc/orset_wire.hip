@@ -841,14 +841,14 @@ __global__ void k_fix_runs(const unsigned long long* __restrict__ skey, const Ta
 }
 
 __global__ void k_gather_recs(const unsigned long long* __restrict__ dk, const Tag16* __restrict__ dt, const uint32_t* __restrict__ ds,
-                              const uint32_t* __restrict__ mint, const uint32_t* __restrict__ perm, uint64_t n, unsigned long long* __restrict__ ok,
-                              Tag16* __restrict__ ot, uint32_t* __restrict__ oo) {
+                              const uint32_t* __restrict__ mint, uint32_t mstride, const uint32_t* __restrict__ perm, uint64_t n,
+                              unsigned long long* __restrict__ ok, Tag16* __restrict__ ot, uint32_t* __restrict__ oo) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t p = perm[i];
     ok[i] = dk[p];
     ot[i] = dt[p];
-    oo[i] = mint[ds[p]];
+    oo[i] = mint[(uint64_t)ds[p] * mstride];  // mstride: 1 (dedup table's array) or 4 (the record table's 16-byte slots)
 }
 
 #include "orset_tables.hpp"
@@ -904,8 +904,8 @@ struct jg_orset_wire {
     uint64_t resorts = 0;  // waves whose entries were sorted again on full keys (a long impure run)
     // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
-    jg::DevBuf st_word, st_first, st_list, rt_word, rt_mint, rt_list, sid_id, ovf;  // ovf: overflow word, sub-list counts
-    jg::DevBuf st_meta, rt_key;  // per claimed slot: the string's {set, length, id}, the record's side << 31 | set
+    jg::DevBuf st_slot, st_list, rt_slot, rt_list, sid_id, ovf;  // 16-byte table slots (orset_tables.hpp); ovf: overflow word, sub-list counts
+    jg::DevBuf st_meta;  // per claimed string slot: the string's {set, length, id}
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
     jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
@@ -1163,12 +1163,12 @@ Entries entries_of(jg_orset_wire* w) {
 
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
 StrTab str_tab(jg_orset_wire* w) {
-    return StrTab{w->st_word.as<unsigned long long>(), w->st_first.as<uint32_t>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
+    return StrTab{w->st_slot.as<StrSlot>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
                   w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8, w->st_meta.as<uint4>()};
 }
 RecTab rec_tab(jg_orset_wire* w) {
-    return RecTab{w->rt_word.as<unsigned long long>(), w->rt_mint.as<uint32_t>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
-                  w->ovf.as<unsigned long long>() + (1 + kLists) * kCountStride, w->rt_cap / 8, w->rt_key.as<uint32_t>()};
+    return RecTab{w->rt_slot.as<RecSlot>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
+                  w->ovf.as<unsigned long long>() + (1 + kLists) * kCountStride, w->rt_cap / 8};
 }
 
 // A wave opens: size and clear its string / record tables (queued on the compute stream, ahead of the first
@@ -1194,27 +1194,25 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     const uint64_t sc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, want_s)));
     const uint64_t rc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, want_r)));
     if (w->st_alloc < sc) {  // allocations only grow; the active part is the first st_cap slots
-        w->st_word.alloc(sc * 8);
-        w->st_first.alloc(sc * 4);
+        w->st_slot.alloc(sc * sizeof(StrSlot));
         w->st_meta.alloc(sc * 16);
         w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
         w->st_alloc = sc;
     }
     if (w->rt_alloc < rc) {
-        w->rt_word.alloc(rc * 8);
-        w->rt_mint.alloc(rc * 4);
-        w->rt_key.alloc(rc * 4);
+        w->rt_slot.alloc(rc * sizeof(RecSlot));
         w->rt_list.alloc((rc / 8) * kLists * 4);
         w->rt_alloc = rc;
     }
     w->st_cap = sc;
     w->rt_cap = rc;
     if (!w->ovf.p) w->ovf.alloc((1 + 2 * kLists) * kCountStride * 8);
-    JG_HIP(hipMemsetAsync(w->st_word.p, 0, w->st_cap * 8, ctx->stream));
-    JG_HIP(hipMemsetAsync(w->st_first.p, 0xFF, w->st_cap * 4, ctx->stream));
-    JG_HIP(hipMemsetAsync(w->rt_word.p, 0, w->rt_cap * 8, ctx->stream));
-    JG_HIP(hipMemsetAsync(w->rt_mint.p, 0xFF, w->rt_cap * 4, ctx->stream));
+    hipLaunchKernelGGL(k_tab_clear, dim3((unsigned)std::min<uint64_t>(4096, (w->st_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       w->st_slot.as<uint4>(), w->st_cap);
+    hipLaunchKernelGGL(k_tab_clear, dim3((unsigned)std::min<uint64_t>(4096, (w->rt_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       w->rt_slot.as<uint4>(), w->rt_cap);
+    JG_HIP(hipGetLastError());
     JG_HIP(hipMemsetAsync(w->ovf.p, 0, (1 + 2 * kLists) * kCountStride * 8, ctx->stream));  // overflow, sub-list counts
 }
 
@@ -1436,7 +1434,8 @@ void sort_side_begin(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_
     JG_HIP(hipGetLastError());
 }
 
-void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out, bool long_run, const uint32_t* mint) {
+void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bits, jg_stream_soa& out, bool long_run, const uint32_t* mint,
+                   uint32_t mstride) {
     if (n == 0) return;
     const auto* dk = w->dk[sd].as<unsigned long long>();
     const auto* dt = w->dt[sd].as<Tag16>();
@@ -1452,8 +1451,8 @@ void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bi
             std::swap(p, q);
         }
     }
-    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), mint, p,
-                       n, out.key.as<unsigned long long>(), out.tag.as<Tag16>(), out.ord.as<uint32_t>());
+    hipLaunchKernelGGL(k_gather_recs, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, dk, dt, w->ds[sd].as<uint32_t>(), mint, mstride,
+                       p, n, out.key.as<unsigned long long>(), out.tag.as<Tag16>(), out.ord.as<uint32_t>());
     JG_HIP(hipGetLastError());
 }
 
@@ -1624,8 +1623,8 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     ensure(w->fslot, nrec * 4 + 4);
     JG_HIP(hipMemsetAsync(st + 4, 0, 16, ctx->stream));
     if (nrec) {
-        select_marked(ctx, w, RecLive{RT.list, RT.word, RT.mint, S.trk, t_lim, 0}, nrec, w->fidx.as<uint32_t>(), st + 4);
-        select_marked(ctx, w, RecLive{RT.list, RT.word, RT.mint, S.trk, t_lim, 1}, nrec, w->fslot.as<uint32_t>(), st + 5);
+        select_marked(ctx, w, RecLive{RT.list, RT.slot, S.trk, t_lim, 0}, nrec, w->fidx.as<uint32_t>(), st + 4);
+        select_marked(ctx, w, RecLive{RT.list, RT.slot, S.trk, t_lim, 1}, nrec, w->fslot.as<uint32_t>(), st + 5);
     }
     unsigned long long hh[6];  // [1] new strings, [2] pool bytes used, [3] id overflow, [4] [5] records per side
     if (tr) tc[1] = now();
@@ -1665,8 +1664,8 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     unsigned long long long_run[2];
     read_words(ctx, st + 6, long_run, 2);
     if (tr) tc[3] = now();
-    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, RT.mint);
-    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, RT.mint);
+    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, &RT.slot[0].mint, 4);
+    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, &RT.slot[0].mint, 4);
     jg::orset_merge_store(s, w->recs);
     if (tr) {
         tc[4] = now();
@@ -1792,8 +1791,8 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     sort_side_begin(ctx, w, 1, cnt[1], key_bits, nt, w->recs->rem, st + 7);
     unsigned long long long_run[2];
     read_words(ctx, st + 6, long_run, 2);
-    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, w->dmin.as<uint32_t>());
-    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, w->dmin.as<uint32_t>());
+    sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, w->dmin.as<uint32_t>(), 1);
+    sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, w->dmin.as<uint32_t>(), 1);
     jg::orset_merge_store(s, w->recs);
 }
 
