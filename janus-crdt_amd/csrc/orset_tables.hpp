@@ -18,6 +18,7 @@
 //                  (set, side) for a null tag set.
 //   k_ow_rins      each tag reference into the record table (exact compare of identity + tag), the slot
 //                  keeping the smallest tag index = the record's arrival ordinal.
+//                  Both: kMsgsPerWave messages per wave, their references dealt over the lanes.
 //
 // The commit then resolves only the distinct strings against the element table and sorts only the
 // distinct records.  A table that runs out of probes (more distinct strings / records than it was sized
@@ -35,7 +36,7 @@ constexpr uint32_t kDupScan = 512;   // entries per message the in-wave duplicat
 constexpr int kTabWaves = kBlock / 64;
 
 // The slots a table's inserts claimed, appended as they are claimed, so the commit walks these instead of the
-// whole table: kLists sub-lists of sub_cap entries (list j of workgroup blockIdx % kLists, count n[j]) —
+// whole table: kLists sub-lists of sub_cap entries (list j = the appending wave's message index % kLists, count n[j]) —
 // one counter took every wave's append and serialised the insert kernels (360 us per 32k-state chunk).
 constexpr uint32_t kLists = 16;
 constexpr uint32_t kCountStride = 32;  // counters 256 B apart: atomics on one L2 line serialise
@@ -78,11 +79,14 @@ __global__ void k_tab_clear(uint4* __restrict__ slots, uint64_t n) {  // {word 0
 
 // Lanes that claimed a slot append it to their workgroup's sub-list: one atomic per wave (claims are a few
 // per message).  A full sub-list raises the overflow word (the wave takes the sort path).
+// spread: the sub-list is spread % kLists — the caller's message index (and round), so a wave's claims land in
+// all sub-lists however few workgroups a chunk has (by workgroup, a 30-message chunk of 4-message waves filled
+// two of the sixteen).
 __device__ __forceinline__ void list_append(bool fresh, uint32_t slot, uint32_t* list, unsigned long long* n, uint64_t sub_cap,
-                                            unsigned long long* overflow) {
+                                            unsigned long long* overflow, uint64_t spread) {
     const unsigned long long b = __ballot(fresh);
     if (!b) return;
-    const uint32_t lane = threadIdx.x & 63, j = blockIdx.x % kLists;
+    const uint32_t lane = threadIdx.x & 63, j = (uint32_t)(spread % kLists);
     const int leader = __ffsll((long long)b) - 1;
     unsigned long long base = 0;
     if ((int)lane == leader) base = atomicAdd(n + j * kCountStride, (unsigned long long)__popcll(b));
@@ -107,6 +111,43 @@ __device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* byte
                                             uint32_t len_a, unsigned long long pfx_a, uint64_t noff_a, uint64_t b) {
     if (S.set[b] != set_a || S.key[b] != key_a || (S.meta[b] & 0x7FFFFFFFu) != len_a || S.pfx[b] != pfx_a) return false;
     return len_a <= 8 || same_bytes(bytes + S.noff[b] + 8, bytes + noff_a + 8, len_a - 8);
+}
+
+// kMsgsPerWave consecutive messages per wave for k_ow_rkeys / k_ow_rins, their tag references dealt over the
+// 64 lanes in rounds: one message per wave left most lanes idle (≈23 references per ORSetWorkload state).
+// Measured (round 4, one box): k_ow_rkeys 99 -> 69 us per wave, k_ow_rins 329 -> 317; the same for
+// k_ow_strings was 7 % SLOWER (549 -> 589 us: its per-entry probe and string compare are a longer dependent
+// chain, so packing its lanes only lengthens each wave) and it keeps one message per wave.
+constexpr int kMsgsPerWave = 4;
+
+// The wave's messages [mb, mb + M) of [m0, m1): lane j < M holds message j's item count (0 for another
+// kind's message or past m1) and its exclusive prefix; the total is wave-uniform.  Every shuffle reads lanes
+// 0..M-1, so the callers run their item rounds with all 64 lanes active (a lane past the total idles).
+template <int M>
+struct WaveMsgs {
+    uint32_t cnt = 0, pre = 0, total = 0;
+    // the message of item q (< total): the last j whose prefix is <= q (a message without items shares its
+    // prefix with the next one and never owns an item)
+    __device__ __forceinline__ uint32_t owner(uint32_t q) const {
+        uint32_t j = 0;
+#pragma unroll
+        for (int x = 1; x < M; ++x)
+            if (q >= (uint32_t)__shfl((int)pre, x, 64)) j = (uint32_t)x;
+        return j;
+    }
+    __device__ __forceinline__ void scan(uint32_t lane) {
+        uint32_t incl = lane < (uint32_t)M ? cnt : 0u;
+#pragma unroll
+        for (int d = 1; d < M; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= (uint32_t)d) incl += y;
+        }
+        total = (uint32_t)__shfl((int)incl, M - 1, 64);
+        pre = incl - cnt;
+    }
+};
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)src, 64) | (uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src, 64) << 32;
 }
 
 // The lane that claims a string's slot also looks the string up in the store's element table (N: committed
@@ -170,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         S.sid[slot] = sid;
         if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
         }
-        list_append(fresh, sid, T.list, T.n, T.sub_cap, overflow);
+        list_append(fresh, sid, T.list, T.n, T.sub_cap, overflow, m + q0 / 64);
     }
     if (cnt > kDupScan) over = true;  // the duplicate check below would miss pairs: the sort path decides
     if (__ballot(over) != 0) {
@@ -192,45 +233,69 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
 
 __global__ __launch_bounds__(kBlock) void k_ow_rkeys(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                      const unsigned long long* __restrict__ nt, uint64_t m0, uint64_t m1) {
+    constexpr int M = kMsgsPerWave;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
-    if (m >= m1) return;
-    const uint32_t set = mset[m];
-    if (set == jg::kSkipIdx) return;
-    const uint32_t k = (uint32_t)nt[m];
-    const uint64_t es = (off[m] + kEntryDiv - 1) / kEntryDiv, ts = (off[m] + kTagDiv - 1) / kTagDiv;
-    for (uint32_t q = lane; q < k; q += 64) {
-        const unsigned long long r = S.tref[ts + q];
+    const uint64_t mb = m0 + ((uint64_t)blockIdx.x * kTabWaves + wv) * M;
+    if (mb >= m1) return;  // wave-uniform
+    WaveMsgs<M> W;
+    uint32_t set = jg::kSkipIdx;
+    uint64_t es = 0, ts = 0;
+    if (lane < (uint32_t)M && mb + lane < m1) {
+        set = mset[mb + lane];
+        if (set != jg::kSkipIdx) {
+            W.cnt = (uint32_t)nt[mb + lane];
+            es = (off[mb + lane] + kEntryDiv - 1) / kEntryDiv;
+            ts = (off[mb + lane] + kTagDiv - 1) / kTagDiv;
+        }
+    }
+    W.scan(lane);
+    for (uint32_t q0 = 0; q0 < W.total; q0 += 64) {  // wave-uniform rounds: the shuffles read lanes 0..M-1, which must be active
+        const uint32_t q = q0 + lane;
+        const uint32_t j = W.owner(q < W.total ? q : 0);
+        const uint32_t qj = q - (uint32_t)__shfl((int)W.pre, (int)j, 64), sj = (uint32_t)__shfl((int)set, (int)j, 64);
+        const uint64_t t = shfl64(ts, j) + qj, e0 = shfl64(es, j);
+        if (q >= W.total) continue;
+        const unsigned long long r = S.tref[t];
         const unsigned long long side = r >> 62 & 1;
         unsigned long long id;
         if (r >> 63) {
-            id = 1ull << 63 | (unsigned long long)set << 1 | side;
+            id = 1ull << 63 | (unsigned long long)sj << 1 | side;
         } else {
-            const uint32_t sid = S.sid[es + (uint32_t)r];
+            const uint32_t sid = S.sid[e0 + (uint32_t)r];
             id = sid == kNoSid ? kNone : ((unsigned long long)sid << 1 | side);
         }
-        S.trk[ts + q] = id;
+        S.trk[t] = id;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                     const unsigned long long* __restrict__ nt, uint64_t m0, uint64_t m1, RecTab T,
                                                     unsigned long long* __restrict__ overflow) {
+    constexpr int M = kMsgsPerWave;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
-    if (m >= m1) return;
-    const uint32_t set = mset[m];
-    if (set == jg::kSkipIdx) return;
-    const uint32_t k = (uint32_t)nt[m];
-    const uint64_t ts = (off[m] + kTagDiv - 1) / kTagDiv;
+    const uint64_t mb = m0 + ((uint64_t)blockIdx.x * kTabWaves + wv) * M;
+    if (mb >= m1) return;  // wave-uniform
+    WaveMsgs<M> W;
+    uint32_t set = jg::kSkipIdx;
+    uint64_t ts = 0;
+    if (lane < (uint32_t)M && mb + lane < m1) {
+        set = mset[mb + lane];
+        if (set != jg::kSkipIdx) {
+            W.cnt = (uint32_t)nt[mb + lane];
+            ts = (off[mb + lane] + kTagDiv - 1) / kTagDiv;
+        }
+    }
+    W.scan(lane);
     bool over = false;
-    for (uint32_t q0 = 0; q0 < k; q0 += 64) {
+    for (uint32_t q0 = 0; q0 < W.total; q0 += 64) {  // wave-uniform bounds: list_append's ballot needs every lane
         const uint32_t q = q0 + lane;
-        const uint64_t t = ts + q;
-        const unsigned long long id = q < k ? S.trk[t] : kNone;
+        const uint32_t j = W.owner(q < W.total ? q : 0);
+        const uint32_t sj = (uint32_t)__shfl((int)set, (int)j, 64);
+        const uint64_t t = shfl64(ts, j) + (q - (uint32_t)__shfl((int)W.pre, (int)j, 64));
+        const unsigned long long id = q < W.total ? S.trk[t] : kNone;
         bool fresh = false;
         uint64_t slot = ~0ull;
-        if (id != kNone) {  // kNone: its string found no slot (the overflow word is up already), or past the message
+        if (id != kNone) {  // kNone: its string found no slot (the overflow word is up already), or past the wave's items
         const Tag16 g = S.tval[t];
         const uint64_t h = rec_hash(id, g, 0);
         const unsigned long long word = (h >> 32) << 32 | (t + 1);
@@ -243,7 +308,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
                 if (w == 0) {
                     slot = p;
                     fresh = true;
-                    T.slot[slot].key = (uint32_t)(id & 1) << 31 | set;  // the record's set is its message's
+                    T.slot[slot].key = (uint32_t)(id & 1) << 31 | sj;  // the record's set is its message's
                     break;
                 }
             }
@@ -258,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
         if (slot == ~0ull) over = true;
         else if (T.slot[slot].mint > (uint32_t)t) atomicMin(&T.slot[slot].mint, (uint32_t)t);
         }
-        list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow);
+        list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow, mb / M + q0 / 64);
     }
     if (__ballot(over) != 0 && lane == 0) *overflow = 1;
 }

@@ -1218,17 +1218,18 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
 
 // The chunk's strings and records into the wave's tables (after its parse, same stream).
 void launch_tables(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
-    const dim3 grid((unsigned)((m1 - m0 + kTabWaves - 1) / kTabWaves));
     const Sparse S = sparse_of(w);
     auto* ovf = w->ovf.as<unsigned long long>();
     // the element table and the sets' generation words as they stand (both only change at a commit); a wave
     // before the first commit has no table yet: every string is resolved by the commit
     const uint32_t set_lim = w->tab_cap ? (uint32_t)std::min<uint64_t>(w->set_cap, 0xFFFFFFFFull) : 0u;
+    const dim3 grid((unsigned)((m1 - m0 + kTabWaves - 1) / kTabWaves));  // one message per wave
+    const dim3 grid_m((unsigned)((m1 - m0 + kTabWaves * kMsgsPerWave - 1) / (kTabWaves * kMsgsPerWave)));  // kMsgsPerWave messages per wave
     hipLaunchKernelGGL(k_ow_strings, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->vbytes, w->ne.as<unsigned long long>(),
                        w->na.as<uint32_t>(), m0, m1, str_tab(w), w->err.as<unsigned long long>(), ovf, names_of(w), set_lim,
                        w->sid_id.as<uint32_t>());
-    hipLaunchKernelGGL(k_ow_rkeys, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1);
-    hipLaunchKernelGGL(k_ow_rins, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1, rec_tab(w), ovf);
+    hipLaunchKernelGGL(k_ow_rkeys, grid_m, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1);
+    hipLaunchKernelGGL(k_ow_rins, grid_m, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1, rec_tab(w), ovf);
     JG_HIP(hipGetLastError());
 }
 
