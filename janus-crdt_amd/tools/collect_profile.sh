@@ -16,5 +16,8 @@ for p in pmc_FETCH_SIZE pmc_WRITE_SIZE pmc_exch_FETCH_SIZE pmc_exch_WRITE_SIZE p
     [ -f "$SRC/$p/run_counter_collection.csv" ] && cp "$SRC/$p/run_counter_collection.csv" "$DST/$p.csv"
 done
 cp "$SRC/pmc_$R.json" "profiles/pmc_$R.json"
-[ -f "$SRC/bench_final.json" ] && cp "$SRC/bench_final.json" "$DST/bench_final.json"
+# the bench line (its last stdout line) and the kernel statistics of the same, traced process
+[ -f "$SRC/bench_final.json" ] && tail -1 "$SRC/bench_final.json" > "$DST/bench_final.json"
+[ -f "$SRC/trace_final/run_kernel_stats.csv" ] && cp "$SRC/trace_final/run_kernel_stats.csv" "$DST/kernel_stats_bench_final.csv"
+[ -f "$SRC/bench_final_untraced.json" ] && tail -1 "$SRC/bench_final_untraced.json" > "$DST/bench_final_untraced.json"
 echo "collected into $DST"
