@@ -244,8 +244,14 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
                       const uint32_t* rem_ord);
 // orset.hip: largest ord + 1 of n device ords (0 if n == 0), synchronous.
 uint64_t ord_span(jg_ctx* ctx, const uint32_t* ord, uint64_t n);
-// orset.hip: s = s ∪ src (both streams), synchronous, src's streams may be dense or chunked.
-void orset_merge_store(jg_orset* s, jg_orset* src);
+// orset.hip: s = s ∪ src (both streams), src's streams may be dense or chunked; synchronous (the union's error
+// flag and counts read back) unless `defer`: then the counts stay pending for orset_pin_pending / _settle.
+void orset_merge_store(jg_orset* s, jg_orset* src, bool defer = false);
+// orset.hip: a deferred union's error flag and counts queued into the context's page-locked bytes at [at, at
+// + 24) (no sync: the caller's own pin_sync brings them with its words; false if nothing is pending), and
+// taken from there after that sync (the flag raised as the synchronous merge would).
+bool orset_pin_pending(jg_orset* s, size_t at);
+void orset_settle_pending(jg_orset* s, size_t at);
 // orset.hip: room in the store's union targets for that many more records (no sync; skipped while counts are pending).
 void orset_reserve_union(jg_orset* s, uint64_t add_in, uint64_t rem_in);
 

@@ -779,6 +779,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
 
     // safe-update completions of the messages before the cut, in commit order
     uint64_t ndone = 0;
+    bool orset_pending = false;  // the OR-Set commit's union counts ride on this phase's page-locked read
     JG_HIP(hipMemsetAsync(d_status + 2, 0, 8, ctx->stream));
     if (cut) hipLaunchKernelGGL(k_count_applied, dim3((unsigned)std::min<uint64_t>(1024, blocks_for(cut))), dim3(kBlock), 0, ctx->stream, d_rows, d_mset, cut,
                                 d_status + 2);
@@ -799,7 +800,9 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         JG_HIP(hipGetLastError());
         unsigned long long k = 0;
         jg::pin_get(ctx, 0, d_status + 1, 16);  // the completions' count and the applied count
+        orset_pending = do_orset && jg::orset_pin_pending(nd->orset, 64);  // and the OR-Set commit's union counts
         jg::pin_sync(ctx);
+        if (orset_pending) jg::orset_settle_pending(nd->orset, 64), orset_pending = false;
         std::memcpy(&k, jg::pin_at(ctx, 0), 8);
         ndone = k;
         if (completed && k) {
@@ -812,12 +815,14 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             JG_HIP(hipGetLastError());
         }
         jg::pin_get(ctx, 8, d_status + 2, 8);  // the applied count with the final sync
+        orset_pending = do_orset && jg::orset_pin_pending(nd->orset, 64);  // and the OR-Set commit's union counts
         jg::pin_sync(ctx);
     }
     JG_HIP(hipEventRecord(nd->event(2 * n_ev + 1), ctx->stream));
     unsigned long long applied = 0;
     JG_HIP(hipEventSynchronize(nd->event(2 * n_ev + 1)));
     std::memcpy(&applied, jg::pin_at(ctx, 8), 8);
+    if (orset_pending) jg::orset_settle_pending(nd->orset, 64);
     nd->stats.msgs_applied = applied;
     te[4] = now_s();
     if (trace) {

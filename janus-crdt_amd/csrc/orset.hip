@@ -815,7 +815,24 @@ void orset_merge_runs(jg_orset* s, uint32_t n_runs, const uint64_t* add_counts, 
     if (!level.empty()) merge_into(s, level[0].get(), false);
 }
 
-void orset_merge_store(jg_orset* s, jg_orset* src) { merge_into(s, src, false); }
+void orset_merge_store(jg_orset* s, jg_orset* src, bool defer) { merge_into(s, src, defer); }
+
+bool orset_pin_pending(jg_orset* s, size_t at) {
+    if (!s->counts_pending) return false;
+    jg::pin_get(s->ctx, at, s->ctx->flags.p, sizeof(unsigned));
+    jg::pin_get(s->ctx, at + 8, s->counts.p, 16);
+    return true;
+}
+void orset_settle_pending(jg_orset* s, size_t at) {
+    unsigned h;
+    std::memcpy(&h, jg::pin_at(s->ctx, at), sizeof h);
+    flag_failed(s->ctx, h, "jg_orset_merge");
+    unsigned long long c[2];
+    std::memcpy(c, jg::pin_at(s->ctx, at + 8), sizeof c);
+    s->add.n = c[0];
+    s->rem.n = c[1];
+    s->counts_pending = false;
+}
 
 // Room in the store's union targets for `add_in` / `rem_in` more records (merge_into reserves again if a
 // union turns out larger).  Called by a node wave while its uploads are in flight, so a growing store's

@@ -1540,7 +1540,7 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
                        a.key.as<unsigned long long>(), a.tag.as<Tag16>(), a.ord.as<uint32_t>(), r.key.as<unsigned long long>(), r.tag.as<Tag16>(),
                        r.ord.as<uint32_t>());
     JG_HIP(hipGetLastError());
-    jg::orset_merge_store(s, w->recs);
+    jg::orset_merge_store(s, w->recs, w->external);  // a node wave: the node's final read brings the counts
     return true;
 }
 
@@ -1667,7 +1667,7 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     if (tr) tc[3] = now();
     sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, &RT.slot[0].mint, 4);
     sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, &RT.slot[0].mint, 4);
-    jg::orset_merge_store(s, w->recs);
+    jg::orset_merge_store(s, w->recs, w->external);  // a node wave: the node's final read brings the counts
     if (tr) {
         tc[4] = now();
         std::fprintf(stderr, "commit_tables: strings queued %.0f us, counts read %.0f, record sorts + long-run read %.0f, union %.0f (%llu strings, %llu + %llu records)\n",
@@ -1794,7 +1794,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     read_words(ctx, st + 6, long_run, 2);
     sort_side_end(ctx, w, 0, cnt[0], key_bits, w->recs->add, long_run[0] != 0, w->dmin.as<uint32_t>(), 1);
     sort_side_end(ctx, w, 1, cnt[1], key_bits, w->recs->rem, long_run[1] != 0, w->dmin.as<uint32_t>(), 1);
-    jg::orset_merge_store(s, w->recs);
+    jg::orset_merge_store(s, w->recs, w->external);  // a node wave: the node's final read brings the counts
 }
 
 void close_wave(jg_orset_wire* w) {
