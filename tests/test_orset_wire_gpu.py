@@ -490,3 +490,39 @@ def test_tables_sized_from_the_last_wave(ctx, monkeypatch):
             assert orc.same_orset(ga, gr, ea, er)
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("chunking", ["one", "odd"])
+def test_tag_references_dealt_over_lanes(ctx, monkeypatch, chunking):
+    """k_ow_rkeys / k_ow_rins deal four messages' tag references over a wave's 64 lanes in rounds
+    (orset_tables.hpp WaveMsgs): tag counts whose running totals fall just below, on and past multiples of 64,
+    empty states (no references) between them, and chunks of odd sizes (a wave's four messages start at any
+    chunk offset).  Records, arrival ordinals and issued names equal the oracle's; the tables path alone
+    (JANUS_ORSET_TAIL=tables: an overflow would be an error, not a fall-back)."""
+    monkeypatch.setenv("JANUS_ORSET_TAIL", "tables")
+    rng = np.random.default_rng(2024)
+    counts = [63, 1, 0, 65, 64, 2, 0, 0, 130, 1, 1, 1, 61, 3, 0, 64, 127, 0, 1, 66, 5]
+    sets, msgs, k = [], [], 0
+    for i, c in enumerate(counts):
+        add = [(f"e{k + j}", J.random_guids(rng, 1)) for j in range(c)]
+        k += c
+        rem = add[: c // 3]  # tombstones of a third of them: references on both sides
+        msgs.append(J.encode_orset(add, rem))
+        sets.append(i % 3)
+    model = {}
+    ea, er, bad, _ = orc.orset_apply_json(sets, msgs, model)
+    assert bad is None
+    if chunking == "one":
+        chunks = [(sets, msgs)]
+    else:
+        cuts = [0, 3, 8, 9, 14, len(msgs)]
+        chunks = [(sets[a:b], msgs[a:b]) for a, b in zip(cuts, cuts[1:])]
+    s = jg.ORSetStore(ctx)
+    try:
+        rc, first_bad = s.wave(chunks)
+        assert rc == jg.JG_OK and first_bad is None
+        ga, gr = s.read()
+        assert orc.same_orset(ga, gr, ea, er)
+        assert s.wave_names() == _model_names(model, {})
+    finally:
+        s.close()
