@@ -792,6 +792,82 @@ def headline(args, world, res, cpu):
     return line
 
 
+LINE_CAP = 8000  # bytes: the driver keeps an 8-KB stdout tail and parses the last line
+
+
+def _r(x, nd=4):
+    """Round a float to nd significant digits for the compact line (ints and None unchanged)."""
+    if isinstance(x, float):
+        return float(f"{x:.{nd}g}")
+    return x
+
+
+def _roof(r, keys=("bound", "frac", "achieved", "unit")):
+    if not isinstance(r, dict):
+        return None
+    return {k: _r(r.get(k)) for k in keys if r.get(k) is not None}
+
+
+def compact_leg(name, leg):
+    """One leg reduced to its figures: time per step/wave, throughput, the roofline's bound and frac (full leg on
+    stderr).  Apply-loop legs also carry their CPU baseline's rate and the page-locked / caller-arena variants."""
+    if not isinstance(leg, dict):
+        return None
+    if "error" in leg:
+        return {"error": str(leg["error"])[:200]}
+    out = {}
+    for k in ("ms_per_step", "ms_per_wave", "value", "unit", "msgs_per_s", "rows_per_s", "client_ops_per_s", "event_ms",
+              "cold_wave_ms", "untimed_pack_ms_per_wave", "scaling"):
+        if leg.get(k) is not None:
+            out[k] = _r(leg[k])
+    roof = leg.get("roofline")
+    if roof is None and isinstance(leg.get("rank0_roofline"), dict):
+        roof = leg["rank0_roofline"]
+    if isinstance(roof, dict):
+        out["roofline"] = _roof(roof, ("bound", "frac", "achieved", "peak", "unit", "traffic", "frac_24B"))
+        ml = roof.get("measured_link")
+        if isinstance(ml, dict):
+            out["roofline"]["frac_of_measured_link"] = _r(ml.get("frac"))
+        dec = roof.get("decode")
+        if isinstance(dec, dict):
+            out["decode_bound"] = dec.get("bound")
+    if isinstance(leg.get("roofline_valu"), dict):
+        out["roofline_valu"] = _roof(leg["roofline_valu"])
+    cb = leg.get("cpu_baseline")
+    if isinstance(cb, dict):
+        out["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("msgs_per_s", "cores", "kind") if cb.get(k) is not None}
+    for sub in ("from_pinned", "caller_arena", "pipelined", "first_level", "merge"):
+        s = leg.get(sub)
+        if isinstance(s, dict):
+            c = {k: _r(s[k]) for k in ("ms_per_wave", "ms", "event_ms", "msgs_per_s", "caller_flatten_ms_per_wave") if s.get(k) is not None}
+            if isinstance(s.get("roofline"), dict):
+                c["frac"] = _r(s["roofline"].get("frac"))
+                ml = s["roofline"].get("measured_link")
+                if isinstance(ml, dict):
+                    c["frac_of_measured_link"] = _r(ml.get("frac"))
+            out[sub] = c
+    return out
+
+
+def compact_line(line, legs):
+    """The driver-parsed stdout line: the headline (metric, value, roofline with traffic, cpu_baseline) in full and
+    one compact object per leg.  Legs are dropped from the end if the line would exceed LINE_CAP."""
+    out = dict(line)
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        out["cpu_baseline"] = {k: _r(v) if not isinstance(v, dict) else {kk: _r(vv) for kk, vv in v.items()} for k, v in cb.items()}
+    for k in ("value", "ms_per_step", "hbm_GBps"):
+        if k in out:
+            out[k] = _r(out[k], 7)
+    if isinstance(out.get("roofline"), dict):
+        out["roofline"] = {k: _r(v, 6) for k, v in out["roofline"].items()}
+    out["legs"] = {k: compact_leg(k, v) for k, v in legs.items()}
+    out["detail"] = "stderr (full legs, one JSON line)"
+    while len(json.dumps(out)) > LINE_CAP and out["legs"]:
+        out["legs"].pop(next(reversed(out["legs"])))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -882,27 +958,17 @@ def main():
         return
 
     line = headline(args, world, res, cpu)
-    orset_leg = line.pop("orset", None)
-    # the verbose apply-loop objects first, the compact legs (OR-Set step, exchange, JSON, digests) last: a
-    # reader that keeps only the line's tail still sees them
-    if apply_loop is not None:
-        line["apply_loop"] = apply_loop
-    if apply_orset is not None:
-        line["apply_loop_orset"] = apply_orset
-    if apply_c1 is not None:
-        line["apply_loop_c1"] = apply_c1
-    if apply_direct is not None:
-        line["apply_loop_direct"] = apply_direct
-    line["cpu_baseline"] = cpu
-    if "digest" in res:
-        line["update_digests"] = res["digest"]
-    if "json" in res:
-        line["json_apply"] = res["json"]
-    if "exchange" in res:
-        line["exchange"] = res["exchange"]
-    if orset_leg is not None:
-        line["orset"] = orset_leg
-    print(json.dumps(line), flush=True)
+    legs = {"orset": line.pop("orset", None), "apply_loop": apply_loop, "apply_loop_orset": apply_orset,
+            "apply_loop_c1": apply_c1, "apply_loop_direct": apply_direct, "update_digests": res.get("digest"),
+            "json_apply": res.get("json"), "exchange": res.get("exchange")}
+    legs = {k: v for k, v in legs.items() if v is not None}
+    # every leg in full (per-kernel dicts, nested rooflines, PMC summaries) on stderr and, if asked, in a file;
+    # the LAST stdout line is the compact one the driver parses (<= LINE_CAP bytes)
+    detail = dict(line, legs=legs)
+    print(json.dumps(detail), file=sys.stderr, flush=True)
+    if os.environ.get("JANUS_BENCH_DETAIL"):
+        Path(os.environ["JANUS_BENCH_DETAIL"]).write_text(json.dumps(detail) + "\n")
+    print(json.dumps(compact_line(line, legs)), flush=True)
 
 
 if __name__ == "__main__":
