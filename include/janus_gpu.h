@@ -327,7 +327,9 @@ typedef struct jg_commit {
  * Task faults at it: every message before *stopped_at was applied and its completions reported, nothing
  * from it on, and the call returns the rejection's code (JG_EINVAL: JsonException; JG_ESTATE: an OR-Set
  * element with an empty tag set, or a key out of replica columns) — the one entry point that applies a
- * prefix on error.  JG_OK with *stopped_at = UINT64_MAX otherwise. */
+ * prefix on error.  JG_OK with *stopped_at = UINT64_MAX otherwise.  An internal failure of the wave's OR-Set
+ * commit (its device error flag) is returned AFTER the completions: completed / *n_completed are valid,
+ * *stopped_at = UINT64_MAX, and the OR-Set store must be reloaded (its union did not finish). */
 int jg_apply_committed(jg_node* node, jg_tracker* tracker, const jg_commit* wave, uint64_t* completed, uint64_t* n_completed,
                        uint64_t* stopped_at);
 /* ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/DAGConnectionManager.cs:40-50,

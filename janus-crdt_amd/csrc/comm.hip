@@ -32,7 +32,6 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -46,26 +45,13 @@
 
 static_assert(sizeof(ncclUniqueId) == 128, "the ABI passes the unique id as 128 bytes");
 
-// Abort of a hung RCCL communicator from outside the blocked call (ncclCommAbort is meant to be called from
-// another thread to stop uncompleted operations): armed for the duration of every exchange on the RCCL
-// transport, it aborts the communicator when the deadline passes and the call is still in RCCL.
-struct Watchdog {
-    std::mutex m;
-    std::condition_variable cv;
-    std::chrono::steady_clock::time_point until{};
-    bool armed = false, quit = false, fired = false;
-    std::thread th;
-};
-
 struct jg_comm {
     jg_ctx* ctx = nullptr;
     ncclComm_t nc = nullptr;               // RCCL transport (nullptr: host transport, or aborted)
-    std::mutex abort_mu;                   // one abort, from the call's thread or the watchdog
-    std::unique_ptr<Watchdog> dog;
     jg_alltoallv_fn host_fn = nullptr;     // host transport
     void* host_user = nullptr;
     bool rccl = false;                     // the RCCL transport (else the host transport)
-    std::atomic<bool> broken{false};       // aborted after a timeout / async error: every call fails
+    bool broken = false;                   // aborted after a timeout / async error: every call fails
     uint32_t rank = 0, world = 1;
     double timeout_s = 120;
     jg::DevBuf dcounts;                    // [world] mine, then [world x world] gathered
@@ -76,14 +62,6 @@ struct jg_comm {
     jg_exchange_stats stats{};
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     ~jg_comm() {
-        if (dog) {
-            {
-                std::lock_guard<std::mutex> g(dog->m);
-                dog->quit = true;
-            }
-            dog->cv.notify_all();
-            if (dog->th.joinable()) dog->th.join();
-        }
         for (hipEvent_t e : ev)
             if (e) (void)hipEventDestroy(e);
         if (pin) (void)hipHostFree(pin);
@@ -101,59 +79,21 @@ bool trace_comm() {
     return t;
 }
 
+// Every abort happens on the calling thread, inside one of the polling loops below (the communicator is
+// non-blocking, so no RCCL call of this library ever blocks): the handle is freed exactly once, and nothing
+// touches it afterwards (nc = nullptr, broken = true; every entry point checks `broken` first).
 void abort_comm(jg_comm* c) {
-    std::lock_guard<std::mutex> g(c->abort_mu);
     if (c->broken) return;
     if (trace_comm()) std::fprintf(stderr, "jg_comm: aborting the communicator\n");
     c->broken = true;
-    if (c->nc) (void)ncclCommAbort(c->nc);  // c->nc stays set: the handle is dead, c->broken says so
+    if (c->nc) (void)ncclCommAbort(c->nc);
+    c->nc = nullptr;
     if (trace_comm()) std::fprintf(stderr, "jg_comm: aborted\n");
 }
 
-void start_watchdog(jg_comm* c) {
-    c->dog = std::make_unique<Watchdog>();
-    Watchdog* d = c->dog.get();
-    const int dev = c->ctx->device;
-    d->th = std::thread([c, d, dev] {
-        (void)hipSetDevice(dev);
-        std::unique_lock<std::mutex> lk(d->m);
-        for (;;) {
-            d->cv.wait(lk, [d] { return d->quit || d->armed; });
-            if (d->quit) return;
-            if (d->cv.wait_until(lk, d->until, [d] { return d->quit || !d->armed; })) {
-                if (d->quit) return;
-                continue;  // disarmed in time
-            }
-            d->fired = true;
-            d->armed = false;
-            lk.unlock();
-            abort_comm(c);  // the blocked RCCL call returns with an error; the call reports the timeout
-            lk.lock();
-        }
-    });
-}
-
-// Arms the watchdog for one exchange on the RCCL transport (no-op for the host transport).
-struct Armed {
-    jg_comm* c;
-    explicit Armed(jg_comm* cc) : c(cc) {
-        if (!c->dog) return;
-        std::lock_guard<std::mutex> g(c->dog->m);
-        c->dog->fired = false;
-        c->dog->until = std::chrono::steady_clock::now() + std::chrono::duration_cast<std::chrono::steady_clock::duration>(std::chrono::duration<double>(c->timeout_s));
-        c->dog->armed = true;
-        c->dog->cv.notify_all();
-    }
-    ~Armed() {
-        if (!c->dog) return;
-        std::lock_guard<std::mutex> g(c->dog->m);
-        c->dog->armed = false;
-        c->dog->cv.notify_all();
-    }
-};
-
 // Poll the communicator until no operation is in progress (non-blocking RCCL), against the deadline.
 void nccl_settle(jg_comm* c, const char* what, int line) {
+    JG_REQUIRE(c->nc && !c->broken, JG_EHIP, "%s: the communicator was aborted (comm.hip:%d)", what, line);
     const auto end = Clock::now() + std::chrono::duration<double>(c->timeout_s);
     for (;;) {
         ncclResult_t a = ncclSuccess;
@@ -174,12 +114,9 @@ void nccl_settle(jg_comm* c, const char* what, int line) {
 }
 
 void nccl_check(jg_comm* c, ncclResult_t r, const char* what, int line) {
-    if (r == ncclSuccess && !c->broken) return;
-    if (r == ncclInProgress && !c->broken) return nccl_settle(c, what, line);
-    const bool timed_out = c->broken;
+    if (r == ncclSuccess) return;
+    if (r == ncclInProgress) return nccl_settle(c, what, line);
     abort_comm(c);
-    if (timed_out)
-        jg::fail(JG_EHIP, "%s: no progress in %.0f s (a rank missing or stuck, comm.hip:%d); the communicator was aborted", what, c->timeout_s, line);
     jg::fail(JG_EHIP, "%s failed: %s (comm.hip:%d); the communicator was aborted", what, ncclGetErrorString(r), line);
 }
 
@@ -411,10 +348,13 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         c->timeout_s = timeout_from_env();
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof u);
-        // The rendezvous waits for every rank inside ncclCommInitRank (this RCCL blocks there even for a
-        // non-blocking config), so it runs on a thread of its own and this call waits for it against the
-        // deadline.  A rank that never joins leaves that thread in the rendezvous: it is abandoned (it destroys
-        // a communicator that completes after all) and the call returns JG_EHIP.
+        // A non-blocking communicator (blocking = 0): every later call returns ncclInProgress instead of
+        // waiting, and this library polls it against the deadline on the calling thread.  The rendezvous itself
+        // can still wait inside ncclCommInitRankConfig for a peer that never arrives (this RCCL's bootstrap
+        // blocks there even for a non-blocking config), so it runs on a thread of its own, which then polls the
+        // communicator until it is ready.  This call waits for that thread against the deadline; past it the
+        // thread is abandoned and aborts the communicator itself if it ever gets one (it is the handle's only
+        // owner until the hand-over), and the call returns JG_EHIP.
         struct Job {
             std::mutex m;
             std::condition_variable cv;
@@ -424,15 +364,28 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         };
         auto job = std::make_shared<Job>();
         const int dev = ctx->device;
-        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRank (rank %u of %u)\n", rank, world);
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRankConfig (rank %u of %u, non-blocking)\n", rank, world);
         std::thread([job, u, rank, world, dev] {
             (void)hipSetDevice(dev);
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
             ncclComm_t nc = nullptr;
-            const ncclResult_t r = ncclCommInitRank(&nc, (int)world, u, (int)rank);
+            ncclResult_t r = ncclCommInitRankConfig(&nc, (int)world, u, (int)rank, &cfg);
+            while (r == ncclInProgress && nc) {
+                {
+                    std::lock_guard<std::mutex> g(job->m);
+                    if (job->abandoned) break;
+                }
+                ncclResult_t a = ncclInProgress;
+                const ncclResult_t q = ncclCommGetAsyncError(nc, &a);
+                r = q != ncclSuccess ? q : a;
+                if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(100));
+            }
             std::lock_guard<std::mutex> g(job->m);
-            if (job->abandoned) {
+            if (job->abandoned || r != ncclSuccess) {
                 if (nc) (void)ncclCommAbort(nc);
-                return;
+                nc = nullptr;
+                if (job->abandoned) return;
             }
             job->r = r;
             job->nc = nc;
@@ -449,11 +402,10 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
                          rank, world);
             }
         }
-        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRank returned %s\n", ncclGetErrorString(job->r));
-        JG_REQUIRE(job->r == ncclSuccess, JG_EHIP, "ncclCommInitRank failed: %s", ncclGetErrorString(job->r));
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRankConfig settled: %s\n", ncclGetErrorString(job->r));
+        JG_REQUIRE(job->r == ncclSuccess && job->nc, JG_EHIP, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(job->r));
         c->nc = job->nc;
         c->rccl = true;
-        start_watchdog(c.get());
         *out = c.release();
     });
 }
@@ -481,14 +433,12 @@ int jg_comm_destroy(jg_comm* c) {
         std::unique_ptr<jg_comm> own(c);
         auto lk_ = jg::lock(c->ctx);
         jg::ensure_device(c->ctx);
-        if (c->broken) return;  // aborted: its queued work was cancelled with it
-        Armed armed_(c);
+        if (c->broken || !c->nc) return;  // host transport, or aborted: its queued work was cancelled with it
         wait_stream(c);
-        if (c->nc && !c->broken) {
-            const ncclResult_t r = ncclCommDestroy(c->nc);
-            if (r == ncclInProgress) nccl_settle(c, "ncclCommDestroy", __LINE__);
-            c->nc = nullptr;
-        }
+        // non-blocking: finalize (flushes the communicator's work) polled to completion, then destroy
+        JG_NCCL(c, ncclCommFinalize(c->nc));
+        (void)ncclCommDestroy(c->nc);
+        c->nc = nullptr;
     });
 }
 
@@ -524,7 +474,6 @@ int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* se
             if (received) received[0] = n;
             return;
         }
-        Armed armed_(c);  // RCCL: a call stuck past the deadline is aborted from the watchdog
         ensure(c->sbuf[0], n * 4 + 16);
         ensure(c->sbuf[1], n * rb + 16);
         ensure(c->sbuf[2], n * rb + 16);
@@ -589,7 +538,6 @@ int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t*
             if (recv_rem) recv_rem[0] = nrm;
             return;
         }
-        Armed armed_(c);  // RCCL: a call stuck past the deadline is aborted from the watchdog
         const size_t es[6] = {8, 16, 4, 8, 16, 4};  // key, tag, ord of the add stream, then of the tombstones
         for (int i = 0; i < 6; ++i) ensure(c->sbuf[i], (i < 3 ? na : nrm) * es[i] + 16);
         JG_HIP(hipEventRecord(event(c, 0), ctx->stream));

@@ -502,6 +502,13 @@ bool host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
+// JANUS_TEST_ORSET_COMMIT_FAIL=1 (tests, read per call): the wave's OR-Set commit raises its device error flag,
+// so the deferred error path (completions reported first, then the error) runs without a real overflow.
+bool test_commit_fail() {
+    const char* e = std::getenv("JANUS_TEST_ORSET_COMMIT_FAIL");
+    return e && e[0] == '1';
+}
+
 // The apply loop over one wave (jg_apply_committed / jg_apply_block).
 void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
     const double t_begin = now_s();
@@ -764,6 +771,8 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         }
         te[2] = now_s();
         if (do_orset) jg::orset_node_commit(nd->orset, cut);
+        if (do_orset && nd->orset->counts_pending && test_commit_fail())  // tests: the commit's union reports a broken precondition
+            JG_HIP(hipMemsetAsync(ctx->flags.p, 0x04, 1, ctx->stream));
         te[3] = now_s();
     } catch (...) {
         // an internal failure past the chunk loop (a check that could not name a message, a prefix that failed
@@ -779,6 +788,8 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
 
     // safe-update completions of the messages before the cut, in commit order
     uint64_t ndone = 0;
+    int late_code = JG_OK;  // the OR-Set commit's deferred error flag, raised once the completions are out
+    std::string late_why;
     bool orset_pending = false;  // the OR-Set commit's union counts ride on this phase's page-locked read
     JG_HIP(hipMemsetAsync(d_status + 2, 0, 8, ctx->stream));
     if (cut) hipLaunchKernelGGL(k_count_applied, dim3((unsigned)std::min<uint64_t>(1024, blocks_for(cut))), dim3(kBlock), 0, ctx->stream, d_rows, d_mset, cut,
@@ -802,7 +813,17 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         jg::pin_get(ctx, 0, d_status + 1, 16);  // the completions' count and the applied count
         orset_pending = do_orset && jg::orset_pin_pending(nd->orset, 64);  // and the OR-Set commit's union counts
         jg::pin_sync(ctx);
-        if (orset_pending) jg::orset_settle_pending(nd->orset, 64), orset_pending = false;
+        if (orset_pending) {
+            // k_complete / k_count_sub have already taken these completions off the tracker: a union failure is
+            // reported AFTER they reach the caller, or they would be lost for good
+            try {
+                jg::orset_settle_pending(nd->orset, 64);
+            } catch (const jg::Error& e) {
+                late_code = e.code;
+                late_why = e.msg;
+            }
+            orset_pending = false;
+        }
         std::memcpy(&k, jg::pin_at(ctx, 0), 8);
         ndone = k;
         if (completed && k) {
@@ -854,6 +875,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     const double t_end = now_s();
     nd->stats.device_wait_s = t_end - t_dev;
     nd->stats.total_s = t_end - t_begin;
+    if (late_code != JG_OK) jg::fail(late_code, "%s (the wave's OR-Set commit; its safe-update completions were reported)", late_why.c_str());
     if (code != JG_OK) jg::fail(code, "%s (commit index %llu)", why.c_str(), (unsigned long long)*stopped_at);
 }
 

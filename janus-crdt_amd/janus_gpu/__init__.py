@@ -763,7 +763,11 @@ class Node:
         nd, at = _u64(), _u64()
         rc = load().jg_apply_committed(self._h, tracker._h if tracker else None, C.byref(c), _ptr(done), C.byref(nd), C.byref(at))
         if rc != JG_OK and at.value == 2**64 - 1:
-            _check(rc)
+            try:
+                _check(rc)
+            except JanusError as e:  # the completions the call reported before its error (the OR-Set commit's flag)
+                e.completed = done[: nd.value].copy()
+                raise
         return done[: nd.value].copy(), (None if at.value == 2**64 - 1 else at.value), rc
 
     def apply_block(self, lo, hi, types, msgs=None, data=None, off=None):

@@ -462,3 +462,32 @@ def test_orset_id_space_rejects_before_anything_commits(ctx):
     finally:
         for h in (node, tr, pnc, st):
             h.close()
+
+
+def test_orset_commit_failure_still_reports_completions(ctx, monkeypatch):
+    """the OR-Set commit's error flag is read with the wave's final read, after k_complete has taken
+    the safe-update completions off the tracker.  A failing commit (forced by JANUS_TEST_ORSET_COMMIT_FAIL)
+    returns its error AFTER the completions: the caller gets every completed origin, in commit order, and the
+    tracker holds exactly the entries not completed."""
+    rng = np.random.default_rng(29)
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, 60, 20)
+    pcl = J.Cluster(rng, 60, R - 1, EB, stable=None)
+    ocl = J.ORSetCluster(rng, 20)
+    try:
+        wave = _wave(rng, m, uids, 60, 20, 1500, pcl, ocl, seq0=0)
+        tr.add(list(m.tracker), list(m.tracker.values()))
+        exp_done, exp_cut = m.apply(wave)
+        assert exp_cut is None and len(exp_done) > 100
+        monkeypatch.setenv("JANUS_TEST_ORSET_COMMIT_FAIL", "1")
+        with pytest.raises(jg.JanusError) as ei:
+            node.apply_committed(tr, [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], [x[2] for x in wave],
+                                 [x[3] for x in wave])
+        assert ei.value.code == jg.JG_ESTATE
+        assert list(ei.value.completed) == exp_done
+        assert tr.size() == len(m.tracker)
+        P, N = pnc.read_rows()  # the PN-Counter commit went through
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+    finally:
+        monkeypatch.delenv("JANUS_TEST_ORSET_COMMIT_FAIL", raising=False)
+        for h in (node, tr, pnc, st):
+            h.close()

@@ -534,6 +534,75 @@ def test_comm_init_without_peers_times_out():
     assert 4.0 <= float(secs) < 30 and time.time() - t < 90
 
 
+def _stall_worker(rank, uid_q, q):
+    """Rank 0 exchanges; rank 1 joins the communicator and then never posts its half (a peer stuck mid-exchange)."""
+    os.environ["JANUS_COMM_TIMEOUT_S"] = "5"
+    sys.path.insert(0, str(ROOT / "janus-crdt_amd"))
+    import time
+    import janus_gpu as jg_
+    try:
+        with jg_.Context(rank) as ctx:
+            if rank == 0:
+                uid = jg_.comm_unique_id()
+                uid_q.put(uid)
+            else:
+                uid = uid_q.get(timeout=60)
+            cm = jg_.Comm(ctx, rank, 2, uid)
+            if rank == 1:
+                q.put((1, "joined", 0.0))
+                time.sleep(40)  # never posts: rank 0's exchange must give up on its own
+                cm.close()
+                return
+            s = jg_.PNCStore(ctx, 1000, 64, 8)
+            rows = jg_.Rows(ctx, 500, 64, 8)
+            rows.upload(np.zeros((500, 64), np.int64), np.zeros((500, 64), np.int64), np.arange(500, dtype=np.uint32) * 2 + 1)  # odd keys: rank 1's
+            t = time.time()
+            codes = []
+            for _ in range(2):  # the second call finds the communicator aborted and fails at once
+                try:
+                    cm.exchange_pnc(s, rows)
+                    codes.append(0)
+                except jg_.JanusError as e:
+                    codes.append(e.code)
+            q.put((0, codes, time.time() - t))
+            cm.close()  # an aborted communicator is released without touching RCCL again
+            for h in (s, rows):
+                h.close()
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc(), 0.0))
+
+
+def test_rccl_exchange_with_a_stalled_peer_times_out():
+    """world 2 over RCCL, one GPU per rank; rank 1 joins and then never posts its sends / receives.
+    Rank 0's jg_pnc_exchange polls its non-blocking communicator against JANUS_COMM_TIMEOUT_S (5 s), aborts it
+    on its own thread and returns JG_EHIP; a second call returns JG_EHIP at once; destroy does not touch the
+    aborted handle.  Needs two GPUs (RCCL refuses two ranks on one device): skipped on a one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import torch.multiprocessing as mp
+    ctxm = mp.get_context("spawn")
+    uid_q, q = ctxm.Queue(), ctxm.Queue()
+    procs = [ctxm.Process(target=_stall_worker, args=(r, uid_q, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = {}
+        for _ in procs:
+            r, what, secs = q.get(timeout=100)
+            res[r] = (what, secs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert res[1][0] == "joined", res
+    codes, secs = res[0]
+    assert codes == [jg.JG_EHIP, jg.JG_EHIP], res
+    assert 4.0 <= secs < 40, secs
+
+
 # ---- the library's own exchange at world > 1: the host transport over gloo, ranks sharing device 0 ----
 def _host_comm_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
