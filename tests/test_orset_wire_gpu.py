@@ -526,3 +526,44 @@ def test_tag_references_dealt_over_lanes(ctx, monkeypatch, chunking):
         assert s.wave_names() == _model_names(model, {})
     finally:
         s.close()
+
+
+def test_names_since_pull_between_marks_with_out_of_order_pool_bytes(ctx):
+    """Regression for round 4's abort inside jg_orset_names_since (gpurun_out/t2.log, rc 134): a wave's
+    new names take their pool bytes by device atomics, in workgroup arrival order, not in name (id) order, so a
+    pull whose `from` falls inside a wave (between two commit marks) must take the pool range from the mark at or
+    before `from`, not from name `from`'s own offset.  Three waves of 800 states naming 3 new elements each, with
+    lengths 1..61 bytes (out-of-order claims move bytes by whole names); every pull from every position inside the
+    second wave (and a stride over the rest) returns exactly the log's tail, and its size query returns exactly the
+    tail's byte count (a short count is what let the fill write past the caller's buffer)."""
+    import ctypes as C
+    rng = np.random.default_rng(97)
+    s = jg.ORSetStore(ctx)
+    try:
+        log, marks = [], [0]
+        for w in range(3):
+            sets = [int(x) for x in rng.integers(0, 64, 800)]
+            msgs = []
+            for m, k in enumerate(sets):
+                adds = []
+                for j in range(3):
+                    ln = int(rng.integers(1, 62))
+                    name = (f"w{w}m{m}e{j}-" + "".join(chr(97 + int(c)) for c in rng.integers(0, 26, 64)))[:ln]
+                    adds.append((name, J.random_guids(rng, 1)))
+                msgs.append(J.encode_orset(adds, []))
+            rc, bad = s.wave([(sets[:400], msgs[:400]), (sets[400:], msgs[400:])])
+            assert rc == jg.JG_OK and bad is None
+            log += s.wave_names()
+            marks.append(len(log))
+        assert marks[1] > 1000  # names differ by prefix, so almost every element is new
+        lib = jg.load()
+        positions = list(range(marks[1] - 2, marks[2] + 3)) + list(range(0, len(log) + 1, 97))
+        for k in positions:
+            to, nb = C.c_uint64(), C.c_uint64()
+            assert lib.jg_orset_names_since(s._h, k, C.byref(to), C.byref(nb), None, None, None, None) == jg.JG_OK
+            assert to.value == len(log)
+            assert nb.value == sum(len(b) for _, _, b in log[k:]), k
+            end, tail = s.names_since(k)
+            assert end == len(log) and tail == log[k:], k
+    finally:
+        s.close()
