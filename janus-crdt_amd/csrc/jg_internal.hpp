@@ -184,7 +184,8 @@ struct jg_stream_soa {
     bool dense = true;    // chunks full except the last (slot = rank): uploads and generated streams
     void reserve_records(uint64_t records);  // room for a dense stream or a union output of `records`
     void swap(jg_stream_soa& o);
-    std::vector<void*> retired;  // blocks of earlier reservations, freed with the stream (reserve_records)
+    std::vector<void*> retired;  // blocks of earlier reservations (reserve_records), freed at the next idle point
+    void free_retired();         // hipFree them (the caller's streams have drained)
     jg_stream_soa() = default;
     jg_stream_soa(const jg_stream_soa&) = delete;
     jg_stream_soa& operator=(const jg_stream_soa&) = delete;
@@ -194,6 +195,7 @@ struct jg_stream_soa {
 struct jg_orset_wire;  // orset_wire.hip: element table + open payload wave (first use only)
 namespace jg {
 void orset_wire_free(jg_orset_wire* w);
+void orset_wire_free_retired(jg_orset_wire* w);
 }
 
 struct jg_orset {
@@ -251,6 +253,8 @@ void orset_merge_store(jg_orset* s, jg_orset* src, bool defer = false);
 // + 24) (no sync: the caller's own pin_sync brings them with its words; false if nothing is pending), and
 // taken from there after that sync (the flag raised as the synchronous merge would).
 bool orset_pin_pending(jg_orset* s, size_t at);
+// hipFree the blocks the store's streams and element table retired while growing (the caller's streams drained)
+void orset_free_retired(jg_orset* s);
 void orset_settle_pending(jg_orset* s, size_t at);
 // orset.hip: room in the store's union targets for that many more records (no sync; skipped while counts are pending).
 void orset_reserve_union(jg_orset* s, uint64_t add_in, uint64_t rem_in);

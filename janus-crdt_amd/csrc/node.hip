@@ -869,6 +869,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         if (k == n_ev) nd->stats.tail_busy_s = ms * 1e-3;  // the final phase's pair
     }
     nd->stats.device_busy_s = busy;
+    if (do_orset) jg::orset_free_retired(nd->orset);  // the wave has drained: blocks its growth retired go now
     nd->stats.chunk_busy_s = busy - nd->stats.tail_busy_s;
     if (n_completed) *n_completed = ndone;
     *stopped_at = cut < nn ? (filter ? nd->dmap[cut] : cut) : UINT64_MAX;

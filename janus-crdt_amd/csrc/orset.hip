@@ -470,6 +470,7 @@ void merge_into(jg_orset* s, jg_orset* src, bool async, jgk::Drop drop = {nullpt
         s->add.n = c[0];
         s->rem.n = c[1];
         s->counts_pending = false;
+        jg::orset_free_retired(s);  // the stream has drained: blocks this union's reservations retired go now
     }
 }
 
@@ -705,9 +706,9 @@ void jg_stream_soa::reserve_records(uint64_t records) {
     }
     cap_chunks = c;
     // the old block is retired, not freed: hipFree waits for the whole device and then costs ms of host time on
-    // the box (measured inside a node wave: 2.9-5.7 ms, uploads in flight); a growing store keeps its retired
-    // blocks until it is destroyed (at most a third of its size more with the 4x growth above, and blocks
-    // stop retiring once the stream stops growing)
+    // the box (measured inside a node wave: 2.9-5.7 ms, uploads in flight).  Retired blocks are freed at the
+    // next point where the store's streams are known idle (jg::orset_free_retired: the end of a node wave, of a
+    // synchronous merge), so they never add up beyond one wave's growth
     if (nb.p) {
         retired.push_back(nb.p);
         nb.p = nullptr;
@@ -718,8 +719,11 @@ void jg_stream_soa::reserve_records(uint64_t records) {
                      std::chrono::duration<double>(t1 - t0).count() * 1e6);
 }
 
-jg_stream_soa::~jg_stream_soa() {
+jg_stream_soa::~jg_stream_soa() { free_retired(); }
+
+void jg_stream_soa::free_retired() {
     for (void* p : retired) (void)hipFree(p);
+    retired.clear();
 }
 
 namespace jg {
@@ -733,6 +737,12 @@ void set_dense(jg_ctx* ctx, jg_stream_soa& s, uint64_t n) {
     s.n = n;
     s.nch = (uint32_t)nch;
     s.dense = true;
+}
+
+void orset_free_retired(jg_orset* s) {
+    for (jg_stream_soa* st : {&s->add, &s->rem, &s->spare_add, &s->spare_rem})
+        if (!st->retired.empty()) st->free_retired();
+    if (s->wire) orset_wire_free_retired(s->wire);
 }
 
 void sync_counts(jg_orset* s) {

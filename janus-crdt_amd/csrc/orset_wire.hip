@@ -868,13 +868,35 @@ int bits_for(uint64_t x) {
 
 }  // namespace
 
+// check_id_room's per-set tier: every message's entry count added to its set (cnt[set_cap + 1] flags a set id past
+// the table), then each set's next id + its count against the id space (cnt[set_cap] flags an overflow).
+__global__ void k_id_room_count(const unsigned long long* __restrict__ ne, const uint32_t* __restrict__ mset, uint64_t n, uint64_t set_cap,
+                                unsigned long long* cnt) {
+    for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n; m += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long c = ne[m];
+        if (c == 0) continue;
+        const uint32_t st = mset[m];
+        if (st < set_cap) atomicAdd(cnt + st, c);
+        else atomicOr(cnt + set_cap + 1, 1ull);
+    }
+}
+
+__global__ void k_id_room_check(const uint32_t* __restrict__ next_id, const unsigned long long* __restrict__ cnt, uint64_t set_cap,
+                                unsigned long long* over) {
+    for (uint64_t st = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; st < set_cap; st += (uint64_t)gridDim.x * blockDim.x)
+        if (cnt[st] && (uint64_t)next_id[st] + cnt[st] > (uint64_t)JG_NULL_ELEM - 1) atomicOr(over, 1ull);
+}
+
 // Element table + open wave of one store.
 struct jg_orset_wire {
     // element table
     jg::DevBuf tab, nset, nid, ngen, nlen, noff, nkey, pool, set_gen, next_id;
     uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
-    // an upper bound of every set's next element id (names_sync's next ids, plus every name a commit issued since)
+    // an upper bound of every set's next element id (names_sync's next ids, plus every name a commit issued since);
+    // a fast check only: when it would refuse a wave it is first tightened to the exact max (tight_id_bound)
     uint64_t id_bound = 0;
+    jg::DevBuf idmax;  // the device max of next_id (tight_id_bound)
+    jg::DevBuf idcnt;  // per-set entry counts of the wave + two flag words (check_id_room's per-set tier)
     // open wave: payload, offsets, set per message, per-message counts / errors
     jg::DevBuf bytes, off, mset, ne, nt, na, err, eoff, toff, slow;  // slow: k_ow_group's per-message flags
     // the wave's payload / offsets / set ids: the buffers above (jg_orset_wave_*), or a node's
@@ -933,7 +955,7 @@ struct jg_orset_wire {
         // or what jg_orset_names_since staged: names [since_from, since_to), pool [since_pool0, since_pool1)
         uint64_t since_from = UINT64_MAX, since_to = 0, since_pool0 = 0, since_pool1 = 0, since_bytes = 0;
     } nout;
-    std::vector<void*> retired;  // blocks the element table outgrew (grow_keep), freed with the wire
+    std::vector<void*> retired;  // blocks the element table outgrew (grow_keep), freed at the next idle point
     ~jg_orset_wire() {
         for (void* p : retired) (void)hipFree(p);
         if (nout.ev) (void)hipEventSynchronize(nout.ev);
@@ -950,7 +972,8 @@ void ensure(jg::DevBuf& b, size_t bytes) {
 
 // Grow to `need` bytes keeping the first `keep` bytes; the new tail is zeroed when `zero`.
 // retire: the old block goes there instead of hipFree (the element table grows wave after wave, and each
-// hipFree costs ~0.2 ms of host time on the box: six arrays per growth); freed with the wire.
+// hipFree costs ~0.2 ms of host time on the box: six arrays per growth); freed by jg::orset_free_retired at the
+// end of the wave (node wave, synchronous merge).
 void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero = false, std::vector<void*>* retire = nullptr) {
     if (b.bytes >= need) return;
     if (ctx->copy) JG_HIP(hipStreamSynchronize(ctx->copy));  // uploads still landing in the old block
@@ -1089,6 +1112,49 @@ void queue_names(jg_ctx* ctx, jg_orset_wire* w) {
 void* cub_temp(jg_orset_wire* w, size_t bytes) {
     ensure(w->cub, bytes);
     return w->cub.p;
+}
+
+// id_bound sums the names every commit issued over ALL sets, so on a store with many sets it grows far past any
+// one set's next id and would refuse waves every set still has room for.  Before refusing, the
+// bound is tightened to the exact largest per-set next id (one device max over the sets, one round trip); the
+// check then asks whether that set plus every name of the wave could pass 2^32 - 2 — still conservative (all
+// names counted against the fullest set), exact in the case that matters (a set near its limit).
+uint64_t tight_id_bound(jg_ctx* ctx, jg_orset_wire* w) {
+    if (w->set_cap == 0) return w->id_bound = 0;
+    ensure(w->idmax, 16);
+    size_t temp = 0;
+    const uint32_t* nx = w->next_id.as<uint32_t>();
+    JG_HIP(hipcub::DeviceReduce::Max(nullptr, temp, nx, w->idmax.as<uint32_t>(), (int)w->set_cap, ctx->stream));
+    JG_HIP(hipcub::DeviceReduce::Max(cub_temp(w, temp), temp, nx, w->idmax.as<uint32_t>(), (int)w->set_cap, ctx->stream));
+    jg::pin_get(ctx, 0, w->idmax.p, 4);
+    jg::pin_sync(ctx);
+    uint32_t mx;
+    std::memcpy(&mx, jg::pin_at(ctx, 0), 4);
+    return w->id_bound = mx;
+}
+
+// A wave must not take any set's element ids past JG_NULL_ELEM - 1 (checked before anything commits).  Three
+// tiers: id_bound + every name of the wave (host, free); the exact largest next id + every name (one device max);
+// then per set, that set's next id + the wave's entries naming it (two small kernels, one round trip) — exact
+// per set up to repeated strings, so one set synced near its limit does not block waves on the others.
+void check_id_room(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t n_msgs) {
+    if (w->id_bound + incoming <= JG_NULL_ELEM - 1) return;
+    if (tight_id_bound(ctx, w) + incoming <= JG_NULL_ELEM - 1) return;
+    ensure(w->idcnt, (w->set_cap + 2) * 8);
+    auto* cnt = w->idcnt.as<unsigned long long>();
+    JG_HIP(hipMemsetAsync(cnt, 0, (w->set_cap + 2) * 8, ctx->stream));
+    if (n_msgs)
+        hipLaunchKernelGGL(k_id_room_count, dim3(blocks_for(n_msgs)), dim3(kBlock), 0, ctx->stream, w->ne.as<unsigned long long>(), w->vmset, n_msgs,
+                           w->set_cap, cnt);
+    hipLaunchKernelGGL(k_id_room_check, dim3(blocks_for(w->set_cap)), dim3(kBlock), 0, ctx->stream, w->next_id.as<uint32_t>(), cnt, w->set_cap,
+                       cnt + w->set_cap);
+    JG_HIP(hipGetLastError());
+    jg::pin_get(ctx, 0, cnt + w->set_cap, 16);
+    jg::pin_sync(ctx);
+    unsigned long long h[2];
+    std::memcpy(h, jg::pin_at(ctx, 0), 16);
+    JG_REQUIRE(h[0] == 0 && h[1] == 0, JG_ESTATE, "jg_orset_wave: a set's element ids would pass an OR-Set's 2^32 - 2 ids in this wave (largest next id %llu)",
+               (unsigned long long)w->id_bound);
 }
 
 template <class K, class V>
@@ -1297,8 +1363,7 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
             // before a node wave commits anything (the commit's own check then never fires mid-wave)
             uint64_t ns = 0;
             for (uint32_t j = 0; j < kLists; ++j) ns += w->lc[(1 + j) * kCountStride];
-            JG_REQUIRE(w->id_bound + ns <= JG_NULL_ELEM - 1, JG_ESTATE, "jg_orset_wave: element ids up to %llu issued + %llu names in this wave pass an OR-Set's 2^32 - 2 ids",
-                       (unsigned long long)w->id_bound, (unsigned long long)ns);
+            check_id_room(ctx, w, ns, n);
             if (h[0] == kNone) return JG_OK;
             unsigned long long e;
             JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + h[0], 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1325,8 +1390,7 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
     const uint64_t ne = tot[0], nt = tot[1];
     JG_REQUIRE(ne < 0x7FFFFFF0ull && nt < 0x7FFFFFF0ull, JG_EINVAL, "jg_orset_wave: %llu entries / %llu tags exceed one wave (2^31)",
                (unsigned long long)ne, (unsigned long long)nt);
-    JG_REQUIRE(w->id_bound + ne <= JG_NULL_ELEM - 1, JG_ESTATE, "jg_orset_wave: element ids up to %llu issued + %llu entries in this wave pass an OR-Set's 2^32 - 2 ids",
-               (unsigned long long)w->id_bound, (unsigned long long)ne);
+    check_id_room(ctx, w, ne, n);
     w->n_ent = ne;
     w->n_tag = nt;
     ensure(w->ekey, ne * 8 + 8);
@@ -1870,6 +1934,11 @@ void orset_node_no_names(jg_orset* s) {
 void orset_wire_free(jg_orset_wire* w) {
     if (w) delete w->recs;
     delete w;
+}
+
+void orset_wire_free_retired(jg_orset_wire* w) {
+    for (void* p : w->retired) (void)hipFree(p);
+    w->retired.clear();
 }
 }  // namespace jg
 

@@ -430,6 +430,30 @@ def test_element_id_space_limit(ctx):
         s.close()
 
 
+@pytest.mark.parametrize("tail", ["tables", "sort"])
+def test_element_id_room_is_per_set(ctx, monkeypatch, tail):
+    """the id-space check is per set.  Set 0 synced 2 ids below the limit does not block a wave of 300
+    new names in set 1 (the old global bound refused it), nor one of 2 names in set 0; 3 names in set 0 are refused
+    with JG_ESTATE and nothing applied — on both wave paths (tables, sort)."""
+    monkeypatch.setenv("JANUS_ORSET_TAIL", tail)
+    rng = np.random.default_rng(5)
+    s = jg.ORSetStore(ctx)
+    try:
+        s.names_sync(sets=[0, 1], next_ids=[0xFFFFFFFC, 0], cleared=[0, 0])
+        many = [(f"n{j}", J.random_guids(rng, 1)) for j in range(300)]
+        s.merge_json([1] * 3, [J.encode_orset(many[k:k + 100], []) for k in range(0, 300, 100)])
+        got = s.wave_names()
+        assert len(got) == 300 and [i for _, i, _ in got] == list(range(300)) and all(st == 1 for st, _, _ in got)
+        with pytest.raises(jg.JanusError) as e:
+            s.merge_json([0, 1], [J.encode_orset([("a", [G1]), ("b", [G2]), ("c", [G3])], []), J.encode_orset([("z", [G1])], [])])
+        assert e.value.code == jg.JG_ESTATE
+        assert sum(len(x) for x in s.read()) == 300  # nothing of the refused wave applied
+        s.merge_json([0], [J.encode_orset([("a", [G1]), ("b", [G2])], [])])
+        assert s.wave_names() == [(0, 0xFFFFFFFC, b"a"), (0, 0xFFFFFFFD, b"b")]
+    finally:
+        s.close()
+
+
 @pytest.mark.parametrize("commit", ["buckets", "radix", "auto"])
 def test_big_set_buckets_fall_back(ctx, commit, monkeypatch):
     """A set with more new names / records in one wave than the bucket commit's LDS sorts hold (2048) takes the
@@ -533,7 +557,7 @@ def test_names_since_pull_between_marks_with_out_of_order_pool_bytes(ctx):
     new names take their pool bytes by device atomics, in workgroup arrival order, not in name (id) order, so a
     pull whose `from` falls inside a wave (between two commit marks) must take the pool range from the mark at or
     before `from`, not from name `from`'s own offset.  Three waves of 800 states naming 3 new elements each, with
-    lengths 1..61 bytes (out-of-order claims move bytes by whole names); every pull from every position inside the
+    lengths 6..61 bytes (out-of-order claims move bytes by whole names); every pull from every position inside the
     second wave (and a stride over the rest) returns exactly the log's tail, and its size query returns exactly the
     tail's byte count (a short count is what let the fill write past the caller's buffer)."""
     import ctypes as C
@@ -547,8 +571,8 @@ def test_names_since_pull_between_marks_with_out_of_order_pool_bytes(ctx):
             for m, k in enumerate(sets):
                 adds = []
                 for j in range(3):
-                    ln = int(rng.integers(1, 62))
-                    name = (f"w{w}m{m}e{j}-" + "".join(chr(97 + int(c)) for c in rng.integers(0, 26, 64)))[:ln]
+                    ln = int(rng.integers(6, 62))  # a unique 6-byte head (no repeated key inside a message), then padding
+                    name = (f"{w}{m:04d}{j}" + "".join(chr(97 + int(c)) for c in rng.integers(0, 26, 64)))[:ln]
                     adds.append((name, J.random_guids(rng, 1)))
                 msgs.append(J.encode_orset(adds, []))
             rc, bad = s.wave([(sets[:400], msgs[:400]), (sets[400:], msgs[400:])])
