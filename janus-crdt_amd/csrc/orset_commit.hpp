@@ -96,7 +96,8 @@ __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __
     uint32_t s_set = 0, s_len = 0, r_key = 0;
     if (i < ns) {
         const uint32_t sid = T.list[i];
-        const uint4 mt = T.meta[sid];  // {set, length, id looked up when the chunk's k_ow_strings claimed the slot}
+        const StrSlot& se = T.slot[sid];  // set, length, id looked up when the chunk's k_ow_strings claimed the slot
+        const uint4 mt = make_uint4(se.set, se.len, se.id0, 0u);
         if (T.slot[sid].first < s_lim) {
             uint32_t id = mt.z;
             if (id == kUnresolved) {
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
     if (cnt <= kCbBlock) lds_rank_sort(perm, cnt, by_first);
     else lds_bitonic(perm, P, by_first);
     for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
-        lens[r] = T.meta[T.list[item[perm[r]]]].y;
+        lens[r] = T.slot[T.list[item[perm[r]]]].len;
     }
     __syncthreads();
     // exclusive prefix of the lengths in rank order (each thread a contiguous run, then the thread sums)

@@ -40,20 +40,34 @@ constexpr int kTabWaves = kBlock / 64;
 // one counter took every wave's append and serialised the insert kernels (360 us per 32k-state chunk).
 constexpr uint32_t kLists = 16;
 constexpr uint32_t kCountStride = 32;  // counters 256 B apart: atomics on one L2 line serialise
-// One 16-byte slot per table entry: a probe's word and the field every probe that hits then updates share
-// one line (round 3 kept them in separate arrays: two scattered lines per entry / tag reference).  Cleared
-// to {0, ~0, 0} per wave (k_tab_clear).
-struct alignas(16) StrSlot {
+// One slot per table entry: a probe's word and the field every probe that hits then updates share one line
+// (round 3 kept them in separate arrays: two scattered lines per entry / tag reference).
+// The string slot (32 B) also carries the string's fingerprint — set, length, first 8 bytes — so a probe that
+// hits a string claimed by an EARLIER chunk's launch compares against its own slot instead of the first
+// inserter's entry arrays (round 4: four scattered lines per hit, 2.37 GB of traffic for a 245 MB ORSetWorkload
+// wave).  The claimant writes the fingerprint with plain stores; the kernel boundary between
+// chunks makes it visible everywhere.  A string claimed in the SAME launch (first inserter's entry slot at or
+// past the chunk's first entry) is compared through the entry arrays as before: publishing the fingerprint
+// within a launch needs an agent-scope release / acquire, which on this chip writes back / invalidates the
+// XCD's whole L2 — measured 12.7x slower (k_ow_strings 538 -> 6855 us per wave, profiles/r05/orset_fp).
+// Strings of <= 8 bytes (the ORSetWorkload's) are decided by the slot alone; longer ones read the tail bytes
+// through the first inserter.
+// Cleared per wave to {0, ~0, kLenUnset | 0, 0, 0} (k_str_clear); record slots to {0, ~0, 0} (k_tab_clear).
+constexpr uint32_t kLenUnset = 0xFFFFFFFFu;
+struct alignas(32) StrSlot {
     unsigned long long word;  // (key >> 32) << 32 | (entry slot + 1) of the string's first inserter; 0 = empty
     uint32_t first;           // smallest canonical entry index naming the string
-    uint32_t pad;
+    uint32_t len;             // the string's length (kLenUnset until claimed)
+    unsigned long long pfx;   // the string's first 8 bytes (zero past its end)
+    uint32_t set;             // the message's set
+    uint32_t id0;             // the id k_ow_strings looked up at claim time (kNoName new, kUnresolved not looked up)
 };
 struct alignas(16) RecSlot {
     unsigned long long word;  // (hash >> 32) << 32 | (tag slot + 1) of the record's first inserter; 0 = empty
     uint32_t mint;            // smallest tag slot holding the record (arrival ordinal)
     uint32_t key;             // side << 31 | set, written by the claimant (the commit's bucket, without the string chain)
 };
-static_assert(sizeof(StrSlot) == 16 && sizeof(RecSlot) == 16, "one 16-byte slot");
+static_assert(sizeof(StrSlot) == 32 && sizeof(RecSlot) == 16, "a 32-byte string slot, a 16-byte record slot");
 
 struct StrTab {
     StrSlot* slot;
@@ -61,8 +75,6 @@ struct StrTab {
     uint32_t* list;
     unsigned long long* n;
     uint64_t sub_cap;
-    uint4* meta;               // per claimed slot, written by the claimant: {set, length, id at claim time, 0} — one
-                               // 16-byte read for the commit instead of a chain through the first entry
 };
 struct RecTab {
     RecSlot* slot;
@@ -75,6 +87,10 @@ struct RecTab {
 __global__ void k_tab_clear(uint4* __restrict__ slots, uint64_t n) {  // {word 0, ~0, 0}: empty, no first / mint yet
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         slots[i] = make_uint4(0u, 0u, 0xFFFFFFFFu, 0u);
+}
+__global__ void k_str_clear(uint4* __restrict__ slots, uint64_t n) {  // n 32-byte slots: empty, no first, fingerprint unset
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n; i += (uint64_t)gridDim.x * blockDim.x)
+        slots[i] = (i & 1) ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(0u, 0u, 0xFFFFFFFFu, kLenUnset);
 }
 
 // Lanes that claimed a slot append it to their workgroup's sub-list: one atomic per wave (claims are a few
@@ -162,6 +178,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                                                        Names N, uint32_t set_lim, uint32_t* __restrict__ sid_id) {
     __shared__ uint32_t sh[kTabWaves][kDupScan];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t es_chunk = (off[m0] + kEntryDiv - 1) / kEntryDiv;  // entry slots from here on: this launch's
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
     if (m >= m1) return;  // one message per wave: no workgroup barrier below
     const uint32_t set = mset[m];
@@ -184,20 +201,28 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         const unsigned long long word = (key >> 32) << 32 | (slot + 1);
         uint64_t p = key & T.mask;
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
-            unsigned long long w = T.slot[p].word;
+            StrSlot* e = T.slot + p;
+            unsigned long long w = e->word;
             if (w == 0) {
-                w = atomicCAS(&T.slot[p].word, 0ull, word);
+                w = atomicCAS(&e->word, 0ull, word);
                 if (w == 0) {
                     sid = (uint32_t)p;
                     fresh = true;
                     const uint32_t id0 = set < set_lim ? tab_find(N, key, set, bytes + noff, len) : kUnresolved;
                     sid_id[sid] = id0;
-                    T.meta[sid] = make_uint4(set, len, id0, 0u);
+                    e->len = len;  // the fingerprint, read by the later chunks' launches
+                    e->pfx = pfx;
+                    e->set = set;
+                    e->id0 = id0;
                     break;
                 }
             }
             if ((w >> 32) != (key >> 32)) continue;
-            if (same_string(S, bytes, slot, set, key, len, pfx, noff, (w & 0xFFFFFFFFull) - 1)) {
+            const uint64_t b = (w & 0xFFFFFFFFull) - 1;
+            const bool same = b >= es_chunk ? same_string(S, bytes, slot, set, key, len, pfx, noff, b)  // claimed in this launch
+                                            : e->len == len && e->set == set && e->pfx == pfx &&
+                                                  (len <= 8 || same_bytes(bytes + S.noff[b] + 8, bytes + noff + 8, len - 8));
+            if (same) {
                 sid = (uint32_t)p;
                 break;
             }

@@ -927,7 +927,6 @@ struct jg_orset_wire {
     // the wave's string and record tables (orset_tables.hpp), filled after each chunk's parse; `tables` =
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
     jg::DevBuf st_slot, st_list, rt_slot, rt_list, sid_id, ovf;  // 16-byte table slots (orset_tables.hpp); ovf: overflow word, sub-list counts
-    jg::DevBuf st_meta;  // per claimed string slot: the string's {set, length, id}
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
     jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
@@ -1230,7 +1229,7 @@ Entries entries_of(jg_orset_wire* w) {
 // Pass 1 over messages [m0, m1) of the open wave (queued on the compute stream).
 StrTab str_tab(jg_orset_wire* w) {
     return StrTab{w->st_slot.as<StrSlot>(), w->st_cap - 1, w->st_list.as<uint32_t>(),
-                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8, w->st_meta.as<uint4>()};
+                  w->ovf.as<unsigned long long>() + kCountStride, w->st_cap / 8};
 }
 RecTab rec_tab(jg_orset_wire* w) {
     return RecTab{w->rt_slot.as<RecSlot>(), w->rt_cap - 1, w->rt_list.as<uint32_t>(),
@@ -1261,7 +1260,6 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     const uint64_t rc = std::min(lim, pow2_at_least(std::max<uint64_t>(4096, want_r)));
     if (w->st_alloc < sc) {  // allocations only grow; the active part is the first st_cap slots
         w->st_slot.alloc(sc * sizeof(StrSlot));
-        w->st_meta.alloc(sc * 16);
         w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
         w->st_alloc = sc;
@@ -1274,7 +1272,7 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
     w->st_cap = sc;
     w->rt_cap = rc;
     if (!w->ovf.p) w->ovf.alloc((1 + 2 * kLists) * kCountStride * 8);
-    hipLaunchKernelGGL(k_tab_clear, dim3((unsigned)std::min<uint64_t>(4096, (w->st_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+    hipLaunchKernelGGL(k_str_clear, dim3((unsigned)std::min<uint64_t>(4096, (2 * w->st_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        w->st_slot.as<uint4>(), w->st_cap);
     hipLaunchKernelGGL(k_tab_clear, dim3((unsigned)std::min<uint64_t>(4096, (w->rt_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        w->rt_slot.as<uint4>(), w->rt_cap);
