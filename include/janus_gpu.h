@@ -162,6 +162,12 @@ int jg_pnc_merge_wave(jg_pnc* pnc, const jg_wave* wave, uint64_t* bad_msg);
  * the row's replica table in column order — what SafeCRDT.Update ships (BFT-CRDT/SafeCRDTs/SafeCRDT.cs:49).
  * out NULL = size query; JG_ESTATE if off[n] > cap (out untouched). */
 int jg_pnc_encode_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap);
+/* The same for the row as it stood before its last dp[i] / dn[i] of Increment / Decrement amounts to column col
+ * (the cell type's wrapping arithmetic): the snapshot SafeCRDT.Update shipped right after an earlier op of a
+ * batch whose later ops on the same key are already applied (SafeCRDT.cs:39-62; PNCounters.cs:97-112).  Lets a
+ * batch of client ops be applied in ONE jg_pnc_apply_ops and every snapshot encoded in ONE call. */
+int jg_pnc_encode_json_before(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn,
+                              uint64_t* off, uint8_t* out, uint64_t cap);
 
 /* Page-locked host memory for staging waves (PCIe DMA at full rate); free with jg_host_free. */
 int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out);

@@ -455,17 +455,28 @@ struct Out {
     }
 };
 
+// Rewind: the row as it stood before its last dp[i] / dn[i] of increments to column `col` (jg_pnc_encode_json_before;
+// the cell type's wrapping arithmetic, as Increment's); NULL dp: the row as it is.
+template <int EB>
+__device__ __forceinline__ long long cell_at(const void* base, uint64_t i, bool rewind, long long d) {
+    if constexpr (EB == 4) return rewind ? (long long)(int)((unsigned)cell<4>(base, i) - (unsigned)d) : cell<4>(base, i);
+    else return rewind ? (long long)((unsigned long long)cell<8>(base, i) - (unsigned long long)d) : cell<8>(base, i);
+}
+
 template <int EB, int PASS>
 __global__ __launch_bounds__(kBlock) void k_encode(const uint32_t* __restrict__ rows, uint64_t n, Table t, const void* P, const void* N,
-                                                   unsigned long long* __restrict__ len_off, uint8_t* __restrict__ out) {
+                                                   unsigned long long* __restrict__ len_off, uint8_t* __restrict__ out, uint32_t col,
+                                                   const long long* __restrict__ dp, const long long* __restrict__ dn) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t row = rows[i];
     const uint32_t nc = t.ncols[row];
     const uint64_t base = (uint64_t)row * t.R;
+    const long long rp = dp ? dp[i] : 0, rn = dp ? dn[i] : 0;
     if (PASS == 0) {
         unsigned long long len = 27 + (nc ? 2ull * (40ull * nc - 1) : 0);
-        for (uint32_t c = 0; c < nc; ++c) len += dec_len(cell<EB>(P, base + c)) + dec_len(cell<EB>(N, base + c));
+        for (uint32_t c = 0; c < nc; ++c)
+            len += dec_len(cell_at<EB>(P, base + c, dp && c == col, rp)) + dec_len(cell_at<EB>(N, base + c, dp && c == col, rn));
         len_off[i] = len;
         return;
     }
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(kBlock) void k_encode(const uint32_t* __restrict__ 
             o.put('"');
             o.guid(t.cols[base + c]);
             o.str("\":");
-            o.dec(cell<EB>(V, base + c));
+            o.dec(cell_at<EB>(V, base + c, dp && c == col, which ? rn : rp));
         }
     }
     o.str("}}");
@@ -1021,45 +1032,70 @@ int jg_host_free(void* p) {
     });
 }
 
+namespace {
+// jg_pnc_encode_json(_before): length pass, scan, offsets to the host; with `out`, the write pass and its bytes.
+void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off, uint8_t* out,
+                 uint64_t cap, const char* fn) {
+    JG_REQUIRE(p && off, JG_EINVAL, "%s: NULL argument", fn);
+    off[0] = 0;
+    if (n == 0) return;
+    JG_REQUIRE(key_idx, JG_EINVAL, "%s: NULL key_idx", fn);
+    JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "%s: at most 2^31-1 rows per call", fn);
+    for (uint64_t i = 0; i < n; ++i)
+        JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "%s: key_idx[%llu] = %u out of range", fn, (unsigned long long)i, key_idx[i]);
+    jg_ctx* ctx = p->ctx;
+    jg::ensure_device(ctx);
+    ensure_table(p);
+    const Table t = table_of(p);
+    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 4 + (n + 1) * 16 + (dp ? n * 16 : 0) + 768));
+    auto* rows = reinterpret_cast<uint32_t*>(s);
+    auto* len = reinterpret_cast<unsigned long long*>(s + ((n * 4 + 255) & ~255ull));
+    auto* doff = len + n + 1;
+    long long* ddp = nullptr;
+    long long* ddn = nullptr;
+    JG_HIP(hipMemcpyAsync(rows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (dp) {
+        ddp = reinterpret_cast<long long*>(doff + n + 1);
+        ddn = ddp + n;
+        JG_HIP(hipMemcpyAsync(ddp, dp, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(ddn, dn, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    const unsigned g = blocks_for(n);
+    if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr, col, ddp, ddn);
+    else hipLaunchKernelGGL((k_encode<4, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr, col, ddp, ddn);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemsetAsync(len + n, 0, 8, ctx->stream));
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, len, doff, (int)(n + 1), ctx->stream));
+    void* tmp = jg::scratch(ctx, ctx->scratch3, temp + 256);
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, temp, len, doff, (int)(n + 1), ctx->stream));
+    JG_HIP(hipMemcpyAsync(off, doff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+    if (!out) return;  // size query
+    JG_REQUIRE(off[n] <= cap, JG_ESTATE, "%s: %llu bytes exceed cap %llu", fn, (unsigned long long)off[n], (unsigned long long)cap);
+    auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
+    if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+    else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+}
+}  // namespace
+
 int jg_pnc_encode_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
-        JG_REQUIRE(p && off, JG_EINVAL, "jg_pnc_encode_json: NULL argument");
-        off[0] = 0;
-        if (n == 0) return;
-        JG_REQUIRE(key_idx, JG_EINVAL, "jg_pnc_encode_json: NULL key_idx");
-        JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "jg_pnc_encode_json: at most 2^31-1 rows per call");
-        for (uint64_t i = 0; i < n; ++i)
-            JG_REQUIRE(key_idx[i] < p->n_keys, JG_EINVAL, "jg_pnc_encode_json: key_idx[%llu] = %u out of range", (unsigned long long)i, key_idx[i]);
-        jg_ctx* ctx = p->ctx;
-        jg::ensure_device(ctx);
-        ensure_table(p);
-        const Table t = table_of(p);
-        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, n * 4 + (n + 1) * 16 + 512));
-        auto* rows = reinterpret_cast<uint32_t*>(s);
-        auto* len = reinterpret_cast<unsigned long long*>(s + ((n * 4 + 255) & ~255ull));
-        auto* doff = len + n + 1;
-        JG_HIP(hipMemcpyAsync(rows, key_idx, n * 4, hipMemcpyHostToDevice, ctx->stream));
-        const unsigned g = blocks_for(n);
-        if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr);
-        else hipLaunchKernelGGL((k_encode<4, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, len, nullptr);
-        JG_HIP(hipGetLastError());
-        JG_HIP(hipMemsetAsync(len + n, 0, 8, ctx->stream));
-        size_t temp = 0;
-        JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, len, doff, (int)(n + 1), ctx->stream));
-        void* tmp = jg::scratch(ctx, ctx->scratch3, temp + 256);
-        JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, temp, len, doff, (int)(n + 1), ctx->stream));
-        JG_HIP(hipMemcpyAsync(off, doff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
-        if (!out) return;  // size query
-        JG_REQUIRE(off[n] <= cap, JG_ESTATE, "jg_pnc_encode_json: %llu bytes exceed cap %llu", (unsigned long long)off[n],
-                   (unsigned long long)cap);
-        auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
-        if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout);
-        else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout);
-        JG_HIP(hipGetLastError());
-        JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
+        encode_rows(p, n, key_idx, 0, nullptr, nullptr, off, out, cap, "jg_pnc_encode_json");
+    });
+}
+
+int jg_pnc_encode_json_before(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off,
+                              uint8_t* out, uint64_t cap) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(p);
+        JG_REQUIRE(p && (n == 0 || (dp && dn)), JG_EINVAL, "jg_pnc_encode_json_before: NULL argument");
+        JG_REQUIRE(col < p->R, JG_EINVAL, "jg_pnc_encode_json_before: column %u past the store's %u replicas", col, p->R);
+        encode_rows(p, n, key_idx, col, dp, dn, off, out, cap, "jg_pnc_encode_json_before");
     });
 }
 

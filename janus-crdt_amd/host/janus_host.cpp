@@ -429,6 +429,23 @@ std::vector<std::string> GpuStableStore::EncodePNCStates(const std::vector<Guid>
     return out;
 }
 
+std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector<Guid>& uids, const std::vector<int64_t>& dp,
+                                                               const std::vector<int64_t>& dn) {
+    flush_registrations();
+    std::vector<uint32_t> rows;
+    rows.reserve(uids.size());
+    for (const Guid& u : uids) rows.push_back(ref(u, CrdtType::PNCounter).idx);
+    std::vector<uint64_t> off(rows.size() + 1, 0);
+    check(jg_pnc_encode_json_before(pnc_, rows.size(), rows.data(), 0, dp.data(), dn.data(), off.data(), nullptr, 0));
+    std::string buf(off.back(), '\0');
+    check(jg_pnc_encode_json_before(pnc_, rows.size(), rows.data(), 0, dp.data(), dn.data(), off.data(), reinterpret_cast<uint8_t*>(buf.data()),
+                                    buf.size()));
+    std::vector<std::string> out;
+    out.reserve(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i) out.emplace_back(buf, off[i], off[i + 1] - off[i]);
+    return out;
+}
+
 std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids) {
     materialize_names();
     std::vector<uint32_t> sets;
@@ -540,33 +557,56 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             if (e.op != kOld) need[(size_t)e.op] = 1;
     for (size_t j = head; j < q.size(); ++j)
         if (q[j].op != kOld) need[(size_t)q[j].op] = 1;
-    // 3. Apply the ops in chunks that end at every needed snapshot whose uid is touched again later
-    //    in the chunk, encode the needed snapshots after each chunk (on the device).
+    // 3. Apply the ops in chunks, encode the needed snapshots after each chunk (on the device).  A PN-Counter
+    //    snapshot is the row rewound by the amounts the chunk's later ops on that key added to the own column
+    //    (jg_pnc_encode_json_before), so PN-Counter keys never end a chunk; a chunk ends where an OR-Set key
+    //    with a snapshot needed earlier in the chunk is touched again.
     std::vector<uint8_t> result(n, 1);
     std::vector<std::string> snap(n);
     size_t c0 = 0;
     while (c0 < n) {
-        std::unordered_map<Guid, size_t, GuidHash> last_need;  // uid -> needed op in this chunk
+        std::unordered_map<Guid, size_t, GuidHash> last_need;  // OR-Set uid -> needed op in this chunk
+        std::vector<size_t> pnc_need;                          // needed PN-Counter ops, in op order
         size_t c1 = c0;
         for (; c1 < n; ++c1) {
-            if (last_need.count(ups[c1].op.uid)) break;
-            if (need[c1]) last_need.emplace(ups[c1].op.uid, c1);
+            const bool is_pnc = uids_.find(ups[c1].op.uid)->second.type == CrdtType::PNCounter;
+            if (!is_pnc && last_need.count(ups[c1].op.uid)) break;
+            if (need[c1]) {
+                if (is_pnc) pnc_need.push_back(c1);
+                else last_need.emplace(ups[c1].op.uid, c1);
+            }
         }
         std::vector<ClientOp> ops;
         ops.reserve(c1 - c0);
         for (size_t i = c0; i < c1; ++i) ops.push_back(ups[i].op);
         const auto r = ApplyOps(ops);
         std::copy(r.begin(), r.end(), result.begin() + c0);
-        std::vector<Guid> pu, ou;
-        std::vector<size_t> pi, oi;
-        for (const auto& kv : last_need) {
-            if (uids_.find(kv.first)->second.type == CrdtType::PNCounter) { pu.push_back(kv.first); pi.push_back(kv.second); }
-            else { ou.push_back(kv.first); oi.push_back(kv.second); }
+        if (!pnc_need.empty()) {
+            // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
+            // cells: walk the chunk backwards
+            std::unordered_map<Guid, std::pair<uint64_t, uint64_t>, GuidHash> after;
+            std::vector<int64_t> dp(pnc_need.size()), dn(pnc_need.size());
+            std::vector<Guid> pu(pnc_need.size());
+            size_t w = pnc_need.size();
+            for (size_t i = c1; i-- > c0;) {
+                const ClientOp& op = ups[i].op;
+                if (uids_.find(op.uid)->second.type != CrdtType::PNCounter) continue;
+                auto& a = after[op.uid];
+                if (w && pnc_need[w - 1] == i) {
+                    --w;
+                    dp[w] = (int64_t)a.first;
+                    dn[w] = (int64_t)a.second;
+                    pu[w] = op.uid;
+                }
+                const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
+                (op.opId == 2 ? a.second : a.first) += amt;
+            }
+            auto enc = EncodePNCStatesBefore(pu, dp, dn);
+            for (size_t j = 0; j < pnc_need.size(); ++j) snap[pnc_need[j]] = std::move(enc[j]);
         }
-        if (!pu.empty()) {
-            auto enc = EncodePNCStates(pu);
-            for (size_t j = 0; j < pi.size(); ++j) snap[pi[j]] = std::move(enc[j]);
-        }
+        std::vector<Guid> ou;
+        std::vector<size_t> oi;
+        for (const auto& kv : last_need) { ou.push_back(kv.first); oi.push_back(kv.second); }
         if (!ou.empty()) {
             auto enc = EncodeORSetStates(ou);
             for (size_t j = 0; j < oi.size(); ++j) snap[oi[j]] = std::move(enc[j]);

@@ -202,6 +202,9 @@ class GpuStableStore {
     // GetLastSynchronizedUpdate().Encode() of PN-Counter keys, encoded on the device — the payload
     // SafeCRDT.Update ships after a client op (SafeCRDT.cs:49; batch producer).
     std::vector<std::string> EncodePNCStates(const std::vector<Guid>& uids);
+    // The same as each row stood before its last dp[i] / dn[i] of own-column Increment / Decrement amounts
+    // (jg_pnc_encode_json_before): the snapshots of a batch of ops applied at once.
+    std::vector<std::string> EncodePNCStatesBefore(const std::vector<Guid>& uids, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn);
     // ORSetWrapper's enumeration / ORSet.LookupAll (ORSet.cs:204-227) in the reference's order.
     std::vector<std::optional<std::string>> QueryStableLookupAll(const Guid& uid);
 

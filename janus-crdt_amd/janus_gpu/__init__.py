@@ -31,7 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
-    "jg_orset_lookup_all", "jg_pnc_encode_json",
+    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
@@ -97,6 +97,7 @@ _SIGS = {
     "jg_pnc_wave_abort": ([_vp], C.c_int),
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
@@ -370,6 +371,17 @@ class PNCStore:
         _check(load().jg_pnc_encode_json(self._h, k.size, _ptr(k), _ptr(off), None, 0))
         out = np.empty(max(16, int(off[-1])), np.uint8)
         _check(load().jg_pnc_encode_json(self._h, k.size, _ptr(k), _ptr(off), _ptr(out), out.size))
+        b = out.tobytes()
+        return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
+
+    def encode_json_before(self, key_idx, dp, dn, col=0) -> list:
+        """jg_pnc_encode_json_before: each row as it stood before its last dp[i] / dn[i] of increments to `col`."""
+        k = _arr(key_idx, np.uint32)
+        p, q = _arr(dp, np.int64), _arr(dn, np.int64)
+        off = np.zeros(k.size + 1, np.uint64)
+        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), None, 0))
+        out = np.empty(max(16, int(off[-1])), np.uint8)
+        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), _ptr(out), out.size))
         b = out.tobytes()
         return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
 

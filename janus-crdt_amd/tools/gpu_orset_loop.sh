@@ -13,6 +13,7 @@ TCC=TCC_ATOMIC_sum,TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum
 for i in 1 2 3; do
     timeout -k 10 120 $ORSET_LOOP > "$OUT/run$i.json" 2> "$OUT/run$i.err" || exit 1
 done
+JANUS_TRACE_APPLY=1 timeout -k 10 120 $ORSET_LOOP > "$OUT/run_trace.json" 2> "$OUT/run_trace.err" || exit 1  # the wave's setup / tail phases
 echo "runs done"
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace_orset_loop" -o run --output-format csv -- $ORSET_LOOP > "$OUT/trace.out" 2>&1 || exit 1
 echo "trace done"

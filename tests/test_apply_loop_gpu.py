@@ -81,3 +81,20 @@ def test_c1_replay_matches_oracle():
     out = subprocess.run([str(BIN.parent / "bench_c1"), "--ops", "300000", "--waves", "2"], capture_output=True, text=True, timeout=200)
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert out.returncode == 0 and res["parity_vs_oracle"] is True, res
+
+
+@pytest.mark.parametrize("args", [
+    ["--workload", "pnc", "--keys", "2000", "--ops", "20000", "--cpu-ops", "20000", "--waves", "1"],     # many repeats per key
+    ["--workload", "pnc", "--keys", "200000", "--ops", "50000", "--cpu-ops", "50000", "--waves", "1"],
+    ["--workload", "orset", "--keys", "300", "--ops", "20000", "--cpu-ops", "6000", "--waves", "1"],     # Clears at 50 elements
+])
+def test_producer_path_matches_oracle(args):
+    """The producer path (SafeCRDT.Update + full-state Encode + ActualPropagateSyncMsg + ComputeDigest,
+    GpuStableStore::SubmitClientUpdates) on the C5 banking and ORSetWorkload op streams: op results, every
+    submitted UpdateMessage (order, identities, payload bytes) and its digest equal the oracle's
+    (host/bench_submit.cpp's parity sample)."""
+    import json
+    out = subprocess.run([str(BIN.parent / "bench_submit")] + args, capture_output=True, text=True, timeout=110)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and res["parity_vs_oracle"] is True, (res, out.stderr[-2000:])
+    assert res["submitted_msgs_per_wave"] > 0

@@ -445,3 +445,41 @@ def test_encode_matches_oracle_encoder(ctx, eb):
     pr.s.merge_json(q, got)  # a state merged into itself changes nothing
     pr.check()
     pr.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
+def test_encode_before_matches_oracle_encoder(ctx, eb):
+    """jg_pnc_encode_json_before: each row as it stood before its last dp / dn of own-column (column 0) amounts
+    — the snapshot SafeCRDT.Update shipped after an earlier op of a batch applied at once — equals the oracle's
+    encoder over the rewound row, byte for byte, with the cell type's wrapping (amounts that cross the int32 /
+    int64 edge included); the same row may be asked several times at different points."""
+    rng = np.random.default_rng(40 + eb)
+    n_keys, R = 50, 8
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, R, eb, stable)
+    cl = Cluster(rng, n_keys, 6, eb, stable)
+    keys = rng.integers(0, n_keys, 1500).astype(np.uint32)
+    msgs = [cl.message(int(k)) for k in keys]
+    pr.oracle(keys, msgs)
+    pr.s.merge_json(keys, msgs)
+    bits = 32 if eb == 4 else 64
+    q = rng.integers(0, n_keys, 400).astype(np.uint32)
+    dp = rng.integers(-2**40, 2**40, 400).astype(np.int64)
+    dn = rng.integers(0, 2**20, 400).astype(np.int64)
+    dp[:20] = 2**31 + 5  # past the int32 edge
+    dn[20:40] = -(2**62)
+    dp[40:60] = 0
+    dn[40:60] = 0
+
+    def wrap(x):
+        x = int(x) % (1 << bits)
+        return x - (1 << bits) if x >= 1 << (bits - 1) else x
+
+    got = pr.s.encode_json_before(q, dp, dn)
+    for i, k in enumerate(q):
+        c = int(pr.ncols[k])
+        P, N = pr.P[k, :c].astype(object).copy(), pr.N[k, :c].astype(object).copy()
+        P[0], N[0] = wrap(int(P[0]) - int(dp[i])), wrap(int(N[0]) - int(dn[i]))
+        exp = orc.json_encode_pnc(pr.cols[k, :c]["lo"], pr.cols[k, :c]["hi"], np.array(P, dtype=pr.P.dtype), np.array(N, dtype=pr.N.dtype), eb)
+        assert got[i] == exp, f"query {i} key {k}"
+    pr.close()
