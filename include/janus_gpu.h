@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 6
+#define JG_ABI_VERSION 7
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -199,6 +199,12 @@ int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int asyn
  * JG_EINVAL before anything changes (the wrapper's InvalidOperationException). */
 int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op,
                        const uint64_t* tag_lo, const uint64_t* tag_hi, uint8_t* result);
+/* The same, and per op i the ord limits of a snapshot of its set taken right after it (SafeCRDT.Update's
+ * GetLastSynchronizedUpdate() after each op, SafeCRDT.cs:39-62): jg_orset_encode_json with add_lim[i] / rem_lim[i]
+ * encodes the set as it stood then — valid while no later op of the batch Clears that set (a Clear drops the
+ * records such a snapshot holds). */
+int jg_orset_apply_ops_ords(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
+                            const uint64_t* tag_hi, uint8_t* result, uint64_t* add_lim, uint64_t* rem_lim);
 /* ORSet.Contains (ORSet.cs:204-237) for (set[i], elem[i]): elem present iff its add set exists
  * and (it has no tombstone set or the two tag sets differ: !SetEquals); the null element is
  * present iff !SetEquals(nullRemove, nullAdd).  out[i] = 0/1. */
@@ -209,6 +215,17 @@ int jg_orset_contains(jg_orset* s, const uint32_t* set, const uint32_t* elem, ui
  * short.  The per-set GetLastSynchronizedUpdate (ORSet.cs:305-308) that SafeCRDT.Update encodes. */
 int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* add_off, jg_tagrec* add, uint64_t cap_add, uint64_t* rem_off,
                        jg_tagrec* rem, uint64_t cap_rem);
+/* ORSetMsg.Encode() (MergeSharp/MergeSharp/CRDTs/ORSet.cs:56-69, 305-308) of sets set[0..n) from the device store,
+ * byte for byte the reference's System.Text.Json output: addSet elements in ascending element id (= the add
+ * Dictionary's insertion order), removeSet elements by their first tombstone's arrival ordinal (ties by id),
+ * tags by (ord, tag) (HashSet<Guid> insertion order), the null element's tags in nullAddGuid / nullRemoveGuid;
+ * element strings from the store's element table (names issued by waves or synced with jg_orset_names_sync —
+ * JG_ESTATE if a record's id has none).  add_lim / rem_lim (both or neither; NULL = everything): state i keeps
+ * only its set's add records with ord < add_lim[i] and tombstones with ord < rem_lim[i] — a snapshot taken
+ * before a batch's later ops (jg_orset_apply_ops_ords).  State i = out[off[i], off[i+1]); out NULL = size
+ * query; JG_ESTATE if off[n] > cap (off filled, out untouched). */
+int jg_orset_encode_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off,
+                         uint8_t* out, uint64_t cap);
 /* ORSet.LookupAll (ORSet.cs:204-227) of sets set[0..n): members of set[i] are elems[off[i], off[i+1])
  * (off has n+1 entries, always filled), in the reference's order: elements with no tombstone set,
  * then elements whose tag sets differ (each group in ascending elem id = the add Dictionary's

@@ -255,6 +255,16 @@ void orset_merge_store(jg_orset* s, jg_orset* src, bool defer = false);
 bool orset_pin_pending(jg_orset* s, size_t at);
 // hipFree the blocks the store's streams and element table retired while growing (the caller's streams drained)
 void orset_free_retired(jg_orset* s);
+// jg_orset_encode_json's first step: every record of the sets d_sets[0..n) (device), query by query, add side then
+// tombstones, in store order (element id, tag), into `buf` (grown as needed): key, tag, ord, query << 1 | side, and
+// keep = ord below d_lim[q << 1 | side] (d_lim NULL: every record).  roff: [2n + 1] segment offsets.  One round trip.
+struct OrsetGathered {
+    uint64_t R;
+    unsigned long long *key, *tlo, *thi, *roff;
+    uint32_t *ord, *qs;
+    uint8_t* keep;
+};
+OrsetGathered orset_gather_sets(jg_orset* s, uint64_t n, const uint32_t* d_sets, const unsigned long long* d_lim, jg::DevBuf& buf);
 void orset_settle_pending(jg_orset* s, size_t at);
 // orset.hip: room in the store's union targets for that many more records (no sync; skipped while counts are pending).
 void orset_reserve_union(jg_orset* s, uint64_t add_in, uint64_t rem_in);

@@ -252,6 +252,39 @@ __global__ __launch_bounds__(kOB) void k_gather_ranges(View v, const uint64_t* _
     }
 }
 
+// jg::orset_gather_sets: per query q and side, the record count of its set's run (bounds from k_set_runs).
+__global__ void k_raw_counts(const uint64_t* __restrict__ bounds, uint64_t n, unsigned long long* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 2 * n) cnt[i] = bounds[2 * i + 1] - bounds[2 * i];
+    if (i == 2 * n) cnt[i] = 0;
+}
+
+// Every record of the queried runs, query by query (add side, then tombstones), in store order: key, tag, ord,
+// query << 1 | side, and whether it lies below the query's ord limit for that side (lim NULL: all do).
+__global__ __launch_bounds__(kOB) void k_gather_raw(View a, View r, const uint64_t* __restrict__ bounds, const unsigned long long* __restrict__ roff,
+                                                    uint64_t n, uint64_t R, const unsigned long long* __restrict__ lim, unsigned long long* __restrict__ key,
+                                                    unsigned long long* __restrict__ tlo, unsigned long long* __restrict__ thi, uint32_t* __restrict__ ord,
+                                                    uint32_t* __restrict__ qs, uint8_t* __restrict__ keep) {
+    for (uint64_t j = (uint64_t)blockIdx.x * kOB + threadIdx.x; j < R; j += (uint64_t)gridDim.x * kOB) {
+        uint64_t lo = 0, hi = 2 * n;  // the last segment whose offset is <= j
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (roff[mid] <= j) lo = mid;
+            else hi = mid;
+        }
+        const View& v = (lo & 1) ? r : a;
+        const uint64_t x = jgk::slot_of(v, bounds[2 * lo] + (j - roff[lo]));
+        const Tag g = ld_tag(v.tag + x);
+        const uint32_t o = v.ord[x];
+        key[j] = v.key[x];
+        tlo[j] = g.lo;
+        thi[j] = g.hi;
+        ord[j] = o;
+        qs[j] = (uint32_t)lo;
+        keep[j] = !lim || o < lim[lo];
+    }
+}
+
 unsigned grid_for(jg_ctx* ctx, uint64_t items, unsigned per_cu = 8) {
     uint64_t g = (items + kOB - 1) / kOB;
     const uint64_t cap = (uint64_t)ctx->num_cus * per_cu;
@@ -555,7 +588,7 @@ void load_group(const jg_tagrec* b, const jg_tagrec* e, std::vector<TagKey>& ord
 // element's add tags it lacks to the tombstone set, in the add set's enumeration order (UnionWith /
 // the copy constructor of addSet[item], :175-183).
 void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
-               const uint64_t* tag_hi, uint8_t* result) {
+               const uint64_t* tag_hi, uint8_t* result, uint64_t* add_lim = nullptr, uint64_t* rem_lim = nullptr) {
     std::vector<uint64_t> order(n_ops);
     for (uint64_t i = 0; i < n_ops; ++i) order[i] = i;
     std::stable_sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return set[a] < set[b]; });
@@ -618,6 +651,7 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
                 was_cleared = true;
                 result[i] = 1;
             }
+            if (add_lim) add_lim[i] = next_a, rem_lim[i] = next_r;  // batch ords so far: rebased below
         }
         if (was_cleared) cleared.push_back(sid);
         dadd.insert(dadd.end(), sa.begin(), sa.end());
@@ -642,12 +676,24 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
         JG_HIP(hipMemcpyAsync(drop.p, bits.data(), bits.size() * 4, hipMemcpyHostToDevice, ctx->stream));
         d = jgk::Drop{drop.as<unsigned>(), (uint32_t)bits.size()};
     }
-    if (dadd.empty() && drem.empty() && cleared.empty()) return;
+    // a snapshot right after op i keeps its set's records with ord below base + the batch ords issued so far: the
+    // union appends the batch's records at base = the store's next (after any renumbering, ensure_ord_room)
+    auto rebase = [&](uint64_t base_a, uint64_t base_r) {
+        if (add_lim)
+            for (uint64_t i = 0; i < n_ops; ++i) add_lim[i] += base_a, rem_lim[i] += base_r;
+    };
+    if (dadd.empty() && drem.empty() && cleared.empty()) {
+        rebase(s->add.next, s->rem.next);
+        return;
+    }
     JG_REQUIRE(next_a < 0xFFFFFFFFull && next_r < 0xFFFFFFFFull, JG_EINVAL, "jg_orset_apply_ops: too many records in one batch");
     jg_orset tmp;
     tmp.ctx = ctx;
     upload_stream(ctx, tmp.add, dadd.data(), dadd.size(), "jg_orset_apply_ops(add)");
     upload_stream(ctx, tmp.rem, drem.data(), drem.size(), "jg_orset_apply_ops(rem)");
+    ensure_ord_room(ctx, s->add, tmp.add);
+    ensure_ord_room(ctx, s->rem, tmp.rem);
+    rebase(s->add.next, s->rem.next);
     merge_into(s, &tmp, false, d);
 }
 
@@ -743,6 +789,54 @@ void orset_free_retired(jg_orset* s) {
     for (jg_stream_soa* st : {&s->add, &s->rem, &s->spare_add, &s->spare_rem})
         if (!st->retired.empty()) st->free_retired();
     if (s->wire) orset_wire_free_retired(s->wire);
+}
+
+OrsetGathered orset_gather_sets(jg_orset* s, uint64_t n, const uint32_t* d_sets, const unsigned long long* d_lim, jg::DevBuf& buf) {
+    jg_ctx* ctx = s->ctx;
+    sync_counts(s);
+    OrsetGathered o{};
+    if (buf.bytes < n * 32 + (2 * n + 1) * 16 + 512) buf.alloc((n * 32 + (2 * n + 1) * 16 + 512) * 5 / 4);
+    auto* bounds = buf.as<uint64_t>();
+    auto* cnt = reinterpret_cast<unsigned long long*>(bounds + 4 * n);
+    auto* roff = cnt + 2 * n + 1;
+    hipLaunchKernelGGL(k_set_runs, dim3(grid_for(ctx, n, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), d_sets, n, bounds);
+    hipLaunchKernelGGL(k_raw_counts, dim3((unsigned)((2 * n + 1 + 255) / 256)), dim3(256), 0, ctx->stream, bounds, n, cnt);
+    JG_HIP(hipGetLastError());
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, cnt, roff, (int)(2 * n + 1), ctx->stream));
+    void* tmp = jg::scratch(ctx, ctx->scratch3, temp + 256);
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, temp, cnt, roff, (int)(2 * n + 1), ctx->stream));
+    jg::pin_get(ctx, 0, roff + 2 * n, 8);
+    jg::pin_sync(ctx);
+    std::memcpy(&o.R, jg::pin_at(ctx, 0), 8);
+    JG_REQUIRE(o.R < 0x7FFFFFF0ull, JG_EINVAL, "jg_orset_encode_json: %llu records exceed one call", (unsigned long long)o.R);
+    o.roff = roff;
+    if (o.R == 0) return o;
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    const uint64_t head = al(n * 32 + (2 * n + 1) * 16);
+    const uint64_t need = head + 3 * al(o.R * 8) + 2 * al(o.R * 4) + al(o.R);
+    if (buf.bytes < need) {  // grown keeping the bounds and offsets
+        jg::DevBuf nb;
+        nb.alloc(need + need / 4);
+        JG_HIP(hipMemcpyAsync(nb.p, buf.p, head, hipMemcpyDeviceToDevice, ctx->stream));
+        std::swap(nb.p, buf.p);
+        std::swap(nb.bytes, buf.bytes);
+        JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block's copy done before it is freed
+        bounds = buf.as<uint64_t>();
+        roff = reinterpret_cast<unsigned long long*>(bounds + 4 * n) + 2 * n + 1;
+        o.roff = roff;
+    }
+    char* p = buf.as<char>() + head;
+    o.key = reinterpret_cast<unsigned long long*>(p);
+    o.tlo = reinterpret_cast<unsigned long long*>(p + al(o.R * 8));
+    o.thi = reinterpret_cast<unsigned long long*>(p + 2 * al(o.R * 8));
+    o.ord = reinterpret_cast<uint32_t*>(p + 3 * al(o.R * 8));
+    o.qs = reinterpret_cast<uint32_t*>(p + 3 * al(o.R * 8) + al(o.R * 4));
+    o.keep = reinterpret_cast<uint8_t*>(p + 3 * al(o.R * 8) + 2 * al(o.R * 4));
+    hipLaunchKernelGGL(k_gather_raw, dim3(grid_for(ctx, o.R, 16)), dim3(kOB), 0, ctx->stream, view(s->add), view(s->rem), bounds, roff, n, o.R, d_lim,
+                       o.key, o.tlo, o.thi, o.ord, o.qs, o.keep);
+    JG_HIP(hipGetLastError());
+    return o;
 }
 
 void sync_counts(jg_orset* s) {
@@ -984,6 +1078,22 @@ int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const u
         jg::ensure_device(s->ctx);
         jg::sync_counts(s);
         apply_ops(s, n_ops, set, elem, op, tag_lo, tag_hi, result);
+    });
+}
+
+int jg_orset_apply_ops_ords(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t* elem, const uint8_t* op, const uint64_t* tag_lo,
+                            const uint64_t* tag_hi, uint8_t* result, uint64_t* add_lim, uint64_t* rem_lim) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(s);
+        JG_REQUIRE(s, JG_EINVAL, "jg_orset_apply_ops_ords: store is NULL");
+        if (n_ops == 0) return;
+        JG_REQUIRE(set && elem && op && tag_lo && tag_hi && result && add_lim && rem_lim, JG_EINVAL, "jg_orset_apply_ops_ords: NULL argument");
+        for (uint64_t i = 0; i < n_ops; ++i)
+            JG_REQUIRE(op[i] >= 1 && op[i] <= 3, JG_EINVAL, "jg_orset_apply_ops_ords: op[%llu] = %u is not 1 (Add), 2 (Remove) or 3 (Clear)",
+                       (unsigned long long)i, op[i]);
+        jg::ensure_device(s->ctx);
+        jg::sync_counts(s);
+        apply_ops(s, n_ops, set, elem, op, tag_lo, tag_hi, result, add_lim, rem_lim);
     });
 }
 

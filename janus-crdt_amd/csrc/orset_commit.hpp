@@ -305,6 +305,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
         N.off[g] = p;
         N.key[g] = S.key[ref];
         tab_insert(N, S.key[ref], (uint32_t)g);
+        itab_insert(N, s, (uint32_t)id, (uint32_t)g);
     }
     __syncthreads();
     if (threadIdx.x == 0) N.next_id[s] = next + cnt;

@@ -413,6 +413,7 @@ __global__ void k_ow_sassign(Sparse S, const uint8_t* __restrict__ bytes, StrTab
     N.off[g] = p;
     N.key[g] = S.key[ref];
     tab_insert(N, S.key[ref], (uint32_t)g);
+    itab_insert(N, set, (uint32_t)id, (uint32_t)g);
 }
 
 // One side's live records (their table slots, compacted): store keys, tags, and the slot (its mint is the ord).

@@ -571,12 +571,35 @@ struct Names {
     uint8_t* pool;
     uint32_t* set_gen;
     uint32_t* next_id;
+    // (set, id) -> name index, for the encoder (jg_orset_encode_json): every name ever issued, dead ones too
+    unsigned long long* ikey;  // (set << 32 | id) + 1; 0 = empty
+    uint32_t* ival;            // the name's index g
+    uint64_t imask;
 };
 
 __device__ __forceinline__ void tab_insert(const Names& N, uint64_t key, uint32_t g) {
     const unsigned long long word = (key >> 32) << 32 | (unsigned long long)(g + 1);
     for (uint64_t s = key & N.mask;; s = (s + 1) & N.mask)
         if (atomicCAS(N.tab + s, 0ull, word) == 0ull) return;
+}
+
+__device__ __forceinline__ void itab_insert(const Names& N, uint32_t set, uint32_t id, uint32_t g) {
+    const unsigned long long k = ((unsigned long long)set << 32 | id) + 1;
+    for (uint64_t s = mix64(k) & N.imask;; s = (s + 1) & N.imask)
+        if (atomicCAS(N.ikey + s, 0ull, k) == 0ull) {
+            N.ival[s] = g;
+            return;
+        }
+}
+
+// The name index of (set, id), or kNoName (a kernel after the inserting ones: no race).
+__device__ __forceinline__ uint32_t itab_find(const Names& N, uint32_t set, uint32_t id) {
+    const unsigned long long k = ((unsigned long long)set << 32 | id) + 1;
+    for (uint64_t s = mix64(k) & N.imask;; s = (s + 1) & N.imask) {
+        const unsigned long long w = N.ikey[s];
+        if (w == k) return N.ival[s];
+        if (w == 0) return kNoName;
+    }
 }
 
 __device__ __forceinline__ uint32_t tab_find(const Names& N, uint64_t key, uint32_t set, const uint8_t* name, uint32_t len) {
@@ -594,6 +617,11 @@ __device__ __forceinline__ uint32_t tab_find(const Names& N, uint64_t key, uint3
 __global__ void k_names_rebuild(Names N, uint64_t n_names) {
     const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (g < n_names && N.gen[g] == N.set_gen[N.set[g]]) tab_insert(N, N.key[g], (uint32_t)g);
+}
+
+__global__ void k_itab_rebuild(Names N, uint64_t n_names) {
+    const uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g < n_names) itab_insert(N, N.set[g], N.id[g], (uint32_t)g);
 }
 
 __global__ void k_sets_update(Names N, const uint32_t* __restrict__ set, const uint32_t* __restrict__ next, const uint8_t* __restrict__ cleared, uint64_t n) {
@@ -620,6 +648,7 @@ __global__ void k_names_put(Names N, uint64_t g0, uint64_t pool0, const uint32_t
     N.off[g] = pool0 + off[i];
     N.key[g] = key;
     tab_insert(N, key, (uint32_t)g);
+    itab_insert(N, set, nid[i], (uint32_t)g);
 }
 
 // commit: each live group head looks its string up; new strings are marked (set << 32 | entry) at their
@@ -688,6 +717,7 @@ __global__ void k_ow_assign(Entries E, const uint8_t* __restrict__ bytes, const 
     N.off[g] = p;
     N.key[g] = skey[i];
     tab_insert(N, skey[i], (uint32_t)g);
+    itab_insert(N, set, (uint32_t)id, (uint32_t)g);
 }
 
 __global__ void k_ow_next_ids(const unsigned long long* __restrict__ snk, uint64_t nnew, Names N) {
@@ -866,6 +896,247 @@ int bits_for(uint64_t x) {
     return b;
 }
 
+
+// ---- ORSetMsg.Encode on the device (jg_orset_encode_json; ORSet.cs:56-69, 305-308) ----------------------------
+// {"addSet":{"<e>":[<tags>],...},"removeSet":{...},"nullAddGuid":[<tags>],"nullRemoveGuid":[<tags>]} in
+// System.Text.Json's compact form: addSet elements in ascending element id (the add Dictionary's insertion
+// order), removeSet elements by their first tombstone's ord (when the element entered the remove Dictionary),
+// ties by id, tags by (ord, tag) (HashSet<Guid> insertion order), the null element's tags in the two lists.
+// Runs = the kept records of one (query, side, element); sections: 0 addSet, 1 removeSet, 2 nullAddGuid,
+// 3 nullRemoveGuid; seg = query * 4 + section.
+constexpr uint32_t kEncFixed = 65;                           // the five fixed texts of one ORSetMsg
+__constant__ const uint32_t kEncBefore[4] = {11, 26, 43, 63};  // fixed bytes before each section
+
+// JavaScriptEncoder.Default for a UTF-8 element string (host/wire.cpp escape): its escaped length, or its bytes.
+template <bool WRITE>
+__device__ uint32_t enc_escape(const uint8_t* s, uint32_t len, uint8_t* o) {
+    const char* HX = "0123456789ABCDEF";
+    uint32_t n = 0;
+    auto unit = [&](uint32_t u) {
+        if (WRITE) {
+            o[n] = '\\', o[n + 1] = 'u', o[n + 2] = HX[u >> 12 & 15], o[n + 3] = HX[u >> 8 & 15], o[n + 4] = HX[u >> 4 & 15], o[n + 5] = HX[u & 15];
+        }
+        n += 6;
+    };
+    for (uint32_t i = 0; i < len;) {
+        const uint32_t c = s[i];
+        if (c >= 0x80) {
+            const uint32_t k = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+            uint32_t cp = c & (k == 4 ? 0x07 : k == 3 ? 0x0F : 0x1F);
+            for (uint32_t q = 1; q < k && i + q < len; ++q) cp = cp << 6 | (s[i + q] & 0x3F);
+            i += k;
+            if (cp >= 0x10000) {
+                unit(0xD800 | (cp - 0x10000) >> 10);
+                unit(0xDC00 | ((cp - 0x10000) & 0x3FF));
+            } else {
+                unit(cp);
+            }
+            continue;
+        }
+        ++i;
+        char e = 0;
+        if (c == '\\') e = '\\';
+        else if (c == '\b') e = 'b';
+        else if (c == '\t') e = 't';
+        else if (c == '\n') e = 'n';
+        else if (c == '\f') e = 'f';
+        else if (c == '\r') e = 'r';
+        if (e) {
+            if (WRITE) o[n] = '\\', o[n + 1] = e;
+            n += 2;
+        } else if (c < 0x20 || c == 0x7F || c == '"' || c == '&' || c == '\'' || c == '+' || c == '<' || c == '>' || c == '`') {
+            unit(c);
+        } else {
+            if (WRITE) o[n] = (uint8_t)c;
+            ++n;
+        }
+    }
+    return n;
+}
+
+__device__ __forceinline__ void enc_put(uint8_t* o, const char* s) {
+    while (*s) *o++ = (uint8_t)*s++;
+}
+
+// "<Guid D>" (38 bytes): b3 b2 b1 b0 - b5 b4 - b7 b6 - b8 b9 - b10..b15, lower-case hex
+__device__ __forceinline__ void enc_guid(uint8_t* o, unsigned long long lo, unsigned long long hi) {
+    const char* hx = "0123456789abcdef";
+    const int order[16] = {3, 2, 1, 0, 5, 4, 7, 6, 8, 9, 10, 11, 12, 13, 14, 15};
+    int p = 0;
+    o[p++] = '"';
+    for (int k = 0; k < 16; ++k) {
+        if (k == 4 || k == 6 || k == 8 || k == 10) o[p++] = '-';
+        const uint32_t b = (uint32_t)((order[k] < 8 ? lo >> (8 * order[k]) : hi >> (8 * (order[k] - 8))) & 0xFF);
+        o[p++] = hx[b >> 4];
+        o[p++] = hx[b & 15];
+    }
+    o[p] = '"';
+}
+
+struct EncRec {  // the gathered records (jg::orset_gather_sets)
+    const unsigned long long *key, *tlo, *thi;
+    const uint32_t *ord, *qs;
+};
+
+// run heads over the kept records kidx[0..K) (K on the device); positions >= K are padding
+__global__ void k_enc_heads(EncRec G, const uint32_t* __restrict__ kidx, const unsigned long long* __restrict__ K, uint64_t R, uint32_t* __restrict__ hf) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= R) return;
+    uint32_t h = 0;
+    if (j < *K) {
+        const uint32_t r = kidx[j];
+        h = j == 0 || G.key[kidx[j - 1]] != G.key[r] || G.qs[kidx[j - 1]] != G.qs[r];
+    }
+    hf[j] = h;
+}
+
+// per run (rid[j] - 1 = the run of kept record j): its first kept record, end, query / side / key; first ord reset
+__global__ void k_enc_runs(EncRec G, const uint32_t* __restrict__ kidx, const unsigned long long* __restrict__ K, const uint32_t* __restrict__ rid,
+                           uint32_t* __restrict__ rstart, uint32_t* __restrict__ rend, uint32_t* __restrict__ rfirst, unsigned long long* __restrict__ nruns) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t k = *K;
+    if (j >= k) return;
+    const uint32_t run = rid[j] - 1;
+    if (j == 0 || rid[j - 1] != rid[j]) {
+        rstart[run] = (uint32_t)j;
+        rfirst[run] = 0xFFFFFFFFu;
+        if (j > 0) rend[run - 1] = (uint32_t)j;
+    }
+    if (j + 1 == k) {
+        rend[run] = (uint32_t)k;
+        *nruns = run + 1;
+    }
+}
+
+__global__ void k_enc_first_ord(EncRec G, const uint32_t* __restrict__ kidx, const unsigned long long* __restrict__ K, const uint32_t* __restrict__ rid,
+                                uint32_t* __restrict__ rfirst) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= *K) return;
+    const uint32_t o = G.ord[kidx[j]], run = rid[j] - 1;
+    if (rfirst[run] > o) atomicMin(rfirst + run, o);
+}
+
+__device__ __forceinline__ uint32_t enc_section(uint32_t qs, unsigned long long key) {
+    return ((uint32_t)key == JG_NULL_ELEM ? 2u : 0u) + (qs & 1u);
+}
+
+// run sort keys: seg << 32 | (removeSet ? first ord : 0), stable over runs in (query, side, id) order; padding ~0
+__global__ void k_enc_run_keys(EncRec G, const uint32_t* __restrict__ kidx, const uint32_t* __restrict__ rstart, const uint32_t* __restrict__ rfirst,
+                               const unsigned long long* __restrict__ nruns, uint64_t R, unsigned long long* __restrict__ rkey, uint32_t* __restrict__ rval) {
+    const uint64_t run = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (run >= R) return;
+    unsigned long long k = ~0ull;
+    if (run < *nruns) {
+        const uint32_t r = kidx[rstart[run]];
+        const uint32_t qs = G.qs[r], sec = enc_section(qs, G.key[r]);
+        const unsigned long long seg = (unsigned long long)(qs >> 1) * 4 + sec;
+        k = seg << 32 | (sec == 1 ? rfirst[run] : 0u);
+    }
+    rkey[run] = k;
+    rval[run] = (uint32_t)run;
+}
+
+// per run in output order (rank): its rank, record count, text length; the per-(query, section) bytes and first rank
+__global__ void k_enc_run_len(EncRec G, Names N, const uint32_t* __restrict__ kidx, const uint32_t* __restrict__ rstart, const uint32_t* __restrict__ rend,
+                              const unsigned long long* __restrict__ skey, const uint32_t* __restrict__ srun, const unsigned long long* __restrict__ nruns,
+                              uint64_t R, uint32_t* __restrict__ rrank, unsigned long long* __restrict__ cnt, unsigned long long* __restrict__ tlen,
+                              unsigned long long* __restrict__ qsec, uint32_t* __restrict__ sfirst, unsigned* __restrict__ err) {
+    const uint64_t rank = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (rank >= R) return;
+    if (rank >= *nruns) {
+        cnt[rank] = 0;
+        tlen[rank] = 0;
+        return;
+    }
+    const uint32_t run = srun[rank];
+    rrank[run] = (uint32_t)rank;
+    const uint32_t c = rend[run] - rstart[run];
+    const unsigned long long key = G.key[kidx[rstart[run]]];
+    const uint32_t seg = (uint32_t)(skey[rank] >> 32), sec = seg & 3;
+    unsigned long long len = 38ull * c + (c - 1);
+    if (sec < 2) {
+        const uint32_t g = itab_find(N, (uint32_t)(key >> 32), (uint32_t)key);
+        if (g == kNoName) {
+            atomicOr(err, 1u);
+        } else {
+            len += 1 + enc_escape<false>(N.pool + N.off[g], N.len[g], nullptr) + 3 + 1;
+            if (rank > 0 && (uint32_t)(skey[rank - 1] >> 32) == seg) len += 1;  // ',' before a later element
+        }
+    }
+    cnt[rank] = c;
+    tlen[rank] = len;
+    atomicAdd(qsec + seg, len);
+    if (sfirst[seg] > rank) atomicMin(sfirst + seg, (uint32_t)rank);
+}
+
+// record sort keys: output rank of its run << 32 | ord (stable: the store's tag order breaks ord ties); padding ~0
+__global__ void k_enc_rec_keys(EncRec G, const uint32_t* __restrict__ kidx, const unsigned long long* __restrict__ K, const uint32_t* __restrict__ rid,
+                               const uint32_t* __restrict__ rrank, uint64_t R, unsigned long long* __restrict__ key, uint32_t* __restrict__ val) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= R) return;
+    key[j] = j < *K ? (unsigned long long)rrank[rid[j] - 1] << 32 | G.ord[kidx[j]] : ~0ull;
+    val[j] = (uint32_t)j;
+}
+
+__global__ void k_enc_qlen(const unsigned long long* __restrict__ qsec, uint64_t n, unsigned long long* __restrict__ qlen) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q < n) qlen[q] = kEncFixed + qsec[4 * q] + qsec[4 * q + 1] + qsec[4 * q + 2] + qsec[4 * q + 3];
+    if (q == n) qlen[q] = 0;
+}
+
+// where a section's text starts in query q's state
+__device__ __forceinline__ unsigned long long enc_sec_at(const unsigned long long* qoff, const unsigned long long* qsec, uint32_t q, uint32_t sec) {
+    unsigned long long p = qoff[q] + kEncBefore[sec];
+    for (uint32_t s = 0; s < sec; ++s) p += qsec[4 * q + s];
+    return p;
+}
+
+__global__ void k_enc_fixed(const unsigned long long* __restrict__ qoff, const unsigned long long* __restrict__ qsec, uint64_t n, uint8_t* __restrict__ out) {
+    const uint64_t q = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n) return;
+    uint8_t* o = out + qoff[q];
+    enc_put(o, "{\"addSet\":{");
+    enc_put(out + enc_sec_at(qoff, qsec, (uint32_t)q, 1) - 15, "},\"removeSet\":{");
+    enc_put(out + enc_sec_at(qoff, qsec, (uint32_t)q, 2) - 17, "},\"nullAddGuid\":[");
+    enc_put(out + enc_sec_at(qoff, qsec, (uint32_t)q, 3) - 20, "],\"nullRemoveGuid\":[");
+    enc_put(out + qoff[q + 1] - 2, "]}");
+}
+
+// each run's element header / closing bracket; rtags[rank] = where its first tag goes
+__global__ void k_enc_run_text(EncRec G, Names N, const uint32_t* __restrict__ kidx, const uint32_t* __restrict__ rstart,
+                               const unsigned long long* __restrict__ skey, const uint32_t* __restrict__ srun, const unsigned long long* __restrict__ nruns,
+                               const unsigned long long* __restrict__ rpos, const unsigned long long* __restrict__ tlen, const uint32_t* __restrict__ sfirst,
+                               const unsigned long long* __restrict__ qoff, const unsigned long long* __restrict__ qsec, unsigned long long* __restrict__ rtags,
+                               uint8_t* __restrict__ out) {
+    const uint64_t rank = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (rank >= *nruns) return;
+    const uint32_t seg = (uint32_t)(skey[rank] >> 32), sec = seg & 3, q = seg >> 2;
+    unsigned long long p = enc_sec_at(qoff, qsec, q, sec) + (rpos[rank] - rpos[sfirst[seg]]);
+    if (sec < 2) {
+        const unsigned long long key = G.key[kidx[rstart[srun[rank]]]];
+        const uint32_t g = itab_find(N, (uint32_t)(key >> 32), (uint32_t)key);
+        if (rank > 0 && (uint32_t)(skey[rank - 1] >> 32) == seg) out[p++] = ',';
+        out[p++] = '"';
+        p += enc_escape<true>(N.pool + N.off[g], N.len[g], out + p);
+        out[p++] = '"', out[p++] = ':', out[p++] = '[';
+        out[enc_sec_at(qoff, qsec, q, sec) + (rpos[rank] - rpos[sfirst[seg]]) + tlen[rank] - 1] = ']';
+    }
+    rtags[rank] = p;
+}
+
+// each record's tag text: ',' before every tag but a run's first
+__global__ void k_enc_rec_text(EncRec G, const uint32_t* __restrict__ kidx, const unsigned long long* __restrict__ K, const uint32_t* __restrict__ srec,
+                               const uint32_t* __restrict__ rid, const uint32_t* __restrict__ rrank, const unsigned long long* __restrict__ cpos,
+                               const unsigned long long* __restrict__ rtags, uint8_t* __restrict__ out) {
+    const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= *K) return;
+    const uint32_t j = srec[p], rank = rrank[rid[j] - 1], r = kidx[j];
+    const unsigned long long k = p - cpos[rank];
+    unsigned long long at = rtags[rank] + 39 * k;
+    if (k) out[at - 1] = ',';
+    enc_guid(out + at, G.tlo[r], G.thi[r]);
+}
+
 }  // namespace
 
 // check_id_room's per-set tier: every message's entry count added to its set (cnt[set_cap + 1] flags a set id past
@@ -892,6 +1163,8 @@ struct jg_orset_wire {
     // element table
     jg::DevBuf tab, nset, nid, ngen, nlen, noff, nkey, pool, set_gen, next_id;
     uint64_t tab_cap = 0, n_names = 0, name_cap = 0, pool_used = 0, pool_cap = 0, set_cap = 0;
+    jg::DevBuf ikey, ival;  // (set, id) -> name index (Names::ikey), every name issued
+    uint64_t itab_cap = 0;
     // an upper bound of every set's next element id (names_sync's next ids, plus every name a commit issued since);
     // a fast check only: when it would refuse a wave it is first tightened to the exact max (tight_id_bound)
     uint64_t id_bound = 0;
@@ -954,6 +1227,7 @@ struct jg_orset_wire {
         // or what jg_orset_names_since staged: names [since_from, since_to), pool [since_pool0, since_pool1)
         uint64_t since_from = UINT64_MAX, since_to = 0, since_pool0 = 0, since_pool1 = 0, since_bytes = 0;
     } nout;
+    jg::DevBuf enc_g, enc;       // jg_orset_encode_json: the gathered records, the encoder's arrays
     std::vector<void*> retired;  // blocks the element table outgrew (grow_keep), freed at the next idle point
     ~jg_orset_wire() {
         for (void* p : retired) (void)hipFree(p);
@@ -1012,7 +1286,8 @@ jg_orset_wire* wire_of(jg_orset* s) {
 Names names_of(jg_orset_wire* w) {
     return Names{w->tab.as<unsigned long long>(), w->tab_cap - 1, w->nset.as<uint32_t>(), w->nid.as<uint32_t>(), w->ngen.as<uint32_t>(),
                  w->nlen.as<uint32_t>(), w->noff.as<unsigned long long>(), w->nkey.as<unsigned long long>(), w->pool.as<uint8_t>(),
-                 w->set_gen.as<uint32_t>(), w->next_id.as<uint32_t>()};
+                 w->set_gen.as<uint32_t>(), w->next_id.as<uint32_t>(), w->ikey.as<unsigned long long>(), w->ival.as<uint32_t>(),
+                 w->itab_cap ? w->itab_cap - 1 : 0};
 }
 
 void ensure_sets(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_sets) {
@@ -1054,6 +1329,23 @@ void ensure_names(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t poo
         JG_HIP(hipMemsetAsync(w->tab.p, 0, cap * 8, ctx->stream));
         if (w->n_names) {
             hipLaunchKernelGGL(k_names_rebuild, dim3(blocks_for(w->n_names)), dim3(kBlock), 0, ctx->stream, names_of(w), w->n_names);
+            JG_HIP(hipGetLastError());
+        }
+    }
+    if (w->itab_cap == 0 || 2 * total > w->itab_cap) {  // the (set, id) index: every name, load <= 1/2
+        const uint64_t cap = pow2_at_least(4 * total);
+        for (jg::DevBuf* b : {&w->ikey, &w->ival})
+            if (b->p) {
+                w->retired.push_back(b->p);
+                b->p = nullptr;
+                b->bytes = 0;
+            }
+        w->ikey.alloc(cap * 8);
+        w->ival.alloc(cap * 4);
+        w->itab_cap = cap;
+        JG_HIP(hipMemsetAsync(w->ikey.p, 0, cap * 8, ctx->stream));
+        if (w->n_names) {
+            hipLaunchKernelGGL(k_itab_rebuild, dim3(blocks_for(w->n_names)), dim3(kBlock), 0, ctx->stream, names_of(w), w->n_names);
             JG_HIP(hipGetLastError());
         }
     }
@@ -1868,6 +2160,124 @@ void close_wave(jg_orset_wire* w) {
     w->first_bad = kNone;
 }
 
+
+// jg_orset_encode_json: gather the sets' records below the limits, order them (runs by section and element, tags
+// by ord), size every state, then write them (see the kernels' header comment).  Two round trips: the record
+// count (gather) and the states' offsets; a third copy brings the bytes.
+void encode_sets(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off, uint8_t* out,
+                 uint64_t cap) {
+    jg_ctx* ctx = s->ctx;
+    jg_orset_wire* w = wire_of(s);
+    if (!w->itab_cap || !w->tab_cap) ensure_names(ctx, w, 0, 0);  // a store that never saw a name: empty tables
+    const bool lim = add_lim != nullptr;
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    char* q0 = static_cast<char*>(jg::scratch(ctx, ctx->scratch, al(n * 4) + (lim ? al(2 * n * 8) : 0) + 256));
+    auto* d_sets = reinterpret_cast<uint32_t*>(q0);
+    auto* d_lim = lim ? reinterpret_cast<unsigned long long*>(q0 + al(n * 4)) : nullptr;
+    JG_HIP(hipMemcpyAsync(d_sets, set, n * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (lim) {
+        std::vector<unsigned long long> l(2 * n);
+        for (uint64_t i = 0; i < n; ++i) l[2 * i] = add_lim[i], l[2 * i + 1] = rem_lim[i];
+        JG_HIP(hipMemcpyAsync(d_lim, l.data(), 2 * n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));  // l is a local
+    }
+    const jg::OrsetGathered G = jg::orset_gather_sets(s, n, d_sets, d_lim, w->enc_g);
+    const uint64_t R = G.R;
+    const EncRec E{G.key, G.tlo, G.thi, G.ord, G.qs};
+    // the encoder's arrays, one block
+    const uint64_t R1 = R + 1;
+    const uint64_t sz[] = {al(R * 4), 256, al(R * 4), al(R * 4), al(R * 4), al(R * 4), al(R * 4), 256, al(R * 8), al(R * 4), al(R * 8), al(R * 4),
+                           al(R * 4), al(R1 * 8), al(R1 * 8), al(R1 * 8), al(R1 * 8), al(4 * n * 8), al(4 * n * 4), al((n + 1) * 8), al((n + 1) * 8),
+                           al(R * 8), al(R * 4), al(R * 8), al(R * 4), al(R * 8), 256};
+    uint64_t tot = 0;
+    for (uint64_t x : sz) tot += x;
+    ensure(w->enc, tot);
+    char* p = w->enc.as<char>();
+    auto take = [&](int i) { char* r = p; p += sz[i]; return r; };
+    auto* kidx = reinterpret_cast<uint32_t*>(take(0));
+    auto* K = reinterpret_cast<unsigned long long*>(take(1));
+    auto* hf = reinterpret_cast<uint32_t*>(take(2));
+    auto* rid = reinterpret_cast<uint32_t*>(take(3));
+    auto* rstart = reinterpret_cast<uint32_t*>(take(4));
+    auto* rend = reinterpret_cast<uint32_t*>(take(5));
+    auto* rfirst = reinterpret_cast<uint32_t*>(take(6));
+    auto* nruns = reinterpret_cast<unsigned long long*>(take(7));
+    auto* rkey = reinterpret_cast<unsigned long long*>(take(8));
+    auto* rval = reinterpret_cast<uint32_t*>(take(9));
+    auto* skey = reinterpret_cast<unsigned long long*>(take(10));
+    auto* srun = reinterpret_cast<uint32_t*>(take(11));
+    auto* rrank = reinterpret_cast<uint32_t*>(take(12));
+    auto* cnt = reinterpret_cast<unsigned long long*>(take(13));
+    auto* tlen = reinterpret_cast<unsigned long long*>(take(14));
+    auto* rpos = reinterpret_cast<unsigned long long*>(take(15));
+    auto* cpos = reinterpret_cast<unsigned long long*>(take(16));
+    auto* qsec = reinterpret_cast<unsigned long long*>(take(17));
+    auto* sfirst = reinterpret_cast<uint32_t*>(take(18));
+    auto* qlen = reinterpret_cast<unsigned long long*>(take(19));
+    auto* qoff = reinterpret_cast<unsigned long long*>(take(20));
+    auto* reck = reinterpret_cast<unsigned long long*>(take(21));
+    auto* recv = reinterpret_cast<uint32_t*>(take(22));
+    auto* reck2 = reinterpret_cast<unsigned long long*>(take(23));
+    auto* srec = reinterpret_cast<uint32_t*>(take(24));
+    auto* rtags = reinterpret_cast<unsigned long long*>(take(25));
+    auto* err = reinterpret_cast<unsigned*>(take(26));
+    JG_HIP(hipMemsetAsync(qsec, 0, 4 * n * 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(sfirst, 0xFF, 4 * n * 4, ctx->stream));
+    JG_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+    JG_HIP(hipMemsetAsync(K, 0, 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(nruns, 0, 8, ctx->stream));
+    const Names N = names_of(w);
+    const unsigned gR = blocks_for(R);
+    if (R) {
+        size_t temp = 0;
+        hipcub::CountingInputIterator<uint32_t> iota(0);
+        JG_HIP(hipcub::DeviceSelect::Flagged(nullptr, temp, iota, G.keep, kidx, K, (int)R, ctx->stream));
+        JG_HIP(hipcub::DeviceSelect::Flagged(cub_temp(w, temp), temp, iota, G.keep, kidx, K, (int)R, ctx->stream));
+        hipLaunchKernelGGL(k_enc_heads, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, R, hf);
+        JG_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, temp, hf, rid, (int)R, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::InclusiveSum(cub_temp(w, temp), temp, hf, rid, (int)R, ctx->stream));
+        hipLaunchKernelGGL(k_enc_runs, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, rid, rstart, rend, rfirst, nruns);
+        hipLaunchKernelGGL(k_enc_first_ord, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, rid, rfirst);
+        hipLaunchKernelGGL(k_enc_run_keys, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, rstart, rfirst, nruns, R, rkey, rval);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, rkey, skey, rval, srun, (int)R, 0, 64, ctx->stream));
+        JG_HIP(hipcub::DeviceRadixSort::SortPairs(cub_temp(w, temp), temp, rkey, skey, rval, srun, (int)R, 0, 64, ctx->stream));
+        hipLaunchKernelGGL(k_enc_run_len, dim3(gR), dim3(kBlock), 0, ctx->stream, E, N, kidx, rstart, rend, skey, srun, nruns, R, rrank, cnt, tlen, qsec,
+                           sfirst, err);
+        hipLaunchKernelGGL(k_enc_rec_keys, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, rid, rrank, R, reck, recv);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp, reck, reck2, recv, srec, (int)R, 0, 64, ctx->stream));
+        JG_HIP(hipcub::DeviceRadixSort::SortPairs(cub_temp(w, temp), temp, reck, reck2, recv, srec, (int)R, 0, 64, ctx->stream));
+        JG_HIP(hipMemsetAsync(tlen + R, 0, 8, ctx->stream));
+        JG_HIP(hipMemsetAsync(cnt + R, 0, 8, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, tlen, rpos, (int)R1, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(cub_temp(w, temp), temp, tlen, rpos, (int)R1, ctx->stream));
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(cub_temp(w, temp), temp, cnt, cpos, (int)R1, ctx->stream));
+    }
+    hipLaunchKernelGGL(k_enc_qlen, dim3(blocks_for(n + 1)), dim3(kBlock), 0, ctx->stream, qsec, n, qlen);
+    JG_HIP(hipGetLastError());
+    size_t temp = 0;
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, temp, qlen, qoff, (int)(n + 1), ctx->stream));
+    JG_HIP(hipcub::DeviceScan::ExclusiveSum(cub_temp(w, temp), temp, qlen, qoff, (int)(n + 1), ctx->stream));
+    JG_HIP(hipMemcpyAsync(off, qoff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+    jg::pin_get(ctx, 0, err, 4);
+    jg::pin_sync(ctx);  // the stream's copies above are done too
+    unsigned e;
+    std::memcpy(&e, jg::pin_at(ctx, 0), 4);
+    JG_REQUIRE(e == 0, JG_ESTATE, "jg_orset_encode_json: a record names an element id the store's element table does not hold (names not synced)");
+    if (!out) return;  // size query
+    JG_REQUIRE(off[n] <= cap, JG_ESTATE, "jg_orset_encode_json: %llu bytes exceed cap %llu", (unsigned long long)off[n], (unsigned long long)cap);
+    auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
+    hipLaunchKernelGGL(k_enc_fixed, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, qoff, qsec, n, dout);
+    if (R) {
+        hipLaunchKernelGGL(k_enc_run_text, dim3(gR), dim3(kBlock), 0, ctx->stream, E, N, kidx, rstart, skey, srun, nruns, rpos, tlen, sfirst, qoff, qsec,
+                           rtags, dout);
+        hipLaunchKernelGGL(k_enc_rec_text, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, srec, rid, rrank, cpos, rtags, dout);
+    }
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
+    JG_HIP(hipStreamSynchronize(ctx->stream));
+}
 }  // namespace
 
 namespace jg {
@@ -2238,6 +2648,22 @@ int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint
         return jg::guard([&] { jg::fail(rc, "%s", keep); });
     }
     return jg_orset_wave_commit(s, n);
+}
+
+
+int jg_orset_encode_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off, uint8_t* out,
+                         uint64_t cap) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        JG_REQUIRE(s && off, JG_EINVAL, "jg_orset_encode_json: NULL argument");
+        off[0] = 0;
+        if (n == 0) return;
+        JG_REQUIRE(set, JG_EINVAL, "jg_orset_encode_json: NULL set list");
+        JG_REQUIRE(!add_lim == !rem_lim, JG_EINVAL, "jg_orset_encode_json: add_lim and rem_lim go together");
+        JG_REQUIRE(n < (1ull << 29), JG_EINVAL, "jg_orset_encode_json: at most 2^29 states per call");
+        jg::ensure_device(s->ctx);
+        encode_sets(s, n, set, add_lim, rem_lim, off, out, cap);
+    });
 }
 
 }  // extern "C"

@@ -11,6 +11,7 @@
 #include <memory>
 #include <condition_variable>
 #include <functional>
+#include <unordered_set>
 #include <mutex>
 #include <thread>
 
@@ -339,7 +340,7 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
     return done;
 }
 
-std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) {
+std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim) {
     materialize_names();
     std::vector<uint8_t> result(ops.size(), 1);
     std::vector<uint32_t> pkey, pcol;
@@ -391,7 +392,16 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops) 
     if (!pkey.empty()) check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
     if (!oset.empty()) {
         std::vector<uint8_t> r(oset.size());
-        check(jg_orset_apply_ops(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data()));
+        if (add_lim) {  // and each op's snapshot limits (jg_orset_apply_ops_ords)
+            std::vector<uint64_t> al(oset.size()), rl(oset.size());
+            check(jg_orset_apply_ops_ords(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data(), al.data(),
+                                          rl.data()));
+            add_lim->assign(ops.size(), 0);
+            rem_lim->assign(ops.size(), 0);
+            for (size_t j = 0; j < oidx.size(); ++j) (*add_lim)[oidx[j]] = al[j], (*rem_lim)[oidx[j]] = rl[j];
+        } else {
+            check(jg_orset_apply_ops(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data()));
+        }
         for (size_t j = 0; j < oidx.size(); ++j) result[oidx[j]] = r[j];
     }
     return result;
@@ -446,54 +456,28 @@ std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector
     return out;
 }
 
-std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids) {
-    materialize_names();
+std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids, const std::vector<uint64_t>* add_lim,
+                                                           const std::vector<uint64_t>* rem_lim) {
+    flush_names();  // every element this mirror interned is in the engine's element table
     std::vector<uint32_t> sets;
     sets.reserve(uids.size());
     for (const Guid& u : uids) sets.push_back(ref(u, CrdtType::ORSet).idx);
     const size_t n = sets.size();
-    std::vector<uint64_t> ao(n + 1, 0), ro(n + 1, 0);
-    check(jg_orset_read_sets(orset_, n, sets.data(), ao.data(), nullptr, 0, ro.data(), nullptr, 0));
-    std::vector<jg_tagrec> a(std::max<uint64_t>(ao[n], 1)), r(std::max<uint64_t>(ro[n], 1));
-    check(jg_orset_read_sets(orset_, n, sets.data(), ao.data(), a.data(), a.size(), ro.data(), r.data(), r.size()));
+    std::vector<uint64_t> off(n + 1, 0);
+    const uint64_t* al = add_lim ? add_lim->data() : nullptr;
+    const uint64_t* rl = rem_lim ? rem_lim->data() : nullptr;
+    // ORSetMsg.Encode() on the device (jg_orset_encode_json) into a buffer kept across calls: one call unless the
+    // states outgrow it
+    if (enc_buf_.size() < 4096) enc_buf_.resize(4096);
+    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), reinterpret_cast<uint8_t*>(enc_buf_.data()), enc_buf_.size());
+    if (rc == JG_ESTATE && off[n] > enc_buf_.size()) {
+        enc_buf_.resize(off[n] + off[n] / 2);
+        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), reinterpret_cast<uint8_t*>(enc_buf_.data()), enc_buf_.size());
+    }
+    check(rc);
     std::vector<std::string> out;
     out.reserve(n);
-    for (size_t i = 0; i < n; ++i) {
-        const SetKey& sk = sets_[sets[i]];
-        ORSetState st;
-        // records come sorted by (elem id, tag): one run per element.  Tags enumerate in ascending
-        // (ord, tag) (HashSet<Guid> insertion order); addSet elements in ascending id (= the add
-        // Dictionary's insertion order); removeSet elements by their first tombstone's ord (= when the
-        // element entered the remove Dictionary), ties by id; null last (its own HashSet member).
-        auto fill = [&](jg_tagrec* b, jg_tagrec* e, std::vector<std::pair<std::string, std::vector<Guid>>>& dict, std::vector<Guid>& nulls,
-                        bool by_first_ord) {
-            struct Run { jg_tagrec* b; jg_tagrec* e; uint32_t id; uint64_t first; };
-            std::vector<Run> runs;
-            for (jg_tagrec* x = b; x < e;) {
-                const uint32_t id = (uint32_t)x->key;
-                jg_tagrec* y = x;
-                uint64_t first = UINT64_MAX;
-                for (; y < e && (uint32_t)y->key == id; ++y) first = std::min(first, y->ord);
-                std::sort(x, y, [](const jg_tagrec& p, const jg_tagrec& q) {
-                    return p.ord != q.ord ? p.ord < q.ord : p.tag_lo != q.tag_lo ? p.tag_lo < q.tag_lo : p.tag_hi < q.tag_hi;
-                });
-                runs.push_back(Run{x, y, id, first});
-                x = y;
-            }
-            if (by_first_ord)
-                std::stable_sort(runs.begin(), runs.end(), [](const Run& p, const Run& q) { return p.first < q.first; });
-            for (const Run& r : runs) {
-                std::vector<Guid> tags;
-                tags.reserve(r.e - r.b);
-                for (const jg_tagrec* x = r.b; x < r.e; ++x) tags.push_back(Guid{x->tag_lo, x->tag_hi});
-                if (r.id == JG_NULL_ELEM) nulls = std::move(tags);
-                else dict.emplace_back(sk.names.at(r.id), std::move(tags));
-            }
-        };
-        fill(a.data() + ao[i], a.data() + ao[i + 1], st.addSet, st.nullAddGuid, false);
-        fill(r.data() + ro[i], r.data() + ro[i + 1], st.removeSet, st.nullRemoveGuid, true);
-        out.push_back(wire::EncodeORSetMsg(st));
-    }
+    for (size_t i = 0; i < n; ++i) out.emplace_back(enc_buf_, off[i], off[i + 1] - off[i]);
     return out;
 }
 
@@ -559,27 +543,29 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         if (q[j].op != kOld) need[(size_t)q[j].op] = 1;
     // 3. Apply the ops in chunks, encode the needed snapshots after each chunk (on the device).  A PN-Counter
     //    snapshot is the row rewound by the amounts the chunk's later ops on that key added to the own column
-    //    (jg_pnc_encode_json_before), so PN-Counter keys never end a chunk; a chunk ends where an OR-Set key
-    //    with a snapshot needed earlier in the chunk is touched again.
+    //    (jg_pnc_encode_json_before); an OR-Set snapshot is its set's records below the ord limits the apply
+    //    reported for its op (jg_orset_apply_ops_ords + jg_orset_encode_json).  A chunk ends only before a Clear
+    //    of an OR-Set key with a snapshot needed earlier in the chunk (the Clear drops the records it holds).
     std::vector<uint8_t> result(n, 1);
     std::vector<std::string> snap(n);
     size_t c0 = 0;
     while (c0 < n) {
-        std::unordered_map<Guid, size_t, GuidHash> last_need;  // OR-Set uid -> needed op in this chunk
-        std::vector<size_t> pnc_need;                          // needed PN-Counter ops, in op order
+        std::unordered_set<Guid, GuidHash> or_needed;  // OR-Set uids with a snapshot needed in this chunk
+        std::vector<size_t> pnc_need, or_need;         // needed ops, in op order
         size_t c1 = c0;
         for (; c1 < n; ++c1) {
             const bool is_pnc = uids_.find(ups[c1].op.uid)->second.type == CrdtType::PNCounter;
-            if (!is_pnc && last_need.count(ups[c1].op.uid)) break;
+            if (!is_pnc && ups[c1].op.opId == 3 && c1 > c0 && or_needed.count(ups[c1].op.uid)) break;
             if (need[c1]) {
                 if (is_pnc) pnc_need.push_back(c1);
-                else last_need.emplace(ups[c1].op.uid, c1);
+                else or_need.push_back(c1), or_needed.insert(ups[c1].op.uid);
             }
         }
         std::vector<ClientOp> ops;
         ops.reserve(c1 - c0);
         for (size_t i = c0; i < c1; ++i) ops.push_back(ups[i].op);
-        const auto r = ApplyOps(ops);
+        std::vector<uint64_t> alim, rlim;
+        const auto r = or_need.empty() ? ApplyOps(ops) : ApplyOps(ops, &alim, &rlim);
         std::copy(r.begin(), r.end(), result.begin() + c0);
         if (!pnc_need.empty()) {
             // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
@@ -604,12 +590,16 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             auto enc = EncodePNCStatesBefore(pu, dp, dn);
             for (size_t j = 0; j < pnc_need.size(); ++j) snap[pnc_need[j]] = std::move(enc[j]);
         }
-        std::vector<Guid> ou;
-        std::vector<size_t> oi;
-        for (const auto& kv : last_need) { ou.push_back(kv.first); oi.push_back(kv.second); }
-        if (!ou.empty()) {
-            auto enc = EncodeORSetStates(ou);
-            for (size_t j = 0; j < oi.size(); ++j) snap[oi[j]] = std::move(enc[j]);
+        if (!or_need.empty()) {
+            std::vector<Guid> ou;
+            std::vector<uint64_t> al, rl;
+            for (size_t i : or_need) {
+                ou.push_back(ups[i].op.uid);
+                al.push_back(alim[i - c0]);
+                rl.push_back(rlim[i - c0]);
+            }
+            auto enc = EncodeORSetStates(ou, &al, &rl);
+            for (size_t j = 0; j < or_need.size(); ++j) snap[or_need[j]] = std::move(enc[j]);
         }
         c0 = c1;
     }

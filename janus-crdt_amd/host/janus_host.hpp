@@ -172,7 +172,8 @@ class GpuStableStore {
     // per set).  Returns each op's bool result.  An unknown op id throws EngineError(JG_EINVAL) (the
     // wrappers' InvalidOperationException) before anything is applied.  A PNC op writes this copy's
     // own replica column (column 0, registered by CreateSafeCRDT).
-    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops);
+    // add_lim / rem_lim (optional): per op, the ord limits of its OR-Set's snapshot right after it (jg_orset_apply_ops_ords)
+    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim = nullptr, std::vector<uint64_t>* rem_lim = nullptr);
 
     // SafeCRDT.Update over a batch of client updates, on this store as the node's PROSPECTIVE copy
     // (SafeCRDT.cs:39-62) followed by the client batcher SafeCRDTManager.ActualPropagateSyncMsg
@@ -187,10 +188,12 @@ class GpuStableStore {
     // each op's bool result; validation failures throw before anything is applied.
     std::vector<uint8_t> SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize, std::vector<UpdateMessage>& submitted,
                                              SafeUpdateTracker& tracker);
-    // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys from the device store (jg_orset_read_sets),
+    // ORSet GetLastSynchronizedUpdate().Encode() of OR-Set keys, encoded on the device (jg_orset_encode_json),
     // byte for byte the reference's: Dictionary and HashSet enumeration orders come from the records'
-    // arrival ordinals (jg_tagrec.ord; addSet elements in ascending interned id).
-    std::vector<std::string> EncodeORSetStates(const std::vector<Guid>& uids);
+    // arrival ordinals (addSet elements in ascending interned id).  add_lim / rem_lim: each state as of those ord
+    // limits (a snapshot before a batch's later ops, ApplyOps' limits).
+    std::vector<std::string> EncodeORSetStates(const std::vector<Guid>& uids, const std::vector<uint64_t>* add_lim = nullptr,
+                                               const std::vector<uint64_t>* rem_lim = nullptr);
     // Identity of the next message SubmitClientUpdates creates (NetworkProtocol.seq; the reference keys
     // its safe-update tracker by message object, so identities only need to be unique per process).
     void SetNextMessageSeq(uint64_t seq) { next_seq_ = seq; }
@@ -284,6 +287,7 @@ class GpuStableStore {
     uint64_t last_msgs_ = 0;
     std::unique_ptr<jg::WorkerPool> pool_;
     std::vector<SetKey> sets_;
+    std::string enc_buf_;  // EncodeORSetStates' output, kept across calls
     std::vector<std::pair<NetworkProtocol, bool>> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167): message, tracked
     double last_submit_ms_ = 0;                 // lastSumittedTime
     uint64_t next_seq_ = 1;                     // message identity for the safe-update tracker

@@ -76,6 +76,10 @@ const char* same_batches(const std::vector<janus::UpdateMessage>& g, const std::
     return nullptr;
 }
 
+// OR-Set element strings of run(): JavaScriptEncoder.Default escapes in most of them (HTML-sensitive ASCII,
+// control bytes, 2-, 3- and 4-byte UTF-8), so the device encoder's snapshots are checked on every escape rule
+const char* const kElem[10] = {"0", "b<&>", "caf\xC3\xA9", "\xF0\x9F\x98\x80x", "q\"\\", "\t\x01", "six", "7", "\xE4\xB8\xAD", "nine+`'"};
+
 int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batch, uint32_t eb, int clock_step = 0) {
     const int n_nodes = 4;
     std::vector<std::unique_ptr<oracle::SafeCRDTManager>> nodes;
@@ -203,7 +207,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
                 }
             } else {
                 for (int e = -1; e < 10; ++e) {
-                    std::optional<std::string> el = e < 0 ? std::nullopt : std::optional<std::string>(std::to_string(e));
+                    std::optional<std::string> el = e < 0 ? std::nullopt : std::optional<std::string>(e < 10 ? kElem[e] : std::to_string(e));
                     std::vector<oracle::Arg> q{e < 0 ? oracle::Arg::N() : oracle::Arg::S(*el)};
                     const bool o = s0.QueryStable(q).b, g = gpu.QueryStableORSet(G(s0.guid), el);
                     (o ? n_in : n_out)++;
@@ -246,7 +250,7 @@ int run(uint64_t seed, int n_pnc, int n_set, int n_ops, int wave_every, int batc
         } else {
             const uint64_t r = rng.below(20);
             const int e = (int)rng.below(10);
-            std::vector<oracle::Arg> a{rng.below(8) == 0 ? oracle::Arg::N() : oracle::Arg::S(std::to_string(e))};
+            std::vector<oracle::Arg> a{rng.below(8) == 0 ? oracle::Arg::N() : oracle::Arg::S(kElem[e])};
             const int opid = r < 11 ? 1 : r < 19 ? 2 : 3;
             oracle::GuidGen peek = *sc.gen;  // the Guid.NewGuid() an Add will draw
             const oracle::Guid tag = peek.next();

@@ -31,7 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
-    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before",
+    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before", "jg_orset_encode_json", "jg_orset_apply_ops_ords",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
@@ -98,6 +98,8 @@ _SIGS = {
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_orset_encode_json": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_orset_apply_ops_ords": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_orset_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
@@ -516,6 +518,29 @@ class ORSetStore:
         out = np.empty(s.size, np.uint8)
         _check(load().jg_orset_apply_ops(self._h, s.size, _ptr(s), _ptr(e), _ptr(o), _ptr(lo), _ptr(hi), _ptr(out)))
         return out
+
+    def apply_ops_ords(self, set_ids, elems, ops, tag_lo, tag_hi):
+        """jg_orset_apply_ops_ords: (results, add_lim, rem_lim) — per op the ord limits of its set's snapshot right after it."""
+        s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)
+        o = _arr(ops, np.uint8)
+        lo, hi = _arr(tag_lo, np.uint64), _arr(tag_hi, np.uint64)
+        out = np.empty(s.size, np.uint8)
+        al, rl = np.zeros(s.size, np.uint64), np.zeros(s.size, np.uint64)
+        _check(load().jg_orset_apply_ops_ords(self._h, s.size, _ptr(s), _ptr(e), _ptr(o), _ptr(lo), _ptr(hi), _ptr(out), _ptr(al), _ptr(rl)))
+        return out, al, rl
+
+    def encode_json(self, set_ids, add_lim=None, rem_lim=None) -> list:
+        """ORSetMsg.Encode() of each set on the device (jg_orset_encode_json), optionally as of ord limits: list of bytes."""
+        s = _arr(set_ids, np.uint32)
+        al = None if add_lim is None else _arr(add_lim, np.uint64)
+        rl = None if rem_lim is None else _arr(rem_lim, np.uint64)
+        off = np.zeros(s.size + 1, np.uint64)
+        args = (_ptr(al) if al is not None else None, _ptr(rl) if rl is not None else None)
+        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), None, 0))
+        out = np.empty(max(16, int(off[-1])), np.uint8)
+        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), _ptr(out), out.size))
+        b = out.tobytes()
+        return [b[int(off[i]):int(off[i + 1])] for i in range(s.size)]
 
     def contains(self, set_ids, elems) -> np.ndarray:
         s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)

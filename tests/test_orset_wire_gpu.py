@@ -591,3 +591,42 @@ def test_names_since_pull_between_marks_with_out_of_order_pool_bytes(ctx):
             assert end == len(log) and tail == log[k:], k
     finally:
         s.close()
+
+
+def test_encode_snapshot_limits_equal_step_by_step_states(ctx):
+    """jg_orset_apply_ops_ords + jg_orset_encode_json(add_lim, rem_lim): the snapshot of op i's set encoded from the
+    store after the WHOLE batch, at op i's ord limits, equals the same set encoded (no limits) from a second store that
+    applied only ops[0..i] — SafeCRDT.Update's GetLastSynchronizedUpdate() after every op (SafeCRDT.cs:39-62), from
+    one apply call.  Adds, Removes (tombstones) and the null element; Clears only before a set's last snapshot (the
+    host mirror cuts its batches at a Clear that follows a needed snapshot).  The encoder's bytes themselves are
+    checked against the oracle's System.Text.Json restatement by the host parity run (test_apply_loop_gpu)."""
+    rng = np.random.default_rng(12)
+    names = [b"a", b"b<&>", "café".encode(), "\U0001F600x".encode(), b"q\"\\", b"\t\x01", b"zz"]
+    n_sets, n_ops = 5, 120
+    a, b = jg.ORSetStore(ctx), jg.ORSetStore(ctx)
+    try:
+        for st in (a, b):
+            st.names_sync(sets=list(range(n_sets)), next_ids=[len(names)] * n_sets, cleared=[0] * n_sets,
+                          names=[(s, i, nm) for s in range(n_sets) for i, nm in enumerate(names)])
+        sets = rng.integers(0, n_sets, n_ops).astype(np.uint32)
+        elems = rng.integers(0, len(names) + 1, n_ops).astype(np.uint32)
+        elems[elems == len(names)] = jg.NULL_ELEM
+        ops = np.where(rng.random(n_ops) < 0.7, 1, 2).astype(np.uint8)
+        ops[60] = 3  # a Clear: the snapshots checked below stop before it for its set... or are after it
+        lo = rng.integers(1, 2**63, n_ops, dtype=np.uint64)
+        hi = rng.integers(1, 2**63, n_ops, dtype=np.uint64)
+        res, al, rl = a.apply_ops_ords(sets, elems, ops, lo, hi)
+        check = [i for i in range(n_ops) if not (i < 60 and sets[i] == sets[60])]
+        snaps = a.encode_json(sets[check], al[check], rl[check])
+        got = dict(zip(check, snaps))
+        for i in range(n_ops):
+            r = b.apply_ops(sets[i:i + 1], elems[i:i + 1], ops[i:i + 1], lo[i:i + 1], hi[i:i + 1])
+            assert r[0] == res[i]
+            if i in got:
+                exp = b.encode_json([sets[i]])[0]
+                assert got[i] == exp, (i, got[i], exp)
+        # no limits: the final states of both stores agree
+        assert a.encode_json(list(range(n_sets))) == b.encode_json(list(range(n_sets)))
+    finally:
+        a.close()
+        b.close()
