@@ -360,6 +360,19 @@ int jg_apply_committed(jg_node* node, jg_tracker* tracker, const jg_commit* wave
  * tracker; a CRDT state of an uid the node never registered stops the block there with JG_EINVAL
  * (KeyNotFoundException, RM:329).  The shard shortcut does not apply. */
 int jg_apply_block(jg_node* node, const jg_commit* wave, uint64_t* stopped_at);
+/* jg_apply_committed handed over part by part, so the caller's own copy of the committed byte[]s into page-locked
+ * memory overlaps the uploads and parses of the parts before (SafeCRDTManager.cs:109-160 over
+ * a wave that arrives block by block).  begin: at most n_max messages and bytes_max payload bytes; append: the next
+ * part (commit indices continue from the previous part; a part whose payloads are page-locked and contiguous is
+ * uploaded in place, else gathered) — its chunks' uploads and parses are queued before it returns; end: the cut,
+ * both commits and the completions, exactly as jg_apply_committed over the concatenated parts.  A part that breaks
+ * the wave's rules (decreasing offsets, past the begin's bounds) rejects the whole wave: nothing of it is applied
+ * and the stream is closed.  No shard shortcut (every part is uploaded whole).  One streamed wave per node.  A
+ * page-locked part's payload bytes are read by the device after append returns: they must stay unchanged until
+ * end returns (a gathered part's arrays and every part's uid / type / identity arrays are copied by append). */
+int jg_apply_stream_begin(jg_node* node, jg_tracker* tracker, uint64_t n_max, uint64_t bytes_max);
+int jg_apply_stream_append(jg_node* node, const jg_commit* part);
+int jg_apply_stream_end(jg_node* node, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at);
 /* Figures of the node's last apply call.  Host: seconds gathering payloads into staging, waiting for the
  * device after the last chunk was queued, the whole call.  Device: kernel time of the wave (hipEvents
  * around each chunk's kernels and around the final phase, on the context's stream) = chunk_busy_s (the

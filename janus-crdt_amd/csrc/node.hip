@@ -369,6 +369,26 @@ struct jg_tracker {
     }
 };
 
+// One wave in flight on a node.  jg_apply_committed / jg_apply_block run it from begin to end in one call; the
+// streamed form (jg_apply_stream_begin / _append / _end) hands the wave over part by part, so a caller that copies
+// its committed byte[]s into page-locked memory block by block overlaps that copy with the
+// uploads and parses of the parts before.  Messages are numbered in hand-over order (= commit order).
+struct WaveRun {
+    bool active = false, block_mode = false, filter = false, trace = false, do_pnc = false, do_orset = false;
+    jg_tracker* tr = nullptr;
+    uint64_t n = 0, total_bytes = 0;  // the wave's messages and payload bytes (stream: upper bounds from begin)
+    uint64_t seen = 0;                // messages handed over (commit index of the next)
+    uint64_t m0 = 0, b0 = 0, mo = 0;  // messages, payload bytes and meta bytes on the device
+    uint64_t meta_cap = 0;
+    size_t n_ev = 0, chunk_msgs = 0, tail = 0, min_par = 0;
+    uint32_t rank = 0, world = 1;
+    double t_begin = 0, t_loop = 0, t_gather = 0;
+    hipEvent_t up_ev[2] = {nullptr, nullptr};
+    DevUids du{};
+    DevTrack dt{};
+    std::vector<uint64_t> tcnt, tbytes;
+};
+
 struct jg_node {
     jg_ctx* ctx;
     jg_pnc* pnc;
@@ -395,6 +415,7 @@ struct jg_node {
     jg_apply_stats stats{};
     std::vector<hipEvent_t> ev;  // pairs around each chunk's kernels and the final phase (device_busy_s)
     hipEvent_t drained = nullptr;  // the compute stream's tail when a wave starts (the copy queue waits on it)
+    WaveRun run;                   // the wave in flight (one call, or a streamed wave between begin and end)
 
     ~jg_node() {
         for (auto& a : arenas) (void)hipHostFree(a.first);
@@ -508,19 +529,13 @@ bool test_commit_fail() {
     const char* e = std::getenv("JANUS_TEST_ORSET_COMMIT_FAIL");
     return e && e[0] == '1';
 }
+constexpr size_t kTask = 2048;
 
-// The apply loop over one wave (jg_apply_committed / jg_apply_block).
-void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
-    const double t_begin = now_s();
-    jg_ctx* ctx = nd->ctx;
-    const uint64_t n = w->n;
-    JG_REQUIRE(n < 0x7FFFFFF0ull, JG_EINVAL, "jg_apply: at most 2^31 - 16 messages per wave");
-    JG_REQUIRE(n == 0 || (w->uid && w->type && (w->off ? w->bytes != nullptr || w->off[n] == 0 : (w->ptr && w->len))), JG_EINVAL,
-               "jg_apply: NULL array in the wave");
-    if (w->off) JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");  // monotonicity: checked by the chunks' first pass
+// Every wave, empty ones too: the figures reset, names pending from the last commit dropped, the uid table's
+// registrations and the tracker's adds to the device, the staging arenas reused.
+void wave_prologue(jg_node* nd, jg_tracker* tr, double* tp) {
     nd->stats = jg_apply_stats{};
-    static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;  // setup phases to stderr
-    double tp[8] = {now_s()};
+    tp[0] = now_s();
     if (nd->orset) jg::orset_node_no_names(nd->orset);
     tp[1] = now_s();
     nd->sync_table();
@@ -529,50 +544,36 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     tp[3] = now_s();
     nd->arena_i = nd->arena_off = 0;  // the previous wave's chunks are no longer referenced
     nd->dmap.clear();
-    if (n == 0) {
-        *stopped_at = UINT64_MAX;
-        return;
-    }
-    jg::WorkerPool& pool = nd->workers();
-    const bool filter = !block_mode && nd->shortcut();
-    const uint32_t rank = nd->shard_rank, world = nd->shard_world;
-    auto pay = [&](uint64_t i) -> const uint8_t* { return w->off ? w->bytes + w->off[i] : w->ptr[i]; };
-    auto plen = [&](uint64_t i) -> uint64_t { return w->off ? w->off[i + 1] - w->off[i] : w->len[i]; };
-    auto keep = [&](uint64_t i) { return !filter || shard_of(w->uid[i].lo, w->uid[i].hi, world) == rank; };
+}
 
+// Setup: the prologue, buffers for `n` messages / `total_bytes` payload bytes and up to `max_chunks` chunks, both
+// parsers opened.
+void wave_begin(jg_node* nd, WaveRun& r, jg_tracker* tr, uint64_t n, uint64_t total_bytes, uint64_t max_chunks, bool block_mode, bool filter) {
+    r = WaveRun{};
+    r.t_begin = now_s();
+    r.tr = tr;
+    r.n = n;
+    r.total_bytes = total_bytes;
+    r.block_mode = block_mode;
+    r.filter = filter;
+    r.rank = nd->shard_rank;
+    r.world = nd->shard_world;
+    jg_ctx* ctx = nd->ctx;
+    static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;  // setup phases to stderr
+    r.trace = trace;
+    double tp[8];
+    wave_prologue(nd, tr, tp);
     // chunks: ~48 MB of payload each (sized from the previous wave's bytes per message), the last 16k
     // messages a chunk of their own (its upload + passes are the part no host work overlaps)
     // (read per call: tests narrow them)
     const char* ce = std::getenv("JANUS_WAVE_CHUNK");
     const size_t chunk_env = ce ? std::max<size_t>(1, std::strtoull(ce, nullptr, 10)) : size_t{0};
     const char* pe = std::getenv("JANUS_HOST_PAR_MIN");  // below this many messages a chunk is gathered on the caller alone
-    const size_t min_par = pe ? (size_t)std::strtoull(pe, nullptr, 10) : size_t{8192};
-    const size_t chunk_msgs = chunk_env ? chunk_env : std::clamp<size_t>((size_t)((48u << 20) / std::max(nd->avg_msg_bytes, 64.0)), 8192, 131072);
-    const size_t tail = std::max<size_t>(1, std::min<size_t>(16384, chunk_msgs / 8));
-    // a small first chunk: the first upload starts after ~0.1 ms of gathering instead of a full chunk's
-    std::vector<uint64_t> cb{0};
-    const uint64_t first = n > 4 * tail ? tail : chunk_msgs;
-    for (uint64_t c0 = first; c0 < n; c0 += chunk_msgs) cb.push_back(c0);
-    if (n > cb.back() + 2 * tail) cb.push_back(n - tail);
-    cb.push_back(n);
-    const size_t n_chunks = cb.size() - 1;
-    constexpr size_t kTask = 2048;
-
-    // capacity for the whole wave (payload bytes: an upper bound when the shard shortcut drops states)
-    uint64_t total_bytes = 0;
-    if (w->off) {
-        total_bytes = w->off[n];
-    } else {
-        const uint64_t per = std::max<uint64_t>(65536, (n + 63) / 64);  // few large tasks: this pass only sums lengths
-        const size_t ntask = (size_t)((n + per - 1) / per);
-        std::vector<uint64_t> part(ntask);
-        jg::deal(pool, n >= min_par, ntask, [&](size_t q, int) {
-            uint64_t b = 0;
-            for (uint64_t i = q * per, e = std::min<uint64_t>(n, (q + 1) * per); i < e; ++i) b += w->len[i];
-            part[q] = b;
-        });
-        for (uint64_t b : part) total_bytes += b;
-    }
+    r.min_par = pe ? (size_t)std::strtoull(pe, nullptr, 10) : size_t{8192};
+    r.chunk_msgs = chunk_env ? chunk_env : std::clamp<size_t>((size_t)((48u << 20) / std::max(nd->avg_msg_bytes, 64.0)), 8192, 131072);
+    r.tail = std::max<size_t>(1, std::min<size_t>(16384, r.chunk_msgs / 8));
+    r.tcnt.assign((r.chunk_msgs + kTask - 1) / kTask + 2, 0);
+    r.tbytes.assign(r.tcnt.size(), 0);
     tp[4] = now_s();
     ensure(nd->bytes, ((total_bytes + 15) & ~15ull) + 64);  // the parsers read aligned 16-byte windows
     ensure(nd->off, (n + 1) * 8);
@@ -583,15 +584,12 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     ensure(nd->mset, n * 4);
     ensure(nd->tslot, n * 4);
     ensure(nd->status, 64);
-    ensure(nd->meta, n * 33 + 72 * (n_chunks + 1));  // per chunk: 33 m + 8 bytes, 64-B aligned
-    uint8_t* d_bytes = nd->bytes.as<uint8_t>();
-    uint64_t* d_off = nd->off.as<uint64_t>();
-    uint32_t* d_rows = nd->rows.as<uint32_t>();
-    uint32_t* d_mset = nd->mset.as<uint32_t>();
-    unsigned long long* d_status = nd->status.as<unsigned long long>();
-    const bool do_pnc = nd->pnc && nd->n_pnc > 0, do_orset = nd->orset && nd->n_orset > 0;
-    const DevUids du{nd->dtab.as<UidSlot>(), nd->htab.size() - 1};
-    const DevTrack dt = tr && tr->cap ? tr->dev() : DevTrack{nullptr, nullptr, 0};
+    r.meta_cap = n * 33 + 72 * (max_chunks + 1);  // per chunk: 33 m + 8 bytes, 64-B aligned
+    ensure(nd->meta, r.meta_cap);
+    r.do_pnc = nd->pnc && nd->n_pnc > 0;
+    r.do_orset = nd->orset && nd->n_orset > 0;
+    r.du = DevUids{nd->dtab.as<UidSlot>(), nd->htab.size() - 1};
+    r.dt = tr && tr->cap ? tr->dev() : DevTrack{nullptr, nullptr, 0};
     // the copy queue must not overwrite buffers kernels queued earlier on the compute stream still read:
     // it waits for the stream's tail on the device (a host sync here also waited for the tracker adds
     // just queued, 0.3-0.4 ms of every C5 wave before the first gather)
@@ -599,137 +597,189 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     JG_HIP(hipEventRecord(nd->drained, ctx->stream));
     JG_HIP(hipStreamWaitEvent(ctx->copy, nd->drained, 0));
     tp[5] = now_s();
-    JG_HIP(hipMemsetAsync(d_off, 0, 8, ctx->stream));
-    JG_HIP(hipMemsetAsync(d_status, 0xFF, 64, ctx->stream));
-    if (do_pnc) jg::pnc_node_begin(nd->pnc, n);
+    JG_HIP(hipMemsetAsync(nd->off.as<uint64_t>(), 0, 8, ctx->stream));
+    JG_HIP(hipMemsetAsync(nd->status.as<unsigned long long>(), 0xFF, 64, ctx->stream));
+    if (r.do_pnc) jg::pnc_node_begin(nd->pnc, n);
     tp[6] = now_s();
-    if (do_orset) jg::orset_node_begin(nd->orset, d_bytes, d_off, d_mset, n, total_bytes, nd->max_set);
+    if (r.do_orset) jg::orset_node_begin(nd->orset, nd->bytes.as<uint8_t>(), nd->off.as<uint64_t>(), nd->mset.as<uint32_t>(), n, total_bytes, nd->max_set);
     tp[7] = now_s();
     if (trace)
         std::fprintf(stderr, "apply setup: checks %.0f us, names %.0f, uid table %.0f, tracker adds %.0f, sizes %.0f, buffers %.0f, pnc begin %.0f, orset begin %.0f\n",
-                     (tp[0] - t_begin) * 1e6, (tp[1] - tp[0]) * 1e6, (tp[2] - tp[1]) * 1e6, (tp[3] - tp[2]) * 1e6, (tp[4] - tp[3]) * 1e6,
+                     (tp[0] - r.t_begin) * 1e6, (tp[1] - tp[0]) * 1e6, (tp[2] - tp[1]) * 1e6, (tp[3] - tp[2]) * 1e6, (tp[4] - tp[3]) * 1e6,
                      (tp[5] - tp[4]) * 1e6, (tp[6] - tp[5]) * 1e6, (tp[7] - tp[6]) * 1e6);
-    const bool direct = w->off && !filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
     if (filter) nd->dmap.resize(n);
-
     // trace mode: timing events on the copy queue before the first upload and after the last one
-    hipEvent_t up_ev[2] = {nullptr, nullptr};
     if (trace) {
-        for (hipEvent_t& e : up_ev) JG_HIP(hipEventCreate(&e));
-        JG_HIP(hipEventRecord(up_ev[0], ctx->copy));
+        for (hipEvent_t& e : r.up_ev) JG_HIP(hipEventCreate(&e));
+        JG_HIP(hipEventRecord(r.up_ev[0], ctx->copy));
     }
-    double t_gather = 0;
-    const double t_loop = now_s();
-    nd->stats.setup_s = t_loop - t_begin;
-    uint64_t m0 = 0, b0 = 0, mo = 0;
-    size_t n_ev = 0;  // event pairs recorded
-    const size_t max_tasks = (chunk_msgs + kTask - 1) / kTask + 1;
-    std::vector<uint64_t> tcnt(max_tasks + 1), tbytes(max_tasks + 1);
-    try {
-        for (size_t c = 0; c < n_chunks; ++c) {
-            const uint64_t c0 = cb[c], c1 = cb[c + 1];
-            const size_t ntask = (size_t)((c1 - c0 + kTask - 1) / kTask);
-            const bool par = c1 - c0 >= min_par;
-            const double tg = now_s();
-            // pass 1: kept messages and their bytes per task (and, for contiguous payloads, that the offsets
-            // never decrease: the wave is rejected before anything of it is applied)
-            std::atomic<uint64_t> bad_off{UINT64_MAX};
-            jg::deal(pool, par, ntask, [&](size_t q, int) {
-                uint64_t k = 0, b = 0;
-                const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
-                for (uint64_t i = c0 + q * kTask; i < e; ++i)
-                    if (keep(i)) ++k, b += plen(i);
-                if (w->off)
-                    for (uint64_t i = c0 + q * kTask; i < e; ++i)
-                        if (w->off[i + 1] < w->off[i]) {
-                            uint64_t cur = bad_off.load();
-                            while (i < cur && !bad_off.compare_exchange_weak(cur, i)) {
-                            }
-                            break;
-                        }
-                tcnt[q + 1] = k;
-                tbytes[q + 1] = b;
-            });
-            JG_REQUIRE(bad_off.load() == UINT64_MAX, JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)bad_off.load());
-            // monotone on [0, c1] and within off[n]: every chunk so far fits the buffers sized from off[n]
-            JG_REQUIRE(!w->off || w->off[c1] <= w->off[n], JG_EINVAL, "jg_apply: offsets decrease after message %llu", (unsigned long long)(c1 - 1));
-            tcnt[0] = tbytes[0] = 0;
-            for (size_t q = 0; q < ntask; ++q) tcnt[q + 1] += tcnt[q], tbytes[q + 1] += tbytes[q];
-            const uint64_t m = tcnt[ntask], nb = tbytes[ntask];
-            if (m == 0) {
-                t_gather += now_s() - tg;
-                continue;
-            }
-            const uint64_t nb_pad = direct ? 0 : (nb + 15) & ~15ull;
-            char* buf = nd->stage(nb_pad + (m + 1) * 8 + m * 16 + m * 8 + m + 64);
-            auto* soff = reinterpret_cast<uint64_t*>(buf + nb_pad);
-            auto* suid = reinterpret_cast<jg_guid*>(soff + m + 1);
-            auto* sseq = reinterpret_cast<uint64_t*>(suid + m);
-            auto* stype = reinterpret_cast<uint8_t*>(sseq + m);
-            soff[0] = 0;
-            // pass 2: payloads (non-temporal lines), chunk-relative end offsets, uids, identities, types
-            jg::deal(pool, par, ntask, [&](size_t q, int) {
-                uint64_t j = tcnt[q], o = tbytes[q];
-                jg::LineStream out(buf, o);
-                const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
-                for (uint64_t i = c0 + q * kTask; i < e; ++i) {
-                    if (!direct && i + 8 < e) {  // every line of the payload 8 messages ahead
-                        const uint8_t* pq = pay(i + 8);
-                        for (uint64_t x = 0, L = plen(i + 8); x < L; x += 64) __builtin_prefetch(pq + x);
+    r.t_loop = now_s();
+    nd->stats.setup_s = r.t_loop - r.t_begin;
+    r.active = true;
+}
+
+// A wave rejected mid-loop (offsets checked chunk by chunk) or a device error: nothing was applied, but the chunks
+// already classified took first-occurrence claims on tracker slots; release them for the next wave.
+void wave_abort(jg_node* nd, WaveRun& r, uint64_t claimed) {
+    jg_ctx* ctx = nd->ctx;
+    if (r.dt.tab && claimed)
+        hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(claimed)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), claimed, r.dt.claim);
+    (void)hipStreamSynchronize(ctx->copy);
+    (void)hipStreamSynchronize(ctx->stream);
+    if (r.do_orset) jg::orset_node_abort(nd->orset);
+    for (hipEvent_t& e : r.up_ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
+    r.active = false;
+}
+
+// Messages [c0, c1) of part `w` (commit indices gbase + i): gathered into page-locked staging (or uploaded in place
+// when the part's payloads are page-locked and contiguous), then classify and both parses of the chunk.
+void wave_chunk(jg_node* nd, WaveRun& r, const jg_commit* w, uint64_t gbase, uint64_t c0, uint64_t c1, bool direct) {
+    jg_ctx* ctx = nd->ctx;
+    jg::WorkerPool& pool = nd->workers();
+    const bool filter = r.filter;
+    const uint32_t rank = r.rank, world = r.world;
+    auto pay = [&](uint64_t i) -> const uint8_t* { return w->off ? w->bytes + w->off[i] : w->ptr[i]; };
+    auto plen = [&](uint64_t i) -> uint64_t { return w->off ? w->off[i + 1] - w->off[i] : w->len[i]; };
+    auto keep = [&](uint64_t i) { return !filter || shard_of(w->uid[i].lo, w->uid[i].hi, world) == rank; };
+    uint8_t* d_bytes = nd->bytes.as<uint8_t>();
+    uint64_t* d_off = nd->off.as<uint64_t>();
+    std::vector<uint64_t>& tcnt = r.tcnt;
+    std::vector<uint64_t>& tbytes = r.tbytes;
+    const size_t ntask = (size_t)((c1 - c0 + kTask - 1) / kTask);
+    if (tcnt.size() < ntask + 1) tcnt.resize(ntask + 1), tbytes.resize(ntask + 1);
+    const bool par = c1 - c0 >= r.min_par;
+    const double tg = now_s();
+    // pass 1: kept messages and their bytes per task (and, for contiguous payloads, that the offsets
+    // never decrease: the wave is rejected before anything of it is applied)
+    std::atomic<uint64_t> bad_off{UINT64_MAX};
+    jg::deal(pool, par, ntask, [&](size_t q, int) {
+        uint64_t k = 0, b = 0;
+        const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
+        for (uint64_t i = c0 + q * kTask; i < e; ++i)
+            if (keep(i)) ++k, b += plen(i);
+        if (w->off)
+            for (uint64_t i = c0 + q * kTask; i < e; ++i)
+                if (w->off[i + 1] < w->off[i]) {
+                    uint64_t cur = bad_off.load();
+                    while (i < cur && !bad_off.compare_exchange_weak(cur, i)) {
                     }
-                    if (!keep(i)) continue;
-                    const uint64_t L = plen(i);
-                    if (!direct) out.put(reinterpret_cast<const char*>(pay(i)), L);
-                    o += L;
-                    soff[j + 1] = o;
-                    suid[j] = w->uid[i];
-                    sseq[j] = w->seq ? w->seq[i] : 0;
-                    stype[j] = w->type[i];
-                    if (filter) nd->dmap[m0 + j] = i;
-                    ++j;
+                    break;
                 }
-                if (!direct) out.finish();
-            });
-            t_gather += now_s() - tg;
-            // upload (copy stream), then classify and both parses of the chunk (compute stream)
-            const uint8_t* src = direct ? w->bytes + w->off[c0] : reinterpret_cast<const uint8_t*>(buf);
-            if (nb) JG_HIP(hipMemcpyAsync(d_bytes + b0, src, nb, hipMemcpyHostToDevice, ctx->copy));
-            const uint64_t meta_bytes = (m + 1) * 8 + m * 25;  // offsets, uids (16), identities (8), types (1)
-            uint8_t* d_meta = nd->meta.as<uint8_t>() + mo;
-            JG_HIP(hipMemcpyAsync(d_meta, soff, meta_bytes, hipMemcpyHostToDevice, ctx->copy));
-            mo += (meta_bytes + 63) & ~63ull;
-            jg::upload_done(ctx);
-            JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));
-            hipLaunchKernelGGL(k_unstage, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d_meta, m, m0, b0, d_off, nd->uid.as<Guid16>(),
-                               nd->seq.as<uint64_t>(), nd->type.as<uint8_t>());
-            hipLaunchKernelGGL(k_classify, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, nd->uid.as<Guid16>(), nd->type.as<uint8_t>(),
-                               nd->seq.as<unsigned long long>(), m0, m0 + m, du, dt, d_rows, d_mset, nd->tslot.as<uint32_t>(), d_status);
-            JG_HIP(hipGetLastError());
-            if (do_pnc) jg::pnc_node_scan(nd->pnc, d_bytes, d_off, d_rows, m0, m0 + m);
-            if (do_orset) jg::orset_node_parse(nd->orset, m0, m0 + m);
-            JG_HIP(hipEventRecord(nd->event(2 * n_ev + 1), ctx->stream));
-            ++n_ev;
-            m0 += m;
-            b0 += nb;
-            ++nd->stats.chunks;
-        }
-    } catch (...) {
-        // a wave rejected mid-loop (offsets checked chunk by chunk): nothing was applied, but the chunks
-        // already classified took first-occurrence claims on tracker slots; release them for the next wave
-        if (dt.tab && m0) hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(m0)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), m0, dt.claim);
-        (void)hipStreamSynchronize(ctx->copy);
-        (void)hipStreamSynchronize(ctx->stream);
-        if (do_orset) jg::orset_node_abort(nd->orset);
-        throw;
+        tcnt[q + 1] = k;
+        tbytes[q + 1] = b;
+    });
+    JG_REQUIRE(bad_off.load() == UINT64_MAX, JG_EINVAL, "jg_apply: offsets decrease at message %llu", (unsigned long long)(gbase + bad_off.load()));
+    // monotone on [0, c1] and within off[n]: every chunk so far fits the buffers sized from off[n]
+    JG_REQUIRE(!w->off || w->off[c1] <= w->off[w->n], JG_EINVAL, "jg_apply: offsets decrease after message %llu", (unsigned long long)(gbase + c1 - 1));
+    tcnt[0] = tbytes[0] = 0;
+    for (size_t q = 0; q < ntask; ++q) tcnt[q + 1] += tcnt[q], tbytes[q + 1] += tbytes[q];
+    const uint64_t m = tcnt[ntask], nb = tbytes[ntask];
+    if (m == 0) {
+        r.t_gather += now_s() - tg;
+        return;
     }
-    const uint64_t nn = m0;  // messages on the device
+    JG_REQUIRE(r.m0 + m <= r.n && r.b0 + nb <= r.total_bytes, JG_EINVAL,
+               "jg_apply_stream_append: %llu messages / %llu payload bytes pass the %llu / %llu declared at begin", (unsigned long long)(r.m0 + m),
+               (unsigned long long)(r.b0 + nb), (unsigned long long)r.n, (unsigned long long)r.total_bytes);
+    const uint64_t meta_bytes = (m + 1) * 8 + m * 25;  // offsets, uids (16), identities (8), types (1)
+    JG_REQUIRE(r.mo + meta_bytes <= r.meta_cap, JG_EINVAL, "jg_apply_stream_append: more chunks than the wave was sized for");
+    const uint64_t nb_pad = direct ? 0 : (nb + 15) & ~15ull;
+    char* buf = nd->stage(nb_pad + (m + 1) * 8 + m * 16 + m * 8 + m + 64);
+    auto* soff = reinterpret_cast<uint64_t*>(buf + nb_pad);
+    auto* suid = reinterpret_cast<jg_guid*>(soff + m + 1);
+    auto* sseq = reinterpret_cast<uint64_t*>(suid + m);
+    auto* stype = reinterpret_cast<uint8_t*>(sseq + m);
+    soff[0] = 0;
+    const uint64_t m0 = r.m0, b0 = r.b0;
+    // pass 2: payloads (non-temporal lines), chunk-relative end offsets, uids, identities, types
+    jg::deal(pool, par, ntask, [&](size_t q, int) {
+        uint64_t j = tcnt[q], o = tbytes[q];
+        jg::LineStream out(buf, o);
+        const uint64_t e = std::min(c1, c0 + (q + 1) * kTask);
+        for (uint64_t i = c0 + q * kTask; i < e; ++i) {
+            if (!direct && i + 8 < e) {  // every line of the payload 8 messages ahead
+                const uint8_t* pq = pay(i + 8);
+                for (uint64_t x = 0, L = plen(i + 8); x < L; x += 64) __builtin_prefetch(pq + x);
+            }
+            if (!keep(i)) continue;
+            const uint64_t L = plen(i);
+            if (!direct) out.put(reinterpret_cast<const char*>(pay(i)), L);
+            o += L;
+            soff[j + 1] = o;
+            suid[j] = w->uid[i];
+            sseq[j] = w->seq ? w->seq[i] : 0;
+            stype[j] = w->type[i];
+            if (filter) nd->dmap[m0 + j] = gbase + i;
+            ++j;
+        }
+        if (!direct) out.finish();
+    });
+    r.t_gather += now_s() - tg;
+    // upload (copy stream), then classify and both parses of the chunk (compute stream)
+    const uint8_t* src = direct ? w->bytes + w->off[c0] : reinterpret_cast<const uint8_t*>(buf);
+    if (nb) JG_HIP(hipMemcpyAsync(d_bytes + b0, src, nb, hipMemcpyHostToDevice, ctx->copy));
+    uint8_t* d_meta = nd->meta.as<uint8_t>() + r.mo;
+    JG_HIP(hipMemcpyAsync(d_meta, soff, meta_bytes, hipMemcpyHostToDevice, ctx->copy));
+    r.mo += (meta_bytes + 63) & ~63ull;
+    jg::upload_done(ctx);
+    JG_HIP(hipEventRecord(nd->event(2 * r.n_ev), ctx->stream));
+    hipLaunchKernelGGL(k_unstage, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, d_meta, m, m0, b0, d_off, nd->uid.as<Guid16>(),
+                       nd->seq.as<uint64_t>(), nd->type.as<uint8_t>());
+    hipLaunchKernelGGL(k_classify, dim3(blocks_for(m)), dim3(kBlock), 0, ctx->stream, nd->uid.as<Guid16>(), nd->type.as<uint8_t>(),
+                       nd->seq.as<unsigned long long>(), m0, m0 + m, r.du, r.dt, nd->rows.as<uint32_t>(), nd->mset.as<uint32_t>(),
+                       nd->tslot.as<uint32_t>(), nd->status.as<unsigned long long>());
+    JG_HIP(hipGetLastError());
+    if (r.do_pnc) jg::pnc_node_scan(nd->pnc, d_bytes, d_off, nd->rows.as<uint32_t>(), m0, m0 + m);
+    if (r.do_orset) jg::orset_node_parse(nd->orset, m0, m0 + m);
+    JG_HIP(hipEventRecord(nd->event(2 * r.n_ev + 1), ctx->stream));
+    ++r.n_ev;
+    r.m0 += m;
+    r.b0 += nb;
+    ++nd->stats.chunks;
+}
+
+// Part `w` (commit indices gbase..) in chunks: ~48 MB of payload each, a small first chunk (the first upload starts
+// after ~0.1 ms of gathering instead of a full chunk's) and, on the wave's end (`last`), its last `tail` messages
+// a chunk of their own (the part no host work overlaps).
+void wave_part(jg_node* nd, WaveRun& r, const jg_commit* w, uint64_t gbase, bool last) {
+    const uint64_t n = w->n;
+    if (n == 0) return;
+    JG_REQUIRE(w->uid && w->type && (w->off ? w->bytes != nullptr || w->off[n] == 0 : (w->ptr && w->len)), JG_EINVAL, "jg_apply: NULL array in the wave");
+    if (w->off) JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");  // monotonicity: checked by the chunks' first pass
+    const bool direct = w->off && !r.filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
+    std::vector<uint64_t> cb{0};
+    const uint64_t first = gbase == 0 && n > 4 * r.tail ? r.tail : r.chunk_msgs;
+    for (uint64_t c0 = first; c0 < n; c0 += r.chunk_msgs) cb.push_back(c0);
+    if (last && n > cb.back() + 2 * r.tail) cb.push_back(n - r.tail);
+    cb.push_back(n);
+    for (size_t c = 0; c + 1 < cb.size(); ++c) wave_chunk(nd, r, w, gbase, cb[c], cb[c + 1], direct);
+}
+
+// The final phase: the cut (the first state the reference's loop would throw at), both commits, the safe-update
+// completions of the messages before the cut in commit order, the figures.
+void wave_end(jg_node* nd, WaveRun& r, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
+    jg_ctx* ctx = nd->ctx;
+    jg_tracker* tr = r.tr;
+    const DevTrack dt = r.dt;
+    const bool do_pnc = r.do_pnc, do_orset = r.do_orset, filter = r.filter, trace = r.trace;
+    uint8_t* d_bytes = nd->bytes.as<uint8_t>();
+    uint64_t* d_off = nd->off.as<uint64_t>();
+    uint32_t* d_rows = nd->rows.as<uint32_t>();
+    uint32_t* d_mset = nd->mset.as<uint32_t>();
+    unsigned long long* d_status = nd->status.as<unsigned long long>();
+    const uint64_t nn = r.m0;  // messages on the device
+    const uint64_t b0 = r.b0;
+    const size_t n_ev = r.n_ev;
+    hipEvent_t* up_ev = r.up_ev;
     if (trace) JG_HIP(hipEventRecord(up_ev[1], ctx->copy));
-    nd->stats.gather_s = t_gather;
+    nd->stats.gather_s = r.t_gather;
     nd->stats.msgs_uploaded = nn;
     nd->stats.bytes_uploaded = b0;
     if (nn) nd->avg_msg_bytes = (double)b0 / (double)nn;
     const double t_dev = now_s();
-    nd->stats.loop_s = t_dev - t_loop;
+    nd->stats.loop_s = t_dev - r.t_loop;
+    r.active = false;
 
     // the cut: the first state the reference's loop would throw at
     JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));  // the final phase's kernels start after the chunks'
@@ -738,7 +788,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
     int code = JG_OK;
     std::string why;
     try {
-        if (block_mode) {
+        if (r.block_mode) {
             unsigned long long unk;
             JG_HIP(hipMemcpyAsync(&unk, d_status, 8, hipMemcpyDeviceToHost, ctx->stream));
             JG_HIP(hipStreamSynchronize(ctx->stream));
@@ -780,9 +830,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         // catch, or a stale claim below the next wave's index would keep that safe update from completing
         // (ADVICE r03).  The OR-Set commit's one data-dependent failure (a set's element ids running out) is
         // ruled out by orset_node_check before the PN-Counter commit, so what is left here is a device error.
-        if (dt.tab && nn) hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
-        (void)hipStreamSynchronize(ctx->stream);
-        if (do_orset) jg::orset_node_abort(nd->orset);
+        wave_abort(nd, r, nn);
         throw;
     }
 
@@ -831,7 +879,7 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
             JG_HIP(hipStreamSynchronize(ctx->stream));
         }
     } else {
-        if (dt.tab) {
+        if (dt.tab && nn) {
             hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(nn)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), nn, dt.claim);
             JG_HIP(hipGetLastError());
         }
@@ -858,8 +906,8 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         JG_HIP(hipEventElapsedTime(&first_ms, up_ev[0], nd->ev[0]));
         std::fprintf(stderr, "apply device: uploads %.0f us (%llu chunks, %.1f GB/s of payload over the span), first chunk's kernels at +%.0f us, "
                      "last kernel %.0f us after the last upload\n",
-                     up_ms * 1e3, (unsigned long long)n_chunks, up_ms > 0 ? b0 / (up_ms * 1e-3) / 1e9 : 0.0, first_ms * 1e3, after_ms * 1e3);
-        for (hipEvent_t e : up_ev) (void)hipEventDestroy(e);
+                     up_ms * 1e3, (unsigned long long)nd->stats.chunks, up_ms > 0 ? b0 / (up_ms * 1e-3) / 1e9 : 0.0, first_ms * 1e3, after_ms * 1e3);
+        for (hipEvent_t& e : r.up_ev) (void)hipEventDestroy(e), e = nullptr;
     }
     double busy = 0;
     for (size_t k = 0; k <= n_ev; ++k) {
@@ -869,17 +917,61 @@ void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode
         if (k == n_ev) nd->stats.tail_busy_s = ms * 1e-3;  // the final phase's pair
     }
     nd->stats.device_busy_s = busy;
-    if (do_orset) jg::orset_free_retired(nd->orset);  // the wave has drained: blocks its growth retired go now
     nd->stats.chunk_busy_s = busy - nd->stats.tail_busy_s;
+    if (do_orset) jg::orset_free_retired(nd->orset);  // the wave has drained: blocks its growth retired go now
     if (n_completed) *n_completed = ndone;
     *stopped_at = cut < nn ? (filter ? nd->dmap[cut] : cut) : UINT64_MAX;
     const double t_end = now_s();
     nd->stats.device_wait_s = t_end - t_dev;
-    nd->stats.total_s = t_end - t_begin;
+    nd->stats.total_s = t_end - r.t_begin;
     if (late_code != JG_OK) jg::fail(late_code, "%s (the wave's OR-Set commit; its safe-update completions were reported)", late_why.c_str());
     if (code != JG_OK) jg::fail(code, "%s (commit index %llu)", why.c_str(), (unsigned long long)*stopped_at);
 }
 
+// The apply loop over one wave in one call (jg_apply_committed / jg_apply_block).
+void apply_wave(jg_node* nd, jg_tracker* tr, const jg_commit* w, bool block_mode, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
+    const uint64_t n = w->n;
+    JG_REQUIRE(n < 0x7FFFFFF0ull, JG_EINVAL, "jg_apply: at most 2^31 - 16 messages per wave");
+    JG_REQUIRE(n == 0 || (w->uid && w->type && (w->off ? w->bytes != nullptr || w->off[n] == 0 : (w->ptr && w->len))), JG_EINVAL,
+               "jg_apply: NULL array in the wave");
+    if (w->off) JG_REQUIRE(w->off[0] == 0, JG_EINVAL, "jg_apply: off[0] must be 0");
+    WaveRun& r = nd->run;
+    JG_REQUIRE(!r.active, JG_EINVAL, "jg_apply: a streamed wave is open on this node (jg_apply_stream_end first)");
+    if (n == 0) {  // the uid table, names and tracker adds still go to the device (the next wave finds them there)
+        double tp[8];
+        wave_prologue(nd, tr, tp);
+        *stopped_at = UINT64_MAX;
+        return;
+    }
+    // capacity for the whole wave (payload bytes: an upper bound when the shard shortcut drops states)
+    uint64_t total_bytes = 0;
+    if (w->off) {
+        total_bytes = w->off[n];
+    } else {
+        jg::WorkerPool& pool = nd->workers();
+        const uint64_t per = std::max<uint64_t>(65536, (n + 63) / 64);  // few large tasks: this pass only sums lengths
+        const size_t ntask = (size_t)((n + per - 1) / per);
+        std::vector<uint64_t> part(ntask);
+        jg::deal(pool, n >= 8192, ntask, [&](size_t q, int) {
+            uint64_t b = 0;
+            for (uint64_t i = q * per, e = std::min<uint64_t>(n, (q + 1) * per); i < e; ++i) b += w->len[i];
+            part[q] = b;
+        });
+        for (uint64_t b : part) total_bytes += b;
+    }
+    const bool filter = !block_mode && nd->shortcut();
+    const size_t chunk_guess = std::clamp<size_t>((size_t)((48u << 20) / std::max(nd->avg_msg_bytes, 64.0)), 8192, 131072);
+    const char* ce = std::getenv("JANUS_WAVE_CHUNK");
+    const size_t cm = ce ? std::max<size_t>(1, std::strtoull(ce, nullptr, 10)) : chunk_guess;
+    wave_begin(nd, r, tr, n, total_bytes, n / cm + 4, block_mode, filter);
+    try {
+        wave_part(nd, r, w, 0, true);
+    } catch (...) {
+        wave_abort(nd, r, r.m0);
+        throw;
+    }
+    wave_end(nd, r, completed, n_completed, stopped_at);
+}
 }  // namespace
 
 extern "C" {
@@ -1064,6 +1156,50 @@ int jg_apply_committed(jg_node* nd, jg_tracker* tr, const jg_commit* wave, uint6
         JG_REQUIRE(!tr || tr->ctx == nd->ctx, JG_EINVAL, "jg_apply_committed: the tracker belongs to another context");
         jg::ensure_device(nd->ctx);
         apply_wave(nd, tr, wave, false, completed, n_completed, stopped_at);
+    });
+}
+
+int jg_apply_stream_begin(jg_node* nd, jg_tracker* tr, uint64_t n_max, uint64_t bytes_max) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd, JG_EINVAL, "jg_apply_stream_begin: NULL node");
+        JG_REQUIRE(!tr || tr->ctx == nd->ctx, JG_EINVAL, "jg_apply_stream_begin: the tracker belongs to another context");
+        JG_REQUIRE(!nd->run.active, JG_EINVAL, "jg_apply_stream_begin: a streamed wave is already open on this node");
+        JG_REQUIRE(n_max > 0 && n_max < 0x7FFFFFF0ull, JG_EINVAL, "jg_apply_stream_begin: 1 .. 2^31 - 16 messages per wave");
+        jg::ensure_device(nd->ctx);
+        // every part may make a chunk of its own: the meta area is sized for one chunk per message at most
+        wave_begin(nd, nd->run, tr, n_max, bytes_max, n_max + 1, false, false);
+    });
+}
+
+int jg_apply_stream_append(jg_node* nd, const jg_commit* part) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd && part, JG_EINVAL, "jg_apply_stream_append: NULL argument");
+        WaveRun& r = nd->run;
+        JG_REQUIRE(r.active, JG_EINVAL, "jg_apply_stream_append: no streamed wave open (jg_apply_stream_begin)");
+        jg::ensure_device(nd->ctx);
+        try {
+            wave_part(nd, r, part, r.seen, false);
+            r.seen += part->n;
+        } catch (...) {  // the wave is rejected as a whole, nothing of it applied (the one-call path's rule)
+            wave_abort(nd, r, r.m0);
+            throw;
+        }
+    });
+}
+
+int jg_apply_stream_end(jg_node* nd, uint64_t* completed, uint64_t* n_completed, uint64_t* stopped_at) {
+    uint64_t dummy = 0;
+    if (!stopped_at) stopped_at = &dummy;
+    *stopped_at = UINT64_MAX;
+    if (n_completed) *n_completed = 0;
+    return jg::guard([&] {
+        auto lk_ = jg::lock(nd);
+        JG_REQUIRE(nd, JG_EINVAL, "jg_apply_stream_end: NULL node");
+        JG_REQUIRE(nd->run.active, JG_EINVAL, "jg_apply_stream_end: no streamed wave open (jg_apply_stream_begin)");
+        jg::ensure_device(nd->ctx);
+        wave_end(nd, nd->run, completed, n_completed, stopped_at);
     });
 }
 

@@ -49,7 +49,8 @@ int main(int argc, char** argv) {
     uint64_t accounts = 1000000, ops = 1000000, cpu_msgs = 100000;
     int waves = 3, nodes = 4, device = 0, batch = 1000, threads_per_node = 3;  // 12 client threads (config example)
     uint32_t rank = 0, world = 1;
-    bool normal = false, parity = false, direct = false, arena = false;
+    bool normal = false, parity = false, direct = false, arena = false, stream = false;
+    size_t part_msgs = 65536;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--accounts") && i + 1 < argc) accounts = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--ops") && i + 1 < argc) ops = std::strtoull(argv[++i], nullptr, 10);
@@ -59,6 +60,8 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--parity")) parity = true;
         else if (!std::strcmp(argv[i], "--direct")) direct = true;  // the wave received into page-locked memory
         else if (!std::strcmp(argv[i], "--arena")) direct = arena = true;  // the caller copies the wave into page-locked memory (timed)
+        else if (!std::strcmp(argv[i], "--arena-stream")) stream = true;  // the same copy part by part, overlapped (jg_apply_stream_*)
+        else if (!std::strcmp(argv[i], "--part-msgs") && i + 1 < argc) part_msgs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--world") && i + 1 < argc) world = (uint32_t)std::atoi(argv[++i]);
@@ -209,7 +212,8 @@ int main(int argc, char** argv) {
         if (direct) gpu.PackCommitted(wave, !arena);
         const double t0 = arena ? tp : now_s();
         if (direct && w > 0) pack_s += now_s() - tp;
-        const std::vector<uint64_t> done = direct ? gpu.ApplyPacked(&tracker_g) : gpu.ApplyCommitted(wave, &tracker_g);
+        const std::vector<uint64_t> done = stream ? gpu.ApplyArenaStreamed(wave, &tracker_g, part_msgs)
+                                           : direct ? gpu.ApplyPacked(&tracker_g) : gpu.ApplyCommitted(wave, &tracker_g);
         const double t1 = now_s();
         if (w == 0) {
             if (parity) {  // the warmup wave reaches the oracle too (untimed), so states stay in step
@@ -284,7 +288,7 @@ int main(int argc, char** argv) {
     const double pcie_bytes = (double)up_bytes + 33.0 * (double)up_msgs;
     std::printf("{\"workload\": \"C5 banking replay (BankingWorload.cs ops: view/deposit/transfer/withdraw at opsRatio [0.25, 0.25, 0.5], "
                 "every d an Increment; %s accounts %llu; %d nodes, clientBatchSize %d with state compaction; committed waves of %llu client ops)\", "
-                "\"waves\": %d, \"direct\": %s, \"arena\": %s, \"untimed_pack_ms_per_wave\": %.3f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
+                "\"waves\": %d, \"direct\": %s, \"arena\": %s, \"stream\": %s, \"untimed_pack_ms_per_wave\": %.3f, \"msgs_per_s\": %.1f, \"client_ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"state_msgs_per_wave\": %.1f, "
                 "\"client_states_per_wave\": %.1f, \"safe_states_per_wave\": %.1f, \"completed_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, "
                 "\"caller_flatten_ms_per_wave\": %.3f, \"library_ms_per_wave\": %.3f, \"gather_ms_per_wave\": %.3f, "
                 "\"device_wait_ms_per_wave\": %.3f, \"device_busy_ms_per_wave\": %.3f, \"chunk_busy_ms_per_wave\": %.3f, \"setup_ms_per_wave\": %.3f, \"loop_ms_per_wave\": %.3f, \"host_ms_per_wave\": %.3f, "
@@ -292,7 +296,7 @@ int main(int argc, char** argv) {
                 "\"host_threads\": %d, \"rank\": %u, \"world\": %u, \"owned_accounts\": %llu, \"applied_msgs_per_wave\": %.1f, "
                 "\"cpu_baseline\": {\"msgs_per_s\": %.1f, \"sample_msgs_per_wave\": %.1f, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle HandleAfterConsensusUpdates: Decode (System.Text.Json restatement) + PNCounter.Merge per message\"}}\n",
-                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, direct ? "true" : "false", arena ? "true" : "false", arena ? 0.0 : 1e3 * pack_s / W, gpu_n / gpu_s,
+                normal ? "normal" : "uniform", (unsigned long long)accounts, nodes, batch, (unsigned long long)ops, waves, direct ? "true" : "false", (arena || stream) ? "true" : "false", stream ? "true" : "false", arena ? 0.0 : 1e3 * pack_s / W, gpu_n / gpu_s,
                 (double)ops * waves / gpu_s, 1e3 * gpu_s / W, (double)gpu_n / W, (double)n_states / W, (double)n_safe / W, (double)n_done / W,
                 (double)payload_timed / std::max<uint64_t>(gpu_n, 1), 1e3 * flat_s / W, 1e3 * lib_s / W, 1e3 * gather_s / W, 1e3 * wait_s / W,
                 1e3 * busy_s / W, 1e3 * chunk_s / W, 1e3 * setup_s / W, 1e3 * loop_s / W, 1e3 * (flat_s + gather_s) / W, (double)up_msgs / W, pcie_bytes / W, pcie_bytes / lib_s / 1e9,

@@ -319,6 +319,72 @@ std::vector<uint64_t> GpuStableStore::ApplyPacked(SafeUpdateTracker* tracker) {
     return run_wave(wave, tracker, false);
 }
 
+std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker,
+                                                         size_t part_msgs) {
+    flush_registrations();
+    flush_names();
+    std::vector<const UpdateMessage*> blocks;
+    for (const auto& list : updates)
+        for (const auto& block : list) blocks.push_back(&block);
+    const size_t n = index_blocks(blocks);
+    flatten_s_ = 0;
+    last_msgs_ = n;
+    if (w_done_.size() < n) w_done_.resize(n + n / 4);
+    if (n == 0) return ApplyCommitted(updates, tracker);
+    p_off_.resize(n + 1);
+    p_off_[0] = 0;
+    for (size_t b = 0, i = 0; b < blocks.size(); ++b)
+        for (const NetworkProtocol& u : blocks[b]->update) p_off_[i + 1] = p_off_[i] + u.message.size(), ++i;
+    const uint64_t nb = p_off_[n];
+    if (p_cap_ < nb + 64) {
+        if (p_bytes_) check(jg_host_free(p_bytes_));
+        p_bytes_ = nullptr;
+        void* p = nullptr;
+        p_cap_ = nb + nb / 4 + 64;
+        check(jg_host_alloc(ctx_, p_cap_, &p));
+        p_bytes_ = static_cast<uint8_t*>(p);
+    }
+    check(jg_apply_stream_begin(node_, tracker ? tracker->handle() : nullptr, n, nb));
+    std::vector<uint64_t> poff;
+    // parts of whole UpdateMessages, ~part_msgs messages each: the caller's copy of part k + 1 (plain cached copies,
+    // what a C# caller's parallel Span.CopyTo does) runs while part k uploads
+    for (size_t b0 = 0; b0 < blocks.size();) {
+        size_t b1 = b0;
+        while (b1 < blocks.size() && (b1 == b0 || block_off_[b1] - block_off_[b0] < part_msgs)) ++b1;
+        const size_t i0 = block_off_[b0], i1 = block_off_[b1];
+        parallel_ranges(pool(), i1 - i0, [&](size_t a, size_t e, int) {
+            if (a >= e) return;
+            a += i0, e += i0;
+            size_t b = (size_t)(std::upper_bound(block_off_.begin(), block_off_.end(), a) - block_off_.begin()) - 1;
+            for (size_t i = a; i < e; ++b) {
+                const NetworkProtocol* u = blocks[b]->update.data() + (i - block_off_[b]);
+                for (const size_t f = std::min(e, block_off_[b + 1]); i < f; ++i, ++u) {
+                    w_uid_[i] = jg_guid{u->uid.lo, u->uid.hi};
+                    w_type_[i] = u->syncMsgType == NetworkProtocol::CRDTMsg ? 1 : 0;
+                    w_seq_[i] = u->seq;
+                    std::memcpy(p_bytes_ + p_off_[i], u->message.data(), u->message.size());
+                }
+            }
+        });
+        poff.resize(i1 - i0 + 1);
+        for (size_t i = i0; i <= i1; ++i) poff[i - i0] = p_off_[i] - p_off_[i0];
+        const jg_commit part{i1 - i0, w_uid_.data() + i0, w_type_.data() + i0, w_seq_.data() + i0, poff.data(), p_bytes_ + p_off_[i0], nullptr, nullptr};
+        const int rc = jg_apply_stream_append(node_, &part);
+        if (rc != JG_OK) throw EngineError(rc, last_error());  // the library closed the stream: nothing applied
+        b0 = b1;
+    }
+    uint64_t n_done = 0, at = UINT64_MAX;
+    const int rc = jg_apply_stream_end(node_, w_done_.data(), &n_done, &at);
+    const std::string why = rc == JG_OK ? std::string() : last_error();
+    jg_node_last_stats(node_, &stats_);
+    std::vector<uint64_t> done(w_done_.begin(), w_done_.begin() + (ptrdiff_t)n_done);
+    if (rc != JG_OK) {
+        if (at == UINT64_MAX) throw EngineError(rc, why);
+        throw ApplyError(rc, why, at, std::move(done));
+    }
+    return done;
+}
+
 std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdateTracker* tracker, bool block_mode) {
     const uint64_t n = wave.n;
     last_msgs_ = n;
@@ -485,6 +551,11 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                                                          std::vector<UpdateMessage>& submitted,
                                                          SafeUpdateTracker& tracker) {
     const size_t n = ups.size();
+    static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;  // phase times to stderr
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    double tt[6] = {trace ? now() : 0};
+    double t_apply = 0, t_enc_p = 0, t_enc_o = 0;
+    size_t n_chunks = 0;
     for (const ClientUpdate& u : ups) {  // the wrappers' checks, before anything is applied or queued
         const auto it = uids_.find(u.op.uid);
         if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
@@ -534,6 +605,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             }
         }
     }
+    if (trace) tt[1] = now();
     // 2. Which ops' snapshots are needed: those submitted now or still queued.
     std::vector<uint8_t> need(n, 0);
     for (const Flush& f : flushes)
@@ -565,7 +637,11 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         ops.reserve(c1 - c0);
         for (size_t i = c0; i < c1; ++i) ops.push_back(ups[i].op);
         std::vector<uint64_t> alim, rlim;
+        const double ta = trace ? now() : 0;
         const auto r = or_need.empty() ? ApplyOps(ops) : ApplyOps(ops, &alim, &rlim);
+        const double tb = trace ? now() : 0;
+        t_apply += tb - ta;
+        ++n_chunks;
         std::copy(r.begin(), r.end(), result.begin() + c0);
         if (!pnc_need.empty()) {
             // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
@@ -590,6 +666,8 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             auto enc = EncodePNCStatesBefore(pu, dp, dn);
             for (size_t j = 0; j < pnc_need.size(); ++j) snap[pnc_need[j]] = std::move(enc[j]);
         }
+        const double tc = trace ? now() : 0;
+        t_enc_p += tc - tb;
         if (!or_need.empty()) {
             std::vector<Guid> ou;
             std::vector<uint64_t> al, rl;
@@ -601,8 +679,10 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             auto enc = EncodeORSetStates(ou, &al, &rl);
             for (size_t j = 0; j < or_need.size(); ++j) snap[or_need[j]] = std::move(enc[j]);
         }
+        if (trace) t_enc_o += now() - tc;
         c0 = c1;
     }
+    if (trace) tt[2] = now();
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
     //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).
     const size_t s0 = submitted.size();
@@ -614,11 +694,17 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         }
         submitted.push_back(std::move(um));
     }
+    if (trace) tt[3] = now();
     ComputeDigests(ctx_, submitted, s0);
+    if (trace) tt[4] = now();
     for (size_t j = head; j < q.size(); ++j) {
         if (q[j].op != kOld) q[j].np.message = snap[(size_t)q[j].op];
         batch_queue_.emplace_back(std::move(q[j].np), q[j].tracked);
     }
+    if (trace)
+        std::fprintf(stderr, "SubmitClientUpdates(%zu ops): checks + batcher %.1f ms, %zu chunks: apply %.1f ms, PN-Counter snapshots %.1f ms, "
+                     "OR-Set snapshots %.1f ms (loop %.1f ms), messages %.1f ms, digests %.1f ms, queue %.1f ms\n",
+                     n, tt[1] - tt[0], n_chunks, t_apply, t_enc_p, t_enc_o, tt[2] - tt[1], tt[3] - tt[2], tt[4] - tt[3], now() - tt[4]);
     return result;
 }
 

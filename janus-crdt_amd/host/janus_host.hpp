@@ -159,6 +159,12 @@ class GpuStableStore {
     // the upload then snoops the dirty lines)
     void PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates, bool nontemporal = true);
     std::vector<uint64_t> ApplyPacked(SafeUpdateTracker* tracker = nullptr);
+    // What a C# caller without page-locked receive buffers does with the streamed apply (jg_apply_stream_*): copy
+    // the wave's byte[]s into a jg_host_alloc arena part by part (~part_msgs messages of whole UpdateMessages),
+    // handing each part to the library as soon as it is copied, so the copy of the next part overlaps the upload
+    // of this one.  Same results as ApplyCommitted.
+    std::vector<uint64_t> ApplyArenaStreamed(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker = nullptr,
+                                             size_t part_msgs = 65536);
 
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
     // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the

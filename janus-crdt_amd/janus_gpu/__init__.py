@@ -38,7 +38,7 @@ EXPORTS = [
     "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256",
     "jg_node_create", "jg_node_destroy", "jg_node_register", "jg_node_set_shard", "jg_shard_of", "jg_node_last_stats",
     "jg_tracker_create", "jg_tracker_destroy", "jg_tracker_add", "jg_tracker_size", "jg_tracker_contains",
-    "jg_apply_committed", "jg_apply_block",
+    "jg_apply_committed", "jg_apply_block", "jg_apply_stream_begin", "jg_apply_stream_append", "jg_apply_stream_end",
     "jg_comm_unique_id", "jg_comm_init", "jg_comm_destroy", "jg_pnc_exchange", "jg_orset_exchange", "jg_comm_last_stats",
     "jg_comm_init_host", "jg_exchange_plan", "jg_global_key",
 ]
@@ -127,6 +127,9 @@ _SIGS = {
     "jg_tracker_contains": ([_vp, _u64, _vp, _vp], C.c_int),
     "jg_apply_committed": ([_vp, _vp, _vp, _vp, C.POINTER(_u64), C.POINTER(_u64)], C.c_int),
     "jg_apply_block": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
+    "jg_apply_stream_begin": ([_vp, _vp, _u64, _u64], C.c_int),
+    "jg_apply_stream_append": ([_vp, _vp], C.c_int),
+    "jg_apply_stream_end": ([_vp, _vp, C.POINTER(_u64), C.POINTER(_u64)], C.c_int),
     "jg_comm_unique_id": ([_vp], C.c_int),
     "jg_comm_init": ([_vp, _u32, _u32, _vp, C.POINTER(_vp)], C.c_int),
     "jg_comm_init_host": ([_vp, _u32, _u32, _vp, _vp, C.POINTER(_vp)], C.c_int),
@@ -806,6 +809,33 @@ class Node:
                 e.completed = done[: nd.value].copy()
                 raise
         return done[: nd.value].copy(), (None if at.value == 2**64 - 1 else at.value), rc
+
+    def apply_stream(self, tracker: Tracker | None, parts, pinned=None, n_max=None, bytes_max=None):
+        """jg_apply_stream_begin / _append (one per part) / _end: parts = [(lo, hi, types, seqs, msgs)]; returns
+        (completed origins, stopped_at or None, code) like apply_committed over the concatenated parts."""
+        n_max = n_max or max(1, sum(len(p[4]) for p in parts))
+        bytes_max = bytes_max if bytes_max is not None else sum(len(m) for p in parts for m in p[4])
+        _check(load().jg_apply_stream_begin(self._h, tracker._h if tracker else None, n_max, bytes_max))
+        keeps = []
+        try:
+            for lo, hi, types, seqs, msgs in parts:
+                c, keep = self._commit(lo, hi, types, seqs, msgs, None, None, pinned)
+                keeps.append(keep)
+                _check(load().jg_apply_stream_append(self._h, C.byref(c)))
+            done = np.zeros(max(1, n_max), np.uint64)
+            nd, at = _u64(), _u64()
+            rc = load().jg_apply_stream_end(self._h, _ptr(done), C.byref(nd), C.byref(at))
+            if rc != JG_OK and at.value == 2**64 - 1:
+                try:
+                    _check(rc)
+                except JanusError as e:
+                    e.completed = done[: nd.value].copy()
+                    raise
+            return done[: nd.value].copy(), (None if at.value == 2**64 - 1 else at.value), rc
+        finally:
+            if pinned is not None:
+                for keep in keeps:
+                    keep[3].close()
 
     def apply_block(self, lo, hi, types, msgs=None, data=None, off=None):
         """jg_apply_block: returns (stopped_at or None, code)."""

@@ -62,6 +62,7 @@ def test_sharded_apply_covers_the_wave_once():
     ["--accounts", "100", "--ops", "200000", "--waves", "2", "--normal"],     # the paper's 100 accounts, N(n/2, n/6)
     ["--accounts", "5000", "--ops", "100000", "--waves", "2", "--rank", "1", "--world", "3"],  # one key-space shard
     ["--accounts", "200000", "--ops", "400000", "--waves", "2", "--direct"],  # payloads in page-locked memory, uploaded in place
+    ["--accounts", "200000", "--ops", "400000", "--waves", "2", "--arena-stream", "--part-msgs", "30000"],  # streamed parts (jg_apply_stream_*)
 ])
 def test_banking_replay_matches_oracle(args):
     """C5 parity (BankingWorload.cs ops through the node batchers): after every committed wave, every owned

@@ -126,7 +126,7 @@ def _wave(rng, m, uids, n_pnc, n_set, n, pcl, ocl, seq0, bad_at=None, extras=Tru
     return wave
 
 
-def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=False, block=False, shard=None, pinned=False):
+def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=False, block=False, shard=None, pinned=False, stream=0):
     rng = np.random.default_rng(seed)
     if chunk and monkeypatch:
         monkeypatch.setenv("JANUS_WAVE_CHUNK", str(chunk))
@@ -154,6 +154,10 @@ def _run(ctx, seed, n_pnc, n_set, waves, n, chunk=None, monkeypatch=None, bad=Fa
             if block:
                 cut, rc = node.apply_block(lo, hi, types, msgs)
                 done = []
+            elif stream:  # the wave handed over in `stream` parts of random sizes (jg_apply_stream_*)
+                cuts = sorted(set(rng.integers(0, len(wave) + 1, stream - 1).tolist()) | {0, len(wave)})
+                parts = [(lo[a:b], hi[a:b], types[a:b], seqs[a:b], msgs[a:b]) for a, b in zip(cuts, cuts[1:])]
+                done, cut, rc = node.apply_stream(tr, parts, pinned=ctx if pinned else None)
             else:
                 done, cut, rc = node.apply_committed(tr, lo, hi, types, seqs, msgs, pinned=ctx if pinned else None)
             assert cut == exp_cut, (cut, exp_cut)
@@ -489,5 +493,51 @@ def test_orset_commit_failure_still_reports_completions(ctx, monkeypatch):
         assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
     finally:
         monkeypatch.delenv("JANUS_TEST_ORSET_COMMIT_FAIL", raising=False)
+        for h in (node, tr, pnc, st):
+            h.close()
+
+
+@pytest.mark.parametrize("pinned,chunk,bad", [(False, None, False), (True, None, False), (True, 53, True), (False, 71, False)])
+def test_streamed_wave_matches_one_call(ctx, monkeypatch, pinned, chunk, bad):
+    """jg_apply_stream_begin / _append / _end (a wave handed over in parts): the same stores,
+    completions, cut and tracker as the oracle's loop over the whole wave — parts of random sizes (empty ones too),
+    from page-locked memory (uploaded in place, the device reading them after each append returns) or gathered,
+    with small chunks inside parts, and a rejected state in some part."""
+    if chunk:
+        _run(ctx, 21, 90, 30, 3, 1500, chunk=chunk, monkeypatch=monkeypatch, bad=bad, pinned=pinned, stream=5)
+    else:
+        _run(ctx, 23, 150, 50, 3, 3000, bad=bad, pinned=pinned, stream=7)
+
+
+def test_streamed_wave_rules(ctx):
+    """A part past the begin's bounds rejects the wave (nothing applied, stream closed); append / end without an
+    open stream and a second begin are refused; jg_apply_committed is refused while a stream is open."""
+    import ctypes as C
+    rng = np.random.default_rng(3)
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, 20, 5)
+    pcl = J.Cluster(rng, 20, R - 1, EB, stable=None)
+    lib = jg.load()
+    try:
+        wave = [(uids[k], 1, 0, pcl.message(k)) for k in rng.integers(0, 20, 50).tolist()]
+        lo, hi = [x[0][0] for x in wave], [x[0][1] for x in wave]
+        types, seqs, msgs = [x[1] for x in wave], [x[2] for x in wave], [x[3] for x in wave]
+        with pytest.raises(jg.JanusError):  # 50 messages into a stream declared for 10
+            node.apply_stream(tr, [(lo, hi, types, seqs, msgs)], n_max=10)
+        P, N = pnc.read_rows()
+        assert not P.any() and not N.any()  # nothing applied
+        assert lib.jg_apply_stream_append(node._h, None) == jg.JG_EINVAL
+        at, nd = jg._u64(), jg._u64()
+        assert lib.jg_apply_stream_end(node._h, None, C.byref(nd), C.byref(at)) == jg.JG_EINVAL
+        assert lib.jg_apply_stream_begin(node._h, None, 100, 1 << 20) == jg.JG_OK
+        assert lib.jg_apply_stream_begin(node._h, None, 100, 1 << 20) == jg.JG_EINVAL
+        with pytest.raises(jg.JanusError):
+            node.apply_committed(tr, lo, hi, types, seqs, msgs)
+        assert lib.jg_apply_stream_end(node._h, None, C.byref(nd), C.byref(at)) == jg.JG_OK  # an empty stream
+        done, cut, rc = node.apply_stream(tr, [(lo[:20], hi[:20], types[:20], seqs[:20], msgs[:20]), (lo[20:], hi[20:], types[20:], seqs[20:], msgs[20:])])
+        exp_done, exp_cut = m.apply(wave)
+        assert rc == jg.JG_OK and cut is None and list(done) == exp_done
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+    finally:
         for h in (node, tr, pnc, st):
             h.close()
