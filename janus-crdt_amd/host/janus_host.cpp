@@ -42,6 +42,7 @@ GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas,
 
 GpuStableStore::~GpuStableStore() {
     if (p_bytes_) jg_host_free(p_bytes_);
+    if (pin_buf_) jg_host_free(pin_buf_);
     if (node_) jg_node_destroy(node_);
     if (orset_) jg_orset_destroy(orset_);
     if (pnc_) jg_pnc_destroy(pnc_);
@@ -344,7 +345,13 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
         check(jg_host_alloc(ctx_, p_cap_, &p));
         p_bytes_ = static_cast<uint8_t*>(p);
     }
+    static const bool trace = std::getenv("JANUS_TRACE_APPLY") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double tb = trace ? now() : 0;
     check(jg_apply_stream_begin(node_, tracker ? tracker->handle() : nullptr, n, nb));
+    double t_copy = 0, t_append = 0;
+    size_t n_parts = 0;
+    const double t0 = trace ? now() : 0;
     std::vector<uint64_t> poff;
     // parts of whole UpdateMessages, ~part_msgs messages each: the caller's copy of part k + 1 (plain cached copies,
     // what a C# caller's parallel Span.CopyTo does) runs while part k uploads
@@ -352,6 +359,7 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
         size_t b1 = b0;
         while (b1 < blocks.size() && (b1 == b0 || block_off_[b1] - block_off_[b0] < part_msgs)) ++b1;
         const size_t i0 = block_off_[b0], i1 = block_off_[b1];
+        const double tc = trace ? now() : 0;
         parallel_ranges(pool(), i1 - i0, [&](size_t a, size_t e, int) {
             if (a >= e) return;
             a += i0, e += i0;
@@ -369,12 +377,18 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
         poff.resize(i1 - i0 + 1);
         for (size_t i = i0; i <= i1; ++i) poff[i - i0] = p_off_[i] - p_off_[i0];
         const jg_commit part{i1 - i0, w_uid_.data() + i0, w_type_.data() + i0, w_seq_.data() + i0, poff.data(), p_bytes_ + p_off_[i0], nullptr, nullptr};
+        const double ta = trace ? now() : 0;
         const int rc = jg_apply_stream_append(node_, &part);
         if (rc != JG_OK) throw EngineError(rc, last_error());  // the library closed the stream: nothing applied
+        if (trace) t_copy += ta - tc, t_append += now() - ta, ++n_parts;
         b0 = b1;
     }
+    const double te = trace ? now() : 0;
     uint64_t n_done = 0, at = UINT64_MAX;
     const int rc = jg_apply_stream_end(node_, w_done_.data(), &n_done, &at);
+    if (trace)
+        std::fprintf(stderr, "ApplyArenaStreamed: begin %.2f ms, %zu parts: copies %.2f ms, appends %.2f ms, end %.2f ms\n", t0 - tb, n_parts, t_copy,
+                     t_append, now() - te);
     const std::string why = rc == JG_OK ? std::string() : last_error();
     jg_node_last_stats(node_, &stats_);
     std::vector<uint64_t> done(w_done_.begin(), w_done_.begin() + (ptrdiff_t)n_done);
@@ -406,7 +420,8 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
     return done;
 }
 
-std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim) {
+std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
+                                              const KeyRef* const* refs) {
     materialize_names();
     std::vector<uint8_t> result(ops.size(), 1);
     std::vector<uint32_t> pkey, pcol;
@@ -416,17 +431,24 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
     std::vector<uint8_t> oop;
     std::vector<uint64_t> olo, ohi;
     std::vector<size_t> oidx;
-    for (size_t i = 0; i < ops.size(); ++i) {  // validate everything first: no partial application
-        const auto it = uids_.find(ops[i].uid);
-        if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
-        const KeyRef* kr = &it->second;
-        const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
-        if (ops[i].opId < 1 || ops[i].opId > hi)
-            throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+    std::vector<const KeyRef*> found;
+    if (!refs) {
+        found.resize(ops.size());
+        for (size_t i = 0; i < ops.size(); ++i) {  // validate everything first: no partial application
+            const auto it = uids_.find(ops[i].uid);
+            if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
+            const KeyRef* kr = &it->second;
+            const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
+            if (ops[i].opId < 1 || ops[i].opId > hi)
+                throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+            found[i] = kr;
+        }
+        refs = found.data();
     }
+    pkey.reserve(ops.size()), pcol.reserve(ops.size()), pdelta.reserve(ops.size()), pisn.reserve(ops.size());
     for (size_t i = 0; i < ops.size(); ++i) {
         const ClientOp& op = ops[i];
-        const KeyRef& kr = uids_.find(op.uid)->second;
+        const KeyRef& kr = *refs[i];
         if (kr.type == CrdtType::PNCounter) {
             pkey.push_back(kr.idx);
             pcol.push_back(0);
@@ -505,6 +527,60 @@ std::vector<std::string> GpuStableStore::EncodePNCStates(const std::vector<Guid>
     return out;
 }
 
+uint8_t* GpuStableStore::pinned_buf(size_t bytes) {
+    if (pin_cap_ < bytes) {
+        if (pin_buf_) check(jg_host_free(pin_buf_));
+        pin_buf_ = nullptr;
+        void* p = nullptr;
+        pin_cap_ = bytes + bytes / 4 + 4096;
+        check(jg_host_alloc(ctx_, pin_cap_, &p));
+        pin_buf_ = static_cast<uint8_t*>(p);
+    }
+    return pin_buf_;
+}
+
+void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
+                                         const std::vector<size_t>& at, std::vector<std::string>& out) {
+    flush_registrations();
+    const size_t n = rows.size();
+    std::vector<uint64_t> off(n + 1, 0);
+    // one call into a page-locked buffer sized from the last call (a second only if the states outgrew it)
+    size_t guess = std::max<size_t>(pin_cap_, (size_t)(n * (last_pnc_bytes_ + 8)) + 4096);
+    uint8_t* buf = pinned_buf(guess);
+    int rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_);
+    if (rc == JG_ESTATE && off[n] > pin_cap_) {
+        buf = pinned_buf(off[n]);
+        rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_);
+    }
+    check(rc);
+    if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
+    parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
+        for (size_t i = b; i < e; ++i) out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+    });
+}
+
+// ComputeDigests of msgs[first..] with the payloads gathered into page-locked staging by the workers.
+void GpuStableStore::DigestsPinned(std::vector<UpdateMessage>& msgs, size_t first) {
+    if (first >= msgs.size()) return;
+    const size_t nu = msgs.size() - first;
+    std::vector<uint64_t> upd(nu + 1, 0);
+    for (size_t u = 0; u < nu; ++u) upd[u + 1] = upd[u] + msgs[first + u].update.size();
+    const size_t nm = upd[nu];
+    std::vector<uint64_t> off(nm + 1, 0);
+    for (size_t u = 0, i = 0; u < nu; ++u)
+        for (const auto& np : msgs[first + u].update) off[i + 1] = off[i] + np.message.size(), ++i;
+    uint8_t* buf = pinned_buf(off[nm] + 64);
+    parallel_ranges(pool(), nu, [&](size_t b, size_t e, int) {
+        for (size_t u = b; u < e; ++u) {
+            size_t i = upd[u];
+            for (const auto& np : msgs[first + u].update) std::memcpy(buf + off[i], np.message.data(), np.message.size()), ++i;
+        }
+    });
+    std::vector<uint8_t> dig(32 * nu);
+    check(jg_update_digests(ctx_, nm, off.data(), buf, nullptr, nu, upd.data(), nullptr, dig.data()));
+    for (size_t u = 0; u < nu; ++u) std::memcpy(msgs[first + u].digest.data(), dig.data() + 32 * u, 32);
+}
+
 std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector<Guid>& uids, const std::vector<int64_t>& dp,
                                                                const std::vector<int64_t>& dn) {
     flush_registrations();
@@ -532,18 +608,19 @@ std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Gui
     std::vector<uint64_t> off(n + 1, 0);
     const uint64_t* al = add_lim ? add_lim->data() : nullptr;
     const uint64_t* rl = rem_lim ? rem_lim->data() : nullptr;
-    // ORSetMsg.Encode() on the device (jg_orset_encode_json) into a buffer kept across calls: one call unless the
-    // states outgrow it
-    if (enc_buf_.size() < 4096) enc_buf_.resize(4096);
-    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), reinterpret_cast<uint8_t*>(enc_buf_.data()), enc_buf_.size());
-    if (rc == JG_ESTATE && off[n] > enc_buf_.size()) {
-        enc_buf_.resize(off[n] + off[n] / 2);
-        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), reinterpret_cast<uint8_t*>(enc_buf_.data()), enc_buf_.size());
+    // ORSetMsg.Encode() on the device (jg_orset_encode_json) into a page-locked buffer kept across calls: one call
+    // unless the states outgrow it
+    uint8_t* buf = pinned_buf(4096);
+    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_);
+    if (rc == JG_ESTATE && off[n] > pin_cap_) {
+        buf = pinned_buf(off[n]);
+        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_);
     }
     check(rc);
-    std::vector<std::string> out;
-    out.reserve(n);
-    for (size_t i = 0; i < n; ++i) out.emplace_back(enc_buf_, off[i], off[i + 1] - off[i]);
+    std::vector<std::string> out(n);
+    parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
+        for (size_t i = b; i < e; ++i) out[i].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+    });
     return out;
 }
 
@@ -556,13 +633,16 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     double tt[6] = {trace ? now() : 0};
     double t_apply = 0, t_enc_p = 0, t_enc_o = 0;
     size_t n_chunks = 0;
-    for (const ClientUpdate& u : ups) {  // the wrappers' checks, before anything is applied or queued
+    std::vector<const KeyRef*> kref(n);
+    for (size_t i = 0; i < n; ++i) {  // the wrappers' checks, before anything is applied or queued
+        const ClientUpdate& u = ups[i];
         const auto it = uids_.find(u.op.uid);
         if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
         const KeyRef* kr = &it->second;
         const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
         if (u.op.opId < 1 || u.op.opId > hi)
             throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+        kref[i] = kr;
     }
     // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
     //    q entries: message, op index (kOld: queued by an earlier call), and whether SafeCRDT.Update
@@ -576,6 +656,9 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     struct Flush { std::vector<QE> msgs; };
     std::vector<Flush> flushes;
     size_t head = 0;  // q[head..] is the live queue
+    q.reserve(q.size() + n);
+    std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared` (first appearance), per flush
+    pos.reserve(2 * (size_t)std::max(clientBatchSize, 1));
     for (size_t i = 0; i < n; ++i) {
         NetworkProtocol np;
         np.uid = ups[i].op.uid;
@@ -586,7 +669,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         q.push_back(QE{std::move(np), (int64_t)i, tracked});
         if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
             std::vector<QE> safe, appeared;
-            std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared` (first appearance)
+            pos.clear();
             while (head < q.size()) {
                 QE e = std::move(q[head++]);                          // TryDequeue first ...
                 if (!((int)safe.size() < clientBatchSize)) break;     // ... so this one is lost (:175)
@@ -613,74 +696,94 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             if (e.op != kOld) need[(size_t)e.op] = 1;
     for (size_t j = head; j < q.size(); ++j)
         if (q[j].op != kOld) need[(size_t)q[j].op] = 1;
-    // 3. Apply the ops in chunks, encode the needed snapshots after each chunk (on the device).  A PN-Counter
-    //    snapshot is the row rewound by the amounts the chunk's later ops on that key added to the own column
+    // 3. Apply the ops in rounds, encode the needed snapshots after each round (on the device).  A PN-Counter
+    //    snapshot is the row rewound by the amounts the batch's later ops on that key added to the own column
     //    (jg_pnc_encode_json_before); an OR-Set snapshot is its set's records below the ord limits the apply
-    //    reported for its op (jg_orset_apply_ops_ords + jg_orset_encode_json).  A chunk ends only before a Clear
-    //    of an OR-Set key with a snapshot needed earlier in the chunk (the Clear drops the records it holds).
+    //    reported for its op (jg_orset_apply_ops_ords + jg_orset_encode_json).  Only a Clear of an OR-Set key with a
+    //    snapshot needed earlier in the round forces a new round, and only for that key: sets are independent, so an
+    //    op's round is the number of such Clears of its own set before it (per-set order kept), and every PN-Counter
+    //    op runs in round 0.
     std::vector<uint8_t> result(n, 1);
     std::vector<std::string> snap(n);
-    size_t c0 = 0;
-    while (c0 < n) {
-        std::unordered_set<Guid, GuidHash> or_needed;  // OR-Set uids with a snapshot needed in this chunk
-        std::vector<size_t> pnc_need, or_need;         // needed ops, in op order
-        size_t c1 = c0;
-        for (; c1 < n; ++c1) {
-            const bool is_pnc = uids_.find(ups[c1].op.uid)->second.type == CrdtType::PNCounter;
-            if (!is_pnc && ups[c1].op.opId == 3 && c1 > c0 && or_needed.count(ups[c1].op.uid)) break;
-            if (need[c1]) {
-                if (is_pnc) pnc_need.push_back(c1);
-                else or_need.push_back(c1), or_needed.insert(ups[c1].op.uid);
-            }
+    std::vector<uint32_t> round(n, 0);
+    uint32_t n_rounds = 1;
+    {
+        std::unordered_map<uint32_t, std::pair<uint32_t, bool>> st;  // OR-Set set -> (its round, a snapshot needed in it)
+        for (size_t i = 0; i < n; ++i) {
+            if (kref[i]->type == CrdtType::PNCounter) continue;
+            auto& e = st[kref[i]->idx];
+            if (ups[i].op.opId == 3 && e.second) ++e.first, e.second = false;
+            round[i] = e.first;
+            if (need[i]) e.second = true;
+            n_rounds = std::max(n_rounds, e.first + 1);
         }
+    }
+    for (uint32_t rd = 0; rd < n_rounds; ++rd) {
+        std::vector<size_t> idx;  // this round's ops, in op order
+        for (size_t i = 0; i < n; ++i)
+            if (round[i] == rd) idx.push_back(i);
+        if (idx.empty()) continue;
         std::vector<ClientOp> ops;
-        ops.reserve(c1 - c0);
-        for (size_t i = c0; i < c1; ++i) ops.push_back(ups[i].op);
+        std::vector<const KeyRef*> rr;
+        ops.reserve(idx.size());
+        rr.reserve(idx.size());
+        bool or_snap = false;
+        for (size_t i : idx) {
+            ops.push_back(ups[i].op);
+            rr.push_back(kref[i]);
+            or_snap |= need[i] && kref[i]->type == CrdtType::ORSet;
+        }
         std::vector<uint64_t> alim, rlim;
         const double ta = trace ? now() : 0;
-        const auto r = or_need.empty() ? ApplyOps(ops) : ApplyOps(ops, &alim, &rlim);
+        const auto r = ApplyOps(ops, or_snap ? &alim : nullptr, or_snap ? &rlim : nullptr, rr.data());
         const double tb = trace ? now() : 0;
         t_apply += tb - ta;
         ++n_chunks;
-        std::copy(r.begin(), r.end(), result.begin() + c0);
+        for (size_t j = 0; j < idx.size(); ++j) result[idx[j]] = r[j];
+        std::vector<size_t> pnc_need, or_need;  // positions in idx
+        for (size_t j = 0; j < idx.size(); ++j)
+            if (need[idx[j]]) (kref[idx[j]]->type == CrdtType::PNCounter ? pnc_need : or_need).push_back(j);
         if (!pnc_need.empty()) {
             // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
-            // cells: walk the chunk backwards
-            std::unordered_map<Guid, std::pair<uint64_t, uint64_t>, GuidHash> after;
+            // cells: walk the round backwards, per row (a row-indexed array, its touched entries reset after)
+            if (pnc_after_.size() < max_keys_) pnc_after_.assign(max_keys_, {0, 0});
             std::vector<int64_t> dp(pnc_need.size()), dn(pnc_need.size());
-            std::vector<Guid> pu(pnc_need.size());
+            std::vector<uint32_t> prow(pnc_need.size());
+            std::vector<size_t> at(pnc_need.size());
             size_t w = pnc_need.size();
-            for (size_t i = c1; i-- > c0;) {
+            for (size_t j = idx.size(); j-- > 0;) {
+                const size_t i = idx[j];
+                if (kref[i]->type != CrdtType::PNCounter) continue;
                 const ClientOp& op = ups[i].op;
-                if (uids_.find(op.uid)->second.type != CrdtType::PNCounter) continue;
-                auto& a = after[op.uid];
-                if (w && pnc_need[w - 1] == i) {
+                auto& a = pnc_after_[kref[i]->idx];
+                if (w && pnc_need[w - 1] == j) {
                     --w;
                     dp[w] = (int64_t)a.first;
                     dn[w] = (int64_t)a.second;
-                    pu[w] = op.uid;
+                    prow[w] = kref[i]->idx;
+                    at[w] = i;
                 }
                 const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
                 (op.opId == 2 ? a.second : a.first) += amt;
             }
-            auto enc = EncodePNCStatesBefore(pu, dp, dn);
-            for (size_t j = 0; j < pnc_need.size(); ++j) snap[pnc_need[j]] = std::move(enc[j]);
+            for (size_t i : idx)
+                if (kref[i]->type == CrdtType::PNCounter) pnc_after_[kref[i]->idx] = {0, 0};
+            EncodePNCRowsBefore(prow, dp, dn, at, snap);
         }
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;
         if (!or_need.empty()) {
             std::vector<Guid> ou;
             std::vector<uint64_t> al, rl;
-            for (size_t i : or_need) {
-                ou.push_back(ups[i].op.uid);
-                al.push_back(alim[i - c0]);
-                rl.push_back(rlim[i - c0]);
+            for (size_t j : or_need) {
+                ou.push_back(ups[idx[j]].op.uid);
+                al.push_back(alim[j]);
+                rl.push_back(rlim[j]);
             }
             auto enc = EncodeORSetStates(ou, &al, &rl);
-            for (size_t j = 0; j < or_need.size(); ++j) snap[or_need[j]] = std::move(enc[j]);
+            for (size_t k = 0; k < or_need.size(); ++k) snap[idx[or_need[k]]] = std::move(enc[k]);
         }
         if (trace) t_enc_o += now() - tc;
-        c0 = c1;
     }
     if (trace) tt[2] = now();
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
@@ -689,20 +792,20 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     for (Flush& f : flushes) {
         UpdateMessage um;
         for (auto& e : f.msgs) {
-            if (e.op != kOld) e.np.message = snap[(size_t)e.op];
+            if (e.op != kOld) e.np.message = std::move(snap[(size_t)e.op]);  // each snapshot goes to one message
             um.update.push_back(std::move(e.np));
         }
         submitted.push_back(std::move(um));
     }
     if (trace) tt[3] = now();
-    ComputeDigests(ctx_, submitted, s0);
+    DigestsPinned(submitted, s0);
     if (trace) tt[4] = now();
     for (size_t j = head; j < q.size(); ++j) {
-        if (q[j].op != kOld) q[j].np.message = snap[(size_t)q[j].op];
+        if (q[j].op != kOld) q[j].np.message = std::move(snap[(size_t)q[j].op]);
         batch_queue_.emplace_back(std::move(q[j].np), q[j].tracked);
     }
     if (trace)
-        std::fprintf(stderr, "SubmitClientUpdates(%zu ops): checks + batcher %.1f ms, %zu chunks: apply %.1f ms, PN-Counter snapshots %.1f ms, "
+        std::fprintf(stderr, "SubmitClientUpdates(%zu ops): checks + batcher %.1f ms, %zu rounds: apply %.1f ms, PN-Counter snapshots %.1f ms, "
                      "OR-Set snapshots %.1f ms (loop %.1f ms), messages %.1f ms, digests %.1f ms, queue %.1f ms\n",
                      n, tt[1] - tt[0], n_chunks, t_apply, t_enc_p, t_enc_o, tt[2] - tt[1], tt[3] - tt[2], tt[4] - tt[3], now() - tt[4]);
     return result;

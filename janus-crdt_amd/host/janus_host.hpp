@@ -179,7 +179,10 @@ class GpuStableStore {
     // wrappers' InvalidOperationException) before anything is applied.  A PNC op writes this copy's
     // own replica column (column 0, registered by CreateSafeCRDT).
     // add_lim / rem_lim (optional): per op, the ord limits of its OR-Set's snapshot right after it (jg_orset_apply_ops_ords)
-    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim = nullptr, std::vector<uint64_t>* rem_lim = nullptr);
+    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim = nullptr, std::vector<uint64_t>* rem_lim = nullptr)
+    {
+        return ApplyOps(ops, add_lim, rem_lim, nullptr);
+    }
 
     // SafeCRDT.Update over a batch of client updates, on this store as the node's PROSPECTIVE copy
     // (SafeCRDT.cs:39-62) followed by the client batcher SafeCRDTManager.ActualPropagateSyncMsg
@@ -237,6 +240,19 @@ class GpuStableStore {
 
   private:
     struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id (queries, ops)
+    // ApplyOps with the ops' keys already resolved and validated (refs[i] for ops[i]; NULL: look them up)
+    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
+                                  const KeyRef* const* refs);
+    // PN-Counter snapshots of rows rewound by (dp, dn) into out[at[i]] (jg_pnc_encode_json_before, one call into
+    // page-locked memory, the strings built by the workers)
+    void EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
+                             const std::vector<size_t>& at, std::vector<std::string>& out);
+    void DigestsPinned(std::vector<UpdateMessage>& msgs, size_t first);  // ComputeDigests through page-locked staging
+    uint8_t* pinned_buf(size_t bytes);  // a page-locked buffer of at least `bytes`, kept across calls
+    uint8_t* pin_buf_ = nullptr;
+    size_t pin_cap_ = 0;
+    double last_pnc_bytes_ = 400;
+    std::vector<std::pair<uint64_t, uint64_t>> pnc_after_;  // SubmitClientUpdates: per row, the amounts of later ops
     std::unordered_map<Guid, KeyRef, GuidHash> uids_;
     struct SetKey {
         std::unordered_map<std::string, uint32_t> elems;  // live interning (reset by Clear), indexed lazily:
@@ -293,7 +309,6 @@ class GpuStableStore {
     uint64_t last_msgs_ = 0;
     std::unique_ptr<jg::WorkerPool> pool_;
     std::vector<SetKey> sets_;
-    std::string enc_buf_;  // EncodeORSetStates' output, kept across calls
     std::vector<std::pair<NetworkProtocol, bool>> batch_queue_;  // clientUpdateBuffer (SafeCRDTManager.cs:167): message, tracked
     double last_submit_ms_ = 0;                 // lastSumittedTime
     uint64_t next_seq_ = 1;                     // message identity for the safe-update tracker
