@@ -614,6 +614,32 @@ def bench_c1(local):
     return json.loads(out.stdout.strip().splitlines()[-1]) if out.stdout.strip() else {"error": out.stderr[-500:]}
 
 
+def bench_submit(local, workload):
+    """The producer path of one node (host/bench_submit.cpp): SafeCRDT.Update
+    over a call of client ops (C5 banking ops on 1M accounts, or ORSetWorkload ops on 2000 sets), every shipped
+    snapshot encoded on the device, ActualPropagateSyncMsg's batches and their digests — against the oracle's
+    SafeCRDT.Update + ActualPropagateSyncMsg + update_digest on a sample, whose batches must equal the GPU's byte for
+    byte (parity).  Roofline: the host link — every snapshot byte comes back to the host once and goes out again
+    for its UpdateMessage's digest."""
+    import subprocess
+    args = (["--workload", "pnc", "--keys", "1000000", "--ops", "1000000", "--cpu-ops", "50000", "--waves", "3"] if workload == "pnc" else
+            ["--workload", "orset", "--keys", "2000", "--ops", "200000", "--cpu-ops", "20000", "--waves", "3"])
+    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / "bench_submit")] + args + ["--device", str(local)],
+                         capture_output=True, text=True, timeout=240)
+    if not out.stdout.strip():
+        return {"error": out.stderr[-500:]}
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    if out.returncode != 0:
+        res["error"] = f"parity failure: {res.get('parity_failure')}"
+        return res
+    link = 2.0 * res["submitted_msgs_per_wave"] * res["payload_bytes_per_msg"]
+    ach = link / (res["ms_per_wave"] / 1e3) / 1e9
+    res["roofline"] = {"bound": "pcie", "achieved": ach, "peak": PCIE_PEAK_GBS, "unit": "GB/s", "frac": ach / PCIE_PEAK_GBS, "traffic": None,
+                       "measured_link": {"GBps": PCIE_MEASURED_GBS, "frac": ach / PCIE_MEASURED_GBS},
+                       "scope": "snapshot bytes down (encode) + up again (digests) per call / call time"}
+    return res
+
+
 DIGEST_MSGS, DIGEST_PER_UPDATE = 1_000_000, 1000  # one C5-sized wave, clientBatchSize-sized UpdateMessages
 DIGEST_PIPE = 8  # waves per pipelined call
 # VALU instructions per 64-byte block of the k_sha_msgs loop (compress + window shift, gfx950 ISA count of
@@ -816,7 +842,7 @@ def compact_leg(name, leg):
     if "error" in leg:
         return {"error": str(leg["error"])[:200]}
     out = {}
-    for k in ("ms_per_step", "ms_per_wave", "value", "unit", "msgs_per_s", "rows_per_s", "client_ops_per_s", "event_ms",
+    for k in ("ms_per_step", "ms_per_wave", "value", "unit", "msgs_per_s", "ops_per_s", "rows_per_s", "client_ops_per_s", "event_ms",
               "cold_wave_ms", "untimed_pack_ms_per_wave", "scaling"):
         if leg.get(k) is not None:
             out[k] = _r(leg[k])
@@ -835,7 +861,9 @@ def compact_leg(name, leg):
         out["roofline_valu"] = _roof(leg["roofline_valu"])
     cb = leg.get("cpu_baseline")
     if isinstance(cb, dict):
-        out["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("msgs_per_s", "cores", "kind") if cb.get(k) is not None}
+        out["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("msgs_per_s", "ops_per_s", "cores", "kind") if cb.get(k) is not None}
+    if "parity_vs_oracle" in leg:
+        out["parity_vs_oracle"] = leg["parity_vs_oracle"]
     for sub in ("from_pinned", "caller_arena", "pipelined", "first_level", "merge"):
         s = leg.get(sub)
         if isinstance(s, dict):
@@ -873,7 +901,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest", "json"], default="all")
+    ap.add_argument("--workload", choices=["all", "pnc", "orset", "pnc-orset", "exchange", "digest", "json", "producer"], default="all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pnc-shape", choices=["auto"] + sorted(PNC_SHAPES), default="auto",
                     help="per-GPU PN-Counter shard: c2 = BASELINE configs[1], c4 = 1/8 of configs[3]; "
@@ -938,6 +966,8 @@ def main():
     apply_orset = guarded(bench_apply_orset, sync, rank, world, local) if args.workload == "all" else None
     apply_c1 = guarded(bench_c1, local) if args.workload == "all" and world == 1 else None
     apply_direct = guarded(bench_apply_direct, local) if args.workload == "all" and world == 1 else None
+    producer_pnc = guarded(bench_submit, local, "pnc") if args.workload in ("all", "producer") and world == 1 else None
+    producer_orset = guarded(bench_submit, local, "orset") if args.workload in ("all", "producer") and world == 1 else None
     for leg in (apply_loop, apply_orset, apply_c1, apply_direct):
         if leg is not None and "error" not in leg and "scaling" not in leg:
             leg["roofline"] = guarded(apply_roofline, leg)
@@ -960,7 +990,7 @@ def main():
     line = headline(args, world, res, cpu)
     legs = {"orset": line.pop("orset", None), "apply_loop": apply_loop, "apply_loop_orset": apply_orset,
             "apply_loop_c1": apply_c1, "apply_loop_direct": apply_direct, "update_digests": res.get("digest"),
-            "json_apply": res.get("json"), "exchange": res.get("exchange")}
+            "json_apply": res.get("json"), "exchange": res.get("exchange"), "producer_pnc": producer_pnc, "producer_orset": producer_orset}
     legs = {k: v for k, v in legs.items() if v is not None}
     # every leg in full (per-kernel dicts, nested rooflines, PMC summaries) on stderr and, if asked, in a file;
     # the LAST stdout line is the compact one the driver parses (<= LINE_CAP bytes)

@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
     uint64_t accounts = 1000000, ops = 1000000, cpu_msgs = 100000;
     int waves = 3, nodes = 4, device = 0, batch = 1000, threads_per_node = 3;  // 12 client threads (config example)
     uint32_t rank = 0, world = 1;
-    bool normal = false, parity = false, direct = false, arena = false, stream = false;
+    bool normal = false, parity = false, direct = false, arena = false, stream = false, stream_cached = false;
     size_t part_msgs = 65536;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--accounts") && i + 1 < argc) accounts = std::strtoull(argv[++i], nullptr, 10);
@@ -61,6 +61,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--direct")) direct = true;  // the wave received into page-locked memory
         else if (!std::strcmp(argv[i], "--arena")) direct = arena = true;  // the caller copies the wave into page-locked memory (timed)
         else if (!std::strcmp(argv[i], "--arena-stream")) stream = true;  // the same copy part by part, overlapped (jg_apply_stream_*)
+        else if (!std::strcmp(argv[i], "--arena-stream-cached")) stream = true, stream_cached = true;  // ... with plain cached copies
         else if (!std::strcmp(argv[i], "--part-msgs") && i + 1 < argc) part_msgs = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--rank") && i + 1 < argc) rank = (uint32_t)std::atoi(argv[++i]);
@@ -212,7 +213,7 @@ int main(int argc, char** argv) {
         if (direct) gpu.PackCommitted(wave, !arena);
         const double t0 = arena ? tp : now_s();
         if (direct && w > 0) pack_s += now_s() - tp;
-        const std::vector<uint64_t> done = stream ? gpu.ApplyArenaStreamed(wave, &tracker_g, part_msgs)
+        const std::vector<uint64_t> done = stream ? gpu.ApplyArenaStreamed(wave, &tracker_g, part_msgs, !stream_cached)
                                            : direct ? gpu.ApplyPacked(&tracker_g) : gpu.ApplyCommitted(wave, &tracker_g);
         const double t1 = now_s();
         if (w == 0) {

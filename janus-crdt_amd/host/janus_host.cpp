@@ -126,6 +126,9 @@ SafeUpdateTracker::~SafeUpdateTracker() { jg_tracker_destroy(t_); }
 void SafeUpdateTracker::add(uint64_t seq, uint64_t origin) {
     if (jg_tracker_add(t_, 1, &seq, &origin) != JG_OK) throw EngineError(JG_EINVAL, last_error());
 }
+void SafeUpdateTracker::add_many(size_t n, const uint64_t* seq, const uint64_t* origin) {
+    if (n && jg_tracker_add(t_, n, seq, origin) != JG_OK) throw EngineError(JG_EINVAL, last_error());
+}
 bool SafeUpdateTracker::contains(uint64_t seq) const {
     uint8_t r = 0;
     if (jg_tracker_contains(t_, 1, &seq, &r) != JG_OK) throw EngineError(JG_EINVAL, last_error());
@@ -321,7 +324,7 @@ std::vector<uint64_t> GpuStableStore::ApplyPacked(SafeUpdateTracker* tracker) {
 }
 
 std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker,
-                                                         size_t part_msgs) {
+                                                         size_t part_msgs, bool nontemporal) {
     flush_registrations();
     flush_names();
     std::vector<const UpdateMessage*> blocks;
@@ -363,6 +366,7 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
         parallel_ranges(pool(), i1 - i0, [&](size_t a, size_t e, int) {
             if (a >= e) return;
             a += i0, e += i0;
+            jg::LineStream out(reinterpret_cast<char*>(p_bytes_), p_off_[a]);
             size_t b = (size_t)(std::upper_bound(block_off_.begin(), block_off_.end(), a) - block_off_.begin()) - 1;
             for (size_t i = a; i < e; ++b) {
                 const NetworkProtocol* u = blocks[b]->update.data() + (i - block_off_[b]);
@@ -370,9 +374,11 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
                     w_uid_[i] = jg_guid{u->uid.lo, u->uid.hi};
                     w_type_[i] = u->syncMsgType == NetworkProtocol::CRDTMsg ? 1 : 0;
                     w_seq_[i] = u->seq;
-                    std::memcpy(p_bytes_ + p_off_[i], u->message.data(), u->message.size());
+                    if (nontemporal) out.put(reinterpret_cast<const char*>(u->message.data()), u->message.size());
+                    else std::memcpy(p_bytes_ + p_off_[i], u->message.data(), u->message.size());
                 }
             }
+            if (nontemporal) out.finish();
         });
         poff.resize(i1 - i0 + 1);
         for (size_t i = i0; i <= i1; ++i) poff[i - i0] = p_off_[i] - p_off_[i0];
@@ -633,16 +639,25 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     double tt[6] = {trace ? now() : 0};
     double t_apply = 0, t_enc_p = 0, t_enc_o = 0;
     size_t n_chunks = 0;
+    // the wrappers' checks, before anything is applied or queued: every op's key resolved by the workers (read-only
+    // lookups), the first failing op then raises its error as the serial loop would
     std::vector<const KeyRef*> kref(n);
-    for (size_t i = 0; i < n; ++i) {  // the wrappers' checks, before anything is applied or queued
-        const ClientUpdate& u = ups[i];
-        const auto it = uids_.find(u.op.uid);
-        if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
-        const KeyRef* kr = &it->second;
-        const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
-        if (u.op.opId < 1 || u.op.opId > hi)
-            throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
-        kref[i] = kr;
+    std::vector<size_t> first_bad(pool().size(), n);
+    parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+        for (size_t i = b; i < e; ++i) {
+            const auto it = uids_.find(ups[i].op.uid);
+            const KeyRef* kr = it == uids_.end() ? nullptr : &it->second;
+            kref[i] = kr;
+            if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
+                first_bad[t] = i;
+                return;
+            }
+        }
+    });
+    const size_t bad = *std::min_element(first_bad.begin(), first_bad.end());
+    if (bad < n) {
+        if (!kref[bad]) throw EngineError(JG_EINVAL, "unknown CRDT uid");
+        throw EngineError(JG_EINVAL, kref[bad]->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
     }
     // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
     //    q entries: message, op index (kOld: queued by an earlier call), and whether SafeCRDT.Update
@@ -657,6 +672,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<Flush> flushes;
     size_t head = 0;  // q[head..] is the live queue
     q.reserve(q.size() + n);
+    std::vector<uint64_t> t_seq, t_org;  // SafeCRDT.Update's TryAdds, handed to the tracker in one call after the loop
     std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared` (first appearance), per flush
     pos.reserve(2 * (size_t)std::max(clientBatchSize, 1));
     for (size_t i = 0; i < n; ++i) {
@@ -665,7 +681,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         np.syncMsgType = NetworkProtocol::CRDTMsg;
         np.seq = next_seq_++;
         const bool tracked = ups[i].isSafe && ups[i].origin != 0;  // SafeCRDT.cs:55-56
-        if (tracked) tracker.add(np.seq, ups[i].origin);
+        if (tracked) t_seq.push_back(np.seq), t_org.push_back(ups[i].origin);
         q.push_back(QE{std::move(np), (int64_t)i, tracked});
         if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
             std::vector<QE> safe, appeared;
@@ -688,6 +704,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             }
         }
     }
+    tracker.add_many(t_seq.size(), t_seq.data(), t_org.data());
     if (trace) tt[1] = now();
     // 2. Which ops' snapshots are needed: those submitted now or still queued.
     std::vector<uint8_t> need(n, 0);

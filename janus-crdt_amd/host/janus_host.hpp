@@ -91,6 +91,7 @@ class SafeUpdateTracker {
     SafeUpdateTracker(const SafeUpdateTracker&) = delete;
     SafeUpdateTracker& operator=(const SafeUpdateTracker&) = delete;
     void add(uint64_t seq, uint64_t origin);  // TryAdd (SafeCRDT.cs:55-56)
+    void add_many(size_t n, const uint64_t* seq, const uint64_t* origin);  // n TryAdds in one call
     bool contains(uint64_t seq) const;         // ContainsKey
     size_t size() const;
     jg_tracker* handle() const { return t_; }
@@ -163,8 +164,10 @@ class GpuStableStore {
     // the wave's byte[]s into a jg_host_alloc arena part by part (~part_msgs messages of whole UpdateMessages),
     // handing each part to the library as soon as it is copied, so the copy of the next part overlaps the upload
     // of this one.  Same results as ApplyCommitted.
+    // nontemporal: the copy with non-temporal line stores (C#: Avx.StoreAlignedNonTemporal over the byte[]s, INTEGRATION.md
+    // §3), so the upload reading part k finds no dirty lines of it in the CPU caches to snoop; false: plain cached copies.
     std::vector<uint64_t> ApplyArenaStreamed(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker = nullptr,
-                                             size_t part_msgs = 65536);
+                                             size_t part_msgs = 65536, bool nontemporal = true);
 
     // ConnectionManager.ReceivedBlock -> ReplicationManager.ReceivedUpdateSyncMsg (BFT-CRDT/Network/
     // DAGConnectionManager.cs:40-50, MergeSharp/MergeSharp/ReplicationManager.cs:290-344): the

@@ -9,6 +9,9 @@ ROOT = Path(__file__).resolve().parent.parent
 REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config", "roofline",
             "cpu_baseline", "higher_is_better", "scaling", "vs_baseline", "data")
 LEGS = ("orset", "apply_loop", "apply_loop_orset", "apply_loop_c1", "apply_loop_direct", "update_digests", "json_apply", "exchange")
+PRODUCER = {"workload": "producer path ...", "waves": 3, "ops_per_s": 2.5e6, "ms_per_wave": 400.0, "submitted_msgs_per_wave": 999874.0,
+            "payload_bytes_per_msg": 366.7, "parity_vs_oracle": True, "roofline": {"bound": "pcie", "achieved": 1.8, "peak": 63.0, "unit": "GB/s",
+            "frac": 0.03, "traffic": None, "measured_link": {"GBps": 56.5, "frac": 0.032}}, "cpu_baseline": {"ops_per_s": 256780.9, "cores": 1, "kind": "port"}}
 
 
 def _bench():
@@ -41,6 +44,10 @@ def test_compact_line_fits_and_holds_the_headline():
         assert k in out["cpu_baseline"], k
     # every leg kept, each with a time and a roofline fraction
     assert set(out["legs"]) == set(LEGS)
+    legs = dict(legs, producer_pnc=PRODUCER, producer_orset=PRODUCER)  # round 5's producer-path legs fit too
+    out = b.compact_line(line, legs)
+    assert len(json.dumps(out)) <= b.LINE_CAP and set(out["legs"]) == set(LEGS) | {"producer_pnc", "producer_orset"}
+    assert out["legs"]["producer_pnc"]["ops_per_s"] == 2.5e6 and out["legs"]["producer_pnc"]["parity_vs_oracle"] is True
     for k, leg in out["legs"].items():
         assert "ms_per_step" in leg or "ms_per_wave" in leg, k
     assert out["legs"]["orset"]["roofline"]["bound"] == "hbm"
