@@ -554,7 +554,8 @@ def run_direct(exe_name, args, local, mode="--direct"):
     """One apply-loop bench binary with --direct (the wave laid out in page-locked memory, uploaded in place) or
     --arena (bench_apply: the caller's own copy of the wave into a jg_host_alloc arena, timed)."""
     import subprocess
-    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / exe_name)] + args + ["--device", str(local), mode],
+    mode = [mode] if isinstance(mode, str) else list(mode)
+    out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / exe_name)] + args + ["--device", str(local)] + mode,
                          capture_output=True, text=True, timeout=240)
     if out.returncode != 0 or not out.stdout.strip():
         return {"error": out.stderr[-500:]}
@@ -864,7 +865,7 @@ def compact_leg(name, leg):
         out["cpu_baseline"] = {k: _r(cb.get(k)) for k in ("msgs_per_s", "ops_per_s", "cores", "kind") if cb.get(k) is not None}
     if "parity_vs_oracle" in leg:
         out["parity_vs_oracle"] = leg["parity_vs_oracle"]
-    for sub in ("from_pinned", "caller_arena", "pipelined", "first_level", "merge"):
+    for sub in ("from_pinned", "caller_arena", "caller_arena_streamed", "pipelined", "first_level", "merge"):
         s = leg.get(sub)
         if isinstance(s, dict):
             c = {k: _r(s[k]) for k in ("ms_per_wave", "ms", "event_ms", "msgs_per_s", "caller_flatten_ms_per_wave") if s.get(k) is not None}
@@ -983,6 +984,9 @@ def main():
     if apply_direct is not None and "error" not in apply_direct:
         apply_direct["caller_arena"] = guarded(run_direct, "bench_apply", ["--accounts", "1000000", "--ops", "1000000", "--waves", "3",
                                                                            "--cpu-msgs", "0"], local, "--arena")
+        # the same copy in parts through jg_apply_stream_begin/append/end: part k + 1's copy overlaps part k's upload
+        apply_direct["caller_arena_streamed"] = guarded(run_direct, "bench_apply", ["--accounts", "1000000", "--ops", "1000000", "--waves", "3",
+                                                                                    "--cpu-msgs", "0"], local, "--arena-stream")
     sync.close()
     if rank != 0:
         return

@@ -11,6 +11,7 @@
 #include <memory>
 #include <condition_variable>
 #include <functional>
+#include <future>
 #include <unordered_set>
 #include <mutex>
 #include <thread>
@@ -355,7 +356,9 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
     double t_copy = 0, t_append = 0;
     size_t n_parts = 0;
     const double t0 = trace ? now() : 0;
-    std::vector<uint64_t> poff;
+    std::vector<uint64_t> poff[2];  // the in-flight part's offsets and the next one's
+    std::future<int> pending;
+    std::string err;
     // parts of whole UpdateMessages, ~part_msgs messages each: the caller's copy of part k + 1 (plain cached copies,
     // what a C# caller's parallel Span.CopyTo does) runs while part k uploads
     for (size_t b0 = 0; b0 < blocks.size();) {
@@ -380,20 +383,35 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
             }
             if (nontemporal) out.finish();
         });
-        poff.resize(i1 - i0 + 1);
-        for (size_t i = i0; i <= i1; ++i) poff[i - i0] = p_off_[i] - p_off_[i0];
-        const jg_commit part{i1 - i0, w_uid_.data() + i0, w_type_.data() + i0, w_seq_.data() + i0, poff.data(), p_bytes_ + p_off_[i0], nullptr, nullptr};
         const double ta = trace ? now() : 0;
-        const int rc = jg_apply_stream_append(node_, &part);
-        if (rc != JG_OK) throw EngineError(rc, last_error());  // the library closed the stream: nothing applied
-        if (trace) t_copy += ta - tc, t_append += now() - ta, ++n_parts;
+        // the part goes to the library on a helper thread while this thread copies the next part (the previous
+        // append has returned first: parts arrive in order)
+        if (pending.valid()) {
+            const int rc = pending.get();
+            if (rc != JG_OK) throw EngineError(rc, err);  // the library closed the stream: nothing applied
+        }
+        std::vector<uint64_t>& po = poff[n_parts & 1];
+        po.resize(i1 - i0 + 1);
+        for (size_t i = i0; i <= i1; ++i) po[i - i0] = p_off_[i] - p_off_[i0];
+        const jg_commit part{i1 - i0, w_uid_.data() + i0, w_type_.data() + i0, w_seq_.data() + i0, po.data(), p_bytes_ + p_off_[i0], nullptr, nullptr};
+        pending = std::async(std::launch::async, [this, part, &err] {
+            const int rc = jg_apply_stream_append(node_, &part);
+            if (rc != JG_OK) err = last_error();  // the thread's own error message
+            return rc;
+        });
+        if (trace) t_copy += ta - tc, t_append += now() - ta;
+        ++n_parts;
         b0 = b1;
+    }
+    if (pending.valid()) {
+        const int rc = pending.get();
+        if (rc != JG_OK) throw EngineError(rc, err);
     }
     const double te = trace ? now() : 0;
     uint64_t n_done = 0, at = UINT64_MAX;
     const int rc = jg_apply_stream_end(node_, w_done_.data(), &n_done, &at);
     if (trace)
-        std::fprintf(stderr, "ApplyArenaStreamed: begin %.2f ms, %zu parts: copies %.2f ms, appends %.2f ms, end %.2f ms\n", t0 - tb, n_parts, t_copy,
+        std::fprintf(stderr, "ApplyArenaStreamed: begin %.2f ms, %zu parts: copies %.2f ms, append waits %.2f ms, end %.2f ms\n", t0 - tb, n_parts, t_copy,
                      t_append, now() - te);
     const std::string why = rc == JG_OK ? std::string() : last_error();
     jg_node_last_stats(node_, &stats_);
