@@ -1,3 +1,4 @@
+#include <algorithm>
 // ctx.hip — context, errors and device buffers of libjanusgpu.
 #include <cstring>
 #include <vector>
@@ -58,7 +59,7 @@ void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes) {
         JG_HIP(hipStreamSynchronize(ctx->stream));  // the old block may still be in use, also by the digest
         if (ctx->side) JG_HIP(hipStreamSynchronize(ctx->side));      // pipeline's streams (scratch3)
         if (ctx->level1) JG_HIP(hipStreamSynchronize(ctx->level1));
-        b.alloc(bytes + bytes / 4);
+        b.alloc(std::max<size_t>(bytes + bytes / 2, 64 << 10));  // headroom: every growth waits for the streams
     }
     return b.p;
 }

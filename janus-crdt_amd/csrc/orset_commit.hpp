@@ -9,6 +9,8 @@
 // Both orders are "by set, then a few hundred items of one set".  The round-3 commit sorted each list with a
 // device-wide radix sort (rocprim's merge sort at these sizes: ~20 launches each, ~0.75 ms of launches, syncs
 // and passes behind the last upload of the ORSetWorkload wave).  Here:
+//   (claims)      when the whole wave commits, the tables' claimants already counted (Claims, orset_tables.hpp) and
+//                 k_cb_scatter_claimed replaces k_cb_count + k_cb_scatter;
 //   k_cb_count    one lane per listed string / record: known strings resolved against the element table,
 //                 new strings (and their bytes) and live records counted per set (one atomic per run of a
 //                 wave's items with one set, all in flight together) with their place in the set's bucket (the
@@ -25,7 +27,12 @@
 #pragma once
 
 constexpr uint32_t kCbMax = 2048;  // items of one set / (side, set) the LDS sorts hold
-constexpr int kCbBlock = 256;
+constexpr int kCbBlock = 256;      // the largest workgroup of k_cb_strings / k_cb_records
+// Both kernels are launched with LDS for the wave's LARGEST bucket (P = its power of two, read back with the
+// totals) and min(256, max(64, P)) threads: the ORSetWorkload's buckets hold tens to a few hundred items, and
+// arrays sized for kCbMax (28 / 52 KB per workgroup) left 5 / 3 workgroups per CU for 2000 / 4000 of them.
+__host__ __device__ constexpr size_t cb_strings_lds(uint32_t P) { return (size_t)P * 30 + 64; }
+__host__ __device__ constexpr size_t cb_records_lds(uint32_t P) { return (size_t)P * 26 + 64; }
 
 struct Buckets {
     uint32_t* scnt;              // [n_sets + 1] new strings per set -> exclusive offsets
@@ -35,34 +42,10 @@ struct Buckets {
     uint32_t* sset;              // [ns] its set
     uint32_t* rpos;              // [nrec] place of listed record j in its (side, set) bucket (kDead: past the limit)
     uint32_t* rset;              // [nrec] side << 31 | set
-    uint32_t* sitem;             // [new strings] list indices in bucket order
-    uint32_t* ritem[2];          // [live records of the side] list indices in bucket order
+    uint32_t* sitem;             // [new strings] their string slots in bucket order
+    uint32_t* ritem[2];          // [live records of the side] their record slots in bucket order
     uint32_t n_sets;
 };
-
-// A place in the bucket of `cell` (the key's counter) for every active lane, from one atomic per RUN of
-// consecutive active lanes with the same key, all of the wave's in flight together (one round trip).  The lists
-// hold each message's claims back to back (one wave per message appends them together) and a message is one
-// set, so a wave's 64 items are a few runs: ~8x fewer atomics than one per lane, and a hot set costs one per
-// wave.  Device-scope atomics execute at the memory side (MI355X_MICROARCH "Global float atomics"); the round-3
-// fold took every distinct key of a wave in turn, a chain of up to 64 dependent ballot + atomic rounds.
-__device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32_t* cell) {
-    const uint32_t lane = threadIdx.x & 63;
-    const unsigned long long act = __ballot(active);
-    if (!act) return kDead;  // wave-uniform
-    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
-    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
-    const unsigned long long heads = __ballot(head);
-    const unsigned long long breaks = heads | ~act;  // a run ends before the next head or inactive lane
-    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
-    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
-    uint32_t r = 0;
-    if (head) r = atomicAdd(cell, end - lane);
-    const unsigned long long hm = heads & (lane == 63 ? ~0ull : (2ull << lane) - 1ull);
-    const uint32_t h = hm ? 63u - (uint32_t)__clzll(hm) : lane;  // this lane's run head (an inactive lane: itself)
-    const uint32_t base = (uint32_t)__shfl((int)r, (int)h);
-    return active ? base + (lane - h) : kDead;
-}
 
 // The bytes of each run of bucket_add (same runs: consecutive active lanes with one key) added to the key's
 // byte counter by the run's head, no return: an inclusive wave scan of the lengths, the head adds the scan at
@@ -189,18 +172,35 @@ __global__ __launch_bounds__(kScanThreads) void k_cb_scan(Buckets B, uint64_t n,
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_cb_scatter(uint64_t ns, uint64_t nrec, Buckets B) {
+__global__ __launch_bounds__(kBlock) void k_cb_scatter(uint64_t ns, uint64_t nrec, const StrTab T, const RecTab R, Buckets B) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < ns) {
         const uint32_t p = B.spos[i];
-        if (p != kDead) B.sitem[B.scnt[B.sset[i]] + p] = (uint32_t)i;
+        if (p != kDead) B.sitem[B.scnt[B.sset[i]] + p] = T.list[i];
     } else if (i - ns < nrec) {
         const uint64_t j = i - ns;
         const uint32_t p = B.rpos[j];
         if (p != kDead) {
             const uint32_t k = B.rset[j], sd = k >> 31;
-            B.ritem[sd][B.rcnt[sd][k & 0x7FFFFFFFu] + p] = (uint32_t)j;
+            B.ritem[sd][B.rcnt[sd][k & 0x7FFFFFFFu] + p] = R.list[j];
         }
+    }
+}
+
+// The same scatter from the places the tables' claimants took (k_ow_strings / k_ow_rins, `Claims`): a commit
+// of the whole wave whose claims all counted reads one 8-byte place per listed item instead of k_cb_count's
+// pass over the slots.
+__global__ __launch_bounds__(kBlock) void k_cb_scatter_claimed(uint64_t ns, uint64_t nrec, const StrTab T, const RecTab R, Claims C, Buckets B) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < ns) {
+        const uint32_t sid = T.list[i];
+        const uint2 pl = C.splace[sid];
+        if (pl.x != kDead) B.sitem[B.scnt[pl.y] + pl.x] = sid;
+    } else if (i - ns < nrec) {
+        const uint32_t slot = R.list[i - ns];
+        const uint2 pl = C.rplace[slot];
+        const uint32_t sd = pl.y >> 31;
+        B.ritem[sd][B.rcnt[sd][pl.y & 0x7FFFFFFFu] + pl.x] = slot;
     }
 }
 
@@ -234,29 +234,46 @@ template <class Less> __device__ void lds_rank_sort(uint16_t* perm, uint32_t cnt
     __syncthreads();
 }
 
-__device__ __forceinline__ uint32_t pow2_ge(uint32_t x) {
+__host__ __device__ __forceinline__ uint32_t pow2_ge(uint32_t x) {
     uint32_t p = 1;
     while (p < x) p <<= 1;
     return p;
 }
 
 // One workgroup per set: its new strings by first entry; ids next_id + rank; names g0 + bucket offset + rank
-// with their bytes at pool0 + the set's byte offset + the prefix of lengths in rank order.
+// with their bytes at pool0 + the set's byte offset + the prefix of lengths in rank order.  Everything a
+// string's name needs (its first entry, length, first inserter's name offset and key) is gathered into LDS
+// before the sort, and the set's counters with it, so the write phase waits on memory only for the bytes and
+// the two table inserts (a chain of ~13 dependent loads became ~8).
 __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, Buckets B, uint64_t g0,
                                                          uint64_t pool0, Names N, uint32_t* __restrict__ sid_id,
                                                          unsigned long long* __restrict__ status) {
     const uint32_t s = blockIdx.x;
     const uint32_t o0 = B.scnt[s], cnt = B.scnt[s + 1] - o0;
     if (cnt == 0) return;
-    __shared__ uint32_t key[kCbMax], item[kCbMax], lens[kCbMax];
-    __shared__ uint16_t perm[kCbMax];
+    const uint64_t pbase = pool0 + B.sbytes[s];
+    const uint32_t next = N.next_id[s], gen = N.set_gen[s];
+    const uint32_t P = pow2_ge(cnt), NT = blockDim.x;
+    extern __shared__ __align__(16) unsigned char cb_lds[];  // cb_strings_lds(the launch's largest P)
     __shared__ unsigned long long wsum[kCbBlock / 64];
-    const uint32_t P = pow2_ge(cnt);
-    for (uint32_t r = threadIdx.x; r < P; r += kCbBlock) {
+    unsigned long long* noff = reinterpret_cast<unsigned long long*>(cb_lds);
+    unsigned long long* skey = noff + P;
+    uint32_t* key = reinterpret_cast<uint32_t*>(skey + P);
+    uint32_t* item = key + P;
+    uint32_t* lens = item + P;
+    uint16_t* perm = reinterpret_cast<uint16_t*>(lens + P);
+    for (uint32_t r = threadIdx.x; r < P; r += NT) {
         if (r < cnt) {
-            const uint32_t i = B.sitem[o0 + r];
-            item[r] = i;
-            key[r] = T.slot[T.list[i]].first;
+            const uint32_t sid = B.sitem[o0 + r];
+            const StrSlot& e = T.slot[sid];
+            const unsigned long long word = e.word;
+            const uint32_t first = e.first, len = e.len;
+            const uint64_t ref = (word & 0xFFFFFFFFull) - 1;
+            item[r] = sid;
+            key[r] = first;
+            lens[r] = len;
+            noff[r] = S.noff[ref];
+            skey[r] = S.key[ref];
         }
         perm[r] = (uint16_t)r;
     }
@@ -265,16 +282,12 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
         const uint32_t ka = a < cnt ? key[a] : 0xFFFFFFFFu, kb = b < cnt ? key[b] : 0xFFFFFFFFu;
         return ka != kb ? ka < kb : a < b;  // pads (index >= cnt) last
     };
-    if (cnt <= kCbBlock) lds_rank_sort(perm, cnt, by_first);
+    if (cnt <= NT) lds_rank_sort(perm, cnt, by_first);
     else lds_bitonic(perm, P, by_first);
-    for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
-        lens[r] = T.slot[T.list[item[perm[r]]]].len;
-    }
-    __syncthreads();
     // exclusive prefix of the lengths in rank order (each thread a contiguous run, then the thread sums)
-    const uint32_t per = (cnt + kCbBlock - 1) / kCbBlock, r0 = threadIdx.x * per, r1 = min(cnt, r0 + per);
+    const uint32_t per = (cnt + NT - 1) / NT, r0 = min(cnt, threadIdx.x * per), r1 = min(cnt, r0 + per);
     unsigned long long mine = 0;
-    for (uint32_t r = r0; r < r1; ++r) mine += lens[r];
+    for (uint32_t r = r0; r < r1; ++r) mine += lens[perm[r]];
     unsigned long long incl = mine;  // inclusive scan over the threads: wave scan, then the wave totals
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int o = 1; o < 64; o <<= 1) {
@@ -285,17 +298,15 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
     __syncthreads();
     unsigned long long before = incl - mine;
     for (uint32_t q = 0; q < wv; ++q) before += wsum[q];
-    const uint64_t pbase = pool0 + B.sbytes[s];
-    const uint32_t next = N.next_id[s], gen = N.set_gen[s];
     for (uint32_t r = r0; r < r1; ++r) {
-        const uint32_t sid = T.list[item[perm[r]]];
-        const uint64_t ref = (T.slot[sid].word & 0xFFFFFFFFull) - 1;
-        const uint32_t len = lens[r];
+        const uint32_t x = perm[r];
+        const uint32_t sid = item[x], len = lens[x];
+        const unsigned long long k = skey[x];
         const uint64_t id = (uint64_t)next + r;
         if (id >= JG_NULL_ELEM - 1) atomicOr(status + 8, 1ull);
         sid_id[sid] = (uint32_t)id;
         const uint64_t g = g0 + o0 + r, p = pbase + before;
-        const uint8_t* src = bytes + S.noff[ref];
+        const uint8_t* src = bytes + noff[x];
         for (uint32_t q = 0; q < len; ++q) N.pool[p + q] = src[q];
         before += len;
         N.set[g] = s;
@@ -303,8 +314,8 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_strings(Sparse S, const uint8_t
         N.gen[g] = gen;
         N.len[g] = len;
         N.off[g] = p;
-        N.key[g] = S.key[ref];
-        tab_insert(N, S.key[ref], (uint32_t)g);
+        N.key[g] = k;
+        tab_insert(N, k, (uint32_t)g);
         itab_insert(N, s, (uint32_t)id, (uint32_t)g);
     }
     __syncthreads();
@@ -320,14 +331,17 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_records(Sparse S, StrTab T, Rec
     const uint32_t* off = B.rcnt[sd];
     const uint32_t o0 = off[s], cnt = off[s + 1] - o0;
     if (cnt == 0) return;
-    __shared__ uint32_t elem[kCbMax], mint[kCbMax];
-    __shared__ unsigned long long lo[kCbMax], hi[kCbMax];
-    __shared__ uint16_t perm[kCbMax];
-    const uint32_t P = pow2_ge(cnt);
+    const uint32_t P = pow2_ge(cnt), NT = blockDim.x;
+    extern __shared__ __align__(16) unsigned char cb_lds[];  // cb_records_lds(the launch's largest P)
+    unsigned long long* lo = reinterpret_cast<unsigned long long*>(cb_lds);
+    unsigned long long* hi = lo + P;
+    uint32_t* elem = reinterpret_cast<uint32_t*>(hi + P);
+    uint32_t* mint = elem + P;
+    uint16_t* perm = reinterpret_cast<uint16_t*>(mint + P);
     const uint32_t* items = B.ritem[sd];
-    for (uint32_t r = threadIdx.x; r < P; r += kCbBlock) {
+    for (uint32_t r = threadIdx.x; r < P; r += NT) {
         if (r < cnt) {
-            const uint32_t slot = R.list[items[o0 + r]];
+            const uint32_t slot = items[o0 + r];
             const uint64_t u = (R.slot[slot].word & 0xFFFFFFFFull) - 1;
             const unsigned long long id = S.trk[u];
             elem[r] = (id >> 63) ? JG_NULL_ELEM : sid_id[(uint32_t)(id >> 1)];
@@ -351,7 +365,7 @@ __global__ __launch_bounds__(kCbBlock) void k_cb_records(Sparse S, StrTab T, Rec
     unsigned long long* ok = sd ? k1 : k0;
     Tag16* ot = sd ? t1 : t0;
     uint32_t* oo = sd ? o1_ : o0_;
-    for (uint32_t r = threadIdx.x; r < cnt; r += kCbBlock) {
+    for (uint32_t r = threadIdx.x; r < cnt; r += NT) {
         const uint32_t x = perm[r];
         ok[o0 + r] = (unsigned long long)s << 32 | elem[x];
         ot[o0 + r] = Tag16{lo[x], hi[x]};

@@ -113,15 +113,75 @@ __device__ __forceinline__ void list_append(bool fresh, uint32_t slot, uint32_t*
     else *overflow = 1;
 }
 
-// The sub-lists packed back to back (offs[j] = where sub-list j starts; offs[kLists] = the total).
+// The sub-lists packed back to back (offs[j] = where sub-list j starts; offs[kLists] = the total), grid-stride
+// (the check queues it before the total is known on the host).
 __global__ void k_list_pack(const uint32_t* __restrict__ list, uint64_t sub_cap, const unsigned long long* __restrict__ offs,
                             uint32_t* __restrict__ out) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= offs[kLists]) return;
-    uint32_t j = 0;
-    while (offs[j + 1] <= i) ++j;
-    out[i] = list[j * sub_cap + (i - offs[j])];
+    const uint64_t total = offs[kLists];
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t j = 0;
+        while (offs[j + 1] <= i) ++j;
+        out[i] = list[j * sub_cap + (i - offs[j])];
+    }
 }
+
+// Both tables' sub-list offsets from their counters on the device (each count clamped to its sub-list: an
+// overflowed table's counts run past it, and that wave never commits from the tables).
+__global__ void k_list_offs(const unsigned long long* __restrict__ ns, uint64_t s_cap, const unsigned long long* __restrict__ nr, uint64_t r_cap,
+                            unsigned long long* __restrict__ offs) {
+    if (threadIdx.x >= 2) return;
+    const unsigned long long* n = threadIdx.x ? nr : ns;
+    const uint64_t cap = threadIdx.x ? r_cap : s_cap;
+    unsigned long long* o = offs + threadIdx.x * (kLists + 1);
+    unsigned long long run = 0;
+    for (uint32_t j = 0; j < kLists; ++j) {
+        o[j] = run;
+        run += min((unsigned long long)cap, n[j * kCountStride]);
+    }
+    o[kLists] = run;
+}
+
+// A place in the bucket of `cell` (the key's counter) for every active lane, from one atomic per RUN of
+// consecutive active lanes with the same key, all of the wave's in flight together (one round trip).  The lists
+// hold each message's claims back to back (one wave per message appends them together) and a message is one
+// set, so a wave's 64 items are a few runs: ~8x fewer atomics than one per lane, and a hot set costs one per
+// wave.  Device-scope atomics execute at the memory side (MI355X_MICROARCH "Global float atomics"); the round-3
+// fold took every distinct key of a wave in turn, a chain of up to 64 dependent ballot + atomic rounds.
+__device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32_t* cell) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long act = __ballot(active);
+    if (!act) return kDead;  // wave-uniform
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long breaks = heads | ~act;  // a run ends before the next head or inactive lane
+    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
+    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
+    uint32_t r = 0;
+    if (head) r = atomicAdd(cell, end - lane);
+    const unsigned long long hm = heads & (lane == 63 ? ~0ull : (2ull << lane) - 1ull);
+    const uint32_t h = hm ? 63u - (uint32_t)__clzll(hm) : lane;  // this lane's run head (an inactive lane: itself)
+    const uint32_t base = (uint32_t)__shfl((int)r, (int)h);
+    return active ? base + (lane - h) : kDead;
+}
+
+// The commit's per-set bucket counts taken at claim time (orset_commit.hpp): a claimant of a NEW string (not in
+// the element table) takes its place in its set's bucket and adds its bytes; a claimant of a record takes its
+// place in its (side, set) bucket.  place[slot] = {place or kDead, set | side << 31}.  A claim the counts cannot
+// hold (a set at or past cap, a string not looked up) raises *uncounted and the commit counts from the lists
+// (k_cb_count); so does a commit with a limit (claims past it are counted here).
+inline constexpr uint64_t cb_al(uint64_t b) { return (b + 255) & ~255ull; }
+// the four count arrays of cap + 1 entries: new strings, records (two sides) per set, then the strings' bytes
+inline constexpr uint64_t cb_counts_bytes(uint64_t cap) { return 3 * cb_al((cap + 1) * 4) + cb_al((cap + 1) * 8); }
+struct Claims {
+    uint32_t* scnt;              // [cap + 1] new strings per set
+    unsigned long long* sbytes;  // [cap + 1] their bytes
+    uint32_t* rcnt[2];           // [cap + 1] records per set, per side
+    uint2* splace;               // [string slots]
+    uint2* rplace;               // [record slots]
+    unsigned long long* uncounted;
+    uint32_t cap;
+};
 
 __device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* bytes, uint64_t a, uint32_t set_a, unsigned long long key_a,
                                             uint32_t len_a, unsigned long long pfx_a, uint64_t noff_a, uint64_t b) {
@@ -175,7 +235,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                                                        const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ ne,
                                                        const uint32_t* __restrict__ na, uint64_t m0, uint64_t m1, StrTab T,
                                                        unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow,
-                                                       Names N, uint32_t set_lim, uint32_t* __restrict__ sid_id) {
+                                                       Names N, uint32_t set_lim, uint32_t* __restrict__ sid_id, Claims C) {
     __shared__ uint32_t sh[kTabWaves][kDupScan];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t es_chunk = (off[m0] + kEntryDiv - 1) / kEntryDiv;  // entry slots from here on: this launch's
@@ -191,8 +251,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
     bool over = false;
     for (uint32_t q0 = 0; q0 < cnt; q0 += 64) {  // wave-uniform bounds: list_append's ballot needs every lane
         const uint32_t q = q0 + lane;
-        bool fresh = false;
-        uint32_t sid = kNoSid;
+        bool fresh = false, is_new = false;
+        uint32_t sid = kNoSid, new_len = 0;
         if (q < cnt) {
         const uint64_t slot = es + q;
         const unsigned long long key = S.key[slot], pfx = S.pfx[slot];
@@ -214,6 +274,9 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
                     e->pfx = pfx;
                     e->set = set;
                     e->id0 = id0;
+                    is_new = id0 == kNoName;
+                    new_len = len;
+                    if (id0 == kUnresolved) *C.uncounted = 1;
                     break;
                 }
             }
@@ -237,6 +300,25 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
         }
         list_append(fresh, sid, T.list, T.n, T.sub_cap, overflow, m + q0 / 64);
+        // the claim counted (one message per wave: every lane's set is `set`)
+        const unsigned long long nb = __ballot(is_new);
+        if (nb) {  // wave-uniform
+            const int leader = __ffsll((long long)nb) - 1;
+            unsigned long long bytes_sum = new_len;
+            for (int o = 32; o > 0; o >>= 1) bytes_sum += __shfl_xor(bytes_sum, o);
+            uint32_t base = 0;
+            if ((int)lane == leader) {
+                if (set < C.cap) {
+                    base = atomicAdd(C.scnt + set, (uint32_t)__popcll(nb));
+                    atomicAdd(C.sbytes + set, bytes_sum);
+                } else {
+                    *C.uncounted = 1;
+                }
+            }
+            base = (uint32_t)__shfl((int)base, leader);
+            if (is_new) C.splace[sid] = make_uint2(base + (uint32_t)__popcll(nb & ((1ull << lane) - 1ull)), set);
+        }
+        if (fresh && !is_new) C.splace[sid] = make_uint2(kDead, set);
     }
     if (cnt > kDupScan) over = true;  // the duplicate check below would miss pairs: the sort path decides
     if (__ballot(over) != 0) {
@@ -295,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rkeys(Sparse S, const uint64_t* _
 
 __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                     const unsigned long long* __restrict__ nt, uint64_t m0, uint64_t m1, RecTab T,
-                                                    unsigned long long* __restrict__ overflow) {
+                                                    unsigned long long* __restrict__ overflow, Claims C) {
     constexpr int M = kMsgsPerWave;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t mb = m0 + ((uint64_t)blockIdx.x * kTabWaves + wv) * M;
@@ -320,6 +402,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
         const unsigned long long id = q < W.total ? S.trk[t] : kNone;
         bool fresh = false;
         uint64_t slot = ~0ull;
+        uint32_t rkey = 0;
         if (id != kNone) {  // kNone: its string found no slot (the overflow word is up already), or past the wave's items
         const Tag16 g = S.tval[t];
         const uint64_t h = rec_hash(id, g, 0);
@@ -333,7 +416,8 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
                 if (w == 0) {
                     slot = p;
                     fresh = true;
-                    T.slot[slot].key = (uint32_t)(id & 1) << 31 | sj;  // the record's set is its message's
+                    rkey = (uint32_t)(id & 1) << 31 | sj;  // the record's set is its message's
+                    T.slot[slot].key = rkey;
                     break;
                 }
             }
@@ -349,6 +433,11 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
         else if (T.slot[slot].mint > (uint32_t)t) atomicMin(&T.slot[slot].mint, (uint32_t)t);
         }
         list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow, mb / M + q0 / 64);
+        // the claim counted in its (side, set) bucket
+        const bool counted = fresh && sj < C.cap;
+        const uint32_t pos = bucket_add(counted, rkey, C.rcnt[rkey >> 31] + (rkey & 0x7FFFFFFFu));
+        if (counted) C.rplace[slot] = make_uint2(pos, rkey);
+        else if (fresh) *C.uncounted = 1;
     }
     if (__ballot(over) != 0 && lane == 0) *overflow = 1;
 }

@@ -1201,7 +1201,17 @@ struct jg_orset_wire {
     // they are being filled this wave, `tables_ok` = the check found them complete (no overflow)
     jg::DevBuf st_slot, st_list, rt_slot, rt_list, sid_id, ovf;  // 16-byte table slots (orset_tables.hpp); ovf: overflow word, sub-list counts
     jg::DevBuf st_packed, rt_packed, loffs;  // the sub-lists packed for the commit
-    jg::DevBuf cb;                           // the bucket commit's counts, places and bucket orders (orset_commit.hpp)
+    jg::DevBuf cb;                           // the bucket commit's places and bucket orders (orset_commit.hpp)
+    // the bucket counts the tables' claimants take (Claims, orset_tables.hpp): zeroed per wave for cb_cap sets,
+    // and one place per string / record slot
+    jg::DevBuf cbc, splace, rplace;
+    uint64_t cb_cap = 0;
+    uint64_t waves_claimed = 0;  // bucket commits whose counts came from the claims (tests read them)
+    // the check queued the commit's first steps ahead of its one read (lists packed, the claims' counts scanned:
+    // spec_h = k_cb_scan's eight status words), for a commit of the whole wave from the tables
+    bool spec = false;
+    unsigned long long spec_h[8] = {};
+    jg::DevBuf specst;
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
     uint64_t st_cap = 0, rt_cap = 0;     // slots in use this wave (a power of two, <= the allocations)
     uint64_t st_alloc = 0, rt_alloc = 0, seen_s = 0, seen_r = 0;  // allocated slots; the last checked wave's distinct strings / records
@@ -1255,7 +1265,10 @@ void grow_keep(jg_ctx* ctx, jg::DevBuf& b, size_t need, size_t keep, bool zero =
     if (zero) JG_HIP(hipMemsetAsync(nb.p, 0, nb.bytes, ctx->stream));
     keep = std::min(keep, b.p ? b.bytes : 0);
     if (keep) JG_HIP(hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, ctx->stream));
-    JG_HIP(hipStreamSynchronize(ctx->stream));
+    // a retired block lives until the wave has drained: the kernels queued before this copy may still use it, and
+    // those queued after it use the new one (stream order) — no host wait in the middle of a commit (~30 us each,
+    // six arrays per names growth).  A block freed right here needs the stream idle first.
+    if (!retire) JG_HIP(hipStreamSynchronize(ctx->stream));
     std::swap(nb.p, b.p);
     std::swap(nb.bytes, b.bytes);
     if (retire && nb.p) {
@@ -1313,8 +1326,9 @@ void ensure_names(jg_ctx* ctx, jg_orset_wire* w, uint64_t incoming, uint64_t poo
         grow_keep(ctx, w->nkey, cap * 8, w->n_names * 8, false, &w->retired);
         w->name_cap = std::min({w->nset.bytes / 4, w->nid.bytes / 4, w->ngen.bytes / 4, w->nlen.bytes / 4, w->noff.bytes / 8, w->nkey.bytes / 8});
     }
-    if (w->pool_used + pool_bytes > w->pool_cap) {
-        grow_keep(ctx, w->pool, std::max<uint64_t>(w->pool_used + pool_bytes, 1 << 20), w->pool_used, false, &w->retired);
+    if (w->pool_used + pool_bytes > w->pool_cap) {  // x1.5: a pool grown to the exact need grew again every wave
+        grow_keep(ctx, w->pool, std::max<uint64_t>({w->pool_used + pool_bytes, w->pool_cap + w->pool_cap / 2, 1 << 20}), w->pool_used, false,
+                  &w->retired);
         w->pool_cap = w->pool.bytes;
     }
     if (w->tab_cap == 0 || 2 * total > w->tab_cap) {
@@ -1554,22 +1568,50 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
         w->st_slot.alloc(sc * sizeof(StrSlot));
         w->st_list.alloc((sc / 8) * kLists * 4);  // sub-lists of cap / 8 (a table is at most half full)
         w->sid_id.alloc(sc * 4);
+        w->splace.alloc(sc * 8);
+        w->st_packed.alloc((sc / 8) * kLists * 4 + 4);  // the packed list (spec_commit_prep: no allocation behind the uploads)
         w->st_alloc = sc;
     }
     if (w->rt_alloc < rc) {
         w->rt_slot.alloc(rc * sizeof(RecSlot));
         w->rt_list.alloc((rc / 8) * kLists * 4);
+        w->rplace.alloc(rc * 8);
+        w->rt_packed.alloc((rc / 8) * kLists * 4 + 4);
         w->rt_alloc = rc;
     }
     w->st_cap = sc;
     w->rt_cap = rc;
     if (!w->ovf.p) w->ovf.alloc((1 + 2 * kLists) * kCountStride * 8);
+    ensure(w->loffs, 2 * (kLists + 1) * 8);
+    ensure(w->specst, sizeof w->spec_h);
     hipLaunchKernelGGL(k_str_clear, dim3((unsigned)std::min<uint64_t>(4096, (2 * w->st_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        w->st_slot.as<uint4>(), w->st_cap);
     hipLaunchKernelGGL(k_tab_clear, dim3((unsigned)std::min<uint64_t>(4096, (w->rt_cap + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
                        w->rt_slot.as<uint4>(), w->rt_cap);
     JG_HIP(hipGetLastError());
-    JG_HIP(hipMemsetAsync(w->ovf.p, 0, (1 + 2 * kLists) * kCountStride * 8, ctx->stream));  // overflow, sub-list counts
+    JG_HIP(hipMemsetAsync(w->ovf.p, 0, (1 + 2 * kLists) * kCountStride * 8, ctx->stream));  // overflow, uncounted, sub-list counts
+    // the claim-time bucket counts: one per set the store knows (a set past them sends the commit to k_cb_count)
+    const uint64_t cap = std::min<uint64_t>(0x7FFFFFF0ull, std::max<uint64_t>({w->cb_cap, w->set_cap, (uint64_t)w->max_set + 1, 1024}));
+    if (cap > w->cb_cap) {
+        w->cbc.alloc(cb_counts_bytes(cap));
+        w->cb_cap = cap;
+    }
+    JG_HIP(hipMemsetAsync(w->cbc.p, 0, cb_counts_bytes(w->cb_cap), ctx->stream));
+}
+
+Claims claims_of(jg_orset_wire* w) {
+    Claims C{};
+    char* p = w->cbc.as<char>();
+    const uint64_t c4 = cb_al((w->cb_cap + 1) * 4);
+    C.scnt = reinterpret_cast<uint32_t*>(p);
+    C.rcnt[0] = reinterpret_cast<uint32_t*>(p + c4);
+    C.rcnt[1] = reinterpret_cast<uint32_t*>(p + 2 * c4);
+    C.sbytes = reinterpret_cast<unsigned long long*>(p + 3 * c4);
+    C.splace = w->splace.as<uint2>();
+    C.rplace = w->rplace.as<uint2>();
+    C.uncounted = w->ovf.as<unsigned long long>() + 1;  // ovf word 1: zeroed with the overflow word, read by the check
+    C.cap = (uint32_t)w->cb_cap;
+    return C;
 }
 
 // The chunk's strings and records into the wave's tables (after its parse, same stream).
@@ -1583,9 +1625,10 @@ void launch_tables(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
     const dim3 grid_m((unsigned)((m1 - m0 + kTabWaves * kMsgsPerWave - 1) / (kTabWaves * kMsgsPerWave)));  // kMsgsPerWave messages per wave
     hipLaunchKernelGGL(k_ow_strings, grid, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->vbytes, w->ne.as<unsigned long long>(),
                        w->na.as<uint32_t>(), m0, m1, str_tab(w), w->err.as<unsigned long long>(), ovf, names_of(w), set_lim,
-                       w->sid_id.as<uint32_t>());
+                       w->sid_id.as<uint32_t>(), claims_of(w));
     hipLaunchKernelGGL(k_ow_rkeys, grid_m, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1);
-    hipLaunchKernelGGL(k_ow_rins, grid_m, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1, rec_tab(w), ovf);
+    hipLaunchKernelGGL(k_ow_rins, grid_m, dim3(kBlock), 0, ctx->stream, S, w->voff, w->vmset, w->nt.as<unsigned long long>(), m0, m1, rec_tab(w), ovf,
+                       claims_of(w));
     JG_HIP(hipGetLastError());
 }
 
@@ -1615,6 +1658,40 @@ void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
     if (w->tables) launch_tables(ctx, w, m0, m1);
 }
 
+// Queued by the check of a table wave before its one read, for a commit of the whole wave from the claims'
+// counts (commit_buckets): both lists packed from offsets computed on the device, and the per-set counts
+// scanned into bucket offsets (k_cb_scan's totals come back with the check's read).  A commit that cannot
+// use them (a limit, an uncounted claim, an overflowed table, JANUS_ORSET_COMMIT=radix / count) repacks or
+// recounts as before; this only writes the packed lists, the counts and specst.
+void spec_commit_prep(jg_ctx* ctx, jg_orset_wire* w) {
+    const char* e = std::getenv("JANUS_ORSET_COMMIT");
+    const uint64_t n_sets = (uint64_t)w->max_set + 1;
+    const char* sp = std::getenv("JANUS_ORSET_SPEC");  // =0: the commit packs and scans after the check (A/B runs)
+    w->spec = !(e && (std::strcmp(e, "radix") == 0 || std::strcmp(e, "count") == 0)) && !(sp && std::strcmp(sp, "0") == 0) && n_sets <= w->cb_cap;
+    if (!w->spec) return;
+    const StrTab ST = str_tab(w);
+    const RecTab RT = rec_tab(w);
+    const uint64_t cs = kLists * ST.sub_cap, cr = kLists * RT.sub_cap;
+    // buffers sized by tables_begin: an allocation here (hipFree / hipMalloc behind the uploads) cost ~0.5 ms
+    if (w->st_packed.bytes < cs * 4 + 4 || w->rt_packed.bytes < cr * 4 + 4 || !w->loffs.p || !w->specst.p) {
+        w->spec = false;
+        return;
+    }
+    auto* doffs = w->loffs.as<unsigned long long>();
+    hipLaunchKernelGGL(k_list_offs, dim3(1), dim3(64), 0, ctx->stream, ST.n, ST.sub_cap, RT.n, RT.sub_cap, doffs);
+    // grid-stride over the packed lists: enough workgroups for the last wave's distinct strings / records
+    auto grid = [](uint64_t seen, uint64_t cap) {
+        return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks_for(seen ? std::min(cap, 2 * seen + 4096) : cap), 4096)));
+    };
+    hipLaunchKernelGGL(k_list_pack, grid(w->seen_s, cs), dim3(kBlock), 0, ctx->stream, ST.list, ST.sub_cap, doffs, w->st_packed.as<uint32_t>());
+    hipLaunchKernelGGL(k_list_pack, grid(w->seen_r, cr), dim3(kBlock), 0, ctx->stream, RT.list, RT.sub_cap, doffs + kLists + 1, w->rt_packed.as<uint32_t>());
+    const Claims C = claims_of(w);
+    Buckets B{};
+    B.scnt = C.scnt, B.rcnt[0] = C.rcnt[0], B.rcnt[1] = C.rcnt[1], B.sbytes = C.sbytes;
+    hipLaunchKernelGGL(k_cb_scan, dim3(4), dim3(kScanThreads), 0, ctx->stream, B, n_sets + 1, w->specst.as<unsigned long long>());
+    JG_HIP(hipGetLastError());
+}
+
 // Passes 2 + grouping over the whole wave; sets w->first_bad.  Returns the first bad message's code.
 int check_wave(jg_orset* s, jg_orset_wire* w) {
     jg_ctx* ctx = s->ctx;
@@ -1629,13 +1706,17 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         JG_HIP(hipMemsetAsync(st, 0xFF, 8, ctx->stream));
         hipLaunchKernelGGL(k_ow_first_bad, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, w->err.as<unsigned long long>(), n, st);
         JG_HIP(hipGetLastError());
-        // the overflow word and the tables' sub-list counts (the commit's) come back with the first bad message:
-        // one round trip, page-locked
+        spec_commit_prep(ctx, w);
+        // the overflow word and the tables' sub-list counts (the commit's) come back with the first bad message,
+        // and with them the claims' bucket totals: one round trip, page-locked
         w->lc.resize((1 + 2 * kLists) * kCountStride);
+        const size_t at_spec = 64 + w->lc.size() * 8;
         jg::pin_get(ctx, 0, st, 8);
         jg::pin_get(ctx, 64, w->ovf.p, w->lc.size() * 8);
+        if (w->spec) jg::pin_get(ctx, at_spec, w->specst.p, sizeof w->spec_h);
         jg::pin_sync(ctx);
         std::memcpy(w->lc.data(), jg::pin_at(ctx, 64), w->lc.size() * 8);
+        if (w->spec) std::memcpy(w->spec_h, jg::pin_at(ctx, at_spec), sizeof w->spec_h);
         unsigned long long h[2];
         std::memcpy(h, jg::pin_at(ctx, 0), 8);
         h[1] = w->lc[0];
@@ -1811,6 +1892,9 @@ void sort_side_end(jg_ctx* ctx, jg_orset_wire* w, int sd, uint64_t n, int key_bi
     JG_HIP(hipGetLastError());
 }
 
+void commit_packed(jg_orset* s, jg_orset_wire* w, StrTab ST, RecTab RT, uint64_t ns, uint64_t nrec, uint32_t csi_lim, uint32_t t_lim,
+                   uint64_t t_next, double* tc, bool tr);
+
 // The bucket commit (orset_commit.hpp): false if a set's bucket is past the LDS sorts (or JANUS_ORSET_COMMIT=radix),
 // with nothing changed but the resolved ids of known strings (the radix path writes them again).
 bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTab& RT, uint64_t ns, uint64_t nrec, uint32_t csi_lim,
@@ -1828,16 +1912,19 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
                    (unsigned long long)(ns + nrec));
         return false;
     }
-    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
-    const uint64_t c4 = al((n_sets + 1) * 4), c8 = al((n_sets + 1) * 8), s4 = al(ns * 4 + 4), r4 = al(nrec * 4 + 4);
-    ensure(w->cb, 3 * c4 + c8 + 3 * s4 + 4 * r4);
-    char* p = w->cb.as<char>();
+    // the whole wave commits and every claim counted (the check read the uncounted word): the claimants' counts
+    // and places stand, and neither k_cb_count nor its memsets run
+    const bool claimed = csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0 && n_sets <= w->cb_cap &&
+                         !(e && std::strcmp(e, "count") == 0);  // JANUS_ORSET_COMMIT=count: the counting pass always (tests)
+    const uint64_t s4 = cb_al(ns * 4 + 4), r4 = cb_al(nrec * 4 + 4);
+    ensure(w->cb, 3 * s4 + 4 * r4);
+    const Claims C = claims_of(w);
     Buckets B{};
-    B.scnt = reinterpret_cast<uint32_t*>(p);
-    B.rcnt[0] = reinterpret_cast<uint32_t*>(p + c4);
-    B.rcnt[1] = reinterpret_cast<uint32_t*>(p + 2 * c4);
-    B.sbytes = reinterpret_cast<unsigned long long*>(p + 3 * c4);
-    char* q = p + 3 * c4 + c8;
+    B.scnt = C.scnt;  // the counts: cb_cap + 1 entries each (the scan covers the wave's n_sets + 1)
+    B.rcnt[0] = C.rcnt[0];
+    B.rcnt[1] = C.rcnt[1];
+    B.sbytes = C.sbytes;
+    char* q = w->cb.as<char>();
     B.spos = reinterpret_cast<uint32_t*>(q);
     B.sset = reinterpret_cast<uint32_t*>(q + s4);
     B.sitem = reinterpret_cast<uint32_t*>(q + 2 * s4);
@@ -1848,27 +1935,47 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     B.ritem[1] = reinterpret_cast<uint32_t*>(q + 3 * r4);
     B.n_sets = (uint32_t)n_sets;
     unsigned long long* st = status_words(w);
-    JG_HIP(hipMemsetAsync(p, 0, 3 * c4 + c8, ctx->stream));  // the four count arrays (and their trailing zeros)
+    if (n_sets > w->cb_cap) {  // (a set the wave's claims could not count) room for every set's counts
+        w->cbc.alloc(cb_counts_bytes(n_sets));  // the tables' claims are done with the old block (same stream)
+        w->cb_cap = n_sets;
+        const Claims C2 = claims_of(w);
+        B.scnt = C2.scnt, B.rcnt[0] = C2.rcnt[0], B.rcnt[1] = C2.rcnt[1], B.sbytes = C2.sbytes;
+    }
+    // not from the claims: the counts again from the lists (the check may have scanned the claims' counts in place)
+    if (!claimed) JG_HIP(hipMemsetAsync(w->cbc.p, 0, cb_counts_bytes(w->cb_cap), ctx->stream));  // the four count arrays (and their trailing zeros)
     JG_HIP(hipMemsetAsync(st, 0, 9 * 8, ctx->stream));
     const Sparse S = sparse_of(w);
     const Names N = names_of(w);
-    if (ns + nrec)
-        hipLaunchKernelGGL(k_cb_count, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, RT, ns, nrec, csi_lim, t_lim, N,
-                           w->sid_id.as<uint32_t>(), B);
-    hipLaunchKernelGGL(k_cb_scan, dim3(4), dim3(kScanThreads), 0, ctx->stream, B, n_sets + 1, st);
-    JG_HIP(hipGetLastError());
     unsigned long long h[8];  // totals: new strings, their bytes, records per side; then the largest buckets
-    read_words(ctx, st, h, 8);
+    if (claimed && w->spec) {  // scanned by the check, totals read with it (spec_commit_prep)
+        std::memcpy(h, w->spec_h, sizeof h);
+    } else {
+        if (claimed) {  // (a wave the check did not prepare) the claims' counts scanned here
+        } else if (ns + nrec) {
+            hipLaunchKernelGGL(k_cb_count, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, RT, ns, nrec, csi_lim, t_lim, N,
+                               w->sid_id.as<uint32_t>(), B);
+        }
+        hipLaunchKernelGGL(k_cb_scan, dim3(4), dim3(kScanThreads), 0, ctx->stream, B, n_sets + 1, st);
+        JG_HIP(hipGetLastError());
+        read_words(ctx, st, h, 8);
+    }
     if (h[4] > kCbMax || h[6] > kCbMax || h[7] > kCbMax) {
         JG_REQUIRE(!strict, JG_ESTATE, "OR-Set bucket commit: a set holds %llu new strings / %llu + %llu records of the wave (> %u, JANUS_ORSET_COMMIT=buckets)",
                    h[4], h[6], h[7], kCbMax);
         return false;
     }
     const uint64_t n_new = h[0], nb = h[1], cnt[2] = {h[2], h[3]};
-    if (ns + nrec) hipLaunchKernelGGL(k_cb_scatter, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, B);
+    if (ns + nrec && claimed)
+        hipLaunchKernelGGL(k_cb_scatter_claimed, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, ST, RT, C, B);
+    else if (ns + nrec)
+        hipLaunchKernelGGL(k_cb_scatter, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, ST, RT, B);
+    if (claimed) ++w->waves_claimed;
+    // LDS and threads for the largest bucket (orset_commit.hpp)
+    auto cb_threads = [](uint32_t P) { return std::min<uint32_t>(kCbBlock, std::max<uint32_t>(64, P)); };
+    const uint32_t Ps = pow2_ge(std::max<uint32_t>(1, (uint32_t)h[4])), Pr = pow2_ge(std::max<uint32_t>(1, (uint32_t)std::max(h[6], h[7])));
     if (n_new)
-        hipLaunchKernelGGL(k_cb_strings, dim3((unsigned)n_sets), dim3(kCbBlock), 0, ctx->stream, S, w->vbytes, ST, B, w->n_names, w->pool_used, N,
-                           w->sid_id.as<uint32_t>(), st);
+        hipLaunchKernelGGL(k_cb_strings, dim3((unsigned)n_sets), dim3(cb_threads(Ps)), cb_strings_lds(Ps), ctx->stream, S, w->vbytes, ST, B, w->n_names,
+                           w->pool_used, N, w->sid_id.as<uint32_t>(), st);
     JG_HIP(hipGetLastError());
     ++w->waves_bucketed;
     // ids issued (the check ruled out running past 2^32 - 2: id_bound), names in (set, first entry) order
@@ -1890,7 +1997,7 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     w->recs->add.next = w->recs->rem.next = t_next;
     jg_stream_soa& a = w->recs->add;
     jg_stream_soa& r = w->recs->rem;
-    hipLaunchKernelGGL(k_cb_records, dim3((unsigned)n_sets, 2), dim3(kCbBlock), 0, ctx->stream, S, ST, RT, B, w->sid_id.as<uint32_t>(),
+    hipLaunchKernelGGL(k_cb_records, dim3((unsigned)n_sets, 2), dim3(cb_threads(Pr)), cb_records_lds(Pr), ctx->stream, S, ST, RT, B, w->sid_id.as<uint32_t>(),
                        a.key.as<unsigned long long>(), a.tag.as<Tag16>(), a.ord.as<uint32_t>(), r.key.as<unsigned long long>(), r.tag.as<Tag16>(),
                        r.ord.as<uint32_t>());
     JG_HIP(hipGetLastError());
@@ -1918,13 +2025,19 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     const uint64_t t_next = (w->wnb + kTagDiv - 1) / kTagDiv + 1;  // every tag slot of the wave is below this
     ensure_sets(ctx, w, (uint64_t)w->max_set + 1);
     ensure_names(ctx, w, 0, 0);
-    unsigned long long* st = status_words(w);
-    const Sparse S = sparse_of(w);
     StrTab ST = str_tab(w);
     RecTab RT = rec_tab(w);
     // the wave's strings (the table's list; those first named past the limit are skipped)
     // the sub-lists packed into one list each (offsets from the counts: one read, one pack launch per table)
     const std::vector<unsigned long long>& lc = w->lc;  // read by the check with the first bad message
+    if (w->spec) {  // packed by the check (spec_commit_prep): the offsets on the device gave the same layout
+        uint64_t ns = 0, nrec = 0;
+        for (uint32_t j = 0; j < kLists; ++j) ns += lc[(1 + j) * kCountStride], nrec += lc[(1 + kLists + j) * kCountStride];
+        ST.list = w->st_packed.as<uint32_t>();
+        RT.list = w->rt_packed.as<uint32_t>();
+        commit_packed(s, w, ST, RT, ns, nrec, csi_lim, t_lim, t_next, tc, tr);
+        return;
+    }
     unsigned long long offs[2][kLists + 1];
     for (int t = 0; t < 2; ++t) {
         offs[t][0] = 0;
@@ -1949,7 +2062,22 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     JG_HIP(hipGetLastError());
     ST.list = w->st_packed.as<uint32_t>();  // the commit kernels read the packed lists
     RT.list = w->rt_packed.as<uint32_t>();
-    if (ns) ensure_names(ctx, w, ns, w->wnb);  // room for every listed string (an upper bound of the new ones)
+    commit_packed(s, w, ST, RT, ns, nrec, csi_lim, t_lim, t_next, tc, tr);
+}
+
+// The table commit from the packed lists: the bucket commit, or the radix path.
+void commit_packed(jg_orset* s, jg_orset_wire* w, StrTab ST, RecTab RT, uint64_t ns, uint64_t nrec, uint32_t csi_lim, uint32_t t_lim,
+                   uint64_t t_next, double* tc, bool tr) {
+    jg_ctx* ctx = s->ctx;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e6; };
+    unsigned long long* st = status_words(w);
+    const Sparse S = sparse_of(w);
+    // room for every listed string (an upper bound of the new ones: the element tables then grow ahead of the
+    // names, not at each doubling of exact counts — measured, the exact count moved a table rebuild into the
+    // timed waves) and their bytes: exactly the claims' total when the check scanned them for a whole-wave commit
+    // (both commit paths issue exactly those names), else the wave's bytes
+    const bool exact = w->spec && csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0;
+    if (ns) ensure_names(ctx, w, ns, exact ? w->spec_h[1] : w->wnb);
     if (commit_buckets(s, w, ST, RT, ns, nrec, csi_lim, t_lim, t_next)) {
         if (tr) std::fprintf(stderr, "commit_tables: bucket commit %.0f us (%llu strings, %llu records listed)\n", now() - tc[0],
                              (unsigned long long)ns, (unsigned long long)nrec);
@@ -2153,6 +2281,7 @@ void commit_wave(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
 
 void close_wave(jg_orset_wire* w) {
     w->open = false;
+    w->spec = false;
     w->external = false;
     w->checked = false;
     w->wn = w->wnb = 0;

@@ -14,7 +14,7 @@
 // GPU: janus::GpuStableStore::SubmitClientUpdates — one call per wave of `ops` client ops (ApplyOps in chunks,
 // snapshots encoded on the device for PN-Counters and by the host writer for OR-Sets, the batcher, digests in
 // one device call).  CPU baseline: the oracle's SafeCRDT.Update + ActualPropagateSyncMsg + update_digest per
-// submitted UpdateMessage on the first `cpu_ops` ops of the first wave, one thread (the reference's
+// submitted UpdateMessage on `cpu_ops` ops after `cpu_warm` untimed ones, one thread (the reference's
 // per-request path).  Parity: a second GPU store built from the oracle's own Guids runs the same sample and its
 // results, UpdateMessages (order, identities, payload bytes) and digests must equal the oracle's (exit 1).
 // Prints one JSON object.
@@ -88,13 +88,14 @@ std::vector<Op> make_ops(bool pnc, uint64_t keys, uint64_t n, std::mt19937_64& r
 
 int main(int argc, char** argv) {
     bool pnc = true;
-    uint64_t keys = 1000000, ops_n = 1000000, cpu_ops = 50000;
+    uint64_t keys = 1000000, ops_n = 1000000, cpu_ops = 50000, cpu_warm = UINT64_MAX;
     int waves = 3, device = 0, batch = 1000;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--workload") && i + 1 < argc) pnc = std::strcmp(argv[++i], "orset") != 0;
         else if (!std::strcmp(argv[i], "--keys") && i + 1 < argc) keys = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--ops") && i + 1 < argc) ops_n = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--cpu-ops") && i + 1 < argc) cpu_ops = std::strtoull(argv[++i], nullptr, 10);
+        else if (!std::strcmp(argv[i], "--cpu-warm") && i + 1 < argc) cpu_warm = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--batch") && i + 1 < argc) batch = std::atoi(argv[++i]);
@@ -102,6 +103,10 @@ int main(int argc, char** argv) {
     constexpr int kNodes = 4;
     const uint32_t R = kNodes + 1;
     std::mt19937_64 rng(0x4A414E5553ull + (pnc ? 0 : 1));
+    // OR-Set states grow with the ops a set has seen (Clear at 50): the timed sample starts after `cpu_warm` untimed
+    // ops (parity covers both), so its states are the size the full-size run's are (25 ops per set by default)
+    if (cpu_warm == UINT64_MAX) cpu_warm = pnc ? 0 : 25 * keys;
+    if (!cpu_ops) cpu_warm = 0;
 
     // ---- parity + CPU baseline on the sample: the oracle node and a GPU store built from its Guids ----
     std::vector<uint8_t> fill(keys, 0);
@@ -113,7 +118,7 @@ int main(int argc, char** argv) {
     if (cpu_ops) {
         std::mt19937_64 srng(0x5EED0000ull + (pnc ? 0 : 1));
         std::vector<uint8_t> sfill(keys, 0);
-        sample = make_ops(pnc, keys, cpu_ops, srng, sfill);
+        sample = make_ops(pnc, keys, cpu_warm + cpu_ops, srng, sfill);
         oracle::SafeCRDTManager node(batch, 77);
         node.nextSeq = 1;
         janus::GpuStableStore gp(device, (uint32_t)(pnc ? keys : 1), R, 4);
@@ -178,14 +183,17 @@ int main(int argc, char** argv) {
         // UpdateMessage it submitted
         std::vector<uint8_t> ores;
         ores.reserve(sample.size());
-        const double c0 = now_s();
-        for (const Op& o : sample) {
+        double c0 = now_s();
+        size_t u_timed = 0;  // the UpdateMessages submitted from the timed ops on
+        for (size_t i = 0; i < sample.size(); ++i) {
+            if (i == cpu_warm) c0 = now_s(), u_timed = node.submitted.size();
+            const Op& o = sample[i];
             const std::vector<oracle::Arg> a{pnc ? oracle::Arg::I(o.amount) : oracle::Arg::S(o.elem)};
             const auto r = o.op == 3 ? sc[o.k]->Update(3, {}, false, 0) : sc[o.k]->Update(o.op, a, o.safe, o.origin);
             ores.push_back(r.b ? 1 : 0);
         }
         std::vector<std::array<uint8_t, 32>> odig(node.submitted.size());
-        for (size_t u = 0; u < node.submitted.size(); ++u) {
+        for (size_t u = u_timed; u < node.submitted.size(); ++u) {
             std::vector<const uint8_t*> ptr;
             std::vector<uint64_t> len;
             for (const auto& np : node.submitted[u].update) {
@@ -197,10 +205,16 @@ int main(int argc, char** argv) {
             cpu_msgs += ptr.size();
         }
         cpu_s = now_s() - c0;
-        cpu_n = sample.size();
+        cpu_n = sample.size() - cpu_warm;
+        for (size_t u = 0; u < u_timed; ++u) {  // the warm-up's digests, untimed, for the parity check
+            std::vector<const uint8_t*> ptr;
+            std::vector<uint64_t> len;
+            for (const auto& np : node.submitted[u].update) ptr.push_back(reinterpret_cast<const uint8_t*>(np.bytes.data())), len.push_back(np.bytes.size());
+            oracle::update_digest(ptr.size(), ptr.data(), len.data(), nullptr, odig[u].data());
+        }
         // parity: results, the submitted UpdateMessages (the oracle batches flushed on size only, like the GPU's
         // call: no 100 ms rule in either), identities, payload bytes and digests
-        if (gres != ores) parity_ok = false, parity_why = "op results";
+        if (gres != ores) parity_ok = false, parity_why = "op results";  // the warm-up's and the timed ops'
         else if (gsub.size() != node.submitted.size()) parity_ok = false, parity_why = "number of UpdateMessages";
         for (size_t u = 0; parity_ok && u < gsub.size(); ++u) {
             const auto& a = gsub[u].update;
@@ -277,12 +291,12 @@ int main(int argc, char** argv) {
                 "\"parity_vs_oracle\": %s, \"parity_sample_ops\": %llu, \"parity_failure\": \"%s\", "
                 "\"cpu_baseline\": {\"ops_per_s\": %.1f, \"msgs_per_s\": %.1f, \"payload_bytes_per_msg\": %.1f, \"cores\": 1, \"kind\": \"port\", "
                 "\"sample\": \"oracle SafeCRDT.Update (ApplyOp + GetLastSynchronizedUpdate().Encode()) + ActualPropagateSyncMsg + update_digest "
-                "per submitted UpdateMessage over the first %llu ops\"}}\n",
+                "per submitted UpdateMessage over %llu ops after %llu untimed ones\"}}\n",
                 pnc ? "C5 banking client ops (deposit / transfer / withdraw as Increments, 4-replica states)"
                     : "ORSetWorkload client ops (Add of random 5-char strings, Clear at 50 elements)",
                 (unsigned long long)keys, batch, (unsigned long long)ops_n, waves, gpu_n / gpu_s, 1e3 * gpu_s / W, n_msgs / W, n_um / W,
                 n_msgs ? (double)n_bytes / n_msgs : 0.0, jg::host_threads(), parity_ok ? "true" : "false", (unsigned long long)cpu_n,
                 parity_why.c_str(), cpu_s > 0 ? cpu_n / cpu_s : 0.0, cpu_s > 0 ? cpu_msgs / cpu_s : 0.0, cpu_msgs ? (double)cpu_bytes / cpu_msgs : 0.0,
-                (unsigned long long)cpu_n);
+                (unsigned long long)cpu_n, (unsigned long long)cpu_warm);
     return parity_ok ? 0 : 1;
 }

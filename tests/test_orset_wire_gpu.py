@@ -66,13 +66,14 @@ def _run_waves(ctx, seed, n_sets, waves, per_wave, modes=("default",), chunks=3)
 
 
 # JANUS_ORSET_TAIL: the per-chunk string / record tables (strict: no fall-back), committed by set buckets
-# (JANUS_ORSET_COMMIT=buckets, strict) or by the radix path; or the sort path
-TAIL = ["tables", "tables-radix", "sort"]
+# (JANUS_ORSET_COMMIT=buckets, strict: from the counts the tables' claimants took when the whole wave commits),
+# by set buckets counted from the lists (=count), or by the radix path; or the sort path
+TAIL = ["tables", "tables-count", "tables-radix", "sort"]
 
 
 def _tail(monkeypatch, tail):
     monkeypatch.setenv("JANUS_ORSET_TAIL", "tables" if tail.startswith("tables") else tail)
-    monkeypatch.setenv("JANUS_ORSET_COMMIT", "radix" if tail == "tables-radix" else "buckets")
+    monkeypatch.setenv("JANUS_ORSET_COMMIT", {"tables-radix": "radix", "tables-count": "count"}.get(tail, "buckets"))
 PARSE = ["auto", "serial"]  # JANUS_ORSET_PARSE: one wave per message (k_ow_group) + serial fall-back, or serial only
 
 
