@@ -750,6 +750,8 @@ void wave_part(jg_node* nd, WaveRun& r, const jg_commit* w, uint64_t gbase, bool
     const bool direct = w->off && !r.filter && host_pinned(w->bytes);  // payload uploaded from the caller's pinned buffer
     std::vector<uint64_t> cb{0};
     const uint64_t first = gbase == 0 && n > 4 * r.tail ? r.tail : r.chunk_msgs;
+    // (measured, round 5: planning the last chunks from the end — a `tail` chunk after a 2 x `tail` one, so each
+    // chunk's kernels hide under the next upload — moved neither the OR-Set nor the C5 wave, interleaved A/B)
     for (uint64_t c0 = first; c0 < n; c0 += r.chunk_msgs) cb.push_back(c0);
     if (last && n > cb.back() + 2 * r.tail) cb.push_back(n - r.tail);
     cb.push_back(n);

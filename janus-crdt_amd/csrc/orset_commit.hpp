@@ -189,18 +189,32 @@ __global__ __launch_bounds__(kBlock) void k_cb_scatter(uint64_t ns, uint64_t nre
 
 // The same scatter from the places the tables' claimants took (k_ow_strings / k_ow_rins, `Claims`): a commit
 // of the whole wave whose claims all counted reads one 8-byte place per listed item instead of k_cb_count's
-// pass over the slots.
-__global__ __launch_bounds__(kBlock) void k_cb_scatter_claimed(uint64_t ns, uint64_t nrec, const StrTab T, const RecTab R, Claims C, Buckets B) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < ns) {
-        const uint32_t sid = T.list[i];
-        const uint2 pl = C.splace[sid];
-        if (pl.x != kDead) B.sitem[B.scnt[pl.y] + pl.x] = sid;
-    } else if (i - ns < nrec) {
-        const uint32_t slot = R.list[i - ns];
-        const uint2 pl = C.rplace[slot];
-        const uint32_t sd = pl.y >> 31;
-        B.ritem[sd][B.rcnt[sd][pl.y & 0x7FFFFFFFu] + pl.x] = slot;
+// pass over the slots.  Grid-stride over the packed lists (offs: both tables' sub-list offsets, on the device):
+// the check queues it before its read, so it leaves without writing when a claim went uncounted or a table
+// overflowed (places then may be stale or past the bucket arrays) — such a wave never commits from the claims.
+__global__ __launch_bounds__(kBlock) void k_cb_scatter_claimed(const unsigned long long* __restrict__ offs, const StrTab T, const RecTab R,
+                                                               Claims C, Buckets B, const unsigned long long* __restrict__ overflow) {
+    if (*overflow != 0 || *C.uncounted != 0) return;
+    const uint64_t ns = offs[kLists], nrec = offs[2 * kLists + 1];
+    // (bounds: the lists' and bucket arrays' capacities — a speculative launch never writes outside them)
+    const uint64_t cap_s = kLists * T.sub_cap, cap_r = kLists * R.sub_cap;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < ns + nrec; i += (uint64_t)gridDim.x * kBlock) {
+        if (i < ns) {
+            const uint32_t sid = T.list[i];
+            if (sid > T.mask) continue;
+            const uint2 pl = C.splace[sid];
+            if (pl.x == kDead || pl.y >= C.cap) continue;
+            const uint64_t at = (uint64_t)B.scnt[pl.y] + pl.x;
+            if (at < cap_s) B.sitem[at] = sid;
+        } else {
+            const uint32_t slot = R.list[i - ns];
+            if (slot > R.mask) continue;
+            const uint2 pl = C.rplace[slot];
+            const uint32_t sd = pl.y >> 31, set = pl.y & 0x7FFFFFFFu;
+            if (set >= C.cap) continue;
+            const uint64_t at = (uint64_t)B.rcnt[sd][set] + pl.x;
+            if (at < cap_r) B.ritem[sd][at] = slot;
+        }
     }
 }
 

@@ -173,6 +173,10 @@ __device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32
 inline constexpr uint64_t cb_al(uint64_t b) { return (b + 255) & ~255ull; }
 // the four count arrays of cap + 1 entries: new strings, records (two sides) per set, then the strings' bytes
 inline constexpr uint64_t cb_counts_bytes(uint64_t cap) { return 3 * cb_al((cap + 1) * 4) + cb_al((cap + 1) * 8); }
+// places and bucket orders for every entry the two tables' lists can hold (orset_wire.hip buckets_of)
+inline constexpr uint64_t cb_items_bytes(uint64_t st_cap, uint64_t rt_cap) {
+    return 3 * cb_al((st_cap / 8) * kLists * 4 + 4) + 4 * cb_al((rt_cap / 8) * kLists * 4 + 4);
+}
 struct Claims {
     uint32_t* scnt;              // [cap + 1] new strings per set
     unsigned long long* sbytes;  // [cap + 1] their bytes

@@ -1597,6 +1597,7 @@ void tables_begin(jg_ctx* ctx, jg_orset_wire* w, uint64_t n_msgs, uint64_t nbyte
         w->cb_cap = cap;
     }
     JG_HIP(hipMemsetAsync(w->cbc.p, 0, cb_counts_bytes(w->cb_cap), ctx->stream));
+    ensure(w->cb, cb_items_bytes(w->st_cap, w->rt_cap));
 }
 
 Claims claims_of(jg_orset_wire* w) {
@@ -1612,6 +1613,29 @@ Claims claims_of(jg_orset_wire* w) {
     C.uncounted = w->ovf.as<unsigned long long>() + 1;  // ovf word 1: zeroed with the overflow word, read by the check
     C.cap = (uint32_t)w->cb_cap;
     return C;
+}
+
+// The bucket commit's arrays: the claims' counts, then places and bucket orders for every entry the two tables'
+// lists can hold this wave (w->cb, sized by tables_begin, so the check can queue the scatter before its read).
+Buckets buckets_of(jg_orset_wire* w) {
+    const Claims C = claims_of(w);
+    Buckets B{};
+    B.scnt = C.scnt;  // the counts: cb_cap + 1 entries each (the scan covers the wave's n_sets + 1)
+    B.rcnt[0] = C.rcnt[0];
+    B.rcnt[1] = C.rcnt[1];
+    B.sbytes = C.sbytes;
+    const uint64_t s4 = cb_al((w->st_cap / 8) * kLists * 4 + 4), r4 = cb_al((w->rt_cap / 8) * kLists * 4 + 4);
+    char* q = w->cb.as<char>();
+    B.spos = reinterpret_cast<uint32_t*>(q);
+    B.sset = reinterpret_cast<uint32_t*>(q + s4);
+    B.sitem = reinterpret_cast<uint32_t*>(q + 2 * s4);
+    q += 3 * s4;
+    B.rpos = reinterpret_cast<uint32_t*>(q);
+    B.rset = reinterpret_cast<uint32_t*>(q + r4);
+    B.ritem[0] = reinterpret_cast<uint32_t*>(q + 2 * r4);
+    B.ritem[1] = reinterpret_cast<uint32_t*>(q + 3 * r4);
+    B.n_sets = (uint32_t)std::min<uint64_t>((uint64_t)w->max_set + 1, 0xFFFFFFFFull);
+    return B;
 }
 
 // The chunk's strings and records into the wave's tables (after its parse, same stream).
@@ -1658,6 +1682,10 @@ void launch_parse(jg_ctx* ctx, jg_orset_wire* w, uint64_t m0, uint64_t m1) {
     if (w->tables) launch_tables(ctx, w, m0, m1);
 }
 
+// JANUS_TRACE_MERGE: host times (us) from the check's read to the commit's first launch
+double g_tmark[6] = {};
+double tnow_us() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e6; }
+
 // Queued by the check of a table wave before its one read, for a commit of the whole wave from the claims'
 // counts (commit_buckets): both lists packed from offsets computed on the device, and the per-set counts
 // scanned into bucket offsets (k_cb_scan's totals come back with the check's read).  A commit that cannot
@@ -1673,7 +1701,8 @@ void spec_commit_prep(jg_ctx* ctx, jg_orset_wire* w) {
     const RecTab RT = rec_tab(w);
     const uint64_t cs = kLists * ST.sub_cap, cr = kLists * RT.sub_cap;
     // buffers sized by tables_begin: an allocation here (hipFree / hipMalloc behind the uploads) cost ~0.5 ms
-    if (w->st_packed.bytes < cs * 4 + 4 || w->rt_packed.bytes < cr * 4 + 4 || !w->loffs.p || !w->specst.p) {
+    if (w->st_packed.bytes < cs * 4 + 4 || w->rt_packed.bytes < cr * 4 + 4 || !w->loffs.p || !w->specst.p ||
+        w->cb.bytes < cb_items_bytes(w->st_cap, w->rt_cap)) {
         w->spec = false;
         return;
     }
@@ -1686,9 +1715,15 @@ void spec_commit_prep(jg_ctx* ctx, jg_orset_wire* w) {
     hipLaunchKernelGGL(k_list_pack, grid(w->seen_s, cs), dim3(kBlock), 0, ctx->stream, ST.list, ST.sub_cap, doffs, w->st_packed.as<uint32_t>());
     hipLaunchKernelGGL(k_list_pack, grid(w->seen_r, cr), dim3(kBlock), 0, ctx->stream, RT.list, RT.sub_cap, doffs + kLists + 1, w->rt_packed.as<uint32_t>());
     const Claims C = claims_of(w);
-    Buckets B{};
-    B.scnt = C.scnt, B.rcnt[0] = C.rcnt[0], B.rcnt[1] = C.rcnt[1], B.sbytes = C.sbytes;
+    const Buckets B = buckets_of(w);
     hipLaunchKernelGGL(k_cb_scan, dim3(4), dim3(kScanThreads), 0, ctx->stream, B, n_sets + 1, w->specst.as<unsigned long long>());
+    // and every item of the PACKED lists into its bucket (a no-op when a claim went uncounted or a table overflowed)
+    StrTab PT = ST;
+    RecTab PR = RT;
+    PT.list = w->st_packed.as<uint32_t>();
+    PR.list = w->rt_packed.as<uint32_t>();
+    hipLaunchKernelGGL(k_cb_scatter_claimed, grid(w->seen_s + w->seen_r, cs + cr), dim3(kBlock), 0, ctx->stream, doffs, PT, PR, C, B,
+                       w->ovf.as<unsigned long long>());
     JG_HIP(hipGetLastError());
 }
 
@@ -1715,6 +1750,7 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         jg::pin_get(ctx, 64, w->ovf.p, w->lc.size() * 8);
         if (w->spec) jg::pin_get(ctx, at_spec, w->specst.p, sizeof w->spec_h);
         jg::pin_sync(ctx);
+        g_tmark[0] = tnow_us();
         std::memcpy(w->lc.data(), jg::pin_at(ctx, 64), w->lc.size() * 8);
         if (w->spec) std::memcpy(w->spec_h, jg::pin_at(ctx, at_spec), sizeof w->spec_h);
         unsigned long long h[2];
@@ -1735,6 +1771,7 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
             uint64_t ns = 0;
             for (uint32_t j = 0; j < kLists; ++j) ns += w->lc[(1 + j) * kCountStride];
             check_id_room(ctx, w, ns, n);
+            g_tmark[1] = tnow_us();
             if (h[0] == kNone) return JG_OK;
             unsigned long long e;
             JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + h[0], 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1916,24 +1953,9 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     // and places stand, and neither k_cb_count nor its memsets run
     const bool claimed = csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0 && n_sets <= w->cb_cap &&
                          !(e && std::strcmp(e, "count") == 0);  // JANUS_ORSET_COMMIT=count: the counting pass always (tests)
-    const uint64_t s4 = cb_al(ns * 4 + 4), r4 = cb_al(nrec * 4 + 4);
-    ensure(w->cb, 3 * s4 + 4 * r4);
+    ensure(w->cb, cb_items_bytes(w->st_cap, w->rt_cap));  // (sized by tables_begin)
     const Claims C = claims_of(w);
-    Buckets B{};
-    B.scnt = C.scnt;  // the counts: cb_cap + 1 entries each (the scan covers the wave's n_sets + 1)
-    B.rcnt[0] = C.rcnt[0];
-    B.rcnt[1] = C.rcnt[1];
-    B.sbytes = C.sbytes;
-    char* q = w->cb.as<char>();
-    B.spos = reinterpret_cast<uint32_t*>(q);
-    B.sset = reinterpret_cast<uint32_t*>(q + s4);
-    B.sitem = reinterpret_cast<uint32_t*>(q + 2 * s4);
-    q += 3 * s4;
-    B.rpos = reinterpret_cast<uint32_t*>(q);
-    B.rset = reinterpret_cast<uint32_t*>(q + r4);
-    B.ritem[0] = reinterpret_cast<uint32_t*>(q + 2 * r4);
-    B.ritem[1] = reinterpret_cast<uint32_t*>(q + 3 * r4);
-    B.n_sets = (uint32_t)n_sets;
+    Buckets B = buckets_of(w);
     unsigned long long* st = status_words(w);
     if (n_sets > w->cb_cap) {  // (a set the wave's claims could not count) room for every set's counts
         w->cbc.alloc(cb_counts_bytes(n_sets));  // the tables' claims are done with the old block (same stream)
@@ -1943,7 +1965,16 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     }
     // not from the claims: the counts again from the lists (the check may have scanned the claims' counts in place)
     if (!claimed) JG_HIP(hipMemsetAsync(w->cbc.p, 0, cb_counts_bytes(w->cb_cap), ctx->stream));  // the four count arrays (and their trailing zeros)
-    JG_HIP(hipMemsetAsync(st, 0, 9 * 8, ctx->stream));
+    // the scan's words (and k_cb_strings' id flag, a device-side guard no host reads: the check ruled the overflow
+    // out); a commit from the check's scan reads no word here, and skips the call (~25-40 us of host time right
+    // behind the check's sync, with the device idle)
+    if (!(claimed && w->spec)) JG_HIP(hipMemsetAsync(st, 0, 9 * 8, ctx->stream));
+    static const bool trm = std::getenv("JANUS_TRACE_MERGE") != nullptr;
+    if (trm) {
+        g_tmark[5] = tnow_us();
+        std::fprintf(stderr, "commit host: read -> check end %.0f us, -> commit %.0f, -> names %.0f, names %.0f, -> first launch %.0f\n", g_tmark[1] - g_tmark[0],
+                     g_tmark[2] - g_tmark[1], g_tmark[3] - g_tmark[2], g_tmark[4] - g_tmark[3], g_tmark[5] - g_tmark[4]);
+    }
     const Sparse S = sparse_of(w);
     const Names N = names_of(w);
     unsigned long long h[8];  // totals: new strings, their bytes, records per side; then the largest buckets
@@ -1965,9 +1996,12 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
         return false;
     }
     const uint64_t n_new = h[0], nb = h[1], cnt[2] = {h[2], h[3]};
-    if (ns + nrec && claimed)
-        hipLaunchKernelGGL(k_cb_scatter_claimed, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, ST, RT, C, B);
-    else if (ns + nrec)
+    if (claimed && w->spec) {
+        // scattered by the check (spec_commit_prep)
+    } else if (ns + nrec && claimed) {
+        hipLaunchKernelGGL(k_cb_scatter_claimed, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, w->loffs.as<unsigned long long>(), ST, RT, C,
+                           B, w->ovf.as<unsigned long long>());
+    } else if (ns + nrec)
         hipLaunchKernelGGL(k_cb_scatter, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, ST, RT, B);
     if (claimed) ++w->waves_claimed;
     // LDS and threads for the largest bucket (orset_commit.hpp)
@@ -2014,6 +2048,7 @@ void commit_tables(jg_orset* s, jg_orset_wire* w, uint64_t limit) {
     static const bool tr = std::getenv("JANUS_TRACE_MERGE") != nullptr;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e6; };
     double tc[5] = {tr ? now() : 0};
+    g_tmark[2] = tc[0];
     uint64_t lim_off = w->wnb;
     if (limit < n) {  // the limit message's byte offset
         jg::pin_get(ctx, 0, w->voff + limit, 8);
@@ -2077,7 +2112,9 @@ void commit_packed(jg_orset* s, jg_orset_wire* w, StrTab ST, RecTab RT, uint64_t
     // timed waves) and their bytes: exactly the claims' total when the check scanned them for a whole-wave commit
     // (both commit paths issue exactly those names), else the wave's bytes
     const bool exact = w->spec && csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0;
+    if (tr) g_tmark[3] = now();
     if (ns) ensure_names(ctx, w, ns, exact ? w->spec_h[1] : w->wnb);
+    if (tr) g_tmark[4] = now();
     if (commit_buckets(s, w, ST, RT, ns, nrec, csi_lim, t_lim, t_next)) {
         if (tr) std::fprintf(stderr, "commit_tables: bucket commit %.0f us (%llu strings, %llu records listed)\n", now() - tc[0],
                              (unsigned long long)ns, (unsigned long long)nrec);
