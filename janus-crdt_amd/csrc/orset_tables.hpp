@@ -264,9 +264,14 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
         const uint64_t noff = S.noff[slot];
         const unsigned long long word = (key >> 32) << 32 | (slot + 1);
         uint64_t p = key & T.mask;
+        uint32_t first_seen = 0xFFFFFFFFu;  // the slot's `first` as the probe loaded it (it only decreases)
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
             StrSlot* e = T.slot + p;
-            unsigned long long w = e->word;
+            // the whole 32-byte slot in one pair of loads: word, first, length | prefix, set, id (one dependent
+            // memory level per probe instead of three: word, then the fingerprint, then `first` for the atomicMin)
+            const uint4 h0 = reinterpret_cast<const uint4*>(e)[0], h1 = reinterpret_cast<const uint4*>(e)[1];
+            unsigned long long w = (unsigned long long)h0.x | (unsigned long long)h0.y << 32;
+            first_seen = h0.z;
             if (w == 0) {
                 w = atomicCAS(&e->word, 0ull, word);
                 if (w == 0) {
@@ -286,8 +291,10 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
             }
             if ((w >> 32) != (key >> 32)) continue;
             const uint64_t b = (w & 0xFFFFFFFFull) - 1;
-            const bool same = b >= es_chunk ? same_string(S, bytes, slot, set, key, len, pfx, noff, b)  // claimed in this launch
-                                            : e->len == len && e->set == set && e->pfx == pfx &&
+            // claimed in this launch: through the first inserter's entry (the loaded fingerprint may predate the
+            // claim); by an earlier launch: the fingerprint, visible since that launch ended
+            const bool same = b >= es_chunk ? same_string(S, bytes, slot, set, key, len, pfx, noff, b)
+                                            : h0.w == len && h1.z == set && ((unsigned long long)h1.x | (unsigned long long)h1.y << 32) == pfx &&
                                                   (len <= 8 || same_bytes(bytes + S.noff[b] + 8, bytes + noff + 8, len - 8));
             if (same) {
                 sid = (uint32_t)p;
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t*
             over = true;
         } else {
             const uint32_t c = (uint32_t)es + (!rem_first ? q : (q < n_rem ? n_add + q : q - n_rem));  // canonical: addSet first
-            if (T.slot[sid].first > c) atomicMin(&T.slot[sid].first, c);
+            if (first_seen > c) atomicMin(&T.slot[sid].first, c);  // a stale `first` is only larger: the filter holds
         }
         S.sid[slot] = sid;
         if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
@@ -412,9 +419,13 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
         const uint64_t h = rec_hash(id, g, 0);
         const unsigned long long word = (h >> 32) << 32 | (t + 1);
         uint64_t p = h & T.mask;
+        uint32_t mint_seen = 0xFFFFFFFFu;  // the slot's mint as the probe loaded it (it only decreases)
         for (uint32_t probe = 0; probe < kProbeCap; ++probe, p = (p + 1) & T.mask) {
-            // most references repeat a record seen earlier in the wave: a plain load settles those
-            unsigned long long w = T.slot[p].word;
+            // most references repeat a record seen earlier in the wave: a plain load settles those (word and
+            // mint in one 16-byte load: the atomicMin's filter needs no second trip)
+            const uint4 hs = *reinterpret_cast<const uint4*>(T.slot + p);
+            unsigned long long w = (unsigned long long)hs.x | (unsigned long long)hs.y << 32;
+            mint_seen = hs.z;
             if (w == 0) {
                 w = atomicCAS(&T.slot[p].word, 0ull, word);
                 if (w == 0) {
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void k_ow_rins(Sparse S, const uint64_t* __
             }
         }
         if (slot == ~0ull) over = true;
-        else if (T.slot[slot].mint > (uint32_t)t) atomicMin(&T.slot[slot].mint, (uint32_t)t);
+        else if (mint_seen > (uint32_t)t) atomicMin(&T.slot[slot].mint, (uint32_t)t);  // a stale mint is only larger
         }
         list_append(fresh, (uint32_t)slot, T.list, T.n, T.sub_cap, overflow, mb / M + q0 / 64);
         // the claim counted in its (side, set) bucket
