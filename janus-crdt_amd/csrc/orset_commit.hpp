@@ -47,29 +47,6 @@ struct Buckets {
     uint32_t n_sets;
 };
 
-// The bytes of each run of bucket_add (same runs: consecutive active lanes with one key) added to the key's
-// byte counter by the run's head, no return: an inclusive wave scan of the lengths, the head adds the scan at
-// the run's last lane minus the scan before it.  Lengths that could overflow the 32-bit scan (>= 2^25 each):
-// one add per lane.  Every lane of the wave calls it.
-__device__ __forceinline__ void run_bytes(bool active, uint32_t key, unsigned long long* cell, uint32_t len) {
-    const uint32_t lane = threadIdx.x & 63;
-    const unsigned long long act = __ballot(active);
-    if (!act) return;  // wave-uniform
-    const uint32_t v = active ? len : 0u;
-    if (__ballot(v >= (1u << 25))) {  // wave-uniform
-        if (active) atomicAdd(cell, (unsigned long long)len);
-        return;
-    }
-    const uint32_t incl = jgw::wave_incl_scan(v);
-    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
-    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
-    const unsigned long long breaks = __ballot(head) | ~act;
-    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
-    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
-    const uint32_t at_end = (uint32_t)__shfl((int)incl, (int)(end - 1));
-    if (head) atomicAdd(cell, (unsigned long long)(at_end - (incl - v)));
-}
-
 __global__ __launch_bounds__(kBlock) void k_cb_count(Sparse S, const uint8_t* __restrict__ bytes, StrTab T, RecTab R, uint64_t ns, uint64_t nrec,
                                                      uint32_t s_lim, uint32_t t_lim, Names N, uint32_t* __restrict__ sid_id, Buckets B) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;

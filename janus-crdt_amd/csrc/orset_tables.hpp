@@ -165,6 +165,29 @@ __device__ __forceinline__ uint32_t bucket_add(bool active, uint32_t key, uint32
     return active ? base + (lane - h) : kDead;
 }
 
+// The bytes of each run of bucket_add (same runs: consecutive active lanes with one key) added to the key's
+// byte counter by the run's head, no return: an inclusive wave scan of the lengths, the head adds the scan at
+// the run's last lane minus the scan before it.  Lengths that could overflow the 32-bit scan (>= 2^25 each):
+// one add per lane.  Every lane of the wave calls it.
+__device__ __forceinline__ void run_bytes(bool active, uint32_t key, unsigned long long* cell, uint32_t len) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long act = __ballot(active);
+    if (!act) return;  // wave-uniform
+    const uint32_t v = active ? len : 0u;
+    if (__ballot(v >= (1u << 25))) {  // wave-uniform
+        if (active) atomicAdd(cell, (unsigned long long)len);
+        return;
+    }
+    const uint32_t incl = jgw::wave_incl_scan(v);
+    const uint32_t prev = (uint32_t)__shfl_up((int)key, 1);
+    const bool head = active && (lane == 0 || !((act >> (lane - 1)) & 1) || prev != key);
+    const unsigned long long breaks = __ballot(head) | ~act;
+    const unsigned long long above = lane == 63 ? 0ull : breaks & (~0ull << (lane + 1));
+    const uint32_t end = above ? (uint32_t)(__ffsll((long long)above) - 1) : 64u;
+    const uint32_t at_end = (uint32_t)__shfl((int)incl, (int)(end - 1));
+    if (head) atomicAdd(cell, (unsigned long long)(at_end - (incl - v)));
+}
+
 // The commit's per-set bucket counts taken at claim time (orset_commit.hpp): a claimant of a NEW string (not in
 // the element table) takes its place in its set's bucket and adds its bytes; a claimant of a record takes its
 // place in its (side, set) bucket.  place[slot] = {place or kDead, set | side << 31}.  A claim the counts cannot
@@ -199,6 +222,8 @@ __device__ __forceinline__ bool same_string(const Sparse& S, const uint8_t* byte
 // k_ow_strings was 7 % SLOWER (549 -> 589 us: its per-entry probe and string compare are a longer dependent
 // chain, so packing its lanes only lengthens each wave) and it keeps one message per wave.
 constexpr int kMsgsPerWave = 4;
+// (round 5, the probe one load per slot: 2 and 4 messages per wave of k_ow_strings measured 491 and 522 us per wave
+// against 505 at one — within noise either way, so it keeps one message per wave and its simpler duplicate check)
 
 // The wave's messages [mb, mb + M) of [m0, m1): lane j < M holds message j's item count (0 for another
 // kind's message or past m1) and its exclusive prefix; the total is wave-uniform.  Every shuffle reads lanes
