@@ -143,6 +143,7 @@ struct jg_pnc {
     // resolved entries per message and its list of messages pass B must parse again (json.hip)
     jg::DevBuf wbytes, woff, wrows, wstat, wemit, wguid, wslow;
     uint64_t wn = 0, wnb = 0;
+    uint64_t scan_hi = 0;  // messages pass A scanned since the wave began (its fused applies are undone below this)
     bool wopen = false;
 };
 
@@ -275,6 +276,7 @@ void pnc_node_begin(jg_pnc* p, uint64_t n);
 void pnc_node_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1);
 int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
 int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
+void pnc_node_undo(jg_pnc* p, const uint32_t* rows);  // a node wave abandoned after its chunks' (fused) pass A
 // orset_wire.hip (OR-Set):
 void orset_node_begin(jg_orset* s, uint8_t* bytes, uint64_t* off, uint32_t* mset, uint64_t n, uint64_t nbytes, uint32_t max_set);
 void orset_node_parse(jg_orset* s, uint64_t m0, uint64_t m1);

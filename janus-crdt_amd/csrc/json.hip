@@ -28,6 +28,15 @@
 //   pass B  k_apply_emit  one lane per record entry, atomicMax into P / N (messages of one wave may
 //                       repeat a key; max is order-free); k_apply_list parses the slow list again.
 //
+// Fused pass A (round 5, the default; JANUS_JSON_FUSE=0 turns it off): a message whose replicas are all known
+// is applied by pass A itself once its checks are done, and its record then holds only the entries that
+// raised their cell, each with the cell's old value.  All or nothing still holds: max has no inverse, but a
+// cell's smallest recorded old value is its value before the wave whatever order the raises took, so a wave
+// that fails later (a bad message, a full row, a node wave cut or aborted) is undone exactly by atomicMin over
+// the records (k_undo_applied).  The steady state — every replica known, the common wave — writes no record
+// entries at all when its states repeat the cells and runs no pass B: the 64-byte records pass B read back and
+// the second touch of every cell's lines (pass A + pass B moved 3.1x the algorithmic bytes) go.
+//
 // JANUS_JSON_GROUP=1 runs the serial parser (scan_one / resolve_one / apply_one: byte-serial per thread
 // through a 16-byte window register) for every message: the reference the group path is tested
 // against.  The bound of the end-to-end call is the PCIe upload of the payload.
@@ -224,6 +233,8 @@ struct ScanVis {
 constexpr uint32_t kEmitMax = 14;
 constexpr uint16_t kReparse = 0xFFFF;
 constexpr uint32_t kNeedsCols = 0x4000;  // count flag: a deferred record whose columns pass C resolves
+constexpr uint32_t kApplied = 0x2000;    // count flag: pass A applied the message itself (fused); low bits = the
+                                         // entries it raised, recorded as (column code, old value) for the undo
 __host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kEmitMax * eb; }
 
 // deferred[m] (pass A): row << 32 | m for a message naming a replica its row has not seen, else this.
@@ -637,13 +648,33 @@ void reset_status(jg_ctx* ctx, unsigned long long* status) {
     JG_HIP(hipGetLastError());
 }
 
+// JANUS_JSON_FUSE=0: pass A leaves every message to pass B (read per launch: tests and A/B runs switch it)
+bool json_fuse() {
+    const char* e = std::getenv("JANUS_JSON_FUSE");
+    return !(e && std::strcmp(e, "0") == 0);
+}
+
 void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1,
                  const WaveScratch& w) {
     if (m1 <= m0) return;
     const Table t = table_of(p);
     const int G = json_group();
-    if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow);
-    else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow);
+    const bool fuse = json_fuse();
+    if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow, p->P.p, p->N.p, fuse);
+    else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow, p->P.p, p->N.p, fuse);
+    JG_HIP(hipGetLastError());
+    p->scan_hi = std::max(p->scan_hi, m1);
+}
+
+// A fused pass A over messages [0, p->scan_hi) taken back (stream-ordered): the wave failed after it, or a node
+// wave was cut or aborted.  Idempotent; a no-op for messages pass A left to pass B.
+void undo_applied(jg_pnc* p, const uint32_t* rows) {
+    const uint64_t n = p->scan_hi;
+    if (n == 0 || !p->wemit.p) return;
+    const Table t = table_of(p);
+    const unsigned g = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
+    if (p->eb == 8) hipLaunchKernelGGL(k_undo_applied<8>, dim3(g), dim3(kBlock), 0, p->ctx->stream, p->wemit.as<uint8_t>(), rows, n, t.R, p->P.p, p->N.p);
+    else hipLaunchKernelGGL(k_undo_applied<4>, dim3(g), dim3(kBlock), 0, p->ctx->stream, p->wemit.as<uint8_t>(), rows, n, t.R, p->P.p, p->N.p);
     JG_HIP(hipGetLastError());
 }
 
@@ -660,25 +691,28 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         JG_HIP(hipGetLastError());
         // The steady state (every payload valid, every replica known): pass B right away, guarded on the
         // device by pass A's status, so the wave costs one status read.  If pass A failed or deferred a
-        // message both launches are no-ops and the full path below runs (all or nothing).
+        // message both launches are no-ops and the full path below runs (all or nothing).  A fused pass A
+        // (json_fuse) applied every record pass B would read here (a deferral sends the wave to the full path,
+        // whose pass B runs unguarded): only the slow list's launch is left.
+        const bool fused = json_fuse();
         if (p->eb == 8) {
-            hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
+            if (!fused) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
             hipLaunchKernelGGL(k_apply_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, w.slow, t, p->P.p, p->N.p, w.status);
         } else {
-            hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
+            if (!fused) hipLaunchKernelGGL(k_apply_emit<4>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
             hipLaunchKernelGGL(k_apply_slow<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, w.slow, t, p->P.p, p->N.p, w.status);
         }
         JG_HIP(hipGetLastError());
         const Status st = read_status(ctx, w.status);
-        if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
+        if (st.first_bad != ~0ull) undo_applied(p, rows), fail_msg(st.first_bad, bad_msg, "state message");
         if (!st.n_deferred) {
-            if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
+            if (st.resolve_bad != ~0ull) undo_applied(p, rows), fail_msg(st.resolve_bad, bad_msg, "state message");
             return;
         }
     }
     DeferredLists dl = select_deferred(ctx, w.deferred, n, p->n_keys, w.status + 1);
     Status st = read_status(ctx, w.status);
-    if (st.first_bad != ~0ull) fail_msg(st.first_bad, bad_msg, "state message");
+    if (st.first_bad != ~0ull) undo_applied(p, rows), fail_msg(st.first_bad, bad_msg, "state message");
     unsigned long long* sorted_deferred = nullptr;
     if (st.n_deferred) {
         const uint64_t nd = st.n_deferred;
@@ -701,6 +735,7 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         if (st.resolve_bad != ~0ull) {
             hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, w.saved);
             JG_HIP(hipGetLastError());
+            undo_applied(p, rows);
             JG_HIP(hipStreamSynchronize(ctx->stream));
             fail_msg(st.resolve_bad, bad_msg, "state message");
         }
@@ -729,6 +764,7 @@ void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
     ensure_table(p);
     const WaveScratch w = wave_scratch(p, n);
     reset_status(p->ctx, w.status);
+    p->scan_hi = 0;
     launch_scan(p, bytes, off, rows, 0, n, w);
     finish_wave(p, bytes, off, rows, n, w, bad_msg);
 }
@@ -753,6 +789,7 @@ namespace jg {
 void pnc_node_begin(jg_pnc* p, uint64_t n) {
     ensure_table(p);
     reset_status(p->ctx, wave_scratch(p, n).status);
+    p->scan_hi = 0;
     p->wn = n;  // the node wave's capacity (no jg_pnc_wave_* wave is open while a node wave runs)
 }
 
@@ -781,9 +818,17 @@ int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
     *bad = UINT64_MAX;
     if (n == 0) return JG_OK;
     const WaveScratch w = wave_scratch(p, p->wn);
+    undo_applied(p, rows);  // the chunks' fused pass A applied messages past the cut too: back to the state before the wave
     reset_status(p->ctx, w.status);
+    p->scan_hi = 0;
     launch_scan(p, bytes, off, rows, 0, n, w);
     return pnc_node_finish(p, bytes, off, rows, n, bad, why);
+}
+
+// A node wave abandoned after its chunks' pass A (an internal failure): the fused applies taken back.
+void pnc_node_undo(jg_pnc* p, const uint32_t* rows) {
+    undo_applied(p, rows);
+    p->scan_hi = 0;
 }
 
 }  // namespace jg
@@ -937,6 +982,7 @@ int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
         grow_keep(ctx, p->wrows, cap_msgs * 4 + 4, 0);
         const WaveScratch w = wave_scratch(p, cap_msgs);
         reset_status(ctx, w.status);
+        p->scan_hi = 0;
         JG_HIP(hipMemsetAsync(p->woff.p, 0, 8, ctx->stream));  // off[0] = 0
         p->wn = 0;
         p->wnb = 0;
@@ -990,7 +1036,9 @@ int jg_pnc_wave_abort(jg_pnc* p) {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_abort: store is NULL");
         jg::ensure_device(p->ctx);
-        JG_HIP(hipStreamSynchronize(p->ctx->stream));  // pass A only read the wave: nothing to undo
+        if (p->wopen) undo_applied(p, p->wrows.as<uint32_t>());  // the appended chunks' fused pass A
+        p->scan_hi = 0;
+        JG_HIP(hipStreamSynchronize(p->ctx->stream));
         p->wopen = false;
     });
 }

@@ -45,6 +45,7 @@ struct GroupShared {
     uint32_t tk[kGroups];                          // tokens | the "nVector" token << 8 | "nVector" tokens seen << 16
     uint32_t flags[kGroups];
     uint32_t geo[kGroups], row[kGroups], nc[kGroups];  // alignment offset | length << 4; the row, its columns
+    uint32_t nr[kGroups];                          // fused pass A: entries the group's message raised (undo records)
 };
 __device__ __forceinline__ uint32_t tk_ntok(uint32_t tk) { return tk & 0xFFu; }
 __device__ __forceinline__ uint32_t tk_kn(uint32_t tk) { return (tk >> 8) & 0xFFu; }
@@ -273,6 +274,7 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
         sh.geo[grp] = a | L << 4;
         sh.row[grp] = rc.row;
         sh.nc[grp] = rc.nc;
+        sh.nr[grp] = 0;
     }
     for (uint32_t i = g; i < 2 * kMaskCols / 32; i += G) sh.mask[grp][i] = 0;
     wave_sync();
@@ -353,7 +355,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
                                                  const uint32_t* __restrict__ rows, uint64_t m0, uint64_t m1, Table t,
                                                  unsigned long long* __restrict__ status /* [0] first bad, [1] n deferred, [3] n slow */,
                                                  unsigned long long* __restrict__ deferred, uint8_t* __restrict__ emit,
-                                                 Guid16* __restrict__ eguid, unsigned long long* __restrict__ slow) {
+                                                 Guid16* __restrict__ eguid, unsigned long long* __restrict__ slow, void* P, void* N,
+                                                 bool fuse) {
     using T = typename ApplyVis<EB>::T;
     if constexpr (G == 1) {  // every accepted message not deferred also goes to the slow list
         const uint64_t m = m0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -368,15 +371,17 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         const RowCache rc = row_cache(t, rows, m, live, g);
         GroupParse<EB, G> gp;
         group_parse<EB, G>(sh, bytes, off, m, live, rc, gp);
-        // each parsed entry (on the lane its token was dealt to): its column, repeat check, emit slot
+        // each parsed entry (on the lane its token was dealt to): its column and the repeat check
+        uint32_t colr[GroupParse<EB, G>::kRounds];
 #pragma unroll
         for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
+            colr[u] = UINT32_MAX;
             const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
             if (!gp.has[u] || (sh.flags[gq] & kSlow)) continue;
-            const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
             const uint32_t kn = tk_kn(sh.tk[gq]), rq = sh.row[gq];
             const uint32_t vv = k < kn ? 0 : 1;
             const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, sh.nc[gq], gp.eg[u], vv ? k - kn - 1 : k - 1);
+            colr[u] = col;
             if (col == UINT32_MAX) {
                 atomicOr(&sh.flags[gq], (uint32_t)kMiss);
             } else if (col >= kMaskCols) {
@@ -384,28 +389,44 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             } else {
                 const uint32_t bit = 1u << (col & 31);
                 if (atomicOr(&sh.mask[gq][vv * (kMaskCols / 32) + (col >> 5)], bit) & bit) atomicOr(&sh.flags[gq], (uint32_t)kDup);
-                const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
-                uint8_t* h = emit + mq * emit_stride(EB);
-                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(col | vv << 15);
-                reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
             }
         }
         wave_sync();
-        // messages with an unknown replica: pass C resolves the columns from these Guids, pass B then
-        // applies the record
+        // the message's flags are final: its entries into the record pass B reads (a message with an unknown replica:
+        // every entry by Guid, pass C resolves the columns) or — fused (the steady state: every replica known) — into
+        // the cells right here, each entry that raised its cell recorded as (column, old value) so a wave that fails
+        // later is undone exactly (k_undo_applied: the min of a cell's recorded old values is its value before the
+        // wave; max has no inverse, the record is the inverse).  Pass B then has nothing to do for it.
 #pragma unroll
         for (int u = 0; u < GroupParse<EB, G>::kRounds; ++u) {
             const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
             const uint32_t fq = sh.flags[gq];
-            if (!gp.has[u] || (fq & (kSlow | kDup)) || !(fq & kMiss)) continue;
+            if (!gp.has[u] || (fq & (kSlow | kDup))) continue;
             const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
             const uint32_t vv = k < tk_kn(sh.tk[gq]) ? 0 : 1;
-            const uint32_t e = vv ? k - 2 : k - 1;
+            const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
             uint8_t* h = emit + mq * emit_stride(EB);
-            eguid[mq * kEmitMax + e] = gp.eg[u];
-            reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(0x7FFF | vv << 15);
-            reinterpret_cast<T*>(h + 32)[e] = (T)gp.ev[u];
+            const T v = (T)gp.ev[u];
+            if (fq & kMiss) {
+                eguid[mq * kEmitMax + e] = gp.eg[u];
+                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(0x7FFF | vv << 15);
+                reinterpret_cast<T*>(h + 32)[e] = v;
+            } else if (fuse) {
+                T* cell = static_cast<T*>(vv ? N : P) + (uint64_t)sh.row[gq] * t.R + colr[u];
+                if (*cell < v) {  // most states repeat what the cell holds: a plain read settles them
+                    const T old = atomicMax(cell, v);
+                    if (old < v) {
+                        const uint32_t r = atomicAdd(&sh.nr[gq], 1u);
+                        reinterpret_cast<uint16_t*>(h)[1 + r] = (uint16_t)(colr[u] | vv << 15);
+                        reinterpret_cast<T*>(h + 32)[r] = old;
+                    }
+                }
+            } else {
+                reinterpret_cast<uint16_t*>(h)[1 + e] = (uint16_t)(colr[u] | vv << 15);
+                reinterpret_cast<T*>(h + 32)[e] = v;
+            }
         }
+        wave_sync();
         const uint32_t f = sh.flags[grp];
         const bool fast = live && !(f & kSlow);
         const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
@@ -421,7 +442,9 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         }
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
-                (f & kDup) ? kReparse : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
+                (f & kDup) ? kReparse
+                           : (fuse && !(f & kMiss)) ? (uint16_t)(kApplied | sh.nr[grp])
+                                                    : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
             if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
     }
@@ -457,13 +480,32 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
     const uint64_t m = n - 1 - tid / kEmitLanes;
     const uint8_t* h = emit + m * emit_stride(EB);
     const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
-    if (cnt == kReparse || (cnt & kNeedsCols) || e >= cnt) return;
+    if (cnt == kReparse || (cnt & (kNeedsCols | kApplied)) || e >= cnt) return;  // kApplied: pass A applied it (fused)
     const uint32_t code = reinterpret_cast<const uint16_t*>(h)[1 + e];
     const T v = reinterpret_cast<const T*>(h + 32)[e];
     T* cell = static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF);
     // a wave repeats hot keys (C1: 100 keys, ~3000 states each): most values do not raise the cell, and
     // a plain read settles those without an atomic on a hot address
     if (*cell < v) atomicMax(cell, v);
+}
+
+// The fused pass A undone (a wave that failed after it, or a node wave cut or aborted): every entry it recorded as
+// having raised its cell takes the cell back down with atomicMin(old) — a cell's smallest recorded old value is
+// what it held before the wave, whichever order the raises took.  Idempotent.
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_undo_applied(const uint8_t* __restrict__ emit, const uint32_t* __restrict__ rows, uint64_t n,
+                                                         uint32_t R, void* P, void* N) {
+    using T = typename ApplyVis<EB>::T;
+    const uint64_t tid = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t e = (uint32_t)(tid % kEmitLanes);
+    const uint64_t m = tid / kEmitLanes;
+    if (m >= n) return;
+    const uint8_t* h = emit + m * emit_stride(EB);
+    const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
+    if (cnt == kReparse || !(cnt & kApplied) || e >= (cnt & 0xFFu)) return;
+    const uint32_t code = reinterpret_cast<const uint16_t*>(h)[1 + e];
+    T* cell = static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF);
+    atomicMin(cell, reinterpret_cast<const T*>(h + 32)[e]);
 }
 
 // Pass B for the messages left to the serial parser (list entries: [row << 32 |] message): parse again,
@@ -611,16 +653,17 @@ void launch_resolve_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_
 template <int EB>
 void launch_scan_g(int G, hipStream_t st, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1,
                    const Table& t, unsigned long long* status, unsigned long long* deferred, uint8_t* emit, Guid16* eguid,
-                   unsigned long long* slow) {
+                   unsigned long long* slow, void* P, void* N, bool fuse) {
     const unsigned gr = json_blocks(m1 - m0, G);
+#define JG_SCAN(GG) hipLaunchKernelGGL((k_scan<EB, GG>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow, P, N, fuse)
     switch (G) {
-        case 1: hipLaunchKernelGGL((k_scan<EB, 1>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        case 4: hipLaunchKernelGGL((k_scan<EB, 4>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        case 16: hipLaunchKernelGGL((k_scan<EB, 16>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        case 8: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        case 32: hipLaunchKernelGGL((k_scan<EB, 32>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        case 64: hipLaunchKernelGGL((k_scan<EB, 64>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
-        default: hipLaunchKernelGGL((k_scan<EB, 8>), dim3(gr), dim3(kBlock), 0, st, bytes, off, rows, m0, m1, t, status, deferred, emit, eguid, slow); break;
+        case 1: JG_SCAN(1); break;
+        case 4: JG_SCAN(4); break;
+        case 16: JG_SCAN(16); break;
+        case 32: JG_SCAN(32); break;
+        case 64: JG_SCAN(64); break;
+        default: JG_SCAN(8); break;
     }
+#undef JG_SCAN
 }
 

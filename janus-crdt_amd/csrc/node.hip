@@ -618,12 +618,19 @@ void wave_begin(jg_node* nd, WaveRun& r, jg_tracker* tr, uint64_t n, uint64_t to
     r.active = true;
 }
 
-// A wave rejected mid-loop (offsets checked chunk by chunk) or a device error: nothing was applied, but the chunks
+// A wave rejected mid-loop (offsets checked chunk by chunk) or a device error: what pass A applied is undone, and the chunks
 // already classified took first-occurrence claims on tracker slots; release them for the next wave.
 void wave_abort(jg_node* nd, WaveRun& r, uint64_t claimed) {
     jg_ctx* ctx = nd->ctx;
     if (r.dt.tab && claimed)
         hipLaunchKernelGGL(k_claim_reset, dim3(blocks_for(claimed)), dim3(kBlock), 0, ctx->stream, nd->tslot.as<uint32_t>(), claimed, r.dt.claim);
+    // the chunks' pass A applied the PN-Counter states it proved (fused): taken back, the store as before the wave
+    if (r.do_pnc) {
+        try {
+            jg::pnc_node_undo(nd->pnc, nd->rows.as<uint32_t>());
+        } catch (...) {
+        }
+    }
     (void)hipStreamSynchronize(ctx->copy);
     (void)hipStreamSynchronize(ctx->stream);
     if (r.do_orset) jg::orset_node_abort(nd->orset);

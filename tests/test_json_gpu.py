@@ -74,14 +74,17 @@ def test_decode_contract_on_device(ctx, eb, group, monkeypatch):
         pr.close()
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
 @pytest.mark.parametrize("ws", [0.0, 0.3])
 @pytest.mark.parametrize("group", ["1", "8", "16"])
 @pytest.mark.parametrize("eb,R,pool", [(4, 8, 6), (8, 8, 6), (4, 64, 40), (8, 200, 150)])
-def test_random_waves_match_oracle(ctx, eb, R, pool, group, ws, monkeypatch):
+def test_random_waves_match_oracle(ctx, eb, R, pool, group, ws, fuse, monkeypatch):
     """ws: the fraction of states written with a space after every ':' (valid, not the compact form), so
     one row's walk mixes group-parsed and serially parsed messages: pass C hands a walk to the serial
-    resume kernel, which also resolves the records of the compact messages after it."""
+    resume kernel, which also resolves the records of the compact messages after it.  fuse: pass A applies
+    the messages whose replicas are all known itself (JANUS_JSON_FUSE, default on) or leaves them to pass B."""
     monkeypatch.setenv("JANUS_JSON_GROUP", group)
+    monkeypatch.setenv("JANUS_JSON_FUSE", fuse)
     rng = np.random.default_rng(R * 10 + eb + int(ws * 100))
     n_keys = 40
     stable = random_guids(rng, n_keys)
@@ -275,6 +278,48 @@ def test_bad_message_is_all_or_nothing_then_prefix(ctx):
     bad, rc = pr.oracle(keys, msgs)  # the reference's loop: messages before the throwing one applied
     assert bad == 700
     pr.s.merge_json(keys[:700], msgs[:700])  # the host re-submits the prefix
+    pr.check()
+    pr.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
+def test_fused_apply_undone_on_failure(ctx, eb):
+    """The fused pass A applies every message whose replicas are all known before the wave is judged; a wave
+    that then fails (a bad message late in it, a streamed wave aborted after its chunks) must leave the store as
+    it was: the undo records take every raised cell back (k_undo_applied).  Waves of growing states over known
+    replicas, so nearly every entry raises its cell, several messages per key."""
+    rng = np.random.default_rng(70 + eb)
+    n_keys = 200
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, 8, eb, stable)
+    cl = Cluster(rng, n_keys, 5, eb, stable)
+    keys = rng.integers(0, n_keys, 3000).astype(np.uint32)
+    msgs = [cl.message(int(k), grow=0.3) for k in keys]
+    assert pr.oracle(keys, msgs) == (None, 0)
+    pr.s.merge_json(keys, msgs)  # every replica known from here on
+    pr.check()
+    keys = rng.integers(0, n_keys, 3000).astype(np.uint32)
+    msgs = [cl.message(int(k), grow=0.0) for k in keys]  # larger values, the same replicas
+    bad_msgs = list(msgs)
+    bad_msgs[2990] = b'{"pVector":{},"nVector":{}'
+    with pytest.raises(jg.JanusError) as e:
+        pr.s.merge_json(keys, bad_msgs)
+    assert e.value.code == jg.JG_EINVAL and e.value.bad_msg == 2990
+    pr.check()  # every raise undone
+    # the same as a device-resident wave, and as a streamed wave that is aborted after its appends
+    w = jg.Wave(ctx, 3000, 4 << 20)
+    w.upload(keys, bad_msgs)
+    with pytest.raises(jg.JanusError):
+        pr.s.merge_wave(w)
+    pr.check()
+    w.close()
+    pr.s.wave_begin(3000, 4 << 20)
+    for c in range(0, 3000, 1000):
+        pr.s.wave_append(keys[c:c + 1000], msgs[c:c + 1000])
+    pr.s.wave_abort()
+    pr.check()
+    assert pr.oracle(keys, msgs) == (None, 0)
+    pr.s.merge_json(keys, msgs)
     pr.check()
     pr.close()
 
