@@ -364,7 +364,12 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
     } else {
         __shared__ GroupShared<G> sh;
         const uint32_t grp = threadIdx.x / G, g = threadIdx.x % G;
-        const uint64_t m = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + grp;
+        // workgroups take the messages from the wave's end: the fused apply then meets a key's newest state first
+        // (states grow along a wave), and its older ones settle with a plain read instead of raising the cell
+        // again (C1: ~3000 states per hot key per wave — in commit order each raised the cell, an atomic and an
+        // undo record apiece)
+        const uint64_t bx = gridDim.x - 1 - blockIdx.x;
+        const uint64_t m = m0 + bx * GroupShared<G>::kGroups + grp;
         // a node wave (csrc/node.hip) holds every kind's messages: those of other kinds carry kSkipIdx
         const bool skip = m < m1 && rows[m] == jg::kSkipIdx;
         const bool live = m < m1 && !skip;
@@ -402,7 +407,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             const uint32_t gq = gp.tg[u] >> 16, k = gp.tg[u] & 0xFFFFu;
             const uint32_t fq = sh.flags[gq];
             if (!gp.has[u] || (fq & (kSlow | kDup))) continue;
-            const uint64_t mq = m0 + (uint64_t)blockIdx.x * GroupShared<G>::kGroups + gq;
+            const uint64_t mq = m0 + bx * GroupShared<G>::kGroups + gq;
             const uint32_t vv = k < tk_kn(sh.tk[gq]) ? 0 : 1;
             const uint32_t e = vv ? k - 2 : k - 1;  // entry index: tokens minus the names before it
             uint8_t* h = emit + mq * emit_stride(EB);
