@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 7
+#define JG_ABI_VERSION 8
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -482,6 +482,16 @@ int jg_comm_last_stats(jg_comm* comm, jg_exchange_stats* out);
  * each payload's SHA256 (zeros for null).  Synchronous; JG_EINVAL on malformed offsets. */
 int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, const uint8_t* is_null, uint64_t n_updates,
                       const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);
+/* SHA256.HashData of n payloads (payload i = bytes[off[i], off[i+1]), off[0] = 0) into out (n * 32 bytes): the
+ * per-message hashes ComputeDigest takes (DAGUpdateMessage.cs:43), for a caller that assembles UpdateMessages
+ * later from payloads it already holds in one buffer (a page-locked `bytes` uploads in place).  Synchronous. */
+int jg_sha256_batch(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, uint8_t* out);
+/* ComputeDigest's second level from per-payload hashes the caller already has (jg_sha256_batch, or
+ * jg_update_digests' msg_digest): msg_digest[32i..32i+32) = SHA256 of payload i (ignored for a null payload,
+ * is_null[i] != 0: hashed as 32 zero bytes), update u = payloads [first[u], first[u+1]) as in jg_update_digests.
+ * digest[32u..) = the same bytes jg_update_digests gives.  Synchronous. */
+int jg_update_digests_of(jg_ctx* ctx, uint64_t n, const uint8_t* msg_digest, const uint8_t* is_null, uint64_t n_updates, const uint64_t* first,
+                         uint8_t* digest);
 /* The same over a wave already in device memory (jg_wave_upload; no null payloads): first[n_updates]
  * must equal the wave's message count. */
 int jg_wave_update_digests(const jg_wave* wave, uint64_t n_updates, const uint64_t* first, uint8_t* msg_digest, uint8_t* digest);

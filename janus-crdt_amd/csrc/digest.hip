@@ -292,6 +292,44 @@ uint64_t chain_offsets(const uint64_t* first, uint64_t n_upd, uint64_t* boff) {
 
 inline uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 
+// The second level from per-payload digests already on the device (D: n state-word digests, zeros for null):
+// update digests to the host (synchronous).
+void chain_digests(jg_ctx* ctx, const uint4* D, uint64_t n, uint64_t n_upd, const uint64_t* first, uint8_t* digest) {
+    if (n_upd == 0) return;
+    std::vector<uint64_t> hb(2 * (n_upd + 1));
+    std::memcpy(hb.data(), first, (n_upd + 1) * 8);
+    const uint64_t B = chain_offsets(first, n_upd, hb.data() + n_upd + 1);
+    char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, n_upd * 32 + hb.size() * 8 + B * 256 + 512));
+    auto* out = reinterpret_cast<uint4*>(s);
+    auto* d_first = reinterpret_cast<uint64_t*>(s + n_upd * 32);
+    uint64_t* d_boff = d_first + n_upd + 1;
+    auto* KW = reinterpret_cast<uint4*>(s + ((n_upd * 32 + hb.size() * 8 + 255) & ~255ull));
+    hipStream_t st = ctx->stream;
+    // from the context's page-locked write area when it fits (a pageable source is staged by the runtime)
+    const void* src = hb.data();
+    if (hb.size() * 8 <= jg::kPinBytes - jg::kPinRead) {
+        void* pin = static_cast<char*>(ctx->hstat) + jg::kPinRead;
+        std::memcpy(pin, hb.data(), hb.size() * 8);
+        src = pin;
+    }
+    JG_HIP(hipMemcpyAsync(d_first, src, hb.size() * 8, hipMemcpyHostToDevice, st));
+    k_sha_expand<<<grid_for(B), kBlock, 0, st>>>(D, d_first, d_boff, n_upd, KW);
+    k_sha_chain<<<chain_grid(n_upd), kChainBlock, 0, st>>>(KW, d_boff, n_upd, out);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(digest, out, n_upd * 32, hipMemcpyDeviceToHost, st));
+    JG_HIP(hipStreamSynchronize(st));
+}
+
+__global__ void k_zero_null(uint4* D, const uint8_t* is_null, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && is_null[i]) D[2 * i] = D[2 * i + 1] = make_uint4(0, 0, 0, 0);
+}
+
+// Digest bytes <-> SHA-256 state words (big-endian words), in place, on the device.
+__global__ void k_bswap_words(uint32_t* w, uint64_t n_words) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_words; i += (uint64_t)gridDim.x * kBlock) w[i] = __builtin_bswap32(w[i]);
+}
+
 // Both levels on device buffers already in place (d_bytes: payloads; d_off: n+1 offsets); results to host.
 void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, const uint8_t* d_null, uint64_t n, uint64_t n_upd,
                  const uint64_t* first, uint8_t* msg_digest, uint8_t* digest) {
@@ -347,6 +385,58 @@ int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_
         JG_HIP(hipMemcpyAsync(d_off, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
         if (is_null && n) JG_HIP(hipMemcpyAsync(d_null, is_null, n, hipMemcpyHostToDevice, st));
         run_digests(ctx, d_bytes, d_off, d_null, n, n_updates, first, msg_digest, digest);
+    });
+}
+
+int jg_sha256_batch(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, uint8_t* out) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
+        JG_REQUIRE(ctx && off && (out || n == 0), JG_EINVAL, "jg_sha256_batch: NULL argument");
+        JG_REQUIRE(n < 0xFFFFFFFFull * kBlock, JG_EINVAL, "jg_sha256_batch: too many payloads");
+        JG_REQUIRE(off[0] == 0, JG_EINVAL, "jg_sha256_batch: off[0] must be 0");
+        for (uint64_t i = 0; i < n; ++i)
+            JG_REQUIRE(off[i + 1] >= off[i], JG_EINVAL, "jg_sha256_batch: offsets decrease at payload %llu", (unsigned long long)i);
+        JG_REQUIRE(bytes || off[n] == 0, JG_EINVAL, "jg_sha256_batch: bytes is NULL");
+        if (n == 0) return;
+        jg::ensure_device(ctx);
+        const uint64_t nb = off[n];
+        char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch, ((nb + 15) & ~15ull) + (n + 1) * 8 + n * 32 + 256));
+        auto* d_bytes = reinterpret_cast<uint8_t*>(s);
+        auto* d_off = reinterpret_cast<uint64_t*>(s + ((nb + 15) & ~15ull));
+        auto* D = reinterpret_cast<uint4*>(s + ((((nb + 15) & ~15ull) + (n + 1) * 8 + 15) & ~15ull));
+        hipStream_t st = ctx->stream;
+        if (nb) JG_HIP(hipMemcpyAsync(d_bytes, bytes, nb, hipMemcpyHostToDevice, st));
+        JG_HIP(hipMemcpyAsync(d_off, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+        k_sha_msgs<false><<<grid_for(n), kBlock, 0, st>>>(d_bytes, d_off, nullptr, n, D);
+        k_bswap_words<<<std::min<uint64_t>(grid_for(n * 8), 4096), kBlock, 0, st>>>(reinterpret_cast<uint32_t*>(D), n * 8);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(out, D, n * 32, hipMemcpyDeviceToHost, st));
+        JG_HIP(hipStreamSynchronize(st));
+    });
+}
+
+int jg_update_digests_of(jg_ctx* ctx, uint64_t n, const uint8_t* msg_digest, const uint8_t* is_null, uint64_t n_updates, const uint64_t* first,
+                         uint8_t* digest) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(ctx);  // calls on one context are serialised (shared scratch, stream)
+        JG_REQUIRE(ctx && first && (msg_digest || n == 0) && (digest || n_updates == 0), JG_EINVAL, "jg_update_digests_of: NULL argument");
+        JG_REQUIRE(n < 0xFFFFFFFFull * kBlock, JG_EINVAL, "jg_update_digests_of: too many payloads");
+        check_first(n, n_updates, first);
+        if (n_updates == 0) return;
+        jg::ensure_device(ctx);
+        auto* D = static_cast<uint4*>(jg::scratch(ctx, ctx->scratch, n * 32 + n + 256));
+        auto* d_null = reinterpret_cast<uint8_t*>(D + 2 * n);  // D: two uint4 per digest
+        hipStream_t st = ctx->stream;
+        if (n) {
+            JG_HIP(hipMemcpyAsync(D, msg_digest, n * 32, hipMemcpyHostToDevice, st));
+            k_bswap_words<<<std::min<uint64_t>(grid_for(n * 8), 4096), kBlock, 0, st>>>(reinterpret_cast<uint32_t*>(D), n * 8);
+            if (is_null) {  // a null payload hashes as 32 zero bytes whatever its row holds
+                JG_HIP(hipMemcpyAsync(d_null, is_null, n, hipMemcpyHostToDevice, st));
+                k_zero_null<<<grid_for(n), kBlock, 0, st>>>(D, d_null, n);
+            }
+            JG_HIP(hipGetLastError());
+        }
+        chain_digests(ctx, D, n, n_updates, first, digest);
     });
 }
 

@@ -564,7 +564,8 @@ uint8_t* GpuStableStore::pinned_buf(size_t bytes) {
 }
 
 void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
-                                         const std::vector<size_t>& at, std::vector<std::string>& out) {
+                                         const std::vector<size_t>& at, std::vector<std::string>& out,
+                                         std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has) {
     flush_registrations();
     const size_t n = rows.size();
     std::vector<uint64_t> off(n + 1, 0);
@@ -578,9 +579,47 @@ void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, cons
     }
     check(rc);
     if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
+    std::vector<uint8_t> h;
+    if (sha && n) {  // from the page-locked output as it stands (uploaded in place)
+        h.resize(32 * n);
+        check(jg_sha256_batch(ctx_, n, off.data(), buf, h.data()));
+    }
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
-        for (size_t i = b; i < e; ++i) out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+        for (size_t i = b; i < e; ++i) {
+            out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+            if (!h.empty()) std::memcpy((*sha)[at[i]].data(), h.data() + 32 * i, 32), (*has)[at[i]] = 1;
+        }
     });
+}
+
+// ComputeDigests of msgs[first..] from per-payload SHA-256s: the ones not given (has[i] = 0: states queued by an earlier
+// call) hashed here, then the second level in one call (jg_update_digests_of).
+void GpuStableStore::DigestsOf(std::vector<UpdateMessage>& msgs, size_t first, std::vector<std::array<uint8_t, 32>>& sha,
+                               const std::vector<uint8_t>& has) {
+    if (first >= msgs.size()) return;
+    const size_t nu = msgs.size() - first;
+    std::vector<uint64_t> upd(nu + 1, 0);
+    for (size_t u = 0; u < nu; ++u) upd[u + 1] = upd[u] + msgs[first + u].update.size();
+    const size_t nm = upd[nu];
+    std::vector<const std::string*> miss;
+    std::vector<size_t> miss_at;
+    for (size_t u = 0, i = 0; u < nu; ++u)
+        for (const auto& np : msgs[first + u].update) {
+            if (!has[i]) miss.push_back(&np.message), miss_at.push_back(i);
+            ++i;
+        }
+    if (!miss.empty()) {
+        std::vector<uint64_t> off(miss.size() + 1, 0);
+        for (size_t k = 0; k < miss.size(); ++k) off[k + 1] = off[k] + miss[k]->size();
+        uint8_t* buf = pinned_buf(off.back() + 64);
+        for (size_t k = 0; k < miss.size(); ++k) std::memcpy(buf + off[k], miss[k]->data(), miss[k]->size());
+        std::vector<uint8_t> h(32 * miss.size());
+        check(jg_sha256_batch(ctx_, miss.size(), off.data(), buf, h.data()));
+        for (size_t k = 0; k < miss.size(); ++k) std::memcpy(sha[miss_at[k]].data(), h.data() + 32 * k, 32);
+    }
+    std::vector<uint8_t> dig(32 * nu);
+    check(jg_update_digests_of(ctx_, nm, reinterpret_cast<const uint8_t*>(sha.data()), nullptr, nu, upd.data(), dig.data()));
+    for (size_t u = 0; u < nu; ++u) std::memcpy(msgs[first + u].digest.data(), dig.data() + 32 * u, 32);
 }
 
 // ComputeDigests of msgs[first..] with the payloads gathered into page-locked staging by the workers.
@@ -623,7 +662,7 @@ std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector
 }
 
 std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids, const std::vector<uint64_t>* add_lim,
-                                                           const std::vector<uint64_t>* rem_lim) {
+                                                           const std::vector<uint64_t>* rem_lim, std::vector<std::array<uint8_t, 32>>* sha) {
     flush_names();  // every element this mirror interned is in the engine's element table
     std::vector<uint32_t> sets;
     sets.reserve(uids.size());
@@ -641,6 +680,10 @@ std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Gui
         rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_);
     }
     check(rc);
+    if (sha) {  // SHA-256 of each state from the page-locked output (uploaded in place)
+        sha->resize(n);
+        if (n) check(jg_sha256_batch(ctx_, n, off.data(), buf, reinterpret_cast<uint8_t*>(sha->data())));
+    }
     std::vector<std::string> out(n);
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
         for (size_t i = b; i < e; ++i) out[i].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
@@ -740,6 +783,8 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     //    op runs in round 0.
     std::vector<uint8_t> result(n, 1);
     std::vector<std::string> snap(n);
+    std::vector<std::array<uint8_t, 32>> ssha(n);  // each snapshot's SHA-256, taken where it was encoded
+    std::vector<uint8_t> shas(n, 0);
     std::vector<uint32_t> round(n, 0);
     uint32_t n_rounds = 1;
     {
@@ -803,7 +848,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             }
             for (size_t i : idx)
                 if (kref[i]->type == CrdtType::PNCounter) pnc_after_[kref[i]->idx] = {0, 0};
-            EncodePNCRowsBefore(prow, dp, dn, at, snap);
+            EncodePNCRowsBefore(prow, dp, dn, at, snap, &ssha, &shas);
         }
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;
@@ -815,8 +860,13 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                 al.push_back(alim[j]);
                 rl.push_back(rlim[j]);
             }
-            auto enc = EncodeORSetStates(ou, &al, &rl);
-            for (size_t k = 0; k < or_need.size(); ++k) snap[idx[or_need[k]]] = std::move(enc[k]);
+            std::vector<std::array<uint8_t, 32>> esha;
+            auto enc = EncodeORSetStates(ou, &al, &rl, &esha);
+            for (size_t k = 0; k < or_need.size(); ++k) {
+                snap[idx[or_need[k]]] = std::move(enc[k]);
+                ssha[idx[or_need[k]]] = esha[k];
+                shas[idx[or_need[k]]] = 1;
+            }
         }
         if (trace) t_enc_o += now() - tc;
     }
@@ -824,16 +874,21 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
     //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).
     const size_t s0 = submitted.size();
+    std::vector<std::array<uint8_t, 32>> msha;  // per submitted payload, in UpdateMessage order
+    std::vector<uint8_t> mhas;
     for (Flush& f : flushes) {
         UpdateMessage um;
         for (auto& e : f.msgs) {
+            const bool mine = e.op != kOld && shas[(size_t)e.op];
+            msha.push_back(mine ? ssha[(size_t)e.op] : std::array<uint8_t, 32>{});
+            mhas.push_back(mine ? 1 : 0);
             if (e.op != kOld) e.np.message = std::move(snap[(size_t)e.op]);  // each snapshot goes to one message
             um.update.push_back(std::move(e.np));
         }
         submitted.push_back(std::move(um));
     }
     if (trace) tt[3] = now();
-    DigestsPinned(submitted, s0);
+    DigestsOf(submitted, s0, msha, mhas);
     if (trace) tt[4] = now();
     for (size_t j = head; j < q.size(); ++j) {
         if (q[j].op != kOld) q[j].np.message = std::move(snap[(size_t)q[j].op]);

@@ -205,7 +205,8 @@ class GpuStableStore {
     // arrival ordinals (addSet elements in ascending interned id).  add_lim / rem_lim: each state as of those ord
     // limits (a snapshot before a batch's later ops, ApplyOps' limits).
     std::vector<std::string> EncodeORSetStates(const std::vector<Guid>& uids, const std::vector<uint64_t>* add_lim = nullptr,
-                                               const std::vector<uint64_t>* rem_lim = nullptr);
+                                               const std::vector<uint64_t>* rem_lim = nullptr,
+                                               std::vector<std::array<uint8_t, 32>>* sha = nullptr);
     // Identity of the next message SubmitClientUpdates creates (NetworkProtocol.seq; the reference keys
     // its safe-update tracker by message object, so identities only need to be unique per process).
     void SetNextMessageSeq(uint64_t seq) { next_seq_ = seq; }
@@ -248,9 +249,14 @@ class GpuStableStore {
                                   const KeyRef* const* refs);
     // PN-Counter snapshots of rows rewound by (dp, dn) into out[at[i]] (jg_pnc_encode_json_before, one call into
     // page-locked memory, the strings built by the workers)
+    // sha (optional): SHA-256 of snapshot i into (*sha)[at[i]], (*has)[at[i]] = 1, hashed from the encoder's page-locked
+    // output (jg_sha256_batch) — ComputeDigest's first level without a second copy of the payloads
     void EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
-                             const std::vector<size_t>& at, std::vector<std::string>& out);
+                             const std::vector<size_t>& at, std::vector<std::string>& out,
+                             std::vector<std::array<uint8_t, 32>>* sha = nullptr, std::vector<uint8_t>* has = nullptr);
     void DigestsPinned(std::vector<UpdateMessage>& msgs, size_t first);  // ComputeDigests through page-locked staging
+    // ComputeDigests from per-payload SHA-256s (sha[i]: payload i of msgs[first..] in order; has[i] = 0: hash it here)
+    void DigestsOf(std::vector<UpdateMessage>& msgs, size_t first, std::vector<std::array<uint8_t, 32>>& sha, const std::vector<uint8_t>& has);
     uint8_t* pinned_buf(size_t bytes);  // a page-locked buffer of at least `bytes`, kept across calls
     uint8_t* pin_buf_ = nullptr;
     size_t pin_cap_ = 0;

@@ -35,7 +35,7 @@ EXPORTS = [
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
-    "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256",
+    "jg_update_digests", "jg_wave_update_digests", "jg_waves_update_digests", "jg_wave_sha256", "jg_sha256_batch", "jg_update_digests_of",
     "jg_node_create", "jg_node_destroy", "jg_node_register", "jg_node_set_shard", "jg_shard_of", "jg_node_last_stats",
     "jg_tracker_create", "jg_tracker_destroy", "jg_tracker_add", "jg_tracker_size", "jg_tracker_contains",
     "jg_apply_committed", "jg_apply_block", "jg_apply_stream_begin", "jg_apply_stream_append", "jg_apply_stream_end",
@@ -87,6 +87,8 @@ _SIGS = {
     "jg_wave_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_waves_update_digests": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_wave_sha256": ([_vp, _vp, C.c_uint8], C.c_int),
+    "jg_sha256_batch": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
+    "jg_update_digests_of": ([_vp, _u64, _vp, _vp, _u64, _vp, _vp], C.c_int),
     "jg_wave_upload": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
     "jg_pnc_merge_wave": ([_vp, _vp, C.POINTER(_u64)], C.c_int),
     "jg_host_alloc": ([_vp, _u64, C.POINTER(_vp)], C.c_int),
@@ -466,6 +468,25 @@ def update_digests(ctx: Context, msgs, first, msg_digests: bool = False):
     _check(load().jg_update_digests(ctx.handle, len(msgs), _ptr(off), _ptr(data), _ptr(is_null) if is_null.any() else None, nu,
                                     _ptr(first), _ptr(md), _ptr(dig)))
     return (dig, md) if msg_digests else dig
+
+
+def sha256_batch(ctx: Context, msgs) -> np.ndarray:
+    """SHA-256 of every payload (jg_sha256_batch): u8[n, 32]."""
+    data, off = pack_wave(list(msgs))
+    out = np.zeros((len(msgs), 32), np.uint8)
+    _check(load().jg_sha256_batch(ctx.handle, len(msgs), _ptr(off), _ptr(data), _ptr(out)))
+    return out
+
+
+def update_digests_of(ctx: Context, msg_digests, first, is_null=None) -> np.ndarray:
+    """ComputeDigest's second level from per-payload SHA-256s (jg_update_digests_of): u8[n_updates, 32]."""
+    md = np.ascontiguousarray(msg_digests, np.uint8).reshape(-1, 32)
+    first = _arr(first, np.uint64)
+    nu = first.size - 1
+    dig = np.zeros((max(nu, 0), 32), np.uint8)
+    nl = None if is_null is None else np.ascontiguousarray(is_null, np.uint8)
+    _check(load().jg_update_digests_of(ctx.handle, md.shape[0], _ptr(md), _ptr(nl) if nl is not None else None, nu, _ptr(first), _ptr(dig)))
+    return dig
 
 
 def records(key=None, tag_lo=None, tag_hi=None, n: int = 0, ord=None) -> np.ndarray:

@@ -110,6 +110,30 @@ def test_gpu_updates_nulls_and_empty(ctx):
 
 
 @pytest.mark.gpu
+def test_gpu_sha256_batch_and_second_level_of(ctx):
+    """jg_sha256_batch = hashlib per payload; jg_update_digests_of over those hashes = jg_update_digests over the
+    payloads (nulls zeroed whatever their rows hold, rent boundaries, empty updates) — the producer path hashes
+    each snapshot where it was encoded and takes the second level from the hashes (host/janus_host.cpp DigestsOf)."""
+    import janus_gpu as jg
+    rng = np.random.default_rng(14)
+    msgs = random_msgs(rng, 3000, 0, 1500, null_every=9)
+    h = jg.sha256_batch(ctx, [b"" if m is None else m for m in msgs])
+    for i in range(0, 3000, 37):
+        assert h[i].tobytes() == hashlib.sha256(b"" if msgs[i] is None else msgs[i]).digest()
+    sizes = [0, 1, 2, 31, 32, 33, 1000, 0, 1901]
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    assert first[-1] == len(msgs)
+    is_null = np.array([m is None for m in msgs], np.uint8)
+    got = jg.update_digests_of(ctx, h, first, is_null)
+    want = jg.update_digests(ctx, msgs, first)
+    assert np.array_equal(got, want)
+    for u in range(len(sizes)):
+        assert got[u].tobytes() == py_digest(msgs[first[u]:first[u + 1]])
+    assert jg.sha256_batch(ctx, []).shape == (0, 32)
+    assert jg.update_digests_of(ctx, np.zeros((0, 32), np.uint8), [0]).shape == (0, 32)
+
+
+@pytest.mark.gpu
 def test_gpu_no_updates_and_all_null(ctx):
     import janus_gpu as jg
     d = jg.update_digests(ctx, [], [0])
