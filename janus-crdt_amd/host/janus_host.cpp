@@ -703,12 +703,16 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     // the wrappers' checks, before anything is applied or queued: every op's key resolved by the workers (read-only
     // lookups), the first failing op then raises its error as the serial loop would
     std::vector<const KeyRef*> kref(n);
+    // each op's key as plain arrays: the serial walks below would chase every KeyRef through the uid map's nodes
+    std::vector<uint32_t> krow(n);
+    std::vector<uint8_t> kpn(n);  // 1: a PN-Counter key
     std::vector<size_t> first_bad(pool().size(), n);
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
         for (size_t i = b; i < e; ++i) {
             const auto it = uids_.find(ups[i].op.uid);
             const KeyRef* kr = it == uids_.end() ? nullptr : &it->second;
             kref[i] = kr;
+            if (kr) krow[i] = kr->idx, kpn[i] = kr->type == CrdtType::PNCounter ? 1 : 0;
             if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
                 first_bad[t] = i;
                 return;
@@ -720,53 +724,80 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         if (!kref[bad]) throw EngineError(JG_EINVAL, "unknown CRDT uid");
         throw EngineError(JG_EINVAL, kref[bad]->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
     }
+    const double t_chk = trace ? now() : 0;
     // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
     //    q entries: message, op index (kOld: queued by an earlier call), and whether SafeCRDT.Update
     //    tracked it.  The batcher's safeUpdateTracker.ContainsKey(msg) (:176) is that flag: a message the
     //    batcher drains has not been submitted yet, so nothing can have removed its entry.
     constexpr int64_t kOld = -1;
-    struct QE { NetworkProtocol np; int64_t op; bool tracked; };
-    std::vector<QE> q;
-    for (auto& e : batch_queue_) q.push_back(QE{std::move(e.first), kOld, e.second});
+    struct QE { int64_t op; uint32_t old; bool tracked; };  // op: a client op of this call, or kOld: oldq[old]
+    std::vector<std::pair<NetworkProtocol, bool>> oldq = std::move(batch_queue_);
     batch_queue_.clear();
-    struct Flush { std::vector<QE> msgs; };
-    std::vector<Flush> flushes;
+    std::vector<QE> q;
+    q.reserve(oldq.size() + n);
+    for (size_t k = 0; k < oldq.size(); ++k) q.push_back(QE{kOld, (uint32_t)k, oldq[k].second});
+    const uint64_t seq0 = next_seq_;  // op i's message carries seq0 + i (next_seq_++ per Update)
+    next_seq_ += n;
+    // (a) serial and light: which queue entries each flush drains, and the one it loses.  A flush drains the whole
+    //     queue unless its safe entries reach clientBatchSize first; the entry dequeued then is lost (:175).
+    struct Range { size_t h0, h1; };
+    std::vector<Range> ranges;
     size_t head = 0;  // q[head..] is the live queue
-    q.reserve(q.size() + n);
     std::vector<uint64_t> t_seq, t_org;  // SafeCRDT.Update's TryAdds, handed to the tracker in one call after the loop
-    std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared` (first appearance), per flush
-    pos.reserve(2 * (size_t)std::max(clientBatchSize, 1));
     for (size_t i = 0; i < n; ++i) {
-        NetworkProtocol np;
-        np.uid = ups[i].op.uid;
-        np.syncMsgType = NetworkProtocol::CRDTMsg;
-        np.seq = next_seq_++;
         const bool tracked = ups[i].isSafe && ups[i].origin != 0;  // SafeCRDT.cs:55-56
-        if (tracked) t_seq.push_back(np.seq), t_org.push_back(ups[i].origin);
-        q.push_back(QE{std::move(np), (int64_t)i, tracked});
+        if (tracked) t_seq.push_back(seq0 + i), t_org.push_back(ups[i].origin);
+        q.push_back(QE{(int64_t)i, 0, tracked});
         if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
-            std::vector<QE> safe, appeared;
-            pos.clear();
+            const size_t h0 = head;
+            size_t safe_n = 0, kept = 0, end = 0;
             while (head < q.size()) {
-                QE e = std::move(q[head++]);                          // TryDequeue first ...
-                if (!((int)safe.size() < clientBatchSize)) break;     // ... so this one is lost (:175)
-                if (!e.tracked) {
-                    auto it = pos.find(e.np.uid);
-                    if (it == pos.end()) { pos.emplace(e.np.uid, appeared.size()); appeared.push_back(std::move(e)); }
-                    else appeared[it->second] = std::move(e);        // last state wins, position kept
-                } else {
-                    safe.push_back(std::move(e));
-                }
+                const size_t k = head++;                              // TryDequeue first ...
+                if (!((int)safe_n < clientBatchSize)) break;          // ... so this one is lost (:175)
+                if (q[k].tracked) ++safe_n;
+                ++kept;
+                end = head;
             }
-            for (auto& e : appeared) safe.push_back(std::move(e));
-            if (!safe.empty()) {
-                flushes.push_back(Flush{std::move(safe)});
+            if (kept) {
+                ranges.push_back(Range{h0, end});
                 last_submit_ms_ = ups[i].now_ms;
             }
         }
     }
+    const double t_sim = trace ? now() : 0;
+    // (b) each flush's messages by the workers (flushes are independent): safe states in queue order, then the
+    //     non-safe ones compacted per uid (first appearance keeps its place, the last state wins)
+    struct Flush { std::vector<QE> msgs; };
+    std::vector<Flush> flushes(ranges.size());
+    auto uid_of = [&](const QE& e) -> const Guid& { return e.op == kOld ? oldq[e.old].first.uid : ups[(size_t)e.op].op.uid; };
+    parallel_ranges(pool(), ranges.size(), [&](size_t rb, size_t re, int) {
+        std::unordered_map<Guid, size_t, GuidHash> pos;  // uid -> slot in `appeared`
+        pos.reserve(2 * (size_t)std::max(clientBatchSize, 1));
+        std::vector<QE> appeared;
+        for (size_t r = rb; r < re; ++r) {
+            std::vector<QE>& safe = flushes[r].msgs;
+            pos.clear();
+            appeared.clear();
+            for (size_t k = ranges[r].h0; k < ranges[r].h1; ++k) {
+                const QE& e = q[k];
+                if (!e.tracked) {
+                    auto it = pos.find(uid_of(e));
+                    if (it == pos.end()) pos.emplace(uid_of(e), appeared.size()), appeared.push_back(e);
+                    else appeared[it->second] = e;
+                } else {
+                    safe.push_back(e);
+                }
+            }
+            safe.insert(safe.end(), appeared.begin(), appeared.end());
+        }
+    });
+    const double t_fl = trace ? now() : 0;
     tracker.add_many(t_seq.size(), t_seq.data(), t_org.data());
-    if (trace) tt[1] = now();
+    if (trace) {
+        tt[1] = now();
+        std::fprintf(stderr, "SubmitClientUpdates: checks %.1f ms, batcher walk %.1f ms, flushes %.1f ms, tracker adds %.1f ms\n", t_chk - tt[0],
+                     t_sim - t_chk, t_fl - t_sim, tt[1] - t_fl);
+    }
     // 2. Which ops' snapshots are needed: those submitted now or still queued.
     std::vector<uint8_t> need(n, 0);
     for (const Flush& f : flushes)
@@ -790,8 +821,8 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     {
         std::unordered_map<uint32_t, std::pair<uint32_t, bool>> st;  // OR-Set set -> (its round, a snapshot needed in it)
         for (size_t i = 0; i < n; ++i) {
-            if (kref[i]->type == CrdtType::PNCounter) continue;
-            auto& e = st[kref[i]->idx];
+            if (kpn[i]) continue;
+            auto& e = st[krow[i]];
             if (ups[i].op.opId == 3 && e.second) ++e.first, e.second = false;
             round[i] = e.first;
             if (need[i]) e.second = true;
@@ -803,26 +834,55 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         for (size_t i = 0; i < n; ++i)
             if (round[i] == rd) idx.push_back(i);
         if (idx.empty()) continue;
+        // PN-Counter ops straight to the store as (row, amount, P or N) arrays the workers fill (no ClientOp copies);
+        // OR-Set ops through ApplyOps (element ids interned in op order on the host)
         std::vector<ClientOp> ops;
         std::vector<const KeyRef*> rr;
-        ops.reserve(idx.size());
-        rr.reserve(idx.size());
+        std::vector<size_t> opos, ppos;  // positions in idx of the round's OR-Set / PN-Counter ops
         bool or_snap = false;
-        for (size_t i : idx) {
+        for (size_t j = 0; j < idx.size(); ++j) {
+            const size_t i = idx[j];
+            if (kpn[i]) {
+                ppos.push_back(j);
+                continue;
+            }
             ops.push_back(ups[i].op);
             rr.push_back(kref[i]);
-            or_snap |= need[i] && kref[i]->type == CrdtType::ORSet;
+            opos.push_back(j);
+            or_snap |= need[i] != 0;
         }
-        std::vector<uint64_t> alim, rlim;
+        std::vector<uint64_t> alim(or_snap ? idx.size() : 0), rlim(or_snap ? idx.size() : 0);
         const double ta = trace ? now() : 0;
-        const auto r = ApplyOps(ops, or_snap ? &alim : nullptr, or_snap ? &rlim : nullptr, rr.data());
+        if (!ppos.empty()) {
+            std::vector<uint32_t> pkey(ppos.size()), pcol(ppos.size(), 0);
+            std::vector<int64_t> pdelta(ppos.size());
+            std::vector<uint8_t> pisn(ppos.size());
+            parallel_ranges(pool(), ppos.size(), [&](size_t b, size_t e, int) {
+                for (size_t k = b; k < e; ++k) {
+                    const size_t i = idx[ppos[k]];
+                    const ClientOp& op = ups[i].op;
+                    pkey[k] = krow[i];
+                    pdelta[k] = eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount;
+                    pisn[k] = op.opId == 2 ? 1 : 0;
+                }
+            });
+            materialize_names();
+            check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
+        }
+        if (!ops.empty()) {
+            std::vector<uint64_t> al, rl;
+            const auto r = ApplyOps(ops, or_snap ? &al : nullptr, or_snap ? &rl : nullptr, rr.data());
+            for (size_t k = 0; k < opos.size(); ++k) {
+                result[idx[opos[k]]] = r[k];
+                if (or_snap) alim[opos[k]] = al[k], rlim[opos[k]] = rl[k];
+            }
+        }
         const double tb = trace ? now() : 0;
         t_apply += tb - ta;
         ++n_chunks;
-        for (size_t j = 0; j < idx.size(); ++j) result[idx[j]] = r[j];
         std::vector<size_t> pnc_need, or_need;  // positions in idx
         for (size_t j = 0; j < idx.size(); ++j)
-            if (need[idx[j]]) (kref[idx[j]]->type == CrdtType::PNCounter ? pnc_need : or_need).push_back(j);
+            if (need[idx[j]]) (kpn[idx[j]] ? pnc_need : or_need).push_back(j);
         if (!pnc_need.empty()) {
             // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
             // cells: walk the round backwards, per row (a row-indexed array, its touched entries reset after)
@@ -833,21 +893,21 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             size_t w = pnc_need.size();
             for (size_t j = idx.size(); j-- > 0;) {
                 const size_t i = idx[j];
-                if (kref[i]->type != CrdtType::PNCounter) continue;
+                if (!kpn[i]) continue;
                 const ClientOp& op = ups[i].op;
-                auto& a = pnc_after_[kref[i]->idx];
+                auto& a = pnc_after_[krow[i]];
                 if (w && pnc_need[w - 1] == j) {
                     --w;
                     dp[w] = (int64_t)a.first;
                     dn[w] = (int64_t)a.second;
-                    prow[w] = kref[i]->idx;
+                    prow[w] = krow[i];
                     at[w] = i;
                 }
                 const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
                 (op.opId == 2 ? a.second : a.first) += amt;
             }
             for (size_t i : idx)
-                if (kref[i]->type == CrdtType::PNCounter) pnc_after_[kref[i]->idx] = {0, 0};
+                if (kpn[i]) pnc_after_[krow[i]] = {0, 0};
             EncodePNCRowsBefore(prow, dp, dn, at, snap, &ssha, &shas);
         }
         const double tc = trace ? now() : 0;
@@ -874,25 +934,36 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
     //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).
     const size_t s0 = submitted.size();
-    std::vector<std::array<uint8_t, 32>> msha;  // per submitted payload, in UpdateMessage order
-    std::vector<uint8_t> mhas;
-    for (Flush& f : flushes) {
-        UpdateMessage um;
-        for (auto& e : f.msgs) {
-            const bool mine = e.op != kOld && shas[(size_t)e.op];
-            msha.push_back(mine ? ssha[(size_t)e.op] : std::array<uint8_t, 32>{});
-            mhas.push_back(mine ? 1 : 0);
-            if (e.op != kOld) e.np.message = std::move(snap[(size_t)e.op]);  // each snapshot goes to one message
-            um.update.push_back(std::move(e.np));
+    auto make_np = [&](const QE& e) {  // the queued message with its state (each snapshot goes to one message)
+        if (e.op == kOld) return std::move(oldq[e.old].first);
+        NetworkProtocol np;
+        np.uid = ups[(size_t)e.op].op.uid;
+        np.syncMsgType = NetworkProtocol::CRDTMsg;
+        np.seq = seq0 + (uint64_t)e.op;
+        np.message = std::move(snap[(size_t)e.op]);
+        return np;
+    };
+    std::vector<size_t> mo(flushes.size() + 1, 0);  // first payload of each new UpdateMessage
+    for (size_t f = 0; f < flushes.size(); ++f) mo[f + 1] = mo[f] + flushes[f].msgs.size();
+    std::vector<std::array<uint8_t, 32>> msha(mo.back());  // per submitted payload, in UpdateMessage order
+    std::vector<uint8_t> mhas(mo.back(), 0);
+    submitted.resize(s0 + flushes.size());
+    parallel_ranges(pool(), flushes.size(), [&](size_t fb, size_t fe, int) {
+        for (size_t f = fb; f < fe; ++f) {
+            UpdateMessage& um = submitted[s0 + f];
+            um.update.reserve(flushes[f].msgs.size());
+            for (size_t j = 0; j < flushes[f].msgs.size(); ++j) {
+                const QE& e = flushes[f].msgs[j];
+                if (e.op != kOld && shas[(size_t)e.op]) msha[mo[f] + j] = ssha[(size_t)e.op], mhas[mo[f] + j] = 1;
+                um.update.push_back(make_np(e));
+            }
         }
-        submitted.push_back(std::move(um));
-    }
+    });
     if (trace) tt[3] = now();
     DigestsOf(submitted, s0, msha, mhas);
     if (trace) tt[4] = now();
     for (size_t j = head; j < q.size(); ++j) {
-        if (q[j].op != kOld) q[j].np.message = std::move(snap[(size_t)q[j].op]);
-        batch_queue_.emplace_back(std::move(q[j].np), q[j].tracked);
+        batch_queue_.emplace_back(make_np(q[j]), q[j].tracked);
     }
     if (trace)
         std::fprintf(stderr, "SubmitClientUpdates(%zu ops): checks + batcher %.1f ms, %zu rounds: apply %.1f ms, PN-Counter snapshots %.1f ms, "
