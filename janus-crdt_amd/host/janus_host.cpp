@@ -144,11 +144,14 @@ size_t SafeUpdateTracker::size() const {
 
 namespace {
 // Static contiguous split of [0, n) over the pool's workers: fn(begin, end, worker).
-template <class F> void parallel_ranges(jg::WorkerPool& pool, size_t n, F&& fn) {
-    static const size_t min_par = [] {  // below this many items a phase runs inline
+// min_items: below this many items the phase runs inline (default JANUS_HOST_PAR_MIN or 8192: element-wise
+// loops; a loop over heavy items — a batcher flush of ~1000 messages — passes its own)
+template <class F> void parallel_ranges(jg::WorkerPool& pool, size_t n, F&& fn, size_t min_items = 0) {
+    static const size_t min_par_default = [] {
         const char* e = std::getenv("JANUS_HOST_PAR_MIN");
         return e ? (size_t)std::strtoull(e, nullptr, 10) : size_t{8192};
     }();
+    const size_t min_par = min_items ? min_items : min_par_default;
     const int T = pool.size();
     if (T <= 1 || n < min_par || n < (size_t)T) {
         fn(size_t{0}, n, 0);
@@ -790,7 +793,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             }
             safe.insert(safe.end(), appeared.begin(), appeared.end());
         }
-    });
+    }, 32);
     const double t_fl = trace ? now() : 0;
     tracker.add_many(t_seq.size(), t_seq.data(), t_org.data());
     if (trace) {
@@ -958,7 +961,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                 um.update.push_back(make_np(e));
             }
         }
-    });
+    }, 32);
     if (trace) tt[3] = now();
     DigestsOf(submitted, s0, msha, mhas);
     if (trace) tt[4] = now();
