@@ -61,18 +61,23 @@ const GpuStableStore::KeyRef& GpuStableStore::ref(const Guid& uid, CrdtType want
 uint32_t GpuStableStore::elem_id(uint32_t set, const std::optional<std::string>& e, bool create) {
     if (!e) return JG_NULL_ELEM;
     materialize_names();
-    SetKey& s = sets_[set];
+    return elem_id_in(sets_[set], create ? &pending_names_[set] : nullptr, *e, create);
+}
+
+// One set's interning (the caller has materialized the names; pn: the set's pending entry, when creating).  Touches
+// only this set's tables: the producer path runs it for different sets on different workers.
+uint32_t GpuStableStore::elem_id_in(SetKey& s, PendingNames* pn, const std::string& e, bool create) {
     for (; s.indexed < s.names.size(); ++s.indexed) s.elems.emplace(s.names[s.indexed], s.indexed);  // ids a wave issued
-    auto it = s.elems.find(*e);
+    auto it = s.elems.find(e);
     if (it != s.elems.end()) return it->second;
     if (!create) return JG_NULL_ELEM - 1;  // never allocated: no records carry it
     // ids only grow (also across Clear), so ascending id = insertion order into the add Dictionary
     const uint32_t id = (uint32_t)s.names.size();
     if (id >= JG_NULL_ELEM - 1) throw EngineError(JG_ESTATE, "too many elements in one OR-Set");
-    s.elems.emplace(*e, id);
-    s.names.push_back(*e);
+    s.elems.emplace(e, id);
+    s.names.push_back(e);
     s.indexed = (uint32_t)s.names.size();
-    pending_names_[set].ids.push_back(id);
+    pn->ids.push_back(id);
     return id;
 }
 
@@ -449,6 +454,7 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
 
 std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
                                               const KeyRef* const* refs) {
+    const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3;
     materialize_names();
     std::vector<uint8_t> result(ops.size(), 1);
     std::vector<uint32_t> pkey, pcol;
@@ -473,6 +479,47 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
         refs = found.data();
     }
     pkey.reserve(ops.size()), pcol.reserve(ops.size()), pdelta.reserve(ops.size()), pisn.reserve(ops.size());
+    // the OR-Set ops' element ids, interned per set in op order (sets are independent: a large batch by the
+    // workers, each taking the sets with set % T == its index; the pending-name entries made first, serially)
+    std::vector<uint32_t> oid(ops.size(), 0);
+    std::vector<uint8_t> oid_done(ops.size(), 0);
+    if (ops.size() >= 4096) {
+        std::vector<size_t> ors;
+        for (size_t i = 0; i < ops.size(); ++i)
+            if (refs[i]->type == CrdtType::ORSet) {
+                ors.push_back(i);
+                if (ops[i].opId != 2) (void)pending_names_[refs[i]->idx];
+            }
+        const size_t T = (size_t)std::max(1, pool().size());
+        std::vector<std::string> err(T);
+        parallel_ranges(pool(), T, [&](size_t tb0, size_t te0, int) {
+            for (size_t t = tb0; t < te0; ++t)
+                try {
+                    for (size_t i : ors) {
+                        const uint32_t set = refs[i]->idx;
+                        if (set % T != t) continue;
+                        const ClientOp& op = ops[i];
+                        SetKey& sk = sets_[set];
+                        if (op.opId == 3) {
+                            sk.elems.clear();
+                            sk.indexed = (uint32_t)sk.names.size();  // every id issued so far is dead
+                            PendingNames& pn = pending_names_.find(set)->second;
+                            pn.cleared = true;
+                            pn.ids.clear();
+                        } else if (op.elem) {
+                            oid[i] = elem_id_in(sk, op.opId == 1 ? &pending_names_.find(set)->second : nullptr, *op.elem, op.opId == 1);
+                        } else {
+                            oid[i] = JG_NULL_ELEM;
+                        }
+                        oid_done[i] = 1;
+                    }
+                } catch (const std::exception& e) {
+                    err[t] = e.what();
+                }
+        }, 2);
+        for (const auto& e : err)
+            if (!e.empty()) throw EngineError(JG_ESTATE, e);
+    }
     for (size_t i = 0; i < ops.size(); ++i) {
         const ClientOp& op = ops[i];
         const KeyRef& kr = *refs[i];
@@ -488,7 +535,8 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
             // carries (Contains is false, ORSet.cs:174); Clear empties the Dictionaries, so elements
             // added afterwards take new, larger ids in their new insertion order (ORSet.cs:192-198)
             uint32_t id = 0;
-            if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
+            if (oid_done[i]) id = oid[i];  // interned by the workers above (Clear included)
+            else if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
             else if (op.opId == 2) id = elem_id(kr.idx, op.elem, false);
             else {
                 sk.elems.clear();
@@ -504,6 +552,9 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
             oidx.push_back(i);
         }
     }
+    static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t1 = trace ? now() : 0;
     if (!pkey.empty()) check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
     if (!oset.empty()) {
         std::vector<uint8_t> r(oset.size());
@@ -519,6 +570,7 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
         }
         for (size_t j = 0; j < oidx.size(); ++j) result[oidx[j]] = r[j];
     }
+    if (trace) std::fprintf(stderr, "ApplyOps(%zu): host prep %.1f ms, device %.1f ms\n", ops.size(), t1 - t0, now() - t1);
     return result;
 }
 
@@ -569,6 +621,7 @@ uint8_t* GpuStableStore::pinned_buf(size_t bytes) {
 void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
                                          const std::vector<size_t>& at, std::vector<std::string>& out,
                                          std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has) {
+    const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3;
     flush_registrations();
     const size_t n = rows.size();
     std::vector<uint64_t> off(n + 1, 0);
@@ -581,18 +634,23 @@ void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, cons
         rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_);
     }
     check(rc);
+    static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t1 = trace ? now() : 0;
     if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
     std::vector<uint8_t> h;
     if (sha && n) {  // from the page-locked output as it stands (uploaded in place)
         h.resize(32 * n);
         check(jg_sha256_batch(ctx_, n, off.data(), buf, h.data()));
     }
+    const double t2 = trace ? now() : 0;
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
         for (size_t i = b; i < e; ++i) {
             out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
             if (!h.empty()) std::memcpy((*sha)[at[i]].data(), h.data() + 32 * i, 32), (*has)[at[i]] = 1;
         }
     });
+    if (trace) std::fprintf(stderr, "EncodePNCRowsBefore(%zu): encode %.1f ms, hashes %.1f ms, strings %.1f ms\n", n, t1 - t0, t2 - t1, now() - t2);
 }
 
 // ComputeDigests of msgs[first..] from per-payload SHA-256s: the ones not given (has[i] = 0: states queued by an earlier
@@ -893,25 +951,34 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             std::vector<int64_t> dp(pnc_need.size()), dn(pnc_need.size());
             std::vector<uint32_t> prow(pnc_need.size());
             std::vector<size_t> at(pnc_need.size());
-            size_t w = pnc_need.size();
-            for (size_t j = idx.size(); j-- > 0;) {
-                const size_t i = idx[j];
-                if (!kpn[i]) continue;
-                const ClientOp& op = ups[i].op;
-                auto& a = pnc_after_[krow[i]];
-                if (w && pnc_need[w - 1] == j) {
-                    --w;
-                    dp[w] = (int64_t)a.first;
-                    dn[w] = (int64_t)a.second;
-                    prow[w] = krow[i];
-                    at[w] = i;
+            std::vector<int32_t> wof(idx.size(), -1);  // position in pnc_need of a needed op
+            for (size_t w = 0; w < pnc_need.size(); ++w) wof[pnc_need[w]] = (int32_t)w;
+            // rows are independent: worker t walks the round backwards over the rows with row % T == t
+            const size_t T = (size_t)std::max(1, pool().size());
+            parallel_ranges(pool(), T, [&](size_t tb0, size_t te0, int) {
+                for (size_t t = tb0; t < te0; ++t) {
+                    for (size_t j = idx.size(); j-- > 0;) {
+                        const size_t i = idx[j];
+                        if (!kpn[i] || krow[i] % T != t) continue;
+                        const ClientOp& op = ups[i].op;
+                        auto& a = pnc_after_[krow[i]];
+                        if (wof[j] >= 0) {
+                            const size_t w = (size_t)wof[j];
+                            dp[w] = (int64_t)a.first;
+                            dn[w] = (int64_t)a.second;
+                            prow[w] = krow[i];
+                            at[w] = i;
+                        }
+                        const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
+                        (op.opId == 2 ? a.second : a.first) += amt;
+                    }
+                    for (size_t i : idx)
+                        if (kpn[i] && krow[i] % T == t) pnc_after_[krow[i]] = {0, 0};
                 }
-                const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
-                (op.opId == 2 ? a.second : a.first) += amt;
-            }
-            for (size_t i : idx)
-                if (kpn[i]) pnc_after_[krow[i]] = {0, 0};
+            }, 2);
+            const double trw = trace ? now() : 0;
             EncodePNCRowsBefore(prow, dp, dn, at, snap, &ssha, &shas);
+            if (trace) std::fprintf(stderr, "SubmitClientUpdates: PN-Counter rewind %.1f ms, encode + hashes + strings %.1f ms\n", trw - tb, now() - trw);
         }
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;

@@ -269,6 +269,8 @@ class GpuStableStore {
         std::vector<std::string> names;                   // id -> element, every id ever issued
     };
     uint32_t elem_id(uint32_t set, const std::optional<std::string>& e, bool create);
+    struct PendingNames;
+    uint32_t elem_id_in(SetKey& s, PendingNames* pn, const std::string& e, bool create);
     // Interning changes made here (ORSet.Add of a new element, Clear) that the engine's element table
     // (the wave path, jg_orset_names_sync) has not seen yet, per set: cleared since the last sync, and
     // the ids issued since then (or since the Clear).
