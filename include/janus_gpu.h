@@ -167,7 +167,10 @@ int jg_pnc_encode_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint64_
  * batch whose later ops on the same key are already applied (SafeCRDT.cs:39-62; PNCounters.cs:97-112).  Lets a
  * batch of client ops be applied in ONE jg_pnc_apply_ops and every snapshot encoded in ONE call. */
 int jg_pnc_encode_json_before(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn,
-                              uint64_t* off, uint8_t* out, uint64_t cap);
+                              uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* sha);
+/* (sha, here and in jg_orset_encode_json: NULL, or n * 32 bytes receiving each encoded state's SHA256 — the hash
+ * UpdateMessage.ComputeDigest takes of it, DAGUpdateMessage.cs:43 — computed on the device from the bytes just
+ * written; filled only when out is.  The producer path feeds them to jg_update_digests_of.) */
 
 /* Page-locked host memory for staging waves (PCIe DMA at full rate); free with jg_host_free. */
 int jg_host_alloc(jg_ctx* ctx, uint64_t bytes, void** out);
@@ -225,7 +228,7 @@ int jg_orset_read_sets(jg_orset* s, uint64_t n, const uint32_t* set, uint64_t* a
  * before a batch's later ops (jg_orset_apply_ops_ords).  State i = out[off[i], off[i+1]); out NULL = size
  * query; JG_ESTATE if off[n] > cap (off filled, out untouched). */
 int jg_orset_encode_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off,
-                         uint8_t* out, uint64_t cap);
+                         uint8_t* out, uint64_t cap, uint8_t* sha);
 /* ORSet.LookupAll (ORSet.cs:204-227) of sets set[0..n): members of set[i] are elems[off[i], off[i+1])
  * (off has n+1 entries, always filled), in the reference's order: elements with no tombstone set,
  * then elements whose tag sets differ (each group in ascending elem id = the add Dictionary's

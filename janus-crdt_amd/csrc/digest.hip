@@ -361,6 +361,20 @@ void run_digests(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, con
 
 }  // namespace
 
+namespace jg {
+// SHA-256 of n payloads already in device memory (d_bytes at d_off[i]..d_off[i+1]) into host `out` (n * 32 digest
+// bytes), queued on ctx->stream: the caller's next sync covers it.  The encoders hash what they just wrote.
+void sha256_device(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* out) {
+    if (n == 0) return;
+    auto* D = static_cast<uint4*>(jg::scratch(ctx, ctx->scratch3, n * 32 + 256));
+    hipStream_t st = ctx->stream;
+    k_sha_msgs<false><<<grid_for(n), kBlock, 0, st>>>(d_bytes, d_off, nullptr, n, D);
+    k_bswap_words<<<std::min<uint64_t>(grid_for(n * 8), 4096), kBlock, 0, st>>>(reinterpret_cast<uint32_t*>(D), n * 8);
+    JG_HIP(hipGetLastError());
+    JG_HIP(hipMemcpyAsync(out, D, n * 32, hipMemcpyDeviceToHost, st));
+}
+}  // namespace jg
+
 extern "C" {
 
 int jg_update_digests(jg_ctx* ctx, uint64_t n, const uint64_t* off, const uint8_t* bytes, const uint8_t* is_null, uint64_t n_updates,

@@ -276,7 +276,9 @@ void pnc_node_begin(jg_pnc* p, uint64_t n);
 void pnc_node_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1);
 int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
 int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why);
-void pnc_node_undo(jg_pnc* p, const uint32_t* rows);  // a node wave abandoned after its chunks' (fused) pass A
+void pnc_node_undo(jg_pnc* p, const uint32_t* rows);
+// SHA-256 of n device-resident payloads into host out (n * 32 bytes), queued on ctx->stream (digest.hip)
+void sha256_device(jg_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_off, uint64_t n, uint8_t* out);  // a node wave abandoned after its chunks' (fused) pass A
 // orset_wire.hip (OR-Set):
 void orset_node_begin(jg_orset* s, uint8_t* bytes, uint64_t* off, uint32_t* mset, uint64_t n, uint64_t nbytes, uint32_t max_set);
 void orset_node_parse(jg_orset* s, uint64_t m0, uint64_t m1);

@@ -1083,7 +1083,7 @@ int jg_host_free(void* p) {
 namespace {
 // jg_pnc_encode_json(_before): length pass, scan, offsets to the host; with `out`, the write pass and its bytes.
 void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off, uint8_t* out,
-                 uint64_t cap, const char* fn) {
+                 uint64_t cap, const char* fn, uint8_t* sha = nullptr) {
     JG_REQUIRE(p && off, JG_EINVAL, "%s: NULL argument", fn);
     off[0] = 0;
     if (n == 0) return;
@@ -1125,6 +1125,7 @@ void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, c
     if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
     else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
     JG_HIP(hipGetLastError());
+    if (sha) jg::sha256_device(ctx, dout, reinterpret_cast<const uint64_t*>(doff), n, sha);  // each state's SHA-256 (ComputeDigest's first level)
     JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
 }
@@ -1138,12 +1139,12 @@ int jg_pnc_encode_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint64_t*
 }
 
 int jg_pnc_encode_json_before(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off,
-                              uint8_t* out, uint64_t cap) {
+                              uint8_t* out, uint64_t cap, uint8_t* sha) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);
         JG_REQUIRE(p && (n == 0 || (dp && dn)), JG_EINVAL, "jg_pnc_encode_json_before: NULL argument");
         JG_REQUIRE(col < p->R, JG_EINVAL, "jg_pnc_encode_json_before: column %u past the store's %u replicas", col, p->R);
-        encode_rows(p, n, key_idx, col, dp, dn, off, out, cap, "jg_pnc_encode_json_before");
+        encode_rows(p, n, key_idx, col, dp, dn, off, out, cap, "jg_pnc_encode_json_before", out ? sha : nullptr);
     });
 }
 

@@ -2331,7 +2331,7 @@ void close_wave(jg_orset_wire* w) {
 // by ord), size every state, then write them (see the kernels' header comment).  Two round trips: the record
 // count (gather) and the states' offsets; a third copy brings the bytes.
 void encode_sets(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off, uint8_t* out,
-                 uint64_t cap) {
+                 uint64_t cap, uint8_t* sha) {
     jg_ctx* ctx = s->ctx;
     jg_orset_wire* w = wire_of(s);
     if (!w->itab_cap || !w->tab_cap) ensure_names(ctx, w, 0, 0);  // a store that never saw a name: empty tables
@@ -2441,6 +2441,7 @@ void encode_sets(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* a
         hipLaunchKernelGGL(k_enc_rec_text, dim3(gR), dim3(kBlock), 0, ctx->stream, E, kidx, K, srec, rid, rrank, cpos, rtags, dout);
     }
     JG_HIP(hipGetLastError());
+    if (sha) jg::sha256_device(ctx, dout, reinterpret_cast<const uint64_t*>(qoff), n, sha);  // each state's SHA-256 (ComputeDigest's first level)
     JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
     JG_HIP(hipStreamSynchronize(ctx->stream));
 }
@@ -2818,7 +2819,7 @@ int jg_orset_merge_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint
 
 
 int jg_orset_encode_json(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* add_lim, const uint64_t* rem_lim, uint64_t* off, uint8_t* out,
-                         uint64_t cap) {
+                         uint64_t cap, uint8_t* sha) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
         JG_REQUIRE(s && off, JG_EINVAL, "jg_orset_encode_json: NULL argument");
@@ -2828,7 +2829,7 @@ int jg_orset_encode_json(jg_orset* s, uint64_t n, const uint32_t* set, const uin
         JG_REQUIRE(!add_lim == !rem_lim, JG_EINVAL, "jg_orset_encode_json: add_lim and rem_lim go together");
         JG_REQUIRE(n < (1ull << 29), JG_EINVAL, "jg_orset_encode_json: at most 2^29 states per call");
         jg::ensure_device(s->ctx);
-        encode_sets(s, n, set, add_lim, rem_lim, off, out, cap);
+        encode_sets(s, n, set, add_lim, rem_lim, off, out, cap, out ? sha : nullptr);
     });
 }
 

@@ -628,22 +628,18 @@ void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, cons
     // one call into a page-locked buffer sized from the last call (a second only if the states outgrew it)
     size_t guess = std::max<size_t>(pin_cap_, (size_t)(n * (last_pnc_bytes_ + 8)) + 4096);
     uint8_t* buf = pinned_buf(guess);
-    int rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_);
+    std::vector<uint8_t> h(sha ? 32 * n : 0);  // each state's SHA-256, hashed on the device as it is encoded
+    int rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, sha ? h.data() : nullptr);
     if (rc == JG_ESTATE && off[n] > pin_cap_) {
         buf = pinned_buf(off[n]);
-        rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_);
+        rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, sha ? h.data() : nullptr);
     }
     check(rc);
     static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
     const double t1 = trace ? now() : 0;
     if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
-    std::vector<uint8_t> h;
-    if (sha && n) {  // from the page-locked output as it stands (uploaded in place)
-        h.resize(32 * n);
-        check(jg_sha256_batch(ctx_, n, off.data(), buf, h.data()));
-    }
-    const double t2 = trace ? now() : 0;
+    const double t2 = t1;
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
         for (size_t i = b; i < e; ++i) {
             out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
@@ -712,10 +708,10 @@ std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector
     rows.reserve(uids.size());
     for (const Guid& u : uids) rows.push_back(ref(u, CrdtType::PNCounter).idx);
     std::vector<uint64_t> off(rows.size() + 1, 0);
-    check(jg_pnc_encode_json_before(pnc_, rows.size(), rows.data(), 0, dp.data(), dn.data(), off.data(), nullptr, 0));
+    check(jg_pnc_encode_json_before(pnc_, rows.size(), rows.data(), 0, dp.data(), dn.data(), off.data(), nullptr, 0, nullptr));
     std::string buf(off.back(), '\0');
     check(jg_pnc_encode_json_before(pnc_, rows.size(), rows.data(), 0, dp.data(), dn.data(), off.data(), reinterpret_cast<uint8_t*>(buf.data()),
-                                    buf.size()));
+                                    buf.size(), nullptr));
     std::vector<std::string> out;
     out.reserve(rows.size());
     for (size_t i = 0; i < rows.size(); ++i) out.emplace_back(buf, off[i], off[i + 1] - off[i]);
@@ -735,16 +731,14 @@ std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Gui
     // ORSetMsg.Encode() on the device (jg_orset_encode_json) into a page-locked buffer kept across calls: one call
     // unless the states outgrow it
     uint8_t* buf = pinned_buf(4096);
-    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_);
+    if (sha) sha->resize(n);  // each state's SHA-256, hashed on the device as it is encoded
+    uint8_t* hs = sha ? reinterpret_cast<uint8_t*>(sha->data()) : nullptr;
+    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
     if (rc == JG_ESTATE && off[n] > pin_cap_) {
         buf = pinned_buf(off[n]);
-        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_);
+        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
     }
     check(rc);
-    if (sha) {  // SHA-256 of each state from the page-locked output (uploaded in place)
-        sha->resize(n);
-        if (n) check(jg_sha256_batch(ctx_, n, off.data(), buf, reinterpret_cast<uint8_t*>(sha->data())));
-    }
     std::vector<std::string> out(n);
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
         for (size_t i = b; i < e; ++i) out[i].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);

@@ -99,8 +99,8 @@ _SIGS = {
     "jg_pnc_wave_abort": ([_vp], C.c_int),
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
-    "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64], C.c_int),
-    "jg_orset_encode_json": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64], C.c_int),
+    "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
+    "jg_orset_encode_json": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
     "jg_orset_apply_ops_ords": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_merge_device": ([_vp, _u64, _vp, _vp, _vp], C.c_int),
@@ -381,16 +381,20 @@ class PNCStore:
         b = out.tobytes()
         return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
 
-    def encode_json_before(self, key_idx, dp, dn, col=0) -> list:
-        """jg_pnc_encode_json_before: each row as it stood before its last dp[i] / dn[i] of increments to `col`."""
+    def encode_json_before(self, key_idx, dp, dn, col=0, sha=False):
+        """jg_pnc_encode_json_before: each row as it stood before its last dp[i] / dn[i] of increments to `col`
+        (list of bytes; with sha=True also each state's SHA-256, u8[n, 32])."""
         k = _arr(key_idx, np.uint32)
         p, q = _arr(dp, np.int64), _arr(dn, np.int64)
         off = np.zeros(k.size + 1, np.uint64)
-        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), None, 0))
+        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), None, 0, None))
         out = np.empty(max(16, int(off[-1])), np.uint8)
-        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), _ptr(out), out.size))
+        h = np.zeros((k.size, 32), np.uint8) if sha else None
+        _check(load().jg_pnc_encode_json_before(self._h, k.size, _ptr(k), col, _ptr(p), _ptr(q), _ptr(off), _ptr(out), out.size,
+                                                _ptr(h) if sha else None))
         b = out.tobytes()
-        return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
+        states = [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
+        return (states, h) if sha else states
 
     def merge_wave(self, wave: "Wave") -> None:
         bad = _u64(0)
@@ -553,18 +557,21 @@ class ORSetStore:
         _check(load().jg_orset_apply_ops_ords(self._h, s.size, _ptr(s), _ptr(e), _ptr(o), _ptr(lo), _ptr(hi), _ptr(out), _ptr(al), _ptr(rl)))
         return out, al, rl
 
-    def encode_json(self, set_ids, add_lim=None, rem_lim=None) -> list:
-        """ORSetMsg.Encode() of each set on the device (jg_orset_encode_json), optionally as of ord limits: list of bytes."""
+    def encode_json(self, set_ids, add_lim=None, rem_lim=None, sha=False):
+        """ORSetMsg.Encode() of each set on the device (jg_orset_encode_json), optionally as of ord limits: list of bytes
+        (with sha=True also each state's SHA-256, u8[n, 32])."""
         s = _arr(set_ids, np.uint32)
         al = None if add_lim is None else _arr(add_lim, np.uint64)
         rl = None if rem_lim is None else _arr(rem_lim, np.uint64)
         off = np.zeros(s.size + 1, np.uint64)
         args = (_ptr(al) if al is not None else None, _ptr(rl) if rl is not None else None)
-        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), None, 0))
+        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), None, 0, None))
         out = np.empty(max(16, int(off[-1])), np.uint8)
-        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), _ptr(out), out.size))
+        h = np.zeros((s.size, 32), np.uint8) if sha else None
+        _check(load().jg_orset_encode_json(self._h, s.size, _ptr(s), *args, _ptr(off), _ptr(out), out.size, _ptr(h) if sha else None))
         b = out.tobytes()
-        return [b[int(off[i]):int(off[i + 1])] for i in range(s.size)]
+        states = [b[int(off[i]):int(off[i + 1])] for i in range(s.size)]
+        return (states, h) if sha else states
 
     def contains(self, set_ids, elems) -> np.ndarray:
         s, e = _arr(set_ids, np.uint32), _arr(elems, np.uint32)

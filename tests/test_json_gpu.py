@@ -2,6 +2,8 @@
 against the oracle's Decode + Merge loop (oracle/json.hpp, oracle/capi.cpp orc_pnc_apply_json), through
 the C ABI: the decode contract, replica interning in commit order, all-or-nothing errors, row capacity,
 and the device-resident wave.  Bit-exact on values, replica Guids and column order."""
+import hashlib
+
 import numpy as np
 import pytest
 
@@ -527,4 +529,7 @@ def test_encode_before_matches_oracle_encoder(ctx, eb):
         P[0], N[0] = wrap(int(P[0]) - int(dp[i])), wrap(int(N[0]) - int(dn[i]))
         exp = orc.json_encode_pnc(pr.cols[k, :c]["lo"], pr.cols[k, :c]["hi"], np.array(P, dtype=pr.P.dtype), np.array(N, dtype=pr.N.dtype), eb)
         assert got[i] == exp, f"query {i} key {k}"
+    states, h = pr.s.encode_json_before(q, dp, dn, sha=True)  # and each state's SHA-256, hashed on the device
+    assert states == got
+    assert all(h[i].tobytes() == hashlib.sha256(got[i]).digest() for i in range(len(got)))
     pr.close()

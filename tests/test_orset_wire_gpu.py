@@ -6,6 +6,7 @@ tests/oracle_ref.orset_apply_json: Decode + Merge in commit order, element ids i
 insertion.  Comparisons are exact: the store's record streams, the ids each wave issued (set, id,
 string), and the first rejected message with its code.
 """
+import hashlib
 import os
 
 import numpy as np
@@ -618,7 +619,8 @@ def test_encode_snapshot_limits_equal_step_by_step_states(ctx):
         hi = rng.integers(1, 2**63, n_ops, dtype=np.uint64)
         res, al, rl = a.apply_ops_ords(sets, elems, ops, lo, hi)
         check = [i for i in range(n_ops) if not (i < 60 and sets[i] == sets[60])]
-        snaps = a.encode_json(sets[check], al[check], rl[check])
+        snaps, h = a.encode_json(sets[check], al[check], rl[check], sha=True)
+        assert all(h[k].tobytes() == hashlib.sha256(snaps[k]).digest() for k in range(len(snaps)))  # hashed on the device
         got = dict(zip(check, snaps))
         for i in range(n_ops):
             r = b.apply_ops(sets[i:i + 1], elems[i:i + 1], ops[i:i + 1], lo[i:i + 1], hi[i:i + 1])
