@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "host_pool.hpp"
 #include "jg_internal.hpp"
 #include "orset_union.hpp"
 
@@ -599,16 +600,32 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
     need.erase(std::unique(need.begin(), need.end()), need.end());
     const Runs runs = fetch_runs(s, need);
 
-    std::vector<jg_tagrec> dadd, drem;
-    std::vector<uint32_t> cleared;
-    uint64_t next_a = 0, next_r = 0;  // batch ords (op order within a set; sets are independent)
+    // the sets' groups of ops (order is sorted by set): each group processed on its own — sets are independent —
+    // by the workers for a large batch, its records numbered from 0 in op order and sorted by (key, tag); then
+    // every group's records and snapshot limits shifted by the records of the groups before it, so the batch ords
+    // run in (set, op) order and the concatenation in set order is sorted (keys are set << 32 | elem)
+    std::vector<uint64_t> gbeg;
     for (uint64_t g = 0; g < n_ops;) {
+        gbeg.push_back(g);
         const uint32_t sid = set[order[g]];
-        uint64_t h = g;
-        while (h < n_ops && set[order[h]] == sid) ++h;
+        while (g < n_ops && set[order[g]] == sid) ++g;
+    }
+    const size_t G = gbeg.size();
+    gbeg.push_back(n_ops);
+    std::vector<std::vector<jg_tagrec>> ga(G), gr(G);
+    std::vector<uint8_t> gclr(G, 0);
+    std::vector<uint64_t> issued_a(G, 0), issued_r(G, 0);  // ords a group issued, those of records a Clear dropped included
+    auto lt = [](const jg_tagrec& a, const jg_tagrec& b) {
+        return a.key != b.key ? a.key < b.key : a.tag_lo != b.tag_lo ? a.tag_lo < b.tag_lo : a.tag_hi < b.tag_hi;
+    };
+    auto one_group = [&](size_t q) {
+        const uint64_t g = gbeg[q], h = gbeg[q + 1];
+        const uint32_t sid = set[order[g]];
         std::unordered_map<uint32_t, ElemState> st;
         bool was_cleared = false;
-        std::vector<jg_tagrec> sa, sr;
+        std::vector<jg_tagrec>& sa = ga[q];
+        std::vector<jg_tagrec>& sr = gr[q];
+        uint64_t next_a = 0, next_r = 0;  // the group's ords (op order within the set)
         auto state = [&](uint32_t e) -> ElemState& {
             auto it = st.find(e);
             if (it != st.end()) return it->second;
@@ -616,9 +633,9 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
             const unsigned long long key = ((unsigned long long)sid << 32) | e;
             auto nk = std::lower_bound(need.begin(), need.end(), key);
             if (!was_cleared && nk != need.end() && *nk == key) {
-                const size_t q = nk - need.begin();
-                load_group(runs.add.data() + runs.add_off[q], runs.add.data() + runs.add_off[q + 1], es.add, es.add_has);
-                load_group(runs.rem.data() + runs.rem_off[q], runs.rem.data() + runs.rem_off[q + 1], es.rem, es.rem_has);
+                const size_t k = nk - need.begin();
+                load_group(runs.add.data() + runs.add_off[k], runs.add.data() + runs.add_off[k + 1], es.add, es.add_has);
+                load_group(runs.rem.data() + runs.rem_off[k], runs.rem.data() + runs.rem_off[k + 1], es.rem, es.rem_has);
             }
             return st.emplace(e, std::move(es)).first->second;
         };
@@ -651,19 +668,42 @@ void apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const uint32_t*
                 was_cleared = true;
                 result[i] = 1;
             }
-            if (add_lim) add_lim[i] = next_a, rem_lim[i] = next_r;  // batch ords so far: rebased below
+            if (add_lim) add_lim[i] = next_a, rem_lim[i] = next_r;  // the group's ords so far: shifted below
         }
-        if (was_cleared) cleared.push_back(sid);
-        dadd.insert(dadd.end(), sa.begin(), sa.end());
-        drem.insert(drem.end(), sr.begin(), sr.end());
-        g = h;
-    }
-    // the batch's records carry no duplicate (key, tag): the ElemStates filtered them
-    auto lt = [](const jg_tagrec& a, const jg_tagrec& b) {
-        return a.key != b.key ? a.key < b.key : a.tag_lo != b.tag_lo ? a.tag_lo < b.tag_lo : a.tag_hi < b.tag_hi;
+        gclr[q] = was_cleared ? 1 : 0;
+        issued_a[q] = next_a, issued_r[q] = next_r;
+        // the batch's records carry no duplicate (key, tag): the ElemStates filtered them
+        std::sort(sa.begin(), sa.end(), lt);
+        std::sort(sr.begin(), sr.end(), lt);
     };
-    std::sort(dadd.begin(), dadd.end(), lt);
-    std::sort(drem.begin(), drem.end(), lt);
+    static thread_local std::unique_ptr<jg::WorkerPool> pool;
+    const bool par = n_ops >= 8192 && G > 1;
+    if (par && !pool) pool = std::make_unique<jg::WorkerPool>(jg::host_threads());
+    if (par) jg::deal(*pool, true, G, [&](size_t q, int) { one_group(q); });
+    else
+        for (size_t q = 0; q < G; ++q) one_group(q);
+    // base_*: the ords the groups before issued (the serial walk's running counters); at_*: where a group's kept
+    // records go in the batch streams
+    std::vector<uint64_t> base_a(G + 1, 0), base_r(G + 1, 0), at_a(G + 1, 0), at_r(G + 1, 0);
+    std::vector<uint32_t> cleared;
+    for (size_t q = 0; q < G; ++q) {
+        base_a[q + 1] = base_a[q] + issued_a[q];
+        base_r[q + 1] = base_r[q] + issued_r[q];
+        at_a[q + 1] = at_a[q] + ga[q].size();
+        at_r[q + 1] = at_r[q] + gr[q].size();
+        if (gclr[q]) cleared.push_back(set[order[gbeg[q]]]);
+    }
+    const uint64_t next_a = base_a[G], next_r = base_r[G];
+    std::vector<jg_tagrec> dadd(at_a[G]), drem(at_r[G]);
+    auto place = [&](size_t q) {
+        for (size_t k = 0; k < ga[q].size(); ++k) dadd[at_a[q] + k] = ga[q][k], dadd[at_a[q] + k].ord += base_a[q];
+        for (size_t k = 0; k < gr[q].size(); ++k) drem[at_r[q] + k] = gr[q][k], drem[at_r[q] + k].ord += base_r[q];
+        if (add_lim)
+            for (uint64_t x = gbeg[q]; x < gbeg[q + 1]; ++x) add_lim[order[x]] += base_a[q], rem_lim[order[x]] += base_r[q];
+    };
+    if (par) jg::deal(*pool, true, G, [&](size_t q, int) { place(q); });
+    else
+        for (size_t q = 0; q < G; ++q) place(q);
 
     jg_ctx* ctx = s->ctx;
     jg::DevBuf drop;

@@ -207,7 +207,7 @@ def test_full_size_c3(ctx):
 
 
 @pytest.mark.parametrize("seed,n_sets,n_elems,n_ops,p_clear", [(1, 3, 4, 60, 0.05), (2, 40, 12, 3000, 0.01), (3, 5, 3, 500, 0.2),
-                                                                (4, 300, 20, 20000, 0.002)])
+                                                                (4, 300, 20, 20000, 0.002), (5, 50, 8, 30000, 0.02)])
 def test_apply_ops_match_oracle(ctx, seed, n_sets, n_elems, n_ops, p_clear):
     """ORSet.Add/Remove/Clear (ORSet.cs:134-198) batched on the device in op order per set,
     interleaved across sets, on top of an existing merged state, vs the oracle op by op."""
