@@ -440,7 +440,12 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         if (defer) status[1] = 1;  // any deferral (select_deferred later overwrites it with the count)
         const bool to_slow = g == 0 && live && !fast;
         const unsigned long long at = wave_slot(to_slow, status + 3);
-        if (to_slow) slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
+        if (to_slow) {
+            slow[at] = m;  // k_scan_slow parses it (and marks / emits it) before the wave's status is read
+            // its record header now, not only when k_scan_slow runs: an undo before then (a node wave cut or aborted
+            // right after its chunks' pass A) must not read a header an earlier wave left here as an applied record
+            *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = kReparse;
+        }
         if (g == 0 && skip) {  // no entries, not deferred
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) = 0;
             deferred[m] = kNotDeferred;
