@@ -429,10 +429,11 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
     # the parse is instruction-bound, not HBM-bound: VALU wave instructions per wave (PMC SQ_INSTS_VALU of
     # k_scan + k_apply_emit, profiles/pmc_*.json) against the chip's issue rate (one wave instruction per
     # SIMD every 2 cycles: 256 CUs x 4 SIMDs x 0.5 x 2.4 GHz)
+    # (with pass A fused, the default, the steady-state wave launches no k_apply_emit: its share is then 0)
     sv, av = load_traffic("json_scan_valu"), load_traffic("json_apply_emit_valu")
     valu = None
-    if sv and av:
-        insts, peak = sv[0] + av[0], VALU_LANE_OPS / 64
+    if sv:
+        insts, peak = sv[0] + (av[0] if av else 0), VALU_LANE_OPS / 64
         valu = {"bound": "valu", "achieved": insts / kern / 1e12, "peak": peak / 1e12, "unit": "T wave-instructions/s",
                 "frac": insts / kern / peak, "valu_insts_per_wave": insts, "source": sv[1],
                 "scope": "k_scan + k_apply_emit VALU instructions over the jg_pnc_merge_wave event time"}
