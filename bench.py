@@ -436,7 +436,7 @@ def bench_json(jg, ctx, sync, rank, steps, warmup):
         insts, peak = sv[0] + (av[0] if av else 0), VALU_LANE_OPS / 64
         valu = {"bound": "valu", "achieved": insts / kern / 1e12, "peak": peak / 1e12, "unit": "T wave-instructions/s",
                 "frac": insts / kern / peak, "valu_insts_per_wave": insts, "source": sv[1],
-                "scope": "k_scan + k_apply_emit VALU instructions over the jg_pnc_merge_wave event time"}
+                "scope": "k_scan (+ k_apply_emit, which a steady-state wave does not launch) VALU instructions over the jg_pnc_merge_wave event time"}
     return {"workload": f"PNCounterMsg wave from wire bytes (C5 shape: {JSON_MSGS} states of {JSON_KEYS} accounts, "
                         f"{JSON_R - 1}-node replicas, int32), resident in HBM, steady state (replicas known)",
             "msgs_per_s": JSON_MSGS / (wall / steps), "ms_per_wave": wall / steps * 1e3, "event_ms": kern * 1e3,

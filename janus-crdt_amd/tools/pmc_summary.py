@@ -56,6 +56,23 @@ def per_kernel(path, counter, key=lambda n: n):
     return out
 
 
+def json_scan_split(path, counter):
+    """k_scan<4, 8> counter values (bytes) of the steady-state waves and of the cold ones, by dispatch order: a cold
+    wave's scan is followed by k_resolve_rows / k_apply_emit before the next scan."""
+    with open(path) as f:
+        rows = sorted((r for r in csv.DictReader(f) if r["Counter_Name"] == counter), key=lambda r: int(r["Dispatch_Id"]))
+    out, cur = {"steady": [], "cold": []}, None
+    for r in rows + [None]:
+        n = r["Kernel_Name"] if r else "k_scan<4, 8>"
+        if "k_scan<4, 8>" in n:
+            if cur is not None:
+                out["cold" if cur[1] else "steady"].append(cur[0])
+            cur = [float(r["Counter_Value"]) * 1024, False] if r else None
+        elif cur is not None and ("k_resolve_rows" in n or "k_apply_emit" in n):
+            cur[1] = True
+    return out
+
+
 def durations(trace_dir):
     """Kernel durations (ns) per short name from a --kernel-trace run."""
     out = collections.defaultdict(list)
@@ -150,24 +167,45 @@ def main():
             res[key] = v
             if key in ALGO:
                 res[key + "_algorithmic"] = ALGO[key]
+    # the json leg's steady-state waves (every replica known: pass A applies the cells itself, nothing follows it)
+    # apart from its cold ones (first sight of the replicas: k_resolve_rows + k_apply_emit follow the scan)
+    if (d / "pmc_json_FETCH_SIZE").exists():
+        js = {}
+        for c in ("FETCH_SIZE", "WRITE_SIZE"):
+            js[c] = json_scan_split(d / f"pmc_json_{c}" / "run_counter_collection.csv", c)
+        if js["FETCH_SIZE"]["steady"] and js["WRITE_SIZE"]["steady"]:
+            f, w = statistics.median(js["FETCH_SIZE"]["steady"]), statistics.median(js["WRITE_SIZE"]["steady"])
+            res["json_scan"] = 2 * f + w
+            res["json_scan_steady"] = {"fetch_size_bytes": f, "write_size_bytes": w, "streaming_reading": 2 * f + w,
+                                       "random_line_reading": f + w, "launches": [len(js["FETCH_SIZE"]["steady"]), len(js["WRITE_SIZE"]["steady"])]}
+        if js["FETCH_SIZE"]["cold"] and js["WRITE_SIZE"]["cold"]:
+            res["json_scan_cold"] = 2 * statistics.median(js["FETCH_SIZE"]["cold"]) + statistics.median(js["WRITE_SIZE"]["cold"])
+            res["json_apply_emit_cold"] = res.pop("json_apply_emit", None)
     # VALU instructions per launch of the json leg's group kernels (SQ_INSTS_VALU, one wave instruction = 64
     # lanes), for the bench's instruction-issue roofline of jg_pnc_merge_wave, with the stall shares beside them
     sq = d / "sq_json" / "run_counter_collection.csv"
     if sq.exists():
-        for key, prefix in [("json_scan", "k_scan<4, 8>"), ("json_apply_emit", "k_apply_emit<4>")]:
+        # (the scan's steady-state launches only, as the bytes above; k_apply_emit runs in cold waves alone)
+        def counter(path, c, prefix):
+            if prefix.startswith("k_scan<"):
+                v = json_scan_split(path, c)["steady"]
+                return statistics.median(v) / 1024 if v else None
+            vals = per_kernel(path, c)
+            names = [k for k in vals if prefix in k]
+            return statistics.median(vals[names[0]]) if names else None
+
+        for key, prefix in [("json_scan", "k_scan<4, 8>"), ("json_apply_emit_cold", "k_apply_emit<4>")]:
             cs = {}
             for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES"):
-                vals = per_kernel(sq, c)
-                names = [k for k in vals if prefix in k]
-                if names:
-                    cs[c] = statistics.median(vals[names[0]])
+                v = counter(sq, c, prefix)
+                if v is not None:
+                    cs[c] = v
             sq2 = d / "sq2_json" / "run_counter_collection.csv"
             if sq2.exists():
                 for c in ("SQ_ACTIVE_INST_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"):
-                    vals = per_kernel(sq2, c)
-                    names = [k for k in vals if prefix in k]
-                    if names:
-                        cs[c] = statistics.median(vals[names[0]])
+                    v = counter(sq2, c, prefix)
+                    if v is not None:
+                        cs[c] = v
             if "SQ_INSTS_VALU" in cs:
                 res[key + "_valu"] = cs["SQ_INSTS_VALU"]
                 wc = cs.get("SQ_WAVE_CYCLES")
