@@ -335,13 +335,17 @@ __device__ void resolve_one(const uint8_t* __restrict__ bytes, const uint64_t* _
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rollback(const unsigned long long* __restrict__ keys, uint64_t nd, uint32_t* __restrict__ ncols,
+// The row's count back to its value before the walk, and every slot past it zeroed: a failed walk may have
+// written columns it never counted (k_resolve_rows keeps its count in a register until the row is done),
+// and pass A reads a row's columns as its leading non-zero slots (json_wave.hpp row_cache).
+__global__ __launch_bounds__(kBlock) void k_rollback(const unsigned long long* __restrict__ keys, uint64_t nd, Table t,
                                                      const uint32_t* __restrict__ saved) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= nd) return;
     const uint32_t row = (uint32_t)(keys[i] >> 32);
     if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;
-    ncols[row] = saved[i];
+    t.ncols[row] = saved[i];
+    for (uint32_t c = saved[i]; c < t.R; ++c) t.cols[(uint64_t)row * t.R + c] = Guid16{0, 0};
 }
 
 // Pass B visitor: max into the cells.
@@ -511,6 +515,7 @@ void ensure_table(jg_pnc* p) {
     JG_REQUIRE(p->R <= kMaxJsonReplicas, JG_EINVAL, "replica table: at most %u replicas per key (store has %u)", kMaxJsonReplicas, p->R);
     p->cols.alloc((size_t)p->n_keys * p->R * sizeof(Guid16));
     p->ncols.alloc((size_t)p->n_keys * 4);
+    JG_HIP(hipMemsetAsync(p->cols.p, 0, p->cols.bytes, p->ctx->stream));  // unused slots are zero (json_wave.hpp row_cache)
     JG_HIP(hipMemsetAsync(p->ncols.p, 0, p->ncols.bytes, p->ctx->stream));
 }
 
@@ -733,7 +738,7 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
             st = read_status(ctx, w.status);
         }
         if (st.resolve_bad != ~0ull) {
-            hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t.ncols, w.saved);
+            hipLaunchKernelGGL(k_rollback, dim3(gd), dim3(kBlock), 0, ctx->stream, sorted, nd, t, w.saved);
             JG_HIP(hipGetLastError());
             undo_applied(p, rows);
             JG_HIP(hipStreamSynchronize(ctx->stream));
@@ -866,7 +871,7 @@ int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid*
         JG_HIP(hipGetLastError());
         const Status st = read_status(ctx, status);
         if (st.resolve_bad != ~0ull) {
-            hipLaunchKernelGGL(k_rollback, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, sorted, n, t.ncols, saved);
+            hipLaunchKernelGGL(k_rollback, dim3(blocks_for(n)), dim3(kBlock), 0, ctx->stream, sorted, n, t, saved);
             JG_HIP(hipStreamSynchronize(ctx->stream));
             jg::fail(JG_ESTATE, "jg_pnc_intern: entry %llu: its key holds more replicas than the store's columns",
                      (unsigned long long)(st.resolve_bad >> 2));

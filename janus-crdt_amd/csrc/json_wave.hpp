@@ -169,28 +169,41 @@ struct GroupParse {
     bool has[kRounds];
 };
 
-// The group's row: its column count and first G columns, loaded before the payload so that both
-// latencies overlap; lane g holds column g.
+// The group's row: its first G columns, loaded before the payload so that both latencies overlap; lane g
+// holds column g.  The row's column COUNT is not read: a column slot at or past the count is all-zero (the
+// table starts zeroed, columns are appended in order, and every roll-back of a count zeroes the slots it
+// drops, k_rollback), so the columns are the row's leading non-zero slots.  That saves each message a
+// random line for 4 bytes (the count array is as large as the row count; round 5 PMC: the count, the
+// columns and the P / N lines were ~290 of the ~560 bytes per message pass A moved).  A hit is therefore
+// always a real column; a replica whose Guid is all-zero (or any column after it) reads as a miss, which
+// the deferred path resolves against the true count (slower, same result).
 struct RowCache {
-    uint32_t row = 0, nc = 0;
-    Guid16 cg{0, 0};
+    uint32_t row = 0, nc = 0;  // nc: the row's leading non-zero slots among the first G, or t.R when all G are
+    Guid16 cg{0, 0};           // (then the lookup walks on in global memory up to the first zero slot)
     bool has = false;
 };
 
+template <int G>
 __device__ __forceinline__ RowCache row_cache(const Table& t, const uint32_t* __restrict__ rows, uint64_t m, bool live, uint32_t g) {
     RowCache rc;
     if (live) {
         rc.row = rows[m];
-        rc.nc = t.ncols[rc.row];
         if (g < t.R) {
             rc.cg = t.cols[(uint64_t)rc.row * t.R + g];
             rc.has = true;
         }
     }
+    const unsigned long long b = __ballot(rc.has && (rc.cg.lo | rc.cg.hi) != 0);  // every lane of the wave
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long gm = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+    const unsigned long long bits = (b >> (lane - g)) & gm;
+    const uint32_t lead = bits == gm ? (uint32_t)G : (uint32_t)__ffsll((long long)~bits) - 1;
+    rc.nc = lead == (uint32_t)G && t.R > (uint32_t)G ? t.R : lead;
     return rc;
 }
 
-// Column of Guid x in the row (find_col's answer), from the LDS cache and, past G columns, global.
+// Column of Guid x in the row (find_col's answer), from the LDS cache and, past G columns, global (up to
+// the first zero slot, the end of the row's columns).
 template <int G>
 __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16* __restrict__ gcols, uint32_t nc, const Guid16& x,
                                                uint32_t hint) {
@@ -198,8 +211,11 @@ __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16
     if (hint < ncache && same(cache[hint], x)) return hint;
     for (uint32_t j = 0; j < ncache; ++j)
         if (same(cache[j], x)) return j;
-    for (uint32_t j = ncache; j < nc; ++j)
-        if (same(gcols[j], x)) return j;
+    for (uint32_t j = ncache; j < nc; ++j) {
+        const Guid16 h = gcols[j];
+        if ((h.lo | h.hi) == 0) break;
+        if (same(h, x)) return j;
+    }
     return UINT32_MAX;
 }
 
@@ -373,7 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         // a node wave (csrc/node.hip) holds every kind's messages: those of other kinds carry kSkipIdx
         const bool skip = m < m1 && rows[m] == jg::kSkipIdx;
         const bool live = m < m1 && !skip;
-        const RowCache rc = row_cache(t, rows, m, live, g);
+        const RowCache rc = row_cache<G>(t, rows, m, live, g);
         GroupParse<EB, G> gp;
         group_parse<EB, G>(sh, bytes, off, m, live, rc, gp);
         // each parsed entry (on the lane its token was dealt to): its column and the repeat check

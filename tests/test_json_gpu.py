@@ -344,6 +344,48 @@ def test_row_capacity_rolls_back(ctx):
     pr.close()
 
 
+@pytest.mark.parametrize("group", ["1", "8"])
+def test_rolled_back_slots_never_match(ctx, group, monkeypatch):
+    """Pass A finds a row's columns as its leading non-zero slots (it reads no column count), so a roll-back
+    must zero the slots it uncounts: a failed wave appended gs[0], gs[1] to key 1 and was rolled back; the
+    next wave names gs[1] alone, which must become key 1's column 1 (the oracle's order), not match the
+    stale slot 2 the failed walk wrote.  Then steady waves over the new columns (the fused path)."""
+    monkeypatch.setenv("JANUS_JSON_GROUP", group)
+    rng = np.random.default_rng(61)
+    stable = random_guids(rng, 3)
+    pr = Pair(ctx, 3, 3, 4, stable)
+    gs = random_guids(rng, 4)
+    msgs = [encode_pnc(gs[:2], [2, 2], [0, 0]), encode_pnc(gs[:3], [1, 1, 1], [0, 0, 0])]
+    keys = np.array([1, 2], np.uint32)  # key 2 would need 1 + 3 = 4 columns: the wave fails in pass C
+    with pytest.raises(jg.JanusError):
+        pr.s.merge_json(keys, msgs)
+    pr.check()
+    for wave in ([encode_pnc([gs[1]], [5], [1])], [encode_pnc([gs[1], gs[2]], [6, 7], [1, 2])],
+                 [encode_pnc([stable[1], gs[1], gs[2]], [1, 9, 9], [0, 3, 3])]):
+        keys = np.array([1], np.uint32)
+        assert pr.oracle(keys, wave) == (None, 0)
+        pr.s.merge_json(keys, wave)
+        pr.check()
+    pr.close()
+
+
+def test_all_zero_guid_replica(ctx):
+    """A replica whose Guid is all-zero (Guid.Empty) is a column like any other; pass A cannot tell it from an
+    unused slot and leaves its messages to the deferred path, whose result must equal the oracle's."""
+    rng = np.random.default_rng(62)
+    stable = random_guids(rng, 4)
+    pr = Pair(ctx, 4, 4, 8, stable)
+    zero = (0, 0)
+    g1 = random_guids(rng, 1)[0]
+    for k, wave in enumerate([[encode_pnc([zero, g1], [3, 4], [0, 1])], [encode_pnc([g1, zero], [5, 2], [1, 7])],
+                              [encode_pnc([stable[2], zero, g1], [1, 8, 8], [0, 0, 9])], [encode_pnc([zero], [9], [9])]]):
+        keys = np.array([2], np.uint32)
+        assert pr.oracle(keys, wave) == (None, 0)
+        pr.s.merge_json(keys, wave)
+        pr.check()
+    pr.close()
+
+
 def test_intern_order_repeats_and_capacity(ctx):
     s = jg.PNCStore(ctx, 4, 3, 8)
     keys = np.array([1, 0, 1, 1, 0, 1], np.uint32)
