@@ -81,6 +81,20 @@ uint32_t GpuStableStore::elem_id_in(SetKey& s, PendingNames* pn, const std::stri
     return id;
 }
 
+void GpuStableStore::ensure_uid_index() {
+    if (uidx_n_ == uids_.size()) return;
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)uids_.size()) cap <<= 1;
+    uidx_.assign(cap, UidSlot{0, 0, nullptr, 0});
+    uidx_mask_ = cap - 1;
+    for (const auto& kv : uids_) {
+        uint64_t h = uid_slot0(kv.first);
+        while (uidx_[h].kr) h = (h + 1) & uidx_mask_;
+        uidx_[h] = UidSlot{kv.first.lo, kv.first.hi, &kv.second, 0};
+    }
+    uidx_n_ = uids_.size();
+}
+
 void GpuStableStore::CreateSafeCRDT(const Guid& uid, CrdtType type, const Guid& stableReplicaGuid) {
     if (uids_.count(uid)) return;
     KeyRef kr{type, 0};
@@ -762,10 +776,13 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<uint32_t> krow(n);
     std::vector<uint8_t> kpn(n);  // 1: a PN-Counter key
     std::vector<size_t> first_bad(pool().size(), n);
+    ensure_uid_index();
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+        constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
+        for (size_t i = b; i < std::min(e, b + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
         for (size_t i = b; i < e; ++i) {
-            const auto it = uids_.find(ups[i].op.uid);
-            const KeyRef* kr = it == uids_.end() ? nullptr : &it->second;
+            if (i + kAhead < e) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
+            const KeyRef* kr = find_uid(ups[i].op.uid);
             kref[i] = kr;
             if (kr) krow[i] = kr->idx, kpn[i] = kr->type == CrdtType::PNCounter ? 1 : 0;
             if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
@@ -947,13 +964,18 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             std::vector<size_t> at(pnc_need.size());
             std::vector<int32_t> wof(idx.size(), -1);  // position in pnc_need of a needed op
             for (size_t w = 0; w < pnc_need.size(); ++w) wof[pnc_need[w]] = (int32_t)w;
-            // rows are independent: worker t walks the round backwards over the rows with row % T == t
+            // rows are independent: worker t walks the round backwards over the rows with row % T == t (each op's
+            // owner computed once, by the workers: a division per op in every worker's walk was most of the rewind)
             const size_t T = (size_t)std::max(1, pool().size());
+            std::vector<uint16_t> own(idx.size());
+            parallel_ranges(pool(), idx.size(), [&](size_t b, size_t e, int) {
+                for (size_t j = b; j < e; ++j) own[j] = kpn[idx[j]] ? (uint16_t)(krow[idx[j]] % T) : (uint16_t)0xFFFF;
+            });
             parallel_ranges(pool(), T, [&](size_t tb0, size_t te0, int) {
                 for (size_t t = tb0; t < te0; ++t) {
                     for (size_t j = idx.size(); j-- > 0;) {
+                        if (own[j] != t) continue;
                         const size_t i = idx[j];
-                        if (!kpn[i] || krow[i] % T != t) continue;
                         const ClientOp& op = ups[i].op;
                         auto& a = pnc_after_[krow[i]];
                         if (wof[j] >= 0) {
@@ -966,8 +988,8 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                         const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
                         (op.opId == 2 ? a.second : a.first) += amt;
                     }
-                    for (size_t i : idx)
-                        if (kpn[i] && krow[i] % T == t) pnc_after_[krow[i]] = {0, 0};
+                    for (size_t j = 0; j < idx.size(); ++j)
+                        if (own[j] == t) pnc_after_[krow[idx[j]]] = {0, 0};
                 }
             }, 2);
             const double trw = trace ? now() : 0;
