@@ -44,9 +44,15 @@ struct GroupShared {
     uint32_t mask[kGroups][2 * kMaskCols / 32];    // pass A: columns seen per vector (LDS: 7 workgroups per CU, not 6)
     uint32_t tk[kGroups];                          // tokens | the "nVector" token << 8 | "nVector" tokens seen << 16
     uint32_t flags[kGroups];
-    uint32_t geo[kGroups], row[kGroups], nc[kGroups];  // alignment offset | length << 4; the row, its columns
-    uint32_t nr[kGroups];                          // fused pass A: entries the group's message raised (undo records)
+    // alignment offset | length << 4 | the row's cached column count << 14 | (fused pass A) entries the message
+    // raised (its undo records) << 23: one word, so the block's LDS (23,040 B) stays a whole number of 512-B
+    // allocation granules below a seventh of the CU's 160 KB
+    uint32_t geo[kGroups], row[kGroups];
 };
+__device__ __forceinline__ uint32_t geo_len(uint32_t geo) { return (geo >> 4) & 0x3FFu; }
+__device__ __forceinline__ uint32_t geo_nc(uint32_t geo) { return (geo >> 14) & 0x1FFu; }
+constexpr uint32_t kGeoNr = 23;
+static_assert(kGroupBytes <= 0x3FFu && kMaxJsonReplicas <= 0x1FFu && kEmitMax <= 0x1FFu, "geo's fields fit");
 __device__ __forceinline__ uint32_t tk_ntok(uint32_t tk) { return tk & 0xFFu; }
 __device__ __forceinline__ uint32_t tk_kn(uint32_t tk) { return (tk >> 8) & 0xFFu; }
 __device__ __forceinline__ uint32_t tk_nn(uint32_t tk) { return tk >> 16; }
@@ -220,7 +226,7 @@ __device__ __forceinline__ uint32_t cached_col(const Guid16* cache, const Guid16
 }
 
 // Phases 1-3 for message m on every lane of the group; on return sh.flags[grp] & kSlow is clear iff
-// the payload is proven compact, and the row cache is in sh.cols / sh.row / sh.nc.
+// the payload is proven compact, and the row cache is in sh.cols / sh.row / sh.geo.
 template <int EB, int G>
 __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                             uint64_t m, bool live, const RowCache& rc, GroupParse<EB, G>& gp) {
@@ -287,10 +293,8 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
     if (g == 0) {
         sh.flags[grp] = go ? 0 : kSlow;
         sh.tk[grp] = nt;
-        sh.geo[grp] = a | L << 4;
+        sh.geo[grp] = a | L << 4 | rc.nc << 14;
         sh.row[grp] = rc.row;
-        sh.nc[grp] = rc.nc;
-        sh.nr[grp] = 0;
     }
     for (uint32_t i = g; i < 2 * kMaskCols / 32; i += G) sh.mask[grp][i] = 0;
     wave_sync();
@@ -341,7 +345,7 @@ __device__ __forceinline__ void group_parse(GroupShared<G>& sh, const uint8_t* _
         for (uint32_t i = 1; i < GW; ++i)
             if (tw >= base[i]) { j = i; bj = base[i]; }
         const uint32_t gq = wg0 + j, e = tw - bj;
-        const uint32_t geo = sh.geo[gq], aq = geo & 15u, Lq = geo >> 4, tkq = sh.tk[gq], ntq = tk_ntok(tkq), kn = tk_kn(tkq);
+        const uint32_t geo = sh.geo[gq], aq = geo & 15u, Lq = geo_len(geo), tkq = sh.tk[gq], ntq = tk_ntok(tkq), kn = tk_kn(tkq);
         const uint32_t k = e + 1 + (e + 1 >= kn ? 1u : 0u);  // entry e's token: tokens 0 and kn are the names
         const uint8_t* cq = reinterpret_cast<const uint8_t*>(sh.buf[gq]) + aq;
         bool bad = false;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
             if (!gp.has[u] || (sh.flags[gq] & kSlow)) continue;
             const uint32_t kn = tk_kn(sh.tk[gq]), rq = sh.row[gq];
             const uint32_t vv = k < kn ? 0 : 1;
-            const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, sh.nc[gq], gp.eg[u], vv ? k - kn - 1 : k - 1);
+            const uint32_t col = cached_col<G>(sh.cols[gq], t.cols + (uint64_t)rq * t.R, geo_nc(sh.geo[gq]), gp.eg[u], vv ? k - kn - 1 : k - 1);
             colr[u] = col;
             if (col == UINT32_MAX) {
                 atomicOr(&sh.flags[gq], (uint32_t)kMiss);
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
                 if (*cell < v) {  // most states repeat what the cell holds: a plain read settles them
                     const T old = atomicMax(cell, v);
                     if (old < v) {
-                        const uint32_t r = atomicAdd(&sh.nr[gq], 1u);
+                        const uint32_t r = atomicAdd(&sh.geo[gq], 1u << kGeoNr) >> kGeoNr;
                         reinterpret_cast<uint16_t*>(h)[1 + r] = (uint16_t)(colr[u] | vv << 15);
                         reinterpret_cast<T*>(h + 32)[r] = old;
                     }
@@ -469,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
                 (f & kDup) ? kReparse
-                           : (fuse && !(f & kMiss)) ? (uint16_t)(kApplied | sh.nr[grp])
+                           : (fuse && !(f & kMiss)) ? (uint16_t)(kApplied | sh.geo[grp] >> kGeoNr)
                                                     : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
             if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
         }
