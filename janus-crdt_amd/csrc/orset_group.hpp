@@ -79,7 +79,7 @@ __device__ __forceinline__ uint32_t og_prefix_le(unsigned long long ballot, uint
     return (uint32_t)__popcll(ballot & (lane == 63 ? ~0ull : (2ull << lane) - 1ull));
 }
 
-__global__ __launch_bounds__(kBlock) void k_ow_group(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_ow_group(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                      const uint32_t* __restrict__ mset, uint64_t m0, uint64_t m1, Sparse S, uint64_t kmask, uint64_t salt,
                                                      unsigned long long* __restrict__ ne, unsigned long long* __restrict__ nt,
                                                      uint32_t* __restrict__ na, unsigned long long* __restrict__ err, uint8_t* __restrict__ slow) {

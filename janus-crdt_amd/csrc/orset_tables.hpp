@@ -260,7 +260,7 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
 // string, kUnresolved when the table or the set's generation word does not exist yet): the commit's
 // per-string lookup — a chain of dependent random loads, 141 us behind the last upload of the ORSetWorkload
 // wave — runs here, under the next chunk's upload.
-__global__ __launch_bounds__(kBlock) void k_ow_strings(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void k_ow_strings(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,
                                                        const uint8_t* __restrict__ bytes, const unsigned long long* __restrict__ ne,
                                                        const uint32_t* __restrict__ na, uint64_t m0, uint64_t m1, StrTab T,
                                                        unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow,
