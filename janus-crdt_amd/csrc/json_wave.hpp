@@ -589,6 +589,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve_rows(const unsigned long lon
     const uint32_t row = (uint32_t)(keys[i] >> 32);
     if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == row) return;  // not a segment head
     Guid16* gcols = t.cols + (uint64_t)row * t.R;
+    // the row's first kRC columns in registers, loaded together with its count (one round trip: the slots past
+    // the count are zero, row_cache), and each message's first kRC Guids loaded before its walk — the walk was a
+    // chain of dependent loads per entry (the Guid, then the columns one by one), 0.30 ms of a C5 wave's tail
+    constexpr uint32_t kRC = 8;
+    Guid16 rcol[kRC];
+#pragma unroll
+    for (uint32_t c = 0; c < kRC; ++c) rcol[c] = c < t.R ? gcols[c] : Guid16{0, 0};
     uint32_t nc = t.ncols[row];
     saved[i] = nc;
     for (uint64_t j = i; j < nd && (uint32_t)(keys[j] >> 32) == row; ++j) {
@@ -602,18 +609,35 @@ __global__ __launch_bounds__(kBlock) void k_resolve_rows(const unsigned long lon
         }
         const uint32_t cnt = hdr & ~kNeedsCols;
         uint16_t* codes = reinterpret_cast<uint16_t*>(h) + 1;
+        Guid16 xg[kRC];
+#pragma unroll
+        for (uint32_t e = 0; e < kRC; ++e) xg[e] = e < cnt ? eguid[m * kEmitMax + e] : Guid16{0, 0};
         Mask256 seen[2];  // columns met per vector
-        uint32_t err = UINT32_MAX, pos = 0, pv = 0;
+        uint32_t err = UINT32_MAX;
         for (uint32_t e = 0; e < cnt; ++e) {
             const uint32_t vv = codes[e] >> 15;
-            pos = e == 0 || vv != pv ? 0 : pos + 1;  // position within its vector (find_col's hint)
-            pv = vv;
-            const Guid16 x = eguid[m * kEmitMax + e];
-            uint32_t col = find_col(gcols, nc, x, pos);
+            Guid16 x = eguid[0];
+            if (e < kRC) {
+#pragma unroll
+                for (uint32_t q = 0; q < kRC; ++q)
+                    if (q == e) x = xg[q];
+            } else {
+                x = eguid[m * kEmitMax + e];
+            }
+            // the row's Guids are distinct: any match is the one find_col returns
+            uint32_t col = UINT32_MAX;
+#pragma unroll
+            for (uint32_t c = 0; c < kRC; ++c)
+                if (c < nc && same(rcol[c], x)) col = c;
+            for (uint32_t c = kRC; col == UINT32_MAX && c < nc; ++c)
+                if (same(gcols[c], x)) col = c;
             if (col == UINT32_MAX) {
                 if (nc >= t.R) { err = kErrFull; break; }
                 col = nc++;
                 gcols[col] = x;
+#pragma unroll
+                for (uint32_t c = 0; c < kRC; ++c)
+                    if (c == col) rcol[c] = x;
             }
             if (vv ? seen[1].test_set(col) : seen[0].test_set(col)) { err = kErrSyntax; break; }  // repeated Guid in one vector
             codes[e] = (uint16_t)(col | vv << 15);
