@@ -538,6 +538,15 @@ struct DeferredLists {
     int end_bit;
 };
 
+// Radix sorts of the (row << 32 | index) keys on the row bits: Onesweep at every size.  hipcub's default takes a
+// block sort plus merge passes below 1M items (the config's merge_sort_limit), ~200 us for a C5 wave's ~0.5M
+// deferred entries, whatever the bit range; three 8-bit Onesweep passes cover 1M rows.
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+hipError_t sort_row_keys(void* tmp, size_t& bytes, const unsigned long long* in, unsigned long long* out, uint64_t n, int end_bit,
+                         hipStream_t stream) {
+    return rocprim::radix_sort_keys<OnesweepSort>(tmp, bytes, in, out, (size_t)n, 32u, (unsigned)end_bit, stream);
+}
+
 DeferredLists select_deferred(jg_ctx* ctx, const unsigned long long* marks, uint64_t n, uint64_t n_keys, unsigned long long* count) {
     JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "sort: %llu entries exceed one radix sort", (unsigned long long)n);
     using ull = unsigned long long;
@@ -547,7 +556,7 @@ DeferredLists select_deferred(jg_ctx* ctx, const unsigned long long* marks, uint
     d.end_bit = 32 + row_bits;
     size_t tsel = 0, tsort = 0;
     JG_HIP(hipcub::DeviceSelect::If(nullptr, tsel, marks, (ull*)nullptr, (ull*)nullptr, (int)n, IsDeferred(), ctx->stream));
-    JG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tsort, (ull*)nullptr, (ull*)nullptr, (int)n, 0, d.end_bit, ctx->stream));
+    JG_HIP(sort_row_keys(nullptr, tsort, (const ull*)nullptr, (ull*)nullptr, n, d.end_bit, ctx->stream));
     const size_t a = (n * 8 + 255) & ~255ull;
     d.tmp_bytes = std::max(tsel, tsort);
     char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, 2 * a + d.tmp_bytes + 256));
@@ -558,24 +567,27 @@ DeferredLists select_deferred(jg_ctx* ctx, const unsigned long long* marks, uint
     return d;
 }
 
+// The list comes out of the (stable) select in message order, so a stable sort on the row bits alone gives the
+// order of the whole key (row, then message): 20 bits for 1M keys instead of 52.
 unsigned long long* sort_deferred(jg_ctx* ctx, DeferredLists& d, uint64_t nd) {
     size_t t = d.tmp_bytes;
-    JG_HIP(hipcub::DeviceRadixSort::SortKeys(d.tmp, t, d.list, d.sorted, (int)nd, 0, d.end_bit, ctx->stream));
+    JG_HIP(sort_row_keys(d.tmp, t, d.list, d.sorted, nd, d.end_bit, ctx->stream));
     return d.sorted;
 }
 
-// Sort `n` 64-bit keys (row << 32 | index) in place through ctx scratch.  end_bit covers the row bits.
+// Sort `n` 64-bit keys (row << 32 | index) in place through ctx scratch.  end_bit covers the row bits; the keys
+// arrive in index order (k_make_keys), so a stable sort on the row bits alone orders the whole key.
 unsigned long long* sort_keys(jg_ctx* ctx, unsigned long long* keys, uint64_t n, uint64_t n_keys) {
     JG_REQUIRE(n <= 0x7FFFFFFFull, JG_EINVAL, "sort: %llu entries exceed one radix sort", (unsigned long long)n);
     int row_bits = 1;
     while (row_bits < 32 && (1ull << row_bits) < n_keys) ++row_bits;
     const int end_bit = 32 + row_bits;
     size_t temp = 0;
-    JG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, temp, keys, keys, (int)n, 0, end_bit, ctx->stream));
+    JG_HIP(sort_row_keys(nullptr, temp, keys, keys, n, end_bit, ctx->stream));
     char* s = static_cast<char*>(jg::scratch(ctx, ctx->scratch3, temp + n * 8 + 256));
     unsigned long long* out = reinterpret_cast<unsigned long long*>(s);
     void* tmp = s + ((n * 8 + 255) & ~255ull);
-    JG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, temp, keys, out, (int)n, 0, end_bit, ctx->stream));
+    JG_HIP(sort_row_keys(tmp, temp, keys, out, n, end_bit, ctx->stream));
     return out;
 }
 
