@@ -97,3 +97,24 @@ def test_bench_names_the_decode_bound_from_the_newest_summary(tmp_path, monkeypa
     roof2 = {"decode": {"bound": "hbm"}}
     bench.name_decode_bound(roof2)
     assert roof2["decode_counters"] is None and roof2["decode"]["bound"] == "hbm"
+
+
+def test_json_scan_split_separates_steady_and_cold_waves(tmp_path):
+    """The json leg's profile holds steady waves (the scan alone: pass A applies the cells) and cold ones (the scan,
+    then k_resolve_rows and k_apply_emit); pmc_summary reports the scan's bytes of the steady ones, in dispatch order
+    whatever the CSV's row order."""
+    ps = _load("pmc_summary", ROOT / "janus-crdt_amd" / "tools" / "pmc_summary.py")
+    seq = [("k_reset_status", 0), ("void k_scan<4, 8>(x)", 300), ("k_scan_slow<4>", 0), ("void k_resolve_rows<4>(x)", 240),
+           ("void k_apply_emit<4>(x)", 66),
+           ("k_reset_status", 0), ("void k_scan<4, 8>(x)", 400), ("k_scan_slow<4>", 0),
+           ("k_reset_status", 0), ("void k_scan<4, 8>(x)", 410), ("rocprim::detail::sort", 3),
+           ("void k_scan<4, 8>(x)", 290), ("void k_apply_emit<4>(x)", 66)]
+    path = tmp_path / "run_counter_collection.csv"
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for i, (k, v) in reversed(list(enumerate(seq))):  # rows out of dispatch order
+            w.writerow({"Dispatch_Id": i + 1, "Kernel_Name": k, "Counter_Name": "FETCH_SIZE", "Counter_Value": v})
+    out = ps.json_scan_split(path, "FETCH_SIZE")
+    assert out["steady"] == [400 * 1024, 410 * 1024]
+    assert out["cold"] == [300 * 1024, 290 * 1024]
