@@ -348,13 +348,20 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         c->timeout_s = timeout_from_env();
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof u);
-        // A non-blocking communicator (blocking = 0): every later call returns ncclInProgress instead of
-        // waiting, and this library polls it against the deadline on the calling thread.  The rendezvous itself
-        // can still wait inside ncclCommInitRankConfig for a peer that never arrives (this RCCL's bootstrap
-        // blocks there even for a non-blocking config), so it runs on a thread of its own, which then polls the
-        // communicator until it is ready.  This call waits for that thread against the deadline; past it the
-        // thread is abandoned and aborts the communicator itself if it ever gets one (it is the handle's only
-        // owner until the hand-over), and the call returns JG_EHIP.
+        // A non-blocking communicator (blocking = 0): every later call returns ncclInProgress instead of waiting,
+        // and this library polls it against the deadline on the calling thread.
+        //
+        // The rendezvous.  ncclCommInitRankConfig OUTSIDE a group runs the whole init, the bootstrap's wait for every
+        // rank included, on the calling thread even for a non-blocking config (RCCL queues it as an async job and,
+        // with no group open, runs the job at once).  Round 5 therefore ran it on a detached thread; a rank that
+        // gave up left that thread inside the bootstrap, and static teardown at exit then faulted under it (rc 139
+        // after the timeout, gpurun_out/comm_dbg.log).  INSIDE ncclGroupStart / ncclGroupEnd the
+        // non-blocking config makes ncclGroupEnd hand the job to RCCL's own thread and return ncclInProgress with the
+        // handle set: the handle is polled here against the deadline and, past it, aborted here (ncclCommAbort raises
+        // the init's abort flag, which the bootstrap's sockets check, and reclaims the job), so nothing of the
+        // rendezvous outlives the call.  The group calls themselves run on a helper thread this call joins within
+        // the deadline; should they block after all, the helper is left behind as before and the call still
+        // returns JG_EHIP on time.
         struct Job {
             std::mutex m;
             std::condition_variable cv;
@@ -364,47 +371,68 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         };
         auto job = std::make_shared<Job>();
         const int dev = ctx->device;
-        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRankConfig (rank %u of %u, non-blocking)\n", rank, world);
-        std::thread([job, u, rank, world, dev] {
+        const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(c->timeout_s));
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRankConfig in a group (rank %u of %u, non-blocking)\n", rank, world);
+        std::thread helper([job, u, rank, world, dev] {
             (void)hipSetDevice(dev);
             ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
             cfg.blocking = 0;
             ncclComm_t nc = nullptr;
-            ncclResult_t r = ncclCommInitRankConfig(&nc, (int)world, u, (int)rank, &cfg);
-            while (r == ncclInProgress && nc) {
-                {
-                    std::lock_guard<std::mutex> g(job->m);
-                    if (job->abandoned) break;
-                }
-                ncclResult_t a = ncclInProgress;
-                const ncclResult_t q = ncclCommGetAsyncError(nc, &a);
-                r = q != ncclSuccess ? q : a;
-                if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(100));
+            ncclResult_t r = ncclGroupStart();
+            if (r == ncclSuccess) {
+                r = ncclCommInitRankConfig(&nc, (int)world, u, (int)rank, &cfg);
+                const ncclResult_t e = ncclGroupEnd();
+                if (r == ncclSuccess || r == ncclInProgress) r = e;
             }
             std::lock_guard<std::mutex> g(job->m);
-            if (job->abandoned || r != ncclSuccess) {
+            if (job->abandoned) {  // the caller gave up first (this RCCL blocked in the group calls): the handle is ours
                 if (nc) (void)ncclCommAbort(nc);
-                nc = nullptr;
-                if (job->abandoned) return;
+                return;
             }
             job->r = r;
             job->nc = nc;
             job->done = true;
             job->cv.notify_all();
-        }).detach();
+        });
         {
             std::unique_lock<std::mutex> g(job->m);
-            const auto end = Clock::now() + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(c->timeout_s));
             if (!job->cv.wait_until(g, end, [&] { return job->done; })) {
                 job->abandoned = true;
-                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous timed out\n");
+                g.unlock();
+                helper.detach();
+                if (trace_comm()) std::fprintf(stderr, "jg_comm: the group calls did not return; helper left behind\n");
                 jg::fail(JG_EHIP, "jg_comm_init: not every rank joined in %.0f s (rank %u of %u); JANUS_COMM_TIMEOUT_S sets the wait", c->timeout_s,
                          rank, world);
             }
         }
-        if (trace_comm()) std::fprintf(stderr, "jg_comm: ncclCommInitRankConfig settled: %s\n", ncclGetErrorString(job->r));
-        JG_REQUIRE(job->r == ncclSuccess && job->nc, JG_EHIP, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(job->r));
+        helper.join();
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: group returned: %s\n", ncclGetErrorString(job->r));
+        if (job->r != ncclSuccess && job->r != ncclInProgress) {
+            if (job->nc) (void)ncclCommAbort(job->nc);
+            jg::fail(JG_EHIP, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(job->r));
+        }
+        JG_REQUIRE(job->nc, JG_EHIP, "ncclCommInitRankConfig returned no communicator");
         c->nc = job->nc;
+        // the rendezvous polled to completion on this thread against what is left of the deadline; past it the
+        // communicator is aborted here (abort_comm) and the call returns JG_EHIP
+        for (;;) {
+            ncclResult_t a = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(c->nc, &a);
+            if (q != ncclSuccess) a = q;
+            if (a == ncclSuccess) break;
+            if (a != ncclInProgress) {
+                abort_comm(c.get());
+                jg::fail(JG_EHIP, "jg_comm_init: the rendezvous failed: %s; the communicator was aborted", ncclGetErrorString(a));
+            }
+            if (Clock::now() > end) {
+                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous timed out\n");
+                abort_comm(c.get());
+                jg::fail(JG_EHIP, "jg_comm_init: not every rank joined in %.0f s (rank %u of %u); JANUS_COMM_TIMEOUT_S sets the wait", c->timeout_s,
+                         rank, world);
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous complete\n");
         c->rccl = true;
         *out = c.release();
     });
@@ -454,6 +482,7 @@ int jg_pnc_exchange(jg_comm* c, jg_pnc* store, const jg_rows* rows, uint64_t* se
     return jg::guard([&] {
         usable(c, "jg_pnc_exchange");
         JG_REQUIRE(store, JG_EINVAL, "jg_pnc_exchange: NULL argument");
+        jg::require_writable(store, "jg_pnc_exchange");
         JG_REQUIRE(store->ctx == c->ctx && (!rows || rows->ctx == c->ctx), JG_EINVAL,
                    "jg_pnc_exchange: the store and the batch must be on the communicator's context");
         JG_REQUIRE(!rows || (store->R == rows->R && store->eb == rows->eb), JG_EINVAL,
@@ -520,6 +549,8 @@ int jg_orset_exchange(jg_comm* c, jg_orset* store, jg_orset* received, uint64_t*
         JG_REQUIRE(store && received, JG_EINVAL, "jg_orset_exchange: NULL argument");
         JG_REQUIRE(store->ctx == c->ctx && received->ctx == c->ctx, JG_EINVAL, "jg_orset_exchange: the stores must be on the communicator's context");
         JG_REQUIRE(store != received, JG_EINVAL, "jg_orset_exchange: the received state cannot be the store itself");
+        jg::require_writable(store, "jg_orset_exchange");
+        jg::require_writable(received, "jg_orset_exchange");
         auto lk_ = jg::lock(c->ctx);
         jg_ctx* ctx = c->ctx;
         jg::ensure_device(ctx);

@@ -145,6 +145,8 @@ struct jg_pnc {
     uint64_t wn = 0, wnb = 0;
     uint64_t scan_hi = 0;  // messages pass A scanned since the wave began (its fused applies are undone below this)
     bool wopen = false;
+    bool fuse = true;       // the wave's pass A applies what it proves (JANUS_JSON_FUSE, latched when the wave begins)
+    bool node_open = false;  // a node wave (node.hip) holds the store: see jg::require_writable
 };
 
 // Device-resident wave of encoded state messages (json.hip jg_wave_*; digest.hip reads it too).
@@ -206,6 +208,7 @@ struct jg_orset {
     jg::DevBuf counts;     // device-side uint64 [2]: n_add, n_rem written by the union kernel
     bool counts_pending = false;  // an async union wrote `counts`; host n's are stale
     jg_orset_wire* wire = nullptr;
+    bool node_open = false;  // a node wave (node.hip) holds the store: see jg::require_writable
     jg_orset() = default;
     jg_orset(const jg_orset&) = delete;
     jg_orset& operator=(const jg_orset&) = delete;
@@ -226,6 +229,14 @@ inline void pin_get(jg_ctx* ctx, size_t at, const void* d, size_t n) {
 inline void pin_sync(jg_ctx* ctx) { JG_HIP(hipStreamSynchronize(ctx->stream)); }  // (polling measured no gain)
 inline const void* pin_at(jg_ctx* ctx, size_t at) { return static_cast<const char*>(ctx->hstat) + at; }
 template <class H> inline CtxLock lock(const H* h) { return lock(h ? h->ctx : nullptr); }
+// A node wave (node.hip) holds its stores from its begin to its end: the PN-Counter store's wave scratch and
+// fused pass A's undo records, the OR-Set store's wave tables (whose element-table lookups assume the committed
+// names do not change until the commit).  The one-call form runs under the context lock, but the streamed form
+// (jg_apply_stream_begin / _append / _end) keeps the wave open across unlocked calls, so every call that writes
+// a store, or reuses the scratch its open wave holds, is refused until the wave ends.
+template <class S> inline void require_writable(const S* s, const char* fn) {
+    JG_REQUIRE(!s || !s->node_open, JG_EINVAL, "%s: a node wave (jg_apply_stream_begin .. _end) holds this store", fn);
+}
 void ensure_device(jg_ctx* ctx);  // hipSetDevice(ctx->device) on the calling thread
 void* scratch(jg_ctx* ctx, DevBuf& b, size_t bytes);
 // After H2D copies queued on ctx->copy: make ctx->stream wait for them (stream order for the kernels

@@ -9,7 +9,8 @@
 //   pass A  k_scan      8 lanes per message (json_wave.hpp) prove the payload is the compact form
 //                       System.Text.Json writes and check it against the wire contract of
 //                       oracle/json.hpp; every Guid is looked up in its row's replica table (read-only);
-//                       a Guid repeated among a vector's known replicas is an error.  Each message
+//                       a Guid repeated among a vector's known replicas sends the message to the serial
+//                       parser (System.Text.Json keeps the key's last value at its first place).  Each message
 //                       leaves a record: its entries' columns and values (pass B applies it), or, when
 //                       it names a replica its row has not seen (DEFERRED, marked per message), the
 //                       entries' Guids and values with the columns still open.  Payloads not in the
@@ -22,9 +23,9 @@
 //                       order and appends the new replica Guids (pVector entries first, then nVector —
 //                       Merge's order) to the row's table: first-insertion order = the stable
 //                       Dictionary's enumeration order; the columns go back into the records.  A walk
-//                       reaching a non-compact message continues serially (k_resolve_resume).  A full
-//                       row or a Guid repeated in one vector rolls the appended columns back and fails
-//                       the call.
+//                       reaching a non-compact message continues serially (k_resolve_resume).  A Guid
+//                       repeated in one vector keeps its first place and its last value (the earlier
+//                       entries are voided).  A full row rolls the appended columns back and fails the call.
 //   pass B  k_apply_emit  one lane per record entry, atomicMax into P / N (messages of one wave may
 //                       repeat a key; max is order-free); k_apply_list parses the slow list again.
 //
@@ -130,42 +131,99 @@ __device__ __forceinline__ bool read_int(Cursor& c, long long& out) {
     return true;
 }
 
-// Property name "pVector" / "nVector" (no escapes).  Returns 0 / 1, or -1.
-__device__ __forceinline__ int read_name(Cursor& c) {
+// ---- the decode contract (oracle/json.hpp, System.Text.Json 6.0's defaults) ------------------------------------
+// Property names are matched after unescaping; a member the type does not have is skipped (jgw::skip_value); a
+// member given twice takes its last occurrence; a Guid key repeated inside one vector keeps its first place and
+// takes its last value (Dictionary's indexer).  The compact form System.Text.Json writes — every state a reference
+// node emits — is proven by the group parse (json_wave.hpp); the serial parser below runs only on the rest.
+
+struct PncPropSink {  // "pVector" -> 0, "nVector" -> 1, anything else -> 2 (case-sensitive, unescaped)
+    uint32_t len = 0, mask = 3;
+    __device__ void esc() {}
+    __device__ void put(int b) {
+        const char* rest = "Vector";
+        if (len == 0) mask &= (b == 'p' ? 1u : 0u) | (b == 'n' ? 2u : 0u);
+        else if (len > 6 || rest[len - 1] != (char)b) mask = 0;
+        ++len;
+    }
+    __device__ int which() const { return len == 7 && mask ? (mask & 1 ? 0 : 1) : 2; }
+};
+
+// A property name (after its opening quote has been found): 0 / 1 / 2 as PncPropSink, -1 if not a string.
+__device__ __forceinline__ int read_prop(Cursor& c) {
     if (!c.expect('"')) return -1;
-    const int f = c.get();
-    const char* rest = "Vector\"";
-    for (int i = 0; i < 7; ++i)
-        if (c.get() != rest[i]) return -1;
-    return f == 'p' ? 0 : f == 'n' ? 1 : -1;
+    PncPropSink ps;
+    if (!jgw::read_string(c, ps)) return -1;
+    return ps.which();
 }
 
-// Parse one PNCounterMsg; vis.entry(which, pos, guid, value) returns false to abort (error).
-// `only` = -1 visits both vectors, 0 / 1 only pVector / nVector (the other is still validated).
-template <int EB, class V>
-__device__ bool parse_pnc(Cursor& c, V& vis, int only = -1) {
+// A Guid key after its opening quote: the raw 36-character form, or (escapes) the unescaped string's.
+__device__ __forceinline__ bool read_key(Cursor& c, Guid16& g) {
+    Cursor t = c;
+    if (read_guid(t, g)) {
+        c = t;
+        return true;
+    }
+    jgw::GuidSink gs;
+    if (!jgw::read_string(c, gs) || !gs.ok()) return false;
+    g.lo = gs.lo();
+    g.hi = gs.hi;
+    return true;
+}
+
+__device__ __forceinline__ bool same_guid(const Guid16& a, const Guid16& b) { return a.lo == b.lo && a.hi == b.hi; }
+
+// Per vector, over the whole message: occurrences of the member, whether the last one is `null`, and whether the
+// last one may repeat a key (a 128-bit filter of its keys: no shared bit = no repeat, so the common state skips the
+// repeat scans).
+struct VecInfo {
+    uint32_t occ = 0;
+    bool null_last = false, maybe_dup = false;
+};
+
+// The whole payload checked (every occurrence of every member, skipped ones included): true iff System.Text.Json
+// decodes it and both vectors end non-null (else Merge would throw).  No visits.
+template <int EB>
+__device__ bool validate_pnc(Cursor& c, VecInfo (&vi)[2]) {
     if (!c.expect('{')) return false;
-    int seen = 0;
+    c.ws();
+    if (c.peek() == '}') return false;  // {}: both vectors missing
     for (;;) {
-        const int which = read_name(c);
-        if (which < 0 || (seen >> which & 1)) return false;
-        seen |= 1 << which;
-        if (!c.expect(':') || !c.expect('{')) return false;  // `null` fails here too
-        vis.begin_vector(which);
-        c.ws();
-        if (c.peek() == '}') {
-            ++c.p;
+        const int which = read_prop(c);
+        if (which < 0 || !c.expect(':')) return false;
+        if (which == 2) {
+            if (!jgw::skip_value(c, 1)) return false;
         } else {
-            for (uint32_t pos = 0;; ++pos) {
-                if (!c.expect('"')) return false;
-                Guid16 g;
-                long long v;
-                if (!read_guid(c, g) || !c.expect(':') || !read_int<EB>(c, v)) return false;
-                if ((only < 0 || only == which) && !vis.entry(which, pos, g, v)) return false;
+            VecInfo& v = vi[which];
+            ++v.occ;
+            v.maybe_dup = false;
+            c.ws();
+            v.null_last = c.peek() == 'n';
+            if (v.null_last) {
+                if (!jgw::take_literal(c, "null")) return false;
+            } else {
+                if (!c.expect('{')) return false;
+                unsigned long long f0 = 0, f1 = 0;
                 c.ws();
-                const int ch = c.get();
-                if (ch == '}') break;
-                if (ch != ',') return false;
+                if (c.peek() == '}') {
+                    ++c.p;
+                } else {
+                    for (;;) {
+                        Guid16 g;
+                        long long x;
+                        if (!c.expect('"') || !read_key(c, g) || !c.expect(':') || !read_int<EB>(c, x)) return false;
+                        const uint32_t h = (uint32_t)((g.lo ^ g.hi) * 0x9E3779B97F4A7C15ull >> 57);  // 7 bits
+                        const unsigned long long b = 1ull << (h & 63);
+                        const bool hit = (h & 64) ? (f1 & b) != 0 : (f0 & b) != 0;
+                        v.maybe_dup |= hit;
+                        if (h & 64) f1 |= b;
+                        else f0 |= b;
+                        c.ws();
+                        const int ch = c.get();
+                        if (ch == '}') break;
+                        if (ch != ',') return false;
+                    }
+                }
             }
         }
         c.ws();
@@ -174,7 +232,97 @@ __device__ bool parse_pnc(Cursor& c, V& vis, int only = -1) {
         if (ch != ',') return false;
     }
     c.ws();
-    return seen == 3 && c.p == c.end;
+    return c.p == c.end && vi[0].occ && vi[1].occ && !vi[0].null_last && !vi[1].null_last;
+}
+
+// Parse one PNCounterMsg: vis.entry(which, pos, guid, value) for every entry of the decoded message (the last
+// occurrence of each vector; a repeated key once, at its first place, with its last value; pos = its place among
+// the vector's distinct keys), returning false to abort.  `only` = -1 visits both vectors, 0 / 1 only pVector /
+// nVector; begin_vector(which) opens each visited occurrence either way.  The payload is validated whole first
+// (validate_pnc), so a message is visited only if System.Text.Json decodes it.
+template <int EB, class V>
+__device__ bool parse_pnc(Cursor& c, V& vis, int only = -1) {
+    VecInfo vi[2];
+    {
+        Cursor t = c;
+        if (!validate_pnc<EB>(t, vi)) {
+            c = t;
+            return false;
+        }
+    }
+    uint32_t occ[2] = {0, 0};
+    (void)c.expect('{');
+    for (;;) {
+        const int which = read_prop(c);
+        (void)c.expect(':');
+        if (which == 2 || ++occ[which] < vi[which].occ) {
+            (void)jgw::skip_value(c, 1);  // validated: a skipped member, or an occurrence a later one replaces
+        } else {
+            vis.begin_vector(which);
+            (void)c.expect('{');
+            c.ws();
+            if (c.peek() == '}') {
+                ++c.p;
+            } else {
+                const Cursor vstart = c;
+                const bool dups = vi[which].maybe_dup;
+                uint32_t pos = 0;
+                for (;;) {
+                    c.ws();
+                    const uint64_t at = c.p;
+                    Guid16 g;
+                    long long v;
+                    (void)c.expect('"');
+                    (void)read_key(c, g);
+                    (void)c.expect(':');
+                    (void)read_int<EB>(c, v);
+                    bool first = true;
+                    if (dups) {  // a key met earlier in this vector was visited there; else its LAST value counts
+                        Cursor t = vstart;
+                        for (;;) {
+                            t.ws();
+                            if (t.p >= at) break;
+                            Guid16 h;
+                            long long y;
+                            (void)t.expect('"');
+                            (void)read_key(t, h);
+                            (void)t.expect(':');
+                            (void)read_int<EB>(t, y);
+                            if (same_guid(h, g)) {
+                                first = false;
+                                break;
+                            }
+                            (void)t.expect(',');
+                        }
+                        if (first) {
+                            Cursor t2 = c;
+                            for (;;) {
+                                t2.ws();
+                                if (t2.get() != ',') break;
+                                Guid16 h;
+                                long long y;
+                                (void)t2.expect('"');
+                                (void)read_key(t2, h);
+                                (void)t2.expect(':');
+                                (void)read_int<EB>(t2, y);
+                                if (same_guid(h, g)) v = y;
+                            }
+                        }
+                    }
+                    if (first) {
+                        if ((only < 0 || only == which) && !vis.entry(which, pos, g, v)) return false;
+                        ++pos;
+                    }
+                    c.ws();
+                    if (c.get() == '}') break;
+                }
+            }
+        }
+        c.ws();
+        if (c.get() == '}') break;
+    }
+    c.ws();
+    return true;
 }
 
 // ---- replica table helpers -------------------------------------------------------------------------
@@ -213,17 +361,15 @@ struct Mask256 {
     }
 };
 
-// Pass A visitor: known Guids checked for repeats; unknown Guids mark the message deferred.
+// Pass A visitor: unknown Guids mark the message deferred (parse_pnc visits a repeated key once).
 struct ScanVis {
     const Guid16* row;
     uint32_t n;
-    Mask256 m;
     bool miss = false;
-    __device__ void begin_vector(int) { m.clear(); }
+    __device__ void begin_vector(int) {}
     __device__ bool entry(int, uint32_t pos, const Guid16& g, long long) {
-        const uint32_t c = find_col(row, n, g, pos);
-        if (c == UINT32_MAX) { miss = true; return true; }
-        return !m.test_set(c);
+        if (find_col(row, n, g, pos) == UINT32_MAX) miss = true;
+        return true;
     }
 };
 
@@ -233,6 +379,7 @@ struct ScanVis {
 constexpr uint32_t kEmitMax = 14;
 constexpr uint16_t kReparse = 0xFFFF;
 constexpr uint32_t kNeedsCols = 0x4000;  // count flag: a deferred record whose columns pass C resolves
+constexpr uint32_t kVoidCol = 0x7FFF;    // entry code column of a voided entry (a key its vector repeats later)
 constexpr uint32_t kApplied = 0x2000;    // count flag: pass A applied the message itself (fused); low bits = the
                                          // entries it raised, recorded as (column code, old value) for the undo
 __host__ __device__ constexpr uint64_t emit_stride(uint32_t eb) { return 32 + kEmitMax * eb; }
@@ -282,11 +429,9 @@ struct ResolveVis {
     Guid16* row;
     uint32_t* ncol;
     uint32_t R;
-    Mask256 m;
     uint32_t err = UINT32_MAX;
     bool p_seen = false, n_skipped = false;
     __device__ void begin_vector(int which) {
-        m.clear();
         if (which == 0) p_seen = true;
     }
     __device__ bool entry(int which, uint32_t pos, const Guid16& g, long long) {
@@ -297,7 +442,6 @@ struct ResolveVis {
             c = (*ncol)++;
             row[c] = g;
         }
-        if (m.test_set(c)) { err = kErrSyntax; return false; }  // repeated Guid in one vector
         return true;
     }
 };
@@ -605,10 +749,13 @@ Status read_status(jg_ctx* ctx, const unsigned long long* d) {
     return s;
 }
 
+// kErrInternal (a message pass A accepted that a later pass could not parse or resolve again) is the library's
+// own inconsistency, never a verdict on the message: it leaves *bad_msg unset, so a node wave does not take it for
+// the reference's cut (pnc_node_finish rethrows, wave_end aborts the wave) and no caller blames the payload.
 [[noreturn]] void fail_msg(unsigned long long code, uint64_t* bad_msg, const char* what) {
     const uint64_t m = code >> 2;
     const uint32_t kind = (uint32_t)(code & 3);
-    if (bad_msg) *bad_msg = m;
+    if (bad_msg && kind != kErrInternal) *bad_msg = m;
     if (kind == kErrFull)
         jg::fail(JG_ESTATE, "%s %llu: its key holds more replicas than the store's columns", what, (unsigned long long)m);
     if (kind == kErrInternal) jg::fail(JG_EHIP, "%s %llu: internal replica-table inconsistency", what, (unsigned long long)m);
@@ -666,6 +813,9 @@ void reset_status(jg_ctx* ctx, unsigned long long* status) {
 }
 
 // JANUS_JSON_FUSE=0: pass A leaves every message to pass B (read per launch: tests and A/B runs switch it)
+// Latched into jg_pnc::fuse when a wave begins (merge_wave_dev, jg_pnc_wave_begin, pnc_node_begin): the chunks'
+// pass A and the wave's finish must agree on it, or finish_wave would skip pass B for records pass A left to it
+// (ADVICE r05).
 bool json_fuse() {
     const char* e = std::getenv("JANUS_JSON_FUSE");
     return !(e && std::strcmp(e, "0") == 0);
@@ -676,7 +826,7 @@ void launch_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     if (m1 <= m0) return;
     const Table t = table_of(p);
     const int G = json_group();
-    const bool fuse = json_fuse();
+    const bool fuse = p->fuse;
     if (p->eb == 8) launch_scan_g<8>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow, p->P.p, p->N.p, fuse);
     else launch_scan_g<4>(G, p->ctx->stream, bytes, off, rows, m0, m1, t, w.status, w.deferred, w.emit, w.eguid, w.slow, p->P.p, p->N.p, fuse);
     JG_HIP(hipGetLastError());
@@ -711,7 +861,7 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         // message both launches are no-ops and the full path below runs (all or nothing).  A fused pass A
         // (json_fuse) applied every record pass B would read here (a deferral sends the wave to the full path,
         // whose pass B runs unguarded): only the slow list's launch is left.
-        const bool fused = json_fuse();
+        const bool fused = p->fuse;
         if (p->eb == 8) {
             if (!fused) hipLaunchKernelGGL(k_apply_emit<8>, dim3(ge), dim3(kBlock), 0, ctx->stream, w.emit, rows, n, t.R, p->P.p, p->N.p, w.status);
             hipLaunchKernelGGL(k_apply_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, w.slow, t, p->P.p, p->N.p, w.status);
@@ -723,6 +873,8 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         const Status st = read_status(ctx, w.status);
         if (st.first_bad != ~0ull) undo_applied(p, rows), fail_msg(st.first_bad, bad_msg, "state message");
         if (!st.n_deferred) {
+            // only k_apply_slow can have set it here (no walk ran): kErrInternal, a JG_EHIP without a cut; the
+            // fused applies are taken back, the slow list's raises (no undo records) stay — an internal failure
             if (st.resolve_bad != ~0ull) undo_applied(p, rows), fail_msg(st.resolve_bad, bad_msg, "state message");
             return;
         }
@@ -773,7 +925,14 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
         JG_HIP(hipGetLastError());
     }
     st = read_status(ctx, w.status);
-    if (st.resolve_bad != ~0ull) fail_msg(st.resolve_bad, bad_msg, "state message");
+    // Past pass C every message has been judged, so only k_apply_list's re-parse (apply_one: kErrInternal) can set
+    // it now: the library's own inconsistency, raised as JG_EHIP without naming a message (fail_msg), so it is never
+    // taken for a cut whose prefix re-run would leave pass B's raises (no undo records) in the store.
+    if (st.resolve_bad != ~0ull) {
+        JG_REQUIRE((st.resolve_bad & 3) == kErrInternal, JG_EHIP, "pass B: status %llx after every message was judged", st.resolve_bad);
+        undo_applied(p, rows);
+        fail_msg(st.resolve_bad, bad_msg, "state message");
+    }
 }
 
 // The whole device side of a wave already in device memory.
@@ -782,6 +941,7 @@ void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
     const WaveScratch w = wave_scratch(p, n);
     reset_status(p->ctx, w.status);
     p->scan_hi = 0;
+    p->fuse = json_fuse();
     launch_scan(p, bytes, off, rows, 0, n, w);
     finish_wave(p, bytes, off, rows, n, w, bad_msg);
 }
@@ -807,7 +967,8 @@ void pnc_node_begin(jg_pnc* p, uint64_t n) {
     ensure_table(p);
     reset_status(p->ctx, wave_scratch(p, n).status);
     p->scan_hi = 0;
-    p->wn = n;  // the node wave's capacity (no jg_pnc_wave_* wave is open while a node wave runs)
+    p->fuse = json_fuse();
+    p->wn = n;  // the node wave's capacity (jg_pnc_wave_* calls are refused while it is open: node_open)
 }
 
 void pnc_node_scan(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t m0, uint64_t m1) {
@@ -821,6 +982,7 @@ int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
     if (n == 0) return JG_OK;
     try {
         finish_wave(p, bytes, off, rows, n, wave_scratch(p, p->wn), bad);
+        p->scan_hi = 0;  // committed: a later abort of the node wave (an OR-Set commit failing) must not undo it
         return JG_OK;
     } catch (const Error& e) {
         if (*bad == UINT64_MAX) throw;
@@ -833,9 +995,10 @@ int pnc_node_finish(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
 // applied the messages before the one that threw).
 int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad, std::string* why) {
     *bad = UINT64_MAX;
-    if (n == 0) return JG_OK;
-    const WaveScratch w = wave_scratch(p, p->wn);
     undo_applied(p, rows);  // the chunks' fused pass A applied messages past the cut too: back to the state before the wave
+    p->scan_hi = 0;
+    if (n == 0) return JG_OK;  // a cut at message 0: nothing applied (the undo used to come after this return)
+    const WaveScratch w = wave_scratch(p, p->wn);
     reset_status(p->ctx, w.status);
     p->scan_hi = 0;
     launch_scan(p, bytes, off, rows, 0, n, w);
@@ -856,6 +1019,7 @@ extern "C" {
 int jg_pnc_intern(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const jg_guid* replica, uint32_t* col_out) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_intern");
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_intern: store is NULL");
         if (n == 0) return;
         JG_REQUIRE(key_idx && replica && col_out, JG_EINVAL, "jg_pnc_intern: NULL argument");
@@ -976,6 +1140,7 @@ int jg_wave_upload(jg_wave* w, uint64_t n, const uint32_t* key_idx, const uint64
 int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_merge_wave");
         if (bad_msg) *bad_msg = UINT64_MAX;
         JG_REQUIRE(p && w, JG_EINVAL, "jg_pnc_merge_wave: NULL argument");
         JG_REQUIRE(p->ctx == w->ctx, JG_EINVAL, "jg_pnc_merge_wave: wave and store belong to different contexts");
@@ -990,6 +1155,7 @@ int jg_pnc_merge_wave(jg_pnc* p, const jg_wave* w, uint64_t* bad_msg) {
 int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_wave_begin");
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_begin: store is NULL");
         jg_ctx* ctx = p->ctx;
         jg::ensure_device(ctx);
@@ -1000,6 +1166,7 @@ int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
         const WaveScratch w = wave_scratch(p, cap_msgs);
         reset_status(ctx, w.status);
         p->scan_hi = 0;
+        p->fuse = json_fuse();
         JG_HIP(hipMemsetAsync(p->woff.p, 0, 8, ctx->stream));  // off[0] = 0
         p->wn = 0;
         p->wnb = 0;
@@ -1010,6 +1177,7 @@ int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
 int jg_pnc_wave_append(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_wave_append");
         JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_append: no open wave (jg_pnc_wave_begin)");
         if (n == 0) return;
         JG_REQUIRE(key_idx && off && bytes, JG_EINVAL, "jg_pnc_wave_append: NULL argument");
@@ -1039,6 +1207,7 @@ int jg_pnc_wave_append(jg_pnc* p, uint64_t n, const uint32_t* key_idx, const uin
 int jg_pnc_wave_commit(jg_pnc* p, uint64_t* bad_msg) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_wave_commit");
         if (bad_msg) *bad_msg = UINT64_MAX;
         JG_REQUIRE(p && p->wopen, JG_EINVAL, "jg_pnc_wave_commit: no open wave (jg_pnc_wave_begin)");
         jg::ensure_device(p->ctx);
@@ -1051,6 +1220,7 @@ int jg_pnc_wave_commit(jg_pnc* p, uint64_t* bad_msg) {
 int jg_pnc_wave_abort(jg_pnc* p) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_wave_abort");
         JG_REQUIRE(p, JG_EINVAL, "jg_pnc_wave_abort: store is NULL");
         jg::ensure_device(p->ctx);
         if (p->wopen) undo_applied(p, p->wrows.as<uint32_t>());  // the appended chunks' fused pass A

@@ -14,9 +14,9 @@
 //      form System.Text.Json writes — {"pVector":{E,...},"nVector":{E,...}}, E = "<guid D>":<int>,
 //      no whitespace — which the serial parser accepts with the same entries.
 //   4  each entry is looked up in its row's replica table, whose first G columns the lanes loaded
-//      into LDS while the payload was in flight (pass A: repeats among known replicas via an LDS
-//      column mask per vector, unknown replicas defer the message; pass B: atomicMax; pass C: the
-//      group's first lane appends new replicas in token order = Merge's order).
+//      into LDS while the payload was in flight (pass A: a repeat among known replicas, found by an LDS
+//      column mask per vector, sends the message to the serial parser; unknown replicas defer it; pass B:
+//      atomicMax; pass C: the group's first lane appends new replicas in token order = Merge's order).
 //
 // A group never spans two waves, so the phases are separated by wave-level syncs, not block
 // barriers: every wave runs its groups at its own pace.
@@ -453,8 +453,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         }
         wave_sync();
         const uint32_t f = sh.flags[grp];
-        const bool fast = live && !(f & kSlow);
-        const bool deferred_msg = fast && !(f & kDup) && (f & kMiss);
+        // a Guid repeated among the known replicas of one vector (kDup): System.Text.Json keeps its LAST value at its
+        // first place, which the serial parser visits (oracle/json.hpp) — the message goes to the slow list unapplied
+        const bool fast = live && !(f & (kSlow | kDup));
+        const bool deferred_msg = fast && (f & kMiss);
         const bool defer = g == 0 && deferred_msg;
         if (g == 0 && fast) deferred[m] = defer ? (unsigned long long)rc.row << 32 | m : kNotDeferred;
         if (defer) status[1] = 1;  // any deferral (select_deferred later overwrites it with the count)
@@ -472,10 +474,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint8_t* __restrict__ byt
         }
         if (g == 0 && fast) {
             *reinterpret_cast<uint16_t*>(emit + m * emit_stride(EB)) =
-                (f & kDup) ? kReparse
-                           : (fuse && !(f & kMiss)) ? (uint16_t)(kApplied | sh.geo[grp] >> kGeoNr)
-                                                    : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
-            if (f & kDup) atomicMin(status, (unsigned long long)m << 2 | kErrSyntax);
+                (fuse && !(f & kMiss)) ? (uint16_t)(kApplied | sh.geo[grp] >> kGeoNr)
+                                       : (uint16_t)((tk_ntok(sh.tk[grp]) - 2) | ((f & kMiss) ? kNeedsCols : 0u));
         }
     }
 }
@@ -512,6 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_emit(const uint8_t* __restrict
     const uint32_t cnt = *reinterpret_cast<const uint16_t*>(h);
     if (cnt == kReparse || (cnt & (kNeedsCols | kApplied)) || e >= cnt) return;  // kApplied: pass A applied it (fused)
     const uint32_t code = reinterpret_cast<const uint16_t*>(h)[1 + e];
+    if ((code & 0x7FFF) == kVoidCol) return;  // an earlier entry of a key the vector repeats (pass C)
     const T v = reinterpret_cast<const T*>(h + 32)[e];
     T* cell = static_cast<T*>(code >> 15 ? N : P) + (uint64_t)rows[m] * R + (code & 0x7FFF);
     // a wave repeats hot keys (C1: 100 keys, ~3000 states each): most values do not raise the cell, and
@@ -564,8 +565,8 @@ __global__ __launch_bounds__(kBlock) void k_apply_slow(const uint8_t* __restrict
 // Pass C (new replicas appended in commit order) from pass A's records: no payload is parsed again.
 // One lane per sorted deferred entry; the lane of a row's first entry walks the row's deferred messages
 // in commit order, finds or appends each entry's Guid in token order (every pVector entry before any
-// nVector entry, PNCounters.cs:133-143) against the row's columns, checks repeats within a vector, and
-// writes the columns into the record for pass B.  At a message the group parse did not prove compact
+// nVector entry, PNCounters.cs:133-143) against the row's columns, voids the earlier entries of a key its
+// vector repeats (the last value counts), and writes the columns into the record for pass B.  At a message the group parse did not prove compact
 // (record kReparse) the rest of the walk goes to k_resolve_resume (serial ResolveVis).  G == 1
 // (JANUS_JSON_GROUP=1): the serial walk throughout (k_resolve_serial).  saved[i] = ncols before the walk
 // (for roll-back).  The walk is serial per row either way; round 3 gave each row a 16-lane group whose
@@ -639,7 +640,11 @@ __global__ __launch_bounds__(kBlock) void k_resolve_rows(const unsigned long lon
                 for (uint32_t c = 0; c < kRC; ++c)
                     if (c == col) rcol[c] = x;
             }
-            if (vv ? seen[1].test_set(col) : seen[0].test_set(col)) { err = kErrSyntax; break; }  // repeated Guid in one vector
+            // a Guid repeated in one vector: System.Text.Json's Dictionary keeps its LAST value at its FIRST place
+            // (oracle/json.hpp) — the column stays where the first occurrence put it, the earlier entries are voided
+            if (vv ? seen[1].test_set(col) : seen[0].test_set(col))
+                for (uint32_t q = 0; q < e; ++q)
+                    if (codes[q] == (uint16_t)(col | vv << 15)) codes[q] = (uint16_t)(kVoidCol | vv << 15);
             codes[e] = (uint16_t)(col | vv << 15);
         }
         *reinterpret_cast<uint16_t*>(h) = (uint16_t)cnt;  // resolved: pass B applies the record
@@ -677,7 +682,10 @@ __global__ __launch_bounds__(kBlock) void k_resolve_resume(const uint8_t* __rest
                 const uint32_t cnt = h[0] & ~kNeedsCols;
                 for (uint32_t e = 0; e < cnt; ++e) {
                     const uint32_t col = find_col(gcols, t.ncols[row], eguid[m * kEmitMax + e], UINT32_MAX);
-                    h[1 + e] = (uint16_t)((col & 0x7FFF) | (h[1 + e] & 0x8000));
+                    const uint16_t code = (uint16_t)((col & 0x7FFF) | (h[1 + e] & 0x8000));
+                    for (uint32_t q = 0; q < e; ++q)  // a repeated key: its last value only (as k_resolve_rows)
+                        if (h[1 + q] == code) h[1 + q] = (uint16_t)(kVoidCol | (code & 0x8000));
+                    h[1 + e] = code;
                 }
                 h[0] = (uint16_t)cnt;
             }

@@ -283,6 +283,7 @@ struct jg_tracker {
     jg::DevBuf spare_tab, spare_claim;  // the other pair of a rebuild (tables are rebuilt into it, then swapped)
     uint64_t cap = 0;
     uint64_t used = 0;  // live + tombstones, an upper bound (TryAdd of a present identity counted too)
+    int waves = 0;      // node waves using the tracker (a streamed one spans unlocked calls): destroy is refused
 
     ~jg_tracker() {
         for (Pin& b : pin) {
@@ -375,6 +376,7 @@ struct jg_tracker {
 // uploads and parses of the parts before.  Messages are numbered in hand-over order (= commit order).
 struct WaveRun {
     bool active = false, block_mode = false, filter = false, trace = false, do_pnc = false, do_orset = false;
+    bool held = false;  // wave_end is running: the stores are still held (hold) though no more parts are taken
     jg_tracker* tr = nullptr;
     uint64_t n = 0, total_bytes = 0;  // the wave's messages and payload bytes (stream: upper bounds from begin)
     uint64_t seen = 0;                // messages handed over (commit index of the next)
@@ -546,9 +548,19 @@ void wave_prologue(jg_node* nd, jg_tracker* tr, double* tp) {
     nd->dmap.clear();
 }
 
+// A wave holds its node's stores (and tracker) from wave_begin to the end of wave_end / wave_abort: the calls that
+// would write them or reuse the scratch the wave keeps are refused meanwhile (jg::require_writable).
+void hold(jg_node* nd, jg_tracker* tr, bool on) {
+    if (nd->pnc) nd->pnc->node_open = on;
+    if (nd->orset) nd->orset->node_open = on;
+    if (tr) tr->waves += on ? 1 : -1;
+}
+
 // Setup: the prologue, buffers for `n` messages / `total_bytes` payload bytes and up to `max_chunks` chunks, both
 // parsers opened.
 void wave_begin(jg_node* nd, WaveRun& r, jg_tracker* tr, uint64_t n, uint64_t total_bytes, uint64_t max_chunks, bool block_mode, bool filter) {
+    jg::require_writable(nd->pnc, "jg_apply");  // another node's streamed wave holds a shared store
+    jg::require_writable(nd->orset, "jg_apply");
     r = WaveRun{};
     r.t_begin = now_s();
     r.tr = tr;
@@ -616,6 +628,7 @@ void wave_begin(jg_node* nd, WaveRun& r, jg_tracker* tr, uint64_t n, uint64_t to
     r.t_loop = now_s();
     nd->stats.setup_s = r.t_loop - r.t_begin;
     r.active = true;
+    hold(nd, tr, true);
 }
 
 // A wave rejected mid-loop (offsets checked chunk by chunk) or a device error: what pass A applied is undone, and the chunks
@@ -636,7 +649,8 @@ void wave_abort(jg_node* nd, WaveRun& r, uint64_t claimed) {
     if (r.do_orset) jg::orset_node_abort(nd->orset);
     for (hipEvent_t& e : r.up_ev)
         if (e) (void)hipEventDestroy(e), e = nullptr;
-    r.active = false;
+    if (r.active || r.held) hold(nd, r.tr, false);
+    r.active = r.held = false;
 }
 
 // Messages [c0, c1) of part `w` (commit indices gbase + i): gathered into page-locked staging (or uploaded in place
@@ -789,6 +803,14 @@ void wave_end(jg_node* nd, WaveRun& r, uint64_t* completed, uint64_t* n_complete
     const double t_dev = now_s();
     nd->stats.loop_s = t_dev - r.t_loop;
     r.active = false;
+    r.held = true;
+    struct Release {  // every way out of wave_end lets the stores go (wave_abort on the failure paths does too)
+        jg_node* nd;
+        WaveRun& r;
+        ~Release() {
+            if (r.held) hold(nd, r.tr, false), r.held = false;
+        }
+    } release_{nd, r};
 
     // the cut: the first state the reference's loop would throw at
     JG_HIP(hipEventRecord(nd->event(2 * n_ev), ctx->stream));  // the final phase's kernels start after the chunks'
@@ -1005,6 +1027,7 @@ int jg_node_destroy(jg_node* nd) {
         if (!nd) return;
         auto lk_ = jg::lock(nd->ctx);
         jg::ensure_device(nd->ctx);
+        if (nd->run.active) wave_abort(nd, nd->run, nd->run.m0);  // an open streamed wave: undone, its stores let go
         JG_HIP(hipStreamSynchronize(nd->ctx->stream));
         JG_HIP(hipStreamSynchronize(nd->ctx->copy));
         delete nd;
@@ -1101,6 +1124,7 @@ int jg_tracker_destroy(jg_tracker* t) {
     return jg::guard([&] {
         if (!t) return;
         auto lk_ = jg::lock(t->ctx);
+        JG_REQUIRE(t->waves == 0, JG_EINVAL, "jg_tracker_destroy: a node wave (jg_apply_stream_begin .. _end) is using the tracker");
         jg::ensure_device(t->ctx);
         JG_HIP(hipStreamSynchronize(t->ctx->stream));
         delete t;

@@ -1018,6 +1018,7 @@ int jg_orset_create(jg_ctx* ctx, uint64_t cap_add, uint64_t cap_rem, jg_orset** 
 int jg_orset_destroy(jg_orset* s) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_destroy");
         if (!s) return;
         jg::ensure_device(s->ctx);
         JG_HIP(hipStreamSynchronize(s->ctx->stream));
@@ -1028,6 +1029,7 @@ int jg_orset_destroy(jg_orset* s) {
 int jg_orset_load(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_load");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_load: store is NULL");
         JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_load: NULL records");
         jg::ensure_device(s->ctx);
@@ -1067,6 +1069,7 @@ int jg_orset_read(jg_orset* s, jg_tagrec* add, uint64_t cap_add, jg_tagrec* rem,
 int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_tagrec* rem, uint64_t n_rem) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_merge");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_merge: store is NULL");
         JG_REQUIRE((add || n_add == 0) && (rem || n_rem == 0), JG_EINVAL, "jg_orset_merge: NULL records");
         jg_ctx* ctx = s->ctx;
@@ -1082,6 +1085,7 @@ int jg_orset_merge(jg_orset* s, const jg_tagrec* add, uint64_t n_add, const jg_t
 int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
     return jg::guard([&] {
         auto lk_ = jg::lock(dst);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(dst, "jg_orset_merge_store");
         JG_REQUIRE(dst && src && dst != src, JG_EINVAL, "jg_orset_merge_store: bad stores");
         JG_REQUIRE(dst->ctx == src->ctx, JG_EINVAL, "jg_orset_merge_store: stores belong to different contexts");
         jg::ensure_device(dst->ctx);
@@ -1093,6 +1097,7 @@ int jg_orset_merge_store(jg_orset* dst, const jg_orset* src, int async) {
 int jg_orset_union(const jg_orset* a, const jg_orset* b, jg_orset* out, int async) {
     return jg::guard([&] {
         auto lk_ = jg::lock(a);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(out, "jg_orset_union");
         JG_REQUIRE(a && b && out, JG_EINVAL, "jg_orset_union: NULL store");
         JG_REQUIRE(out != a && out != b, JG_EINVAL, "jg_orset_union: out may not alias an input");
         JG_REQUIRE(a->ctx == b->ctx && a->ctx == out->ctx, JG_EINVAL, "jg_orset_union: stores belong to different contexts");
@@ -1112,6 +1117,7 @@ int jg_orset_apply_ops(jg_orset* s, uint64_t n_ops, const uint32_t* set, const u
                        const uint64_t* tag_hi, uint8_t* result) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_apply_ops");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_apply_ops: store is NULL");
         if (n_ops == 0) return;
         JG_REQUIRE(set && elem && op && tag_lo && tag_hi && result, JG_EINVAL, "jg_orset_apply_ops: NULL argument");
@@ -1128,6 +1134,7 @@ int jg_orset_apply_ops_ords(jg_orset* s, uint64_t n_ops, const uint32_t* set, co
                             const uint64_t* tag_hi, uint8_t* result, uint64_t* add_lim, uint64_t* rem_lim) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);
+        jg::require_writable(s, "jg_orset_apply_ops_ords");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_apply_ops_ords: store is NULL");
         if (n_ops == 0) return;
         JG_REQUIRE(set && elem && op && tag_lo && tag_hi && result && add_lim && rem_lim, JG_EINVAL, "jg_orset_apply_ops_ords: NULL argument");

@@ -166,31 +166,41 @@ __global__ __launch_bounds__(kBlock) void k_cb_scatter(uint64_t ns, uint64_t nre
 
 // The same scatter from the places the tables' claimants took (k_ow_strings / k_ow_rins, `Claims`): a commit
 // of the whole wave whose claims all counted reads one 8-byte place per listed item instead of k_cb_count's
-// pass over the slots.  Grid-stride over the packed lists (offs: both tables' sub-list offsets, on the device):
-// the check queues it before its read, so it leaves without writing when a claim went uncounted or a table
-// overflowed (places then may be stale or past the bucket arrays) — such a wave never commits from the claims.
+// pass over the slots.  Grid-stride over the packed lists (offs: both tables' sub-list offsets, on the device).
+// The check queues it before its one read (spec_commit_prep), so it runs before anyone knows whether the wave's
+// claims all counted: it leaves without writing when a claim went uncounted or a table overflowed (places may then
+// be stale, or name sets past the count arrays) — such a wave never commits from the claims.
+//
+// Round 5's fault (gpurun_out/r05/cb10): the first version of this speculative launch stored through
+// bucket arrays carved from a block the commit had sized for the previous wave's items (or not yet allocated), so
+// its stores ran past the block.  The block is now sized by tables_begin for the tables' capacities and the check
+// refuses to queue the launch otherwise.  Past the guard, a listed slot outside its table, a place naming a set past
+// the count arrays, or a bucket position past the arrays can only mean the tables are inconsistent: such an item is
+// not written, and `bad` (zeroed by k_list_offs, read with the check's words) fails the wave's check with JG_EHIP —
+// before anything of it commits — instead of committing a bucket with a stale slot.
 __global__ __launch_bounds__(kBlock) void k_cb_scatter_claimed(const unsigned long long* __restrict__ offs, const StrTab T, const RecTab R,
-                                                               Claims C, Buckets B, const unsigned long long* __restrict__ overflow) {
+                                                               Claims C, Buckets B, const unsigned long long* __restrict__ overflow,
+                                                               unsigned long long* __restrict__ bad) {
     if (*overflow != 0 || *C.uncounted != 0) return;
     const uint64_t ns = offs[kLists], nrec = offs[2 * kLists + 1];
-    // (bounds: the lists' and bucket arrays' capacities — a speculative launch never writes outside them)
-    const uint64_t cap_s = kLists * T.sub_cap, cap_r = kLists * R.sub_cap;
+    const uint64_t cap_s = kLists * T.sub_cap, cap_r = kLists * R.sub_cap;  // the bucket arrays' capacities
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < ns + nrec; i += (uint64_t)gridDim.x * kBlock) {
         if (i < ns) {
             const uint32_t sid = T.list[i];
-            if (sid > T.mask) continue;
+            if (sid > T.mask) { atomicOr(bad, 1ull); continue; }
             const uint2 pl = C.splace[sid];
-            if (pl.x == kDead || pl.y >= C.cap) continue;
-            const uint64_t at = (uint64_t)B.scnt[pl.y] + pl.x;
-            if (at < cap_s) B.sitem[at] = sid;
+            if (pl.x == kDead) continue;  // a name the element table already holds: no new id, no bucket place
+            const uint64_t at = pl.y < C.cap ? (uint64_t)B.scnt[pl.y] + pl.x : ~0ull;
+            if (at >= cap_s) { atomicOr(bad, 2ull); continue; }
+            B.sitem[at] = sid;
         } else {
             const uint32_t slot = R.list[i - ns];
-            if (slot > R.mask) continue;
+            if (slot > R.mask) { atomicOr(bad, 4ull); continue; }
             const uint2 pl = C.rplace[slot];
             const uint32_t sd = pl.y >> 31, set = pl.y & 0x7FFFFFFFu;
-            if (set >= C.cap) continue;
-            const uint64_t at = (uint64_t)B.rcnt[sd][set] + pl.x;
-            if (at < cap_r) B.ritem[sd][at] = slot;
+            const uint64_t at = set < C.cap ? (uint64_t)B.rcnt[sd][set] + pl.x : ~0ull;
+            if (at >= cap_r) { atomicOr(bad, 8ull); continue; }
+            B.ritem[sd][at] = slot;
         }
     }
 }

@@ -19,8 +19,9 @@
 //      entry (name hash, offset, length, side, position) or tag (reference, value) where the serial parse
 //      would: the same slots of the same sparse regions, in the same order.
 //
-// Anything the chain does not prove (whitespace, members out of order, escapes, non-ASCII names, an empty
-// tag set, more than kOgBytes or kOgTok, or a malformed payload) marks the message slow; k_ow_parse then
+// Anything the chain does not prove (whitespace, members out of order or repeated, an unknown member, escapes,
+// non-ASCII names, an empty tag set, an element named twice in one map, more than kOgBytes or kOgTok, or a
+// malformed payload) marks the message slow; k_ow_parse then
 // parses it serially (its flag array), so the fast path accepts a subset of what the serial parser accepts,
 // with identical outputs, and never reports an error itself.  Writes are bounded by the message's own
 // sparse regions, so a message that turns out slow overwrites nothing of another's.
@@ -36,6 +37,7 @@ constexpr int kOgWaves = kBlock / 64;          // messages per workgroup
 struct OgShared {
     uint4 buf[kOgWaves][kOgWin + 1];           // +1 window: realigned reads near the end stay inside
     uint16_t q[kOgWaves][2 * kOgTok];          // quote positions (message-relative)
+    unsigned long long nh[kOgWaves][kOgTok];   // element names: 64-bit FNV-1a with the map's side in bit 0
 };
 
 // glue codes: the bytes packed little-endian (no pattern holds a zero byte, so the length is implicit)
@@ -220,6 +222,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
                     S.meta[es + q] = n | sec << 31;
                     S.pos[es + q] = (uint32_t)s;
                     S.set[es + q] = set;
+                    sh.nh[wv][q] = (h & ~1ull) | sec;  // q < ntok <= kOgTok
                 }
             } else if (nbrk) {  // "nullRemoveGuid"
                 ok = nsub == 1 && og_name_is(c, s + 1, n, "nullRemoveGuid", 14) && (ga == kGlArr || (last && ga == kGlEndEmpty));
@@ -245,6 +248,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         c_ent += (uint32_t)__popcll(bname);
         c_add += (uint32_t)__popcll(badd);
         c_tag += (uint32_t)__popcll(bval);
+    }
+    // an element named twice in one map: System.Text.Json keeps its LAST tag set at its FIRST place (oracle/json.hpp),
+    // which the serial parse reproduces, so the message leaves the fast path here (names compared by their 64-bit
+    // hashes in LDS; two different names sharing one only cost the slow path)
+    if (__ballot(bad) == 0 && c_ent > 1) {  // wave-uniform
+        jgw::wave_sync();
+        bool dup = false;
+        for (uint32_t q = lane; q < c_ent; q += 64) {
+            const unsigned long long x = sh.nh[wv][q];
+            for (uint32_t p = 0; p < q; ++p) dup |= sh.nh[wv][p] == x;
+        }
+        bad |= dup;
     }
     const bool fast = __ballot(bad) == 0;
     if (lane == 0) {

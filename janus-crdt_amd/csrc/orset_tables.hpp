@@ -12,8 +12,9 @@
 //   k_ow_strings   one wave per message, one lane per entry: the (set, string) goes into an open-addressing
 //                  table (exact byte compare on a hash match; slot = the string's id for this wave), the
 //                  slot keeps the smallest canonical entry index (atomicMin; entry slots are ordered like
-//                  commit order), and a string named twice in one map of one message is Decode's
-//                  duplicate-key error at the second name (the messages' entries compared in LDS).
+//                  commit order).  Both parsers hand over each (map, element) of a message once — System.Text.Json
+//                  keeps a repeated key's last value at its first place, which the serial parse reproduces and the
+//                  group parse leaves to it (round 6; the tables used to reject the repeat in LDS).
 //   k_ow_rkeys     each tag reference's record identity without its tag: (string slot, side), or
 //                  (set, side) for a null tag set.
 //   k_ow_rins      each tag reference into the record table (exact compare of identity + tag), the slot
@@ -22,8 +23,7 @@
 //
 // The commit then resolves only the distinct strings against the element table and sorts only the
 // distinct records.  A table that runs out of probes (more distinct strings / records than it was sized
-// for, or tests narrowing the hashes) or a message with more than kDupScan entries raises the overflow
-// word, and the wave falls back to the sort-based check and commit (k_ow_compact ... k_ow_dedup), which
+// for, or tests narrowing the hashes) raises the overflow word, and the wave falls back to the sort-based check and commit (k_ow_compact ... k_ow_dedup), which
 // reads the same sparse regions.  Messages past the commit limit are in the tables too; the commit keeps
 // the strings and records whose first occurrence lies before the limit (entry / tag slots are ordered
 // like messages).
@@ -32,7 +32,6 @@
 constexpr uint32_t kNoSid = 0xFFFFFFFFu;
 constexpr uint32_t kUnresolved = 0xFFFFFFFEu;  // sid_id of a string not looked up at claim time (ids stay below it)
 constexpr uint32_t kProbeCap = 256;  // probes before a table insert gives up (the wave falls back)
-constexpr uint32_t kDupScan = 512;   // entries per message the in-wave duplicate check holds in LDS
 constexpr int kTabWaves = kBlock / 64;
 
 // The slots a table's inserts claimed, appended as they are claimed, so the commit walks these instead of the
@@ -128,7 +127,8 @@ __global__ void k_list_pack(const uint32_t* __restrict__ list, uint64_t sub_cap,
 // Both tables' sub-list offsets from their counters on the device (each count clamped to its sub-list: an
 // overflowed table's counts run past it, and that wave never commits from the tables).
 __global__ void k_list_offs(const unsigned long long* __restrict__ ns, uint64_t s_cap, const unsigned long long* __restrict__ nr, uint64_t r_cap,
-                            unsigned long long* __restrict__ offs) {
+                            unsigned long long* __restrict__ offs, unsigned long long* __restrict__ scatter_bad) {
+    if (threadIdx.x == 2) *scatter_bad = 0;  // k_cb_scatter_claimed's bound flag, queued after this launch
     if (threadIdx.x >= 2) return;
     const unsigned long long* n = threadIdx.x ? nr : ns;
     const uint64_t cap = threadIdx.x ? r_cap : s_cap;
@@ -265,7 +265,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
                                                        const uint32_t* __restrict__ na, uint64_t m0, uint64_t m1, StrTab T,
                                                        unsigned long long* __restrict__ err, unsigned long long* __restrict__ overflow,
                                                        Names N, uint32_t set_lim, uint32_t* __restrict__ sid_id, Claims C) {
-    __shared__ uint32_t sh[kTabWaves][kDupScan];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t es_chunk = (off[m0] + kEntryDiv - 1) / kEntryDiv;  // entry slots from here on: this launch's
     const uint64_t m = m0 + (uint64_t)blockIdx.x * kTabWaves + wv;
@@ -333,7 +332,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
             if (first_seen > c) atomicMin(&T.slot[sid].first, c);  // a stale `first` is only larger: the filter holds
         }
         S.sid[slot] = sid;
-        if (q < kDupScan) sh[wv][q] = sid == kNoSid ? kNoSid : (sid | (meta & 0x80000000u));  // sid | side (sids < 2^31)
         }
         list_append(fresh, sid, T.list, T.n, T.sub_cap, overflow, m + q0 / 64);
         // the claim counted (one message per wave: every lane's set is `set`)
@@ -356,22 +354,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) voi
         }
         if (fresh && !is_new) C.splace[sid] = make_uint2(kDead, set);
     }
-    if (cnt > kDupScan) over = true;  // the duplicate check below would miss pairs: the sort path decides
-    if (__ballot(over) != 0) {
-        if (lane == 0) *overflow = 1;
-        return;
-    }
-    jgw::wave_sync();
-    // Decode's duplicate key: a (string, side) an earlier entry of this message already named (error at the
-    // later name; the message's error is the smallest position, k_ow_first_bad)
-    for (uint32_t q = lane; q < cnt; q += 64) {
-        const uint32_t x = sh[wv][q];
-        for (uint32_t p = 0; p < q; ++p)
-            if (sh[wv][p] == x) {
-                atomicMin(err + m, (unsigned long long)S.pos[es + q] << 2 | kKindInval);
-                break;
-            }
-    }
+    if (__ballot(over) != 0 && lane == 0) *overflow = 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_ow_rkeys(Sparse S, const uint64_t* __restrict__ off, const uint32_t* __restrict__ mset,

@@ -48,6 +48,9 @@ namespace {
 
 using jgw::Cursor;
 using jgw::hexv;
+using jgw::GuidSink;
+using jgw::read_string;
+using jgw::put_utf8;
 
 constexpr int kBlock = 256;
 constexpr unsigned long long kNone = ~0ull;
@@ -92,34 +95,6 @@ struct PropSink {  // which of the four ORSetMsg members (after unescaping, as S
     }
 };
 
-struct GuidSink {  // Guid.Parse of the "D" form (what Guid's JSON converter accepts), C# byte order
-    uint32_t k = 0, va = 0, vb = 0, vc = 0;
-    unsigned long long hi = 0;
-    bool bad = false;
-    __device__ void esc() {}
-    __device__ void put(int b) {
-        if (k == 8 || k == 13 || k == 18 || k == 23) {
-            bad |= b != '-';
-        } else if (k < 36) {
-            const int h = hexv(b);
-            bad |= h < 0;
-            const uint32_t x = (uint32_t)h & 15;
-            if (k < 8) va = va << 4 | x;
-            else if (k < 13) vb = vb << 4 | x;
-            else if (k < 18) vc = vc << 4 | x;
-            else {
-                const uint32_t j = k < 23 ? k - 19 : k - 20;  // hex digit among the last 16
-                hi |= (unsigned long long)x << (8 * (j >> 1) + ((j & 1) ? 0 : 4));
-            }
-        } else {
-            bad = true;
-        }
-        ++k;
-    }
-    __device__ bool ok() const { return !bad && k == 36; }
-    __device__ Tag16 tag() const { return Tag16{(unsigned long long)va | (unsigned long long)vb << 32 | (unsigned long long)vc << 48, hi}; }
-};
-
 struct NameSink {  // FNV-1a of the unescaped bytes and the first 8 of them; with w set, the bytes after the
                    // first escape are written back at the string's start (unescaping never lengthens a string)
     unsigned long long h = kFnvBasis, pf = 0;
@@ -134,80 +109,6 @@ struct NameSink {  // FNV-1a of the unescaped bytes and the first 8 of them; wit
         ++len;
     }
 };
-
-__device__ __forceinline__ bool hex4(Cursor& c, uint32_t& u) {
-    u = 0;
-    for (int k = 0; k < 4; ++k) {
-        const int h = hexv(c.get());
-        if (h < 0) return false;
-        u = u << 4 | (uint32_t)h;
-    }
-    return true;
-}
-
-template <class S> __device__ __forceinline__ void put_utf8(S& s, uint32_t u) {
-    if (u < 0x80) { s.put((int)u); return; }
-    if (u < 0x800) { s.put((int)(0xC0 | u >> 6)); s.put((int)(0x80 | (u & 0x3F))); return; }
-    if (u < 0x10000) { s.put((int)(0xE0 | u >> 12)); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F))); return; }
-    s.put((int)(0xF0 | u >> 18)); s.put((int)(0x80 | (u >> 12 & 0x3F))); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F)));
-}
-
-// The rest of a JSON string after its opening quote: escapes decoded (surrogate pairs joined), raw
-// UTF-8 validated, control characters rejected — host/wire.cpp Scan::str.
-template <class S> __device__ __forceinline__ bool read_string(Cursor& c, S& s) {
-    for (;;) {
-        const int ch = c.get();
-        if (ch < 0) return false;
-        if (ch == '"') return true;
-        if (ch < 0x20) return false;
-        if (ch == '\\') {
-            s.esc();
-            const int e = c.get();
-            int out;
-            switch (e) {
-                case '"': out = '"'; break;
-                case '\\': out = '\\'; break;
-                case '/': out = '/'; break;
-                case 'b': out = 8; break;
-                case 'f': out = 12; break;
-                case 'n': out = 10; break;
-                case 'r': out = 13; break;
-                case 't': out = 9; break;
-                case 'u': {
-                    uint32_t u;
-                    if (!hex4(c, u) || (u >= 0xDC00 && u <= 0xDFFF)) return false;
-                    if (u >= 0xD800 && u <= 0xDBFF) {
-                        if (c.get() != '\\' || c.get() != 'u') return false;
-                        uint32_t lo;
-                        if (!hex4(c, lo) || lo < 0xDC00 || lo > 0xDFFF) return false;
-                        u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
-                    }
-                    put_utf8(s, u);
-                    continue;
-                }
-                default: return false;
-            }
-            s.put(out);
-            continue;
-        }
-        if (ch < 0x80) { s.put(ch); continue; }
-        int extra;
-        uint32_t cp;
-        if (ch >= 0xC2 && ch <= 0xDF) { extra = 1; cp = ch & 0x1F; }
-        else if (ch >= 0xE0 && ch <= 0xEF) { extra = 2; cp = ch & 0x0F; }
-        else if (ch >= 0xF0 && ch <= 0xF4) { extra = 3; cp = ch & 0x07; }
-        else return false;
-        s.put(ch);
-        for (int k = 0; k < extra; ++k) {
-            const int cc = c.get();
-            if (cc < 0 || (cc & 0xC0) != 0x80) return false;
-            cp = cp << 6 | (uint32_t)(cc & 0x3F);
-            s.put(cc);
-        }
-        if (extra == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) return false;
-        if (extra == 3 && (cp < 0x10000 || cp > 0x10FFFF)) return false;
-    }
-}
 
 // The common case of a tag string, decoded without the byte loop: [p, p + 37) holds exactly the
 // 36-character "D" form with hex digits and the closing quote.  Eleven independent dword loads cover it
@@ -272,7 +173,7 @@ template <class V> __device__ __forceinline__ bool read_tags(Cursor& c, V& v, in
         }
         GuidSink gs;
         if (!read_string(c, gs) || !gs.ok()) return false;
-        v.tag(side, is_null, gs.tag());
+        v.tag(side, is_null, Tag16{gs.lo(), gs.hi});
         ++nt;
         c.ws();
         const int ch = c.get();
@@ -281,55 +182,68 @@ template <class V> __device__ __forceinline__ bool read_tags(Cursor& c, V& v, in
     }
 }
 
-// One ORSetMsg<string>: {"addSet":{"e":[guid,...],...},"removeSet":{...},"nullAddGuid":[...],
-// "nullRemoveGuid":[...]}, members in any order, each exactly once, none null (Merge would throw).
-// W: unescape element strings in place (pass 2).
-template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c, uint8_t* wbase, V& v) {
+// ---- the decode contract (oracle/json.hpp, System.Text.Json 6.0's defaults) ---------------------------------------
+// Members in any order; a name that is not a member is skipped (jgw::skip_value); a member given twice takes its
+// last occurrence; an element named twice in one map keeps its first place and takes its last tag set (Dictionary's
+// indexer); a `null` last occurrence of a member or an element is rejected (Merge would throw).
+
+// Per member over the whole message: occurrences, the last one `null`, and (maps) whether its last occurrence may
+// name an element twice (a 128-bit filter of the names' hashes: no shared bit, no repeat, no scans).
+struct MemInfo {
+    uint32_t occ = 0;
+    bool null_last = false, maybe_dup = false;
+};
+
+struct NoTags {  // read_tags' visitor for a validation pass
+    __device__ __forceinline__ void tag(int, bool, const Tag16&) {}
+};
+
+// The whole payload checked, every occurrence of every member (skipped ones included): true iff System.Text.Json
+// decodes it and no member ends `null`.  Writes nothing.
+__device__ bool validate_orset(Cursor& c, MemInfo (&mi)[4]) {
     if (!c.expect('{')) return false;
-    int seen = 0;
     c.ws();
-    if (c.peek() == '}') {
-        ++c.p;
-    } else {
-        for (;;) {
-            if (!c.expect('"')) return false;
-            PropSink ps;
-            if (!read_string(c, ps)) return false;
-            const int which = ps.which();
-            if (which < 0 || (seen >> which & 1)) return false;
-            seen |= 1 << which;
-            if (!c.expect(':')) return false;
+    if (c.peek() == '}') return false;  // {}: every member missing
+    NoTags nv;
+    for (;;) {
+        if (!c.expect('"')) return false;
+        PropSink ps;
+        if (!read_string(c, ps) || !c.expect(':')) return false;
+        const int which = ps.which();
+        if (which < 0) {
+            if (!jgw::skip_value(c, 1)) return false;
+        } else {
+            MemInfo& v = mi[which];
+            ++v.occ;
+            v.maybe_dup = false;
             c.ws();
-            if (which >= 2) {
-                if (c.peek() != '[') return false;  // `null` included
-                ++c.p;
-                uint32_t nt;
-                if (!read_tags(c, v, which - 2, true, nt)) return false;
+            v.null_last = c.peek() == 'n';
+            uint32_t nt;
+            if (v.null_last) {
+                if (!jgw::take_literal(c, "null")) return false;
+            } else if (which >= 2) {
+                if (!c.expect('[') || !read_tags(c, nv, 0, true, nt)) return false;
             } else {
-                if (c.peek() != '{') return false;
-                ++c.p;
-                v.map(which);
+                if (!c.expect('{')) return false;
+                unsigned long long f0 = 0, f1 = 0;
                 c.ws();
                 if (c.peek() == '}') {
                     ++c.p;
                 } else {
                     for (;;) {
-                        c.ws();
-                        const uint64_t npos = c.p;
-                        if (c.peek() != '"') return false;
-                        ++c.p;
-                        const uint64_t noff = c.p;
                         NameSink ns;
-                        if (W) ns.w = wbase + noff;
-                        if (!read_string(c, ns)) return false;
-                        if (!c.expect(':')) return false;
+                        if (!c.expect('"') || !read_string(c, ns) || !c.expect(':')) return false;
                         c.ws();
-                        if (c.peek() != '[') return false;  // a null tag set, or not an array
-                        ++c.p;
-                        v.entry(which, npos, noff, ns.len, ns.h, ns.pf);
-                        uint32_t nt;
-                        if (!read_tags(c, v, which, false, nt)) return false;
-                        v.entry_end(which, c.p, nt);
+                        if (c.peek() == 'n') {  // a null tag set: valid JSON, judged by the visiting pass if it is the last
+                            if (!jgw::take_literal(c, "null")) return false;
+                        } else if (!c.expect('[') || !read_tags(c, nv, 0, false, nt)) {
+                            return false;
+                        }
+                        const uint32_t h = (uint32_t)(ns.h * 0x9E3779B97F4A7C15ull >> 57);  // 7 bits
+                        const unsigned long long b = 1ull << (h & 63);
+                        v.maybe_dup |= (h & 64) ? (f1 & b) != 0 : (f0 & b) != 0;
+                        if (h & 64) f1 |= b;
+                        else f0 |= b;
                         c.ws();
                         const int ch = c.get();
                         if (ch == '}') break;
@@ -337,14 +251,120 @@ template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c
                     }
                 }
             }
-            c.ws();
-            const int ch = c.get();
-            if (ch == '}') break;
-            if (ch != ',') return false;
         }
+        c.ws();
+        const int ch = c.get();
+        if (ch == '}') break;
+        if (ch != ',') return false;
     }
     c.ws();
-    return seen == 15 && c.p == c.end;
+    if (c.p != c.end) return false;
+    for (int k = 0; k < 4; ++k)
+        if (!mi[k].occ || mi[k].null_last) return false;
+    return true;
+}
+
+// A name's unescaped bytes compared with `want` (len bytes) as they are decoded.
+struct CmpSink {
+    const uint8_t* want;
+    uint32_t len, k = 0;
+    bool eq = true;
+    __device__ void esc() {}
+    __device__ void put(int b) {
+        eq &= k < len && want[k] == (uint8_t)b;
+        ++k;
+    }
+    __device__ bool same() const { return eq && k == len; }
+};
+
+// One ORSetMsg<string> as System.Text.Json decodes it: the last occurrence of each member visited (v.map / v.entry /
+// v.tag / v.entry_end), an element named twice in one map visited once, at its first place, with the tags of its
+// last occurrence — so entry and tag slots come in ORSet.Merge's walk order.  The payload is validated whole first;
+// the visiting pass can still fail on an element whose last tag set is `null`.  W: unescape element strings in
+// place (pass 2).
+template <bool W, class V> __device__ __forceinline__ bool parse_orset(Cursor& c, uint8_t* wbase, V& v) {
+    MemInfo mi[4];
+    {
+        Cursor t = c;
+        if (!validate_orset(t, mi)) {
+            c = t;
+            return false;
+        }
+    }
+    uint32_t occ[4] = {0, 0, 0, 0};
+    (void)c.expect('{');
+    for (;;) {
+        (void)c.expect('"');
+        PropSink ps;
+        (void)read_string(c, ps);
+        (void)c.expect(':');
+        const int which = ps.which();
+        if (which < 0 || ++occ[which] < mi[which].occ) {
+            (void)jgw::skip_value(c, 1);  // validated: a skipped member, or an occurrence a later one replaces
+        } else if (which >= 2) {
+            uint32_t nt;
+            (void)c.expect('[');
+            (void)read_tags(c, v, which - 2, true, nt);
+        } else {
+            (void)c.expect('{');
+            v.map(which);
+            c.ws();
+            if (c.peek() == '}') {
+                ++c.p;
+            } else {
+                const bool dups = mi[which].maybe_dup;
+                const uint32_t e0 = v.entries();  // this map's first entry (a repeat looks among e0 ..)
+                for (;;) {
+                    c.ws();
+                    const uint64_t npos = c.p;
+                    ++c.p;  // the opening quote
+                    const uint64_t noff = c.p;
+                    NameSink ns;
+                    if (W) ns.w = wbase + noff;
+                    (void)read_string(c, ns);
+                    (void)c.expect(':');
+                    Cursor val = c;  // the tag set this entry takes (the element's last occurrence's)
+                    bool first = true;
+                    if (dups) {
+                        first = !v.named_before(e0, ns, c.base, noff);
+                        if (first) {
+                            Cursor t = c;
+                            (void)jgw::skip_value(t, 2);
+                            for (;;) {
+                                t.ws();
+                                if (t.get() != ',') break;
+                                CmpSink cs{c.base + noff, ns.len};
+                                (void)t.expect('"');
+                                (void)read_string(t, cs);
+                                (void)t.expect(':');
+                                if (cs.same()) val = t;
+                                (void)jgw::skip_value(t, 2);
+                            }
+                        }
+                    }
+                    if (first) {
+                        val.ws();
+                        if (val.peek() != '[') {  // the element's last tag set is null: UnionWith(null) throws
+                            c = val;
+                            return false;
+                        }
+                        ++val.p;
+                        v.entry(which, npos, noff, ns.len, ns.h, ns.pf);
+                        uint32_t nt;
+                        (void)read_tags(val, v, which, false, nt);
+                        v.entry_end(which, val.p, nt);
+                    }
+                    (void)jgw::skip_value(c, 2);  // this occurrence's value
+                    c.ws();
+                    if (c.get() == '}') break;
+                }
+            }
+        }
+        c.ws();
+        if (c.get() == '}') break;
+    }
+    c.ws();
+    return true;
 }
 
 // Pass 1 writes each message's entries and tags into SPARSE regions addressed by its byte offset, so
@@ -398,6 +418,20 @@ struct ParseVis {
     }
     __device__ __forceinline__ void entry_end(int side, uint64_t pos, uint32_t ntags) {
         if (ntags == 0 && estate == kNone) estate = (unsigned long long)(pos - base) << 2 | kKindState;  // add or tombstone
+    }
+    __device__ __forceinline__ uint32_t entries() const { return n_add + n_rem; }
+    // an entry of this map (entries e0 ..) already names the string ns decoded at payload offset noff (both unescaped
+    // in place: parse_orset<true>)
+    __device__ bool named_before(uint32_t e0, const NameSink& ns, const uint8_t* base, uint64_t noff) const {
+        const unsigned long long key = name_key(set, ns.h, salt) & kmask;
+        for (uint32_t q = e0; q < n_add + n_rem; ++q) {
+            const uint64_t e = es + q;
+            if (S.key[e] != key || (S.meta[e] & 0x7FFFFFFFu) != ns.len || S.pfx[e] != ns.pf) continue;
+            bool same = true;
+            for (uint32_t i = 8; i < ns.len && same; ++i) same = base[S.noff[e] + i] == base[noff + i];
+            if (same) return true;
+        }
+        return false;
     }
 };
 
@@ -1210,7 +1244,7 @@ struct jg_orset_wire {
     // the check queued the commit's first steps ahead of its one read (lists packed, the claims' counts scanned:
     // spec_h = k_cb_scan's eight status words), for a commit of the whole wave from the tables
     bool spec = false;
-    unsigned long long spec_h[8] = {};
+    unsigned long long spec_h[9] = {};  // [8]: k_cb_scatter_claimed's bound flag (orset_commit.hpp)
     jg::DevBuf specst;
     uint64_t waves_bucketed = 0;             // table commits that took the bucket path (tests read them)
     uint64_t st_cap = 0, rt_cap = 0;     // slots in use this wave (a power of two, <= the allocations)
@@ -1707,7 +1741,8 @@ void spec_commit_prep(jg_ctx* ctx, jg_orset_wire* w) {
         return;
     }
     auto* doffs = w->loffs.as<unsigned long long>();
-    hipLaunchKernelGGL(k_list_offs, dim3(1), dim3(64), 0, ctx->stream, ST.n, ST.sub_cap, RT.n, RT.sub_cap, doffs);
+    auto* spec_words = w->specst.as<unsigned long long>();
+    hipLaunchKernelGGL(k_list_offs, dim3(1), dim3(64), 0, ctx->stream, ST.n, ST.sub_cap, RT.n, RT.sub_cap, doffs, spec_words + 8);
     // grid-stride over the packed lists: enough workgroups for the last wave's distinct strings / records
     auto grid = [](uint64_t seen, uint64_t cap) {
         return dim3((unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks_for(seen ? std::min(cap, 2 * seen + 4096) : cap), 4096)));
@@ -1723,7 +1758,7 @@ void spec_commit_prep(jg_ctx* ctx, jg_orset_wire* w) {
     PT.list = w->st_packed.as<uint32_t>();
     PR.list = w->rt_packed.as<uint32_t>();
     hipLaunchKernelGGL(k_cb_scatter_claimed, grid(w->seen_s + w->seen_r, cs + cr), dim3(kBlock), 0, ctx->stream, doffs, PT, PR, C, B,
-                       w->ovf.as<unsigned long long>());
+                       w->ovf.as<unsigned long long>(), spec_words + 8);
     JG_HIP(hipGetLastError());
 }
 
@@ -1756,6 +1791,11 @@ int check_wave(jg_orset* s, jg_orset_wire* w) {
         unsigned long long h[2];
         std::memcpy(h, jg::pin_at(ctx, 0), 8);
         h[1] = w->lc[0];
+        // the speculative scatter found a claimed place outside its arrays in a wave whose claims all counted: the
+        // tables are inconsistent, and nothing of the wave may commit (it would commit a bucket with a stale slot)
+        JG_REQUIRE(!(w->spec && h[1] == 0 && w->lc[1] == 0 && w->spec_h[8] != 0), JG_EHIP,
+                   "OR-Set wave check: the claims' scatter found places outside the bucket arrays (flags %llx): internal table inconsistency",
+                   w->spec_h[8]);
         const char* e = std::getenv("JANUS_ORSET_TAIL");  // =tables (tests): no fall-back, an overflow is an error
         JG_REQUIRE(h[1] == 0 || !(e && std::strcmp(e, "tables") == 0), JG_ESTATE, "OR-Set wave tables overflowed (JANUS_ORSET_TAIL=tables)");
         w->seen_s = w->seen_r = 0;  // an overflowed wave: the next one sizes its tables from the bound
@@ -1951,10 +1991,10 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     }
     // the whole wave commits and every claim counted (the check read the uncounted word): the claimants' counts
     // and places stand, and neither k_cb_count nor its memsets run
-    const bool claimed = csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0 && n_sets <= w->cb_cap &&
+    // (only a wave the check prepared: its scatter's bound flag was read with the check's words)
+    const bool claimed = w->spec && csi_lim == 0xFFFFFFFFu && t_lim == 0xFFFFFFFFu && w->lc.size() > 1 && w->lc[1] == 0 && n_sets <= w->cb_cap &&
                          !(e && std::strcmp(e, "count") == 0);  // JANUS_ORSET_COMMIT=count: the counting pass always (tests)
     ensure(w->cb, cb_items_bytes(w->st_cap, w->rt_cap));  // (sized by tables_begin)
-    const Claims C = claims_of(w);
     Buckets B = buckets_of(w);
     unsigned long long* st = status_words(w);
     if (n_sets > w->cb_cap) {  // (a set the wave's claims could not count) room for every set's counts
@@ -1978,11 +2018,10 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
     const Sparse S = sparse_of(w);
     const Names N = names_of(w);
     unsigned long long h[8];  // totals: new strings, their bytes, records per side; then the largest buckets
-    if (claimed && w->spec) {  // scanned by the check, totals read with it (spec_commit_prep)
+    if (claimed) {  // scanned by the check, totals read with it (spec_commit_prep)
         std::memcpy(h, w->spec_h, sizeof h);
     } else {
-        if (claimed) {  // (a wave the check did not prepare) the claims' counts scanned here
-        } else if (ns + nrec) {
+        if (ns + nrec) {
             hipLaunchKernelGGL(k_cb_count, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, S, w->vbytes, ST, RT, ns, nrec, csi_lim, t_lim, N,
                                w->sid_id.as<uint32_t>(), B);
         }
@@ -1996,12 +2035,7 @@ bool commit_buckets(jg_orset* s, jg_orset_wire* w, const StrTab& ST, const RecTa
         return false;
     }
     const uint64_t n_new = h[0], nb = h[1], cnt[2] = {h[2], h[3]};
-    if (claimed && w->spec) {
-        // scattered by the check (spec_commit_prep)
-    } else if (ns + nrec && claimed) {
-        hipLaunchKernelGGL(k_cb_scatter_claimed, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, w->loffs.as<unsigned long long>(), ST, RT, C,
-                           B, w->ovf.as<unsigned long long>());
-    } else if (ns + nrec)
+    if (!claimed && ns + nrec)  // (a claimed wave was scattered by the check: spec_commit_prep)
         hipLaunchKernelGGL(k_cb_scatter, dim3(blocks_for(ns + nrec)), dim3(kBlock), 0, ctx->stream, ns, nrec, ST, RT, B);
     if (claimed) ++w->waves_claimed;
     // LDS and threads for the largest bucket (orset_commit.hpp)
@@ -2523,6 +2557,7 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
                         const uint32_t* name_set, const uint32_t* name_id, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_names_sync");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_names_sync: store is NULL");
         JG_REQUIRE((n_sets == 0 || (set && next_id && cleared)) && (n_names == 0 || (name_set && name_id && off && bytes)), JG_EINVAL,
                    "jg_orset_names_sync: NULL argument");
@@ -2578,6 +2613,7 @@ int jg_orset_names_sync(jg_orset* s, uint64_t n_sets, const uint32_t* set, const
 int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_wave_begin");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_begin: store is NULL");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -2595,6 +2631,7 @@ int jg_orset_wave_begin(jg_orset* s, uint64_t cap_msgs, uint64_t cap_bytes) {
 int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* off, const uint8_t* bytes) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_wave_append");
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_append: no open wave (jg_orset_wave_begin)");
         jg_orset_wire* w = s->wire;
         JG_REQUIRE(!w->checked, JG_EINVAL, "jg_orset_wave_append: the wave was already checked");
@@ -2630,6 +2667,7 @@ int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
     if (bad_msg) *bad_msg = UINT64_MAX;
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_wave_check");
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_check: no open wave (jg_orset_wave_begin)");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -2649,6 +2687,7 @@ int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
 int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_wave_commit");
         JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_commit: no open wave (jg_orset_wave_begin)");
         jg_ctx* ctx = s->ctx;
         jg::ensure_device(ctx);
@@ -2671,6 +2710,7 @@ int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
 int jg_orset_wave_abort(jg_orset* s) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_wave_abort");
         JG_REQUIRE(s, JG_EINVAL, "jg_orset_wave_abort: store is NULL");
         jg::ensure_device(s->ctx);
         JG_HIP(hipStreamSynchronize(s->ctx->stream));

@@ -434,6 +434,7 @@ int jg_pnc_create(jg_ctx* ctx, uint64_t n_keys, uint32_t n_replicas, uint32_t el
 int jg_pnc_destroy(jg_pnc* p) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_destroy");
         if (!p) return;
         jg::ensure_device(p->ctx);
         JG_HIP(hipStreamSynchronize(p->ctx->stream));
@@ -444,6 +445,7 @@ int jg_pnc_destroy(jg_pnc* p) {
 int jg_pnc_write_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_write_rows");
         check_store(p, "jg_pnc_write_rows");
         JG_REQUIRE(P && N, JG_EINVAL, "jg_pnc_write_rows: NULL rows");
         if (n_rows == 0) return;
@@ -494,6 +496,7 @@ int jg_pnc_read_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, void* 
 int jg_pnc_merge_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const void* P, const void* N) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_merge_rows");
         check_store(p, "jg_pnc_merge_rows");
         JG_REQUIRE(P && N, JG_EINVAL, "jg_pnc_merge_rows: NULL rows");
         if (n_rows == 0) return;
@@ -516,6 +519,7 @@ int jg_pnc_merge_rows(jg_pnc* p, const uint32_t* key_idx, uint64_t n_rows, const
 int jg_pnc_apply_ops(jg_pnc* p, uint64_t n_ops, const uint32_t* key, const uint32_t* col, const int64_t* delta, const uint8_t* is_n) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_apply_ops");
         check_store(p, "jg_pnc_apply_ops");
         if (n_ops == 0) return;
         JG_REQUIRE(key && col && delta && is_n, JG_EINVAL, "jg_pnc_apply_ops: NULL argument");
@@ -630,6 +634,7 @@ int jg_rows_upload(jg_rows* r, const uint32_t* key_idx, const void* P, const voi
 int jg_pnc_merge_batch(jg_pnc* p, const jg_rows* r, int async) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_merge_batch");
         check_store(p, "jg_pnc_merge_batch");
         JG_REQUIRE(r, JG_EINVAL, "jg_pnc_merge_batch: rows is NULL");
         JG_REQUIRE(r->ctx == p->ctx, JG_EINVAL, "jg_pnc_merge_batch: rows and store belong to different contexts");

@@ -329,6 +329,7 @@ int jg_rows_route(const jg_rows* r, uint32_t world, uint64_t* counts, void* d_ke
 int jg_pnc_merge_device(jg_pnc* p, uint64_t n_rows, const void* d_keys, const void* d_P, const void* d_N) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_merge_device");
         const char* fn = "jg_pnc_merge_device";
         JG_REQUIRE(p, JG_EINVAL, "%s: store is NULL", fn);
         if (n_rows == 0) return;
@@ -383,6 +384,7 @@ int jg_orset_merge_device(jg_orset* s, uint32_t n_runs, const uint64_t* add_coun
                           const void* d_add_tag, const void* d_add_ord, const void* d_rem_key, const void* d_rem_tag, const void* d_rem_ord) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_orset_merge_device");
         const char* fn = "jg_orset_merge_device";
         JG_REQUIRE(s && (n_runs == 0 || (add_counts && rem_counts)), JG_EINVAL, "%s: NULL argument", fn);
         jg_ctx* ctx = s->ctx;

@@ -67,6 +67,7 @@ extern "C" {
 int jg_synth_pnc_store(jg_pnc* p, uint64_t seed) {
     return jg::guard([&] {
         auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_synth_pnc_store");
         JG_REQUIRE(p, JG_EINVAL, "jg_synth_pnc_store: store is NULL");
         jg::ensure_device(p->ctx);
         if (p->eb == 8) fill_pnc<long long>(p->ctx, p->P.p, p->N.p, 0, p->n_keys, p->R, 0, seed);
@@ -90,6 +91,7 @@ int jg_synth_orset(jg_orset* s, uint64_t seed, uint64_t n_groups, uint32_t elems
                    uint32_t rem_per_group, uint32_t rem_u0) {
     return jg::guard([&] {
         auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(s, "jg_synth_orset");
         JG_REQUIRE(s, JG_EINVAL, "jg_synth_orset: store is NULL");
         JG_REQUIRE(elems_per_set > 0 && add_u0 + add_per_group <= 256 && rem_u0 + rem_per_group <= 256, JG_EINVAL,
                    "jg_synth_orset: tag index u must stay below 256");

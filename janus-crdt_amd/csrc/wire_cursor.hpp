@@ -55,6 +55,207 @@ __device__ __forceinline__ int hexv(int c) {
 }
 
 
+// ---- JSON strings: read_string feeds each unescaped UTF-8 byte to sink.put(), sink.esc() at a backslash -------
+struct GuidSink {  // Guid.Parse of the "D" form (what Guid's JSON converter accepts), C# byte order
+    uint32_t k = 0, va = 0, vb = 0, vc = 0;
+    unsigned long long hi = 0;
+    bool bad = false;
+    __device__ void esc() {}
+    __device__ void put(int b) {
+        if (k == 8 || k == 13 || k == 18 || k == 23) {
+            bad |= b != '-';
+        } else if (k < 36) {
+            const int h = hexv(b);
+            bad |= h < 0;
+            const uint32_t x = (uint32_t)h & 15;
+            if (k < 8) va = va << 4 | x;
+            else if (k < 13) vb = vb << 4 | x;
+            else if (k < 18) vc = vc << 4 | x;
+            else {
+                const uint32_t j = k < 23 ? k - 19 : k - 20;  // hex digit among the last 16
+                hi |= (unsigned long long)x << (8 * (j >> 1) + ((j & 1) ? 0 : 4));
+            }
+        } else {
+            bad = true;
+        }
+        ++k;
+    }
+    __device__ bool ok() const { return !bad && k == 36; }
+    __device__ unsigned long long lo() const { return (unsigned long long)va | (unsigned long long)vb << 32 | (unsigned long long)vc << 48; }
+};
+
+__device__ __forceinline__ bool hex4(Cursor& c, uint32_t& u) {
+    u = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int h = hexv(c.get());
+        if (h < 0) return false;
+        u = u << 4 | (uint32_t)h;
+    }
+    return true;
+}
+
+template <class S> __device__ __forceinline__ void put_utf8(S& s, uint32_t u) {
+    if (u < 0x80) { s.put((int)u); return; }
+    if (u < 0x800) { s.put((int)(0xC0 | u >> 6)); s.put((int)(0x80 | (u & 0x3F))); return; }
+    if (u < 0x10000) { s.put((int)(0xE0 | u >> 12)); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F))); return; }
+    s.put((int)(0xF0 | u >> 18)); s.put((int)(0x80 | (u >> 12 & 0x3F))); s.put((int)(0x80 | (u >> 6 & 0x3F))); s.put((int)(0x80 | (u & 0x3F)));
+}
+
+// The rest of a JSON string after its opening quote: escapes decoded (surrogate pairs joined), raw
+// UTF-8 validated, control characters rejected — host/wire.cpp Scan::str.
+template <class S> __device__ __forceinline__ bool read_string(Cursor& c, S& s) {
+    for (;;) {
+        const int ch = c.get();
+        if (ch < 0) return false;
+        if (ch == '"') return true;
+        if (ch < 0x20) return false;
+        if (ch == '\\') {
+            s.esc();
+            const int e = c.get();
+            int out;
+            switch (e) {
+                case '"': out = '"'; break;
+                case '\\': out = '\\'; break;
+                case '/': out = '/'; break;
+                case 'b': out = 8; break;
+                case 'f': out = 12; break;
+                case 'n': out = 10; break;
+                case 'r': out = 13; break;
+                case 't': out = 9; break;
+                case 'u': {
+                    uint32_t u;
+                    if (!hex4(c, u) || (u >= 0xDC00 && u <= 0xDFFF)) return false;
+                    if (u >= 0xD800 && u <= 0xDBFF) {
+                        if (c.get() != '\\' || c.get() != 'u') return false;
+                        uint32_t lo;
+                        if (!hex4(c, lo) || lo < 0xDC00 || lo > 0xDFFF) return false;
+                        u = 0x10000 + ((u - 0xD800) << 10) + (lo - 0xDC00);
+                    }
+                    put_utf8(s, u);
+                    continue;
+                }
+                default: return false;
+            }
+            s.put(out);
+            continue;
+        }
+        if (ch < 0x80) { s.put(ch); continue; }
+        int extra;
+        uint32_t cp;
+        if (ch >= 0xC2 && ch <= 0xDF) { extra = 1; cp = ch & 0x1F; }
+        else if (ch >= 0xE0 && ch <= 0xEF) { extra = 2; cp = ch & 0x0F; }
+        else if (ch >= 0xF0 && ch <= 0xF4) { extra = 3; cp = ch & 0x07; }
+        else return false;
+        s.put(ch);
+        for (int k = 0; k < extra; ++k) {
+            const int cc = c.get();
+            if (cc < 0 || (cc & 0xC0) != 0x80) return false;
+            cp = cp << 6 | (uint32_t)(cc & 0x3F);
+            s.put(cc);
+        }
+        if (extra == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) return false;
+        if (extra == 3 && (cp < 0x10000 || cp > 0x10FFFF)) return false;
+    }
+}
+
+
+// A string whose bytes nobody needs (a skipped member's names and values).
+struct NullSink {
+    __device__ void esc() {}
+    __device__ void put(int) {}
+};
+
+// `lit` at the cursor (true / false / null)
+__device__ __forceinline__ bool take_literal(Cursor& c, const char* lit) {
+    for (; *lit; ++lit)
+        if (c.get() != *lit) return false;
+    return true;
+}
+
+// -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)? and no number character after it
+__device__ inline bool skip_number(Cursor& c) {
+    auto digits = [&c]() {
+        uint32_t k = 0;
+        for (int ch = c.peek(); ch >= '0' && ch <= '9'; ch = c.peek()) ++c.p, ++k;
+        return k;
+    };
+    if (c.peek() == '-') ++c.p;
+    const int d0 = c.peek();
+    if (d0 < '0' || d0 > '9') return false;
+    if (d0 == '0') ++c.p;
+    else digits();
+    if (c.peek() == '.') {
+        ++c.p;
+        if (!digits()) return false;
+    }
+    if (c.peek() == 'e' || c.peek() == 'E') {
+        ++c.p;
+        if (c.peek() == '+' || c.peek() == '-') ++c.p;
+        if (!digits()) return false;
+    }
+    const int n = c.peek();
+    return !((n >= '0' && n <= '9') || n == '.' || n == 'e' || n == 'E' || n == '+' || n == '-');
+}
+
+// The value of a member the message type does not have (System.Text.Json skips it; oracle/json.hpp Reader::
+// skip_value): any well-formed JSON value, validated and dropped.  `depth` = containers open around it (the message
+// object = 1); a container that would open level 65 fails (MaxDepth 64).  Iterative: bit k of `obj` says whether
+// the k-th container open inside the value is an object (at most 63 of them).
+__device__ inline bool skip_value(Cursor& c, int depth) {
+    unsigned long long obj = 0;
+    int n = 0;
+    bool want = true;  // a value next (else: a separator or a closing bracket of the innermost container)
+    for (;;) {
+        c.ws();
+        if (want) {
+            const int ch = c.peek();
+            if (ch == '{' || ch == '[') {
+                if (depth + n + 1 > 64) return false;
+                ++c.p;
+                const bool o = ch == '{';
+                obj = o ? obj | 1ull << n : obj & ~(1ull << n);
+                ++n;
+                c.ws();
+                if (c.peek() == (o ? '}' : ']')) {
+                    ++c.p;
+                    --n;
+                    want = false;
+                } else if (o) {
+                    NullSink ns;
+                    if (!c.expect('"') || !read_string(c, ns) || !c.expect(':')) return false;
+                }
+                continue;
+            }
+            bool ok;
+            if (ch == '"') {
+                ++c.p;
+                NullSink ns;
+                ok = read_string(c, ns);
+            } else if (ch == 't') ok = take_literal(c, "true");
+            else if (ch == 'f') ok = take_literal(c, "false");
+            else if (ch == 'n') ok = take_literal(c, "null");
+            else ok = skip_number(c);
+            if (!ok) return false;
+            want = false;
+            continue;
+        }
+        if (n == 0) return true;
+        const bool o = (obj >> (n - 1)) & 1;
+        const int ch = c.get();
+        if (ch == ',') {
+            if (o) {
+                NullSink ns;
+                if (!c.expect('"') || !read_string(c, ns) || !c.expect(':')) return false;
+            }
+            want = true;
+        } else if (ch == (o ? '}' : ']')) {
+            --n;
+        } else {
+            return false;
+        }
+    }
+}
+
 // LDS written by some lanes of a wave, then read by others: order them (a group never spans waves).
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

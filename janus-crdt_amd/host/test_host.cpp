@@ -303,8 +303,25 @@ int codec_cross_check() {
         janus::ORSetState d = janus::wire::DecodeORSetMsg(enc);
         if (janus::wire::EncodeORSetMsg(d) != enc) { std::printf("FAIL ORSetMsg round trip differs: %s\n", enc.c_str()); return 1; }
     }
-    for (const char* bad : {"{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[]}", "{\"addSet\":{\"a\":[],\"a\":[]},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}",
-                            "{\"addSet\":null,\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"}) {
+    // System.Text.Json's rules (oracle/json.hpp): unknown members skipped, a repeated member or element key: the last
+    // value, at the first key's place — the reader and the oracle decode these to the same state
+    {
+        const std::string g1 = "00000001-0000-0000-0000-000000000000", g2 = "00000002-0000-0000-0000-000000000000",
+                          g3 = "00000003-0000-0000-0000-000000000000";
+        const std::string wild = "{\"x\":{\"y\":[1,-2.5e3,{\"z\":null},true]},\"addSet\":{\"q\":[]},\"removeSet\":{},\"nullAddGuid\":null,"
+                                 "\"nullRemoveGuid\":[],\"addSet\":{\"a\":[\"" + g1 + "\"],\"b\":[\"" + g2 + "\"],\"a\":[\"" + g3 + "\"]},"
+                                 "\"nullAddGuid\":[\"" + g2 + "\"],\"extra\":\"s\\u0041\"}";
+        const std::string want = "{\"addSet\":{\"a\":[\"" + g3 + "\"],\"b\":[\"" + g2 + "\"]},\"removeSet\":{},\"nullAddGuid\":[\"" + g2 +
+                                 "\"],\"nullRemoveGuid\":[]}";
+        if (janus::wire::EncodeORSetMsg(janus::wire::DecodeORSetMsg(wild)) != want || oracle::json::EncodeORSet(oracle::json::DecodeORSet(wild)) != want) {
+            std::printf("FAIL ORSetMsg reader: STJ's skip / last-wins rules\n");
+            return 1;
+        }
+    }
+    for (const char* bad : {"{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[]}", "{\"addSet\":{\"a\":null},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}",
+                            "{\"addSet\":null,\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}",
+                            "{\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[],\"addSet\":null}",
+                            "{\"x\":[1,],\"addSet\":{},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"}) {
         bool threw = false;
         try { janus::wire::DecodeORSetMsg(bad); } catch (const janus::EngineError& e) { threw = e.code == JG_EINVAL; }
         bool othrew = false;

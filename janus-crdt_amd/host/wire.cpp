@@ -2,6 +2,7 @@
 #include "wire.hpp"
 
 #include <cstring>
+#include <unordered_map>
 #include <unordered_set>
 
 namespace janus::wire {
@@ -169,6 +170,49 @@ struct Scan {
         }
         need(']');
     }
+    // An unmapped member's value, validated and dropped (oracle/json.hpp: MaxDepth 64 counting the message object).
+    void skip_value(int depth) {
+        skip_ws();
+        if (i >= s.size()) reject("unexpected end", i);
+        const char c = s[i];
+        if (c == '{' || c == '[') {
+            if (depth + 1 > 64) reject("depth past MaxDepth", i);
+            ++i;
+            const char close = c == '{' ? '}' : ']';
+            if (take(close)) return;
+            do {
+                if (c == '{') {
+                    (void)str();
+                    need(':');
+                }
+                skip_value(depth + 1);
+            } while (take(','));
+            need(close);
+            return;
+        }
+        if (c == '"') { (void)str(); return; }
+        for (const char* lit : {"true", "false", "null"})
+            if (s.compare(i, std::strlen(lit), lit) == 0) { i += std::strlen(lit); return; }
+        auto digits = [&] {
+            const size_t b = i;
+            while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i;
+            return i - b;
+        };
+        if (s[i] == '-') ++i;
+        if (i >= s.size() || s[i] < '0' || s[i] > '9') reject("not a value", i);
+        if (s[i] == '0') ++i;
+        else digits();
+        if (i < s.size() && s[i] == '.') {
+            ++i;
+            if (!digits()) reject("bad number", i);
+        }
+        if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+            ++i;
+            if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+            if (!digits()) reject("bad number", i);
+        }
+        if (i < s.size() && std::strchr("0123456789.eE+-", s[i])) reject("bad number", i);
+    }
 };
 
 // JavaScriptEncoder.Default for a UTF-8 element string.
@@ -314,123 +358,72 @@ std::string EncodeORSetMsg(const ORSetState& m) {
 ORSetState DecodeORSetMsg(std::string_view bytes) {
     Scan sc{bytes};
     ORSetState m;
-    unsigned seen = 0;
+    bool seen[4] = {false, false, false, false}, null_last[4] = {false, false, false, false};
     sc.need('{');
     if (!sc.at('}')) {
         do {
-            const size_t at = sc.i;
             const std::string name = sc.str();
             static const char* names[4] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
             int which = -1;
             for (int k = 0; k < 4; ++k)
                 if (name == names[k]) which = k;
-            if (which < 0) reject("unknown property", at);
-            if (seen >> which & 1) reject("duplicate property", at);
-            seen |= 1u << which;
             sc.need(':');
-            if (sc.take_null()) reject("null member (Merge would throw NullReferenceException)", sc.i);
+            if (which < 0) {  // not a member: skipped (System.Text.Json's default)
+                sc.skip_value(1);
+                continue;
+            }
+            seen[which] = true;  // a repeated member: the last occurrence wins
+            null_last[which] = sc.take_null();
             if (which >= 2) {
-                sc.guids(which == 2 ? m.nullAddGuid : m.nullRemoveGuid);
+                auto& v = which == 2 ? m.nullAddGuid : m.nullRemoveGuid;
+                v.clear();
+                if (!null_last[which]) sc.guids(v);
                 continue;
             }
             auto& map = which == 0 ? m.addSet : m.removeSet;
-            std::unordered_set<std::string> keys;  // duplicate names: linear scan below 32 entries
+            map.clear();
+            if (null_last[which]) continue;
+            std::unordered_map<std::string, size_t> at;  // element -> its place (Dictionary indexer: first place, last value)
+            std::vector<bool> is_null;
             sc.need('{');
             if (!sc.at('}')) {
                 do {
-                    const size_t ek = sc.i;
                     std::string e = sc.str();
-                    bool dup = false;
-                    if (map.size() < 32) {
-                        for (const auto& kv : map) dup |= kv.first == e;
-                    } else {
-                        if (keys.empty())
-                            for (const auto& kv : map) keys.insert(kv.first);
-                        dup = !keys.insert(e).second;
-                    }
-                    if (dup) reject("duplicate element in one map", ek);
                     sc.need(':');
-                    if (sc.take_null()) reject("null tag set", sc.i);
-                    map.emplace_back(std::move(e), std::vector<Guid>());
-                    sc.guids(map.back().second);
+                    const bool nul = sc.take_null();
+                    std::vector<Guid> tags;
+                    if (!nul) sc.guids(tags);
+                    auto it = at.find(e);
+                    if (it == at.end()) {
+                        at.emplace(e, map.size());
+                        map.emplace_back(std::move(e), std::move(tags));
+                        is_null.push_back(nul);
+                    } else {
+                        map[it->second].second = std::move(tags);
+                        is_null[it->second] = nul;
+                    }
                 } while (sc.take(','));
             }
             sc.need('}');
+            for (bool b : is_null)
+                if (b) reject("null tag set (Merge's UnionWith would throw)", sc.i);
         } while (sc.take(','));
     }
     sc.need('}');
     sc.skip_ws();
     if (sc.i != bytes.size()) reject("trailing data", sc.i);
-    if (seen != 15) reject("missing member (Merge would throw NullReferenceException)", sc.i);
+    for (int k = 0; k < 4; ++k)
+        if (!seen[k] || null_last[k]) reject("missing or null member (Merge would throw NullReferenceException)", sc.i);
     return m;
 }
 
 void ScanORSetMsg(std::string_view bytes, ORSetEntryFn fn, void* ctx) {
-    Scan sc{bytes};
-    unsigned seen = 0;
-    std::string scratch;
-    std::vector<std::string> names;  // this map's element names so far (duplicate check)
-    std::unordered_set<std::string> big;  // ... hashed once a map holds 32 names
-    std::vector<Guid> tags;
-    // removeSet entries listed before addSet are held back: the receiver's Merge walks addSet first
-    std::vector<std::pair<std::string, std::vector<Guid>>> held;
-    bool add_done = false;
-    sc.need('{');
-    if (!sc.at('}')) {
-        do {
-            const size_t at = sc.i;
-            const std::string_view name = sc.str_view(scratch);
-            static const char* pnames[4] = {"addSet", "removeSet", "nullAddGuid", "nullRemoveGuid"};
-            int which = -1;
-            for (int k = 0; k < 4; ++k)
-                if (name == pnames[k]) which = k;
-            if (which < 0) reject("unknown property", at);
-            if (seen >> which & 1) reject("duplicate property", at);
-            seen |= 1u << which;
-            sc.need(':');
-            if (sc.take_null()) reject("null member (Merge would throw NullReferenceException)", sc.i);
-            if (which >= 2) {
-                tags.clear();
-                sc.guids(tags);
-                fn(ctx, which == 2 ? 0 : 1, std::string_view(), true, tags.data(), tags.size());
-                continue;
-            }
-            names.clear();
-            big.clear();
-            sc.need('{');
-            if (!sc.at('}')) {
-                do {
-                    const size_t ek = sc.i;
-                    const std::string_view e = sc.str_view(scratch);
-                    bool dup = false;
-                    if (names.size() < 32) {
-                        for (const auto& x : names) dup |= x == e;
-                    } else {
-                        if (big.empty()) big.insert(names.begin(), names.end());
-                        dup = !big.emplace(e).second;
-                    }
-                    if (dup) reject("duplicate element in one map", ek);
-                    names.emplace_back(e);
-                    sc.need(':');
-                    if (sc.take_null()) reject("null tag set", sc.i);
-                    tags.clear();
-                    sc.guids(tags);
-                    if (which == 1 && !add_done) held.emplace_back(names.back(), tags);
-                    else fn(ctx, which, names.back(), false, tags.data(), tags.size());
-                } while (sc.take(','));
-            }
-            sc.need('}');
-            if (which == 0) {
-                add_done = true;
-                for (const auto& h : held) fn(ctx, 1, h.first, false, h.second.data(), h.second.size());
-                held.clear();
-            }
-        } while (sc.take(','));
-    }
-    sc.need('}');
-    sc.skip_ws();
-    if (sc.i != bytes.size()) reject("trailing data", sc.i);
-    if (seen != 15) reject("missing member (Merge would throw NullReferenceException)", sc.i);
+    // the decoded state in ORSet.Merge's walk (ORSet.cs:255-282): addSet entries, removeSet entries, null tag sets
+    const ORSetState m = DecodeORSetMsg(bytes);
+    for (const auto& e : m.addSet) fn(ctx, 0, e.first, false, e.second.data(), e.second.size());
+    for (const auto& e : m.removeSet) fn(ctx, 1, e.first, false, e.second.data(), e.second.size());
+    fn(ctx, 0, std::string_view(), true, m.nullAddGuid.data(), m.nullAddGuid.size());
+    fn(ctx, 1, std::string_view(), true, m.nullRemoveGuid.data(), m.nullRemoveGuid.size());
 }
 
 }  // namespace janus::wire

@@ -24,16 +24,15 @@ bool ParseGuidD(std::string_view s, Guid& g);
 // order with values p[i] / n[i]: {"pVector":{"<g>":p,...},"nVector":{"<g>":n,...}}.  Appends.
 void AppendPNCounterMsg(std::string& out, const Guid* g, const int64_t* p, const int64_t* n, size_t k);
 
-// ORSetMsg<string?> codec.  Decode throws EngineError(JG_EINVAL) where System.Text.Json (or the
-// narrowed contract) rejects the payload.
+// ORSetMsg<string?> codec.  Decode throws EngineError(JG_EINVAL) where System.Text.Json rejects the payload or
+// the reference's Merge would throw (oracle/json.hpp's contract: unknown members skipped, repeats last-wins).
 std::string EncodeORSetMsg(const ORSetState& m);
 ORSetState DecodeORSetMsg(std::string_view bytes);
 
-// The same reader without building an ORSetState: fn(ctx, side, name, is_null, tags, n) once per entry —
-// side 0 = addSet / nullAddGuid, 1 = removeSet / nullRemoveGuid; is_null = the null tag set (name
-// empty); every addSet entry is reported before any removeSet entry, whatever the property order
-// (ORSet.Merge walks addSet first, ORSet.cs:255-279).  `name` and `tags` are valid during the call.
-// Accepts and rejects exactly what DecodeORSetMsg does; an error may come after some callbacks.
+// The decoded state in ORSet.Merge's walk: fn(ctx, side, name, is_null, tags, n) once per entry — side 0 =
+// addSet / nullAddGuid, 1 = removeSet / nullRemoveGuid; is_null = the null tag set (name empty, reported last,
+// after every element: ORSet.cs:255-282).  `name` and `tags` are valid during the call.  Accepts and rejects
+// exactly what DecodeORSetMsg does (nothing is reported for a rejected payload).
 using ORSetEntryFn = void (*)(void* ctx, int side, std::string_view name, bool is_null, const Guid* tags, size_t n);
 void ScanORSetMsg(std::string_view bytes, ORSetEntryFn fn, void* ctx);
 

@@ -324,9 +324,11 @@ TEST(Json_PNCRejects) {
     const char* bad[] = {
         "{\"pVector\":{}}",                                   // nVector missing -> null -> NRE in Merge
         "{\"pVector\":null,\"nVector\":{}}",                // null vector
-        "{\"pVector\":{},\"nVector\":{},\"x\":1}",        // unknown property (narrowed)
-        "{\"pVector\":{},\"nVector\":{},\"pVector\":{}}", // duplicate property
-        "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":1,\"55667788-3344-1122-00ff-eeddccbbaa99\":2},\"nVector\":{}}",
+        "{\"pVector\":{},\"nVector\":{},\"pVector\":null}", // the last occurrence is null
+        "{\"x\":[1,],\"pVector\":{},\"nVector\":{}}",      // a skipped member must still be JSON
+        "{\"x\":01,\"pVector\":{},\"nVector\":{}}",
+        "{\"x\":tru,\"pVector\":{},\"nVector\":{}}",
+        "{\"pvector\":{},\"nVector\":{}}",                // case-sensitive: pVector missing
         "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":01},\"nVector\":{}}",
         "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":1.0},\"nVector\":{}}",
         "{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":2147483648},\"nVector\":{}}",
@@ -337,6 +339,36 @@ TEST(Json_PNCRejects) {
     for (const char* b : bad) CHECK_THROWS<json::JsonException>([&] { json::DecodePNC<int32_t>(b); }, __LINE__);
     CHECK_EQ(json::DecodePNC<int32_t>("{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":-2147483648},\"nVector\":{}}").pVector.size(), (size_t)1);
     CHECK_EQ(json::DecodePNC<int64_t>("{\"pVector\":{\"55667788-3344-1122-00ff-eeddccbbaa99\":2147483648},\"nVector\":{}}").pVector.size(), (size_t)1);
+}
+// System.Text.Json's rules past the compact form (oracle/json.hpp, round 6): unknown members skipped, a repeated
+// member's last occurrence, a repeated key's last value at its first place, escaped names and Guid keys, MaxDepth.
+TEST(Json_STJRules) {
+    const std::string A = "55667788-3344-1122-00ff-eeddccbbaa99", B = "00000001-0002-0003-0405-060708090a0b";
+    Guid ga, gb;
+    CHECK(json::ParseGuidD(A, ga) && json::ParseGuidD(B, gb));
+    auto dec = [](const std::string& x) { return json::DecodePNC<int32_t>(x); };
+    auto items = [](const OrderedDict<Guid, int32_t, GuidHash>& d) {
+        std::vector<std::pair<Guid, int32_t>> v(d.begin(), d.end());
+        return v;
+    };
+    using IV = std::vector<std::pair<Guid, int32_t>>;
+    CHECK(items(dec("{\"pVector\":{},\"nVector\":{},\"x\":1}").pVector).empty());
+    CHECK(items(dec("{\"pVector\":{\"" + A + "\":1},\"nVector\":{},\"pVector\":{\"" + B + "\":5}}").pVector) == (IV{{gb, 5}}));
+    CHECK(items(dec("{\"pVector\":{\"" + A + "\":1,\"" + B + "\":2,\"" + A + "\":3},\"nVector\":{}}").pVector) == (IV{{ga, 3}, {gb, 2}}));
+    CHECK(items(dec("{\"pVector\":{\"" + A + "\":1,\"" + json::GuidD(ga).substr(0, 35) + "9\":-4},\"nVector\":{}}").pVector) == (IV{{ga, -4}}));
+    CHECK(items(dec("{\"p\\u0056ector\":{\"5566\\u0037788-3344-1122-00FF-eeddccbbaa99\":4},\"nVector\":{}}").pVector) == (IV{{ga, 4}}));
+    CHECK(dec("{\"pVector\":null,\"nVector\":{},\"pVector\":{}}").pVector.size() == 0);
+    CHECK(dec("{\"z\":{\"a\":[1,-2.5e+3,{\"b\":[]},true,false,null],\"c\":\"\\u00e9\"},\"pVector\":{},\"nVector\":{}}").pVector.size() == 0);
+    // MaxDepth 64 counting the message object: a skipped value may open 63 more containers, not 64
+    const std::string d63 = std::string(63, '[') + std::string(63, ']'), d64 = std::string(64, '[') + std::string(64, ']');
+    CHECK(dec("{\"x\":" + d63 + ",\"pVector\":{},\"nVector\":{}}").nVector.size() == 0);
+    CHECK_THROWS<json::JsonException>([&] { dec("{\"x\":" + d64 + ",\"pVector\":{},\"nVector\":{}}"); }, __LINE__);
+    // ORSetMsg: an element named twice in one map keeps its first place and its last tag set; `null` only as a last value fails
+    const std::string T1 = "\"" + A + "\"", T2 = "\"" + B + "\"";
+    const ORSetMsg m = json::DecodeORSet("{\"q\":[],\"addSet\":{\"a\":[" + T1 + "],\"b\":[" + T2 + "],\"a\":null,\"a\":[" + T2 + "," + T2 + "]},"
+                                         "\"removeSet\":{},\"nullAddGuid\":null,\"nullRemoveGuid\":[],\"nullAddGuid\":[" + T1 + "]}");
+    CHECK_EQ(json::EncodeORSet(m), "{\"addSet\":{\"a\":[" + T2 + "],\"b\":[" + T2 + "]},\"removeSet\":{},\"nullAddGuid\":[" + T1 + "],\"nullRemoveGuid\":[]}");
+    CHECK_THROWS<json::JsonException>([&] { json::DecodeORSet("{\"addSet\":{\"a\":[],\"a\":null},\"removeSet\":{},\"nullAddGuid\":[],\"nullRemoveGuid\":[]}"); }, __LINE__);
 }
 TEST(Json_ORSetEscapesAndRoundTrip) {  // ORSet.cs:56-69; JavaScriptEncoder.Default
     ORSet s;

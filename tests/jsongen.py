@@ -82,13 +82,25 @@ CONTRACT = [
     (b'', False, False),
     (b'   ', False, False),
     (b'{"pVector":null,"nVector":{}}', False, False),
-    (b'{"pVector":{},"nVector":{},"x":1}', False, False),
-    (b'{"pVector":{},"nVector":{},"pVector":{}}', False, False),
+    # System.Text.Json past the compact form (oracle/json.hpp, round 6): unknown members skipped, a repeated member's
+    # last occurrence, a repeated key's last value at its first place, escaped names and keys, MaxDepth 64
+    (b'{"pVector":{},"nVector":{},"x":1}', True, True),
+    (b'{"pVector":{},"nVector":{},"pVector":{}}', True, True),
     (b'{"pvector":{},"nVector":{}}', False, False),
-    (b'{"p\\u0056ector":{},"nVector":{}}', False, False),
-    (f'{{"pVector":{{"{_A}":1,"{_A}":2}},"nVector":{{}}}}'.encode(), False, False),
-    (f'{{"pVector":{{"{_A}":1,"{_A.upper()}":2}},"nVector":{{}}}}'.encode(), False, False),
-    (f'{{"pVector":{{"{_A}":1}},"nVector":{{"{_A}":1,"{_B}":0,"{_A}":3}}}}'.encode(), False, False),
+    (b'{"p\\u0056ector":{},"nVector":{}}', True, True),
+    (f'{{"pVector":{{"{_A}":1,"{_A}":2}},"nVector":{{}}}}'.encode(), True, True),
+    (f'{{"pVector":{{"{_A}":1,"{_A.upper()}":2}},"nVector":{{}}}}'.encode(), True, True),
+    (f'{{"pVector":{{"{_A}":1}},"nVector":{{"{_A}":1,"{_B}":0,"{_A}":3}}}}'.encode(), True, True),
+    (f'{{"pVector":{{"\\u0031{_B[1:]}":5}},"nVector":{{}}}}'.encode(), True, True),
+    (f'{{"zz":{{"a":[1,-2.5e+3,{{"b":null}},true,false],"c":"\\u00e9x"}},"pVector":{{"{_A}":1}},"nVector":{{}}}}'.encode(), True, True),
+    (f'{{"pVector":null,"nVector":{{}},"pVector":{{"{_A}":9}}}}'.encode(), True, True),
+    (f'{{"pVector":{{"{_A}":9}},"nVector":{{}},"pVector":null}}'.encode(), False, False),
+    (b'{"x":' + b'[' * 63 + b']' * 63 + b',"pVector":{},"nVector":{}}', True, True),
+    (b'{"x":' + b'[' * 64 + b']' * 64 + b',"pVector":{},"nVector":{}}', False, False),
+    (b'{"x":[1,],"pVector":{},"nVector":{}}', False, False),
+    (b'{"x":01,"pVector":{},"nVector":{}}', False, False),
+    (b'{"x":"\\q","pVector":{},"nVector":{}}', False, False),
+    (b'{"x":nul,"pVector":{},"nVector":{}}', False, False),
     (f'{{"pVector":{{"{_A}":01}},"nVector":{{}}}}'.encode(), False, False),
     (f'{{"pVector":{{"{_A}":1.0}},"nVector":{{}}}}'.encode(), False, False),
     (f'{{"pVector":{{"{_A}":1e3}},"nVector":{{}}}}'.encode(), False, False),

@@ -9,7 +9,7 @@ import pytest
 
 import janus_gpu as jg
 import oracle_ref as orc
-from jsongen import CONTRACT, G1, G2, Cluster, encode_pnc, random_guids
+from jsongen import CONTRACT, G1, G2, Cluster, encode_pnc, guid_d, random_guids
 
 pytestmark = pytest.mark.gpu
 
@@ -102,6 +102,61 @@ def test_random_waves_match_oracle(ctx, eb, R, pool, group, ws, fuse, monkeypatc
         pr.s.merge_json(keys, msgs)
         pr.check()
     pr.close()
+
+
+def _stj_variant(rng, m: bytes, eb) -> bytes:
+    """The same decoded state written the ways System.Text.Json also accepts (oracle/json.hpp, round 6): an unknown
+    member before it, an earlier pVector occurrence the real one replaces, a key repeated in its vector with the
+    LARGEST value first (max-merging every occurrence would differ from the last-value rule), a key repeated after
+    itself, an escaped key."""
+    import re
+    s = m.decode()
+    k = int(rng.integers(0, 5))
+    hi = 2**31 - 1 if eb == 4 else 2**63 - 1
+    if k == 0:
+        return ('{"zz":{"a":[1,-2.5e3,{"b":null}],"c":"\\u00e9"},' + s[1:]).encode()
+    if k == 1:
+        return ('{"pVector":{"' + guid_d(*G1) + '":' + str(hi) + '},' + s[1:]).encode()
+    ents = list(re.finditer(r'"([0-9a-fA-F-]{36})":(-?[0-9]+)', s))
+    if not ents:
+        return m
+    e = ents[int(rng.integers(0, len(ents)))]
+    g, v = e.group(1), e.group(2)
+    if k == 2:  # an earlier occurrence holding the largest value
+        return (s[:e.start()] + f'"{g}":{hi},' + s[e.start():]).encode()
+    if k == 3:  # the same key again right after, with a smaller value: it wins
+        return (s[:e.end()] + f',"{g}":{max(0, int(v) // 2)}' + s[e.end():]).encode()
+    return (s[:e.start()] + '"\\u00' + format(ord(g[0]), "02x") + g[1:] + '":' + v + s[e.end():]).encode()
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+@pytest.mark.parametrize("group", ["1", "8"])
+@pytest.mark.parametrize("eb", [4, 8])
+def test_stj_forms_match_oracle(ctx, eb, group, fuse, monkeypatch):
+    """states System.Text.Json decodes beyond the compact form — unknown members, a repeated
+    vector, a key repeated inside one vector (last value, first place), escaped keys — merge on the device exactly
+    as the oracle's Decode + Merge loop merges them, mixed into waves of compact states: the fast path hands them to
+    the serial parser (a repeat among known replicas) or voids the earlier entries in pass C (a repeat among new
+    ones).  Parity unpinned by reference fixtures (none hold such a state)."""
+    monkeypatch.setenv("JANUS_JSON_GROUP", group)
+    monkeypatch.setenv("JANUS_JSON_FUSE", fuse)
+    rng = np.random.default_rng(eb * 7 + int(group) + int(fuse))
+    n_keys = 30
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, 8, eb, stable)
+    cl = Cluster(rng, n_keys, 6, eb, stable)
+    try:
+        for wave in range(5):
+            n = int(rng.integers(50, 1200))
+            keys = rng.integers(0, n_keys, n).astype(np.uint32)
+            msgs = [cl.message(int(k)) for k in keys]
+            msgs = [_stj_variant(rng, m, eb) if rng.random() < 0.3 else m for m in msgs]
+            bad, rc = pr.oracle(keys, msgs)
+            assert bad is None and rc == 0
+            pr.s.merge_json(keys, msgs)
+            pr.check()
+    finally:
+        pr.close()
 
 
 @pytest.mark.parametrize("group", ["8", "16"])

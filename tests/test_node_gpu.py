@@ -541,3 +541,113 @@ def test_streamed_wave_rules(ctx):
     finally:
         for h in (node, tr, pnc, st):
             h.close()
+
+
+def _known_states(rng, n_pnc):
+    """Per key three replica Guids and a state message listing all of them (the wave after it is fully known)."""
+    reps = [J.random_guids(rng, 3) for _ in range(n_pnc)]
+    return reps, lambda k, v: J.encode_pnc(reps[k], [v, v + 1, v + 2], [v // 2, 0, v // 3])
+
+
+@pytest.mark.parametrize("how", ["block_unknown_uid", "orset_rejects_first"])
+def test_cut_at_message_zero_applies_nothing(ctx, how):
+    """a node wave cut at its first message applies nothing.  The chunks' fused pass A has
+    already raised the counters of every PN-Counter state whose replicas the store knows; the prefix of length 0
+    must take them back too (pnc_node_prefix used to return before its undo).  The cut comes from block mode's
+    unknown uid at index 0 (KeyNotFoundException, ReplicationManager.cs:329) or from the OR-Set check rejecting
+    message 0 (the apply Task faults there, SafeCRDTManager.cs:136-139)."""
+    rng = np.random.default_rng(31)
+    n_pnc = 40
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, n_pnc, 6)
+    reps, state = _known_states(rng, n_pnc)
+    try:
+        warm = [(uids[k], 1, 0, state(k, 10 + k)) for k in range(n_pnc)]
+        m.apply(warm)
+        done, cut, rc = node.apply_committed(None, [x[0][0] for x in warm], [x[0][1] for x in warm], [1] * n_pnc, None, [x[3] for x in warm])
+        assert rc == jg.JG_OK and cut is None
+        wave = [(uids[k % n_pnc], 1, 0, state(k % n_pnc, 1000 + 7 * k)) for k in range(400)]
+        if how == "block_unknown_uid":
+            wave[0] = ((0x5151, 0x7373), 1, 0, b'{"pVector":{},"nVector":{}}')
+        else:
+            wave[0] = (uids[n_pnc], 1, 0, b'{"addSet":{}}')  # an ORSetMsg Decode rejects (missing members)
+        exp_done, exp_cut = m.apply(wave, block=how == "block_unknown_uid")
+        assert exp_cut == 0
+        lo, hi, types = [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave]
+        if how == "block_unknown_uid":
+            cut, rc = node.apply_block(lo, hi, types, [x[3] for x in wave])
+        else:
+            done, cut, rc = node.apply_committed(tr, lo, hi, types, [0] * len(wave), [x[3] for x in wave])
+        assert cut == 0 and rc != jg.JG_OK
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)  # the fused raises of messages 1..399 undone
+        assert node.stats()["msgs_applied"] == 0
+    finally:
+        for h in (node, tr, pnc, st):
+            h.close()
+
+
+def test_streamed_wave_holds_its_stores(ctx):
+    """between jg_apply_stream_begin and _end (unlocked calls) the stores' wave scratch, fused pass
+    A's undo records and the OR-Set wave tables belong to the open wave.  Every call that writes the stores, a
+    jg_pnc_wave_* / jg_orset_wave_* wave, another node's wave over a shared store and the tracker's destroy are
+    refused (JG_EINVAL) and change nothing; reads are allowed.  The wave then ends exactly as the oracle's loop
+    says and the stores are free again.  A node destroyed with a stream open aborts it: nothing of it stays."""
+    import ctypes as C
+    rng = np.random.default_rng(37)
+    n_pnc = 30
+    pnc, st, node, tr, m, uids = _setup(ctx, rng, n_pnc, 4)
+    reps, state = _known_states(rng, n_pnc)
+    lib = jg.load()
+    other = None
+    try:
+        warm = [(uids[k], 1, 0, state(k, 5 + k)) for k in range(n_pnc)]
+        m.apply(warm)
+        node.apply_committed(None, [x[0][0] for x in warm], [x[0][1] for x in warm], [1] * n_pnc, None, [x[3] for x in warm])
+        wave = [(uids[k % n_pnc], 1, 0, state(k % n_pnc, 500 + 3 * k)) for k in range(300)]
+        lo, hi, types, msgs = [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], [x[3] for x in wave]
+        assert lib.jg_apply_stream_begin(node._h, tr._h, len(wave), sum(map(len, msgs))) == jg.JG_OK
+        c, keep = node._commit(lo[:150], hi[:150], types[:150], None, msgs[:150])
+        assert lib.jg_apply_stream_append(node._h, C.byref(c)) == jg.JG_OK  # pass A ran (fused) on these 150
+        one = np.zeros((1, R), np.int32)
+        refused = [
+            lambda: pnc.merge_rows(one + 2**30, one + 2**30, [0]),
+            lambda: pnc.write_rows(one, one, [0]),
+            lambda: pnc.apply_ops([0], [0], [5], [0]),
+            lambda: pnc.wave_begin(10, 1000),
+            lambda: pnc.merge_json([0], [state(0, 9999)]),
+            lambda: st.merge(jg.records(n=0), jg.records(n=0)),
+            lambda: st.merge_json([0], [J.encode_orset([("e", [(1, 2)])], [])]),
+        ]
+        for f in refused:
+            with pytest.raises(jg.JanusError) as e:
+                f()
+            assert e.value.code == jg.JG_EINVAL and "node wave" in str(e.value)
+        assert lib.jg_tracker_destroy(tr._h) == jg.JG_EINVAL
+        other = jg.Node(pnc, None)
+        other.register([uids[0][0]], [uids[0][1]], [0], [0])
+        with pytest.raises(jg.JanusError) as e:
+            other.apply_committed(None, [uids[0][0]], [uids[0][1]], [1], None, [state(0, 12345)])
+        assert e.value.code == jg.JG_EINVAL
+        pnc.values()  # reads are allowed
+        c2, keep2 = node._commit(lo[150:], hi[150:], types[150:], None, msgs[150:])
+        assert lib.jg_apply_stream_append(node._h, C.byref(c2)) == jg.JG_OK
+        at, nd = jg._u64(), jg._u64()
+        done = np.zeros(len(wave), np.uint64)
+        assert lib.jg_apply_stream_end(node._h, jg._ptr(done), C.byref(nd), C.byref(at)) == jg.JG_OK
+        m.apply(wave)
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+        pnc.merge_rows(one, one, [0])  # free again (a no-op merge)
+        # a stream left open when its node is destroyed: aborted, the fused raises taken back, the stores let go
+        assert lib.jg_apply_stream_begin(node._h, None, 100, 1 << 20) == jg.JG_OK
+        c3, keep3 = node._commit(lo[:100], hi[:100], types[:100], None, [state(k % n_pnc, 10**6 + k) for k in range(100)])
+        assert lib.jg_apply_stream_append(node._h, C.byref(c3)) == jg.JG_OK
+        node.close()
+        P, N = pnc.read_rows()
+        assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
+        pnc.merge_rows(one, one, [0])
+        other.apply_committed(None, [uids[0][0]], [uids[0][1]], [1], None, [J.encode_pnc(reps[0], [1, 1, 1], [0, 0, 0])])
+    finally:
+        for h in (other, node, tr, pnc, st):
+            if h is not None:
+                h.close()

@@ -516,7 +516,10 @@ def test_routes_follow_the_uid_owner(ctx, world):
 # ---- the RCCL communicator's deadline: a rank that never joins costs a bounded wait, not a hang ----
 def test_comm_init_without_peers_times_out():
     """jg_comm_init(world 2, rank 0) with no rank 1: the non-blocking communicator's init polls against
-    JANUS_COMM_TIMEOUT_S (5 s here), aborts and returns JG_EHIP (run in a child process with its own limit)."""
+    JANUS_COMM_TIMEOUT_S (5 s here), aborts and returns JG_EHIP (run in a child process with its own limit).
+    The child then closes its context and exits cleanly: nothing of the abandoned rendezvous may still run
+    when static teardown does (round 4's detached rendezvous thread left a SIGSEGV at exit, rc 139,
+    which this test did not see because it never looked at the child's exit status)."""
     import subprocess
     import time
     code = ("import sys, time; sys.path.insert(0, %r); import janus_gpu as jg\n"
@@ -532,6 +535,7 @@ def test_comm_init_without_peers_times_out():
     _, rc, secs = line[0].split()
     assert int(rc) == jg.JG_EHIP
     assert 4.0 <= float(secs) < 30 and time.time() - t < 90
+    assert out.returncode == 0, "child exit status %d after the timed-out rendezvous:\n%s" % (out.returncode, out.stderr[-3000:])
 
 
 def _stall_worker(rank, uid_q, q):
