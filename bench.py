@@ -32,6 +32,7 @@ sys.path.insert(0, str(ROOT / "janus-crdt_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 SEED = 0x4A414E5553
+CPU_REPS = 11  # timed passes of every CPU baseline after 3 warm-ups (median of >= 10)
 
 PNC_KEYS, PNC_R, PNC_EB = 10_000_000, 64, 8
 PNC_BYTES_PER_CELL = 6 * PNC_EB  # read A.P A.N B.P B.N, write A.P A.N
@@ -588,8 +589,9 @@ def bench_apply_direct(local):
 
 def bench_apply_orset(sync, rank, world, local):
     """The committed-batch apply loop for OR-Set states (ORSetWorkload-shaped, host/bench_orset.cpp):
-    2000 sets, 4 nodes, 200k full-state ORSetMsg payloads per wave, through the host mirror (host
-    decode + element interning + one jg_orset_merge), vs the oracle's decode + ORSet.Merge loop."""
+    2000 sets, 4 nodes, 200k full-state ORSetMsg payloads per wave, through jg_apply_committed (the payloads
+    decoded, element strings interned and the states merged on the device), vs the oracle's decode +
+    ORSet.Merge loop."""
     import subprocess
     exe = ROOT / "janus-crdt_amd" / "build" / "bench_orset"
     out = subprocess.run([str(exe), "--sets", "2000", "--msgs", "200000", "--waves", "3", "--cpu-msgs", "20000" if world == 1 else "0",
@@ -725,7 +727,7 @@ def cpu_digest_baseline():
     n = 50_000
     data, off = digest_wave(n, SEED + 31)
     first = np.arange(0, n + 1, DIGEST_PER_UPDATE, dtype=np.uint64)
-    t = orc.lib().orc_bench_update_digests(n, off.ctypes.data, data.ctypes.data, first.size - 1, first.ctypes.data, 3)
+    t = orc.lib().orc_bench_update_digests(n, off.ctypes.data, data.ctypes.data, first.size - 1, first.ctypes.data, CPU_REPS)
     buf = data.tobytes()
     t0 = time.perf_counter()
     for u in range(first.size - 1):
@@ -735,7 +737,7 @@ def cpu_digest_baseline():
         hashlib.sha256(toSign).digest()
     t_ssl = time.perf_counter() - t0
     return {"msgs_per_s": n / t, "cores": 1, "kind": "port",
-            "sample": f"oracle UpdateMessage.ComputeDigest (scalar FIPS 180-4 restatement) over the first {n} payloads, median of 3",
+            "sample": f"oracle UpdateMessage.ComputeDigest (scalar FIPS 180-4 restatement) over the first {n} payloads, 3 warm-ups, median of {CPU_REPS}",
             "openssl": {"msgs_per_s": n / t_ssl, "cores": 1,
                         "sample": "the same with Python hashlib (OpenSSL SHA-256, SHA extensions where the CPU has them)"}}
 
@@ -743,11 +745,11 @@ def cpu_digest_baseline():
 def cpu_baseline():
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ref as orc
-    n_keys, reps = 100_000, 5
+    n_keys, reps = 100_000, CPU_REPS
     t = orc.bench_pnc_merge(n_keys, PNC_R, SEED, 1, reps)
     model, ncpu = cpu_info()
     n_sets = 20_000
-    t_or = orc.bench_orset_merge(n_sets, ORSET_E, ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV, SEED, 1, 3)
+    t_or = orc.bench_orset_merge(n_sets, ORSET_E, ORSET_ADD, ORSET_ADD_OV, ORSET_REM, ORSET_REM_OV, SEED, 1, CPU_REPS)
     # the same merge split over the host cores this job may use; the box
     # grants 16 CPUs per GPU, os.cpu_count() shows the whole machine
     par = max(1, min(16, ncpu or 1))
@@ -758,7 +760,7 @@ def cpu_baseline():
         "cores": 1,
         "kind": "port",
         "sample": f"PNCounter.Merge over pre-decoded messages, first {n_keys} keys x {PNC_R} replicas of the C2 "
-                  f"synthetic workload, int64, dictionary-faithful oracle (oracle/), median of {reps}, 1 thread "
+                  f"synthetic workload, int64, dictionary-faithful oracle (oracle/), 3 warm-ups, median of {reps}, 1 thread "
                   f"(the reference's serialized apply task); host: {model}, {ncpu} logical CPUs",
         "orset_records_per_s": n_sets * ORSET_E * 2 * (ORSET_ADD + ORSET_REM) / t_or,
         "parallel": {"value": 4 * n_keys * PNC_R / t_par, "cores": par,

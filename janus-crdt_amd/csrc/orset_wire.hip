@@ -2481,6 +2481,54 @@ void encode_sets(jg_orset* s, uint64_t n, const uint32_t* set, const uint64_t* a
 }
 }  // namespace
 
+namespace {
+// The check and the commit of the open wave: the ABI's (which a held store refuses) and a node wave's own
+// (orset_node_check / orset_node_commit, which hold the store).
+int wave_check_call(jg_orset* s, uint64_t* bad_msg, bool node) {
+    if (bad_msg) *bad_msg = UINT64_MAX;
+    return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        if (!node) jg::require_writable(s, "jg_orset_wave_check");
+        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_check: no open wave (jg_orset_wave_begin)");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = s->wire;
+        if (!w->checked) check_wave(s, w);
+        if (w->first_bad == kNone) return;
+        if (bad_msg) *bad_msg = w->first_bad;
+        unsigned long long e;
+        JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + w->first_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        const bool state = (e & 3) == kKindState;
+        jg::fail(state ? JG_ESTATE : JG_EINVAL, "OR-Set state message %llu is rejected by ORSetMsg.Decode / Merge (%s at byte %llu)",
+                 (unsigned long long)w->first_bad, state ? "an element with an empty tag set" : "JsonException", (unsigned long long)(e >> 2));
+    });
+}
+
+int wave_commit_call(jg_orset* s, uint64_t limit, bool node) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
+        if (!node) jg::require_writable(s, "jg_orset_wave_commit");
+        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_commit: no open wave (jg_orset_wave_begin)");
+        jg_ctx* ctx = s->ctx;
+        jg::ensure_device(ctx);
+        jg_orset_wire* w = s->wire;
+        if (!w->checked) check_wave(s, w);
+        JG_REQUIRE(limit <= w->wn, JG_EINVAL, "jg_orset_wave_commit: limit %llu beyond the wave (%llu messages)", (unsigned long long)limit,
+                   (unsigned long long)w->wn);
+        JG_REQUIRE(w->first_bad == kNone || limit <= w->first_bad, JG_EINVAL, "jg_orset_wave_commit: limit %llu passes the bad message %llu",
+                   (unsigned long long)limit, (unsigned long long)w->first_bad);
+        try {
+            commit_wave(s, w, limit);
+        } catch (...) {
+            close_wave(w);
+            throw;
+        }
+        close_wave(w);
+    });
+}
+}  // namespace
+
 namespace jg {
 // ---- node waves (csrc/node.hip): the node's buffers hold every kind's messages; mset[m] = kSkipIdx for
 // another kind's.  begin sizes the per-message arrays for n messages / nbytes payload bytes.
@@ -2513,7 +2561,7 @@ int orset_node_check(jg_orset* s, uint64_t n, uint64_t nbytes, uint64_t* bad, st
     const auto t0 = std::chrono::steady_clock::now();
     orset_reserve_union(s, 2 * lc[0] + 4096, 2 * lc[1] + 4096);
     if (tr) std::fprintf(stderr, "orset_node_check: union targets reserved in %.0f us\n", std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
-    const int rc = jg_orset_wave_check(s, bad);
+    const int rc = wave_check_call(s, bad, true);
     if (rc != JG_OK) {
         char buf[1024];
         jg_last_error(buf, sizeof buf);
@@ -2522,7 +2570,7 @@ int orset_node_check(jg_orset* s, uint64_t n, uint64_t nbytes, uint64_t* bad, st
     return rc;
 }
 void orset_node_commit(jg_orset* s, uint64_t limit) {
-    const int rc = jg_orset_wave_commit(s, limit);
+    const int rc = wave_commit_call(s, limit, true);
     if (rc != JG_OK) {
         char buf[1024];
         jg_last_error(buf, sizeof buf);
@@ -2663,49 +2711,8 @@ int jg_orset_wave_append(jg_orset* s, uint64_t n, const uint32_t* set, const uin
     });
 }
 
-int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) {
-    if (bad_msg) *bad_msg = UINT64_MAX;
-    return jg::guard([&] {
-        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
-        jg::require_writable(s, "jg_orset_wave_check");
-        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_check: no open wave (jg_orset_wave_begin)");
-        jg_ctx* ctx = s->ctx;
-        jg::ensure_device(ctx);
-        jg_orset_wire* w = s->wire;
-        if (!w->checked) check_wave(s, w);
-        if (w->first_bad == kNone) return;
-        if (bad_msg) *bad_msg = w->first_bad;
-        unsigned long long e;
-        JG_HIP(hipMemcpyAsync(&e, w->err.as<unsigned long long>() + w->first_bad, 8, hipMemcpyDeviceToHost, ctx->stream));
-        JG_HIP(hipStreamSynchronize(ctx->stream));
-        const bool state = (e & 3) == kKindState;
-        jg::fail(state ? JG_ESTATE : JG_EINVAL, "OR-Set state message %llu is rejected by ORSetMsg.Decode / Merge (%s at byte %llu)",
-                 (unsigned long long)w->first_bad, state ? "an element with an empty tag set" : "JsonException", (unsigned long long)(e >> 2));
-    });
-}
-
-int jg_orset_wave_commit(jg_orset* s, uint64_t limit) {
-    return jg::guard([&] {
-        auto lk_ = jg::lock(s);  // calls on one context are serialised (shared scratch, stream)
-        jg::require_writable(s, "jg_orset_wave_commit");
-        JG_REQUIRE(s && s->wire && s->wire->open, JG_EINVAL, "jg_orset_wave_commit: no open wave (jg_orset_wave_begin)");
-        jg_ctx* ctx = s->ctx;
-        jg::ensure_device(ctx);
-        jg_orset_wire* w = s->wire;
-        if (!w->checked) check_wave(s, w);
-        JG_REQUIRE(limit <= w->wn, JG_EINVAL, "jg_orset_wave_commit: limit %llu beyond the wave (%llu messages)", (unsigned long long)limit,
-                   (unsigned long long)w->wn);
-        JG_REQUIRE(w->first_bad == kNone || limit <= w->first_bad, JG_EINVAL, "jg_orset_wave_commit: limit %llu passes the bad message %llu",
-                   (unsigned long long)limit, (unsigned long long)w->first_bad);
-        try {
-            commit_wave(s, w, limit);
-        } catch (...) {
-            close_wave(w);
-            throw;
-        }
-        close_wave(w);
-    });
-}
+int jg_orset_wave_check(jg_orset* s, uint64_t* bad_msg) { return wave_check_call(s, bad_msg, false); }
+int jg_orset_wave_commit(jg_orset* s, uint64_t limit) { return wave_commit_call(s, limit, false); }
 
 int jg_orset_wave_abort(jg_orset* s) {
     return jg::guard([&] {

@@ -292,6 +292,8 @@ int64_t orc_orset_lookup_all(const Rec* A, uint64_t nA, const Rec* Rm, uint64_t 
 }
 
 // ---- CPU baseline (bench.py cpu_baseline, kind "port") --------------------------------------
+constexpr int kWarmups = 3;  // untimed passes before the timed ones (3 warm-ups, median of >= 10)
+
 // PNCounter.Merge over pre-decoded messages for keys [0, n_keys) of the synthetic C2 workload,
 // with `threads` workers splitting the keys (1 = the reference's serialized apply task,
 // SafeCRDTManager.cs:115-117).  Returns the median seconds of `reps` passes; one pass merges
@@ -314,7 +316,7 @@ double orc_bench_pnc_merge(uint64_t n_keys, uint32_t R, uint64_t seed, int threa
     }
     if (threads < 1) threads = 1;
     std::vector<double> times;
-    for (int rep = 0; rep < reps; ++rep) {
+    for (int rep = -kWarmups; rep < reps; ++rep) {  // 3 warm-ups, then the median of reps
         auto t0 = std::chrono::steady_clock::now();
         auto work = [&](uint64_t lo, uint64_t hi) { for (uint64_t k = lo; k < hi; ++k) local[k].Merge(msgs[k]); };
         if (threads == 1) work(0, n_keys);
@@ -323,7 +325,7 @@ double orc_bench_pnc_merge(uint64_t n_keys, uint32_t R, uint64_t seed, int threa
             for (int t = 0; t < threads; ++t) ts.emplace_back(work, n_keys * t / threads, n_keys * (t + 1) / threads);
             for (auto& t : ts) t.join();
         }
-        times.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        if (rep >= 0) times.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     return median_of(times);
 }
@@ -347,7 +349,7 @@ double orc_bench_orset_merge(uint64_t n_sets, uint32_t E, uint32_t a, uint32_t o
     for (auto& kv : rmap) msgs.push_back(kv.second.GetLastSynchronizedUpdate());
     if (threads < 1) threads = 1;
     std::vector<double> times;
-    for (int rep = 0; rep < reps; ++rep) {
+    for (int rep = -kWarmups; rep < reps; ++rep) {
         std::vector<ORSet> local = base;
         auto t0 = std::chrono::steady_clock::now();
         auto work = [&](size_t lo, size_t hi) { for (size_t s = lo; s < hi; ++s) local[s].Merge(msgs[s]); };
@@ -357,7 +359,7 @@ double orc_bench_orset_merge(uint64_t n_sets, uint32_t E, uint32_t a, uint32_t o
             for (int th = 0; th < threads; ++th) ts.emplace_back(work, local.size() * th / threads, local.size() * (th + 1) / threads);
             for (auto& x : ts) x.join();
         }
-        times.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        if (rep >= 0) times.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     return median_of(times);
 }
@@ -527,10 +529,10 @@ void orc_update_digests(uint64_t n, const uint64_t* off, const uint8_t* bytes, c
 double orc_bench_update_digests(uint64_t n, const uint64_t* off, const uint8_t* bytes, uint64_t n_updates, const uint64_t* first, int reps) {
     std::vector<uint8_t> out(32 * (n_updates ? n_updates : 1));
     std::vector<double> t;
-    for (int r = 0; r < reps; ++r) {
+    for (int r = -kWarmups; r < reps; ++r) {
         auto t0 = std::chrono::steady_clock::now();
         orc_update_digests(n, off, bytes, nullptr, n_updates, first, nullptr, out.data());
-        t.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        if (r >= 0) t.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     }
     return median_of(t);
 }

@@ -285,7 +285,7 @@ _CASES = [
     (J.encode_orset([("x", [G1]), ("a", [G2]), ("y", [G3]), ("a", [G1, G3])], [("a", [G3]), ("x", [G1]), ("a", [G1])]), None),
     (b'{"addSet":{"a":null,"a":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', None),
     (b'{"addSet":{"a":["' + _A.encode() + b'"]},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[],"addSet":null}', jg.JG_EINVAL),
-    (b'{"q":{"w":[1,2.5,{"e":"\u00e9"}],"t":true},"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', None),
+    (b'{"q":{"w":[1,2.5,{"e":"\\u00e9"}],"t":true},"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', None),
     (b'{"q":[1,},"addSet":{},"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
     (b'{"addSet":{},"removeSet":{},"nullAddGuid":[]}', jg.JG_EINVAL),
     (b'{"addSet":null,"removeSet":{},"nullAddGuid":[],"nullRemoveGuid":[]}', jg.JG_EINVAL),
