@@ -353,19 +353,21 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
         //
         // The rendezvous.  ncclCommInitRankConfig OUTSIDE a group runs the whole init, the bootstrap's wait for every
         // rank included, on the calling thread even for a non-blocking config (RCCL queues it as an async job and,
-        // with no group open, runs the job at once).  Round 5 therefore ran it on a detached thread; a rank that
-        // gave up left that thread inside the bootstrap, and static teardown at exit then faulted under it (rc 139
-        // after the timeout, gpurun_out/comm_dbg.log).  INSIDE ncclGroupStart / ncclGroupEnd the
-        // non-blocking config makes ncclGroupEnd hand the job to RCCL's own thread and return ncclInProgress with the
-        // handle set: the handle is polled here against the deadline and, past it, aborted here (ncclCommAbort raises
-        // the init's abort flag, which the bootstrap's sockets check, and reclaims the job), so nothing of the
-        // rendezvous outlives the call.  The group calls themselves run on a helper thread this call joins within
-        // the deadline; should they block after all, the helper is left behind as before and the call still
-        // returns JG_EHIP on time.
+        // with no group open, runs the job at once).  Round 5 ran it that way on a detached thread; a rank that gave
+        // up left that thread inside the bootstrap, and static teardown at exit then faulted under it (rc 139 after
+        // the timeout, gpurun_out/comm_dbg.log).  INSIDE ncclGroupStart / ncclGroupEnd the non-blocking
+        // config makes ncclGroupEnd hand the job to RCCL's own thread and return ncclInProgress with the handle set.
+        // A helper thread issues the group and polls the handle to ready (every RCCL call of the rendezvous on the
+        // thread that opened the group, whose thread-local group state RCCL's job may still use); the call waits for
+        // it against the deadline.  Past the deadline the helper, no longer stuck in the bootstrap, sees the call give
+        // up within a poll, aborts the handle (ncclCommAbort raises the init's abort flag, which the bootstrap's
+        // sockets check) and exits, and the call JOINS it: nothing of the rendezvous outlives the call.  Should this
+        // RCCL block inside the group calls after all, the helper is left behind (detached) as in round 5, and the
+        // call still returns JG_EHIP on time.
         struct Job {
             std::mutex m;
             std::condition_variable cv;
-            bool done = false, abandoned = false;
+            bool done = false, abandoned = false, exited = false;
             ncclResult_t r = ncclSuccess;
             ncclComm_t nc = nullptr;
         };
@@ -384,54 +386,49 @@ int jg_comm_init(jg_ctx* ctx, uint32_t rank, uint32_t world, const uint8_t* id, 
                 const ncclResult_t e = ncclGroupEnd();
                 if (r == ncclSuccess || r == ncclInProgress) r = e;
             }
-            std::lock_guard<std::mutex> g(job->m);
-            if (job->abandoned) {  // the caller gave up first (this RCCL blocked in the group calls): the handle is ours
-                if (nc) (void)ncclCommAbort(nc);
-                return;
+            while (r == ncclInProgress && nc) {
+                {
+                    std::lock_guard<std::mutex> g(job->m);
+                    if (job->abandoned) break;
+                }
+                ncclResult_t a = ncclInProgress;
+                const ncclResult_t q = ncclCommGetAsyncError(nc, &a);
+                r = q != ncclSuccess ? q : a;
+                if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(100));
             }
-            job->r = r;
-            job->nc = nc;
-            job->done = true;
+            std::lock_guard<std::mutex> g(job->m);
+            if (job->abandoned || r != ncclSuccess) {
+                if (nc) (void)ncclCommAbort(nc);
+                nc = nullptr;
+            }
+            if (!job->abandoned) {
+                job->r = r;
+                job->nc = nc;
+                job->done = true;
+            }
+            job->exited = true;
             job->cv.notify_all();
         });
+        bool joined = false;
         {
             std::unique_lock<std::mutex> g(job->m);
-            if (!job->cv.wait_until(g, end, [&] { return job->done; })) {
+            if (!job->cv.wait_until(g, end, [&] { return job->done || job->exited; })) {
                 job->abandoned = true;
+                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous timed out\n");
+                // the helper aborts the handle and exits within a poll, unless RCCL holds it inside the group calls
+                joined = job->cv.wait_for(g, std::chrono::seconds(10), [&] { return job->exited; });
                 g.unlock();
-                helper.detach();
-                if (trace_comm()) std::fprintf(stderr, "jg_comm: the group calls did not return; helper left behind\n");
+                if (joined) helper.join();
+                else helper.detach();
+                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous helper %s\n", joined ? "joined" : "left behind");
                 jg::fail(JG_EHIP, "jg_comm_init: not every rank joined in %.0f s (rank %u of %u); JANUS_COMM_TIMEOUT_S sets the wait", c->timeout_s,
                          rank, world);
             }
         }
         helper.join();
-        if (trace_comm()) std::fprintf(stderr, "jg_comm: group returned: %s\n", ncclGetErrorString(job->r));
-        if (job->r != ncclSuccess && job->r != ncclInProgress) {
-            if (job->nc) (void)ncclCommAbort(job->nc);
-            jg::fail(JG_EHIP, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(job->r));
-        }
-        JG_REQUIRE(job->nc, JG_EHIP, "ncclCommInitRankConfig returned no communicator");
+        if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous settled: %s\n", ncclGetErrorString(job->r));
+        JG_REQUIRE(job->r == ncclSuccess && job->nc, JG_EHIP, "ncclCommInitRankConfig failed: %s", ncclGetErrorString(job->r));
         c->nc = job->nc;
-        // the rendezvous polled to completion on this thread against what is left of the deadline; past it the
-        // communicator is aborted here (abort_comm) and the call returns JG_EHIP
-        for (;;) {
-            ncclResult_t a = ncclSuccess;
-            const ncclResult_t q = ncclCommGetAsyncError(c->nc, &a);
-            if (q != ncclSuccess) a = q;
-            if (a == ncclSuccess) break;
-            if (a != ncclInProgress) {
-                abort_comm(c.get());
-                jg::fail(JG_EHIP, "jg_comm_init: the rendezvous failed: %s; the communicator was aborted", ncclGetErrorString(a));
-            }
-            if (Clock::now() > end) {
-                if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous timed out\n");
-                abort_comm(c.get());
-                jg::fail(JG_EHIP, "jg_comm_init: not every rank joined in %.0f s (rank %u of %u); JANUS_COMM_TIMEOUT_S sets the wait", c->timeout_s,
-                         rank, world);
-            }
-            std::this_thread::sleep_for(std::chrono::microseconds(100));
-        }
         if (trace_comm()) std::fprintf(stderr, "jg_comm: rendezvous complete\n");
         c->rccl = true;
         *out = c.release();

@@ -90,7 +90,7 @@ CONTRACT = [
     (b'{"p\\u0056ector":{},"nVector":{}}', True, True),
     (f'{{"pVector":{{"{_A}":1,"{_A}":2}},"nVector":{{}}}}'.encode(), True, True),
     (f'{{"pVector":{{"{_A}":1,"{_A.upper()}":2}},"nVector":{{}}}}'.encode(), True, True),
-    (f'{{"pVector":{{"{_A}":1}},"nVector":{{"{_A}":1,"{_B}":0,"{_A}":3}}}}'.encode(), True, True),
+    (f'{{"pVector":{{"{_A}":1,"{_B}":2}},"nVector":{{"{_A}":1,"{_B}":0,"{_A}":3}}}}'.encode(), True, True),
     (f'{{"pVector":{{"\\u0031{_B[1:]}":5}},"nVector":{{}}}}'.encode(), True, True),
     (f'{{"zz":{{"a":[1,-2.5e+3,{{"b":null}},true,false],"c":"\\u00e9x"}},"pVector":{{"{_A}":1}},"nVector":{{}}}}'.encode(), True, True),
     (f'{{"pVector":null,"nVector":{{}},"pVector":{{"{_A}":9}}}}'.encode(), True, True),
