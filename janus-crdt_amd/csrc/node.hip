@@ -525,12 +525,18 @@ bool host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// JANUS_TEST_ORSET_COMMIT_FAIL=1 (tests, read per call): the wave's OR-Set commit raises its device error flag,
-// so the deferred error path (completions reported first, then the error) runs without a real overflow.
+// A fault injector for one test: JANUS_TEST_ORSET_COMMIT_FAIL=1 makes the wave's OR-Set commit raise its device
+// error flag, so the deferred error path (completions reported first, then the error) runs without a real
+// overflow.  Compiled into the test build only (lib/libjanusgpu_test.so, -DJANUS_TEST_HOOKS): the
+// production library has no injector on its path.
+#ifdef JANUS_TEST_HOOKS
 bool test_commit_fail() {
     const char* e = std::getenv("JANUS_TEST_ORSET_COMMIT_FAIL");
     return e && e[0] == '1';
 }
+#else
+constexpr bool test_commit_fail() { return false; }
+#endif
 constexpr size_t kTask = 2048;
 
 // Every wave, empty ones too: the figures reset, names pending from the last commit dropped, the uid table's

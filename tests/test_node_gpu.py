@@ -468,11 +468,30 @@ def test_orset_id_space_rejects_before_anything_commits(ctx):
             h.close()
 
 
-def test_orset_commit_failure_still_reports_completions(ctx, monkeypatch):
+def test_orset_commit_failure_still_reports_completions():
     """the OR-Set commit's error flag is read with the wave's final read, after k_complete has taken
-    the safe-update completions off the tracker.  A failing commit (forced by JANUS_TEST_ORSET_COMMIT_FAIL)
-    returns its error AFTER the completions: the caller gets every completed origin, in commit order, and the
-    tracker holds exactly the entries not completed."""
+    the safe-update completions off the tracker.  A failing commit (forced by JANUS_TEST_ORSET_COMMIT_FAIL, an
+    injector only the test build lib/libjanusgpu_test.so has: ADVICE r05) returns its error AFTER the completions:
+    the caller gets every completed origin, in commit order, and the tracker holds exactly the entries not
+    completed.  Runs in a child process that loads the test build (JANUS_GPU_LIB)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    lib = root / "janus-crdt_amd" / "lib" / "libjanusgpu_test.so"
+    assert lib.exists(), "the test build is made by __graft_entry__.build()"
+    env = dict(os.environ, JANUS_GPU_LIB=str(lib), JANUS_TEST_ORSET_COMMIT_FAIL="1")
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import janus_gpu as jg, test_node_gpu as t\n"
+            "ctx = jg.Context(0)\nt._commit_failure_scenario(ctx)\nctx.close()\nprint('SCENARIO OK')\n"
+            % (str(root / "janus-crdt_amd"), str(root / "tests")))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=str(root / "tests"))
+    assert out.returncode == 0 and "SCENARIO OK" in out.stdout, out.stdout[-2000:] + out.stderr[-3000:]
+
+
+def _commit_failure_scenario(ctx):
+    assert "libjanusgpu_test" in str(jg.LIB_PATH)
     rng = np.random.default_rng(29)
     pnc, st, node, tr, m, uids = _setup(ctx, rng, 60, 20)
     pcl = J.Cluster(rng, 60, R - 1, EB, stable=None)
@@ -482,7 +501,6 @@ def test_orset_commit_failure_still_reports_completions(ctx, monkeypatch):
         tr.add(list(m.tracker), list(m.tracker.values()))
         exp_done, exp_cut = m.apply(wave)
         assert exp_cut is None and len(exp_done) > 100
-        monkeypatch.setenv("JANUS_TEST_ORSET_COMMIT_FAIL", "1")
         with pytest.raises(jg.JanusError) as ei:
             node.apply_committed(tr, [x[0][0] for x in wave], [x[0][1] for x in wave], [x[1] for x in wave], [x[2] for x in wave],
                                  [x[3] for x in wave])
@@ -492,7 +510,6 @@ def test_orset_commit_failure_still_reports_completions(ctx, monkeypatch):
         P, N = pnc.read_rows()  # the PN-Counter commit went through
         assert np.array_equal(P, m.P) and np.array_equal(N, m.N)
     finally:
-        monkeypatch.delenv("JANUS_TEST_ORSET_COMMIT_FAIL", raising=False)
         for h in (node, tr, pnc, st):
             h.close()
 
