@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 8
+#define JG_ABI_VERSION 9
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -168,6 +168,14 @@ int jg_pnc_encode_json(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint64_
  * batch of client ops be applied in ONE jg_pnc_apply_ops and every snapshot encoded in ONE call. */
 int jg_pnc_encode_json_before(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn,
                               uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* sha);
+/* A round of SafeCRDT.Update's PN-Counter client ops at once (SafeCRDT.cs:39-62; PNCounterWrapper.Update ->
+ * Increment / Decrement, PNCounters.cs:96-112, on this copy's own column col): every op applied (as jg_pnc_apply_ops),
+ * and for each op with need[i] != 0, in op order, dp / dn = the Increment / Decrement amounts the batch's LATER ops
+ * on the same key added (wrapping at the store's width) — the rewind jg_pnc_encode_json_before takes to encode the
+ * snapshot that op shipped.  Computed on the device (a sort of the ops by key, newest first, and a segmented sum).
+ * dp / dn hold count(need) entries.  ABI v9. */
+int jg_pnc_apply_ops_rewind(jg_pnc* pnc, uint64_t n_ops, const uint32_t* key, uint32_t col, const int64_t* delta, const uint8_t* is_n,
+                            const uint8_t* need, int64_t* dp, int64_t* dn);
 /* (sha, here and in jg_orset_encode_json: NULL, or n * 32 bytes receiving each encoded state's SHA256 — the hash
  * UpdateMessage.ComputeDigest takes of it, DAGUpdateMessage.cs:43 — computed on the device from the bytes just
  * written; filled only when out is.  The producer path feeds them to jg_update_digests_of.) */

@@ -549,6 +549,18 @@ __global__ __launch_bounds__(kBlock) void k_intern(const unsigned long long* __r
     }
 }
 
+// Increment / Decrement of one column (PNCounters.cs:97-112, unchecked '+='): wrapping atomic adds.
+template <int EB>
+__global__ __launch_bounds__(kBlock) void k_apply_ops_col(void* P, void* N, const uint32_t* __restrict__ key, uint32_t col,
+                                                          const long long* __restrict__ delta, const uint8_t* __restrict__ is_n, uint64_t n,
+                                                          uint32_t R) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t at = (uint64_t)key[i] * R + col;
+    if constexpr (EB == 4) atomicAdd(static_cast<unsigned int*>(is_n[i] ? N : P) + at, (unsigned int)delta[i]);
+    else atomicAdd(static_cast<unsigned long long*>(is_n[i] ? N : P) + at, (unsigned long long)delta[i]);
+}
+
 __global__ void k_make_keys(const uint32_t* __restrict__ rows, uint64_t n, unsigned long long* __restrict__ keys) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) keys[i] = (unsigned long long)rows[i] << 32 | i;
@@ -1268,6 +1280,53 @@ int jg_host_free(void* p) {
 }
 
 namespace {
+// ---- SafeCRDT.Update's rewinds on the device (jg_pnc_apply_ops_rewind) -------------------------------------------
+// A batch of own-column client ops applied at once (PNCounters.cs:96-112), and for every op whose snapshot ships
+// (SafeCRDT.cs:39-62), the amounts the batch's LATER ops on the same key added to P (Increment) and N (Decrement):
+// jg_pnc_encode_json_before rewinds the row by them.  Keys are made in reverse op order and sorted stably on the row
+// bits, so each key's ops sit together newest first, and an exclusive segmented sum over that order is exactly the
+// later ops' amounts (wrapping, as the host's walk of round 5 summed them: 13-18 ms of host time per 1M C5 ops).
+struct PN2 { unsigned long long p, n; };
+struct PN2Add {
+    __host__ __device__ PN2 operator()(const PN2& a, const PN2& b) const { return PN2{a.p + b.p, a.n + b.n}; }
+};
+
+__global__ void k_make_keys_rev(const uint32_t* __restrict__ rows, uint64_t n, unsigned long long* __restrict__ keys) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) {
+        const uint64_t i = n - 1 - j;
+        keys[j] = (unsigned long long)rows[i] << 32 | i;
+    }
+}
+
+// sorted position s: the op's amount on its vector (the store's width first, as the cells wrap), its key's row
+__global__ void k_rewind_vals(const unsigned long long* __restrict__ sorted, uint64_t n, const long long* __restrict__ delta,
+                              const uint8_t* __restrict__ is_n, uint32_t eb, PN2* __restrict__ vals, uint32_t* __restrict__ seg) {
+    const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t i = (uint32_t)sorted[s];
+    const unsigned long long a = (unsigned long long)(eb == 4 ? (long long)(int)delta[i] : delta[i]);
+    vals[s] = is_n[i] ? PN2{0, a} : PN2{a, 0};
+    seg[s] = (uint32_t)(sorted[s] >> 32);
+}
+
+__global__ void k_flags_u32(const uint8_t* __restrict__ f, uint64_t n, uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) out[i] = f[i] ? 1u : 0u;
+}
+
+// the needed ops' rewinds into need order (need_pos = exclusive count of needed ops before op i)
+__global__ void k_rewind_scatter(const unsigned long long* __restrict__ sorted, uint64_t n, const PN2* __restrict__ later,
+                                 const uint8_t* __restrict__ need, const uint32_t* __restrict__ need_pos, long long* __restrict__ dp,
+                                 long long* __restrict__ dn) {
+    const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t i = (uint32_t)sorted[s];
+    if (!need[i]) return;
+    dp[need_pos[i]] = (long long)later[s].p;
+    dn[need_pos[i]] = (long long)later[s].n;
+}
+
 // jg_pnc_encode_json(_before): length pass, scan, offsets to the host; with `out`, the write pass and its bytes.
 void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off, uint8_t* out,
                  uint64_t cap, const char* fn, uint8_t* sha = nullptr) {
@@ -1317,6 +1376,82 @@ void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, c
     JG_HIP(hipStreamSynchronize(ctx->stream));
 }
 }  // namespace
+
+int jg_pnc_apply_ops_rewind(jg_pnc* p, uint64_t n_ops, const uint32_t* key, uint32_t col, const int64_t* delta, const uint8_t* is_n,
+                            const uint8_t* need, int64_t* dp, int64_t* dn) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        jg::require_writable(p, "jg_pnc_apply_ops_rewind");
+        JG_REQUIRE(p, JG_EINVAL, "jg_pnc_apply_ops_rewind: store is NULL");
+        if (n_ops == 0) return;
+        JG_REQUIRE(key && delta && is_n && need && dp && dn, JG_EINVAL, "jg_pnc_apply_ops_rewind: NULL argument");
+        JG_REQUIRE(col < p->R, JG_EINVAL, "jg_pnc_apply_ops_rewind: column %u past the store's %u replicas", col, p->R);
+        JG_REQUIRE(n_ops <= 0x7FFFFFFFull, JG_EINVAL, "jg_pnc_apply_ops_rewind: at most 2^31-1 ops per call");
+        uint64_t n_need = 0;
+        for (uint64_t i = 0; i < n_ops; ++i) {
+            JG_REQUIRE(key[i] < p->n_keys, JG_EINVAL, "jg_pnc_apply_ops_rewind: op %llu addresses key %u outside the store", (unsigned long long)i,
+                       key[i]);
+            n_need += need[i] != 0;
+        }
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        using ull = unsigned long long;
+        const uint64_t n = n_ops;
+        auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+        // the ops (scratch2): key, delta, is_n, need, then the need positions
+        const uint64_t o_del = al(n * 4), o_isn = o_del + al(n * 8), o_need = o_isn + al(n), o_pos = o_need + al(n), o_end = o_pos + al(n * 4);
+        char* a = static_cast<char*>(jg::scratch(ctx, ctx->scratch2, o_end + 256));
+        auto* dkey = reinterpret_cast<uint32_t*>(a);
+        auto* ddel = reinterpret_cast<long long*>(a + o_del);
+        auto* disn = reinterpret_cast<uint8_t*>(a + o_isn);
+        auto* dneed = reinterpret_cast<uint8_t*>(a + o_need);
+        auto* dpos = reinterpret_cast<uint32_t*>(a + o_pos);
+        JG_HIP(hipMemcpyAsync(dkey, key, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(ddel, delta, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(disn, is_n, n, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(dneed, need, n, hipMemcpyHostToDevice, ctx->stream));
+        // Increment / Decrement (k_apply_ops with every op on column col)
+        const unsigned g = blocks_for(n);
+        if (p->eb == 8) hipLaunchKernelGGL(k_apply_ops_col<8>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
+        else hipLaunchKernelGGL(k_apply_ops_col<4>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
+        JG_HIP(hipGetLastError());
+        if (n_need == 0) {
+            JG_HIP(hipStreamSynchronize(ctx->stream));
+            return;
+        }
+        // the rewinds (scratch: keys, values, sums, segments, the scans' temp; sort_keys uses scratch3)
+        const uint64_t o_val = al(n * 8), o_sum = o_val + al(n * 16), o_seg = o_sum + al(n * 16), o_dp = o_seg + al(n * 4),
+                       o_tmp = o_dp + al(n_need * 16);
+        size_t t_scan = 0, t_pos = 0;
+        JG_HIP(hipcub::DeviceScan::ExclusiveScanByKey(nullptr, t_scan, (const uint32_t*)nullptr, (const PN2*)nullptr, (PN2*)nullptr, PN2Add(),
+                                                      PN2{0, 0}, (int)n, hipcub::Equality(), ctx->stream));
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_pos, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, ctx->stream));
+        char* b = static_cast<char*>(jg::scratch(ctx, ctx->scratch, o_tmp + std::max(t_scan, t_pos) + 256));
+        auto* keys = reinterpret_cast<ull*>(b);
+        auto* vals = reinterpret_cast<PN2*>(b + o_val);
+        auto* later = reinterpret_cast<PN2*>(b + o_sum);
+        auto* seg = reinterpret_cast<uint32_t*>(b + o_seg);
+        auto* ddp = reinterpret_cast<long long*>(b + o_dp);
+        auto* ddn = ddp + n_need;
+        void* tmp = b + o_tmp;
+        // need positions first (the flags as u32 in `seg`: a scan of u8 would sum in u8), then the keys
+        hipLaunchKernelGGL(k_flags_u32, dim3(g), dim3(kBlock), 0, ctx->stream, dneed, n, seg);
+        size_t t = t_pos;
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, seg, dpos, (int)n, ctx->stream));
+        hipLaunchKernelGGL(k_make_keys_rev, dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, keys);
+        JG_HIP(hipGetLastError());
+        const ull* sorted = sort_keys(ctx, keys, n, p->n_keys);
+        hipLaunchKernelGGL(k_rewind_vals, dim3(g), dim3(kBlock), 0, ctx->stream, sorted, n, ddel, disn, p->eb, vals, seg);
+        JG_HIP(hipGetLastError());
+        t = t_scan;
+        JG_HIP(hipcub::DeviceScan::ExclusiveScanByKey(tmp, t, seg, vals, later, PN2Add(), PN2{0, 0}, (int)n, hipcub::Equality(), ctx->stream));
+        hipLaunchKernelGGL(k_rewind_scatter, dim3(g), dim3(kBlock), 0, ctx->stream, sorted, n, later, dneed, dpos, ddp, ddn);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemcpyAsync(dp, ddp, n_need * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipMemcpyAsync(dn, ddn, n_need * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
 
 int jg_pnc_encode_json(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint64_t* off, uint8_t* out, uint64_t cap) {
     return jg::guard([&] {

@@ -925,10 +925,14 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         }
         std::vector<uint64_t> alim(or_snap ? idx.size() : 0), rlim(or_snap ? idx.size() : 0);
         const double ta = trace ? now() : 0;
+        // the round's PN-Counter ops applied, and the rewind of every needed snapshot (the amounts of the key's later
+        // ops in the round) computed, in ONE call on the device (jg_pnc_apply_ops_rewind): dp / dn in op order over the
+        // needed ops, which is pnc_need's order below
+        std::vector<int64_t> dp, dn;
         if (!ppos.empty()) {
-            std::vector<uint32_t> pkey(ppos.size()), pcol(ppos.size(), 0);
+            std::vector<uint32_t> pkey(ppos.size());
             std::vector<int64_t> pdelta(ppos.size());
-            std::vector<uint8_t> pisn(ppos.size());
+            std::vector<uint8_t> pisn(ppos.size()), pneed(ppos.size());
             parallel_ranges(pool(), ppos.size(), [&](size_t b, size_t e, int) {
                 for (size_t k = b; k < e; ++k) {
                     const size_t i = idx[ppos[k]];
@@ -936,10 +940,15 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                     pkey[k] = krow[i];
                     pdelta[k] = eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount;
                     pisn[k] = op.opId == 2 ? 1 : 0;
+                    pneed[k] = need[i];
                 }
             });
+            size_t nn = 0;
+            for (uint8_t x : pneed) nn += x;
+            dp.resize(nn);
+            dn.resize(nn);
             materialize_names();
-            check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
+            check(jg_pnc_apply_ops_rewind(pnc_, pkey.size(), pkey.data(), 0, pdelta.data(), pisn.data(), pneed.data(), dp.data(), dn.data()));
         }
         if (!ops.empty()) {
             std::vector<uint64_t> al, rl;
@@ -956,45 +965,12 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         for (size_t j = 0; j < idx.size(); ++j)
             if (need[idx[j]]) (kpn[idx[j]] ? pnc_need : or_need).push_back(j);
         if (!pnc_need.empty()) {
-            // the amounts each key's ops after a needed op added (Increment -> P, Decrement -> N), wrapping like the
-            // cells: walk the round backwards, per row (a row-indexed array, its touched entries reset after)
-            if (pnc_after_.size() < max_keys_) pnc_after_.assign(max_keys_, {0, 0});
-            std::vector<int64_t> dp(pnc_need.size()), dn(pnc_need.size());
             std::vector<uint32_t> prow(pnc_need.size());
             std::vector<size_t> at(pnc_need.size());
-            std::vector<int32_t> wof(idx.size(), -1);  // position in pnc_need of a needed op
-            for (size_t w = 0; w < pnc_need.size(); ++w) wof[pnc_need[w]] = (int32_t)w;
-            // rows are independent: worker t walks the round backwards over the rows with row % T == t (each op's
-            // owner computed once, by the workers: a division per op in every worker's walk was most of the rewind)
-            const size_t T = (size_t)std::max(1, pool().size());
-            std::vector<uint16_t> own(idx.size());
-            parallel_ranges(pool(), idx.size(), [&](size_t b, size_t e, int) {
-                for (size_t j = b; j < e; ++j) own[j] = kpn[idx[j]] ? (uint16_t)(krow[idx[j]] % T) : (uint16_t)0xFFFF;
-            });
-            parallel_ranges(pool(), T, [&](size_t tb0, size_t te0, int) {
-                for (size_t t = tb0; t < te0; ++t) {
-                    for (size_t j = idx.size(); j-- > 0;) {
-                        if (own[j] != t) continue;
-                        const size_t i = idx[j];
-                        const ClientOp& op = ups[i].op;
-                        auto& a = pnc_after_[krow[i]];
-                        if (wof[j] >= 0) {
-                            const size_t w = (size_t)wof[j];
-                            dp[w] = (int64_t)a.first;
-                            dn[w] = (int64_t)a.second;
-                            prow[w] = krow[i];
-                            at[w] = i;
-                        }
-                        const uint64_t amt = (uint64_t)(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
-                        (op.opId == 2 ? a.second : a.first) += amt;
-                    }
-                    for (size_t j = 0; j < idx.size(); ++j)
-                        if (own[j] == t) pnc_after_[krow[idx[j]]] = {0, 0};
-                }
-            }, 2);
+            for (size_t w = 0; w < pnc_need.size(); ++w) prow[w] = krow[idx[pnc_need[w]]], at[w] = idx[pnc_need[w]];
             const double trw = trace ? now() : 0;
             EncodePNCRowsBefore(prow, dp, dn, at, snap, &ssha, &shas);
-            if (trace) std::fprintf(stderr, "SubmitClientUpdates: PN-Counter rewind %.1f ms, encode + hashes + strings %.1f ms\n", trw - tb, now() - trw);
+            if (trace) std::fprintf(stderr, "SubmitClientUpdates: PN-Counter rows %.1f ms, encode + hashes + strings %.1f ms\n", trw - tb, now() - trw);
         }
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;

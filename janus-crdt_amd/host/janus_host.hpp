@@ -261,7 +261,6 @@ class GpuStableStore {
     uint8_t* pin_buf_ = nullptr;
     size_t pin_cap_ = 0;
     double last_pnc_bytes_ = 400;
-    std::vector<std::pair<uint64_t, uint64_t>> pnc_after_;  // SubmitClientUpdates: per row, the amounts of later ops
     std::unordered_map<Guid, KeyRef, GuidHash> uids_;
     // A flat open-addressing copy of uids_ for the producer path's per-op lookups (one 32-byte slot per probe,
     // prefetched a few ops ahead; the node map costs two dependent cache misses per lookup: 12-20 ms per 1M ops

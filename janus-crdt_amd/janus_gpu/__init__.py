@@ -31,7 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
-    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before", "jg_orset_encode_json", "jg_orset_apply_ops_ords",
+    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before", "jg_pnc_apply_ops_rewind", "jg_orset_encode_json", "jg_orset_apply_ops_ords",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
@@ -100,6 +100,7 @@ _SIGS = {
     "jg_orset_lookup_all": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
+    "jg_pnc_apply_ops_rewind": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_orset_encode_json": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
     "jg_orset_apply_ops_ords": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
@@ -380,6 +381,16 @@ class PNCStore:
         _check(load().jg_pnc_encode_json(self._h, k.size, _ptr(k), _ptr(off), _ptr(out), out.size))
         b = out.tobytes()
         return [b[int(off[i]):int(off[i + 1])] for i in range(k.size)]
+
+    def apply_ops_rewind(self, key, delta, is_n, need, col=0):
+        """jg_pnc_apply_ops_rewind: apply the ops to column `col`; for each op with need[i], in op order, the amounts
+        the later ops on its key added to P and N (the rewind jg_pnc_encode_json_before takes)."""
+        key, delta = _arr(key, np.uint32), _arr(delta, np.int64)
+        is_n, need = _arr(is_n, np.uint8), _arr(need, np.uint8)
+        k = int(np.count_nonzero(need))
+        dp, dn = np.zeros(max(1, k), np.int64), np.zeros(max(1, k), np.int64)
+        _check(load().jg_pnc_apply_ops_rewind(self._h, key.size, _ptr(key), col, _ptr(delta), _ptr(is_n), _ptr(need), _ptr(dp), _ptr(dn)))
+        return dp[:k], dn[:k]
 
     def encode_json_before(self, key_idx, dp, dn, col=0, sha=False):
         """jg_pnc_encode_json_before: each row as it stood before its last dp[i] / dn[i] of increments to `col`

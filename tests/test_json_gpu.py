@@ -631,3 +631,46 @@ def test_encode_before_matches_oracle_encoder(ctx, eb):
     assert states == got
     assert all(h[i].tobytes() == hashlib.sha256(got[i]).digest() for i in range(len(got)))
     pr.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
+@pytest.mark.parametrize("n_keys,n_ops", [(40, 3000), (200000, 100000), (3, 1)])
+def test_apply_ops_rewind_matches_walk(ctx, eb, n_keys, n_ops):
+    """jg_pnc_apply_ops_rewind (round 6): a batch of own-column Increment / Decrement ops (PNCounters.cs:96-112)
+    applied at once, and for every op whose snapshot ships (SafeCRDT.cs:39-62) the amounts the batch's LATER ops on
+    the same key added to P and N — computed on the device by a sort and a segmented sum — equal the host's
+    backward walk (round 5's SubmitClientUpdates), wrapping included; the store then holds every op's amount."""
+    rng = np.random.default_rng(7 * eb + n_ops)
+    pr = Pair(ctx, n_keys, 4, eb, random_guids(rng, n_keys))
+    hot = rng.integers(0, n_keys, max(1, n_keys // 10))
+    key = np.where(rng.random(n_ops) < 0.5, rng.choice(hot, n_ops), rng.integers(0, n_keys, n_ops)).astype(np.uint32)
+    delta = rng.integers(1, 1000, n_ops).astype(np.int64)
+    delta[rng.random(n_ops) < 0.01] = 2**31 - 3  # past the int32 edge once summed
+    is_n = (rng.random(n_ops) < 0.3).astype(np.uint8)
+    need = (rng.random(n_ops) < 0.6).astype(np.uint8)
+    bits = 32 if eb == 4 else 64
+    mask = (1 << bits) - 1
+    amt = [(int(d) & 0xFFFFFFFF) if eb == 4 else int(d) for d in delta]
+    exp_p, exp_n, after = [], [], {}
+    for i in range(n_ops - 1, -1, -1):  # the walk: newest first, per key
+        a = after.setdefault(int(key[i]), [0, 0])
+        if need[i]:
+            exp_p.append(a[0])
+            exp_n.append(a[1])
+        a[int(is_n[i])] += amt[i] if eb == 8 else (amt[i] if amt[i] < 2**31 else amt[i] - 2**32)
+    exp_p, exp_n = exp_p[::-1], exp_n[::-1]
+    dp, dn = pr.s.apply_ops_rewind(key, delta, is_n, need)
+
+    def w64(x):
+        x &= (1 << 64) - 1
+        return x - (1 << 64) if x >= 1 << 63 else x
+    assert [w64(int(x)) for x in dp] == [w64(x) for x in exp_p]
+    assert [w64(int(x)) for x in dn] == [w64(x) for x in exp_n]
+    P, N = pr.s.read_rows()
+    tot = np.zeros((2, n_keys), object)
+    for i in range(n_ops):
+        tot[int(is_n[i]), int(key[i])] += int(delta[i])
+    for which, M in ((0, P), (1, N)):
+        got = [int(x) & mask for x in M[:, 0]]
+        assert got == [int(t) & mask for t in tot[which]]
+    pr.close()
