@@ -632,35 +632,44 @@ uint8_t* GpuStableStore::pinned_buf(size_t bytes) {
     return pin_buf_;
 }
 
-void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
-                                         const std::vector<size_t>& at, std::vector<std::string>& out,
-                                         std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has) {
-    const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3;
-    flush_registrations();
+const uint8_t* GpuStableStore::EncodePNCRowsRaw(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
+                                                std::vector<uint64_t>& off, std::vector<uint8_t>* sha) {
     const size_t n = rows.size();
-    std::vector<uint64_t> off(n + 1, 0);
+    off.assign(n + 1, 0);
     // one call into a page-locked buffer sized from the last call (a second only if the states outgrew it)
     size_t guess = std::max<size_t>(pin_cap_, (size_t)(n * (last_pnc_bytes_ + 8)) + 4096);
     uint8_t* buf = pinned_buf(guess);
-    std::vector<uint8_t> h(sha ? 32 * n : 0);  // each state's SHA-256, hashed on the device as it is encoded
-    int rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, sha ? h.data() : nullptr);
+    if (sha) sha->assign(32 * n, 0);  // each state's SHA-256, hashed on the device as it is encoded
+    uint8_t* h = sha ? sha->data() : nullptr;
+    int rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, h);
     if (rc == JG_ESTATE && off[n] > pin_cap_) {
         buf = pinned_buf(off[n]);
-        rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, sha ? h.data() : nullptr);
+        rc = jg_pnc_encode_json_before(pnc_, n, rows.data(), 0, dp.data(), dn.data(), off.data(), buf, pin_cap_, h);
     }
     check(rc);
+    if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
+    return buf;
+}
+
+void GpuStableStore::EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
+                                         const std::vector<size_t>& at, std::vector<std::string>& out,
+                                         std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has) {
     static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t0 = trace ? now() : 0;
+    flush_registrations();
+    const size_t n = rows.size();
+    std::vector<uint64_t> off;
+    std::vector<uint8_t> h;
+    const uint8_t* buf = EncodePNCRowsRaw(rows, dp, dn, off, sha ? &h : nullptr);
     const double t1 = trace ? now() : 0;
-    if (n) last_pnc_bytes_ = (double)off[n] / (double)n;
-    const double t2 = t1;
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
         for (size_t i = b; i < e; ++i) {
             out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
             if (!h.empty()) std::memcpy((*sha)[at[i]].data(), h.data() + 32 * i, 32), (*has)[at[i]] = 1;
         }
     });
-    if (trace) std::fprintf(stderr, "EncodePNCRowsBefore(%zu): encode %.1f ms, hashes %.1f ms, strings %.1f ms\n", n, t1 - t0, t2 - t1, now() - t2);
+    if (trace) std::fprintf(stderr, "EncodePNCRowsBefore(%zu): encode %.1f ms, strings %.1f ms\n", n, t1 - t0, now() - t1);
 }
 
 // ComputeDigests of msgs[first..] from per-payload SHA-256s: the ones not given (has[i] = 0: states queued by an earlier
@@ -769,74 +778,151 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     double tt[6] = {trace ? now() : 0};
     double t_apply = 0, t_enc_p = 0, t_enc_o = 0;
     size_t n_chunks = 0;
-    // the wrappers' checks, before anything is applied or queued: every op's key resolved by the workers (read-only
-    // lookups), the first failing op then raises its error as the serial loop would
+    // Round 6: three things overlap.  A helper thread runs the wrappers' checks on the workers (every op's key resolved,
+    // read-only) while this thread walks the batcher over message identities (serial, nothing committed until the
+    // checks pass); then, for a batch of PN-Counter ops only (one round), the helper applies them, computes every
+    // snapshot's rewind and encodes ALL of them on the device (jg_pnc_apply_ops_rewind + jg_pnc_encode_json_before:
+    // library calls, no workers) while this thread computes the flushes and the tracker adds on the workers.  Only
+    // the snapshots the batcher keeps become strings.  A failing check still raises before anything is applied or
+    // queued, as the serial loop would.
     std::vector<const KeyRef*> kref(n);
     // each op's key as plain arrays: the serial walks below would chase every KeyRef through the uid map's nodes
     std::vector<uint32_t> krow(n);
     std::vector<uint8_t> kpn(n);  // 1: a PN-Counter key
     std::vector<size_t> first_bad(pool().size(), n);
     ensure_uid_index();
-    parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
-        constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
-        for (size_t i = b; i < std::min(e, b + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
-        for (size_t i = b; i < e; ++i) {
-            if (i + kAhead < e) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
-            const KeyRef* kr = find_uid(ups[i].op.uid);
-            kref[i] = kr;
-            if (kr) krow[i] = kr->idx, kpn[i] = kr->type == CrdtType::PNCounter ? 1 : 0;
-            if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
-                first_bad[t] = i;
-                return;
+    flush_registrations();  // (the helper's encode needs every registered row's columns on the device)
+    struct Spec {  // the helper's device results for a PN-Counter-only batch
+        bool on = false;
+        std::vector<int64_t> dp, dn;
+        std::vector<uint64_t> off;
+        std::vector<uint8_t> sha;
+        const uint8_t* buf = nullptr;
+    } spec;
+    std::mutex hm;
+    std::condition_variable hcv;
+    bool checks_done = false;
+    size_t bad = n;
+    std::exception_ptr herr;
+    double t_chk = 0, t_spec = 0;
+    std::thread helper([&] {
+        try {
+            parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
+                constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
+                for (size_t i = b; i < std::min(e, b + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
+                for (size_t i = b; i < e; ++i) {
+                    if (i + kAhead < e) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
+                    const KeyRef* kr = find_uid(ups[i].op.uid);
+                    kref[i] = kr;
+                    if (kr) krow[i] = kr->idx, kpn[i] = kr->type == CrdtType::PNCounter ? 1 : 0;
+                    if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
+                        first_bad[t] = i;
+                        return;
+                    }
+                }
+            });
+            const size_t b = *std::min_element(first_bad.begin(), first_bad.end());
+            const bool pnc_only = b == n && n > 0 && std::all_of(kpn.begin(), kpn.end(), [](uint8_t x) { return x != 0; });
+            {
+                std::lock_guard<std::mutex> g(hm);
+                bad = b;
+                checks_done = true;
+                t_chk = trace ? now() : 0;
             }
+            hcv.notify_all();
+            if (!pnc_only) return;
+            std::vector<int64_t> delta(n);
+            std::vector<uint8_t> isn(n), all(n, 1);
+            for (size_t i = 0; i < n; ++i) {
+                delta[i] = eb_ == 4 ? (int64_t)(int32_t)ups[i].op.amount : ups[i].op.amount;
+                isn[i] = ups[i].op.opId == 2 ? 1 : 0;
+            }
+            spec.dp.resize(n);
+            spec.dn.resize(n);
+            check(jg_pnc_apply_ops_rewind(pnc_, n, krow.data(), 0, delta.data(), isn.data(), all.data(), spec.dp.data(), spec.dn.data()));
+            spec.buf = EncodePNCRowsRaw(krow, spec.dp, spec.dn, spec.off, &spec.sha);
+            spec.on = true;
+            t_spec = trace ? now() : 0;
+        } catch (...) {
+            std::lock_guard<std::mutex> g(hm);
+            herr = std::current_exception();
+            checks_done = true;
+            hcv.notify_all();
         }
     });
-    const size_t bad = *std::min_element(first_bad.begin(), first_bad.end());
-    if (bad < n) {
-        if (!kref[bad]) throw EngineError(JG_EINVAL, "unknown CRDT uid");
-        throw EngineError(JG_EINVAL, kref[bad]->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
-    }
-    const double t_chk = trace ? now() : 0;
+    struct JoinGuard {  // the helper never outlives the call, whatever throws
+        std::thread& t;
+        ~JoinGuard() {
+            if (t.joinable()) t.join();
+        }
+    } join_guard{helper};
     // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
     //    q entries: message, op index (kOld: queued by an earlier call), and whether SafeCRDT.Update
     //    tracked it.  The batcher's safeUpdateTracker.ContainsKey(msg) (:176) is that flag: a message the
     //    batcher drains has not been submitted yet, so nothing can have removed its entry.
     constexpr int64_t kOld = -1;
     struct QE { int64_t op; uint32_t old; bool tracked; };  // op: a client op of this call, or kOld: oldq[old]
-    std::vector<std::pair<NetworkProtocol, bool>> oldq = std::move(batch_queue_);
-    batch_queue_.clear();
     std::vector<QE> q;
-    q.reserve(oldq.size() + n);
-    for (size_t k = 0; k < oldq.size(); ++k) q.push_back(QE{kOld, (uint32_t)k, oldq[k].second});
+    q.reserve(batch_queue_.size() + n);
+    for (size_t k = 0; k < batch_queue_.size(); ++k) q.push_back(QE{kOld, (uint32_t)k, batch_queue_[k].second});
     const uint64_t seq0 = next_seq_;  // op i's message carries seq0 + i (next_seq_++ per Update)
-    next_seq_ += n;
     // (a) serial and light: which queue entries each flush drains, and the one it loses.  A flush drains the whole
-    //     queue unless its safe entries reach clientBatchSize first; the entry dequeued then is lost (:175).
+    //     queue unless its safe entries reach clientBatchSize first; the entry dequeued then is lost (:175).  The live
+    //     queue's safe count is kept as entries arrive and leave, so the entry-by-entry drain runs only in that case.
     struct Range { size_t h0, h1; };
     std::vector<Range> ranges;
     size_t head = 0;  // q[head..] is the live queue
+    size_t safe_live = 0;
+    for (const QE& e : q) safe_live += e.tracked;
+    double last_submit = last_submit_ms_;
     std::vector<uint64_t> t_seq, t_org;  // SafeCRDT.Update's TryAdds, handed to the tracker in one call after the loop
+    t_seq.reserve(n);
+    t_org.reserve(n);
+    const size_t batch = (size_t)std::max(clientBatchSize, 0);
     for (size_t i = 0; i < n; ++i) {
         const bool tracked = ups[i].isSafe && ups[i].origin != 0;  // SafeCRDT.cs:55-56
         if (tracked) t_seq.push_back(seq0 + i), t_org.push_back(ups[i].origin);
         q.push_back(QE{(int64_t)i, 0, tracked});
-        if ((int)(q.size() - head) >= clientBatchSize || ups[i].now_ms - last_submit_ms_ > 100.0) {
+        safe_live += tracked;
+        if (q.size() - head >= batch || ups[i].now_ms - last_submit > 100.0) {
             const size_t h0 = head;
-            size_t safe_n = 0, kept = 0, end = 0;
-            while (head < q.size()) {
-                const size_t k = head++;                              // TryDequeue first ...
-                if (!((int)safe_n < clientBatchSize)) break;          // ... so this one is lost (:175)
-                if (q[k].tracked) ++safe_n;
-                ++kept;
-                end = head;
+            size_t end = 0, kept = 0;
+            if (safe_live < batch) {  // every live entry drains
+                kept = q.size() - head;
+                end = head = q.size();
+                safe_live = 0;
+            } else {
+                size_t safe_n = 0;
+                while (head < q.size()) {
+                    const size_t k = head++;                              // TryDequeue first ...
+                    safe_live -= q[k].tracked;
+                    if (!(safe_n < batch)) break;                         // ... so this one is lost (:175)
+                    if (q[k].tracked) ++safe_n;
+                    ++kept;
+                    end = head;
+                }
             }
             if (kept) {
                 ranges.push_back(Range{h0, end});
-                last_submit_ms_ = ups[i].now_ms;
+                last_submit = ups[i].now_ms;
             }
         }
     }
     const double t_sim = trace ? now() : 0;
+    {
+        std::unique_lock<std::mutex> g(hm);
+        hcv.wait(g, [&] { return checks_done; });
+    }
+    if (herr || bad < n) {  // nothing applied, nothing queued: the serial loop's first throw
+        helper.join();
+        if (herr) std::rethrow_exception(herr);
+        if (!kref[bad]) throw EngineError(JG_EINVAL, "unknown CRDT uid");
+        throw EngineError(JG_EINVAL, kref[bad]->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
+    }
+    std::vector<std::pair<NetworkProtocol, bool>> oldq = std::move(batch_queue_);
+    batch_queue_.clear();
+    next_seq_ += n;
+    last_submit_ms_ = last_submit;
     // (b) each flush's messages by the workers (flushes are independent): safe states in queue order, then the
     //     non-safe ones compacted per uid (first appearance keeps its place, the last state wins)
     struct Flush { std::vector<QE> msgs; };
@@ -867,8 +953,8 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     tracker.add_many(t_seq.size(), t_seq.data(), t_org.data());
     if (trace) {
         tt[1] = now();
-        std::fprintf(stderr, "SubmitClientUpdates: checks %.1f ms, batcher walk %.1f ms, flushes %.1f ms, tracker adds %.1f ms\n", t_chk - tt[0],
-                     t_sim - t_chk, t_fl - t_sim, tt[1] - t_fl);
+        std::fprintf(stderr, "SubmitClientUpdates: checks %.1f ms (helper), batcher walk %.1f ms, flushes %.1f ms (after the checks), tracker adds %.1f ms\n",
+                     t_chk - tt[0], t_sim - tt[0], t_fl - std::max(t_sim, t_chk), tt[1] - t_fl);
     }
     // 2. Which ops' snapshots are needed: those submitted now or still queued.
     std::vector<uint8_t> need(n, 0);
@@ -888,9 +974,29 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<std::string> snap(n);
     std::vector<std::array<uint8_t, 32>> ssha(n);  // each snapshot's SHA-256, taken where it was encoded
     std::vector<uint8_t> shas(n, 0);
+    helper.join();
+    if (herr) std::rethrow_exception(herr);
+    if (spec.on) {  // a PN-Counter-only batch, applied and encoded by the helper: the kept snapshots become strings
+        const double ts = trace ? now() : 0;
+        parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
+            for (size_t i = b; i < e; ++i) {
+                if (!need[i]) continue;
+                snap[i].assign(reinterpret_cast<const char*>(spec.buf) + spec.off[i], spec.off[i + 1] - spec.off[i]);
+                std::memcpy(ssha[i].data(), spec.sha.data() + 32 * i, 32);
+                shas[i] = 1;
+            }
+        });
+        if (trace) {
+            const double te = now();
+            t_enc_p = te - ts;
+            std::fprintf(stderr, "SubmitClientUpdates: helper's apply + rewind + encode of every snapshot done at +%.1f ms (waited %.1f ms), "
+                         "strings %.1f ms\n", t_spec - tt[0], ts - tt[1], te - ts);
+        }
+        n_chunks = 1;
+    }
     std::vector<uint32_t> round(n, 0);
-    uint32_t n_rounds = 1;
-    {
+    uint32_t n_rounds = spec.on ? 0 : 1;
+    if (!spec.on) {
         std::unordered_map<uint32_t, std::pair<uint32_t, bool>> st;  // OR-Set set -> (its round, a snapshot needed in it)
         for (size_t i = 0; i < n; ++i) {
             if (kpn[i]) continue;

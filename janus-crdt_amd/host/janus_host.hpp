@@ -254,6 +254,9 @@ class GpuStableStore {
     void EncodePNCRowsBefore(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
                              const std::vector<size_t>& at, std::vector<std::string>& out,
                              std::vector<std::array<uint8_t, 32>>* sha = nullptr, std::vector<uint8_t>* has = nullptr);
+    // the encode alone: states in op order in the returned page-locked buffer at off[i] .. off[i + 1], hashes in *sha
+    const uint8_t* EncodePNCRowsRaw(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
+                                    std::vector<uint64_t>& off, std::vector<uint8_t>* sha);
     void DigestsPinned(std::vector<UpdateMessage>& msgs, size_t first);  // ComputeDigests through page-locked staging
     // ComputeDigests from per-payload SHA-256s (sha[i]: payload i of msgs[first..] in order; has[i] = 0: hash it here)
     void DigestsOf(std::vector<UpdateMessage>& msgs, size_t first, std::vector<std::array<uint8_t, 32>>& sha, const std::vector<uint8_t>& has);
