@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define JG_ABI_VERSION 9
+#define JG_ABI_VERSION 10
 
 /* Error codes.  The C# layer maps them to the exceptions the reference throws (B1 "Errors"). */
 #define JG_OK        0
@@ -176,6 +176,14 @@ int jg_pnc_encode_json_before(jg_pnc* pnc, uint64_t n, const uint32_t* key_idx, 
  * dp / dn hold count(need) entries.  ABI v9. */
 int jg_pnc_apply_ops_rewind(jg_pnc* pnc, uint64_t n_ops, const uint32_t* key, uint32_t col, const int64_t* delta, const uint8_t* is_n,
                             const uint8_t* need, int64_t* dp, int64_t* dn);
+/* The whole PN-Counter round in one call (SafeCRDT.cs:39-62 per op: Increment / Decrement on column col, then
+ * GetLastSynchronizedUpdate().Encode()): op i's snapshot — the key's row right after op i, i.e. the row before the
+ * batch plus the key's ops 0..i — into out[off[i], off[i+1]) (and its SHA-256 into sha + 32 i when sha is not
+ * NULL), then every op applied.  The prefixes are a sort + segmented sum on the device; nothing crosses the host
+ * link but the ops, the offsets and the bytes.  JG_ESTATE if off[n] > cap: off filled, NOTHING applied (call
+ * again with a larger out).  ABI v10. */
+int jg_pnc_apply_ops_encode(jg_pnc* pnc, uint64_t n_ops, const uint32_t* key, uint32_t col, const int64_t* delta, const uint8_t* is_n,
+                            uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* sha);
 /* (sha, here and in jg_orset_encode_json: NULL, or n * 32 bytes receiving each encoded state's SHA256 — the hash
  * UpdateMessage.ComputeDigest takes of it, DAGUpdateMessage.cs:43 — computed on the device from the bytes just
  * written; filled only when out is.  The producer path feeds them to jg_update_digests_of.) */

@@ -1327,6 +1327,18 @@ __global__ void k_rewind_scatter(const unsigned long long* __restrict__ sorted, 
     dn[need_pos[i]] = (long long)later[s].n;
 }
 
+// op i's snapshot from the row as it stands BEFORE the batch (jg_pnc_apply_ops_encode): the key's ops up to and
+// including i added to it, i.e. minus the rewind k_encode subtracts.  `excl` is the exclusive segmented sum over the
+// stably sorted (forward) order, `vals` each op's own amount.
+__global__ void k_prefix_scatter(const unsigned long long* __restrict__ sorted, uint64_t n, const PN2* __restrict__ vals,
+                                 const PN2* __restrict__ excl, long long* __restrict__ dp, long long* __restrict__ dn) {
+    const uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t i = (uint32_t)sorted[s];
+    dp[i] = (long long)(0ull - (excl[s].p + vals[s].p));
+    dn[i] = (long long)(0ull - (excl[s].n + vals[s].n));
+}
+
 // jg_pnc_encode_json(_before): length pass, scan, offsets to the host; with `out`, the write pass and its bytes.
 void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, const int64_t* dp, const int64_t* dn, uint64_t* off, uint8_t* out,
                  uint64_t cap, const char* fn, uint8_t* sha = nullptr) {
@@ -1449,6 +1461,89 @@ int jg_pnc_apply_ops_rewind(jg_pnc* p, uint64_t n_ops, const uint32_t* key, uint
         JG_HIP(hipGetLastError());
         JG_HIP(hipMemcpyAsync(dp, ddp, n_need * 8, hipMemcpyDeviceToHost, ctx->stream));
         JG_HIP(hipMemcpyAsync(dn, ddn, n_need * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int jg_pnc_apply_ops_encode(jg_pnc* p, uint64_t n_ops, const uint32_t* key, uint32_t col, const int64_t* delta, const uint8_t* is_n,
+                            uint64_t* off, uint8_t* out, uint64_t cap, uint8_t* sha) {
+    return jg::guard([&] {
+        auto lk_ = jg::lock(p);  // calls on one context are serialised (shared scratch, stream)
+        JG_REQUIRE(p && off, JG_EINVAL, "jg_pnc_apply_ops_encode: NULL argument");
+        jg::require_writable(p, "jg_pnc_apply_ops_encode");
+        off[0] = 0;
+        if (n_ops == 0) return;
+        JG_REQUIRE(key && delta && is_n && out, JG_EINVAL, "jg_pnc_apply_ops_encode: NULL argument");
+        JG_REQUIRE(col < p->R, JG_EINVAL, "jg_pnc_apply_ops_encode: column %u past the store's %u replicas", col, p->R);
+        JG_REQUIRE(n_ops <= 0x7FFFFFFFull, JG_EINVAL, "jg_pnc_apply_ops_encode: at most 2^31-1 ops per call");
+        for (uint64_t i = 0; i < n_ops; ++i)
+            JG_REQUIRE(key[i] < p->n_keys, JG_EINVAL, "jg_pnc_apply_ops_encode: op %llu addresses key %u outside the store",
+                       (unsigned long long)i, key[i]);
+        jg_ctx* ctx = p->ctx;
+        jg::ensure_device(ctx);
+        ensure_table(p);
+        const Table t = table_of(p);
+        using ull = unsigned long long;
+        const uint64_t n = n_ops;
+        auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+        // everything but the sort (scratch3) and the bytes (scratch2) in ctx->scratch, sized once
+        const uint64_t o_del = al(n * 4), o_isn = o_del + al(n * 8), o_k64 = o_isn + al(n), o_val = o_k64 + al(n * 8),
+                       o_exc = o_val + al(n * 16), o_seg = o_exc + al(n * 16), o_dp = o_seg + al(n * 4), o_dn = o_dp + al(n * 8),
+                       o_len = o_dn + al(n * 8), o_off = o_len + al((n + 1) * 8), o_tmp = o_off + al((n + 1) * 8);
+        size_t t_scan = 0, t_sum = 0;
+        JG_HIP(hipcub::DeviceScan::ExclusiveScanByKey(nullptr, t_scan, (const uint32_t*)nullptr, (const PN2*)nullptr, (PN2*)nullptr, PN2Add(),
+                                                      PN2{0, 0}, (int)n, hipcub::Equality(), ctx->stream));
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_sum, (const ull*)nullptr, (ull*)nullptr, (int)(n + 1), ctx->stream));
+        char* a = static_cast<char*>(jg::scratch(ctx, ctx->scratch, o_tmp + std::max(t_scan, t_sum) + 256));
+        auto* dkey = reinterpret_cast<uint32_t*>(a);
+        auto* ddel = reinterpret_cast<long long*>(a + o_del);
+        auto* disn = reinterpret_cast<uint8_t*>(a + o_isn);
+        auto* keys = reinterpret_cast<ull*>(a + o_k64);
+        auto* vals = reinterpret_cast<PN2*>(a + o_val);
+        auto* excl = reinterpret_cast<PN2*>(a + o_exc);
+        auto* seg = reinterpret_cast<uint32_t*>(a + o_seg);
+        auto* ddp = reinterpret_cast<long long*>(a + o_dp);
+        auto* ddn = reinterpret_cast<long long*>(a + o_dn);
+        auto* len = reinterpret_cast<ull*>(a + o_len);
+        auto* doff = reinterpret_cast<ull*>(a + o_off);
+        void* tmp = a + o_tmp;
+        JG_HIP(hipMemcpyAsync(dkey, key, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(ddel, delta, n * 8, hipMemcpyHostToDevice, ctx->stream));
+        JG_HIP(hipMemcpyAsync(disn, is_n, n, hipMemcpyHostToDevice, ctx->stream));
+        // each op's amounts up to and including it, per key (forward keys: a stable sort keeps op order per key)
+        const unsigned g = blocks_for(n);
+        hipLaunchKernelGGL(k_make_keys, dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, keys);
+        JG_HIP(hipGetLastError());
+        const ull* sorted = sort_keys(ctx, keys, n, p->n_keys);
+        hipLaunchKernelGGL(k_rewind_vals, dim3(g), dim3(kBlock), 0, ctx->stream, sorted, n, ddel, disn, p->eb, vals, seg);
+        JG_HIP(hipGetLastError());
+        size_t tt = t_scan;
+        JG_HIP(hipcub::DeviceScan::ExclusiveScanByKey(tmp, tt, seg, vals, excl, PN2Add(), PN2{0, 0}, (int)n, hipcub::Equality(), ctx->stream));
+        hipLaunchKernelGGL(k_prefix_scatter, dim3(g), dim3(kBlock), 0, ctx->stream, sorted, n, vals, excl, ddp, ddn);
+        JG_HIP(hipGetLastError());
+        // the snapshots' lengths from the rows as they stand (nothing applied yet), their offsets to the host
+        if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, len, nullptr, col, ddp, ddn);
+        else hipLaunchKernelGGL((k_encode<4, 0>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, len, nullptr, col, ddp, ddn);
+        JG_HIP(hipGetLastError());
+        JG_HIP(hipMemsetAsync(len + n, 0, 8, ctx->stream));
+        tt = t_sum;
+        JG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tt, len, doff, (int)(n + 1), ctx->stream));
+        JG_HIP(hipMemcpyAsync(off, doff, (n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        JG_HIP(hipStreamSynchronize(ctx->stream));
+        JG_REQUIRE(off[n] <= cap, JG_ESTATE, "jg_pnc_apply_ops_encode: %llu bytes exceed cap %llu (nothing applied)", (unsigned long long)off[n],
+                   (unsigned long long)cap);
+        // the bytes, then the ops (stream order: the write pass reads the rows before the adds land), the hashes
+        auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
+        if (p->eb == 8) {
+            hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+            hipLaunchKernelGGL(k_apply_ops_col<8>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
+        } else {
+            hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+            hipLaunchKernelGGL(k_apply_ops_col<4>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
+        }
+        JG_HIP(hipGetLastError());
+        if (sha) jg::sha256_device(ctx, dout, reinterpret_cast<const uint64_t*>(doff), n, sha);
+        JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
         JG_HIP(hipStreamSynchronize(ctx->stream));
     });
 }

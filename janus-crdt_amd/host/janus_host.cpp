@@ -14,6 +14,7 @@
 #include <future>
 #include <unordered_set>
 #include <mutex>
+#include <string_view>
 #include <thread>
 
 #include "host_pool.hpp"
@@ -44,6 +45,8 @@ GpuStableStore::GpuStableStore(int device, uint32_t max_keys, uint32_t replicas,
 GpuStableStore::~GpuStableStore() {
     if (p_bytes_) jg_host_free(p_bytes_);
     if (pin_buf_) jg_host_free(pin_buf_);
+    if (pin_aux_) jg_host_free(pin_aux_);
+    for (uint8_t* b : pin_more_) jg_host_free(b);
     if (node_) jg_node_destroy(node_);
     if (orset_) jg_orset_destroy(orset_);
     if (pnc_) jg_pnc_destroy(pnc_);
@@ -632,6 +635,66 @@ uint8_t* GpuStableStore::pinned_buf(size_t bytes) {
     return pin_buf_;
 }
 
+uint8_t* GpuStableStore::pinned_aux(size_t bytes) {
+    if (pin_aux_cap_ < bytes) {
+        if (pin_aux_) check(jg_host_free(pin_aux_));
+        pin_aux_ = nullptr;
+        void* p = nullptr;
+        pin_aux_cap_ = bytes + bytes / 4 + 4096;
+        check(jg_host_alloc(ctx_, pin_aux_cap_, &p));
+        pin_aux_ = static_cast<uint8_t*>(p);
+    }
+    return pin_aux_;
+}
+
+// jg_pnc_apply_ops_encode over consecutive chunks of ops, into page-locked memory: chunk c's states at cbuf[c] (in
+// pinned_buf, or a block of its own when the states outgrew the buffer's guess), their offsets at off + start[c] + c
+// (chunk-relative, n_c + 1 of them) and their SHA-256s at sha + 32 start[c]; on_chunk(c) after each.  Calls in op
+// order give what one call would (each chunk's prefixes start from the rows the chunks before it left).  A chunk
+// refused for room (JG_ESTATE: nothing of it applied) goes again into a buffer of the size it reported.
+void GpuStableStore::ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
+                                    const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
+                                    const std::function<void(size_t)>& on_chunk) {
+    const size_t K = start.size() - 1, n = start[K];
+    for (uint8_t* b : pin_more_) check(jg_host_free(b));
+    pin_more_.clear();
+    uint8_t* aux = pinned_aux((n + K) * 8 + 32 * n + 64);
+    auto* o = reinterpret_cast<uint64_t*>(aux);
+    uint8_t* h = aux + (n + K) * 8;
+    off = o;
+    sha = h;
+    cbuf.assign(K, nullptr);
+    uint8_t* buf = pinned_buf(std::max<size_t>(pin_cap_, (size_t)(n * (last_pnc_bytes_ + 8)) + 4096));
+    size_t cap = pin_cap_, base = 0, total = 0;
+    for (size_t c = 0; c < K; ++c) {
+        const size_t s0 = start[c], m = start[c + 1] - s0;
+        uint64_t* oc = o + s0 + c;
+        auto call = [&] { return jg_pnc_apply_ops_encode(pnc_, m, rows + s0, 0, delta + s0, isn + s0, oc, buf + base, cap - base, h + 32 * s0); };
+        int rc = call();
+        if (rc == JG_ESTATE && oc[m] > cap - base) {
+            if (c == 0) {  // nothing read from the buffer yet: grow it
+                buf = pinned_buf(oc[m] + (n - m) * (oc[m] / std::max<size_t>(m, 1) + 8));
+                cap = pin_cap_;
+            } else {       // earlier chunks live in it: the rest goes to a block of its own
+                void* p = nullptr;
+                const size_t want = oc[m] + (n - start[c + 1]) * (oc[m] / m + 8) + 4096;
+                check(jg_host_alloc(ctx_, want, &p));
+                pin_more_.push_back(static_cast<uint8_t*>(p));
+                buf = static_cast<uint8_t*>(p);
+                cap = want;
+            }
+            base = 0;
+            rc = call();
+        }
+        check(rc);
+        cbuf[c] = buf + base;
+        base += (oc[m] + 63) & ~size_t(63);
+        total += oc[m];
+        on_chunk(c);
+    }
+    if (n) last_pnc_bytes_ = (double)total / (double)n;
+}
+
 const uint8_t* GpuStableStore::EncodePNCRowsRaw(const std::vector<uint32_t>& rows, const std::vector<int64_t>& dp, const std::vector<int64_t>& dn,
                                                 std::vector<uint64_t>& off, std::vector<uint8_t>* sha) {
     const size_t n = rows.size();
@@ -780,11 +843,11 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     size_t n_chunks = 0;
     // Round 6: three things overlap.  A helper thread runs the wrappers' checks on the workers (every op's key resolved,
     // read-only) while this thread walks the batcher over message identities (serial, nothing committed until the
-    // checks pass); then, for a batch of PN-Counter ops only (one round), the helper applies them, computes every
-    // snapshot's rewind and encodes ALL of them on the device (jg_pnc_apply_ops_rewind + jg_pnc_encode_json_before:
-    // library calls, no workers) while this thread computes the flushes and the tracker adds on the workers.  Only
-    // the snapshots the batcher keeps become strings.  A failing check still raises before anything is applied or
-    // queued, as the serial loop would.
+    // checks pass); then, for a batch of PN-Counter ops only (one round), the helper encodes EVERY op's snapshot and
+    // applies the ops in one library call (jg_pnc_apply_ops_encode: per-key prefixes, encode and apply on the device,
+    // no workers) while this thread computes the flushes and the tracker adds on the workers.  Only the snapshots
+    // the batcher keeps become strings, where the messages are built.  A failing check still raises before anything
+    // is applied or queued, as the serial loop would.
     std::vector<const KeyRef*> kref(n);
     // each op's key as plain arrays: the serial walks below would chase every KeyRef through the uid map's nodes
     std::vector<uint32_t> krow(n);
@@ -792,57 +855,83 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<size_t> first_bad(pool().size(), n);
     ensure_uid_index();
     flush_registrations();  // (the helper's encode needs every registered row's columns on the device)
-    struct Spec {  // the helper's device results for a PN-Counter-only batch
-        bool on = false;
-        std::vector<int64_t> dp, dn;
-        std::vector<uint64_t> off;
-        std::vector<uint8_t> sha;
-        const uint8_t* buf = nullptr;
+    struct Spec {  // the helper's device results for a PN-Counter-only batch (page-locked, ApplyEncodePNC)
+        bool on = false;           // set with checks_done
+        size_t done = 0;           // chunks encoded and applied (under hm)
+        std::vector<size_t> start; // chunk c = ops [start[c], start[c + 1])
+        std::vector<const uint8_t*> cbuf;
+        const uint64_t* off = nullptr;
+        const uint8_t* sha = nullptr;
+        size_t clen = 1;
+        std::string_view state(size_t i) const {  // op i's snapshot
+            const size_t c = std::min(i / clen, start.size() - 2);
+            const uint64_t* o = off + i + c;
+            return {reinterpret_cast<const char*>(cbuf[c]) + o[0], (size_t)(o[1] - o[0])};
+        }
     } spec;
+    std::vector<int64_t> delta(n);  // each op's amount at the store's width, 1: a Decrement (the check pass fills them)
+    std::vector<uint8_t> isn(n);
+    std::vector<uint8_t> saw_set(pool().size(), 0);
     std::mutex hm;
     std::condition_variable hcv;
     bool checks_done = false;
     size_t bad = n;
     std::exception_ptr herr;
-    double t_chk = 0, t_spec = 0;
+    double t_chk = 0;
+    std::vector<double> t_chunk;
     std::thread helper([&] {
         try {
             parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
                 constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
                 for (size_t i = b; i < std::min(e, b + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
+                uint8_t set_seen = 0;  // (one store per range: the workers' flags share a cache line)
+                struct Put {
+                    uint8_t& to;
+                    uint8_t& v;
+                    ~Put() { to = v; }
+                } put{saw_set[t], set_seen};
                 for (size_t i = b; i < e; ++i) {
                     if (i + kAhead < e) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
-                    const KeyRef* kr = find_uid(ups[i].op.uid);
+                    const ClientOp& op = ups[i].op;
+                    const KeyRef* kr = find_uid(op.uid);
                     kref[i] = kr;
-                    if (kr) krow[i] = kr->idx, kpn[i] = kr->type == CrdtType::PNCounter ? 1 : 0;
-                    if (!kr || ups[i].op.opId < 1 || ups[i].op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
+                    if (kr) {
+                        const bool pn = kr->type == CrdtType::PNCounter;
+                        krow[i] = kr->idx, kpn[i] = pn ? 1 : 0;
+                        set_seen |= pn ? 0 : 1;
+                        delta[i] = eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount;
+                        isn[i] = op.opId == 2 ? 1 : 0;
+                    }
+                    if (!kr || op.opId < 1 || op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
                         first_bad[t] = i;
                         return;
                     }
                 }
             });
             const size_t b = *std::min_element(first_bad.begin(), first_bad.end());
-            const bool pnc_only = b == n && n > 0 && std::all_of(kpn.begin(), kpn.end(), [](uint8_t x) { return x != 0; });
+            const bool pnc_only = b == n && n > 0 && std::all_of(saw_set.begin(), saw_set.end(), [](uint8_t x) { return x == 0; });
+            if (pnc_only) {  // chunks of ops, so the messages of the first are built while the next is encoded
+                const size_t K = n >= (size_t(1) << 18) ? 4 : 1;
+                spec.clen = (n + K - 1) / K;
+                for (size_t c = 0; c <= K; ++c) spec.start.push_back(std::min(n, c * spec.clen));
+            }
             {
                 std::lock_guard<std::mutex> g(hm);
                 bad = b;
+                spec.on = pnc_only;
                 checks_done = true;
                 t_chk = trace ? now() : 0;
             }
             hcv.notify_all();
             if (!pnc_only) return;
-            std::vector<int64_t> delta(n);
-            std::vector<uint8_t> isn(n), all(n, 1);
-            for (size_t i = 0; i < n; ++i) {
-                delta[i] = eb_ == 4 ? (int64_t)(int32_t)ups[i].op.amount : ups[i].op.amount;
-                isn[i] = ups[i].op.opId == 2 ? 1 : 0;
-            }
-            spec.dp.resize(n);
-            spec.dn.resize(n);
-            check(jg_pnc_apply_ops_rewind(pnc_, n, krow.data(), 0, delta.data(), isn.data(), all.data(), spec.dp.data(), spec.dn.data()));
-            spec.buf = EncodePNCRowsRaw(krow, spec.dp, spec.dn, spec.off, &spec.sha);
-            spec.on = true;
-            t_spec = trace ? now() : 0;
+            ApplyEncodePNC(krow.data(), delta.data(), isn.data(), spec.start, spec.off, spec.sha, spec.cbuf, [&](size_t c) {
+                {
+                    std::lock_guard<std::mutex> g(hm);
+                    spec.done = c + 1;
+                    if (trace) t_chunk.push_back(now());
+                }
+                hcv.notify_all();
+            });
         } catch (...) {
             std::lock_guard<std::mutex> g(hm);
             herr = std::current_exception();
@@ -957,12 +1046,15 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                      t_chk - tt[0], t_sim - tt[0], t_fl - std::max(t_sim, t_chk), tt[1] - t_fl);
     }
     // 2. Which ops' snapshots are needed: those submitted now or still queued.
-    std::vector<uint8_t> need(n, 0);
-    for (const Flush& f : flushes)
-        for (const auto& e : f.msgs)
-            if (e.op != kOld) need[(size_t)e.op] = 1;
-    for (size_t j = head; j < q.size(); ++j)
-        if (q[j].op != kOld) need[(size_t)q[j].op] = 1;
+    //    (A PN-Counter-only batch encodes every op's: the helper is at it already.)
+    std::vector<uint8_t> need(spec.on ? 0 : n, 0);
+    if (!spec.on) {
+        for (const Flush& f : flushes)
+            for (const auto& e : f.msgs)
+                if (e.op != kOld) need[(size_t)e.op] = 1;
+        for (size_t j = head; j < q.size(); ++j)
+            if (q[j].op != kOld) need[(size_t)q[j].op] = 1;
+    }
     // 3. Apply the ops in rounds, encode the needed snapshots after each round (on the device).  A PN-Counter
     //    snapshot is the row rewound by the amounts the batch's later ops on that key added to the own column
     //    (jg_pnc_encode_json_before); an OR-Set snapshot is its set's records below the ord limits the apply
@@ -971,29 +1063,17 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     //    op's round is the number of such Clears of its own set before it (per-set order kept), and every PN-Counter
     //    op runs in round 0.
     std::vector<uint8_t> result(n, 1);
-    std::vector<std::string> snap(n);
-    std::vector<std::array<uint8_t, 32>> ssha(n);  // each snapshot's SHA-256, taken where it was encoded
-    std::vector<uint8_t> shas(n, 0);
-    helper.join();
-    if (herr) std::rethrow_exception(herr);
-    if (spec.on) {  // a PN-Counter-only batch, applied and encoded by the helper: the kept snapshots become strings
-        const double ts = trace ? now() : 0;
-        parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
-            for (size_t i = b; i < e; ++i) {
-                if (!need[i]) continue;
-                snap[i].assign(reinterpret_cast<const char*>(spec.buf) + spec.off[i], spec.off[i + 1] - spec.off[i]);
-                std::memcpy(ssha[i].data(), spec.sha.data() + 32 * i, 32);
-                shas[i] = 1;
-            }
-        });
-        if (trace) {
-            const double te = now();
-            t_enc_p = te - ts;
-            std::fprintf(stderr, "SubmitClientUpdates: helper's apply + rewind + encode of every snapshot done at +%.1f ms (waited %.1f ms), "
-                         "strings %.1f ms\n", t_spec - tt[0], ts - tt[1], te - ts);
-        }
-        n_chunks = 1;
+    if (!spec.on) {  // (the helper ended with the checks)
+        helper.join();
+        if (herr) std::rethrow_exception(herr);
     }
+    // A PN-Counter-only batch is applied and encoded by the helper, chunk by chunk: its snapshots stay in page-locked
+    // memory and become the messages' strings where the messages are built (step 4), each flush as soon as the
+    // chunks holding its ops are done.
+    std::vector<std::string> snap(spec.on ? 0 : n);
+    std::vector<std::array<uint8_t, 32>> ssha(spec.on ? 0 : n);  // each snapshot's SHA-256, taken where it was encoded
+    std::vector<uint8_t> shas(spec.on ? 0 : n, 0);
+    if (spec.on) n_chunks = spec.start.size() - 1;
     std::vector<uint32_t> round(n, 0);
     uint32_t n_rounds = spec.on ? 0 : 1;
     if (!spec.on) {
@@ -1108,7 +1188,11 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         np.uid = ups[(size_t)e.op].op.uid;
         np.syncMsgType = NetworkProtocol::CRDTMsg;
         np.seq = seq0 + (uint64_t)e.op;
-        np.message = std::move(snap[(size_t)e.op]);
+        if (spec.on) {
+            np.message.assign(spec.state((size_t)e.op));
+        } else {
+            np.message = std::move(snap[(size_t)e.op]);
+        }
         return np;
     };
     std::vector<size_t> mo(flushes.size() + 1, 0);  // first payload of each new UpdateMessage
@@ -1116,17 +1200,51 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<std::array<uint8_t, 32>> msha(mo.back());  // per submitted payload, in UpdateMessage order
     std::vector<uint8_t> mhas(mo.back(), 0);
     submitted.resize(s0 + flushes.size());
-    parallel_ranges(pool(), flushes.size(), [&](size_t fb, size_t fe, int) {
-        for (size_t f = fb; f < fe; ++f) {
-            UpdateMessage& um = submitted[s0 + f];
-            um.update.reserve(flushes[f].msgs.size());
-            for (size_t j = 0; j < flushes[f].msgs.size(); ++j) {
-                const QE& e = flushes[f].msgs[j];
-                if (e.op != kOld && shas[(size_t)e.op]) msha[mo[f] + j] = ssha[(size_t)e.op], mhas[mo[f] + j] = 1;
-                um.update.push_back(make_np(e));
+    auto build = [&](size_t f0, size_t f1) {  // the UpdateMessages of flushes [f0, f1)
+        parallel_ranges(pool(), f1 - f0, [&](size_t fb, size_t fe, int) {
+            for (size_t f = f0 + fb; f < f0 + fe; ++f) {
+                UpdateMessage& um = submitted[s0 + f];
+                um.update.reserve(flushes[f].msgs.size());
+                for (size_t j = 0; j < flushes[f].msgs.size(); ++j) {
+                    const QE& e = flushes[f].msgs[j];
+                    if (e.op != kOld && spec.on) {
+                        std::memcpy(msha[mo[f] + j].data(), spec.sha + 32 * (size_t)e.op, 32);
+                        mhas[mo[f] + j] = 1;
+                    } else if (e.op != kOld && shas[(size_t)e.op]) {
+                        msha[mo[f] + j] = ssha[(size_t)e.op], mhas[mo[f] + j] = 1;
+                    }
+                    um.update.push_back(make_np(e));
+                }
             }
+        }, 8);
+    };
+    if (spec.on) {
+        const int64_t nold = (int64_t)oldq.size();
+        size_t f0 = 0;
+        for (size_t c = 1; c < spec.start.size(); ++c) {
+            {
+                std::unique_lock<std::mutex> g(hm);
+                hcv.wait(g, [&] { return spec.done >= c || herr; });
+            }
+            if (herr) break;  // (a device failure part way: rethrown below)
+            const int64_t lim = (int64_t)spec.start[c];  // ops below it are encoded and applied
+            size_t f1 = f0;
+            while (f1 < flushes.size() && (int64_t)ranges[f1].h1 - 1 - nold < lim) ++f1;
+            build(f0, f1);
+            f0 = f1;
         }
-    }, 32);
+        helper.join();
+        if (herr) std::rethrow_exception(herr);
+        build(f0, flushes.size());
+        if (trace) {
+            std::string ct;
+            for (double t : t_chunk) ct += " +" + std::to_string(t - tt[0]).substr(0, 5);
+            std::fprintf(stderr, "SubmitClientUpdates: helper's chunks (apply + encode + hashes) done at%s ms; all messages built at +%.1f ms\n",
+                         ct.c_str(), now() - tt[0]);
+        }
+    } else {
+        build(0, flushes.size());
+    }
     if (trace) tt[3] = now();
     DigestsOf(submitted, s0, msha, mhas);
     if (trace) tt[4] = now();

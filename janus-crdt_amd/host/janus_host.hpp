@@ -24,6 +24,7 @@
 #include <array>
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <optional>
 #include <stdexcept>
@@ -261,8 +262,15 @@ class GpuStableStore {
     // ComputeDigests from per-payload SHA-256s (sha[i]: payload i of msgs[first..] in order; has[i] = 0: hash it here)
     void DigestsOf(std::vector<UpdateMessage>& msgs, size_t first, std::vector<std::array<uint8_t, 32>>& sha, const std::vector<uint8_t>& has);
     uint8_t* pinned_buf(size_t bytes);  // a page-locked buffer of at least `bytes`, kept across calls
+    uint8_t* pinned_aux(size_t bytes);  // a second one (offsets, hashes beside pinned_buf's bytes)
+    void ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
+                        const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
+                        const std::function<void(size_t)>& on_chunk);
+    std::vector<uint8_t*> pin_more_;  // ApplyEncodePNC's extra page-locked blocks (states past pinned_buf's guess)
     uint8_t* pin_buf_ = nullptr;
     size_t pin_cap_ = 0;
+    uint8_t* pin_aux_ = nullptr;
+    size_t pin_aux_cap_ = 0;
     double last_pnc_bytes_ = 400;
     std::unordered_map<Guid, KeyRef, GuidHash> uids_;
     // A flat open-addressing copy of uids_ for the producer path's per-op lookups (one 32-byte slot per probe,

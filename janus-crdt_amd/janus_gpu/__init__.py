@@ -31,7 +31,7 @@ EXPORTS = [
     "jg_pnc_intern", "jg_pnc_columns", "jg_pnc_merge_json",
     "jg_wave_create", "jg_wave_destroy", "jg_wave_upload", "jg_pnc_merge_wave", "jg_host_alloc", "jg_host_free",
     "jg_pnc_wave_begin", "jg_pnc_wave_append", "jg_pnc_wave_commit", "jg_pnc_wave_abort",
-    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before", "jg_pnc_apply_ops_rewind", "jg_orset_encode_json", "jg_orset_apply_ops_ords",
+    "jg_orset_lookup_all", "jg_pnc_encode_json", "jg_pnc_encode_json_before", "jg_pnc_apply_ops_rewind", "jg_pnc_apply_ops_encode", "jg_orset_encode_json", "jg_orset_apply_ops_ords",
     "jg_rows_route", "jg_pnc_merge_device", "jg_orset_route", "jg_orset_merge_device", "jg_orset_read_sets",
     "jg_orset_names_sync", "jg_orset_wave_begin", "jg_orset_wave_append", "jg_orset_wave_check", "jg_orset_wave_commit",
     "jg_orset_wave_abort", "jg_orset_wave_names", "jg_orset_names_since", "jg_orset_merge_json",
@@ -101,6 +101,7 @@ _SIGS = {
     "jg_pnc_encode_json": ([_vp, _u64, _vp, _vp, _vp, _u64], C.c_int),
     "jg_pnc_encode_json_before": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
     "jg_pnc_apply_ops_rewind": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _vp], C.c_int),
+    "jg_pnc_apply_ops_encode": ([_vp, _u64, _vp, C.c_uint32, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
     "jg_orset_encode_json": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _u64, _vp], C.c_int),
     "jg_orset_apply_ops_ords": ([_vp, _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], C.c_int),
     "jg_rows_route": ([_vp, _u32, _vp, _vp, _vp, _vp, _u64], C.c_int),
@@ -391,6 +392,25 @@ class PNCStore:
         dp, dn = np.zeros(max(1, k), np.int64), np.zeros(max(1, k), np.int64)
         _check(load().jg_pnc_apply_ops_rewind(self._h, key.size, _ptr(key), col, _ptr(delta), _ptr(is_n), _ptr(need), _ptr(dp), _ptr(dn)))
         return dp[:k], dn[:k]
+
+    def apply_ops_encode(self, key, delta, is_n, col=0, cap=None):
+        """jg_pnc_apply_ops_encode: op i's snapshot (the key's row right after op i) for every op, as bytes, with
+        its SHA-256 (u8[n, 32]); the ops applied.  `cap` (bytes) forces a small output buffer (JG_ESTATE: nothing
+        applied)."""
+        key, delta, is_n = _arr(key, np.uint32), _arr(delta, np.int64), _arr(is_n, np.uint8)
+        n = key.size
+        off = np.zeros(n + 1, np.uint64)
+        out = np.empty(max(16, n * 512 if cap is None else cap), np.uint8)
+        h = np.zeros((max(1, n), 32), np.uint8)
+        call = lambda: load().jg_pnc_apply_ops_encode(self._h, n, _ptr(key), col, _ptr(delta), _ptr(is_n), _ptr(off), _ptr(out),
+                                                      out.size if cap is None else cap, _ptr(h))
+        rc = call()
+        if rc == JG_ESTATE and cap is None and int(off[-1]) > out.size:  # nothing applied: again with room for every byte
+            out = np.empty(int(off[-1]), np.uint8)
+            rc = call()
+        _check(rc)
+        b = out[:int(off[-1])].tobytes()
+        return [b[int(off[i]):int(off[i + 1])] for i in range(n)], h[:n]
 
     def encode_json_before(self, key_idx, dp, dn, col=0, sha=False):
         """jg_pnc_encode_json_before: each row as it stood before its last dp[i] / dn[i] of increments to `col`

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
     lib = ctypes.CDLL(str(jg.LIB_PATH))
     for name in header_functions():
         assert hasattr(lib, name), name
-    assert lib.jg_abi_version() == 9  # v9: jg_pnc_apply_ops_rewind; v8: jg_sha256_batch, jg_update_digests_of; v7: jg_orset_encode_json, jg_orset_apply_ops_ords, jg_pnc_encode_json_before (v6: jg_orset_names_since;
+    assert lib.jg_abi_version() == 10  # v10: jg_pnc_apply_ops_encode; v9: jg_pnc_apply_ops_rewind; v8: jg_sha256_batch, jg_update_digests_of; v7: jg_orset_encode_json, jg_orset_apply_ops_ords, jg_pnc_encode_json_before (v6: jg_orset_names_since;
     # v5: jg_apply_stats gains setup_s and loop_s; v4: the RCCL exchange)
 
 

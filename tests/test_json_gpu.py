@@ -634,6 +634,59 @@ def test_encode_before_matches_oracle_encoder(ctx, eb):
 
 
 @pytest.mark.parametrize("eb", [4, 8])
+@pytest.mark.parametrize("n_keys,n_ops,merged", [(50, 1500, True), (200000, 100000, False), (3, 1, False)])
+def test_apply_ops_encode_matches_oracle(ctx, eb, n_keys, n_ops, merged):
+    """jg_pnc_apply_ops_encode (round 6): a batch of own-column Increment / Decrement ops (PNCounters.cs:96-112) and
+    the snapshot each op shipped (SafeCRDT.cs:39-62: the key's row right after the op) in ONE call — every snapshot
+    equals the oracle's encoder over the row walked op by op (replica columns merged in first, amounts across the
+    int32 / int64 edge), each hash is SHA-256 of its bytes, and the store then holds every op's amount.  An output
+    buffer too small is refused with JG_ESTATE and NOTHING applied."""
+    rng = np.random.default_rng(3 * eb + n_ops)
+    R = 8
+    stable = random_guids(rng, n_keys)
+    pr = Pair(ctx, n_keys, R, eb, stable)
+    if merged:  # rows with several replica columns
+        cl = Cluster(rng, n_keys, 6, eb, stable)
+        mk = rng.integers(0, n_keys, 1500).astype(np.uint32)
+        msgs = [cl.message(int(k)) for k in mk]
+        pr.oracle(mk, msgs)
+        pr.s.merge_json(mk, msgs)
+    hot = rng.integers(0, n_keys, max(1, n_keys // 10))
+    key = np.where(rng.random(n_ops) < 0.5, rng.choice(hot, n_ops), rng.integers(0, n_keys, n_ops)).astype(np.uint32)
+    delta = rng.integers(1, 1000, n_ops).astype(np.int64)
+    delta[rng.random(n_ops) < 0.02] = 2**31 - 3  # past the int32 edge once summed
+    if eb == 8:
+        delta[rng.random(n_ops) < 0.01] = 2**62
+    is_n = (rng.random(n_ops) < 0.3).astype(np.uint8)
+    P0, N0 = pr.s.read_rows()
+    with pytest.raises(jg.JanusError):
+        pr.s.apply_ops_encode(key, delta, is_n, cap=16)
+    P1, N1 = pr.s.read_rows()
+    assert np.array_equal(P0, P1) and np.array_equal(N0, N1), "a refused call applied ops"
+    got, h = pr.s.apply_ops_encode(key, delta, is_n)
+    assert len(got) == n_ops
+    bits = 32 if eb == 4 else 64
+
+    def wrap(x):
+        x = int(x) % (1 << bits)
+        return x - (1 << bits) if x >= 1 << (bits - 1) else x
+    P, N = pr.P.astype(object), pr.N.astype(object)
+    for i in range(n_ops):
+        k = int(key[i])
+        M = N if is_n[i] else P
+        M[k, 0] = wrap(M[k, 0] + int(delta[i]))
+        c = int(pr.ncols[k])
+        exp = orc.json_encode_pnc(pr.cols[k, :c]["lo"], pr.cols[k, :c]["hi"], np.array(P[k, :c], dtype=pr.P.dtype),
+                                  np.array(N[k, :c], dtype=pr.N.dtype), eb)
+        assert got[i] == exp, f"op {i} key {k}"
+    sample = range(n_ops) if n_ops <= 5000 else rng.integers(0, n_ops, 5000)
+    assert all(h[i].tobytes() == hashlib.sha256(got[i]).digest() for i in sample)
+    pr.P, pr.N = np.array(P, dtype=pr.P.dtype), np.array(N, dtype=pr.N.dtype)
+    pr.check()
+    pr.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
 @pytest.mark.parametrize("n_keys,n_ops", [(40, 3000), (200000, 100000), (3, 1)])
 def test_apply_ops_rewind_matches_walk(ctx, eb, n_keys, n_ops):
     """jg_pnc_apply_ops_rewind (round 6): a batch of own-column Increment / Decrement ops (PNCounters.cs:96-112)
