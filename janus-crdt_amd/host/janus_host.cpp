@@ -469,7 +469,7 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
     return done;
 }
 
-std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
+std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
                                               const KeyRef* const* refs) {
     const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3;
     materialize_names();
@@ -485,11 +485,11 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
     if (!refs) {
         found.resize(ops.size());
         for (size_t i = 0; i < ops.size(); ++i) {  // validate everything first: no partial application
-            const auto it = uids_.find(ops[i].uid);
+            const auto it = uids_.find(ops[i]->uid);
             if (it == uids_.end()) throw EngineError(JG_EINVAL, "unknown CRDT uid");
             const KeyRef* kr = &it->second;
             const int hi = kr->type == CrdtType::PNCounter ? 2 : 3;
-            if (ops[i].opId < 1 || ops[i].opId > hi)
+            if (ops[i]->opId < 1 || ops[i]->opId > hi)
                 throw EngineError(JG_EINVAL, kr->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
             found[i] = kr;
         }
@@ -505,7 +505,7 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
         for (size_t i = 0; i < ops.size(); ++i)
             if (refs[i]->type == CrdtType::ORSet) {
                 ors.push_back(i);
-                if (ops[i].opId != 2) (void)pending_names_[refs[i]->idx];
+                if (ops[i]->opId != 2) (void)pending_names_[refs[i]->idx];
             }
         const size_t T = (size_t)std::max(1, pool().size());
         std::vector<std::string> err(T);
@@ -515,7 +515,7 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
                     for (size_t i : ors) {
                         const uint32_t set = refs[i]->idx;
                         if (set % T != t) continue;
-                        const ClientOp& op = ops[i];
+                        const ClientOp& op = *ops[i];
                         SetKey& sk = sets_[set];
                         if (op.opId == 3) {
                             sk.elems.clear();
@@ -538,7 +538,7 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<ClientOp>& ops, 
             if (!e.empty()) throw EngineError(JG_ESTATE, e);
     }
     for (size_t i = 0; i < ops.size(); ++i) {
-        const ClientOp& op = ops[i];
+        const ClientOp& op = *ops[i];
         const KeyRef& kr = *refs[i];
         if (kr.type == CrdtType::PNCounter) {
             pkey.push_back(kr.idx);
@@ -806,30 +806,53 @@ std::vector<std::string> GpuStableStore::EncodePNCStatesBefore(const std::vector
 
 std::vector<std::string> GpuStableStore::EncodeORSetStates(const std::vector<Guid>& uids, const std::vector<uint64_t>* add_lim,
                                                            const std::vector<uint64_t>* rem_lim, std::vector<std::array<uint8_t, 32>>* sha) {
-    flush_names();  // every element this mirror interned is in the engine's element table
     std::vector<uint32_t> sets;
     sets.reserve(uids.size());
     for (const Guid& u : uids) sets.push_back(ref(u, CrdtType::ORSet).idx);
     const size_t n = sets.size();
+    std::vector<size_t> at(n);
+    for (size_t i = 0; i < n; ++i) at[i] = i;
+    std::vector<std::string> out(n);
+    std::vector<uint8_t> has;
+    if (sha) sha->resize(n), has.resize(n);
+    EncodeORSetSets(sets, add_lim, rem_lim, at, out, sha, sha ? &has : nullptr);
+    return out;
+}
+
+// ORSetMsg.Encode() of sets[i] (at its ord limits when given) into out[at[i]] (and its SHA-256 into (*sha)[at[i]],
+// (*has)[at[i]] = 1): one jg_orset_encode_json into a page-locked buffer kept across calls (a second only if the
+// states outgrow it), the strings built by the workers
+void GpuStableStore::EncodeORSetSets(const std::vector<uint32_t>& sets, const std::vector<uint64_t>* add_lim, const std::vector<uint64_t>* rem_lim,
+                                     const std::vector<size_t>& at, std::vector<std::string>& out, std::vector<std::array<uint8_t, 32>>* sha,
+                                     std::vector<uint8_t>* has) {
+    static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t0 = trace ? now() : 0;
+    flush_names();  // every element this mirror interned is in the engine's element table
+    const double t1 = trace ? now() : 0;
+    const size_t n = sets.size();
     std::vector<uint64_t> off(n + 1, 0);
     const uint64_t* al = add_lim ? add_lim->data() : nullptr;
     const uint64_t* rl = rem_lim ? rem_lim->data() : nullptr;
-    // ORSetMsg.Encode() on the device (jg_orset_encode_json) into a page-locked buffer kept across calls: one call
-    // unless the states outgrow it
     uint8_t* buf = pinned_buf(4096);
-    if (sha) sha->resize(n);  // each state's SHA-256, hashed on the device as it is encoded
-    uint8_t* hs = sha ? reinterpret_cast<uint8_t*>(sha->data()) : nullptr;
+    std::vector<uint8_t> h(sha ? 32 * n : 0);  // each state's SHA-256, hashed on the device as it is encoded
+    uint8_t* hs = sha ? h.data() : nullptr;
     int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
     if (rc == JG_ESTATE && off[n] > pin_cap_) {
         buf = pinned_buf(off[n]);
         rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
     }
     check(rc);
-    std::vector<std::string> out(n);
+    const double t2 = trace ? now() : 0;
     parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
-        for (size_t i = b; i < e; ++i) out[i].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+        for (size_t i = b; i < e; ++i) {
+            out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
+            if (sha) std::memcpy((*sha)[at[i]].data(), h.data() + 32 * i, 32), (*has)[at[i]] = 1;
+        }
     });
-    return out;
+    if (trace)
+        std::fprintf(stderr, "EncodeORSetSets(%zu, %.1f MB): names %.1f ms, encode %.1f ms, strings %.1f ms\n", n, off[n] / 1e6, t1 - t0, t2 - t1,
+                     now() - t2);
 }
 
 std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize,
@@ -1087,14 +1110,23 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             n_rounds = std::max(n_rounds, e.first + 1);
         }
     }
+    // each round's ops in op order, in one pass (a counting sort on the round)
+    std::vector<size_t> rbeg(n_rounds + 1, 0), rops(spec.on ? 0 : n);
+    if (!spec.on) {
+        for (size_t i = 0; i < n; ++i) ++rbeg[round[i] + 1];
+        for (uint32_t rd = 0; rd < n_rounds; ++rd) rbeg[rd + 1] += rbeg[rd];
+        std::vector<size_t> at(rbeg.begin(), rbeg.end() - 1);
+        for (size_t i = 0; i < n; ++i) rops[at[round[i]]++] = i;
+    }
+    const double t_rounds = trace ? now() : 0;
+    double t_prep = 0;
     for (uint32_t rd = 0; rd < n_rounds; ++rd) {
-        std::vector<size_t> idx;  // this round's ops, in op order
-        for (size_t i = 0; i < n; ++i)
-            if (round[i] == rd) idx.push_back(i);
+        const double tp0 = trace ? now() : 0;
+        const std::vector<size_t> idx(rops.begin() + rbeg[rd], rops.begin() + rbeg[rd + 1]);  // this round's ops, in op order
         if (idx.empty()) continue;
         // PN-Counter ops straight to the store as (row, amount, P or N) arrays the workers fill (no ClientOp copies);
-        // OR-Set ops through ApplyOps (element ids interned in op order on the host)
-        std::vector<ClientOp> ops;
+        // OR-Set ops through ApplyOps (element ids interned in op order on the host; the ops where they are)
+        std::vector<const ClientOp*> ops;
         std::vector<const KeyRef*> rr;
         std::vector<size_t> opos, ppos;  // positions in idx of the round's OR-Set / PN-Counter ops
         bool or_snap = false;
@@ -1104,13 +1136,14 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                 ppos.push_back(j);
                 continue;
             }
-            ops.push_back(ups[i].op);
+            ops.push_back(&ups[i].op);
             rr.push_back(kref[i]);
             opos.push_back(j);
             or_snap |= need[i] != 0;
         }
         std::vector<uint64_t> alim(or_snap ? idx.size() : 0), rlim(or_snap ? idx.size() : 0);
         const double ta = trace ? now() : 0;
+        t_prep += ta - tp0;
         // the round's PN-Counter ops applied, and the rewind of every needed snapshot (the amounts of the key's later
         // ops in the round) computed, in ONE call on the device (jg_pnc_apply_ops_rewind): dp / dn in op order over the
         // needed ops, which is pnc_need's order below
@@ -1161,24 +1194,21 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;
         if (!or_need.empty()) {
-            std::vector<Guid> ou;
-            std::vector<uint64_t> al, rl;
-            for (size_t j : or_need) {
-                ou.push_back(ups[idx[j]].op.uid);
-                al.push_back(alim[j]);
-                rl.push_back(rlim[j]);
-            }
-            std::vector<std::array<uint8_t, 32>> esha;
-            auto enc = EncodeORSetStates(ou, &al, &rl, &esha);
+            std::vector<uint32_t> os(or_need.size());
+            std::vector<uint64_t> al(or_need.size()), rl(or_need.size());
+            std::vector<size_t> at(or_need.size());
             for (size_t k = 0; k < or_need.size(); ++k) {
-                snap[idx[or_need[k]]] = std::move(enc[k]);
-                ssha[idx[or_need[k]]] = esha[k];
-                shas[idx[or_need[k]]] = 1;
+                const size_t j = or_need[k];
+                os[k] = krow[idx[j]], al[k] = alim[j], rl[k] = rlim[j], at[k] = idx[j];
             }
+            EncodeORSetSets(os, &al, &rl, at, snap, &ssha, &shas);
         }
         if (trace) t_enc_o += now() - tc;
     }
-    if (trace) tt[2] = now();
+    if (trace) {
+        tt[2] = now();
+        std::fprintf(stderr, "SubmitClientUpdates: before the rounds %.1f ms, rounds' op lists %.1f ms\n", t_rounds - tt[1], t_prep);
+    }
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
     //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).
     const size_t s0 = submitted.size();

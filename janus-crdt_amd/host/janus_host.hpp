@@ -185,7 +185,9 @@ class GpuStableStore {
     // add_lim / rem_lim (optional): per op, the ord limits of its OR-Set's snapshot right after it (jg_orset_apply_ops_ords)
     std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim = nullptr, std::vector<uint64_t>* rem_lim = nullptr)
     {
-        return ApplyOps(ops, add_lim, rem_lim, nullptr);
+        std::vector<const ClientOp*> p(ops.size());
+        for (size_t i = 0; i < ops.size(); ++i) p[i] = &ops[i];
+        return ApplyOps(p, add_lim, rem_lim, nullptr);
     }
 
     // SafeCRDT.Update over a batch of client updates, on this store as the node's PROSPECTIVE copy
@@ -245,8 +247,9 @@ class GpuStableStore {
 
   private:
     struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id (queries, ops)
-    // ApplyOps with the ops' keys already resolved and validated (refs[i] for ops[i]; NULL: look them up)
-    std::vector<uint8_t> ApplyOps(const std::vector<ClientOp>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
+    // ApplyOps over ops held elsewhere (no copies), with the ops' keys already resolved and validated (refs[i] for
+    // *ops[i]; NULL: look them up)
+    std::vector<uint8_t> ApplyOps(const std::vector<const ClientOp*>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
                                   const KeyRef* const* refs);
     // PN-Counter snapshots of rows rewound by (dp, dn) into out[at[i]] (jg_pnc_encode_json_before, one call into
     // page-locked memory, the strings built by the workers)
@@ -263,6 +266,9 @@ class GpuStableStore {
     void DigestsOf(std::vector<UpdateMessage>& msgs, size_t first, std::vector<std::array<uint8_t, 32>>& sha, const std::vector<uint8_t>& has);
     uint8_t* pinned_buf(size_t bytes);  // a page-locked buffer of at least `bytes`, kept across calls
     uint8_t* pinned_aux(size_t bytes);  // a second one (offsets, hashes beside pinned_buf's bytes)
+    void EncodeORSetSets(const std::vector<uint32_t>& sets, const std::vector<uint64_t>* add_lim, const std::vector<uint64_t>* rem_lim,
+                         const std::vector<size_t>& at, std::vector<std::string>& out, std::vector<std::array<uint8_t, 32>>* sha,
+                         std::vector<uint8_t>* has);
     void ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
                         const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
                         const std::function<void(size_t)>& on_chunk);
