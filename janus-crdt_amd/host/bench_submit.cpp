@@ -19,6 +19,7 @@
 // results, UpdateMessages (order, identities, payload bytes) and digests must equal the oracle's (exit 1).
 // Prints one JSON object.
 #include <array>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -253,6 +254,7 @@ int main(int argc, char** argv) {
     }
     janus::SafeUpdateTracker tracker(gpu.ctx());
     double gpu_s = 0;
+    std::vector<double> wave_ms;
     uint64_t gpu_n = 0, n_msgs = 0, n_um = 0, n_bytes = 0;
     for (int w = 0; w < waves + 1; ++w) {  // wave 0 = warmup
         const auto ops = make_ops(pnc, keys, ops_n, rng, fill);
@@ -277,6 +279,7 @@ int main(int argc, char** argv) {
         const double t1 = now_s();
         if (w == 0) continue;
         gpu_s += t1 - t0;
+        wave_ms.push_back(1e3 * (t1 - t0));
         gpu_n += ops.size();
         n_um += sub.size();
         for (const auto& um : sub) {
@@ -285,8 +288,13 @@ int main(int argc, char** argv) {
         }
     }
     const double W = waves;
+    std::string wl;
+    for (double x : wave_ms) wl += (wl.empty() ? "" : ", ") + std::to_string(x).substr(0, 6);
+    std::vector<double> sorted_ms = wave_ms;
+    std::sort(sorted_ms.begin(), sorted_ms.end());
+    const double med = sorted_ms.empty() ? 0.0 : sorted_ms[sorted_ms.size() / 2];
     std::printf("{\"workload\": \"producer path (SafeCRDT.Update + full-state Encode + ActualPropagateSyncMsg + ComputeDigest) of one node: %s, "
-                "%llu keys, clientBatchSize %d, %llu client ops per call\", \"waves\": %d, \"ops_per_s\": %.1f, \"ms_per_wave\": %.3f, "
+                "%llu keys, clientBatchSize %d, %llu client ops per call\", \"waves\": %d, \"ops_per_s\": %.1f, \"ms_per_wave\": %.3f, \"ms_per_wave_median\": %.3f, \"wave_ms\": [%s], "
                 "\"submitted_msgs_per_wave\": %.1f, \"update_messages_per_wave\": %.1f, \"payload_bytes_per_msg\": %.1f, \"host_threads\": %d, "
                 "\"parity_vs_oracle\": %s, \"parity_sample_ops\": %llu, \"parity_failure\": \"%s\", "
                 "\"cpu_baseline\": {\"ops_per_s\": %.1f, \"msgs_per_s\": %.1f, \"payload_bytes_per_msg\": %.1f, \"cores\": 1, \"kind\": \"port\", "
@@ -294,7 +302,7 @@ int main(int argc, char** argv) {
                 "per submitted UpdateMessage over %llu ops after %llu untimed ones\"}}\n",
                 pnc ? "C5 banking client ops (deposit / transfer / withdraw as Increments, 4-replica states)"
                     : "ORSetWorkload client ops (Add of random 5-char strings, Clear at 50 elements)",
-                (unsigned long long)keys, batch, (unsigned long long)ops_n, waves, gpu_n / gpu_s, 1e3 * gpu_s / W, n_msgs / W, n_um / W,
+                (unsigned long long)keys, batch, (unsigned long long)ops_n, waves, gpu_n / gpu_s, 1e3 * gpu_s / W, med, wl.c_str(), n_msgs / W, n_um / W,
                 n_msgs ? (double)n_bytes / n_msgs : 0.0, jg::host_threads(), parity_ok ? "true" : "false", (unsigned long long)cpu_n,
                 parity_why.c_str(), cpu_s > 0 ? cpu_n / cpu_s : 0.0, cpu_s > 0 ? cpu_msgs / cpu_s : 0.0, cpu_msgs ? (double)cpu_bytes / cpu_msgs : 0.0,
                 (unsigned long long)cpu_n, (unsigned long long)cpu_warm);

@@ -192,26 +192,50 @@ jg::WorkerPool& GpuStableStore::pool() {
 void GpuStableStore::flush_names() {
     if (pending_names_.empty()) return;
     materialize_names();
-    std::vector<uint32_t> set, next, nset, nid;
-    std::vector<uint8_t> cleared, bytes;
-    std::vector<uint64_t> off{0};
+    // per pending set: its entry, then its names' slots and bytes (counted, then filled by the workers)
+    const size_t P = pending_names_.size();
+    std::vector<const std::pair<const uint32_t, PendingNames>*> pv;
+    pv.reserve(P);
+    std::vector<uint32_t> set(P), next(P);
+    std::vector<uint8_t> cleared(P);
+    std::vector<size_t> nat(P + 1, 0), bat(P + 1, 0);
     for (const auto& kv : pending_names_) {
-        const SetKey& sk = sets_[kv.first];
-        set.push_back(kv.first);
-        next.push_back((uint32_t)sk.names.size());
-        cleared.push_back(kv.second.cleared ? 1 : 0);
-        for (uint32_t id : kv.second.ids) {
-            const std::string& nm = sk.names[id];
-            nset.push_back(kv.first);
-            nid.push_back(id);
-            bytes.insert(bytes.end(), nm.begin(), nm.end());
-            off.push_back(bytes.size());
-        }
+        const size_t k = pv.size();
+        pv.push_back(&kv);
+        set[k] = kv.first;
+        next[k] = (uint32_t)sets_[kv.first].names.size();
+        cleared[k] = kv.second.cleared ? 1 : 0;
+        nat[k + 1] = kv.second.ids.size();
     }
-    if (bytes.empty()) bytes.push_back(0);
-    check(jg_orset_names_sync(orset_, set.size(), set.data(), next.data(), cleared.data(), nid.size(), nset.data(), nid.data(), off.data(),
-                              bytes.data()));
-    names_seen_ += nid.size();  // caught up before the sync (materialize_names above): the log's new tail is ours
+    parallel_ranges(pool(), P, [&](size_t b, size_t e, int) {
+        for (size_t k = b; k < e; ++k) {
+            const SetKey& sk = sets_[pv[k]->first];
+            size_t nb = 0;
+            for (uint32_t id : pv[k]->second.ids) nb += sk.names[id].size();
+            bat[k + 1] = nb;
+        }
+    }, 64);
+    for (size_t k = 0; k < P; ++k) nat[k + 1] += nat[k], bat[k + 1] += bat[k];
+    const size_t nn = nat[P];
+    std::vector<uint32_t> nset(nn), nid(nn);
+    std::vector<uint64_t> off(nn + 1, 0);
+    std::vector<uint8_t> bytes(std::max<size_t>(bat[P], 1));
+    parallel_ranges(pool(), P, [&](size_t b, size_t e, int) {
+        for (size_t k = b; k < e; ++k) {
+            const SetKey& sk = sets_[pv[k]->first];
+            size_t j = nat[k], at = bat[k];
+            for (uint32_t id : pv[k]->second.ids) {
+                const std::string& nm = sk.names[id];
+                nset[j] = pv[k]->first;
+                nid[j] = id;
+                std::memcpy(bytes.data() + at, nm.data(), nm.size());
+                at += nm.size();
+                off[++j] = at;
+            }
+        }
+    }, 64);
+    check(jg_orset_names_sync(orset_, P, set.data(), next.data(), cleared.data(), nn, nset.data(), nid.data(), off.data(), bytes.data()));
+    names_seen_ += nn;  // caught up before the sync (materialize_names above): the log's new tail is ours
     pending_names_.clear();
 }
 
@@ -499,36 +523,47 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>
     // the OR-Set ops' element ids, interned per set in op order (sets are independent: a large batch by the
     // workers, each taking the sets with set % T == its index; the pending-name entries made first, serially)
     std::vector<uint32_t> oid(ops.size(), 0);
-    std::vector<uint8_t> oid_done(ops.size(), 0);
-    if (ops.size() >= 4096) {
-        std::vector<size_t> ors;
+    const bool par = ops.size() >= 4096;
+    std::vector<size_t> ors;  // (par) the OR-Set ops, in op order
+    if (par) {
+        std::vector<PendingNames*> pnp(sets_.size(), nullptr);  // each set's pending-name entry, made once
+        const size_t T = (size_t)std::max(1, pool().size());
+        std::vector<uint32_t> oset_of;  // (the set of ors[j])
+        std::vector<size_t> tat(T + 1, 0);
         for (size_t i = 0; i < ops.size(); ++i)
             if (refs[i]->type == CrdtType::ORSet) {
                 ors.push_back(i);
-                if (ops[i]->opId != 2) (void)pending_names_[refs[i]->idx];
+                const uint32_t set = refs[i]->idx;
+                oset_of.push_back(set);
+                ++tat[set % T + 1];
+                if (ops[i]->opId != 2 && !pnp[set]) pnp[set] = &pending_names_[set];
             }
-        const size_t T = (size_t)std::max(1, pool().size());
+        // each worker's ops (its sets: set % T == its index), op order kept
+        for (size_t t = 0; t < T; ++t) tat[t + 1] += tat[t];
+        std::vector<uint32_t> tops(ors.size());
+        {
+            std::vector<size_t> at(tat.begin(), tat.end() - 1);
+            for (size_t j = 0; j < ors.size(); ++j) tops[at[oset_of[j] % T]++] = (uint32_t)j;
+        }
         std::vector<std::string> err(T);
         parallel_ranges(pool(), T, [&](size_t tb0, size_t te0, int) {
             for (size_t t = tb0; t < te0; ++t)
                 try {
-                    for (size_t i : ors) {
-                        const uint32_t set = refs[i]->idx;
-                        if (set % T != t) continue;
+                    for (size_t x = tat[t]; x < tat[t + 1]; ++x) {
+                        const size_t i = ors[tops[x]];
+                        const uint32_t set = oset_of[tops[x]];
                         const ClientOp& op = *ops[i];
                         SetKey& sk = sets_[set];
                         if (op.opId == 3) {
                             sk.elems.clear();
                             sk.indexed = (uint32_t)sk.names.size();  // every id issued so far is dead
-                            PendingNames& pn = pending_names_.find(set)->second;
-                            pn.cleared = true;
-                            pn.ids.clear();
+                            pnp[set]->cleared = true;
+                            pnp[set]->ids.clear();
                         } else if (op.elem) {
-                            oid[i] = elem_id_in(sk, op.opId == 1 ? &pending_names_.find(set)->second : nullptr, *op.elem, op.opId == 1);
+                            oid[i] = elem_id_in(sk, op.opId == 1 ? pnp[set] : nullptr, *op.elem, op.opId == 1);
                         } else {
                             oid[i] = JG_NULL_ELEM;
                         }
-                        oid_done[i] = 1;
                     }
                 } catch (const std::exception& e) {
                     err[t] = e.what();
@@ -536,6 +571,16 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>
         }, 2);
         for (const auto& e : err)
             if (!e.empty()) throw EngineError(JG_ESTATE, e);
+        // the OR-Set ops' arrays by the workers (the PN-Counter ops, if any, below)
+        const size_t m = ors.size();
+        oset.resize(m), oelem.resize(m), oop.resize(m), olo.resize(m), ohi.resize(m), oidx.assign(ors.begin(), ors.end());
+        parallel_ranges(pool(), m, [&](size_t b, size_t e, int) {
+            for (size_t j = b; j < e; ++j) {
+                const size_t i = ors[j];
+                const ClientOp& op = *ops[i];
+                oset[j] = refs[i]->idx, oelem[j] = oid[i], oop[j] = (uint8_t)op.opId, olo[j] = op.tag.lo, ohi[j] = op.tag.hi;
+            }
+        });
     }
     for (size_t i = 0; i < ops.size(); ++i) {
         const ClientOp& op = *ops[i];
@@ -545,15 +590,14 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>
             pcol.push_back(0);
             pdelta.push_back(eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount);
             pisn.push_back(op.opId == 2 ? 1 : 0);
-        } else {
+        } else if (!par) {
             SetKey& sk = sets_[kr.idx];
             oset.push_back(kr.idx);
             // Add interns (first insertion); Remove of an unknown element addresses an id no record
             // carries (Contains is false, ORSet.cs:174); Clear empties the Dictionaries, so elements
             // added afterwards take new, larger ids in their new insertion order (ORSet.cs:192-198)
             uint32_t id = 0;
-            if (oid_done[i]) id = oid[i];  // interned by the workers above (Clear included)
-            else if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
+            if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
             else if (op.opId == 2) id = elem_id(kr.idx, op.elem, false);
             else {
                 sk.elems.clear();
