@@ -74,6 +74,7 @@ using jgw::hex_pairs;
 using jgw::hex_be16;
 using jgw::hex_le16;
 using jgw::lds_words;
+using jgw::lds_words_b64;
 
 // 36-char "D" Guid (Guid.ToString() layout: b3b2b1b0-b5b4-b7b6-b8b9-b10..b15) + the closing quote.
 __device__ __forceinline__ bool read_guid(Cursor& c, Guid16& g) {

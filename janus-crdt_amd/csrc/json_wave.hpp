@@ -109,7 +109,10 @@ __device__ __forceinline__ bool entry_at(const uint8_t* base, uint32_t q, Guid16
     constexpr uint32_t kMaxDigits = EB == 4 ? 10 : 19;
     constexpr int kYW = (kMaxDigits + 1 + 3) / 4;  // words holding the longest run and the character after it
     uint32_t X[10 + kYW];                           // characters 0 .. 40 + 4 kYW
-    lds_words<10 + kYW>(base, q, X);
+    // 8-byte reads: ds_read_b64 moves twice the bytes per LDS cycle of the ds_read2_b32 pairs 4-byte reads compile
+    // to, over 64 banks (round 6, tools/json_lds_ab.sh: LDS-active cycles 190M -> 152M per bench leg, bank-conflict
+    // cycles 66M -> 49M; the kernel's time did not move — it waits on memory, not on LDS)
+    lds_words_b64<10 + kYW>(base, q, X);
     bool ok = jgw::guid_d(X, g.lo, g.hi);
     ok &= (X[9] & 0xFFFFu) == ('"' | ':' << 8);
     // -?(0|[1-9][0-9]*) from character 38; more digits than the width can hold never pass the limit

@@ -370,4 +370,24 @@ __device__ __forceinline__ void lds_words(const uint8_t* base, uint32_t q, uint3
     for (int i = 0; i < K; ++i) X[i] = __builtin_amdgcn_alignbyte(W[i + 1], W[i], sh);
 }
 
+// The same from 8-byte aligned reads (base 8-byte aligned): ceil((q % 8 + 4K + 4) / 8) ds_read_b64 (twice the
+// bytes per LDS cycle of ds_read2_b32, banks over 64), one mask stage for the dword offset.
+template <int K>
+__device__ __forceinline__ void lds_words_b64(const uint8_t* base, uint32_t q, uint32_t (&X)[K]) {
+    constexpr int NQ = (7 + 4 * K + 4 + 7) / 8;
+    const uint2* w = reinterpret_cast<const uint2*>(base) + (q >> 3);
+    uint32_t W[2 * NQ];
+#pragma unroll
+    for (int b = 0; b < NQ; ++b) {
+        const uint2 v = w[b];
+        W[2 * b] = v.x, W[2 * b + 1] = v.y;
+    }
+    const uint32_t m1 = (q & 4) ? ~0u : 0u, sh = q & 3;
+    uint32_t B[K + 1];
+#pragma unroll
+    for (int i = 0; i < K + 1; ++i) B[i] = W[i] ^ ((W[i] ^ W[i + 1]) & m1);
+#pragma unroll
+    for (int i = 0; i < K; ++i) X[i] = __builtin_amdgcn_alignbyte(B[i + 1], B[i], sh);
+}
+
 }  // namespace jgw

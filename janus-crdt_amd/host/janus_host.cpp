@@ -405,6 +405,10 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
     double t_copy = 0, t_append = 0;
     size_t n_parts = 0;
     const double t0 = trace ? now() : 0;
+    static const size_t copiers = [] {
+        const char* e = std::getenv("JANUS_ARENA_COPY_THREADS");
+        return e && std::atoi(e) > 0 ? (size_t)std::atoi(e) : SIZE_MAX;
+    }();
     std::vector<uint64_t> poff[2];  // the in-flight part's offsets and the next one's
     std::future<int> pending;
     std::string err;
@@ -415,7 +419,10 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
         while (b1 < blocks.size() && (b1 == b0 || block_off_[b1] - block_off_[b0] < part_msgs)) ++b1;
         const size_t i0 = block_off_[b0], i1 = block_off_[b1];
         const double tc = trace ? now() : 0;
-        parallel_ranges(pool(), i1 - i0, [&](size_t a, size_t e, int) {
+        // the copy on `copiers` of the workers (JANUS_ARENA_COPY_THREADS; default all): fewer copiers leave more of the
+        // host's memory bandwidth to the part the DMA is reading at the same time
+        const size_t m = i1 - i0;
+        auto copy_range = [&](size_t a, size_t e) {
             if (a >= e) return;
             a += i0, e += i0;
             jg::LineStream out(reinterpret_cast<char*>(p_bytes_), p_off_[a]);
@@ -431,7 +438,14 @@ std::vector<uint64_t> GpuStableStore::ApplyArenaStreamed(const std::vector<std::
                 }
             }
             if (nontemporal) out.finish();
-        });
+        };
+        if (copiers >= (size_t)pool().size() || m < 8192) {
+            parallel_ranges(pool(), m, [&](size_t a, size_t e, int) { copy_range(a, e); });
+        } else {
+            pool().run([&](int t) {
+                if ((size_t)t < copiers) copy_range(m * t / copiers, m * (t + 1) / copiers);
+            });
+        }
         const double ta = trace ? now() : 0;
         // the part goes to the library on a helper thread while this thread copies the next part (the previous
         // append has returned first: parts arrive in order)
