@@ -509,16 +509,29 @@ std::vector<uint64_t> GpuStableStore::run_wave(const jg_commit& wave, SafeUpdate
 
 std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
                                               const KeyRef* const* refs) {
-    const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3;
-    materialize_names();
-    std::vector<uint8_t> result(ops.size(), 1);
-    std::vector<uint32_t> pkey, pcol;
-    std::vector<int64_t> pdelta;
-    std::vector<uint8_t> pisn;
-    std::vector<uint32_t> oset, oelem;
-    std::vector<uint8_t> oop;
-    std::vector<uint64_t> olo, ohi;
-    std::vector<size_t> oidx;
+    PreparedOps p = PrepareOps(ops, refs, true);
+    return RunOps(p, add_lim, rem_lim);
+}
+
+// ApplyOps' host half: every op validated (unless refs are given), the OR-Set ops' element ids interned, the
+// engine's arrays built.  Nothing reaches the library but the names pull (materialize).
+GpuStableStore::PreparedOps GpuStableStore::PrepareOps(const std::vector<const ClientOp*>& ops, const KeyRef* const* refs, bool materialize) {
+    static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t0 = trace ? now() : 0;
+    if (materialize) materialize_names();
+    PreparedOps P;
+    P.n = ops.size();
+    auto& pkey = P.pkey;
+    auto& pcol = P.pcol;
+    auto& pdelta = P.pdelta;
+    auto& pisn = P.pisn;
+    auto& oset = P.oset;
+    auto& oelem = P.oelem;
+    auto& oop = P.oop;
+    auto& olo = P.olo;
+    auto& ohi = P.ohi;
+    auto& oidx = P.oidx;
     std::vector<const KeyRef*> found;
     if (!refs) {
         found.resize(ops.size());
@@ -627,25 +640,33 @@ std::vector<uint8_t> GpuStableStore::ApplyOps(const std::vector<const ClientOp*>
             oidx.push_back(i);
         }
     }
+    if (trace) P.prep_ms = now() - t0;
+    return P;
+}
+
+// ApplyOps' library half: the prepared arrays applied (jg_pnc_apply_ops, jg_orset_apply_ops(_ords)); per op its
+// result and, with add_lim / rem_lim, its OR-Set snapshot limits.
+std::vector<uint8_t> GpuStableStore::RunOps(PreparedOps& P, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim) {
     static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
     const double t1 = trace ? now() : 0;
-    if (!pkey.empty()) check(jg_pnc_apply_ops(pnc_, pkey.size(), pkey.data(), pcol.data(), pdelta.data(), pisn.data()));
-    if (!oset.empty()) {
-        std::vector<uint8_t> r(oset.size());
+    std::vector<uint8_t> result(P.n, 1);
+    if (!P.pkey.empty()) check(jg_pnc_apply_ops(pnc_, P.pkey.size(), P.pkey.data(), P.pcol.data(), P.pdelta.data(), P.pisn.data()));
+    if (!P.oset.empty()) {
+        std::vector<uint8_t> r(P.oset.size());
         if (add_lim) {  // and each op's snapshot limits (jg_orset_apply_ops_ords)
-            std::vector<uint64_t> al(oset.size()), rl(oset.size());
-            check(jg_orset_apply_ops_ords(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data(), al.data(),
-                                          rl.data()));
-            add_lim->assign(ops.size(), 0);
-            rem_lim->assign(ops.size(), 0);
-            for (size_t j = 0; j < oidx.size(); ++j) (*add_lim)[oidx[j]] = al[j], (*rem_lim)[oidx[j]] = rl[j];
+            std::vector<uint64_t> al(P.oset.size()), rl(P.oset.size());
+            check(jg_orset_apply_ops_ords(orset_, P.oset.size(), P.oset.data(), P.oelem.data(), P.oop.data(), P.olo.data(), P.ohi.data(), r.data(),
+                                          al.data(), rl.data()));
+            add_lim->assign(P.n, 0);
+            rem_lim->assign(P.n, 0);
+            for (size_t j = 0; j < P.oidx.size(); ++j) (*add_lim)[P.oidx[j]] = al[j], (*rem_lim)[P.oidx[j]] = rl[j];
         } else {
-            check(jg_orset_apply_ops(orset_, oset.size(), oset.data(), oelem.data(), oop.data(), olo.data(), ohi.data(), r.data()));
+            check(jg_orset_apply_ops(orset_, P.oset.size(), P.oset.data(), P.oelem.data(), P.oop.data(), P.olo.data(), P.ohi.data(), r.data()));
         }
-        for (size_t j = 0; j < oidx.size(); ++j) result[oidx[j]] = r[j];
+        for (size_t j = 0; j < P.oidx.size(); ++j) result[P.oidx[j]] = r[j];
     }
-    if (trace) std::fprintf(stderr, "ApplyOps(%zu): host prep %.1f ms, device %.1f ms\n", ops.size(), t1 - t0, now() - t1);
+    if (trace) std::fprintf(stderr, "ApplyOps(%zu): host prep %.1f ms, device %.1f ms\n", P.n, P.prep_ms, now() - t1);
     return result;
 }
 
@@ -888,29 +909,45 @@ void GpuStableStore::EncodeORSetSets(const std::vector<uint32_t>& sets, const st
     const double t0 = trace ? now() : 0;
     flush_names();  // every element this mirror interned is in the engine's element table
     const double t1 = trace ? now() : 0;
+    OrEnc e;
+    EncodeORSetSetsDevice(sets, add_lim, rem_lim, sha != nullptr, e);
+    const double t2 = trace ? now() : 0;
+    EncodeORSetSetsPlace(e, at, out, sha, has);
+    if (trace)
+        std::fprintf(stderr, "EncodeORSetSets(%zu, %.1f MB): names %.1f ms, encode %.1f ms, strings %.1f ms\n", sets.size(), e.off.back() / 1e6,
+                     t1 - t0, t2 - t1, now() - t2);
+}
+
+// The library half (no workers, nothing of the mirror's tables but the pinned buffer: it may run beside the workers)
+void GpuStableStore::EncodeORSetSetsDevice(const std::vector<uint32_t>& sets, const std::vector<uint64_t>* add_lim, const std::vector<uint64_t>* rem_lim,
+                                           bool sha, OrEnc& e) {
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() * 1e3; };
+    const double t0 = now();
     const size_t n = sets.size();
-    std::vector<uint64_t> off(n + 1, 0);
+    e.off.assign(n + 1, 0);
     const uint64_t* al = add_lim ? add_lim->data() : nullptr;
     const uint64_t* rl = rem_lim ? rem_lim->data() : nullptr;
     uint8_t* buf = pinned_buf(4096);
-    std::vector<uint8_t> h(sha ? 32 * n : 0);  // each state's SHA-256, hashed on the device as it is encoded
-    uint8_t* hs = sha ? h.data() : nullptr;
-    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
-    if (rc == JG_ESTATE && off[n] > pin_cap_) {
-        buf = pinned_buf(off[n]);
-        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, off.data(), buf, pin_cap_, hs);
+    e.h.assign(sha ? 32 * n : 0, 0);  // each state's SHA-256, hashed on the device as it is encoded
+    uint8_t* hs = sha ? e.h.data() : nullptr;
+    int rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, e.off.data(), buf, pin_cap_, hs);
+    if (rc == JG_ESTATE && e.off[n] > pin_cap_) {
+        buf = pinned_buf(e.off[n]);
+        rc = jg_orset_encode_json(orset_, n, sets.data(), al, rl, e.off.data(), buf, pin_cap_, hs);
     }
     check(rc);
-    const double t2 = trace ? now() : 0;
-    parallel_ranges(pool(), n, [&](size_t b, size_t e, int) {
-        for (size_t i = b; i < e; ++i) {
-            out[at[i]].assign(reinterpret_cast<const char*>(buf) + off[i], off[i + 1] - off[i]);
-            if (sha) std::memcpy((*sha)[at[i]].data(), h.data() + 32 * i, 32), (*has)[at[i]] = 1;
+    e.buf = buf;
+    e.ms = now() - t0;
+}
+
+void GpuStableStore::EncodeORSetSetsPlace(const OrEnc& e, const std::vector<size_t>& at, std::vector<std::string>& out,
+                                          std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has) {
+    parallel_ranges(pool(), at.size(), [&](size_t b, size_t x, int) {
+        for (size_t i = b; i < x; ++i) {
+            out[at[i]].assign(reinterpret_cast<const char*>(e.buf) + e.off[i], e.off[i + 1] - e.off[i]);
+            if (sha) std::memcpy((*sha)[at[i]].data(), e.h.data() + 32 * i, 32), (*has)[at[i]] = 1;
         }
     });
-    if (trace)
-        std::fprintf(stderr, "EncodeORSetSets(%zu, %.1f MB): names %.1f ms, encode %.1f ms, strings %.1f ms\n", n, off[n] / 1e6, t1 - t0, t2 - t1,
-                     now() - t2);
 }
 
 std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<ClientUpdate>& ups, int clientBatchSize,
@@ -1177,35 +1214,49 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         for (size_t i = 0; i < n; ++i) rops[at[round[i]]++] = i;
     }
     const double t_rounds = trace ? now() : 0;
-    double t_prep = 0;
-    for (uint32_t rd = 0; rd < n_rounds; ++rd) {
-        const double tp0 = trace ? now() : 0;
-        const std::vector<size_t> idx(rops.begin() + rbeg[rd], rops.begin() + rbeg[rd + 1]);  // this round's ops, in op order
-        if (idx.empty()) continue;
-        // PN-Counter ops straight to the store as (row, amount, P or N) arrays the workers fill (no ClientOp copies);
-        // OR-Set ops through ApplyOps (element ids interned in op order on the host; the ops where they are)
+    double t_prep = 0, t_over = 0;
+    // A round's lists (its ops in op order; the OR-Set ops as pointers, no ClientOp copies) and its OR-Set ops
+    // prepared (element ids interned in op order, the engine's arrays).  Round r + 1 is prepared on this thread's
+    // workers while round r's OR-Set snapshots encode in the library on a helper thread (its device work and D2H):
+    // the preparation touches only the mirror's tables, the encode only the library and the page-locked buffer.
+    struct Round {
+        std::vector<size_t> idx;
         std::vector<const ClientOp*> ops;
         std::vector<const KeyRef*> rr;
         std::vector<size_t> opos, ppos;  // positions in idx of the round's OR-Set / PN-Counter ops
         bool or_snap = false;
-        for (size_t j = 0; j < idx.size(); ++j) {
-            const size_t i = idx[j];
+        PreparedOps prep;
+    };
+    auto make_round = [&](uint32_t rd, Round& R) {
+        const double tp0 = trace ? now() : 0;
+        R.idx.assign(rops.begin() + rbeg[rd], rops.begin() + rbeg[rd + 1]);
+        for (size_t j = 0; j < R.idx.size(); ++j) {
+            const size_t i = R.idx[j];
             if (kpn[i]) {
-                ppos.push_back(j);
+                R.ppos.push_back(j);
                 continue;
             }
-            ops.push_back(&ups[i].op);
-            rr.push_back(kref[i]);
-            opos.push_back(j);
-            or_snap |= need[i] != 0;
+            R.ops.push_back(&ups[i].op);
+            R.rr.push_back(kref[i]);
+            R.opos.push_back(j);
+            R.or_snap |= need[i] != 0;
         }
-        std::vector<uint64_t> alim(or_snap ? idx.size() : 0), rlim(or_snap ? idx.size() : 0);
+        if (!R.ops.empty()) R.prep = PrepareOps(R.ops, R.rr.data(), false);
+        if (trace) t_prep += now() - tp0;
+    };
+    if (n_rounds) materialize_names();  // (once: nothing issues names during this call)
+    Round cur;
+    if (n_rounds) make_round(0, cur);
+    for (uint32_t rd = 0; rd < n_rounds; ++rd) {
+        const std::vector<size_t>& idx = cur.idx;
+        std::vector<uint64_t> alim(cur.or_snap ? idx.size() : 0), rlim(cur.or_snap ? idx.size() : 0);
         const double ta = trace ? now() : 0;
-        t_prep += ta - tp0;
         // the round's PN-Counter ops applied, and the rewind of every needed snapshot (the amounts of the key's later
         // ops in the round) computed, in ONE call on the device (jg_pnc_apply_ops_rewind): dp / dn in op order over the
         // needed ops, which is pnc_need's order below
         std::vector<int64_t> dp, dn;
+        const std::vector<size_t>& ppos = cur.ppos;
+        const std::vector<size_t>& opos = cur.opos;
         if (!ppos.empty()) {
             std::vector<uint32_t> pkey(ppos.size());
             std::vector<int64_t> pdelta(ppos.size());
@@ -1224,15 +1275,14 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             for (uint8_t x : pneed) nn += x;
             dp.resize(nn);
             dn.resize(nn);
-            materialize_names();
             check(jg_pnc_apply_ops_rewind(pnc_, pkey.size(), pkey.data(), 0, pdelta.data(), pisn.data(), pneed.data(), dp.data(), dn.data()));
         }
-        if (!ops.empty()) {
+        if (!cur.ops.empty()) {
             std::vector<uint64_t> al, rl;
-            const auto r = ApplyOps(ops, or_snap ? &al : nullptr, or_snap ? &rl : nullptr, rr.data());
+            const auto r = RunOps(cur.prep, cur.or_snap ? &al : nullptr, cur.or_snap ? &rl : nullptr);
             for (size_t k = 0; k < opos.size(); ++k) {
                 result[idx[opos[k]]] = r[k];
-                if (or_snap) alim[opos[k]] = al[k], rlim[opos[k]] = rl[k];
+                if (cur.or_snap) alim[opos[k]] = al[k], rlim[opos[k]] = rl[k];
             }
         }
         const double tb = trace ? now() : 0;
@@ -1251,21 +1301,50 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         }
         const double tc = trace ? now() : 0;
         t_enc_p += tc - tb;
-        if (!or_need.empty()) {
-            std::vector<uint32_t> os(or_need.size());
-            std::vector<uint64_t> al(or_need.size()), rl(or_need.size());
-            std::vector<size_t> at(or_need.size());
-            for (size_t k = 0; k < or_need.size(); ++k) {
-                const size_t j = or_need[k];
-                os[k] = krow[idx[j]], al[k] = alim[j], rl[k] = rlim[j], at[k] = idx[j];
-            }
-            EncodeORSetSets(os, &al, &rl, at, snap, &ssha, &shas);
+        // the OR-Set snapshots: names flushed here, the library's encode on the helper while round rd + 1 is prepared
+        std::vector<uint32_t> os(or_need.size());
+        std::vector<uint64_t> oal(or_need.size()), orl(or_need.size());
+        std::vector<size_t> oat(or_need.size());
+        for (size_t k = 0; k < or_need.size(); ++k) {
+            const size_t j = or_need[k];
+            os[k] = krow[idx[j]], oal[k] = alim[j], orl[k] = rlim[j], oat[k] = idx[j];
         }
-        if (trace) t_enc_o += now() - tc;
+        OrEnc oe;
+        std::exception_ptr eerr;
+        std::thread enc;
+        if (!or_need.empty()) {
+            flush_names();  // every element this mirror interned so far (this round's included) in the engine's table
+            enc = std::thread([&] {
+                try {
+                    EncodeORSetSetsDevice(os, &oal, &orl, true, oe);
+                } catch (...) {
+                    eerr = std::current_exception();
+                }
+            });
+        }
+        struct EncJoin {
+            std::thread& t;
+            ~EncJoin() {
+                if (t.joinable()) t.join();
+            }
+        } enc_join{enc};
+        Round next;
+        const double tn = trace ? now() : 0;
+        if (rd + 1 < n_rounds) make_round(rd + 1, next);
+        const double tn1 = trace ? now() : 0;
+        if (enc.joinable()) enc.join();
+        if (eerr) std::rethrow_exception(eerr);
+        if (!or_need.empty()) EncodeORSetSetsPlace(oe, oat, snap, &ssha, &shas);
+        if (trace) {
+            t_enc_o += now() - tc - (tn1 - tn);
+            t_over += std::min(tn1 - tn, oe.ms);
+        }
+        cur = std::move(next);
     }
     if (trace) {
         tt[2] = now();
-        std::fprintf(stderr, "SubmitClientUpdates: before the rounds %.1f ms, rounds' op lists %.1f ms\n", t_rounds - tt[1], t_prep);
+        std::fprintf(stderr, "SubmitClientUpdates: before the rounds %.1f ms, rounds' op lists + preparation %.1f ms (%.1f ms of it beside the encodes)\n",
+                     t_rounds - tt[1], t_prep, t_over);
     }
     // 4. Submitted UpdateMessages and the remaining queue carry the snapshots; each new UpdateMessage
     //    gets its digest (the constructor's ComputeDigest, DAGUpdateMessage.cs:25-30).

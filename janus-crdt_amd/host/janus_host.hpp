@@ -247,6 +247,20 @@ class GpuStableStore {
 
   private:
     struct KeyRef { CrdtType type; uint32_t idx; };  // idx = PNC row or OR-Set set id (queries, ops)
+    // ApplyOps in two halves (SubmitClientUpdates prepares a round's ops while the previous round's snapshots encode)
+    struct PreparedOps {
+        size_t n = 0;
+        std::vector<uint32_t> pkey, pcol;
+        std::vector<int64_t> pdelta;
+        std::vector<uint8_t> pisn;
+        std::vector<uint32_t> oset, oelem;
+        std::vector<uint8_t> oop;
+        std::vector<uint64_t> olo, ohi;
+        std::vector<size_t> oidx;
+        double prep_ms = 0;
+    };
+    PreparedOps PrepareOps(const std::vector<const ClientOp*>& ops, const KeyRef* const* refs, bool materialize);
+    std::vector<uint8_t> RunOps(PreparedOps& p, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim);
     // ApplyOps over ops held elsewhere (no copies), with the ops' keys already resolved and validated (refs[i] for
     // *ops[i]; NULL: look them up)
     std::vector<uint8_t> ApplyOps(const std::vector<const ClientOp*>& ops, std::vector<uint64_t>* add_lim, std::vector<uint64_t>* rem_lim,
@@ -269,6 +283,17 @@ class GpuStableStore {
     void EncodeORSetSets(const std::vector<uint32_t>& sets, const std::vector<uint64_t>* add_lim, const std::vector<uint64_t>* rem_lim,
                          const std::vector<size_t>& at, std::vector<std::string>& out, std::vector<std::array<uint8_t, 32>>* sha,
                          std::vector<uint8_t>* has);
+    // its two halves: the library call (names flushed before it; no workers) and the strings (the workers)
+    struct OrEnc {
+        std::vector<uint64_t> off;
+        std::vector<uint8_t> h;
+        const uint8_t* buf = nullptr;
+        double ms = 0;
+    };
+    void EncodeORSetSetsDevice(const std::vector<uint32_t>& sets, const std::vector<uint64_t>* add_lim, const std::vector<uint64_t>* rem_lim,
+                               bool sha, OrEnc& e);
+    void EncodeORSetSetsPlace(const OrEnc& e, const std::vector<size_t>& at, std::vector<std::string>& out,
+                              std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has);
     void ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
                         const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
                         const std::function<void(size_t)>& on_chunk);
