@@ -626,8 +626,8 @@ def bench_submit(local, workload):
     byte (parity).  Roofline: the host link — every snapshot byte comes back to the host once and goes out again
     for its UpdateMessage's digest."""
     import subprocess
-    args = (["--workload", "pnc", "--keys", "1000000", "--ops", "1000000", "--cpu-ops", "50000", "--waves", "3"] if workload == "pnc" else
-            ["--workload", "orset", "--keys", "2000", "--ops", "200000", "--cpu-ops", "20000", "--waves", "3"])
+    args = (["--workload", "pnc", "--keys", "1000000", "--ops", "1000000", "--cpu-ops", "50000", "--waves", "5"] if workload == "pnc" else
+            ["--workload", "orset", "--keys", "2000", "--ops", "200000", "--cpu-ops", "20000", "--waves", "5"])
     out = subprocess.run([str(ROOT / "janus-crdt_amd" / "build" / "bench_submit")] + args + ["--device", str(local)],
                          capture_output=True, text=True, timeout=240)
     if not out.stdout.strip():

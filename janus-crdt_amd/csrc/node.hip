@@ -272,11 +272,24 @@ struct jg_tracker {
     // first append after a switch waits on it): no call has to end with a stream sync for the pair of
     // buffers to be safe (an empty wave returned after a flush without one).
     std::mutex pend_mu;
-    struct Pin {
+    // A buffer is a list of page-locked blocks filled in order and kept across flushes (round 6: one block grown by
+    // doubling cost a hipHostMalloc + copy + hipHostFree — which waits for the device — each time the pending adds
+    // outgrew it: 10-30 ms spikes in the producer bench, whose adds accumulate with no wave to flush them).
+    struct Block {
         unsigned long long* p = nullptr;
-        size_t cap = 0, n = 0;
+        size_t cap = 0, n = 0;  // pairs
+    };
+    struct Pin {
+        std::vector<Block> blocks;
+        size_t at = 0;            // the block being filled
+        size_t n = 0;             // pairs pending over all blocks
         hipEvent_t up = nullptr;  // recorded after the buffer's last upload
-        bool wait = false;        // the upload may still be queued: wait on `up` before touching p
+        bool wait = false;        // the upload may still be queued: wait on `up` before touching the blocks
+        void reset() {
+            for (Block& k : blocks) k.n = 0;
+            at = 0;
+            n = 0;
+        }
     } pin[2];
     int cur = 0;
     jg::DevBuf tab, claim, count, dpairs;
@@ -288,7 +301,8 @@ struct jg_tracker {
     ~jg_tracker() {
         for (Pin& b : pin) {
             if (b.up) (void)hipEventSynchronize(b.up);
-            if (b.p) (void)hipHostFree(b.p);
+            for (Block& k : b.blocks)
+                if (k.p) (void)hipHostFree(k.p);
             if (b.up) (void)hipEventDestroy(b.up);
         }
     }
@@ -300,20 +314,26 @@ struct jg_tracker {
             JG_HIP(hipEventSynchronize(b.up));
             b.wait = false;
         }
-        if (b.n + n > b.cap) {
-            const size_t nc = std::max<size_t>({2 * b.cap, b.n + n, 4096});
-            void* p = nullptr;
-            JG_HIP(hipHostMalloc(&p, nc * 16, hipHostMallocDefault));
-            if (b.n) std::memcpy(p, b.p, b.n * 16);
-            if (b.p) (void)hipHostFree(b.p);
-            b.p = static_cast<unsigned long long*>(p);
-            b.cap = nc;
+        uint64_t i = 0;
+        while (i < n) {
+            if (b.at == b.blocks.size()) {  // a new block, twice the last (64k .. 4M pairs), at least what is left
+                const size_t last = b.blocks.empty() ? 0 : b.blocks.back().cap;
+                const size_t nc = std::max<size_t>(std::min<size_t>(std::max<size_t>(2 * last, 65536), size_t(1) << 22), std::min<uint64_t>(n - i, size_t(1) << 22));
+                void* p = nullptr;
+                JG_HIP(hipHostMalloc(&p, nc * 16, hipHostMallocDefault));
+                b.blocks.push_back(Block{static_cast<unsigned long long*>(p), nc, 0});
+            }
+            Block& k = b.blocks[b.at];
+            const uint64_t take = std::min<uint64_t>(n - i, k.cap - k.n);
+            for (uint64_t j = 0; j < take; ++j) {
+                k.p[2 * (k.n + j)] = seq[i + j];
+                k.p[2 * (k.n + j) + 1] = origin[i + j];
+            }
+            k.n += take;
+            b.n += take;
+            i += take;
+            if (k.n == k.cap) ++b.at;
         }
-        for (uint64_t i = 0; i < n; ++i) {
-            b.p[2 * (b.n + i)] = seq[i];
-            b.p[2 * (b.n + i) + 1] = origin[i];
-        }
-        b.n += n;
     }
 
     // The pending adds into the device table, queued on the context's stream (under the context lock).
@@ -323,7 +343,7 @@ struct jg_tracker {
             std::lock_guard<std::mutex> g(pend_mu);
             b = &pin[cur];
             cur ^= 1;
-            pin[cur].n = 0;
+            pin[cur].reset();
             pin[cur].wait = pin[cur].up != nullptr;  // appends to it wait for its previous upload first
         }
         if (!count.p) {
@@ -358,7 +378,12 @@ struct jg_tracker {
             used = live;
         }
         ensure(dpairs, np * 20);  // pairs, then each pair's slot
-        JG_HIP(hipMemcpyAsync(dpairs.p, b->p, np * 16, hipMemcpyHostToDevice, ctx->stream));
+        uint64_t at = 0;
+        for (const Block& k : b->blocks) {
+            if (k.n == 0) break;  // blocks fill in order
+            JG_HIP(hipMemcpyAsync(dpairs.as<char>() + at * 16, k.p, k.n * 16, hipMemcpyHostToDevice, ctx->stream));
+            at += k.n;
+        }
         if (!b->up) JG_HIP(hipEventCreateWithFlags(&b->up, hipEventDisableTiming));
         JG_HIP(hipEventRecord(b->up, ctx->stream));
         auto* slot_of = reinterpret_cast<uint32_t*>(dpairs.as<char>() + np * 16);

@@ -623,9 +623,11 @@ GpuStableStore::PreparedOps GpuStableStore::PrepareOps(const std::vector<const C
             // Add interns (first insertion); Remove of an unknown element addresses an id no record
             // carries (Contains is false, ORSet.cs:174); Clear empties the Dictionaries, so elements
             // added afterwards take new, larger ids in their new insertion order (ORSet.cs:192-198)
+            // (elem_id_in: the names were materialized by the caller, not once per op — that is a library call)
             uint32_t id = 0;
-            if (op.opId == 1) id = elem_id(kr.idx, op.elem, true);
-            else if (op.opId == 2) id = elem_id(kr.idx, op.elem, false);
+            if (op.opId != 3 && !op.elem) id = JG_NULL_ELEM;
+            else if (op.opId == 1) id = elem_id_in(sk, &pending_names_[kr.idx], *op.elem, true);
+            else if (op.opId == 2) id = elem_id_in(sk, nullptr, *op.elem, false);
             else {
                 sk.elems.clear();
                 sk.indexed = (uint32_t)sk.names.size();  // every id issued so far is dead
@@ -1195,7 +1197,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::vector<uint32_t> round(n, 0);
     uint32_t n_rounds = spec.on ? 0 : 1;
     if (!spec.on) {
-        std::unordered_map<uint32_t, std::pair<uint32_t, bool>> st;  // OR-Set set -> (its round, a snapshot needed in it)
+        std::vector<std::pair<uint32_t, bool>> st(sets_.size());  // OR-Set set -> (its round, a snapshot needed in it)
         for (size_t i = 0; i < n; ++i) {
             if (kpn[i]) continue;
             auto& e = st[krow[i]];
