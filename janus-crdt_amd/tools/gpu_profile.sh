@@ -3,7 +3,9 @@
 # leg (incl. the OR-Set apply loop from page-locked payloads), one PMC pass per counter group (FETCH_SIZE and
 # WRITE_SIZE do not fit one pass on gfx950; SQ instruction / wait counters; TCC atomics / hits), the per-launch
 # summary (pmc_summary.py), then the default bench line itself.
-# Usage: [WITH_BENCH=1] gpu_profile.sh <outdir> [round label]
+# Usage: [WITH_BENCH=1] [PHASES="trace pmc summary bench"] gpu_profile.sh <outdir> [round label]
+# (PHASES splits the lease over several gpurun calls of <= 20 min: the summary reads the trace and pmc outputs
+# of the same <outdir>, so the calls share it through gpurun_out/)
 set -o pipefail
 OUT=${1:-gpurun_out/prof}
 LABEL=${2:-r04}
@@ -28,15 +30,20 @@ JSON="python3 bench.py --steps 8 --warmup 1 --no-cpu-baseline --workload json"
 DIGEST="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --workload digest"
 APPLY="janus-crdt_amd/build/bench_apply --accounts 1000000 --ops 1000000 --waves 3 --cpu-msgs 0 --device 0"
 ORSET_LOOP="janus-crdt_amd/build/bench_orset --sets 2000 --msgs 200000 --waves 3 --cpu-msgs 0 --device 0 --direct"
+PHASES=${PHASES:-"trace pmc summary bench"}
+has() { [[ " $PHASES " == *" $1 "* ]]; }
 SQ=SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES
 SQ2=SQ_ACTIVE_INST_ANY,SQ_LDS_BANK_CONFLICT,SQ_LDS_IDX_ACTIVE,SQ_WAIT_INST_LDS
 TCC=TCC_ATOMIC_sum,TCC_HIT_sum,TCC_MISS_sum,TCC_EA0_RDREQ_sum
+if has trace; then
 trace trace 300 $PNC_ORSET
 trace trace_exch 300 $EXCH
 trace trace_digest 300 $DIGEST
 trace trace_json 300 $JSON
 trace trace_apply 300 $APPLY
 trace trace_orset_loop 300 $ORSET_LOOP
+fi
+if has pmc; then
 for C in FETCH_SIZE WRITE_SIZE; do
     pass pmc_$C $C python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --workload pnc-orset
     pass pmc_exch_$C $C python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --workload exchange
@@ -48,15 +55,19 @@ pass sq2_json $SQ2 python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --wor
 pass sq_orset_loop $SQ $ORSET_LOOP
 pass sq2_orset_loop $SQ2 $ORSET_LOOP
 pass tcc_orset_loop $TCC $ORSET_LOOP
+fi
+if has summary; then
 step summary
 python3 janus-crdt_amd/tools/pmc_summary.py "$OUT" "$OUT/pmc_$LABEL.json" "$LABEL" > "$OUT/pmc_summary.out" || exit 1
+fi
 # the default bench line in the same lease, reading the summary just made (its rooflines cite it), measured
 # UNDER the kernel trace: the line and the kernel statistics it is checked against come from one process (two
 # runs a minute apart on one box differed by 4 % in the headline kernel's time; the trace costs a ms-scale
 # kernel nothing measurable — 5.033 ms per step traced vs 5.03 ms kernel average)
-if [ -n "$WITH_BENCH" ]; then
+if [ -n "$WITH_BENCH" ] && has bench; then
     step bench
-    mkdir -p profiles && cp "$OUT/pmc_$LABEL.json" "profiles/pmc_$LABEL.json"
+    mkdir -p profiles
+    if [ -f "$OUT/pmc_$LABEL.json" ]; then cp "$OUT/pmc_$LABEL.json" "profiles/pmc_$LABEL.json"; fi
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace_final" -o run --output-format csv -- python3 bench.py \
         > "$OUT/bench_final.json" 2> "$OUT/bench_final.err" || exit 1
     # and the same command without the profiler: the trace's per-dispatch cost shows on the apply loops' many
