@@ -1,3 +1,7 @@
+#!/bin/bash
+# A/B of OR-Set wave-table builds under kernel trace (round 6): each directory janus-crdt_amd/lib/<v>/ holds a
+# libjanusgpu.so built with the change under test (bench_orset's RUNPATH yields to LD_LIBRARY_PATH); prints
+# ms_per_wave and the per-wave time of k_ow_group / k_ow_strings / k_ow_rins (5 waves + 2 warm-ups = 7).
 set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r06/owab
