@@ -1247,6 +1247,28 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         if (trace) t_prep += now() - tp0;
     };
     if (n_rounds) materialize_names();  // (once: nothing issues names during this call)
+    // Round r's OR-Set strings are placed (by the workers) on a helper while round r + 1's ops apply in the library,
+    // whose apply runs on threads of its own; the helper is joined before this thread next uses the workers.
+    struct Placer {
+        OrEnc e;
+        std::vector<size_t> at;
+        std::thread t;
+        std::exception_ptr err;
+    };
+    std::unique_ptr<Placer> placer;
+    struct PlacerGuard {  // (never a joinable thread left to a destructor while an exception unwinds)
+        std::unique_ptr<Placer>& p;
+        ~PlacerGuard() {
+            if (p && p->t.joinable()) p->t.join();
+        }
+    } placer_guard{placer};
+    auto join_placer = [&] {
+        if (!placer) return;
+        if (placer->t.joinable()) placer->t.join();
+        const std::exception_ptr err = placer->err;
+        placer.reset();
+        if (err) std::rethrow_exception(err);
+    };
     Round cur;
     if (n_rounds) make_round(0, cur);
     for (uint32_t rd = 0; rd < n_rounds; ++rd) {
@@ -1260,6 +1282,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         const std::vector<size_t>& ppos = cur.ppos;
         const std::vector<size_t>& opos = cur.opos;
         if (!ppos.empty()) {
+            join_placer();
             std::vector<uint32_t> pkey(ppos.size());
             std::vector<int64_t> pdelta(ppos.size());
             std::vector<uint8_t> pisn(ppos.size()), pneed(ppos.size());
@@ -1287,6 +1310,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
                 if (cur.or_snap) alim[opos[k]] = al[k], rlim[opos[k]] = rl[k];
             }
         }
+        join_placer();  // (the previous round's strings, placed beside this round's library apply)
         const double tb = trace ? now() : 0;
         t_apply += tb - ta;
         ++n_chunks;
@@ -1336,13 +1360,26 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         const double tn1 = trace ? now() : 0;
         if (enc.joinable()) enc.join();
         if (eerr) std::rethrow_exception(eerr);
-        if (!or_need.empty()) EncodeORSetSetsPlace(oe, oat, snap, &ssha, &shas);
         if (trace) {
             t_enc_o += now() - tc - (tn1 - tn);
             t_over += std::min(tn1 - tn, oe.ms);
         }
+        if (!or_need.empty()) {
+            placer = std::make_unique<Placer>();
+            Placer* pl = placer.get();
+            pl->e = std::move(oe);
+            pl->at = std::move(oat);
+            pl->t = std::thread([this, pl, &snap, &ssha, &shas] {
+                try {
+                    EncodeORSetSetsPlace(pl->e, pl->at, snap, &ssha, &shas);
+                } catch (...) {
+                    pl->err = std::current_exception();
+                }
+            });
+        }
         cur = std::move(next);
     }
+    join_placer();
     if (trace) {
         tt[2] = now();
         std::fprintf(stderr, "SubmitClientUpdates: before the rounds %.1f ms, rounds' op lists + preparation %.1f ms (%.1f ms of it beside the encodes)\n",
