@@ -745,14 +745,25 @@ void GpuStableStore::ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, 
     off = o;
     sha = h;
     cbuf.assign(K, nullptr);
-    uint8_t* buf = pinned_buf(std::max<size_t>(pin_cap_, (size_t)(n * (last_pnc_bytes_ + 8)) + 4096));
-    size_t cap = pin_cap_, base = 0, total = 0;
+    // JANUS_PNC_STATE_GUESS (bytes per state): a test knob that undersizes the first guess, so the refusal paths
+    // below (the first chunk's growth, a later chunk's own block) run
+    static const double forced = [] {
+        const char* e = std::getenv("JANUS_PNC_STATE_GUESS");
+        return e ? std::atof(e) : 0.0;
+    }();
+    const double per = forced > 0 ? forced : last_pnc_bytes_;
+    uint8_t* buf = forced > 0 ? pinned_buf((size_t)(n * per) + 4096) : pinned_buf(std::max<size_t>(pin_cap_, (size_t)(n * (per + 8)) + 4096));
+    size_t cap = forced > 0 ? (size_t)(n * per) + 4096 : pin_cap_, base = 0, total = 0;
     for (size_t c = 0; c < K; ++c) {
         const size_t s0 = start[c], m = start[c + 1] - s0;
         uint64_t* oc = o + s0 + c;
         auto call = [&] { return jg_pnc_apply_ops_encode(pnc_, m, rows + s0, 0, delta + s0, isn + s0, oc, buf + base, cap - base, h + 32 * s0); };
         int rc = call();
         if (rc == JG_ESTATE && oc[m] > cap - base) {
+            static const bool trace = std::getenv("JANUS_TRACE_SUBMIT") != nullptr;
+            if (trace)
+                std::fprintf(stderr, "ApplyEncodePNC: chunk %zu refused (%llu bytes, %zu of room): %s\n", c, (unsigned long long)oc[m], cap - base,
+                             c == 0 ? "buffer grown" : "a block of its own");
             if (c == 0) {  // nothing read from the buffer yet: grow it
                 buf = pinned_buf(oc[m] + (n - m) * (oc[m] / std::max<size_t>(m, 1) + 8));
                 cap = pin_cap_;

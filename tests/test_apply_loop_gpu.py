@@ -84,18 +84,28 @@ def test_c1_replay_matches_oracle():
     assert out.returncode == 0 and res["parity_vs_oracle"] is True, res
 
 
-@pytest.mark.parametrize("args", [
-    ["--workload", "pnc", "--keys", "2000", "--ops", "20000", "--cpu-ops", "20000", "--waves", "1"],     # many repeats per key
-    ["--workload", "pnc", "--keys", "200000", "--ops", "50000", "--cpu-ops", "50000", "--waves", "1"],
-    ["--workload", "orset", "--keys", "300", "--ops", "20000", "--cpu-ops", "6000", "--waves", "1"],     # Clears at 50 elements
+_BIG_PNC = ["--workload", "pnc", "--keys", "100000", "--ops", "1000", "--cpu-ops", "300000", "--waves", "1"]
+
+
+@pytest.mark.parametrize("args,env", [
+    (["--workload", "pnc", "--keys", "2000", "--ops", "20000", "--cpu-ops", "20000", "--waves", "1"], {}),  # many repeats per key
+    (["--workload", "pnc", "--keys", "200000", "--ops", "50000", "--cpu-ops", "50000", "--waves", "1"], {}),
+    (["--workload", "orset", "--keys", "300", "--ops", "20000", "--cpu-ops", "6000", "--waves", "1"], {}),  # Clears at 50 elements
+    # >= 2^18 ops in one call: the PN-Counter batch in 4 encode-and-apply chunks, messages built per chunk
+    (_BIG_PNC, {}),
+    # the same with the states' size underguessed: a later chunk refused for room goes to a block of its own ...
+    (_BIG_PNC, {"JANUS_PNC_STATE_GUESS": "200"}),
+    # ... and the first chunk refused grows the buffer (nothing applied by a refused call)
+    (_BIG_PNC, {"JANUS_PNC_STATE_GUESS": "20"}),
 ])
-def test_producer_path_matches_oracle(args):
+def test_producer_path_matches_oracle(args, env):
     """The producer path (SafeCRDT.Update + full-state Encode + ActualPropagateSyncMsg + ComputeDigest,
     GpuStableStore::SubmitClientUpdates) on the C5 banking and ORSetWorkload op streams: op results, every
     submitted UpdateMessage (order, identities, payload bytes) and its digest equal the oracle's
-    (host/bench_submit.cpp's parity sample)."""
+    (host/bench_submit.cpp's parity sample, one call over the whole sample)."""
     import json
-    out = subprocess.run([str(BIN.parent / "bench_submit")] + args, capture_output=True, text=True, timeout=110)
+    import os
+    out = subprocess.run([str(BIN.parent / "bench_submit")] + args, capture_output=True, text=True, timeout=110, env={**os.environ, **env})
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert out.returncode == 0 and res["parity_vs_oracle"] is True, (res, out.stderr[-2000:])
     assert res["submitted_msgs_per_wave"] > 0
