@@ -146,6 +146,7 @@ struct jg_pnc {
     uint64_t scan_hi = 0;  // messages pass A scanned since the wave began (its fused applies are undone below this)
     bool wopen = false;
     bool fuse = true;       // the wave's pass A applies what it proves (JANUS_JSON_FUSE, latched when the wave begins)
+    bool status_clean = false;  // the wave status words hold their initial values (the last wave ended clean): no reset
     bool node_open = false;  // a node wave (node.hip) holds the store: see jg::require_writable
 };
 

@@ -825,6 +825,13 @@ void reset_status(jg_ctx* ctx, unsigned long long* status) {
     JG_HIP(hipGetLastError());
 }
 
+// A wave's status words at their initial values: reset on the device unless the last wave left them so (a
+// clean wave — nothing bad, deferred, slow or resumed — never writes them: round 6 skips the reset launch).
+void begin_status(jg_pnc* p, unsigned long long* status) {
+    if (!p->status_clean) reset_status(p->ctx, status);
+    p->status_clean = false;
+}
+
 // JANUS_JSON_FUSE=0: pass A leaves every message to pass B (read per launch: tests and A/B runs switch it)
 // Latched into jg_pnc::fuse when a wave begins (merge_wave_dev, jg_pnc_wave_begin, pnc_node_begin): the chunks'
 // pass A and the wave's finish must agree on it, or finish_wave would skip pass B for records pass A left to it
@@ -865,7 +872,18 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
     const Table t = table_of(p);
     const int G = json_group();
     const unsigned ge = (unsigned)((n * kEmitLanes + kBlock - 1) / kBlock);
-    if (G > 1) {  // the payloads the group parse left to the serial parser (count read on the device)
+    if (G > 1) {
+        // The steady state of a fused wave (every payload compact and valid, every replica known): pass A's status
+        // alone ends it — one read, no slow-list launches (round 6: k_scan_slow and k_apply_slow cost ~5 µs each
+        // even with nothing to do, the next wave's status reset another 5).  Otherwise the launches below.
+        if (p->fuse) {
+            const Status s0 = read_status(ctx, w.status);
+            if (s0.first_bad == ~0ull && s0.n_deferred == 0 && s0.resolve_bad == ~0ull && s0.n_slow == 0 && s0.n_resume == 0) {
+                p->status_clean = true;
+                return;
+            }
+        }
+        // the payloads the group parse left to the serial parser (count read on the device)
         if (p->eb == 8) hipLaunchKernelGGL(k_scan_slow<8>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
         else hipLaunchKernelGGL(k_scan_slow<4>, dim3(64), dim3(kBlock), 0, ctx->stream, bytes, off, rows, t, w.status, w.deferred, w.emit, w.slow);
         JG_HIP(hipGetLastError());
@@ -952,7 +970,7 @@ void finish_wave(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uin
 void merge_wave_dev(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const uint32_t* rows, uint64_t n, uint64_t* bad_msg) {
     ensure_table(p);
     const WaveScratch w = wave_scratch(p, n);
-    reset_status(p->ctx, w.status);
+    begin_status(p, w.status);
     p->scan_hi = 0;
     p->fuse = json_fuse();
     launch_scan(p, bytes, off, rows, 0, n, w);
@@ -978,7 +996,7 @@ namespace jg {
 
 void pnc_node_begin(jg_pnc* p, uint64_t n) {
     ensure_table(p);
-    reset_status(p->ctx, wave_scratch(p, n).status);
+    begin_status(p, wave_scratch(p, n).status);
     p->scan_hi = 0;
     p->fuse = json_fuse();
     p->wn = n;  // the node wave's capacity (jg_pnc_wave_* calls are refused while it is open: node_open)
@@ -1012,7 +1030,7 @@ int pnc_node_prefix(jg_pnc* p, const uint8_t* bytes, const uint64_t* off, const 
     p->scan_hi = 0;
     if (n == 0) return JG_OK;  // a cut at message 0: nothing applied (the undo used to come after this return)
     const WaveScratch w = wave_scratch(p, p->wn);
-    reset_status(p->ctx, w.status);
+    begin_status(p, w.status);
     p->scan_hi = 0;
     launch_scan(p, bytes, off, rows, 0, n, w);
     return pnc_node_finish(p, bytes, off, rows, n, bad, why);
@@ -1177,7 +1195,7 @@ int jg_pnc_wave_begin(jg_pnc* p, uint64_t cap_msgs, uint64_t cap_bytes) {
         grow_keep(ctx, p->woff, (cap_msgs + 1) * 8, 0);
         grow_keep(ctx, p->wrows, cap_msgs * 4 + 4, 0);
         const WaveScratch w = wave_scratch(p, cap_msgs);
-        reset_status(ctx, w.status);
+        begin_status(p, w.status);
         p->scan_hi = 0;
         p->fuse = json_fuse();
         JG_HIP(hipMemsetAsync(p->woff.p, 0, 8, ctx->stream));  // off[0] = 0
