@@ -90,6 +90,7 @@ std::vector<Op> make_ops(bool pnc, uint64_t keys, uint64_t n, std::mt19937_64& r
 int main(int argc, char** argv) {
     bool pnc = true;
     uint64_t keys = 1000000, ops_n = 1000000, cpu_ops = 50000, cpu_warm = UINT64_MAX;
+    uint64_t bad_at = UINT64_MAX;  // test: the parity call is first made with op bad_at's method invalid
     int waves = 3, device = 0, batch = 1000;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--workload") && i + 1 < argc) pnc = std::strcmp(argv[++i], "orset") != 0;
@@ -98,6 +99,7 @@ int main(int argc, char** argv) {
         else if (!std::strcmp(argv[i], "--cpu-ops") && i + 1 < argc) cpu_ops = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--cpu-warm") && i + 1 < argc) cpu_warm = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--waves") && i + 1 < argc) waves = std::atoi(argv[++i]);
+        else if (!std::strcmp(argv[i], "--bad-at") && i + 1 < argc) bad_at = std::strtoull(argv[++i], nullptr, 10);
         else if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--batch") && i + 1 < argc) batch = std::atoi(argv[++i]);
     }
@@ -179,6 +181,26 @@ int main(int argc, char** argv) {
         }
         janus::SafeUpdateTracker gt(gp.ctx());
         std::vector<janus::UpdateMessage> gsub;
+        if (bad_at < ups.size()) {
+            // SafeCRDT.Update's wrapper throws on an unknown method (PNCounterWrapper.cs:46, ORSetWrapper.cs): the call
+            // must raise with nothing applied and nothing queued, however many of its chunks reached the device first
+            std::vector<janus::Guid> all;
+            for (uint64_t k = 0; k < keys; ++k)
+                if (sc[k] && pnc) all.push_back(G(sc[k]->guid));
+            const auto before = gp.EncodePNCStates(all);
+            const int saved = ups[bad_at].op.opId;
+            ups[bad_at].op.opId = 9;
+            bool threw = false;
+            try {
+                gp.SubmitClientUpdates(ups, batch, gsub, gt);
+            } catch (const janus::EngineError&) {
+                threw = true;
+            }
+            ups[bad_at].op.opId = saved;
+            if (!threw) parity_ok = false, parity_why = "an invalid method did not raise";
+            else if (!gsub.empty() || gt.size() != 0) parity_ok = false, parity_why = "a raising call submitted or tracked messages";
+            else if (gp.EncodePNCStates(all) != before) parity_ok = false, parity_why = "a raising call left applied ops in the store";
+        }
         const auto gres = gp.SubmitClientUpdates(ups, batch, gsub, gt);
         // the oracle, timed: Update per op (ApplyOp + full-state Encode + the batcher), then ComputeDigest of every
         // UpdateMessage it submitted

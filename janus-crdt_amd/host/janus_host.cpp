@@ -729,13 +729,14 @@ uint8_t* GpuStableStore::pinned_aux(size_t bytes) {
 }
 
 // jg_pnc_apply_ops_encode over consecutive chunks of ops, into page-locked memory: chunk c's states at cbuf[c] (in
-// pinned_buf, or a block of its own when the states outgrew the buffer's guess), their offsets at off + start[c] + c
-// (chunk-relative, n_c + 1 of them) and their SHA-256s at sha + 32 start[c]; on_chunk(c) after each.  Calls in op
+// pinned_buf, or a block of its own when the states outgrow the buffer's guess), their offsets at off + start[c] + c
+// (chunk-relative, n_c + 1 of them) and their SHA-256s at sha + 32 start[c]; before(c) first (false: stop there),
+// on_chunk(c) after each.  Calls in op
 // order give what one call would (each chunk's prefixes start from the rows the chunks before it left).  A chunk
 // refused for room (JG_ESTATE: nothing of it applied) goes again into a buffer of the size it reported.
 void GpuStableStore::ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
                                     const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
-                                    const std::function<void(size_t)>& on_chunk) {
+                                    const std::function<bool(size_t)>& before, const std::function<void(size_t)>& on_chunk) {
     const size_t K = start.size() - 1, n = start[K];
     for (uint8_t* b : pin_more_) check(jg_host_free(b));
     pin_more_.clear();
@@ -755,6 +756,7 @@ void GpuStableStore::ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, 
     uint8_t* buf = forced > 0 ? pinned_buf((size_t)(n * per) + 4096) : pinned_buf(std::max<size_t>(pin_cap_, (size_t)(n * (per + 8)) + 4096));
     size_t cap = forced > 0 ? (size_t)(n * per) + 4096 : pin_cap_, base = 0, total = 0;
     for (size_t c = 0; c < K; ++c) {
+        if (!before(c)) break;  // (the caller's checks stopped the batch: chunks from here on never reach the store)
         const size_t s0 = start[c], m = start[c + 1] - s0;
         uint64_t* oc = o + s0 + c;
         auto call = [&] { return jg_pnc_apply_ops_encode(pnc_, m, rows + s0, 0, delta + s0, isn + s0, oc, buf + base, cap - base, h + 32 * s0); };
@@ -973,12 +975,13 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     double t_apply = 0, t_enc_p = 0, t_enc_o = 0;
     size_t n_chunks = 0;
     // Round 6: three things overlap.  A helper thread runs the wrappers' checks on the workers (every op's key resolved,
-    // read-only) while this thread walks the batcher over message identities (serial, nothing committed until the
-    // checks pass); then, for a batch of PN-Counter ops only (one round), the helper encodes EVERY op's snapshot and
-    // applies the ops in one library call (jg_pnc_apply_ops_encode: per-key prefixes, encode and apply on the device,
-    // no workers) while this thread computes the flushes and the tracker adds on the workers.  Only the snapshots
-    // the batcher keeps become strings, where the messages are built.  A failing check still raises before anything
-    // is applied or queued, as the serial loop would.
+    // read-only), chunk by chunk, while this thread walks the batcher over message identities (serial, nothing
+    // committed until the checks pass); each PN-Counter chunk whose checks passed goes to the device on an encoder
+    // thread (jg_pnc_apply_ops_encode: per-key prefixes, every op's snapshot encoded, then the ops applied; no
+    // workers) while the next chunk is checked and, later, this thread computes the flushes and the tracker adds and
+    // builds the messages of the chunks already encoded.  Only the snapshots the batcher keeps become strings.  A
+    // failing check still raises with nothing applied or queued, as the serial loop would: chunks already applied
+    // are taken back first.
     std::vector<const KeyRef*> kref(n);
     // each op's key as plain arrays: the serial walks below would chase every KeyRef through the uid map's nodes
     std::vector<uint32_t> krow(n);
@@ -1010,72 +1013,113 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     std::exception_ptr herr;
     double t_chk = 0;
     std::vector<double> t_chunk;
+    // The batch in chunks (4 for >= 2^18 ops): the checks run chunk by chunk, and a PN-Counter chunk whose checks
+    // passed goes to the device (jg_pnc_apply_ops_encode, on the encoder thread) while the next chunk is checked.  A
+    // later failing check, or an OR-Set key (the batch then takes the rounds below), stops the encoder, and the
+    // chunks it applied are taken back exactly (the adds wrap: the negated amounts restore every cell) before
+    // anything raises or proceeds — the serial loop's all-or-nothing.
+    const size_t K = n >= (size_t(1) << 18) ? 4 : 1;
+    spec.clen = std::max<size_t>(1, (n + K - 1) / K);
+    for (size_t c = 0; c <= K; ++c) spec.start.push_back(std::min(n, c * spec.clen));
+    size_t checked = 0;  // chunks checked and all PN-Counter (under hm)
+    bool stop = false;   // no further chunk goes to the device (under hm)
+    std::thread encoder;
     std::thread helper([&] {
         try {
-            parallel_ranges(pool(), n, [&](size_t b, size_t e, int t) {
-                constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
-                for (size_t i = b; i < std::min(e, b + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
-                uint8_t set_seen = 0;  // (one store per range: the workers' flags share a cache line)
-                struct Put {
-                    uint8_t& to;
-                    uint8_t& v;
-                    ~Put() { to = v; }
-                } put{saw_set[t], set_seen};
-                for (size_t i = b; i < e; ++i) {
-                    if (i + kAhead < e) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
-                    const ClientOp& op = ups[i].op;
-                    const KeyRef* kr = find_uid(op.uid);
-                    kref[i] = kr;
-                    if (kr) {
-                        const bool pn = kr->type == CrdtType::PNCounter;
-                        krow[i] = kr->idx, kpn[i] = pn ? 1 : 0;
-                        set_seen |= pn ? 0 : 1;
-                        delta[i] = eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount;
-                        isn[i] = op.opId == 2 ? 1 : 0;
-                    }
-                    if (!kr || op.opId < 1 || op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
-                        first_bad[t] = i;
-                        return;
-                    }
+            bool any_set = false, enc_started = false;
+            size_t b = n;
+            // JANUS_SUBMIT_LOCKSTEP (tests): chunk c is checked only once the encoder applied chunk c - 1, so a failing
+            // check in a later chunk always meets applied chunks and the take-back runs
+            static const bool lockstep = std::getenv("JANUS_SUBMIT_LOCKSTEP") != nullptr;
+            for (size_t c = 0; c < K && b == n; ++c) {
+                if (lockstep && enc_started && c > 0) {
+                    std::unique_lock<std::mutex> g(hm);
+                    hcv.wait(g, [&] { return spec.done >= c || stop || herr; });
                 }
-            });
-            const size_t b = *std::min_element(first_bad.begin(), first_bad.end());
-            const bool pnc_only = b == n && n > 0 && std::all_of(saw_set.begin(), saw_set.end(), [](uint8_t x) { return x == 0; });
-            if (pnc_only) {  // chunks of ops, so the messages of the first are built while the next is encoded
-                const size_t K = n >= (size_t(1) << 18) ? 4 : 1;
-                spec.clen = (n + K - 1) / K;
-                for (size_t c = 0; c <= K; ++c) spec.start.push_back(std::min(n, c * spec.clen));
+                const size_t c0 = spec.start[c], c1 = spec.start[c + 1];
+                parallel_ranges(pool(), c1 - c0, [&](size_t rb, size_t re, int t) {
+                    rb += c0, re += c0;
+                    constexpr size_t kAhead = 8;  // the slot of op i + kAhead prefetched while op i is looked up
+                    for (size_t i = rb; i < std::min(re, rb + kAhead); ++i) __builtin_prefetch(&uidx_[uid_slot0(ups[i].op.uid)]);
+                    uint8_t set_seen = 0;  // (one store per range: the workers' flags share a cache line)
+                    struct Put {
+                        uint8_t& to;
+                        uint8_t& v;
+                        ~Put() { to |= v; }
+                    } put{saw_set[t], set_seen};
+                    for (size_t i = rb; i < re; ++i) {
+                        if (i + kAhead < re) __builtin_prefetch(&uidx_[uid_slot0(ups[i + kAhead].op.uid)]);
+                        const ClientOp& op = ups[i].op;
+                        const KeyRef* kr = find_uid(op.uid);
+                        kref[i] = kr;
+                        if (kr) {
+                            const bool pn = kr->type == CrdtType::PNCounter;
+                            krow[i] = kr->idx, kpn[i] = pn ? 1 : 0;
+                            set_seen |= pn ? 0 : 1;
+                            delta[i] = eb_ == 4 ? (int64_t)(int32_t)op.amount : op.amount;
+                            isn[i] = op.opId == 2 ? 1 : 0;
+                        }
+                        if (!kr || op.opId < 1 || op.opId > (kr->type == CrdtType::PNCounter ? 2 : 3)) {
+                            first_bad[t] = std::min(first_bad[t], i);
+                            return;
+                        }
+                    }
+                }, 0);
+                b = *std::min_element(first_bad.begin(), first_bad.end());
+                any_set = any_set || std::any_of(saw_set.begin(), saw_set.end(), [](uint8_t x) { return x != 0; });
+                {
+                    std::lock_guard<std::mutex> g(hm);
+                    if (b < n || any_set) stop = true;  // (an OR-Set key: the later chunks are still checked, for the rounds)
+                    else checked = c + 1;
+                }
+                hcv.notify_all();
+                if (c == 0 && b == n && !any_set && (enc_started = true))  // the encoder takes the chunks as they pass
+                    encoder = std::thread([&] {
+                        try {
+                            ApplyEncodePNC(krow.data(), delta.data(), isn.data(), spec.start, spec.off, spec.sha, spec.cbuf,
+                                           [&](size_t cc) {
+                                               std::unique_lock<std::mutex> g(hm);
+                                               hcv.wait(g, [&] { return stop || checked > cc || checks_done; });
+                                               return !stop && checked > cc;
+                                           },
+                                           [&](size_t cc) {
+                                               {
+                                                   std::lock_guard<std::mutex> g(hm);
+                                                   spec.done = cc + 1;
+                                                   if (trace) t_chunk.push_back(now());
+                                               }
+                                               hcv.notify_all();
+                                           });
+                        } catch (...) {
+                            std::lock_guard<std::mutex> g(hm);
+                            if (!herr) herr = std::current_exception();
+                            stop = true;
+                            hcv.notify_all();
+                        }
+                    });
             }
             {
                 std::lock_guard<std::mutex> g(hm);
                 bad = b;
-                spec.on = pnc_only;
+                spec.on = b == n && n > 0 && !any_set && !stop;
                 checks_done = true;
                 t_chk = trace ? now() : 0;
             }
             hcv.notify_all();
-            if (!pnc_only) return;
-            ApplyEncodePNC(krow.data(), delta.data(), isn.data(), spec.start, spec.off, spec.sha, spec.cbuf, [&](size_t c) {
-                {
-                    std::lock_guard<std::mutex> g(hm);
-                    spec.done = c + 1;
-                    if (trace) t_chunk.push_back(now());
-                }
-                hcv.notify_all();
-            });
         } catch (...) {
             std::lock_guard<std::mutex> g(hm);
-            herr = std::current_exception();
+            if (!herr) herr = std::current_exception();
+            stop = true;
             checks_done = true;
             hcv.notify_all();
         }
     });
-    struct JoinGuard {  // the helper never outlives the call, whatever throws
+    struct JoinGuard {  // the helper and the encoder never outlive the call, whatever throws
         std::thread& t;
         ~JoinGuard() {
             if (t.joinable()) t.join();
         }
-    } join_guard{helper};
+    } join_enc{encoder}, join_guard{helper};  // (the helper first: it is what starts the encoder)
     // 1. The batcher over message identities (SafeCRDTManager.cs:165-198); states are filled in below.
     //    q entries: message, op index (kOld: queued by an earlier call), and whether SafeCRDT.Update
     //    tracked it.  The batcher's safeUpdateTracker.ContainsKey(msg) (:176) is that flag: a message the
@@ -1133,8 +1177,25 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
         std::unique_lock<std::mutex> g(hm);
         hcv.wait(g, [&] { return checks_done; });
     }
-    if (herr || bad < n) {  // nothing applied, nothing queued: the serial loop's first throw
+    if (!spec.on) {
+        // the chunks the encoder applied before the checks stopped it, taken back: the adds wrap, so the negated
+        // amounts restore every cell exactly — nothing applied, as the serial loop's first throw and the rounds below
+        // expect (the helper has set checks_done, so the encoder it may have started exists by now)
         helper.join();
+        if (encoder.joinable()) encoder.join();
+        const size_t applied = spec.start[spec.done];
+        if (applied && !herr) {
+            std::vector<uint32_t> zc(applied, 0);
+            std::vector<int64_t> neg(applied);
+            for (size_t i = 0; i < applied; ++i) neg[i] = (int64_t)(0ull - (uint64_t)delta[i]);
+            check(jg_pnc_apply_ops(pnc_, applied, krow.data(), zc.data(), neg.data(), isn.data()));
+            if (trace) std::fprintf(stderr, "SubmitClientUpdates: %zu ops of %zu chunks taken back (the checks stopped the batch)\n", applied, spec.done);
+        }
+        spec.done = 0;
+    }
+    if (herr || bad < n) {  // nothing applied, nothing queued: the serial loop's first throw
+        if (helper.joinable()) helper.join();
+        if (encoder.joinable()) encoder.join();
         if (herr) std::rethrow_exception(herr);
         if (!kref[bad]) throw EngineError(JG_EINVAL, "unknown CRDT uid");
         throw EngineError(JG_EINVAL, kref[bad]->type == CrdtType::PNCounter ? "Invalid PNC method name" : "Invalid ORSet method name");
@@ -1194,8 +1255,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
     //    op's round is the number of such Clears of its own set before it (per-set order kept), and every PN-Counter
     //    op runs in round 0.
     std::vector<uint8_t> result(n, 1);
-    if (!spec.on) {  // (the helper ended with the checks)
-        helper.join();
+    if (!spec.on) {  // (the helper ended with the checks; joined above)
         if (herr) std::rethrow_exception(herr);
     }
     // A PN-Counter-only batch is applied and encoded by the helper, chunk by chunk: its snapshots stay in page-locked
@@ -1451,6 +1511,7 @@ std::vector<uint8_t> GpuStableStore::SubmitClientUpdates(const std::vector<Clien
             f0 = f1;
         }
         helper.join();
+        encoder.join();
         if (herr) std::rethrow_exception(herr);
         build(f0, flushes.size());
         if (trace) {

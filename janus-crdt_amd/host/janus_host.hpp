@@ -296,7 +296,7 @@ class GpuStableStore {
                               std::vector<std::array<uint8_t, 32>>* sha, std::vector<uint8_t>* has);
     void ApplyEncodePNC(const uint32_t* rows, const int64_t* delta, const uint8_t* isn, const std::vector<size_t>& start,
                         const uint64_t*& off, const uint8_t*& sha, std::vector<const uint8_t*>& cbuf,
-                        const std::function<void(size_t)>& on_chunk);
+                        const std::function<bool(size_t)>& before, const std::function<void(size_t)>& on_chunk);
     std::vector<uint8_t*> pin_more_;  // ApplyEncodePNC's extra page-locked blocks (states past pinned_buf's guess)
     uint8_t* pin_buf_ = nullptr;
     size_t pin_cap_ = 0;

@@ -97,6 +97,10 @@ _BIG_PNC = ["--workload", "pnc", "--keys", "100000", "--ops", "1000", "--cpu-ops
     (_BIG_PNC, {"JANUS_PNC_STATE_GUESS": "200"}),
     # ... and the first chunk refused grows the buffer (nothing applied by a refused call)
     (_BIG_PNC, {"JANUS_PNC_STATE_GUESS": "20"}),
+    # an invalid method in the last chunk: the chunks already on the device are taken back, the call raises with
+    # nothing applied or queued; then the same call, valid, matches the oracle (the restored state included)
+    (_BIG_PNC + ["--bad-at", "290000"], {"JANUS_SUBMIT_LOCKSTEP": "1"}),
+    (_BIG_PNC + ["--bad-at", "10"], {}),
 ])
 def test_producer_path_matches_oracle(args, env):
     """The producer path (SafeCRDT.Update + full-state Encode + ActualPropagateSyncMsg + ComputeDigest,
