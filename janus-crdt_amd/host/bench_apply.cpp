@@ -25,6 +25,7 @@
 // --parity: the oracle applies EVERY wave in full; after each wave every owned account's stable Get and
 // the safe-update completions (origins, in commit order) must equal the oracle's (exit 1 otherwise).
 // Prints one JSON object.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -114,6 +115,7 @@ int main(int argc, char** argv) {
 
     double gpu_s = 0, cpu_s = 0, flat_s = 0, gather_s = 0, wait_s = 0, lib_s = 0, busy_s = 0, chunk_s = 0, setup_s = 0, loop_s = 0, pack_s = 0;
     uint64_t gpu_n = 0, cpu_n = 0, payload_timed = 0, up_bytes = 0, up_msgs = 0, applied = 0, n_safe = 0, n_states = 0, n_done = 0;
+    std::vector<uint64_t> done_buf;  // the direct legs' completion buffer, reused
     bool ok = true;
     std::string why;
     for (int w = 0; w < waves + 1 && ok; ++w) {  // wave 0 = warmup
@@ -213,8 +215,13 @@ int main(int argc, char** argv) {
         if (direct) gpu.PackCommitted(wave, !arena);
         const double t0 = arena ? tp : now_s();
         if (direct && w > 0) pack_s += now_s() - tp;
-        const std::vector<uint64_t> done = stream ? gpu.ApplyArenaStreamed(wave, &tracker_g, part_msgs, !stream_cached)
-                                           : direct ? gpu.ApplyPacked(&tracker_g) : gpu.ApplyCommitted(wave, &tracker_g);
+        // (the direct legs hand the library a reused completion buffer, as a C# caller passes its own array)
+        std::vector<uint64_t> done;
+        size_t k_done = 0;
+        const bool into = !stream;  // (the streamed arena keeps its vector form)
+        if (direct) k_done = gpu.ApplyPackedInto(&tracker_g, done_buf);
+        else if (!stream) k_done = gpu.ApplyCommittedInto(wave, &tracker_g, done_buf);
+        else done = gpu.ApplyArenaStreamed(wave, &tracker_g, part_msgs, !stream_cached), k_done = done.size();
         const double t1 = now_s();
         if (w == 0) {
             if (parity) {  // the warmup wave reaches the oracle too (untimed), so states stay in step
@@ -255,7 +262,7 @@ int main(int argc, char** argv) {
         applied += st.msgs_applied;  // counted by the library: states that reached a registered key
         gpu_n += wave_msgs;
         payload_timed += wave_payload;
-        n_done += done.size();
+        n_done += k_done;
         if (!run_cpu) continue;
         cpu.safeUpdateTracker = tracker_c;
         cpu.notified.clear();
@@ -270,7 +277,9 @@ int main(int argc, char** argv) {
         if (!parity) continue;
         // every owned account's stable Get, and the completions in commit order (unowned uids are
         // skipped on both sides, SafeCRDTManager.cs:136)
-        if (done != cpu.notified) { ok = false; why = "safe-update completions differ"; }
+        const bool same_done = into ? k_done == cpu.notified.size() && std::equal(cpu.notified.begin(), cpu.notified.end(), done_buf.begin())
+                                    : done == cpu.notified;
+        if (!same_done) { ok = false; why = "safe-update completions differ"; }
         for (uint64_t k = 0; k < accounts && ok; ++k) {
             if (!mine[k]) continue;
             if (gpu.QueryStablePNC(G(uid[k])) != cref[k]->QueryStable().i) { ok = false; why = "account " + std::to_string(k) + " differs"; }

@@ -161,6 +161,10 @@ class GpuStableStore {
     // the upload then snoops the dirty lines)
     void PackCommitted(const std::vector<std::vector<UpdateMessage>>& updates, bool nontemporal = true);
     std::vector<uint64_t> ApplyPacked(SafeUpdateTracker* tracker = nullptr);
+    // The same with the completions written into the caller's buffer (grown to the wave's size, reused across
+    // calls): returns how many of its first entries this wave completed.
+    size_t ApplyPackedInto(SafeUpdateTracker* tracker, std::vector<uint64_t>& done);
+    size_t ApplyCommittedInto(const std::vector<std::vector<UpdateMessage>>& updates, SafeUpdateTracker* tracker, std::vector<uint64_t>& done);
     // What a C# caller without page-locked receive buffers does with the streamed apply (jg_apply_stream_*): copy
     // the wave's byte[]s into a jg_host_alloc arena part by part (~part_msgs messages of whole UpdateMessages),
     // handing each part to the library as soon as it is copied, so the copy of the next part overlaps the upload
@@ -347,6 +351,8 @@ class GpuStableStore {
     std::vector<uint64_t> apply(const std::vector<const UpdateMessage*>& blocks, SafeUpdateTracker* tracker, bool block_mode);
     size_t index_blocks(const std::vector<const UpdateMessage*>& blocks);  // block_off_ + the flattened arrays' room
     std::vector<uint64_t> run_wave(const jg_commit& wave, SafeUpdateTracker* tracker, bool block_mode);
+    size_t run_wave_into(const jg_commit& wave, SafeUpdateTracker* tracker, std::vector<uint64_t>& out);
+    jg_commit gather_wave(const std::vector<const UpdateMessage*>& blocks);
     jg::WorkerPool& pool();  // persistent host workers for the flatten
 
     jg_ctx* ctx_ = nullptr;
