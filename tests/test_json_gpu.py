@@ -687,6 +687,55 @@ def test_apply_ops_encode_matches_oracle(ctx, eb, n_keys, n_ops, merged):
 
 
 @pytest.mark.parametrize("eb", [4, 8])
+def test_apply_ops_encode_edges(ctx, eb):
+    """jg_pnc_apply_ops_encode edges: an empty batch writes off[0] = 0 and touches nothing; an op on a key outside
+    the store or a column past the store's replicas is refused with JG_EINVAL before anything is applied; one key
+    hit by 70,000 ops (one segment across many scan tiles) with negative amounts and the int64 / int32 extremes
+    walks op by op like the oracle, wrapping as the reference's checked-off arithmetic does."""
+    rng = np.random.default_rng(90 + eb)
+    n_keys, R = 5, 4
+    pr = Pair(ctx, n_keys, R, eb, random_guids(rng, n_keys))
+    got, h = pr.s.apply_ops_encode(np.zeros(0, np.uint32), np.zeros(0, np.int64), np.zeros(0, np.uint8))
+    assert got == [] and h.shape[0] == 0
+    P0, N0 = pr.s.read_rows()
+    for key, col in ((np.array([0, n_keys], np.uint32), 0), (np.array([1, 2], np.uint32), R)):
+        with pytest.raises(jg.JanusError) as e:
+            pr.s.apply_ops_encode(key, np.ones(2, np.int64), np.zeros(2, np.uint8), col=col)
+        assert e.value.code == jg.JG_EINVAL
+    P1, N1 = pr.s.read_rows()
+    assert np.array_equal(P0, P1) and np.array_equal(N0, N1), "a refused call applied ops"
+    n_ops = 70000
+    key = np.where(rng.random(n_ops) < 0.9, 3, rng.integers(0, n_keys, n_ops)).astype(np.uint32)
+    delta = rng.integers(-1000, 1000, n_ops).astype(np.int64)
+    delta[rng.random(n_ops) < 0.01] = -(2**31)
+    delta[rng.random(n_ops) < 0.01] = 2**31 - 1
+    if eb == 8:
+        delta[rng.random(n_ops) < 0.005] = -(2**63)
+        delta[rng.random(n_ops) < 0.005] = 2**63 - 1
+    is_n = (rng.random(n_ops) < 0.4).astype(np.uint8)
+    got, h = pr.s.apply_ops_encode(key, delta, is_n)
+    bits = 32 if eb == 4 else 64
+
+    def wrap(x):
+        x = int(x) % (1 << bits)
+        return x - (1 << bits) if x >= 1 << (bits - 1) else x
+    P, N = pr.P.astype(object), pr.N.astype(object)
+    for i in range(n_ops):
+        k = int(key[i])
+        M = N if is_n[i] else P
+        M[k, 0] = wrap(M[k, 0] + int(delta[i]))
+        if i % 7 == 0 or i >= n_ops - 50:
+            c = int(pr.ncols[k])
+            exp = orc.json_encode_pnc(pr.cols[k, :c]["lo"], pr.cols[k, :c]["hi"], np.array(P[k, :c], dtype=pr.P.dtype),
+                                      np.array(N[k, :c], dtype=pr.N.dtype), eb)
+            assert got[i] == exp, f"op {i} key {k}"
+            assert h[i].tobytes() == hashlib.sha256(got[i]).digest()
+    pr.P, pr.N = np.array(P, dtype=pr.P.dtype), np.array(N, dtype=pr.N.dtype)
+    pr.check()
+    pr.close()
+
+
+@pytest.mark.parametrize("eb", [4, 8])
 @pytest.mark.parametrize("n_keys,n_ops", [(40, 3000), (200000, 100000), (3, 1)])
 def test_apply_ops_rewind_matches_walk(ctx, eb, n_keys, n_ops):
     """jg_pnc_apply_ops_rewind (round 6): a batch of own-column Increment / Decrement ops (PNCounters.cs:96-112)
