@@ -600,11 +600,18 @@ __device__ __forceinline__ long long cell(const void* base, uint64_t i) {
 struct Out {
     uint8_t* p;
     __device__ void put(char c) { *p++ = (uint8_t)c; }
-    __device__ void str(const char* s) { while (*s) put(*s++); }
+    template <int L>
+    __device__ void str(const char (&s)[L]) {  // literals only: unrolled into immediate stores
+#pragma unroll
+        for (int k = 0; k + 1 < L; ++k) put(s[k]);
+    }
+    __device__ static char hexc(uint32_t v) {  // arithmetic, not a table: an indexed table is a memory load per digit
+        v &= 15;
+        return (char)(v < 10 ? '0' + v : 'a' - 10 + v);
+    }
     __device__ void hex2(uint32_t b) {
-        const char* hx = "0123456789abcdef";
-        put(hx[(b >> 4) & 15]);
-        put(hx[b & 15]);
+        put(hexc(b >> 4));
+        put(hexc(b));
     }
     __device__ void guid(const Guid16& g) {  // Guid.ToString("D"): b3b2b1b0-b5b4-b7b6-b8b9-b10..b15
         for (int k = 3; k >= 0; --k) hex2((uint32_t)(g.lo >> (8 * k)));
@@ -635,36 +642,79 @@ __device__ __forceinline__ long long cell_at(const void* base, uint64_t i, bool 
     else return rewind ? (long long)((unsigned long long)cell<8>(base, i) - (unsigned long long)d) : cell<8>(base, i);
 }
 
-template <int EB, int PASS>
-__global__ __launch_bounds__(kBlock) void k_encode(const uint32_t* __restrict__ rows, uint64_t n, Table t, const void* P, const void* N,
-                                                   unsigned long long* __restrict__ len_off, uint8_t* __restrict__ out, uint32_t col,
-                                                   const long long* __restrict__ dp, const long long* __restrict__ dn) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t row = rows[i];
+template <int EB>
+__device__ __forceinline__ void encode_row(Out o, Table t, const void* P, const void* N, uint32_t row, uint32_t col, bool rewind,
+                                           long long rp, long long rn) {
     const uint32_t nc = t.ncols[row];
     const uint64_t base = (uint64_t)row * t.R;
-    const long long rp = dp ? dp[i] : 0, rn = dp ? dn[i] : 0;
-    if (PASS == 0) {
-        unsigned long long len = 27 + (nc ? 2ull * (40ull * nc - 1) : 0);
-        for (uint32_t c = 0; c < nc; ++c)
-            len += dec_len(cell_at<EB>(P, base + c, dp && c == col, rp)) + dec_len(cell_at<EB>(N, base + c, dp && c == col, rn));
-        len_off[i] = len;
-        return;
-    }
-    Out o{out + len_off[i]};
     for (int which = 0; which < 2; ++which) {
-        o.str(which ? "},\"nVector\":{" : "{\"pVector\":{");
+        if (which) o.str("},\"nVector\":{");
+        else o.str("{\"pVector\":{");
         const void* V = which ? N : P;
         for (uint32_t c = 0; c < nc; ++c) {
             if (c) o.put(',');
             o.put('"');
             o.guid(t.cols[base + c]);
             o.str("\":");
-            o.dec(cell_at<EB>(V, base + c, dp && c == col, which ? rn : rp));
+            o.dec(cell_at<EB>(V, base + c, rewind && c == col, which ? rn : rp));
         }
     }
     o.str("}}");
+}
+
+// The write pass stages each wave's rows in LDS.  A wave's rows are consecutive, so their states are one contiguous
+// span of the output (the offsets are an exclusive scan), and the span goes out in aligned 16-byte stores of whole
+// lines instead of every lane storing its own row a byte at a time ~370 bytes from its neighbours (64 partial lines
+// per store instruction, which the memory side then merges line by line).  The span is placed in LDS at the output
+// address's offset within 16 bytes, so LDS chunk k is output chunk k.  A span past kEncStage (rows with many replica
+// columns) is written directly.  One wave per workgroup: 64 C5 rows (4 replicas) are ~23.5 KB.
+constexpr uint32_t kEncStage = 32768;
+constexpr int kEncLanes = 64;
+
+template <int EB, int PASS>
+__global__ __launch_bounds__(kBlock) void k_encode(const uint32_t* __restrict__ rows, uint64_t n, Table t, const void* P, const void* N,
+                                                   unsigned long long* __restrict__ len_off, uint8_t* __restrict__ out, uint32_t col,
+                                                   const long long* __restrict__ dp, const long long* __restrict__ dn) {
+    if (PASS == 0) {
+        const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        if (i >= n) return;
+        const uint32_t row = rows[i];
+        const uint32_t nc = t.ncols[row];
+        const uint64_t base = (uint64_t)row * t.R;
+        const long long rp = dp ? dp[i] : 0, rn = dp ? dn[i] : 0;
+        unsigned long long len = 27 + (nc ? 2ull * (40ull * nc - 1) : 0);
+        for (uint32_t c = 0; c < nc; ++c)
+            len += dec_len(cell_at<EB>(P, base + c, dp && c == col, rp)) + dec_len(cell_at<EB>(N, base + c, dp && c == col, rn));
+        len_off[i] = len;
+        return;
+    } else {  // launched with kEncLanes threads per workgroup
+        __shared__ __attribute__((aligned(16))) uint8_t stage[kEncStage + 16];
+        const uint64_t first = (uint64_t)blockIdx.x * kEncLanes, i = first + threadIdx.x;
+        const uint64_t last = first + kEncLanes < n ? first + kEncLanes : n;
+        const unsigned long long lo = len_off[first], hi = len_off[last];  // (len_off holds n + 1 offsets)
+        const bool staged = hi - lo <= kEncStage;  // uniform over the workgroup
+        const uint32_t mis = (uint32_t)((uintptr_t)(out + lo) & 15);
+        if (i < n) {
+            const unsigned long long at = len_off[i];
+            const uint32_t row = rows[i];
+            const long long rp = dp ? dp[i] : 0, rn = dp ? dn[i] : 0;
+            if (staged) encode_row<EB>(Out{stage + mis + (at - lo)}, t, P, N, row, col, dp != nullptr, rp, rn);  // LDS stores
+            else encode_row<EB>(Out{out + at}, t, P, N, row, col, dp != nullptr, rp, rn);
+        }
+        if (!staged) return;
+        __syncthreads();
+        uint8_t* g = out + lo - mis;  // 16-byte aligned; only bytes [mis, end) of it are written
+        const uint32_t end = mis + (uint32_t)(hi - lo), chunks = (end + 15) >> 4;
+        for (uint32_t k = threadIdx.x; k < chunks; k += kEncLanes) {
+            const uint32_t b0 = 16 * k;
+            if (b0 >= mis && b0 + 16 <= end) {
+                *reinterpret_cast<uint4*>(g + b0) = *reinterpret_cast<const uint4*>(stage + b0);
+            } else {
+                for (uint32_t b = b0; b < b0 + 16; ++b)
+                    if (b >= mis && b < end) g[b] = stage[b];
+            }
+        }
+    }
 }
 
 void ensure_table(jg_pnc* p) {
@@ -1399,8 +1449,9 @@ void encode_rows(jg_pnc* p, uint64_t n, const uint32_t* key_idx, uint32_t col, c
     if (!out) return;  // size query
     JG_REQUIRE(off[n] <= cap, JG_ESTATE, "%s: %llu bytes exceed cap %llu", fn, (unsigned long long)off[n], (unsigned long long)cap);
     auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
-    if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
-    else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+    const unsigned g1 = (unsigned)((n + kEncLanes - 1) / kEncLanes);  // the write pass: one wave per workgroup
+    if (p->eb == 8) hipLaunchKernelGGL((k_encode<8, 1>), dim3(g1), dim3(kEncLanes), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+    else hipLaunchKernelGGL((k_encode<4, 1>), dim3(g1), dim3(kEncLanes), 0, ctx->stream, rows, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
     JG_HIP(hipGetLastError());
     if (sha) jg::sha256_device(ctx, dout, reinterpret_cast<const uint64_t*>(doff), n, sha);  // each state's SHA-256 (ComputeDigest's first level)
     JG_HIP(hipMemcpyAsync(out, dout, off[n], hipMemcpyDeviceToHost, ctx->stream));
@@ -1553,11 +1604,12 @@ int jg_pnc_apply_ops_encode(jg_pnc* p, uint64_t n_ops, const uint32_t* key, uint
                    (unsigned long long)cap);
         // the bytes, then the ops (stream order: the write pass reads the rows before the adds land), the hashes
         auto* dout = static_cast<uint8_t*>(jg::scratch(ctx, ctx->scratch2, off[n] + 64));
+        const unsigned g1 = (unsigned)((n + kEncLanes - 1) / kEncLanes);  // the write pass: one wave per workgroup
         if (p->eb == 8) {
-            hipLaunchKernelGGL((k_encode<8, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+            hipLaunchKernelGGL((k_encode<8, 1>), dim3(g1), dim3(kEncLanes), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
             hipLaunchKernelGGL(k_apply_ops_col<8>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
         } else {
-            hipLaunchKernelGGL((k_encode<4, 1>), dim3(g), dim3(kBlock), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
+            hipLaunchKernelGGL((k_encode<4, 1>), dim3(g1), dim3(kEncLanes), 0, ctx->stream, dkey, n, t, p->P.p, p->N.p, doff, dout, col, ddp, ddn);
             hipLaunchKernelGGL(k_apply_ops_col<4>, dim3(g), dim3(kBlock), 0, ctx->stream, p->P.p, p->N.p, dkey, col, ddel, disn, n, p->R);
         }
         JG_HIP(hipGetLastError());
